@@ -1,0 +1,76 @@
+// common.h -- shared types and 32-bit modular arithmetic for the MI355X CKKS engine.
+//
+// Every RNS prime q lies in (2^30, floor(2^32/3)), which lets all
+// modular products run on 32-bit VALU multiplies (v_mul_lo_u32 / v_mul_hi_u32) with
+// no 64-bit emulation:
+//   * Shoup    (constant operand w, w' = floor(w*2^32/q)):  3 multiplies, result < 2q
+//   * Barrett  (two variable operands, mu = floor(2^62/q)): 4 multiplies, result < 3q
+// 3q < 2^32, so the wrapped 32-bit differences below are exact.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+typedef int64_t i64;
+
+#define HD __host__ __device__ __forceinline__
+
+HD u32 mulhi32(u32 a, u32 b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __umulhi(a, b);
+#else
+    return (u32)(((u64)a * b) >> 32);
+#endif
+}
+
+HD u32 csub(u32 x, u32 q) { return x >= q ? x - q : x; }
+HD u32 add_mod(u32 a, u32 b, u32 q) { return csub(a + b, q); }
+HD u32 sub_mod(u32 a, u32 b, u32 q) { return csub(a + q - b, q); }
+
+// a * w mod q, w' = floor(w * 2^32 / q) precomputed; a < 2^32 (any), result in [0, q)
+HD u32 shoup_mul(u32 a, u32 w, u32 wp, u32 q) {
+    u32 qh = mulhi32(a, wp);
+    u32 r = a * w - qh * q;
+    return csub(r, q);
+}
+HD u32 shoup_pre(u32 w, u32 q) { return (u32)(((u64)w << 32) / q); }
+
+// a * b mod q for a, b < q; mu = floor(2^62 / q) (fits 32 bits since q > 2^30)
+HD u32 barrett_mul(u32 a, u32 b, u32 q, u32 mu) {
+    u32 lo = a * b, hi = mulhi32(a, b);
+    u32 t = (hi << 2) | (lo >> 30);          // floor(a*b / 2^30) < 2^32
+    u32 qh = mulhi32(t, mu);                  // within 2 of floor(a*b/q)
+    u32 r = lo - qh * q;                      // < 3q < 2^32
+    r = csub(r, q);
+    return csub(r, q);
+}
+HD u32 barrett_pre(u32 q) { return (u32)((1ull << 62) / q); }
+
+// reduce a 64-bit accumulator (x < 2^62) with the Barrett constant
+HD u32 barrett_reduce64(u64 x, u32 q, u32 mu) {
+    u32 lo = (u32)x, hi = (u32)(x >> 32);
+    u32 t = (hi << 2) | (lo >> 30);
+    u32 qh = mulhi32(t, mu);
+    u32 r = lo - qh * q;
+    r = csub(r, q);
+    return csub(r, q);
+}
+
+// per-prime constant table kept in device memory
+struct PrimeConst {
+    u32 q;       // modulus
+    u32 mu;      // floor(2^62 / q)
+    u32 ninv;    // N^{-1} mod q
+    u32 ninv_p;  // Shoup companion
+    u32 im;      // psi^{N/2}: the "imaginary unit" of Z_q (X^{N/2} at psi)
+    u32 im_p;
+    u32 pad0, pad1;
+};
+
+// limb -> prime map of an RNS polynomial: limbs [0, n1) use primes off1 + l,
+// limbs [n1, ...) use primes off2 + (l - n1)  (a Q-prefix followed by the P block)
+struct LimbMap {
+    int n1, off1, off2;
+    HD int prime(int l) const { return l < n1 ? off1 + l : off2 + (l - n1); }
+};

@@ -1,0 +1,110 @@
+// params.cpp -- prime chain, scales and 2N-th roots.
+#include "params.h"
+
+#include <algorithm>
+#include <cmath>
+#include <set>
+
+u32 hpowm(u32 a, uint64_t e, u32 q) {
+    uint64_t r = 1, b = a % q;
+    for (; e; e >>= 1) {
+        if (e & 1) r = r * b % q;
+        b = b * b % q;
+    }
+    return (u32)r;
+}
+u32 hinvm(u32 a, u32 q) { return hpowm(a, q - 2, q); }
+u32 hbitrev(u32 x, int bits) {
+    u32 r = 0;
+    for (int i = 0; i < bits; ++i, x >>= 1) r = (r << 1) | (x & 1);
+    return r;
+}
+
+// deterministic Miller-Rabin, exact for 32-bit n (bases 2, 7, 61)
+static bool prime32(u32 n) {
+    if (n < 2) return false;
+    for (u32 p : {2u, 3u, 5u, 7u, 11u, 13u, 17u, 19u, 23u, 29u, 31u, 37u}) {
+        if (n == p) return true;
+        if (n % p == 0) return false;
+    }
+    u32 d = n - 1;
+    int s = 0;
+    while (!(d & 1)) d >>= 1, ++s;
+    for (u32 a : {2u, 7u, 61u}) {
+        uint64_t x = hpowm(a, d, n);
+        if (x == 1 || x == n - 1) continue;
+        bool witness = true;
+        for (int r = 1; r < s && witness; ++r) {
+            x = x * x % n;
+            if (x == n - 1) witness = false;
+        }
+        if (witness) return false;
+    }
+    return true;
+}
+
+// first c = x^((q-1)/2N), x = 2, 3, ... with c^N = -1
+static u32 root_2n(u32 q, int logn) {
+    uint64_t two_n = 2ull << logn;
+    for (u32 x = 2;; ++x) {
+        u32 c = hpowm(x, (q - 1) / two_n, q);
+        if (hpowm(c, two_n / 2, q) == q - 1) return c;
+    }
+}
+
+std::string HostParams::build(int logn_, int L_, int dnum_, uint64_t seed_) {
+    if (logn_ < 10 || logn_ > 17) return "log_n must lie in [10, 17]";
+    if (L_ < 1 || L_ > 60) return "max_level must lie in [1, 60]";
+    if (dnum_ < 1) return "dnum must be >= 1";
+    logn = logn_; n = 1 << logn; L = L_; dnum = dnum_; seed = seed_;
+    n_q = L + 3;
+    n_ks = L + 2;
+    alpha = (n_ks + dnum - 1) / dnum;
+    n_p = alpha;
+    mod.assign(n_tot(), 0);
+
+    const uint64_t kMax = 1431655765ull;  // floor(2^32 / 3): keeps 3q < 2^32
+    const uint64_t kMin = 1ull << 30;     // q > 2^30: Barrett mu fits 32 bits
+    const uint64_t two_n = 2ull << logn;
+    std::set<u32> taken;
+
+    // largest admissible primes: 2 base, alpha special, 1 encryption
+    std::vector<u32> top;
+    for (uint64_t c = (kMax - 1) / two_n * two_n + 1; top.size() < (size_t)(2 + alpha + 1); c -= two_n) {
+        if (c <= kMin) return "ran out of NTT-friendly primes";
+        if (c < kMax && prime32((u32)c)) top.push_back((u32)c);
+    }
+    mod[0] = top[0];
+    mod[1] = top[1];
+    for (int k = 0; k < alpha; ++k) mod[n_q + k] = top[2 + k];
+    mod[n_q - 1] = top[2 + alpha];
+    taken.insert(top.begin(), top.end());
+
+    // rescaling chain: delta_L = 1.25 * 2^30; limb l+1 = prime closest to delta_l^2 / target
+    const double kTarget = 1342177280.0;
+    delta.assign(L + 1, 0.0);
+    delta[L] = kTarget;
+    for (int l = L; l >= 1; --l) {
+        const double want = delta[l] * delta[l] / kTarget;
+        const int64_t centre = (int64_t)((want - 1.0) / (double)two_n + 0.5) * (int64_t)two_n + 1;
+        u32 best = 0;
+        double best_d = 1e300;
+        for (int64_t s = 0; s < 100000; ++s) {
+            for (int sg : {-1, 1}) {
+                int64_t c = centre + sg * s * (int64_t)two_n;
+                if (c <= (int64_t)kMin || c >= (int64_t)kMax) continue;
+                if (!prime32((u32)c) || taken.count((u32)c)) continue;
+                double d = std::fabs((double)c - want);
+                if (d < best_d || (d == best_d && (u32)c < best)) { best_d = d; best = (u32)c; }
+            }
+            if (best && (double)s * (double)two_n > best_d + (double)two_n) break;
+        }
+        if (!best) return "could not place a rescaling prime";
+        mod[l + 1] = best;
+        taken.insert(best);
+        delta[l - 1] = delta[l] * delta[l] / (double)best;
+    }
+    psi.resize(n_tot());
+    for (int i = 0; i < n_tot(); ++i) psi[i] = root_2n(mod[i], logn);
+    return "";
+}

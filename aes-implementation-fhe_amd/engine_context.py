@@ -1,0 +1,155 @@
+"""EngineContext -- drop-in of the reference adapter (REF/engine_context.py:6-204) over
+the MI355X engine (mi355x_ckks, a ctypes binding of libaesfhe.so).
+
+Same constructor keywords, same methods, same error-string behaviour; the AES round
+modules only ever talk to this object.  Extra keywords: ``log_n`` (N = 2^log_n, default
+2^16 as in the reference harness; config 1 of BASELINE.json uses 2^15), ``dnum`` and
+``seed`` (deterministic key material).
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+from mi355x_ckks import Ciphertext, Engine, Plaintext
+
+_SIG_DEFAULT_LEVEL = 17
+
+
+class EngineContext:
+    def __init__(self, signature: int, *, max_level: int = 17, use_bootstrap: bool = True,
+                 use_multiparty: bool = False, mode: str = "cpu", device_id: int = 0,
+                 thread_count: int | None = None, log_n: int = 16, dnum: int = 3, seed: int = 0x5EED):
+        # REF/engine_context.py:17-42: signature selects the engine constructor form
+        if signature == 1:
+            kw = dict(use_bootstrap=use_bootstrap, max_level=_SIG_DEFAULT_LEVEL)
+        elif signature == 2:
+            kw = dict(max_level=max_level)
+        elif signature == 3:
+            kw = dict(max_level=_SIG_DEFAULT_LEVEL)
+        else:
+            raise ValueError(f"Unsupported signature: {signature}")
+        self.signature = signature
+        self.engine = Engine(mode=mode, use_multiparty=use_multiparty, thread_count=thread_count or 0,
+                             device_id=device_id, log_n=log_n, dnum=dnum, seed=seed, **kw)
+        eng = self.engine
+        # REF/engine_context.py:44-50
+        self.secret_key = eng.create_secret_key()
+        self.public_key = eng.create_public_key(self.secret_key)
+        self.relinearization_key = eng.create_relinearization_key(self.secret_key)
+        self.conjugation_key = eng.create_conjugation_key(self.secret_key)
+        self.rotation_key = eng.create_rotation_key(self.secret_key)
+        self.bootstrap_key = eng.create_bootstrap_key(self.secret_key)
+        self._bs_count = 0
+        self._bs_total_s = 0.0
+
+    # -------------------------------------------------------------- codec
+    def encrypt(self, data: np.ndarray):
+        return self.engine.encrypt(data, self.public_key)
+
+    def decrypt(self, ct) -> np.ndarray:
+        return self.engine.decrypt(ct, self.secret_key)
+
+    def encode(self, vec: np.ndarray):
+        return self.engine.encode(vec)
+
+    # -------------------------------------------------------------- arithmetic
+    def multiply(self, a, b):
+        """ct x ct -> relinearised product; otherwise ct x plaintext/scalar (REF :65-68)."""
+        if isinstance(a, Ciphertext) and isinstance(b, Ciphertext):
+            return self.engine.multiply(a, b, self.relinearization_key)
+        return self.engine.multiply(a, b)
+
+    def add(self, a, b):
+        return self.engine.add(a, b)
+
+    def sub(self, a, b):
+        return self.engine.subtract(a, b)
+
+    def _full(self, val):
+        if np.isscalar(val):
+            return np.full(self.engine.slot_count, val, dtype=np.complex128)
+        return np.asarray(val, dtype=np.complex128)
+
+    def add_plain(self, ct, val):
+        """Scalar or vector plaintext addition; complex values go through encode (REF :76-98)."""
+        if np.iscomplexobj(val):
+            return self.engine.add(ct, self.engine.encode(self._full(val)))
+        try:
+            return self.engine.add_plain(ct, float(val))
+        except (TypeError, ValueError):
+            return self.engine.add(ct, self.engine.encode(self._full(val)))
+
+    def multiply_plain(self, ct, val):
+        """Scalar (real or complex) or vector plaintext product (REF :106-125)."""
+        if np.isscalar(val):
+            if np.iscomplexobj(val):
+                return self.engine.multiply(ct, self.engine.encode(self._full(val)))
+            return self.engine.multiply(ct, float(val))
+        arr = np.asarray(val)
+        return self.engine.multiply(ct, self.engine.encode(arr.astype(np.complex128 if np.iscomplexobj(arr) else np.float64)))
+
+    def make_power_basis(self, ct, degree: int):
+        return self.engine.make_power_basis(ct, degree, self.relinearization_key)
+
+    def conjugate(self, ct):
+        return self.engine.conjugate(ct, self.conjugation_key)
+
+    def rotate(self, ct, steps: int):
+        """np.roll(slots, steps) semantics."""
+        return self.engine.rotate(ct, self.rotation_key, steps)
+
+    def relinearize(self, ct):
+        """Relinearise degree-2 ciphertexts; a degree-1 ciphertext comes back as is (REF :134-145)."""
+        try:
+            return self.engine.relinearize(ct, self.relinearization_key)
+        except RuntimeError as err:
+            if "should have 3 polynomials" in str(err):
+                return ct
+            raise
+
+    # -------------------------------------------------------------- bootstrap
+    def bootstrap(self, ct):
+        t0 = time.perf_counter()
+        out = self.engine.bootstrap(ct, self.relinearization_key, self.conjugation_key, self.bootstrap_key)
+        self._bs_count += 1
+        self._bs_total_s += time.perf_counter() - t0
+        return out
+
+    def bootstrap_stats(self):
+        n = self._bs_count
+        return {"count": n, "total_s": self._bs_total_s, "avg_s": self._bs_total_s / n if n else 0.0}
+
+    def reset_bootstrap_stats(self):
+        self._bs_count = 0
+        self._bs_total_s = 0
+
+    # -------------------------------------------------------------- representation
+    def to_ntt(self, x):
+        return self.engine.ntt(x)
+
+    def to_intt(self, x):
+        return self.engine.intt(x)
+
+    def make_power_basis_safe(self, ct, deg):
+        """Retry after INTT on an "NTT" complaint, bootstrap on a level complaint (REF :180-195)."""
+        try:
+            return self.engine.make_power_basis(ct, deg, self.relinearization_key)
+        except RuntimeError as err:
+            msg = str(err)
+            if "NTT" in msg:
+                return self.engine.make_power_basis(self.to_intt(ct), deg, self.relinearization_key)
+            if "level" in msg or "positive" in msg:
+                fresh = self.bootstrap(self.to_intt(ct))
+                return self.engine.make_power_basis(fresh, deg, self.relinearization_key)
+            raise
+
+    def bootstrap_safe(self, ct):
+        return self.engine.bootstrap(self.to_intt(ct), self.relinearization_key, self.conjugation_key,
+                                     self.bootstrap_key)
+
+    # -------------------------------------------------------------- MI355X extras
+    def renorm_pair(self, hi, lo):
+        """Device-side Zeta16 secret-key renorm of a (hi, lo) state pair (REF/pipeline.py:65-69)."""
+        return self.engine.renorm_pair(hi, lo)

@@ -1,0 +1,87 @@
+"""InvMixColumnsFHE: GF×14(x) ⊕ GF×11(r1) ⊕ GF×13(r2) ⊕ GF×9(r3)
+(REF/invmixcolumns_fhe.py:34-170), same rotation orientation as MixColFinal so the two
+are mutually inverse.  Renorm after each XOR pair when use_hard_renorm (default True).
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List
+
+from mixcol_final import _CoeffCache, gf_basis16, gf_poly_eval
+from shift_rows import row_masks
+from state_encoder import StateEncoder
+from xor4_lut import XOR4LUT
+
+
+class InvMixColumnsFHE:
+    def __init__(self, ctx, xor4: XOR4LUT, use_hard_renorm: bool = True):
+        self.ctx = ctx
+        self.xor4 = xor4
+        self.sc = ctx.engine.slot_count
+        self.stride = self.sc // 16
+        self._coeffs = _CoeffCache()
+        self.enc = StateEncoder(ctx)
+        self.use_hard_renorm = use_hard_renorm
+        self._pt_row: List[Any] = row_masks(ctx, self.sc)
+
+    def _basis16(self, ct):
+        return gf_basis16(self.ctx, ct)
+
+    def _poly2_eval(self, ct_hi, ct_lo, mult: int, which: str):
+        return gf_poly_eval(self.ctx, self._coeffs.load_plaintexts(self.ctx, mult, which), ct_hi, ct_lo)
+
+    def _xor(self, a, b):
+        return self.xor4.apply(a, b)
+
+    def _renorm_pair(self, hi, lo):
+        return self.enc.renorm(hi, lo) if self.use_hard_renorm else (hi, lo)
+
+    def _rot_rows_in_col(self, ct, k_rows: int):
+        """Masked per-row rotation by k*stride (REF :100-109; unused by __call__)."""
+        ctx = self.ctx
+        out = ctx.multiply(ct, 0.0)
+        for mask in self._pt_row:
+            out = ctx.add(out, ctx.rotate(ctx.multiply(ct, mask), k_rows * self.stride))
+        return out
+
+    def _gf(self, mult, hi, lo):
+        return self._poly2_eval(hi, lo, mult, "hi"), self._poly2_eval(hi, lo, mult, "lo")
+
+    def gf_mult_9(self, hi, lo):
+        return self._gf(9, hi, lo)
+
+    def gf_mult_11(self, hi, lo):
+        return self._gf(11, hi, lo)
+
+    def gf_mult_13(self, hi, lo):
+        return self._gf(13, hi, lo)
+
+    def gf_mult_14(self, hi, lo):
+        return self._gf(14, hi, lo)
+
+    def _col_shift_rowmajor(self, ct, k_up: int):
+        return self.ctx.rotate(ct, -4 * k_up * self.stride)
+
+    def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
+        log = (lambda k, v: debug.__setitem__(k, v)) if debug is not None else (lambda k, v: None)
+        rot = {k: (self._col_shift_rowmajor(ct_hi, k), self._col_shift_rowmajor(ct_lo, k)) for k in (1, 2, 3)}
+        for k in (1, 2, 3):
+            log(f"rotc{k}", rot[k])
+        e14 = self.gf_mult_14(ct_hi, ct_lo)
+        log("mul14", e14)
+        e11 = self.gf_mult_11(*rot[1])
+        log("mul11", e11)
+        e13 = self.gf_mult_13(*rot[2])
+        log("mul13", e13)
+        e9 = self.gf_mult_9(*rot[3])
+        log("mul9", e9)
+        acc = (self._xor(e14[0], e11[0]), self._xor(e14[1], e11[1]))
+        log("acc1", acc)
+        acc = self._renorm_pair(*acc)
+        acc = (self._xor(acc[0], e13[0]), self._xor(acc[1], e13[1]))
+        log("acc2", acc)
+        acc = self._renorm_pair(*acc)
+        out = self._renorm_pair(self._xor(acc[0], e9[0]), self._xor(acc[1], e9[1]))
+        if do_final_bootstrap:
+            out = (self.ctx.bootstrap(out[0]), self.ctx.bootstrap(out[1]))
+        log("out", out)
+        return out

@@ -1,0 +1,414 @@
+"""mi355x_ckks -- ctypes binding of libaesfhe.so, the MI355X-native RNS-CKKS engine.
+
+The classes mirror the part of ``desilofhe``'s API that the reference's adapter uses
+(REF/engine_context.py:1,17-204): ``Engine``, ``Ciphertext``, ``Plaintext`` and the key
+objects, with the same method names and argument meaning, so that
+``engine_context.EngineContext`` is a line-for-line drop-in of the reference adapter.
+
+There is no CPU fallback: constructing an ``Engine`` without the HIP library or without
+a visible GPU raises ``RuntimeError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import numbers
+from pathlib import Path
+from typing import List, Optional
+
+import numpy as np
+
+_PKG = Path(__file__).resolve().parent
+_LIB_PATH = _PKG / "libaesfhe.so"
+_lib = None
+
+_H = ctypes.c_uint64
+_Hp = ctypes.POINTER(ctypes.c_uint64)
+_dp = np.ctypeslib.ndpointer(dtype=np.float64, flags="C_CONTIGUOUS")
+_up = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
+
+EXPORTED = [
+    "aesfhe_create", "aesfhe_destroy", "aesfhe_last_error", "aesfhe_keygen", "aesfhe_slot_count",
+    "aesfhe_max_level", "aesfhe_info", "aesfhe_moduli", "aesfhe_scales", "aesfhe_sync", "aesfhe_free",
+    "aesfhe_level", "aesfhe_plaintext", "aesfhe_encrypt", "aesfhe_decrypt", "aesfhe_add", "aesfhe_sub",
+    "aesfhe_add_pt", "aesfhe_add_scalar", "aesfhe_mul_scalar", "aesfhe_mul_pt", "aesfhe_mul",
+    "aesfhe_relinearize", "aesfhe_rescale", "aesfhe_level_down", "aesfhe_rotate", "aesfhe_conjugate",
+    "aesfhe_power_basis", "aesfhe_to_ntt", "aesfhe_to_intt", "aesfhe_bootstrap", "aesfhe_renorm_pair",
+    "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
+    "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters",
+]
+
+COUNTER_NAMES = ["mul", "relin", "rot", "conj", "ptmul", "scalar", "rescale", "ntt_rows", "keyswitch",
+                 "encrypt", "decrypt", "bootstrap", "add"]
+
+
+def load_library(path: Optional[Path] = None):
+    """Load (never silently replace) the HIP engine library."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path) if path else _LIB_PATH
+    if not p.exists():
+        raise RuntimeError(f"MI355X engine library missing: {p} (run build_ext.py / __graft_entry__.build())")
+    L = ctypes.CDLL(str(p))
+    c_int, vp, c_dbl = ctypes.c_int, ctypes.c_void_p, ctypes.c_double
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    sig = {
+        "aesfhe_create": [pp, c_int, c_int, c_int, c_int, ctypes.c_uint64],
+        "aesfhe_destroy": [vp], "aesfhe_keygen": [vp], "aesfhe_slot_count": [vp], "aesfhe_max_level": [vp],
+        "aesfhe_info": [vp, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")],
+        "aesfhe_moduli": [vp, _up], "aesfhe_scales": [vp, _dp], "aesfhe_sync": [vp], "aesfhe_free": [vp, _H],
+        "aesfhe_level": [vp, _H, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)],
+        "aesfhe_plaintext": [vp, _dp, _dp, c_int, _Hp],
+        "aesfhe_encrypt": [vp, _dp, _dp, c_int, _Hp],
+        "aesfhe_decrypt": [vp, _H, _dp, _dp, c_int],
+        "aesfhe_add": [vp, _H, _H, _Hp], "aesfhe_sub": [vp, _H, _H, _Hp], "aesfhe_add_pt": [vp, _H, _H, _Hp],
+        "aesfhe_add_scalar": [vp, _H, c_dbl, c_dbl, _Hp], "aesfhe_mul_scalar": [vp, _H, c_dbl, c_dbl, _Hp],
+        "aesfhe_mul_pt": [vp, _H, _H, _Hp], "aesfhe_mul": [vp, _H, _H, c_int, _Hp],
+        "aesfhe_relinearize": [vp, _H, _Hp], "aesfhe_rescale": [vp, _H, _Hp],
+        "aesfhe_level_down": [vp, _H, c_int, _Hp], "aesfhe_rotate": [vp, _H, c_int, _Hp],
+        "aesfhe_conjugate": [vp, _H, _Hp], "aesfhe_power_basis": [vp, _H, c_int, _Hp],
+        "aesfhe_to_ntt": [vp, _H, _Hp], "aesfhe_to_intt": [vp, _H, _Hp], "aesfhe_bootstrap": [vp, _H, _Hp],
+        "aesfhe_renorm_pair": [vp, _H, _H, _Hp, _Hp],
+        "aesfhe_export": [vp, _H, _up, ctypes.c_uint64], "aesfhe_import": [vp, c_int, c_int, _up, _Hp],
+        "aesfhe_export_secret": [vp, _up], "aesfhe_export_pk": [vp, _up],
+        "aesfhe_export_ksk": [vp, ctypes.c_uint64, _up],
+        "aesfhe_debug_ntt": [vp, _up, c_int, c_int, c_int],
+        "aesfhe_debug_keyswitch": [vp, c_int, ctypes.c_uint64, _up, _up],
+        "aesfhe_counters": [vp, np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS"), c_int],
+        "aesfhe_reset_counters": [vp],
+    }
+    for name in EXPORTED:
+        fn = getattr(L, name)
+        fn.restype = ctypes.c_char_p if name == "aesfhe_last_error" else ctypes.c_int
+        fn.argtypes = [vp] if name == "aesfhe_last_error" else sig[name]
+    _lib = L
+    return L
+
+
+class _Context:
+    """Owns one aesfhe_ctx; destroyed when the last object referring to it dies."""
+
+    def __init__(self, log_n, max_level, dnum, device_id, seed):
+        self.lib = load_library()
+        ptr = ctypes.c_void_p()
+        rc = self.lib.aesfhe_create(ctypes.byref(ptr), log_n, max_level, dnum, device_id, seed)
+        self.ptr = ptr
+        if rc != 0:
+            msg = self.lib.aesfhe_last_error(ptr).decode() if ptr.value else "aesfhe_create failed"
+            if ptr.value:
+                self.lib.aesfhe_destroy(ptr)
+            self.ptr = None
+            raise RuntimeError(msg)
+
+    def check(self, rc):
+        if rc != 0:
+            raise RuntimeError(self.lib.aesfhe_last_error(self.ptr).decode())
+
+    def __del__(self):
+        if getattr(self, "ptr", None):
+            try:
+                self.lib.aesfhe_destroy(self.ptr)
+            except Exception:
+                pass
+            self.ptr = None
+
+
+class _Handle:
+    __slots__ = ("_ctx", "handle", "__weakref__")
+
+    def __init__(self, ctx: _Context, handle: int):
+        self._ctx = ctx
+        self.handle = handle
+
+    def __del__(self):
+        ctx = getattr(self, "_ctx", None)
+        if ctx is not None and ctx.ptr:
+            try:
+                ctx.lib.aesfhe_free(ctx.ptr, self.handle)
+            except Exception:
+                pass
+
+
+class Ciphertext(_Handle):
+    """Device-resident RNS-CKKS ciphertext (opaque handle)."""
+
+    __slots__ = ()
+
+    @property
+    def level(self) -> int:
+        lv, npoly = ctypes.c_int32(), ctypes.c_int32()
+        self._ctx.check(self._ctx.lib.aesfhe_level(self._ctx.ptr, self.handle, ctypes.byref(lv), ctypes.byref(npoly)))
+        return lv.value
+
+    @property
+    def num_polys(self) -> int:
+        lv, npoly = ctypes.c_int32(), ctypes.c_int32()
+        self._ctx.check(self._ctx.lib.aesfhe_level(self._ctx.ptr, self.handle, ctypes.byref(lv), ctypes.byref(npoly)))
+        return npoly.value
+
+
+class Plaintext(_Handle):
+    """Encoded slot vector; encoded at the level of the ciphertext it meets."""
+
+    __slots__ = ()
+
+
+class _Key:
+    def __init__(self, kind: str):
+        self.kind = kind
+
+
+class SecretKey(_Key):
+    pass
+
+
+class PublicKey(_Key):
+    pass
+
+
+class RelinearizationKey(_Key):
+    pass
+
+
+class ConjugationKey(_Key):
+    pass
+
+
+class RotationKey(_Key):
+    pass
+
+
+class BootstrapKey(_Key):
+    pass
+
+
+def _complex_vec(data, n: int):
+    a = np.asarray(data)
+    if a.ndim == 0:
+        a = np.full(n, a.item(), dtype=np.complex128)
+    a = a.astype(np.complex128, copy=False).ravel()
+    if a.size > n:
+        raise ValueError(f"vector of length {a.size} exceeds slot_count {n}")
+    re = np.zeros(n)
+    im = np.zeros(n)
+    re[: a.size] = a.real
+    im[: a.size] = a.imag
+    return re, im
+
+
+class Engine:
+    """RNS-CKKS engine on one MI355X (desilofhe.Engine-shaped, REF/engine_context.py:17-39).
+
+    ``mode`` and ``thread_count`` are accepted for API compatibility; the engine always
+    runs on HIP device ``device_id``.
+    """
+
+    def __init__(self, *, mode: str = "gpu", use_bootstrap: bool = False, use_multiparty: bool = False,
+                 thread_count: int = 0, device_id: int = 0, max_level: int = 17, log_n: int = 16,
+                 dnum: int = 3, seed: int = 0x5EED):
+        if use_multiparty:
+            raise ValueError("multiparty key generation is not supported")
+        self.mode = mode
+        self.use_bootstrap = use_bootstrap
+        self._ctx = _Context(log_n, max_level, dnum, device_id, seed)
+        L = self._ctx.lib
+        self.slot_count = int(L.aesfhe_slot_count(self._ctx.ptr))
+        self.max_level = int(L.aesfhe_max_level(self._ctx.ptr))
+        info = np.zeros(8, np.int32)
+        self._ctx.check(L.aesfhe_info(self._ctx.ptr, info))
+        self.n, self.L, self.n_q, self.n_ks, self.n_p, self.alpha, self.dnum, self.log_n = map(int, info)
+        self._keys_ready = False
+
+    # ------------------------------------------------------------------ internals
+    @property
+    def _lib(self):
+        return self._ctx.lib
+
+    def _new(self, fn, *args, cls=Ciphertext):
+        h = ctypes.c_uint64()
+        self._ctx.check(fn(self._ctx.ptr, *args, ctypes.byref(h)))
+        return cls(self._ctx, h.value)
+
+    def _ensure_keys(self):
+        if not self._keys_ready:
+            self._ctx.check(self._lib.aesfhe_keygen(self._ctx.ptr))
+            self._keys_ready = True
+
+    # ------------------------------------------------------------------ keys
+    def create_secret_key(self):
+        self._ensure_keys()
+        return SecretKey("secret")
+
+    def create_public_key(self, sk=None):
+        self._ensure_keys()
+        return PublicKey("public")
+
+    def create_relinearization_key(self, sk=None):
+        self._ensure_keys()
+        return RelinearizationKey("relin")
+
+    def create_conjugation_key(self, sk=None):
+        self._ensure_keys()
+        return ConjugationKey("conj")
+
+    def create_rotation_key(self, sk=None):
+        """Rotation keys are generated on the device on first use of each rotation amount."""
+        self._ensure_keys()
+        return RotationKey("rotation")
+
+    def create_bootstrap_key(self, sk=None):
+        self._ensure_keys()
+        return BootstrapKey("bootstrap")
+
+    # ------------------------------------------------------------------ codec
+    def encode(self, vec) -> Plaintext:
+        re, im = _complex_vec(vec, self.slot_count)
+        return self._new(self._lib.aesfhe_plaintext, re, im, self.slot_count, cls=Plaintext)
+
+    def encrypt(self, data, pk=None) -> Ciphertext:
+        self._ensure_keys()
+        re, im = _complex_vec(data, self.slot_count)
+        return self._new(self._lib.aesfhe_encrypt, re, im, self.slot_count)
+
+    def decrypt(self, ct: Ciphertext, sk=None) -> np.ndarray:
+        re = np.zeros(self.slot_count)
+        im = np.zeros(self.slot_count)
+        self._ctx.check(self._lib.aesfhe_decrypt(self._ctx.ptr, ct.handle, re, im, self.slot_count))
+        return re + 1j * im
+
+    # ------------------------------------------------------------------ arithmetic
+    def add(self, a, b):
+        if isinstance(b, Ciphertext):
+            return self._new(self._lib.aesfhe_add, a.handle, b.handle)
+        if isinstance(b, Plaintext):
+            return self._new(self._lib.aesfhe_add_pt, a.handle, b.handle)
+        if isinstance(b, numbers.Number):
+            v = complex(b)
+            return self._new(self._lib.aesfhe_add_scalar, a.handle, v.real, v.imag)
+        return self.add(a, self.encode(b))
+
+    def subtract(self, a, b):
+        if isinstance(b, Ciphertext):
+            return self._new(self._lib.aesfhe_sub, a.handle, b.handle)
+        if isinstance(b, numbers.Number):
+            return self.add(a, -complex(b))
+        return self.add(a, self.encode(-np.asarray(b, dtype=np.complex128)))
+
+    def add_plain(self, ct, val):
+        return self.add(ct, complex(val) if np.isscalar(val) else val)
+
+    def multiply(self, a, b, relinearization_key=None):
+        if isinstance(a, Ciphertext) and isinstance(b, Ciphertext):
+            return self._new(self._lib.aesfhe_mul, a.handle, b.handle, 1 if relinearization_key is not None else 0)
+        if isinstance(a, (Plaintext, numbers.Number)) and isinstance(b, Ciphertext):
+            a, b = b, a
+        if isinstance(b, Plaintext):
+            return self._new(self._lib.aesfhe_mul_pt, a.handle, b.handle)
+        if isinstance(b, numbers.Number):
+            v = complex(b)
+            return self._new(self._lib.aesfhe_mul_scalar, a.handle, v.real, v.imag)
+        return self.multiply(a, self.encode(b))
+
+    def relinearize(self, ct, relinearization_key=None):
+        return self._new(self._lib.aesfhe_relinearize, ct.handle)
+
+    def rescale(self, ct):
+        return self._new(self._lib.aesfhe_rescale, ct.handle)
+
+    def level_down(self, ct, level: int):
+        return self._new(self._lib.aesfhe_level_down, ct.handle, int(level))
+
+    def make_power_basis(self, ct, degree: int, relinearization_key=None) -> List[Ciphertext]:
+        out = (ctypes.c_uint64 * int(degree))()
+        self._ctx.check(self._lib.aesfhe_power_basis(self._ctx.ptr, ct.handle, int(degree), out))
+        return [Ciphertext(self._ctx, out[i]) for i in range(int(degree))]
+
+    def conjugate(self, ct, conjugation_key=None):
+        return self._new(self._lib.aesfhe_conjugate, ct.handle)
+
+    def rotate(self, ct, rotation_key=None, delta: int = 0):
+        """np.roll(slots, delta)."""
+        return self._new(self._lib.aesfhe_rotate, ct.handle, int(delta))
+
+    def bootstrap(self, ct, relinearization_key=None, conjugation_key=None, bootstrap_key=None):
+        return self._new(self._lib.aesfhe_bootstrap, ct.handle)
+
+    def ntt(self, ct):
+        return self._new(self._lib.aesfhe_to_ntt, ct.handle)
+
+    def intt(self, ct):
+        return self._new(self._lib.aesfhe_to_intt, ct.handle)
+
+    def renorm_pair(self, hi, lo):
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        self._ctx.check(self._lib.aesfhe_renorm_pair(self._ctx.ptr, hi.handle, lo.handle, ctypes.byref(a), ctypes.byref(b)))
+        return Ciphertext(self._ctx, a.value), Ciphertext(self._ctx, b.value)
+
+    def sync(self):
+        self._ctx.check(self._lib.aesfhe_sync(self._ctx.ptr))
+
+    # ------------------------------------------------------------------ raw access (tests)
+    def moduli(self) -> np.ndarray:
+        out = np.zeros(self.n_q + self.n_p, np.uint32)
+        self._ctx.check(self._lib.aesfhe_moduli(self._ctx.ptr, out))
+        return out
+
+    def scales(self) -> np.ndarray:
+        out = np.zeros(self.L + 1, np.float64)
+        self._ctx.check(self._lib.aesfhe_scales(self._ctx.ptr, out))
+        return out
+
+    def export(self, ct: Ciphertext) -> np.ndarray:
+        npoly = ct.num_polys
+        out = np.zeros((npoly, ct.level + 2, self.n), np.uint32)
+        self._ctx.check(self._lib.aesfhe_export(self._ctx.ptr, ct.handle, out, out.size))
+        return out
+
+    def import_ct(self, data: np.ndarray, level: int) -> Ciphertext:
+        data = np.ascontiguousarray(data, np.uint32)
+        return self._new(self._lib.aesfhe_import, int(level), int(data.shape[0]), data)
+
+    def export_secret(self) -> np.ndarray:
+        self._ensure_keys()
+        out = np.zeros((self.n_q + self.n_p, self.n), np.uint32)
+        self._ctx.check(self._lib.aesfhe_export_secret(self._ctx.ptr, out))
+        return out
+
+    def export_pk(self) -> np.ndarray:
+        self._ensure_keys()
+        out = np.zeros((2, self.n_q, self.n), np.uint32)
+        self._ctx.check(self._lib.aesfhe_export_pk(self._ctx.ptr, out))
+        return out
+
+    def export_ksk(self, galois: int) -> np.ndarray:
+        self._ensure_keys()
+        out = np.zeros((self.dnum, 2, self.n_ks + self.n_p, self.n), np.uint32)
+        self._ctx.check(self._lib.aesfhe_export_ksk(self._ctx.ptr, int(galois), out))
+        return out
+
+    def debug_ntt(self, rows: np.ndarray, first_prime: int, inverse: bool = False) -> np.ndarray:
+        d = np.ascontiguousarray(rows, np.uint32).copy()
+        self._ctx.check(self._lib.aesfhe_debug_ntt(self._ctx.ptr, d, d.shape[0], int(first_prime), int(inverse)))
+        return d
+
+    def debug_keyswitch(self, level: int, galois: int, d: np.ndarray) -> np.ndarray:
+        self._ensure_keys()
+        out = np.zeros((2, level + 2, self.n), np.uint32)
+        self._ctx.check(self._lib.aesfhe_debug_keyswitch(self._ctx.ptr, int(level), int(galois),
+                                                         np.ascontiguousarray(d, np.uint32), out))
+        return out
+
+    def counters(self) -> dict:
+        out = np.zeros(len(COUNTER_NAMES), np.uint64)
+        self._ctx.check(self._lib.aesfhe_counters(self._ctx.ptr, out, len(COUNTER_NAMES)))
+        return dict(zip(COUNTER_NAMES, map(int, out)))
+
+    def reset_counters(self):
+        self._ctx.check(self._lib.aesfhe_reset_counters(self._ctx.ptr))
+
+    def galois_rotate(self, steps: int) -> int:
+        return pow(5, (-steps) % self.slot_count, 2 * self.n)
+
+    @property
+    def galois_conj(self) -> int:
+        return 2 * self.n - 1

@@ -1,0 +1,120 @@
+"""MixColFinal: "MixColumns" as GF×2(x) ⊕ GF×3(r1) ⊕ r2 ⊕ r3 (REF/mixcol_final.py:40-165).
+
+r_k = rotate(x, -4k*stride) shifts every row left by k columns under column-first
+packing, so the output is out[r,c] = 2a[r,c] ^ 3a[r,c+1] ^ a[r,c+2] ^ a[r,c+3] -- the
+reference's orientation, reproduced as is.  GF multipliers are
+bivariate LUTs over (hi, lo); each XOR pair is followed by a secret-key renorm and the
+result is bootstrapped (do_final_bootstrap, default True).
+"""
+from __future__ import annotations
+
+import json
+from typing import Any, Dict, Tuple
+
+import numpy as np
+
+from lut import COEFF_DIR, ensure_coeffs
+from state_encoder import StateEncoder
+from xor4_lut import XOR4LUT
+
+
+class _CoeffCache:
+    """gf_mult{k}_{hi|lo} plaintext coefficients, encoded once per engine (REF :19-37)."""
+
+    def __init__(self, coeff_dir=COEFF_DIR):
+        self.dir = coeff_dir
+        self.pt_cache: Dict[Tuple[int, str], Dict[Tuple[int, int], Any]] = {}
+
+    def load_plaintexts(self, ctx, mult: int, which: str):
+        key = (mult, which)
+        if key not in self.pt_cache:
+            path = ensure_coeffs(self.dir) / f"gf_mult{mult}_{which}_coeffs.json"
+            sc = ctx.engine.slot_count
+            self.pt_cache[key] = {(p, q): ctx.encode(np.full(sc, complex(re, im), dtype=np.complex128))
+                                  for p, q, re, im in json.loads(path.read_text(encoding="utf-8"))["entries"]}
+        return self.pt_cache[key]
+
+
+def gf_basis16(ctx, ct) -> Dict[int, Any]:
+    """REF/mixcol_final.py:64-77 (bootstrap fallback only; zero via multiply by 0.0)."""
+    try:
+        pos = ctx.make_power_basis(ct, 8)
+    except RuntimeError:
+        ct = ctx.bootstrap(ct)
+        pos = ctx.make_power_basis(ct, 8)
+    basis = {0: ctx.add_plain(ctx.multiply(ct, 0.0), 1.0)}
+    basis.update({k: pos[k - 1] for k in range(1, 9)})
+    basis.update({k: ctx.conjugate(pos[15 - k]) for k in range(9, 16)})
+    return basis
+
+
+def gf_poly_eval(ctx, coeffs, ct_hi, ct_lo) -> Any:
+    """Σ c[p,q] X^p Y^q over the hi / lo bases (REF/mixcol_final.py:80-91)."""
+    bx, by = gf_basis16(ctx, ct_hi), gf_basis16(ctx, ct_lo)
+    acc = ctx.multiply(ct_hi, 0.0)
+    for (p, q), pt in coeffs.items():
+        acc = ctx.add(acc, ctx.multiply(ctx.multiply(bx[p], by[q]), pt))
+    return acc
+
+
+class MixColFinal:
+    def __init__(self, ctx, xor4: XOR4LUT, stride: int | None = None):
+        self.ctx = ctx
+        self.xor4 = xor4
+        self.sc = ctx.engine.slot_count
+        self.stride = stride if stride is not None else self.sc // 16
+        self._coeffs = _CoeffCache()
+        self.enc = StateEncoder(ctx)
+        self._zero = None
+
+    # zero-state pair, built lazily (REF :58-62 builds it eagerly; only _normalize_via_xor_zero uses it)
+    def _normalize_via_xor_zero(self, ct, which: str):
+        if self._zero is None:
+            self._zero = self.enc.encode(np.zeros(16, dtype=np.uint8))
+        return self._xor_ct(ct, self._zero[0] if which == "hi" else self._zero[1])
+
+    def _basis16(self, ct):
+        return gf_basis16(self.ctx, ct)
+
+    def _gf_poly_eval_2var(self, ct_hi, ct_lo, mult: int, which: str):
+        return gf_poly_eval(self.ctx, self._coeffs.load_plaintexts(self.ctx, mult, which), ct_hi, ct_lo)
+
+    def gf_mult_2(self, ct_hi, ct_lo):
+        return self._gf_poly_eval_2var(ct_hi, ct_lo, 2, "hi"), self._gf_poly_eval_2var(ct_hi, ct_lo, 2, "lo")
+
+    def gf_mult_3(self, ct_hi, ct_lo):
+        return self._gf_poly_eval_2var(ct_hi, ct_lo, 3, "hi"), self._gf_poly_eval_2var(ct_hi, ct_lo, 3, "lo")
+
+    def _col_shift_rowmajor(self, ct, k_up: int):
+        return self.ctx.rotate(ct, -4 * k_up * self.stride)
+
+    def _renorm_pair(self, hi, lo):
+        return self.enc.renorm(hi, lo)
+
+    def _xor_ct(self, a, b):
+        return self.xor4.apply(a, b)
+
+    def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
+        log = (lambda k, v: debug.__setitem__(k, v)) if isinstance(debug, dict) else (lambda k, v: None)
+        rot = {k: (self._col_shift_rowmajor(ct_hi, k), self._col_shift_rowmajor(ct_lo, k)) for k in (1, 2, 3)}
+        for k in (1, 2, 3):
+            log(f"rotc{k}", rot[k])
+        log("in", (ct_hi, ct_lo))
+        two = self.gf_mult_2(ct_hi, ct_lo)
+        thr = self.gf_mult_3(*rot[1])
+        log("two", two)
+        log("thr", thr)
+        acc = (self._xor_ct(two[0], thr[0]), self._xor_ct(two[1], thr[1]))
+        log("acc1", acc)
+        acc = self._renorm_pair(*acc)
+        acc = (self._xor_ct(acc[0], rot[2][0]), self._xor_ct(acc[1], rot[2][1]))
+        log("acc2", acc)
+        acc = self._renorm_pair(*acc)
+        acc = self._renorm_pair(self._xor_ct(acc[0], rot[3][0]), self._xor_ct(acc[1], rot[3][1]))
+        log("acc3", acc)
+        out_hi, out_lo = acc
+        if do_final_bootstrap:
+            out_hi = self.ctx.bootstrap(self.ctx.to_intt(out_hi))
+            out_lo = self.ctx.bootstrap(self.ctx.to_intt(out_lo))
+            log("out", (out_hi, out_lo))
+        return out_hi, out_lo

@@ -1,0 +1,154 @@
+"""AESPipeline: AES-128 round orchestration on CKKS/Zeta16 (REF/pipeline.py:17-254).
+
+Drop-in for the reference class: same constructor, same coefficient keys ('xor4',
+'sub_hi', 'sub_lo', 'inv_sub_hi', 'inv_sub_lo'), same step order, optional renorm
+between steps, per-stage debug snapshots.
+
+Documented deviation: the shipped decrypt (REF/pipeline.py:230-237)
+never applies InvMixColumns, so it cannot invert encrypt.  ``decrypt`` here inserts it
+after AddRoundKey as the reference README prescribes (REF/README.md:87-94);
+``with_inv_mix_columns=False`` reproduces the shipped order.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List, Tuple
+
+import numpy as np
+
+from add_round_key import AddRoundKey
+from invmixcolumns_fhe import InvMixColumnsFHE
+from inv_shiftrows import InvShiftRows
+from mixcol_final import MixColFinal
+from shift_rows import ShiftRows
+from state_encoder import StateEncoder
+from sub_bytes_lut import SubBytesLUT
+from xor4_lut import XOR4LUT
+
+
+class AESPipeline:
+    def __init__(self, ctx, coeffs: Dict[str, Any], *, mixcolumns: MixColFinal | None = None,
+                 inv_mixcolumns: InvMixColumnsFHE | None = None, use_hard_renorm_between_steps: bool = False,
+                 with_inv_mix_columns: bool = True):
+        self.ctx = ctx
+        self.encoder = StateEncoder(ctx)
+        self.sc = ctx.engine.slot_count
+        self.stride = self.sc // 16
+        self.xor4 = XOR4LUT(ctx, coeffs["xor4"])
+        self.sub = SubBytesLUT(ctx, coeffs["sub_hi"], coeffs["sub_lo"])
+        self.isub = SubBytesLUT(ctx, coeffs["inv_sub_hi"], coeffs["inv_sub_lo"]) if "inv_sub_hi" in coeffs else None
+        self.shift = ShiftRows(ctx)
+        self.invshift = InvShiftRows(ctx)
+        self.mix = mixcolumns if mixcolumns is not None else MixColFinal(ctx, self.xor4)
+        self.invmix = inv_mixcolumns if inv_mixcolumns is not None else InvMixColumnsFHE(ctx, self.xor4)
+        self.ark = AddRoundKey(self.xor4)
+        self.use_hard_renorm_between_steps = use_hard_renorm_between_steps
+        self.with_inv_mix_columns = with_inv_mix_columns
+        self._rk_cache: List[Tuple[Any, Any]] | None = None
+
+    # ---------------------------------------------------------------- utils
+    def _renorm_pair(self, hi, lo):
+        return self.encoder.renorm(hi, lo) if self.use_hard_renorm_between_steps else (hi, lo)
+
+    def _encode_key(self, key_bytes: np.ndarray):
+        assert key_bytes.shape == (16,)
+        return self.encoder.encode(key_bytes.astype(np.uint8))
+
+    def _prepare_round_keys(self, round_keys: List[np.ndarray]):
+        if self._rk_cache is None or len(self._rk_cache) != len(round_keys):
+            self._rk_cache = [self._encode_key(np.asarray(k, dtype=np.uint8)) for k in round_keys]
+        return self._rk_cache
+
+    def _log_pair(self, dbg, tag: str, ct_hi, ct_lo, **meta) -> None:
+        if dbg is None:
+            return
+        entry = {"ct_hi": ct_hi, "ct_lo": ct_lo, "meta": meta}
+        try:
+            entry["plain"] = self.encoder.decode(ct_hi, ct_lo)
+        except Exception as err:  # keep the snapshot, record why decoding failed
+            entry["plain"] = None
+            entry["plain_err"] = repr(err)
+        dbg[tag] = entry
+
+    # ---------------------------------------------------------------- steps
+    def add_round_key(self, ct_hi, ct_lo, key_hi, key_lo):
+        return self.ark(ct_hi, ct_lo, key_hi, key_lo)
+
+    def sub_bytes(self, ct_hi, ct_lo):
+        return self.sub.apply(ct_hi, ct_lo)
+
+    def inv_sub_bytes(self, ct_hi, ct_lo):
+        if self.isub is None:
+            raise KeyError("inv_sub_hi")
+        return self.isub.apply(ct_hi, ct_lo)
+
+    def shift_rows(self, ct_hi, ct_lo):
+        return self.shift.apply(ct_hi, ct_lo)
+
+    def inv_shift_rows(self, ct_hi, ct_lo):
+        return self.invshift.apply(ct_hi, ct_lo)
+
+    def mix_columns(self, ct_hi, ct_lo):
+        return self.mix(ct_hi, ct_lo)
+
+    def inv_mix_columns(self, ct_hi, ct_lo):
+        return self.invmix(ct_hi, ct_lo)
+
+    # ---------------------------------------------------------------- encrypt
+    def encrypt_round(self, ct, key_pair):
+        """One middle round r = 1..9: SB, renorm, SR, MC, ARK, renorm (REF :142-151)."""
+        ct = self._renorm_pair(*self.sub_bytes(*ct))
+        ct = self.shift_rows(*ct)
+        ct = self.mix_columns(*ct)
+        return self._renorm_pair(*self.add_round_key(*ct, *key_pair))
+
+    def encrypt(self, state: np.ndarray, round_keys: List[np.ndarray], debug: Dict[str, Any] | None = None):
+        if debug is not None:
+            debug.clear()
+        ct = self.encoder.encode(np.asarray(state, dtype=np.uint8))
+        self._log_pair(debug, "enc.input", *ct)
+        rk = self._prepare_round_keys(round_keys)
+        ct = self.add_round_key(*ct, *rk[0])
+        self._log_pair(debug, "enc.r0.ark", *ct)
+        ct = self._renorm_pair(*ct)
+        self._log_pair(debug, "enc.r0.renorm", *ct)
+        for r in range(1, 10):
+            ct = self.encrypt_round(ct, rk[r])
+        ct = self.sub_bytes(*ct)
+        self._log_pair(debug, "enc.final.sub", *ct)
+        ct = self._renorm_pair(*ct)
+        self._log_pair(debug, "enc.final.sub.renorm", *ct)
+        ct = self.shift_rows(*ct)
+        self._log_pair(debug, "enc.final.sr", *ct)
+        ct = self.add_round_key(*ct, *rk[10])
+        self._log_pair(debug, "enc.final.ark10", *ct)
+        ct = self._renorm_pair(*ct)
+        self._log_pair(debug, "enc.output", *ct)
+        return ct
+
+    # ---------------------------------------------------------------- decrypt
+    def decrypt(self, ct_hi, ct_lo, round_keys: List[np.ndarray], debug: Dict[str, Any] | None = None):
+        if debug is not None:
+            debug.clear()
+        rk = self._prepare_round_keys(round_keys)
+        self._log_pair(debug, "dec.input", ct_hi, ct_lo)
+        ct = self.add_round_key(ct_hi, ct_lo, *rk[10])
+        self._log_pair(debug, "dec.init.ark10", *ct)
+        ct = self._renorm_pair(*ct)
+        self._log_pair(debug, "dec.init.ark10.renorm", *ct)
+        for r in range(9, 0, -1):
+            ct = self.inv_shift_rows(*ct)
+            ct = self._renorm_pair(*self.inv_sub_bytes(*ct))
+            ct = self._renorm_pair(*self.add_round_key(*ct, *rk[r]))
+            if self.with_inv_mix_columns:
+                ct = self.inv_mix_columns(*ct)
+        ct = self.inv_shift_rows(*ct)
+        self._log_pair(debug, "dec.final.isr", *ct)
+        ct = self.inv_sub_bytes(*ct)
+        self._log_pair(debug, "dec.final.isb", *ct)
+        ct = self._renorm_pair(*ct)
+        self._log_pair(debug, "dec.final.isb.renorm", *ct)
+        ct = self.add_round_key(*ct, *rk[0])
+        self._log_pair(debug, "dec.final.ark0", *ct)
+        ct = self._renorm_pair(*ct)
+        self._log_pair(debug, "dec.output", *ct)
+        return ct

@@ -1,0 +1,40 @@
+"""ShiftRows under column-first packing (REF/shift_rows.py:7-56).
+
+Row r occupies slots (r + 4c)*stride; ShiftRows rotates row r left by r columns, i.e.
+the masked row is rotated by -4r*stride slots (np.roll semantics).
+"""
+from typing import Any, List
+
+import numpy as np
+
+
+def row_masks(ctx, sc: int) -> List[Any]:
+    stride = sc // 16
+    masks = []
+    for r in range(4):
+        m = np.zeros(sc, dtype=np.complex128)
+        m[[(r + 4 * c) * stride for c in range(4)]] = 1.0
+        masks.append(ctx.encode(m))
+    return masks
+
+
+class ShiftRows:
+    direction = -1
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+        self.sc = ctx.engine.slot_count
+        self.stride = self.sc // 16
+        self._pt_masks = row_masks(ctx, self.sc)
+        self._rot_steps = [self.direction * 4 * r * self.stride for r in range(4)]
+
+    def _apply_one(self, ct: Any) -> Any:
+        ctx = self.ctx
+        out = ctx.multiply(ct, 0.0)
+        for mask, step in zip(self._pt_masks, self._rot_steps):
+            part = ctx.multiply(ct, mask)
+            out = ctx.add(out, ctx.rotate(part, step) if step else part)
+        return out
+
+    def apply(self, ct_hi: Any, ct_lo: Any):
+        return self._apply_one(ct_hi), self._apply_one(ct_lo)

@@ -1,0 +1,70 @@
+"""SubBytes / InvSubBytes via two 8->4 LUT polynomials sharing one power basis
+(REF/sub_bytes_lut.py:8-73).
+
+1. lift lo: L(y) = Σ_{k<16} ℓ_k y^k with ℓ = ifft(ζ256^0..15) maps ζ16^l -> ζ256^l;
+2. b = hi · L(lo) = ζ256^(16h + l) = ζ256^byte;
+3. out_hi / out_lo = Σ_{k=1..255} H[k] / Lo[k] · b^k with b^k = conj(b^(256-k)) for k > 128.
+
+``SubBytesLUT`` is the name AESPipeline imports (REF/pipeline.py:9); the snapshot only
+defines ``SubBytesLUTFastCached``, so both names are provided.
+"""
+from typing import Any, Dict, Tuple
+
+import numpy as np
+
+_TOL = 1e-12
+
+
+class SubBytesLUTFastCached:
+    def __init__(self, ctx, hi_coeffs: np.ndarray, lo_coeffs: np.ndarray):
+        self.ctx = ctx
+        self.sc = ctx.engine.slot_count
+        self.hi = np.asarray(hi_coeffs, dtype=np.complex128)
+        self.lo = np.asarray(lo_coeffs, dtype=np.complex128)
+        const = lambda c: ctx.encode(np.full(self.sc, c, dtype=np.complex128))
+
+        self.ks_hi = [k for k, c in enumerate(self.hi) if abs(c) > _TOL]
+        self.ks_lo = [k for k, c in enumerate(self.lo) if abs(c) > _TOL]
+        union = sorted(set(self.ks_hi) | set(self.ks_lo))
+        self.ks_union = [k for k in union if k != 0]
+        self.deg256 = min(max(union) if union else 0, 128)
+        self.pt_hi: Dict[int, Any] = {k: const(self.hi[k]) for k in self.ks_hi}
+        self.pt_lo: Dict[int, Any] = {k: const(self.lo[k]) for k in self.ks_lo}
+        self.c0_hi = self.hi[0] if self.hi.size else 0j
+        self.c0_lo = self.lo[0] if self.lo.size else 0j
+
+        lift = np.fft.ifft(np.exp(-2j * np.pi * np.arange(16) / 256))
+        self.ks_lift = [k for k, c in enumerate(lift) if k != 0 and abs(c) > _TOL]
+        self.deg16 = min(max(self.ks_lift) if self.ks_lift else 0, 8)
+        self.pt_lift = {k: const(lift[k]) for k in self.ks_lift}
+        self.c0_lift = lift[0]
+
+    @staticmethod
+    def _power(basis, k: int, domain: int, ctx):
+        return basis[k - 1] if k <= len(basis) else ctx.conjugate(basis[domain - k - 1])
+
+    def apply(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:
+        ctx = self.ctx
+        # 1) ζ16^l -> ζ256^l
+        lifted = ctx.add_plain(ctx.multiply(ct_lo, 0.0), self.c0_lift)
+        pos16 = ctx.make_power_basis(ct_lo, self.deg16) if self.deg16 > 0 else []
+        for k in self.ks_lift:
+            lifted = ctx.add(lifted, ctx.multiply(self._power(pos16, k, 16, ctx), self.pt_lift[k]))
+        # 2) ζ256^byte
+        ct_b = ctx.multiply(ct_hi, lifted)
+        # 3) one shared 128-power basis, two 255-term sums
+        pos256 = ctx.make_power_basis(ct_b, self.deg256) if self.deg256 > 0 else []
+        res_hi = ctx.add_plain(ctx.multiply(ct_b, 0.0), self.c0_hi)
+        res_lo = ctx.add_plain(ctx.multiply(ct_b, 0.0), self.c0_lo)
+        for k in self.ks_union:
+            bk = self._power(pos256, k, 256, ctx)
+            if k in self.pt_hi:
+                res_hi = ctx.add(res_hi, ctx.multiply(bk, self.pt_hi[k]))
+            if k in self.pt_lo:
+                res_lo = ctx.add(res_lo, ctx.multiply(bk, self.pt_lo[k]))
+        return res_hi, res_lo
+
+    __call__ = apply
+
+
+SubBytesLUT = SubBytesLUTFastCached

@@ -1,0 +1,19 @@
+"""Zeta16 nibble codec (REF/utils.py:4-19).
+
+A nibble v is carried as the 16th root of unity ζ^v, ζ = e^{-2πi/16}; decoding reads
+only the phase, so any positive real magnitude (e.g. XOR4's 256×)
+decodes to the same nibble.
+"""
+import numpy as np
+
+
+class ZetaEncoder:
+    @staticmethod
+    def to_zeta(arr: np.ndarray, modulus: int) -> np.ndarray:
+        k = np.asarray(arr) % modulus
+        return np.exp(-2j * np.pi * k / modulus)
+
+    @staticmethod
+    def from_zeta(z_arr: np.ndarray, modulus: int) -> np.ndarray:
+        turns = -np.angle(z_arr) * modulus / (2 * np.pi)
+        return np.mod(np.rint(turns), modulus).astype(np.uint8)

@@ -1,0 +1,114 @@
+/*
+ * aesfhe.h -- C ABI of the MI355X-native CKKS engine (libaesfhe.so).
+ *
+ * This is the drop-in boundary for the reference's hot path: every CKKS primitive the
+ * reference reaches through EngineContext (REF/engine_context.py:56-204), i.e. through
+ * the closed-source `desilofhe.Engine` (REF/engine_context.py:1,17-50), is one entry
+ * point here.  Signatures use plain pointers, sizes and opaque 64-bit handles; the
+ * Python shim (aes-implementation-fhe_amd/mi355x_ckks.py) binds them with ctypes.
+ *
+ * Conventions
+ *   - Every function returns 0 on success or a negative status; the message is then
+ *     available from aesfhe_last_error(ctx).  Level exhaustion messages contain the
+ *     word "level" and relinearising a 2-polynomial ciphertext reports
+ *     "should have 3 polynomials" (the strings REF/engine_context.py:139-145,186-195
+ *     and REF/xor4_lut.py:33-51 branch on).
+ *   - Results are always new handles; inputs are never modified.  Free every handle
+ *     with aesfhe_free.
+ *   - Slots are passed as separate real/imaginary double arrays of slot_count entries.
+ *   - rotate(ct, steps) == np.roll(slots, steps)  (SURVEY.md quirk 4e).
+ *   - A context is bound to one HIP device and one stream; it is not thread safe, but
+ *     independent contexts (one per GPU) are.
+ */
+#ifndef AESFHE_H
+#define AESFHE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct aesfhe_ctx aesfhe_ctx;
+typedef uint64_t aesfhe_handle;
+
+/* --- context / keys -------------------------------------------------------------- */
+/* replaces desilofhe.Engine(...) construction, REF/engine_context.py:17-39 */
+int aesfhe_create(aesfhe_ctx** out, int log_n, int max_level, int dnum, int device_id, uint64_t seed);
+int aesfhe_destroy(aesfhe_ctx* ctx);
+const char* aesfhe_last_error(aesfhe_ctx* ctx);
+/* replaces create_secret_key / create_public_key / create_relinearization_key /
+ * create_conjugation_key, REF/engine_context.py:44-48 (rotation keys are made on first use) */
+int aesfhe_keygen(aesfhe_ctx* ctx);
+/* engine.slot_count, read by every module (e.g. REF/state_encoder.py:14) */
+int aesfhe_slot_count(aesfhe_ctx* ctx);
+int aesfhe_max_level(aesfhe_ctx* ctx);
+/* info: [n, L, n_q, n_ks, n_p, alpha, dnum, log_n] */
+int aesfhe_info(aesfhe_ctx* ctx, int32_t* info8);
+int aesfhe_moduli(aesfhe_ctx* ctx, uint32_t* out);   /* n_q + n_p primes */
+int aesfhe_scales(aesfhe_ctx* ctx, double* out);     /* delta_0 .. delta_L */
+int aesfhe_sync(aesfhe_ctx* ctx);
+int aesfhe_free(aesfhe_ctx* ctx, aesfhe_handle h);
+int aesfhe_level(aesfhe_ctx* ctx, aesfhe_handle ct, int32_t* level, int32_t* npoly);
+
+/* --- plaintexts / codec ------------------------------------------------------------ */
+/* engine.encode(vec), REF/engine_context.py:62-63 (level-agnostic; encoded on use) */
+int aesfhe_plaintext(aesfhe_ctx* ctx, const double* re, const double* im, int n, aesfhe_handle* out);
+/* engine.encrypt(data, public_key), REF/engine_context.py:56-57 */
+int aesfhe_encrypt(aesfhe_ctx* ctx, const double* re, const double* im, int n, aesfhe_handle* out);
+/* engine.decrypt(ct, secret_key), REF/engine_context.py:59-60 */
+int aesfhe_decrypt(aesfhe_ctx* ctx, aesfhe_handle ct, double* re, double* im, int n);
+
+/* --- arithmetic ---------------------------------------------------------------------- */
+/* engine.add / engine.subtract, REF/engine_context.py:70-74 (levels auto-aligned) */
+int aesfhe_add(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, aesfhe_handle* out);
+int aesfhe_sub(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, aesfhe_handle* out);
+/* engine.add(ct, pt) / engine.add_plain(ct, scalar), REF/engine_context.py:76-98 */
+int aesfhe_add_pt(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle pt, aesfhe_handle* out);
+int aesfhe_add_scalar(aesfhe_ctx* ctx, aesfhe_handle ct, double re, double im, aesfhe_handle* out);
+/* engine.multiply(ct, scalar|pt), REF/engine_context.py:65-68,106-125 */
+int aesfhe_mul_scalar(aesfhe_ctx* ctx, aesfhe_handle ct, double re, double im, aesfhe_handle* out);
+int aesfhe_mul_pt(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle pt, aesfhe_handle* out);
+/* engine.multiply(a, b, relinearization_key), REF/engine_context.py:65-67:
+ * tensor + relinearise + rescale; relin = 0 returns the 3-polynomial tensor (rescaled) */
+int aesfhe_mul(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int relin, aesfhe_handle* out);
+/* engine.relinearize, REF/engine_context.py:134-145 */
+int aesfhe_relinearize(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
+int aesfhe_rescale(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
+/* drop to a lower level with exact scale */
+int aesfhe_level_down(aesfhe_ctx* ctx, aesfhe_handle ct, int level, aesfhe_handle* out);
+/* engine.rotate(ct, rotation_key, steps), REF/engine_context.py:127-132 */
+int aesfhe_rotate(aesfhe_ctx* ctx, aesfhe_handle ct, int steps, aesfhe_handle* out);
+/* engine.conjugate(ct, conjugation_key), REF/engine_context.py:103-104 */
+int aesfhe_conjugate(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
+/* engine.make_power_basis(ct, degree, relinearization_key), REF/engine_context.py:100-101;
+ * out[k-1] = ct^k, k = 1..degree */
+int aesfhe_power_basis(aesfhe_ctx* ctx, aesfhe_handle ct, int degree, aesfhe_handle* out);
+/* engine.ntt / engine.intt, REF/engine_context.py:173-177 */
+int aesfhe_to_ntt(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
+int aesfhe_to_intt(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
+/* engine.bootstrap(ct, relin, conj, bootstrap_key), REF/engine_context.py:147-162 */
+int aesfhe_bootstrap(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
+/* Zeta16 secret-key renorm of a (hi, lo) state pair (REF/pipeline.py:65-69): decrypt,
+ * snap the 16 strided slots to the nearest codeword, refill others with 1, re-encrypt */
+int aesfhe_renorm_pair(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle* out_hi, aesfhe_handle* out_lo);
+
+/* --- raw access (tests, parity against the oracle) ------------------------------------ */
+/* limbs of a ciphertext: npoly x (level+2) x N uint32, NTT form */
+int aesfhe_export(aesfhe_ctx* ctx, aesfhe_handle ct, uint32_t* out, uint64_t words);
+int aesfhe_import(aesfhe_ctx* ctx, int level, int npoly, const uint32_t* data, aesfhe_handle* out);
+/* secret key (NTT form, all n_q + n_p limbs) / public key / key-switching key of galois g (0 = relin) */
+int aesfhe_export_secret(aesfhe_ctx* ctx, uint32_t* out);
+int aesfhe_export_pk(aesfhe_ctx* ctx, uint32_t* out);
+int aesfhe_export_ksk(aesfhe_ctx* ctx, uint64_t galois, uint32_t* out);
+/* forward / inverse NTT of host rows whose limb l is prime first_prime + l */
+int aesfhe_debug_ntt(aesfhe_ctx* ctx, uint32_t* data, int rows, int first_prime, int inverse);
+/* key switch of a raw polynomial d (level+2 limbs, NTT) with the key of galois g */
+int aesfhe_debug_keyswitch(aesfhe_ctx* ctx, int level, uint64_t galois, const uint32_t* d, uint32_t* out);
+/* per-kernel timing of the last N ops (HIP events); op counters */
+int aesfhe_counters(aesfhe_ctx* ctx, uint64_t* out, int n);
+int aesfhe_reset_counters(aesfhe_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

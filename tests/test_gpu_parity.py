@@ -1,0 +1,121 @@
+"""Bit-exact parity of the HIP kernels against the CPU oracle (oracle/ckks_oracle.c).
+
+Same parameters and seed on both sides -> identical primes, scales, keys; identical
+input limbs -> identical output limbs for NTT/INTT, key switching, tensor, rescale,
+automorphism, level alignment.
+"""
+import numpy as np
+import pytest
+
+from conftest import gpu_engine
+
+pytestmark = pytest.mark.gpu
+
+SETS = [(13, 6), (16, 17)]
+
+
+@pytest.fixture(scope="module", params=SETS, ids=lambda s: f"logn{s[0]}_L{s[1]}")
+def pair(request):
+    from oracle.ckks_cpu import OracleParams
+    log_n, L = request.param
+    E = gpu_engine(log_n=log_n, max_level=L, seed=0x5EED)
+    O = OracleParams(log_n=log_n, max_level=L, dnum=3, seed=0x5EED)
+    return E, O
+
+
+def rand_rows(O, limbs, rng):
+    return np.stack([rng.integers(0, int(O.moduli[t]), O.n, dtype=np.uint64) for t in limbs]).astype(np.uint32)
+
+
+def rand_ct(O, level, npoly, rng):
+    return np.stack([rand_rows(O, range(level + 2), rng) for _ in range(npoly)])
+
+
+def test_parameters_match(pair):
+    E, O = pair
+    assert np.array_equal(E.moduli(), O.moduli)
+    assert np.array_equal(E.scales(), O.deltas)
+    assert all(q > 2 ** 30 and q < 2 ** 32 // 3 for q in O.moduli.tolist())
+
+
+def test_ntt_bitexact(pair):
+    E, O = pair
+    rng = np.random.default_rng(1)
+    ntot = O.n_q + O.n_p
+    for first in (0, O.n_q - 3, O.n_q):
+        limbs = list(range(first, min(first + 3, ntot)))
+        x = rand_rows(O, limbs, rng)
+        fwd = E.debug_ntt(x, first)
+        assert np.array_equal(fwd, O.ntt(x, limbs))
+        assert np.array_equal(E.debug_ntt(fwd, first, inverse=True), x)
+
+
+def test_secret_and_public_key_bitexact(pair):
+    E, O = pair
+    assert np.array_equal(E.export_secret(), O.secret_ntt())
+    assert np.array_equal(E.export_pk(), O.gen_pk())
+
+
+@pytest.mark.parametrize("which", ["relin", "conj", "rot"])
+def test_keyswitch_keys_bitexact(pair, which):
+    E, O = pair
+    g = {"relin": 0, "conj": E.galois_conj, "rot": E.galois_rotate(-(E.slot_count // 4))}[which]
+    assert np.array_equal(E.export_ksk(g), O.gen_ksk(g))
+
+
+def test_keyswitch_bitexact(pair):
+    E, O = pair
+    rng = np.random.default_rng(2)
+    g = E.galois_conj
+    key = O.gen_ksk(g)
+    for level in sorted({O.L, O.L // 2, 1, 0}):
+        d = rand_rows(O, range(level + 2), rng)
+        assert np.array_equal(E.debug_keyswitch(level, g, d), O.keyswitch(level, d, key)), level
+
+
+def test_rescale_tensor_automorph_bitexact(pair):
+    E, O = pair
+    rng = np.random.default_rng(3)
+    level = min(5, O.L)
+    a, b = rand_ct(O, level, 2, rng), rand_ct(O, level, 2, rng)
+    ca, cb = E.import_ct(a, level), E.import_ct(b, level)
+    # rescale
+    assert np.array_equal(E.export(E.rescale(ca)), O.rescale(level, a))
+    # tensor (no relinearisation) followed by rescale
+    t = O.tensor(level, a, b)
+    assert np.array_equal(E.export(E.multiply(ca, cb)), O.rescale(level, t))
+    # relinearised product: (d0, d1) + KS(d2), then rescale
+    ks = O.keyswitch(level, t[2], O.gen_ksk(0))
+    q = O.limbs_mod(level + 2)
+    relin = ((t[:2].astype(np.uint64) + ks) % q).astype(np.uint32)
+    assert np.array_equal(E.export(E.multiply(ca, cb, "rlk")), O.rescale(level, relin))
+    # rotation: automorphism + key switch of the second polynomial
+    steps = E.slot_count // 8
+    g = E.galois_rotate(steps)
+    x = O.automorph(level, g, a)
+    ks = O.keyswitch(level, x[1], O.gen_ksk(g))
+    ks[0] = ((ks[0].astype(np.uint64) + x[0]) % q).astype(np.uint32)
+    assert np.array_equal(E.export(E.rotate(ca, None, steps)), ks)
+
+
+def test_level_down_bitexact(pair):
+    E, O = pair
+    rng = np.random.default_rng(4)
+    a_lv, b_lv = min(6, O.L), 2
+    a = rand_ct(O, a_lv, 2, rng)
+    ca = E.import_ct(a, a_lv)
+    c = int(round(O.deltas[b_lv] * float(O.moduli[b_lv + 2]) / O.deltas[a_lv]))
+    x = O.mul_limb_consts(O.const_residues(c, b_lv + 3), np.ascontiguousarray(a[:, : b_lv + 3]))
+    assert np.array_equal(E.export(E.level_down(ca, b_lv)), O.rescale(b_lv + 1, x))
+
+
+def test_encrypt_decrypt_cross(pair):
+    """GPU encryption decrypts correctly with the oracle's secret key and vice versa."""
+    E, O = pair
+    rng = np.random.default_rng(5)
+    z = np.exp(2j * np.pi * rng.random(E.slot_count))
+    ct = E.encrypt(z)
+    assert ct.level == O.L
+    assert np.abs(E.decrypt(ct) - z).max() < 1e-4
+    m = O.decrypt_coeffs(O.L, E.export(ct), O.secret_ntt())
+    assert np.abs(O.embed(m / O.deltas[O.L]) - z).max() < 1e-4
