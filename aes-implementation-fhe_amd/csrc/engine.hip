@@ -71,6 +71,7 @@ struct Ct {
     int level = 0;
     int npoly = 2;
     bool ntt = true;
+    bool pending = false;  // tensor product awaiting rescale (scale delta_level^2)
 };
 
 struct Pt {
@@ -109,6 +110,10 @@ public:
     }
 
     const HostParams& hp() const { return hp_; }
+    void set_fresh(int level) {
+        if (level < 0 || level > hp_.L) throw std::runtime_error("fresh level must lie in [0, max_level]");
+        hp_.fresh = level;
+    }
     int slot_count() const { return hp_.n / 2; }
     void sync() { HIP_OK(hipStreamSynchronize(st_)); }
 
@@ -268,9 +273,11 @@ public:
 
     aesfhe_handle encrypt(const double* re, const double* im) {
         if (!d_pk_) throw std::runtime_error("keys not generated");
-        const int n = hp_.n, nq = hp_.n_q, L = hp_.L;
+        // encode at delta_f * q_{f+2} on limbs 0..f+2, encrypt at level f+1, rescale to f
+        const int n = hp_.n, f = hp_.fresh, nq = f + 3;
+        const int L = f;
         std::vector<u32> host;
-        encode_host(re, im, hp_.delta[L] * (double)hp_.mod[hp_.enc_limb()], nq, host);
+        encode_host(re, im, hp_.delta[f] * (double)hp_.mod[f + 2], nq, host);
         u32* m = upload_ntt(host, nq);
         u32* v = tmp(nq);
         u32* e = tmp(2 * nq);
@@ -282,7 +289,8 @@ public:
         ntt(e, 2 * nq, nq, qmap());
         Ct top = alloc_ct(L + 1, 2);
         launch_add(st_, T_, e, e, m, nq, nq, qmap());  // e0 + m
-        launch_fma_poly(st_, T_, top.data, e, d_pk_, v, 2 * nq, nq, qmap());
+        launch_fma_poly(st_, T_, top.data, e, d_pk_, v, nq, nq, qmap());
+        launch_fma_poly(st_, T_, top.data + (size_t)nq * n, e + (size_t)nq * n, d_pk_ + (size_t)hp_.n_q * n, v, nq, nq, qmap());
         untmp(m, nq);
         untmp(v, nq);
         untmp(e, 2 * nq);
@@ -293,9 +301,10 @@ public:
     }
 
     // decryption to real coefficients (message * delta_level)
-    void decrypt_coeffs(const Ct& c_in, std::vector<double>& m) {
+    int decrypt_coeffs(const Ct& c_in, std::vector<double>& m) {
         const int n = hp_.n;
         Ct c = ensure_ntt(c_in);
+        const int level = c.level;
         const int nl = c.level + 2;
         u32* x = tmp(2);
         HIP_OK(hipMemcpyAsync(x, c.data, sizeof(u32) * 2 * n, hipMemcpyDeviceToDevice, st_));
@@ -328,12 +337,12 @@ public:
             m[k] = (double)sv;
         }
         cnt_[C_DEC]++;
+        return level;
     }
     void decrypt(aesfhe_handle h, double* re, double* im) {
-        const Ct& c = ct(h);
         std::vector<double> m;
-        decrypt_coeffs(c, m);
-        const double inv = 1.0 / hp_.delta[c.level];
+        const int level = decrypt_coeffs(ct(h), m);
+        const double inv = 1.0 / hp_.delta[level];
         for (double& v : m) v *= inv;
         emb_.forward(m.data(), re, im);
     }
@@ -343,15 +352,23 @@ public:
     Ct copy(const Ct& c) {
         Ct o = alloc_ct(c.level, c.npoly);
         o.ntt = c.ntt;
+        o.pending = c.pending;
         HIP_OK(hipMemcpyAsync(o.data, c.data, c.words * sizeof(u32), hipMemcpyDeviceToDevice, st_));
         return o;
     }
     // returns c itself (same data) when already in NTT form, else a converted copy
-    Ct ensure_ntt(const Ct& c) {
-        if (c.ntt) return c;
-        Ct o = copy(c);
-        ntt(o.data, o.npoly * (o.level + 2), o.level + 2, qmap());
-        o.ntt = true;
+    Ct ensure_ntt(const Ct& c, bool resolve_pending = true) {
+        Ct o = c;
+        if (!c.ntt) {
+            o = copy(c);
+            ntt(o.data, o.npoly * (o.level + 2), o.level + 2, qmap());
+            o.ntt = true;
+        }
+        if (resolve_pending && o.pending) {
+            Ct r = rescale(o);
+            if (o.data != c.data) release(o);
+            o = r;
+        }
         return o;
     }
     Ct to_intt(const Ct& c) {
@@ -379,6 +396,7 @@ public:
         launch_rescale_spread(st_, T_, v, last, np, r, hp_.mod[r]);
         ntt(v, np * r, r, qmap());
         Ct o = alloc_ct(c.level - 1, np);
+        o.pending = false;
         launch_rescale_finish(st_, T_, o.data, c.data, v, d_rescale_qinv_ + rescale_off_[c.level], np, r, nl);
         untmp(last, np);
         untmp(v, (size_t)np * r);
@@ -453,13 +471,20 @@ public:
     }
     // two ciphertexts at a common level (copies only when a level change is needed)
     std::pair<Ct, Ct> align(const Ct& a, const Ct& b, bool& fa, bool& fb) {
-        const int lv = std::min(a.level, b.level);
-        Ct x = a, y = b;
-        fa = fb = false;
-        if (a.level != lv) x = level_down(a, lv), fa = true;
-        else if (!a.ntt) x = ensure_ntt(a), fa = true;
-        if (b.level != lv) y = level_down(b, lv), fb = true;
-        else if (!b.ntt) y = ensure_ntt(b), fb = true;
+        const int lv = std::min(a.level - (a.pending ? 1 : 0), b.level - (b.pending ? 1 : 0));
+        Ct x = ensure_ntt(a), y = ensure_ntt(b);
+        fa = x.data != a.data;
+        fb = y.data != b.data;
+        if (x.level != lv) {
+            Ct t = level_down(x, lv);
+            if (fa) release(x);
+            x = t, fa = true;
+        }
+        if (y.level != lv) {
+            Ct t = level_down(y, lv);
+            if (fb) release(y);
+            y = t, fb = true;
+        }
         return {x, y};
     }
 
@@ -506,10 +531,11 @@ public:
         const int nl = c.level + 2;
         Ct o;
         cnt_[C_SCALAR]++;
-        if (im == 0.0 && re == std::floor(re) && std::fabs(re) < 1048576.0) {
-            std::vector<u32> r(nl);
-            for (int t = 0; t < nl; ++t) r[t] = mod_i64((i64)re, hp_.mod[t]);
-            u32* d = const_half(r, r);
+        if (re == std::floor(re) && im == std::floor(im) && std::fabs(re) < 1048576.0 && std::fabs(im) < 1048576.0) {
+            // Gaussian integer a + b i: exact multiplication by a + b X^{N/2}, no level consumed
+            std::vector<u32> lo, hi;
+            scalar_residues((i64)re, (i64)im, nl, lo, hi);
+            u32* d = const_half(lo, hi);
             o = alloc_ct(c.level, c.npoly);
             launch_mul_const_half(st_, T_, o.data, c.data, d, c.npoly * nl, nl, qmap());
         } else {
@@ -580,7 +606,8 @@ public:
             const int lo = j * alpha, h = std::min(alpha, nl - lo);
             u32* ej = ext + (size_t)j * ne * n;
             HIP_OK(hipMemcpyAsync(ej + (size_t)lo * n, d + (size_t)lo * n, sizeof(u32) * h * n, hipMemcpyDeviceToDevice, st_));
-            launch_base_convert(st_, T_, ej, coef + (size_t)lo * n, h, lo, ne, em, lo, d_modup_ + toff[j], d_modup_qhinv_ + toff[j] + (size_t)2 * h * ne);
+            launch_base_convert(st_, T_, ej, coef + (size_t)lo * n, h, lo, ne, em, lo, d_modup_ + toff[j],
+                                d_modup_ + toff[j] + (size_t)2 * h * ne, d_modup_ + toff[j] + (size_t)2 * h * ne + 2 * h);
             if (lo > 0) ntt(ej, lo, lo, qmap());
             const int rest = ne - (lo + h);
             if (rest > 0) ntt(ej + (size_t)(lo + h) * n, rest, rest, LimbMap{nl - (lo + h), lo + h, hp_.p_off()});
@@ -598,7 +625,7 @@ public:
         const size_t doff = moddown_off_[level];
         for (int p = 0; p < 2; ++p)
             launch_base_convert(st_, T_, conv + (size_t)p * nl * n, yp + (size_t)p * np * n, np, hp_.p_off(), nl, qmap(), 1 << 30,
-                                d_moddown_ + doff, d_moddown_phinv_);
+                                d_moddown_ + doff, d_moddown_phinv_, d_negp_);
         ntt(conv, 2 * nl, nl, qmap());
         Ct o = alloc_ct(level, 2);
         launch_moddown_finish(st_, T_, o.data, acc, conv, d_pinv_ + (size_t)2 * 0, add0, add1, nl, ne);
@@ -622,9 +649,8 @@ public:
         if (fb) release(y);
         cnt_[C_MUL]++;
         if (!relin) {
-            Ct o = rescale(d);
-            release(d);
-            return o;
+            d.pending = true;
+            return d;
         }
         Ct r = keyswitch(d.data + (size_t)2 * nl * n, d.level, ksk(0), d.data, d.data + (size_t)nl * n);
         release(d);
@@ -636,12 +662,15 @@ public:
 
     Ct relinearize(const Ct& c_in) {
         if (c_in.npoly != 3) throw std::runtime_error("relinearize: ciphertext should have 3 polynomials");
-        Ct c = ensure_ntt(c_in);
+        Ct c = ensure_ntt(c_in, false);
         const int nl = c.level + 2, n = hp_.n;
         Ct r = keyswitch(c.data + (size_t)2 * nl * n, c.level, ksk(0), c.data, c.data + (size_t)nl * n);
         if (c.data != c_in.data) release(c);
         cnt_[C_RELIN]++;
-        return r;
+        if (!c_in.pending) return r;
+        Ct o = rescale(r);
+        release(r);
+        return o;
     }
 
     Ct galois(const Ct& c_in, u64 g) {
@@ -694,8 +723,8 @@ public:
         int nib[2][16];
         aesfhe_handle in[2] = {hh, hl};
         for (int w = 0; w < 2; ++w) {
-            decrypt_coeffs(ct(in[w]), m);
-            const double inv = 1.0 / hp_.delta[ct(in[w]).level];
+            const int level = decrypt_coeffs(ct(in[w]), m);
+            const double inv = 1.0 / hp_.delta[level];
             for (int k = 0; k < n; ++k) m[k] *= inv;
             emb_.forward(m.data(), re.data(), im.data());
             for (int i = 0; i < 16; ++i) {
@@ -722,7 +751,7 @@ public:
     // ------------------------------------------------------------------ raw access
     void export_ct(aesfhe_handle h, u32* out, u64 words) {
         const Ct& c0 = ct(h);
-        Ct c = ensure_ntt(c0);
+        Ct c = ensure_ntt(c0, false);
         if (words < c.words) throw std::runtime_error("export buffer too small");
         HIP_OK(hipMemcpyAsync(out, c.data, c.words * sizeof(u32), hipMemcpyDeviceToHost, st_));
         HIP_OK(hipStreamSynchronize(st_));
@@ -872,10 +901,15 @@ private:
                     mu.push_back(inv);
                     mu.push_back(shoup_pre(inv, qi));
                 }
+                for (int x = 0; x < ne; ++x) {  // -Q_digit mod target
+                    const u32 tq = x < nl ? q[x] : q[hp_.p_off() + x - nl];
+                    u32 v = 1;
+                    for (int k = 0; k < h; ++k) v = mulm(v, q[lo + k], tq);
+                    mu.push_back(v ? tq - v : 0);
+                }
             }
         }
-        d_modup_ = dev_upload(mu);
-        d_modup_qhinv_ = d_modup_;  // qhinv rides right after each [h][ne] block
+        d_modup_ = dev_upload(mu);  // per (level, digit): [h][ne] qhat pairs, [h] qhat^-1 pairs, [ne] -Q
 
         // ModDown tables per level: [np][nl] Shoup pairs of phat_k mod q_t; phat_k^{-1} mod p_k; P^{-1} mod q_t
         std::vector<u32> md;
@@ -905,15 +939,17 @@ private:
             phinv.push_back(shoup_pre(inv, pk));
         }
         d_moddown_phinv_ = dev_upload(phinv);
-        std::vector<u32> pinv;
+        std::vector<u32> pinv, negp;
         for (int t = 0; t < hp_.n_q; ++t) {
             u32 v = 1;
             for (int k = 0; k < np; ++k) v = mulm(v, q[hp_.p_off() + k], q[t]);
             const u32 inv = hinvm(v, q[t]);
             pinv.push_back(inv);
             pinv.push_back(shoup_pre(inv, q[t]));
+            negp.push_back(v ? q[t] - v : 0);
         }
         d_pinv_ = dev_upload(pinv);
+        d_negp_ = dev_upload(negp);
 
         void* r = nullptr;
         HIP_OK(hipMalloc(&r, kRingWords * sizeof(u32)));
@@ -943,12 +979,12 @@ private:
     std::vector<size_t> rescale_off_;
     u32* d_gadget_ = nullptr;
     u32* d_modup_ = nullptr;
-    u32* d_modup_qhinv_ = nullptr;
     std::vector<size_t> modup_off_;
     u32* d_moddown_ = nullptr;
     u32* d_moddown_phinv_ = nullptr;
     std::vector<size_t> moddown_off_;
     u32* d_pinv_ = nullptr;
+    u32* d_negp_ = nullptr;
     static constexpr size_t kRingWords = 1 << 20;
     u32* ring_ = nullptr;
     u32* ring_host_ = nullptr;
@@ -1004,6 +1040,10 @@ int aesfhe_keygen(aesfhe_ctx* ctx) {
 }
 int aesfhe_slot_count(aesfhe_ctx* ctx) { return ctx && ctx->eng ? ctx->eng->slot_count() : -1; }
 int aesfhe_max_level(aesfhe_ctx* ctx) { return ctx && ctx->eng ? ctx->eng->hp().L : -1; }
+int aesfhe_set_fresh_level(aesfhe_ctx* ctx, int level) {
+    API_BEGIN ctx->eng->set_fresh(level);
+    API_END
+}
 int aesfhe_info(aesfhe_ctx* ctx, int32_t* info) {
     API_BEGIN const HostParams& p = ctx->eng->hp();
     int32_t v[8] = {p.n, p.L, p.n_q, p.n_ks, p.n_p, p.alpha, p.dnum, p.logn};

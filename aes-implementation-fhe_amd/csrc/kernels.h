@@ -45,9 +45,10 @@ void launch_rescale_finish(hipStream_t st, const DevTables& T, u32* out, const u
 // --- key switching -----------------------------------------------------------------
 // digit coefficient rows x[i] (i < h, primes d0 + i) -> ext rows for all targets of
 // map (nt rows), skipping rows [skip0, skip0 + h) which are copied from src_ntt.
-// tab: [h][nt] Shoup pairs of (qhat_i mod t); qhinv: [h] Shoup pairs of qhat_i^{-1} mod q_i
+// tab: [h][nt] Shoup pairs of (qhat_i mod t); qhinv: [h] Shoup pairs of qhat_i^{-1} mod q_i;
+// negq: [nt] values of (-Q mod t), Q = prod of the h source primes (centred conversion)
 void launch_base_convert(hipStream_t st, const DevTables& T, u32* ext, const u32* x, int h, int d0, int nt, LimbMap map,
-                         int skip0, const u32* tab, const u32* qhinv);
+                         int skip0, const u32* tab, const u32* qhinv, const u32* negq);
 // acc[0|1][x] = sum_j ext[j][x] * key[j][b|a][krow(x)]; ext: [nd][ne][N]; key: [dnum][2][nkey][N]
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* key, int nd, int ne, int nl,
                       int nkey, int nks, LimbMap map);

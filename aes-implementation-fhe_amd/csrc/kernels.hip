@@ -263,20 +263,26 @@ __global__ void k_rescale_finish(u32* out, const u32* x, const u32* v, const u32
 // ------------------------------------------------------------------------------------
 constexpr int kMaxDigit = 32;
 
-// one thread per coefficient; loops over the nt target rows
+// one thread per coefficient; loops over the nt target rows.  Centred conversion
+// (DESIGN.md §3.6): u = round(sum_i y_i / q_i) from a 32-bit fixed-point estimate
+// (mu_i = floor(2^62/q_i)), ext_t = sum_i y_i qhat_i - u Q  (mod t).
 __global__ void __launch_bounds__(kBlock) k_base_convert(u32* ext, const u32* x, int h, int d0, int nt, LimbMap map, int skip0,
-                                                         const u32* tab, const u32* qhinv, const PrimeConst* pc, int logn) {
+                                                         const u32* tab, const u32* qhinv, const u32* negq, const PrimeConst* pc,
+                                                         int logn) {
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
     u32 y[kMaxDigit];
+    u64 f = 0;
 #pragma unroll 4
     for (int i = 0; i < h; ++i) {
-        const u32 q = pc[d0 + i].q;
-        y[i] = shoup_mul(x[((size_t)i << logn) + k], qhinv[2 * i], qhinv[2 * i + 1], q);
+        const PrimeConst Pi = pc[d0 + i];
+        y[i] = shoup_mul(x[((size_t)i << logn) + k], qhinv[2 * i], qhinv[2 * i + 1], Pi.q);
+        f += ((u64)y[i] * Pi.mu) >> 30;
     }
+    const u32 u = (u32)((f + (1ull << 31)) >> 32);
     for (int t = 0; t < nt; ++t) {
         if (t >= skip0 && t < skip0 + h) continue;
         const PrimeConst P = pc[map.prime(t)];
-        u64 acc = 0;
+        u64 acc = (u64)u * negq[t];
         const u32* tt = tab + 2 * (size_t)t;
         for (int i = 0; i < h; ++i) acc += shoup_mul(y[i], tt[2 * (size_t)i * nt], tt[2 * (size_t)i * nt + 1], P.q);
         ext[((size_t)t << logn) + k] = barrett_reduce64(acc, P.q, P.mu);
@@ -412,9 +418,9 @@ void launch_rescale_finish(hipStream_t st, const DevTables& T, u32* out, const u
                        T.pc, T.logn);
 }
 void launch_base_convert(hipStream_t st, const DevTables& T, u32* ext, const u32* x, int h, int d0, int nt, LimbMap map, int skip0,
-                         const u32* tab, const u32* qhinv) {
+                         const u32* tab, const u32* qhinv, const u32* negq) {
     hipLaunchKernelGGL(k_base_convert, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, ext, x, h, d0, nt, map, skip0, tab, qhinv,
-                       T.pc, T.logn);
+                       negq, T.pc, T.logn);
 }
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* key, int nd, int ne, int nl, int nkey,
                       int nks, LimbMap map) {

@@ -60,7 +60,8 @@ std::string HostParams::build(int logn_, int L_, int dnum_, uint64_t seed_) {
     n_q = L + 3;
     n_ks = L + 2;
     alpha = (n_ks + dnum - 1) / dnum;
-    n_p = alpha;
+    n_p = alpha + 1;  // P exceeds every digit modulus by one prime
+    fresh = L;
     mod.assign(n_tot(), 0);
 
     const uint64_t kMax = 1431655765ull;  // floor(2^32 / 3): keeps 3q < 2^32
@@ -70,14 +71,14 @@ std::string HostParams::build(int logn_, int L_, int dnum_, uint64_t seed_) {
 
     // largest admissible primes: 2 base, alpha special, 1 encryption
     std::vector<u32> top;
-    for (uint64_t c = (kMax - 1) / two_n * two_n + 1; top.size() < (size_t)(2 + alpha + 1); c -= two_n) {
+    for (uint64_t c = (kMax - 1) / two_n * two_n + 1; top.size() < (size_t)(2 + n_p + 1); c -= two_n) {
         if (c <= kMin) return "ran out of NTT-friendly primes";
         if (c < kMax && prime32((u32)c)) top.push_back((u32)c);
     }
     mod[0] = top[0];
     mod[1] = top[1];
-    for (int k = 0; k < alpha; ++k) mod[n_q + k] = top[2 + k];
-    mod[n_q - 1] = top[2 + alpha];
+    for (int k = 0; k < n_p; ++k) mod[n_q + k] = top[2 + k];
+    mod[n_q - 1] = top[2 + n_p];
     taken.insert(top.begin(), top.end());
 
     // rescaling chain: delta_L = 1.25 * 2^30; limb l+1 = prime closest to delta_l^2 / target

@@ -17,7 +17,8 @@ struct HostParams {
     int alpha = 7;    // limbs per digit (= special primes)
     int n_q = 20;     // L + 3
     int n_ks = 19;    // L + 2 (limbs reachable by key switching)
-    int n_p = 7;
+    int n_p = 8;
+    int fresh = 17;   // level of fresh encryptions (<= L)
     uint64_t seed = 0;
 
     std::vector<u32> mod;       // n_q + n_p primes

@@ -28,7 +28,7 @@ _up = np.ctypeslib.ndpointer(dtype=np.uint32, flags="C_CONTIGUOUS")
 
 EXPORTED = [
     "aesfhe_create", "aesfhe_destroy", "aesfhe_last_error", "aesfhe_keygen", "aesfhe_slot_count",
-    "aesfhe_max_level", "aesfhe_info", "aesfhe_moduli", "aesfhe_scales", "aesfhe_sync", "aesfhe_free",
+    "aesfhe_max_level", "aesfhe_set_fresh_level", "aesfhe_info", "aesfhe_moduli", "aesfhe_scales", "aesfhe_sync", "aesfhe_free",
     "aesfhe_level", "aesfhe_plaintext", "aesfhe_encrypt", "aesfhe_decrypt", "aesfhe_add", "aesfhe_sub",
     "aesfhe_add_pt", "aesfhe_add_scalar", "aesfhe_mul_scalar", "aesfhe_mul_pt", "aesfhe_mul",
     "aesfhe_relinearize", "aesfhe_rescale", "aesfhe_level_down", "aesfhe_rotate", "aesfhe_conjugate",
@@ -54,7 +54,7 @@ def load_library(path: Optional[Path] = None):
     pp = ctypes.POINTER(ctypes.c_void_p)
     sig = {
         "aesfhe_create": [pp, c_int, c_int, c_int, c_int, ctypes.c_uint64],
-        "aesfhe_destroy": [vp], "aesfhe_keygen": [vp], "aesfhe_slot_count": [vp], "aesfhe_max_level": [vp],
+        "aesfhe_destroy": [vp], "aesfhe_keygen": [vp], "aesfhe_slot_count": [vp], "aesfhe_max_level": [vp], "aesfhe_set_fresh_level": [vp, c_int],
         "aesfhe_info": [vp, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")],
         "aesfhe_moduli": [vp, _up], "aesfhe_scales": [vp, _dp], "aesfhe_sync": [vp], "aesfhe_free": [vp, _H],
         "aesfhe_level": [vp, _H, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_int32)],

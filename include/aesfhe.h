@@ -42,6 +42,8 @@ int aesfhe_keygen(aesfhe_ctx* ctx);
 /* engine.slot_count, read by every module (e.g. REF/state_encoder.py:14) */
 int aesfhe_slot_count(aesfhe_ctx* ctx);
 int aesfhe_max_level(aesfhe_ctx* ctx);
+/* level of fresh encryptions (default max_level; lower when the chain is extended for bootstrapping) */
+int aesfhe_set_fresh_level(aesfhe_ctx* ctx, int level);
 /* info: [n, L, n_q, n_ks, n_p, alpha, dnum, log_n] */
 int aesfhe_info(aesfhe_ctx* ctx, int32_t* info8);
 int aesfhe_moduli(aesfhe_ctx* ctx, uint32_t* out);   /* n_q + n_p primes */

@@ -62,7 +62,7 @@ def lib():
         "orc_tensor": (None, [vp, c_int, u32p, u32p, u32p]),
         "orc_mul_limb_consts": (None, [vp, c_int, c_int, u32p, u32p, u32p]),
         "orc_automorph": (None, [vp, c_int, c_u64, c_int, u32p, u32p]),
-        "orc_encrypt": (None, [vp, u32p, u32p, c_u64, u32p]),
+        "orc_encrypt": (None, [vp, c_int, u32p, u32p, c_u64, u32p]),
         "orc_decrypt_coeffs": (None, [vp, c_int, c_int, u32p, u32p, f64p]),
         "orc_const_residues": (None, [vp, c_i64, c_int, u32p]),
     }
@@ -182,9 +182,10 @@ class OracleParams:
         self._L.orc_const_residues(self.h, int(c), nl, out)
         return out
 
-    def encrypt(self, pt_top: np.ndarray, pk: np.ndarray, ctr: int) -> np.ndarray:
-        out = np.zeros((2, self.L + 2, self.n), np.uint32)
-        self._L.orc_encrypt(self.h, np.ascontiguousarray(pt_top, np.uint32), np.ascontiguousarray(pk, np.uint32), ctr, out)
+    def encrypt(self, pt_top: np.ndarray, pk: np.ndarray, ctr: int, fresh_level: int | None = None) -> np.ndarray:
+        f = self.L if fresh_level is None else fresh_level
+        out = np.zeros((2, f + 2, self.n), np.uint32)
+        self._L.orc_encrypt(self.h, f, np.ascontiguousarray(pt_top, np.uint32), np.ascontiguousarray(pk, np.uint32), ctr, out)
         return out
 
     def decrypt_coeffs(self, level: int, ct: np.ndarray, s_ntt: np.ndarray) -> np.ndarray:
@@ -220,8 +221,9 @@ class OracleEngine:
     REF/engine_context.py:56-204).  Same conventions as the HIP engine
      so that levels, scales and key streams coincide."""
 
-    def __init__(self, log_n: int = 16, max_level: int = 17, dnum: int = 3, seed: int = 0):
+    def __init__(self, log_n: int = 16, max_level: int = 17, dnum: int = 3, seed: int = 0, fresh_level: int | None = None):
         self.p = OracleParams(log_n, max_level, dnum, seed)
+        self.fresh = self.p.L if fresh_level is None else fresh_level
         self.slot_count = self.p.slot_count
         self.s_ntt = self.p.secret_ntt()
         self.pk = self.p.gen_pk()
@@ -235,12 +237,11 @@ class OracleEngine:
 
     # -- codec -------------------------------------------------------------------------
     def encrypt(self, z) -> OracleCiphertext:
-        p = self.p
-        q_enc = float(p.moduli[p.n_q - 1])
-        pt = p.encode(z, p.deltas[p.L] * q_enc, p.n_q)
-        data = p.encrypt(pt, self.pk, self._enc_ctr)
+        p, f = self.p, self.fresh
+        pt = p.encode(z, p.deltas[f] * float(p.moduli[f + 2]), f + 3)
+        data = p.encrypt(pt, self.pk, self._enc_ctr, f)
         self._enc_ctr += 1
-        return OracleCiphertext(data, p.L)
+        return OracleCiphertext(data, f)
 
     def decrypt(self, ct: OracleCiphertext) -> np.ndarray:
         m = self.p.decrypt_coeffs(ct.level, ct.data, self.s_ntt)

@@ -125,7 +125,7 @@ void *orc_create(int logn, int L, int dnum, u64 seed) {
     o->logn = logn; o->n = 1 << logn; o->L = L; o->dnum = dnum; o->seed = seed;
     o->n_q = L + 3; o->n_ks = L + 2;
     o->alpha = (o->n_ks + dnum - 1) / dnum;
-    o->n_p = o->alpha;
+    o->n_p = o->alpha + 1; /* P exceeds every digit modulus by one prime */
     int tot = o->n_q + o->n_p;
     o->mod = (u32 *)calloc(tot, sizeof(u32));
     u32 *used = (u32 *)calloc(tot, sizeof(u32));
@@ -135,12 +135,12 @@ void *orc_create(int logn, int L, int dnum, u64 seed) {
      * Largest such NTT-friendly primes: base(2), special(alpha), encryption(1). */
     const u64 PMAX = 1431655765ull, PMIN = 1ull << 30;
     u64 cand = (PMAX - 1) / twon * twon + 1;
-    int want = 2 + o->alpha + 1, got = 0;
+    int want = 2 + o->n_p + 1, got = 0;
     u32 big[64];
     while (got < want) { if (cand < PMAX && is_prime32((u32)cand)) big[got++] = (u32)cand; cand -= twon; }
     o->mod[0] = big[0]; o->mod[1] = big[1];
-    for (int k = 0; k < o->alpha; k++) o->mod[o->n_q + k] = big[2 + k];
-    o->mod[o->n_q - 1] = big[2 + o->alpha];
+    for (int k = 0; k < o->n_p; k++) o->mod[o->n_q + k] = big[2 + k];
+    o->mod[o->n_q - 1] = big[2 + o->n_p];
     for (int i = 0; i < want; i++) used[nused++] = big[i];
     /* rescaling chain: level l drops limb l+1; delta_L = 1.25 * 2^30 and each
      * chain prime is the unused one closest to delta_l^2 / (1.25 * 2^30) */
@@ -472,6 +472,21 @@ void orc_rescale(void *h, int level, int npoly, const u32 *in, u32 *out) {
 }
 
 /* ------------------------------------------------------------------ */
+/* centred fast base conversion                       */
+/* y_i in [0, q_i): u = round(sum_i y_i / q_i) from a 32-bit fixed-point */
+/* estimate, mu_i = floor(2^62 / q_i); sum_i y_i qhat_i - u Q is the   */
+/* centred representative of the digit (up to rare boundary ties).     */
+/* ------------------------------------------------------------------ */
+static u32 overflow_count(const u32 *y, size_t stride, int h, const u32 *primes) {
+    u64 f = 0;
+    for (int i = 0; i < h; i++) {
+        u64 mu = (1ull << 62) / primes[i];
+        f += ((u64)y[(size_t)i * stride] * mu) >> 30;
+    }
+    return (u32)((f + (1ull << 31)) >> 32);
+}
+
+/* ------------------------------------------------------------------ */
 /* hybrid key switching                               */
 /* d: (l+2) limbs NTT form; out: 2 x (l+2) limbs NTT form              */
 /* ------------------------------------------------------------------ */
@@ -501,6 +516,8 @@ void orc_keyswitch(void *h, int level, const u32 *d, const u32 *ksk, u32 *out) {
             u32 qhi = invm(qh, q);
             for (int k = 0; k < n; k++) y[(size_t)(i - lo) * n + k] = mulm(coef[(size_t)i * n + k], qhi, q);
         }
+        u32 *ucnt = (u32 *)malloc(sizeof(u32) * n);
+        for (int k = 0; k < n; k++) ucnt[k] = overflow_count(y + k, n, hi - lo, o->mod + lo);
 #pragma omp parallel for schedule(static)
         for (int x = 0; x < ne; x++) {
             u32 *dst = ext + (size_t)x * n;
@@ -512,15 +529,18 @@ void orc_keyswitch(void *h, int level, const u32 *d, const u32 *ksk, u32 *out) {
                 for (int k = lo; k < hi; k++) if (k != i) v = mulm(v, o->mod[k] % t, t);
                 qh_t[i - lo] = v;
             }
+            u32 negQ = 1; /* -Q_j mod t */
+            for (int k = lo; k < hi; k++) negQ = mulm(negQ, o->mod[k] % t, t);
+            negQ = negQ ? t - negQ : 0;
             for (int k = 0; k < n; k++) {
-                u128 s = 0;
+                u128 s = (u64)ucnt[k] * negQ;
                 for (int i = lo; i < hi; i++) s += (u64)y[(size_t)(i - lo) * n + k] * qh_t[i - lo];
                 dst[k] = (u32)(s % t);
             }
             free(qh_t);
             ntt_limb(o, gid[x], dst);
         }
-        free(y);
+        free(y); free(ucnt);
         const u32 *kb = ksk + (size_t)j * 2 * next_key * n, *ka = kb + (size_t)next_key * n;
 #pragma omp parallel for schedule(static)
         for (int x = 0; x < ne; x++) {
@@ -545,6 +565,8 @@ void orc_keyswitch(void *h, int level, const u32 *d, const u32 *ksk, u32 *out) {
             intt_limb(o, g, yp + (size_t)k2 * n);
             for (int k = 0; k < n; k++) yp[(size_t)k2 * n + k] = mulm(yp[(size_t)k2 * n + k], phi, q);
         }
+        u32 *ucnt = (u32 *)malloc(sizeof(u32) * n);
+        for (int k = 0; k < n; k++) ucnt[k] = overflow_count(yp + k, n, np, o->mod + o->n_q);
 #pragma omp parallel for schedule(static)
         for (int t = 0; t < nl; t++) {
             u32 q = o->mod[t];
@@ -556,10 +578,11 @@ void orc_keyswitch(void *h, int level, const u32 *d, const u32 *ksk, u32 *out) {
                 ph_t[k2] = v;
                 pinv = mulm(pinv, o->mod[o->n_q + k2] % q, q);
             }
+            u32 negP = pinv ? q - pinv : 0; /* -P mod q */
             pinv = invm(pinv, q);
             u32 *conv = (u32 *)malloc(sizeof(u32) * n);
             for (int k = 0; k < n; k++) {
-                u128 s = 0;
+                u128 s = (u64)ucnt[k] * negP;
                 for (int k2 = 0; k2 < np; k2++) s += (u64)yp[(size_t)k2 * n + k] * ph_t[k2];
                 conv[k] = (u32)(s % q);
             }
@@ -568,7 +591,7 @@ void orc_keyswitch(void *h, int level, const u32 *d, const u32 *ksk, u32 *out) {
             for (int k = 0; k < n; k++) dst[k] = mulm(subm(a[(size_t)t * n + k], conv[k], q), pinv, q);
             free(conv); free(ph_t);
         }
-        free(yp);
+        free(yp); free(ucnt);
     }
     free(gid); free(kid); free(acc); free(ext); free(coef);
 }
@@ -617,12 +640,13 @@ void orc_automorph(void *h, int level, u64 g, int npoly, const u32 *in, u32 *out
             automorph_limb(o, t, g, in + ((size_t)p * nl + t) * n, out + ((size_t)p * nl + t) * n);
 }
 
-/* public-key encryption of an encoded plaintext given on limbs 0..L+2 (NTT form,
- * encoded at scale delta[L] * q_enc); result rescaled to level L */
-void orc_encrypt(void *h, const u32 *pt, const u32 *pk, u64 ctr, u32 *out) {
+/* public-key encryption at fresh level f: the plaintext is given on
+ * limbs 0..f+2 (NTT form, encoded at scale delta[f] * q_{f+2}); the ciphertext is
+ * formed at level f+1 and rescaled to level f */
+void orc_encrypt(void *h, int f, const u32 *pt, const u32 *pk, u64 ctr, u32 *out) {
     orc_t *o = (orc_t *)h;
-    int n = o->n, nq = o->n_q;
-    size_t P = (size_t)nq * n;
+    int n = o->n, nq = f + 3, npk = o->n_q;
+    size_t P = (size_t)nq * n, PK = (size_t)npk * n;
     int *ids = (int *)malloc(sizeof(int) * nq);
     for (int i = 0; i < nq; i++) ids[i] = i;
     int *v = (int *)malloc(sizeof(int) * n), *e = (int *)malloc(sizeof(int) * n);
@@ -637,10 +661,10 @@ void orc_encrypt(void *h, const u32 *pt, const u32 *pk, u64 ctr, u32 *out) {
         for (int k = 0; k < n; k++) {
             size_t x = (size_t)t * n + k;
             tmp[x] = addm(addm(mulm(vN[x], pk[x], q), e0[x], q), pt[x], q);
-            tmp[P + x] = addm(mulm(vN[x], pk[P + x], q), e1[x], q);
+            tmp[P + x] = addm(mulm(vN[x], pk[PK + x], q), e1[x], q);
         }
     }
-    orc_rescale(h, o->L + 1, 2, tmp, out);
+    orc_rescale(h, f + 1, 2, tmp, out);
     free(ids); free(v); free(e); free(vN); free(e0); free(e1); free(tmp);
 }
 
