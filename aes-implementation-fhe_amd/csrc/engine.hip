@@ -990,6 +990,10 @@ private:
     u32* ring_host_ = nullptr;
     size_t ring_off_ = 0;
     u64 cnt_[C_N] = {};
+
+public:
+    KernelProfiler prof_;
+    void activate() { prof_set(&prof_); }
 };
 
 }  // namespace
@@ -1002,8 +1006,9 @@ struct aesfhe_ctx {
     std::string err;
 };
 
-#define API_BEGIN        \
-    if (!ctx) return -2; \
+#define API_BEGIN                          \
+    if (!ctx) return -2;                   \
+    if (ctx->eng) ctx->eng->activate();    \
     try {
 #define API_END                         \
     return 0;                           \
@@ -1167,6 +1172,22 @@ int aesfhe_debug_keyswitch(aesfhe_ctx* ctx, int level, uint64_t g, const uint32_
 }
 int aesfhe_counters(aesfhe_ctx* ctx, uint64_t* out, int n) {
     API_BEGIN for (int i = 0; i < n; ++i) out[i] = ctx->eng->counter(i);
+    API_END
+}
+int aesfhe_profile(aesfhe_ctx* ctx, uint32_t mask) {
+    API_BEGIN ctx->eng->prof_.flush();
+    ctx->eng->prof_.mask = mask;
+    API_END
+}
+int aesfhe_kernel_stats(aesfhe_ctx* ctx, double* out, int n, int reset) {
+    API_BEGIN KernelProfiler& p = ctx->eng->prof_;
+    p.flush();
+    for (int k = 0; k < n && k < KID_N; ++k) {
+        out[3 * k] = (double)p.launches[k];
+        out[3 * k + 1] = p.ms[k];
+        out[3 * k + 2] = p.bytes[k];
+    }
+    if (reset) p.reset();
     API_END
 }
 int aesfhe_reset_counters(aesfhe_ctx* ctx) {

@@ -3,7 +3,34 @@
 // RNS tensors are row-major [rows][N] u32 with rows = npoly * nl; row r lives modulo
 // prime map.prime(r % nl).  All wrappers are asynchronous on `st`.
 #pragma once
+#include <vector>
+
 #include "common.h"
+
+// --- live kernel timing (HIP events on the launch stream) ----------------------------
+// Kernel ids for per-kernel accounting; bytes are ALGORITHMIC bytes of one launch
+// (every input word read once, every output word written once).
+enum KernelId {
+    KID_NTT_COLS_FWD, KID_NTT_ROWS_FWD, KID_NTT_ROWS_INV, KID_NTT_COLS_INV, KID_BASE_CONVERT, KID_KEY_INNER,
+    KID_MODDOWN, KID_TENSOR, KID_RESCALE, KID_AUTOMORPH, KID_ELEMENTWISE, KID_SAMPLE, KID_N
+};
+struct KernelProfiler {
+    unsigned mask = 0;  // bit k enables event timing of KernelId k
+    struct Rec {
+        hipEvent_t a, b;
+        int kid;
+        double bytes;
+    };
+    std::vector<Rec> recs;
+    std::vector<hipEvent_t> pool;
+    double ms[KID_N] = {}, bytes[KID_N] = {};
+    unsigned long long launches[KID_N] = {};
+    hipEvent_t get();
+    void flush();   // waits for recorded events and folds them into the totals
+    void reset();
+};
+// the profiler of the engine currently issuing launches (set per API call)
+void prof_set(KernelProfiler* p);
 
 struct DevTables {
     const PrimeConst* pc = nullptr;  // [n_tot]

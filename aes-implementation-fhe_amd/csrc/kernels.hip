@@ -359,87 +359,182 @@ inline dim3 ew_grid(int logn, int rows) { return dim3((1u << logn) / kBlock, row
 }  // namespace
 
 // ======================================================================================
+// live timing
+// ======================================================================================
+static thread_local KernelProfiler* g_prof = nullptr;
+void prof_set(KernelProfiler* p) { g_prof = p; }
+
+hipEvent_t KernelProfiler::get() {
+    if (!pool.empty()) {
+        hipEvent_t e = pool.back();
+        pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+}
+void KernelProfiler::flush() {
+    for (auto& r : recs) {
+        float t = 0.f;
+        (void)hipEventSynchronize(r.b);
+        (void)hipEventElapsedTime(&t, r.a, r.b);
+        ms[r.kid] += t;
+        bytes[r.kid] += r.bytes;
+        launches[r.kid] += 1;
+        pool.push_back(r.a);
+        pool.push_back(r.b);
+    }
+    recs.clear();
+}
+void KernelProfiler::reset() {
+    flush();
+    for (int k = 0; k < KID_N; ++k) ms[k] = bytes[k] = 0, launches[k] = 0;
+}
+
+namespace {
+// records a start/stop event pair around one launch when its kernel id is enabled
+struct ProfScope {
+    KernelProfiler* p;
+    hipStream_t st;
+    int kid;
+    double bytes;
+    hipEvent_t a = nullptr;
+    ProfScope(hipStream_t s, int k, double b) : p(g_prof), st(s), kid(k), bytes(b) {
+        if (p && (p->mask >> kid & 1u)) {
+            a = p->get();
+            (void)hipEventRecord(a, st);
+        } else {
+            p = nullptr;
+        }
+    }
+    ~ProfScope() {
+        if (!p) return;
+        hipEvent_t b = p->get();
+        (void)hipEventRecord(b, st);
+        p->recs.push_back({a, b, kid, bytes});
+    }
+};
+inline double words(double w) { return 4.0 * w; }
+}  // namespace
+
+// ======================================================================================
 // launch wrappers
 // ======================================================================================
 void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map) {
     const int S1 = T.logn - 8, ROWS = 1 << S1;
     const size_t lds = sizeof(u32) * ROWS * (kColTile + 1);
-    hipLaunchKernelGGL(k_ntt_cols_fwd, dim3(kR / kColTile, rows), dim3(kBlock), lds, st, data, nl, map, T.pc, T.psi, T.psip, T.logn);
-    hipLaunchKernelGGL(k_ntt_rows_fwd, dim3(ROWS / kRowsPerBlock, rows), dim3(kBlock), 0, st, data, nl, map, T.pc, T.psi, T.psip,
-                       T.logn);
+    const double io = words(2.0 * rows * (1u << T.logn));
+    {
+        ProfScope ps(st, KID_NTT_COLS_FWD, io);
+        hipLaunchKernelGGL(k_ntt_cols_fwd, dim3(kR / kColTile, rows), dim3(kBlock), lds, st, data, nl, map, T.pc, T.psi, T.psip, T.logn);
+    }
+    {
+        ProfScope ps(st, KID_NTT_ROWS_FWD, io);
+        hipLaunchKernelGGL(k_ntt_rows_fwd, dim3(ROWS / kRowsPerBlock, rows), dim3(kBlock), 0, st, data, nl, map, T.pc, T.psi, T.psip,
+                           T.logn);
+    }
     CHECK_LAUNCH();
 }
 void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map) {
     const int S1 = T.logn - 8, ROWS = 1 << S1;
     const size_t lds = sizeof(u32) * ROWS * (kColTile + 1);
-    hipLaunchKernelGGL(k_ntt_rows_inv, dim3(ROWS / kRowsPerBlock, rows), dim3(kBlock), 0, st, data, nl, map, T.pc, T.ipsi, T.ipsip,
-                       T.logn);
-    hipLaunchKernelGGL(k_ntt_cols_inv, dim3(kR / kColTile, rows), dim3(kBlock), lds, st, data, nl, map, T.pc, T.ipsi, T.ipsip, T.logn);
+    const double io = words(2.0 * rows * (1u << T.logn));
+    {
+        ProfScope ps(st, KID_NTT_ROWS_INV, io);
+        hipLaunchKernelGGL(k_ntt_rows_inv, dim3(ROWS / kRowsPerBlock, rows), dim3(kBlock), 0, st, data, nl, map, T.pc, T.ipsi, T.ipsip,
+                           T.logn);
+    }
+    {
+        ProfScope ps(st, KID_NTT_COLS_INV, io);
+        hipLaunchKernelGGL(k_ntt_cols_inv, dim3(kR / kColTile, rows), dim3(kBlock), lds, st, data, nl, map, T.pc, T.ipsi, T.ipsip, T.logn);
+    }
     CHECK_LAUNCH();
 }
+#define EW_WRAP(bytes_words) ProfScope ps_(st, KID_ELEMENTWISE, words((double)(bytes_words) * (1u << T.logn)))
 void launch_add(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int rows, int nl, LimbMap map) {
+    EW_WRAP(3.0 * rows);
     hipLaunchKernelGGL(k_add, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, b, nl, map, T.pc, T.logn);
 }
 void launch_sub(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int rows, int nl, LimbMap map) {
+    EW_WRAP(3.0 * rows);
     hipLaunchKernelGGL(k_sub, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, b, nl, map, T.pc, T.logn);
 }
 void launch_neg(hipStream_t st, const DevTables& T, u32* out, const u32* a, int rows, int nl, LimbMap map) {
+    EW_WRAP(2.0 * rows);
     hipLaunchKernelGGL(k_neg, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, nl, map, T.pc, T.logn);
 }
 void launch_square(hipStream_t st, const DevTables& T, u32* out, const u32* a, int rows, int nl, LimbMap map) {
+    EW_WRAP(2.0 * rows);
     hipLaunchKernelGGL(k_square, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, nl, map, T.pc, T.logn);
 }
 void launch_tensor(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int nl, LimbMap map) {
+    ProfScope ps(st, KID_TENSOR, words(7.0 * nl * (1u << T.logn)));
     hipLaunchKernelGGL(k_tensor, ew_grid(T.logn, nl), dim3(kBlock), 0, st, out, a, b, nl, map, T.pc, T.logn);
 }
 void launch_mul_poly(hipStream_t st, const DevTables& T, u32* out, const u32* in, const u32* pt, int npoly, int nl, LimbMap map) {
+    EW_WRAP((2.0 * npoly + 1.0) * nl);
     hipLaunchKernelGGL(k_mul_poly, ew_grid(T.logn, npoly * nl), dim3(kBlock), 0, st, out, in, pt, nl, map, T.pc, T.logn);
 }
 void launch_fma_poly(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, const u32* c, int rows, int nl,
                      LimbMap map) {
+    EW_WRAP(3.0 * rows + nl);
     hipLaunchKernelGGL(k_fma_poly, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, b, c, nl, map, T.pc, T.logn);
 }
 void launch_mul_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const u32* cst, int rows, int nl, LimbMap map) {
+    EW_WRAP(2.0 * rows);
     hipLaunchKernelGGL(k_mul_const_half, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, cst, nl, map, T.pc, T.logn);
 }
 void launch_add_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const u32* cst, int rows, int nl, LimbMap map) {
+    EW_WRAP(2.0 * rows);
     hipLaunchKernelGGL(k_add_const_half, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, cst, nl, map, T.pc, T.logn);
 }
 void launch_automorph(hipStream_t st, const DevTables& T, u32* out, const u32* in, u64 g, int rows) {
+    ProfScope ps(st, KID_AUTOMORPH, words(2.0 * rows * (1u << T.logn)));
     hipLaunchKernelGGL(k_automorph, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, g, T.logn);
 }
 void launch_rescale_spread(hipStream_t st, const DevTables& T, u32* v, const u32* last, int npoly, int nt, u32 q_last) {
+    ProfScope ps(st, KID_RESCALE, words((double)npoly * (1 + nt) * (1u << T.logn)));
     hipLaunchKernelGGL(k_rescale_spread, dim3((1u << T.logn) / kBlock, nt, npoly), dim3(kBlock), 0, st, v, last, nt, q_last, T.pc,
                        T.logn);
 }
 void launch_rescale_finish(hipStream_t st, const DevTables& T, u32* out, const u32* x, const u32* v, const u32* qinv, int npoly, int nt,
                            int nl_in) {
+    ProfScope ps(st, KID_RESCALE, words(3.0 * npoly * nt * (1u << T.logn)));
     hipLaunchKernelGGL(k_rescale_finish, dim3((1u << T.logn) / kBlock, nt, npoly), dim3(kBlock), 0, st, out, x, v, qinv, nt, nl_in,
                        T.pc, T.logn);
 }
 void launch_base_convert(hipStream_t st, const DevTables& T, u32* ext, const u32* x, int h, int d0, int nt, LimbMap map, int skip0,
                          const u32* tab, const u32* qhinv, const u32* negq) {
+    const int skipped = (skip0 >= 0 && skip0 < nt) ? h : 0;
+    ProfScope ps(st, KID_BASE_CONVERT, words((double)(h + nt - skipped) * (1u << T.logn)));
     hipLaunchKernelGGL(k_base_convert, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, ext, x, h, d0, nt, map, skip0, tab, qhinv,
                        negq, T.pc, T.logn);
 }
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* key, int nd, int ne, int nl, int nkey,
                       int nks, LimbMap map) {
+    // ext (nd x ne) + key (nd x 2 x ne) read, acc (2 x ne) written
+    ProfScope ps(st, KID_KEY_INNER, words((3.0 * nd + 2.0) * ne * (1u << T.logn)));
     hipLaunchKernelGGL(k_key_inner, ew_grid(T.logn, ne), dim3(kBlock), 0, st, acc, ext, key, nd, ne, nl, nkey, nks, map, T.pc, T.logn);
 }
 void launch_moddown_finish(hipStream_t st, const DevTables& T, u32* out, const u32* acc, const u32* conv, const u32* pinv,
                            const u32* add0, const u32* add1, int nl, int ne) {
+    ProfScope ps(st, KID_MODDOWN, words((6.0 + (add0 ? 1 : 0) + (add1 ? 1 : 0)) * nl * (1u << T.logn)));
     hipLaunchKernelGGL(k_moddown_finish, dim3((1u << T.logn) / kBlock, nl, 2), dim3(kBlock), 0, st, out, acc, conv, pinv, add0, add1,
                        nl, ne, T.pc, T.logn);
 }
 void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, u64 seed, u64 stream, int kind) {
+    ProfScope ps(st, KID_SAMPLE, words((double)nl * (1u << T.logn)));
     hipLaunchKernelGGL(k_sample_small, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, nl, map, seed, stream, kind, T.pc,
                        T.logn);
 }
 void launch_sample_uniform(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, u64 seed, u64 stream) {
+    ProfScope ps(st, KID_SAMPLE, words((double)nl * (1u << T.logn)));
     hipLaunchKernelGGL(k_sample_uniform, ew_grid(T.logn, nl), dim3(kBlock), 0, st, out, nl, map, seed, stream, T.pc, T.logn);
 }
 void launch_keygen_combine(hipStream_t st, const DevTables& T, u32* b, const u32* a, const u32* s, const u32* e, const u32* sp,
                            const u32* gadget, int nl, LimbMap map, int glo, int ghi) {
+    EW_WRAP(4.0 * nl);
     hipLaunchKernelGGL(k_keygen_combine, ew_grid(T.logn, nl), dim3(kBlock), 0, st, b, a, s, e, sp, gadget, nl, map, glo, ghi, T.pc,
                        T.logn);
 }

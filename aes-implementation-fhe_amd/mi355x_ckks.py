@@ -35,7 +35,15 @@ EXPORTED = [
     "aesfhe_power_basis", "aesfhe_to_ntt", "aesfhe_to_intt", "aesfhe_bootstrap", "aesfhe_renorm_pair",
     "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
     "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters",
+    "aesfhe_profile", "aesfhe_kernel_stats",
 ]
+
+KERNEL_IDS = ["ntt_cols_fwd", "ntt_rows_fwd", "ntt_rows_inv", "ntt_cols_inv", "base_convert", "key_inner",
+              "moddown", "tensor", "rescale", "automorph", "elementwise", "sample"]
+# the __global__ symbol behind each kernel id (for matching rocprofv3 summaries)
+KERNEL_SYMBOLS = {"ntt_cols_fwd": "k_ntt_cols_fwd", "ntt_rows_fwd": "k_ntt_rows_fwd", "ntt_rows_inv": "k_ntt_rows_inv",
+                  "ntt_cols_inv": "k_ntt_cols_inv", "base_convert": "k_base_convert", "key_inner": "k_key_inner",
+                  "moddown": "k_moddown_finish", "tensor": "k_tensor", "automorph": "k_automorph"}
 
 COUNTER_NAMES = ["mul", "relin", "rot", "conj", "ptmul", "scalar", "rescale", "ntt_rows", "keyswitch",
                  "encrypt", "decrypt", "bootstrap", "add"]
@@ -76,6 +84,8 @@ def load_library(path: Optional[Path] = None):
         "aesfhe_debug_keyswitch": [vp, c_int, ctypes.c_uint64, _up, _up],
         "aesfhe_counters": [vp, np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS"), c_int],
         "aesfhe_reset_counters": [vp],
+        "aesfhe_profile": [vp, ctypes.c_uint32],
+        "aesfhe_kernel_stats": [vp, _dp, c_int, c_int],
     }
     for name in EXPORTED:
         fn = getattr(L, name)
@@ -405,6 +415,19 @@ class Engine:
 
     def reset_counters(self):
         self._ctx.check(self._lib.aesfhe_reset_counters(self._ctx.ptr))
+
+    def profile(self, kernels=()):
+        """Enable HIP-event timing for the named kernel ids (see KERNEL_IDS); () disables."""
+        mask = 0
+        for k in kernels:
+            mask |= 1 << KERNEL_IDS.index(k)
+        self._ctx.check(self._lib.aesfhe_profile(self._ctx.ptr, mask))
+
+    def kernel_stats(self, reset: bool = True) -> dict:
+        out = np.zeros(3 * len(KERNEL_IDS))
+        self._ctx.check(self._lib.aesfhe_kernel_stats(self._ctx.ptr, out, len(KERNEL_IDS), int(reset)))
+        return {k: {"launches": int(out[3 * i]), "ms": float(out[3 * i + 1]), "bytes": float(out[3 * i + 2])}
+                for i, k in enumerate(KERNEL_IDS) if out[3 * i] > 0}
 
     def galois_rotate(self, steps: int) -> int:
         return pow(5, (-steps) % self.slot_count, 2 * self.n)

@@ -1,0 +1,214 @@
+#!/usr/bin/env python
+"""bench.py -- homomorphic AES-128 encryption throughput on MI355X.
+
+Workload (BASELINE.json configs[1], "C2"): full 10-round AES-128 encryption
+(AESPipeline.encrypt, REF/pipeline.py:123-188) of one packed 16-byte state per ciphertext
+pair at N = 2^16, secret-key renorm between steps on (as the reference harness,
+REF/test/test_aes_pipeline_roundtrip.py:132), synthetic random states, FIPS key schedule
+from a seed-7 master key.  One "step" = one full encryption of one state on every rank.
+
+Metric: homomorphic AES-128 rounds/sec (enc) = 10 * states / wall time, summed over ranks
+(independent states shard across GPUs with no collective -- weak scaling).
+
+Launch: python bench.py [--gpus N --steps K --warmup W]; N > 1 under
+torch.distributed.run (one process per GPU; RANK/LOCAL_RANK/WORLD_SIZE from the env).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+PKG = ROOT / "aes-implementation-fhe_amd"
+for _p in (str(ROOT), str(PKG)):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--kernel", default="key_inner", help="kernel id timed live for the roofline")
+    ap.add_argument("--profile-all", action="store_true", help="time every kernel id (diagnostic; slower)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-final-bootstrap", action="store_true",
+                    help="diagnostic only: skip MixColFinal's final bootstrap (not the benchmark workload)")
+    ap.add_argument("--traffic-json", default=None, help="per-launch HBM bytes from a rocprofv3 PMC pass")
+    return ap.parse_args()
+
+
+def dist_setup(want: int):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+        return rank, world, local, dist
+    if want > 1:
+        raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one process per GPU)")
+    return 0, 1, 0, None
+
+
+def barrier(dist):
+    if dist is not None:
+        dist.barrier()
+
+
+def max_over_ranks(dist, x: float) -> float:
+    if dist is None:
+        return x
+    import torch
+    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_baseline(coeffs) -> dict:
+    """Oracle CPU CKKS engine (oracle/ckks_cpu.py), same parameters, timed on one XOR4 LUT
+    (half of an AddRoundKey) and scaled to a round by key-switch count."""
+    from oracle.ckks_cpu import OracleContext
+    from state_encoder import StateEncoder
+    from xor4_lut import XOR4LUT
+    ctx = OracleContext(log_n=16, max_level=17, seed=7)
+    enc = StateEncoder(ctx)
+    xor4 = XOR4LUT(ctx, coeffs["xor4"])
+    rng = np.random.default_rng(0)
+    a = enc.encode(rng.integers(0, 256, 16).astype(np.uint8))
+    b = enc.encode(rng.integers(0, 256, 16).astype(np.uint8))
+    xor4.apply(a[0], b[0])  # warm: relin + conjugation keys
+    t0 = time.perf_counter()
+    xor4.apply(a[0], b[0])
+    dt = time.perf_counter() - t0
+    # one encrypt round = 1,034 relin + 302 conj + 12 rot key switches;
+    # one XOR4 = 78 relin + 14 conj (bootstraps not included in the extrapolation)
+    round_s = dt * (1034 + 302 + 12) / (78 + 14)
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    return {"value": 1.0 / round_s, "unit": "rounds/s", "cores": threads, "kind": "port",
+            "sample": f"one XOR4 LUT (78 relin + 14 conj key switches) on the C oracle at N=2^16, L=17: "
+                      f"{dt:.2f} s; scaled x{(1034 + 302 + 12) / (78 + 14):.2f} to one encrypt round "
+                      f"(key-switch count, bootstraps excluded)"}
+
+
+class _NoFinalBootstrap:
+    """Diagnostic wrapper: MixColFinal without its final bootstrap."""
+
+    def __init__(self, mix):
+        self.mix = mix
+
+    def __call__(self, ct_hi, ct_lo, **kw):
+        return self.mix(ct_hi, ct_lo, do_final_bootstrap=False)
+
+
+def main():
+    args = parse()
+    rank, world, local, dist = dist_setup(args.gpus)
+
+    from aes_keyschedule import expand_aes128_key, load_all_coeffs
+    from engine_context import EngineContext
+    from mixcol_final import MixColFinal
+    from oracle import aes_plain  # checker only: verifies the ciphertext after the timed region
+    from pipeline import AESPipeline
+    from xor4_lut import XOR4LUT
+
+    coeffs = load_all_coeffs()
+    signature = 2 if args.no_final_bootstrap else 1
+    ctx = EngineContext(signature=signature, max_level=17, thread_count=1, device_id=local, seed=0x5EED + rank)
+    xor4 = XOR4LUT(ctx, coeffs["xor4"])
+    mix = MixColFinal(ctx, xor4)
+    if args.no_final_bootstrap:
+        mix = _NoFinalBootstrap(mix)
+    pipe = AESPipeline(ctx, coeffs, mixcolumns=mix, use_hard_renorm_between_steps=True)
+
+    np.random.seed(7)
+    key = np.random.randint(0, 256, 16, dtype=np.uint8)
+    rks = expand_aes128_key(key)
+    rng = np.random.default_rng(2025 + rank)
+    states = [rng.integers(0, 256, 16).astype(np.uint8) for _ in range(args.warmup + args.steps)]
+
+    E = ctx.engine
+    for i in range(args.warmup):
+        pipe.encrypt(states[i], rks)
+    E.sync()
+    kernels = list(__import__("mi355x_ckks").KERNEL_IDS) if args.profile_all else [args.kernel]
+    E.profile(kernels)
+    E.kernel_stats(reset=True)
+    E.reset_counters()
+
+    outs = []
+    barrier(dist)
+    E.sync()
+    t0 = time.perf_counter()
+    for i in range(args.warmup, args.warmup + args.steps):
+        outs.append(pipe.encrypt(states[i], rks))
+    E.sync()
+    barrier(dist)
+    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(dist, elapsed)
+    stats = E.kernel_stats(reset=True)
+    counters = E.counters()
+    E.profile(())
+
+    # correctness of the timed outputs (outside the timed region)
+    ok = all(np.array_equal(pipe.encoder.decode(*o), aes_plain.ref_encrypt(states[args.warmup + j], rks))
+             for j, o in enumerate(outs))
+
+    states_done = args.steps * world
+    value = 10.0 * states_done / elapsed
+    ks = stats.get(args.kernel, {"launches": 0, "ms": 0.0, "bytes": 0.0})
+    achieved = ks["bytes"] / (ks["ms"] * 1e-3) / 1e9 if ks["ms"] > 0 else 0.0
+    traffic = None
+    if args.traffic_json and Path(args.traffic_json).exists():
+        traffic = json.loads(Path(args.traffic_json).read_text()).get(args.kernel)
+    line = {
+        "metric": "homomorphic AES-128 rounds/sec (enc) at N=2^16",
+        "value": value,
+        "unit": "rounds/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32 (RNS residues, primes < 2^32/3)",
+        "data": "synthetic random 16-byte states, FIPS key schedule of a seed-7 master key",
+        "config": {"workload": "C2: full AES-128 encrypt (10 rounds), 1 packed state per ciphertext pair, "
+                               "N=2^16, renorm on" + ("" if not args.no_final_bootstrap else ", FINAL BOOTSTRAP SKIPPED"),
+                   "log_n": 16, "states_per_rank_per_step": 1, "parallelism": f"replicas x{world}",
+                   "blocks_per_s": states_done / elapsed, "verified_against_plaintext_model": bool(ok)},
+        "roofline": {"kernel": args.kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "launches": ks["launches"], "avg_us": ks["ms"] / max(ks["launches"], 1) * 1e3,
+                     "bytes_per_launch": ks["bytes"] / max(ks["launches"], 1)},
+        "op_counts_per_round": {k: v / (10.0 * args.steps) for k, v in counters.items()},
+    }
+    if args.profile_all:
+        line["kernels"] = {k: {"launches": v["launches"], "ms": v["ms"], "GBps": v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] else 0}
+                           for k, v in stats.items()}
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = cpu_baseline(coeffs)
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -108,6 +108,12 @@ int aesfhe_debug_ntt(aesfhe_ctx* ctx, uint32_t* data, int rows, int first_prime,
 int aesfhe_debug_keyswitch(aesfhe_ctx* ctx, int level, uint64_t galois, const uint32_t* d, uint32_t* out);
 /* per-kernel timing of the last N ops (HIP events); op counters */
 int aesfhe_counters(aesfhe_ctx* ctx, uint64_t* out, int n);
+/* live kernel timing with HIP events on the engine stream: bit k of mask enables kernel id k
+ * (order: ntt_cols_fwd, ntt_rows_fwd, ntt_rows_inv, ntt_cols_inv, base_convert, key_inner,
+ * moddown, tensor, rescale, automorph, elementwise, sample); stats: per id
+ * [launches, total ms, algorithmic bytes] */
+int aesfhe_profile(aesfhe_ctx* ctx, uint32_t mask);
+int aesfhe_kernel_stats(aesfhe_ctx* ctx, double* out, int n, int reset);
 int aesfhe_reset_counters(aesfhe_ctx* ctx);
 
 #ifdef __cplusplus
