@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "../../include/aesfhe.h"
+#include "bootstrap.h"
 #include "encoder.h"
 #include "kernels.h"
 #include "params.h"
@@ -32,6 +33,20 @@ namespace {
     } while (0)
 
 inline u64 stream_id(u64 kind, u64 a, u64 b) { return (kind << 56) | (a << 16) | b; }
+
+// host copy of the counter-based PRNG of kernels.hip
+inline u64 hmix64(u64 z) {
+    z ^= z >> 30;
+    z *= 0xbf58476d1ce4e5b9ULL;
+    z ^= z >> 27;
+    z *= 0x94d049bb133111ebULL;
+    z ^= z >> 31;
+    return z;
+}
+inline u64 hprng(u64 seed, u64 stream, u64 ctr) {
+    const u64 k = hmix64(seed ^ hmix64(stream + 0x9E3779B97F4A7C15ULL));
+    return hmix64(k + (ctr + 1) * 0x9E3779B97F4A7C15ULL);
+}
 
 // ---------------------------------------------------------------------------------
 // device memory pool: exact-size free lists (ciphertext sizes repeat constantly)
@@ -77,15 +92,15 @@ struct Ct {
 struct Pt {
     std::vector<double> re, im;
     bool constant = false;
-    std::map<int, u32*> enc;  // level -> NTT-form encoding at scale delta[level]
+    std::map<int, std::pair<u32*, size_t>> enc;  // 2*level + mult -> (NTT-form encoding, words)
 };
 
 enum Counter { C_MUL, C_RELIN, C_ROT, C_CONJ, C_PTMUL, C_SCALAR, C_RESCALE, C_NTT_ROWS, C_KS, C_ENC, C_DEC, C_BOOT, C_ADD, C_N };
 
 class Engine {
 public:
-    Engine(int logn, int L, int dnum, int device, u64 seed) : emb_(logn) {
-        std::string err = hp_.build(logn, L, dnum, seed);
+    Engine(int logn, int L1, int n_double, int dnum, int device, u64 seed) : emb_(logn) {
+        std::string err = hp_.build(logn, L1, n_double, dnum, seed);
         if (!err.empty()) throw std::runtime_error(err);
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
@@ -101,7 +116,7 @@ public:
         (void)hipStreamSynchronize(st_);
         for (auto& kv : cts_) pool_.put(kv.second.data, kv.second.words);
         for (auto& kv : pts_)
-            for (auto& e : kv.second.enc) pool_.put(e.second, (size_t)(e.first + 2) * hp_.n);
+            for (auto& e : kv.second.enc) pool_.put(e.second.first, e.second.second);
         pool_.release_all();
         for (void* p : owned_) (void)hipFree(p);
         for (auto& kv : ksk_) (void)hipFree(kv.second);
@@ -111,7 +126,8 @@ public:
 
     const HostParams& hp() const { return hp_; }
     void set_fresh(int level) {
-        if (level < 0 || level > hp_.L) throw std::runtime_error("fresh level must lie in [0, max_level]");
+        if (level < 0 || level > hp_.L1 || (hp_.L > hp_.L1 && level >= hp_.L1))
+            throw std::runtime_error("fresh level must lie in the single-prime region below its top");
         hp_.fresh = level;
     }
     int slot_count() const { return hp_.n / 2; }
@@ -142,7 +158,7 @@ public:
         }
         auto ip = pts_.find(h);
         if (ip != pts_.end()) {
-            for (auto& e : ip->second.enc) pool_.put(e.second, (size_t)(e.first + 2) * hp_.n);
+            for (auto& e : ip->second.enc) pool_.put(e.second.first, e.second.second);
             pts_.erase(ip);
         }
     }
@@ -163,7 +179,7 @@ public:
         Ct c;
         c.level = level;
         c.npoly = npoly;
-        c.words = (size_t)npoly * (level + 2) * hp_.n;
+        c.words = (size_t)npoly * hp_.nl(level) * hp_.n;
         c.data = pool_.get(c.words);
         return c;
     }
@@ -226,9 +242,19 @@ public:
         void* raw = nullptr;
         HIP_OK(hipMalloc(&raw, ksk_words() * sizeof(u32)));
         u32* key = (u32*)raw;
+        // source secret s' (Q limbs 0..n_ks-1) and target secret (all primes) of the key
         u32* sp = tmp(nks);
-        if (g == 0) launch_square(st_, T_, sp, d_s_, nks, nks, qmap());
-        else launch_automorph(st_, T_, sp, d_s_, g, nks);
+        const u32* target = d_s_;
+        if (g == 0) {
+            launch_square(st_, T_, sp, d_s_, nks, nks, qmap());
+        } else if (g == tag_d2s()) {  // dense s -> sparse ephemeral s_sp (bootstrapping)
+            HIP_OK(hipMemcpyAsync(sp, d_s_, sizeof(u32) * nks * n, hipMemcpyDeviceToDevice, st_));
+            target = sparse_secret();
+        } else if (g == tag_s2d()) {  // sparse s_sp -> dense s
+            HIP_OK(hipMemcpyAsync(sp, sparse_secret(), sizeof(u32) * nks * n, hipMemcpyDeviceToDevice, st_));
+        } else {
+            launch_automorph(st_, T_, sp, d_s_, g, nks);
+        }
         u32* e = tmp(nkey);
         const LimbMap em = extmap(nks);
         for (int j = 0; j < hp_.dnum; ++j) {
@@ -238,7 +264,7 @@ public:
             launch_sample_small(st_, T_, e, nkey, em, hp_.seed, stream_id(5, g, j), 1);
             ntt(e, nkey, nkey, em);
             const int lo = j * hp_.alpha, hi = std::min(nks, lo + hp_.alpha);
-            launch_keygen_combine(st_, T_, b, a, d_s_, e, sp, d_gadget_, nkey, em, lo, hi);
+            launch_keygen_combine(st_, T_, b, a, target, e, sp, d_gadget_, nkey, em, lo, hi);
         }
         untmp(e, nkey);
         untmp(sp, nks);
@@ -274,10 +300,10 @@ public:
     aesfhe_handle encrypt(const double* re, const double* im) {
         if (!d_pk_) throw std::runtime_error("keys not generated");
         // encode at delta_f * q_{f+2} on limbs 0..f+2, encrypt at level f+1, rescale to f
-        const int n = hp_.n, f = hp_.fresh, nq = f + 3;
+        const int n = hp_.n, f = hp_.fresh, nq = hp_.nl(f) + 1;
         const int L = f;
         std::vector<u32> host;
-        encode_host(re, im, hp_.delta[f] * (double)hp_.mod[f + 2], nq, host);
+        encode_host(re, im, hp_.delta[f] * (double)hp_.mod[hp_.nl(f)], nq, host);
         u32* m = upload_ntt(host, nq);
         u32* v = tmp(nq);
         u32* e = tmp(2 * nq);
@@ -305,36 +331,47 @@ public:
         const int n = hp_.n;
         Ct c = ensure_ntt(c_in);
         const int level = c.level;
-        const int nl = c.level + 2;
-        u32* x = tmp(2);
-        HIP_OK(hipMemcpyAsync(x, c.data, sizeof(u32) * 2 * n, hipMemcpyDeviceToDevice, st_));
+        const int nl = hp_.nl(c.level);
+        // limbs used for the CRT: 2 (Q0 ~ 2^60.8) unless the scale is double-prime sized
+        const int kd = (level >= 0 && hp_.delta[level] > 35184372088832.0 && nl >= 4) ? 4 : std::min(2, nl);
+        u32* x = tmp(kd);
+        HIP_OK(hipMemcpyAsync(x, c.data, sizeof(u32) * kd * n, hipMemcpyDeviceToDevice, st_));
         u32* spow = nullptr;
         for (int p = 1; p < c.npoly; ++p) {
             const u32* s_use = d_s_;
             if (p == 2) {
-                spow = tmp(2);
-                launch_square(st_, T_, spow, d_s_, 2, 2, qmap());
+                spow = tmp(kd);
+                launch_square(st_, T_, spow, d_s_, kd, kd, qmap());
                 s_use = spow;
             }
-            launch_fma_poly(st_, T_, x, x, c.data + (size_t)p * nl * n, s_use, 2, 2, qmap());
+            launch_fma_poly(st_, T_, x, x, c.data + (size_t)p * nl * n, s_use, kd, kd, qmap());
         }
-        intt(x, 2, 2, qmap());
-        std::vector<u32> h((size_t)2 * n);
-        HIP_OK(hipMemcpyAsync(h.data(), x, sizeof(u32) * 2 * n, hipMemcpyDeviceToHost, st_));
+        intt(x, kd, kd, qmap());
+        std::vector<u32> h((size_t)kd * n);
+        HIP_OK(hipMemcpyAsync(h.data(), x, sizeof(u32) * kd * n, hipMemcpyDeviceToHost, st_));
         HIP_OK(hipStreamSynchronize(st_));
-        untmp(x, 2);
-        if (spow) untmp(spow, 2);
+        untmp(x, kd);
+        if (spow) untmp(spow, kd);
         if (c.data != c_in.data) release(c);
-        const u32 q0 = hp_.mod[0], q1 = hp_.mod[1];
-        const u64 q0inv = hinvm(q0 % q1, q1);
-        const u64 Q = (u64)q0 * q1;
+        // Garner mixed-radix CRT in 128-bit integers, centred
+        typedef unsigned __int128 u128;
+        std::vector<u64> minv(kd, 0);
+        u128 Qall = 1;
+        for (int i = 0; i < kd; ++i) {
+            if (i) minv[i] = hinvm((u32)(Qall % hp_.mod[i]), hp_.mod[i]);
+            Qall *= hp_.mod[i];
+        }
         m.resize(n);
         for (int k = 0; k < n; ++k) {
-            const u64 a = h[k], b = h[(size_t)n + k];
-            const u64 t = ((b + q1 - a % q1) % q1) * q0inv % q1;
-            const u64 v = a + t * q0;
-            const i64 sv = v > Q / 2 ? (i64)v - (i64)Q : (i64)v;
-            m[k] = (double)sv;
+            u128 v = h[k], M = hp_.mod[0];
+            for (int i = 1; i < kd; ++i) {
+                const u64 qi = hp_.mod[i];
+                const u64 vi = (u64)(v % qi);
+                const u64 t = ((h[(size_t)i * n + k] + qi - vi) % qi) * minv[i] % qi;
+                v += (u128)t * M;
+                M *= qi;
+            }
+            m[k] = v > Qall / 2 ? -(double)(Qall - v) : (double)v;
         }
         cnt_[C_DEC]++;
         return level;
@@ -361,7 +398,7 @@ public:
         Ct o = c;
         if (!c.ntt) {
             o = copy(c);
-            ntt(o.data, o.npoly * (o.level + 2), o.level + 2, qmap());
+            ntt(o.data, o.npoly * hp_.nl(o.level), hp_.nl(o.level), qmap());
             o.ntt = true;
         }
         if (resolve_pending && o.pending) {
@@ -373,33 +410,53 @@ public:
     }
     Ct to_intt(const Ct& c) {
         Ct o = copy(c);
-        if (c.ntt) intt(o.data, o.npoly * (o.level + 2), o.level + 2, qmap());
+        if (c.ntt) intt(o.data, o.npoly * hp_.nl(o.level), hp_.nl(o.level), qmap());
         o.ntt = false;
         return o;
     }
     Ct to_ntt(const Ct& c) {
         Ct o = copy(c);
-        if (!c.ntt) ntt(o.data, o.npoly * (o.level + 2), o.level + 2, qmap());
+        if (!c.ntt) ntt(o.data, o.npoly * hp_.nl(o.level), hp_.nl(o.level), qmap());
         o.ntt = true;
         return o;
     }
 
-    // rescale by the last limb: level l -> l-1
-    Ct rescale(const Ct& c) {
-        if (c.level < 1) throw std::runtime_error("cannot rescale: ciphertext is at level 0 (not enough level)");
-        const int n = hp_.n, nl = c.level + 2, r = nl - 1, np = c.npoly;
-        u32* last = tmp(np);
-        for (int p = 0; p < np; ++p)
-            HIP_OK(hipMemcpyAsync(last + (size_t)p * n, c.data + ((size_t)p * nl + r) * n, sizeof(u32) * n, hipMemcpyDeviceToDevice, st_));
-        intt(last, np, 1, single(r));
-        u32* v = tmp((size_t)np * r);
-        launch_rescale_spread(st_, T_, v, last, np, r, hp_.mod[r]);
-        ntt(v, np * r, r, qmap());
-        Ct o = alloc_ct(c.level - 1, np);
-        o.pending = false;
-        launch_rescale_finish(st_, T_, o.data, c.data, v, d_rescale_qinv_ + rescale_off_[c.level], np, r, nl);
-        untmp(last, np);
-        untmp(v, (size_t)np * r);
+    // drop the last k limbs of an npoly x nl tensor, dividing by each dropped prime with
+    // rounding; returns a pool buffer of npoly x (nl - k) rows
+    u32* drop_limbs(const u32* x, int np, int nl, int k) {
+        const int n = hp_.n;
+        const u32* cur = x;
+        u32* owned = nullptr;
+        for (int step = 0; step < k; ++step) {
+            const int r = nl - 1 - step;  // limb dropped now; cur has r + 1 limbs per poly
+            u32* last = tmp(np);
+            for (int p = 0; p < np; ++p)
+                HIP_OK(hipMemcpyAsync(last + (size_t)p * n, cur + ((size_t)p * (r + 1) + r) * n, sizeof(u32) * n,
+                                      hipMemcpyDeviceToDevice, st_));
+            intt(last, np, 1, single(r));
+            u32* v = tmp((size_t)np * r);
+            launch_rescale_spread(st_, T_, v, last, np, r, hp_.mod[r]);
+            ntt(v, np * r, r, qmap());
+            u32* o = tmp((size_t)np * r);
+            launch_rescale_finish(st_, T_, o, cur, v, d_rescale_qinv_ + rescale_off_[r], np, r, r + 1);
+            untmp(last, np);
+            untmp(v, (size_t)np * r);
+            if (owned) untmp(owned, (size_t)np * (r + 1));
+            owned = o;
+            cur = o;
+        }
+        return owned;
+    }
+
+    // rescale: level l -> l-1, dropping nl(l) - nl(l-1) limbs (1 or 2)
+    Ct rescale(const Ct& c, bool into_base = false) {
+        if (c.level < (into_base ? 0 : 1)) throw std::runtime_error("cannot rescale: ciphertext is at level 0 (not enough level)");
+        const int nl = hp_.nl(c.level), nlo = hp_.nl(c.level - 1);
+        Ct o;
+        o.level = c.level - 1;
+        o.npoly = c.npoly;
+        o.words = (size_t)c.npoly * nlo * hp_.n;
+        o.data = drop_limbs(c.data, c.npoly, nl, nl - nlo);
         cnt_[C_RESCALE]++;
         return o;
     }
@@ -449,29 +506,39 @@ public:
         }
     }
 
+    // exact-scale level drop: keep limbs 0..nl(b)+k-1, multiply by
+    // c = round(delta_b * q_{nl(b)} ... q_{nl(b)+k-1} / delta_a) and divide the k limbs away;
+    // k is the smallest count that keeps c >= 2^24 (k = 1 inside a region, 2 across)
     Ct level_down(const Ct& c_in, int level) {
         if (level == c_in.level) return copy(c_in);
         if (level > c_in.level) throw std::runtime_error("level_down: target level above ciphertext level");
         Ct c = ensure_ntt(c_in);
-        const int n = hp_.n, nl_mid = level + 3;
-        // keep limbs 0..level+2, multiply by round(delta_b q_{b+2} / delta_a), rescale
-        Ct mid = alloc_ct(level + 1, c.npoly);
+        const int n = hp_.n, nb = hp_.nl(level), na = hp_.nl(c.level);
+        int k = 1;
+        double ratio = hp_.delta[level] / hp_.delta[c.level] * (double)hp_.mod[nb];
+        while (ratio < 16777216.0 && nb + k < na) ratio *= (double)hp_.mod[nb + k], ++k;
+        const int nk = nb + k;
+        u32* mid = tmp((size_t)c.npoly * nk);
         for (int p = 0; p < c.npoly; ++p)
-            HIP_OK(hipMemcpyAsync(mid.data + (size_t)p * nl_mid * n, c.data + (size_t)p * (c.level + 2) * n, sizeof(u32) * nl_mid * n,
-                                  hipMemcpyDeviceToDevice, st_));
-        const i64 cst = std::llround(hp_.delta[level] * (double)hp_.mod[level + 2] / hp_.delta[c.level]);
-        std::vector<u32> r(nl_mid);
-        for (int t = 0; t < nl_mid; ++t) r[t] = mod_i64(cst, hp_.mod[t]);
-        u32* d = const_half(r, r);
-        launch_mul_const_half(st_, T_, mid.data, mid.data, d, c.npoly * nl_mid, nl_mid, qmap());
-        Ct o = rescale(mid);
-        release(mid);
+            HIP_OK(hipMemcpyAsync(mid + (size_t)p * nk * n, c.data + (size_t)p * na * n, sizeof(u32) * nk * n, hipMemcpyDeviceToDevice,
+                                  st_));
+        const i64 cst = std::llround(ratio);
+        std::vector<u32> r(nk);
+        for (int t = 0; t < nk; ++t) r[t] = mod_i64(cst, hp_.mod[t]);
+        launch_mul_const_half(st_, T_, mid, mid, const_half(r, r), c.npoly * nk, nk, qmap());
+        Ct o;
+        o.level = level;
+        o.npoly = c.npoly;
+        o.words = (size_t)c.npoly * nb * n;
+        o.data = drop_limbs(mid, c.npoly, nk, k);
+        untmp(mid, (size_t)c.npoly * nk);
         if (c.data != c_in.data) release(c);
         return o;
     }
     // two ciphertexts at a common level (copies only when a level change is needed)
-    std::pair<Ct, Ct> align(const Ct& a, const Ct& b, bool& fa, bool& fb) {
-        const int lv = std::min(a.level - (a.pending ? 1 : 0), b.level - (b.pending ? 1 : 0));
+    std::pair<Ct, Ct> align(const Ct& a, const Ct& b, bool& fa, bool& fb, bool for_mul = false) {
+        int lv = std::min(a.level - (a.pending ? 1 : 0), b.level - (b.pending ? 1 : 0));
+        if (for_mul && !hp_.homogeneous(lv)) --lv;  // never square across the region boundary
         Ct x = ensure_ntt(a), y = ensure_ntt(b);
         fa = x.data != a.data;
         fb = y.data != b.data;
@@ -492,7 +559,7 @@ public:
         bool fa, fb;
         auto xy = align(a, b, fa, fb);
         const Ct &x = xy.first, &y = xy.second;
-        const int nl = x.level + 2;
+        const int nl = hp_.nl(x.level);
         const int np = std::max(x.npoly, y.npoly);
         Ct o = alloc_ct(x.level, np);
         const int common = std::min(x.npoly, y.npoly) * nl;
@@ -514,7 +581,7 @@ public:
 
     Ct add_scalar(const Ct& c_in, double re, double im) {
         Ct c = ensure_ntt(c_in);
-        const int nl = c.level + 2;
+        const int nl = hp_.nl(c.level);
         std::vector<u32> lo, hi;
         scalar_residues(std::llround(re * hp_.delta[c.level]), std::llround(im * hp_.delta[c.level]), nl, lo, hi);
         std::vector<u32> h(2 * (size_t)nl);
@@ -528,7 +595,7 @@ public:
 
     Ct mul_scalar(const Ct& c_in, double re, double im) {
         Ct c = ensure_ntt(c_in);
-        const int nl = c.level + 2;
+        const int nl = hp_.nl(c.level);
         Ct o;
         cnt_[C_SCALAR]++;
         if (re == std::floor(re) && im == std::floor(im) && std::fabs(re) < 1048576.0 && std::fabs(im) < 1048576.0) {
@@ -541,7 +608,8 @@ public:
         } else {
             if (c.level < 1) throw std::runtime_error("not enough level to multiply by a scalar (level 0)");
             std::vector<u32> lo, hi;
-            scalar_residues(std::llround(re * hp_.delta[c.level]), std::llround(im * hp_.delta[c.level]), nl, lo, hi);
+            const double sc = hp_.ptscale[c.level];
+            scalar_residues(std::llround(re * sc), std::llround(im * sc), nl, lo, hi);
             u32* d = const_half(lo, hi);
             Ct t = alloc_ct(c.level, c.npoly);
             launch_mul_const_half(st_, T_, t.data, c.data, d, c.npoly * nl, nl, qmap());
@@ -552,14 +620,17 @@ public:
         return o;
     }
 
-    // plaintext encoded at (level, delta_level), NTT form, cached on the plaintext
-    u32* pt_at(Pt& p, int level) {
-        auto it = p.enc.find(level);
-        if (it != p.enc.end()) return it->second;
+    // plaintext encoded at `level`, NTT form, cached on the plaintext; multiplicative operands
+    // use ptscale[level] (the product rescales onto delta[level-1]), additive ones delta[level]
+    u32* pt_at(Pt& p, int level, bool mult) {
+        const int key = 2 * level + (mult ? 1 : 0);
+        auto it = p.enc.find(key);
+        if (it != p.enc.end()) return it->second.first;
         std::vector<u32> host;
-        encode_host(p.re.data(), p.im.data(), hp_.delta[level], level + 2, host);
-        u32* d = upload_ntt(host, level + 2);
-        p.enc[level] = d;
+        const int nl = hp_.nl(level);
+        encode_host(p.re.data(), p.im.data(), mult ? hp_.ptscale[level] : hp_.delta[level], nl, host);
+        u32* d = upload_ntt(host, nl);
+        p.enc[key] = {d, (size_t)nl * hp_.n};
         return d;
     }
 
@@ -568,8 +639,8 @@ public:
         if (p.constant) return mul_scalar(c_in, p.re[0], p.im[0]);
         if (c_in.level < 1) throw std::runtime_error("not enough level to multiply by a plaintext (level 0)");
         Ct c = ensure_ntt(c_in);
-        const int nl = c.level + 2;
-        u32* e = pt_at(p, c.level);
+        const int nl = hp_.nl(c.level);
+        u32* e = pt_at(p, c.level, true);
         Ct t = alloc_ct(c.level, c.npoly);
         launch_mul_poly(st_, T_, t.data, c.data, e, c.npoly, nl, qmap());
         Ct o = rescale(t);
@@ -583,8 +654,8 @@ public:
         Pt& p = pt(hp);
         if (p.constant) return add_scalar(c_in, p.re[0], p.im[0]);
         Ct c = ensure_ntt(c_in);
-        const int nl = c.level + 2;
-        u32* e = pt_at(p, c.level);
+        const int nl = hp_.nl(c.level);
+        u32* e = pt_at(p, c.level, false);
         Ct o = copy(c);
         launch_add(st_, T_, o.data, c.data, e, nl, nl, qmap());
         if (c.data != c_in.data) release(c);
@@ -594,14 +665,14 @@ public:
     // ------------------------------------------------------------------ key switching
     // returns (c0', c1') with c0' + c1' s = d s' (+ add0/add1 folded in); d NTT, level l
     Ct keyswitch(const u32* d, int level, const u32* key, const u32* add0, const u32* add1) {
-        const int n = hp_.n, nl = level + 2, np = hp_.n_p, ne = nl + np, alpha = hp_.alpha;
+        const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, alpha = hp_.alpha;
         const int nd = (nl + alpha - 1) / alpha;
         const LimbMap em = extmap(nl);
         u32* coef = tmp(nl);
         HIP_OK(hipMemcpyAsync(coef, d, sizeof(u32) * nl * n, hipMemcpyDeviceToDevice, st_));
         intt(coef, nl, nl, qmap());
         u32* ext = tmp((size_t)nd * ne);
-        const size_t* toff = &modup_off_[(size_t)level * hp_.dnum];
+        const size_t* toff = &modup_off_[(size_t)nl * hp_.dnum];
         for (int j = 0; j < nd; ++j) {
             const int lo = j * alpha, h = std::min(alpha, nl - lo);
             u32* ej = ext + (size_t)j * ne * n;
@@ -622,7 +693,7 @@ public:
             HIP_OK(hipMemcpyAsync(yp + (size_t)p * np * n, acc + ((size_t)p * ne + nl) * n, sizeof(u32) * np * n, hipMemcpyDeviceToDevice, st_));
         intt(yp, 2 * np, np, LimbMap{np, hp_.p_off(), 0});
         u32* conv = tmp(2 * (size_t)nl);
-        const size_t doff = moddown_off_[level];
+        const size_t doff = moddown_off_[nl];
         for (int p = 0; p < 2; ++p)
             launch_base_convert(st_, T_, conv + (size_t)p * nl * n, yp + (size_t)p * np * n, np, hp_.p_off(), nl, qmap(), 1 << 30,
                                 d_moddown_ + doff, d_moddown_phinv_, d_negp_);
@@ -640,9 +711,9 @@ public:
         if (a.npoly != 2 || b.npoly != 2) throw std::runtime_error("multiply expects 2-polynomial ciphertexts");
         if (a.level < 1 || b.level < 1) throw std::runtime_error("not enough level to multiply (level 0)");
         bool fa, fb;
-        auto xy = align(a, b, fa, fb);
+        auto xy = align(a, b, fa, fb, true);
         const Ct &x = xy.first, &y = xy.second;
-        const int nl = x.level + 2, n = hp_.n;
+        const int nl = hp_.nl(x.level), n = hp_.n;
         Ct d = alloc_ct(x.level, 3);
         launch_tensor(st_, T_, d.data, x.data, y.data, nl, qmap());
         if (fa) release(x);
@@ -663,7 +734,7 @@ public:
     Ct relinearize(const Ct& c_in) {
         if (c_in.npoly != 3) throw std::runtime_error("relinearize: ciphertext should have 3 polynomials");
         Ct c = ensure_ntt(c_in, false);
-        const int nl = c.level + 2, n = hp_.n;
+        const int nl = hp_.nl(c.level), n = hp_.n;
         Ct r = keyswitch(c.data + (size_t)2 * nl * n, c.level, ksk(0), c.data, c.data + (size_t)nl * n);
         if (c.data != c_in.data) release(c);
         cnt_[C_RELIN]++;
@@ -676,7 +747,7 @@ public:
     Ct galois(const Ct& c_in, u64 g) {
         if (c_in.npoly != 2) throw std::runtime_error("rotation/conjugation expects a 2-polynomial ciphertext");
         Ct c = ensure_ntt(c_in);
-        const int nl = c.level + 2, n = hp_.n;
+        const int nl = hp_.nl(c.level), n = hp_.n;
         const u32* key = ksk(g);
         u32* perm = tmp(2 * (size_t)nl);
         launch_automorph(st_, T_, perm, c.data, g, 2 * nl);
@@ -748,6 +819,283 @@ public:
         *ol = outs[1];
     }
 
+    // ------------------------------------------------------------------ bootstrapping
+    static constexpr int kBootCts = 3, kBootStc = 3, kBootK = 12, kBootR = 3, kBootDeg = 27, kBootMsgBits = 5, kSparseH = 32;
+    static int boot_evalmod_depth() {
+        int cheb = 0;
+        while ((1 << cheb) < kBootDeg) ++cheb;
+        return (cheb + 1) + kBootR;
+    }
+    static int boot_depth() { return kBootCts + boot_evalmod_depth() + kBootStc; }
+    // double-prime levels: CoeffToSlot + EvalMod + the region-crossing first SlotToCoeff group
+    static int boot_double_levels() { return kBootCts + boot_evalmod_depth() + 1; }
+    u64 tag_d2s() const { return 2ull * hp_.n + 1; }
+    u64 tag_s2d() const { return 2ull * hp_.n + 3; }
+
+    // ephemeral sparse ternary secret (h = 32): positions and signs from PRNG stream 9 (host)
+    std::vector<int> sparse_coeffs() const {
+        std::vector<int> s(hp_.n, 0);
+        int cnt = 0;
+        for (u64 ctr = 0; cnt < kSparseH; ++ctr) {
+            const u64 r = hprng(hp_.seed, stream_id(9, 0, 0), ctr);
+            const u64 pos = r % (u64)hp_.n;
+            if (s[pos] == 0) {
+                s[pos] = (r >> 63) ? -1 : 1;
+                ++cnt;
+            }
+        }
+        return s;
+    }
+    const u32* sparse_secret() {
+        if (d_ssp_) return d_ssp_;
+        const int n = hp_.n, nt = hp_.n_tot();
+        const std::vector<int> s = sparse_coeffs();
+        std::vector<u32> h((size_t)nt * n);
+        for (int t = 0; t < nt; ++t)
+            for (int k = 0; k < n; ++k) h[(size_t)t * n + k] = s[k] >= 0 ? (u32)s[k] : hp_.mod[t] - 1;
+        d_ssp_ = dev_alloc((size_t)nt * n);
+        HIP_OK(hipMemcpy(d_ssp_, h.data(), h.size() * sizeof(u32), hipMemcpyHostToDevice));
+        ntt(d_ssp_, nt, nt, qmap());
+        return d_ssp_;
+    }
+
+    struct BootGroupDev {
+        const LinGroup* g = nullptr;
+        std::map<int, std::vector<std::vector<u32*>>> pts;  // level -> [giant][baby] encoded diagonals
+    };
+    struct BootState {
+        bool ready = false;
+        BootPlan plan;
+        int top = 0;
+        double s_bt = 0.0;  // scale of the single-limb (q0) ciphertext
+        i64 k1 = 0;         // integer factor taking delta_0 to s_bt before dropping q1
+        std::vector<BootGroupDev> cts, stc;
+    } bs_;
+
+    void boot_setup() {
+        if (bs_.ready) return;
+        if (hp_.L - hp_.L1 != boot_double_levels() || hp_.L - hp_.fresh < boot_depth())
+            throw std::runtime_error("bootstrap needs the bootstrappable parameter set (use_bootstrap=True): chain has " +
+                                     std::to_string(hp_.L - hp_.fresh) + " spare levels, need " + std::to_string(boot_depth()));
+        bs_.top = hp_.L;
+        const double q0 = hp_.mod[0], q1 = hp_.mod[1];
+        bs_.k1 = std::llround(q0 / std::ldexp(1.0, kBootMsgBits) * q1 / hp_.delta[0]);
+        bs_.s_bt = hp_.delta[0] * (double)bs_.k1 / q1;
+        const double cts_scale = hp_.delta[bs_.top] / (2.0 * q0 * kBootK);
+        const double stc_scale = q0 / (2.0 * M_PI * bs_.s_bt);
+        bs_.plan = make_boot_plan(hp_.logn, kBootCts, kBootStc, cts_scale, stc_scale, kBootK, kBootR, kBootDeg);
+        bs_.cts.assign(bs_.plan.cts.size(), {});
+        bs_.stc.assign(bs_.plan.stc.size(), {});
+        for (size_t i = 0; i < bs_.cts.size(); ++i) bs_.cts[i].g = &bs_.plan.cts[i];
+        for (size_t i = 0; i < bs_.stc.size(); ++i) bs_.stc[i].g = &bs_.plan.stc[i];
+        ksk(tag_d2s());
+        ksk(tag_s2d());
+        bs_.ready = true;
+    }
+
+    Ct rotl(const Ct& c, long k) { return rotate(c, (int)(-k)); }
+    // debug: apply CoeffToSlot group `which` (0..2) or SlotToCoeff group (3..5)
+    Ct debug_lin_group(const Ct& c, int which) {
+        boot_setup();
+        auto& G = which < kBootCts ? bs_.cts[which] : bs_.stc[which - kBootCts];
+        return lin_group(c, G);
+    }
+    void boot_info(double* out) const {
+        out[0] = bs_.s_bt;
+        out[1] = (double)bs_.k1;
+        out[2] = bs_.top;
+        out[3] = kBootK;
+        out[4] = kBootR;
+        out[5] = kBootDeg;
+    }
+
+    // diagonals of one group encoded at `level` (scale delta_level), cached
+    std::vector<std::vector<u32*>>& group_pts(BootGroupDev& G, int level) {
+        auto it = G.pts.find(level);
+        if (it != G.pts.end()) return it->second;
+        const LinGroup& g = *G.g;
+        const int M = slot_count();
+        std::vector<std::vector<u32*>> P(g.G, std::vector<u32*>(g.B, nullptr));
+        std::vector<double> re(M), im(M);
+        std::vector<u32> host;
+        for (int gg = 0; gg < g.G; ++gg)
+            for (int b = 0; b < g.B; ++b) {
+                const auto& d = g.diag[gg][b];
+                if (d.empty()) continue;
+                for (int p = 0; p < M; ++p) re[p] = d[p].real(), im[p] = d[p].imag();
+                encode_host(re.data(), im.data(), hp_.ptscale[level], hp_.nl(level), host);
+                P[gg][b] = upload_ntt(host, hp_.nl(level));
+            }
+        return G.pts.emplace(level, std::move(P)).first->second;
+    }
+
+    // one merged butterfly group, baby-step giant-step (bootstrap.h)
+    Ct lin_group(const Ct& in, BootGroupDev& G) {
+        const LinGroup& g = *G.g;
+        const int l = in.level, nl = hp_.nl(l), n = hp_.n;
+        auto& P = group_pts(G, l);
+        std::vector<Ct> baby(g.B);
+        std::vector<bool> own(g.B, false);
+        for (int b = 0; b < g.B; ++b) {
+            bool used = false;
+            for (int gg = 0; gg < g.G; ++gg) used = used || P[gg][b];
+            if (!used) continue;
+            if (b == 0) baby[b] = in;
+            else baby[b] = rotl(in, (long)g.h * b), own[b] = true;
+        }
+        Ct out;
+        bool have = false;
+        u32* prod = tmp(2 * (size_t)nl);
+        for (int gg = 0; gg < g.G; ++gg) {
+            Ct inner = alloc_ct(l, 2);
+            bool any = false;
+            for (int b = 0; b < g.B; ++b) {
+                if (!P[gg][b]) continue;
+                if (!any) {
+                    launch_mul_poly(st_, T_, inner.data, baby[b].data, P[gg][b], 2, nl, qmap());
+                    any = true;
+                } else {
+                    launch_mul_poly(st_, T_, prod, baby[b].data, P[gg][b], 2, nl, qmap());
+                    launch_add(st_, T_, inner.data, inner.data, prod, 2 * nl, nl, qmap());
+                }
+            }
+            if (!any) {
+                release(inner);
+                continue;
+            }
+            Ct rs = rescale(inner);
+            release(inner);
+            Ct part = g.giant[gg] ? rotl(rs, g.giant[gg]) : rs;
+            if (g.giant[gg]) release(rs);
+            if (!have) {
+                out = part, have = true;
+            } else {
+                Ct s = add_sub(out, part, false);
+                release(out);
+                release(part);
+                out = s;
+            }
+        }
+        untmp(prod, 2 * (size_t)nl);
+        for (int b = 0; b < g.B; ++b)
+            if (own[b]) release(baby[b]);
+        (void)n;
+        return out;
+    }
+
+    Ct lin_transform(const Ct& in, std::vector<BootGroupDev>& groups) {
+        Ct cur = in;
+        bool own = false;
+        for (auto& G : groups) {
+            Ct nx = lin_group(cur, G);
+            if (own) release(cur);
+            cur = nx, own = true;
+        }
+        return cur;
+    }
+
+    // (1/2pi)-free EvalMod: sin(2 pi K y) via Chebyshev cos + r double angles
+    Ct eval_mod(const Ct& y) {
+        const auto& c = bs_.plan.cheb;
+        const int d = (int)c.size() - 1;
+        std::vector<Ct> T(d + 1);
+        T[1] = copy(y);
+        for (int k = 2; k <= d; ++k) {
+            const int a = (k + 1) / 2, b = k / 2;
+            Ct p = mul(T[a], T[b], true);
+            Ct p2 = mul_scalar(p, 2.0, 0.0);
+            release(p);
+            T[k] = (a == b) ? add_scalar(p2, -1.0, 0.0) : add_sub(p2, T[a - b], true);
+            release(p2);
+        }
+        Ct acc = mul_scalar(T[1], c[1], 0.0);
+        for (int k = 2; k <= d; ++k) {
+            Ct t = mul_scalar(T[k], c[k], 0.0);
+            Ct s = add_sub(acc, t, false);
+            release(acc);
+            release(t);
+            acc = s;
+        }
+        Ct g = add_scalar(acc, c[0], 0.0);
+        release(acc);
+        for (int k = 1; k <= d; ++k) release(T[k]);
+        for (int i = 0; i < bs_.plan.r; ++i) {
+            Ct sq = mul(g, g, true);
+            Ct sq2 = mul_scalar(sq, 2.0, 0.0);
+            release(sq);
+            release(g);
+            g = add_scalar(sq2, -1.0, 0.0);
+            release(sq2);
+        }
+        return g;
+    }
+
+    // stop_after (debug): 1 q0-only, 2 after SSE, 3 ModRaise, 4 back to dense, 5 CoeffToSlot,
+    // 6 real part, 7 imaginary part, 8 EvalMod(real), 9 EvalMod(imag), 10 recombined, 11 output
+    Ct bootstrap(const Ct& in, int stop_after = 99) {
+        boot_setup();
+        if (in.npoly != 2) throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
+        const int n = hp_.n, top = bs_.top;
+        // 1. level 0, then scale delta_0 -> s_bt and drop q1: a single-limb ciphertext mod q0
+        Ct c = ensure_ntt(in);
+        Ct z = level_down(c, 0);
+        if (c.data != in.data) release(c);
+        std::vector<u32> r(2);
+        for (int t = 0; t < 2; ++t) r[t] = mod_i64(bs_.k1, hp_.mod[t]);
+        launch_mul_const_half(st_, T_, z.data, z.data, const_half(r, r), 4, 2, qmap());
+        Ct b = rescale(z, true);
+        release(z);
+        if (stop_after == 1) return b;
+        // 2. sparse-secret encapsulation: dense s -> sparse s_sp at modulus q0
+        Ct sp = keyswitch(b.data + n, -1, ksk(tag_d2s()), b.data, nullptr);
+        release(b);
+        if (stop_after == 2) return sp;
+        // 3. ModRaise: centred lift of both polynomials to every limb of the top level
+        intt(sp.data, 2, 1, single(0));
+        Ct raised = alloc_ct(top, 2);
+        launch_rescale_spread(st_, T_, raised.data, sp.data, 2, hp_.nl(top), hp_.mod[0]);
+        release(sp);
+        const int nlt = hp_.nl(top);
+        ntt(raised.data, 2 * nlt, nlt, qmap());
+        if (stop_after == 3) return raised;
+        // 4. back to the dense secret
+        Ct u = keyswitch(raised.data + (size_t)nlt * n, top, ksk(tag_s2d()), raised.data, nullptr);
+        release(raised);
+        if (stop_after == 4) return u;
+        // 5. CoeffToSlot (bit-reversed coefficient halves / (2 q0 K))
+        Ct w = lin_transform(u, bs_.cts);
+        release(u);
+        if (stop_after == 5) return w;
+        // 6. real / imaginary parts (exact: conjugation, add, multiply by -i)
+        Ct cj = conjugate(w);
+        Ct re = add_sub(w, cj, false);
+        Ct dif = add_sub(w, cj, true);
+        release(w);
+        release(cj);
+        Ct im = mul_scalar(dif, 0.0, -1.0);
+        release(dif);
+        if (stop_after == 6) return release(im), re;
+        if (stop_after == 7) return release(re), im;
+        // 7. EvalMod on both halves
+        Ct fre = eval_mod(re);
+        release(re);
+        if (stop_after == 8) return release(im), fre;
+        Ct fim = eval_mod(im);
+        release(im);
+        if (stop_after == 9) return release(fre), fim;
+        Ct ifim = mul_scalar(fim, 0.0, 1.0);
+        release(fim);
+        Ct wp = add_sub(fre, ifim, false);
+        release(fre);
+        release(ifim);
+        if (stop_after == 10) return wp;
+        // 8. SlotToCoeff (scaled back to the message)
+        Ct out = lin_transform(wp, bs_.stc);
+        release(wp);
+        cnt_[C_BOOT]++;
+        return out;
+    }
+
     // ------------------------------------------------------------------ raw access
     void export_ct(aesfhe_handle h, u32* out, u64 words) {
         const Ct& c0 = ct(h);
@@ -758,7 +1106,7 @@ public:
         if (c.data != c0.data) release(c);
     }
     aesfhe_handle import_ct(int level, int npoly, const u32* data) {
-        if (level < 0 || level > hp_.L + 1 || npoly < 1 || npoly > 3) throw std::runtime_error("import: bad level/npoly");
+        if (level < -1 || level > hp_.L || npoly < 1 || npoly > 3) throw std::runtime_error("import: bad level/npoly");
         Ct c = alloc_ct(level, npoly);
         HIP_OK(hipMemcpyAsync(c.data, data, c.words * sizeof(u32), hipMemcpyHostToDevice, st_));
         HIP_OK(hipStreamSynchronize(st_));
@@ -787,7 +1135,7 @@ public:
         untmp(d, rows);
     }
     void debug_keyswitch(int level, u64 g, const u32* d_host, u32* out) {
-        const int nl = level + 2;
+        const int nl = hp_.nl(level);
         u32* d = tmp(nl);
         HIP_OK(hipMemcpyAsync(d, d_host, sizeof(u32) * nl * hp_.n, hipMemcpyHostToDevice, st_));
         Ct o = keyswitch(d, level, ksk(g), nullptr, nullptr);
@@ -849,13 +1197,13 @@ private:
 
         const auto& q = hp_.mod;
         auto mulm = [](u64 a, u64 b, u32 m) { return (u32)(a % m * (b % m) % m); };
-        // rescale: per level l >= 1, q_{l+1}^{-1} mod q_t for t <= l
+        // rescale: per dropped limb r >= 1, q_r^{-1} mod q_t for t < r
         std::vector<u32> rq;
-        rescale_off_.assign(hp_.L + 2, 0);
-        for (int l = 1; l <= hp_.L + 1; ++l) {
-            rescale_off_[l] = rq.size();
-            const u32 qr = q[l + 1];
-            for (int t = 0; t <= l; ++t) {
+        rescale_off_.assign(hp_.n_q, 0);
+        for (int r = 1; r < hp_.n_q; ++r) {
+            rescale_off_[r] = rq.size();
+            const u32 qr = q[r];
+            for (int t = 0; t < r; ++t) {
                 const u32 v = hinvm(qr % q[t], q[t]);
                 rq.push_back(v);
                 rq.push_back(shoup_pre(v, q[t]));
@@ -875,12 +1223,12 @@ private:
 
         // ModUp tables per (level, digit): [h][ne] Shoup pairs of qhat_i mod target, then [h] qhat_i^{-1} mod q_i
         std::vector<u32> mu;
-        modup_off_.assign((size_t)(hp_.L + 1) * hp_.dnum, 0);
-        for (int l = 0; l <= hp_.L; ++l) {
-            const int nl = l + 2, ne = nl + hp_.n_p;
+        modup_off_.assign((size_t)(hp_.n_ks + 1) * hp_.dnum, 0);  // indexed by limb count nl = 1..n_ks
+        for (int nl = 1; nl <= hp_.n_ks; ++nl) {
+            const int ne = nl + hp_.n_p;
             for (int j = 0; j < hp_.dnum; ++j) {
                 const int lo = j * hp_.alpha;
-                modup_off_[(size_t)l * hp_.dnum + j] = mu.size();
+                modup_off_[(size_t)nl * hp_.dnum + j] = mu.size();
                 if (lo >= nl) continue;
                 const int h = std::min(hp_.alpha, nl - lo);
                 for (int i = 0; i < h; ++i)
@@ -913,11 +1261,10 @@ private:
 
         // ModDown tables per level: [np][nl] Shoup pairs of phat_k mod q_t; phat_k^{-1} mod p_k; P^{-1} mod q_t
         std::vector<u32> md;
-        moddown_off_.assign(hp_.L + 2, 0);
+        moddown_off_.assign(hp_.n_ks + 1, 0);  // indexed by limb count nl = 1..n_ks
         const int np = hp_.n_p;
-        for (int l = 0; l <= hp_.L; ++l) {
-            const int nl = l + 2;
-            moddown_off_[l] = md.size();
+        for (int nl = 1; nl <= hp_.n_ks; ++nl) {
+            moddown_off_[nl] = md.size();
             for (int k = 0; k < np; ++k)
                 for (int t = 0; t < nl; ++t) {
                     u32 v = 1;
@@ -972,6 +1319,7 @@ private:
     aesfhe_handle next_ = 1;
     u32* d_s_ = nullptr;
     u32* d_pk_ = nullptr;
+    u32* d_ssp_ = nullptr;
     std::map<u64, u32*> ksk_;
     u64 enc_ctr_ = 0;
     std::vector<u32> im_;
@@ -1025,7 +1373,7 @@ int aesfhe_create(aesfhe_ctx** out, int log_n, int max_level, int dnum, int devi
     *out = nullptr;
     auto* c = new aesfhe_ctx();
     try {
-        c->eng.reset(new Engine(log_n, max_level, dnum, device_id, seed));
+        c->eng.reset(new Engine(log_n, max_level, 0, dnum, device_id, seed));
     } catch (const std::exception& e) {
         c->err = e.what();
         *out = c;
@@ -1033,6 +1381,25 @@ int aesfhe_create(aesfhe_ctx** out, int log_n, int max_level, int dnum, int devi
     }
     *out = c;
     return 0;
+}
+int aesfhe_create_boot(aesfhe_ctx** out, int log_n, int fresh_level, int dnum, int device_id, uint64_t seed) {
+    *out = nullptr;
+    auto* c = new aesfhe_ctx();
+    *out = c;
+    try {
+        const int L1 = fresh_level + Engine::kBootStc - 1;
+        c->eng.reset(new Engine(log_n, L1, Engine::boot_double_levels(), dnum, device_id, seed));
+        c->eng->set_fresh(fresh_level);
+    } catch (const std::exception& e) {
+        c->err = e.what();
+        return -1;
+    }
+    return 0;
+}
+int aesfhe_level_limbs(aesfhe_ctx* ctx, int32_t* out) {
+    API_BEGIN const HostParams& p = ctx->eng->hp();
+    for (int l = 0; l <= p.L; ++l) out[l] = p.nl(l);
+    API_END
 }
 int aesfhe_destroy(aesfhe_ctx* ctx) {
     delete ctx;
@@ -1133,10 +1500,22 @@ int aesfhe_power_basis(aesfhe_ctx* ctx, aesfhe_handle c, int degree, aesfhe_hand
 }
 int aesfhe_to_ntt(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.to_ntt(e.ct(c))) }
 int aesfhe_to_intt(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.to_intt(e.ct(c))) }
-int aesfhe_bootstrap(aesfhe_ctx* ctx, aesfhe_handle, aesfhe_handle*) {
-    if (!ctx) return -2;
-    ctx->err = "bootstrap is not available in this build (use_bootstrap parameter set pending)";
-    return -1;
+int aesfhe_bootstrap(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.bootstrap(e.ct(c))) }
+int aesfhe_bootstrap_depth(void) { return Engine::boot_depth(); }
+int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle c, int stage, aesfhe_handle* out) { CT_OP(e.bootstrap(e.ct(c), stage)) }
+int aesfhe_debug_lin_group(aesfhe_ctx* ctx, aesfhe_handle c, int which, aesfhe_handle* out) {
+    CT_OP(e.debug_lin_group(e.ct(c), which))
+}
+int aesfhe_export_sparse(aesfhe_ctx* ctx, uint32_t* out) {
+    API_BEGIN Engine& e = *ctx->eng;
+    e.export_dev(e.sparse_secret(), (size_t)e.hp().n_tot() * e.hp().n, out);
+    API_END
+}
+int aesfhe_boot_info(aesfhe_ctx* ctx, double* out) {
+    API_BEGIN Engine& e = *ctx->eng;
+    e.boot_setup();
+    e.boot_info(out);
+    API_END
 }
 int aesfhe_renorm_pair(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle* out_hi, aesfhe_handle* out_lo) {
     API_BEGIN ctx->eng->renorm_pair(hi, lo, out_hi, out_lo);

@@ -52,16 +52,22 @@ static u32 root_2n(u32 q, int logn) {
     }
 }
 
-std::string HostParams::build(int logn_, int L_, int dnum_, uint64_t seed_) {
+bool HostParams::homogeneous(int level) const { return !(L > L1 && level == L1 + 1); }
+
+std::string HostParams::build(int logn_, int L1_, int n_double, int dnum_, uint64_t seed_) {
     if (logn_ < 10 || logn_ > 17) return "log_n must lie in [10, 17]";
-    if (L_ < 1 || L_ > 60) return "max_level must lie in [1, 60]";
+    if (L1_ < 1 || L1_ > 60 || n_double < 0 || n_double > 30) return "max_level must lie in [1, 60]";
     if (dnum_ < 1) return "dnum must be >= 1";
-    logn = logn_; n = 1 << logn; L = L_; dnum = dnum_; seed = seed_;
-    n_q = L + 3;
-    n_ks = L + 2;
+    logn = logn_; n = 1 << logn; L1 = L1_; L = L1 + n_double; dnum = dnum_; seed = seed_;
+    nl_of.assign(L + 3, 0);
+    nl_of[0] = 1;  // level -1: q0 only
+    for (int l = 0; l <= L; ++l) nl_of[l + 1] = l <= L1 ? l + 2 : L1 + 2 + 2 * (l - L1);
+    nl_of[L + 2] = nl_of[L + 1] + 1;  // transient level of a top-level encryption
+    n_ks = nl(L);
+    n_q = n_ks + 1;
     alpha = (n_ks + dnum - 1) / dnum;
     n_p = alpha + 1;  // P exceeds every digit modulus by one prime
-    fresh = L;
+    fresh = L1;
     mod.assign(n_tot(), 0);
 
     const uint64_t kMax = 1431655765ull;  // floor(2^32 / 3): keeps 3q < 2^32
@@ -69,7 +75,7 @@ std::string HostParams::build(int logn_, int L_, int dnum_, uint64_t seed_) {
     const uint64_t two_n = 2ull << logn;
     std::set<u32> taken;
 
-    // largest admissible primes: 2 base, alpha special, 1 encryption
+    // largest admissible primes: 2 base, n_p special, 1 encryption
     std::vector<u32> top;
     for (uint64_t c = (kMax - 1) / two_n * two_n + 1; top.size() < (size_t)(2 + n_p + 1); c -= two_n) {
         if (c <= kMin) return "ran out of NTT-friendly primes";
@@ -81,12 +87,8 @@ std::string HostParams::build(int logn_, int L_, int dnum_, uint64_t seed_) {
     mod[n_q - 1] = top[2 + n_p];
     taken.insert(top.begin(), top.end());
 
-    // rescaling chain: delta_L = 1.25 * 2^30; limb l+1 = prime closest to delta_l^2 / target
-    const double kTarget = 1342177280.0;
-    delta.assign(L + 1, 0.0);
-    delta[L] = kTarget;
-    for (int l = L; l >= 1; --l) {
-        const double want = delta[l] * delta[l] / kTarget;
+    // unused admissible prime closest to `want` (ties -> smaller)
+    auto closest = [&](double want) -> u32 {
         const int64_t centre = (int64_t)((want - 1.0) / (double)two_n + 0.5) * (int64_t)two_n + 1;
         u32 best = 0;
         double best_d = 1e300;
@@ -100,10 +102,44 @@ std::string HostParams::build(int logn_, int L_, int dnum_, uint64_t seed_) {
             }
             if (best && (double)s * (double)two_n > best_d + (double)two_n) break;
         }
-        if (!best) return "could not place a rescaling prime";
-        mod[l + 1] = best;
-        taken.insert(best);
-        delta[l - 1] = delta[l] * delta[l] / (double)best;
+        if (best) taken.insert(best);
+        return best;
+    };
+
+    const double kT = 1342177280.0;  // 1.25 * 2^30
+    delta.assign(L + 1, 0.0);
+    // single-prime region: delta_L1 = T; limb nl(l)-1 = l+1 is the prime closest to delta_l^2 / T
+    delta[L1] = kT;
+    for (int l = L1; l >= 1; --l) {
+        const u32 q = closest(delta[l] * delta[l] / kT);
+        if (!q) return "could not place a rescaling prime";
+        mod[l + 1] = q;
+        delta[l - 1] = delta[l] * delta[l] / (double)q;
+    }
+    // double-prime region: delta_L = T^2; levels L..L1+2 drop the pair (qa, qb) closest to
+    // sqrt(delta_l^2 / T^2) and its cofactor
+    if (L > L1) {
+        delta[L] = kT * kT;
+        for (int l = L; l >= L1 + 2; --l) {
+            const double want = delta[l] * delta[l] / (kT * kT);
+            const u32 qa = closest(std::sqrt(want));
+            const u32 qb = qa ? closest(want / (double)qa) : 0;
+            if (!qa || !qb) return "could not place a rescaling prime pair";
+            mod[nl(l) - 1] = qa;
+            mod[nl(l) - 2] = qb;
+            delta[l - 1] = delta[l] * delta[l] / ((double)qa * (double)qb);
+        }
+        // transition level L1+1 -> L1: a pair near T, crossed only by plaintext products
+        const u32 qa = closest(kT), qb = closest(kT);
+        if (!qa || !qb) return "could not place the transition primes";
+        mod[nl(L1 + 1) - 1] = qa;
+        mod[nl(L1 + 1) - 2] = qb;
+    }
+    ptscale.assign(L + 1, 0.0);
+    for (int l = 1; l <= L; ++l) {
+        double qd = 1.0;
+        for (int t = nl(l - 1); t < nl(l); ++t) qd *= (double)mod[t];
+        ptscale[l] = delta[l - 1] * qd / delta[l];
     }
     psi.resize(n_tot());
     for (int i = 0; i < n_tot(); ++i) psi[i] = root_2n(mod[i], logn);

@@ -1,8 +1,10 @@
 // params.h -- RNS-CKKS parameter set for the MI355X engine.
 //
-// Limb layout: Q limbs 0..n_q-1 = [2 base][L rescaling primes][1 encryption prime],
-// followed by the n_p special (key-switching) primes.  A ciphertext at level l lives
-// on Q limbs 0..l+1; level l rescales by dropping limb l+1.
+// Limb layout: Q limbs 0..n_q-1 = [2 base][rescaling primes][1 encryption prime], then the
+// n_p special (key-switching) primes.  Levels 0..L1 drop one prime per rescale (scale
+// delta ~ 1.25 * 2^30); levels L1+1..L drop two primes per rescale (scale ~ 2^60.6, the
+// bootstrapping region).  A ciphertext at level l lives on Q limbs
+// 0..nl(l)-1; level -1 (one limb, q0) exists only inside bootstrapping.
 #pragma once
 #include <cstdint>
 #include <string>
@@ -12,25 +14,31 @@
 
 struct HostParams {
     int logn = 16, n = 1 << 16;
-    int L = 17;       // top user level (fresh ciphertexts)
-    int dnum = 3;     // key-switching digits
-    int alpha = 7;    // limbs per digit (= special primes)
-    int n_q = 20;     // L + 3
-    int n_ks = 19;    // L + 2 (limbs reachable by key switching)
-    int n_p = 8;
-    int fresh = 17;   // level of fresh encryptions (<= L)
+    int L = 17;        // top level
+    int L1 = 17;       // top level of the single-prime region (== L without bootstrapping)
+    int dnum = 3;      // key-switching digits
+    int alpha = 7;     // limbs per digit
+    int n_q = 20;      // Q limbs incl. the encryption limb
+    int n_ks = 19;     // limbs reachable by key switching
+    int n_p = 8;       // special primes (alpha + 1)
+    int fresh = 17;    // level of fresh encryptions (<= L1)
     uint64_t seed = 0;
 
-    std::vector<u32> mod;       // n_q + n_p primes
-    std::vector<double> delta;  // delta[l], l = 0..L
-    std::vector<u32> psi;       // primitive 2N-th root per prime
+    std::vector<u32> mod;        // n_q + n_p primes
+    std::vector<double> delta;   // delta[l], l = 0..L
+    std::vector<double> ptscale; // ptscale[l]: plaintext scale so that ct x pt -> rescale lands on delta[l-1]
+    std::vector<int> nl_of;      // limbs at level l, stored at index l + 1 for l = -1..L+1
+    std::vector<u32> psi;        // primitive 2N-th root per prime
 
     int n_tot() const { return n_q + n_p; }
-    int p_off() const { return n_q; }     // global index of the first special prime
+    int p_off() const { return n_q; }        // global index of the first special prime
     int enc_limb() const { return n_q - 1; }
+    int nl(int level) const { return nl_of[level + 1]; }
+    // Delta_l^2 / Q_drop(l) == Delta_{l-1}: ct x ct products may be rescaled directly
+    bool homogeneous(int level) const;
 
     // builds the prime chain and scales; returns "" or an error message
-    std::string build(int logn, int L, int dnum, uint64_t seed);
+    std::string build(int logn, int L1, int n_double, int dnum, uint64_t seed);
 };
 
 // host modular helpers (64-bit, used for table generation only)

@@ -35,7 +35,9 @@ EXPORTED = [
     "aesfhe_power_basis", "aesfhe_to_ntt", "aesfhe_to_intt", "aesfhe_bootstrap", "aesfhe_renorm_pair",
     "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
     "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters",
-    "aesfhe_profile", "aesfhe_kernel_stats",
+    "aesfhe_profile", "aesfhe_kernel_stats", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan",
+    "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot",
+    "aesfhe_level_limbs", "aesfhe_debug_lin_group",
 ]
 
 KERNEL_IDS = ["ntt_cols_fwd", "ntt_rows_fwd", "ntt_rows_inv", "ntt_cols_inv", "base_convert", "key_inner",
@@ -87,6 +89,14 @@ def load_library(path: Optional[Path] = None):
         "aesfhe_profile": [vp, ctypes.c_uint32],
         "aesfhe_kernel_stats": [vp, _dp, c_int, c_int],
     }
+    sig["aesfhe_bootstrap_depth"] = []
+    sig["aesfhe_debug_bootplan"] = [c_int, _dp]
+    sig["aesfhe_debug_boot_stage"] = [vp, _H, c_int, _Hp]
+    sig["aesfhe_export_sparse"] = [vp, _up]
+    sig["aesfhe_boot_info"] = [vp, _dp]
+    sig["aesfhe_debug_lin_group"] = [vp, _H, c_int, _Hp]
+    sig["aesfhe_create_boot"] = [pp, c_int, c_int, c_int, c_int, ctypes.c_uint64]
+    sig["aesfhe_level_limbs"] = [vp, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")]
     for name in EXPORTED:
         fn = getattr(L, name)
         fn.restype = ctypes.c_char_p if name == "aesfhe_last_error" else ctypes.c_int
@@ -98,10 +108,11 @@ def load_library(path: Optional[Path] = None):
 class _Context:
     """Owns one aesfhe_ctx; destroyed when the last object referring to it dies."""
 
-    def __init__(self, log_n, max_level, dnum, device_id, seed):
+    def __init__(self, log_n, max_level, dnum, device_id, seed, bootstrappable=False):
         self.lib = load_library()
         ptr = ctypes.c_void_p()
-        rc = self.lib.aesfhe_create(ctypes.byref(ptr), log_n, max_level, dnum, device_id, seed)
+        create = self.lib.aesfhe_create_boot if bootstrappable else self.lib.aesfhe_create
+        rc = create(ctypes.byref(ptr), log_n, max_level, dnum, device_id, seed)
         self.ptr = ptr
         if rc != 0:
             msg = self.lib.aesfhe_last_error(ptr).decode() if ptr.value else "aesfhe_create failed"
@@ -220,13 +231,18 @@ class Engine:
             raise ValueError("multiparty key generation is not supported")
         self.mode = mode
         self.use_bootstrap = use_bootstrap
-        self._ctx = _Context(log_n, max_level, dnum, device_id, seed)
+        # bootstrappable set: the chain is extended by the bootstrap depth above the fresh level
+        self._ctx = _Context(log_n, max_level, dnum, device_id, seed, bootstrappable=use_bootstrap)
         L = self._ctx.lib
+        self.fresh_level = max_level
         self.slot_count = int(L.aesfhe_slot_count(self._ctx.ptr))
         self.max_level = int(L.aesfhe_max_level(self._ctx.ptr))
         info = np.zeros(8, np.int32)
         self._ctx.check(L.aesfhe_info(self._ctx.ptr, info))
         self.n, self.L, self.n_q, self.n_ks, self.n_p, self.alpha, self.dnum, self.log_n = map(int, info)
+        limbs = np.zeros(self.L + 1, np.int32)
+        self._ctx.check(L.aesfhe_level_limbs(self._ctx.ptr, limbs))
+        self.level_limbs = [int(x) for x in limbs]
         self._keys_ready = False
 
     # ------------------------------------------------------------------ internals
@@ -343,6 +359,23 @@ class Engine:
     def bootstrap(self, ct, relinearization_key=None, conjugation_key=None, bootstrap_key=None):
         return self._new(self._lib.aesfhe_bootstrap, ct.handle)
 
+    def debug_boot_stage(self, ct, stage: int):
+        return self._new(self._lib.aesfhe_debug_boot_stage, ct.handle, int(stage))
+
+    def debug_lin_group(self, ct, which: int):
+        return self._new(self._lib.aesfhe_debug_lin_group, ct.handle, int(which))
+
+    def export_sparse(self) -> np.ndarray:
+        out = np.zeros((self.n_q + self.n_p, self.n), np.uint32)
+        self._ctx.check(self._lib.aesfhe_export_sparse(self._ctx.ptr, out))
+        return out
+
+    def boot_info(self) -> dict:
+        self._ensure_keys()
+        out = np.zeros(6)
+        self._ctx.check(self._lib.aesfhe_boot_info(self._ctx.ptr, out))
+        return dict(zip(["s_bt", "k1", "top", "K", "r", "deg"], out.tolist()))
+
     def ntt(self, ct):
         return self._new(self._lib.aesfhe_to_ntt, ct.handle)
 
@@ -370,7 +403,7 @@ class Engine:
 
     def export(self, ct: Ciphertext) -> np.ndarray:
         npoly = ct.num_polys
-        out = np.zeros((npoly, ct.level + 2, self.n), np.uint32)
+        out = np.zeros((npoly, self.nl(ct.level), self.n), np.uint32)
         self._ctx.check(self._lib.aesfhe_export(self._ctx.ptr, ct.handle, out, out.size))
         return out
 
@@ -401,9 +434,13 @@ class Engine:
         self._ctx.check(self._lib.aesfhe_debug_ntt(self._ctx.ptr, d, d.shape[0], int(first_prime), int(inverse)))
         return d
 
+    def nl(self, level: int) -> int:
+        """limbs of a ciphertext at `level` (level -1: the single bootstrapping limb)"""
+        return 1 if level == -1 else self.level_limbs[level]
+
     def debug_keyswitch(self, level: int, galois: int, d: np.ndarray) -> np.ndarray:
         self._ensure_keys()
-        out = np.zeros((2, level + 2, self.n), np.uint32)
+        out = np.zeros((2, self.nl(level), self.n), np.uint32)
         self._ctx.check(self._lib.aesfhe_debug_keyswitch(self._ctx.ptr, int(level), int(galois),
                                                          np.ascontiguousarray(d, np.uint32), out))
         return out
@@ -435,3 +472,14 @@ class Engine:
     @property
     def galois_conj(self) -> int:
         return 2 * self.n - 1
+
+
+def bootstrap_depth() -> int:
+    return int(load_library().aesfhe_bootstrap_depth())
+
+
+def debug_bootplan(log_n: int = 16) -> np.ndarray:
+    """Host self-check of the bootstrap plan (errors of StC, CtS, EvalMod polynomial)."""
+    err = np.zeros(3)
+    load_library().aesfhe_debug_bootplan(int(log_n), err)
+    return err

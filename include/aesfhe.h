@@ -34,6 +34,11 @@ typedef uint64_t aesfhe_handle;
 /* --- context / keys -------------------------------------------------------------- */
 /* replaces desilofhe.Engine(...) construction, REF/engine_context.py:17-39 */
 int aesfhe_create(aesfhe_ctx** out, int log_n, int max_level, int dnum, int device_id, uint64_t seed);
+/* bootstrappable parameter set: fresh ciphertexts at fresh_level, the chain extended by
+ * aesfhe_bootstrap_depth() levels (CoeffToSlot/EvalMod on double-prime levels) */
+int aesfhe_create_boot(aesfhe_ctx** out, int log_n, int fresh_level, int dnum, int device_id, uint64_t seed);
+/* limbs per level 0..max_level (a ciphertext at level l has npoly x limbs[l] x N words) */
+int aesfhe_level_limbs(aesfhe_ctx* ctx, int32_t* out);
 int aesfhe_destroy(aesfhe_ctx* ctx);
 const char* aesfhe_last_error(aesfhe_ctx* ctx);
 /* replaces create_secret_key / create_public_key / create_relinearization_key /
@@ -88,8 +93,21 @@ int aesfhe_power_basis(aesfhe_ctx* ctx, aesfhe_handle ct, int degree, aesfhe_han
 /* engine.ntt / engine.intt, REF/engine_context.py:173-177 */
 int aesfhe_to_ntt(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
 int aesfhe_to_intt(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
-/* engine.bootstrap(ct, relin, conj, bootstrap_key), REF/engine_context.py:147-162 */
+/* engine.bootstrap(ct, relin, conj, bootstrap_key), REF/engine_context.py:147-162.
+ * Full-slot complex bootstrapping: sparse-secret encapsulation, ModRaise,
+ * CoeffToSlot, EvalMod, SlotToCoeff.  Input slots must satisfy |z| <= 1; the output is at
+ * level max_level - aesfhe_bootstrap_depth() of the bootstrappable parameter set. */
 int aesfhe_bootstrap(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
+int aesfhe_bootstrap_depth(void);
+/* host self-check of the bootstrap plan: err[0] SlotToCoeff, err[1] CoeffToSlot vs the
+ * canonical embedding, err[2] EvalMod Chebyshev error (no GPU needed) */
+int aesfhe_debug_bootplan(int log_n, double* err3);
+/* debug: run bootstrap up to a stage (1..11, see engine.hip) and return that ciphertext;
+ * ephemeral sparse secret (NTT form, all limbs); [s_bt, k1, top, K, r, deg] */
+int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle ct, int stage, aesfhe_handle* out);
+int aesfhe_export_sparse(aesfhe_ctx* ctx, uint32_t* out);
+int aesfhe_debug_lin_group(aesfhe_ctx* ctx, aesfhe_handle ct, int which, aesfhe_handle* out);
+int aesfhe_boot_info(aesfhe_ctx* ctx, double* out6);
 /* Zeta16 secret-key renorm of a (hi, lo) state pair (REF/pipeline.py:65-69): decrypt,
  * snap the 16 strided slots to the nearest codeword, refill others with 1, re-encrypt */
 int aesfhe_renorm_pair(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle* out_hi, aesfhe_handle* out_lo);
