@@ -134,7 +134,9 @@ BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts
         Diags D;
         D[0] = std::vector<cplx>(M, 1.0);
         for (int s : sg[gi]) D = compose(stage(logn, s, false), D, M);
-        if (gi + 1 == sg.size())
+        // the gain goes into the FIRST group: the signal is smallest right after EvalMod,
+        // where SlotToCoeff crosses into the single-prime (2^30-scale) region
+        if (gi == 0)
             for (auto& kv : D)
                 for (auto& x : kv.second) x *= stc_scale;
         P.stc.push_back(layout(D, 1 << (sg[gi].front() - 1), M));

@@ -30,7 +30,7 @@ struct BootPlan {
 };
 
 // cts_scale multiplies CoeffToSlot (folded into its first group), stc_scale multiplies
-// SlotToCoeff (folded into its last group)
+// SlotToCoeff (folded into its first group)
 BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts_scale, double stc_scale, int K, int r, int deg);
 
 // reference evaluation of the planned transforms on plain vectors (self-check)

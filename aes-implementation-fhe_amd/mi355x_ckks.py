@@ -226,12 +226,15 @@ class Engine:
 
     def __init__(self, *, mode: str = "gpu", use_bootstrap: bool = False, use_multiparty: bool = False,
                  thread_count: int = 0, device_id: int = 0, max_level: int = 17, log_n: int = 16,
-                 dnum: int = 3, seed: int = 0x5EED):
+                 dnum: int | None = None, seed: int = 0x5EED):
         if use_multiparty:
             raise ValueError("multiparty key generation is not supported")
         self.mode = mode
         self.use_bootstrap = use_bootstrap
-        # bootstrappable set: the chain is extended by the bootstrap depth above the fresh level
+        # bootstrappable set: the chain is extended by the bootstrap depth above the fresh level;
+        # more key-switching digits there keep log2(PQ) under the 128-bit bound (1772 at N=2^16)
+        if dnum is None:
+            dnum = 6 if use_bootstrap else 3
         self._ctx = _Context(log_n, max_level, dnum, device_id, seed, bootstrappable=use_bootstrap)
         L = self._ctx.lib
         self.fresh_level = max_level

@@ -1,0 +1,19 @@
+"""Host-side bootstrap plan (homomorphic DFT factorisation + EvalMod polynomial) against
+the canonical embedding; no GPU needed (aesfhe_debug_bootplan)."""
+import pytest
+
+
+@pytest.mark.parametrize("log_n", [10, 13, 16])
+def test_bootstrap_plan_factorisation(log_n):
+    import build_ext
+    import mi355x_ckks
+    build_ext.build()
+    err = mi355x_ckks.debug_bootplan(log_n)
+    assert err[0] < 1e-10   # SlotToCoeff groups == canonical embedding
+    assert err[1] < 1e-10   # CoeffToSlot groups == its inverse
+    assert err[2] < 1e-9    # Chebyshev approximation of the EvalMod kernel
+
+
+def test_bootstrap_depth():
+    import mi355x_ckks
+    assert mi355x_ckks.bootstrap_depth() == 15

@@ -1,0 +1,82 @@
+"""CKKS bootstrapping on the MI355X engine and the pipeline steps that
+use it.  Slot tolerances are stated in the asserts; decoded nibbles must be exact."""
+import numpy as np
+import pytest
+
+from conftest import gpu_context
+
+pytestmark = pytest.mark.gpu
+
+BOOT_TOL = 0.02  # max |slot error| for |z| <= 1 inputs at N = 2^16 (decode margin pi/16 = 0.196)
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return gpu_context(log_n=16, signature=1)
+
+
+def test_bootstrap_accuracy_and_level(ctx):
+    E = ctx.engine
+    S = E.slot_count
+    rng = np.random.default_rng(1)
+    z = np.exp(2j * np.pi * rng.random(S)) * rng.random(S)
+    ct = ctx.encrypt(z)
+    out = ctx.bootstrap(ct)
+    assert out.level == E.fresh_level
+    assert np.abs(ctx.decrypt(out) - z).max() < BOOT_TOL
+    # from an exhausted ciphertext (the reference's fallback path, REF/xor4_lut.py:46-51)
+    low = ct
+    for _ in range(E.fresh_level):
+        low = ctx.multiply(low, 1.0 + 0j) if False else E.multiply(low, 0.999)
+    assert low.level == 0
+    out = ctx.bootstrap(ctx.to_intt(low))
+    assert np.abs(ctx.decrypt(out) - z * 0.999 ** E.fresh_level).max() < BOOT_TOL
+    assert ctx.bootstrap_stats()["count"] >= 2
+
+
+def test_bootstrap_zeta16_state(ctx):
+    from state_encoder import StateEncoder
+    enc = StateEncoder(ctx)
+    rng = np.random.default_rng(2)
+    state = rng.integers(0, 256, 16).astype(np.uint8)
+    hi, lo = enc.encode(state)
+    bh, bl = ctx.bootstrap(hi), ctx.bootstrap(lo)
+    assert np.array_equal(enc.decode(bh, bl), state)
+    sc = E_slots = ctx.engine.slot_count
+    z = ctx.decrypt(bh)[:: sc // 16][:16]
+    assert np.abs(np.angle(z / np.exp(-2j * np.pi * (state >> 4) / 16))).max() < np.pi / 64
+
+
+def test_mixcolumns_with_final_bootstrap(ctx, coeff_dir):
+    from aes_keyschedule import load_all_coeffs
+    from mixcol_final import MixColFinal
+    from oracle import aes_plain
+    from state_encoder import StateEncoder
+    from xor4_lut import XOR4LUT
+    co = load_all_coeffs(coeff_dir)
+    enc = StateEncoder(ctx)
+    mc = MixColFinal(ctx, XOR4LUT(ctx, co["xor4"]))
+    np.random.seed(0)
+    state = np.random.randint(0, 256, 16, dtype=np.uint8)
+    out = mc(*enc.encode(state))
+    assert out[0].level == ctx.engine.fresh_level
+    assert np.array_equal(enc.decode(*out), aes_plain.ref_mix_columns(state))
+
+
+def test_config2_full_encrypt_and_roundtrip(ctx, coeff_dir):
+    """BASELINE config 2 on one state (REF/test/test_aes_pipeline_roundtrip.py:114-163):
+    10-round encrypt with renorm + final bootstraps, then decrypt with InvMixColumns."""
+    from aes_keyschedule import expand_aes128_key, load_all_coeffs
+    from oracle import aes_plain
+    from pipeline import AESPipeline
+    pipe = AESPipeline(ctx, load_all_coeffs(coeff_dir), use_hard_renorm_between_steps=True)
+    np.random.seed(7)
+    key = np.random.randint(0, 256, 16, dtype=np.uint8)
+    rks = expand_aes128_key(key)
+    pt = np.random.randint(0, 256, 16, dtype=np.uint8)
+    dbg = {}
+    ct = pipe.encrypt(pt, rks, debug=dbg)
+    assert np.array_equal(pipe.encoder.decode(*ct), aes_plain.ref_encrypt(pt, rks))
+    assert np.array_equal(dbg["enc.r0.ark"]["plain"], pt ^ rks[0])
+    back = pipe.decrypt(*ct, rks)
+    assert np.array_equal(pipe.encoder.decode(*back), pt)
