@@ -137,10 +137,15 @@ class AESPipeline:
         self._log_pair(debug, "dec.init.ark10.renorm", *ct)
         for r in range(9, 0, -1):
             ct = self.inv_shift_rows(*ct)
+            self._log_pair(debug, f"dec.r{r}.isr", *ct)
             ct = self._renorm_pair(*self.inv_sub_bytes(*ct))
+            self._log_pair(debug, f"dec.r{r}.isb", *ct)
             ct = self._renorm_pair(*self.add_round_key(*ct, *rk[r]))
+            self._log_pair(debug, f"dec.r{r}.ark", *ct)
             if self.with_inv_mix_columns:
-                ct = self.inv_mix_columns(*ct)
+                # InvSubBytes' LUT needs a clean input, as SubBytes gets one after ARK in encrypt
+                ct = self._renorm_pair(*self.inv_mix_columns(*ct))
+                self._log_pair(debug, f"dec.r{r}.imc", *ct)
         ct = self.inv_shift_rows(*ct)
         self._log_pair(debug, "dec.final.isr", *ct)
         ct = self.inv_sub_bytes(*ct)
