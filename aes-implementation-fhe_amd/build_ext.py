@@ -13,8 +13,8 @@ from pathlib import Path
 PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 LIB = PKG / "libaesfhe.so"
-SOURCES = ["engine.hip", "kernels.hip", "params.cpp", "encoder.cpp", "bootstrap.cpp"]
-HEADERS = ["common.h", "kernels.h", "params.h", "encoder.h", "bootstrap.h"]
+SOURCES = ["engine.hip", "kernels.hip", "ntt.hip", "params.cpp", "encoder.cpp", "bootstrap.cpp"]
+HEADERS = ["common.h", "kernels.h", "launch.h", "params.h", "encoder.h", "bootstrap.h"]
 ARCH = os.environ.get("AESFHE_ARCH", "gfx950")
 
 

@@ -120,7 +120,6 @@ public:
         pool_.release_all();
         for (void* p : owned_) (void)hipFree(p);
         for (auto& kv : ksk_) (void)hipFree(kv.second);
-        if (ring_host_) (void)hipHostFree(ring_host_);
         (void)hipStreamDestroy(st_);
     }
 
@@ -197,6 +196,15 @@ public:
     }
     void intt(u32* d, int rows, int nl, LimbMap m) {
         launch_ntt_inv(st_, T_, d, rows, nl, m);
+        cnt_[C_NTT_ROWS] += rows;
+    }
+    // out-of-place forms (dense rows unless a RowMap is given)
+    void ntt(u32* dst, const u32* src, int rows, RowMap rm, LimbMap m) {
+        launch_ntt_fwd(st_, T_, dst, src, rows, rm, m);
+        cnt_[C_NTT_ROWS] += rows;
+    }
+    void intt(u32* dst, const u32* src, int rows, RowMap rm, LimbMap m) {
+        launch_ntt_inv(st_, T_, dst, src, rows, rm, m);
         cnt_[C_NTT_ROWS] += rows;
     }
 
@@ -397,8 +405,10 @@ public:
     Ct ensure_ntt(const Ct& c, bool resolve_pending = true) {
         Ct o = c;
         if (!c.ntt) {
-            o = copy(c);
-            ntt(o.data, o.npoly * hp_.nl(o.level), hp_.nl(o.level), qmap());
+            o = alloc_ct(c.level, c.npoly);
+            o.pending = c.pending;
+            const int nl = hp_.nl(o.level);
+            ntt(o.data, c.data, o.npoly * nl, rows_dense(nl), qmap());
             o.ntt = true;
         }
         if (resolve_pending && o.pending) {
@@ -409,14 +419,20 @@ public:
         return o;
     }
     Ct to_intt(const Ct& c) {
-        Ct o = copy(c);
-        if (c.ntt) intt(o.data, o.npoly * hp_.nl(o.level), hp_.nl(o.level), qmap());
+        if (!c.ntt) return copy(c);
+        Ct o = alloc_ct(c.level, c.npoly);
+        o.pending = c.pending;
+        const int nl = hp_.nl(o.level);
+        intt(o.data, c.data, o.npoly * nl, rows_dense(nl), qmap());
         o.ntt = false;
         return o;
     }
     Ct to_ntt(const Ct& c) {
-        Ct o = copy(c);
-        if (!c.ntt) ntt(o.data, o.npoly * hp_.nl(o.level), hp_.nl(o.level), qmap());
+        if (c.ntt) return copy(c);
+        Ct o = alloc_ct(c.level, c.npoly);
+        o.pending = c.pending;
+        const int nl = hp_.nl(o.level);
+        ntt(o.data, c.data, o.npoly * nl, rows_dense(nl), qmap());
         o.ntt = true;
         return o;
     }
@@ -429,16 +445,14 @@ public:
         u32* owned = nullptr;
         for (int step = 0; step < k; ++step) {
             const int r = nl - 1 - step;  // limb dropped now; cur has r + 1 limbs per poly
+            // coefficients of the dropped limb (one row per poly, read in place), then the
+            // fused spread -> NTT -> (cur - v) q_r^{-1} on the r remaining limbs
             u32* last = tmp(np);
-            for (int p = 0; p < np; ++p)
-                HIP_OK(hipMemcpyAsync(last + (size_t)p * n, cur + ((size_t)p * (r + 1) + r) * n, sizeof(u32) * n,
-                                      hipMemcpyDeviceToDevice, st_));
-            intt(last, np, 1, single(r));
+            intt(last, cur, np, RowMap{1, r + 1, 1, r, 0}, single(r));
             u32* v = tmp((size_t)np * r);
-            launch_rescale_spread(st_, T_, v, last, np, r, hp_.mod[r]);
-            ntt(v, np * r, r, qmap());
             u32* o = tmp((size_t)np * r);
-            launch_rescale_finish(st_, T_, o, cur, v, d_rescale_qinv_ + rescale_off_[r], np, r, r + 1);
+            launch_rescale_ntt(st_, T_, o, cur, last, v, d_rescale_qinv_ + rescale_off_[r], np, r, r + 1, hp_.mod[r]);
+            cnt_[C_NTT_ROWS] += (size_t)np * r;
             untmp(last, np);
             untmp(v, (size_t)np * r);
             if (owned) untmp(owned, (size_t)np * (r + 1));
@@ -462,31 +476,18 @@ public:
     }
 
     // per-limb constant residues (Shoup pairs, lo/hi halves) on limbs 0..nl-1
-    u32* const_half(const std::vector<u32>& lo, const std::vector<u32>& hi) {
+    LimbConsts const_half(const std::vector<u32>& lo, const std::vector<u32>& hi) {
         const int nl = (int)lo.size();
-        std::vector<u32> h(4 * (size_t)nl);
+        if (nl > kMaxConstLimbs) throw std::runtime_error("const_half: too many limbs");
+        LimbConsts h{};
         for (int t = 0; t < nl; ++t) {
             const u32 q = hp_.mod[t];
-            h[4 * t] = lo[t];
-            h[4 * t + 1] = shoup_pre(lo[t], q);
-            h[4 * t + 2] = hi[t];
-            h[4 * t + 3] = shoup_pre(hi[t], q);
+            h.v[4 * t] = lo[t];
+            h.v[4 * t + 1] = shoup_pre(lo[t], q);
+            h.v[4 * t + 2] = hi[t];
+            h.v[4 * t + 3] = shoup_pre(hi[t], q);
         }
-        return upload_small(h);
-    }
-    u32* upload_small(const std::vector<u32>& h) {
-        // small constant buffers: pinned host ring -> device ring; on wrap-around the
-        // stream is drained so no in-flight kernel still reads a recycled slot
-        const size_t words = (h.size() + 63) & ~size_t(63);
-        if (ring_off_ + words > kRingWords) {
-            HIP_OK(hipStreamSynchronize(st_));
-            ring_off_ = 0;
-        }
-        u32* d = ring_ + ring_off_;
-        std::memcpy(ring_host_ + ring_off_, h.data(), h.size() * sizeof(u32));
-        HIP_OK(hipMemcpyAsync(d, ring_host_ + ring_off_, h.size() * sizeof(u32), hipMemcpyHostToDevice, st_));
-        ring_off_ += words;
-        return d;
+        return h;
     }
     static u32 mod_i64(i64 v, u32 q) {
         i64 r = v % (i64)q;
@@ -584,9 +585,9 @@ public:
         const int nl = hp_.nl(c.level);
         std::vector<u32> lo, hi;
         scalar_residues(std::llround(re * hp_.delta[c.level]), std::llround(im * hp_.delta[c.level]), nl, lo, hi);
-        std::vector<u32> h(2 * (size_t)nl);
-        for (int t = 0; t < nl; ++t) h[2 * t] = lo[t], h[2 * t + 1] = hi[t];
-        u32* d = upload_small(h);
+        if (nl > 2 * kMaxConstLimbs) throw std::runtime_error("add_scalar: too many limbs");
+        LimbConsts d{};
+        for (int t = 0; t < nl; ++t) d.v[2 * t] = lo[t], d.v[2 * t + 1] = hi[t];
         Ct o = copy(c);
         launch_add_const_half(st_, T_, o.data, c.data, d, nl, nl, qmap());
         if (c.data != c_in.data) release(c);
@@ -602,7 +603,7 @@ public:
             // Gaussian integer a + b i: exact multiplication by a + b X^{N/2}, no level consumed
             std::vector<u32> lo, hi;
             scalar_residues((i64)re, (i64)im, nl, lo, hi);
-            u32* d = const_half(lo, hi);
+            const LimbConsts d = const_half(lo, hi);
             o = alloc_ct(c.level, c.npoly);
             launch_mul_const_half(st_, T_, o.data, c.data, d, c.npoly * nl, nl, qmap());
         } else {
@@ -610,7 +611,7 @@ public:
             std::vector<u32> lo, hi;
             const double sc = hp_.ptscale[c.level];
             scalar_residues(std::llround(re * sc), std::llround(im * sc), nl, lo, hi);
-            u32* d = const_half(lo, hi);
+            const LimbConsts d = const_half(lo, hi);
             Ct t = alloc_ct(c.level, c.npoly);
             launch_mul_const_half(st_, T_, t.data, c.data, d, c.npoly * nl, nl, qmap());
             o = rescale(t);
@@ -667,39 +668,54 @@ public:
     Ct keyswitch(const u32* d, int level, const u32* key, const u32* add0, const u32* add1) {
         const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, alpha = hp_.alpha;
         const int nd = (nl + alpha - 1) / alpha;
+        if (alpha > kMaxConvH || np > kMaxConvH || nd > kMaxConvGroups) throw std::runtime_error("keyswitch: digit too large");
         const LimbMap em = extmap(nl);
+        // ModUp: coefficient form of d, every digit converted to all other limbs of Q*P in
+        // one launch, one NTT launch over all converted rows (own limbs skipped: key_inner
+        // reads those straight from d)
         u32* coef = tmp(nl);
-        HIP_OK(hipMemcpyAsync(coef, d, sizeof(u32) * nl * n, hipMemcpyDeviceToDevice, st_));
-        intt(coef, nl, nl, qmap());
+        intt(coef, d, nl, rows_dense(nl), qmap());
         u32* ext = tmp((size_t)nd * ne);
         const size_t* toff = &modup_off_[(size_t)nl * hp_.dnum];
+        ConvBatch up;
+        up.n = nd;
         for (int j = 0; j < nd; ++j) {
             const int lo = j * alpha, h = std::min(alpha, nl - lo);
-            u32* ej = ext + (size_t)j * ne * n;
-            HIP_OK(hipMemcpyAsync(ej + (size_t)lo * n, d + (size_t)lo * n, sizeof(u32) * h * n, hipMemcpyDeviceToDevice, st_));
-            launch_base_convert(st_, T_, ej, coef + (size_t)lo * n, h, lo, ne, em, lo, d_modup_ + toff[j],
-                                d_modup_ + toff[j] + (size_t)2 * h * ne, d_modup_ + toff[j] + (size_t)2 * h * ne + 2 * h);
-            if (lo > 0) ntt(ej, lo, lo, qmap());
-            const int rest = ne - (lo + h);
-            if (rest > 0) ntt(ej + (size_t)(lo + h) * n, rest, rest, LimbMap{nl - (lo + h), lo + h, hp_.p_off()});
+            up.h[j] = h, up.d0[j] = lo, up.skip0[j] = lo;
+            up.src[j] = coef + (size_t)lo * n;
+            up.dst[j] = ext + (size_t)j * ne * n;
+            up.tab[j] = d_modup_ + toff[j];
+            up.qhinv[j] = up.tab[j] + (size_t)2 * h * ne;
+            up.negq[j] = up.qhinv[j] + 2 * h;
         }
+        launch_base_convert(st_, T_, up, ne, em);
+        RowMap xr = rows_dense(ne);
+        xr.skip_alpha = alpha, xr.skip_nl = nl;
+        ntt(ext, ext, nd * ne, xr, em);
         u32* acc = tmp(2 * (size_t)ne);
-        launch_key_inner(st_, T_, acc, ext, key, nd, ne, nl, hp_.n_ks + np, hp_.n_ks, em);
+        launch_key_inner(st_, T_, acc, ext, d, key, nd, ne, nl, alpha, hp_.n_ks + np, hp_.n_ks, em);
         untmp(ext, (size_t)nd * ne);
         untmp(coef, nl);
-        // ModDown by P
+        // ModDown by P: coefficients of the P rows (read in place from acc), conversion of
+        // both polys in one launch, NTT fused with (acc_Q - conv) P^{-1} (+ add)
         u32* yp = tmp(2 * (size_t)np);
-        for (int p = 0; p < 2; ++p)
-            HIP_OK(hipMemcpyAsync(yp + (size_t)p * np * n, acc + ((size_t)p * ne + nl) * n, sizeof(u32) * np * n, hipMemcpyDeviceToDevice, st_));
-        intt(yp, 2 * np, np, LimbMap{np, hp_.p_off(), 0});
+        intt(yp, acc, 2 * np, RowMap{np, ne, np, nl, 0}, LimbMap{np, hp_.p_off(), 0});
         u32* conv = tmp(2 * (size_t)nl);
         const size_t doff = moddown_off_[nl];
-        for (int p = 0; p < 2; ++p)
-            launch_base_convert(st_, T_, conv + (size_t)p * nl * n, yp + (size_t)p * np * n, np, hp_.p_off(), nl, qmap(), 1 << 30,
-                                d_moddown_ + doff, d_moddown_phinv_, d_negp_);
-        ntt(conv, 2 * nl, nl, qmap());
+        ConvBatch dn;
+        dn.n = 2;
+        for (int p = 0; p < 2; ++p) {
+            dn.h[p] = np, dn.d0[p] = hp_.p_off(), dn.skip0[p] = 1 << 30;
+            dn.src[p] = yp + (size_t)p * np * n;
+            dn.dst[p] = conv + (size_t)p * nl * n;
+            dn.tab[p] = d_moddown_ + doff;
+            dn.qhinv[p] = d_moddown_phinv_;
+            dn.negq[p] = d_negp_;
+        }
+        launch_base_convert(st_, T_, dn, nl, qmap());
         Ct o = alloc_ct(level, 2);
-        launch_moddown_finish(st_, T_, o.data, acc, conv, d_pinv_ + (size_t)2 * 0, add0, add1, nl, ne);
+        launch_ntt_finish(st_, T_, o.data, conv, acc, ne, d_pinv_, add0, add1, 2, nl);
+        cnt_[C_NTT_ROWS] += 2 * (size_t)nl;
         untmp(yp, 2 * (size_t)np);
         untmp(conv, 2 * (size_t)nl);
         untmp(acc, 2 * (size_t)ne);
@@ -1143,6 +1159,44 @@ public:
         release(o);
         untmp(d, nl);
     }
+    // micro-benchmark of one engine primitive, back to back on the engine stream (HIP events
+    // around the loop: device time incl. launch gaps).  op 0: NTT of arg rows, 1: inverse
+    // NTT of arg rows, 2: key switch (relinearisation key) at level arg, 3: rescale of a
+    // 2-poly ciphertext at level arg, 4: ct x ct + relinearise + rescale at level arg
+    double bench_op(int op, int arg, int iters) {
+        if (iters <= 0) throw std::runtime_error("bench_op: iters must be positive");
+        const int n = hp_.n;
+        if ((op == 0 || op == 1) && (arg <= 0 || arg > 4 * hp_.n_tot())) throw std::runtime_error("bench_op: bad row count");
+        if (op >= 2 && (arg < 1 || arg > hp_.L)) throw std::runtime_error("bench_op: bad level");
+        if (op > 4 || op < 0) throw std::runtime_error("bench_op: unknown op");
+        const int rows = op <= 1 ? arg : 3 * hp_.nl(arg);
+        u32* buf = tmp(rows);
+        HIP_OK(hipMemsetAsync(buf, 0, sizeof(u32) * rows * n, st_));
+        const int nl = op <= 1 ? std::min(arg, hp_.n_q) : hp_.nl(arg);
+        Ct c;
+        c.data = buf, c.level = op <= 1 ? 0 : arg, c.npoly = 2, c.ntt = true, c.words = (size_t)2 * nl * n;
+        auto run = [&]() {
+            if (op == 0) ntt(buf, buf, arg, rows_dense(nl), qmap());
+            else if (op == 1) intt(buf, buf, arg, rows_dense(nl), qmap());
+            else if (op == 2) release(keyswitch(buf + (size_t)2 * nl * n, arg, ksk(0), buf, buf + (size_t)nl * n));
+            else if (op == 3) release(rescale(c));
+            else release(mul(c, c, true));
+        };
+        run();
+        hipEvent_t a, b;
+        HIP_OK(hipEventCreate(&a));
+        HIP_OK(hipEventCreate(&b));
+        HIP_OK(hipEventRecord(a, st_));
+        for (int i = 0; i < iters; ++i) run();
+        HIP_OK(hipEventRecord(b, st_));
+        HIP_OK(hipEventSynchronize(b));
+        float ms = 0.f;
+        HIP_OK(hipEventElapsedTime(&ms, a, b));
+        (void)hipEventDestroy(a);
+        (void)hipEventDestroy(b);
+        untmp(buf, rows);
+        return 1000.0 * ms / iters;
+    }
     u64 counter(int i) const { return i < C_N ? cnt_[i] : 0; }
     void reset_counters() { std::memset(cnt_, 0, sizeof(cnt_)); }
 
@@ -1298,13 +1352,6 @@ private:
         d_pinv_ = dev_upload(pinv);
         d_negp_ = dev_upload(negp);
 
-        void* r = nullptr;
-        HIP_OK(hipMalloc(&r, kRingWords * sizeof(u32)));
-        owned_.push_back(r);
-        ring_ = (u32*)r;
-        void* rh = nullptr;
-        HIP_OK(hipHostMalloc(&rh, kRingWords * sizeof(u32), hipHostMallocDefault));
-        ring_host_ = (u32*)rh;
     }
 
     HostParams hp_;
@@ -1333,10 +1380,6 @@ private:
     std::vector<size_t> moddown_off_;
     u32* d_pinv_ = nullptr;
     u32* d_negp_ = nullptr;
-    static constexpr size_t kRingWords = 1 << 20;
-    u32* ring_ = nullptr;
-    u32* ring_host_ = nullptr;
-    size_t ring_off_ = 0;
     u64 cnt_[C_N] = {};
 
 public:
@@ -1547,6 +1590,10 @@ int aesfhe_debug_ntt(aesfhe_ctx* ctx, uint32_t* data, int rows, int first_prime,
 }
 int aesfhe_debug_keyswitch(aesfhe_ctx* ctx, int level, uint64_t g, const uint32_t* d, uint32_t* out) {
     API_BEGIN ctx->eng->debug_keyswitch(level, g, d, out);
+    API_END
+}
+int aesfhe_bench_op(aesfhe_ctx* ctx, int op, int arg, int iters, double* us) {
+    API_BEGIN * us = ctx->eng->bench_op(op, arg, iters);
     API_END
 }
 int aesfhe_counters(aesfhe_ctx* ctx, uint64_t* out, int n) {

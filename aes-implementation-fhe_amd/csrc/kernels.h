@@ -41,7 +41,38 @@ struct DevTables {
     int logn = 16;
 };
 
-// --- number-theoretic transforms -------------------------------------------------
+// --- number-theoretic transforms (ntt.hip) ----------------------------------------------
+// launch row y -> group g = y / cnt, index i = y % cnt (the limb index fed to LimbMap);
+// source row = src_off + g * src_stride + i, destination row = dst_off + g * dst_stride + i
+// skip_alpha > 0 (forward only): rows with i < skip_nl and i / skip_alpha == g are left
+// untouched (ModUp: a digit's own limbs)
+struct RowMap {
+    int cnt, src_stride, dst_stride, src_off, dst_off;
+    int skip_alpha = 0, skip_nl = 0;
+};
+inline RowMap rows_dense(int nl) { return RowMap{nl, nl, nl, 0, 0}; }
+// fused prologue / epilogue operands of the forward NTT (ntt.hip)
+struct NttAux {
+    const u32* cur = nullptr;  // finish: rows g * cur_stride + i
+    u32* out = nullptr;        // finish: rows g * out_stride + i
+    const u32* qinv = nullptr; // finish: [i] Shoup pairs
+    const u32* add0 = nullptr; // finish: optional addend rows for group 0 / 1
+    const u32* add1 = nullptr;
+    int cur_stride = 0, out_stride = 0;
+    u32 q_last = 0;            // spread: modulus of the source row
+};
+// out-of-place (src may equal dst); supported ring sizes 2^13 .. 2^16
+void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map);
+void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map);
+// rescale by the prime q_last, fused: v[p][t] = centred(last[p]) mod q_t -> NTT ->
+// out[p][t] = (cur[p][t] - v) * qinv_t;  cur has nl_in rows per poly, out/v have nt
+void launch_rescale_ntt(hipStream_t st, const DevTables& T, u32* out, const u32* cur, const u32* last, u32* v, const u32* qinv,
+                        int npoly, int nt, int nl_in, u32 q_last);
+// NTT of conv (npoly x nt dense rows, destroyed) fused with
+// out[p][t] = (cur[p * cur_stride + t] - NTT(conv)[p][t]) * qinv_t (+ add_p[t])   (ModDown)
+void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, const u32* cur, int cur_stride, const u32* qinv,
+                       const u32* add0, const u32* add1, int npoly, int nt);
+// in place on rows = npoly * nl dense rows
 void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map);
 void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map);
 
@@ -55,33 +86,48 @@ void launch_tensor(hipStream_t st, const DevTables& T, u32* out, const u32* a, c
 void launch_mul_poly(hipStream_t st, const DevTables& T, u32* out, const u32* in, const u32* pt, int npoly, int nl, LimbMap map);
 // out = a + b*c  (b, c: rows; used for decryption and encryption)
 void launch_fma_poly(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, const u32* c, int rows, int nl, LimbMap map);
-// out[row][k] = in[row][k] * (k < N/2 ? clo[l] : chi[l]) with l = row % nl (Shoup pairs in cst)
-// cst layout: [nl][4] = {clo, clo', chi, chi'}
-void launch_mul_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const u32* cst, int rows, int nl, LimbMap map);
-// out[row][k] = in[row][k] + (k < N/2 ? alo[l] : ahi[l]); cst layout [nl][2]
-void launch_add_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const u32* cst, int rows, int nl, LimbMap map);
+// per-limb constants passed BY VALUE as a kernel argument (1 KiB kernarg, read with scalar
+// loads): no host->device copy per scalar operation
+constexpr int kMaxConstLimbs = 64;
+struct LimbConsts {
+    u32 v[4 * kMaxConstLimbs];
+};
+// out[row][k] = in[row][k] * (k < N/2 ? clo[l] : chi[l]) with l = row % nl (Shoup pairs)
+// layout: v[4 l .. 4 l + 3] = {clo, clo', chi, chi'}
+void launch_mul_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const LimbConsts& cst, int rows, int nl, LimbMap map);
+// out[row][k] = in[row][k] + (k < N/2 ? alo[l] : ahi[l]); layout v[2 l .. 2 l + 1]
+void launch_add_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const LimbConsts& cst, int rows, int nl, LimbMap map);
 // X -> X^g in the NTT domain (bit-reversed evaluation order)
 void launch_automorph(hipStream_t st, const DevTables& T, u32* out, const u32* in, u64 g, int rows);
 
 // --- rescale -------------------------------------------------------------------------
 // last: npoly rows (coefficient form, prime q_last); writes v[p][t] = centred(last) mod q_t
 void launch_rescale_spread(hipStream_t st, const DevTables& T, u32* v, const u32* last, int npoly, int nt, u32 q_last);
-// out[p][t] = (x[p][t] - v[p][t]) * qinv_t ; x has nl_in rows per poly, out/v have nt rows per poly
-void launch_rescale_finish(hipStream_t st, const DevTables& T, u32* out, const u32* x, const u32* v, const u32* qinv, int npoly, int nt, int nl_in);
 
 // --- key switching -----------------------------------------------------------------
-// digit coefficient rows x[i] (i < h, primes d0 + i) -> ext rows for all targets of
-// map (nt rows), skipping rows [skip0, skip0 + h) which are copied from src_ntt.
+// fast base conversion of several groups in one launch (ModUp: one group per digit,
+// ModDown: one per polynomial).  Group g: h source coefficient rows (primes d0 ..
+// d0 + h - 1) -> nt target rows of dst (primes map.prime(t)); targets
+// [skip0, skip0 + h) are skipped (the digit's own limbs; 1 << 30 = none).
 // tab: [h][nt] Shoup pairs of (qhat_i mod t); qhinv: [h] Shoup pairs of qhat_i^{-1} mod q_i;
 // negq: [nt] values of (-Q mod t), Q = prod of the h source primes (centred conversion)
-void launch_base_convert(hipStream_t st, const DevTables& T, u32* ext, const u32* x, int h, int d0, int nt, LimbMap map,
-                         int skip0, const u32* tab, const u32* qhinv, const u32* negq);
-// acc[0|1][x] = sum_j ext[j][x] * key[j][b|a][krow(x)]; ext: [nd][ne][N]; key: [dnum][2][nkey][N]
-void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* key, int nd, int ne, int nl,
-                      int nkey, int nks, LimbMap map);
-// out[p][t] = (acc[p][t] - conv[p][t]) * Pinv_t (+ add0[t] for p = 0, + add1[t] for p = 1; nullable)
-void launch_moddown_finish(hipStream_t st, const DevTables& T, u32* out, const u32* acc, const u32* conv, const u32* pinv,
-                           const u32* add0, const u32* add1, int nl, int ne);
+constexpr int kMaxConvGroups = 8;
+constexpr int kMaxConvH = 16;
+struct ConvBatch {
+    int n = 0;
+    int h[kMaxConvGroups] = {}, d0[kMaxConvGroups] = {}, skip0[kMaxConvGroups] = {};
+    const u32* src[kMaxConvGroups] = {};
+    u32* dst[kMaxConvGroups] = {};
+    const u32* tab[kMaxConvGroups] = {};
+    const u32* qhinv[kMaxConvGroups] = {};
+    const u32* negq[kMaxConvGroups] = {};
+};
+void launch_base_convert(hipStream_t st, const DevTables& T, const ConvBatch& cb, int nt, LimbMap map);
+// acc[0|1][x] = sum_j e_j[x] * key[j][b|a][krow(x)] with e_j = ext[j] except on digit j's
+// own limbs (x < nl, x / alpha == j) where e_j = d (the NTT-form input);
+// ext: [nd][ne][N]; key: [dnum][2][nkey][N]
+void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
+                      int alpha, int nkey, int nks, LimbMap map);
 
 // --- sampling --------------------------------------------------------
 // kind: 0 ternary, 1 centred binomial (eta = 21); writes value mod prime into nl rows

@@ -5,6 +5,9 @@
 // global access below is unit-stride across consecutive lanes.
 #include "kernels.h"
 
+#include <algorithm>
+#include "launch.h"
+
 #define CHECK_LAUNCH() (void)hipGetLastError()
 
 namespace {
@@ -18,145 +21,6 @@ __device__ __forceinline__ u64 mix64(u64 z) {
 }
 __device__ __forceinline__ u64 prng_key(u64 seed, u64 stream) { return mix64(seed ^ mix64(stream + 0x9E3779B97F4A7C15ULL)); }
 __device__ __forceinline__ u64 prng_at(u64 key, u64 ctr) { return mix64(key + (ctr + 1) * 0x9E3779B97F4A7C15ULL); }
-
-// ------------------------------------------------------------------------------------
-// NTT.  N = R * ROWS with R = 256 contiguous elements per row.  Pass "cols" runs the
-// log2(ROWS) stages whose butterfly span is >= R (each column of the R x ROWS view is an
-// independent ROWS-point transform); pass "rows" runs the last 8 stages inside each
-// contiguous 256-element row.  Both stage the tile through LDS.
-// ------------------------------------------------------------------------------------
-constexpr int kR = 256;
-constexpr int kColTile = 16;
-constexpr int kRowsPerBlock = 4;
-
-__global__ void __launch_bounds__(kBlock) k_ntt_cols_fwd(u32* data, int nl, LimbMap map, const PrimeConst* pc, const u32* psi,
-                                                         const u32* psip, int logn) {
-    extern __shared__ u32 sm[];
-    const int S1 = logn - 8, ROWS = 1 << S1, LD = kColTile + 1;
-    const int row = blockIdx.y;
-    const int prime = map.prime(row % nl);
-    const u32 q = pc[prime].q;
-    const u32* w = psi + ((size_t)prime << logn);
-    const u32* wp = psip + ((size_t)prime << logn);
-    u32* base = data + ((size_t)row << logn) + blockIdx.x * kColTile;
-    for (int e = threadIdx.x; e < ROWS * kColTile; e += kBlock) {
-        int r = e / kColTile, c = e % kColTile;
-        sm[r * LD + c] = base[(size_t)r * kR + c];
-    }
-    __syncthreads();
-    for (int s = 0; s < S1; ++s) {
-        const int m = 1 << s, t = ROWS >> (s + 1);
-        for (int b = threadIdx.x; b < (ROWS / 2) * kColTile; b += kBlock) {
-            int c = b % kColTile, p = b / kColTile;
-            int i = p / t, j = p % t, r0 = 2 * i * t + j;
-            u32 W = w[m + i], Wp = wp[m + i];
-            u32 u = sm[r0 * LD + c];
-            u32 v = shoup_mul(sm[(r0 + t) * LD + c], W, Wp, q);
-            sm[r0 * LD + c] = add_mod(u, v, q);
-            sm[(r0 + t) * LD + c] = sub_mod(u, v, q);
-        }
-        __syncthreads();
-    }
-    for (int e = threadIdx.x; e < ROWS * kColTile; e += kBlock) {
-        int r = e / kColTile, c = e % kColTile;
-        base[(size_t)r * kR + c] = sm[r * LD + c];
-    }
-}
-
-__global__ void __launch_bounds__(kBlock) k_ntt_rows_fwd(u32* data, int nl, LimbMap map, const PrimeConst* pc, const u32* psi,
-                                                         const u32* psip, int logn) {
-    __shared__ u32 sm[kRowsPerBlock * kR];
-    const int S1 = logn - 8;
-    const int row = blockIdx.y;
-    const int prime = map.prime(row % nl);
-    const u32 q = pc[prime].q;
-    const u32* w = psi + ((size_t)prime << logn);
-    const u32* wp = psip + ((size_t)prime << logn);
-    const int r_first = blockIdx.x * kRowsPerBlock;
-    u32* base = data + ((size_t)row << logn) + (size_t)r_first * kR;
-    for (int e = threadIdx.x; e < kRowsPerBlock * kR; e += kBlock) sm[e] = base[e];
-    __syncthreads();
-    for (int s = S1; s < logn; ++s) {
-        const int m = 1 << s, t = kR >> (s - S1 + 1);
-        for (int b = threadIdx.x; b < kRowsPerBlock * kR / 2; b += kBlock) {
-            int rr = b / (kR / 2), p = b % (kR / 2);
-            int il = p / t, j = p % t, j0 = 2 * il * t + j;
-            int ig = (r_first + rr) * (kR / (2 * t)) + il;
-            u32 W = w[m + ig], Wp = wp[m + ig];
-            u32* x = sm + rr * kR;
-            u32 u = x[j0];
-            u32 v = shoup_mul(x[j0 + t], W, Wp, q);
-            x[j0] = add_mod(u, v, q);
-            x[j0 + t] = sub_mod(u, v, q);
-        }
-        __syncthreads();
-    }
-    for (int e = threadIdx.x; e < kRowsPerBlock * kR; e += kBlock) base[e] = sm[e];
-}
-
-__global__ void __launch_bounds__(kBlock) k_ntt_rows_inv(u32* data, int nl, LimbMap map, const PrimeConst* pc, const u32* ipsi,
-                                                         const u32* ipsip, int logn) {
-    __shared__ u32 sm[kRowsPerBlock * kR];
-    const int S1 = logn - 8;
-    const int row = blockIdx.y;
-    const int prime = map.prime(row % nl);
-    const u32 q = pc[prime].q;
-    const u32* w = ipsi + ((size_t)prime << logn);
-    const u32* wp = ipsip + ((size_t)prime << logn);
-    const int r_first = blockIdx.x * kRowsPerBlock;
-    u32* base = data + ((size_t)row << logn) + (size_t)r_first * kR;
-    for (int e = threadIdx.x; e < kRowsPerBlock * kR; e += kBlock) sm[e] = base[e];
-    __syncthreads();
-    for (int s = logn - 1; s >= S1; --s) {
-        const int m = 1 << s, t = kR >> (s - S1 + 1);
-        for (int b = threadIdx.x; b < kRowsPerBlock * kR / 2; b += kBlock) {
-            int rr = b / (kR / 2), p = b % (kR / 2);
-            int il = p / t, j = p % t, j0 = 2 * il * t + j;
-            int ig = (r_first + rr) * (kR / (2 * t)) + il;
-            u32 W = w[m + ig], Wp = wp[m + ig];
-            u32* x = sm + rr * kR;
-            u32 u = x[j0], v = x[j0 + t];
-            x[j0] = add_mod(u, v, q);
-            x[j0 + t] = shoup_mul(u + q - v, W, Wp, q);
-        }
-        __syncthreads();
-    }
-    for (int e = threadIdx.x; e < kRowsPerBlock * kR; e += kBlock) base[e] = sm[e];
-}
-
-__global__ void __launch_bounds__(kBlock) k_ntt_cols_inv(u32* data, int nl, LimbMap map, const PrimeConst* pc, const u32* ipsi,
-                                                         const u32* ipsip, int logn) {
-    extern __shared__ u32 sm[];
-    const int S1 = logn - 8, ROWS = 1 << S1, LD = kColTile + 1;
-    const int row = blockIdx.y;
-    const int prime = map.prime(row % nl);
-    const PrimeConst P = pc[prime];
-    const u32 q = P.q;
-    const u32* w = ipsi + ((size_t)prime << logn);
-    const u32* wp = ipsip + ((size_t)prime << logn);
-    u32* base = data + ((size_t)row << logn) + blockIdx.x * kColTile;
-    for (int e = threadIdx.x; e < ROWS * kColTile; e += kBlock) {
-        int r = e / kColTile, c = e % kColTile;
-        sm[r * LD + c] = base[(size_t)r * kR + c];
-    }
-    __syncthreads();
-    for (int s = S1 - 1; s >= 0; --s) {
-        const int m = 1 << s, t = ROWS >> (s + 1);
-        for (int b = threadIdx.x; b < (ROWS / 2) * kColTile; b += kBlock) {
-            int c = b % kColTile, p = b / kColTile;
-            int i = p / t, j = p % t, r0 = 2 * i * t + j;
-            u32 W = w[m + i], Wp = wp[m + i];
-            u32 u = sm[r0 * LD + c], v = sm[(r0 + t) * LD + c];
-            sm[r0 * LD + c] = add_mod(u, v, q);
-            sm[(r0 + t) * LD + c] = shoup_mul(u + q - v, W, Wp, q);
-        }
-        __syncthreads();
-    }
-    for (int e = threadIdx.x; e < ROWS * kColTile; e += kBlock) {
-        int r = e / kColTile, c = e % kColTile;
-        base[(size_t)r * kR + c] = shoup_mul(sm[r * LD + c], P.ninv, P.ninv_p, q);
-    }
-}
 
 // ------------------------------------------------------------------------------------
 // element-wise kernels: one thread per coefficient, rows on blockIdx.y
@@ -206,16 +70,16 @@ __global__ void k_tensor(u32* out, const u32* a, const u32* b, int nl, LimbMap m
     out[idx + off] = add_mod(barrett_mul(a0, b1, q, mu), barrett_mul(a1, b0, q, mu), q);
     out[idx + 2 * off] = barrett_mul(a1, b1, q, mu);
 }
-__global__ void k_mul_const_half(u32* out, const u32* in, const u32* cst, int nl, LimbMap map, const PrimeConst* pc, int logn) {
+__global__ void k_mul_const_half(u32* out, const u32* in, LimbConsts cst, int nl, LimbMap map, const PrimeConst* pc, int logn) {
     EW_PROLOGUE
     const int hi = (int)(k >> (logn - 1));
-    const u32* c = cst + 4 * limb + 2 * hi;
+    const u32* c = cst.v + 4 * limb + 2 * hi;
     out[idx] = shoup_mul(in[idx], c[0], c[1], P.q);
 }
-__global__ void k_add_const_half(u32* out, const u32* in, const u32* cst, int nl, LimbMap map, const PrimeConst* pc, int logn) {
+__global__ void k_add_const_half(u32* out, const u32* in, LimbConsts cst, int nl, LimbMap map, const PrimeConst* pc, int logn) {
     EW_PROLOGUE
     const int hi = (int)(k >> (logn - 1));
-    out[idx] = add_mod(in[idx], cst[2 * limb + hi], P.q);
+    out[idx] = add_mod(in[idx], cst.v[2 * limb + hi], P.q);
 }
 
 // X -> X^g: NTT slot i holds a(psi^{2 brv(i) + 1}); the image at i is slot j with
@@ -248,56 +112,63 @@ __global__ void k_rescale_spread(u32* v, const u32* last, int nt, u32 q_last, co
     }
     v[(((size_t)p * nt + t) << logn) + k] = r;
 }
-__global__ void k_rescale_finish(u32* out, const u32* x, const u32* v, const u32* qinv, int nt, int nl_in, const PrimeConst* pc,
-                                 int logn) {
-    const int p = blockIdx.z, t = blockIdx.y;
-    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    const u32 q = pc[t].q;
-    const u32 a = x[(((size_t)p * nl_in + t) << logn) + k];
-    const u32 b = v[(((size_t)p * nt + t) << logn) + k];
-    out[(((size_t)p * nt + t) << logn) + k] = shoup_mul(a + q - b, qinv[2 * t], qinv[2 * t + 1], q);
-}
-
 // ------------------------------------------------------------------------------------
 // key switching
 // ------------------------------------------------------------------------------------
-constexpr int kMaxDigit = 32;
-
-// one thread per coefficient; loops over the nt target rows.  Centred conversion
-// (DESIGN.md §3.6): u = round(sum_i y_i / q_i) from a 32-bit fixed-point estimate
-// (mu_i = floor(2^62/q_i)), ext_t = sum_i y_i qhat_i - u Q  (mod t).
-__global__ void __launch_bounds__(kBlock) k_base_convert(u32* ext, const u32* x, int h, int d0, int nt, LimbMap map, int skip0,
-                                                         const u32* tab, const u32* qhinv, const u32* negq, const PrimeConst* pc,
-                                                         int logn) {
+// One launch converts every group (ModUp: each digit; ModDown: each polynomial).  Grid
+// (N / 256, target chunks of kConvTargets, groups).  Each thread recomputes the h values
+// y_i = x_i qhat_i^{-1} (kept in VGPRs: fixed-size guarded unroll, no scratch) and the
+// centred overflow estimate u = round(sum y_i / q_i), then emits its chunk of targets:
+// ext_t = sum_i y_i [qhat_i]_t + u [-Q]_t  (mod t).  Table reads are block-uniform
+// (scalar loads).
+constexpr int kConvTargets = 8;
+__global__ void __launch_bounds__(kBlock) k_base_convert(ConvBatch cb, int nt, LimbMap map, const PrimeConst* pc, int logn) {
+    const int gi = blockIdx.z;
+    const int h = cb.h[gi], d0 = cb.d0[gi], skip0 = cb.skip0[gi];
+    const int t0 = blockIdx.y * kConvTargets, t1 = min(t0 + kConvTargets, nt);
+    if (t0 >= skip0 && t1 <= skip0 + h) return;  // chunk entirely inside the own range
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    u32 y[kMaxDigit];
+    const u32* x = cb.src[gi];
+    const u32* qhinv = cb.qhinv[gi];
+    u32 y[kMaxConvH];
     u64 f = 0;
-#pragma unroll 4
-    for (int i = 0; i < h; ++i) {
-        const PrimeConst Pi = pc[d0 + i];
-        y[i] = shoup_mul(x[((size_t)i << logn) + k], qhinv[2 * i], qhinv[2 * i + 1], Pi.q);
-        f += ((u64)y[i] * Pi.mu) >> 30;
+#pragma unroll
+    for (int i = 0; i < kMaxConvH; ++i) {
+        if (i < h) {
+            const PrimeConst Pi = pc[d0 + i];
+            y[i] = shoup_mul(x[((size_t)i << logn) + k], qhinv[2 * i], qhinv[2 * i + 1], Pi.q);
+            f += ((u64)y[i] * Pi.mu) >> 30;
+        } else {
+            y[i] = 0;
+        }
     }
     const u32 u = (u32)((f + (1ull << 31)) >> 32);
-    for (int t = 0; t < nt; ++t) {
+    const u32* tab = cb.tab[gi];
+    const u32* negq = cb.negq[gi];
+    u32* ext = cb.dst[gi];
+    for (int t = t0; t < t1; ++t) {
         if (t >= skip0 && t < skip0 + h) continue;
         const PrimeConst P = pc[map.prime(t)];
         u64 acc = (u64)u * negq[t];
         const u32* tt = tab + 2 * (size_t)t;
-        for (int i = 0; i < h; ++i) acc += shoup_mul(y[i], tt[2 * (size_t)i * nt], tt[2 * (size_t)i * nt + 1], P.q);
+#pragma unroll
+        for (int i = 0; i < kMaxConvH; ++i)
+            if (i < h) acc += shoup_mul(y[i], tt[2 * (size_t)i * nt], tt[2 * (size_t)i * nt + 1], P.q);
         ext[((size_t)t << logn) + k] = barrett_reduce64(acc, P.q, P.mu);
     }
 }
 
-__global__ void k_key_inner(u32* acc, const u32* ext, const u32* key, int nd, int ne, int nl, int nkey, int nks, LimbMap map,
-                            const PrimeConst* pc, int logn) {
+// digit j's own limbs (x < nl, x / alpha == j) come straight from the NTT-form input d
+__global__ void k_key_inner(u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl, int alpha, int nkey, int nks,
+                            LimbMap map, const PrimeConst* pc, int logn) {
     const int x = blockIdx.y;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const PrimeConst P = pc[map.prime(x)];
     const int krow = x < nl ? x : nks + (x - nl);
+    const int own = x < nl ? x / alpha : -1;
     u32 s0 = 0, s1 = 0;
     for (int j = 0; j < nd; ++j) {
-        const u32 e = ext[(((size_t)j * ne + x) << logn) + k];
+        const u32 e = j == own ? d[((size_t)x << logn) + k] : ext[(((size_t)j * ne + x) << logn) + k];
         const u32* kb = key + (((size_t)j * 2 * nkey + krow) << logn) + k;
         const u32* ka = kb + ((size_t)nkey << logn);
         s0 = add_mod(s0, barrett_mul(e, *kb, P.q, P.mu), P.q);
@@ -305,19 +176,6 @@ __global__ void k_key_inner(u32* acc, const u32* ext, const u32* key, int nd, in
     }
     acc[((size_t)x << logn) + k] = s0;
     acc[(((size_t)ne + x) << logn) + k] = s1;
-}
-
-__global__ void k_moddown_finish(u32* out, const u32* acc, const u32* conv, const u32* pinv, const u32* add0, const u32* add1,
-                                 int nl, int ne, const PrimeConst* pc, int logn) {
-    const int p = blockIdx.z, t = blockIdx.y;
-    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    const u32 q = pc[t].q;
-    const u32 a = acc[(((size_t)p * ne + t) << logn) + k];
-    const u32 c = conv[(((size_t)p * nl + t) << logn) + k];
-    u32 r = shoup_mul(a + q - c, pinv[2 * t], pinv[2 * t + 1], q);
-    const u32* add = p == 0 ? add0 : add1;
-    if (add) r = add_mod(r, add[((size_t)t << logn) + k], q);
-    out[(((size_t)p * nl + t) << logn) + k] = r;
 }
 
 // ------------------------------------------------------------------------------------
@@ -361,7 +219,7 @@ inline dim3 ew_grid(int logn, int rows) { return dim3((1u << logn) / kBlock, row
 // ======================================================================================
 // live timing
 // ======================================================================================
-static thread_local KernelProfiler* g_prof = nullptr;
+thread_local KernelProfiler* g_prof = nullptr;
 void prof_set(KernelProfiler* p) { g_prof = p; }
 
 hipEvent_t KernelProfiler::get() {
@@ -393,148 +251,73 @@ void KernelProfiler::reset() {
 }
 
 namespace {
-// records a start/stop event pair around one launch when its kernel id is enabled
-struct ProfScope {
-    KernelProfiler* p;
-    hipStream_t st;
-    int kid;
-    double bytes;
-    hipEvent_t a = nullptr;
-    ProfScope(hipStream_t s, int k, double b) : p(g_prof), st(s), kid(k), bytes(b) {
-        if (p && (p->mask >> kid & 1u)) {
-            a = p->get();
-            (void)hipEventRecord(a, st);
-        } else {
-            p = nullptr;
-        }
-    }
-    ~ProfScope() {
-        if (!p) return;
-        hipEvent_t b = p->get();
-        (void)hipEventRecord(b, st);
-        p->recs.push_back({a, b, kid, bytes});
-    }
-};
 inline double words(double w) { return 4.0 * w; }
 }  // namespace
 
 // ======================================================================================
 // launch wrappers
 // ======================================================================================
-void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map) {
-    const int S1 = T.logn - 8, ROWS = 1 << S1;
-    const size_t lds = sizeof(u32) * ROWS * (kColTile + 1);
-    const double io = words(2.0 * rows * (1u << T.logn));
-    {
-        ProfScope ps(st, KID_NTT_COLS_FWD, io);
-        hipLaunchKernelGGL(k_ntt_cols_fwd, dim3(kR / kColTile, rows), dim3(kBlock), lds, st, data, nl, map, T.pc, T.psi, T.psip, T.logn);
-    }
-    {
-        ProfScope ps(st, KID_NTT_ROWS_FWD, io);
-        hipLaunchKernelGGL(k_ntt_rows_fwd, dim3(ROWS / kRowsPerBlock, rows), dim3(kBlock), 0, st, data, nl, map, T.pc, T.psi, T.psip,
-                           T.logn);
-    }
-    CHECK_LAUNCH();
-}
-void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map) {
-    const int S1 = T.logn - 8, ROWS = 1 << S1;
-    const size_t lds = sizeof(u32) * ROWS * (kColTile + 1);
-    const double io = words(2.0 * rows * (1u << T.logn));
-    {
-        ProfScope ps(st, KID_NTT_ROWS_INV, io);
-        hipLaunchKernelGGL(k_ntt_rows_inv, dim3(ROWS / kRowsPerBlock, rows), dim3(kBlock), 0, st, data, nl, map, T.pc, T.ipsi, T.ipsip,
-                           T.logn);
-    }
-    {
-        ProfScope ps(st, KID_NTT_COLS_INV, io);
-        hipLaunchKernelGGL(k_ntt_cols_inv, dim3(kR / kColTile, rows), dim3(kBlock), lds, st, data, nl, map, T.pc, T.ipsi, T.ipsip, T.logn);
-    }
-    CHECK_LAUNCH();
-}
-#define EW_WRAP(bytes_words) ProfScope ps_(st, KID_ELEMENTWISE, words((double)(bytes_words) * (1u << T.logn)))
+#define EW_BYTES(bytes_words) words((double)(bytes_words) * (1u << T.logn))
 void launch_add(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int rows, int nl, LimbMap map) {
-    EW_WRAP(3.0 * rows);
-    hipLaunchKernelGGL(k_add, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, b, nl, map, T.pc, T.logn);
+    prof_launch(KID_ELEMENTWISE, EW_BYTES(3.0 * rows), k_add, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, b, nl, map, T.pc, T.logn);
 }
 void launch_sub(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int rows, int nl, LimbMap map) {
-    EW_WRAP(3.0 * rows);
-    hipLaunchKernelGGL(k_sub, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, b, nl, map, T.pc, T.logn);
+    prof_launch(KID_ELEMENTWISE, EW_BYTES(3.0 * rows), k_sub, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, b, nl, map, T.pc, T.logn);
 }
 void launch_neg(hipStream_t st, const DevTables& T, u32* out, const u32* a, int rows, int nl, LimbMap map) {
-    EW_WRAP(2.0 * rows);
-    hipLaunchKernelGGL(k_neg, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, nl, map, T.pc, T.logn);
+    prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows), k_neg, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, nl, map, T.pc, T.logn);
 }
 void launch_square(hipStream_t st, const DevTables& T, u32* out, const u32* a, int rows, int nl, LimbMap map) {
-    EW_WRAP(2.0 * rows);
-    hipLaunchKernelGGL(k_square, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, nl, map, T.pc, T.logn);
+    prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows), k_square, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, nl, map, T.pc, T.logn);
 }
 void launch_tensor(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int nl, LimbMap map) {
-    ProfScope ps(st, KID_TENSOR, words(7.0 * nl * (1u << T.logn)));
-    hipLaunchKernelGGL(k_tensor, ew_grid(T.logn, nl), dim3(kBlock), 0, st, out, a, b, nl, map, T.pc, T.logn);
+    prof_launch(KID_TENSOR, words(7.0 * nl * (1u << T.logn)), k_tensor, ew_grid(T.logn, nl), dim3(kBlock), 0, st, out, a, b, nl, map, T.pc, T.logn);
 }
 void launch_mul_poly(hipStream_t st, const DevTables& T, u32* out, const u32* in, const u32* pt, int npoly, int nl, LimbMap map) {
-    EW_WRAP((2.0 * npoly + 1.0) * nl);
-    hipLaunchKernelGGL(k_mul_poly, ew_grid(T.logn, npoly * nl), dim3(kBlock), 0, st, out, in, pt, nl, map, T.pc, T.logn);
+    prof_launch(KID_ELEMENTWISE, EW_BYTES((2.0 * npoly + 1.0) * nl), k_mul_poly, ew_grid(T.logn, npoly * nl), dim3(kBlock), 0, st, out, in, pt, nl, map, T.pc, T.logn);
 }
 void launch_fma_poly(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, const u32* c, int rows, int nl,
                      LimbMap map) {
-    EW_WRAP(3.0 * rows + nl);
-    hipLaunchKernelGGL(k_fma_poly, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, b, c, nl, map, T.pc, T.logn);
+    prof_launch(KID_ELEMENTWISE, EW_BYTES(3.0 * rows + nl), k_fma_poly, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, b, c, nl, map, T.pc, T.logn);
 }
-void launch_mul_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const u32* cst, int rows, int nl, LimbMap map) {
-    EW_WRAP(2.0 * rows);
-    hipLaunchKernelGGL(k_mul_const_half, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, cst, nl, map, T.pc, T.logn);
+void launch_mul_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const LimbConsts& cst, int rows, int nl, LimbMap map) {
+    prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows), k_mul_const_half, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, cst, nl, map, T.pc, T.logn);
 }
-void launch_add_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const u32* cst, int rows, int nl, LimbMap map) {
-    EW_WRAP(2.0 * rows);
-    hipLaunchKernelGGL(k_add_const_half, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, cst, nl, map, T.pc, T.logn);
+void launch_add_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const LimbConsts& cst, int rows, int nl, LimbMap map) {
+    prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows), k_add_const_half, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, cst, nl, map, T.pc, T.logn);
 }
 void launch_automorph(hipStream_t st, const DevTables& T, u32* out, const u32* in, u64 g, int rows) {
-    ProfScope ps(st, KID_AUTOMORPH, words(2.0 * rows * (1u << T.logn)));
-    hipLaunchKernelGGL(k_automorph, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, g, T.logn);
+    prof_launch(KID_AUTOMORPH, words(2.0 * rows * (1u << T.logn)), k_automorph, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, g, T.logn);
 }
 void launch_rescale_spread(hipStream_t st, const DevTables& T, u32* v, const u32* last, int npoly, int nt, u32 q_last) {
-    ProfScope ps(st, KID_RESCALE, words((double)npoly * (1 + nt) * (1u << T.logn)));
-    hipLaunchKernelGGL(k_rescale_spread, dim3((1u << T.logn) / kBlock, nt, npoly), dim3(kBlock), 0, st, v, last, nt, q_last, T.pc,
+    prof_launch(KID_RESCALE, words((double)npoly * (1 + nt) * (1u << T.logn)), k_rescale_spread, dim3((1u << T.logn) / kBlock, nt, npoly), dim3(kBlock), 0, st, v, last, nt, q_last, T.pc,
                        T.logn);
 }
-void launch_rescale_finish(hipStream_t st, const DevTables& T, u32* out, const u32* x, const u32* v, const u32* qinv, int npoly, int nt,
-                           int nl_in) {
-    ProfScope ps(st, KID_RESCALE, words(3.0 * npoly * nt * (1u << T.logn)));
-    hipLaunchKernelGGL(k_rescale_finish, dim3((1u << T.logn) / kBlock, nt, npoly), dim3(kBlock), 0, st, out, x, v, qinv, nt, nl_in,
-                       T.pc, T.logn);
+void launch_base_convert(hipStream_t st, const DevTables& T, const ConvBatch& cb, int nt, LimbMap map) {
+    double w = 0;
+    for (int g = 0; g < cb.n; ++g) {
+        const bool own = cb.skip0[g] >= 0 && cb.skip0[g] < nt;
+        w += cb.h[g] + nt - (own ? std::min(cb.h[g], nt - cb.skip0[g]) : 0);
+    }
+    prof_launch(KID_BASE_CONVERT, words(w * (1u << T.logn)), k_base_convert,
+                dim3((1u << T.logn) / kBlock, (nt + kConvTargets - 1) / kConvTargets, cb.n), dim3(kBlock), 0, st, cb, nt, map, T.pc,
+                T.logn);
 }
-void launch_base_convert(hipStream_t st, const DevTables& T, u32* ext, const u32* x, int h, int d0, int nt, LimbMap map, int skip0,
-                         const u32* tab, const u32* qhinv, const u32* negq) {
-    const int skipped = (skip0 >= 0 && skip0 < nt) ? h : 0;
-    ProfScope ps(st, KID_BASE_CONVERT, words((double)(h + nt - skipped) * (1u << T.logn)));
-    hipLaunchKernelGGL(k_base_convert, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, ext, x, h, d0, nt, map, skip0, tab, qhinv,
-                       negq, T.pc, T.logn);
-}
-void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* key, int nd, int ne, int nl, int nkey,
-                      int nks, LimbMap map) {
-    // ext (nd x ne) + key (nd x 2 x ne) read, acc (2 x ne) written
-    ProfScope ps(st, KID_KEY_INNER, words((3.0 * nd + 2.0) * ne * (1u << T.logn)));
-    hipLaunchKernelGGL(k_key_inner, ew_grid(T.logn, ne), dim3(kBlock), 0, st, acc, ext, key, nd, ne, nl, nkey, nks, map, T.pc, T.logn);
-}
-void launch_moddown_finish(hipStream_t st, const DevTables& T, u32* out, const u32* acc, const u32* conv, const u32* pinv,
-                           const u32* add0, const u32* add1, int nl, int ne) {
-    ProfScope ps(st, KID_MODDOWN, words((6.0 + (add0 ? 1 : 0) + (add1 ? 1 : 0)) * nl * (1u << T.logn)));
-    hipLaunchKernelGGL(k_moddown_finish, dim3((1u << T.logn) / kBlock, nl, 2), dim3(kBlock), 0, st, out, acc, conv, pinv, add0, add1,
-                       nl, ne, T.pc, T.logn);
+void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
+                      int alpha, int nkey, int nks, LimbMap map) {
+    // ext/d (nd x ne) + key (nd x 2 x ne) read, acc (2 x ne) written
+    prof_launch(KID_KEY_INNER, words((3.0 * nd + 2.0) * ne * (1u << T.logn)), k_key_inner, ew_grid(T.logn, ne), dim3(kBlock), 0, st, acc,
+                ext, d, key, nd, ne, nl, alpha, nkey, nks, map, T.pc, T.logn);
 }
 void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, u64 seed, u64 stream, int kind) {
-    ProfScope ps(st, KID_SAMPLE, words((double)nl * (1u << T.logn)));
-    hipLaunchKernelGGL(k_sample_small, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, nl, map, seed, stream, kind, T.pc,
+    prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_small, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, nl, map, seed, stream, kind, T.pc,
                        T.logn);
 }
 void launch_sample_uniform(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, u64 seed, u64 stream) {
-    ProfScope ps(st, KID_SAMPLE, words((double)nl * (1u << T.logn)));
-    hipLaunchKernelGGL(k_sample_uniform, ew_grid(T.logn, nl), dim3(kBlock), 0, st, out, nl, map, seed, stream, T.pc, T.logn);
+    prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_uniform, ew_grid(T.logn, nl), dim3(kBlock), 0, st, out, nl, map, seed, stream, T.pc, T.logn);
 }
 void launch_keygen_combine(hipStream_t st, const DevTables& T, u32* b, const u32* a, const u32* s, const u32* e, const u32* sp,
                            const u32* gadget, int nl, LimbMap map, int glo, int ghi) {
-    EW_WRAP(4.0 * nl);
-    hipLaunchKernelGGL(k_keygen_combine, ew_grid(T.logn, nl), dim3(kBlock), 0, st, b, a, s, e, sp, gadget, nl, map, glo, ghi, T.pc,
+    prof_launch(KID_ELEMENTWISE, EW_BYTES(4.0 * nl), k_keygen_combine, ew_grid(T.logn, nl), dim3(kBlock), 0, st, b, a, s, e, sp, gadget, nl, map, glo, ghi, T.pc,
                        T.logn);
 }

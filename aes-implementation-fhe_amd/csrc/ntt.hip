@@ -1,0 +1,387 @@
+// ntt.hip -- negacyclic NTT / inverse NTT for CDNA4.
+//
+// N = R1 x 256 (R1 = 2^(logn-8), 32..256).  View a limb as R1 rows of 256 contiguous
+// words.  Forward (Cooley-Tukey, natural -> bit-reversed, psi^{bitrev} twiddles):
+//   pass 1 ("cols"): stages 0..log2(R1)-1, butterflies between rows; a 512-thread block
+//                    owns CB = 512 * 16 / R1 columns of all R1 rows,
+//   pass 2 ("rows"): stages log2(R1)..logn-1 inside each 256-word row; a block owns
+//                    32 rows.
+// Each thread keeps 16 elements in VGPRs.  Phase A holds elements 16 apart (rows
+// g + T k in pass 1, words j + 16 k in pass 2) and runs the first 4 stages in registers;
+// one LDS exchange regroups them into 16 consecutive elements (rows 16 g + k, words
+// 16 j + k) for the remaining stages.  So a pass is: one global read, 4 register stages,
+// one LDS round trip, up to 4 register stages, one global write -- instead of one LDS
+// round trip and barrier per stage.  The inverse (Gentleman-Sande) runs the same passes
+// backwards (rows first, then cols with the N^{-1} scaling fused into the store).
+//
+// Global access: pass 1 reads/writes 32..256 consecutive columns per row (>= 128 B
+// segments); pass 2's phase-B side moves 16 contiguous words per thread (4 x b128).
+// LDS: pass 1 tile [R1][CB] -- every 32-lane half touches 32 consecutive columns, no
+// conflicts; pass 2 tile [32][272] with the 16-word-group XOR swizzle swz(), conflict-free
+// for both the (j + 16 k) and the (16 j + k) pattern (rows r, r+1 share a half-wave and
+// sit 272 = 16 mod 32 banks apart).
+//
+// Rows of one launch are addressed through a RowMap (out-of-place, strided groups), so
+// callers never copy limbs around just to transform them.
+#include "kernels.h"
+#include "launch.h"
+
+namespace {
+
+constexpr int kThreads = 512;
+constexpr int kRowsP2 = 32;
+constexpr int kPitchP2 = 272;
+
+__device__ __forceinline__ void ct_bfly(u32& a, u32& b, u32 w, u32 wp, u32 q) {
+    const u32 t = shoup_mul(b, w, wp, q);
+    b = sub_mod(a, t, q);
+    a = add_mod(a, t, q);
+}
+__device__ __forceinline__ void gs_bfly(u32& a, u32& b, u32 w, u32 wp, u32 q) {
+    const u32 u = a, v = b;
+    a = add_mod(u, v, q);
+    b = shoup_mul(u + q - v, w, wp, q);
+}
+__device__ __forceinline__ int swz(int w) { return w ^ ((w >> 4) & 15); }
+
+enum { kPlain = 0, kSpread = 1, kFinish = 1 };
+
+// key-switching ModUp: digit g's own limbs [g alpha, min(nl, (g + 1) alpha)) are not
+// transformed (they are already in NTT form in the input); block-uniform early exit
+__device__ __forceinline__ bool skipped(const RowMap& rm) {
+    if (rm.skip_alpha <= 0) return false;
+    const int g = blockIdx.y / rm.cnt, i = blockIdx.y - g * rm.cnt;
+    return i < rm.skip_nl && i / rm.skip_alpha == g;
+}
+
+struct RowAddr {
+    const u32* src;
+    u32* dst;
+    int prime;
+};
+template <int LOGN>
+__device__ __forceinline__ RowAddr row_addr(u32* dst, const u32* src, const RowMap& rm, const LimbMap& map) {
+    const int y = blockIdx.y;
+    const int g = y / rm.cnt, i = y - g * rm.cnt;
+    RowAddr a;
+    a.src = src + ((size_t)(rm.src_off + g * rm.src_stride + i) << LOGN);
+    a.dst = dst + ((size_t)(rm.dst_off + g * rm.dst_stride + i) << LOGN);
+    a.prime = map.prime(i);
+    return a;
+}
+
+// ---------------------------------------------------------------- forward, pass 1
+// MODE kPlain: x = src row.  MODE kSpread (rescale): the source is one coefficient-form
+// row per group modulo aux.q_last (src row = src_off + g * src_stride, independent of the
+// limb) and x = its centred representative reduced mod the target prime.
+template <int LOGR1, int MODE>
+__global__ void __launch_bounds__(kThreads) k_ntt1_fwd(u32* dst, const u32* src, RowMap rm, LimbMap map, const PrimeConst* pc,
+                                                       const u32* psi, const u32* psip, NttAux aux) {
+    constexpr int LOGN = LOGR1 + 8, R1 = 1 << LOGR1, T = R1 / 16, CB = kThreads / T;
+    __shared__ u32 sm[R1 * CB];
+    if (skipped(rm)) return;
+    RowAddr ra = row_addr<LOGN>(dst, src, rm, map);
+    const u32 q = pc[ra.prime].q;
+    const u32* w = psi + ((size_t)ra.prime << LOGN);
+    const u32* wp = psip + ((size_t)ra.prime << LOGN);
+    const int col = threadIdx.x % CB, g = threadIdx.x / CB;
+    const int c = blockIdx.x * CB + col;
+    u32 x[16];
+    if (MODE == kSpread) {
+        const int grp = blockIdx.y / rm.cnt;
+        ra.src = src + ((size_t)(rm.src_off + grp * rm.src_stride) << LOGN);
+        const u32 ql = aux.q_last, half = ql >> 1;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const u32 v = ra.src[(size_t)(g + T * k) * 256 + c];
+            // q_last < 2^32/3 < 2q: the reductions are single conditional subtracts
+            x[k] = v > half ? q - (ql - v) : csub(v, q);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) x[k] = ra.src[(size_t)(g + T * k) * 256 + c];
+    }
+    // stages 0..3: row distance R1 / 2^(s+1) = T * (8 >> s); block index k >> (4 - s)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int h = 8 >> s;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!(k & h)) {
+                const int ti = (1 << s) + (k >> (4 - s));
+                ct_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sm[(g + T * k) * CB + col] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = sm[(16 * g + k) * CB + col];
+    // stages 4..LOGR1-1 on rows 16 g + k
+#pragma unroll
+    for (int s = 4; s < LOGR1; ++s) {
+        const int h = 1 << (LOGR1 - 1 - s);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!(k & h)) {
+                const int ti = (1 << s) + ((16 * g + k) >> (LOGR1 - s));
+                ct_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ra.dst[(size_t)(16 * g + k) * 256 + c] = x[k];
+}
+
+// ---------------------------------------------------------------- forward, pass 2 (in place on dst rows)
+// MODE kPlain: result stored in place.  MODE kFinish (rescale / ModDown): with
+// g = group, i = limb, out[g][i] = (cur[g][i] - x) * qinv_i (+ add_g[i]), rows addressed
+// through aux (cur row g * cur_stride + i, out row g * out_stride + i).
+template <int LOGR1, int MODE>
+__global__ void __launch_bounds__(kThreads) k_ntt2_fwd(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const u32* psi,
+                                                       const u32* psip, NttAux aux) {
+    constexpr int LOGN = LOGR1 + 8;
+    __shared__ u32 sm[kRowsP2 * kPitchP2];
+    if (skipped(rm)) return;
+    const RowAddr ra = row_addr<LOGN>(data, data, rm, map);
+    const u32 q = pc[ra.prime].q;
+    const u32* w = psi + ((size_t)ra.prime << LOGN);
+    const u32* wp = psip + ((size_t)ra.prime << LOGN);
+    const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
+    const int R = blockIdx.x * kRowsP2 + r;
+    u32* p = ra.dst + (size_t)R * 256;
+    u32 x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = p[j + 16 * k];
+    // stage LOGR1 + s: twiddle index 2^(LOGR1+s) + R 2^s + (word >> (8 - s))
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int h = 8 >> s;
+        const int base = (1 << (LOGR1 + s)) + (R << s);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!(k & h)) {
+                const int ti = base + (k >> (4 - s));
+                ct_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+            }
+    }
+    u32* row = sm + r * kPitchP2;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) row[swz(j + 16 * k)] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = row[swz(16 * j + k)];
+#pragma unroll
+    for (int s = 4; s < 8; ++s) {
+        const int h = 1 << (7 - s);
+        const int base = (1 << (LOGR1 + s)) + (R << s);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!(k & h)) {
+                const int ti = base + ((16 * j + k) >> (8 - s));
+                ct_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+            }
+    }
+    if (MODE == kFinish) {
+        const int grp = blockIdx.y / rm.cnt, li = blockIdx.y - grp * rm.cnt;
+        const size_t woff = (size_t)R * 256 + 16 * j;
+        const uint4* cu = reinterpret_cast<const uint4*>(aux.cur + ((size_t)(grp * aux.cur_stride + li) << LOGN) + woff);
+        const u32* addp = grp == 0 ? aux.add0 : aux.add1;
+        const uint4* ad = addp ? reinterpret_cast<const uint4*>(addp + ((size_t)li << LOGN) + woff) : nullptr;
+        uint4* o = reinterpret_cast<uint4*>(aux.out + ((size_t)(grp * aux.out_stride + li) << LOGN) + woff);
+        const u32 qi = aux.qinv[2 * li], qip = aux.qinv[2 * li + 1];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const uint4 cv = cu[v];
+            uint4 r;
+            r.x = shoup_mul(cv.x + q - x[4 * v], qi, qip, q);
+            r.y = shoup_mul(cv.y + q - x[4 * v + 1], qi, qip, q);
+            r.z = shoup_mul(cv.z + q - x[4 * v + 2], qi, qip, q);
+            r.w = shoup_mul(cv.w + q - x[4 * v + 3], qi, qip, q);
+            if (ad) {
+                const uint4 a = ad[v];
+                r.x = add_mod(r.x, a.x, q), r.y = add_mod(r.y, a.y, q), r.z = add_mod(r.z, a.z, q), r.w = add_mod(r.w, a.w, q);
+            }
+            o[v] = r;
+        }
+    } else {
+        uint4* o = reinterpret_cast<uint4*>(p + 16 * j);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) o[v] = make_uint4(x[4 * v], x[4 * v + 1], x[4 * v + 2], x[4 * v + 3]);
+    }
+}
+
+// ---------------------------------------------------------------- inverse, pass 2 (src -> dst)
+template <int LOGR1>
+__global__ void __launch_bounds__(kThreads) k_ntt2_inv(u32* dst, const u32* src, RowMap rm, LimbMap map, const PrimeConst* pc,
+                                                       const u32* ipsi, const u32* ipsip) {
+    constexpr int LOGN = LOGR1 + 8;
+    __shared__ u32 sm[kRowsP2 * kPitchP2];
+    if (skipped(rm)) return;
+    const RowAddr ra = row_addr<LOGN>(dst, src, rm, map);
+    const u32 q = pc[ra.prime].q;
+    const u32* w = ipsi + ((size_t)ra.prime << LOGN);
+    const u32* wp = ipsip + ((size_t)ra.prime << LOGN);
+    const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
+    const int R = blockIdx.x * kRowsP2 + r;
+    u32 x[16];
+    const uint4* in = reinterpret_cast<const uint4*>(ra.src + (size_t)R * 256 + 16 * j);
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+        const uint4 t = in[v];
+        x[4 * v] = t.x, x[4 * v + 1] = t.y, x[4 * v + 2] = t.z, x[4 * v + 3] = t.w;
+    }
+#pragma unroll
+    for (int s = 7; s >= 4; --s) {
+        const int h = 1 << (7 - s);
+        const int base = (1 << (LOGR1 + s)) + (R << s);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!(k & h)) {
+                const int ti = base + ((16 * j + k) >> (8 - s));
+                gs_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+            }
+    }
+    u32* row = sm + r * kPitchP2;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) row[swz(16 * j + k)] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = row[swz(j + 16 * k)];
+#pragma unroll
+    for (int s = 3; s >= 0; --s) {
+        const int h = 8 >> s;
+        const int base = (1 << (LOGR1 + s)) + (R << s);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!(k & h)) {
+                const int ti = base + (k >> (4 - s));
+                gs_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+            }
+    }
+    u32* p = ra.dst + (size_t)R * 256;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) p[j + 16 * k] = x[k];
+}
+
+// ---------------------------------------------------------------- inverse, pass 1 (in place on dst rows)
+template <int LOGR1>
+__global__ void __launch_bounds__(kThreads) k_ntt1_inv(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const u32* ipsi,
+                                                       const u32* ipsip) {
+    constexpr int LOGN = LOGR1 + 8, R1 = 1 << LOGR1, T = R1 / 16, CB = kThreads / T;
+    __shared__ u32 sm[R1 * CB];
+    if (skipped(rm)) return;
+    const RowAddr ra = row_addr<LOGN>(data, data, rm, map);
+    const PrimeConst P = pc[ra.prime];
+    const u32 q = P.q;
+    const u32* w = ipsi + ((size_t)ra.prime << LOGN);
+    const u32* wp = ipsip + ((size_t)ra.prime << LOGN);
+    const int col = threadIdx.x % CB, g = threadIdx.x / CB;
+    const int c = blockIdx.x * CB + col;
+    u32 x[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = ra.dst[(size_t)(16 * g + k) * 256 + c];
+#pragma unroll
+    for (int s = LOGR1 - 1; s >= 4; --s) {
+        const int h = 1 << (LOGR1 - 1 - s);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!(k & h)) {
+                const int ti = (1 << s) + ((16 * g + k) >> (LOGR1 - s));
+                gs_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sm[(16 * g + k) * CB + col] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = sm[(g + T * k) * CB + col];
+#pragma unroll
+    for (int s = 3; s >= 0; --s) {
+        const int h = 8 >> s;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!(k & h)) {
+                const int ti = (1 << s) + (k >> (4 - s));
+                gs_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) ra.dst[(size_t)(g + T * k) * 256 + c] = shoup_mul(x[k], P.ninv, P.ninv_p, q);
+}
+
+// io_rows: rows actually transformed (launch rows minus skipped ones), for the byte count
+template <int LOGR1, int M1, int M2>
+void ntt_fwd_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, int io_rows, RowMap rm, LimbMap map,
+               const NttAux& aux) {
+    constexpr int R1 = 1 << LOGR1, CB = kThreads / (R1 / 16);
+    const double row_bytes = 4.0 * 256.0 * R1;
+    const double io1 = 2.0 * io_rows * row_bytes;
+    const double io2 = (M2 == kFinish ? (3.0 + (aux.add0 ? 0.5 : 0.0) + (aux.add1 ? 0.5 : 0.0)) : 2.0) * io_rows * row_bytes;
+    prof_launch(KID_NTT_COLS_FWD, io1, k_ntt1_fwd<LOGR1, M1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, src, rm, map, Tb.pc,
+                Tb.psi, Tb.psip, aux);
+    prof_launch(KID_NTT_ROWS_FWD, io2, k_ntt2_fwd<LOGR1, M2>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, rm, map, Tb.pc,
+                Tb.psi, Tb.psip, aux);
+}
+template <int LOGR1>
+void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {
+    constexpr int R1 = 1 << LOGR1, CB = kThreads / (R1 / 16);
+    const double io = 4.0 * 2.0 * rows * (256.0 * R1);  // the inverse is never launched with skips
+    prof_launch(KID_NTT_ROWS_INV, io, k_ntt2_inv<LOGR1>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, src, rm, map, Tb.pc,
+                Tb.ipsi, Tb.ipsip);
+    prof_launch(KID_NTT_COLS_INV, io, k_ntt1_inv<LOGR1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, rm, map, Tb.pc, Tb.ipsi,
+                Tb.ipsip);
+}
+
+}  // namespace
+
+template <int M1, int M2>
+void ntt_fwd_dispatch(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, int io_rows, RowMap rm, LimbMap map,
+                      const NttAux& aux) {
+    if (rows <= 0) return;
+    switch (T.logn) {
+        case 13: ntt_fwd_t<5, M1, M2>(st, T, dst, src, rows, io_rows, rm, map, aux); break;
+        case 14: ntt_fwd_t<6, M1, M2>(st, T, dst, src, rows, io_rows, rm, map, aux); break;
+        case 15: ntt_fwd_t<7, M1, M2>(st, T, dst, src, rows, io_rows, rm, map, aux); break;
+        case 16: ntt_fwd_t<8, M1, M2>(st, T, dst, src, rows, io_rows, rm, map, aux); break;
+        default: break;  // HostParams::build rejects other ring sizes
+    }
+}
+
+void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {
+    int io_rows = rows;
+    if (rm.skip_alpha > 0)
+        for (int y = 0; y < rows; ++y) {
+            const int g = y / rm.cnt, i = y - g * rm.cnt;
+            if (i < rm.skip_nl && i / rm.skip_alpha == g) --io_rows;
+        }
+    ntt_fwd_dispatch<kPlain, kPlain>(st, T, dst, src, rows, io_rows, rm, map, NttAux{});
+}
+void launch_rescale_ntt(hipStream_t st, const DevTables& T, u32* out, const u32* cur, const u32* last, u32* v, const u32* qinv,
+                        int npoly, int nt, int nl_in, u32 q_last) {
+    NttAux aux{};
+    aux.cur = cur, aux.out = out, aux.qinv = qinv, aux.cur_stride = nl_in, aux.out_stride = nt, aux.q_last = q_last;
+    const RowMap rm{nt, 1, nt, 0, 0};
+    ntt_fwd_dispatch<kSpread, kFinish>(st, T, v, last, npoly * nt, npoly * nt, rm, LimbMap{1 << 30, 0, 0}, aux);
+}
+void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, const u32* cur, int cur_stride, const u32* qinv,
+                       const u32* add0, const u32* add1, int npoly, int nt) {
+    NttAux aux{};
+    aux.cur = cur, aux.out = out, aux.qinv = qinv, aux.cur_stride = cur_stride, aux.out_stride = nt, aux.add0 = add0, aux.add1 = add1;
+    ntt_fwd_dispatch<kPlain, kFinish>(st, T, conv, conv, npoly * nt, npoly * nt, rows_dense(nt), LimbMap{1 << 30, 0, 0}, aux);
+}
+void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {
+    if (rows <= 0) return;
+    switch (T.logn) {
+        case 13: ntt_inv_t<5>(st, T, dst, src, rows, rm, map); break;
+        case 14: ntt_inv_t<6>(st, T, dst, src, rows, rm, map); break;
+        case 15: ntt_inv_t<7>(st, T, dst, src, rows, rm, map); break;
+        case 16: ntt_inv_t<8>(st, T, dst, src, rows, rm, map); break;
+        default: break;
+    }
+}
+void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map) {
+    launch_ntt_fwd(st, T, data, data, rows, rows_dense(nl), map);
+}
+void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map) {
+    launch_ntt_inv(st, T, data, data, rows, rows_dense(nl), map);
+}

@@ -55,7 +55,7 @@ static u32 root_2n(u32 q, int logn) {
 bool HostParams::homogeneous(int level) const { return !(L > L1 && level == L1 + 1); }
 
 std::string HostParams::build(int logn_, int L1_, int n_double, int dnum_, uint64_t seed_) {
-    if (logn_ < 10 || logn_ > 17) return "log_n must lie in [10, 17]";
+    if (logn_ < 13 || logn_ > 16) return "log_n must lie in [13, 16] (NTT kernels, ntt.hip)";
     if (L1_ < 1 || L1_ > 60 || n_double < 0 || n_double > 30) return "max_level must lie in [1, 60]";
     if (dnum_ < 1) return "dnum must be >= 1";
     logn = logn_; n = 1 << logn; L1 = L1_; L = L1 + n_double; dnum = dnum_; seed = seed_;

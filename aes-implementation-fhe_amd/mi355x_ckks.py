@@ -34,7 +34,7 @@ EXPORTED = [
     "aesfhe_relinearize", "aesfhe_rescale", "aesfhe_level_down", "aesfhe_rotate", "aesfhe_conjugate",
     "aesfhe_power_basis", "aesfhe_to_ntt", "aesfhe_to_intt", "aesfhe_bootstrap", "aesfhe_renorm_pair",
     "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
-    "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters",
+    "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_bench_op",
     "aesfhe_profile", "aesfhe_kernel_stats", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan",
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group",
@@ -85,6 +85,7 @@ def load_library(path: Optional[Path] = None):
         "aesfhe_debug_ntt": [vp, _up, c_int, c_int, c_int],
         "aesfhe_debug_keyswitch": [vp, c_int, ctypes.c_uint64, _up, _up],
         "aesfhe_counters": [vp, np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS"), c_int],
+        "aesfhe_bench_op": [vp, c_int, c_int, c_int, ctypes.POINTER(c_dbl)],
         "aesfhe_reset_counters": [vp],
         "aesfhe_profile": [vp, ctypes.c_uint32],
         "aesfhe_kernel_stats": [vp, _dp, c_int, c_int],
@@ -455,6 +456,15 @@ class Engine:
 
     def reset_counters(self):
         self._ctx.check(self._lib.aesfhe_reset_counters(self._ctx.ptr))
+
+    BENCH_OPS = {"ntt": 0, "intt": 1, "keyswitch": 2, "rescale": 3, "mul_relin_rescale": 4}
+
+    def bench_op(self, op: str, arg: int, iters: int = 50) -> float:
+        """microseconds per back-to-back iteration of one primitive (aesfhe_bench_op)"""
+        self._ensure_keys()
+        us = ctypes.c_double(0.0)
+        self._ctx.check(self._lib.aesfhe_bench_op(self._ctx.ptr, self.BENCH_OPS[op], int(arg), int(iters), ctypes.byref(us)))
+        return us.value
 
     def profile(self, kernels=()):
         """Enable HIP-event timing for the named kernel ids (see KERNEL_IDS); () disables."""

@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-final-bootstrap", action="store_true",
                     help="diagnostic only: skip MixColFinal's final bootstrap (not the benchmark workload)")
-    ap.add_argument("--traffic-json", default=None, help="per-launch HBM bytes from a rocprofv3 PMC pass")
+    ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r1_pmc_traffic.json"), help="per-launch HBM bytes from a rocprofv3 PMC pass")
     return ap.parse_args()
 
 
@@ -116,6 +116,20 @@ class _NoFinalBootstrap:
         return self.mix(ct_hi, ct_lo, do_final_bootstrap=False)
 
 
+def _progress(ctx, every_s: float = 30.0):
+    """stderr heartbeat with real progress (bootstraps done), for long profiled runs."""
+    import threading
+    t0 = time.perf_counter()
+
+    def run():
+        while True:
+            time.sleep(every_s)
+            print(f"[bench] {time.perf_counter() - t0:.0f}s bootstraps={ctx.bootstrap_stats()['count']}",
+                  file=sys.stderr, flush=True)
+
+    threading.Thread(target=run, daemon=True).start()
+
+
 def main():
     args = parse()
     rank, world, local, dist = dist_setup(args.gpus)
@@ -143,6 +157,7 @@ def main():
     states = [rng.integers(0, 256, 16).astype(np.uint8) for _ in range(args.warmup + args.steps)]
 
     E = ctx.engine
+    _progress(ctx)
     for i in range(args.warmup):
         pipe.encrypt(states[i], rks)
     E.sync()
@@ -175,7 +190,8 @@ def main():
     achieved = ks["bytes"] / (ks["ms"] * 1e-3) / 1e9 if ks["ms"] > 0 else 0.0
     traffic = None
     if args.traffic_json and Path(args.traffic_json).exists():
-        traffic = json.loads(Path(args.traffic_json).read_text()).get(args.kernel)
+        t = json.loads(Path(args.traffic_json).read_text()).get(args.kernel)
+        traffic = t["bytes_per_launch"] if t else None
     line = {
         "metric": "homomorphic AES-128 rounds/sec (enc) at N=2^16",
         "value": value,

@@ -125,6 +125,11 @@ int aesfhe_debug_ntt(aesfhe_ctx* ctx, uint32_t* data, int rows, int first_prime,
 /* key switch of a raw polynomial d (level+2 limbs, NTT) with the key of galois g */
 int aesfhe_debug_keyswitch(aesfhe_ctx* ctx, int level, uint64_t galois, const uint32_t* d, uint32_t* out);
 /* per-kernel timing of the last N ops (HIP events); op counters */
+/* Micro-benchmark of one primitive, iters back-to-back launches on the engine stream;
+ * *us = microseconds per iteration (device time incl. launch gaps).  op 0: NTT of arg
+ * rows, 1: inverse NTT of arg rows, 2: key switch at level arg, 3: rescale at level arg,
+ * 4: ct x ct + relinearise + rescale at level arg.  MI355X-side tooling. */
+int aesfhe_bench_op(aesfhe_ctx* ctx, int op, int arg, int iters, double* us);
 int aesfhe_counters(aesfhe_ctx* ctx, uint64_t* out, int n);
 /* live kernel timing with HIP events on the engine stream: bit k of mask enables kernel id k
  * (order: ntt_cols_fwd, ntt_rows_fwd, ntt_rows_inv, ntt_cols_inv, base_convert, key_inner,

@@ -1,0 +1,50 @@
+"""Reduce a rocprofv3 --pmc counter_collection.csv to per-kernel mean HBM bytes per launch.
+
+gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of
+wide coalesced reads -> x2; WRITE_SIZE is exact.  Both counters are in KB.  Usage:
+  python tools/pmc_reduce.py OUT.json DIR [DIR ...]   (one DIR per --pmc pass)
+Deletes the (large) CSVs after reading so gpurun can copy the result back."""
+import csv
+import json
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+SCALE = {"FETCH_SIZE": 2 * 1024.0, "WRITE_SIZE": 1024.0}
+
+
+def short(name: str) -> str:
+    name = name.replace("(anonymous namespace)::", "").split("(")[0]
+    for pre in ("k_", "void k_"):
+        if name.startswith(pre):
+            return name[len(pre):]
+    return name
+
+
+def main():
+    out, dirs = Path(sys.argv[1]), sys.argv[2:]
+    acc = defaultdict(lambda: defaultdict(float))
+    cnt = defaultdict(lambda: defaultdict(int))
+    for d in dirs:
+        for f in Path(d).rglob("*counter_collection.csv"):
+            with open(f) as fh:
+                head = [next(fh, "") for _ in range(3)]
+                out.with_suffix(".sample.txt").write_text("".join(head))
+                fh.seek(0)
+                for row in csv.DictReader(fh):
+                    c = row["Counter_Name"]
+                    k = short(row["Kernel_Name"])
+                    acc[k][c] += float(row["Counter_Value"]) * SCALE.get(c, 1.0)
+                    cnt[k][c] += 1
+            f.unlink()
+    res = {}
+    for k in acc:
+        per = {c: acc[k][c] / cnt[k][c] for c in acc[k]}
+        res[k] = {"bytes_per_launch": sum(per.values()), "launches": max(cnt[k].values()),
+                  **{c.lower() + "_bytes": v for c, v in per.items()}}
+    out.write_text(json.dumps(res, indent=1))
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
