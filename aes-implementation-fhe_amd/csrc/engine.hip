@@ -80,13 +80,20 @@ private:
     size_t bytes_ = 0;
 };
 
+// A ciphertext tensor.  `level` is the DATA level (nl(level) limbs per polynomial); `pend`
+// rescales are still owed, so the logical level is level - pend and the raw scale is
+// raw_scale(level, pend).  `lazy` marks work the engine deferred on its own
+// (relinearisation of a product, rescales of scalar products): the API shows such a
+// ciphertext as 2 polynomials at its logical level.  `zero`: an exact encryption of 0.
 struct Ct {
     u32* data = nullptr;
     size_t words = 0;
     int level = 0;
     int npoly = 2;
     bool ntt = true;
-    bool pending = false;  // tensor product awaiting rescale (scale delta_level^2)
+    int pend = 0;
+    bool lazy = false;
+    bool zero = false;
 };
 
 struct Pt {
@@ -335,13 +342,28 @@ public:
     }
 
     // decryption to real coefficients (message * delta_level)
-    int decrypt_coeffs(const Ct& c_in, std::vector<double>& m) {
+    // decryption works on the raw tensor: a deferred third polynomial is decrypted with s^2
+    // and owed rescales are folded into the returned scale raw_scale(level, pend); the CRT
+    // uses the fewest limbs (2..4) whose product exceeds that scale by 2^26
+    double decrypt_coeffs(const Ct& c_in, std::vector<double>& m) {
         const int n = hp_.n;
         Ct c = ensure_ntt(c_in);
-        const int level = c.level;
         const int nl = hp_.nl(c.level);
-        // limbs used for the CRT: 2 (Q0 ~ 2^60.8) unless the scale is double-prime sized
-        const int kd = (level >= 0 && hp_.delta[level] > 35184372088832.0 && nl >= 4) ? 4 : std::min(2, nl);
+        const double need = c.level >= 0 ? std::log2(raw_scale(c.level, c.pend)) + 26.0 : 0.0;
+        int kd = std::min(2, nl);
+        double have = 0.0;
+        for (int i = 0; i < kd; ++i) have += std::log2((double)hp_.mod[i]);
+        while (have < need && kd < std::min(4, nl)) have += std::log2((double)hp_.mod[kd++]);
+        if (have < need && c.pend > 0) {  // too large for 128-bit CRT: apply the owed work first
+            Ct nc = normalize(c, true);
+            if (c.data != c_in.data) release(c);
+            std::vector<double> mm;
+            const double sc = decrypt_coeffs(nc, mm);
+            if (nc.data != c_in.data) release(nc);
+            m.swap(mm);
+            return sc;
+        }
+        const double scale = c.level >= 0 ? raw_scale(c.level, c.pend) : (bs_.ready ? bs_.s_bt : 1.0);
         u32* x = tmp(kd);
         HIP_OK(hipMemcpyAsync(x, c.data, sizeof(u32) * kd * n, hipMemcpyDeviceToDevice, st_));
         u32* spow = nullptr;
@@ -382,46 +404,40 @@ public:
             m[k] = v > Qall / 2 ? -(double)(Qall - v) : (double)v;
         }
         cnt_[C_DEC]++;
-        return level;
+        return scale;
     }
     void decrypt(aesfhe_handle h, double* re, double* im) {
         std::vector<double> m;
-        const int level = decrypt_coeffs(ct(h), m);
-        const double inv = 1.0 / hp_.delta[level];
+        const double inv = 1.0 / decrypt_coeffs(ct(h), m);
         for (double& v : m) v *= inv;
         emb_.forward(m.data(), re, im);
     }
 
     // ------------------------------------------------------------------ basic ops
     void release(const Ct& c) { pool_.put(c.data, c.words); }
+    static void copy_meta(Ct& o, const Ct& c) {
+        o.ntt = c.ntt, o.pend = c.pend, o.lazy = c.lazy, o.zero = c.zero;
+    }
     Ct copy(const Ct& c) {
         Ct o = alloc_ct(c.level, c.npoly);
-        o.ntt = c.ntt;
-        o.pending = c.pending;
+        copy_meta(o, c);
         HIP_OK(hipMemcpyAsync(o.data, c.data, c.words * sizeof(u32), hipMemcpyDeviceToDevice, st_));
         return o;
     }
     // returns c itself (same data) when already in NTT form, else a converted copy
-    Ct ensure_ntt(const Ct& c, bool resolve_pending = true) {
-        Ct o = c;
-        if (!c.ntt) {
-            o = alloc_ct(c.level, c.npoly);
-            o.pending = c.pending;
-            const int nl = hp_.nl(o.level);
-            ntt(o.data, c.data, o.npoly * nl, rows_dense(nl), qmap());
-            o.ntt = true;
-        }
-        if (resolve_pending && o.pending) {
-            Ct r = rescale(o);
-            if (o.data != c.data) release(o);
-            o = r;
-        }
+    Ct ensure_ntt(const Ct& c) {
+        if (c.ntt) return c;
+        Ct o = alloc_ct(c.level, c.npoly);
+        copy_meta(o, c);
+        const int nl = hp_.nl(o.level);
+        ntt(o.data, c.data, o.npoly * nl, rows_dense(nl), qmap());
+        o.ntt = true;
         return o;
     }
     Ct to_intt(const Ct& c) {
         if (!c.ntt) return copy(c);
         Ct o = alloc_ct(c.level, c.npoly);
-        o.pending = c.pending;
+        copy_meta(o, c);
         const int nl = hp_.nl(o.level);
         intt(o.data, c.data, o.npoly * nl, rows_dense(nl), qmap());
         o.ntt = false;
@@ -430,11 +446,92 @@ public:
     Ct to_ntt(const Ct& c) {
         if (c.ntt) return copy(c);
         Ct o = alloc_ct(c.level, c.npoly);
-        o.pending = c.pending;
+        copy_meta(o, c);
         const int nl = hp_.nl(o.level);
         ntt(o.data, c.data, o.npoly * nl, rows_dense(nl), qmap());
         o.ntt = true;
         return o;
+    }
+
+    // ------------------------------------------------------------------ deferred work
+    // product of the primes a rescale at level l drops
+    double qdrop(int l) const {
+        double d = 1.0;
+        for (int i = hp_.nl(l - 1); i < hp_.nl(l); ++i) d *= (double)hp_.mod[i];
+        return d;
+    }
+    // raw scale of a tensor at data level l owing p rescales: delta_{l-p} * Q_drop(l) ... Q_drop(l-p+1)
+    double raw_scale(int l, int p) const {
+        double sc = hp_.delta[l - p];
+        for (int j = 0; j < p; ++j) sc *= qdrop(l - j);
+        return sc;
+    }
+    double log2q(int l) const {
+        double b = 0.0;
+        for (int i = 0; i < hp_.nl(l); ++i) b += std::log2((double)hp_.mod[i]);
+        return b;
+    }
+    // a message of magnitude <= 2^kMsgBits times `mag` fits below Q_l / 2 at raw scale (l, p)
+    static constexpr double kMsgBits = 20.0;
+    bool headroom(int l, int p, double mag) const {
+        if (l - p < 0) return false;
+        return std::log2(raw_scale(l, p)) + std::log2(std::max(1.0, mag)) + kMsgBits < log2q(l) - 1.0;
+    }
+    static int vis_npoly(const Ct& c) { return c.lazy ? 2 : c.npoly; }
+
+    // key switch of the third polynomial at the data level; keeps pend
+    Ct relin_raw(const Ct& c) {
+        const int nl = hp_.nl(c.level), n = hp_.n;
+        Ct r = keyswitch(c.data + (size_t)2 * nl * n, c.level, ksk(0), c.data, c.data + (size_t)nl * n);
+        r.pend = c.pend;
+        r.lazy = c.lazy && c.pend > 0;
+        cnt_[C_RELIN]++;
+        return r;
+    }
+    // canonical form: every owed rescale applied and (need2) relinearised; c itself when
+    // nothing is owed.  The caller releases the result when its data differs from c's.
+    // A 3-polynomial tensor is only rescaled while its scale stays >= 2^50 (pend 2 -> 1):
+    // below that the rounding term r2 s^2 / q (|s^2| ~ 2^14 per coefficient for a dense
+    // ternary s) would show in the message, so it is relinearised first.
+    Ct normalize(const Ct& c_in, bool need2 = true) {
+        Ct cur = ensure_ntt(c_in);
+        bool own = cur.data != c_in.data;
+        while (cur.npoly == 3 && cur.pend >= 2) {
+            Ct r = rescale(cur);
+            if (own) release(cur);
+            cur = r, own = true;
+        }
+        if (cur.npoly == 3 && (need2 || cur.pend > 0)) {
+            Ct r = relin_raw(cur);
+            if (own) release(cur);
+            cur = r, own = true;
+        }
+        while (cur.pend > 0) {
+            Ct r = rescale(cur);
+            if (own) release(cur);
+            cur = r, own = true;
+        }
+        cur.lazy = false;
+        return cur;
+    }
+    // stored ciphertext in canonical form; the table entry is replaced so that deferred work
+    // is done once however often the handle is used
+    const Ct& canon(aesfhe_handle h) {
+        auto it = cts_.find(h);
+        if (it == cts_.end()) throw std::runtime_error("invalid ciphertext handle");
+        Ct& c = it->second;
+        if (c.lazy) {
+            Ct nc = normalize(c, true);
+            if (nc.data != c.data) release(c);
+            c = nc;
+        }
+        return c;
+    }
+    Ct zero_ct(int level) {
+        Ct z = alloc_ct(level, 2);
+        HIP_OK(hipMemsetAsync(z.data, 0, z.words * sizeof(u32), st_));
+        z.zero = true;
+        return z;
     }
 
     // drop the last k limbs of an npoly x nl tensor, dividing by each dropped prime with
@@ -471,6 +568,9 @@ public:
         o.npoly = c.npoly;
         o.words = (size_t)c.npoly * nlo * hp_.n;
         o.data = drop_limbs(c.data, c.npoly, nl, nl - nlo);
+        o.pend = c.pend > 0 ? c.pend - 1 : 0;
+        o.lazy = c.lazy && (o.pend > 0 || o.npoly == 3);
+        o.zero = c.zero;
         cnt_[C_RESCALE]++;
         return o;
     }
@@ -507,48 +607,75 @@ public:
         }
     }
 
-    // exact-scale level drop: keep limbs 0..nl(b)+k-1, multiply by
-    // c = round(delta_b * q_{nl(b)} ... q_{nl(b)+k-1} / delta_a) and divide the k limbs away;
-    // k is the smallest count that keeps c >= 2^24 (k = 1 inside a region, 2 across)
-    Ct level_down(const Ct& c_in, int level) {
-        if (level == c_in.level) return copy(c_in);
-        if (level > c_in.level) throw std::runtime_error("level_down: target level above ciphertext level");
+    // exact-scale change of representation: re-express a tensor at
+    // (data level t, owing p rescales), logical level t - p <= the input's.  Owed rescales
+    // are applied first down to the target data level; the rest is one exact-scale step:
+    // keep nl(t) + k limbs, multiply by c = round(S(t,p) q_{nl(t)} ... q_{nl(t)+k-1} / S(l,q))
+    // and divide the k limbs away, k the smallest count keeping c >= 2^24.  Always returns a
+    // new buffer.
+    Ct convert(const Ct& c_in, int t, int p) {
+        if (p < 0 || t > c_in.level || t - p > c_in.level - c_in.pend)
+            throw std::runtime_error("level_down: target level above ciphertext level");
         Ct c = ensure_ntt(c_in);
-        const int n = hp_.n, nb = hp_.nl(level), na = hp_.nl(c.level);
-        int k = 1;
-        double ratio = hp_.delta[level] / hp_.delta[c.level] * (double)hp_.mod[nb];
+        bool own = c.data != c_in.data;
+        if (c.level == t && c.pend == p) return own ? c : copy(c);
+        const int n = hp_.n, nb = hp_.nl(t), na = hp_.nl(c.level);
+        int k = 0;
+        double ratio = raw_scale(t, p) / raw_scale(c.level, c.pend);
         while (ratio < 16777216.0 && nb + k < na) ratio *= (double)hp_.mod[nb + k], ++k;
+        if (!(ratio >= 0.999999 && ratio < 9.0e18)) throw std::runtime_error("level_down: scale ratio out of range");
+        if (c.npoly == 3 && k > 0 && raw_scale(t, p) < 1.0e15) {  // see normalize()
+            Ct r = relin_raw(c);
+            if (own) release(c);
+            Ct o = convert(r, t, p);
+            release(r);
+            return o;
+        }
         const int nk = nb + k;
         u32* mid = tmp((size_t)c.npoly * nk);
-        for (int p = 0; p < c.npoly; ++p)
-            HIP_OK(hipMemcpyAsync(mid + (size_t)p * nk * n, c.data + (size_t)p * na * n, sizeof(u32) * nk * n, hipMemcpyDeviceToDevice,
+        for (int q = 0; q < c.npoly; ++q)
+            HIP_OK(hipMemcpyAsync(mid + (size_t)q * nk * n, c.data + (size_t)q * na * n, sizeof(u32) * nk * n, hipMemcpyDeviceToDevice,
                                   st_));
         const i64 cst = std::llround(ratio);
         std::vector<u32> r(nk);
-        for (int t = 0; t < nk; ++t) r[t] = mod_i64(cst, hp_.mod[t]);
+        for (int i = 0; i < nk; ++i) r[i] = mod_i64(cst, hp_.mod[i]);
         launch_mul_const_half(st_, T_, mid, mid, const_half(r, r), c.npoly * nk, nk, qmap());
         Ct o;
-        o.level = level;
-        o.npoly = c.npoly;
+        o.level = t, o.npoly = c.npoly, o.pend = p, o.lazy = c.lazy || p > 0, o.zero = c.zero;
         o.words = (size_t)c.npoly * nb * n;
-        o.data = drop_limbs(mid, c.npoly, nk, k);
-        untmp(mid, (size_t)c.npoly * nk);
-        if (c.data != c_in.data) release(c);
+        if (k == 0) {
+            o.data = mid;
+        } else {
+            o.data = drop_limbs(mid, c.npoly, nk, k);
+            untmp(mid, (size_t)c.npoly * nk);
+        }
+        if (own) release(c);
         return o;
     }
-    // two ciphertexts at a common level (copies only when a level change is needed)
+    // logical level drop of a canonical (pend 0) tensor
+    Ct level_down(const Ct& c_in, int level) {
+        if (c_in.pend > 0) {
+            Ct nc = normalize(c_in, false);
+            Ct o = level_down(nc, level);
+            if (nc.data != c_in.data) release(nc);
+            return o;
+        }
+        if (level > c_in.level) throw std::runtime_error("level_down: target level above ciphertext level");
+        return convert(c_in, level, 0);
+    }
+    // two canonical ciphertexts at a common level (copies only when a level change is needed)
     std::pair<Ct, Ct> align(const Ct& a, const Ct& b, bool& fa, bool& fb, bool for_mul = false) {
-        int lv = std::min(a.level - (a.pending ? 1 : 0), b.level - (b.pending ? 1 : 0));
+        int lv = std::min(a.level - a.pend, b.level - b.pend);
         if (for_mul && !hp_.homogeneous(lv)) --lv;  // never square across the region boundary
         Ct x = ensure_ntt(a), y = ensure_ntt(b);
         fa = x.data != a.data;
         fb = y.data != b.data;
-        if (x.level != lv) {
+        if (x.level != lv || x.pend) {
             Ct t = level_down(x, lv);
             if (fa) release(x);
             x = t, fa = true;
         }
-        if (y.level != lv) {
+        if (y.level != lv || y.pend) {
             Ct t = level_down(y, lv);
             if (fb) release(y);
             y = t, fb = true;
@@ -556,15 +683,40 @@ public:
         return {x, y};
     }
 
+    // a + b / a - b.  Operands owing the same work at the same data level combine directly;
+    // otherwise both are re-expressed at data level t = min(l_a, l_b, m + 2) owing t - m
+    // rescales (m = the lower logical level), falling back to canonical form when the raw
+    // scale would not fit
     Ct add_sub(const Ct& a, const Ct& b, bool sub) {
-        bool fa, fb;
-        auto xy = align(a, b, fa, fb);
-        const Ct &x = xy.first, &y = xy.second;
+        cnt_[C_ADD]++;
+        if (sub && a.data == b.data) return zero_ct(a.level - a.pend);
+        if (b.zero) return copy(a);
+        if (a.zero && !sub) return copy(b);
+        Ct x = ensure_ntt(a), y = ensure_ntt(b);
+        bool fa = x.data != a.data, fb = y.data != b.data;
+        if (x.level != y.level || x.pend != y.pend) {
+            const int m = std::min(x.level - x.pend, y.level - y.pend);
+            int t = std::min(std::min(x.level, y.level), m + 2), p = t - m;
+            if (p > 0 && !headroom(t, p, 1.0)) t = m, p = 0;
+            if (x.level != t || x.pend != p) {
+                Ct c = convert(x, t, p);
+                if (fa) release(x);
+                x = c, fa = true;
+            }
+            if (y.level != t || y.pend != p) {
+                Ct c = convert(y, t, p);
+                if (fb) release(y);
+                y = c, fb = true;
+            }
+        }
         const int nl = hp_.nl(x.level);
         const int np = std::max(x.npoly, y.npoly);
         Ct o = alloc_ct(x.level, np);
+        o.pend = x.pend;
+        o.lazy = x.lazy || y.lazy;
         const int common = std::min(x.npoly, y.npoly) * nl;
-        if (sub) launch_sub(st_, T_, o.data, x.data, y.data, common, nl, qmap());
+        if (x.zero) launch_neg(st_, T_, o.data, y.data, common, nl, qmap());
+        else if (sub) launch_sub(st_, T_, o.data, x.data, y.data, common, nl, qmap());
         else launch_add(st_, T_, o.data, x.data, y.data, common, nl, qmap());
         if (x.npoly > y.npoly)
             HIP_OK(hipMemcpyAsync(o.data + (size_t)common * hp_.n, x.data + (size_t)common * hp_.n, sizeof(u32) * nl * hp_.n,
@@ -576,88 +728,151 @@ public:
         }
         if (fa) release(x);
         if (fb) release(y);
-        cnt_[C_ADD]++;
         return o;
     }
 
+    // + constant at the tensor's raw scale: round(c delta_m) times the primes the owed
+    // rescales will divide out (m = logical level), so nothing has to be applied first
     Ct add_scalar(const Ct& c_in, double re, double im) {
         Ct c = ensure_ntt(c_in);
-        const int nl = hp_.nl(c.level);
+        const int nl = hp_.nl(c.level), m = c.level - c.pend;
         std::vector<u32> lo, hi;
-        scalar_residues(std::llround(re * hp_.delta[c.level]), std::llround(im * hp_.delta[c.level]), nl, lo, hi);
+        scalar_residues(std::llround(re * hp_.delta[m]), std::llround(im * hp_.delta[m]), nl, lo, hi);
+        if (c.pend > 0)
+            for (int t = 0; t < nl; ++t) {
+                u64 f = 1;
+                for (int i = hp_.nl(m); i < nl; ++i) f = f * (hp_.mod[i] % hp_.mod[t]) % hp_.mod[t];
+                lo[t] = (u32)((u64)lo[t] * f % hp_.mod[t]);
+                hi[t] = (u32)((u64)hi[t] * f % hp_.mod[t]);
+            }
         if (nl > 2 * kMaxConstLimbs) throw std::runtime_error("add_scalar: too many limbs");
         LimbConsts d{};
         for (int t = 0; t < nl; ++t) d.v[2 * t] = lo[t], d.v[2 * t + 1] = hi[t];
         Ct o = copy(c);
+        o.zero = false;
         launch_add_const_half(st_, T_, o.data, c.data, d, nl, nl, qmap());
         if (c.data != c_in.data) release(c);
         return o;
     }
 
-    Ct mul_scalar(const Ct& c_in, double re, double im) {
+    // applies owed rescales until at most one is left (before one more deferred product)
+    Ct upto_one_pend(const Ct& c_in, bool& own) {
         Ct c = ensure_ntt(c_in);
-        const int nl = hp_.nl(c.level);
-        Ct o;
+        own = c.data != c_in.data;
+        while (c.pend >= 2) {
+            Ct r = rescale(c);
+            if (own) release(c);
+            c = r, own = true;
+        }
+        return c;
+    }
+
+    // ct x scalar.  Gaussian integers multiply exactly (no level).  Otherwise the product
+    // consumes one level: eagerly (x round(c ptscale_l), rescale) or, when allow_lazy and the
+    // raw scale fits, deferred (x round(c S(l,p+1)/S(l,p)), one more owed rescale)
+    Ct mul_scalar(const Ct& c_in, double re, double im, bool allow_lazy = false) {
         cnt_[C_SCALAR]++;
-        if (re == std::floor(re) && im == std::floor(im) && std::fabs(re) < 1048576.0 && std::fabs(im) < 1048576.0) {
-            // Gaussian integer a + b i: exact multiplication by a + b X^{N/2}, no level consumed
+        const bool gauss = re == std::floor(re) && im == std::floor(im) && std::fabs(re) < 1048576.0 && std::fabs(im) < 1048576.0;
+        if (!gauss && c_in.level - c_in.pend < 1) throw std::runtime_error("not enough level to multiply by a scalar (level 0)");
+        if (c_in.zero) return gauss ? copy(c_in) : zero_ct(c_in.level - c_in.pend - 1);
+        if (gauss) {
+            Ct c = ensure_ntt(c_in);
+            const int nl = hp_.nl(c.level);
             std::vector<u32> lo, hi;
             scalar_residues((i64)re, (i64)im, nl, lo, hi);
-            const LimbConsts d = const_half(lo, hi);
-            o = alloc_ct(c.level, c.npoly);
-            launch_mul_const_half(st_, T_, o.data, c.data, d, c.npoly * nl, nl, qmap());
-        } else {
-            if (c.level < 1) throw std::runtime_error("not enough level to multiply by a scalar (level 0)");
-            std::vector<u32> lo, hi;
-            const double sc = hp_.ptscale[c.level];
-            scalar_residues(std::llround(re * sc), std::llround(im * sc), nl, lo, hi);
-            const LimbConsts d = const_half(lo, hi);
-            Ct t = alloc_ct(c.level, c.npoly);
-            launch_mul_const_half(st_, T_, t.data, c.data, d, c.npoly * nl, nl, qmap());
-            o = rescale(t);
-            release(t);
+            Ct o = alloc_ct(c.level, c.npoly);
+            copy_meta(o, c);
+            o.zero = re == 0.0 && im == 0.0;
+            launch_mul_const_half(st_, T_, o.data, c.data, const_half(lo, hi), c.npoly * nl, nl, qmap());
+            if (c.data != c_in.data) release(c);
+            return o;
         }
-        if (c.data != c_in.data) release(c);
+        bool own;
+        Ct c = upto_one_pend(c_in, own);
+        const double mag = std::hypot(re, im);
+        Ct o;
+        if (allow_lazy && headroom(c.level, c.pend + 1, mag)) {
+            const int nl = hp_.nl(c.level);
+            const double f = raw_scale(c.level, c.pend + 1) / raw_scale(c.level, c.pend);
+            std::vector<u32> lo, hi;
+            scalar_residues(std::llround(re * f), std::llround(im * f), nl, lo, hi);
+            o = alloc_ct(c.level, c.npoly);
+            o.pend = c.pend + 1;
+            o.lazy = true;
+            launch_mul_const_half(st_, T_, o.data, c.data, const_half(lo, hi), c.npoly * nl, nl, qmap());
+        } else {
+            Ct nc = normalize(c, false);
+            const int nl = hp_.nl(nc.level);
+            std::vector<u32> lo, hi;
+            const double sc = hp_.ptscale[nc.level];
+            scalar_residues(std::llround(re * sc), std::llround(im * sc), nl, lo, hi);
+            Ct t = alloc_ct(nc.level, nc.npoly);
+            launch_mul_const_half(st_, T_, t.data, nc.data, const_half(lo, hi), nc.npoly * nl, nl, qmap());
+            o = rescale(t);
+            o.lazy = c_in.lazy && o.npoly == 3;
+            release(t);
+            if (nc.data != c.data) release(nc);
+        }
+        if (own) release(c);
         return o;
     }
 
-    // plaintext encoded at `level`, NTT form, cached on the plaintext; multiplicative operands
-    // use ptscale[level] (the product rescales onto delta[level-1]), additive ones delta[level]
-    u32* pt_at(Pt& p, int level, bool mult) {
-        const int key = 2 * level + (mult ? 1 : 0);
+    // plaintext encoded on nl(level) limbs, NTT form, cached on the plaintext.  kind 0:
+    // additive (delta_level); 1: multiplicative, ptscale[level] (the product rescales onto
+    // delta_{level-1}); 2: multiplicative on a tensor owing one rescale, ptscale[level-1]
+    u32* pt_at(Pt& p, int level, int kind) {
+        const int key = 4 * level + kind;
         auto it = p.enc.find(key);
         if (it != p.enc.end()) return it->second.first;
         std::vector<u32> host;
         const int nl = hp_.nl(level);
-        encode_host(p.re.data(), p.im.data(), mult ? hp_.ptscale[level] : hp_.delta[level], nl, host);
+        const double sc = kind == 0 ? hp_.delta[level] : kind == 1 ? hp_.ptscale[level] : hp_.ptscale[level - 1];
+        encode_host(p.re.data(), p.im.data(), sc, nl, host);
         u32* d = upload_ntt(host, nl);
         p.enc[key] = {d, (size_t)nl * hp_.n};
         return d;
     }
 
-    Ct mul_pt(const Ct& c_in, aesfhe_handle hp) {
+    Ct mul_pt(const Ct& c_in, aesfhe_handle hp, bool allow_lazy = false) {
         Pt& p = pt(hp);
-        if (p.constant) return mul_scalar(c_in, p.re[0], p.im[0]);
-        if (c_in.level < 1) throw std::runtime_error("not enough level to multiply by a plaintext (level 0)");
-        Ct c = ensure_ntt(c_in);
-        const int nl = hp_.nl(c.level);
-        u32* e = pt_at(p, c.level, true);
-        Ct t = alloc_ct(c.level, c.npoly);
-        launch_mul_poly(st_, T_, t.data, c.data, e, c.npoly, nl, qmap());
-        Ct o = rescale(t);
-        release(t);
-        if (c.data != c_in.data) release(c);
+        if (p.constant) return mul_scalar(c_in, p.re[0], p.im[0], allow_lazy);
+        if (c_in.level - c_in.pend < 1) throw std::runtime_error("not enough level to multiply by a plaintext (level 0)");
         cnt_[C_PTMUL]++;
+        if (c_in.zero) return zero_ct(c_in.level - c_in.pend - 1);
+        bool own;
+        Ct c = upto_one_pend(c_in, own);
+        Ct o;
+        if (allow_lazy && headroom(c.level, c.pend + 1, 1.0)) {
+            const int nl = hp_.nl(c.level);
+            u32* e = pt_at(p, c.level, 1 + c.pend);
+            o = alloc_ct(c.level, c.npoly);
+            o.pend = c.pend + 1;
+            o.lazy = true;
+            launch_mul_poly(st_, T_, o.data, c.data, e, c.npoly, nl, qmap());
+        } else {
+            Ct nc = normalize(c, false);
+            const int nl = hp_.nl(nc.level);
+            u32* e = pt_at(p, nc.level, 1);
+            Ct t = alloc_ct(nc.level, nc.npoly);
+            launch_mul_poly(st_, T_, t.data, nc.data, e, nc.npoly, nl, qmap());
+            o = rescale(t);
+            o.lazy = c_in.lazy && o.npoly == 3;
+            release(t);
+            if (nc.data != c.data) release(nc);
+        }
+        if (own) release(c);
         return o;
     }
 
     Ct add_pt(const Ct& c_in, aesfhe_handle hp) {
         Pt& p = pt(hp);
         if (p.constant) return add_scalar(c_in, p.re[0], p.im[0]);
-        Ct c = ensure_ntt(c_in);
+        Ct c = normalize(c_in, false);
         const int nl = hp_.nl(c.level);
-        u32* e = pt_at(p, c.level, false);
+        u32* e = pt_at(p, c.level, 0);
         Ct o = copy(c);
+        o.zero = false;
+        o.lazy = c_in.lazy && o.npoly == 3;
         launch_add(st_, T_, o.data, c.data, e, nl, nl, qmap());
         if (c.data != c_in.data) release(c);
         return o;
@@ -723,46 +938,53 @@ public:
         return o;
     }
 
-    Ct mul(const Ct& a, const Ct& b, bool relin) {
-        if (a.npoly != 2 || b.npoly != 2) throw std::runtime_error("multiply expects 2-polynomial ciphertexts");
-        if (a.level < 1 || b.level < 1) throw std::runtime_error("not enough level to multiply (level 0)");
+    // ct x ct.  Inputs are brought to canonical form; the tensor owes one rescale.  relin:
+    // key switch now (eager) or leave it to the first consumer that needs two polynomials
+    // (lazy)
+    Ct mul(const Ct& a_in, const Ct& b_in, bool relin, bool lazy = false) {
+        if (vis_npoly(a_in) != 2 || vis_npoly(b_in) != 2) throw std::runtime_error("multiply expects 2-polynomial ciphertexts");
+        if (a_in.level - a_in.pend < 1 || b_in.level - b_in.pend < 1)
+            throw std::runtime_error("not enough level to multiply (level 0)");
+        Ct a = normalize(a_in);
+        Ct b = b_in.data == a_in.data ? a : normalize(b_in);
+        const bool oa = a.data != a_in.data, ob = b.data != b_in.data && b.data != a.data;
         bool fa, fb;
         auto xy = align(a, b, fa, fb, true);
         const Ct &x = xy.first, &y = xy.second;
-        const int nl = hp_.nl(x.level), n = hp_.n;
+        const int nl = hp_.nl(x.level);
         Ct d = alloc_ct(x.level, 3);
+        d.pend = 1;
         launch_tensor(st_, T_, d.data, x.data, y.data, nl, qmap());
         if (fa) release(x);
-        if (fb) release(y);
+        if (fb && y.data != x.data) release(y);
+        if (oa) release(a);
+        if (ob) release(b);
         cnt_[C_MUL]++;
-        if (!relin) {
-            d.pending = true;
+        if (!relin) return d;
+        if (lazy) {
+            d.lazy = true;
             return d;
         }
-        Ct r = keyswitch(d.data + (size_t)2 * nl * n, d.level, ksk(0), d.data, d.data + (size_t)nl * n);
+        Ct r = relin_raw(d);
         release(d);
-        cnt_[C_RELIN]++;
         Ct o = rescale(r);
         release(r);
         return o;
     }
 
     Ct relinearize(const Ct& c_in) {
-        if (c_in.npoly != 3) throw std::runtime_error("relinearize: ciphertext should have 3 polynomials");
-        Ct c = ensure_ntt(c_in, false);
-        const int nl = hp_.nl(c.level), n = hp_.n;
-        Ct r = keyswitch(c.data + (size_t)2 * nl * n, c.level, ksk(0), c.data, c.data + (size_t)nl * n);
+        if (vis_npoly(c_in) != 3) throw std::runtime_error("relinearize: ciphertext should have 3 polynomials");
+        Ct c = ensure_ntt(c_in);
+        Ct r = relin_raw(c);
         if (c.data != c_in.data) release(c);
-        cnt_[C_RELIN]++;
-        if (!c_in.pending) return r;
-        Ct o = rescale(r);
-        release(r);
+        Ct o = normalize(r, true);
+        if (o.data != r.data) release(r);
         return o;
     }
 
     Ct galois(const Ct& c_in, u64 g) {
-        if (c_in.npoly != 2) throw std::runtime_error("rotation/conjugation expects a 2-polynomial ciphertext");
-        Ct c = ensure_ntt(c_in);
+        if (vis_npoly(c_in) != 2) throw std::runtime_error("rotation/conjugation expects a 2-polynomial ciphertext");
+        Ct c = normalize(c_in);
         const int nl = hp_.nl(c.level), n = hp_.n;
         const u32* key = ksk(g);
         u32* perm = tmp(2 * (size_t)nl);
@@ -785,7 +1007,8 @@ public:
 
     // x^k at depth ceil(log2 k): x^(2^i) by squaring, x^k = x^(2^t) x^(k - 2^t)
     void power_basis(aesfhe_handle h, int degree, aesfhe_handle* out) {
-        const Ct& x = ct(h);
+        const Ct& x = canon(h);
+        if (x.npoly != 2) throw std::runtime_error("make_power_basis expects a 2-polynomial ciphertext");
         if (degree < 1) throw std::runtime_error("power basis degree must be >= 1");
         int depth = 0;
         while ((1 << depth) < degree) ++depth;
@@ -810,8 +1033,7 @@ public:
         int nib[2][16];
         aesfhe_handle in[2] = {hh, hl};
         for (int w = 0; w < 2; ++w) {
-            const int level = decrypt_coeffs(ct(in[w]), m);
-            const double inv = 1.0 / hp_.delta[level];
+            const double inv = 1.0 / decrypt_coeffs(ct(in[w]), m);
             for (int k = 0; k < n; ++k) m[k] *= inv;
             emb_.forward(m.data(), re.data(), im.data());
             for (int i = 0; i < 16; ++i) {
@@ -1050,10 +1272,10 @@ public:
     // 6 real part, 7 imaginary part, 8 EvalMod(real), 9 EvalMod(imag), 10 recombined, 11 output
     Ct bootstrap(const Ct& in, int stop_after = 99) {
         boot_setup();
-        if (in.npoly != 2) throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
+        if (vis_npoly(in) != 2) throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
         const int n = hp_.n, top = bs_.top;
         // 1. level 0, then scale delta_0 -> s_bt and drop q1: a single-limb ciphertext mod q0
-        Ct c = ensure_ntt(in);
+        Ct c = normalize(in);
         Ct z = level_down(c, 0);
         if (c.data != in.data) release(c);
         std::vector<u32> r(2);
@@ -1114,8 +1336,8 @@ public:
 
     // ------------------------------------------------------------------ raw access
     void export_ct(aesfhe_handle h, u32* out, u64 words) {
-        const Ct& c0 = ct(h);
-        Ct c = ensure_ntt(c0, false);
+        const Ct& c0 = canon(h);
+        Ct c = ensure_ntt(c0);
         if (words < c.words) throw std::runtime_error("export buffer too small");
         HIP_OK(hipMemcpyAsync(out, c.data, c.words * sizeof(u32), hipMemcpyDeviceToHost, st_));
         HIP_OK(hipStreamSynchronize(st_));
@@ -1198,6 +1420,8 @@ public:
         return 1000.0 * ms / iters;
     }
     u64 counter(int i) const { return i < C_N ? cnt_[i] : 0; }
+    bool lazy() const { return lazy_; }
+    void set_lazy(bool on) { lazy_ = on; }
     void reset_counters() { std::memset(cnt_, 0, sizeof(cnt_)); }
 
 private:
@@ -1381,6 +1605,7 @@ private:
     u32* d_pinv_ = nullptr;
     u32* d_negp_ = nullptr;
     u64 cnt_[C_N] = {};
+    bool lazy_ = true;  // defer relinearisation / rescales of API-level products
 
 public:
     KernelProfiler prof_;
@@ -1485,8 +1710,10 @@ int aesfhe_free(aesfhe_ctx* ctx, aesfhe_handle h) {
 }
 int aesfhe_level(aesfhe_ctx* ctx, aesfhe_handle h, int32_t* level, int32_t* npoly) {
     API_BEGIN const Ct& c = ctx->eng->ct(h);
-    *level = c.level;
-    *npoly = c.npoly;
+    // deferred work is invisible: a lazy tensor shows its logical level and 2 polynomials;
+    // an explicitly unrelinearised product shows its data level and 3 polynomials
+    *level = c.lazy ? c.level - c.pend : c.level;
+    *npoly = c.lazy ? 2 : c.npoly;
     API_END
 }
 int aesfhe_plaintext(aesfhe_ctx* ctx, const double* re, const double* im, int n, aesfhe_handle* out) {
@@ -1519,35 +1746,40 @@ int aesfhe_add_scalar(aesfhe_ctx* ctx, aesfhe_handle c, double re, double im, ae
     CT_OP(e.add_scalar(e.ct(c), re, im))
 }
 int aesfhe_mul_scalar(aesfhe_ctx* ctx, aesfhe_handle c, double re, double im, aesfhe_handle* out) {
-    CT_OP(e.mul_scalar(e.ct(c), re, im))
+    CT_OP(e.mul_scalar(e.ct(c), re, im, e.lazy()))
 }
-int aesfhe_mul_pt(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle p, aesfhe_handle* out) { CT_OP(e.mul_pt(e.ct(c), p)) }
+int aesfhe_mul_pt(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle p, aesfhe_handle* out) { CT_OP(e.mul_pt(e.ct(c), p, e.lazy())) }
 int aesfhe_mul(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int relin, aesfhe_handle* out) {
-    CT_OP(e.mul(e.ct(a), e.ct(b), relin != 0))
+    CT_OP(e.mul(e.canon(a), e.canon(b), relin != 0, e.lazy()))
+}
+int aesfhe_set_lazy(aesfhe_ctx* ctx, int on) {
+    API_BEGIN ctx->eng->set_lazy(on != 0);
+    API_END
 }
 int aesfhe_relinearize(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.relinearize(e.ct(c))) }
 int aesfhe_rescale(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) {
     API_BEGIN Engine& e = *ctx->eng;
-    Ct x = e.ensure_ntt(e.ct(c));
+    const Ct& c0 = e.canon(c);
+    Ct x = e.normalize(c0, false);
     Ct o = e.rescale(x);
-    if (x.data != e.ct(c).data) e.release(x);
+    if (x.data != c0.data) e.release(x);
     *out = e.put_ct(o);
     API_END
 }
-int aesfhe_level_down(aesfhe_ctx* ctx, aesfhe_handle c, int level, aesfhe_handle* out) { CT_OP(e.level_down(e.ct(c), level)) }
-int aesfhe_rotate(aesfhe_ctx* ctx, aesfhe_handle c, int steps, aesfhe_handle* out) { CT_OP(e.rotate(e.ct(c), steps)) }
-int aesfhe_conjugate(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.conjugate(e.ct(c))) }
+int aesfhe_level_down(aesfhe_ctx* ctx, aesfhe_handle c, int level, aesfhe_handle* out) { CT_OP(e.level_down(e.canon(c), level)) }
+int aesfhe_rotate(aesfhe_ctx* ctx, aesfhe_handle c, int steps, aesfhe_handle* out) { CT_OP(e.rotate(e.canon(c), steps)) }
+int aesfhe_conjugate(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.conjugate(e.canon(c))) }
 int aesfhe_power_basis(aesfhe_ctx* ctx, aesfhe_handle c, int degree, aesfhe_handle* out) {
     API_BEGIN ctx->eng->power_basis(c, degree, out);
     API_END
 }
-int aesfhe_to_ntt(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.to_ntt(e.ct(c))) }
-int aesfhe_to_intt(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.to_intt(e.ct(c))) }
-int aesfhe_bootstrap(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.bootstrap(e.ct(c))) }
+int aesfhe_to_ntt(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.to_ntt(e.canon(c))) }
+int aesfhe_to_intt(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.to_intt(e.canon(c))) }
+int aesfhe_bootstrap(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.bootstrap(e.canon(c))) }
 int aesfhe_bootstrap_depth(void) { return Engine::boot_depth(); }
-int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle c, int stage, aesfhe_handle* out) { CT_OP(e.bootstrap(e.ct(c), stage)) }
+int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle c, int stage, aesfhe_handle* out) { CT_OP(e.bootstrap(e.canon(c), stage)) }
 int aesfhe_debug_lin_group(aesfhe_ctx* ctx, aesfhe_handle c, int which, aesfhe_handle* out) {
-    CT_OP(e.debug_lin_group(e.ct(c), which))
+    CT_OP(e.debug_lin_group(e.canon(c), which))
 }
 int aesfhe_export_sparse(aesfhe_ctx* ctx, uint32_t* out) {
     API_BEGIN Engine& e = *ctx->eng;

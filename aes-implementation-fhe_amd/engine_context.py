@@ -4,7 +4,7 @@ the MI355X engine (mi355x_ckks, a ctypes binding of libaesfhe.so).
 Same constructor keywords, same methods, same error-string behaviour; the AES round
 modules only ever talk to this object.  Extra keywords: ``log_n`` (N = 2^log_n, default
 2^16 as in the reference harness; config 1 of BASELINE.json uses 2^15), ``dnum`` and
-``seed`` (deterministic key material).
+``seed`` (deterministic key material) and ``lazy`` (deferred relinearisation).
 """
 from __future__ import annotations
 
@@ -20,7 +20,8 @@ _SIG_DEFAULT_LEVEL = 17
 class EngineContext:
     def __init__(self, signature: int, *, max_level: int = 17, use_bootstrap: bool = True,
                  use_multiparty: bool = False, mode: str = "cpu", device_id: int = 0,
-                 thread_count: int | None = None, log_n: int = 16, dnum: int | None = None, seed: int = 0x5EED):
+                 thread_count: int | None = None, log_n: int = 16, dnum: int | None = None, seed: int = 0x5EED,
+                 lazy: bool = True):
         # REF/engine_context.py:17-42: signature selects the engine constructor form
         if signature == 1:
             kw = dict(use_bootstrap=use_bootstrap, max_level=_SIG_DEFAULT_LEVEL)
@@ -32,7 +33,7 @@ class EngineContext:
             raise ValueError(f"Unsupported signature: {signature}")
         self.signature = signature
         self.engine = Engine(mode=mode, use_multiparty=use_multiparty, thread_count=thread_count or 0,
-                             device_id=device_id, log_n=log_n, dnum=dnum, seed=seed, **kw)
+                             device_id=device_id, log_n=log_n, dnum=dnum, seed=seed, lazy=lazy, **kw)
         eng = self.engine
         # REF/engine_context.py:44-50
         self.secret_key = eng.create_secret_key()

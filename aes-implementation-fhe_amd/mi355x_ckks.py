@@ -34,7 +34,7 @@ EXPORTED = [
     "aesfhe_relinearize", "aesfhe_rescale", "aesfhe_level_down", "aesfhe_rotate", "aesfhe_conjugate",
     "aesfhe_power_basis", "aesfhe_to_ntt", "aesfhe_to_intt", "aesfhe_bootstrap", "aesfhe_renorm_pair",
     "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
-    "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_bench_op",
+    "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
     "aesfhe_profile", "aesfhe_kernel_stats", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan",
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group",
@@ -86,6 +86,7 @@ def load_library(path: Optional[Path] = None):
         "aesfhe_debug_keyswitch": [vp, c_int, ctypes.c_uint64, _up, _up],
         "aesfhe_counters": [vp, np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS"), c_int],
         "aesfhe_bench_op": [vp, c_int, c_int, c_int, ctypes.POINTER(c_dbl)],
+        "aesfhe_set_lazy": [vp, c_int],
         "aesfhe_reset_counters": [vp],
         "aesfhe_profile": [vp, ctypes.c_uint32],
         "aesfhe_kernel_stats": [vp, _dp, c_int, c_int],
@@ -227,7 +228,7 @@ class Engine:
 
     def __init__(self, *, mode: str = "gpu", use_bootstrap: bool = False, use_multiparty: bool = False,
                  thread_count: int = 0, device_id: int = 0, max_level: int = 17, log_n: int = 16,
-                 dnum: int | None = None, seed: int = 0x5EED):
+                 dnum: int | None = None, seed: int = 0x5EED, lazy: bool = True):
         if use_multiparty:
             raise ValueError("multiparty key generation is not supported")
         self.mode = mode
@@ -248,6 +249,12 @@ class Engine:
         self._ctx.check(L.aesfhe_level_limbs(self._ctx.ptr, limbs))
         self.level_limbs = [int(x) for x in limbs]
         self._keys_ready = False
+        self.set_lazy(lazy)
+
+    def set_lazy(self, on: bool):
+        """Deferred relinearisation / rescale of products; False = eager."""
+        self.lazy = bool(on)
+        self._ctx.check(self._ctx.lib.aesfhe_set_lazy(self._ctx.ptr, int(self.lazy)))
 
     # ------------------------------------------------------------------ internals
     @property

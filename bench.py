@@ -43,6 +43,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-final-bootstrap", action="store_true",
                     help="diagnostic only: skip MixColFinal's final bootstrap (not the benchmark workload)")
+    ap.add_argument("--eager", action="store_true", help="relinearise and rescale after every product (no deferred evaluation)")
     ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r1_pmc_traffic.json"), help="per-launch HBM bytes from a rocprofv3 PMC pass")
     return ap.parse_args()
 
@@ -143,7 +144,7 @@ def main():
 
     coeffs = load_all_coeffs()
     signature = 2 if args.no_final_bootstrap else 1
-    ctx = EngineContext(signature=signature, max_level=17, thread_count=1, device_id=local, seed=0x5EED + rank)
+    ctx = EngineContext(signature=signature, max_level=17, thread_count=1, device_id=local, seed=0x5EED + rank, lazy=not args.eager)
     xor4 = XOR4LUT(ctx, coeffs["xor4"])
     mix = MixColFinal(ctx, xor4)
     if args.no_final_bootstrap:
@@ -208,6 +209,8 @@ def main():
         "config": {"workload": "C2: full AES-128 encrypt (10 rounds), 1 packed state per ciphertext pair, "
                                "N=2^16, renorm on" + ("" if not args.no_final_bootstrap else ", FINAL BOOTSTRAP SKIPPED"),
                    "log_n": 16, "states_per_rank_per_step": 1, "parallelism": f"replicas x{world}",
+                   "evaluation": "eager (relinearise + rescale after every product)" if args.eager else
+                   "deferred relinearisation/rescale of products (DESIGN.md 3.7); module call sequence unchanged",
                    "blocks_per_s": states_done / elapsed, "verified_against_plaintext_model": bool(ok)},
         "roofline": {"kernel": args.kernel, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

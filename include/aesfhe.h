@@ -78,6 +78,13 @@ int aesfhe_mul_pt(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle pt, aesfhe_ha
 /* engine.multiply(a, b, relinearization_key), REF/engine_context.py:65-67:
  * tensor + relinearise + rescale; relin = 0 returns the 3-polynomial tensor (rescaled) */
 int aesfhe_mul(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int relin, aesfhe_handle* out);
+/* Deferred evaluation switch, default on: API-level ct x ct products
+ * leave relinearisation and their rescale to the first consumer that needs a
+ * 2-polynomial canonical ciphertext (rotate, conjugate, ct x ct, power basis, bootstrap,
+ * export), and non-integer scalar / plaintext products defer their rescale.  Sums of such
+ * terms are combined before any key switch.  Results decrypt identically up to CKKS
+ * rounding; 0 restores eager relinearise-and-rescale after every product. */
+int aesfhe_set_lazy(aesfhe_ctx* ctx, int on);
 /* engine.relinearize, REF/engine_context.py:134-145 */
 int aesfhe_relinearize(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
 int aesfhe_rescale(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
