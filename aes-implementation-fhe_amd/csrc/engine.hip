@@ -294,12 +294,18 @@ public:
         std::vector<double> m(n);
         emb_.inverse(re, im, m.data());
         out.assign((size_t)nl * n, 0);
+        // residues of the integer-valued double x = round(m_k scale): with k = floor(x / q)
+        // the remainder fma(-q, k, x) is exact (it is small), one correction step fixes the
+        // quotient's rounding; identical to the 128-bit integer reduction, ~20x cheaper
+        std::vector<double> qd(nl), qinv(nl);
+        for (int t = 0; t < nl; ++t) qd[t] = (double)hp_.mod[t], qinv[t] = 1.0 / qd[t];
         for (int k = 0; k < n; ++k) {
-            const double x = m[k] * scale;
-            __int128 v = std::fabs(x) < 4503599627370496.0 ? (__int128)std::llround(x) : (__int128)x;
+            const double y = m[k] * scale;
+            const double x = std::fabs(y) < 4503599627370496.0 ? (double)std::llround(y) : y;
             for (int t = 0; t < nl; ++t) {
-                __int128 r = v % (__int128)hp_.mod[t];
-                if (r < 0) r += hp_.mod[t];
+                double r = std::fma(-qd[t], std::floor(x * qinv[t]), x);
+                if (r < 0) r += qd[t];
+                if (r >= qd[t]) r -= qd[t];
                 out[(size_t)t * n + k] = (u32)r;
             }
         }
@@ -315,11 +321,19 @@ public:
     aesfhe_handle encrypt(const double* re, const double* im) {
         if (!d_pk_) throw std::runtime_error("keys not generated");
         // encode at delta_f * q_{f+2} on limbs 0..f+2, encrypt at level f+1, rescale to f
-        const int n = hp_.n, f = hp_.fresh, nq = hp_.nl(f) + 1;
-        const int L = f;
+        const int f = hp_.fresh, nq = hp_.nl(f) + 1;
         std::vector<u32> host;
         encode_host(re, im, hp_.delta[f] * (double)hp_.mod[hp_.nl(f)], nq, host);
         u32* m = upload_ntt(host, nq);
+        Ct out = encrypt_ntt(m);
+        untmp(m, nq);
+        return put_ct(out);
+    }
+    // public-key encryption of an encoded message m (NTT form on nl(f) + 1 limbs, scale
+    // delta_f q_{nl(f)}): c = (v pk0 + e0 + m, v pk1 + e1) at level f + 1, rescaled to f
+    Ct encrypt_ntt(const u32* m) {
+        const int n = hp_.n, f = hp_.fresh, nq = hp_.nl(f) + 1;
+        const int L = f;
         u32* v = tmp(nq);
         u32* e = tmp(2 * nq);
         const u64 ctr = enc_ctr_++;
@@ -332,13 +346,12 @@ public:
         launch_add(st_, T_, e, e, m, nq, nq, qmap());  // e0 + m
         launch_fma_poly(st_, T_, top.data, e, d_pk_, v, nq, nq, qmap());
         launch_fma_poly(st_, T_, top.data + (size_t)nq * n, e + (size_t)nq * n, d_pk_ + (size_t)hp_.n_q * n, v, nq, nq, qmap());
-        untmp(m, nq);
         untmp(v, nq);
         untmp(e, 2 * nq);
         Ct out = rescale(top);
         release(top);
         cnt_[C_ENC]++;
-        return put_ct(out);
+        return out;
     }
 
     // decryption to real coefficients (message * delta_level)
@@ -1026,35 +1039,101 @@ public:
         for (int k = 1; k <= degree; ++k) out[k - 1] = pw[k];
     }
 
-    // secret-key Zeta16 renorm of a state pair (REF/pipeline.py:65-69, REF/state_encoder.py:17-38)
+    // CRT limbs (2..4) covering raw_scale * 2^26, or 0 when 4 are not enough
+    int crt_limbs(const Ct& c) const {
+        const int nl = hp_.nl(c.level);
+        const double need = c.level >= 0 ? std::log2(raw_scale(c.level, c.pend)) + 26.0 : 0.0;
+        int kd = std::min(2, nl);
+        double have = 0.0;
+        for (int i = 0; i < kd; ++i) have += std::log2((double)hp_.mod[i]);
+        while (have < need && kd < std::min(4, nl)) have += std::log2((double)hp_.mod[kd++]);
+        return have >= need ? kd : 0;
+    }
+    const CrtConsts& crt_consts(int kd) {
+        CrtConsts& cc = crt_[kd - 1];
+        if (cc.q[0]) return cc;
+        double P = 1.0;
+        for (int i = 0; i < kd; ++i) {
+            const u32 qi = hp_.mod[i];
+            cc.q[i] = qi;
+            cc.pd[i] = P;
+            u64 pm = 1;
+            for (int j = 0; j < i; ++j) {
+                cc.p_mod[i][j] = (u32)pm;
+                pm = pm * (hp_.mod[j] % qi) % qi;
+            }
+            cc.minv[i] = i ? hinvm((u32)pm, qi) : 1;
+            P *= (double)qi;
+        }
+        return cc;
+    }
+    // s^2 on the first four limbs (NTT form), for decrypting deferred 3-polynomial tensors
+    const u32* s_sq4() {
+        if (!d_s2_) {
+            d_s2_ = dev_alloc((size_t)4 * hp_.n);
+            launch_square(st_, T_, d_s2_, d_s_, std::min(4, hp_.n_tot()), 4, qmap());
+        }
+        return d_s2_;
+    }
+
+    // secret-key Zeta16 renorm of a state pair (REF/pipeline.py:65-69, REF/state_encoder.py:17-38),
+    // entirely on the device: raw decryption of both tensors on 2..4 limbs, mixed-radix CRT,
+    // the 16 state slots evaluated directly, snap to the nearest zeta16 power, closed-form
+    // re-encoding (every other slot 1) and fresh encryption -- no host round trip
     void renorm_pair(aesfhe_handle hh, aesfhe_handle hl, aesfhe_handle* oh, aesfhe_handle* ol) {
-        const int s = slot_count(), stride = s / 16, n = hp_.n;
-        std::vector<double> re(s), im(s), m;
-        int nib[2][16];
-        aesfhe_handle in[2] = {hh, hl};
-        for (int w = 0; w < 2; ++w) {
-            const double inv = 1.0 / decrypt_coeffs(ct(in[w]), m);
-            for (int k = 0; k < n; ++k) m[k] *= inv;
-            emb_.forward(m.data(), re.data(), im.data());
-            for (int i = 0; i < 16; ++i) {
-                const double ang = std::atan2(im[(size_t)i * stride], re[(size_t)i * stride]);
-                const double k = std::nearbyint(-ang * 16.0 / (2.0 * M_PI));
-                nib[w][i] = (int)(((long)k % 16 + 16) % 16);
+        if (!d_pk_) throw std::runtime_error("keys not generated");
+        const int n = hp_.n, s = slot_count(), stride = s / 16;
+        if (slots_.e[1] == 0) {
+            const u64 two_n = 2ull * n;
+            u64 e = 1;
+            for (int j = 0; j < s; ++j) {
+                if (j % stride == 0) slots_.e[j / stride] = (u32)e;
+                e = e * 5 % two_n;
             }
+            d_codec_ = (double*)dev_alloc(2 * 64 * 2);  // acc[64] + w[64] doubles
+            d_nib_ = (int*)dev_alloc(32);
         }
-        aesfhe_handle outs[2];
+        u32* x = tmp(8);  // [2][4][N]
+        int kd[2];
+        CrtConsts cc[2];
+        double isc[2];
+        const aesfhe_handle in[2] = {hh, hl};
         for (int w = 0; w < 2; ++w) {
-            std::fill(re.begin(), re.end(), 1.0);
-            std::fill(im.begin(), im.end(), 0.0);
-            for (int i = 0; i < 16; ++i) {
-                const double a = -2.0 * M_PI * nib[w][i] / 16.0;
-                re[(size_t)i * stride] = std::cos(a);
-                im[(size_t)i * stride] = std::sin(a);
+            Ct c = ensure_ntt(ct(in[w]));
+            bool own = c.data != ct(in[w]).data;
+            kd[w] = crt_limbs(c);
+            if (!kd[w]) {
+                Ct nc = normalize(c, true);
+                if (own) release(c);
+                c = nc, own = nc.data != ct(in[w]).data;
+                kd[w] = crt_limbs(c);
             }
-            outs[w] = encrypt(re.data(), im.data());
+            const int nl = hp_.nl(c.level);
+            u32* xw = x + (size_t)w * 4 * n;
+            HIP_OK(hipMemcpyAsync(xw, c.data, sizeof(u32) * kd[w] * n, hipMemcpyDeviceToDevice, st_));
+            for (int p = 1; p < c.npoly; ++p)
+                launch_fma_poly(st_, T_, xw, xw, c.data + (size_t)p * nl * n, p == 2 ? s_sq4() : d_s_, kd[w], kd[w], qmap());
+            intt(xw, kd[w], kd[w], qmap());
+            cc[w] = crt_consts(kd[w]);
+            isc[w] = 1.0 / (c.level >= 0 ? raw_scale(c.level, c.pend) : 1.0);
+            if (own) release(c);
+            cnt_[C_DEC]++;
         }
-        *oh = outs[0];
-        *ol = outs[1];
+        double* acc = d_codec_;
+        double* wv = d_codec_ + 64;
+        HIP_OK(hipMemsetAsync(acc, 0, 64 * sizeof(double), st_));
+        launch_decode16(st_, T_, x, kd, cc, slots_, isc, acc);
+        launch_snap16(st_, acc, wv, d_nib_);
+        const int f = hp_.fresh, nq = hp_.nl(f) + 1;
+        u32* m = tmp(2 * (size_t)nq);
+        launch_encode16(st_, T_, m, wv, slots_, hp_.delta[f] * (double)hp_.mod[hp_.nl(f)], nq);
+        ntt(m, 2 * nq, nq, qmap());
+        Ct a = encrypt_ntt(m);
+        Ct b = encrypt_ntt(m + (size_t)nq * n);
+        untmp(m, 2 * (size_t)nq);
+        untmp(x, 8);
+        *oh = put_ct(a);
+        *ol = put_ct(b);
     }
 
     // ------------------------------------------------------------------ bootstrapping
@@ -1605,6 +1684,11 @@ private:
     u32* d_pinv_ = nullptr;
     u32* d_negp_ = nullptr;
     u64 cnt_[C_N] = {};
+    CrtConsts crt_[4] = {};
+    Slot16 slots_ = {};
+    double* d_codec_ = nullptr;
+    int* d_nib_ = nullptr;
+    u32* d_s2_ = nullptr;
     bool lazy_ = true;  // defer relinearisation / rescales of API-level products
 
 public:

@@ -139,3 +139,24 @@ void launch_keygen_combine(hipStream_t st, const DevTables& T, u32* b, const u32
                            const u32* gadget, int nl, LimbMap map, int gadget_lo, int gadget_hi);
 // out = a*a (dyadic square)
 void launch_square(hipStream_t st, const DevTables& T, u32* out, const u32* a, int rows, int nl, LimbMap map);
+
+// --- device Zeta16 renorm codec (REF/pipeline.py:65-69, REF/state_encoder.py:17-38) ----
+// mixed-radix CRT constants for up to 4 limbs: p_mod[i][j] = (q_0 ... q_{j-1}) mod q_i,
+// minv[i] = (q_0 ... q_{i-1})^{-1} mod q_i, pd[i] = q_0 ... q_{i-1} as a double
+struct CrtConsts {
+    u32 q[4], minv[4], p_mod[4][4];
+    double pd[4];
+};
+// the 16 state slots i * stride: evaluation exponents e_i = 5^(i stride) mod 2N
+struct Slot16 {
+    u32 e[16];
+};
+// x: [2][4][N] coefficient residues of the two decryptions (kd[c] limbs used);
+// acc[c][i][re|im] += sum_k (m_k / scale_c) e^{i pi e_i k / N}   (acc zeroed by the caller)
+void launch_decode16(hipStream_t st, const DevTables& T, const u32* x, const int kd[2], const CrtConsts cc[2], const Slot16& sl,
+                     const double inv_scale[2], double* acc);
+// per slot: nibble = round(-angle 16 / 2 pi) mod 16, w = zeta16^nibble - 1 (acc -> w, nib)
+void launch_snap16(hipStream_t st, const double* acc, double* w, int* nib);
+// out[c][t][k] = round(scale (delta_{k0} + (2/N) Re sum_i w_ci e^{-i pi e_i k / N})) mod q_t, t < nq
+void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq);
+

@@ -251,6 +251,96 @@ void KernelProfiler::reset() {
 }
 
 namespace {
+// ------------------------------------------------------------------------------------
+// device Zeta16 renorm codec
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ double crt_centered(const u32* r, int kd, const CrtConsts& cc) {
+    u32 a[4];
+    a[0] = r[0];
+    for (int i = 1; i < kd; ++i) {
+        const u32 qi = cc.q[i];
+        u64 v = 0;
+        for (int j = 0; j < i; ++j) v += (u64)a[j] * cc.p_mod[i][j];  // < 3 * 2^62
+        const u32 vm = (u32)(v % qi);
+        const u32 d = r[i] >= vm ? r[i] - vm : r[i] + qi - vm;
+        a[i] = (u32)((u64)d * cc.minv[i] % qi);
+    }
+    // negative iff the top digit is in the upper half (|m| << Q, so never near Q/2)
+    if (a[kd - 1] >= (cc.q[kd - 1] >> 1)) {
+        double s = 1.0;  // Q - v = sum (q_i - 1 - a_i) P_i + 1
+        for (int i = 0; i < kd; ++i) s += (double)(cc.q[i] - 1 - a[i]) * cc.pd[i];
+        return -s;
+    }
+    double s = 0.0;
+    for (int i = 0; i < kd; ++i) s += (double)a[i] * cc.pd[i];
+    return s;
+}
+
+__global__ void __launch_bounds__(kBlock) k_decode16(const u32* x, int kd0, int kd1, CrtConsts cc0, CrtConsts cc1, Slot16 sl,
+                                                     double is0, double is1, double* acc, int logn) {
+    const int c = blockIdx.y;
+    const int n = 1 << logn;
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    const int kd = c ? kd1 : kd0;
+    u32 r[4];
+    for (int i = 0; i < kd; ++i) r[i] = x[((size_t)(c * 4 + i) << logn) + k];
+    const double m = crt_centered(r, kd, c ? cc1 : cc0) * (c ? is1 : is0);
+    __shared__ double red[kBlock / 64][32];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const u32 mask = 2u * n - 1;
+    const double inv_n = 1.0 / n;
+    for (int i = 0; i < 16; ++i) {
+        double sn, cs;
+        sincospi((double)((sl.e[i] * (u32)k) & mask) * inv_n, &sn, &cs);
+        double vr = m * cs, vi = m * sn;
+        for (int o = 32; o > 0; o >>= 1) vr += __shfl_down(vr, o, 64), vi += __shfl_down(vi, o, 64);
+        if (lane == 0) red[wv][2 * i] = vr, red[wv][2 * i + 1] = vi;
+    }
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        double t = 0.0;
+        for (int w = 0; w < kBlock / 64; ++w) t += red[w][threadIdx.x];
+        atomicAdd(acc + c * 32 + threadIdx.x, t);
+    }
+}
+
+__global__ void k_snap16(const double* acc, double* w, int* nib) {
+    const int t = threadIdx.x;  // 32 = 2 ciphertexts x 16 slots
+    if (t >= 32) return;
+    const double ang = atan2(acc[2 * t + 1], acc[2 * t]);
+    const double kf = rint(-ang * 16.0 / (2.0 * M_PI));
+    const int v = (int)((((long)kf) % 16 + 16) % 16);
+    nib[t] = v;
+    double sn, cs;
+    sincospi(-2.0 * v / 16.0, &sn, &cs);
+    w[2 * t] = cs - 1.0;
+    w[2 * t + 1] = sn;
+}
+
+__global__ void __launch_bounds__(kBlock) k_encode16(u32* out, const double* w, Slot16 sl, double scale, int nq, const PrimeConst* pc,
+                                                     int logn) {
+    const int c = blockIdx.y;
+    const int n = 1 << logn;
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    const u32 mask = 2u * n - 1;
+    const double inv_n = 1.0 / n;
+    double v = 0.0;
+    for (int i = 0; i < 16; ++i) {
+        double sn, cs;
+        sincospi((double)((sl.e[i] * (u32)k) & mask) * inv_n, &sn, &cs);
+        v += w[c * 32 + 2 * i] * cs + w[c * 32 + 2 * i + 1] * sn;
+    }
+    v = v * 2.0 * inv_n + (k == 0 ? 1.0 : 0.0);
+    const double x = rint(v * scale);
+    for (int t = 0; t < nq; ++t) {
+        const double q = (double)pc[t].q;
+        double r = fma(-q, floor(x / q), x);
+        if (r < 0) r += q;
+        if (r >= q) r -= q;
+        out[((size_t)(c * nq + t) << logn) + k] = (u32)r;
+    }
+}
+
 inline double words(double w) { return 4.0 * w; }
 }  // namespace
 
@@ -321,3 +411,17 @@ void launch_keygen_combine(hipStream_t st, const DevTables& T, u32* b, const u32
     prof_launch(KID_ELEMENTWISE, EW_BYTES(4.0 * nl), k_keygen_combine, ew_grid(T.logn, nl), dim3(kBlock), 0, st, b, a, s, e, sp, gadget, nl, map, glo, ghi, T.pc,
                        T.logn);
 }
+
+void launch_decode16(hipStream_t st, const DevTables& T, const u32* x, const int kd[2], const CrtConsts cc[2], const Slot16& sl,
+                     const double inv_scale[2], double* acc) {
+    prof_launch(KID_ELEMENTWISE, words((double)(kd[0] + kd[1]) * (1u << T.logn)), k_decode16, dim3((1u << T.logn) / kBlock, 2),
+                dim3(kBlock), 0, st, x, kd[0], kd[1], cc[0], cc[1], sl, inv_scale[0], inv_scale[1], acc, T.logn);
+}
+void launch_snap16(hipStream_t st, const double* acc, double* w, int* nib) {
+    hipLaunchKernelGGL(k_snap16, dim3(1), dim3(64), 0, st, acc, w, nib);
+}
+void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq) {
+    prof_launch(KID_ELEMENTWISE, words(2.0 * nq * (1u << T.logn)), k_encode16, dim3((1u << T.logn) / kBlock, 2), dim3(kBlock), 0, st, out,
+                w, sl, scale, nq, T.pc, T.logn);
+}
+
