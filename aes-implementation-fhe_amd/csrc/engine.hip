@@ -1138,11 +1138,16 @@ public:
 
     // ------------------------------------------------------------------ bootstrapping
     static constexpr int kBootCts = 3, kBootStc = 3, kBootK = 12, kBootR = 3, kBootDeg = 27, kBootMsgBits = 5, kSparseH = 32;
-    static int boot_evalmod_depth() {
-        int cheb = 0;
-        while ((1 << cheb) < kBootDeg) ++cheb;
-        return (cheb + 1) + kBootR;
+    // depth of cheb_eval for a degree-d series: baby T_k at ceil(log2 k), a leaf one more
+    // (its scalar products), giant T_m at log2 m, p = q + T_m r at max(q, 1 + max(T_m, r))
+    static int cheb_depth(int d) {
+        auto clog2 = [](int k) { int e = 0; while ((1 << e) < k) ++e; return e; };
+        if (d <= kBabyDeg) return clog2(std::max(d, 1)) + 1;
+        int m = kBabyDeg;
+        while (2 * m <= d) m *= 2;
+        return std::max(cheb_depth(m - 1), 1 + std::max(clog2(m), cheb_depth(d - m)));
     }
+    static int boot_evalmod_depth() { return cheb_depth(kBootDeg) + kBootR; }
     static int boot_depth() { return kBootCts + boot_evalmod_depth() + kBootStc; }
     // double-prime levels: CoeffToSlot + EvalMod + the region-crossing first SlotToCoeff group
     static int boot_double_levels() { return kBootCts + boot_evalmod_depth() + 1; }
@@ -1311,13 +1316,62 @@ public:
         return cur;
     }
 
-    // (1/2pi)-free EvalMod: sin(2 pi K y) via Chebyshev cos + r double angles
+    // sum_{k <= deg} c_k T_k from the baby table T[1..8] (T_0 = 1): scalar products deferred
+    // (one rescale for the whole leaf), constant term added at the raw scale
+    Ct cheb_leaf(const std::vector<Ct>& T, const std::vector<double>& c) {
+        Ct acc;
+        bool have = false;
+        for (size_t k = 1; k < c.size(); ++k) {
+            if (c[k] == 0.0) continue;
+            Ct t = mul_scalar(T[k], c[k], 0.0, true);
+            if (!have) {
+                acc = t, have = true;
+            } else {
+                Ct s = add_sub(acc, t, false);
+                release(acc);
+                release(t);
+                acc = s;
+            }
+        }
+        if (!have) throw std::runtime_error("EvalMod: empty Chebyshev leaf");
+        if (c[0] != 0.0) {
+            Ct s = add_scalar(acc, c[0], 0.0);
+            release(acc);
+            acc = s;
+        }
+        Ct o = normalize(acc, true);
+        if (o.data != acc.data) release(acc);
+        return o;
+    }
+    // p = q + T_m r with q_i = c_i - c_{2m-i} (i < m), r_0 = c_m, r_j = 2 c_{m+j}; recurse
+    // until the degree is within the baby table (Paterson-Stockmeyer in the Chebyshev basis)
+    Ct cheb_eval(const std::vector<Ct>& T, const std::map<int, Ct>& giant, const std::vector<double>& c) {
+        const int d = (int)c.size() - 1;
+        if (d <= kBabyDeg) return cheb_leaf(T, c);
+        int m = kBabyDeg;
+        while (2 * m <= d) m *= 2;
+        std::vector<double> q(m), r(d - m + 1);
+        for (int i = 0; i < m; ++i) q[i] = c[i] - (2 * m - i <= d ? c[2 * m - i] : 0.0);
+        r[0] = c[m];
+        for (int j = 1; j <= d - m; ++j) r[j] = 2.0 * c[m + j];
+        Ct qv = cheb_eval(T, giant, q), rv = cheb_eval(T, giant, r);
+        Ct tr = mul(giant.at(m), rv, true);
+        release(rv);
+        Ct o = add_sub(qv, tr, false);
+        release(qv);
+        release(tr);
+        return o;
+    }
+    static constexpr int kBabyDeg = 8;
+
+    // EvalMod: sin(2 pi K y) via the Chebyshev interpolant of cos(2 pi (K y - 1/4) / 2^r)
+    // (baby T_1..T_8, giant T_8, T_16, ...) and r double angles
     Ct eval_mod(const Ct& y) {
         const auto& c = bs_.plan.cheb;
         const int d = (int)c.size() - 1;
-        std::vector<Ct> T(d + 1);
+        std::vector<Ct> T(kBabyDeg + 1);
         T[1] = copy(y);
-        for (int k = 2; k <= d; ++k) {
+        for (int k = 2; k <= kBabyDeg; ++k) {
             const int a = (k + 1) / 2, b = k / 2;
             Ct p = mul(T[a], T[b], true);
             Ct p2 = mul_scalar(p, 2.0, 0.0);
@@ -1325,17 +1379,20 @@ public:
             T[k] = (a == b) ? add_scalar(p2, -1.0, 0.0) : add_sub(p2, T[a - b], true);
             release(p2);
         }
-        Ct acc = mul_scalar(T[1], c[1], 0.0);
-        for (int k = 2; k <= d; ++k) {
-            Ct t = mul_scalar(T[k], c[k], 0.0);
-            Ct s = add_sub(acc, t, false);
-            release(acc);
-            release(t);
-            acc = s;
+        std::map<int, Ct> giant;
+        giant[kBabyDeg] = T[kBabyDeg];
+        for (int m = 2 * kBabyDeg; m <= d; m *= 2) {
+            const Ct& h = giant.at(m / 2);
+            Ct p = mul(h, h, true);
+            Ct p2 = mul_scalar(p, 2.0, 0.0);
+            release(p);
+            giant[m] = add_scalar(p2, -1.0, 0.0);
+            release(p2);
         }
-        Ct g = add_scalar(acc, c[0], 0.0);
-        release(acc);
-        for (int k = 1; k <= d; ++k) release(T[k]);
+        Ct g = cheb_eval(T, giant, c);
+        for (int k = 1; k <= kBabyDeg; ++k) release(T[k]);
+        for (auto& kv : giant)
+            if (kv.first != kBabyDeg) release(kv.second);
         for (int i = 0; i < bs_.plan.r; ++i) {
             Ct sq = mul(g, g, true);
             Ct sq2 = mul_scalar(sq, 2.0, 0.0);
