@@ -11,6 +11,7 @@ import numpy as np
 
 from lut import COEFF_DIR, ensure_coeffs
 from xor4_lut import XOR4LUT
+from utils import pair
 
 
 def load_xor4_coeffs(path: Path) -> np.ndarray:
@@ -29,4 +30,4 @@ class AddRoundKey:
         self.xor4 = xor4
 
     def __call__(self, ct_hi, ct_lo, key_hi, key_lo) -> Tuple[Any, Any]:
-        return self.xor4.apply(ct_hi, key_hi), self.xor4.apply(ct_lo, key_lo)
+        return pair(self.xor4.ctx, lambda: self.xor4.apply(ct_hi, key_hi), lambda: self.xor4.apply(ct_lo, key_lo))

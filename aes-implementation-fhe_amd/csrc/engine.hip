@@ -10,7 +10,10 @@
 
 #include <cmath>
 #include <cstring>
+#include <cstdlib>
+#include <deque>
 #include <map>
+#include <mutex>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -53,13 +56,25 @@ inline u64 hprng(u64 seed, u64 stream, u64 ctr) {
 // ---------------------------------------------------------------------------------
 class Pool {
 public:
-    u32* get(size_t words) {
-        auto& fl = free_[words];
-        if (!fl.empty()) {
-            u32* p = fl.back();
-            fl.pop_back();
-            return p;
+    u32* try_get(size_t words) {
+        auto it = free_.find(words);
+        if (it == free_.end() || it->second.empty()) return nullptr;
+        u32* p = it->second.back();
+        it->second.pop_back();
+        return p;
+    }
+    // moves every free buffer of `o` into this pool
+    void absorb(Pool& o) {
+        for (auto& kv : o.free_) {
+            auto& fl = free_[kv.first];
+            fl.insert(fl.end(), kv.second.begin(), kv.second.end());
         }
+        o.free_.clear();
+        bytes_ += o.bytes_;
+        o.bytes_ = 0;
+    }
+    u32* get(size_t words) {
+        if (u32* p = try_get(words)) return p;
         void* p = nullptr;
         HIP_OK(hipMalloc(&p, words * sizeof(u32)));
         bytes_ += words * sizeof(u32);
@@ -106,6 +121,7 @@ enum Counter { C_MUL, C_RELIN, C_ROT, C_CONJ, C_PTMUL, C_SCALAR, C_RESCALE, C_NT
 
 class Engine {
 public:
+    static constexpr int kStreams = 3;  // see fork() / join()
     Engine(int logn, int L1, int n_double, int dnum, int device, u64 seed) : emb_(logn) {
         std::string err = hp_.build(logn, L1, n_double, dnum, seed);
         if (!err.empty()) throw std::runtime_error(err);
@@ -115,19 +131,26 @@ public:
         if (device < 0 || device >= ndev) throw std::runtime_error("device_id out of range");
         device_ = device;
         HIP_OK(hipSetDevice(device_));
-        HIP_OK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+        for (int k = 0; k < kStreams; ++k) {
+            HIP_OK(hipStreamCreateWithFlags(&streams_[k], hipStreamNonBlocking));
+            HIP_OK(hipEventCreateWithFlags(&fj_ev_[k], hipEventDisableTiming));
+        }
         build_tables();
     }
     ~Engine() {
         (void)hipSetDevice(device_);
-        (void)hipStreamSynchronize(st_);
-        for (auto& kv : cts_) pool_.put(kv.second.data, kv.second.words);
+        (void)hipDeviceSynchronize();
+        for (auto& kv : cts_) pools_[0].put(kv.second.data, kv.second.words);
         for (auto& kv : pts_)
-            for (auto& e : kv.second.enc) pool_.put(e.second.first, e.second.second);
-        pool_.release_all();
+            for (auto& e : kv.second.enc) pools_[0].put(e.second.first, e.second.second);
+        for (auto& d : deferred_) pools_[0].put(d.first, d.second);
+        for (auto& pl : pools_) pl.release_all();
         for (void* p : owned_) (void)hipFree(p);
         for (auto& kv : ksk_) (void)hipFree(kv.second);
-        (void)hipStreamDestroy(st_);
+        for (int k = 0; k < kStreams; ++k) {
+            (void)hipEventDestroy(fj_ev_[k]);
+            (void)hipStreamDestroy(streams_[k]);
+        }
     }
 
     const HostParams& hp() const { return hp_; }
@@ -137,7 +160,55 @@ public:
         hp_.fresh = level;
     }
     int slot_count() const { return hp_.n / 2; }
-    void sync() { HIP_OK(hipStreamSynchronize(st_)); }
+    void sync() {
+        for (int k = 0; k < kStreams; ++k) HIP_OK(hipStreamSynchronize(streams_[k]));
+    }
+
+    // ------------------------------------------------------------------ streams (fork / join)
+    // the calling host thread's stream and buffer pool: 0 unless bound to a branch stream
+    static thread_local int t_sidx;
+    hipStream_t S() const { return streams_[t_sidx]; }
+    Pool& pool() { return pools_[t_sidx]; }
+    // allocation on the calling thread's stream: its own pool, then (branch streams) buffers
+    // stream 0 released before the fork -- ordered before every branch by the fork event
+    u32* alloc_words(size_t words) {
+        if (t_sidx != 0) {
+            if (u32* p = pools_[t_sidx].try_get(words)) return p;
+            if (no_share_) return pools_[t_sidx].get(words);
+        }
+        return pools_[0].get(words);
+    }
+    bool no_share_ = std::getenv("AESFHE_NO_POOL_SHARE") != nullptr;  // debug switch
+    bool fj_active_ = false;
+    static int streams() { return kStreams; }
+    void bind_stream(int k) {
+        if (k < 0 || k >= kStreams) throw std::runtime_error("bind_stream: stream index out of range");
+        t_sidx = k;
+    }
+    // branch streams start after everything already queued on stream 0
+    void fork() {
+        if (t_sidx != 0) throw std::runtime_error("fork must be called from the main stream");
+        HIP_OK(hipEventRecord(fj_ev_[0], streams_[0]));
+        for (int k = 1; k < kStreams; ++k) HIP_OK(hipStreamWaitEvent(streams_[k], fj_ev_[0], 0));
+        fj_active_ = true;
+    }
+    // stream 0 continues after every branch; handles the branch threads dropped go back to
+    // stream 0's pool only now (another stream may have read them until here)
+    void join() {
+        if (t_sidx != 0) throw std::runtime_error("join must be called from the main stream");
+        for (int k = 1; k < kStreams; ++k) {
+            HIP_OK(hipEventRecord(fj_ev_[k], streams_[k]));
+            HIP_OK(hipStreamWaitEvent(streams_[0], fj_ev_[k], 0));
+        }
+        for (auto& d : deferred_) pools_[0].put(d.first, d.second);
+        deferred_.clear();
+        for (int k = 1; k < kStreams; ++k) pools_[0].absorb(pools_[k]);  // stream 0 is after them now
+        fj_active_ = false;
+    }
+    void give_back(u32* p, size_t words) {
+        if (t_sidx != 0 || fj_active_) deferred_.push_back({p, words});
+        else pools_[0].put(p, words);
+    }
 
     // ------------------------------------------------------------------ handles
     aesfhe_handle put_ct(Ct c) {
@@ -158,13 +229,13 @@ public:
     void free_handle(aesfhe_handle h) {
         auto it = cts_.find(h);
         if (it != cts_.end()) {
-            pool_.put(it->second.data, it->second.words);
+            give_back(it->second.data, it->second.words);
             cts_.erase(it);
             return;
         }
         auto ip = pts_.find(h);
         if (ip != pts_.end()) {
-            for (auto& e : ip->second.enc) pool_.put(e.second.first, e.second.second);
+            for (auto& e : ip->second.enc) give_back(e.second.first, e.second.second);
             pts_.erase(ip);
         }
     }
@@ -186,11 +257,11 @@ public:
         c.level = level;
         c.npoly = npoly;
         c.words = (size_t)npoly * hp_.nl(level) * hp_.n;
-        c.data = pool_.get(c.words);
+        c.data = alloc_words(c.words);
         return c;
     }
-    u32* tmp(size_t rows) { return pool_.get(rows * hp_.n); }
-    void untmp(u32* p, size_t rows) { pool_.put(p, rows * hp_.n); }
+    u32* tmp(size_t rows) { return alloc_words(rows * hp_.n); }
+    void untmp(u32* p, size_t rows) { pool().put(p, rows * hp_.n); }
 
     // ------------------------------------------------------------------ maps
     static LimbMap qmap() { return LimbMap{1 << 30, 0, 0}; }
@@ -198,20 +269,20 @@ public:
     static LimbMap single(int prime) { return LimbMap{1, prime, 0}; }
 
     void ntt(u32* d, int rows, int nl, LimbMap m) {
-        launch_ntt_fwd(st_, T_, d, rows, nl, m);
+        launch_ntt_fwd(S(), T_, d, rows, nl, m);
         cnt_[C_NTT_ROWS] += rows;
     }
     void intt(u32* d, int rows, int nl, LimbMap m) {
-        launch_ntt_inv(st_, T_, d, rows, nl, m);
+        launch_ntt_inv(S(), T_, d, rows, nl, m);
         cnt_[C_NTT_ROWS] += rows;
     }
     // out-of-place forms (dense rows unless a RowMap is given)
     void ntt(u32* dst, const u32* src, int rows, RowMap rm, LimbMap m) {
-        launch_ntt_fwd(st_, T_, dst, src, rows, rm, m);
+        launch_ntt_fwd(S(), T_, dst, src, rows, rm, m);
         cnt_[C_NTT_ROWS] += rows;
     }
     void intt(u32* dst, const u32* src, int rows, RowMap rm, LimbMap m) {
-        launch_ntt_inv(st_, T_, dst, src, rows, rm, m);
+        launch_ntt_inv(S(), T_, dst, src, rows, rm, m);
         cnt_[C_NTT_ROWS] += rows;
     }
 
@@ -220,17 +291,17 @@ public:
         const int n = hp_.n, nt = hp_.n_tot();
         if (!d_s_) {
             d_s_ = dev_alloc((size_t)nt * n);
-            launch_sample_small(st_, T_, d_s_, nt, qmap(), hp_.seed, stream_id(1, 0, 0), 0);
+            launch_sample_small(S(), T_, d_s_, nt, qmap(), hp_.seed, stream_id(1, 0, 0), 0);
             ntt(d_s_, nt, nt, qmap());
         }
         if (!d_pk_) {
             const int nq = hp_.n_q;
             d_pk_ = dev_alloc((size_t)2 * nq * n);
             u32* e = tmp(nq);
-            launch_sample_uniform(st_, T_, d_pk_ + (size_t)nq * n, nq, qmap(), hp_.seed, stream_id(2, 0, 0));
-            launch_sample_small(st_, T_, e, nq, qmap(), hp_.seed, stream_id(3, 0, 0), 1);
+            launch_sample_uniform(S(), T_, d_pk_ + (size_t)nq * n, nq, qmap(), hp_.seed, stream_id(2, 0, 0));
+            launch_sample_small(S(), T_, e, nq, qmap(), hp_.seed, stream_id(3, 0, 0), 1);
             ntt(e, nq, nq, qmap());
-            launch_keygen_combine(st_, T_, d_pk_, d_pk_ + (size_t)nq * n, d_s_, e, nullptr, nullptr, nq, qmap(), 0, 0);
+            launch_keygen_combine(S(), T_, d_pk_, d_pk_ + (size_t)nq * n, d_s_, e, nullptr, nullptr, nq, qmap(), 0, 0);
             untmp(e, nq);
         }
         ksk(0);
@@ -261,29 +332,30 @@ public:
         u32* sp = tmp(nks);
         const u32* target = d_s_;
         if (g == 0) {
-            launch_square(st_, T_, sp, d_s_, nks, nks, qmap());
+            launch_square(S(), T_, sp, d_s_, nks, nks, qmap());
         } else if (g == tag_d2s()) {  // dense s -> sparse ephemeral s_sp (bootstrapping)
-            HIP_OK(hipMemcpyAsync(sp, d_s_, sizeof(u32) * nks * n, hipMemcpyDeviceToDevice, st_));
+            HIP_OK(hipMemcpyAsync(sp, d_s_, sizeof(u32) * nks * n, hipMemcpyDeviceToDevice, S()));
             target = sparse_secret();
         } else if (g == tag_s2d()) {  // sparse s_sp -> dense s
-            HIP_OK(hipMemcpyAsync(sp, sparse_secret(), sizeof(u32) * nks * n, hipMemcpyDeviceToDevice, st_));
+            HIP_OK(hipMemcpyAsync(sp, sparse_secret(), sizeof(u32) * nks * n, hipMemcpyDeviceToDevice, S()));
         } else {
-            launch_automorph(st_, T_, sp, d_s_, g, nks);
+            launch_automorph(S(), T_, sp, d_s_, g, nks);
         }
         u32* e = tmp(nkey);
         const LimbMap em = extmap(nks);
         for (int j = 0; j < hp_.dnum; ++j) {
             u32* b = key + (size_t)j * 2 * nkey * n;
             u32* a = b + (size_t)nkey * n;
-            launch_sample_uniform(st_, T_, a, nkey, em, hp_.seed, stream_id(4, g, j));
-            launch_sample_small(st_, T_, e, nkey, em, hp_.seed, stream_id(5, g, j), 1);
+            launch_sample_uniform(S(), T_, a, nkey, em, hp_.seed, stream_id(4, g, j));
+            launch_sample_small(S(), T_, e, nkey, em, hp_.seed, stream_id(5, g, j), 1);
             ntt(e, nkey, nkey, em);
             const int lo = j * hp_.alpha, hi = std::min(nks, lo + hp_.alpha);
-            launch_keygen_combine(st_, T_, b, a, target, e, sp, d_gadget_, nkey, em, lo, hi);
+            launch_keygen_combine(S(), T_, b, a, target, e, sp, d_gadget_, nkey, em, lo, hi);
         }
         untmp(e, nkey);
         untmp(sp, nks);
         ksk_[g] = key;
+        HIP_OK(hipStreamSynchronize(S()));  // shared by every stream from now on
         return key;
     }
 
@@ -312,8 +384,8 @@ public:
     }
     u32* upload_ntt(const std::vector<u32>& host, int nl) {
         u32* d = tmp(nl);
-        HIP_OK(hipMemcpyAsync(d, host.data(), host.size() * sizeof(u32), hipMemcpyHostToDevice, st_));
-        HIP_OK(hipStreamSynchronize(st_));  // host vector may die after return
+        HIP_OK(hipMemcpyAsync(d, host.data(), host.size() * sizeof(u32), hipMemcpyHostToDevice, S()));
+        HIP_OK(hipStreamSynchronize(S()));  // host vector may die after return
         ntt(d, nl, nl, qmap());
         return d;
     }
@@ -337,15 +409,15 @@ public:
         u32* v = tmp(nq);
         u32* e = tmp(2 * nq);
         const u64 ctr = enc_ctr_++;
-        launch_sample_small(st_, T_, v, nq, qmap(), hp_.seed, stream_id(6, 0, ctr), 0);
-        launch_sample_small(st_, T_, e, nq, qmap(), hp_.seed, stream_id(7, 0, ctr), 1);
-        launch_sample_small(st_, T_, e + (size_t)nq * n, nq, qmap(), hp_.seed, stream_id(8, 0, ctr), 1);
+        launch_sample_small(S(), T_, v, nq, qmap(), hp_.seed, stream_id(6, 0, ctr), 0);
+        launch_sample_small(S(), T_, e, nq, qmap(), hp_.seed, stream_id(7, 0, ctr), 1);
+        launch_sample_small(S(), T_, e + (size_t)nq * n, nq, qmap(), hp_.seed, stream_id(8, 0, ctr), 1);
         ntt(v, nq, nq, qmap());
         ntt(e, 2 * nq, nq, qmap());
         Ct top = alloc_ct(L + 1, 2);
-        launch_add(st_, T_, e, e, m, nq, nq, qmap());  // e0 + m
-        launch_fma_poly(st_, T_, top.data, e, d_pk_, v, nq, nq, qmap());
-        launch_fma_poly(st_, T_, top.data + (size_t)nq * n, e + (size_t)nq * n, d_pk_ + (size_t)hp_.n_q * n, v, nq, nq, qmap());
+        launch_add(S(), T_, e, e, m, nq, nq, qmap());  // e0 + m
+        launch_fma_poly(S(), T_, top.data, e, d_pk_, v, nq, nq, qmap());
+        launch_fma_poly(S(), T_, top.data + (size_t)nq * n, e + (size_t)nq * n, d_pk_ + (size_t)hp_.n_q * n, v, nq, nq, qmap());
         untmp(v, nq);
         untmp(e, 2 * nq);
         Ct out = rescale(top);
@@ -378,21 +450,21 @@ public:
         }
         const double scale = c.level >= 0 ? raw_scale(c.level, c.pend) : (bs_.ready ? bs_.s_bt : 1.0);
         u32* x = tmp(kd);
-        HIP_OK(hipMemcpyAsync(x, c.data, sizeof(u32) * kd * n, hipMemcpyDeviceToDevice, st_));
+        HIP_OK(hipMemcpyAsync(x, c.data, sizeof(u32) * kd * n, hipMemcpyDeviceToDevice, S()));
         u32* spow = nullptr;
         for (int p = 1; p < c.npoly; ++p) {
             const u32* s_use = d_s_;
             if (p == 2) {
                 spow = tmp(kd);
-                launch_square(st_, T_, spow, d_s_, kd, kd, qmap());
+                launch_square(S(), T_, spow, d_s_, kd, kd, qmap());
                 s_use = spow;
             }
-            launch_fma_poly(st_, T_, x, x, c.data + (size_t)p * nl * n, s_use, kd, kd, qmap());
+            launch_fma_poly(S(), T_, x, x, c.data + (size_t)p * nl * n, s_use, kd, kd, qmap());
         }
         intt(x, kd, kd, qmap());
         std::vector<u32> h((size_t)kd * n);
-        HIP_OK(hipMemcpyAsync(h.data(), x, sizeof(u32) * kd * n, hipMemcpyDeviceToHost, st_));
-        HIP_OK(hipStreamSynchronize(st_));
+        HIP_OK(hipMemcpyAsync(h.data(), x, sizeof(u32) * kd * n, hipMemcpyDeviceToHost, S()));
+        HIP_OK(hipStreamSynchronize(S()));
         untmp(x, kd);
         if (spow) untmp(spow, kd);
         if (c.data != c_in.data) release(c);
@@ -427,14 +499,14 @@ public:
     }
 
     // ------------------------------------------------------------------ basic ops
-    void release(const Ct& c) { pool_.put(c.data, c.words); }
+    void release(const Ct& c) { pool().put(c.data, c.words); }
     static void copy_meta(Ct& o, const Ct& c) {
         o.ntt = c.ntt, o.pend = c.pend, o.lazy = c.lazy, o.zero = c.zero;
     }
     Ct copy(const Ct& c) {
         Ct o = alloc_ct(c.level, c.npoly);
         copy_meta(o, c);
-        HIP_OK(hipMemcpyAsync(o.data, c.data, c.words * sizeof(u32), hipMemcpyDeviceToDevice, st_));
+        HIP_OK(hipMemcpyAsync(o.data, c.data, c.words * sizeof(u32), hipMemcpyDeviceToDevice, S()));
         return o;
     }
     // returns c itself (same data) when already in NTT form, else a converted copy
@@ -529,20 +601,34 @@ public:
     }
     // stored ciphertext in canonical form; the table entry is replaced so that deferred work
     // is done once however often the handle is used
+    // Inside a fork/join section another stream may read the same handle, so the table entry
+    // is left alone and a private canonical copy (released when the API call ends) is used.
     const Ct& canon(aesfhe_handle h) {
         auto it = cts_.find(h);
         if (it == cts_.end()) throw std::runtime_error("invalid ciphertext handle");
         Ct& c = it->second;
-        if (c.lazy) {
-            Ct nc = normalize(c, true);
-            if (nc.data != c.data) release(c);
-            c = nc;
+        if (!c.lazy) return c;
+        Ct nc = normalize(c, true);
+        if (nc.data == c.data) {  // nothing was owed: only the flag changes
+            c.lazy = false;
+            return c;
         }
+        if (fj_active_) {
+            scratch_.push_back(nc);
+            return scratch_.back();
+        }
+        if (nc.data != c.data) release(c);
+        c = nc;
         return c;
+    }
+    std::deque<Ct> scratch_;
+    void end_call() {
+        for (const Ct& c : scratch_) release(c);
+        scratch_.clear();
     }
     Ct zero_ct(int level) {
         Ct z = alloc_ct(level, 2);
-        HIP_OK(hipMemsetAsync(z.data, 0, z.words * sizeof(u32), st_));
+        HIP_OK(hipMemsetAsync(z.data, 0, z.words * sizeof(u32), S()));
         z.zero = true;
         return z;
     }
@@ -561,7 +647,7 @@ public:
             intt(last, cur, np, RowMap{1, r + 1, 1, r, 0}, single(r));
             u32* v = tmp((size_t)np * r);
             u32* o = tmp((size_t)np * r);
-            launch_rescale_ntt(st_, T_, o, cur, last, v, d_rescale_qinv_ + rescale_off_[r], np, r, r + 1, hp_.mod[r]);
+            launch_rescale_ntt(S(), T_, o, cur, last, v, d_rescale_qinv_ + rescale_off_[r], np, r, r + 1, hp_.mod[r]);
             cnt_[C_NTT_ROWS] += (size_t)np * r;
             untmp(last, np);
             untmp(v, (size_t)np * r);
@@ -648,11 +734,11 @@ public:
         u32* mid = tmp((size_t)c.npoly * nk);
         for (int q = 0; q < c.npoly; ++q)
             HIP_OK(hipMemcpyAsync(mid + (size_t)q * nk * n, c.data + (size_t)q * na * n, sizeof(u32) * nk * n, hipMemcpyDeviceToDevice,
-                                  st_));
+                                  S()));
         const i64 cst = std::llround(ratio);
         std::vector<u32> r(nk);
         for (int i = 0; i < nk; ++i) r[i] = mod_i64(cst, hp_.mod[i]);
-        launch_mul_const_half(st_, T_, mid, mid, const_half(r, r), c.npoly * nk, nk, qmap());
+        launch_mul_const_half(S(), T_, mid, mid, const_half(r, r), c.npoly * nk, nk, qmap());
         Ct o;
         o.level = t, o.npoly = c.npoly, o.pend = p, o.lazy = c.lazy || p > 0, o.zero = c.zero;
         o.words = (size_t)c.npoly * nb * n;
@@ -728,16 +814,16 @@ public:
         o.pend = x.pend;
         o.lazy = x.lazy || y.lazy;
         const int common = std::min(x.npoly, y.npoly) * nl;
-        if (x.zero) launch_neg(st_, T_, o.data, y.data, common, nl, qmap());
-        else if (sub) launch_sub(st_, T_, o.data, x.data, y.data, common, nl, qmap());
-        else launch_add(st_, T_, o.data, x.data, y.data, common, nl, qmap());
+        if (x.zero) launch_neg(S(), T_, o.data, y.data, common, nl, qmap());
+        else if (sub) launch_sub(S(), T_, o.data, x.data, y.data, common, nl, qmap());
+        else launch_add(S(), T_, o.data, x.data, y.data, common, nl, qmap());
         if (x.npoly > y.npoly)
             HIP_OK(hipMemcpyAsync(o.data + (size_t)common * hp_.n, x.data + (size_t)common * hp_.n, sizeof(u32) * nl * hp_.n,
-                                  hipMemcpyDeviceToDevice, st_));
+                                  hipMemcpyDeviceToDevice, S()));
         else if (y.npoly > x.npoly) {
-            if (sub) launch_neg(st_, T_, o.data + (size_t)common * hp_.n, y.data + (size_t)common * hp_.n, nl, nl, qmap());
+            if (sub) launch_neg(S(), T_, o.data + (size_t)common * hp_.n, y.data + (size_t)common * hp_.n, nl, nl, qmap());
             else HIP_OK(hipMemcpyAsync(o.data + (size_t)common * hp_.n, y.data + (size_t)common * hp_.n, sizeof(u32) * nl * hp_.n,
-                                       hipMemcpyDeviceToDevice, st_));
+                                       hipMemcpyDeviceToDevice, S()));
         }
         if (fa) release(x);
         if (fb) release(y);
@@ -763,7 +849,7 @@ public:
         for (int t = 0; t < nl; ++t) d.v[2 * t] = lo[t], d.v[2 * t + 1] = hi[t];
         Ct o = copy(c);
         o.zero = false;
-        launch_add_const_half(st_, T_, o.data, c.data, d, nl, nl, qmap());
+        launch_add_const_half(S(), T_, o.data, c.data, d, nl, nl, qmap());
         if (c.data != c_in.data) release(c);
         return o;
     }
@@ -796,7 +882,7 @@ public:
             Ct o = alloc_ct(c.level, c.npoly);
             copy_meta(o, c);
             o.zero = re == 0.0 && im == 0.0;
-            launch_mul_const_half(st_, T_, o.data, c.data, const_half(lo, hi), c.npoly * nl, nl, qmap());
+            launch_mul_const_half(S(), T_, o.data, c.data, const_half(lo, hi), c.npoly * nl, nl, qmap());
             if (c.data != c_in.data) release(c);
             return o;
         }
@@ -812,7 +898,7 @@ public:
             o = alloc_ct(c.level, c.npoly);
             o.pend = c.pend + 1;
             o.lazy = true;
-            launch_mul_const_half(st_, T_, o.data, c.data, const_half(lo, hi), c.npoly * nl, nl, qmap());
+            launch_mul_const_half(S(), T_, o.data, c.data, const_half(lo, hi), c.npoly * nl, nl, qmap());
         } else {
             Ct nc = normalize(c, false);
             const int nl = hp_.nl(nc.level);
@@ -820,7 +906,7 @@ public:
             const double sc = hp_.ptscale[nc.level];
             scalar_residues(std::llround(re * sc), std::llround(im * sc), nl, lo, hi);
             Ct t = alloc_ct(nc.level, nc.npoly);
-            launch_mul_const_half(st_, T_, t.data, nc.data, const_half(lo, hi), nc.npoly * nl, nl, qmap());
+            launch_mul_const_half(S(), T_, t.data, nc.data, const_half(lo, hi), nc.npoly * nl, nl, qmap());
             o = rescale(t);
             o.lazy = c_in.lazy && o.npoly == 3;
             release(t);
@@ -842,6 +928,7 @@ public:
         const double sc = kind == 0 ? hp_.delta[level] : kind == 1 ? hp_.ptscale[level] : hp_.ptscale[level - 1];
         encode_host(p.re.data(), p.im.data(), sc, nl, host);
         u32* d = upload_ntt(host, nl);
+        HIP_OK(hipStreamSynchronize(S()));  // cached for every stream
         p.enc[key] = {d, (size_t)nl * hp_.n};
         return d;
     }
@@ -861,13 +948,13 @@ public:
             o = alloc_ct(c.level, c.npoly);
             o.pend = c.pend + 1;
             o.lazy = true;
-            launch_mul_poly(st_, T_, o.data, c.data, e, c.npoly, nl, qmap());
+            launch_mul_poly(S(), T_, o.data, c.data, e, c.npoly, nl, qmap());
         } else {
             Ct nc = normalize(c, false);
             const int nl = hp_.nl(nc.level);
             u32* e = pt_at(p, nc.level, 1);
             Ct t = alloc_ct(nc.level, nc.npoly);
-            launch_mul_poly(st_, T_, t.data, nc.data, e, nc.npoly, nl, qmap());
+            launch_mul_poly(S(), T_, t.data, nc.data, e, nc.npoly, nl, qmap());
             o = rescale(t);
             o.lazy = c_in.lazy && o.npoly == 3;
             release(t);
@@ -886,7 +973,7 @@ public:
         Ct o = copy(c);
         o.zero = false;
         o.lazy = c_in.lazy && o.npoly == 3;
-        launch_add(st_, T_, o.data, c.data, e, nl, nl, qmap());
+        launch_add(S(), T_, o.data, c.data, e, nl, nl, qmap());
         if (c.data != c_in.data) release(c);
         return o;
     }
@@ -916,12 +1003,12 @@ public:
             up.qhinv[j] = up.tab[j] + (size_t)2 * h * ne;
             up.negq[j] = up.qhinv[j] + 2 * h;
         }
-        launch_base_convert(st_, T_, up, ne, em);
+        launch_base_convert(S(), T_, up, ne, em);
         RowMap xr = rows_dense(ne);
         xr.skip_alpha = alpha, xr.skip_nl = nl;
         ntt(ext, ext, nd * ne, xr, em);
         u32* acc = tmp(2 * (size_t)ne);
-        launch_key_inner(st_, T_, acc, ext, d, key, nd, ne, nl, alpha, hp_.n_ks + np, hp_.n_ks, em);
+        launch_key_inner(S(), T_, acc, ext, d, key, nd, ne, nl, alpha, hp_.n_ks + np, hp_.n_ks, em);
         untmp(ext, (size_t)nd * ne);
         untmp(coef, nl);
         // ModDown by P: coefficients of the P rows (read in place from acc), conversion of
@@ -940,9 +1027,9 @@ public:
             dn.qhinv[p] = d_moddown_phinv_;
             dn.negq[p] = d_negp_;
         }
-        launch_base_convert(st_, T_, dn, nl, qmap());
+        launch_base_convert(S(), T_, dn, nl, qmap());
         Ct o = alloc_ct(level, 2);
-        launch_ntt_finish(st_, T_, o.data, conv, acc, ne, d_pinv_, add0, add1, 2, nl);
+        launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_pinv_, add0, add1, 2, nl);
         cnt_[C_NTT_ROWS] += 2 * (size_t)nl;
         untmp(yp, 2 * (size_t)np);
         untmp(conv, 2 * (size_t)nl);
@@ -967,7 +1054,7 @@ public:
         const int nl = hp_.nl(x.level);
         Ct d = alloc_ct(x.level, 3);
         d.pend = 1;
-        launch_tensor(st_, T_, d.data, x.data, y.data, nl, qmap());
+        launch_tensor(S(), T_, d.data, x.data, y.data, nl, qmap());
         if (fa) release(x);
         if (fb && y.data != x.data) release(y);
         if (oa) release(a);
@@ -1001,7 +1088,7 @@ public:
         const int nl = hp_.nl(c.level), n = hp_.n;
         const u32* key = ksk(g);
         u32* perm = tmp(2 * (size_t)nl);
-        launch_automorph(st_, T_, perm, c.data, g, 2 * nl);
+        launch_automorph(S(), T_, perm, c.data, g, 2 * nl);
         Ct o = keyswitch(perm + (size_t)nl * n, c.level, key, perm, nullptr);
         untmp(perm, 2 * (size_t)nl);
         if (c.data != c_in.data) release(c);
@@ -1071,7 +1158,8 @@ public:
     const u32* s_sq4() {
         if (!d_s2_) {
             d_s2_ = dev_alloc((size_t)4 * hp_.n);
-            launch_square(st_, T_, d_s2_, d_s_, std::min(4, hp_.n_tot()), 4, qmap());
+            launch_square(S(), T_, d_s2_, d_s_, std::min(4, hp_.n_tot()), 4, qmap());
+            HIP_OK(hipStreamSynchronize(S()));
         }
         return d_s2_;
     }
@@ -1090,8 +1178,10 @@ public:
                 if (j % stride == 0) slots_.e[j / stride] = (u32)e;
                 e = e * 5 % two_n;
             }
-            d_codec_ = (double*)dev_alloc(2 * 64 * 2);  // acc[64] + w[64] doubles
-            d_nib_ = (int*)dev_alloc(32);
+            for (int k = 0; k < kStreams; ++k) {
+                d_codec_[k] = (double*)dev_alloc(2 * 64 * 2);  // acc[64] + w[64] doubles
+                d_nib_[k] = (int*)dev_alloc(32);
+            }
         }
         u32* x = tmp(8);  // [2][4][N]
         int kd[2];
@@ -1110,23 +1200,23 @@ public:
             }
             const int nl = hp_.nl(c.level);
             u32* xw = x + (size_t)w * 4 * n;
-            HIP_OK(hipMemcpyAsync(xw, c.data, sizeof(u32) * kd[w] * n, hipMemcpyDeviceToDevice, st_));
+            HIP_OK(hipMemcpyAsync(xw, c.data, sizeof(u32) * kd[w] * n, hipMemcpyDeviceToDevice, S()));
             for (int p = 1; p < c.npoly; ++p)
-                launch_fma_poly(st_, T_, xw, xw, c.data + (size_t)p * nl * n, p == 2 ? s_sq4() : d_s_, kd[w], kd[w], qmap());
+                launch_fma_poly(S(), T_, xw, xw, c.data + (size_t)p * nl * n, p == 2 ? s_sq4() : d_s_, kd[w], kd[w], qmap());
             intt(xw, kd[w], kd[w], qmap());
             cc[w] = crt_consts(kd[w]);
             isc[w] = 1.0 / (c.level >= 0 ? raw_scale(c.level, c.pend) : 1.0);
             if (own) release(c);
             cnt_[C_DEC]++;
         }
-        double* acc = d_codec_;
-        double* wv = d_codec_ + 64;
-        HIP_OK(hipMemsetAsync(acc, 0, 64 * sizeof(double), st_));
-        launch_decode16(st_, T_, x, kd, cc, slots_, isc, acc);
-        launch_snap16(st_, acc, wv, d_nib_);
+        double* acc = d_codec_[t_sidx];
+        double* wv = acc + 64;
+        HIP_OK(hipMemsetAsync(acc, 0, 64 * sizeof(double), S()));
+        launch_decode16(S(), T_, x, kd, cc, slots_, isc, acc);
+        launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
         const int f = hp_.fresh, nq = hp_.nl(f) + 1;
         u32* m = tmp(2 * (size_t)nq);
-        launch_encode16(st_, T_, m, wv, slots_, hp_.delta[f] * (double)hp_.mod[hp_.nl(f)], nq);
+        launch_encode16(S(), T_, m, wv, slots_, hp_.delta[f] * (double)hp_.mod[hp_.nl(f)], nq);
         ntt(m, 2 * nq, nq, qmap());
         Ct a = encrypt_ntt(m);
         Ct b = encrypt_ntt(m + (size_t)nq * n);
@@ -1178,6 +1268,7 @@ public:
         d_ssp_ = dev_alloc((size_t)nt * n);
         HIP_OK(hipMemcpy(d_ssp_, h.data(), h.size() * sizeof(u32), hipMemcpyHostToDevice));
         ntt(d_ssp_, nt, nt, qmap());
+        HIP_OK(hipStreamSynchronize(S()));
         return d_ssp_;
     }
 
@@ -1248,6 +1339,7 @@ public:
                 encode_host(re.data(), im.data(), hp_.ptscale[level], hp_.nl(level), host);
                 P[gg][b] = upload_ntt(host, hp_.nl(level));
             }
+        HIP_OK(hipStreamSynchronize(S()));  // cached for every stream
         return G.pts.emplace(level, std::move(P)).first->second;
     }
 
@@ -1274,11 +1366,11 @@ public:
             for (int b = 0; b < g.B; ++b) {
                 if (!P[gg][b]) continue;
                 if (!any) {
-                    launch_mul_poly(st_, T_, inner.data, baby[b].data, P[gg][b], 2, nl, qmap());
+                    launch_mul_poly(S(), T_, inner.data, baby[b].data, P[gg][b], 2, nl, qmap());
                     any = true;
                 } else {
-                    launch_mul_poly(st_, T_, prod, baby[b].data, P[gg][b], 2, nl, qmap());
-                    launch_add(st_, T_, inner.data, inner.data, prod, 2 * nl, nl, qmap());
+                    launch_mul_poly(S(), T_, prod, baby[b].data, P[gg][b], 2, nl, qmap());
+                    launch_add(S(), T_, inner.data, inner.data, prod, 2 * nl, nl, qmap());
                 }
             }
             if (!any) {
@@ -1416,7 +1508,7 @@ public:
         if (c.data != in.data) release(c);
         std::vector<u32> r(2);
         for (int t = 0; t < 2; ++t) r[t] = mod_i64(bs_.k1, hp_.mod[t]);
-        launch_mul_const_half(st_, T_, z.data, z.data, const_half(r, r), 4, 2, qmap());
+        launch_mul_const_half(S(), T_, z.data, z.data, const_half(r, r), 4, 2, qmap());
         Ct b = rescale(z, true);
         release(z);
         if (stop_after == 1) return b;
@@ -1427,7 +1519,7 @@ public:
         // 3. ModRaise: centred lift of both polynomials to every limb of the top level
         intt(sp.data, 2, 1, single(0));
         Ct raised = alloc_ct(top, 2);
-        launch_rescale_spread(st_, T_, raised.data, sp.data, 2, hp_.nl(top), hp_.mod[0]);
+        launch_rescale_spread(S(), T_, raised.data, sp.data, 2, hp_.nl(top), hp_.mod[0]);
         release(sp);
         const int nlt = hp_.nl(top);
         ntt(raised.data, 2 * nlt, nlt, qmap());
@@ -1475,20 +1567,20 @@ public:
         const Ct& c0 = canon(h);
         Ct c = ensure_ntt(c0);
         if (words < c.words) throw std::runtime_error("export buffer too small");
-        HIP_OK(hipMemcpyAsync(out, c.data, c.words * sizeof(u32), hipMemcpyDeviceToHost, st_));
-        HIP_OK(hipStreamSynchronize(st_));
+        HIP_OK(hipMemcpyAsync(out, c.data, c.words * sizeof(u32), hipMemcpyDeviceToHost, S()));
+        HIP_OK(hipStreamSynchronize(S()));
         if (c.data != c0.data) release(c);
     }
     aesfhe_handle import_ct(int level, int npoly, const u32* data) {
         if (level < -1 || level > hp_.L || npoly < 1 || npoly > 3) throw std::runtime_error("import: bad level/npoly");
         Ct c = alloc_ct(level, npoly);
-        HIP_OK(hipMemcpyAsync(c.data, data, c.words * sizeof(u32), hipMemcpyHostToDevice, st_));
-        HIP_OK(hipStreamSynchronize(st_));
+        HIP_OK(hipMemcpyAsync(c.data, data, c.words * sizeof(u32), hipMemcpyHostToDevice, S()));
+        HIP_OK(hipStreamSynchronize(S()));
         return put_ct(c);
     }
     void export_dev(const u32* d, size_t words, u32* out) {
-        HIP_OK(hipMemcpyAsync(out, d, words * sizeof(u32), hipMemcpyDeviceToHost, st_));
-        HIP_OK(hipStreamSynchronize(st_));
+        HIP_OK(hipMemcpyAsync(out, d, words * sizeof(u32), hipMemcpyDeviceToHost, S()));
+        HIP_OK(hipStreamSynchronize(S()));
     }
     void export_secret(u32* out) {
         if (!d_s_) throw std::runtime_error("keys not generated");
@@ -1501,7 +1593,7 @@ public:
     void export_ksk(u64 g, u32* out) { export_dev(ksk(g), ksk_words(), out); }
     void debug_ntt(u32* data, int rows, int first_prime, int inverse) {
         u32* d = tmp(rows);
-        HIP_OK(hipMemcpyAsync(d, data, sizeof(u32) * rows * hp_.n, hipMemcpyHostToDevice, st_));
+        HIP_OK(hipMemcpyAsync(d, data, sizeof(u32) * rows * hp_.n, hipMemcpyHostToDevice, S()));
         LimbMap m{rows, first_prime, 0};
         if (inverse) intt(d, rows, rows, m);
         else ntt(d, rows, rows, m);
@@ -1511,7 +1603,7 @@ public:
     void debug_keyswitch(int level, u64 g, const u32* d_host, u32* out) {
         const int nl = hp_.nl(level);
         u32* d = tmp(nl);
-        HIP_OK(hipMemcpyAsync(d, d_host, sizeof(u32) * nl * hp_.n, hipMemcpyHostToDevice, st_));
+        HIP_OK(hipMemcpyAsync(d, d_host, sizeof(u32) * nl * hp_.n, hipMemcpyHostToDevice, S()));
         Ct o = keyswitch(d, level, ksk(g), nullptr, nullptr);
         export_dev(o.data, o.words, out);
         release(o);
@@ -1529,7 +1621,7 @@ public:
         if (op > 4 || op < 0) throw std::runtime_error("bench_op: unknown op");
         const int rows = op <= 1 ? arg : 3 * hp_.nl(arg);
         u32* buf = tmp(rows);
-        HIP_OK(hipMemsetAsync(buf, 0, sizeof(u32) * rows * n, st_));
+        HIP_OK(hipMemsetAsync(buf, 0, sizeof(u32) * rows * n, S()));
         const int nl = op <= 1 ? std::min(arg, hp_.n_q) : hp_.nl(arg);
         Ct c;
         c.data = buf, c.level = op <= 1 ? 0 : arg, c.npoly = 2, c.ntt = true, c.words = (size_t)2 * nl * n;
@@ -1544,9 +1636,9 @@ public:
         hipEvent_t a, b;
         HIP_OK(hipEventCreate(&a));
         HIP_OK(hipEventCreate(&b));
-        HIP_OK(hipEventRecord(a, st_));
+        HIP_OK(hipEventRecord(a, S()));
         for (int i = 0; i < iters; ++i) run();
-        HIP_OK(hipEventRecord(b, st_));
+        HIP_OK(hipEventRecord(b, S()));
         HIP_OK(hipEventSynchronize(b));
         float ms = 0.f;
         HIP_OK(hipEventElapsedTime(&ms, a, b));
@@ -1717,9 +1809,14 @@ private:
     HostParams hp_;
     Embedding emb_;
     DevTables T_;
-    hipStream_t st_ = nullptr;
+    // stream 0 carries the caller's work; streams 1..kStreams-1 carry the branches of a
+    // fork/join section (aesfhe_fork / aesfhe_join), each bound to one host thread
+    hipStream_t streams_[kStreams] = {};
+    hipEvent_t fj_ev_[kStreams] = {};
+    Pool pools_[kStreams];
+    std::vector<std::pair<u32*, size_t>> deferred_;  // handle frees from branch threads
     int device_ = 0;
-    Pool pool_;
+
     std::vector<void*> owned_;
     std::unordered_map<aesfhe_handle, Ct> cts_;
     std::unordered_map<aesfhe_handle, Pt> pts_;
@@ -1743,8 +1840,8 @@ private:
     u64 cnt_[C_N] = {};
     CrtConsts crt_[4] = {};
     Slot16 slots_ = {};
-    double* d_codec_ = nullptr;
-    int* d_nib_ = nullptr;
+    double* d_codec_[kStreams] = {};
+    int* d_nib_[kStreams] = {};
     u32* d_s2_ = nullptr;
     bool lazy_ = true;  // defer relinearisation / rescales of API-level products
 
@@ -1752,39 +1849,45 @@ public:
     KernelProfiler prof_;
     void activate() { prof_set(&prof_); }
 };
+thread_local int Engine::t_sidx = 0;
 
 }  // namespace
 
 // =====================================================================================
 // C ABI
 // =====================================================================================
+// One engine may be driven by several host threads (one per stream, aesfhe_bind_stream):
+// every call holds the context mutex while it queues work; errors are per thread.
 struct aesfhe_ctx {
     std::unique_ptr<Engine> eng;
-    std::string err;
+    std::recursive_mutex mu;
 };
+static thread_local std::string t_err;
 
-#define API_BEGIN                          \
-    if (!ctx) return -2;                   \
-    if (ctx->eng) ctx->eng->activate();    \
+#define API_BEGIN                                      \
+    if (!ctx) return -2;                               \
+    std::lock_guard<std::recursive_mutex> lock_(ctx->mu); \
+    if (ctx->eng) ctx->eng->activate();                \
     try {
-#define API_END                         \
-    return 0;                           \
-    }                                   \
-    catch (const std::exception& e) {   \
-        ctx->err = e.what();            \
-        return -1;                      \
+#define API_END                                        \
+    if (ctx->eng) ctx->eng->end_call();                \
+    return 0;                                          \
+    }                                                  \
+    catch (const std::exception& e) {                  \
+        t_err = e.what();                              \
+        if (ctx->eng) ctx->eng->end_call();            \
+        return -1;                                     \
     }
 
 extern "C" {
 
 int aesfhe_create(aesfhe_ctx** out, int log_n, int max_level, int dnum, int device_id, uint64_t seed) {
-    static thread_local std::string create_err;
     *out = nullptr;
     auto* c = new aesfhe_ctx();
     try {
         c->eng.reset(new Engine(log_n, max_level, 0, dnum, device_id, seed));
     } catch (const std::exception& e) {
-        c->err = e.what();
+        t_err = e.what();
         *out = c;
         return -1;
     }
@@ -1800,7 +1903,7 @@ int aesfhe_create_boot(aesfhe_ctx** out, int log_n, int fresh_level, int dnum, i
         c->eng.reset(new Engine(log_n, L1, Engine::boot_double_levels(), dnum, device_id, seed));
         c->eng->set_fresh(fresh_level);
     } catch (const std::exception& e) {
-        c->err = e.what();
+        t_err = e.what();
         return -1;
     }
     return 0;
@@ -1814,7 +1917,24 @@ int aesfhe_destroy(aesfhe_ctx* ctx) {
     delete ctx;
     return 0;
 }
-const char* aesfhe_last_error(aesfhe_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+const char* aesfhe_last_error(aesfhe_ctx* ctx) { return ctx ? t_err.c_str() : "null context"; }
+int aesfhe_streams(aesfhe_ctx* ctx) { return ctx && ctx->eng ? Engine::streams() : -1; }
+int aesfhe_bind_stream(aesfhe_ctx* ctx, int index) {
+    API_BEGIN ctx->eng->bind_stream(index);
+    API_END
+}
+int aesfhe_settle(aesfhe_ctx* ctx, aesfhe_handle c) {
+    API_BEGIN(void) ctx->eng->canon(c);
+    API_END
+}
+int aesfhe_fork(aesfhe_ctx* ctx) {
+    API_BEGIN ctx->eng->fork();
+    API_END
+}
+int aesfhe_join(aesfhe_ctx* ctx) {
+    API_BEGIN ctx->eng->join();
+    API_END
+}
 int aesfhe_keygen(aesfhe_ctx* ctx) {
     API_BEGIN ctx->eng->keygen();
     API_END

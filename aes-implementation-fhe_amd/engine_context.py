@@ -21,7 +21,7 @@ class EngineContext:
     def __init__(self, signature: int, *, max_level: int = 17, use_bootstrap: bool = True,
                  use_multiparty: bool = False, mode: str = "cpu", device_id: int = 0,
                  thread_count: int | None = None, log_n: int = 16, dnum: int | None = None, seed: int = 0x5EED,
-                 lazy: bool = True):
+                 lazy: bool = True, concurrent: bool = True):
         # REF/engine_context.py:17-42: signature selects the engine constructor form
         if signature == 1:
             kw = dict(use_bootstrap=use_bootstrap, max_level=_SIG_DEFAULT_LEVEL)
@@ -33,7 +33,8 @@ class EngineContext:
             raise ValueError(f"Unsupported signature: {signature}")
         self.signature = signature
         self.engine = Engine(mode=mode, use_multiparty=use_multiparty, thread_count=thread_count or 0,
-                             device_id=device_id, log_n=log_n, dnum=dnum, seed=seed, lazy=lazy, **kw)
+                             device_id=device_id, log_n=log_n, dnum=dnum, seed=seed, lazy=lazy,
+                             concurrent=concurrent, **kw)
         eng = self.engine
         # REF/engine_context.py:44-50
         self.secret_key = eng.create_secret_key()
@@ -151,6 +152,11 @@ class EngineContext:
                                      self.bootstrap_key)
 
     # -------------------------------------------------------------- MI355X extras
+    def run_parallel(self, *fns):
+        """Independent branches (e.g. the hi and lo nibble halves of an AES step) on separate
+        HIP streams; sequential when the context was built with concurrent=False."""
+        return self.engine.parallel(*fns)
+
     def renorm_pair(self, hi, lo):
         """Device-side Zeta16 secret-key renorm of a (hi, lo) state pair (REF/pipeline.py:65-69)."""
         return self.engine.renorm_pair(hi, lo)

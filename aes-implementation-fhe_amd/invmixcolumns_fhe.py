@@ -10,6 +10,7 @@ from mixcol_final import _CoeffCache, gf_basis16, gf_poly_eval
 from shift_rows import row_masks
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT
+from utils import pair
 
 
 class InvMixColumnsFHE:
@@ -44,7 +45,8 @@ class InvMixColumnsFHE:
         return out
 
     def _gf(self, mult, hi, lo):
-        return self._poly2_eval(hi, lo, mult, "hi"), self._poly2_eval(hi, lo, mult, "lo")
+        return pair(self.ctx, lambda: self._poly2_eval(hi, lo, mult, "hi"), lambda: self._poly2_eval(hi, lo, mult, "lo"),
+                    shared=(hi, lo))
 
     def gf_mult_9(self, hi, lo):
         return self._gf(9, hi, lo)
@@ -63,7 +65,9 @@ class InvMixColumnsFHE:
 
     def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
         log = (lambda k, v: debug.__setitem__(k, v)) if debug is not None else (lambda k, v: None)
-        rot = {k: (self._col_shift_rowmajor(ct_hi, k), self._col_shift_rowmajor(ct_lo, k)) for k in (1, 2, 3)}
+        rh, rl = pair(self.ctx, lambda: [self._col_shift_rowmajor(ct_hi, k) for k in (1, 2, 3)],
+                      lambda: [self._col_shift_rowmajor(ct_lo, k) for k in (1, 2, 3)])
+        rot = {k: (rh[k - 1], rl[k - 1]) for k in (1, 2, 3)}
         for k in (1, 2, 3):
             log(f"rotc{k}", rot[k])
         e14 = self.gf_mult_14(ct_hi, ct_lo)
@@ -74,14 +78,14 @@ class InvMixColumnsFHE:
         log("mul13", e13)
         e9 = self.gf_mult_9(*rot[3])
         log("mul9", e9)
-        acc = (self._xor(e14[0], e11[0]), self._xor(e14[1], e11[1]))
+        acc = pair(self.ctx, lambda: self._xor(e14[0], e11[0]), lambda: self._xor(e14[1], e11[1]))
         log("acc1", acc)
         acc = self._renorm_pair(*acc)
-        acc = (self._xor(acc[0], e13[0]), self._xor(acc[1], e13[1]))
+        acc = pair(self.ctx, lambda: self._xor(acc[0], e13[0]), lambda: self._xor(acc[1], e13[1]))
         log("acc2", acc)
         acc = self._renorm_pair(*acc)
-        out = self._renorm_pair(self._xor(acc[0], e9[0]), self._xor(acc[1], e9[1]))
+        out = self._renorm_pair(*pair(self.ctx, lambda: self._xor(acc[0], e9[0]), lambda: self._xor(acc[1], e9[1])))
         if do_final_bootstrap:
-            out = (self.ctx.bootstrap(out[0]), self.ctx.bootstrap(out[1]))
+            out = pair(self.ctx, lambda: self.ctx.bootstrap(out[0]), lambda: self.ctx.bootstrap(out[1]))
         log("out", out)
         return out

@@ -10,7 +10,9 @@ a visible GPU raises ``RuntimeError``.
 """
 from __future__ import annotations
 
+import concurrent.futures
 import ctypes
+import threading
 import numbers
 from pathlib import Path
 from typing import List, Optional
@@ -35,6 +37,7 @@ EXPORTED = [
     "aesfhe_power_basis", "aesfhe_to_ntt", "aesfhe_to_intt", "aesfhe_bootstrap", "aesfhe_renorm_pair",
     "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
     "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
+    "aesfhe_streams", "aesfhe_bind_stream", "aesfhe_fork", "aesfhe_join", "aesfhe_settle",
     "aesfhe_profile", "aesfhe_kernel_stats", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan",
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group",
@@ -87,6 +90,7 @@ def load_library(path: Optional[Path] = None):
         "aesfhe_counters": [vp, np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS"), c_int],
         "aesfhe_bench_op": [vp, c_int, c_int, c_int, ctypes.POINTER(c_dbl)],
         "aesfhe_set_lazy": [vp, c_int],
+        "aesfhe_streams": [vp], "aesfhe_bind_stream": [vp, c_int], "aesfhe_fork": [vp], "aesfhe_join": [vp], "aesfhe_settle": [vp, _H],
         "aesfhe_reset_counters": [vp],
         "aesfhe_profile": [vp, ctypes.c_uint32],
         "aesfhe_kernel_stats": [vp, _dp, c_int, c_int],
@@ -228,7 +232,7 @@ class Engine:
 
     def __init__(self, *, mode: str = "gpu", use_bootstrap: bool = False, use_multiparty: bool = False,
                  thread_count: int = 0, device_id: int = 0, max_level: int = 17, log_n: int = 16,
-                 dnum: int | None = None, seed: int = 0x5EED, lazy: bool = True):
+                 dnum: int | None = None, seed: int = 0x5EED, lazy: bool = True, concurrent: bool = True):
         if use_multiparty:
             raise ValueError("multiparty key generation is not supported")
         self.mode = mode
@@ -250,6 +254,52 @@ class Engine:
         self.level_limbs = [int(x) for x in limbs]
         self._keys_ready = False
         self.set_lazy(lazy)
+        self.concurrent = bool(concurrent)
+        self._pool = None
+        self._tls = threading.local()
+
+    # ------------------------------------------------------------------ concurrency
+    def _executor(self):
+        if self._pool is None:
+            n_branch = int(self._ctx.lib.aesfhe_streams(self._ctx.ptr)) - 1
+            ids = iter(range(1, n_branch + 1))
+            lock = threading.Lock()
+
+            def bind():
+                with lock:
+                    k = next(ids)
+                self._tls.worker = True
+                self._ctx.check(self._ctx.lib.aesfhe_bind_stream(self._ctx.ptr, k))
+
+            self._pool = concurrent.futures.ThreadPoolExecutor(max_workers=n_branch, initializer=bind,
+                                                               thread_name_prefix="aesfhe-stream")
+        return self._pool
+
+    def parallel(self, *fns):
+        """Run independent branches concurrently: one host thread and one HIP stream each,
+        between aesfhe_fork and aesfhe_join.  Results in order; nested calls and
+        concurrent=False run sequentially."""
+        if len(fns) <= 1 or not self.concurrent or getattr(self._tls, "worker", False):
+            return [f() for f in fns]
+        ex = self._executor()
+        self._ctx.check(self._ctx.lib.aesfhe_fork(self._ctx.ptr))
+        futs = [ex.submit(f) for f in fns]
+        out, err = [], None
+        for fu in futs:
+            try:
+                out.append(fu.result())
+            except BaseException as e:  # join before re-raising
+                err = err or e
+                out.append(None)
+        self._ctx.check(self._ctx.lib.aesfhe_join(self._ctx.ptr))
+        if err is not None:
+            raise err
+        return out
+
+    def settle(self, *cts):
+        """Apply deferred work of shared inputs before they are used by parallel branches."""
+        for c in cts:
+            self._ctx.check(self._ctx.lib.aesfhe_settle(self._ctx.ptr, c.handle))
 
     def set_lazy(self, on: bool):
         """Deferred relinearisation / rescale of products; False = eager."""

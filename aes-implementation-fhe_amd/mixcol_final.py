@@ -16,6 +16,7 @@ import numpy as np
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT
+from utils import pair
 
 
 class _CoeffCache:
@@ -80,10 +81,12 @@ class MixColFinal:
         return gf_poly_eval(self.ctx, self._coeffs.load_plaintexts(self.ctx, mult, which), ct_hi, ct_lo)
 
     def gf_mult_2(self, ct_hi, ct_lo):
-        return self._gf_poly_eval_2var(ct_hi, ct_lo, 2, "hi"), self._gf_poly_eval_2var(ct_hi, ct_lo, 2, "lo")
+        return pair(self.ctx, lambda: self._gf_poly_eval_2var(ct_hi, ct_lo, 2, "hi"),
+                    lambda: self._gf_poly_eval_2var(ct_hi, ct_lo, 2, "lo"), shared=(ct_hi, ct_lo))
 
     def gf_mult_3(self, ct_hi, ct_lo):
-        return self._gf_poly_eval_2var(ct_hi, ct_lo, 3, "hi"), self._gf_poly_eval_2var(ct_hi, ct_lo, 3, "lo")
+        return pair(self.ctx, lambda: self._gf_poly_eval_2var(ct_hi, ct_lo, 3, "hi"),
+                    lambda: self._gf_poly_eval_2var(ct_hi, ct_lo, 3, "lo"), shared=(ct_hi, ct_lo))
 
     def _col_shift_rowmajor(self, ct, k_up: int):
         return self.ctx.rotate(ct, -4 * k_up * self.stride)
@@ -96,7 +99,9 @@ class MixColFinal:
 
     def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
         log = (lambda k, v: debug.__setitem__(k, v)) if isinstance(debug, dict) else (lambda k, v: None)
-        rot = {k: (self._col_shift_rowmajor(ct_hi, k), self._col_shift_rowmajor(ct_lo, k)) for k in (1, 2, 3)}
+        rh, rl = pair(self.ctx, lambda: [self._col_shift_rowmajor(ct_hi, k) for k in (1, 2, 3)],
+                      lambda: [self._col_shift_rowmajor(ct_lo, k) for k in (1, 2, 3)])
+        rot = {k: (rh[k - 1], rl[k - 1]) for k in (1, 2, 3)}
         for k in (1, 2, 3):
             log(f"rotc{k}", rot[k])
         log("in", (ct_hi, ct_lo))
@@ -104,17 +109,17 @@ class MixColFinal:
         thr = self.gf_mult_3(*rot[1])
         log("two", two)
         log("thr", thr)
-        acc = (self._xor_ct(two[0], thr[0]), self._xor_ct(two[1], thr[1]))
+        acc = pair(self.ctx, lambda: self._xor_ct(two[0], thr[0]), lambda: self._xor_ct(two[1], thr[1]))
         log("acc1", acc)
         acc = self._renorm_pair(*acc)
-        acc = (self._xor_ct(acc[0], rot[2][0]), self._xor_ct(acc[1], rot[2][1]))
+        acc = pair(self.ctx, lambda: self._xor_ct(acc[0], rot[2][0]), lambda: self._xor_ct(acc[1], rot[2][1]))
         log("acc2", acc)
         acc = self._renorm_pair(*acc)
-        acc = self._renorm_pair(self._xor_ct(acc[0], rot[3][0]), self._xor_ct(acc[1], rot[3][1]))
+        acc = self._renorm_pair(*pair(self.ctx, lambda: self._xor_ct(acc[0], rot[3][0]), lambda: self._xor_ct(acc[1], rot[3][1])))
         log("acc3", acc)
         out_hi, out_lo = acc
         if do_final_bootstrap:
-            out_hi = self.ctx.bootstrap(self.ctx.to_intt(out_hi))
-            out_lo = self.ctx.bootstrap(self.ctx.to_intt(out_lo))
+            out_hi, out_lo = pair(self.ctx, lambda: self.ctx.bootstrap(self.ctx.to_intt(out_hi)),
+                                  lambda: self.ctx.bootstrap(self.ctx.to_intt(out_lo)))
             log("out", (out_hi, out_lo))
         return out_hi, out_lo

@@ -6,6 +6,7 @@ the masked row is rotated by -4r*stride slots (np.roll semantics, SURVEY quirk 4
 from typing import Any, List
 
 import numpy as np
+from utils import pair
 
 
 def row_masks(ctx, sc: int) -> List[Any]:
@@ -37,4 +38,4 @@ class ShiftRows:
         return out
 
     def apply(self, ct_hi: Any, ct_lo: Any):
-        return self._apply_one(ct_hi), self._apply_one(ct_lo)
+        return pair(self.ctx, lambda: self._apply_one(ct_hi), lambda: self._apply_one(ct_lo))

@@ -11,6 +11,7 @@ defines ``SubBytesLUTFastCached``, so both names are provided.
 from typing import Any, Dict, Tuple
 
 import numpy as np
+from utils import pair
 
 _TOL = 1e-12
 
@@ -54,15 +55,22 @@ class SubBytesLUTFastCached:
         ct_b = ctx.multiply(ct_hi, lifted)
         # 3) one shared 128-power basis, two 255-term sums
         pos256 = ctx.make_power_basis(ct_b, self.deg256) if self.deg256 > 0 else []
-        res_hi = ctx.add_plain(ctx.multiply(ct_b, 0.0), self.c0_hi)
-        res_lo = ctx.add_plain(ctx.multiply(ct_b, 0.0), self.c0_lo)
-        for k in self.ks_union:
-            bk = self._power(pos256, k, 256, ctx)
-            if k in self.pt_hi:
-                res_hi = ctx.add(res_hi, ctx.multiply(bk, self.pt_hi[k]))
-            if k in self.pt_lo:
-                res_lo = ctx.add(res_lo, ctx.multiply(bk, self.pt_lo[k]))
-        return res_hi, res_lo
+        # b^k for every used k; the conjugate mirrors (k > 128) once each, split over two streams
+        mirror = [k for k in self.ks_union if k > len(pos256)]
+        half = len(mirror) // 2
+        ma, mb = pair(ctx, lambda: {k: self._power(pos256, k, 256, ctx) for k in mirror[:half]},
+                      lambda: {k: self._power(pos256, k, 256, ctx) for k in mirror[half:]})
+        bk = {**ma, **mb}
+        bk.update({k: pos256[k - 1] for k in self.ks_union if k <= len(pos256)})
+
+        def lut(pts, c0):
+            res = ctx.add_plain(ctx.multiply(ct_b, 0.0), c0)
+            for k in self.ks_union:
+                if k in pts:
+                    res = ctx.add(res, ctx.multiply(bk[k], pts[k]))
+            return res
+
+        return pair(ctx, lambda: lut(self.pt_hi, self.c0_hi), lambda: lut(self.pt_lo, self.c0_lo), shared=(ct_b,))
 
     __call__ = apply
 

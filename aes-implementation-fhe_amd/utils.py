@@ -17,3 +17,17 @@ class ZetaEncoder:
     def from_zeta(z_arr: np.ndarray, modulus: int) -> np.ndarray:
         turns = -np.angle(z_arr) * modulus / (2 * np.pi)
         return np.mod(np.rint(turns), modulus).astype(np.uint8)
+
+
+def pair(ctx, fa, fb, shared=()):
+    """(fa(), fb()) -- the hi / lo halves of an AES step, run concurrently on two HIP streams
+    when the context supports it (EngineContext.run_parallel); `shared` ciphertexts read by
+    both halves are settled first.  Results are identical to the sequential order."""
+    run = getattr(ctx, "run_parallel", None)
+    if run is None:
+        return fa(), fb()
+    if shared:
+        ctx.engine.settle(*shared)
+    a, b = run(fa, fb)
+    return a, b
+

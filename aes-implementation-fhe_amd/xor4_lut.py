@@ -9,6 +9,7 @@ coefficient 1.
 from typing import Any, Dict
 
 import numpy as np
+from utils import pair
 
 
 def basis16(ctx, ct, *, retry_intt: bool = True) -> Dict[int, Any]:
@@ -48,8 +49,7 @@ class XOR4LUT:
 
     def apply(self, a_ct, b_ct):
         ctx = self.ctx
-        A = self._build_power_basis_16(a_ct)
-        B = self._build_power_basis_16(b_ct)
+        A, B = pair(ctx, lambda: self._build_power_basis_16(a_ct), lambda: self._build_power_basis_16(b_ct))
         acc = ctx.sub(A[0], A[0])
         for (p, q), pt in self.pt.items():
             acc = ctx.add(acc, ctx.multiply(ctx.multiply(A[p], B[q]), pt))

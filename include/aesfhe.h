@@ -41,6 +41,22 @@ int aesfhe_create_boot(aesfhe_ctx** out, int log_n, int fresh_level, int dnum, i
 int aesfhe_level_limbs(aesfhe_ctx* ctx, int32_t* out);
 int aesfhe_destroy(aesfhe_ctx* ctx);
 const char* aesfhe_last_error(aesfhe_ctx* ctx);
+
+/* Concurrency (MI355X-side; the reference engine is single-stream).  A context owns
+ * aesfhe_streams() HIP streams.  Stream 0 serves every host thread by default; a host
+ * thread that calls aesfhe_bind_stream(ctx, k) queues its work on stream k.
+ * aesfhe_fork() makes streams 1.. start after all work queued so far on stream 0;
+ * aesfhe_join() makes stream 0 continue only after them.  Between fork and join the
+ * branches must be independent (they may read handles created before the fork); handles
+ * freed by branch threads are recycled at the join.  Calls are serialised by a context
+ * mutex and errors are per thread. */
+int aesfhe_streams(aesfhe_ctx* ctx);
+int aesfhe_bind_stream(aesfhe_ctx* ctx, int index);
+int aesfhe_fork(aesfhe_ctx* ctx);
+/* applies a handle's deferred work now, so branches that share it read one
+ * canonical copy instead of each normalising its own */
+int aesfhe_settle(aesfhe_ctx* ctx, aesfhe_handle c);
+int aesfhe_join(aesfhe_ctx* ctx);
 /* replaces create_secret_key / create_public_key / create_relinearization_key /
  * create_conjugation_key, REF/engine_context.py:44-48 (rotation keys are made on first use) */
 int aesfhe_keygen(aesfhe_ctx* ctx);
