@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--no-final-bootstrap", action="store_true",
                     help="diagnostic only: skip MixColFinal's final bootstrap (not the benchmark workload)")
     ap.add_argument("--eager", action="store_true", help="relinearise and rescale after every product (no deferred evaluation)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="host orchestration only (process group, sharding, barrier, max-over-ranks, rank-0 line) with the "
+                         "byte-level AES in place of the FHE engine; prints value null -- a test harness, not a measurement")
     ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r1_pmc_traffic.json"), help="per-launch HBM bytes from a rocprofv3 PMC pass")
     return ap.parse_args()
 
@@ -131,9 +134,43 @@ def _progress(ctx, every_s: float = 30.0):
     threading.Thread(target=run, daemon=True).start()
 
 
+def rank_states(rank: int, n: int):
+    """Independent synthetic states of one rank (weak scaling: each rank owns its own)."""
+    rng = np.random.default_rng(2025 + rank)
+    return [rng.integers(0, 256, 16).astype(np.uint8) for _ in range(n)]
+
+
+def dry_run(args, rank, world, dist):
+    from aes_keyschedule import expand_aes128_key
+    from oracle import aes_plain
+    np.random.seed(7)
+    rks = expand_aes128_key(np.random.randint(0, 256, 16, dtype=np.uint8))
+    states = rank_states(rank, args.warmup + args.steps)
+    barrier(dist)
+    t0 = time.perf_counter()
+    outs = [aes_plain.ref_encrypt(states[i], rks) for i in range(args.warmup, args.warmup + args.steps)]
+    barrier(dist)
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    firsts = [int(states[args.warmup][0])]
+    if dist is not None:
+        import torch
+        t = torch.tensor(firsts, dtype=torch.int64)
+        got = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(got, t)
+        firsts = [int(g.item()) for g in got]
+    if rank == 0:
+        print(json.dumps({"metric": "homomorphic AES-128 rounds/sec (enc) at N=2^16", "value": None, "dry_run": True,
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "elapsed_max_s": elapsed,
+                          "first_byte_per_rank": firsts, "outputs": len(outs) * world}), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     rank, world, local, dist = dist_setup(args.gpus)
+    if args.dry_run:
+        return dry_run(args, rank, world, dist)
 
     from aes_keyschedule import expand_aes128_key, load_all_coeffs
     from engine_context import EngineContext
@@ -154,8 +191,7 @@ def main():
     np.random.seed(7)
     key = np.random.randint(0, 256, 16, dtype=np.uint8)
     rks = expand_aes128_key(key)
-    rng = np.random.default_rng(2025 + rank)
-    states = [rng.integers(0, 256, 16).astype(np.uint8) for _ in range(args.warmup + args.steps)]
+    states = rank_states(rank, args.warmup + args.steps)
 
     E = ctx.engine
     _progress(ctx)
