@@ -1649,6 +1649,10 @@ public:
     }
     u64 counter(int i) const { return i < C_N ? cnt_[i] : 0; }
     bool lazy() const { return lazy_; }
+    void prof_every(int every) {
+        if (every < 1) throw std::runtime_error("profile_every must be >= 1");
+        prof_.every = (unsigned)every;
+    }
     void set_lazy(bool on) { lazy_ = on; }
     void reset_counters() { std::memset(cnt_, 0, sizeof(cnt_)); }
 
@@ -2096,6 +2100,10 @@ int aesfhe_counters(aesfhe_ctx* ctx, uint64_t* out, int n) {
 int aesfhe_profile(aesfhe_ctx* ctx, uint32_t mask) {
     API_BEGIN ctx->eng->prof_.flush();
     ctx->eng->prof_.mask = mask;
+    API_END
+}
+int aesfhe_profile_every(aesfhe_ctx* ctx, int every) {
+    API_BEGIN ctx->eng->prof_every(every);
     API_END
 }
 int aesfhe_kernel_stats(aesfhe_ctx* ctx, double* out, int n, int reset) {

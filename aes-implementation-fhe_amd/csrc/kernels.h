@@ -16,6 +16,8 @@ enum KernelId {
 };
 struct KernelProfiler {
     unsigned mask = 0;  // bit k enables event timing of KernelId k
+    unsigned every = 1; // time one launch in `every` of an enabled kernel (live sample)
+    unsigned long long seen[KID_N] = {};
     struct Rec {
         hipEvent_t a, b;
         int kid;
@@ -26,8 +28,22 @@ struct KernelProfiler {
     double ms[KID_N] = {}, bytes[KID_N] = {};
     unsigned long long launches[KID_N] = {};
     hipEvent_t get();
-    void flush();   // waits for recorded events and folds them into the totals
+    void flush();   // waits for recorded events and clock slots and folds them into the totals
     void reset();
+    // In-kernel clock (s_memrealtime, 100 MHz) for the NTT, base-conversion and key-switch
+    // kernels: a timed launch gets a slot {earliest block start, latest block end}, the span
+    // rocprofv3 reports.  HIP event pairs around a launch add ~4 us per launch on this stack
+    // (DESIGN.md §5), so they are kept only for the element-wise kernels.
+    static constexpr int kTsSlots = 1 << 15;
+    unsigned long long* d_ts = nullptr;  // [2][kTsSlots]: starts, then ends
+    int ts_next = 0;
+    struct TsRec {
+        int slot, kid;
+        double bytes;
+    };
+    std::vector<TsRec> ts_recs;
+    unsigned long long* ts_slot(int kid, double bytes);
+    void ts_flush();
 };
 // the profiler of the engine currently issuing launches (set per API call)
 void prof_set(KernelProfiler* p);

@@ -122,11 +122,13 @@ __global__ void k_rescale_spread(u32* v, const u32* last, int nt, u32 q_last, co
 // ext_t = sum_i y_i [qhat_i]_t + u [-Q]_t  (mod t).  Table reads are block-uniform
 // (scalar loads).
 constexpr int kConvTargets = 8;
-__global__ void __launch_bounds__(kBlock) k_base_convert(ConvBatch cb, int nt, LimbMap map, const PrimeConst* pc, int logn) {
+__global__ void __launch_bounds__(kBlock) k_base_convert(ConvBatch cb, int nt, LimbMap map, const PrimeConst* pc, int logn,
+                                                         unsigned long long* ts) {
     const int gi = blockIdx.z;
     const int h = cb.h[gi], d0 = cb.d0[gi], skip0 = cb.skip0[gi];
     const int t0 = blockIdx.y * kConvTargets, t1 = min(t0 + kConvTargets, nt);
     if (t0 >= skip0 && t1 <= skip0 + h) return;  // chunk entirely inside the own range
+    ts_begin(ts);
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const u32* x = cb.src[gi];
     const u32* qhinv = cb.qhinv[gi];
@@ -156,11 +158,13 @@ __global__ void __launch_bounds__(kBlock) k_base_convert(ConvBatch cb, int nt, L
             if (i < h) acc += shoup_mul(y[i], tt[2 * (size_t)i * nt], tt[2 * (size_t)i * nt + 1], P.q);
         ext[((size_t)t << logn) + k] = barrett_reduce64(acc, P.q, P.mu);
     }
+    ts_end(ts);
 }
 
 // digit j's own limbs (x < nl, x / alpha == j) come straight from the NTT-form input d
 __global__ void k_key_inner(u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl, int alpha, int nkey, int nks,
-                            LimbMap map, const PrimeConst* pc, int logn) {
+                            LimbMap map, const PrimeConst* pc, int logn, unsigned long long* ts) {
+    ts_begin(ts);
     const int x = blockIdx.y;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const PrimeConst P = pc[map.prime(x)];
@@ -176,6 +180,7 @@ __global__ void k_key_inner(u32* acc, const u32* ext, const u32* d, const u32* k
     }
     acc[((size_t)x << logn) + k] = s0;
     acc[(((size_t)ne + x) << logn) + k] = s1;
+    ts_end(ts);
 }
 
 // ------------------------------------------------------------------------------------
@@ -233,6 +238,7 @@ hipEvent_t KernelProfiler::get() {
     return e;
 }
 void KernelProfiler::flush() {
+    ts_flush();
     for (auto& r : recs) {
         float t = 0.f;
         (void)hipEventSynchronize(r.b);
@@ -244,6 +250,35 @@ void KernelProfiler::flush() {
         pool.push_back(r.b);
     }
     recs.clear();
+}
+unsigned long long* KernelProfiler::ts_slot(int kid, double b) {
+    if (!d_ts) {
+        void* p = nullptr;
+        if (hipMalloc(&p, sizeof(unsigned long long) * 2 * kTsSlots) != hipSuccess) return nullptr;
+        d_ts = (unsigned long long*)p;
+        (void)hipMemset(d_ts, 0xFF, sizeof(unsigned long long) * kTsSlots);
+        (void)hipMemset(d_ts + kTsSlots, 0, sizeof(unsigned long long) * kTsSlots);
+    }
+    if (ts_next == kTsSlots) ts_flush();
+    ts_recs.push_back({ts_next, kid, b});
+    return d_ts + ts_next++;
+}
+void KernelProfiler::ts_flush() {
+    if (!d_ts || ts_recs.empty()) return;
+    (void)hipDeviceSynchronize();
+    std::vector<unsigned long long> h(2 * (size_t)kTsSlots);
+    (void)hipMemcpy(h.data(), d_ts, sizeof(unsigned long long) * 2 * kTsSlots, hipMemcpyDeviceToHost);
+    for (const auto& r : ts_recs) {
+        const unsigned long long a = h[r.slot], e = h[(size_t)kTsSlots + r.slot];
+        if (a == ~0ull || e < a) continue;
+        ms[r.kid] += (double)(e - a) * 1e-5;  // 100 MHz ticks -> ms
+        bytes[r.kid] += r.bytes;
+        launches[r.kid] += 1;
+    }
+    ts_recs.clear();
+    ts_next = 0;
+    (void)hipMemset(d_ts, 0xFF, sizeof(unsigned long long) * kTsSlots);
+    (void)hipMemset(d_ts + kTsSlots, 0, sizeof(unsigned long long) * kTsSlots);
 }
 void KernelProfiler::reset() {
     flush();
@@ -389,14 +424,14 @@ void launch_base_convert(hipStream_t st, const DevTables& T, const ConvBatch& cb
         const bool own = cb.skip0[g] >= 0 && cb.skip0[g] < nt;
         w += cb.h[g] + nt - (own ? std::min(cb.h[g], nt - cb.skip0[g]) : 0);
     }
-    prof_launch(KID_BASE_CONVERT, words(w * (1u << T.logn)), k_base_convert,
+    prof_launch_ts(KID_BASE_CONVERT, words(w * (1u << T.logn)), k_base_convert,
                 dim3((1u << T.logn) / kBlock, (nt + kConvTargets - 1) / kConvTargets, cb.n), dim3(kBlock), 0, st, cb, nt, map, T.pc,
                 T.logn);
 }
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
                       int alpha, int nkey, int nks, LimbMap map) {
     // ext/d (nd x ne) + key (nd x 2 x ne) read, acc (2 x ne) written
-    prof_launch(KID_KEY_INNER, words((3.0 * nd + 2.0) * ne * (1u << T.logn)), k_key_inner, ew_grid(T.logn, ne), dim3(kBlock), 0, st, acc,
+    prof_launch_ts(KID_KEY_INNER, words((3.0 * nd + 2.0) * ne * (1u << T.logn)), k_key_inner, ew_grid(T.logn, ne), dim3(kBlock), 0, st, acc,
                 ext, d, key, nd, ne, nl, alpha, nkey, nks, map, T.pc, T.logn);
 }
 void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, u64 seed, u64 stream, int kind) {

@@ -15,11 +15,40 @@ extern thread_local KernelProfiler* g_prof;
 template <typename F, typename... Args>
 inline void prof_launch(int kid, double bytes, F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st, Args... args) {
     KernelProfiler* p = g_prof;
-    if (p && (p->mask >> kid & 1u)) {
+    if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) {
         hipEvent_t a = p->get(), b = p->get();
         hipExtLaunchKernelGGL(kernel, grid, block, (std::uint32_t)lds, st, a, b, 0u, args...);
         p->recs.push_back({a, b, kid, bytes});
     } else {
         hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
+    }
+}
+
+// launch of a kernel whose last parameter is an in-kernel clock slot (nullptr = untimed)
+template <typename F, typename... Args>
+inline void prof_launch_ts(int kid, double bytes, F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st, Args... args) {
+    KernelProfiler* p = g_prof;
+    unsigned long long* ts = nullptr;
+    if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) ts = p->ts_slot(kid, bytes);
+    hipLaunchKernelGGL(kernel, grid, block, lds, st, args..., ts);
+}
+
+// device side: the first thread of a sample of blocks (<= ~256 evenly spaced ones, always the
+// first and the last) widens the launch's [start, end] span; sampling keeps atomic contention
+// on the slot negligible for grids of thousands of blocks
+__device__ __forceinline__ bool ts_block() {
+    const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
+    const unsigned lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
+    const unsigned stride = nb > 256 ? nb / 256 : 1;
+    return lin % stride == 0 || lin == nb - 1;
+}
+__device__ __forceinline__ void ts_begin(unsigned long long* ts) {
+    if (ts && threadIdx.x == 0 && ts_block()) atomicMin(ts, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void ts_end(unsigned long long* ts) {
+    if (ts) {  // uniform: every thread of the block reaches the barrier
+        __syncthreads();
+        if (threadIdx.x == 0 && ts_block())
+            atomicMax(ts + KernelProfiler::kTsSlots, (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
 }

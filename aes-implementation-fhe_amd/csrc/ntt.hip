@@ -76,10 +76,11 @@ __device__ __forceinline__ RowAddr row_addr(u32* dst, const u32* src, const RowM
 // limb) and x = its centred representative reduced mod the target prime.
 template <int LOGR1, int MODE>
 __global__ void __launch_bounds__(kThreads) k_ntt1_fwd(u32* dst, const u32* src, RowMap rm, LimbMap map, const PrimeConst* pc,
-                                                       const u32* psi, const u32* psip, NttAux aux) {
+                                                       const u32* psi, const u32* psip, NttAux aux, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8, R1 = 1 << LOGR1, T = R1 / 16, CB = kThreads / T;
     __shared__ u32 sm[R1 * CB];
     if (skipped(rm)) return;
+    ts_begin(ts);
     RowAddr ra = row_addr<LOGN>(dst, src, rm, map);
     const u32 q = pc[ra.prime].q;
     const u32* w = psi + ((size_t)ra.prime << LOGN);
@@ -130,6 +131,7 @@ __global__ void __launch_bounds__(kThreads) k_ntt1_fwd(u32* dst, const u32* src,
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k) ra.dst[(size_t)(16 * g + k) * 256 + c] = x[k];
+    ts_end(ts);
 }
 
 // ---------------------------------------------------------------- forward, pass 2 (in place on dst rows)
@@ -138,10 +140,11 @@ __global__ void __launch_bounds__(kThreads) k_ntt1_fwd(u32* dst, const u32* src,
 // through aux (cur row g * cur_stride + i, out row g * out_stride + i).
 template <int LOGR1, int MODE>
 __global__ void __launch_bounds__(kThreads) k_ntt2_fwd(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const u32* psi,
-                                                       const u32* psip, NttAux aux) {
+                                                       const u32* psip, NttAux aux, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8;
     __shared__ u32 sm[kRowsP2 * kPitchP2];
     if (skipped(rm)) return;
+    ts_begin(ts);
     const RowAddr ra = row_addr<LOGN>(data, data, rm, map);
     const u32 q = pc[ra.prime].q;
     const u32* w = psi + ((size_t)ra.prime << LOGN);
@@ -208,15 +211,17 @@ __global__ void __launch_bounds__(kThreads) k_ntt2_fwd(u32* data, RowMap rm, Lim
 #pragma unroll
         for (int v = 0; v < 4; ++v) o[v] = make_uint4(x[4 * v], x[4 * v + 1], x[4 * v + 2], x[4 * v + 3]);
     }
+    ts_end(ts);
 }
 
 // ---------------------------------------------------------------- inverse, pass 2 (src -> dst)
 template <int LOGR1>
 __global__ void __launch_bounds__(kThreads) k_ntt2_inv(u32* dst, const u32* src, RowMap rm, LimbMap map, const PrimeConst* pc,
-                                                       const u32* ipsi, const u32* ipsip) {
+                                                       const u32* ipsi, const u32* ipsip, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8;
     __shared__ u32 sm[kRowsP2 * kPitchP2];
     if (skipped(rm)) return;
+    ts_begin(ts);
     const RowAddr ra = row_addr<LOGN>(dst, src, rm, map);
     const u32 q = pc[ra.prime].q;
     const u32* w = ipsi + ((size_t)ra.prime << LOGN);
@@ -261,15 +266,17 @@ __global__ void __launch_bounds__(kThreads) k_ntt2_inv(u32* dst, const u32* src,
     u32* p = ra.dst + (size_t)R * 256;
 #pragma unroll
     for (int k = 0; k < 16; ++k) p[j + 16 * k] = x[k];
+    ts_end(ts);
 }
 
 // ---------------------------------------------------------------- inverse, pass 1 (in place on dst rows)
 template <int LOGR1>
 __global__ void __launch_bounds__(kThreads) k_ntt1_inv(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const u32* ipsi,
-                                                       const u32* ipsip) {
+                                                       const u32* ipsip, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8, R1 = 1 << LOGR1, T = R1 / 16, CB = kThreads / T;
     __shared__ u32 sm[R1 * CB];
     if (skipped(rm)) return;
+    ts_begin(ts);
     const RowAddr ra = row_addr<LOGN>(data, data, rm, map);
     const PrimeConst P = pc[ra.prime];
     const u32 q = P.q;
@@ -307,6 +314,7 @@ __global__ void __launch_bounds__(kThreads) k_ntt1_inv(u32* data, RowMap rm, Lim
     }
 #pragma unroll
     for (int k = 0; k < 16; ++k) ra.dst[(size_t)(g + T * k) * 256 + c] = shoup_mul(x[k], P.ninv, P.ninv_p, q);
+    ts_end(ts);
 }
 
 // io_rows: rows actually transformed (launch rows minus skipped ones), for the byte count
@@ -317,18 +325,18 @@ void ntt_fwd_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
     const double row_bytes = 4.0 * 256.0 * R1;
     const double io1 = 2.0 * io_rows * row_bytes;
     const double io2 = (M2 == kFinish ? (3.0 + (aux.add0 ? 0.5 : 0.0) + (aux.add1 ? 0.5 : 0.0)) : 2.0) * io_rows * row_bytes;
-    prof_launch(KID_NTT_COLS_FWD, io1, k_ntt1_fwd<LOGR1, M1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, src, rm, map, Tb.pc,
+    prof_launch_ts(KID_NTT_COLS_FWD, io1, k_ntt1_fwd<LOGR1, M1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, src, rm, map, Tb.pc,
                 Tb.psi, Tb.psip, aux);
-    prof_launch(KID_NTT_ROWS_FWD, io2, k_ntt2_fwd<LOGR1, M2>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, rm, map, Tb.pc,
+    prof_launch_ts(KID_NTT_ROWS_FWD, io2, k_ntt2_fwd<LOGR1, M2>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, rm, map, Tb.pc,
                 Tb.psi, Tb.psip, aux);
 }
 template <int LOGR1>
 void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {
     constexpr int R1 = 1 << LOGR1, CB = kThreads / (R1 / 16);
     const double io = 4.0 * 2.0 * rows * (256.0 * R1);  // the inverse is never launched with skips
-    prof_launch(KID_NTT_ROWS_INV, io, k_ntt2_inv<LOGR1>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, src, rm, map, Tb.pc,
+    prof_launch_ts(KID_NTT_ROWS_INV, io, k_ntt2_inv<LOGR1>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, src, rm, map, Tb.pc,
                 Tb.ipsi, Tb.ipsip);
-    prof_launch(KID_NTT_COLS_INV, io, k_ntt1_inv<LOGR1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, rm, map, Tb.pc, Tb.ipsi,
+    prof_launch_ts(KID_NTT_COLS_INV, io, k_ntt1_inv<LOGR1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, rm, map, Tb.pc, Tb.ipsi,
                 Tb.ipsip);
 }
 

@@ -38,7 +38,7 @@ EXPORTED = [
     "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
     "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
     "aesfhe_streams", "aesfhe_bind_stream", "aesfhe_fork", "aesfhe_join", "aesfhe_settle",
-    "aesfhe_profile", "aesfhe_kernel_stats", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan",
+    "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan",
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group",
 ]
@@ -92,7 +92,7 @@ def load_library(path: Optional[Path] = None):
         "aesfhe_set_lazy": [vp, c_int],
         "aesfhe_streams": [vp], "aesfhe_bind_stream": [vp, c_int], "aesfhe_fork": [vp], "aesfhe_join": [vp], "aesfhe_settle": [vp, _H],
         "aesfhe_reset_counters": [vp],
-        "aesfhe_profile": [vp, ctypes.c_uint32],
+        "aesfhe_profile": [vp, ctypes.c_uint32], "aesfhe_profile_every": [vp, c_int],
         "aesfhe_kernel_stats": [vp, _dp, c_int, c_int],
     }
     sig["aesfhe_bootstrap_depth"] = []
@@ -523,11 +523,13 @@ class Engine:
         self._ctx.check(self._lib.aesfhe_bench_op(self._ctx.ptr, self.BENCH_OPS[op], int(arg), int(iters), ctypes.byref(us)))
         return us.value
 
-    def profile(self, kernels=()):
-        """Enable HIP-event timing for the named kernel ids (see KERNEL_IDS); () disables."""
+    def profile(self, kernels=(), every: int = 1):
+        """Enable HIP-event timing for the named kernel ids (see KERNEL_IDS); () disables.
+        every > 1 times one launch in `every` of each (a live sample, less overhead)."""
         mask = 0
         for k in kernels:
             mask |= 1 << KERNEL_IDS.index(k)
+        self._ctx.check(self._lib.aesfhe_profile_every(self._ctx.ptr, int(every)))
         self._ctx.check(self._lib.aesfhe_profile(self._ctx.ptr, mask))
 
     def kernel_stats(self, reset: bool = True) -> dict:

@@ -154,6 +154,9 @@ int aesfhe_debug_keyswitch(aesfhe_ctx* ctx, int level, uint64_t galois, const ui
  * 4: ct x ct + relinearise + rescale at level arg.  MI355X-side tooling. */
 int aesfhe_bench_op(aesfhe_ctx* ctx, int op, int arg, int iters, double* us);
 int aesfhe_counters(aesfhe_ctx* ctx, uint64_t* out, int n);
+/* time only one launch in `every` of each enabled kernel (default 1): an unbiased live sample
+ * with less event overhead in the measured run */
+int aesfhe_profile_every(aesfhe_ctx* ctx, int every);
 /* live kernel timing with HIP events on the engine stream: bit k of mask enables kernel id k
  * (order: ntt_cols_fwd, ntt_rows_fwd, ntt_rows_inv, ntt_cols_inv, base_convert, key_inner,
  * moddown, tensor, rescale, automorph, elementwise, sample); stats: per id

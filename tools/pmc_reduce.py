@@ -2,7 +2,7 @@
 
 gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of
 wide coalesced reads -> x2; WRITE_SIZE is exact.  Both counters are in KB.  Usage:
-  python tools/pmc_reduce.py OUT.json DIR [DIR ...]   (one DIR per --pmc pass)
+  python tools/pmc_reduce.py [--source=LABEL] OUT.json DIR [DIR ...]   (one DIR per --pmc pass)
 Deletes the (large) CSVs after reading so gpurun can copy the result back."""
 import csv
 import json
@@ -22,7 +22,11 @@ def short(name: str) -> str:
 
 
 def main():
-    out, dirs = Path(sys.argv[1]), sys.argv[2:]
+    src = None
+    args = sys.argv[1:]
+    if args and args[0].startswith("--source="):
+        src, args = args[0].split("=", 1)[1], args[1:]
+    out, dirs = Path(args[0]), args[1:]
     acc = defaultdict(lambda: defaultdict(float))
     cnt = defaultdict(lambda: defaultdict(int))
     for d in dirs:
@@ -42,6 +46,20 @@ def main():
         per = {c: acc[k][c] / cnt[k][c] for c in acc[k]}
         res[k] = {"bytes_per_launch": sum(per.values()), "launches": max(cnt[k].values()),
                   **{c.lower() + "_bytes": v for c, v in per.items()}}
+    # aggregate template instances under the engine's kernel ids (launch-weighted)
+    ids = {"ntt1_fwd": "ntt_cols_fwd", "ntt2_fwd": "ntt_rows_fwd", "ntt2_inv": "ntt_rows_inv", "ntt1_inv": "ntt_cols_inv",
+           "key_inner": "key_inner", "base_convert": "base_convert"}
+    agg = {}
+    for k, v in list(res.items()):
+        kid = ids.get(k.split("<")[0])
+        if kid and kid != k:
+            a = agg.setdefault(kid, {"bytes": 0.0, "launches": 0})
+            a["bytes"] += v["bytes_per_launch"] * v["launches"]
+            a["launches"] += v["launches"]
+    for kid, a in agg.items():
+        res[kid] = {"bytes_per_launch": a["bytes"] / max(a["launches"], 1), "launches": a["launches"]}
+    if src:
+        res["_source"] = src
     out.write_text(json.dumps(res, indent=1))
     print(json.dumps(res))
 
