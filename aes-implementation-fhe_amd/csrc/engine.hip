@@ -111,13 +111,21 @@ struct Ct {
     bool zero = false;
 };
 
+// coefficient set of a fused LUT evaluation: C[n_a][n_b] (n_b = 1: univariate)
+struct Lut {
+    int n_a = 0, n_b = 0;
+    std::vector<double> re, im;
+    double c0_re = 0.0, c0_im = 0.0;
+    std::map<std::string, std::pair<u32*, size_t>> cst;  // (output level, element levels) -> constants
+};
+
 struct Pt {
     std::vector<double> re, im;
     bool constant = false;
     std::map<int, std::pair<u32*, size_t>> enc;  // 2*level + mult -> (NTT-form encoding, words)
 };
 
-enum Counter { C_MUL, C_RELIN, C_ROT, C_CONJ, C_PTMUL, C_SCALAR, C_RESCALE, C_NTT_ROWS, C_KS, C_ENC, C_DEC, C_BOOT, C_ADD, C_N };
+enum Counter { C_MUL, C_RELIN, C_ROT, C_CONJ, C_PTMUL, C_SCALAR, C_RESCALE, C_NTT_ROWS, C_KS, C_ENC, C_DEC, C_BOOT, C_ADD, C_LUT, C_N };
 
 class Engine {
 public:
@@ -231,6 +239,12 @@ public:
         if (it != cts_.end()) {
             give_back(it->second.data, it->second.words);
             cts_.erase(it);
+            return;
+        }
+        auto il = luts_.find(h);
+        if (il != luts_.end()) {
+            for (auto& e : il->second.cst) give_back(e.second.first, e.second.second);
+            luts_.erase(il);
             return;
         }
         auto ip = pts_.find(h);
@@ -975,6 +989,125 @@ public:
         o.lazy = c_in.lazy && o.npoly == 3;
         launch_add(S(), T_, o.data, c.data, e, nl, nl, qmap());
         if (c.data != c_in.data) release(c);
+        return o;
+    }
+
+    // ------------------------------------------------------------------ fused LUT evaluation
+    aesfhe_handle lut_create(int n_a, int n_b, const double* re, const double* im, double c0_re, double c0_im) {
+        if (n_a < 1 || n_b < 1 || (n_b > 1 && (n_a > kLutMax || n_b > kLutMax)))
+            throw std::runtime_error("lut_create: bad shape (bivariate LUTs are at most 16 x 16)");
+        Lut L;
+        L.n_a = n_a, L.n_b = n_b;
+        L.re.assign(re, re + (size_t)n_a * n_b);
+        L.im.assign(im, im + (size_t)n_a * n_b);
+        L.c0_re = c0_re, L.c0_im = c0_im;
+        const aesfhe_handle h = next_++;
+        luts_.emplace(h, std::move(L));
+        return h;
+    }
+    Lut& lut(aesfhe_handle h) {
+        auto it = luts_.find(h);
+        if (it == luts_.end()) throw std::runtime_error("invalid LUT handle");
+        return it->second;
+    }
+    // Shoup pairs of the integer constants round(c_j f_j), per term j, limb t < nl, slot half
+    const u32* lut_consts(Lut& L, const std::string& key, const std::vector<std::pair<int, double>>& terms, int nl) {
+        auto it = L.cst.find(key);
+        if (it != L.cst.end()) return it->second.first;
+        std::vector<u32> h(terms.size() * (size_t)nl * 4);
+        std::vector<u32> lo, hi;
+        for (size_t j = 0; j < terms.size(); ++j) {
+            const int c = terms[j].first;
+            const double f = terms[j].second;
+            const double a = L.re[c] * f, b = L.im[c] * f;
+            if (std::fabs(a) > 9.0e18 || std::fabs(b) > 9.0e18) throw std::runtime_error("level: LUT constant out of range");
+            scalar_residues(std::llround(a), std::llround(b), nl, lo, hi);
+            for (int t = 0; t < nl; ++t) {
+                u32* e = &h[(j * nl + t) * 4];
+                e[0] = lo[t], e[1] = shoup_pre(lo[t], hp_.mod[t]);
+                e[2] = hi[t], e[3] = shoup_pre(hi[t], hp_.mod[t]);
+            }
+        }
+        const size_t words = (h.size() + (size_t)hp_.n - 1) / hp_.n * hp_.n;
+        u32* d = alloc_words(words);
+        HIP_OK(hipMemcpyAsync(d, h.data(), h.size() * sizeof(u32), hipMemcpyHostToDevice, S()));
+        HIP_OK(hipStreamSynchronize(S()));  // cached for every stream; host vector dies here
+        L.cst[key] = {d, words};
+        return d;
+    }
+    // sum_{p,q} C_pq A_p B_q (n_b > 1) or sum_p C_p A_p + c0 (n_b = 1), as a deferred tensor at
+    // the lowest data level l of the elements used: (l, 2 owed rescales, 3 polys) or
+    // (l, 1 owed rescale, 2 polys) -- the same logical level as the per-term products
+    Ct lut_eval(aesfhe_handle hl, const aesfhe_handle* A, const aesfhe_handle* B) {
+        Lut& L = lut(hl);
+        const bool bi = L.n_b > 1;
+        if (!A || (bi && !B)) throw std::runtime_error("lut_eval: missing element handles");
+        std::vector<const Ct*> ea(L.n_a, nullptr), eb(bi ? L.n_b : 0, nullptr);
+        double mag = std::hypot(L.c0_re, L.c0_im);
+        for (int p = 0; p < L.n_a; ++p)
+            for (int q = 0; q < L.n_b; ++q) {
+                const size_t c = (size_t)p * L.n_b + q;
+                if (L.re[c] == 0.0 && L.im[c] == 0.0) continue;
+                mag += std::hypot(L.re[c], L.im[c]);
+                if (!ea[p]) ea[p] = &canon(A[p]);
+                if (bi && !eb[q]) eb[q] = &canon(B[q]);
+            }
+        int l = 1 << 30;
+        for (auto* e : ea) if (e) l = std::min(l, e->level);
+        for (auto* e : eb) if (e) l = std::min(l, e->level);
+        if (l == (1 << 30)) throw std::runtime_error("lut_eval: all coefficients are zero");
+        for (auto* e : ea) if (e && e->npoly != 2) throw std::runtime_error("lut_eval expects 2-polynomial ciphertexts");
+        for (auto* e : eb) if (e && e->npoly != 2) throw std::runtime_error("lut_eval expects 2-polynomial ciphertexts");
+        const int pend = bi ? 2 : 1;
+        if (l - pend < 0 || !headroom(l, pend, mag)) throw std::runtime_error("not enough level for the fused LUT (level)");
+        const int nl = hp_.nl(l);
+        const double S_out = raw_scale(l, pend);
+        std::string key = std::to_string(l) + ":";
+        for (auto* e : ea) key += (e ? std::to_string(e->level) : "-") + ",";
+        for (auto* e : eb) key += (e ? std::to_string(e->level) : "-") + ",";
+        Ct o;
+        if (bi) {
+            LutOperands op{};
+            std::vector<std::pair<int, double>> terms;
+            int j = 0;
+            for (int p = 0; p < L.n_a; ++p) {
+                op.p_start[p] = j;
+                for (int q = 0; q < L.n_b; ++q) {
+                    const size_t c = (size_t)p * L.n_b + q;
+                    if (L.re[c] == 0.0 && L.im[c] == 0.0) continue;
+                    op.q_of[j++] = (unsigned char)q;
+                    terms.push_back({(int)c, S_out / (hp_.delta[ea[p]->level] * hp_.delta[eb[q]->level])});
+                }
+                op.a[p] = ea[p] ? ea[p]->data : nullptr;
+                op.na[p] = ea[p] ? hp_.nl(ea[p]->level) : 0;
+            }
+            for (int p = L.n_a; p <= kLutMax; ++p) op.p_start[p] = j;
+            for (int q = 0; q < L.n_b; ++q) op.b[q] = eb[q] ? eb[q]->data : nullptr, op.nb[q] = eb[q] ? hp_.nl(eb[q]->level) : 0;
+            const u32* cst = lut_consts(L, key, terms, nl);
+            o = alloc_ct(l, 3);
+            launch_lut_bivariate(S(), T_, o.data, op, L.n_a, cst, nl);
+        } else {
+            std::vector<std::pair<int, double>> terms;
+            std::vector<int> idx;
+            for (int p = 0; p < L.n_a; ++p)
+                if (ea[p]) terms.push_back({p, S_out / hp_.delta[ea[p]->level]}), idx.push_back(p);
+            const u32* cst = lut_consts(L, key, terms, nl);
+            o = alloc_ct(l, 2);
+            for (size_t c0 = 0; c0 < idx.size(); c0 += kLutChunk) {
+                LutChunk ch{};
+                const int n = (int)std::min<size_t>(kLutChunk, idx.size() - c0);
+                for (int j = 0; j < n; ++j) ch.x[j] = ea[idx[c0 + j]]->data, ch.nx[j] = hp_.nl(ea[idx[c0 + j]]->level);
+                launch_lut_univariate(S(), T_, o.data, c0 ? o.data : nullptr, ch, n, cst + c0 * (size_t)nl * 4, 2, nl);
+            }
+        }
+        o.pend = pend;
+        o.lazy = true;
+        cnt_[C_LUT]++;
+        if (!bi && (L.c0_re != 0.0 || L.c0_im != 0.0)) {
+            Ct r = add_scalar(o, L.c0_re, L.c0_im);
+            release(o);
+            o = r;
+        }
         return o;
     }
 
@@ -1843,6 +1976,7 @@ private:
     u32* d_negp_ = nullptr;
     u64 cnt_[C_N] = {};
     CrtConsts crt_[4] = {};
+    std::unordered_map<aesfhe_handle, Lut> luts_;
     Slot16 slots_ = {};
     double* d_codec_[kStreams] = {};
     int* d_nib_[kStreams] = {};
@@ -2016,6 +2150,14 @@ int aesfhe_mul_scalar(aesfhe_ctx* ctx, aesfhe_handle c, double re, double im, ae
 int aesfhe_mul_pt(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle p, aesfhe_handle* out) { CT_OP(e.mul_pt(e.ct(c), p, e.lazy())) }
 int aesfhe_mul(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int relin, aesfhe_handle* out) {
     CT_OP(e.mul(e.canon(a), e.canon(b), relin != 0, e.lazy()))
+}
+int aesfhe_lut_create(aesfhe_ctx* ctx, int n_a, int n_b, const double* re, const double* im, double c0_re, double c0_im,
+                      aesfhe_handle* out) {
+    API_BEGIN* out = ctx->eng->lut_create(n_a, n_b, re, im, c0_re, c0_im);
+    API_END
+}
+int aesfhe_lut_eval(aesfhe_ctx* ctx, aesfhe_handle lut, const aesfhe_handle* a, const aesfhe_handle* b, aesfhe_handle* out) {
+    CT_OP(e.lut_eval(lut, a, b))
 }
 int aesfhe_set_lazy(aesfhe_ctx* ctx, int on) {
     API_BEGIN ctx->eng->set_lazy(on != 0);

@@ -176,3 +176,27 @@ void launch_snap16(hipStream_t st, const double* acc, double* w, int* nib);
 // out[c][t][k] = round(scale (delta_{k0} + (2/N) Re sum_i w_ci e^{-i pi e_i k / N})) mod q_t, t < nq
 void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq);
 
+// --- fused LUT evaluation ---------------------------
+// Elements are canonical ciphertexts at data levels >= the output level l; only their first
+// nl(l) limbs are read (exact modulo Q_l) and each element's own scale is folded into the
+// integer constants.  Constants: cst[term][limb][half][Shoup pair] (half = slot half of
+// the constant a + b X^{N/2}).
+constexpr int kLutMax = 16;
+struct LutOperands {
+    const u32* a[kLutMax];  // A_p, 2 polys of na[p] limbs each
+    const u32* b[kLutMax];
+    int na[kLutMax], nb[kLutMax];
+    int p_start[kLutMax + 1];  // terms of A_p: [p_start[p], p_start[p + 1]) in q_of
+    unsigned char q_of[kLutMax * kLutMax];
+};
+// out (3 polys, nl rows each) = sum_p A_p (x) (sum_q C_pq B_q)
+void launch_lut_bivariate(hipStream_t st, const DevTables& T, u32* out, const LutOperands& op, int n_a, const u32* cst, int nl);
+// chunk of a univariate sum: out (npoly x nl) = (acc ? acc : 0) + sum_{k < n} C_k X_k
+constexpr int kLutChunk = 32;
+struct LutChunk {
+    const u32* x[kLutChunk];
+    int nx[kLutChunk];
+};
+void launch_lut_univariate(hipStream_t st, const DevTables& T, u32* out, const u32* acc, const LutChunk& ch, int n, const u32* cst,
+                           int npoly, int nl);
+

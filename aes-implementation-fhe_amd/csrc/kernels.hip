@@ -376,6 +376,57 @@ __global__ void __launch_bounds__(kBlock) k_encode16(u32* out, const double* w, 
     }
 }
 
+// ------------------------------------------------------------------------------------
+// fused LUT evaluation: one launch per LUT instead of a tensor + constant + add per term
+// ------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock) k_lut_bivariate(u32* out, LutOperands op, int n_a, const u32* cst, int nl,
+                                                          const PrimeConst* pc, int logn) {
+    const int t = blockIdx.y;
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const int half = (int)(k >> (logn - 1));
+    const PrimeConst P = pc[t];
+    const u32 q = P.q;
+    const size_t off = ((size_t)t << logn) + k;
+    u32 acc0 = 0, acc1 = 0, acc2 = 0;
+    for (int p = 0; p < n_a; ++p) {
+        const int t0 = op.p_start[p], t1 = op.p_start[p + 1];
+        if (t0 == t1) continue;
+        u32 u0 = 0, u1 = 0;
+        for (int j = t0; j < t1; ++j) {
+            const int qq = op.q_of[j];
+            const u32* bq = op.b[qq];
+            const u32* c = cst + ((size_t)j * nl + t) * 4 + 2 * half;
+            u0 = add_mod(u0, shoup_mul(bq[off], c[0], c[1], q), q);
+            u1 = add_mod(u1, shoup_mul(bq[((size_t)op.nb[qq] << logn) + off], c[0], c[1], q), q);
+        }
+        const u32 a0 = op.a[p][off], a1 = op.a[p][((size_t)op.na[p] << logn) + off];
+        acc0 = add_mod(acc0, barrett_mul(a0, u0, q, P.mu), q);
+        acc1 = add_mod(acc1, add_mod(barrett_mul(a0, u1, q, P.mu), barrett_mul(a1, u0, q, P.mu), q), q);
+        acc2 = add_mod(acc2, barrett_mul(a1, u1, q, P.mu), q);
+    }
+    out[off] = acc0;
+    out[((size_t)nl << logn) + off] = acc1;
+    out[((size_t)(2 * nl) << logn) + off] = acc2;
+}
+
+__global__ void __launch_bounds__(kBlock) k_lut_univariate(u32* out, const u32* acc, LutChunk ch, int n, const u32* cst, int npoly,
+                                                           int nl, const PrimeConst* pc, int logn) {
+    const int t = blockIdx.y;
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const int half = (int)(k >> (logn - 1));
+    const u32 q = pc[t].q;
+    const size_t off = ((size_t)t << logn) + k;
+    for (int p = 0; p < npoly; ++p) {
+        const size_t o = ((size_t)(p * nl) << logn) + off;
+        u32 v = acc ? acc[o] : 0;
+        for (int j = 0; j < n; ++j) {
+            const u32* c = cst + ((size_t)j * nl + t) * 4 + 2 * half;
+            v = add_mod(v, shoup_mul(ch.x[j][((size_t)(p * ch.nx[j]) << logn) + off], c[0], c[1], q), q);
+        }
+        out[o] = v;
+    }
+}
+
 inline double words(double w) { return 4.0 * w; }
 }  // namespace
 
@@ -458,5 +509,19 @@ void launch_snap16(hipStream_t st, const double* acc, double* w, int* nib) {
 void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq) {
     prof_launch(KID_ELEMENTWISE, words(2.0 * nq * (1u << T.logn)), k_encode16, dim3((1u << T.logn) / kBlock, 2), dim3(kBlock), 0, st, out,
                 w, sl, scale, nq, T.pc, T.logn);
+}
+
+void launch_lut_bivariate(hipStream_t st, const DevTables& T, u32* out, const LutOperands& op, int n_a, const u32* cst, int nl) {
+    double reads = 0;
+    for (int p = 0; p < n_a; ++p)
+        if (op.p_start[p + 1] > op.p_start[p]) reads += 2;
+    reads += 2.0 * kLutMax;  // upper bound on the B elements read
+    prof_launch(KID_ELEMENTWISE, words((reads + 3.0) * nl * (1u << T.logn)), k_lut_bivariate, ew_grid(T.logn, nl), dim3(kBlock), 0,
+                st, out, op, n_a, cst, nl, T.pc, T.logn);
+}
+void launch_lut_univariate(hipStream_t st, const DevTables& T, u32* out, const u32* acc, const LutChunk& ch, int n, const u32* cst,
+                           int npoly, int nl) {
+    prof_launch(KID_ELEMENTWISE, words((double)(n + (acc ? 2 : 1)) * npoly * nl * (1u << T.logn)), k_lut_univariate,
+                ew_grid(T.logn, nl), dim3(kBlock), 0, st, out, acc, ch, n, cst, npoly, nl, T.pc, T.logn);
 }
 

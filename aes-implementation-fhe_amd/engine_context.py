@@ -4,10 +4,13 @@ the MI355X engine (mi355x_ckks, a ctypes binding of libaesfhe.so).
 Same constructor keywords, same methods, same error-string behaviour; the AES round
 modules only ever talk to this object.  Extra keywords: ``log_n`` (N = 2^log_n, default
 2^16 as in the reference harness; config 1 of BASELINE.json uses 2^15), ``dnum`` and
-``seed`` (deterministic key material) and ``lazy`` (deferred relinearisation).
+``seed`` (deterministic key material), ``lazy`` (deferred relinearisation),
+``concurrent`` (hi / lo halves on two HIP streams) and ``fused_luts`` (one-kernel LUT sums,
+DESIGN.md §3.8).
 """
 from __future__ import annotations
 
+import threading
 import time
 
 import numpy as np
@@ -21,7 +24,7 @@ class EngineContext:
     def __init__(self, signature: int, *, max_level: int = 17, use_bootstrap: bool = True,
                  use_multiparty: bool = False, mode: str = "cpu", device_id: int = 0,
                  thread_count: int | None = None, log_n: int = 16, dnum: int | None = None, seed: int = 0x5EED,
-                 lazy: bool = True, concurrent: bool = True):
+                 lazy: bool = True, concurrent: bool = True, fused_luts: bool = True):
         # REF/engine_context.py:17-42: signature selects the engine constructor form
         if signature == 1:
             kw = dict(use_bootstrap=use_bootstrap, max_level=_SIG_DEFAULT_LEVEL)
@@ -45,6 +48,9 @@ class EngineContext:
         self.bootstrap_key = eng.create_bootstrap_key(self.secret_key)
         self._bs_count = 0
         self._bs_total_s = 0.0
+        self.fused_luts = bool(fused_luts)
+        self._luts = {}
+        self._lut_lock = threading.Lock()
 
     # -------------------------------------------------------------- codec
     def encrypt(self, data: np.ndarray):
@@ -160,3 +166,15 @@ class EngineContext:
     def renorm_pair(self, hi, lo):
         """Device-side Zeta16 secret-key renorm of a (hi, lo) state pair (REF/pipeline.py:65-69)."""
         return self.engine.renorm_pair(hi, lo)
+
+    def lut(self, key, coeffs, c0: complex = 0j):
+        """Engine-side coefficient set of a LUT polynomial, created once per key."""
+        with self._lut_lock:
+            t = self._luts.get(key)
+            if t is None:
+                t = self._luts[key] = self.engine.lut_create(coeffs, c0)
+            return t
+
+    def lut_eval(self, lut, a, b=None):
+        """sum C[p,q] a[p] b[q] (or c0 + sum C[k] a[k]) in one fused kernel."""
+        return self.engine.lut_eval(lut, a, b)

@@ -6,7 +6,7 @@ from __future__ import annotations
 
 from typing import Any, Dict, List
 
-from mixcol_final import _CoeffCache, gf_basis16, gf_poly_eval
+from mixcol_final import _CoeffCache, gf_basis16, gf_eval
 from shift_rows import row_masks
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT
@@ -28,7 +28,7 @@ class InvMixColumnsFHE:
         return gf_basis16(self.ctx, ct)
 
     def _poly2_eval(self, ct_hi, ct_lo, mult: int, which: str):
-        return gf_poly_eval(self.ctx, self._coeffs.load_plaintexts(self.ctx, mult, which), ct_hi, ct_lo)
+        return gf_eval(self.ctx, self._coeffs, mult, which, ct_hi, ct_lo)
 
     def _xor(self, a, b):
         return self.xor4.apply(a, b)

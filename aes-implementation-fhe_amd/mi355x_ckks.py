@@ -40,7 +40,7 @@ EXPORTED = [
     "aesfhe_streams", "aesfhe_bind_stream", "aesfhe_fork", "aesfhe_join", "aesfhe_settle",
     "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan",
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot",
-    "aesfhe_level_limbs", "aesfhe_debug_lin_group",
+    "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_lut_create", "aesfhe_lut_eval",
 ]
 
 KERNEL_IDS = ["ntt_cols_fwd", "ntt_rows_fwd", "ntt_rows_inv", "ntt_cols_inv", "base_convert", "key_inner",
@@ -51,7 +51,7 @@ KERNEL_SYMBOLS = {"ntt_cols_fwd": "k_ntt_cols_fwd", "ntt_rows_fwd": "k_ntt_rows_
                   "moddown": "k_moddown_finish", "tensor": "k_tensor", "automorph": "k_automorph"}
 
 COUNTER_NAMES = ["mul", "relin", "rot", "conj", "ptmul", "scalar", "rescale", "ntt_rows", "keyswitch",
-                 "encrypt", "decrypt", "bootstrap", "add"]
+                 "encrypt", "decrypt", "bootstrap", "add", "lut"]
 
 
 def load_library(path: Optional[Path] = None):
@@ -102,6 +102,8 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_boot_info"] = [vp, _dp]
     sig["aesfhe_debug_lin_group"] = [vp, _H, c_int, _Hp]
     sig["aesfhe_create_boot"] = [pp, c_int, c_int, c_int, c_int, ctypes.c_uint64]
+    sig["aesfhe_lut_create"] = [vp, c_int, c_int, _dp, _dp, c_dbl, c_dbl, _Hp]
+    sig["aesfhe_lut_eval"] = [vp, _H, _Hp, _Hp, _Hp]
     sig["aesfhe_level_limbs"] = [vp, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")]
     for name in EXPORTED:
         fn = getattr(L, name)
@@ -178,6 +180,12 @@ class Plaintext(_Handle):
     """Encoded slot vector; encoded at the level of the ciphertext it meets."""
 
     __slots__ = ()
+
+
+class LookupTable(_Handle):
+    """Coefficient set of a fused LUT evaluation (aesfhe_lut_create)."""
+
+    __slots__ = ("n_a", "n_b")
 
 
 class _Key:
@@ -451,6 +459,38 @@ class Engine:
     def sync(self):
         self._ctx.check(self._lib.aesfhe_sync(self._ctx.ptr))
 
+    # ------------------------------------------------------------------ fused LUT evaluation
+    def lut_create(self, coeffs, c0: complex = 0j) -> LookupTable:
+        """coeffs: (n_a, n_b) matrix of a bivariate LUT sum_{p,q} C[p,q] A_p B_q, or a vector of
+        a univariate one c0 + sum_k C[k] A_k."""
+        c = np.asarray(coeffs, dtype=np.complex128)
+        c2 = c.reshape(c.shape[0], 1) if c.ndim == 1 else c
+        re, im = np.ascontiguousarray(c2.real), np.ascontiguousarray(c2.imag)
+        h = ctypes.c_uint64()
+        c0 = complex(c0)
+        self._ctx.check(self._lib.aesfhe_lut_create(self._ctx.ptr, c2.shape[0], c2.shape[1] if c.ndim == 2 else 1,
+                                                    np.ascontiguousarray(re, np.float64), np.ascontiguousarray(im, np.float64),
+                                                    c0.real, c0.imag, ctypes.byref(h)))
+        t = LookupTable(self._ctx, h.value)
+        t.n_a, t.n_b = c2.shape[0], (c2.shape[1] if c.ndim == 2 else 1)
+        return t
+
+    def lut_eval(self, lut: LookupTable, a, b=None) -> Ciphertext:
+        """One fused kernel for the LUT sum over the element ciphertexts a[p] (b[q]); a / b are
+        sequences or dicts index -> Ciphertext (missing = unused).  Raises RuntimeError with
+        "level" in the message when the elements are too low for the fused form."""
+        def handles(x, n):
+            arr = (ctypes.c_uint64 * n)()
+            items = x.items() if isinstance(x, dict) else enumerate(x)
+            for k, ct in items:
+                if ct is not None and 0 <= k < n:
+                    arr[k] = ct.handle
+            return arr
+        self._ensure_keys()
+        ha = handles(a, lut.n_a)
+        hb = handles(b, lut.n_b) if lut.n_b > 1 else None
+        return self._new(self._lib.aesfhe_lut_eval, lut.handle, ha, hb)
+
     # ------------------------------------------------------------------ raw access (tests)
     def moduli(self) -> np.ndarray:
         out = np.zeros(self.n_q + self.n_p, np.uint32)
@@ -469,6 +509,7 @@ class Engine:
         return out
 
     def import_ct(self, data: np.ndarray, level: int) -> Ciphertext:
+        self._ensure_keys()
         data = np.ascontiguousarray(data, np.uint32)
         return self._new(self._lib.aesfhe_import, int(level), int(data.shape[0]), data)
 

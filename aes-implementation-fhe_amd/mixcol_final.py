@@ -16,7 +16,7 @@ import numpy as np
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT
-from utils import pair
+from utils import fused_lut, pair
 
 
 class _CoeffCache:
@@ -25,14 +25,28 @@ class _CoeffCache:
     def __init__(self, coeff_dir=COEFF_DIR):
         self.dir = coeff_dir
         self.pt_cache: Dict[Tuple[int, str], Dict[Tuple[int, int], Any]] = {}
+        self.mat_cache: Dict[Tuple[int, str], np.ndarray] = {}
+
+    def _entries(self, mult: int, which: str):
+        path = ensure_coeffs(self.dir) / f"gf_mult{mult}_{which}_coeffs.json"
+        return json.loads(path.read_text(encoding="utf-8"))["entries"]
+
+    def matrix(self, mult: int, which: str) -> np.ndarray:
+        """the same coefficients as a dense 16 x 16 matrix C[p, q] (fused LUT form)"""
+        key = (mult, which)
+        if key not in self.mat_cache:
+            m = np.zeros((16, 16), np.complex128)
+            for p, q, re, im in self._entries(mult, which):
+                m[int(p), int(q)] = complex(re, im)
+            self.mat_cache[key] = m
+        return self.mat_cache[key]
 
     def load_plaintexts(self, ctx, mult: int, which: str):
         key = (mult, which)
         if key not in self.pt_cache:
-            path = ensure_coeffs(self.dir) / f"gf_mult{mult}_{which}_coeffs.json"
             sc = ctx.engine.slot_count
             self.pt_cache[key] = {(p, q): ctx.encode(np.full(sc, complex(re, im), dtype=np.complex128))
-                                  for p, q, re, im in json.loads(path.read_text(encoding="utf-8"))["entries"]}
+                                  for p, q, re, im in self._entries(mult, which)}
         return self.pt_cache[key]
 
 
@@ -49,13 +63,26 @@ def gf_basis16(ctx, ct) -> Dict[int, Any]:
     return basis
 
 
-def gf_poly_eval(ctx, coeffs, ct_hi, ct_lo) -> Any:
-    """Σ c[p,q] X^p Y^q over the hi / lo bases (REF/mixcol_final.py:80-91)."""
-    bx, by = gf_basis16(ctx, ct_hi), gf_basis16(ctx, ct_lo)
+def _gf_sum(ctx, coeffs, bx, by, ct_hi):
     acc = ctx.multiply(ct_hi, 0.0)
     for (p, q), pt in coeffs.items():
         acc = ctx.add(acc, ctx.multiply(ctx.multiply(bx[p], by[q]), pt))
     return acc
+
+
+def gf_poly_eval(ctx, coeffs, ct_hi, ct_lo) -> Any:
+    """Σ c[p,q] X^p Y^q over the hi / lo bases (REF/mixcol_final.py:80-91)."""
+    return _gf_sum(ctx, coeffs, gf_basis16(ctx, ct_hi), gf_basis16(ctx, ct_lo), ct_hi)
+
+
+def gf_eval(ctx, cache: _CoeffCache, mult: int, which: str, ct_hi, ct_lo) -> Any:
+    """gf_mult{mult}_{which}(hi, lo): the 2-variable LUT as one fused engine call when the
+    context has it, else the reference's product loop."""
+    bx, by = gf_basis16(ctx, ct_hi), gf_basis16(ctx, ct_lo)
+    out = fused_lut(ctx, ("gf", mult, which), cache.matrix(mult, which), bx, by)
+    if out is not None:
+        return out
+    return _gf_sum(ctx, cache.load_plaintexts(ctx, mult, which), bx, by, ct_hi)
 
 
 class MixColFinal:
@@ -78,7 +105,7 @@ class MixColFinal:
         return gf_basis16(self.ctx, ct)
 
     def _gf_poly_eval_2var(self, ct_hi, ct_lo, mult: int, which: str):
-        return gf_poly_eval(self.ctx, self._coeffs.load_plaintexts(self.ctx, mult, which), ct_hi, ct_lo)
+        return gf_eval(self.ctx, self._coeffs, mult, which, ct_hi, ct_lo)
 
     def gf_mult_2(self, ct_hi, ct_lo):
         return pair(self.ctx, lambda: self._gf_poly_eval_2var(ct_hi, ct_lo, 2, "hi"),

@@ -11,7 +11,7 @@ defines ``SubBytesLUTFastCached``, so both names are provided.
 from typing import Any, Dict, Tuple
 
 import numpy as np
-from utils import pair
+from utils import fused_lut, pair
 
 _TOL = 1e-12
 
@@ -39,6 +39,13 @@ class SubBytesLUTFastCached:
         self.deg16 = min(max(self.ks_lift) if self.ks_lift else 0, 8)
         self.pt_lift = {k: const(lift[k]) for k in self.ks_lift}
         self.c0_lift = lift[0]
+        # the same sums as coefficient vectors for the fused LUT form
+        self.vec_lift = np.where(np.abs(lift) > _TOL, lift, 0)
+        self.vec_lift[0] = 0
+        self.vec_hi, self.vec_lo = np.zeros(256, np.complex128), np.zeros(256, np.complex128)
+        for k in self.ks_union:
+            self.vec_hi[k] = self.hi[k] if k in self.pt_hi else 0
+            self.vec_lo[k] = self.lo[k] if k in self.pt_lo else 0
 
     @staticmethod
     def _power(basis, k: int, domain: int, ctx):
@@ -47,10 +54,13 @@ class SubBytesLUTFastCached:
     def apply(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:
         ctx = self.ctx
         # 1) ζ16^l -> ζ256^l
-        lifted = ctx.add_plain(ctx.multiply(ct_lo, 0.0), self.c0_lift)
         pos16 = ctx.make_power_basis(ct_lo, self.deg16) if self.deg16 > 0 else []
-        for k in self.ks_lift:
-            lifted = ctx.add(lifted, ctx.multiply(self._power(pos16, k, 16, ctx), self.pt_lift[k]))
+        p16 = {k: self._power(pos16, k, 16, ctx) for k in self.ks_lift}
+        lifted = fused_lut(ctx, ("sb-lift", id(self)), self.vec_lift, p16, c0=self.c0_lift)
+        if lifted is None:
+            lifted = ctx.add_plain(ctx.multiply(ct_lo, 0.0), self.c0_lift)
+            for k in self.ks_lift:
+                lifted = ctx.add(lifted, ctx.multiply(p16[k], self.pt_lift[k]))
         # 2) ζ256^byte
         ct_b = ctx.multiply(ct_hi, lifted)
         # 3) one shared 128-power basis, two 255-term sums
@@ -64,6 +74,10 @@ class SubBytesLUTFastCached:
         bk.update({k: pos256[k - 1] for k in self.ks_union if k <= len(pos256)})
 
         def lut(pts, c0):
+            res = fused_lut(ctx, ("sb", id(self), pts is self.pt_hi), self.vec_hi if pts is self.pt_hi else self.vec_lo,
+                            bk, c0=c0)
+            if res is not None:
+                return res
             res = ctx.add_plain(ctx.multiply(ct_b, 0.0), c0)
             for k in self.ks_union:
                 if k in pts:

@@ -31,3 +31,16 @@ def pair(ctx, fa, fb, shared=()):
     a, b = run(fa, fb)
     return a, b
 
+
+def fused_lut(ctx, key, coeffs, a, b=None, c0: complex = 0j):
+    """The LUT sum sum_{p,q} C[p,q] a[p] b[q] (b given) or c0 + sum_k C[k] a[k] as one engine
+    call, or None when the context has no fused form or the elements sit too
+    low for it -- the caller then runs the reference's per-term product loop."""
+    if not getattr(ctx, "fused_luts", False):
+        return None
+    try:
+        return ctx.lut_eval(ctx.lut(key, coeffs, c0), a, b)
+    except RuntimeError as e:
+        if "level" in str(e):
+            return None
+        raise

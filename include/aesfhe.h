@@ -94,6 +94,21 @@ int aesfhe_mul_pt(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle pt, aesfhe_ha
 /* engine.multiply(a, b, relinearization_key), REF/engine_context.py:65-67:
  * tensor + relinearise + rescale; relin = 0 returns the 3-polynomial tensor (rescaled) */
 int aesfhe_mul(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int relin, aesfhe_handle* out);
+/* Fused LUT evaluation.  One kernel replaces the per-term product loops of
+ *   REF/xor4_lut.py:63-74           XOR4LUT.apply:        sum_{p,q} C[p,q] A^p B^q
+ *   REF/mixcol_final.py:80-91       _gf_poly_eval_2var    (same form, GF LUT coefficients)
+ *   REF/invmixcolumns_fhe.py:76-87  _poly2_eval           (same form)
+ *   REF/sub_bytes_lut.py:46-74      lift / hi / lo sums:  c0 + sum_k C[k] X^k
+ *   REF/lut.py:71-94                LUTEvaluator.apply    (same univariate form)
+ * lut_create stores the n_a x n_b coefficient matrix (row-major re / im; n_b = 1 makes a
+ * univariate LUT with constant term c0; bivariate LUTs are at most 16 x 16).  lut_eval takes
+ * the element handles a[0..n_a) (and b[0..n_b) for bivariate LUTs; entries whose coefficients
+ * are all zero may be 0) and returns the sum at the logical level of the per-term products
+ * (lowest element level - 2, resp. - 1); it fails with a message containing "level" when the
+ * elements are too low for the fused form, and the caller falls back to the product loop. */
+int aesfhe_lut_create(aesfhe_ctx* ctx, int n_a, int n_b, const double* re, const double* im, double c0_re, double c0_im,
+                      aesfhe_handle* out);
+int aesfhe_lut_eval(aesfhe_ctx* ctx, aesfhe_handle lut, const aesfhe_handle* a, const aesfhe_handle* b, aesfhe_handle* out);
 /* Deferred evaluation switch, default on: API-level ct x ct products
  * leave relinearisation and their rescale to the first consumer that needs a
  * 2-polynomial canonical ciphertext (rotate, conjugate, ct x ct, power basis, bootstrap,
