@@ -7,6 +7,16 @@
 
 ``SubBytesLUT`` is the name AESPipeline imports (REF/pipeline.py:9); the snapshot only
 defines ``SubBytesLUTFastCached``, so both names are provided.
+
+Evaluation forms (same polynomials, same output level, outputs equal up to CKKS noise):
+
+* direct (the reference's, used when the context has no fused LUT op): the 128-power basis
+  of b, 127 conjugated mirrors b^k = conj(b^(256-k)), and a 255-term product loop per output;
+* baby-step giant-step over the conjugate split: b is a 256th root of unity,
+  so f(b) = sum_{k<=128} c_k b^k + conj(sum_{j<128} conj(c_{256-j}) b^j) = P(b) + conj(Q(b));
+  P and Q (degree <= 128) are sum_i S_i(b) G_i with inner sums S_i over the baby steps
+  b^1..b^15 (one fused LUT kernel each) and giant steps G_i = b^(16 i).  The lift is split
+  the same way over y^1..y^8.  Key switches per SubBytes drop from ~270 to ~37.
 """
 from typing import Any, Dict, Tuple
 
@@ -52,6 +62,86 @@ class SubBytesLUTFastCached:
         return basis[k - 1] if k <= len(basis) else ctx.conjugate(basis[domain - k - 1])
 
     def apply(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:
+        if getattr(self.ctx, "fused_luts", False):
+            return self._apply_bsgs(ct_hi, ct_lo)
+        return self._apply_direct(ct_hi, ct_lo)
+
+    # ------------------------------------------------------------------ BSGS form
+    def _lin(self, key, vec, elems, c0, like):
+        """c0 + sum_k vec[k] elems[k]: one fused kernel, or scalar products if unavailable"""
+        out = fused_lut(self.ctx, (key, id(self)), vec, elems, c0=c0)
+        if out is not None:
+            return out
+        ctx = self.ctx
+        res = ctx.add_plain(ctx.multiply(like, 0.0), complex(c0))
+        for k, c in enumerate(vec):
+            if c != 0 and k in elems:
+                res = ctx.add(res, ctx.multiply(elems[k], complex(c)))
+        return res
+
+    @staticmethod
+    def _split(c: np.ndarray, half: int):
+        """f(x) = P(x) + conj(Q(x)) on roots of unity of order 2*half: P[k] = c[k] (k <= half),
+        Q[j] = conj(c[2*half - j]) (1 <= j < half)"""
+        c = np.where(np.abs(c) > _TOL, c, 0)
+        P = np.zeros(half + 1, np.complex128)
+        Q = np.zeros(half, np.complex128)
+        n = min(len(c), half + 1)
+        P[:n] = c[:n]
+        for j in range(1, half):
+            if 2 * half - j < len(c):
+                Q[j] = np.conj(c[2 * half - j])
+        return P, Q
+
+    def _poly_bsgs(self, key, coef, baby, giant, like):
+        """sum_i S_i G_i, S_i = sum_{j<16} coef[16 i + j] b^j (one fused kernel each)"""
+        ctx = self.ctx
+        acc = None
+        for i in range((len(coef) + 15) // 16):
+            chunk = np.zeros(16, np.complex128)
+            seg = coef[16 * i: 16 * i + 16]
+            chunk[: len(seg)] = seg
+            if not np.any(chunk):
+                continue
+            if i == 0:
+                term = self._lin((key, i), np.r_[0, chunk[1:]], baby, chunk[0], like)
+            elif not np.any(chunk[1:]):
+                term = ctx.multiply(giant[i], complex(chunk[0]))
+            else:
+                term = ctx.multiply(self._lin((key, i), np.r_[0, chunk[1:]], baby, chunk[0], like), giant[i])
+            acc = term if acc is None else ctx.add(acc, term)
+        return acc if acc is not None else ctx.multiply(like, 0.0)
+
+    def _apply_bsgs(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:
+        ctx = self.ctx
+        if not hasattr(self, "_bsgs"):
+            lift = np.fft.ifft(np.exp(-2j * np.pi * np.arange(16) / 256))
+            lp, lq = self._split(lift, 8)
+            self._bsgs = dict(lift=(lp, lq), hi=self._split(self.hi, 128), lo=self._split(self.lo, 128))
+        lp, lq = self._bsgs["lift"]
+        # 1) zeta16^l -> zeta256^l: L(y) = P(y) + conj(Q(y)) over y^1..y^8
+        pos16 = ctx.make_power_basis(ct_lo, 8)
+        y = {k: pos16[k - 1] for k in range(1, 9)}
+        lifted = ctx.add(self._lin("lift-p", np.r_[0, lp[1:]], y, lp[0], ct_lo),
+                         ctx.conjugate(self._lin("lift-q", lq, y, 0j, ct_lo)))
+        # 2) b = zeta256^byte; baby steps b^1..b^16, giant steps G_i = b^(16 i), i <= 8
+        ct_b = ctx.multiply(ct_hi, lifted)
+        pw = ctx.make_power_basis(ct_b, 16)
+        baby = {k: pw[k - 1] for k in range(1, 16)}
+        g = {1: pw[15]}
+        for i, (u, v) in ((2, (1, 1)), (4, (2, 2)), (3, (1, 2)), (5, (1, 4)), (6, (2, 4)), (7, (3, 4)), (8, (4, 4))):
+            g[i] = ctx.multiply(g[u], g[v])  # depth: G_2 +1, G_3 / G_4 +2, G_5..G_8 +3 over b^16
+
+        # 3) out = P(b) + conj(Q(b)) per output nibble
+        def lut(which):
+            P, Q = self._bsgs[which]
+            return ctx.add(self._poly_bsgs((which, "p"), P, baby, g, ct_b),
+                           ctx.conjugate(self._poly_bsgs((which, "q"), Q, baby, g, ct_b)))
+
+        return pair(ctx, lambda: lut("hi"), lambda: lut("lo"), shared=(*baby.values(), *g.values()))
+
+    # ------------------------------------------------------------------ direct (reference) form
+    def _apply_direct(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:
         ctx = self.ctx
         # 1) ζ16^l -> ζ256^l
         pos16 = ctx.make_power_basis(ct_lo, self.deg16) if self.deg16 > 0 else []
