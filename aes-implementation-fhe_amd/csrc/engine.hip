@@ -109,6 +109,8 @@ struct Ct {
     int pend = 0;
     bool lazy = false;
     bool zero = false;
+    int sid = 0;            // stream of the call that stored the handle
+    unsigned epoch = 0;     // fork section it was stored in (0: outside any)
 };
 
 // coefficient set of a fused LUT evaluation: C[n_a][n_b] (n_b = 1: univariate)
@@ -188,6 +190,7 @@ public:
     }
     bool no_share_ = std::getenv("AESFHE_NO_POOL_SHARE") != nullptr;  // debug switch
     bool fj_active_ = false;
+    unsigned fj_epoch_ = 0;
     static int streams() { return kStreams; }
     void bind_stream(int k) {
         if (k < 0 || k >= kStreams) throw std::runtime_error("bind_stream: stream index out of range");
@@ -199,6 +202,7 @@ public:
         HIP_OK(hipEventRecord(fj_ev_[0], streams_[0]));
         for (int k = 1; k < kStreams; ++k) HIP_OK(hipStreamWaitEvent(streams_[k], fj_ev_[0], 0));
         fj_active_ = true;
+        ++fj_epoch_;
     }
     // stream 0 continues after every branch; handles the branch threads dropped go back to
     // stream 0's pool only now (another stream may have read them until here)
@@ -221,6 +225,8 @@ public:
     // ------------------------------------------------------------------ handles
     aesfhe_handle put_ct(Ct c) {
         aesfhe_handle h = next_++;
+        c.sid = t_sidx;
+        c.epoch = fj_active_ ? fj_epoch_ : 0;
         cts_[h] = c;
         return h;
     }
@@ -616,7 +622,8 @@ public:
     // stored ciphertext in canonical form; the table entry is replaced so that deferred work
     // is done once however often the handle is used
     // Inside a fork/join section another stream may read the same handle, so the table entry
-    // is left alone and a private canonical copy (released when the API call ends) is used.
+    // is left alone and a private canonical copy (released when the API call ends) is used --
+    // unless the calling branch itself stored the handle in this section.
     const Ct& canon(aesfhe_handle h) {
         auto it = cts_.find(h);
         if (it == cts_.end()) throw std::runtime_error("invalid ciphertext handle");
@@ -627,11 +634,14 @@ public:
             c.lazy = false;
             return c;
         }
-        if (fj_active_) {
+        // a handle this branch stored in this fork section is invisible to the other branches
+        // until the join, so it is memoized like outside a section
+        if (fj_active_ && !(c.sid == t_sidx && c.epoch == fj_epoch_)) {
             scratch_.push_back(nc);
             return scratch_.back();
         }
         if (nc.data != c.data) release(c);
+        nc.sid = c.sid, nc.epoch = c.epoch;
         c = nc;
         return c;
     }

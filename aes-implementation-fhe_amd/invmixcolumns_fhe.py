@@ -6,7 +6,7 @@ from __future__ import annotations
 
 from typing import Any, Dict, List
 
-from mixcol_final import _CoeffCache, gf_basis16, gf_eval
+from mixcol_final import _CoeffCache, gf_basis16, gf_eval, gf_mult_pair
 from shift_rows import row_masks
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT
@@ -45,8 +45,7 @@ class InvMixColumnsFHE:
         return out
 
     def _gf(self, mult, hi, lo):
-        return pair(self.ctx, lambda: self._poly2_eval(hi, lo, mult, "hi"), lambda: self._poly2_eval(hi, lo, mult, "lo"),
-                    shared=(hi, lo))
+        return gf_mult_pair(self.ctx, self._coeffs, mult, hi, lo)
 
     def gf_mult_9(self, hi, lo):
         return self._gf(9, hi, lo)

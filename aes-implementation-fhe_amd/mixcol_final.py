@@ -15,7 +15,7 @@ import numpy as np
 
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
-from xor4_lut import XOR4LUT
+from xor4_lut import XOR4LUT, SplitLUT2, powers, std_basis
 from utils import fused_lut, pair
 
 
@@ -30,6 +30,12 @@ class _CoeffCache:
     def _entries(self, mult: int, which: str):
         path = ensure_coeffs(self.dir) / f"gf_mult{mult}_{which}_coeffs.json"
         return json.loads(path.read_text(encoding="utf-8"))["entries"]
+
+    def split(self, mult: int, which: str) -> SplitLUT2:
+        key = (mult, which, "split")
+        if key not in self.mat_cache:
+            self.mat_cache[key] = SplitLUT2(self.matrix(mult, which))
+        return self.mat_cache[key]
 
     def matrix(self, mult: int, which: str) -> np.ndarray:
         """the same coefficients as a dense 16 x 16 matrix C[p, q] (fused LUT form)"""
@@ -85,6 +91,28 @@ def gf_eval(ctx, cache: _CoeffCache, mult: int, which: str, ct_hi, ct_lo) -> Any
     return _gf_sum(ctx, cache.load_plaintexts(ctx, mult, which), bx, by, ct_hi)
 
 
+def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo):
+    """(gf_mult{mult}_hi, gf_mult{mult}_lo)(hi, lo).  With a fused-LUT context both LUTs are
+    evaluated in the conjugate-split form (xor4_lut.SplitLUT2) over ONE pair
+    of bases -- positive powers of hi, standard basis of lo -- instead of four 16-element
+    bases; otherwise the reference's per-LUT product loops (REF/mixcol_final.py:80-99)."""
+    if getattr(ctx, "fused_luts", False):
+        sh, sl = cache.split(mult, "hi"), cache.split(mult, "lo")
+        try:
+            A, B = pair(ctx, lambda: powers(ctx, ct_hi, sh.need_a | sl.need_a),
+                        lambda: std_basis(ctx, ct_lo, sh.need_b | sl.need_b))
+        except RuntimeError as e:
+            if "level" not in str(e):
+                raise
+        else:
+            out = pair(ctx, lambda: sh.eval(ctx, ("gf", mult, "hi"), A, B), lambda: sl.eval(ctx, ("gf", mult, "lo"), A, B),
+                       shared=(*A.values(), *B.values()))
+            if out[0] is not None and out[1] is not None:
+                return out
+    return pair(ctx, lambda: gf_eval(ctx, cache, mult, "hi", ct_hi, ct_lo),
+                lambda: gf_eval(ctx, cache, mult, "lo", ct_hi, ct_lo), shared=(ct_hi, ct_lo))
+
+
 class MixColFinal:
     def __init__(self, ctx, xor4: XOR4LUT, stride: int | None = None):
         self.ctx = ctx
@@ -108,12 +136,10 @@ class MixColFinal:
         return gf_eval(self.ctx, self._coeffs, mult, which, ct_hi, ct_lo)
 
     def gf_mult_2(self, ct_hi, ct_lo):
-        return pair(self.ctx, lambda: self._gf_poly_eval_2var(ct_hi, ct_lo, 2, "hi"),
-                    lambda: self._gf_poly_eval_2var(ct_hi, ct_lo, 2, "lo"), shared=(ct_hi, ct_lo))
+        return gf_mult_pair(self.ctx, self._coeffs, 2, ct_hi, ct_lo)
 
     def gf_mult_3(self, ct_hi, ct_lo):
-        return pair(self.ctx, lambda: self._gf_poly_eval_2var(ct_hi, ct_lo, 3, "hi"),
-                    lambda: self._gf_poly_eval_2var(ct_hi, ct_lo, 3, "lo"), shared=(ct_hi, ct_lo))
+        return gf_mult_pair(self.ctx, self._coeffs, 3, ct_hi, ct_lo)
 
     def _col_shift_rowmajor(self, ct, k_up: int):
         return self.ctx.rotate(ct, -4 * k_up * self.stride)

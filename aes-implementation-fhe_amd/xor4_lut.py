@@ -5,6 +5,14 @@
 with C from xor4_coeffs.json (only odd p, q are non-zero; the output carries the
 reference's 256x magnitude).  Depth 5: power basis 3, product 1,
 coefficient 1.
+
+With a fused-LUT context the sum is split over the conjugate mirrors: a and
+b are 16th roots of unity, so the rows p >= 9 (A^p = conj(A^(16-p))) satisfy
+    sum_{p>=9,q} C[p,q] conj(A^(16-p)) B^q = conj( sum C'[p',q'] A^p' B^q' ),
+    C'[p',q'] = conj(C[16-p', (16-q') mod 16]),
+and the whole LUT is S1 + conj(S2) over the positive powers of a and the standard basis of
+b: a needs no conjugations at all, only the powers the coefficients use are formed (x^6 and
+x^8 are skipped for XOR4), and each S is one fused kernel.  Output level unchanged.
 """
 from typing import Any, Dict
 
@@ -36,6 +44,86 @@ def basis16(ctx, ct, *, retry_intt: bool = True) -> Dict[int, Any]:
     return basis
 
 
+# ---------------------------------------------------------------- conjugate-split bivariate LUTs
+def _chain(need):
+    """products (k, u, v), x^k = x^u x^v, forming x^k for every k in need (<= 8) at depth
+    ceil(log2 k) -- the engine's power-basis rule, restricted to what is used"""
+    have, order = {1}, []
+
+    def get(k):
+        if k in have:
+            return
+        t = 1 << (k.bit_length() - 1)
+        u, v = (k // 2, k // 2) if t == k else (t, k - t)
+        get(u)
+        get(v)
+        order.append((k, u, v))
+        have.add(k)
+
+    for k in sorted(need):
+        if k >= 1:
+            get(k)
+    return order
+
+
+def powers(ctx, ct, need) -> Dict[int, Any]:
+    """{k: x^k} for k in need (0 = the constant 1 at x's level)"""
+    pw = {1: ct}
+    for k, u, v in _chain(need):
+        pw[k] = ctx.multiply(pw[u], pw[v])
+    if 0 in need:
+        pw[0] = ctx.add_plain(ctx.multiply(ct, 0.0), 1.0)
+    return {k: pw[k] for k in need}
+
+
+def std_basis(ctx, ct, need) -> Dict[int, Any]:
+    """{q: B[q]} for q in need, B[q] = x^q (q <= 8), conj(x^(16-q)) (q >= 9)"""
+    pos = powers(ctx, ct, {q if q <= 8 else 16 - q for q in need})
+    return {q: pos[q] if q <= 8 else ctx.conjugate(pos[16 - q]) for q in need}
+
+
+class SplitLUT2:
+    """sum_{p,q} C[p,q] A[p] B[q] over Zeta16 inputs as S1 + conj(S2) (module docstring)."""
+
+    def __init__(self, C: np.ndarray, tol: float = 1e-12):
+        C = np.where(np.abs(C) > tol, np.asarray(C, np.complex128), 0)
+        self.c1 = C[:9].copy()
+        self.c2 = np.zeros((8, 16), np.complex128)
+        for pp in range(1, 8):
+            for qq in range(16):
+                self.c2[pp, qq] = np.conj(C[16 - pp, (16 - qq) % 16])
+        rows = lambda M: {i for i in range(M.shape[0]) if np.any(M[i])}
+        cols = lambda M: {j for j in range(16) if np.any(M[:, j])}
+        self.need_a = rows(self.c1) | rows(self.c2)
+        self.need_b = cols(self.c1) | cols(self.c2)
+        self.has2 = bool(np.any(self.c2))
+
+    def bases(self, ctx, a, b):
+        return pair(ctx, lambda: powers(ctx, a, self.need_a), lambda: std_basis(ctx, b, self.need_b))
+
+    def eval(self, ctx, key, A, B):
+        s1 = fused_lut(ctx, (key, 1), self.c1, A, B)
+        if s1 is None:
+            return None
+        if not self.has2:
+            return s1
+        s2 = fused_lut(ctx, (key, 2), self.c2, A, B)
+        return None if s2 is None else ctx.add(s1, ctx.conjugate(s2))
+
+
+def split_lut2(ctx, split: SplitLUT2, key, a, b):
+    """the split evaluation, or None (no fused op / not enough level: use the product loop)"""
+    if not getattr(ctx, "fused_luts", False):
+        return None
+    try:
+        A, B = split.bases(ctx, a, b)
+    except RuntimeError as e:
+        if "level" in str(e):
+            return None
+        raise
+    return split.eval(ctx, key, A, B)
+
+
 class XOR4LUT:
     def __init__(self, ctx, coeffs: np.ndarray):
         self.ctx = ctx
@@ -49,6 +137,11 @@ class XOR4LUT:
 
     def apply(self, a_ct, b_ct):
         ctx = self.ctx
+        if not hasattr(self, "_split"):
+            self._split = SplitLUT2(self.coeffs)
+        out = split_lut2(ctx, self._split, ("xor4", id(self)), a_ct, b_ct)
+        if out is not None:
+            return out
         A, B = pair(ctx, lambda: self._build_power_basis_16(a_ct), lambda: self._build_power_basis_16(b_ct))
         out = fused_lut(ctx, "xor4", self.coeffs, A, B)  # one kernel for all 64 terms
         if out is not None:

@@ -147,7 +147,7 @@ def test_xor4_fused_matches_loop(coeffs):
     x = XOR4LUT(ctx, coeffs["xor4"])
     before = ctx.engine.counters()["lut"]
     fused = x.apply(ah, bh)
-    assert ctx.engine.counters()["lut"] == before + 1
+    assert ctx.engine.counters()["lut"] == before + 2  # conjugate split: S1 + conj(S2)
     ctx.fused_luts = False
     try:
         loop = x.apply(ah, bh)
@@ -181,3 +181,26 @@ def test_subbytes_fused_matches_loop(coeffs):
     for f, g in ((fh, lh), (fl, ll)):
         assert np.abs(_slots(ctx, f) - _slots(ctx, g)).max() < 2e-2
     assert np.array_equal(enc.decode(fh, fl), aes_plain.SBOX[state])
+
+
+@pytest.mark.parametrize("mult", [2, 3, 9, 11, 13, 14])
+def test_gf_mult_split_matches_loop(mult):
+    """GF multipliers: the conjugate-split form over shared bases vs the reference's loops"""
+    from mixcol_final import _CoeffCache, gf_mult_pair
+    from oracle import aes_plain
+    from state_encoder import StateEncoder
+    ctx = gpu_context(log_n=16)
+    enc = StateEncoder(ctx)
+    state = np.random.default_rng(mult).integers(0, 256, 16).astype(np.uint8)
+    hi, lo = enc.encode(state)
+    cache = _CoeffCache()
+    fh, fl = gf_mult_pair(ctx, cache, mult, hi, lo)
+    ctx.fused_luts = False
+    try:
+        lh, ll = gf_mult_pair(ctx, cache, mult, hi, lo)
+    finally:
+        ctx.fused_luts = True
+    assert (fh.level, fl.level) == (lh.level, ll.level)
+    for f, g in ((fh, lh), (fl, ll)):
+        assert np.abs(_slots(ctx, f) - _slots(ctx, g)).max() < 1e-3
+    assert np.array_equal(enc.decode(fh, fl), aes_plain.GF_MUL[mult][state])
