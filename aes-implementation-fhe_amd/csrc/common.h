@@ -57,6 +57,16 @@ HD u32 barrett_reduce64(u64 x, u32 q, u32 mu) {
     return csub(r, q);
 }
 
+// fold a full 64-bit accumulator below 2^61 (x mod q unchanged); r32 = 2^32 mod q
+HD u64 fold64(u64 x, u32 q, u32 r32) {
+    u32 hi = (u32)(x >> 32);
+    hi = hi >= 2 * q ? hi - 2 * q : hi;  // hi < 2^32 < 4q
+    hi = csub(hi, q);
+    return (u64)hi * r32 + (u32)x;
+}
+// any 64-bit x mod q
+HD u32 reduce64(u64 x, u32 q, u32 mu, u32 r32) { return barrett_reduce64(fold64(x, q, r32), q, mu); }
+
 // per-prime constant table kept in device memory
 struct PrimeConst {
     u32 q;       // modulus
@@ -65,7 +75,8 @@ struct PrimeConst {
     u32 ninv_p;  // Shoup companion
     u32 im;      // psi^{N/2}: the "imaginary unit" of Z_q (X^{N/2} at psi)
     u32 im_p;
-    u32 pad0, pad1;
+    u32 r32;     // 2^32 mod q
+    u32 pad1;
 };
 
 // limb -> prime map of an RNS polynomial: limbs [0, n1) use primes off1 + l,

@@ -1828,6 +1828,7 @@ private:
             pc[i].ninv_p = shoup_pre(pc[i].ninv, q);
             pc[i].im = hpowm(w, n / 2, q);
             pc[i].im_p = shoup_pre(pc[i].im, q);
+            pc[i].r32 = (u32)((1ull << 32) % q);
             im_[i] = pc[i].im;
             u64 p = 1, ip = 1;
             for (int k = 0; k < n; ++k) {

@@ -151,12 +151,17 @@ __global__ void __launch_bounds__(kBlock) k_base_convert(ConvBatch cb, int nt, L
     for (int t = t0; t < t1; ++t) {
         if (t >= skip0 && t < skip0 + h) continue;
         const PrimeConst P = pc[map.prime(t)];
+        // plain 32x32 -> 64-bit multiply-adds (v_mad_u64_u32); y_i < q_i, w < q_t, so eight
+        // products stay below 2^64 and one fold makes room for eight more
         u64 acc = (u64)u * negq[t];
         const u32* tt = tab + 2 * (size_t)t;
 #pragma unroll
         for (int i = 0; i < kMaxConvH; ++i)
-            if (i < h) acc += shoup_mul(y[i], tt[2 * (size_t)i * nt], tt[2 * (size_t)i * nt + 1], P.q);
-        ext[((size_t)t << logn) + k] = barrett_reduce64(acc, P.q, P.mu);
+            if (i < h) {
+                if (i == 8) acc = fold64(acc, P.q, P.r32);
+                acc += (u64)y[i] * tt[2 * (size_t)i * nt];
+            }
+        ext[((size_t)t << logn) + k] = reduce64(acc, P.q, P.mu, P.r32);
     }
     ts_end(ts);
 }
@@ -170,16 +175,18 @@ __global__ void k_key_inner(u32* acc, const u32* ext, const u32* d, const u32* k
     const PrimeConst P = pc[map.prime(x)];
     const int krow = x < nl ? x : nks + (x - nl);
     const int own = x < nl ? x / alpha : -1;
-    u32 s0 = 0, s1 = 0;
+    // 64-bit multiply-adds (operands < q < 2^32/3: eight products fit), folded every 8 digits
+    u64 s0 = 0, s1 = 0;
     for (int j = 0; j < nd; ++j) {
+        if (j && (j & 7) == 0) s0 = fold64(s0, P.q, P.r32), s1 = fold64(s1, P.q, P.r32);
         const u32 e = j == own ? d[((size_t)x << logn) + k] : ext[(((size_t)j * ne + x) << logn) + k];
         const u32* kb = key + (((size_t)j * 2 * nkey + krow) << logn) + k;
         const u32* ka = kb + ((size_t)nkey << logn);
-        s0 = add_mod(s0, barrett_mul(e, *kb, P.q, P.mu), P.q);
-        s1 = add_mod(s1, barrett_mul(e, *ka, P.q, P.mu), P.q);
+        s0 += (u64)e * *kb;
+        s1 += (u64)e * *ka;
     }
-    acc[((size_t)x << logn) + k] = s0;
-    acc[(((size_t)ne + x) << logn) + k] = s1;
+    acc[((size_t)x << logn) + k] = reduce64(s0, P.q, P.mu, P.r32);
+    acc[(((size_t)ne + x) << logn) + k] = reduce64(s1, P.q, P.mu, P.r32);
     ts_end(ts);
 }
 

@@ -13,6 +13,7 @@ sys.path[:0] = [str(ROOT), str(ROOT / "aes-implementation-fhe_amd")]
 from aes_keyschedule import expand_aes128_key, load_all_coeffs  # noqa: E402
 from engine_context import EngineContext  # noqa: E402
 from pipeline import AESPipeline  # noqa: E402
+from utils import pair  # noqa: E402
 
 
 def main():
@@ -38,19 +39,30 @@ def main():
         return out
 
     mix = pipe.mix
-    orig_xor, orig_renorm, orig_boot = mix._xor_ct, mix._renorm_pair, ctx.bootstrap
-    mix._xor_ct = lambda a, b: timed("mc.xor4", orig_xor, a, b)
-    mix._renorm_pair = lambda h, l: timed("mc.renorm", orig_renorm, h, l)
-    ctx.bootstrap = lambda c: timed("bootstrap", orig_boot, c)
     t0 = time.perf_counter()
     c = timed("sub_bytes", pipe.sub_bytes, *ct)
     c = timed("renorm", pipe._renorm_pair, *c)
     c = timed("shift_rows", pipe.shift_rows, *c)
-    c = timed("mix_columns(total)", pipe.mix_columns, *c)
+    # MixColFinal.__call__ step by step (same calls, each pair timed as a whole)
+    t_mc = time.perf_counter()
+    hi, lo = c
+    rh, rl = timed("mc.rotations", lambda: pair(ctx, lambda: [mix._col_shift_rowmajor(hi, k) for k in (1, 2, 3)],
+                                                  lambda: [mix._col_shift_rowmajor(lo, k) for k in (1, 2, 3)]))
+    two = timed("mc.gf_mult_2", mix.gf_mult_2, hi, lo)
+    thr = timed("mc.gf_mult_3", mix.gf_mult_3, rh[0], rl[0])
+    xor_pair = lambda a, b: pair(ctx, lambda: mix._xor_ct(a[0], b[0]), lambda: mix._xor_ct(a[1], b[1]))
+    acc = timed("mc.xor4_pairs", xor_pair, two, thr)
+    acc = timed("mc.renorm", mix._renorm_pair, *acc)
+    acc = timed("mc.xor4_pairs", xor_pair, acc, (rh[1], rl[1]))
+    acc = timed("mc.renorm", mix._renorm_pair, *acc)
+    acc = timed("mc.xor4_pairs", xor_pair, acc, (rh[2], rl[2]))
+    acc = timed("mc.renorm", mix._renorm_pair, *acc)
+    c = timed("mc.bootstrap_pair", lambda: pair(ctx, lambda: ctx.bootstrap(ctx.to_intt(acc[0])),
+                                                lambda: ctx.bootstrap(ctx.to_intt(acc[1]))))
+    res["mix_columns(total)"] = (time.perf_counter() - t_mc) * 1e3
     c = timed("add_round_key", pipe.add_round_key, *c, *rk[2])
     c = timed("renorm", pipe._renorm_pair, *c)
     res["round_total"] = (time.perf_counter() - t0) * 1e3
-    res["mc.gf_luts+rest"] = res["mix_columns(total)"] - res.get("mc.xor4", 0) - res.get("mc.renorm", 0) - res.get("bootstrap", 0)
     print(json.dumps({"lazy": lazy, "ms": {k: round(v, 2) for k, v in res.items()}}, indent=1))
 
 
