@@ -119,9 +119,43 @@ __global__ void k_rescale_spread(u32* v, const u32* last, int nt, u32 q_last, co
 // (N / 256, target chunks of kConvTargets, groups).  Each thread recomputes the h values
 // y_i = x_i qhat_i^{-1} (kept in VGPRs: fixed-size guarded unroll, no scratch) and the
 // centred overflow estimate u = round(sum y_i / q_i), then emits its chunk of targets:
-// ext_t = sum_i y_i [qhat_i]_t + u [-Q]_t  (mod t).  Table reads are block-uniform
-// (scalar loads).
+// ext_t = sum_i y_i [qhat_i]_t + u [-Q]_t  (mod t).
+// The block's constants (source primes, qhat^{-1}, the h x kConvTargets table slice, -Q,
+// target primes) are staged in LDS first: read from global memory next to the stores to
+// ext they would be re-fetched, one dependent load per multiply-add.
 constexpr int kConvTargets = 8;
+// H sources, compile-time: every load issued up front, the multiply-adds unrolled without
+// branches; targets outside [t0, t1) or inside the own range compute on zero weights and
+// are not stored
+template <int H>
+__device__ __forceinline__ void conv_body(const u32* __restrict__ x, u32* __restrict__ ext, size_t k, int t0, int t1, int skip0,
+                                          int logn, const u32 (*s_w)[kMaxConvH], const u32 (*s_tq)[4], const u32 (*s_src)[4]) {
+    u32 y[H];
+#pragma unroll
+    for (int i = 0; i < H; ++i) y[i] = x[((size_t)i << logn) + k];
+    u64 f = 0;
+#pragma unroll
+    for (int i = 0; i < H; ++i) {
+        y[i] = shoup_mul(y[i], s_src[i][2], s_src[i][3], s_src[i][0]);
+        f += ((u64)y[i] * s_src[i][1]) >> 30;
+    }
+    const u32 u = (u32)((f + (1ull << 31)) >> 32);
+#pragma unroll
+    for (int tl = 0; tl < kConvTargets; ++tl) {
+        const int t = t0 + tl;
+        if (t >= t1) break;
+        const u32 q = s_tq[tl][0], r32 = s_tq[tl][2];
+        // plain 32x32 -> 64-bit multiply-adds (v_mad_u64_u32); y_i < q_i, w < q_t, so eight
+        // products stay below 2^64 and one fold makes room for eight more
+        u64 acc = (u64)u * s_tq[tl][3];
+#pragma unroll
+        for (int i = 0; i < H; ++i) {
+            if (i == 8) acc = fold64(acc, q, r32);
+            acc += (u64)y[i] * s_w[tl][i];
+        }
+        if (t < skip0 || t >= skip0 + H) ext[((size_t)t << logn) + k] = reduce64(acc, q, s_tq[tl][1], r32);
+    }
+}
 __global__ void __launch_bounds__(kBlock) k_base_convert(ConvBatch cb, int nt, LimbMap map, const PrimeConst* pc, int logn,
                                                          unsigned long long* ts) {
     const int gi = blockIdx.z;
@@ -129,39 +163,35 @@ __global__ void __launch_bounds__(kBlock) k_base_convert(ConvBatch cb, int nt, L
     const int t0 = blockIdx.y * kConvTargets, t1 = min(t0 + kConvTargets, nt);
     if (t0 >= skip0 && t1 <= skip0 + h) return;  // chunk entirely inside the own range
     ts_begin(ts);
-    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    const u32* x = cb.src[gi];
-    const u32* qhinv = cb.qhinv[gi];
-    u32 y[kMaxConvH];
-    u64 f = 0;
-#pragma unroll
-    for (int i = 0; i < kMaxConvH; ++i) {
+    __shared__ u32 s_w[kConvTargets][kMaxConvH];
+    __shared__ u32 s_tq[kConvTargets][4];  // q, mu, r32, -Q mod q
+    __shared__ u32 s_src[kMaxConvH][4];    // q, mu, qhat^-1, Shoup companion
+    const int tid = threadIdx.x;
+    if (tid < kConvTargets * kMaxConvH) {
+        const int tl = tid / kMaxConvH, i = tid % kMaxConvH, t = t0 + tl;
+        s_w[tl][i] = (i < h && t < t1) ? cb.tab[gi][2 * ((size_t)i * nt + t)] : 0u;
+    } else if (tid < kConvTargets * kMaxConvH + kConvTargets) {
+        const int tl = tid - kConvTargets * kMaxConvH, t = t0 + tl;
+        if (t < t1) {
+            const PrimeConst P = pc[map.prime(t)];
+            s_tq[tl][0] = P.q, s_tq[tl][1] = P.mu, s_tq[tl][2] = P.r32, s_tq[tl][3] = cb.negq[gi][t];
+        }
+    } else if (tid < kConvTargets * kMaxConvH + kConvTargets + kMaxConvH) {
+        const int i = tid - kConvTargets * kMaxConvH - kConvTargets;
         if (i < h) {
-            const PrimeConst Pi = pc[d0 + i];
-            y[i] = shoup_mul(x[((size_t)i << logn) + k], qhinv[2 * i], qhinv[2 * i + 1], Pi.q);
-            f += ((u64)y[i] * Pi.mu) >> 30;
-        } else {
-            y[i] = 0;
+            const PrimeConst P = pc[d0 + i];
+            s_src[i][0] = P.q, s_src[i][1] = P.mu, s_src[i][2] = cb.qhinv[gi][2 * i], s_src[i][3] = cb.qhinv[gi][2 * i + 1];
         }
     }
-    const u32 u = (u32)((f + (1ull << 31)) >> 32);
-    const u32* tab = cb.tab[gi];
-    const u32* negq = cb.negq[gi];
-    u32* ext = cb.dst[gi];
-    for (int t = t0; t < t1; ++t) {
-        if (t >= skip0 && t < skip0 + h) continue;
-        const PrimeConst P = pc[map.prime(t)];
-        // plain 32x32 -> 64-bit multiply-adds (v_mad_u64_u32); y_i < q_i, w < q_t, so eight
-        // products stay below 2^64 and one fold makes room for eight more
-        u64 acc = (u64)u * negq[t];
-        const u32* tt = tab + 2 * (size_t)t;
-#pragma unroll
-        for (int i = 0; i < kMaxConvH; ++i)
-            if (i < h) {
-                if (i == 8) acc = fold64(acc, P.q, P.r32);
-                acc += (u64)y[i] * tt[2 * (size_t)i * nt];
-            }
-        ext[((size_t)t << logn) + k] = reduce64(acc, P.q, P.mu, P.r32);
+    __syncthreads();
+    const size_t k = (size_t)blockIdx.x * kBlock + tid;
+    switch (h) {
+#define CONV_CASE(H) \
+    case H: conv_body<H>(cb.src[gi], cb.dst[gi], k, t0, t1, skip0, logn, s_w, s_tq, s_src); break;
+        CONV_CASE(1) CONV_CASE(2) CONV_CASE(3) CONV_CASE(4) CONV_CASE(5) CONV_CASE(6) CONV_CASE(7) CONV_CASE(8)
+        CONV_CASE(9) CONV_CASE(10) CONV_CASE(11) CONV_CASE(12) CONV_CASE(13) CONV_CASE(14) CONV_CASE(15) CONV_CASE(16)
+#undef CONV_CASE
+        default: break;
     }
     ts_end(ts);
 }
