@@ -77,16 +77,22 @@ LinGroup layout(const Diags& D, int h, int M) {
         R = std::max(R, std::abs(i));
     }
     const int n = 2 * R + 1;
-    g.R = R;
-    g.B = (int)std::ceil(std::sqrt((double)n));
-    g.G = (n + g.B - 1) / g.B;
+    // baby steps are hoisted (one ModUp for all of them, no ModDown each) and cost a key
+    // inner product; giant steps are full key switches: about 2 sqrt(n) babies, a power of
+    // two (<= 16), and offsets starting at a multiple of B so that one giant step is 0
+    int B = 1;
+    while (B < 16 && B < 2.0 * std::sqrt((double)n)) B *= 2;
+    const int R0 = (R + B - 1) / B * B;
+    g.R = R0;
+    g.B = B;
+    g.G = (R + R0 + 1 + B - 1) / B;
     g.giant.resize(g.G);
     g.diag.assign(g.G, std::vector<std::vector<cplx>>(g.B));
     for (int gg = 0; gg < g.G; ++gg) {
-        const long sg = (long)h * (gg * g.B - R);
+        const long sg = (long)h * (gg * g.B - R0);
         g.giant[gg] = (int)sg;
         for (int b = 0; b < g.B; ++b) {
-            const int i = gg * g.B + b - R;
+            const int i = gg * g.B + b - R0;
             auto it = by_i.find(i);
             if (it == by_i.end()) continue;
             g.diag[gg][b] = rotl(*it->second, -sg);

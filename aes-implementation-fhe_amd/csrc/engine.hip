@@ -381,20 +381,22 @@ public:
 
     // ------------------------------------------------------------------ codec
     // host: slots -> residues on limbs 0..nl-1 at `scale` (coefficient form)
-    void encode_host(const double* re, const double* im, double scale, int nl, std::vector<u32>& out) {
+    // residues on limbs 0..nl-1 (primes q_0..), then `np` limbs of the P block when np > 0
+    void encode_host(const double* re, const double* im, double scale, int nl, std::vector<u32>& out, int np = 0) {
         const int n = hp_.n;
         std::vector<double> m(n);
         emb_.inverse(re, im, m.data());
-        out.assign((size_t)nl * n, 0);
+        const int nr = nl + np;
+        out.assign((size_t)nr * n, 0);
         // residues of the integer-valued double x = round(m_k scale): with k = floor(x / q)
         // the remainder fma(-q, k, x) is exact (it is small), one correction step fixes the
         // quotient's rounding; identical to the 128-bit integer reduction, ~20x cheaper
-        std::vector<double> qd(nl), qinv(nl);
-        for (int t = 0; t < nl; ++t) qd[t] = (double)hp_.mod[t], qinv[t] = 1.0 / qd[t];
+        std::vector<double> qd(nr), qinv(nr);
+        for (int t = 0; t < nr; ++t) qd[t] = (double)hp_.mod[t < nl ? t : hp_.p_off() + t - nl], qinv[t] = 1.0 / qd[t];
         for (int k = 0; k < n; ++k) {
             const double y = m[k] * scale;
             const double x = std::fabs(y) < 4503599627370496.0 ? (double)std::llround(y) : y;
-            for (int t = 0; t < nl; ++t) {
+            for (int t = 0; t < nr; ++t) {
                 double r = std::fma(-qd[t], std::floor(x * qinv[t]), x);
                 if (r < 0) r += qd[t];
                 if (r >= qd[t]) r -= qd[t];
@@ -1123,14 +1125,14 @@ public:
 
     // ------------------------------------------------------------------ key switching
     // returns (c0', c1') with c0' + c1' s = d s' (+ add0/add1 folded in); d NTT, level l
-    Ct keyswitch(const u32* d, int level, const u32* key, const u32* add0, const u32* add1) {
+    // ModUp: coefficient form of d, every digit converted to all other limbs of Q*P in one
+    // launch, one NTT launch over all converted rows (own limbs skipped: key_inner reads
+    // those straight from d).  Returns nd x ne rows (tmp; the caller untmps).
+    u32* modup(const u32* d, int level) {
         const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, alpha = hp_.alpha;
         const int nd = (nl + alpha - 1) / alpha;
         if (alpha > kMaxConvH || np > kMaxConvH || nd > kMaxConvGroups) throw std::runtime_error("keyswitch: digit too large");
         const LimbMap em = extmap(nl);
-        // ModUp: coefficient form of d, every digit converted to all other limbs of Q*P in
-        // one launch, one NTT launch over all converted rows (own limbs skipped: key_inner
-        // reads those straight from d)
         u32* coef = tmp(nl);
         intt(coef, d, nl, rows_dense(nl), qmap());
         u32* ext = tmp((size_t)nd * ne);
@@ -1150,12 +1152,20 @@ public:
         RowMap xr = rows_dense(ne);
         xr.skip_alpha = alpha, xr.skip_nl = nl;
         ntt(ext, ext, nd * ne, xr, em);
-        u32* acc = tmp(2 * (size_t)ne);
-        launch_key_inner(S(), T_, acc, ext, d, key, nd, ne, nl, alpha, hp_.n_ks + np, hp_.n_ks, em);
-        untmp(ext, (size_t)nd * ne);
         untmp(coef, nl);
-        // ModDown by P: coefficients of the P rows (read in place from acc), conversion of
-        // both polys in one launch, NTT fused with (acc_Q - conv) P^{-1} (+ add)
+        return ext;
+    }
+    int ext_rows(int level) const { return (hp_.nl(level) + hp_.alpha - 1) / hp_.alpha * (hp_.nl(level) + hp_.n_p); }
+    // acc (2 x ne rows, Q*P) = sum_j ext_j * key_j; g != 0 reads ext and d through X -> X^g
+    void key_inner(u32* acc, const u32* ext, const u32* d, const u32* key, int level, u64 g) {
+        const int nl = hp_.nl(level), np = hp_.n_p, ne = nl + np;
+        const int nd = (nl + hp_.alpha - 1) / hp_.alpha;
+        launch_key_inner(S(), T_, acc, ext, d, key, nd, ne, nl, hp_.alpha, hp_.n_ks + np, hp_.n_ks, extmap(nl), g);
+    }
+    // ModDown by P: coefficients of the P rows (read in place from acc), conversion of both
+    // polys in one launch, NTT fused with (acc_Q - conv) P^{-1} (+ add)
+    Ct moddown(const u32* acc, int level, const u32* add0, const u32* add1) {
+        const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np;
         u32* yp = tmp(2 * (size_t)np);
         intt(yp, acc, 2 * np, RowMap{np, ne, np, nl, 0}, LimbMap{np, hp_.p_off(), 0});
         u32* conv = tmp(2 * (size_t)nl);
@@ -1176,6 +1186,15 @@ public:
         cnt_[C_NTT_ROWS] += 2 * (size_t)nl;
         untmp(yp, 2 * (size_t)np);
         untmp(conv, 2 * (size_t)nl);
+        return o;
+    }
+    Ct keyswitch(const u32* d, int level, const u32* key, const u32* add0, const u32* add1) {
+        const int ne = hp_.nl(level) + hp_.n_p;
+        u32* ext = modup(d, level);
+        u32* acc = tmp(2 * (size_t)ne);
+        key_inner(acc, ext, d, key, level, 0);
+        untmp(ext, ext_rows(level));
+        Ct o = moddown(acc, level, add0, add1);
         untmp(acc, 2 * (size_t)ne);
         cnt_[C_KS]++;
         return o;
@@ -1465,7 +1484,8 @@ public:
         out[5] = kBootDeg;
     }
 
-    // diagonals of one group encoded at `level` (scale delta_level), cached
+    // diagonals of one group encoded at `level` (scale ptscale_level) on the Q limbs AND the
+    // P block (nl + n_p rows): the hoisted baby steps are summed in Q*P (lin_group); cached
     std::vector<std::vector<u32*>>& group_pts(BootGroupDev& G, int level) {
         auto it = G.pts.find(level);
         if (it != G.pts.end()) return it->second;
@@ -1479,46 +1499,78 @@ public:
                 const auto& d = g.diag[gg][b];
                 if (d.empty()) continue;
                 for (int p = 0; p < M; ++p) re[p] = d[p].real(), im[p] = d[p].imag();
-                encode_host(re.data(), im.data(), hp_.ptscale[level], hp_.nl(level), host);
-                P[gg][b] = upload_ntt(host, hp_.nl(level));
+                const int nl = hp_.nl(level), ne = nl + hp_.n_p;
+                encode_host(re.data(), im.data(), hp_.ptscale[level], nl, host, hp_.n_p);
+                u32* dv = tmp(ne);
+                HIP_OK(hipMemcpyAsync(dv, host.data(), host.size() * sizeof(u32), hipMemcpyHostToDevice, S()));
+                HIP_OK(hipStreamSynchronize(S()));
+                ntt(dv, ne, ne, extmap(nl));
+                P[gg][b] = dv;
             }
         HIP_OK(hipStreamSynchronize(S()));  // cached for every stream
         return G.pts.emplace(level, std::move(P)).first->second;
     }
 
-    // one merged butterfly group, baby-step giant-step (bootstrap.h)
+    // one merged butterfly group, baby-step giant-step (bootstrap.h) with hoisted baby steps
+    // (DESIGN.md §4): c1 is ModUp'ed ONCE; every baby rotation b is only a key inner product
+    // read through X -> X^{g_b} (u_b, in Q*P) plus the automorphism of c0 (a_b).  Each giant
+    // step sums its diagonals in Q*P and pays ONE ModDown:
+    //   inner = ModDown(sum_b P_b u_b) + (sum_b P_b a_b, P_0 c1),  a_0 = c0,
+    // then rescales and takes its giant rotation (a full key switch).
     Ct lin_group(const Ct& in, BootGroupDev& G) {
         const LinGroup& g = *G.g;
-        const int l = in.level, nl = hp_.nl(l), n = hp_.n;
+        const int l = in.level, nl = hp_.nl(l), np = hp_.n_p, ne = nl + np, n = hp_.n;
+        if (g.B > kMacMax) throw std::runtime_error("lin_group: more than 16 baby steps");
         auto& P = group_pts(G, l);
-        std::vector<Ct> baby(g.B);
-        std::vector<bool> own(g.B, false);
-        for (int b = 0; b < g.B; ++b) {
-            bool used = false;
-            for (int gg = 0; gg < g.G; ++gg) used = used || P[gg][b];
-            if (!used) continue;
-            if (b == 0) baby[b] = in;
-            else baby[b] = rotl(in, (long)g.h * b), own[b] = true;
+        const u32* c0 = in.data;
+        const u32* c1 = in.data + (size_t)nl * n;
+        std::vector<u32*> u(g.B, nullptr), a(g.B, nullptr);
+        bool any_baby = false;
+        for (int b = 1; b < g.B; ++b)
+            for (int gg = 0; gg < g.G; ++gg) any_baby = any_baby || P[gg][b];
+        if (any_baby) {
+            u32* ext = modup(c1, l);
+            for (int b = 1; b < g.B; ++b) {
+                bool used = false;
+                for (int gg = 0; gg < g.G; ++gg) used = used || P[gg][b];
+                if (!used) continue;
+                const u64 gal = rot_galois(-(int)((long)g.h * b));  // left rotation by h b
+                u[b] = tmp(2 * (size_t)ne);
+                key_inner(u[b], ext, c1, ksk(gal), l, gal);
+                a[b] = tmp(nl);
+                launch_automorph(S(), T_, a[b], c0, gal, nl);
+                cnt_[C_ROT]++;
+            }
+            untmp(ext, ext_rows(l));
         }
         Ct out;
         bool have = false;
-        u32* prod = tmp(2 * (size_t)nl);
+        u32* add0 = tmp(nl);
+        u32* add1 = tmp(nl);
         for (int gg = 0; gg < g.G; ++gg) {
-            Ct inner = alloc_ct(l, 2);
-            bool any = false;
+            MacTerms qp{}, q0{};
             for (int b = 0; b < g.B; ++b) {
                 if (!P[gg][b]) continue;
-                if (!any) {
-                    launch_mul_poly(S(), T_, inner.data, baby[b].data, P[gg][b], 2, nl, qmap());
-                    any = true;
-                } else {
-                    launch_mul_poly(S(), T_, prod, baby[b].data, P[gg][b], 2, nl, qmap());
-                    launch_add(S(), T_, inner.data, inner.data, prod, 2 * nl, nl, qmap());
-                }
+                q0.x[q0.n] = b == 0 ? c0 : a[b], q0.pt[q0.n++] = P[gg][b];
+                if (b) qp.x[qp.n] = u[b], qp.pt[qp.n++] = P[gg][b];
             }
-            if (!any) {
-                release(inner);
-                continue;
+            if (!q0.n) continue;
+            launch_mac(S(), T_, add0, q0, 0, 0, nl, 1, qmap());
+            Ct inner;
+            if (P[gg][0]) {
+                MacTerms q1{};
+                q1.x[0] = c1, q1.pt[0] = P[gg][0], q1.n = 1;
+                launch_mac(S(), T_, add1, q1, 0, 0, nl, 1, qmap());
+            }
+            if (qp.n) {
+                u32* acc = tmp(2 * (size_t)ne);
+                launch_mac(S(), T_, acc, qp, (size_t)ne * n, (size_t)ne * n, ne, 2, extmap(nl));
+                inner = moddown(acc, l, add0, P[gg][0] ? add1 : nullptr);
+                untmp(acc, 2 * (size_t)ne);
+            } else {  // only the unrotated diagonal
+                inner = alloc_ct(l, 2);
+                HIP_OK(hipMemcpyAsync(inner.data, add0, (size_t)nl * n * sizeof(u32), hipMemcpyDeviceToDevice, S()));
+                HIP_OK(hipMemcpyAsync(inner.data + (size_t)nl * n, add1, (size_t)nl * n * sizeof(u32), hipMemcpyDeviceToDevice, S()));
             }
             Ct rs = rescale(inner);
             release(inner);
@@ -1527,16 +1579,18 @@ public:
             if (!have) {
                 out = part, have = true;
             } else {
-                Ct s = add_sub(out, part, false);
+                Ct s2 = add_sub(out, part, false);
                 release(out);
                 release(part);
-                out = s;
+                out = s2;
             }
         }
-        untmp(prod, 2 * (size_t)nl);
-        for (int b = 0; b < g.B; ++b)
-            if (own[b]) release(baby[b]);
-        (void)n;
+        untmp(add0, nl);
+        untmp(add1, nl);
+        for (int b = 1; b < g.B; ++b) {
+            if (u[b]) untmp(u[b], 2 * (size_t)ne);
+            if (a[b]) untmp(a[b], nl);
+        }
         return out;
     }
 

@@ -142,8 +142,18 @@ void launch_base_convert(hipStream_t st, const DevTables& T, const ConvBatch& cb
 // acc[0|1][x] = sum_j e_j[x] * key[j][b|a][krow(x)] with e_j = ext[j] except on digit j's
 // own limbs (x < nl, x / alpha == j) where e_j = d (the NTT-form input);
 // ext: [nd][ne][N]; key: [dnum][2][nkey][N]
+// g != 0: ext and d are read through the automorphism X -> X^g (hoisted rotation)
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
-                      int alpha, int nkey, int nks, LimbMap map);
+                      int alpha, int nkey, int nks, LimbMap map, u64 g = 0);
+// out[p][t] = sum_j x_j[p][t] pt_j[t] over rows t < rows, polys p < npoly (x poly stride xs,
+// out poly stride os, in words)
+constexpr int kMacMax = 16;
+struct MacTerms {
+    const u32* x[kMacMax];
+    const u32* pt[kMacMax];
+    int n;
+};
+void launch_mac(hipStream_t st, const DevTables& T, u32* out, const MacTerms& m, size_t xs, size_t os, int rows, int npoly, LimbMap map);
 
 // --- sampling --------------------------------------------------------
 // kind: 0 ternary, 1 centred binomial (eta = 21); writes value mod prime into nl rows

@@ -197,11 +197,22 @@ __global__ void __launch_bounds__(kBlock) k_base_convert(ConvBatch cb, int nt, L
 }
 
 // digit j's own limbs (x < nl, x / alpha == j) come straight from the NTT-form input d
+// NTT-domain index read by the automorphism X -> X^g at output index i (bit-reversed order)
+__device__ __forceinline__ u32 galois_src(u32 i, u64 g, int logn) {
+    const u32 mask2n = (2u << logn) - 1;
+    const u32 e = 2u * (__brev(i) >> (32 - logn)) + 1u;
+    const u32 eg = (u32)(((u64)e * (g & mask2n)) & mask2n);
+    return __brev((eg - 1u) >> 1) >> (32 - logn);
+}
+
+// g != 0: the inputs (ext and d) are read through the automorphism X -> X^g -- a hoisted
+// rotation: one ModUp of c1 serves every rotation of the same ciphertext
 __global__ void k_key_inner(u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl, int alpha, int nkey, int nks,
-                            LimbMap map, const PrimeConst* pc, int logn, unsigned long long* ts) {
+                            u64 g, LimbMap map, const PrimeConst* pc, int logn, unsigned long long* ts) {
     ts_begin(ts);
     const int x = blockIdx.y;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t ks = g ? galois_src((u32)k, g, logn) : k;
     const PrimeConst P = pc[map.prime(x)];
     const int krow = x < nl ? x : nks + (x - nl);
     const int own = x < nl ? x / alpha : -1;
@@ -209,7 +220,7 @@ __global__ void k_key_inner(u32* acc, const u32* ext, const u32* d, const u32* k
     u64 s0 = 0, s1 = 0;
     for (int j = 0; j < nd; ++j) {
         if (j && (j & 7) == 0) s0 = fold64(s0, P.q, P.r32), s1 = fold64(s1, P.q, P.r32);
-        const u32 e = j == own ? d[((size_t)x << logn) + k] : ext[(((size_t)j * ne + x) << logn) + k];
+        const u32 e = j == own ? d[((size_t)x << logn) + ks] : ext[(((size_t)j * ne + x) << logn) + ks];
         const u32* kb = key + (((size_t)j * 2 * nkey + krow) << logn) + k;
         const u32* ka = kb + ((size_t)nkey << logn);
         s0 += (u64)e * *kb;
@@ -516,11 +527,35 @@ void launch_base_convert(hipStream_t st, const DevTables& T, const ConvBatch& cb
                 dim3((1u << T.logn) / kBlock, (nt + kConvTargets - 1) / kConvTargets, cb.n), dim3(kBlock), 0, st, cb, nt, map, T.pc,
                 T.logn);
 }
+
+namespace {
+// out[p][t] = sum_j x_j[p][t] * pt_j[t]  (mod the limb's prime): the diagonal products of
+// a linear transform, all terms of one giant step in one pass (64-bit multiply-adds)
+__global__ void k_mac(u32* out, MacTerms m, size_t xs, size_t os, LimbMap map, const PrimeConst* pc, int logn) {
+    const int t = blockIdx.y, p = blockIdx.z;
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t at = ((size_t)t << logn) + k;
+    const PrimeConst P = pc[map.prime(t)];
+    u64 acc = 0;
+    for (int j = 0; j < m.n; ++j) {
+        if (j && (j & 7) == 0) acc = fold64(acc, P.q, P.r32);
+        acc += (u64)m.x[j][p * xs + at] * m.pt[j][at];
+    }
+    out[p * os + at] = reduce64(acc, P.q, P.mu, P.r32);
+}
+}  // namespace
+
+void launch_mac(hipStream_t st, const DevTables& T, u32* out, const MacTerms& m, size_t xs, size_t os, int rows, int npoly, LimbMap map) {
+    if (m.n < 1 || m.n > kMacMax) throw std::runtime_error("launch_mac: 1..16 terms");
+    prof_launch(KID_ELEMENTWISE, words((2.0 * m.n + 1.0) * npoly * rows * (1u << T.logn)), k_mac,
+                dim3((1u << T.logn) / kBlock, rows, npoly), dim3(kBlock), 0, st, out, m, xs, os, map, T.pc, T.logn);
+}
+
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
-                      int alpha, int nkey, int nks, LimbMap map) {
+                      int alpha, int nkey, int nks, LimbMap map, u64 g) {
     // ext/d (nd x ne) + key (nd x 2 x ne) read, acc (2 x ne) written
     prof_launch_ts(KID_KEY_INNER, words((3.0 * nd + 2.0) * ne * (1u << T.logn)), k_key_inner, ew_grid(T.logn, ne), dim3(kBlock), 0, st, acc,
-                ext, d, key, nd, ne, nl, alpha, nkey, nks, map, T.pc, T.logn);
+                ext, d, key, nd, ne, nl, alpha, nkey, nks, g, map, T.pc, T.logn);
 }
 void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, u64 seed, u64 stream, int kind) {
     prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_small, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, nl, map, seed, stream, kind, T.pc,
