@@ -12,6 +12,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <deque>
+#include <chrono>
 #include <map>
 #include <mutex>
 #include <memory>
@@ -663,6 +664,23 @@ public:
     // rounding; returns a pool buffer of npoly x (nl - k) rows
     u32* drop_limbs(const u32* x, int np, int nl, int k) {
         const int n = hp_.n;
+        if (k == 2 && nl >= 3) {
+            // both primes at once: INTT of the two dropped rows per poly, then one fused
+            // CRT-spread -> NTT -> (cur - v) (q_a q_b)^{-1} pass over the r = nl - 2 kept limbs
+            const int r = nl - 2;
+            const u32 qa = hp_.mod[r], qb = hp_.mod[r + 1];
+            const u32 ainv = hinvm(qa % qb, qb);
+            u32* last = tmp(2 * (size_t)np);
+            intt(last, x, 2 * np, RowMap{2, nl, 2, r, 0}, LimbMap{2, r, 0});
+            u32* v = tmp((size_t)np * r);
+            u32* o = tmp((size_t)np * r);
+            launch_rescale2_ntt(S(), T_, o, x, last, v, d_rescale2_qinv_ + rescale2_off_[r], np, r, nl, qa, qb, ainv,
+                                shoup_pre(ainv, qb));
+            cnt_[C_NTT_ROWS] += (size_t)np * r;
+            untmp(last, 2 * (size_t)np);
+            untmp(v, (size_t)np * r);
+            return o;
+        }
         const u32* cur = x;
         u32* owned = nullptr;
         for (int step = 0; step < k; ++step) {
@@ -1810,6 +1828,7 @@ public:
     // around the loop: device time incl. launch gaps).  op 0: NTT of arg rows, 1: inverse
     // NTT of arg rows, 2: key switch (relinearisation key) at level arg, 3: rescale of a
     // 2-poly ciphertext at level arg, 4: ct x ct + relinearise + rescale at level arg
+    double bench_host_us_ = 0.0;  // host enqueue time per iteration of the last bench_op
     double bench_op(int op, int arg, int iters) {
         if (iters <= 0) throw std::runtime_error("bench_op: iters must be positive");
         const int n = hp_.n;
@@ -1834,7 +1853,9 @@ public:
         HIP_OK(hipEventCreate(&a));
         HIP_OK(hipEventCreate(&b));
         HIP_OK(hipEventRecord(a, S()));
+        const auto h0 = std::chrono::steady_clock::now();
         for (int i = 0; i < iters; ++i) run();
+        bench_host_us_ = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - h0).count() / iters;
         HIP_OK(hipEventRecord(b, S()));
         HIP_OK(hipEventSynchronize(b));
         float ms = 0.f;
@@ -1918,6 +1939,18 @@ private:
             }
         }
         d_rescale_qinv_ = dev_upload(rq);
+        // double rescale: dropping limbs r and r + 1 at once, (q_r q_{r+1})^{-1} mod q_t, t < r
+        rq.clear();
+        rescale2_off_.assign(hp_.n_q, 0);
+        for (int r = 1; r + 1 < hp_.n_q; ++r) {
+            rescale2_off_[r] = rq.size();
+            for (int t = 0; t < r; ++t) {
+                const u32 v = hinvm(mulm(q[r], q[r + 1], q[t]), q[t]);
+                rq.push_back(v);
+                rq.push_back(shoup_pre(v, q[t]));
+            }
+        }
+        d_rescale2_qinv_ = dev_upload(rq);
 
         // gadget: P mod q_t on Q limbs 0..n_ks-1 (Shoup pairs), indexed by ext row
         std::vector<u32> gad(2 * (size_t)(hp_.n_ks + hp_.n_p), 0);
@@ -2030,6 +2063,8 @@ private:
     u64 enc_ctr_ = 0;
     std::vector<u32> im_;
     u32* d_rescale_qinv_ = nullptr;
+    u32* d_rescale2_qinv_ = nullptr;
+    std::vector<size_t> rescale2_off_;
     std::vector<size_t> rescale_off_;
     u32* d_gadget_ = nullptr;
     u32* d_modup_ = nullptr;
@@ -2298,6 +2333,7 @@ int aesfhe_debug_keyswitch(aesfhe_ctx* ctx, int level, uint64_t g, const uint32_
 }
 int aesfhe_bench_op(aesfhe_ctx* ctx, int op, int arg, int iters, double* us) {
     API_BEGIN * us = ctx->eng->bench_op(op, arg, iters);
+    if (std::getenv("AESFHE_BENCH_HOST")) std::fprintf(stderr, "bench_op %d %d: gpu %.2f us, host enqueue %.2f us\n", op, arg, *us, ctx->eng->bench_host_us_);
     API_END
 }
 int aesfhe_counters(aesfhe_ctx* ctx, uint64_t* out, int n) {

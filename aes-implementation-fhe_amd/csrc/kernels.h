@@ -76,6 +76,8 @@ struct NttAux {
     const u32* add1 = nullptr;
     int cur_stride = 0, out_stride = 0;
     u32 q_last = 0;            // spread: modulus of the source row
+    u32 q_last2 = 0;           // spread2: second dropped prime (source rows a, b per group)
+    u32 qa_inv = 0, qa_inv_p = 0;  // spread2: q_last^{-1} mod q_last2 (Shoup pair)
 };
 // out-of-place (src may equal dst); supported ring sizes 2^13 .. 2^16
 void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map);
@@ -84,6 +86,11 @@ void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* dst, const u32* src
 // out[p][t] = (cur[p][t] - v) * qinv_t;  cur has nl_in rows per poly, out/v have nt
 void launch_rescale_ntt(hipStream_t st, const DevTables& T, u32* out, const u32* cur, const u32* last, u32* v, const u32* qinv,
                         int npoly, int nt, int nl_in, u32 q_last);
+// rescale by the two primes qa = q_last, qb = q_last2 at once (double-prime levels):
+// v = centred CRT of last[p][0..1] (mod qa qb) reduced mod q_t -> NTT ->
+// out[p][t] = (cur[p][t] - v) * (qa qb)^{-1}_t;  last has 2 rows per poly
+void launch_rescale2_ntt(hipStream_t st, const DevTables& T, u32* out, const u32* cur, const u32* last, u32* v, const u32* qinv,
+                         int npoly, int nt, int nl_in, u32 qa, u32 qb, u32 qa_inv, u32 qa_inv_p);
 // NTT of conv (npoly x nt dense rows, destroyed) fused with
 // out[p][t] = (cur[p * cur_stride + t] - NTT(conv)[p][t]) * qinv_t (+ add_p[t])   (ModDown)
 void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, const u32* cur, int cur_stride, const u32* qinv,

@@ -44,7 +44,7 @@ __device__ __forceinline__ void gs_bfly(u32& a, u32& b, u32 w, u32 wp, u32 q) {
 }
 __device__ __forceinline__ int swz(int w) { return w ^ ((w >> 4) & 15); }
 
-enum { kPlain = 0, kSpread = 1, kFinish = 1 };
+enum { kPlain = 0, kSpread = 1, kFinish = 1, kSpread2 = 2 };
 
 // key-switching ModUp: digit g's own limbs [g alpha, min(nl, (g + 1) alpha)) are not
 // transformed (they are already in NTT form in the input); block-uniform early exit
@@ -97,6 +97,28 @@ __global__ void __launch_bounds__(kThreads) k_ntt1_fwd(u32* dst, const u32* src,
             const u32 v = ra.src[(size_t)(g + T * k) * 256 + c];
             // q_last < 2^32/3 < 2q: the reductions are single conditional subtracts
             x[k] = v > half ? q - (ql - v) : csub(v, q);
+        }
+    } else if (MODE == kSpread2) {
+        // two dropped limbs a, b (rows src_off + grp * src_stride + {0, 1}): mixed-radix CRT
+        // v = x_a + qa ((x_b - x_a) qa^{-1} mod qb) in [0, qa qb), centred, reduced mod q
+        const int grp = blockIdx.y / rm.cnt;
+        const u32* sa = src + ((size_t)(rm.src_off + grp * rm.src_stride) << LOGN);
+        const u32* sb = sa + ((size_t)1 << LOGN);
+        const u32 qa = aux.q_last, qb = aux.q_last2;
+        const u64 Q2 = (u64)qa * qb, half = Q2 >> 1;
+        const u32 mu = pc[ra.prime].mu;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const size_t at = (size_t)(g + T * k) * 256 + c;
+            const u32 xa = sa[at], xb = sb[at];
+            const u32 d = shoup_mul(xb + qb - csub(xa, qb), aux.qa_inv, aux.qa_inv_p, qb);
+            const u64 v = (u64)xa + (u64)qa * d;
+            if (v > half) {
+                const u32 r = barrett_reduce64(Q2 - v, q, mu);
+                x[k] = r ? q - r : 0u;
+            } else {
+                x[k] = barrett_reduce64(v, q, mu);
+            }
         }
     } else {
 #pragma unroll
@@ -370,6 +392,14 @@ void launch_rescale_ntt(hipStream_t st, const DevTables& T, u32* out, const u32*
     aux.cur = cur, aux.out = out, aux.qinv = qinv, aux.cur_stride = nl_in, aux.out_stride = nt, aux.q_last = q_last;
     const RowMap rm{nt, 1, nt, 0, 0};
     ntt_fwd_dispatch<kSpread, kFinish>(st, T, v, last, npoly * nt, npoly * nt, rm, LimbMap{1 << 30, 0, 0}, aux);
+}
+void launch_rescale2_ntt(hipStream_t st, const DevTables& T, u32* out, const u32* cur, const u32* last, u32* v, const u32* qinv,
+                         int npoly, int nt, int nl_in, u32 qa, u32 qb, u32 qa_inv, u32 qa_inv_p) {
+    NttAux aux{};
+    aux.cur = cur, aux.out = out, aux.qinv = qinv, aux.cur_stride = nl_in, aux.out_stride = nt;
+    aux.q_last = qa, aux.q_last2 = qb, aux.qa_inv = qa_inv, aux.qa_inv_p = qa_inv_p;
+    const RowMap rm{nt, 2, nt, 0, 0};
+    ntt_fwd_dispatch<kSpread2, kFinish>(st, T, v, last, npoly * nt, npoly * nt, rm, LimbMap{1 << 30, 0, 0}, aux);
 }
 void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, const u32* cur, int cur_stride, const u32* qinv,
                        const u32* add0, const u32* add1, int npoly, int nt) {

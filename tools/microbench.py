@@ -19,7 +19,7 @@ def main():
             us = E.bench_op(op, rows, 200)
             res[f"{op}_{rows}"] = {"us": us, "GBps_2pass": 4 * rows * row_bytes / us / 1e3}
     for op in ("keyswitch", "rescale", "mul_relin_rescale"):
-        for lv in (2, 10, 17, 25, 32):
+        for lv in sorted({2, 10, 17, 25, E.L}):
             res[f"{op}_L{lv}"] = {"us": E.bench_op(op, lv, 50), "limbs": E.nl(lv)}
     print(json.dumps(res, indent=1))
 
