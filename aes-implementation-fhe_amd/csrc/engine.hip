@@ -1348,9 +1348,25 @@ public:
     // entirely on the device: raw decryption of both tensors on 2..4 limbs, mixed-radix CRT,
     // the 16 state slots evaluated directly, snap to the nearest zeta16 power, closed-form
     // re-encoding (every other slot 1) and fresh encryption -- no host round trip
-    void renorm_pair(aesfhe_handle hh, aesfhe_handle hl, aesfhe_handle* oh, aesfhe_handle* ol) {
+    //
+    // states > 1 is the slot-packed layout: state b of the
+    // batch holds byte i in slot i * stride + b, so every slot with (j mod stride) < states is
+    // snapped and the rest are reset to 1.  The whole slot vector is decoded and re-encoded
+    // with a device fp64 FFT (launch_fft2); states == 1 keeps the 16-slot direct evaluation.
+    void renorm_pair(aesfhe_handle hh, aesfhe_handle hl, aesfhe_handle* oh, aesfhe_handle* ol) { renorm_states(hh, hl, 1, oh, ol); }
+    void renorm_states(aesfhe_handle hh, aesfhe_handle hl, int states, aesfhe_handle* oh, aesfhe_handle* ol) {
         if (!d_pk_) throw std::runtime_error("keys not generated");
         const int n = hp_.n, s = slot_count(), stride = s / 16;
+        if (states < 1 || states > stride)
+            throw std::runtime_error("renorm: states per ciphertext must be in [1, slot_count / 16]");
+        if (states > 1 && !d_slot_pos_) {
+            std::vector<u32> pos(s);
+            const u64 two_n = 2ull * n;
+            u64 e = 1;
+            for (int j = 0; j < s; ++j) pos[j] = (u32)((e - 1) / 2), e = e * 5 % two_n;
+            d_slot_pos_ = dev_alloc(s);
+            HIP_OK(hipMemcpy(d_slot_pos_, pos.data(), sizeof(u32) * s, hipMemcpyHostToDevice));
+        }
         if (slots_.e[1] == 0) {
             const u64 two_n = 2ull * n;
             u64 e = 1;
@@ -1389,14 +1405,27 @@ public:
             if (own) release(c);
             cnt_[C_DEC]++;
         }
-        double* acc = d_codec_[t_sidx];
-        double* wv = acc + 64;
-        HIP_OK(hipMemsetAsync(acc, 0, 64 * sizeof(double), S()));
-        launch_decode16(S(), T_, x, kd, cc, slots_, isc, acc);
-        launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
         const int f = hp_.fresh, nq = hp_.nl(f) + 1;
+        const double enc_scale = hp_.delta[f] * (double)hp_.mod[hp_.nl(f)];
         u32* m = tmp(2 * (size_t)nq);
-        launch_encode16(S(), T_, m, wv, slots_, hp_.delta[f] * (double)hp_.mod[hp_.nl(f)], nq);
+        if (states == 1) {
+            double* acc = d_codec_[t_sidx];
+            double* wv = acc + 64;
+            HIP_OK(hipMemsetAsync(acc, 0, 64 * sizeof(double), S()));
+            launch_decode16(S(), T_, x, kd, cc, slots_, isc, acc);
+            launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
+            launch_encode16(S(), T_, m, wv, slots_, enc_scale, nq);
+        } else {
+            double*& zbuf = d_fft_[t_sidx];
+            if (!zbuf) zbuf = (double*)dev_alloc((size_t)2 * 2 * 2 * 2 * n);  // 2 buffers x [2][N] complex double
+            double* z = zbuf;
+            double* w = zbuf + (size_t)2 * 2 * n;
+            launch_decode_twist(S(), T_, x, kd, cc, isc, z);
+            launch_fft2(S(), T_, z, 1);
+            launch_snap_slots(S(), T_, z, w, d_slot_pos_, states);
+            launch_fft2(S(), T_, w, -1);
+            launch_encode_untwist(S(), T_, m, w, enc_scale, nq);
+        }
         ntt(m, 2 * nq, nq, qmap());
         Ct a = encrypt_ntt(m);
         Ct b = encrypt_ntt(m + (size_t)nq * n);
@@ -2080,6 +2109,8 @@ private:
     Slot16 slots_ = {};
     double* d_codec_[kStreams] = {};
     int* d_nib_[kStreams] = {};
+    double* d_fft_[kStreams] = {};  // slot-packed renorm: [2 buffers][2 cts][N] complex double
+    u32* d_slot_pos_ = nullptr;     // (5^j mod 2N - 1) / 2 for slot j < N/2
     u32* d_s2_ = nullptr;
     bool lazy_ = true;  // defer relinearisation / rescales of API-level products
 
@@ -2301,6 +2332,11 @@ int aesfhe_boot_info(aesfhe_ctx* ctx, double* out) {
 }
 int aesfhe_renorm_pair(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle* out_hi, aesfhe_handle* out_lo) {
     API_BEGIN ctx->eng->renorm_pair(hi, lo, out_hi, out_lo);
+    API_END
+}
+int aesfhe_renorm_states(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, int states, aesfhe_handle* out_hi,
+                         aesfhe_handle* out_lo) {
+    API_BEGIN ctx->eng->renorm_states(hi, lo, states, out_hi, out_lo);
     API_END
 }
 int aesfhe_export(aesfhe_ctx* ctx, aesfhe_handle c, uint32_t* out, uint64_t words) {

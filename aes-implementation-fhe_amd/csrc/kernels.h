@@ -193,6 +193,23 @@ void launch_snap16(hipStream_t st, const double* acc, double* w, int* nib);
 // out[c][t][k] = round(scale (delta_{k0} + (2/N) Re sum_i w_ci e^{-i pi e_i k / N})) mod q_t, t < nq
 void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq);
 
+// --- slot-packed Zeta16 renorm ----------------------
+// Full canonical-embedding decode / encode on the device in fp64: the slots of a real
+// polynomial m are a length-N DFT of the twisted coefficients m_k zeta^k (encoder.cpp),
+// computed as a four-step FFT over an N1 x N2 row-major matrix (N1 = 2^ceil(logn/2)).
+// Element t of a transform's output is stored at fft_loc(t) = (t mod N1) N2 + t / N1.
+// x: [2][4][N] coefficient residues (kd[c] limbs) -> z[c][k] = m_k / scale_c * zeta^k
+void launch_decode_twist(hipStream_t st, const DevTables& T, const u32* x, const int kd[2], const CrtConsts cc[2],
+                         const double inv_scale[2], double* z);
+// in-place X_k = sum_n x_n e^{sign 2 pi i n k / N} on 2 vectors (complex double, [2][N]);
+// input in natural order, output at fft_loc
+void launch_fft2(hipStream_t st, const DevTables& T, double* z, int sign);
+// snap: slot j (value at fft_loc(slot_pos[j]) of zin) -> zeta16 power if (j mod stride) < states,
+// else 1; writes w[slot_pos[j]] = v and w[N - 1 - slot_pos[j]] = conj(v) (natural order)
+void launch_snap_slots(hipStream_t st, const DevTables& T, const double* zin, double* w, const u32* slot_pos, int states);
+// out[c][t][k] = round(scale Re(v[fft_loc(k)] zeta^{-k}) / N) mod q_t, t < nq
+void launch_encode_untwist(hipStream_t st, const DevTables& T, u32* out, const double* v, double scale, int nq);
+
 // --- fused LUT evaluation ---------------------------
 // Elements are canonical ciphertexts at data levels >= the output level l; only their first
 // nl(l) limbs are read (exact modulo Q_l) and each element's own scale is folded into the

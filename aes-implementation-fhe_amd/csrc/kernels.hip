@@ -425,6 +425,116 @@ __global__ void __launch_bounds__(kBlock) k_encode16(u32* out, const double* w, 
 }
 
 // ------------------------------------------------------------------------------------
+// slot-packed renorm: fp64 canonical embedding on the device (four-step FFT)
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ int fft_log1(int logn) { return logn - logn / 2; }  // log N1 (N1 >= N2)
+
+__global__ void __launch_bounds__(kBlock) k_decode_twist(const u32* x, int kd0, int kd1, CrtConsts cc0, CrtConsts cc1, double is0,
+                                                         double is1, double2* z, int logn) {
+    const int c = blockIdx.y;
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    const int kd = c ? kd1 : kd0;
+    u32 r[4];
+    for (int i = 0; i < kd; ++i) r[i] = x[((size_t)(c * 4 + i) << logn) + k];
+    const double m = crt_centered(r, kd, c ? cc1 : cc0) * (c ? is1 : is0);
+    double sn, cs;
+    sincospi((double)k / (double)(1 << logn), &sn, &cs);
+    z[((size_t)c << logn) + k] = make_double2(m * cs, m * sn);
+}
+
+// kFftTpb transforms of length L = 2^logl per block, one LDS row each, radix-2 DIT after a
+// bit-reversed load.  pass 0: the columns of the N1 x N2 matrix (element stride N2), then the
+// four-step twiddle e^{sign 2 pi i n2 k1 / N}; pass 1: its rows (contiguous)
+constexpr int kFftTpb = 16;
+__global__ void __launch_bounds__(kBlock) k_fft_pass(double2* data, int logn, int pass, int sign) {
+    __shared__ double2 buf[kFftTpb][257];
+    const int l1 = fft_log1(logn), l2 = logn - l1;
+    const int logl = pass ? l2 : l1;
+    const int L = 1 << logl, n2 = 1 << l2;
+    double2* d = data + ((size_t)blockIdx.y << logn);
+    const int t0 = blockIdx.x * kFftTpb;  // first column (pass 0) / row (pass 1)
+    for (int idx = threadIdx.x; idx < kFftTpb * L; idx += kBlock) {
+        int e, i;
+        size_t a;
+        if (pass == 0) e = idx / kFftTpb, i = idx % kFftTpb, a = (size_t)e * n2 + t0 + i;
+        else i = idx >> logl, e = idx & (L - 1), a = (size_t)(t0 + i) * n2 + e;
+        buf[i][__brev((unsigned)e) >> (32 - logl)] = d[a];
+    }
+    __syncthreads();
+    for (int h = 1; h < L; h <<= 1) {
+        for (int b = threadIdx.x; b < kFftTpb * L / 2; b += kBlock) {
+            const int i = b >> (logl - 1), j = b & (L / 2 - 1);
+            const int pos = j & (h - 1);
+            const int i0 = ((j - pos) << 1) + pos, i1 = i0 + h;
+            double sn, cs;
+            sincospi((double)(sign * pos) / (double)h, &sn, &cs);
+            const double2 u = buf[i][i0], v = buf[i][i1];
+            const double2 vw = make_double2(v.x * cs - v.y * sn, v.x * sn + v.y * cs);
+            buf[i][i0] = make_double2(u.x + vw.x, u.y + vw.y);
+            buf[i][i1] = make_double2(u.x - vw.x, u.y - vw.y);
+        }
+        __syncthreads();
+    }
+    const double inv_half_n = 2.0 / (double)(1 << logn);
+    for (int idx = threadIdx.x; idx < kFftTpb * L; idx += kBlock) {
+        if (pass == 0) {
+            const int e = idx / kFftTpb, i = idx % kFftTpb;
+            const long tw = (long)(t0 + i) * e;  // n2 k1 < N
+            double sn, cs;
+            sincospi((double)(sign * tw) * inv_half_n, &sn, &cs);
+            const double2 v = buf[i][e];
+            d[(size_t)e * n2 + t0 + i] = make_double2(v.x * cs - v.y * sn, v.x * sn + v.y * cs);
+        } else {
+            const int i = idx >> logl, e = idx & (L - 1);
+            d[(size_t)(t0 + i) * n2 + e] = buf[i][e];
+        }
+    }
+}
+
+__device__ __forceinline__ size_t fft_loc(u32 t, int logn) {
+    const int l1 = fft_log1(logn);
+    return ((size_t)(t & ((1u << l1) - 1)) << (logn - l1)) + (t >> l1);
+}
+
+__global__ void __launch_bounds__(kBlock) k_snap_slots(const double2* zin, double2* w, const u32* slot_pos, int states, int logn) {
+    const int c = blockIdx.y;
+    const int j = blockIdx.x * kBlock + threadIdx.x;  // slot < N/2
+    const int n = 1 << logn;
+    const u32 t = slot_pos[j];
+    const int stride = (n / 2) / 16;
+    double2 v = make_double2(1.0, 0.0);
+    if (j % stride < states) {
+        const double2 z = zin[((size_t)c << logn) + fft_loc(t, logn)];
+        const double kf = rint(-atan2(z.y, z.x) * 16.0 / (2.0 * M_PI));
+        const int nib = (int)((((long)kf) % 16 + 16) % 16);
+        double sn, cs;
+        sincospi(-2.0 * nib / 16.0, &sn, &cs);
+        v = make_double2(cs, sn);
+    }
+    double2* wc = w + ((size_t)c << logn);
+    wc[t] = v;
+    wc[n - 1 - t] = make_double2(v.x, -v.y);
+}
+
+__global__ void __launch_bounds__(kBlock) k_encode_untwist(u32* out, const double2* v, double scale, int nq, const PrimeConst* pc,
+                                                           int logn) {
+    const int c = blockIdx.y;
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    const double2 z = v[((size_t)c << logn) + fft_loc((u32)k, logn)];
+    double sn, cs;
+    sincospi((double)k / (double)(1 << logn), &sn, &cs);
+    const double m = (z.x * cs + z.y * sn) / (double)(1 << logn);
+    const double x = rint(m * scale);
+    for (int t = 0; t < nq; ++t) {
+        const double q = (double)pc[t].q;
+        double r = fma(-q, floor(x / q), x);
+        if (r < 0) r += q;
+        if (r >= q) r -= q;
+        out[((size_t)(c * nq + t) << logn) + k] = (u32)r;
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // fused LUT evaluation: one launch per LUT instead of a tensor + constant + add per term
 // ------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(kBlock) k_lut_bivariate(u32* out, LutOperands op, int n_a, const u32* cst, int nl,
@@ -581,6 +691,29 @@ void launch_snap16(hipStream_t st, const double* acc, double* w, int* nib) {
 void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq) {
     prof_launch(KID_ELEMENTWISE, words(2.0 * nq * (1u << T.logn)), k_encode16, dim3((1u << T.logn) / kBlock, 2), dim3(kBlock), 0, st, out,
                 w, sl, scale, nq, T.pc, T.logn);
+}
+
+void launch_decode_twist(hipStream_t st, const DevTables& T, const u32* x, const int kd[2], const CrtConsts cc[2],
+                         const double inv_scale[2], double* z) {
+    const double n = (double)(1u << T.logn);
+    prof_launch(KID_ELEMENTWISE, words((kd[0] + kd[1]) * n) + 32.0 * n, k_decode_twist, dim3((1u << T.logn) / kBlock, 2), dim3(kBlock),
+                0, st, x, kd[0], kd[1], cc[0], cc[1], inv_scale[0], inv_scale[1], (double2*)z, T.logn);
+}
+void launch_fft2(hipStream_t st, const DevTables& T, double* z, int sign) {
+    const int l1 = T.logn - T.logn / 2, l2 = T.logn - l1;
+    for (int pass = 0; pass < 2; ++pass)
+        prof_launch(KID_ELEMENTWISE, 64.0 * (1u << T.logn), k_fft_pass, dim3((1u << (pass ? l1 : l2)) / kFftTpb, 2), dim3(kBlock), 0, st,
+                    (double2*)z, T.logn, pass, sign);
+}
+void launch_snap_slots(hipStream_t st, const DevTables& T, const double* zin, double* w, const u32* slot_pos, int states) {
+    const double s = (double)(1u << (T.logn - 1));
+    prof_launch(KID_ELEMENTWISE, 2.0 * (16.0 * s + 4.0 * s + 32.0 * s), k_snap_slots, dim3((1u << (T.logn - 1)) / kBlock, 2),
+                dim3(kBlock), 0, st, (const double2*)zin, (double2*)w, slot_pos, states, T.logn);
+}
+void launch_encode_untwist(hipStream_t st, const DevTables& T, u32* out, const double* v, double scale, int nq) {
+    const double n = (double)(1u << T.logn);
+    prof_launch(KID_ELEMENTWISE, 32.0 * n + words(2.0 * nq * n), k_encode_untwist, dim3((1u << T.logn) / kBlock, 2), dim3(kBlock), 0,
+                st, out, (const double2*)v, scale, nq, T.pc, T.logn);
 }
 
 void launch_lut_bivariate(hipStream_t st, const DevTables& T, u32* out, const LutOperands& op, int n_a, const u32* cst, int nl) {

@@ -163,9 +163,10 @@ class EngineContext:
         HIP streams; sequential when the context was built with concurrent=False."""
         return self.engine.parallel(*fns)
 
-    def renorm_pair(self, hi, lo):
-        """Device-side Zeta16 secret-key renorm of a (hi, lo) state pair (REF/pipeline.py:65-69)."""
-        return self.engine.renorm_pair(hi, lo)
+    def renorm_pair(self, hi, lo, states: int = 1):
+        """Device-side Zeta16 secret-key renorm of a (hi, lo) state pair (REF/pipeline.py:65-69);
+        `states` > 1: that many slot-packed states per pair (StateEncoder)."""
+        return self.engine.renorm_pair(hi, lo, states)
 
     def lut(self, key, coeffs, c0: complex = 0j):
         """Engine-side coefficient set of a LUT polynomial, created once per key."""

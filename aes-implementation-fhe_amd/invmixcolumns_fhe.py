@@ -14,15 +14,15 @@ from utils import pair
 
 
 class InvMixColumnsFHE:
-    def __init__(self, ctx, xor4: XOR4LUT, use_hard_renorm: bool = True):
+    def __init__(self, ctx, xor4: XOR4LUT, use_hard_renorm: bool = True, states: int = 1):
         self.ctx = ctx
         self.xor4 = xor4
         self.sc = ctx.engine.slot_count
         self.stride = self.sc // 16
         self._coeffs = _CoeffCache()
-        self.enc = StateEncoder(ctx)
+        self.enc = StateEncoder(ctx, states)  # states > 1: slot-packed batch (state_encoder.py)
         self.use_hard_renorm = use_hard_renorm
-        self._pt_row: List[Any] = row_masks(ctx, self.sc)
+        self._pt_row: List[Any] = row_masks(ctx, self.sc, states)
 
     def _basis16(self, ct):
         return gf_basis16(self.ctx, ct)

@@ -114,19 +114,19 @@ def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo):
 
 
 class MixColFinal:
-    def __init__(self, ctx, xor4: XOR4LUT, stride: int | None = None):
+    def __init__(self, ctx, xor4: XOR4LUT, stride: int | None = None, states: int = 1):
         self.ctx = ctx
         self.xor4 = xor4
         self.sc = ctx.engine.slot_count
         self.stride = stride if stride is not None else self.sc // 16
         self._coeffs = _CoeffCache()
-        self.enc = StateEncoder(ctx)
+        self.enc = StateEncoder(ctx, states)  # states > 1: slot-packed batch (state_encoder.py)
         self._zero = None
 
     # zero-state pair, built lazily (REF :58-62 builds it eagerly; only _normalize_via_xor_zero uses it)
     def _normalize_via_xor_zero(self, ct, which: str):
         if self._zero is None:
-            self._zero = self.enc.encode(np.zeros(16, dtype=np.uint8))
+            self._zero = self.enc.encode(np.zeros(16 if self.enc.states == 1 else (self.enc.states, 16), dtype=np.uint8))
         return self._xor_ct(ct, self._zero[0] if which == "hi" else self._zero[1])
 
     def _basis16(self, ct):

@@ -8,6 +8,11 @@ Documented deviation: the shipped decrypt (REF/pipeline.py:230
 never applies InvMixColumns, so it cannot invert encrypt.  ``decrypt`` here inserts it
 after AddRoundKey as the reference README prescribes (REF/README.md:87-94);
 ``with_inv_mix_columns=False`` reproduces the shipped order.
+
+``states`` = B > 1 runs B independent AES states per ciphertext pair in the slot-packed
+layout (state_encoder.py): ``encrypt`` / ``decrypt`` take and return
+(B, 16) arrays through the same step sequence, and a (16,) round key is shared by all B
+states (a (B, 16) key array gives each state its own).
 """
 from __future__ import annotations
 
@@ -28,34 +33,45 @@ from xor4_lut import XOR4LUT
 class AESPipeline:
     def __init__(self, ctx, coeffs: Dict[str, Any], *, mixcolumns: MixColFinal | None = None,
                  inv_mixcolumns: InvMixColumnsFHE | None = None, use_hard_renorm_between_steps: bool = False,
-                 with_inv_mix_columns: bool = True):
+                 with_inv_mix_columns: bool = True, states: int = 1):
         self.ctx = ctx
-        self.encoder = StateEncoder(ctx)
+        self.states = states
+        self.encoder = StateEncoder(ctx, states)
         self.sc = ctx.engine.slot_count
         self.stride = self.sc // 16
         self.xor4 = XOR4LUT(ctx, coeffs["xor4"])
         self.sub = SubBytesLUT(ctx, coeffs["sub_hi"], coeffs["sub_lo"])
         self.isub = SubBytesLUT(ctx, coeffs["inv_sub_hi"], coeffs["inv_sub_lo"]) if "inv_sub_hi" in coeffs else None
-        self.shift = ShiftRows(ctx)
-        self.invshift = InvShiftRows(ctx)
-        self.mix = mixcolumns if mixcolumns is not None else MixColFinal(ctx, self.xor4)
-        self.invmix = inv_mixcolumns if inv_mixcolumns is not None else InvMixColumnsFHE(ctx, self.xor4)
+        self.shift = ShiftRows(ctx, states=states)
+        self.invshift = InvShiftRows(ctx, states=states)
+        self.mix = mixcolumns if mixcolumns is not None else MixColFinal(ctx, self.xor4, states=states)
+        self.invmix = inv_mixcolumns if inv_mixcolumns is not None else InvMixColumnsFHE(ctx, self.xor4, states=states)
+        for mod in (self.mix, self.invmix):
+            enc = getattr(mod, "enc", None)
+            if enc is not None and getattr(enc, "states", 1) != states:
+                raise ValueError("mixcolumns / inv_mixcolumns were built for a different states-per-ciphertext count")
         self.ark = AddRoundKey(self.xor4)
         self.use_hard_renorm_between_steps = use_hard_renorm_between_steps
         self.with_inv_mix_columns = with_inv_mix_columns
         self._rk_cache: List[Tuple[Any, Any]] | None = None
+        self._rk_tag = b""
 
     # ---------------------------------------------------------------- utils
     def _renorm_pair(self, hi, lo):
         return self.encoder.renorm(hi, lo) if self.use_hard_renorm_between_steps else (hi, lo)
 
     def _encode_key(self, key_bytes: np.ndarray):
-        assert key_bytes.shape == (16,)
-        return self.encoder.encode(key_bytes.astype(np.uint8))
+        key_bytes = np.asarray(key_bytes, dtype=np.uint8)
+        if self.states > 1 and key_bytes.shape == (16,):
+            key_bytes = np.broadcast_to(key_bytes, (self.states, 16))
+        assert key_bytes.shape == ((16,) if self.states == 1 else (self.states, 16))
+        return self.encoder.encode(key_bytes)
 
     def _prepare_round_keys(self, round_keys: List[np.ndarray]):
-        if self._rk_cache is None or len(self._rk_cache) != len(round_keys):
+        tag = b"".join(np.ascontiguousarray(k, dtype=np.uint8).tobytes() for k in round_keys)
+        if self._rk_cache is None or self._rk_tag != tag:  # encrypted round keys are reused across calls
             self._rk_cache = [self._encode_key(np.asarray(k, dtype=np.uint8)) for k in round_keys]
+            self._rk_tag = tag
         return self._rk_cache
 
     def _log_pair(self, dbg, tag: str, ct_hi, ct_lo, **meta) -> None:
@@ -104,7 +120,7 @@ class AESPipeline:
     def encrypt(self, state: np.ndarray, round_keys: List[np.ndarray], debug: Dict[str, Any] | None = None):
         if debug is not None:
             debug.clear()
-        ct = self.encoder.encode(np.asarray(state, dtype=np.uint8))
+        ct = self.encoder.encode(state)
         self._log_pair(debug, "enc.input", *ct)
         rk = self._prepare_round_keys(round_keys)
         ct = self.add_round_key(*ct, *rk[0])

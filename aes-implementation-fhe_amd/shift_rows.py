@@ -2,6 +2,9 @@
 
 Row r occupies slots (r + 4c)*stride; ShiftRows rotates row r left by r columns, i.e.
 the masked row is rotated by -4r*stride slots (np.roll semantics).
+With ``states`` = B slot-packed states (state_encoder.py) the row masks cover slots
+(r + 4c)*stride + b for b < B (REF/temp/mixcolumns_desilo_port.py:60-65 builds the same
+per-block masks); B = 1 is the reference's mask exactly.
 """
 from typing import Any, List
 
@@ -9,12 +12,13 @@ import numpy as np
 from utils import pair
 
 
-def row_masks(ctx, sc: int) -> List[Any]:
+def row_masks(ctx, sc: int, states: int = 1) -> List[Any]:
     stride = sc // 16
     masks = []
     for r in range(4):
         m = np.zeros(sc, dtype=np.complex128)
-        m[[(r + 4 * c) * stride for c in range(4)]] = 1.0
+        for c in range(4):
+            m[(r + 4 * c) * stride:(r + 4 * c) * stride + states] = 1.0
         masks.append(ctx.encode(m))
     return masks
 
@@ -22,11 +26,12 @@ def row_masks(ctx, sc: int) -> List[Any]:
 class ShiftRows:
     direction = -1
 
-    def __init__(self, ctx):
+    def __init__(self, ctx, states: int = 1):
         self.ctx = ctx
         self.sc = ctx.engine.slot_count
         self.stride = self.sc // 16
-        self._pt_masks = row_masks(ctx, self.sc)
+        self.states = states
+        self._pt_masks = row_masks(ctx, self.sc, states)
         self._rot_steps = [self.direction * 4 * r * self.stride for r in range(4)]
 
     def _apply_one(self, ct: Any) -> Any:

@@ -2,6 +2,12 @@
 
 Byte i (column-first order, REF/README.md:103-104) goes to slot i*stride with
 stride = slot_count/16; every other slot holds 1+0j.
+
+``states`` > 1 selects the slot-packed layout (the paper's layout in
+REF/main.py:121-140): state b of a batch of B <= stride states holds byte i in slot
+i*stride + b.  Every rotation the AES modules issue is a multiple of stride, so the B
+columns never mix; slots with (j mod stride) >= B hold 1+0j as in the reference.
+``encode`` then takes a (B, 16) uint8 array and ``decode`` returns one.
 """
 from typing import Any, Tuple
 
@@ -11,30 +17,46 @@ from utils import ZetaEncoder
 
 
 class StateEncoder:
-    def __init__(self, ctx):
+    def __init__(self, ctx, states: int = 1):
         self.ctx = ctx
         self.sc = ctx.engine.slot_count
         self.stride = self.sc // 16
+        if not 1 <= states <= self.stride:
+            raise ValueError(f"states per ciphertext must be in [1, {self.stride}], got {states}")
+        self.states = states
+
+    def _as_batch(self, state: np.ndarray) -> np.ndarray:
+        state = np.asarray(state, dtype=np.uint8)
+        if state.shape == (16,) and self.states == 1:
+            return state[None, :]
+        if state.shape != (self.states, 16):
+            raise ValueError(f"expected a ({self.states}, 16) uint8 state array, got {state.shape}")
+        return state
 
     def _pack(self, nibbles: np.ndarray) -> np.ndarray:
+        """nibbles (B, 16) -> slot vector; slot i*stride + b <- zeta^nibbles[b, i]"""
         vec = np.ones(self.sc, dtype=np.complex128)
-        vec[0:16 * self.stride:self.stride] = ZetaEncoder.to_zeta(nibbles.astype(np.uint8), 16)
+        grid = vec[:16 * self.stride].reshape(16, self.stride)
+        grid[:, :nibbles.shape[0]] = ZetaEncoder.to_zeta(nibbles.astype(np.uint8).T, 16)
         return vec
 
+    def _take(self, slots: np.ndarray) -> np.ndarray:
+        """slot vector -> (B, 16) state slots"""
+        return slots[:16 * self.stride].reshape(16, self.stride)[:, :self.states].T
+
     def encode(self, state: np.ndarray) -> Tuple[Any, Any]:
-        state = np.asarray(state, dtype=np.uint8)
-        assert state.shape == (16,)
-        return self.ctx.encrypt(self._pack(state >> 4)), self.ctx.encrypt(self._pack(state & 0x0F))
+        st = self._as_batch(state)
+        return self.ctx.encrypt(self._pack(st >> 4)), self.ctx.encrypt(self._pack(st & 0x0F))
 
     def decode(self, ct_hi, ct_lo) -> np.ndarray:
-        take = slice(0, 16 * self.stride, self.stride)
-        hi = ZetaEncoder.from_zeta(self.ctx.decrypt(ct_hi)[take], 16)
-        lo = ZetaEncoder.from_zeta(self.ctx.decrypt(ct_lo)[take], 16)
-        return ((hi << 4) | lo).astype(np.uint8)
+        hi = ZetaEncoder.from_zeta(self._take(self.ctx.decrypt(ct_hi)), 16)
+        lo = ZetaEncoder.from_zeta(self._take(self.ctx.decrypt(ct_lo)), 16)
+        out = ((hi << 4) | lo).astype(np.uint8)
+        return out[0] if self.states == 1 else out
 
     def renorm(self, ct_hi, ct_lo) -> Tuple[Any, Any]:
         """decode -> re-encode (REF/pipeline.py:65-69), done on the device when available."""
         fast = getattr(self.ctx, "renorm_pair", None)
         if fast is not None:
-            return fast(ct_hi, ct_lo)
+            return fast(ct_hi, ct_lo) if self.states == 1 else fast(ct_hi, ct_lo, states=self.states)
         return self.encode(self.decode(ct_hi, ct_lo))

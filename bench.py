@@ -50,6 +50,10 @@ def parse():
     ap.add_argument("--dry-run", action="store_true",
                     help="host orchestration only (process group, sharding, barrier, max-over-ranks, rank-0 line) with the "
                          "byte-level AES in place of the FHE engine; prints value null -- a test harness, not a measurement")
+    ap.add_argument("--batch-states", type=int, default=1024,
+                    help="secondary measurement (BASELINE configs 3/4): this many independent states per rank, "
+                         "slot-packed into one ciphertext pair (SURVEY.md 8(f)1); 0 = skip")
+    ap.add_argument("--batch-steps", type=int, default=1)
     ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r1_pmc_traffic.json"), help="per-launch HBM bytes from a rocprofv3 PMC pass")
     return ap.parse_args()
 
@@ -143,6 +147,37 @@ def rank_states(rank: int, n: int):
     return [rng.integers(0, 256, 16).astype(np.uint8) for _ in range(n)]
 
 
+def run_batch(ctx, coeffs, rks, args, rank, world, dist) -> dict:
+    """BASELINE configs 3/4: `--batch-states` independent states per rank under one shared
+    key, slot-packed in one ciphertext pair (state b in slots i*stride + b), full 10-round
+    encrypt with renorm and final bootstraps.  Whole-job blocks/s = states x ranks / max time."""
+    from oracle import aes_plain  # checker only, after the timed region
+    from pipeline import AESPipeline
+    B = args.batch_states
+    pipe = AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=True, states=B)
+    rng = np.random.default_rng(4096 + rank)
+    batches = [rng.integers(0, 256, (B, 16), dtype=np.uint8) for _ in range(1 + args.batch_steps)]
+    E = ctx.engine
+    pipe.encrypt(batches[0], rks)  # warmup: masks, LUT constants, FFT buffers
+    E.sync()
+    barrier(dist)
+    t0 = time.perf_counter()
+    outs = [pipe.encrypt(b, rks) for b in batches[1:]]
+    E.sync()
+    barrier(dist)
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    ok = True
+    for b, o in zip(batches[1:], outs):
+        got = pipe.encoder.decode(*o)
+        ok &= all(np.array_equal(got[j], aes_plain.ref_encrypt(b[j], rks)) for j in range(B))
+    blocks = B * args.batch_steps * world
+    return {"workload": f"C3/C4: {B} independent states per GPU slot-packed in one ciphertext pair (SURVEY.md 8(f)1), "
+                        f"full AES-128 encrypt, N=2^16, renorm on, shared key",
+            "states_per_rank_per_step": B, "steps": args.batch_steps, "n_gpus": world,
+            "blocks_per_s": blocks / elapsed, "rounds_per_s": 10.0 * blocks / elapsed,
+            "ms_per_step": elapsed / args.batch_steps * 1e3, "verified_against_plaintext_model": bool(ok)}
+
+
 def dry_run(args, rank, world, dist):
     from aes_keyschedule import expand_aes128_key
     from oracle import aes_plain
@@ -219,6 +254,7 @@ def main():
     stats = E.kernel_stats(reset=True)
     counters = E.counters()
     E.profile(())
+    batch = run_batch(ctx, coeffs, rks, args, rank, world, dist) if args.batch_states > 0 else None
 
     # correctness of the timed outputs (outside the timed region)
     ok = all(np.array_equal(pipe.encoder.decode(*o), aes_plain.ref_encrypt(states[args.warmup + j], rks))
@@ -263,6 +299,8 @@ def main():
         "roofline_secondary": roofline(args.kernel2, "key-switch inner product: HBM-bound"),
         "op_counts_per_round": {k: v / (10.0 * args.steps) for k, v in counters.items()},
     }
+    if batch is not None:
+        line["batch"] = batch
     if args.profile_all:
         line["kernels"] = {k: {"launches": v["launches"], "ms": v["ms"], "GBps": v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] else 0}
                            for k, v in stats.items()}

@@ -149,6 +149,12 @@ int aesfhe_boot_info(aesfhe_ctx* ctx, double* out6);
 /* Zeta16 secret-key renorm of a (hi, lo) state pair (REF/pipeline.py:65-69): decrypt,
  * snap the 16 strided slots to the nearest codeword, refill others with 1, re-encrypt */
 int aesfhe_renorm_pair(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle* out_hi, aesfhe_handle* out_lo);
+/* the same renorm for the slot-packed layout: `states` AES states per
+ * ciphertext pair, byte i of state b in slot i*stride + b (1 <= states <= slot_count/16);
+ * every slot with (j mod stride) < states is snapped, the others refilled with 1.
+ * Replaces the per-state loop over REF/pipeline.py:65-69 for a batch of states. */
+int aesfhe_renorm_states(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, int states, aesfhe_handle* out_hi,
+                         aesfhe_handle* out_lo);
 
 /* --- raw access (tests, parity against the oracle) ------------------------------------ */
 /* limbs of a ciphertext: npoly x (level+2) x N uint32, NTT form */

@@ -38,25 +38,30 @@ def from_zeta(z):
 
 
 def encode_state(state, sc: int):
-    """REF/state_encoder.py:17-28: byte i -> slot i*stride, other slots 1."""
+    """REF/state_encoder.py:17-28: byte i -> slot i*stride, other slots 1.  A (B, 16) array
+    is the slot-packed batch: byte i of state b -> slot i*stride + b."""
     state = np.asarray(state, np.uint8)
+    batch = state.reshape(-1, 16)
     stride = sc // 16
+    assert batch.shape[0] <= stride
     hi = np.ones(sc, np.complex128)
     lo = np.ones(sc, np.complex128)
-    hi[::stride][:16] = to_zeta(state >> 4)
-    lo[::stride][:16] = to_zeta(state & 15)
+    hi[:16 * stride].reshape(16, stride)[:, :batch.shape[0]] = to_zeta(batch.T >> 4)
+    lo[:16 * stride].reshape(16, stride)[:, :batch.shape[0]] = to_zeta(batch.T & 15)
     return hi, lo
 
 
-def decode_state(hi, lo):
-    """REF/state_encoder.py:30-38: read only the 16 strided slots."""
+def decode_state(hi, lo, states: int = 1):
+    """REF/state_encoder.py:30-38: read only the 16 strided slots (x `states` packed states)."""
     stride = len(hi) // 16
-    return ((from_zeta(hi[::stride][:16]) << 4) | from_zeta(lo[::stride][:16])).astype(np.uint8)
+    take = lambda v: v[:16 * stride].reshape(16, stride)[:, :states].T
+    out = ((from_zeta(take(hi)) << 4) | from_zeta(take(lo))).astype(np.uint8)
+    return out[0] if states == 1 else out
 
 
-def renorm(hi, lo):
+def renorm(hi, lo, states: int = 1):
     """REF/pipeline.py:65-69 / REF/mixcol_final.py:104-106: decode then re-encode."""
-    return encode_state(decode_state(hi, lo), len(hi))
+    return encode_state(decode_state(hi, lo, states), len(hi))
 
 
 # --------------------------------------------------------------------------------
@@ -115,23 +120,23 @@ def subbytes(hi, lo, H, Lo, tol=1e-12):
     return out_h, out_l
 
 
-def _row_masks(sc):
+def _row_masks(sc, states=1):
     stride = sc // 16
     M = []
     for r in range(4):
         m = np.zeros(sc)
         for c in range(4):
-            m[(r + 4 * c) * stride] = 1.0
+            m[(r + 4 * c) * stride:(r + 4 * c) * stride + states] = 1.0
         M.append(m)
     return M
 
 
-def shift_rows(x, inverse=False):
+def shift_rows(x, inverse=False, states=1):
     """REF/shift_rows.py:39-56 (steps -4r*stride), REF/inv_shiftrows.py:37-47 (+4r*stride)."""
     sc = len(x)
     stride = sc // 16
     out = np.zeros_like(x)
-    for r, m in enumerate(_row_masks(sc)):
+    for r, m in enumerate(_row_masks(sc, states)):
         step = (4 * r * stride) * (1 if inverse else -1)
         out = out + np.roll(x * m, step)
     return out
@@ -145,13 +150,24 @@ def col_shift(x, k):
 class Golden:
     """Stage-by-stage golden model of AESPipeline (REF/pipeline.py) over slot vectors."""
 
-    def __init__(self, coeff_dir, renorm_between_steps: bool = True):
+    def __init__(self, coeff_dir, renorm_between_steps: bool = True, states: int = 1):
         d = Path(coeff_dir)
         self.xor = load_2d(d / "xor4_coeffs.json")
         self.sb = (load_1d(d / "mod256_to_16_hi.json"), load_1d(d / "mod256_to_16_lo.json"))
         self.isb = (load_1d(d / "inv_mod256_to_16_hi.json"), load_1d(d / "inv_mod256_to_16_lo.json"))
         self.gf = {(m, w): load_2d(d / f"gf_mult{m}_{w}_coeffs.json") for m in (2, 3, 9, 11, 13, 14) for w in ("hi", "lo")}
         self.renorm_between = renorm_between_steps
+        self.states = states  # slot-packed states per vector (SURVEY.md §8(f)1)
+
+    def _renorm(self, hi, lo):
+        return renorm(hi, lo, self.states)
+
+    def _sr(self, ct, inverse=False):
+        return shift_rows(ct[0], inverse, self.states), shift_rows(ct[1], inverse, self.states)
+
+    def _keys(self, rks, sc):
+        return [encode_state(np.broadcast_to(np.asarray(k, np.uint8), (self.states, 16)) if self.states > 1 else k, sc)
+                for k in rks]
 
     def xor4(self, a, b):
         return bivariate(self.xor, a, b)
@@ -168,9 +184,9 @@ class Golden:
         r = {k: (col_shift(hi, k), col_shift(lo, k)) for k in (1, 2, 3)}
         two = self.gf_mult(2, hi, lo)
         thr = self.gf_mult(3, *r[1])
-        acc = renorm(self.xor4(two[0], thr[0]), self.xor4(two[1], thr[1]))
-        acc = renorm(self.xor4(acc[0], r[2][0]), self.xor4(acc[1], r[2][1]))
-        acc = renorm(self.xor4(acc[0], r[3][0]), self.xor4(acc[1], r[3][1]))
+        acc = self._renorm(self.xor4(two[0], thr[0]), self.xor4(two[1], thr[1]))
+        acc = self._renorm(self.xor4(acc[0], r[2][0]), self.xor4(acc[1], r[2][1]))
+        acc = self._renorm(self.xor4(acc[0], r[3][0]), self.xor4(acc[1], r[3][1]))
         if log is not None:
             log.update(two=two, thr=thr)
         return acc
@@ -182,26 +198,27 @@ class Golden:
         e11 = self.gf_mult(11, *r[1])
         e13 = self.gf_mult(13, *r[2])
         e9 = self.gf_mult(9, *r[3])
-        acc = renorm(self.xor4(e14[0], e11[0]), self.xor4(e14[1], e11[1]))
-        acc = renorm(self.xor4(acc[0], e13[0]), self.xor4(acc[1], e13[1]))
-        return renorm(self.xor4(acc[0], e9[0]), self.xor4(acc[1], e9[1]))
+        acc = self._renorm(self.xor4(e14[0], e11[0]), self.xor4(e14[1], e11[1]))
+        acc = self._renorm(self.xor4(acc[0], e13[0]), self.xor4(acc[1], e13[1]))
+        return self._renorm(self.xor4(acc[0], e9[0]), self.xor4(acc[1], e9[1]))
 
     def _rn(self, hi, lo):
-        return renorm(hi, lo) if self.renorm_between else (hi, lo)
+        return self._renorm(hi, lo) if self.renorm_between else (hi, lo)
 
-    def encrypt(self, state, rks, sc=16, stages=None):
+    def encrypt(self, state, rks, sc=None, stages=None):
         """REF/pipeline.py:123-188; `stages` collects decoded bytes per step."""
+        sc = sc or 16 * self.states
         def tag(name, pair):
             if stages is not None:
-                stages[name] = decode_state(*pair)
-        keys = [encode_state(k, sc) for k in rks]
+                stages[name] = decode_state(*pair, self.states)
+        keys = self._keys(rks, sc)
         ct = encode_state(state, sc)
         ct = self._rn(*self.ark(*ct, *keys[0]))
         tag("r0.ark", ct)
         for r in range(1, 10):
             ct = self._rn(*subbytes(*ct, *self.sb))
             tag(f"r{r}.sb", ct)
-            ct = shift_rows(ct[0]), shift_rows(ct[1])
+            ct = self._sr(ct)
             tag(f"r{r}.sr", ct)
             ct = self.mix_columns(*ct)
             tag(f"r{r}.mc", ct)
@@ -209,22 +226,22 @@ class Golden:
             tag(f"r{r}.ark", ct)
         ct = self._rn(*subbytes(*ct, *self.sb))
         tag("r10.sb", ct)
-        ct = shift_rows(ct[0]), shift_rows(ct[1])
+        ct = self._sr(ct)
         tag("r10.sr", ct)
         ct = self._rn(*self.ark(*ct, *keys[10]))
         tag("r10.ark", ct)
         return ct
 
-    def decrypt(self, ct, rks, sc=16, with_inv_mix=True):
+    def decrypt(self, ct, rks, sc=None, with_inv_mix=True):
         """REF/pipeline.py:193-254 with InvMixColumns after ARK (REF/README.md:87-94)."""
-        keys = [encode_state(k, sc) for k in rks]
+        keys = self._keys(rks, sc or len(ct[0]))
         ct = self._rn(*self.ark(*ct, *keys[10]))
         for r in range(9, 0, -1):
-            ct = shift_rows(ct[0], True), shift_rows(ct[1], True)
+            ct = self._sr(ct, True)
             ct = self._rn(*subbytes(*ct, *self.isb))
             ct = self._rn(*self.ark(*ct, *keys[r]))
             if with_inv_mix:
                 ct = self.inv_mix_columns(*ct)
-        ct = shift_rows(ct[0], True), shift_rows(ct[1], True)
+        ct = self._sr(ct, True)
         ct = self._rn(*subbytes(*ct, *self.isb))
         return self._rn(*self.ark(*ct, *keys[0]))
