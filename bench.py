@@ -54,6 +54,8 @@ def parse():
                     help="secondary measurement (BASELINE configs 3/4): this many independent states per rank, "
                          "slot-packed into one ciphertext pair (SURVEY.md 8(f)1); 0 = skip")
     ap.add_argument("--batch-steps", type=int, default=1)
+    ap.add_argument("--no-batch-roundtrip", dest="batch_roundtrip", action="store_false",
+                    help="skip the decrypt leg of the batch (BASELINE config 5)")
     ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r1_pmc_traffic.json"), help="per-launch HBM bytes from a rocprofv3 PMC pass")
     return ap.parse_args()
 
@@ -170,12 +172,27 @@ def run_batch(ctx, coeffs, rks, args, rank, world, dist) -> dict:
     for b, o in zip(batches[1:], outs):
         got = pipe.encoder.decode(*o)
         ok &= all(np.array_equal(got[j], aes_plain.ref_encrypt(b[j], rks)) for j in range(B))
+    rt = None
+    if args.batch_roundtrip:
+        # BASELINE config 5: decrypt the same batch (InvMixColumns inserted)
+        barrier(dist)
+        t1 = time.perf_counter()
+        backs = [pipe.decrypt(*o, rks) for o in outs]
+        E.sync()
+        barrier(dist)
+        dec_s = max_over_ranks(dist, time.perf_counter() - t1)
+        exact = all(np.array_equal(pipe.encoder.decode(*bk), b) for bk, b in zip(backs, batches[1:]))
+        rt = {"workload": "C5: decrypt of the encrypted batch (InvMixColumns + bootstrap + snap), enc->dec round trip",
+              "dec_ms_per_step": dec_s / args.batch_steps * 1e3,
+              "roundtrip_blocks_per_s": B * args.batch_steps * world / (elapsed + dec_s),
+              "roundtrip_bit_exact": bool(exact)}
     blocks = B * args.batch_steps * world
     return {"workload": f"C3/C4: {B} independent states per GPU slot-packed in one ciphertext pair (SURVEY.md 8(f)1), "
                         f"full AES-128 encrypt, N=2^16, renorm on, shared key",
             "states_per_rank_per_step": B, "steps": args.batch_steps, "n_gpus": world,
             "blocks_per_s": blocks / elapsed, "rounds_per_s": 10.0 * blocks / elapsed,
-            "ms_per_step": elapsed / args.batch_steps * 1e3, "verified_against_plaintext_model": bool(ok)}
+            "ms_per_step": elapsed / args.batch_steps * 1e3, "verified_against_plaintext_model": bool(ok),
+            **({"roundtrip": rt} if rt else {})}
 
 
 def dry_run(args, rank, world, dist):
