@@ -776,13 +776,11 @@ public:
         }
         const int nk = nb + k;
         u32* mid = tmp((size_t)c.npoly * nk);
-        for (int q = 0; q < c.npoly; ++q)
-            HIP_OK(hipMemcpyAsync(mid + (size_t)q * nk * n, c.data + (size_t)q * na * n, sizeof(u32) * nk * n, hipMemcpyDeviceToDevice,
-                                  S()));
         const i64 cst = std::llround(ratio);
         std::vector<u32> r(nk);
         for (int i = 0; i < nk; ++i) r[i] = mod_i64(cst, hp_.mod[i]);
-        launch_mul_const_half(S(), T_, mid, mid, const_half(r, r), c.npoly * nk, nk, qmap());
+        // the first nk limbs of every poly, times the constant (copy fused into the multiply)
+        launch_mul_const_half(S(), T_, mid, c.data, const_half(r, r), c.npoly * nk, nk, qmap(), na);
         Ct o;
         o.level = t, o.npoly = c.npoly, o.pend = p, o.lazy = c.lazy || p > 0, o.zero = c.zero;
         o.words = (size_t)c.npoly * nb * n;
@@ -858,16 +856,13 @@ public:
         o.pend = x.pend;
         o.lazy = x.lazy || y.lazy;
         const int common = std::min(x.npoly, y.npoly) * nl;
-        if (x.zero) launch_neg(S(), T_, o.data, y.data, common, nl, qmap());
-        else if (sub) launch_sub(S(), T_, o.data, x.data, y.data, common, nl, qmap());
-        else launch_add(S(), T_, o.data, x.data, y.data, common, nl, qmap());
-        if (x.npoly > y.npoly)
-            HIP_OK(hipMemcpyAsync(o.data + (size_t)common * hp_.n, x.data + (size_t)common * hp_.n, sizeof(u32) * nl * hp_.n,
-                                  hipMemcpyDeviceToDevice, S()));
-        else if (y.npoly > x.npoly) {
-            if (sub) launch_neg(S(), T_, o.data + (size_t)common * hp_.n, y.data + (size_t)common * hp_.n, nl, nl, qmap());
-            else HIP_OK(hipMemcpyAsync(o.data + (size_t)common * hp_.n, y.data + (size_t)common * hp_.n, sizeof(u32) * nl * hp_.n,
-                                       hipMemcpyDeviceToDevice, S()));
+        if (x.zero && x.npoly == y.npoly) {
+            launch_neg(S(), T_, o.data, y.data, common, nl, qmap());
+        } else if (x.npoly == y.npoly) {
+            if (sub) launch_sub(S(), T_, o.data, x.data, y.data, common, nl, qmap());
+            else launch_add(S(), T_, o.data, x.data, y.data, common, nl, qmap());
+        } else {  // the third polynomial of a deferred tensor comes along in the same launch
+            launch_addsub_tail(S(), T_, o.data, x.data, y.data, common, np * nl, x.npoly > y.npoly, sub, nl, qmap());
         }
         if (fa) release(x);
         if (fb) release(y);
@@ -1592,48 +1587,55 @@ public:
         }
         Ct out;
         bool have = false;
-        u32* add0 = tmp(nl);
-        u32* add1 = tmp(nl);
-        for (int gg = 0; gg < g.G; ++gg) {
-            MacTerms qp{}, q0{};
-            for (int b = 0; b < g.B; ++b) {
-                if (!P[gg][b]) continue;
-                q0.x[q0.n] = b == 0 ? c0 : a[b], q0.pt[q0.n++] = P[gg][b];
-                if (b) qp.x[qp.n] = u[b], qp.pt[qp.n++] = P[gg][b];
+        // all giant steps' diagonal sums in one pass per chunk of kLinG giant steps (k_lin_mac):
+        // every baby-step residue is read once instead of once per giant step
+        for (int g0 = 0; g0 < g.G; g0 += kLinG) {
+            const int gn = std::min(kLinG, g.G - g0);
+            LinMacArgs m{};
+            m.B = g.B, m.G = gn, m.c1 = c1;
+            for (int b = 0; b < g.B; ++b) m.a[b] = b == 0 ? c0 : a[b], m.u[b] = b ? u[b] : nullptr;
+            bool any[kLinG] = {}, rot[kLinG] = {};
+            for (int j = 0; j < gn; ++j) {
+                for (int b = 0; b < g.B; ++b) {
+                    m.pt[j][b] = P[g0 + j][b];
+                    any[j] = any[j] || P[g0 + j][b];
+                    rot[j] = rot[j] || (b && P[g0 + j][b]);
+                }
+                m.out0[j] = tmp(nl);
+                m.out1[j] = P[g0 + j][0] ? tmp(nl) : nullptr;
+                m.outp[j] = rot[j] ? tmp(2 * (size_t)ne) : nullptr;
             }
-            if (!q0.n) continue;
-            launch_mac(S(), T_, add0, q0, 0, 0, nl, 1, qmap());
-            Ct inner;
-            if (P[gg][0]) {
-                MacTerms q1{};
-                q1.x[0] = c1, q1.pt[0] = P[gg][0], q1.n = 1;
-                launch_mac(S(), T_, add1, q1, 0, 0, nl, 1, qmap());
-            }
-            if (qp.n) {
-                u32* acc = tmp(2 * (size_t)ne);
-                launch_mac(S(), T_, acc, qp, (size_t)ne * n, (size_t)ne * n, ne, 2, extmap(nl));
-                inner = moddown(acc, l, add0, P[gg][0] ? add1 : nullptr);
-                untmp(acc, 2 * (size_t)ne);
-            } else {  // only the unrotated diagonal
-                inner = alloc_ct(l, 2);
-                HIP_OK(hipMemcpyAsync(inner.data, add0, (size_t)nl * n * sizeof(u32), hipMemcpyDeviceToDevice, S()));
-                HIP_OK(hipMemcpyAsync(inner.data + (size_t)nl * n, add1, (size_t)nl * n * sizeof(u32), hipMemcpyDeviceToDevice, S()));
-            }
-            Ct rs = rescale(inner);
-            release(inner);
-            Ct part = g.giant[gg] ? rotl(rs, g.giant[gg]) : rs;
-            if (g.giant[gg]) release(rs);
-            if (!have) {
-                out = part, have = true;
-            } else {
-                Ct s2 = add_sub(out, part, false);
-                release(out);
-                release(part);
-                out = s2;
+            launch_lin_mac(S(), T_, m, nl, ne, extmap(nl));
+            for (int j = 0; j < gn; ++j) {
+                const int gg = g0 + j;
+                if (any[j]) {
+                    Ct inner;
+                    if (rot[j]) {
+                        inner = moddown(m.outp[j], l, m.out0[j], m.out1[j]);
+                    } else {  // only the unrotated diagonal
+                        inner = alloc_ct(l, 2);
+                        HIP_OK(hipMemcpyAsync(inner.data, m.out0[j], (size_t)nl * n * sizeof(u32), hipMemcpyDeviceToDevice, S()));
+                        HIP_OK(hipMemcpyAsync(inner.data + (size_t)nl * n, m.out1[j], (size_t)nl * n * sizeof(u32),
+                                              hipMemcpyDeviceToDevice, S()));
+                    }
+                    Ct rs = rescale(inner);
+                    release(inner);
+                    Ct part = g.giant[gg] ? rotl(rs, g.giant[gg]) : rs;
+                    if (g.giant[gg]) release(rs);
+                    if (!have) {
+                        out = part, have = true;
+                    } else {
+                        Ct s2 = add_sub(out, part, false);
+                        release(out);
+                        release(part);
+                        out = s2;
+                    }
+                }
+                untmp(m.out0[j], nl);
+                if (m.out1[j]) untmp(m.out1[j], nl);
+                if (m.outp[j]) untmp(m.outp[j], 2 * (size_t)ne);
             }
         }
-        untmp(add0, nl);
-        untmp(add1, nl);
         for (int b = 1; b < g.B; ++b) {
             if (u[b]) untmp(u[b], 2 * (size_t)ne);
             if (a[b]) untmp(a[b], nl);
@@ -1922,7 +1924,7 @@ private:
     void build_tables() {
         const int n = hp_.n, nt = hp_.n_tot(), logn = hp_.logn;
         std::vector<PrimeConst> pc(nt);
-        std::vector<u32> psi((size_t)nt * n), psip((size_t)nt * n), ipsi((size_t)nt * n), ipsip((size_t)nt * n);
+        std::vector<uint2> tw((size_t)nt * n), itw((size_t)nt * n);
         im_.resize(nt);
         for (int i = 0; i < nt; ++i) {
             const u32 q = hp_.mod[i], w = hp_.psi[i], iw = hinvm(w, q);
@@ -1938,19 +1940,15 @@ private:
             for (int k = 0; k < n; ++k) {
                 const u32 r = hbitrev((u32)k, logn);
                 const size_t at = (size_t)i * n + r;
-                psi[at] = (u32)p;
-                psip[at] = shoup_pre((u32)p, q);
-                ipsi[at] = (u32)ip;
-                ipsip[at] = shoup_pre((u32)ip, q);
+                tw[at] = make_uint2((u32)p, shoup_pre((u32)p, q));
+                itw[at] = make_uint2((u32)ip, shoup_pre((u32)ip, q));
                 p = p * w % q;
                 ip = ip * iw % q;
             }
         }
         T_.pc = dev_upload(pc);
-        T_.psi = dev_upload(psi);
-        T_.psip = dev_upload(psip);
-        T_.ipsi = dev_upload(ipsi);
-        T_.ipsip = dev_upload(ipsip);
+        T_.tw = dev_upload(tw);
+        T_.itw = dev_upload(itw);
         T_.logn = logn;
 
         const auto& q = hp_.mod;

@@ -50,10 +50,8 @@ void prof_set(KernelProfiler* p);
 
 struct DevTables {
     const PrimeConst* pc = nullptr;  // [n_tot]
-    const u32* psi = nullptr;        // [n_tot][N]  psi^{bitrev(k)}
-    const u32* psip = nullptr;       //             Shoup companions
-    const u32* ipsi = nullptr;       // [n_tot][N]  psi^{-bitrev(k)}
-    const u32* ipsip = nullptr;
+    const uint2* tw = nullptr;       // [n_tot][N]  {psi^{bitrev(k)}, Shoup companion}: one 8-byte load per twiddle
+    const uint2* itw = nullptr;      // [n_tot][N]  {psi^{-bitrev(k)}, Shoup companion}
     int logn = 16;
 };
 
@@ -117,7 +115,12 @@ struct LimbConsts {
 };
 // out[row][k] = in[row][k] * (k < N/2 ? clo[l] : chi[l]) with l = row % nl (Shoup pairs)
 // layout: v[4 l .. 4 l + 3] = {clo, clo', chi, chi'}
-void launch_mul_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const LimbConsts& cst, int rows, int nl, LimbMap map);
+// src_nl > 0: `in` holds polys of src_nl >= nl limbs (first nl read), e.g. a level drop
+void launch_mul_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const LimbConsts& cst, int rows, int nl, LimbMap map,
+                           int src_nl = 0);
+// out = a +- b on the first `common` rows, then the longer operand alone (+-b when b is longer)
+void launch_addsub_tail(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int common, int rows, bool a_longer,
+                        bool sub, int nl, LimbMap map);
 // out[row][k] = in[row][k] + (k < N/2 ? alo[l] : ahi[l]); layout v[2 l .. 2 l + 1]
 void launch_add_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const LimbConsts& cst, int rows, int nl, LimbMap map);
 // X -> X^g in the NTT domain (bit-reversed evaluation order)
@@ -161,6 +164,25 @@ struct MacTerms {
     int n;
 };
 void launch_mac(hipStream_t st, const DevTables& T, u32* out, const MacTerms& m, size_t xs, size_t os, int rows, int npoly, LimbMap map);
+// every giant step of one hoisted BSGS linear-transform group in ONE pass:
+// row t < ne of the extended basis (Q limbs t < nl, then the P block), for each giant gg < G:
+//   out0[gg] = sum_b a_b P[gg][b]        (t < nl; a_0 = c0, a_b = automorphed c0)
+//   out1[gg] = c1 P[gg][0]               (t < nl, when out1[gg])
+//   outp[gg] = sum_{b>=1} u_b P[gg][b]   (2 polys of ne rows; u_b = hoisted key inner products)
+// Each input residue is read once for all giant steps (the per-giant k_mac re-read every
+// rotated baby step and every diagonal twice).  Null pointers mark absent terms.
+constexpr int kLinB = 16, kLinG = 4;
+struct LinMacArgs {
+    const u32* a[kLinB];
+    const u32* u[kLinB];
+    const u32* c1;
+    const u32* pt[kLinG][kLinB];
+    u32* out0[kLinG];
+    u32* out1[kLinG];
+    u32* outp[kLinG];
+    int B, G;
+};
+void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int nl, int ne, LimbMap map);
 
 // --- sampling --------------------------------------------------------
 // kind: 0 ternary, 1 centred binomial (eta = 21); writes value mod prime into nl rows

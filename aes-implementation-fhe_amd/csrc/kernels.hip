@@ -41,6 +41,19 @@ __global__ void k_sub(u32* out, const u32* a, const u32* b, int nl, LimbMap map,
     EW_PROLOGUE
     out[idx] = sub_mod(a[idx], b[idx], P.q);
 }
+// a +- b on rows < common; rows in [common, rows): the longer operand alone (a, or +-b)
+__global__ void k_addsub_tail(u32* out, const u32* a, const u32* b, int common, int a_longer, int sub, int nl, LimbMap map,
+                              const PrimeConst* pc, int logn) {
+    EW_PROLOGUE
+    if (row < common) {
+        out[idx] = sub ? sub_mod(a[idx], b[idx], P.q) : add_mod(a[idx], b[idx], P.q);
+    } else if (a_longer) {
+        out[idx] = a[idx];
+    } else {
+        const u32 v = b[idx];
+        out[idx] = sub ? (v ? P.q - v : 0u) : v;
+    }
+}
 __global__ void k_neg(u32* out, const u32* a, int nl, LimbMap map, const PrimeConst* pc, int logn) {
     EW_PROLOGUE
     u32 v = a[idx];
@@ -70,11 +83,14 @@ __global__ void k_tensor(u32* out, const u32* a, const u32* b, int nl, LimbMap m
     out[idx + off] = add_mod(barrett_mul(a0, b1, q, mu), barrett_mul(a1, b0, q, mu), q);
     out[idx + 2 * off] = barrett_mul(a1, b1, q, mu);
 }
-__global__ void k_mul_const_half(u32* out, const u32* in, LimbConsts cst, int nl, LimbMap map, const PrimeConst* pc, int logn) {
+// in: polys of src_nl limbs (>= nl; the first nl of each are read), out: polys of nl limbs
+__global__ void k_mul_const_half(u32* out, const u32* in, LimbConsts cst, int nl, int src_nl, LimbMap map, const PrimeConst* pc,
+                                 int logn) {
     EW_PROLOGUE
     const int hi = (int)(k >> (logn - 1));
     const u32* c = cst.v + 4 * limb + 2 * hi;
-    out[idx] = shoup_mul(in[idx], c[0], c[1], P.q);
+    const size_t sidx = ((size_t)((row / nl) * src_nl + limb) << logn) + k;
+    out[idx] = shoup_mul(in[sidx], c[0], c[1], P.q);
 }
 __global__ void k_add_const_half(u32* out, const u32* in, LimbConsts cst, int nl, LimbMap map, const PrimeConst* pc, int logn) {
     EW_PROLOGUE
@@ -614,8 +630,15 @@ void launch_fma_poly(hipStream_t st, const DevTables& T, u32* out, const u32* a,
                      LimbMap map) {
     prof_launch(KID_ELEMENTWISE, EW_BYTES(3.0 * rows + nl), k_fma_poly, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, b, c, nl, map, T.pc, T.logn);
 }
-void launch_mul_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const LimbConsts& cst, int rows, int nl, LimbMap map) {
-    prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows), k_mul_const_half, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, cst, nl, map, T.pc, T.logn);
+void launch_mul_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const LimbConsts& cst, int rows, int nl, LimbMap map,
+                           int src_nl) {
+    prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows), k_mul_const_half, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, cst, nl,
+                src_nl > 0 ? src_nl : nl, map, T.pc, T.logn);
+}
+void launch_addsub_tail(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int common, int rows, bool a_longer,
+                        bool sub, int nl, LimbMap map) {
+    prof_launch(KID_ELEMENTWISE, EW_BYTES(3.0 * common + 2.0 * (rows - common)), k_addsub_tail, ew_grid(T.logn, rows), dim3(kBlock), 0,
+                st, out, a, b, common, (int)a_longer, (int)sub, nl, map, T.pc, T.logn);
 }
 void launch_add_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const LimbConsts& cst, int rows, int nl, LimbMap map) {
     prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows), k_add_const_half, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, cst, nl, map, T.pc, T.logn);
@@ -653,7 +676,68 @@ __global__ void k_mac(u32* out, MacTerms m, size_t xs, size_t os, LimbMap map, c
     }
     out[p * os + at] = reduce64(acc, P.q, P.mu, P.r32);
 }
+// see launch_lin_mac (kernels.h); grid (N / 256, ne rows)
+__global__ void __launch_bounds__(kBlock) k_lin_mac(LinMacArgs m, int nl, int ne, LimbMap map, const PrimeConst* pc, int logn) {
+    const int t = blockIdx.y;
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const PrimeConst P = pc[map.prime(t)];
+    const bool qrow = t < nl;
+    const size_t at = ((size_t)t << logn) + k;
+    const size_t po = (size_t)ne << logn;  // poly stride of u / outp
+    u64 acc0[kLinG], ap0[kLinG], ap1[kLinG];
+#pragma unroll
+    for (int g = 0; g < kLinG; ++g) acc0[g] = ap0[g] = ap1[g] = 0;
+    for (int b = 0; b < m.B; ++b) {
+        if (b && (b & 7) == 0) {
+#pragma unroll
+            for (int g = 0; g < kLinG; ++g) {
+                acc0[g] = fold64(acc0[g], P.q, P.r32);
+                ap0[g] = fold64(ap0[g], P.q, P.r32);
+                ap1[g] = fold64(ap1[g], P.q, P.r32);
+            }
+        }
+        const u32 av = (qrow && m.a[b]) ? m.a[b][at] : 0u;
+        u32 u0 = 0, u1 = 0;
+        if (m.u[b]) u0 = m.u[b][at], u1 = m.u[b][po + at];
+#pragma unroll
+        for (int g = 0; g < kLinG; ++g) {
+            if (g >= m.G || !m.pt[g][b]) continue;
+            const u32 pv = m.pt[g][b][at];
+            acc0[g] += (u64)av * pv;  // q < 2^32 / 3: 8 products fit beside a folded accumulator
+            ap0[g] += (u64)u0 * pv;
+            ap1[g] += (u64)u1 * pv;
+        }
+    }
+    const u32 c1v = qrow ? m.c1[at] : 0u;
+#pragma unroll
+    for (int g = 0; g < kLinG; ++g) {
+        if (g >= m.G) continue;
+        if (qrow) {
+            m.out0[g][at] = reduce64(acc0[g], P.q, P.mu, P.r32);
+            if (m.out1[g]) m.out1[g][at] = reduce64((u64)c1v * m.pt[g][0][at], P.q, P.mu, P.r32);
+        }
+        if (m.outp[g]) {
+            m.outp[g][at] = reduce64(ap0[g], P.q, P.mu, P.r32);
+            m.outp[g][po + at] = reduce64(ap1[g], P.q, P.mu, P.r32);
+        }
+    }
+}
 }  // namespace
+
+void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int nl, int ne, LimbMap map) {
+    if (m.B < 1 || m.B > kLinB || m.G < 1 || m.G > kLinG) throw std::runtime_error("launch_lin_mac: 1..16 baby, 1..4 giant steps");
+    double reads = 0, writes = 0;  // rows of N words
+    for (int b = 0; b < m.B; ++b) {
+        if (m.a[b]) reads += nl;
+        if (m.u[b]) reads += 2.0 * ne;
+        for (int g = 0; g < m.G; ++g)
+            if (m.pt[g][b]) reads += ne;
+    }
+    reads += nl;  // c1
+    for (int g = 0; g < m.G; ++g) writes += nl + (m.out1[g] ? nl : 0) + (m.outp[g] ? 2.0 * ne : 0);
+    prof_launch(KID_ELEMENTWISE, words((reads + writes) * (1u << T.logn)), k_lin_mac, ew_grid(T.logn, ne), dim3(kBlock), 0, st, m, nl, ne,
+                map, T.pc, T.logn);
+}
 
 void launch_mac(hipStream_t st, const DevTables& T, u32* out, const MacTerms& m, size_t xs, size_t os, int rows, int npoly, LimbMap map) {
     if (m.n < 1 || m.n > kMacMax) throw std::runtime_error("launch_mac: 1..16 terms");

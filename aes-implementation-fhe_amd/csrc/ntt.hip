@@ -76,15 +76,14 @@ __device__ __forceinline__ RowAddr row_addr(u32* dst, const u32* src, const RowM
 // limb) and x = its centred representative reduced mod the target prime.
 template <int LOGR1, int MODE>
 __global__ void __launch_bounds__(kThreads) k_ntt1_fwd(u32* dst, const u32* src, RowMap rm, LimbMap map, const PrimeConst* pc,
-                                                       const u32* psi, const u32* psip, NttAux aux, unsigned long long* ts) {
+                                                       const uint2* tw, NttAux aux, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8, R1 = 1 << LOGR1, T = R1 / 16, CB = kThreads / T;
     __shared__ u32 sm[R1 * CB];
     if (skipped(rm)) return;
     ts_begin(ts);
     RowAddr ra = row_addr<LOGN>(dst, src, rm, map);
     const u32 q = pc[ra.prime].q;
-    const u32* w = psi + ((size_t)ra.prime << LOGN);
-    const u32* wp = psip + ((size_t)ra.prime << LOGN);
+    const uint2* w = tw + ((size_t)ra.prime << LOGN);  // {psi^brv, Shoup companion} pairs
     const int col = threadIdx.x % CB, g = threadIdx.x / CB;
     const int c = blockIdx.x * CB + col;
     u32 x[16];
@@ -132,7 +131,7 @@ __global__ void __launch_bounds__(kThreads) k_ntt1_fwd(u32* dst, const u32* src,
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
                 const int ti = (1 << s) + (k >> (4 - s));
-                ct_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+                ct_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q);
             }
     }
 #pragma unroll
@@ -148,7 +147,7 @@ __global__ void __launch_bounds__(kThreads) k_ntt1_fwd(u32* dst, const u32* src,
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
                 const int ti = (1 << s) + ((16 * g + k) >> (LOGR1 - s));
-                ct_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+                ct_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q);
             }
     }
 #pragma unroll
@@ -161,16 +160,15 @@ __global__ void __launch_bounds__(kThreads) k_ntt1_fwd(u32* dst, const u32* src,
 // g = group, i = limb, out[g][i] = (cur[g][i] - x) * qinv_i (+ add_g[i]), rows addressed
 // through aux (cur row g * cur_stride + i, out row g * out_stride + i).
 template <int LOGR1, int MODE>
-__global__ void __launch_bounds__(kThreads) k_ntt2_fwd(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const u32* psi,
-                                                       const u32* psip, NttAux aux, unsigned long long* ts) {
+__global__ void __launch_bounds__(kThreads) k_ntt2_fwd(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const uint2* tw,
+                                                       NttAux aux, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8;
     __shared__ u32 sm[kRowsP2 * kPitchP2];
     if (skipped(rm)) return;
     ts_begin(ts);
     const RowAddr ra = row_addr<LOGN>(data, data, rm, map);
     const u32 q = pc[ra.prime].q;
-    const u32* w = psi + ((size_t)ra.prime << LOGN);
-    const u32* wp = psip + ((size_t)ra.prime << LOGN);
+    const uint2* w = tw + ((size_t)ra.prime << LOGN);  // {psi^brv, Shoup companion} pairs
     const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
     const int R = blockIdx.x * kRowsP2 + r;
     u32* p = ra.dst + (size_t)R * 256;
@@ -186,7 +184,7 @@ __global__ void __launch_bounds__(kThreads) k_ntt2_fwd(u32* data, RowMap rm, Lim
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
                 const int ti = base + (k >> (4 - s));
-                ct_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+                ct_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q);
             }
     }
     u32* row = sm + r * kPitchP2;
@@ -203,7 +201,7 @@ __global__ void __launch_bounds__(kThreads) k_ntt2_fwd(u32* data, RowMap rm, Lim
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
                 const int ti = base + ((16 * j + k) >> (8 - s));
-                ct_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+                ct_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q);
             }
     }
     if (MODE == kFinish) {
@@ -239,15 +237,14 @@ __global__ void __launch_bounds__(kThreads) k_ntt2_fwd(u32* data, RowMap rm, Lim
 // ---------------------------------------------------------------- inverse, pass 2 (src -> dst)
 template <int LOGR1>
 __global__ void __launch_bounds__(kThreads) k_ntt2_inv(u32* dst, const u32* src, RowMap rm, LimbMap map, const PrimeConst* pc,
-                                                       const u32* ipsi, const u32* ipsip, unsigned long long* ts) {
+                                                       const uint2* tw, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8;
     __shared__ u32 sm[kRowsP2 * kPitchP2];
     if (skipped(rm)) return;
     ts_begin(ts);
     const RowAddr ra = row_addr<LOGN>(dst, src, rm, map);
     const u32 q = pc[ra.prime].q;
-    const u32* w = ipsi + ((size_t)ra.prime << LOGN);
-    const u32* wp = ipsip + ((size_t)ra.prime << LOGN);
+    const uint2* w = tw + ((size_t)ra.prime << LOGN);  // {psi^-brv, Shoup companion} pairs
     const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
     const int R = blockIdx.x * kRowsP2 + r;
     u32 x[16];
@@ -265,7 +262,7 @@ __global__ void __launch_bounds__(kThreads) k_ntt2_inv(u32* dst, const u32* src,
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
                 const int ti = base + ((16 * j + k) >> (8 - s));
-                gs_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q);
             }
     }
     u32* row = sm + r * kPitchP2;
@@ -282,7 +279,7 @@ __global__ void __launch_bounds__(kThreads) k_ntt2_inv(u32* dst, const u32* src,
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
                 const int ti = base + (k >> (4 - s));
-                gs_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q);
             }
     }
     u32* p = ra.dst + (size_t)R * 256;
@@ -293,8 +290,8 @@ __global__ void __launch_bounds__(kThreads) k_ntt2_inv(u32* dst, const u32* src,
 
 // ---------------------------------------------------------------- inverse, pass 1 (in place on dst rows)
 template <int LOGR1>
-__global__ void __launch_bounds__(kThreads) k_ntt1_inv(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const u32* ipsi,
-                                                       const u32* ipsip, unsigned long long* ts) {
+__global__ void __launch_bounds__(kThreads) k_ntt1_inv(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const uint2* tw,
+                                                       unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8, R1 = 1 << LOGR1, T = R1 / 16, CB = kThreads / T;
     __shared__ u32 sm[R1 * CB];
     if (skipped(rm)) return;
@@ -302,8 +299,7 @@ __global__ void __launch_bounds__(kThreads) k_ntt1_inv(u32* data, RowMap rm, Lim
     const RowAddr ra = row_addr<LOGN>(data, data, rm, map);
     const PrimeConst P = pc[ra.prime];
     const u32 q = P.q;
-    const u32* w = ipsi + ((size_t)ra.prime << LOGN);
-    const u32* wp = ipsip + ((size_t)ra.prime << LOGN);
+    const uint2* w = tw + ((size_t)ra.prime << LOGN);  // {psi^-brv, Shoup companion} pairs
     const int col = threadIdx.x % CB, g = threadIdx.x / CB;
     const int c = blockIdx.x * CB + col;
     u32 x[16];
@@ -316,7 +312,7 @@ __global__ void __launch_bounds__(kThreads) k_ntt1_inv(u32* data, RowMap rm, Lim
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
                 const int ti = (1 << s) + ((16 * g + k) >> (LOGR1 - s));
-                gs_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q);
             }
     }
 #pragma unroll
@@ -331,7 +327,7 @@ __global__ void __launch_bounds__(kThreads) k_ntt1_inv(u32* data, RowMap rm, Lim
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
                 const int ti = (1 << s) + (k >> (4 - s));
-                gs_bfly(x[k], x[k + h], w[ti], wp[ti], q);
+                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q);
             }
     }
 #pragma unroll
@@ -348,18 +344,17 @@ void ntt_fwd_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
     const double io1 = 2.0 * io_rows * row_bytes;
     const double io2 = (M2 == kFinish ? (3.0 + (aux.add0 ? 0.5 : 0.0) + (aux.add1 ? 0.5 : 0.0)) : 2.0) * io_rows * row_bytes;
     prof_launch_ts(KID_NTT_COLS_FWD, io1, k_ntt1_fwd<LOGR1, M1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, src, rm, map, Tb.pc,
-                Tb.psi, Tb.psip, aux);
+                Tb.tw, aux);
     prof_launch_ts(KID_NTT_ROWS_FWD, io2, k_ntt2_fwd<LOGR1, M2>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, rm, map, Tb.pc,
-                Tb.psi, Tb.psip, aux);
+                Tb.tw, aux);
 }
 template <int LOGR1>
 void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {
     constexpr int R1 = 1 << LOGR1, CB = kThreads / (R1 / 16);
     const double io = 4.0 * 2.0 * rows * (256.0 * R1);  // the inverse is never launched with skips
     prof_launch_ts(KID_NTT_ROWS_INV, io, k_ntt2_inv<LOGR1>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, src, rm, map, Tb.pc,
-                Tb.ipsi, Tb.ipsip);
-    prof_launch_ts(KID_NTT_COLS_INV, io, k_ntt1_inv<LOGR1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, rm, map, Tb.pc, Tb.ipsi,
-                Tb.ipsip);
+                Tb.itw);
+    prof_launch_ts(KID_NTT_COLS_INV, io, k_ntt1_inv<LOGR1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, rm, map, Tb.pc, Tb.itw);
 }
 
 }  // namespace
