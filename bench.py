@@ -68,7 +68,12 @@ def dist_setup(want: int):
         import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # AESFHE_DIST_BACKEND=gloo rehearses N ranks on fewer GPUs (ranks share a device,
+        # local % device_count); the real N-GPU run is one rank per GPU over RCCL ("nccl")
+        backend = os.environ.get("AESFHE_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        ndev = torch.cuda.device_count()
+        if ndev:
+            local = local % ndev
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend)
@@ -87,7 +92,8 @@ def max_over_ranks(dist, x: float) -> float:
     if dist is None:
         return x
     import torch
-    dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    gpu = dist.get_backend() == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
     t = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
