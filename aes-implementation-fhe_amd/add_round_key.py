@@ -29,5 +29,6 @@ class AddRoundKey:
     def __init__(self, xor4: XOR4LUT):
         self.xor4 = xor4
 
-    def __call__(self, ct_hi, ct_lo, key_hi, key_lo) -> Tuple[Any, Any]:
-        return pair(self.xor4.ctx, lambda: self.xor4.apply(ct_hi, key_hi), lambda: self.xor4.apply(ct_lo, key_lo))
+    def __call__(self, ct_hi, ct_lo, key_hi, key_lo, out_level=None) -> Tuple[Any, Any]:
+        return pair(self.xor4.ctx, lambda: self.xor4.apply(ct_hi, key_hi, out_level),
+                    lambda: self.xor4.apply(ct_lo, key_lo, out_level))

@@ -163,6 +163,10 @@ class EngineContext:
         HIP streams; sequential when the context was built with concurrent=False."""
         return self.engine.parallel(*fns)
 
+    def level_down(self, ct, level: int):
+        """the same message at a lower level (exact scale; used by utils.drop_to)"""
+        return self.engine.level_down(ct, level)
+
     def renorm_pair(self, hi, lo, states: int = 1):
         """Device-side Zeta16 secret-key renorm of a (hi, lo) state pair (REF/pipeline.py:65-69);
         `states` > 1: that many slot-packed states per pair (StateEncoder)."""

@@ -10,7 +10,7 @@ from mixcol_final import _CoeffCache, gf_basis16, gf_eval, gf_mult_pair
 from shift_rows import row_masks
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT
-from utils import pair
+from utils import LUT2_DEPTH, RENORM_FLOOR, pair
 
 
 class InvMixColumnsFHE:
@@ -23,6 +23,9 @@ class InvMixColumnsFHE:
         self.enc = StateEncoder(ctx, states)  # states > 1: slot-packed batch (state_encoder.py)
         self.use_hard_renorm = use_hard_renorm
         self._pt_row: List[Any] = row_masks(ctx, self.sc, states)
+        # with the renorm after every XOR pair, the LUTs run just above RENORM_FLOOR (utils.py)
+        self._xor_level = RENORM_FLOOR if use_hard_renorm else None
+        self._gf_level = RENORM_FLOOR + LUT2_DEPTH if use_hard_renorm else None
 
     def _basis16(self, ct):
         return gf_basis16(self.ctx, ct)
@@ -30,8 +33,8 @@ class InvMixColumnsFHE:
     def _poly2_eval(self, ct_hi, ct_lo, mult: int, which: str):
         return gf_eval(self.ctx, self._coeffs, mult, which, ct_hi, ct_lo)
 
-    def _xor(self, a, b):
-        return self.xor4.apply(a, b)
+    def _xor(self, a, b, out_level=None):
+        return self.xor4.apply(a, b, out_level)
 
     def _renorm_pair(self, hi, lo):
         return self.enc.renorm(hi, lo) if self.use_hard_renorm else (hi, lo)
@@ -44,20 +47,20 @@ class InvMixColumnsFHE:
             out = ctx.add(out, ctx.rotate(ctx.multiply(ct, mask), k_rows * self.stride))
         return out
 
-    def _gf(self, mult, hi, lo):
-        return gf_mult_pair(self.ctx, self._coeffs, mult, hi, lo)
+    def _gf(self, mult, hi, lo, out_level=None):
+        return gf_mult_pair(self.ctx, self._coeffs, mult, hi, lo, out_level)
 
     def gf_mult_9(self, hi, lo):
-        return self._gf(9, hi, lo)
+        return self._gf(9, hi, lo, self._gf_level)
 
     def gf_mult_11(self, hi, lo):
-        return self._gf(11, hi, lo)
+        return self._gf(11, hi, lo, self._gf_level)
 
     def gf_mult_13(self, hi, lo):
-        return self._gf(13, hi, lo)
+        return self._gf(13, hi, lo, self._gf_level)
 
     def gf_mult_14(self, hi, lo):
-        return self._gf(14, hi, lo)
+        return self._gf(14, hi, lo, self._gf_level)
 
     def _col_shift_rowmajor(self, ct, k_up: int):
         return self.ctx.rotate(ct, -4 * k_up * self.stride)
@@ -77,13 +80,14 @@ class InvMixColumnsFHE:
         log("mul13", e13)
         e9 = self.gf_mult_9(*rot[3])
         log("mul9", e9)
-        acc = pair(self.ctx, lambda: self._xor(e14[0], e11[0]), lambda: self._xor(e14[1], e11[1]))
+        fl = self._xor_level
+        acc = pair(self.ctx, lambda: self._xor(e14[0], e11[0], fl), lambda: self._xor(e14[1], e11[1], fl))
         log("acc1", acc)
         acc = self._renorm_pair(*acc)
-        acc = pair(self.ctx, lambda: self._xor(acc[0], e13[0]), lambda: self._xor(acc[1], e13[1]))
+        acc = pair(self.ctx, lambda: self._xor(acc[0], e13[0], fl), lambda: self._xor(acc[1], e13[1], fl))
         log("acc2", acc)
         acc = self._renorm_pair(*acc)
-        out = self._renorm_pair(*pair(self.ctx, lambda: self._xor(acc[0], e9[0]), lambda: self._xor(acc[1], e9[1])))
+        out = self._renorm_pair(*pair(self.ctx, lambda: self._xor(acc[0], e9[0], fl), lambda: self._xor(acc[1], e9[1], fl)))
         if do_final_bootstrap:
             out = pair(self.ctx, lambda: self.ctx.bootstrap(out[0]), lambda: self.ctx.bootstrap(out[1]))
         log("out", out)

@@ -16,7 +16,7 @@ import numpy as np
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT, SplitLUT2, powers, std_basis
-from utils import fused_lut, pair
+from utils import LUT2_DEPTH, RENORM_FLOOR, drop_to, fused_lut, pair
 
 
 class _CoeffCache:
@@ -91,11 +91,14 @@ def gf_eval(ctx, cache: _CoeffCache, mult: int, which: str, ct_hi, ct_lo) -> Any
     return _gf_sum(ctx, cache.load_plaintexts(ctx, mult, which), bx, by, ct_hi)
 
 
-def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo):
+def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo, out_level=None):
     """(gf_mult{mult}_hi, gf_mult{mult}_lo)(hi, lo).  With a fused-LUT context both LUTs are
     evaluated in the conjugate-split form (xor4_lut.SplitLUT2) over ONE pair
     of bases -- positive powers of hi, standard basis of lo -- instead of four 16-element
-    bases; otherwise the reference's per-LUT product loops (REF/mixcol_final.py:80-99)."""
+    bases; otherwise the reference's per-LUT product loops (REF/mixcol_final.py:80-99).
+    out_level: inputs dropped to out_level + LUT2_DEPTH first (utils.drop_to)."""
+    if out_level is not None:
+        ct_hi, ct_lo = drop_to(ctx, ct_hi, out_level + LUT2_DEPTH), drop_to(ctx, ct_lo, out_level + LUT2_DEPTH)
     if getattr(ctx, "fused_luts", False):
         sh, sl = cache.split(mult, "hi"), cache.split(mult, "lo")
         try:
@@ -135,11 +138,11 @@ class MixColFinal:
     def _gf_poly_eval_2var(self, ct_hi, ct_lo, mult: int, which: str):
         return gf_eval(self.ctx, self._coeffs, mult, which, ct_hi, ct_lo)
 
-    def gf_mult_2(self, ct_hi, ct_lo):
-        return gf_mult_pair(self.ctx, self._coeffs, 2, ct_hi, ct_lo)
+    def gf_mult_2(self, ct_hi, ct_lo, out_level=None):
+        return gf_mult_pair(self.ctx, self._coeffs, 2, ct_hi, ct_lo, out_level)
 
-    def gf_mult_3(self, ct_hi, ct_lo):
-        return gf_mult_pair(self.ctx, self._coeffs, 3, ct_hi, ct_lo)
+    def gf_mult_3(self, ct_hi, ct_lo, out_level=None):
+        return gf_mult_pair(self.ctx, self._coeffs, 3, ct_hi, ct_lo, out_level)
 
     def _col_shift_rowmajor(self, ct, k_up: int):
         return self.ctx.rotate(ct, -4 * k_up * self.stride)
@@ -147,8 +150,8 @@ class MixColFinal:
     def _renorm_pair(self, hi, lo):
         return self.enc.renorm(hi, lo)
 
-    def _xor_ct(self, a, b):
-        return self.xor4.apply(a, b)
+    def _xor_ct(self, a, b, out_level=None):
+        return self.xor4.apply(a, b, out_level)
 
     def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
         log = (lambda k, v: debug.__setitem__(k, v)) if isinstance(debug, dict) else (lambda k, v: None)
@@ -158,17 +161,21 @@ class MixColFinal:
         for k in (1, 2, 3):
             log(f"rotc{k}", rot[k])
         log("in", (ct_hi, ct_lo))
-        two = self.gf_mult_2(ct_hi, ct_lo)
-        thr = self.gf_mult_3(*rot[1])
+        # every XOR pair below is renormalised right away (REF :104-106), so the LUTs run on
+        # inputs dropped to the lowest level that leaves their output at RENORM_FLOOR
+        fl = RENORM_FLOOR
+        two = self.gf_mult_2(ct_hi, ct_lo, out_level=fl + LUT2_DEPTH)
+        thr = self.gf_mult_3(*rot[1], out_level=fl + LUT2_DEPTH)
         log("two", two)
         log("thr", thr)
-        acc = pair(self.ctx, lambda: self._xor_ct(two[0], thr[0]), lambda: self._xor_ct(two[1], thr[1]))
+        acc = pair(self.ctx, lambda: self._xor_ct(two[0], thr[0], fl), lambda: self._xor_ct(two[1], thr[1], fl))
         log("acc1", acc)
         acc = self._renorm_pair(*acc)
-        acc = pair(self.ctx, lambda: self._xor_ct(acc[0], rot[2][0]), lambda: self._xor_ct(acc[1], rot[2][1]))
+        acc = pair(self.ctx, lambda: self._xor_ct(acc[0], rot[2][0], fl), lambda: self._xor_ct(acc[1], rot[2][1], fl))
         log("acc2", acc)
         acc = self._renorm_pair(*acc)
-        acc = self._renorm_pair(*pair(self.ctx, lambda: self._xor_ct(acc[0], rot[3][0]), lambda: self._xor_ct(acc[1], rot[3][1])))
+        acc = self._renorm_pair(*pair(self.ctx, lambda: self._xor_ct(acc[0], rot[3][0], fl),
+                                      lambda: self._xor_ct(acc[1], rot[3][1], fl)))
         log("acc3", acc)
         out_hi, out_lo = acc
         if do_final_bootstrap:

@@ -16,7 +16,7 @@ states (a (B, 16) key array gives each state its own).
 """
 from __future__ import annotations
 
-from typing import Any, Dict, List, Tuple
+from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -27,6 +27,7 @@ from mixcol_final import MixColFinal
 from shift_rows import ShiftRows
 from state_encoder import StateEncoder
 from sub_bytes_lut import SubBytesLUT
+from utils import RENORM_FLOOR
 from xor4_lut import XOR4LUT
 
 
@@ -59,6 +60,20 @@ class AESPipeline:
     # ---------------------------------------------------------------- utils
     def _renorm_pair(self, hi, lo):
         return self.encoder.renorm(hi, lo) if self.use_hard_renorm_between_steps else (hi, lo)
+
+    def _floor(self) -> Optional[int]:
+        """output level a step needs when a renorm follows it (utils.RENORM_FLOOR), else None"""
+        return RENORM_FLOOR if self.use_hard_renorm_between_steps else None
+
+    def _ark_renorm(self, ct, key_pair):
+        """AddRoundKey then renorm: the XOR4s run on inputs dropped just above the floor"""
+        return self._renorm_pair(*self.ark(*ct, *key_pair, out_level=self._floor()))
+
+    def _sub_renorm(self, ct, inverse: bool = False):
+        lut = self.isub if inverse else self.sub
+        if lut is None:
+            raise KeyError("inv_sub_hi")
+        return self._renorm_pair(*lut.apply(*ct, out_level=self._floor()))
 
     def _encode_key(self, key_bytes: np.ndarray):
         key_bytes = np.asarray(key_bytes, dtype=np.uint8)
@@ -112,10 +127,10 @@ class AESPipeline:
     # ---------------------------------------------------------------- encrypt
     def encrypt_round(self, ct, key_pair):
         """One middle round r = 1..9: SB, renorm, SR, MC, ARK, renorm (REF :142-151)."""
-        ct = self._renorm_pair(*self.sub_bytes(*ct))
+        ct = self._sub_renorm(ct)
         ct = self.shift_rows(*ct)
         ct = self.mix_columns(*ct)
-        return self._renorm_pair(*self.add_round_key(*ct, *key_pair))
+        return self._ark_renorm(ct, key_pair)
 
     def encrypt(self, state: np.ndarray, round_keys: List[np.ndarray], debug: Dict[str, Any] | None = None):
         if debug is not None:
@@ -123,19 +138,19 @@ class AESPipeline:
         ct = self.encoder.encode(state)
         self._log_pair(debug, "enc.input", *ct)
         rk = self._prepare_round_keys(round_keys)
-        ct = self.add_round_key(*ct, *rk[0])
+        ct = self.ark(*ct, *rk[0], out_level=self._floor())
         self._log_pair(debug, "enc.r0.ark", *ct)
         ct = self._renorm_pair(*ct)
         self._log_pair(debug, "enc.r0.renorm", *ct)
         for r in range(1, 10):
             ct = self.encrypt_round(ct, rk[r])
-        ct = self.sub_bytes(*ct)
+        ct = self.sub.apply(*ct, out_level=self._floor())
         self._log_pair(debug, "enc.final.sub", *ct)
         ct = self._renorm_pair(*ct)
         self._log_pair(debug, "enc.final.sub.renorm", *ct)
         ct = self.shift_rows(*ct)
         self._log_pair(debug, "enc.final.sr", *ct)
-        ct = self.add_round_key(*ct, *rk[10])
+        ct = self.ark(*ct, *rk[10], out_level=self._floor())
         self._log_pair(debug, "enc.final.ark10", *ct)
         ct = self._renorm_pair(*ct)
         self._log_pair(debug, "enc.output", *ct)
@@ -147,16 +162,16 @@ class AESPipeline:
             debug.clear()
         rk = self._prepare_round_keys(round_keys)
         self._log_pair(debug, "dec.input", ct_hi, ct_lo)
-        ct = self.add_round_key(ct_hi, ct_lo, *rk[10])
+        ct = self.ark(ct_hi, ct_lo, *rk[10], out_level=self._floor())
         self._log_pair(debug, "dec.init.ark10", *ct)
         ct = self._renorm_pair(*ct)
         self._log_pair(debug, "dec.init.ark10.renorm", *ct)
         for r in range(9, 0, -1):
             ct = self.inv_shift_rows(*ct)
             self._log_pair(debug, f"dec.r{r}.isr", *ct)
-            ct = self._renorm_pair(*self.inv_sub_bytes(*ct))
+            ct = self._sub_renorm(ct, inverse=True)
             self._log_pair(debug, f"dec.r{r}.isb", *ct)
-            ct = self._renorm_pair(*self.add_round_key(*ct, *rk[r]))
+            ct = self._ark_renorm(ct, rk[r])
             self._log_pair(debug, f"dec.r{r}.ark", *ct)
             if self.with_inv_mix_columns:
                 # InvSubBytes' LUT needs a clean input, as SubBytes gets one after ARK in encrypt
@@ -164,11 +179,13 @@ class AESPipeline:
                 self._log_pair(debug, f"dec.r{r}.imc", *ct)
         ct = self.inv_shift_rows(*ct)
         self._log_pair(debug, "dec.final.isr", *ct)
-        ct = self.inv_sub_bytes(*ct)
+        if self.isub is None:
+            raise KeyError("inv_sub_hi")
+        ct = self.isub.apply(*ct, out_level=self._floor())
         self._log_pair(debug, "dec.final.isb", *ct)
         ct = self._renorm_pair(*ct)
         self._log_pair(debug, "dec.final.isb.renorm", *ct)
-        ct = self.add_round_key(*ct, *rk[0])
+        ct = self.ark(*ct, *rk[0], out_level=self._floor())
         self._log_pair(debug, "dec.final.ark0", *ct)
         ct = self._renorm_pair(*ct)
         self._log_pair(debug, "dec.output", *ct)

@@ -21,7 +21,7 @@ Evaluation forms (same polynomials, same output level, outputs equal up to CKKS 
 from typing import Any, Dict, Tuple
 
 import numpy as np
-from utils import fused_lut, pair
+from utils import SUBBYTES_DEPTH, drop_to, fused_lut, pair
 
 _TOL = 1e-12
 
@@ -61,7 +61,12 @@ class SubBytesLUTFastCached:
     def _power(basis, k: int, domain: int, ctx):
         return basis[k - 1] if k <= len(basis) else ctx.conjugate(basis[domain - k - 1])
 
-    def apply(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:
+    def apply(self, ct_hi: Any, ct_lo: Any, out_level=None) -> Tuple[Any, Any]:
+        """(S_hi, S_lo)(hi, lo); out_level: the lowest level the caller needs the result at
+        (inputs dropped to out_level + SUBBYTES_DEPTH first, utils.drop_to); None = as given."""
+        if out_level is not None:
+            lv = out_level + SUBBYTES_DEPTH
+            ct_hi, ct_lo = drop_to(self.ctx, ct_hi, lv), drop_to(self.ctx, ct_lo, lv)
         if getattr(self.ctx, "fused_luts", False):
             return self._apply_bsgs(ct_hi, ct_lo)
         return self._apply_direct(ct_hi, ct_lo)

@@ -19,6 +19,27 @@ class ZetaEncoder:
         return np.mod(np.rint(turns), modulus).astype(np.uint8)
 
 
+# Level management for LUT steps whose result is renormalised right away:
+# the renorm decrypts at any level, so such a step may run on inputs dropped to the lowest
+# level that still leaves its output at RENORM_FLOOR.  Depths are those of the fused forms
+# from canonical inputs (measured: fresh level 17 -> 12 for XOR4 / GF multipliers, -> 4 for
+# SubBytes).
+RENORM_FLOOR = 2
+LUT2_DEPTH = 5       # bivariate nibble LUT (XOR4, GF multipliers): basis 3 + product + coefficient
+SUBBYTES_DEPTH = 13  # lift, b = hi * L(lo), baby/giant steps (sub_bytes_lut.py)
+
+
+def drop_to(ctx, ct, level):
+    """ct at `level` if it sits higher (exact-scale level drop, no rescale noise), else ct"""
+    if level is None or level < 0:
+        return ct
+    down = getattr(ctx, "level_down", None)
+    lv = getattr(ct, "level", None)
+    if down is None or lv is None or lv <= level:
+        return ct
+    return down(ct, level)
+
+
 def pair(ctx, fa, fb, shared=()):
     """(fa(), fb()) -- the hi / lo halves of an AES step, run concurrently on two HIP streams
     when the context supports it (EngineContext.run_parallel); `shared` ciphertexts read by

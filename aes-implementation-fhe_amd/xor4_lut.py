@@ -17,7 +17,7 @@ x^8 are skipped for XOR4), and each S is one fused kernel.  Output level unchang
 from typing import Any, Dict
 
 import numpy as np
-from utils import fused_lut, pair
+from utils import LUT2_DEPTH, drop_to, fused_lut, pair
 
 
 def basis16(ctx, ct, *, retry_intt: bool = True) -> Dict[int, Any]:
@@ -135,8 +135,12 @@ class XOR4LUT:
     def _build_power_basis_16(self, ct: Any) -> Dict[int, Any]:
         return basis16(self.ctx, ct)
 
-    def apply(self, a_ct, b_ct):
+    def apply(self, a_ct, b_ct, out_level=None):
+        """XOR4(a, b); out_level: the lowest level the caller needs the result at (the inputs
+        are dropped to out_level + LUT2_DEPTH first, utils.drop_to); None = as given."""
         ctx = self.ctx
+        if out_level is not None:
+            a_ct, b_ct = drop_to(ctx, a_ct, out_level + LUT2_DEPTH), drop_to(ctx, b_ct, out_level + LUT2_DEPTH)
         if not hasattr(self, "_split"):
             self._split = SplitLUT2(self.coeffs)
         out = split_lut2(ctx, self._split, ("xor4", id(self)), a_ct, b_ct)
