@@ -425,9 +425,12 @@ public:
         return put_ct(out);
     }
     // public-key encryption of an encoded message m (NTT form on nl(f) + 1 limbs, scale
-    // delta_f q_{nl(f)}): c = (v pk0 + e0 + m, v pk1 + e1) at level f + 1, rescaled to f
-    Ct encrypt_ntt(const u32* m) {
-        const int n = hp_.n, f = hp_.fresh, nq = hp_.nl(f) + 1;
+    // delta_f q_{nl(f)}): c = (v pk0 + e0 + m, v pk1 + e1) at level f + 1, rescaled to f;
+    // level < 0: the fresh level; any level 0..fresh works the same way (the public key
+    // restricted to the first nl(f) + 1 limbs)
+    Ct encrypt_ntt(const u32* m, int level = -1) {
+        const int f = level < 0 ? hp_.fresh : level;
+        const int n = hp_.n, nq = hp_.nl(f) + 1;
         const int L = f;
         u32* v = tmp(nq);
         u32* e = tmp(2 * nq);
@@ -1348,9 +1351,13 @@ public:
     // batch holds byte i in slot i * stride + b, so every slot with (j mod stride) < states is
     // snapped and the rest are reset to 1.  The whole slot vector is decoded and re-encoded
     // with a device fp64 FFT (launch_fft2); states == 1 keeps the 16-slot direct evaluation.
+    //
+    // level >= 0 re-encrypts at min(level, fresh) instead of the fresh level:
+    // callers that know what the next step needs save the limbs
     void renorm_pair(aesfhe_handle hh, aesfhe_handle hl, aesfhe_handle* oh, aesfhe_handle* ol) { renorm_states(hh, hl, 1, oh, ol); }
-    void renorm_states(aesfhe_handle hh, aesfhe_handle hl, int states, aesfhe_handle* oh, aesfhe_handle* ol) {
+    void renorm_states(aesfhe_handle hh, aesfhe_handle hl, int states, aesfhe_handle* oh, aesfhe_handle* ol, int level = -1) {
         if (!d_pk_) throw std::runtime_error("keys not generated");
+        if (level > hp_.fresh) level = hp_.fresh;  // never above a fresh encryption
         const int n = hp_.n, s = slot_count(), stride = s / 16;
         if (states < 1 || states > stride)
             throw std::runtime_error("renorm: states per ciphertext must be in [1, slot_count / 16]");
@@ -1400,7 +1407,7 @@ public:
             if (own) release(c);
             cnt_[C_DEC]++;
         }
-        const int f = hp_.fresh, nq = hp_.nl(f) + 1;
+        const int f = level < 0 ? hp_.fresh : level, nq = hp_.nl(f) + 1;
         const double enc_scale = hp_.delta[f] * (double)hp_.mod[hp_.nl(f)];
         u32* m = tmp(2 * (size_t)nq);
         if (states == 1) {
@@ -1422,8 +1429,8 @@ public:
             launch_encode_untwist(S(), T_, m, w, enc_scale, nq);
         }
         ntt(m, 2 * nq, nq, qmap());
-        Ct a = encrypt_ntt(m);
-        Ct b = encrypt_ntt(m + (size_t)nq * n);
+        Ct a = encrypt_ntt(m, f);
+        Ct b = encrypt_ntt(m + (size_t)nq * n, f);
         untmp(m, 2 * (size_t)nq);
         untmp(x, 8);
         *oh = put_ct(a);
@@ -2335,6 +2342,11 @@ int aesfhe_renorm_pair(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesf
 int aesfhe_renorm_states(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, int states, aesfhe_handle* out_hi,
                          aesfhe_handle* out_lo) {
     API_BEGIN ctx->eng->renorm_states(hi, lo, states, out_hi, out_lo);
+    API_END
+}
+int aesfhe_renorm_at(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, int states, int level, aesfhe_handle* out_hi,
+                     aesfhe_handle* out_lo) {
+    API_BEGIN ctx->eng->renorm_states(hi, lo, states, out_hi, out_lo, level);
     API_END
 }
 int aesfhe_export(aesfhe_ctx* ctx, aesfhe_handle c, uint32_t* out, uint64_t words) {

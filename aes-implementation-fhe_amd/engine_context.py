@@ -167,10 +167,11 @@ class EngineContext:
         """the same message at a lower level (exact scale; used by utils.drop_to)"""
         return self.engine.level_down(ct, level)
 
-    def renorm_pair(self, hi, lo, states: int = 1):
+    def renorm_pair(self, hi, lo, states: int = 1, level=None):
         """Device-side Zeta16 secret-key renorm of a (hi, lo) state pair (REF/pipeline.py:65-69);
-        `states` > 1: that many slot-packed states per pair (StateEncoder)."""
-        return self.engine.renorm_pair(hi, lo, states)
+        `states` > 1: that many slot-packed states per pair (StateEncoder, SURVEY.md §8(f)1);
+        `level`: re-encrypt at that level instead of the fresh one."""
+        return self.engine.renorm_pair(hi, lo, states, level)
 
     def lut(self, key, coeffs, c0: complex = 0j):
         """Engine-side coefficient set of a LUT polynomial, created once per key."""

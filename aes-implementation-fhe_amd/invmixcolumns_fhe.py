@@ -10,7 +10,7 @@ from mixcol_final import _CoeffCache, gf_basis16, gf_eval, gf_mult_pair
 from shift_rows import row_masks
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT
-from utils import LUT2_DEPTH, RENORM_FLOOR, pair
+from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, pair
 
 
 class InvMixColumnsFHE:
@@ -36,8 +36,8 @@ class InvMixColumnsFHE:
     def _xor(self, a, b, out_level=None):
         return self.xor4.apply(a, b, out_level)
 
-    def _renorm_pair(self, hi, lo):
-        return self.enc.renorm(hi, lo) if self.use_hard_renorm else (hi, lo)
+    def _renorm_pair(self, hi, lo, level=None):
+        return self.enc.renorm(hi, lo, level) if self.use_hard_renorm else (hi, lo)
 
     def _rot_rows_in_col(self, ct, k_rows: int):
         """Masked per-row rotation by k*stride (REF :100-109; unused by __call__)."""
@@ -83,11 +83,12 @@ class InvMixColumnsFHE:
         fl = self._xor_level
         acc = pair(self.ctx, lambda: self._xor(e14[0], e11[0], fl), lambda: self._xor(e14[1], e11[1], fl))
         log("acc1", acc)
-        acc = self._renorm_pair(*acc)
+        acc = self._renorm_pair(*acc, level=NEED_XOR)  # internal: only the next XOR4 reads it
         acc = pair(self.ctx, lambda: self._xor(acc[0], e13[0], fl), lambda: self._xor(acc[1], e13[1], fl))
         log("acc2", acc)
-        acc = self._renorm_pair(*acc)
-        out = self._renorm_pair(*pair(self.ctx, lambda: self._xor(acc[0], e9[0], fl), lambda: self._xor(acc[1], e9[1], fl)))
+        acc = self._renorm_pair(*acc, level=NEED_XOR)
+        out = self._renorm_pair(*pair(self.ctx, lambda: self._xor(acc[0], e9[0], fl), lambda: self._xor(acc[1], e9[1], fl)),
+                                level=NEED_BOOTSTRAP if do_final_bootstrap else None)
         if do_final_bootstrap:
             out = pair(self.ctx, lambda: self.ctx.bootstrap(out[0]), lambda: self.ctx.bootstrap(out[1]))
         log("out", out)

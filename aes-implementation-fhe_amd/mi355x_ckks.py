@@ -34,7 +34,7 @@ EXPORTED = [
     "aesfhe_level", "aesfhe_plaintext", "aesfhe_encrypt", "aesfhe_decrypt", "aesfhe_add", "aesfhe_sub",
     "aesfhe_add_pt", "aesfhe_add_scalar", "aesfhe_mul_scalar", "aesfhe_mul_pt", "aesfhe_mul",
     "aesfhe_relinearize", "aesfhe_rescale", "aesfhe_level_down", "aesfhe_rotate", "aesfhe_conjugate",
-    "aesfhe_power_basis", "aesfhe_to_ntt", "aesfhe_to_intt", "aesfhe_bootstrap", "aesfhe_renorm_pair", "aesfhe_renorm_states",
+    "aesfhe_power_basis", "aesfhe_to_ntt", "aesfhe_to_intt", "aesfhe_bootstrap", "aesfhe_renorm_pair", "aesfhe_renorm_states", "aesfhe_renorm_at",
     "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
     "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
     "aesfhe_streams", "aesfhe_bind_stream", "aesfhe_fork", "aesfhe_join", "aesfhe_settle",
@@ -83,6 +83,7 @@ def load_library(path: Optional[Path] = None):
         "aesfhe_to_ntt": [vp, _H, _Hp], "aesfhe_to_intt": [vp, _H, _Hp], "aesfhe_bootstrap": [vp, _H, _Hp],
         "aesfhe_renorm_pair": [vp, _H, _H, _Hp, _Hp],
         "aesfhe_renorm_states": [vp, _H, _H, c_int, _Hp, _Hp],
+        "aesfhe_renorm_at": [vp, _H, _H, c_int, c_int, _Hp, _Hp],
         "aesfhe_export": [vp, _H, _up, ctypes.c_uint64], "aesfhe_import": [vp, c_int, c_int, _up, _Hp],
         "aesfhe_export_secret": [vp, _up], "aesfhe_export_pk": [vp, _up],
         "aesfhe_export_ksk": [vp, ctypes.c_uint64, _up],
@@ -452,10 +453,14 @@ class Engine:
     def intt(self, ct):
         return self._new(self._lib.aesfhe_to_intt, ct.handle)
 
-    def renorm_pair(self, hi, lo, states: int = 1):
-        """secret-key Zeta16 renorm of a (hi, lo) pair holding `states` slot-packed AES states"""
+    def renorm_pair(self, hi, lo, states: int = 1, level=None):
+        """secret-key Zeta16 renorm of a (hi, lo) pair holding `states` slot-packed AES states,
+        re-encrypted at `level` (None = the fresh level)"""
         a, b = ctypes.c_uint64(), ctypes.c_uint64()
-        if states == 1:
+        if level is not None:
+            rc = self._lib.aesfhe_renorm_at(self._ctx.ptr, hi.handle, lo.handle, int(states), int(level), ctypes.byref(a),
+                                            ctypes.byref(b))
+        elif states == 1:
             rc = self._lib.aesfhe_renorm_pair(self._ctx.ptr, hi.handle, lo.handle, ctypes.byref(a), ctypes.byref(b))
         else:
             rc = self._lib.aesfhe_renorm_states(self._ctx.ptr, hi.handle, lo.handle, int(states), ctypes.byref(a), ctypes.byref(b))

@@ -16,7 +16,7 @@ import numpy as np
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT, SplitLUT2, powers, std_basis
-from utils import LUT2_DEPTH, RENORM_FLOOR, drop_to, fused_lut, pair
+from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, drop_to, fused_lut, pair
 
 
 class _CoeffCache:
@@ -147,8 +147,8 @@ class MixColFinal:
     def _col_shift_rowmajor(self, ct, k_up: int):
         return self.ctx.rotate(ct, -4 * k_up * self.stride)
 
-    def _renorm_pair(self, hi, lo):
-        return self.enc.renorm(hi, lo)
+    def _renorm_pair(self, hi, lo, level=None):
+        return self.enc.renorm(hi, lo, level)
 
     def _xor_ct(self, a, b, out_level=None):
         return self.xor4.apply(a, b, out_level)
@@ -170,12 +170,14 @@ class MixColFinal:
         log("thr", thr)
         acc = pair(self.ctx, lambda: self._xor_ct(two[0], thr[0], fl), lambda: self._xor_ct(two[1], thr[1], fl))
         log("acc1", acc)
-        acc = self._renorm_pair(*acc)
+        acc = self._renorm_pair(*acc, level=NEED_XOR)  # internal: only the next XOR4 reads it
         acc = pair(self.ctx, lambda: self._xor_ct(acc[0], rot[2][0], fl), lambda: self._xor_ct(acc[1], rot[2][1], fl))
         log("acc2", acc)
-        acc = self._renorm_pair(*acc)
+        acc = self._renorm_pair(*acc, level=NEED_XOR)
+        # the output is bootstrapped next (from level 0) or returned at the fresh level
         acc = self._renorm_pair(*pair(self.ctx, lambda: self._xor_ct(acc[0], rot[3][0], fl),
-                                      lambda: self._xor_ct(acc[1], rot[3][1], fl)))
+                                      lambda: self._xor_ct(acc[1], rot[3][1], fl)),
+                                level=NEED_BOOTSTRAP if do_final_bootstrap else None)
         log("acc3", acc)
         out_hi, out_lo = acc
         if do_final_bootstrap:

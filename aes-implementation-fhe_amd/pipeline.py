@@ -27,7 +27,7 @@ from mixcol_final import MixColFinal
 from shift_rows import ShiftRows
 from state_encoder import StateEncoder
 from sub_bytes_lut import SubBytesLUT
-from utils import RENORM_FLOOR
+from utils import NEED_GF, NEED_ISR_ISB, NEED_SR_ARK, NEED_SR_MIX, NEED_SUBBYTES, NEED_XOR, RENORM_FLOOR
 from xor4_lut import XOR4LUT
 
 
@@ -58,22 +58,23 @@ class AESPipeline:
         self._rk_tag = b""
 
     # ---------------------------------------------------------------- utils
-    def _renorm_pair(self, hi, lo):
-        return self.encoder.renorm(hi, lo) if self.use_hard_renorm_between_steps else (hi, lo)
+    def _renorm_pair(self, hi, lo, level=None):
+        """renorm between steps; `level` = what the next step needs (utils.NEED_*; None = fresh)"""
+        return self.encoder.renorm(hi, lo, level) if self.use_hard_renorm_between_steps else (hi, lo)
 
     def _floor(self) -> Optional[int]:
         """output level a step needs when a renorm follows it (utils.RENORM_FLOOR), else None"""
         return RENORM_FLOOR if self.use_hard_renorm_between_steps else None
 
-    def _ark_renorm(self, ct, key_pair):
+    def _ark_renorm(self, ct, key_pair, level=None):
         """AddRoundKey then renorm: the XOR4s run on inputs dropped just above the floor"""
-        return self._renorm_pair(*self.ark(*ct, *key_pair, out_level=self._floor()))
+        return self._renorm_pair(*self.ark(*ct, *key_pair, out_level=self._floor()), level=level)
 
-    def _sub_renorm(self, ct, inverse: bool = False):
+    def _sub_renorm(self, ct, inverse: bool = False, level=None):
         lut = self.isub if inverse else self.sub
         if lut is None:
             raise KeyError("inv_sub_hi")
-        return self._renorm_pair(*lut.apply(*ct, out_level=self._floor()))
+        return self._renorm_pair(*lut.apply(*ct, out_level=self._floor()), level=level)
 
     def _encode_key(self, key_bytes: np.ndarray):
         key_bytes = np.asarray(key_bytes, dtype=np.uint8)
@@ -127,10 +128,10 @@ class AESPipeline:
     # ---------------------------------------------------------------- encrypt
     def encrypt_round(self, ct, key_pair):
         """One middle round r = 1..9: SB, renorm, SR, MC, ARK, renorm (REF :142-151)."""
-        ct = self._sub_renorm(ct)
+        ct = self._sub_renorm(ct, level=NEED_SR_MIX)
         ct = self.shift_rows(*ct)
         ct = self.mix_columns(*ct)
-        return self._ark_renorm(ct, key_pair)
+        return self._ark_renorm(ct, key_pair, level=NEED_SUBBYTES)
 
     def encrypt(self, state: np.ndarray, round_keys: List[np.ndarray], debug: Dict[str, Any] | None = None):
         if debug is not None:
@@ -140,13 +141,13 @@ class AESPipeline:
         rk = self._prepare_round_keys(round_keys)
         ct = self.ark(*ct, *rk[0], out_level=self._floor())
         self._log_pair(debug, "enc.r0.ark", *ct)
-        ct = self._renorm_pair(*ct)
+        ct = self._renorm_pair(*ct, level=NEED_SUBBYTES)
         self._log_pair(debug, "enc.r0.renorm", *ct)
         for r in range(1, 10):
             ct = self.encrypt_round(ct, rk[r])
         ct = self.sub.apply(*ct, out_level=self._floor())
         self._log_pair(debug, "enc.final.sub", *ct)
-        ct = self._renorm_pair(*ct)
+        ct = self._renorm_pair(*ct, level=NEED_SR_ARK)
         self._log_pair(debug, "enc.final.sub.renorm", *ct)
         ct = self.shift_rows(*ct)
         self._log_pair(debug, "enc.final.sr", *ct)
@@ -164,18 +165,18 @@ class AESPipeline:
         self._log_pair(debug, "dec.input", ct_hi, ct_lo)
         ct = self.ark(ct_hi, ct_lo, *rk[10], out_level=self._floor())
         self._log_pair(debug, "dec.init.ark10", *ct)
-        ct = self._renorm_pair(*ct)
+        ct = self._renorm_pair(*ct, level=NEED_ISR_ISB)
         self._log_pair(debug, "dec.init.ark10.renorm", *ct)
         for r in range(9, 0, -1):
             ct = self.inv_shift_rows(*ct)
             self._log_pair(debug, f"dec.r{r}.isr", *ct)
-            ct = self._sub_renorm(ct, inverse=True)
+            ct = self._sub_renorm(ct, inverse=True, level=NEED_XOR)
             self._log_pair(debug, f"dec.r{r}.isb", *ct)
-            ct = self._ark_renorm(ct, rk[r])
+            ct = self._ark_renorm(ct, rk[r], level=NEED_GF if self.with_inv_mix_columns else NEED_ISR_ISB)
             self._log_pair(debug, f"dec.r{r}.ark", *ct)
             if self.with_inv_mix_columns:
                 # InvSubBytes' LUT needs a clean input, as SubBytes gets one after ARK in encrypt
-                ct = self._renorm_pair(*self.inv_mix_columns(*ct))
+                ct = self._renorm_pair(*self.inv_mix_columns(*ct), level=NEED_ISR_ISB)
                 self._log_pair(debug, f"dec.r{r}.imc", *ct)
         ct = self.inv_shift_rows(*ct)
         self._log_pair(debug, "dec.final.isr", *ct)
@@ -183,7 +184,7 @@ class AESPipeline:
             raise KeyError("inv_sub_hi")
         ct = self.isub.apply(*ct, out_level=self._floor())
         self._log_pair(debug, "dec.final.isb", *ct)
-        ct = self._renorm_pair(*ct)
+        ct = self._renorm_pair(*ct, level=NEED_XOR)
         self._log_pair(debug, "dec.final.isb.renorm", *ct)
         ct = self.ark(*ct, *rk[0], out_level=self._floor())
         self._log_pair(debug, "dec.final.ark0", *ct)

@@ -9,11 +9,15 @@ i*stride + b.  Every rotation the AES modules issue is a multiple of stride, so 
 columns never mix; slots with (j mod stride) >= B hold 1+0j as in the reference.
 ``encode`` then takes a (B, 16) uint8 array and ``decode`` returns one.
 """
+import os
 from typing import Any, Tuple
 
 import numpy as np
 
 from utils import ZetaEncoder
+
+# AESFHE_RENORM_FRESH=1: ignore renorm target levels (A/B measurements of DESIGN.md §3.11)
+_RENORM_FRESH = os.environ.get("AESFHE_RENORM_FRESH") == "1"
 
 
 class StateEncoder:
@@ -54,9 +58,12 @@ class StateEncoder:
         out = ((hi << 4) | lo).astype(np.uint8)
         return out[0] if self.states == 1 else out
 
-    def renorm(self, ct_hi, ct_lo) -> Tuple[Any, Any]:
-        """decode -> re-encode (REF/pipeline.py:65-69), done on the device when available."""
+    def renorm(self, ct_hi, ct_lo, level=None) -> Tuple[Any, Any]:
+        """decode -> re-encode (REF/pipeline.py:65-69), done on the device when available;
+        `level`: the level the next step needs (None = fresh), honoured by the device path."""
         fast = getattr(self.ctx, "renorm_pair", None)
         if fast is not None:
+            if level is not None and not _RENORM_FRESH:
+                return fast(ct_hi, ct_lo, states=self.states, level=level)
             return fast(ct_hi, ct_lo) if self.states == 1 else fast(ct_hi, ct_lo, states=self.states)
         return self.encode(self.decode(ct_hi, ct_lo))

@@ -27,6 +27,15 @@ class ZetaEncoder:
 RENORM_FLOOR = 2
 LUT2_DEPTH = 5       # bivariate nibble LUT (XOR4, GF multipliers): basis 3 + product + coefficient
 SUBBYTES_DEPTH = 13  # lift, b = hi * L(lo), baby/giant steps (sub_bytes_lut.py)
+SHIFTROWS_DEPTH = 1  # masked rotations (shift_rows.py)
+# the level each renorm re-encrypts at = what the step after it needs (engine renorm `level`)
+NEED_XOR = RENORM_FLOOR + LUT2_DEPTH                 # an XOR4 whose result is renormalised
+NEED_GF = NEED_XOR + LUT2_DEPTH                      # GF multipliers feeding such an XOR4
+NEED_SUBBYTES = RENORM_FLOOR + SUBBYTES_DEPTH        # (Inv)SubBytes, then renorm
+NEED_SR_MIX = NEED_GF + SHIFTROWS_DEPTH              # ShiftRows -> MixColumns
+NEED_SR_ARK = NEED_XOR + SHIFTROWS_DEPTH             # ShiftRows -> AddRoundKey (last round)
+NEED_ISR_ISB = NEED_SUBBYTES + SHIFTROWS_DEPTH       # InvShiftRows -> InvSubBytes
+NEED_BOOTSTRAP = 0                                   # bootstrapping starts from level 0
 
 
 def drop_to(ctx, ct, level):

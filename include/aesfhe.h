@@ -155,6 +155,10 @@ int aesfhe_renorm_pair(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesf
  * Replaces the per-state loop over REF/pipeline.py:65-69 for a batch of states. */
 int aesfhe_renorm_states(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, int states, aesfhe_handle* out_hi,
                          aesfhe_handle* out_lo);
+/* renorm_states re-encrypting at min(level, fresh) (< 0 = the fresh level) instead of the
+ * fresh level: a caller that knows the depth of its next step saves limbs */
+int aesfhe_renorm_at(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, int states, int level, aesfhe_handle* out_hi,
+                     aesfhe_handle* out_lo);
 
 /* --- raw access (tests, parity against the oracle) ------------------------------------ */
 /* limbs of a ciphertext: npoly x (level+2) x N uint32, NTT form */
