@@ -1663,7 +1663,64 @@ public:
 
     // sum_{k <= deg} c_k T_k from the baby table T[1..8] (T_0 = 1): scalar products deferred
     // (one rescale for the whole leaf), constant term added at the raw scale
+    // c_0 + sum_k c_k T_k as ONE fused kernel (k_lut_univariate): integer constants
+    // round(c_k S_out / delta_{level(T_k)}) at the output's raw scale S_out = raw_scale(l, 1),
+    // l = the lowest level of the terms (their first nl(l) limbs are read); cached per
+    // coefficient vector and level signature.  Returns false when the scale has no headroom.
+    bool cheb_leaf_fused(const std::vector<Ct>& T, const std::vector<double>& c, Ct& out) {
+        std::vector<int> ks;
+        double mag = std::fabs(c[0]);
+        int l = 1 << 30;
+        for (size_t k = 1; k < c.size(); ++k) {
+            if (c[k] == 0.0) continue;
+            const Ct& t = T[k];
+            if (t.npoly != 2 || t.pend != 0 || t.lazy || !t.ntt) return false;
+            ks.push_back((int)k);
+            mag += std::fabs(c[k]);
+            l = std::min(l, t.level);
+        }
+        if (ks.empty() || (int)ks.size() > kLutChunk || !headroom(l, 1, mag)) return false;
+        const int nl = hp_.nl(l);
+        const double S_out = raw_scale(l, 1);
+        std::string key = std::to_string(l) + ":";
+        for (int k : ks) key += std::to_string(k) + "@" + std::to_string(T[k].level) + "=" + std::to_string(c[k]) + ",";
+        auto it = leaf_cst_.find(key);
+        if (it == leaf_cst_.end()) {
+            std::vector<u32> h(ks.size() * (size_t)nl * 4), lo, hi;
+            for (size_t j = 0; j < ks.size(); ++j) {
+                scalar_residues(std::llround(c[ks[j]] * S_out / hp_.delta[T[ks[j]].level]), 0, nl, lo, hi);
+                for (int t = 0; t < nl; ++t) {
+                    u32* e = &h[(j * nl + t) * 4];
+                    e[0] = lo[t], e[1] = shoup_pre(lo[t], hp_.mod[t]);
+                    e[2] = hi[t], e[3] = shoup_pre(hi[t], hp_.mod[t]);
+                }
+            }
+            const size_t words = (h.size() + (size_t)hp_.n - 1) / hp_.n * hp_.n;
+            u32* d = dev_alloc(words);  // lives with the context (one per leaf and level signature)
+            HIP_OK(hipMemcpyAsync(d, h.data(), h.size() * sizeof(u32), hipMemcpyHostToDevice, S()));
+            HIP_OK(hipStreamSynchronize(S()));
+            it = leaf_cst_.emplace(key, d).first;
+        }
+        LutChunk ch{};
+        for (size_t j = 0; j < ks.size(); ++j) ch.x[j] = T[ks[j]].data, ch.nx[j] = hp_.nl(T[ks[j]].level);
+        Ct o = alloc_ct(l, 2);
+        launch_lut_univariate(S(), T_, o.data, nullptr, ch, (int)ks.size(), it->second, 2, nl);
+        o.pend = 1;
+        o.lazy = true;
+        if (c[0] != 0.0) {
+            Ct r = add_scalar(o, c[0], 0.0);
+            release(o);
+            o = r;
+        }
+        out = normalize(o, true);
+        if (out.data != o.data) release(o);
+        return true;
+    }
+    std::map<std::string, u32*> leaf_cst_;
+
     Ct cheb_leaf(const std::vector<Ct>& T, const std::vector<double>& c) {
+        Ct fused;
+        if (cheb_leaf_fused(T, c, fused)) return fused;
         Ct acc;
         bool have = false;
         for (size_t k = 1; k < c.size(); ++k) {
