@@ -11,6 +11,7 @@ a visible GPU raises ``RuntimeError``.
 from __future__ import annotations
 
 import concurrent.futures
+import os
 import ctypes
 import threading
 import numbers
@@ -263,6 +264,11 @@ class Engine:
         self._ctx.check(L.aesfhe_level_limbs(self._ctx.ptr, limbs))
         self.level_limbs = [int(x) for x in limbs]
         self._keys_ready = False
+        # AESFHE_PROFILE_FROM_START=kid,kid: engine kernel accounting from the first launch on
+        # (key generation included), to match whole-process rocprofv3 --pmc totals (tools/ks_probe.py)
+        early = os.environ.get("AESFHE_PROFILE_FROM_START")
+        if early:
+            self.profile([k for k in early.split(",") if k])
         self.set_lazy(lazy)
         self.concurrent = bool(concurrent)
         self._pool = None

@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--no-final-bootstrap", action="store_true",
                     help="diagnostic only: skip MixColFinal's final bootstrap (not the benchmark workload)")
     ap.add_argument("--eager", action="store_true", help="relinearise and rescale after every product (no deferred evaluation)")
+    ap.add_argument("--serial", action="store_true",
+                    help="hi/lo halves on one stream (same launches, no overlap): for rocprofv3 --pmc passes, whose "
+                         "counter collection crashes on launches from the branch threads")
     ap.add_argument("--dry-run", action="store_true",
                     help="host orchestration only (process group, sharding, barrier, max-over-ranks, rank-0 line) with the "
                          "byte-level AES in place of the FHE engine; prints value null -- a test harness, not a measurement")
@@ -242,7 +245,8 @@ def main():
 
     coeffs = load_all_coeffs()
     signature = 2 if args.no_final_bootstrap else 1
-    ctx = EngineContext(signature=signature, max_level=17, thread_count=1, device_id=local, seed=0x5EED + rank, lazy=not args.eager)
+    ctx = EngineContext(signature=signature, max_level=17, thread_count=1, device_id=local, seed=0x5EED + rank, lazy=not args.eager,
+                        concurrent=not args.serial)
     xor4 = XOR4LUT(ctx, coeffs["xor4"])
     mix = MixColFinal(ctx, xor4)
     if args.no_final_bootstrap:
@@ -291,8 +295,15 @@ def main():
         ks = stats.get(kid, {"launches": 0, "ms": 0.0, "bytes": 0.0})
         achieved = ks["bytes"] / (ks["ms"] * 1e-3) / 1e9 if ks["ms"] > 0 else 0.0
         t = tj.get(kid)
+        bpl = ks["bytes"] / max(ks["launches"], 1)
+        traffic = None
+        if t and t.get("traffic_over_algorithmic"):  # measured HBM/algorithmic ratio applied to this run's launches
+            traffic = t["traffic_over_algorithmic"] * bpl
+        elif t:
+            traffic = t["bytes_per_launch"]
         return {"kernel": kid, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": t["bytes_per_launch"] if t else None,
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "traffic_over_algorithmic": t.get("traffic_over_algorithmic") if t else None,
                 "traffic_source": tj.get("_source") if t else None,
                 "timed_launches": ks["launches"], "sampled_every": 1 if args.profile_all else args.profile_every,
                 "avg_us": ks["ms"] / max(ks["launches"], 1) * 1e3,

@@ -2,7 +2,7 @@
 
 gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of
 wide coalesced reads -> x2; WRITE_SIZE is exact.  Both counters are in KB.  Usage:
-  python tools/pmc_reduce.py [--source=LABEL] OUT.json DIR [DIR ...]   (one DIR per --pmc pass)
+  python tools/pmc_reduce.py [--source=LABEL] [--alg=STATS.json] OUT.json DIR [DIR ...]   (one DIR per --pmc pass)
 Deletes the (large) CSVs after reading so gpurun can copy the result back."""
 import csv
 import json
@@ -22,10 +22,14 @@ def short(name: str) -> str:
 
 
 def main():
-    src = None
+    src = alg = None
     args = sys.argv[1:]
-    if args and args[0].startswith("--source="):
-        src, args = args[0].split("=", 1)[1], args[1:]
+    while args and args[0].startswith("--"):
+        if args[0].startswith("--source="):
+            src = args[0].split("=", 1)[1]
+        elif args[0].startswith("--alg="):  # the probe's own engine kernel_stats (algorithmic bytes)
+            alg = json.loads(Path(args[0].split("=", 1)[1]).read_text())
+        args = args[1:]
     out, dirs = Path(args[0]), args[1:]
     acc = defaultdict(lambda: defaultdict(float))
     cnt = defaultdict(lambda: defaultdict(int))
@@ -58,6 +62,12 @@ def main():
             a["launches"] += v["launches"]
     for kid, a in agg.items():
         res[kid] = {"bytes_per_launch": a["bytes"] / max(a["launches"], 1), "launches": a["launches"]}
+    if alg:  # traffic per launch over algorithmic bytes per launch, same launches
+        for kid, v in alg.items():
+            if kid in res and v.get("launches"):
+                a_b = v["bytes"] / v["launches"]
+                res[kid]["algorithmic_bytes_per_launch"] = a_b
+                res[kid]["traffic_over_algorithmic"] = res[kid]["bytes_per_launch"] / a_b if a_b else None
     if src:
         res["_source"] = src
     out.write_text(json.dumps(res, indent=1))
