@@ -11,6 +11,13 @@ from collections import defaultdict
 from pathlib import Path
 
 SCALE = {"FETCH_SIZE": 2 * 1024.0, "WRITE_SIZE": 1024.0}
+# kernels whose bulk reads are 4 B per lane in 64-B segments (not 16-B-per-lane streaming):
+# FETCH_SIZE counts those bytes as they are.  Calibrated with tools/ntt_pmc_calib.py (plain
+# 160-row NTTs): pass 1 (16-B-per-lane-equivalent coalesced reads) FETCH x2 = 1.03 x its
+# WRITE bytes, pass 2 (p[j + 16 k] dword reads) FETCH x2 = 2.36 x WRITE, i.e. FETCH x1 =
+# 1.18 x WRITE = its data plus twiddle pairs.  The finish variant's cur / add reads are
+# 16 B per lane, so its total is a lower bound.
+FETCH_AS_IS = ("ntt2_fwd",)
 
 
 def short(name: str) -> str:
@@ -42,7 +49,10 @@ def main():
                 for row in csv.DictReader(fh):
                     c = row["Counter_Name"]
                     k = short(row["Kernel_Name"])
-                    acc[k][c] += float(row["Counter_Value"]) * SCALE.get(c, 1.0)
+                    sc = SCALE.get(c, 1.0)
+                    if c == "FETCH_SIZE" and k.split("<")[0] in FETCH_AS_IS:
+                        sc = 1024.0
+                    acc[k][c] += float(row["Counter_Value"]) * sc
                     cnt[k][c] += 1
             f.unlink()
     res = {}
