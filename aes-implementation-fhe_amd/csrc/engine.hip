@@ -2463,6 +2463,12 @@ int aesfhe_kernel_stats(aesfhe_ctx* ctx, double* out, int n, int reset) {
     if (reset) p.reset();
     API_END
 }
+int aesfhe_kernel_work(aesfhe_ctx* ctx, double* out, int n) {
+    API_BEGIN KernelProfiler& p = ctx->eng->prof_;
+    p.flush();
+    for (int k = 0; k < n && k < KID_N; ++k) out[k] = p.work[k];
+    API_END
+}
 int aesfhe_reset_counters(aesfhe_ctx* ctx) {
     API_BEGIN ctx->eng->reset_counters();
     API_END

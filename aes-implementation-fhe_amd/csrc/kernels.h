@@ -26,6 +26,7 @@ struct KernelProfiler {
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
     double ms[KID_N] = {}, bytes[KID_N] = {};
+    double work[KID_N] = {};  // NTT kernels: radix-2 butterflies of the timed launches (VALU roofline)
     unsigned long long launches[KID_N] = {};
     hipEvent_t get();
     void flush();   // waits for recorded events and clock slots and folds them into the totals
@@ -39,10 +40,10 @@ struct KernelProfiler {
     int ts_next = 0;
     struct TsRec {
         int slot, kid;
-        double bytes;
+        double bytes, work;
     };
     std::vector<TsRec> ts_recs;
-    unsigned long long* ts_slot(int kid, double bytes);
+    unsigned long long* ts_slot(int kid, double bytes, double work = 0.0);
     void ts_flush();
 };
 // the profiler of the engine currently issuing launches (set per API call)

@@ -315,7 +315,7 @@ void KernelProfiler::flush() {
     }
     recs.clear();
 }
-unsigned long long* KernelProfiler::ts_slot(int kid, double b) {
+unsigned long long* KernelProfiler::ts_slot(int kid, double b, double w) {
     if (!d_ts) {
         void* p = nullptr;
         if (hipMalloc(&p, sizeof(unsigned long long) * 2 * kTsSlots) != hipSuccess) return nullptr;
@@ -324,7 +324,7 @@ unsigned long long* KernelProfiler::ts_slot(int kid, double b) {
         (void)hipMemset(d_ts + kTsSlots, 0, sizeof(unsigned long long) * kTsSlots);
     }
     if (ts_next == kTsSlots) ts_flush();
-    ts_recs.push_back({ts_next, kid, b});
+    ts_recs.push_back({ts_next, kid, b, w});
     return d_ts + ts_next++;
 }
 void KernelProfiler::ts_flush() {
@@ -337,6 +337,7 @@ void KernelProfiler::ts_flush() {
         if (a == ~0ull || e < a) continue;
         ms[r.kid] += (double)(e - a) * 1e-5;  // 100 MHz ticks -> ms
         bytes[r.kid] += r.bytes;
+        work[r.kid] += r.work;
         launches[r.kid] += 1;
     }
     ts_recs.clear();
@@ -346,7 +347,7 @@ void KernelProfiler::ts_flush() {
 }
 void KernelProfiler::reset() {
     flush();
-    for (int k = 0; k < KID_N; ++k) ms[k] = bytes[k] = 0, launches[k] = 0;
+    for (int k = 0; k < KID_N; ++k) ms[k] = bytes[k] = work[k] = 0, launches[k] = 0;
 }
 
 namespace {

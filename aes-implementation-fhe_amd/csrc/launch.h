@@ -24,13 +24,19 @@ inline void prof_launch(int kid, double bytes, F kernel, dim3 grid, dim3 block, 
     }
 }
 
-// launch of a kernel whose last parameter is an in-kernel clock slot (nullptr = untimed)
+// launch of a kernel whose last parameter is an in-kernel clock slot (nullptr = untimed);
+// `work` (NTT: butterflies) is accumulated beside the bytes for a VALU roofline
 template <typename F, typename... Args>
-inline void prof_launch_ts(int kid, double bytes, F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st, Args... args) {
+inline void prof_launch_tsw(int kid, double bytes, double work, F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st,
+                            Args... args) {
     KernelProfiler* p = g_prof;
     unsigned long long* ts = nullptr;
-    if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) ts = p->ts_slot(kid, bytes);
+    if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) ts = p->ts_slot(kid, bytes, work);
     hipLaunchKernelGGL(kernel, grid, block, lds, st, args..., ts);
+}
+template <typename F, typename... Args>
+inline void prof_launch_ts(int kid, double bytes, F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st, Args... args) {
+    prof_launch_tsw(kid, bytes, 0.0, kernel, grid, block, lds, st, args...);
 }
 
 // device side: the first thread of a sample of blocks (<= ~256 evenly spaced ones, always the

@@ -343,18 +343,21 @@ void ntt_fwd_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
     const double row_bytes = 4.0 * 256.0 * R1;
     const double io1 = 2.0 * io_rows * row_bytes;
     const double io2 = (M2 == kFinish ? (3.0 + (aux.add0 ? 0.5 : 0.0) + (aux.add1 ? 0.5 : 0.0)) : 2.0) * io_rows * row_bytes;
-    prof_launch_ts(KID_NTT_COLS_FWD, io1, k_ntt1_fwd<LOGR1, M1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, src, rm, map, Tb.pc,
-                Tb.tw, aux);
-    prof_launch_ts(KID_NTT_ROWS_FWD, io2, k_ntt2_fwd<LOGR1, M2>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, rm, map, Tb.pc,
-                Tb.tw, aux);
+    const double bfly = (double)io_rows * 128.0 * R1;  // N / 2 butterflies per stage and row
+    prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, M1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, src,
+                    rm, map, Tb.pc, Tb.tw, aux);
+    prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, rm,
+                    map, Tb.pc, Tb.tw, aux);
 }
 template <int LOGR1>
 void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {
     constexpr int R1 = 1 << LOGR1, CB = kThreads / (R1 / 16);
     const double io = 4.0 * 2.0 * rows * (256.0 * R1);  // the inverse is never launched with skips
-    prof_launch_ts(KID_NTT_ROWS_INV, io, k_ntt2_inv<LOGR1>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, src, rm, map, Tb.pc,
-                Tb.itw);
-    prof_launch_ts(KID_NTT_COLS_INV, io, k_ntt1_inv<LOGR1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, rm, map, Tb.pc, Tb.itw);
+    const double bfly = (double)rows * 128.0 * R1;
+    prof_launch_tsw(KID_NTT_ROWS_INV, io, bfly * 8.0, k_ntt2_inv<LOGR1>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, src, rm,
+                    map, Tb.pc, Tb.itw);
+    prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, rm, map,
+                    Tb.pc, Tb.itw);
 }
 
 }  // namespace

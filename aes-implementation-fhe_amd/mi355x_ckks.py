@@ -39,7 +39,7 @@ EXPORTED = [
     "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
     "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
     "aesfhe_streams", "aesfhe_bind_stream", "aesfhe_fork", "aesfhe_join", "aesfhe_settle",
-    "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan",
+    "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_kernel_work", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan",
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_lut_create", "aesfhe_lut_eval",
 ]
@@ -97,6 +97,7 @@ def load_library(path: Optional[Path] = None):
         "aesfhe_reset_counters": [vp],
         "aesfhe_profile": [vp, ctypes.c_uint32], "aesfhe_profile_every": [vp, c_int],
         "aesfhe_kernel_stats": [vp, _dp, c_int, c_int],
+        "aesfhe_kernel_work": [vp, _dp, c_int],
     }
     sig["aesfhe_bootstrap_depth"] = []
     sig["aesfhe_debug_bootplan"] = [c_int, _dp]
@@ -589,6 +590,12 @@ class Engine:
             mask |= 1 << KERNEL_IDS.index(k)
         self._ctx.check(self._lib.aesfhe_profile_every(self._ctx.ptr, int(every)))
         self._ctx.check(self._lib.aesfhe_profile(self._ctx.ptr, mask))
+
+    def kernel_work(self) -> dict:
+        """butterflies of the timed NTT launches per kernel id (read before kernel_stats resets)"""
+        out = np.zeros(len(KERNEL_IDS))
+        self._ctx.check(self._lib.aesfhe_kernel_work(self._ctx.ptr, out, len(KERNEL_IDS)))
+        return {k: float(out[i]) for i, k in enumerate(KERNEL_IDS)}
 
     def kernel_stats(self, reset: bool = True) -> dict:
         out = np.zeros(3 * len(KERNEL_IDS))

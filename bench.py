@@ -31,6 +31,12 @@ for _p in (str(ROOT), str(PKG)):
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+# VALU roofline of the NTT passes: u32 VALU issue rate measured on this chip with
+# tools/valu_rate.hip (v_mul_lo_u32 / v_mul_hi_u32 / v_min_u32 all at ~3.85e13 lane-instr/s,
+# i.e. the 32-bit multiplies are NOT quarter rate on gfx950) over the VALU instructions per
+# radix-2 butterfly in k_ntt2_fwd's ISA (1006 per thread for 64 butterflies)
+VALU_LANE_INSTR_PER_S = 3.85e13
+NTT_VALU_INSTR_PER_BFLY = 1006.0 / 64.0
 
 
 def parse():
@@ -278,6 +284,7 @@ def main():
     barrier(dist)
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(dist, elapsed)
+    work = E.kernel_work()
     stats = E.kernel_stats(reset=True)
     counters = E.counters()
     E.profile(())
@@ -309,6 +316,17 @@ def main():
                 "avg_us": ks["ms"] / max(ks["launches"], 1) * 1e3,
                 "bytes_per_launch": ks["bytes"] / max(ks["launches"], 1), "note": note}
 
+    def valu_roofline(kid: str) -> dict | None:
+        ks = stats.get(kid, {"ms": 0.0, "launches": 0})
+        if not work.get(kid) or ks["ms"] <= 0:
+            return None
+        achieved = work[kid] / (ks["ms"] * 1e-3)
+        peak = VALU_LANE_INSTR_PER_S / NTT_VALU_INSTR_PER_BFLY
+        return {"kernel": kid, "bound": "valu", "achieved": achieved, "peak": peak, "unit": "butterfly/s", "frac": achieved / peak,
+                "butterflies_per_launch": work[kid] / max(ks["launches"], 1),
+                "note": "peak = measured u32 VALU issue rate (tools/valu_rate.hip) / VALU instructions per butterfly in the "
+                        "kernel's ISA; the NTT passes are VALU-bound (HBM traffic = algorithmic bytes, profiles/r1_pmc_traffic.json)"}
+
     line = {
         "metric": "homomorphic AES-128 rounds/sec (enc) at N=2^16",
         "value": value,
@@ -331,6 +349,7 @@ def main():
         "roofline": roofline(args.kernel, "dominant kernel by time (NTT pass 2 incl. fused rescale/ModDown epilogue); "
                                           "VALU-bound by 3 u32 multiplies per butterfly (DESIGN.md 5)"),
         "roofline_secondary": roofline(args.kernel2, "key-switch inner product: HBM-bound"),
+        "roofline_valu": valu_roofline(args.kernel),
         "op_counts_per_round": {k: v / (10.0 * args.steps) for k, v in counters.items()},
     }
     if batch is not None:

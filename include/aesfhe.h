@@ -188,6 +188,9 @@ int aesfhe_profile_every(aesfhe_ctx* ctx, int every);
  * [launches, total ms, algorithmic bytes] */
 int aesfhe_profile(aesfhe_ctx* ctx, uint32_t mask);
 int aesfhe_kernel_stats(aesfhe_ctx* ctx, double* out, int n, int reset);
+/* radix-2 butterflies of the timed NTT launches per kernel id (out[n]; call before a resetting
+ * aesfhe_kernel_stats): the numerator of the NTT's VALU roofline */
+int aesfhe_kernel_work(aesfhe_ctx* ctx, double* out, int n);
 int aesfhe_reset_counters(aesfhe_ctx* ctx);
 
 #ifdef __cplusplus
