@@ -105,7 +105,8 @@ struct Ct {
     u32* data = nullptr;
     size_t words = 0;
     int level = 0;
-    int npoly = 2;
+    int npoly = 2;          // polynomials in data, all batched ciphertexts together
+    int nb = 1;             // batched ciphertexts stacked in data: [m][npoly / nb][nl] (bootstrap_pair)
     bool ntt = true;
     int pend = 0;
     bool lazy = false;
@@ -273,10 +274,11 @@ public:
         return h;
     }
 
-    Ct alloc_ct(int level, int npoly) {
+    Ct alloc_ct(int level, int npoly, int nb = 1) {
         Ct c;
         c.level = level;
         c.npoly = npoly;
+        c.nb = nb;
         c.words = (size_t)npoly * hp_.nl(level) * hp_.n;
         c.data = alloc_words(c.words);
         return c;
@@ -527,7 +529,7 @@ public:
     // ------------------------------------------------------------------ basic ops
     void release(const Ct& c) { pool().put(c.data, c.words); }
     static void copy_meta(Ct& o, const Ct& c) {
-        o.ntt = c.ntt, o.pend = c.pend, o.lazy = c.lazy, o.zero = c.zero;
+        o.ntt = c.ntt, o.pend = c.pend, o.lazy = c.lazy, o.zero = c.zero, o.nb = c.nb;
     }
     Ct copy(const Ct& c) {
         Ct o = alloc_ct(c.level, c.npoly);
@@ -588,12 +590,14 @@ public:
         if (l - p < 0) return false;
         return std::log2(raw_scale(l, p)) + std::log2(std::max(1.0, mag)) + kMsgBits < log2q(l) - 1.0;
     }
-    static int vis_npoly(const Ct& c) { return c.lazy ? 2 : c.npoly; }
+    static int vis_npoly(const Ct& c) { return c.lazy ? 2 : c.npoly / c.nb; }
+    static int pm(const Ct& c) { return c.npoly / c.nb; }  // polynomials per batched ciphertext
 
     // key switch of the third polynomial at the data level; keeps pend
     Ct relin_raw(const Ct& c) {
         const int nl = hp_.nl(c.level), n = hp_.n;
-        Ct r = keyswitch(c.data + (size_t)2 * nl * n, c.level, ksk(0), c.data, c.data + (size_t)nl * n);
+        const size_t ms = (size_t)3 * nl * n;  // member stride of a batched tensor
+        Ct r = keyswitch(c.data + (size_t)2 * nl * n, c.level, ksk(0), c.data, c.data + (size_t)nl * n, c.nb, ms, ms);
         r.pend = c.pend;
         r.lazy = c.lazy && c.pend > 0;
         cnt_[C_RELIN]++;
@@ -607,12 +611,12 @@ public:
     Ct normalize(const Ct& c_in, bool need2 = true) {
         Ct cur = ensure_ntt(c_in);
         bool own = cur.data != c_in.data;
-        while (cur.npoly == 3 && cur.pend >= 2) {
+        while (pm(cur) == 3 && cur.pend >= 2) {
             Ct r = rescale(cur);
             if (own) release(cur);
             cur = r, own = true;
         }
-        if (cur.npoly == 3 && (need2 || cur.pend > 0)) {
+        if (pm(cur) == 3 && (need2 || cur.pend > 0)) {
             Ct r = relin_raw(cur);
             if (own) release(cur);
             cur = r, own = true;
@@ -656,8 +660,8 @@ public:
         for (const Ct& c : scratch_) release(c);
         scratch_.clear();
     }
-    Ct zero_ct(int level) {
-        Ct z = alloc_ct(level, 2);
+    Ct zero_ct(int level, int nb = 1) {
+        Ct z = alloc_ct(level, 2 * nb, nb);
         HIP_OK(hipMemsetAsync(z.data, 0, z.words * sizeof(u32), S()));
         z.zero = true;
         return z;
@@ -712,10 +716,11 @@ public:
         Ct o;
         o.level = c.level - 1;
         o.npoly = c.npoly;
+        o.nb = c.nb;
         o.words = (size_t)c.npoly * nlo * hp_.n;
         o.data = drop_limbs(c.data, c.npoly, nl, nl - nlo);
         o.pend = c.pend > 0 ? c.pend - 1 : 0;
-        o.lazy = c.lazy && (o.pend > 0 || o.npoly == 3);
+        o.lazy = c.lazy && (o.pend > 0 || pm(o) == 3);
         o.zero = c.zero;
         cnt_[C_RESCALE]++;
         return o;
@@ -770,7 +775,7 @@ public:
         double ratio = raw_scale(t, p) / raw_scale(c.level, c.pend);
         while (ratio < 16777216.0 && nb + k < na) ratio *= (double)hp_.mod[nb + k], ++k;
         if (!(ratio >= 0.999999 && ratio < 9.0e18)) throw std::runtime_error("level_down: scale ratio out of range");
-        if (c.npoly == 3 && k > 0 && raw_scale(t, p) < 1.0e15) {  // see normalize()
+        if (pm(c) == 3 && k > 0 && raw_scale(t, p) < 1.0e15) {  // see normalize()
             Ct r = relin_raw(c);
             if (own) release(c);
             Ct o = convert(r, t, p);
@@ -785,7 +790,7 @@ public:
         // the first nk limbs of every poly, times the constant (copy fused into the multiply)
         launch_mul_const_half(S(), T_, mid, c.data, const_half(r, r), c.npoly * nk, nk, qmap(), na);
         Ct o;
-        o.level = t, o.npoly = c.npoly, o.pend = p, o.lazy = c.lazy || p > 0, o.zero = c.zero;
+        o.level = t, o.npoly = c.npoly, o.nb = c.nb, o.pend = p, o.lazy = c.lazy || p > 0, o.zero = c.zero;
         o.words = (size_t)c.npoly * nb * n;
         if (k == 0) {
             o.data = mid;
@@ -833,7 +838,8 @@ public:
     // scale would not fit
     Ct add_sub(const Ct& a, const Ct& b, bool sub) {
         cnt_[C_ADD]++;
-        if (sub && a.data == b.data) return zero_ct(a.level - a.pend);
+        if (a.nb != b.nb) throw std::runtime_error("add_sub: batched operands of different sizes");
+        if (sub && a.data == b.data) return zero_ct(a.level - a.pend, a.nb);
         if (b.zero) return copy(a);
         if (a.zero && !sub) return copy(b);
         Ct x = ensure_ntt(a), y = ensure_ntt(b);
@@ -855,7 +861,8 @@ public:
         }
         const int nl = hp_.nl(x.level);
         const int np = std::max(x.npoly, y.npoly);
-        Ct o = alloc_ct(x.level, np);
+        if (x.nb > 1 && x.npoly != y.npoly) throw std::runtime_error("add_sub: batched operands with different polynomial counts");
+        Ct o = alloc_ct(x.level, np, x.nb);
         o.pend = x.pend;
         o.lazy = x.lazy || y.lazy;
         const int common = std::min(x.npoly, y.npoly) * nl;
@@ -891,7 +898,10 @@ public:
         for (int t = 0; t < nl; ++t) d.v[2 * t] = lo[t], d.v[2 * t + 1] = hi[t];
         Ct o = copy(c);
         o.zero = false;
-        launch_add_const_half(S(), T_, o.data, c.data, d, nl, nl, qmap());
+        for (int m = 0; m < c.nb; ++m) {  // the first polynomial of every batched ciphertext
+            const size_t off = (size_t)m * pm(c) * nl * hp_.n;
+            launch_add_const_half(S(), T_, o.data + off, c.data + off, d, nl, nl, qmap());
+        }
         if (c.data != c_in.data) release(c);
         return o;
     }
@@ -937,7 +947,7 @@ public:
             const double f = raw_scale(c.level, c.pend + 1) / raw_scale(c.level, c.pend);
             std::vector<u32> lo, hi;
             scalar_residues(std::llround(re * f), std::llround(im * f), nl, lo, hi);
-            o = alloc_ct(c.level, c.npoly);
+            o = alloc_ct(c.level, c.npoly, c.nb);
             o.pend = c.pend + 1;
             o.lazy = true;
             launch_mul_const_half(S(), T_, o.data, c.data, const_half(lo, hi), c.npoly * nl, nl, qmap());
@@ -947,10 +957,10 @@ public:
             std::vector<u32> lo, hi;
             const double sc = hp_.ptscale[nc.level];
             scalar_residues(std::llround(re * sc), std::llround(im * sc), nl, lo, hi);
-            Ct t = alloc_ct(nc.level, nc.npoly);
+            Ct t = alloc_ct(nc.level, nc.npoly, nc.nb);
             launch_mul_const_half(S(), T_, t.data, nc.data, const_half(lo, hi), nc.npoly * nl, nl, qmap());
             o = rescale(t);
-            o.lazy = c_in.lazy && o.npoly == 3;
+            o.lazy = c_in.lazy && pm(o) == 3;
             release(t);
             if (nc.data != c.data) release(nc);
         }
@@ -987,7 +997,7 @@ public:
         if (allow_lazy && headroom(c.level, c.pend + 1, 1.0)) {
             const int nl = hp_.nl(c.level);
             u32* e = pt_at(p, c.level, 1 + c.pend);
-            o = alloc_ct(c.level, c.npoly);
+            o = alloc_ct(c.level, c.npoly, c.nb);
             o.pend = c.pend + 1;
             o.lazy = true;
             launch_mul_poly(S(), T_, o.data, c.data, e, c.npoly, nl, qmap());
@@ -1144,51 +1154,58 @@ public:
     // ModUp: coefficient form of d, every digit converted to all other limbs of Q*P in one
     // launch, one NTT launch over all converted rows (own limbs skipped: key_inner reads
     // those straight from d).  Returns nd x ne rows (tmp; the caller untmps).
-    u32* modup(const u32* d, int level) {
+    // nb > 1: the d polynomials of nb batched ciphertexts (d + m d_ms words), one launch per
+    // stage for all of them; ext = [m][nd][ne]
+    u32* modup(const u32* d, int level, int nb = 1, size_t d_ms = 0) {
         const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, alpha = hp_.alpha;
         const int nd = (nl + alpha - 1) / alpha;
-        if (alpha > kMaxConvH || np > kMaxConvH || nd > kMaxConvGroups) throw std::runtime_error("keyswitch: digit too large");
+        if (alpha > kMaxConvH || np > kMaxConvH || nb * nd > kMaxConvGroups) throw std::runtime_error("keyswitch: digit too large");
         const LimbMap em = extmap(nl);
-        u32* coef = tmp(nl);
-        intt(coef, d, nl, rows_dense(nl), qmap());
-        u32* ext = tmp((size_t)nd * ne);
+        u32* coef = tmp((size_t)nb * nl);
+        intt(coef, d, nb * nl, RowMap{nl, nb > 1 ? (int)(d_ms / n) : nl, nl, 0, 0}, qmap());
+        u32* ext = tmp((size_t)nb * nd * ne);
         const size_t* toff = &modup_off_[(size_t)nl * hp_.dnum];
         ConvBatch up;
-        up.n = nd;
-        for (int j = 0; j < nd; ++j) {
-            const int lo = j * alpha, h = std::min(alpha, nl - lo);
-            up.h[j] = h, up.d0[j] = lo, up.skip0[j] = lo;
-            up.src[j] = coef + (size_t)lo * n;
-            up.dst[j] = ext + (size_t)j * ne * n;
-            up.tab[j] = d_modup_ + toff[j];
-            up.qhinv[j] = up.tab[j] + (size_t)2 * h * ne;
-            up.negq[j] = up.qhinv[j] + 2 * h;
-        }
+        up.n = nb * nd;
+        for (int m = 0; m < nb; ++m)
+            for (int j = 0; j < nd; ++j) {
+                const int lo = j * alpha, h = std::min(alpha, nl - lo), gi = m * nd + j;
+                up.h[gi] = h, up.d0[gi] = lo, up.skip0[gi] = lo;
+                up.src[gi] = coef + ((size_t)m * nl + lo) * n;
+                up.dst[gi] = ext + (size_t)gi * ne * n;
+                up.tab[gi] = d_modup_ + toff[j];
+                up.qhinv[gi] = up.tab[gi] + (size_t)2 * h * ne;
+                up.negq[gi] = up.qhinv[gi] + 2 * h;
+            }
         launch_base_convert(S(), T_, up, ne, em);
         RowMap xr = rows_dense(ne);
-        xr.skip_alpha = alpha, xr.skip_nl = nl;
-        ntt(ext, ext, nd * ne, xr, em);
-        untmp(coef, nl);
+        xr.skip_alpha = alpha, xr.skip_nl = nl, xr.skip_groups = nd;
+        ntt(ext, ext, nb * nd * ne, xr, em);
+        untmp(coef, (size_t)nb * nl);
         return ext;
     }
     int ext_rows(int level) const { return (hp_.nl(level) + hp_.alpha - 1) / hp_.alpha * (hp_.nl(level) + hp_.n_p); }
     // acc (2 x ne rows, Q*P) = sum_j ext_j * key_j; g != 0 reads ext and d through X -> X^g
-    void key_inner(u32* acc, const u32* ext, const u32* d, const u32* key, int level, u64 g) {
-        const int nl = hp_.nl(level), np = hp_.n_p, ne = nl + np;
+    // nb batched ciphertexts (ext = [m][nd][ne], d + m d_ms, acc = [m][2][ne]) share the key reads
+    void key_inner(u32* acc, const u32* ext, const u32* d, const u32* key, int level, u64 g, int nb = 1, size_t d_ms = 0) {
+        const int nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, n = hp_.n;
         const int nd = (nl + hp_.alpha - 1) / hp_.alpha;
-        launch_key_inner(S(), T_, acc, ext, d, key, nd, ne, nl, hp_.alpha, hp_.n_ks + np, hp_.n_ks, extmap(nl), g);
+        launch_key_inner(S(), T_, acc, ext, d, key, nd, ne, nl, hp_.alpha, hp_.n_ks + np, hp_.n_ks, extmap(nl), g, nb,
+                         (size_t)nd * ne * n, d_ms, (size_t)2 * ne * n);
     }
     // ModDown by P: coefficients of the P rows (read in place from acc), conversion of both
     // polys in one launch, NTT fused with (acc_Q - conv) P^{-1} (+ add)
-    Ct moddown(const u32* acc, int level, const u32* add0, const u32* add1) {
-        const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np;
-        u32* yp = tmp(2 * (size_t)np);
-        intt(yp, acc, 2 * np, RowMap{np, ne, np, nl, 0}, LimbMap{np, hp_.p_off(), 0});
-        u32* conv = tmp(2 * (size_t)nl);
+    // nb batched ciphertexts: acc = [m][2][ne]; member m adds add0/add1 + m add_ms words
+    Ct moddown(const u32* acc, int level, const u32* add0, const u32* add1, int nb = 1, size_t add_ms = 0) {
+        const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, npl = 2 * nb;
+        if (npl > kMaxConvGroups) throw std::runtime_error("moddown: batch too large");
+        u32* yp = tmp((size_t)npl * np);
+        intt(yp, acc, npl * np, RowMap{np, ne, np, nl, 0}, LimbMap{np, hp_.p_off(), 0});
+        u32* conv = tmp((size_t)npl * nl);
         const size_t doff = moddown_off_[nl];
         ConvBatch dn;
-        dn.n = 2;
-        for (int p = 0; p < 2; ++p) {
+        dn.n = npl;
+        for (int p = 0; p < npl; ++p) {
             dn.h[p] = np, dn.d0[p] = hp_.p_off(), dn.skip0[p] = 1 << 30;
             dn.src[p] = yp + (size_t)p * np * n;
             dn.dst[p] = conv + (size_t)p * nl * n;
@@ -1197,22 +1214,25 @@ public:
             dn.negq[p] = d_negp_;
         }
         launch_base_convert(S(), T_, dn, nl, qmap());
-        Ct o = alloc_ct(level, 2);
-        launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_pinv_, add0, add1, 2, nl);
-        cnt_[C_NTT_ROWS] += 2 * (size_t)nl;
-        untmp(yp, 2 * (size_t)np);
-        untmp(conv, 2 * (size_t)nl);
+        Ct o = alloc_ct(level, npl, nb);
+        launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_pinv_, add0, add1, npl, nl, add_ms);
+        cnt_[C_NTT_ROWS] += (size_t)npl * nl;
+        untmp(yp, (size_t)npl * np);
+        untmp(conv, (size_t)npl * nl);
         return o;
     }
-    Ct keyswitch(const u32* d, int level, const u32* key, const u32* add0, const u32* add1) {
+    // key switch of d (nl rows); nb > 1: the d polynomials of nb batched ciphertexts (d + m d_ms
+    // words, add0 / add1 + m add_ms), one key read for all of them -> (c0', c1') per member
+    Ct keyswitch(const u32* d, int level, const u32* key, const u32* add0, const u32* add1, int nb = 1, size_t d_ms = 0,
+                 size_t add_ms = 0) {
         const int ne = hp_.nl(level) + hp_.n_p;
-        u32* ext = modup(d, level);
-        u32* acc = tmp(2 * (size_t)ne);
-        key_inner(acc, ext, d, key, level, 0);
-        untmp(ext, ext_rows(level));
-        Ct o = moddown(acc, level, add0, add1);
-        untmp(acc, 2 * (size_t)ne);
-        cnt_[C_KS]++;
+        u32* ext = modup(d, level, nb, d_ms);
+        u32* acc = tmp(2 * (size_t)ne * nb);
+        key_inner(acc, ext, d, key, level, 0, nb, d_ms);
+        untmp(ext, (size_t)nb * ext_rows(level));
+        Ct o = moddown(acc, level, add0, add1, nb, add_ms);
+        untmp(acc, 2 * (size_t)ne * nb);
+        cnt_[C_KS] += nb;
         return o;
     }
 
@@ -1230,9 +1250,10 @@ public:
         auto xy = align(a, b, fa, fb, true);
         const Ct &x = xy.first, &y = xy.second;
         const int nl = hp_.nl(x.level);
-        Ct d = alloc_ct(x.level, 3);
+        if (x.nb != y.nb) throw std::runtime_error("multiply: batched operands of different sizes");
+        Ct d = alloc_ct(x.level, 3 * x.nb, x.nb);
         d.pend = 1;
-        launch_tensor(S(), T_, d.data, x.data, y.data, nl, qmap());
+        launch_tensor(S(), T_, d.data, x.data, y.data, nl, qmap(), x.nb);
         if (fa) release(x);
         if (fb && y.data != x.data) release(y);
         if (oa) release(a);
@@ -1265,10 +1286,11 @@ public:
         Ct c = normalize(c_in);
         const int nl = hp_.nl(c.level), n = hp_.n;
         const u32* key = ksk(g);
-        u32* perm = tmp(2 * (size_t)nl);
-        launch_automorph(S(), T_, perm, c.data, g, 2 * nl);
-        Ct o = keyswitch(perm + (size_t)nl * n, c.level, key, perm, nullptr);
-        untmp(perm, 2 * (size_t)nl);
+        u32* perm = tmp(2 * (size_t)nl * c.nb);
+        launch_automorph(S(), T_, perm, c.data, g, 2 * nl * c.nb);
+        const size_t ms = (size_t)2 * nl * n;  // member stride of a batched ciphertext
+        Ct o = keyswitch(perm + (size_t)nl * n, c.level, key, perm, nullptr, c.nb, ms, ms);
+        untmp(perm, 2 * (size_t)nl * c.nb);
         if (c.data != c_in.data) release(c);
         return o;
     }
@@ -1571,6 +1593,11 @@ public:
         const int l = in.level, nl = hp_.nl(l), np = hp_.n_p, ne = nl + np, n = hp_.n;
         if (g.B > kMacMax) throw std::runtime_error("lin_group: more than 16 baby steps");
         auto& P = group_pts(G, l);
+        // nb batched ciphertexts (bootstrap_pair): member m at + m qs words; every Q-side
+        // buffer below uses the same member stride qs, the Q*P ones ps, so k_lin_mac reads the
+        // diagonals once for all members
+        const int nb = in.nb;
+        const size_t qs = (size_t)2 * nl * n, ps = (size_t)2 * ne * n;
         const u32* c0 = in.data;
         const u32* c1 = in.data + (size_t)nl * n;
         std::vector<u32*> u(g.B, nullptr), a(g.B, nullptr);
@@ -1578,19 +1605,19 @@ public:
         for (int b = 1; b < g.B; ++b)
             for (int gg = 0; gg < g.G; ++gg) any_baby = any_baby || P[gg][b];
         if (any_baby) {
-            u32* ext = modup(c1, l);
+            u32* ext = modup(c1, l, nb, qs);
             for (int b = 1; b < g.B; ++b) {
                 bool used = false;
                 for (int gg = 0; gg < g.G; ++gg) used = used || P[gg][b];
                 if (!used) continue;
                 const u64 gal = rot_galois(-(int)((long)g.h * b));  // left rotation by h b
-                u[b] = tmp(2 * (size_t)ne);
-                key_inner(u[b], ext, c1, ksk(gal), l, gal);
-                a[b] = tmp(nl);
-                launch_automorph(S(), T_, a[b], c0, gal, nl);
-                cnt_[C_ROT]++;
+                u[b] = tmp(2 * (size_t)ne * nb);
+                key_inner(u[b], ext, c1, ksk(gal), l, gal, nb, qs);
+                a[b] = tmp(2 * (size_t)nl * nb);  // member stride qs, first nl rows used
+                for (int mb = 0; mb < nb; ++mb) launch_automorph(S(), T_, a[b] + mb * qs, c0 + mb * qs, gal, nl);
+                cnt_[C_ROT] += nb;
             }
-            untmp(ext, ext_rows(l));
+            untmp(ext, (size_t)nb * ext_rows(l));
         }
         Ct out;
         bool have = false;
@@ -1600,6 +1627,7 @@ public:
             const int gn = std::min(kLinG, g.G - g0);
             LinMacArgs m{};
             m.B = g.B, m.G = gn, m.c1 = c1;
+            m.nb = nb, m.q_ms = qs, m.p_ms = ps;
             for (int b = 0; b < g.B; ++b) m.a[b] = b == 0 ? c0 : a[b], m.u[b] = b ? u[b] : nullptr;
             bool any[kLinG] = {}, rot[kLinG] = {};
             for (int j = 0; j < gn; ++j) {
@@ -1608,9 +1636,9 @@ public:
                     any[j] = any[j] || P[g0 + j][b];
                     rot[j] = rot[j] || (b && P[g0 + j][b]);
                 }
-                m.out0[j] = tmp(nl);
-                m.out1[j] = P[g0 + j][0] ? tmp(nl) : nullptr;
-                m.outp[j] = rot[j] ? tmp(2 * (size_t)ne) : nullptr;
+                m.out0[j] = tmp(2 * (size_t)nl * nb);  // member stride qs, first nl rows used
+                m.out1[j] = P[g0 + j][0] ? tmp(2 * (size_t)nl * nb) : nullptr;
+                m.outp[j] = rot[j] ? tmp(2 * (size_t)ne * nb) : nullptr;
             }
             launch_lin_mac(S(), T_, m, nl, ne, extmap(nl));
             for (int j = 0; j < gn; ++j) {
@@ -1618,12 +1646,15 @@ public:
                 if (any[j]) {
                     Ct inner;
                     if (rot[j]) {
-                        inner = moddown(m.outp[j], l, m.out0[j], m.out1[j]);
+                        inner = moddown(m.outp[j], l, m.out0[j], m.out1[j], nb, qs);
                     } else {  // only the unrotated diagonal
-                        inner = alloc_ct(l, 2);
-                        HIP_OK(hipMemcpyAsync(inner.data, m.out0[j], (size_t)nl * n * sizeof(u32), hipMemcpyDeviceToDevice, S()));
-                        HIP_OK(hipMemcpyAsync(inner.data + (size_t)nl * n, m.out1[j], (size_t)nl * n * sizeof(u32),
-                                              hipMemcpyDeviceToDevice, S()));
+                        inner = alloc_ct(l, 2 * nb, nb);
+                        for (int mb = 0; mb < nb; ++mb) {
+                            HIP_OK(hipMemcpyAsync(inner.data + mb * qs, m.out0[j] + mb * qs, (size_t)nl * n * sizeof(u32),
+                                                  hipMemcpyDeviceToDevice, S()));
+                            HIP_OK(hipMemcpyAsync(inner.data + mb * qs + (size_t)nl * n, m.out1[j] + mb * qs, (size_t)nl * n * sizeof(u32),
+                                                  hipMemcpyDeviceToDevice, S()));
+                        }
                     }
                     Ct rs = rescale(inner);
                     release(inner);
@@ -1638,14 +1669,14 @@ public:
                         out = s2;
                     }
                 }
-                untmp(m.out0[j], nl);
-                if (m.out1[j]) untmp(m.out1[j], nl);
-                if (m.outp[j]) untmp(m.outp[j], 2 * (size_t)ne);
+                untmp(m.out0[j], 2 * (size_t)nl * nb);
+                if (m.out1[j]) untmp(m.out1[j], 2 * (size_t)nl * nb);
+                if (m.outp[j]) untmp(m.outp[j], 2 * (size_t)ne * nb);
             }
         }
         for (int b = 1; b < g.B; ++b) {
-            if (u[b]) untmp(u[b], 2 * (size_t)ne);
-            if (a[b]) untmp(a[b], nl);
+            if (u[b]) untmp(u[b], 2 * (size_t)ne * nb);
+            if (a[b]) untmp(a[b], 2 * (size_t)nl * nb);
         }
         return out;
     }
@@ -1674,7 +1705,7 @@ public:
         for (size_t k = 1; k < c.size(); ++k) {
             if (c[k] == 0.0) continue;
             const Ct& t = T[k];
-            if (t.npoly != 2 || t.pend != 0 || t.lazy || !t.ntt) return false;
+            if (pm(t) != 2 || t.nb != T[1].nb || t.pend != 0 || t.lazy || !t.ntt) return false;
             ks.push_back((int)k);
             mag += std::fabs(c[k]);
             l = std::min(l, t.level);
@@ -1703,8 +1734,9 @@ public:
         }
         LutChunk ch{};
         for (size_t j = 0; j < ks.size(); ++j) ch.x[j] = T[ks[j]].data, ch.nx[j] = hp_.nl(T[ks[j]].level);
-        Ct o = alloc_ct(l, 2);
-        launch_lut_univariate(S(), T_, o.data, nullptr, ch, (int)ks.size(), it->second, 2, nl);
+        const int nb = T[ks[0]].nb;
+        Ct o = alloc_ct(l, 2 * nb, nb);
+        launch_lut_univariate(S(), T_, o.data, nullptr, ch, (int)ks.size(), it->second, 2 * nb, nl);
         o.pend = 1;
         o.lazy = true;
         if (c[0] != 0.0) {
@@ -1810,32 +1842,65 @@ public:
     // 6 real part, 7 imaginary part, 8 EvalMod(real), 9 EvalMod(imag), 10 recombined, 11 output
     Ct bootstrap(const Ct& in, int stop_after = 99) {
         boot_setup();
-        if (vis_npoly(in) != 2) throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
-        const int n = hp_.n, top = bs_.top;
-        // 1. level 0, then scale delta_0 -> s_bt and drop q1: a single-limb ciphertext mod q0
+        if (vis_npoly(in) != 2 || in.nb != 1) throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
         Ct c = normalize(in);
         Ct z = level_down(c, 0);
         if (c.data != in.data) release(c);
+        return bootstrap_l0(z, stop_after);
+    }
+    // the hi / lo bootstraps of an AES step (MixColumns' final bootstrap) as ONE batched
+    // bootstrap of two stacked ciphertexts: every key switch reads its key, and every linear
+    // transform its diagonals, once for both; half the launches
+    void bootstrap_pair(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob) {
+        boot_setup();
+        if (vis_npoly(a_in) != 2 || vis_npoly(b_in) != 2 || a_in.nb != 1 || b_in.nb != 1)
+            throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
+        const int n = hp_.n, nl0 = hp_.nl(0);
+        Ct z = alloc_ct(0, 4, 2);
+        const Ct* in[2] = {&a_in, &b_in};
+        for (int m = 0; m < 2; ++m) {
+            Ct c = normalize(*in[m]);
+            Ct zm = level_down(c, 0);
+            if (c.data != in[m]->data) release(c);
+            HIP_OK(hipMemcpyAsync(z.data + (size_t)m * 2 * nl0 * n, zm.data, sizeof(u32) * 2 * nl0 * n, hipMemcpyDeviceToDevice, S()));
+            release(zm);
+        }
+        Ct out = bootstrap_l0(z, 99);
+        const int nlo = hp_.nl(out.level);
+        aesfhe_handle* dst[2] = {oa, ob};
+        for (int m = 0; m < 2; ++m) {
+            Ct o = alloc_ct(out.level, 2);
+            o.ntt = out.ntt;
+            HIP_OK(hipMemcpyAsync(o.data, out.data + (size_t)m * 2 * nlo * n, sizeof(u32) * 2 * nlo * n, hipMemcpyDeviceToDevice, S()));
+            *dst[m] = put_ct(o);
+        }
+        release(out);
+    }
+    // z: level-0 ciphertext(s), nb batched members, consumed here
+    Ct bootstrap_l0(Ct z, int stop_after) {
+        const int n = hp_.n, top = bs_.top, nb = z.nb;
+        // 1. scale delta_0 -> s_bt and drop q1: a single-limb ciphertext mod q0
         std::vector<u32> r(2);
         for (int t = 0; t < 2; ++t) r[t] = mod_i64(bs_.k1, hp_.mod[t]);
-        launch_mul_const_half(S(), T_, z.data, z.data, const_half(r, r), 4, 2, qmap());
+        launch_mul_const_half(S(), T_, z.data, z.data, const_half(r, r), 2 * z.npoly, 2, qmap());
         Ct b = rescale(z, true);
         release(z);
         if (stop_after == 1) return b;
         // 2. sparse-secret encapsulation: dense s -> sparse s_sp at modulus q0
-        Ct sp = keyswitch(b.data + n, -1, ksk(tag_d2s()), b.data, nullptr);
+        Ct sp = keyswitch(b.data + n, -1, ksk(tag_d2s()), b.data, nullptr, nb, 2 * (size_t)n, 2 * (size_t)n);
         release(b);
         if (stop_after == 2) return sp;
         // 3. ModRaise: centred lift of both polynomials to every limb of the top level
-        intt(sp.data, 2, 1, single(0));
-        Ct raised = alloc_ct(top, 2);
-        launch_rescale_spread(S(), T_, raised.data, sp.data, 2, hp_.nl(top), hp_.mod[0]);
+        intt(sp.data, 2 * nb, 1, single(0));
+        Ct raised = alloc_ct(top, 2 * nb, nb);
+        launch_rescale_spread(S(), T_, raised.data, sp.data, 2 * nb, hp_.nl(top), hp_.mod[0]);
         release(sp);
         const int nlt = hp_.nl(top);
-        ntt(raised.data, 2 * nlt, nlt, qmap());
+        ntt(raised.data, 2 * nb * nlt, nlt, qmap());
         if (stop_after == 3) return raised;
         // 4. back to the dense secret
-        Ct u = keyswitch(raised.data + (size_t)nlt * n, top, ksk(tag_s2d()), raised.data, nullptr);
+        const size_t tms = (size_t)2 * nlt * n;
+        Ct u = keyswitch(raised.data + (size_t)nlt * n, top, ksk(tag_s2d()), raised.data, nullptr, nb, tms, tms);
         release(raised);
         if (stop_after == 4) return u;
         // 5. CoeffToSlot (bit-reversed coefficient halves / (2 q0 K))
@@ -1868,7 +1933,7 @@ public:
         // 8. SlotToCoeff (scaled back to the message)
         Ct out = lin_transform(wp, bs_.stc);
         release(wp);
-        cnt_[C_BOOT]++;
+        cnt_[C_BOOT] += nb;
         return out;
     }
 
@@ -2376,6 +2441,13 @@ int aesfhe_power_basis(aesfhe_ctx* ctx, aesfhe_handle c, int degree, aesfhe_hand
 int aesfhe_to_ntt(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.to_ntt(e.canon(c))) }
 int aesfhe_to_intt(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.to_intt(e.canon(c))) }
 int aesfhe_bootstrap(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.bootstrap(e.canon(c))) }
+int aesfhe_bootstrap_pair(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, aesfhe_handle* out_a, aesfhe_handle* out_b) {
+    API_BEGIN Engine& e = *ctx->eng;
+    const Ct& ca = e.canon(a);
+    const Ct& cb = e.canon(b);
+    e.bootstrap_pair(ca, cb, out_a, out_b);
+    API_END
+}
 int aesfhe_bootstrap_depth(void) { return Engine::boot_depth(); }
 int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle c, int stage, aesfhe_handle* out) { CT_OP(e.bootstrap(e.canon(c), stage)) }
 int aesfhe_debug_lin_group(aesfhe_ctx* ctx, aesfhe_handle c, int which, aesfhe_handle* out) {

@@ -60,10 +60,11 @@ struct DevTables {
 // launch row y -> group g = y / cnt, index i = y % cnt (the limb index fed to LimbMap);
 // source row = src_off + g * src_stride + i, destination row = dst_off + g * dst_stride + i
 // skip_alpha > 0 (forward only): rows with i < skip_nl and i / skip_alpha == g are left
-// untouched (ModUp: a digit's own limbs)
+// untouched (ModUp: a digit's own limbs); skip_groups > 0: g taken mod skip_groups (the
+// digits of several batched ciphertexts in one launch)
 struct RowMap {
     int cnt, src_stride, dst_stride, src_off, dst_off;
-    int skip_alpha = 0, skip_nl = 0;
+    int skip_alpha = 0, skip_nl = 0, skip_groups = 0;
 };
 inline RowMap rows_dense(int nl) { return RowMap{nl, nl, nl, 0, 0}; }
 // fused prologue / epilogue operands of the forward NTT (ntt.hip)
@@ -71,8 +72,9 @@ struct NttAux {
     const u32* cur = nullptr;  // finish: rows g * cur_stride + i
     u32* out = nullptr;        // finish: rows g * out_stride + i
     const u32* qinv = nullptr; // finish: [i] Shoup pairs
-    const u32* add0 = nullptr; // finish: optional addend rows for group 0 / 1
-    const u32* add1 = nullptr;
+    const u32* add0 = nullptr; // finish: optional addend rows for group 0 / 1 (even / odd groups
+    const u32* add1 = nullptr; //   when batched: group 2 m + p adds add_p + m * add_mstride words)
+    size_t add_mstride = 0;
     int cur_stride = 0, out_stride = 0;
     u32 q_last = 0;            // spread: modulus of the source row
     u32 q_last2 = 0;           // spread2: second dropped prime (source rows a, b per group)
@@ -92,8 +94,9 @@ void launch_rescale2_ntt(hipStream_t st, const DevTables& T, u32* out, const u32
                          int npoly, int nt, int nl_in, u32 qa, u32 qb, u32 qa_inv, u32 qa_inv_p);
 // NTT of conv (npoly x nt dense rows, destroyed) fused with
 // out[p][t] = (cur[p * cur_stride + t] - NTT(conv)[p][t]) * qinv_t (+ add_p[t])   (ModDown)
+// npoly = 2 nb for nb batched ciphertexts: group 2 m + p adds add_p + m add_mstride (words)
 void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, const u32* cur, int cur_stride, const u32* qinv,
-                       const u32* add0, const u32* add1, int npoly, int nt);
+                       const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride = 0);
 // in place on rows = npoly * nl dense rows
 void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map);
 void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map);
@@ -103,7 +106,8 @@ void launch_add(hipStream_t st, const DevTables& T, u32* out, const u32* a, cons
 void launch_sub(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int rows, int nl, LimbMap map);
 void launch_neg(hipStream_t st, const DevTables& T, u32* out, const u32* a, int rows, int nl, LimbMap map);
 // out = (a0 b0, a0 b1 + a1 b0, a1 b1); a, b: 2 x nl rows; out: 3 x nl rows
-void launch_tensor(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int nl, LimbMap map);
+// nb > 1: nb ciphertexts stacked ([m][2][nl] in, [m][3][nl] out), one launch
+void launch_tensor(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int nl, LimbMap map, int nb = 1);
 // out = in * pt (pt: nl rows), npoly polys
 void launch_mul_poly(hipStream_t st, const DevTables& T, u32* out, const u32* in, const u32* pt, int npoly, int nl, LimbMap map);
 // out = a + b*c  (b, c: rows; used for decryption and encryption)
@@ -138,7 +142,7 @@ void launch_rescale_spread(hipStream_t st, const DevTables& T, u32* v, const u32
 // [skip0, skip0 + h) are skipped (the digit's own limbs; 1 << 30 = none).
 // tab: [h][nt] Shoup pairs of (qhat_i mod t); qhinv: [h] Shoup pairs of qhat_i^{-1} mod q_i;
 // negq: [nt] values of (-Q mod t), Q = prod of the h source primes (centred conversion)
-constexpr int kMaxConvGroups = 8;
+constexpr int kMaxConvGroups = 16;  // ModUp digits (or ModDown polys) x batched ciphertexts
 constexpr int kMaxConvH = 16;
 struct ConvBatch {
     int n = 0;
@@ -154,8 +158,12 @@ void launch_base_convert(hipStream_t st, const DevTables& T, const ConvBatch& cb
 // own limbs (x < nl, x / alpha == j) where e_j = d (the NTT-form input);
 // ext: [nd][ne][N]; key: [dnum][2][nkey][N]
 // g != 0: ext and d are read through the automorphism X -> X^g (hoisted rotation)
+// nb > 1: nb ciphertexts' key switches with the SAME key in one launch (the key is read once
+// per residue for all of them); member m uses ext + m ext_ms, d + m d_ms, acc + m acc_ms (words)
+constexpr int kMaxKsBatch = 4;
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
-                      int alpha, int nkey, int nks, LimbMap map, u64 g = 0);
+                      int alpha, int nkey, int nks, LimbMap map, u64 g = 0, int nb = 1, size_t ext_ms = 0, size_t d_ms = 0,
+                      size_t acc_ms = 0);
 // out[p][t] = sum_j x_j[p][t] pt_j[t] over rows t < rows, polys p < npoly (x poly stride xs,
 // out poly stride os, in words)
 constexpr int kMacMax = 16;
@@ -173,6 +181,8 @@ void launch_mac(hipStream_t st, const DevTables& T, u32* out, const MacTerms& m,
 // Each input residue is read once for all giant steps (the per-giant k_mac re-read every
 // rotated baby step and every diagonal twice).  Null pointers mark absent terms.
 constexpr int kLinB = 16, kLinG = 4;
+// nb > 1 batched ciphertexts share the diagonals: member m's a / c1 / out0 / out1 are at
+// + m * q_ms words, its u / outp at + m * p_ms words
 struct LinMacArgs {
     const u32* a[kLinB];
     const u32* u[kLinB];
@@ -182,6 +192,8 @@ struct LinMacArgs {
     u32* out1[kLinG];
     u32* outp[kLinG];
     int B, G;
+    int nb = 1;
+    size_t q_ms = 0, p_ms = 0;
 };
 void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int nl, int ne, LimbMap map);
 

@@ -75,8 +75,13 @@ __global__ void k_mul_poly(u32* out, const u32* in, const u32* pt, int nl, LimbM
     out[idx] = barrett_mul(in[idx], pt[pidx], P.q, P.mu);
 }
 __global__ void k_tensor(u32* out, const u32* a, const u32* b, int nl, LimbMap map, const PrimeConst* pc, int logn) {
-    EW_PROLOGUE  // row < nl here
-    const size_t off = (size_t)nl << logn;
+    // row = m * nl + limb: ciphertext m of a stacked batch ([m][2][nl] in, [m][3][nl] out)
+    const int row = blockIdx.y;
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const int m = row / nl, limb = row - m * nl;
+    const PrimeConst P = pc[map.prime(limb)];
+    const size_t off = (size_t)nl << logn, idx = ((size_t)limb << logn) + k;
+    a += (size_t)m * 2 * off, b += (size_t)m * 2 * off, out += (size_t)m * 3 * off;
     const u32 q = P.q, mu = P.mu;
     u32 a0 = a[idx], a1 = a[idx + off], b0 = b[idx], b1 = b[idx + off];
     out[idx] = barrett_mul(a0, b0, q, mu);
@@ -224,7 +229,8 @@ __device__ __forceinline__ u32 galois_src(u32 i, u64 g, int logn) {
 // g != 0: the inputs (ext and d) are read through the automorphism X -> X^g -- a hoisted
 // rotation: one ModUp of c1 serves every rotation of the same ciphertext
 __global__ void k_key_inner(u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl, int alpha, int nkey, int nks,
-                            u64 g, LimbMap map, const PrimeConst* pc, int logn, unsigned long long* ts) {
+                            u64 g, LimbMap map, const PrimeConst* pc, int logn, int nb, size_t ext_ms, size_t d_ms, size_t acc_ms,
+                            unsigned long long* ts) {
     ts_begin(ts);
     const int x = blockIdx.y;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
@@ -232,18 +238,32 @@ __global__ void k_key_inner(u32* acc, const u32* ext, const u32* d, const u32* k
     const PrimeConst P = pc[map.prime(x)];
     const int krow = x < nl ? x : nks + (x - nl);
     const int own = x < nl ? x / alpha : -1;
-    // 64-bit multiply-adds (operands < q < 2^32/3: eight products fit), folded every 8 digits
-    u64 s0 = 0, s1 = 0;
+    // 64-bit multiply-adds (operands < q < 2^32/3: eight products fit), folded every 8 digits;
+    // the key residues are loaded once for every batched ciphertext
+    u64 s0[kMaxKsBatch] = {}, s1[kMaxKsBatch] = {};
     for (int j = 0; j < nd; ++j) {
-        if (j && (j & 7) == 0) s0 = fold64(s0, P.q, P.r32), s1 = fold64(s1, P.q, P.r32);
-        const u32 e = j == own ? d[((size_t)x << logn) + ks] : ext[(((size_t)j * ne + x) << logn) + ks];
+        if (j && (j & 7) == 0) {
+#pragma unroll
+            for (int m = 0; m < kMaxKsBatch; ++m)
+                if (m < nb) s0[m] = fold64(s0[m], P.q, P.r32), s1[m] = fold64(s1[m], P.q, P.r32);
+        }
         const u32* kb = key + (((size_t)j * 2 * nkey + krow) << logn) + k;
         const u32* ka = kb + ((size_t)nkey << logn);
-        s0 += (u64)e * *kb;
-        s1 += (u64)e * *ka;
+        const u64 vb = *kb, va = *ka;
+#pragma unroll
+        for (int m = 0; m < kMaxKsBatch; ++m) {
+            if (m >= nb) break;
+            const u32 e = j == own ? d[m * d_ms + ((size_t)x << logn) + ks] : ext[m * ext_ms + (((size_t)j * ne + x) << logn) + ks];
+            s0[m] += e * vb;
+            s1[m] += e * va;
+        }
     }
-    acc[((size_t)x << logn) + k] = reduce64(s0, P.q, P.mu, P.r32);
-    acc[(((size_t)ne + x) << logn) + k] = reduce64(s1, P.q, P.mu, P.r32);
+#pragma unroll
+    for (int m = 0; m < kMaxKsBatch; ++m) {
+        if (m >= nb) break;
+        acc[m * acc_ms + ((size_t)x << logn) + k] = reduce64(s0[m], P.q, P.mu, P.r32);
+        acc[m * acc_ms + (((size_t)ne + x) << logn) + k] = reduce64(s1[m], P.q, P.mu, P.r32);
+    }
     ts_end(ts);
 }
 
@@ -621,8 +641,9 @@ void launch_neg(hipStream_t st, const DevTables& T, u32* out, const u32* a, int 
 void launch_square(hipStream_t st, const DevTables& T, u32* out, const u32* a, int rows, int nl, LimbMap map) {
     prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows), k_square, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, nl, map, T.pc, T.logn);
 }
-void launch_tensor(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int nl, LimbMap map) {
-    prof_launch(KID_TENSOR, words(7.0 * nl * (1u << T.logn)), k_tensor, ew_grid(T.logn, nl), dim3(kBlock), 0, st, out, a, b, nl, map, T.pc, T.logn);
+void launch_tensor(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int nl, LimbMap map, int nb) {
+    prof_launch(KID_TENSOR, words(7.0 * nb * nl * (1u << T.logn)), k_tensor, ew_grid(T.logn, nb * nl), dim3(kBlock), 0, st, out, a, b, nl,
+                map, T.pc, T.logn);
 }
 void launch_mul_poly(hipStream_t st, const DevTables& T, u32* out, const u32* in, const u32* pt, int npoly, int nl, LimbMap map) {
     prof_launch(KID_ELEMENTWISE, EW_BYTES((2.0 * npoly + 1.0) * nl), k_mul_poly, ew_grid(T.logn, npoly * nl), dim3(kBlock), 0, st, out, in, pt, nl, map, T.pc, T.logn);
@@ -677,51 +698,72 @@ __global__ void k_mac(u32* out, MacTerms m, size_t xs, size_t os, LimbMap map, c
     }
     out[p * os + at] = reduce64(acc, P.q, P.mu, P.r32);
 }
-// see launch_lin_mac (kernels.h); grid (N / 256, ne rows)
+// see launch_lin_mac (kernels.h); grid (N / 256, ne rows, nb batched ciphertexts).  The
+// diagonals are read once per residue and applied to every batched ciphertext (member loop
+// inside the thread); kLinG x 3 accumulators per member.
+template <int NB>
+__device__ __forceinline__ void lin_mac_body(const LinMacArgs& m, int nl, int ne, const PrimeConst& P, int t, size_t k, int logn) {
+    const bool qrow = t < nl;
+    const size_t at = ((size_t)t << logn) + k;
+    const size_t po = (size_t)ne << logn;  // poly stride of u / outp
+    u64 acc0[NB][kLinG], ap0[NB][kLinG], ap1[NB][kLinG];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+        for (int g = 0; g < kLinG; ++g) acc0[b][g] = ap0[b][g] = ap1[b][g] = 0;
+    for (int j = 0; j < m.B; ++j) {
+        if (j && (j & 7) == 0) {
+#pragma unroll
+            for (int b = 0; b < NB; ++b)
+#pragma unroll
+                for (int g = 0; g < kLinG; ++g) {
+                    acc0[b][g] = fold64(acc0[b][g], P.q, P.r32);
+                    ap0[b][g] = fold64(ap0[b][g], P.q, P.r32);
+                    ap1[b][g] = fold64(ap1[b][g], P.q, P.r32);
+                }
+        }
+        u32 av[NB], u0[NB], u1[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            av[b] = (qrow && m.a[j]) ? m.a[j][b * m.q_ms + at] : 0u;
+            u0[b] = u1[b] = 0;
+            if (m.u[j]) u0[b] = m.u[j][b * m.p_ms + at], u1[b] = m.u[j][b * m.p_ms + po + at];
+        }
+#pragma unroll
+        for (int g = 0; g < kLinG; ++g) {
+            if (g >= m.G || !m.pt[g][j]) continue;
+            const u32 pv = m.pt[g][j][at];
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                acc0[b][g] += (u64)av[b] * pv;  // q < 2^32 / 3: 8 products fit beside a folded accumulator
+                ap0[b][g] += (u64)u0[b] * pv;
+                ap1[b][g] += (u64)u1[b] * pv;
+            }
+        }
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const u32 c1v = qrow ? m.c1[b * m.q_ms + at] : 0u;
+#pragma unroll
+        for (int g = 0; g < kLinG; ++g) {
+            if (g >= m.G) continue;
+            if (qrow) {
+                m.out0[g][b * m.q_ms + at] = reduce64(acc0[b][g], P.q, P.mu, P.r32);
+                if (m.out1[g]) m.out1[g][b * m.q_ms + at] = reduce64((u64)c1v * m.pt[g][0][at], P.q, P.mu, P.r32);
+            }
+            if (m.outp[g]) {
+                m.outp[g][b * m.p_ms + at] = reduce64(ap0[b][g], P.q, P.mu, P.r32);
+                m.outp[g][b * m.p_ms + po + at] = reduce64(ap1[b][g], P.q, P.mu, P.r32);
+            }
+        }
+    }
+}
+template <int NB>
 __global__ void __launch_bounds__(kBlock) k_lin_mac(LinMacArgs m, int nl, int ne, LimbMap map, const PrimeConst* pc, int logn) {
     const int t = blockIdx.y;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const PrimeConst P = pc[map.prime(t)];
-    const bool qrow = t < nl;
-    const size_t at = ((size_t)t << logn) + k;
-    const size_t po = (size_t)ne << logn;  // poly stride of u / outp
-    u64 acc0[kLinG], ap0[kLinG], ap1[kLinG];
-#pragma unroll
-    for (int g = 0; g < kLinG; ++g) acc0[g] = ap0[g] = ap1[g] = 0;
-    for (int b = 0; b < m.B; ++b) {
-        if (b && (b & 7) == 0) {
-#pragma unroll
-            for (int g = 0; g < kLinG; ++g) {
-                acc0[g] = fold64(acc0[g], P.q, P.r32);
-                ap0[g] = fold64(ap0[g], P.q, P.r32);
-                ap1[g] = fold64(ap1[g], P.q, P.r32);
-            }
-        }
-        const u32 av = (qrow && m.a[b]) ? m.a[b][at] : 0u;
-        u32 u0 = 0, u1 = 0;
-        if (m.u[b]) u0 = m.u[b][at], u1 = m.u[b][po + at];
-#pragma unroll
-        for (int g = 0; g < kLinG; ++g) {
-            if (g >= m.G || !m.pt[g][b]) continue;
-            const u32 pv = m.pt[g][b][at];
-            acc0[g] += (u64)av * pv;  // q < 2^32 / 3: 8 products fit beside a folded accumulator
-            ap0[g] += (u64)u0 * pv;
-            ap1[g] += (u64)u1 * pv;
-        }
-    }
-    const u32 c1v = qrow ? m.c1[at] : 0u;
-#pragma unroll
-    for (int g = 0; g < kLinG; ++g) {
-        if (g >= m.G) continue;
-        if (qrow) {
-            m.out0[g][at] = reduce64(acc0[g], P.q, P.mu, P.r32);
-            if (m.out1[g]) m.out1[g][at] = reduce64((u64)c1v * m.pt[g][0][at], P.q, P.mu, P.r32);
-        }
-        if (m.outp[g]) {
-            m.outp[g][at] = reduce64(ap0[g], P.q, P.mu, P.r32);
-            m.outp[g][po + at] = reduce64(ap1[g], P.q, P.mu, P.r32);
-        }
-    }
+    lin_mac_body<NB>(m, nl, ne, P, t, k, logn);
 }
 }  // namespace
 
@@ -736,8 +778,17 @@ void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int
     }
     reads += nl;  // c1
     for (int g = 0; g < m.G; ++g) writes += nl + (m.out1[g] ? nl : 0) + (m.outp[g] ? 2.0 * ne : 0);
-    prof_launch(KID_ELEMENTWISE, words((reads + writes) * (1u << T.logn)), k_lin_mac, ew_grid(T.logn, ne), dim3(kBlock), 0, st, m, nl, ne,
-                map, T.pc, T.logn);
+    double shared = 0;  // the diagonals, read once for every batched ciphertext
+    for (int b = 0; b < m.B; ++b)
+        for (int g = 0; g < m.G; ++g)
+            if (m.pt[g][b]) shared += ne;
+    const double bytes = words((m.nb * (reads - shared + writes) + shared) * (1u << T.logn));
+    if (m.nb == 1)
+        prof_launch(KID_ELEMENTWISE, bytes, k_lin_mac<1>, ew_grid(T.logn, ne), dim3(kBlock), 0, st, m, nl, ne, map, T.pc, T.logn);
+    else if (m.nb == 2)
+        prof_launch(KID_ELEMENTWISE, bytes, k_lin_mac<2>, ew_grid(T.logn, ne), dim3(kBlock), 0, st, m, nl, ne, map, T.pc, T.logn);
+    else
+        throw std::runtime_error("launch_lin_mac: 1 or 2 batched ciphertexts");
 }
 
 void launch_mac(hipStream_t st, const DevTables& T, u32* out, const MacTerms& m, size_t xs, size_t os, int rows, int npoly, LimbMap map) {
@@ -747,10 +798,11 @@ void launch_mac(hipStream_t st, const DevTables& T, u32* out, const MacTerms& m,
 }
 
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
-                      int alpha, int nkey, int nks, LimbMap map, u64 g) {
-    // ext/d (nd x ne) + key (nd x 2 x ne) read, acc (2 x ne) written
-    prof_launch_ts(KID_KEY_INNER, words((3.0 * nd + 2.0) * ne * (1u << T.logn)), k_key_inner, ew_grid(T.logn, ne), dim3(kBlock), 0, st, acc,
-                ext, d, key, nd, ne, nl, alpha, nkey, nks, g, map, T.pc, T.logn);
+                      int alpha, int nkey, int nks, LimbMap map, u64 g, int nb, size_t ext_ms, size_t d_ms, size_t acc_ms) {
+    if (nb < 1 || nb > kMaxKsBatch) throw std::runtime_error("launch_key_inner: 1..4 batched ciphertexts");
+    // per ciphertext ext/d (nd x ne) read and acc (2 x ne) written; the key (nd x 2 x ne) once
+    prof_launch_ts(KID_KEY_INNER, words((nb * (nd + 2.0) + 2.0 * nd) * ne * (1u << T.logn)), k_key_inner, ew_grid(T.logn, ne), dim3(kBlock),
+                   0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g, map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms);
 }
 void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, u64 seed, u64 stream, int kind) {
     prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_small, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, nl, map, seed, stream, kind, T.pc,

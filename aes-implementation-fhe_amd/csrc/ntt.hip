@@ -50,7 +50,9 @@ enum { kPlain = 0, kSpread = 1, kFinish = 1, kSpread2 = 2 };
 // transformed (they are already in NTT form in the input); block-uniform early exit
 __device__ __forceinline__ bool skipped(const RowMap& rm) {
     if (rm.skip_alpha <= 0) return false;
-    const int g = blockIdx.y / rm.cnt, i = blockIdx.y - g * rm.cnt;
+    int g = blockIdx.y / rm.cnt;
+    const int i = blockIdx.y - g * rm.cnt;
+    if (rm.skip_groups > 0) g %= rm.skip_groups;
     return i < rm.skip_nl && i / rm.skip_alpha == g;
 }
 
@@ -208,7 +210,8 @@ __global__ void __launch_bounds__(kThreads) k_ntt2_fwd(u32* data, RowMap rm, Lim
         const int grp = blockIdx.y / rm.cnt, li = blockIdx.y - grp * rm.cnt;
         const size_t woff = (size_t)R * 256 + 16 * j;
         const uint4* cu = reinterpret_cast<const uint4*>(aux.cur + ((size_t)(grp * aux.cur_stride + li) << LOGN) + woff);
-        const u32* addp = grp == 0 ? aux.add0 : aux.add1;
+        const u32* addp = (grp & 1) ? aux.add1 : aux.add0;
+        if (grp > 1) addp = (addp && aux.add_mstride) ? addp + (grp >> 1) * aux.add_mstride : nullptr;
         const uint4* ad = addp ? reinterpret_cast<const uint4*>(addp + ((size_t)li << LOGN) + woff) : nullptr;
         uint4* o = reinterpret_cast<uint4*>(aux.out + ((size_t)(grp * aux.out_stride + li) << LOGN) + woff);
         const u32 qi = aux.qinv[2 * li], qip = aux.qinv[2 * li + 1];
@@ -380,7 +383,7 @@ void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* dst, const u32* src
     if (rm.skip_alpha > 0)
         for (int y = 0; y < rows; ++y) {
             const int g = y / rm.cnt, i = y - g * rm.cnt;
-            if (i < rm.skip_nl && i / rm.skip_alpha == g) --io_rows;
+            if (i < rm.skip_nl && i / rm.skip_alpha == (rm.skip_groups > 0 ? g % rm.skip_groups : g)) --io_rows;
         }
     ntt_fwd_dispatch<kPlain, kPlain>(st, T, dst, src, rows, io_rows, rm, map, NttAux{});
 }
@@ -400,9 +403,10 @@ void launch_rescale2_ntt(hipStream_t st, const DevTables& T, u32* out, const u32
     ntt_fwd_dispatch<kSpread2, kFinish>(st, T, v, last, npoly * nt, npoly * nt, rm, LimbMap{1 << 30, 0, 0}, aux);
 }
 void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, const u32* cur, int cur_stride, const u32* qinv,
-                       const u32* add0, const u32* add1, int npoly, int nt) {
+                       const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride) {
     NttAux aux{};
     aux.cur = cur, aux.out = out, aux.qinv = qinv, aux.cur_stride = cur_stride, aux.out_stride = nt, aux.add0 = add0, aux.add1 = add1;
+    aux.add_mstride = add_mstride;
     ntt_fwd_dispatch<kPlain, kFinish>(st, T, conv, conv, npoly * nt, npoly * nt, rows_dense(nt), LimbMap{1 << 30, 0, 0}, aux);
 }
 void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {

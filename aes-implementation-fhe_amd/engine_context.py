@@ -125,6 +125,16 @@ class EngineContext:
         self._bs_total_s += time.perf_counter() - t0
         return out
 
+    def bootstrap_pair(self, a, b):
+        """(bootstrap(a), bootstrap(b)) as one batched bootstrap of two stacked ciphertexts
+        (engine-side: each key switch reads its key, each linear transform its diagonals once
+        for both); the same results as two bootstrap calls"""
+        t0 = time.perf_counter()
+        out = self.engine.bootstrap_pair(a, b)
+        self._bs_count += 2
+        self._bs_total_s += time.perf_counter() - t0
+        return out
+
     def bootstrap_stats(self):
         n = self._bs_count
         return {"count": n, "total_s": self._bs_total_s, "avg_s": self._bs_total_s / n if n else 0.0}

@@ -10,7 +10,7 @@ from mixcol_final import _CoeffCache, gf_basis16, gf_eval, gf_mult_pair
 from shift_rows import row_masks
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT
-from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, pair
+from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap2, pair
 
 
 class InvMixColumnsFHE:
@@ -90,6 +90,6 @@ class InvMixColumnsFHE:
         out = self._renorm_pair(*pair(self.ctx, lambda: self._xor(acc[0], e9[0], fl), lambda: self._xor(acc[1], e9[1], fl)),
                                 level=NEED_BOOTSTRAP if do_final_bootstrap else None)
         if do_final_bootstrap:
-            out = pair(self.ctx, lambda: self.ctx.bootstrap(out[0]), lambda: self.ctx.bootstrap(out[1]))
+            out = bootstrap2(self.ctx, out[0], out[1])
         log("out", out)
         return out

@@ -35,7 +35,7 @@ EXPORTED = [
     "aesfhe_level", "aesfhe_plaintext", "aesfhe_encrypt", "aesfhe_decrypt", "aesfhe_add", "aesfhe_sub",
     "aesfhe_add_pt", "aesfhe_add_scalar", "aesfhe_mul_scalar", "aesfhe_mul_pt", "aesfhe_mul",
     "aesfhe_relinearize", "aesfhe_rescale", "aesfhe_level_down", "aesfhe_rotate", "aesfhe_conjugate",
-    "aesfhe_power_basis", "aesfhe_to_ntt", "aesfhe_to_intt", "aesfhe_bootstrap", "aesfhe_renorm_pair", "aesfhe_renorm_states", "aesfhe_renorm_at",
+    "aesfhe_power_basis", "aesfhe_to_ntt", "aesfhe_to_intt", "aesfhe_bootstrap", "aesfhe_bootstrap_pair", "aesfhe_renorm_pair", "aesfhe_renorm_states", "aesfhe_renorm_at",
     "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
     "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
     "aesfhe_streams", "aesfhe_bind_stream", "aesfhe_fork", "aesfhe_join", "aesfhe_settle",
@@ -43,6 +43,9 @@ EXPORTED = [
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_lut_create", "aesfhe_lut_eval",
 ]
+
+# largest log2(PQ) for 128-bit classical security with a ternary secret (HE standard)
+SECURITY_LOG_PQ_128 = {13: 218, 14: 438, 15: 881, 16: 1772, 17: 3544}
 
 KERNEL_IDS = ["ntt_cols_fwd", "ntt_rows_fwd", "ntt_rows_inv", "ntt_cols_inv", "base_convert", "key_inner",
               "moddown", "tensor", "rescale", "automorph", "elementwise", "sample"]
@@ -83,6 +86,7 @@ def load_library(path: Optional[Path] = None):
         "aesfhe_conjugate": [vp, _H, _Hp], "aesfhe_power_basis": [vp, _H, c_int, _Hp],
         "aesfhe_to_ntt": [vp, _H, _Hp], "aesfhe_to_intt": [vp, _H, _Hp], "aesfhe_bootstrap": [vp, _H, _Hp],
         "aesfhe_renorm_pair": [vp, _H, _H, _Hp, _Hp],
+        "aesfhe_bootstrap_pair": [vp, _H, _H, _Hp, _Hp],
         "aesfhe_renorm_states": [vp, _H, _H, c_int, _Hp, _Hp],
         "aesfhe_renorm_at": [vp, _H, _H, c_int, c_int, _Hp, _Hp],
         "aesfhe_export": [vp, _H, _up, ctypes.c_uint64], "aesfhe_import": [vp, c_int, c_int, _up, _Hp],
@@ -244,15 +248,18 @@ class Engine:
 
     def __init__(self, *, mode: str = "gpu", use_bootstrap: bool = False, use_multiparty: bool = False,
                  thread_count: int = 0, device_id: int = 0, max_level: int = 17, log_n: int = 16,
-                 dnum: int | None = None, seed: int = 0x5EED, lazy: bool = True, concurrent: bool = True):
+                 dnum: int | None = None, seed: int = 0x5EED, lazy: bool = True, concurrent: bool = True,
+                 allow_insecure: bool = False):
         if use_multiparty:
             raise ValueError("multiparty key generation is not supported")
         self.mode = mode
         self.use_bootstrap = use_bootstrap
         # bootstrappable set: the chain is extended by the bootstrap depth above the fresh level;
-        # more key-switching digits there keep log2(PQ) under the 128-bit bound (1772 at N=2^16)
+        # 5 key-switching digits there (alpha = 9, 10 special primes, log2 PQ = 1699) keep log2 PQ
+        # under the 128-bit bound (1772 at N = 2^16); 4 digits would cross it (1790), 6 cost
+        # ~5 % more time (more ModUp rows per key switch)
         if dnum is None:
-            dnum = 6 if use_bootstrap else 3
+            dnum = int(os.environ.get("AESFHE_BOOT_DNUM", "5")) if use_bootstrap else 3
         self._ctx = _Context(log_n, max_level, dnum, device_id, seed, bootstrappable=use_bootstrap)
         L = self._ctx.lib
         self.fresh_level = max_level
@@ -264,6 +271,12 @@ class Engine:
         limbs = np.zeros(self.L + 1, np.int32)
         self._ctx.check(L.aesfhe_level_limbs(self._ctx.ptr, limbs))
         self.level_limbs = [int(x) for x in limbs]
+        # 128-bit security (HE standard, ternary secret): log2(PQ) bound per ring dimension
+        self.log_pq = float(np.log2(self.moduli().astype(np.float64)).sum())
+        bound = SECURITY_LOG_PQ_128.get(self.log_n)
+        if bound is not None and self.log_pq > bound and not allow_insecure:
+            raise ValueError(f"parameter set above the 128-bit security bound: log2(PQ) = {self.log_pq:.1f} > {bound} "
+                             f"at N = 2^{self.log_n} (allow_insecure=True for test-only sets)")
         self._keys_ready = False
         # AESFHE_PROFILE_FROM_START=kid,kid: engine kernel accounting from the first launch on
         # (key generation included), to match whole-process rocprofv3 --pmc totals (tools/ks_probe.py)
@@ -436,6 +449,12 @@ class Engine:
 
     def bootstrap(self, ct, relinearization_key=None, conjugation_key=None, bootstrap_key=None):
         return self._new(self._lib.aesfhe_bootstrap, ct.handle)
+
+    def bootstrap_pair(self, a, b):
+        """bootstrap(a), bootstrap(b) as one batched bootstrap (shared key / diagonal reads)"""
+        x, y = ctypes.c_uint64(), ctypes.c_uint64()
+        self._ctx.check(self._lib.aesfhe_bootstrap_pair(self._ctx.ptr, a.handle, b.handle, ctypes.byref(x), ctypes.byref(y)))
+        return Ciphertext(self._ctx, x.value), Ciphertext(self._ctx, y.value)
 
     def debug_boot_stage(self, ct, stage: int):
         return self._new(self._lib.aesfhe_debug_boot_stage, ct.handle, int(stage))

@@ -16,7 +16,7 @@ import numpy as np
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT, SplitLUT2, powers, std_basis
-from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, drop_to, fused_lut, pair
+from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap2, drop_to, fused_lut, pair
 
 
 class _CoeffCache:
@@ -181,7 +181,6 @@ class MixColFinal:
         log("acc3", acc)
         out_hi, out_lo = acc
         if do_final_bootstrap:
-            out_hi, out_lo = pair(self.ctx, lambda: self.ctx.bootstrap(self.ctx.to_intt(out_hi)),
-                                  lambda: self.ctx.bootstrap(self.ctx.to_intt(out_lo)))
+            out_hi, out_lo = bootstrap2(self.ctx, out_hi, out_lo)
             log("out", (out_hi, out_lo))
         return out_hi, out_lo

@@ -4,6 +4,8 @@ A nibble v is carried as the 16th root of unity ζ^v, ζ = e^{-2πi/16}; decodin
 only the phase, so any positive real magnitude (e.g. XOR4's 256×)
 decodes to the same nibble.
 """
+import os
+
 import numpy as np
 
 
@@ -60,6 +62,16 @@ def pair(ctx, fa, fb, shared=()):
         ctx.engine.settle(*shared)
     a, b = run(fa, fb)
     return a, b
+
+
+def bootstrap2(ctx, a, b):
+    """(bootstrap(a), bootstrap(b)) of the hi / lo halves (REF/mixcol_final.py:158-162): one
+    batched engine bootstrap when the context has it (identical results, shared key and
+    diagonal reads), else the two calls on the two branch streams"""
+    both = getattr(ctx, "bootstrap_pair", None)
+    if both is not None and os.environ.get("AESFHE_BOOT_PAIR", "1") != "0":  # "0": A/B measurements
+        return both(ctx.to_intt(a), ctx.to_intt(b))
+    return pair(ctx, lambda: ctx.bootstrap(ctx.to_intt(a)), lambda: ctx.bootstrap(ctx.to_intt(b)))
 
 
 def fused_lut(ctx, key, coeffs, a, b=None, c0: complex = 0j):

@@ -136,6 +136,10 @@ int aesfhe_to_intt(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
  * CoeffToSlot, EvalMod, SlotToCoeff.  Input slots must satisfy |z| <= 1; the output is at
  * level max_level - aesfhe_bootstrap_depth() of the bootstrappable parameter set. */
 int aesfhe_bootstrap(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
+/* the two bootstraps of a hi / lo pair (REF/mixcol_final.py:158-162, REF/invmixcolumns_fhe.py:166-168)
+ * as one batched bootstrap: same results as two aesfhe_bootstrap calls, each key switch reads
+ * its key and each linear transform its diagonals once for both */
+int aesfhe_bootstrap_pair(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, aesfhe_handle* out_a, aesfhe_handle* out_b);
 int aesfhe_bootstrap_depth(void);
 /* host self-check of the bootstrap plan: err[0] SlotToCoeff, err[1] CoeffToSlot vs the
  * canonical embedding, err[2] EvalMod Chebyshev error (no GPU needed) */

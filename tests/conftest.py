@@ -55,7 +55,8 @@ def gpu_engine(log_n=16, max_level=17, dnum=3, seed=0x5EED):
     key = (log_n, max_level, dnum, seed)
     if key not in _engines:
         from mi355x_ckks import Engine
-        _engines[key] = Engine(log_n=log_n, max_level=max_level, dnum=dnum, seed=seed)
+        # parity-test sets: the N = 2^13 one is far above the 128-bit bound (bit-exactness only)
+        _engines[key] = Engine(log_n=log_n, max_level=max_level, dnum=dnum, seed=seed, allow_insecure=True)
     return _engines[key]
 
 

@@ -80,3 +80,20 @@ def test_config2_full_encrypt_and_roundtrip(ctx, coeff_dir):
     assert np.array_equal(dbg["enc.r0.ark"]["plain"], pt ^ rks[0])
     back = pipe.decrypt(*ct, rks)
     assert np.array_equal(pipe.encoder.decode(*back), pt)
+
+
+def test_bootstrap_pair_bit_exact(ctx):
+    """The batched pair bootstrap (two stacked ciphertexts, shared key and diagonal reads)
+    produces exactly the residues of two single bootstraps."""
+    E = ctx.engine
+    S = E.slot_count
+    rng = np.random.default_rng(4)
+    za = np.exp(2j * np.pi * rng.random(S))
+    zb = np.exp(2j * np.pi * rng.random(S)) * 0.7
+    a, b = ctx.encrypt(za), ctx.encrypt(zb)
+    pa, pb = ctx.bootstrap_pair(a, b)
+    sa, sb = ctx.bootstrap(a), ctx.bootstrap(b)
+    assert pa.level == sa.level == E.fresh_level
+    assert np.array_equal(E.export(pa), E.export(sa))
+    assert np.array_equal(E.export(pb), E.export(sb))
+    assert np.abs(ctx.decrypt(pb) - zb).max() < BOOT_TOL
