@@ -617,7 +617,7 @@ public:
             cur = r, own = true;
         }
         if (pm(cur) == 3 && (need2 || cur.pend > 0)) {
-            Ct r = relin_raw(cur);
+            Ct r = fused_relin_rescale_ok(cur) ? relin_rescale(cur) : relin_raw(cur);
             if (own) release(cur);
             cur = r, own = true;
         }
@@ -1187,11 +1187,12 @@ public:
     int ext_rows(int level) const { return (hp_.nl(level) + hp_.alpha - 1) / hp_.alpha * (hp_.nl(level) + hp_.n_p); }
     // acc (2 x ne rows, Q*P) = sum_j ext_j * key_j; g != 0 reads ext and d through X -> X^g
     // nb batched ciphertexts (ext = [m][nd][ne], d + m d_ms, acc = [m][2][ne]) share the key reads
-    void key_inner(u32* acc, const u32* ext, const u32* d, const u32* key, int level, u64 g, int nb = 1, size_t d_ms = 0) {
+    void key_inner(u32* acc, const u32* ext, const u32* d, const u32* key, int level, u64 g, int nb = 1, size_t d_ms = 0,
+                   KsFold fold = {}) {
         const int nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, n = hp_.n;
         const int nd = (nl + hp_.alpha - 1) / hp_.alpha;
         launch_key_inner(S(), T_, acc, ext, d, key, nd, ne, nl, hp_.alpha, hp_.n_ks + np, hp_.n_ks, extmap(nl), g, nb,
-                         (size_t)nd * ne * n, d_ms, (size_t)2 * ne * n);
+                         (size_t)nd * ne * n, d_ms, (size_t)2 * ne * n, fold);
     }
     // ModDown by P: coefficients of the P rows (read in place from acc), conversion of both
     // polys in one launch, NTT fused with (acc_Q - conv) P^{-1} (+ add)
@@ -1236,6 +1237,53 @@ public:
         return o;
     }
 
+    // relinearisation fused with the rescale that follows it: one ModDown by
+    // Q' = P * (the dropped limbs of level l).  key_inner folds P (c0, c1) into acc's Q rows, so
+    // acc = P * (relinearised ciphertext); the dropped and P rows (contiguous in acc) go to
+    // coefficients together, one conversion to the r kept limbs, and the NTT finish computes
+    // (acc - conv) Q'^{-1}.  Saves the separate rescale's INTT + spread + NTT of 2 r rows.
+    bool fused_relin_rescale_ok(const Ct& c) const {
+        if (!fuse_rr_ || pm(c) != 3 || c.pend < 1 || c.level < 1 || c.zero) return false;
+        return mdr_off_[c.level] != SIZE_MAX && 2 * c.nb <= kMaxConvGroups && c.nb <= kMaxKsBatch;
+    }
+    Ct relin_rescale(const Ct& c) {
+        const int l = c.level, n = hp_.n, nl = hp_.nl(l), r = hp_.nl(l - 1), k = nl - r, np = hp_.n_p, ne = nl + np;
+        const int nb = c.nb, npl = 2 * nb, h = k + np;
+        const size_t ms = (size_t)3 * nl * n;
+        const u32* d2 = c.data + (size_t)2 * nl * n;
+        u32* ext = modup(d2, l, nb, ms);
+        u32* acc = tmp(2 * (size_t)ne * nb);
+        key_inner(acc, ext, d2, ksk(0), l, 0, nb, ms, KsFold{c.data, c.data + (size_t)nl * n, ms, d_gadget_});
+        untmp(ext, (size_t)nb * ext_rows(l));
+        u32* ys = tmp((size_t)npl * h);
+        intt(ys, acc, npl * h, RowMap{h, ne, h, r, 0}, LimbMap{k, r, hp_.p_off()});
+        u32* conv = tmp((size_t)npl * r);
+        const size_t off = mdr_off_[l];
+        ConvBatch cb;
+        cb.n = npl;
+        for (int p = 0; p < npl; ++p) {
+            cb.h[p] = h, cb.d0[p] = r, cb.split[p] = k, cb.d1[p] = hp_.p_off(), cb.skip0[p] = 1 << 30;
+            cb.src[p] = ys + (size_t)p * h * n;
+            cb.dst[p] = conv + (size_t)p * r * n;
+            cb.tab[p] = d_mdr_ + off;                           // [h][r] pairs
+            cb.qhinv[p] = d_mdr_ + off + 2 * (size_t)h * r;     // [h] pairs
+            cb.negq[p] = d_mdr_ + off + 2 * (size_t)h * (r + 1);  // [r]
+        }
+        launch_base_convert(S(), T_, cb, r, qmap());
+        untmp(ys, (size_t)npl * h);
+        Ct o = alloc_ct(l - 1, npl, nb);
+        launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_mdr_ + off + 2 * (size_t)h * (r + 1) + r, nullptr, nullptr, npl, r);
+        cnt_[C_NTT_ROWS] += (size_t)npl * r;
+        untmp(conv, (size_t)npl * r);
+        untmp(acc, 2 * (size_t)ne * nb);
+        o.pend = c.pend - 1;
+        o.lazy = c.lazy && o.pend > 0;
+        cnt_[C_KS] += nb;
+        cnt_[C_RELIN]++;
+        cnt_[C_RESCALE]++;
+        return o;
+    }
+
     // ct x ct.  Inputs are brought to canonical form; the tensor owes one rescale.  relin:
     // key switch now (eager) or leave it to the first consumer that needs two polynomials
     // (lazy)
@@ -1263,6 +1311,11 @@ public:
         if (lazy) {
             d.lazy = true;
             return d;
+        }
+        if (fused_relin_rescale_ok(d)) {
+            Ct o = relin_rescale(d);
+            release(d);
+            return o;
         }
         Ct r = relin_raw(d);
         release(d);
@@ -2195,6 +2248,49 @@ private:
         d_pinv_ = dev_upload(pinv);
         d_negp_ = dev_upload(negp);
 
+        // ModDown fused with the rescale, per level l (sources: the k = nl(l) - nl(l-1) dropped
+        // limbs, then P; Q' their product; r = nl(l-1) targets): [h][r] pairs of Q'/s_i mod q_t,
+        // [h] pairs of (Q'/s_i)^{-1} mod s_i, [r] values of -Q' mod q_t, [r] pairs of Q'^{-1} mod q_t
+        std::vector<u32> mdr;
+        mdr_off_.assign(hp_.L + 1, SIZE_MAX);
+        for (int l = 1; l <= hp_.L; ++l) {
+            const int nl = hp_.nl(l), r = hp_.nl(l - 1), k = nl - r, h = k + np;
+            if (nl > hp_.n_ks || k < 1 || h > kMaxConvH) continue;
+            std::vector<u32> src;
+            for (int i = 0; i < k; ++i) src.push_back(q[r + i]);
+            for (int i = 0; i < np; ++i) src.push_back(q[hp_.p_off() + i]);
+            mdr_off_[l] = mdr.size();
+            for (int i = 0; i < h; ++i)
+                for (int t = 0; t < r; ++t) {
+                    u32 v = 1;
+                    for (int m2 = 0; m2 < h; ++m2)
+                        if (m2 != i) v = mulm(v, src[m2], q[t]);
+                    mdr.push_back(v);
+                    mdr.push_back(shoup_pre(v, q[t]));
+                }
+            for (int i = 0; i < h; ++i) {
+                u32 v = 1;
+                for (int m2 = 0; m2 < h; ++m2)
+                    if (m2 != i) v = mulm(v, src[m2], src[i]);
+                const u32 inv = hinvm(v, src[i]);
+                mdr.push_back(inv);
+                mdr.push_back(shoup_pre(inv, src[i]));
+            }
+            std::vector<u32> all(r);
+            for (int t = 0; t < r; ++t) {
+                u32 v = 1;
+                for (int m2 = 0; m2 < h; ++m2) v = mulm(v, src[m2], q[t]);
+                all[t] = v;
+                mdr.push_back(v ? q[t] - v : 0);
+            }
+            for (int t = 0; t < r; ++t) {
+                const u32 inv = hinvm(all[t], q[t]);
+                mdr.push_back(inv);
+                mdr.push_back(shoup_pre(inv, q[t]));
+            }
+        }
+        d_mdr_ = dev_upload(mdr);
+
     }
 
     HostParams hp_;
@@ -2228,6 +2324,9 @@ private:
     u32* d_moddown_ = nullptr;
     u32* d_moddown_phinv_ = nullptr;
     std::vector<size_t> moddown_off_;
+    u32* d_mdr_ = nullptr;       // ModDown fused with the rescale, per level (see build_tables)
+    std::vector<size_t> mdr_off_;
+    bool fuse_rr_ = std::getenv("AESFHE_FUSED_RESCALE") == nullptr || std::getenv("AESFHE_FUSED_RESCALE")[0] != '0';
     u32* d_pinv_ = nullptr;
     u32* d_negp_ = nullptr;
     u64 cnt_[C_N] = {};

@@ -147,6 +147,9 @@ constexpr int kMaxConvH = 16;
 struct ConvBatch {
     int n = 0;
     int h[kMaxConvGroups] = {}, d0[kMaxConvGroups] = {}, skip0[kMaxConvGroups] = {};
+    // split > 0: sources i >= split are primes d1 + (i - split) (ModDown fused with rescale:
+    // the dropped Q limbs, then P)
+    int split[kMaxConvGroups] = {}, d1[kMaxConvGroups] = {};
     const u32* src[kMaxConvGroups] = {};
     u32* dst[kMaxConvGroups] = {};
     const u32* tab[kMaxConvGroups] = {};
@@ -161,9 +164,18 @@ void launch_base_convert(hipStream_t st, const DevTables& T, const ConvBatch& cb
 // nb > 1: nb ciphertexts' key switches with the SAME key in one launch (the key is read once
 // per residue for all of them); member m uses ext + m ext_ms, d + m d_ms, acc + m acc_ms (words)
 constexpr int kMaxKsBatch = 4;
+// fold (g == 0 only): acc[p][x] += gad_x add_p[x] on the Q rows x < nl (member m: add_p + m ms),
+// gad = P mod q_x Shoup pairs -- the relinearised P (c0, c1) + acc before a ModDown that also
+// divides by the dropped limbs
+struct KsFold {
+    const u32* add0 = nullptr;
+    const u32* add1 = nullptr;
+    size_t ms = 0;
+    const u32* gad = nullptr;
+};
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
                       int alpha, int nkey, int nks, LimbMap map, u64 g = 0, int nb = 1, size_t ext_ms = 0, size_t d_ms = 0,
-                      size_t acc_ms = 0);
+                      size_t acc_ms = 0, KsFold fold = {});
 // out[p][t] = sum_j x_j[p][t] pt_j[t] over rows t < rows, polys p < npoly (x poly stride xs,
 // out poly stride os, in words)
 constexpr int kMacMax = 16;

@@ -84,12 +84,20 @@ def test_rescale_tensor_automorph_bitexact(pair):
     # tensor (no relinearisation): kept un-rescaled until relinearised or consumed
     t = O.tensor(level, a, b)
     assert np.array_equal(E.export(E.multiply(ca, cb)), t)
-    # relinearised product: (d0, d1) + KS(d2), then rescale
-    ks = O.keyswitch(level, t[2], O.gen_ksk(0))
-    q = O.limbs_mod(level + 2)
-    relin = ((t[:2].astype(np.uint64) + ks) % q).astype(np.uint32)
-    assert np.array_equal(E.export(E.multiply(ca, cb, "rlk")), O.rescale(level, relin))
+    # relinearised product: (d0, d1) + KS(d2), then rescale.  The engine fuses the two
+    # (one ModDown by P * q_l, engine.hip relin_rescale); with centred conversions
+    # (X - [X]_{PD}) / PD == (Y - [Y]_D) / D for X = P Y + [X]_P, so the oracle's two-step
+    # composition is matched bit for bit
+    for lv in sorted({1, level, O.L - 1}):  # nl(L) includes the encryption limb
+        x, y = rand_ct(O, lv, 2, rng), rand_ct(O, lv, 2, rng)
+        t2 = O.tensor(lv, x, y)
+        ks = O.keyswitch(lv, t2[2], O.gen_ksk(0))
+        qq = O.limbs_mod(lv + 2)
+        relin = ((t2[:2].astype(np.uint64) + ks) % qq).astype(np.uint32)
+        got = E.export(E.multiply(E.import_ct(x, lv), E.import_ct(y, lv), "rlk"))
+        assert np.array_equal(got, O.rescale(lv, relin)), lv
     # rotation: automorphism + key switch of the second polynomial
+    q = O.limbs_mod(level + 2)
     steps = E.slot_count // 8
     g = E.galois_rotate(steps)
     x = O.automorph(level, g, a)
