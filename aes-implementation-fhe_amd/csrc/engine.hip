@@ -1247,14 +1247,27 @@ public:
         return mdr_off_[c.level] != SIZE_MAX && 2 * c.nb <= kMaxConvGroups && c.nb <= kMaxKsBatch;
     }
     Ct relin_rescale(const Ct& c) {
-        const int l = c.level, n = hp_.n, nl = hp_.nl(l), r = hp_.nl(l - 1), k = nl - r, np = hp_.n_p, ne = nl + np;
-        const int nb = c.nb, npl = 2 * nb, h = k + np;
+        const int l = c.level, n = hp_.n, nl = hp_.nl(l), ne = nl + hp_.n_p, nb = c.nb;
         const size_t ms = (size_t)3 * nl * n;
         const u32* d2 = c.data + (size_t)2 * nl * n;
         u32* ext = modup(d2, l, nb, ms);
         u32* acc = tmp(2 * (size_t)ne * nb);
         key_inner(acc, ext, d2, ksk(0), l, 0, nb, ms, KsFold{c.data, c.data + (size_t)nl * n, ms, d_gadget_});
         untmp(ext, (size_t)nb * ext_rows(l));
+        Ct o = moddown_rescale(acc, l, nb);
+        untmp(acc, 2 * (size_t)ne * nb);
+        o.pend = c.pend - 1;
+        o.lazy = c.lazy && o.pend > 0;
+        cnt_[C_KS] += nb;
+        cnt_[C_RELIN]++;
+        return o;
+    }
+    // acc = [m][2][ne] in Q*P, NTT form, already holding P * (the ciphertext) -> the ciphertext
+    // divided by the dropped limbs of level l, at level l - 1 (one ModDown by Q' = P * D)
+    Ct moddown_rescale(const u32* acc, int l, int nb) {
+        const int n = hp_.n, nl = hp_.nl(l), r = hp_.nl(l - 1), k = nl - r, np = hp_.n_p, ne = nl + np;
+        const int npl = 2 * nb, h = k + np;
+        if (mdr_off_[l] == SIZE_MAX || npl > kMaxConvGroups) throw std::runtime_error("moddown_rescale: unsupported level or batch");
         u32* ys = tmp((size_t)npl * h);
         intt(ys, acc, npl * h, RowMap{h, ne, h, r, 0}, LimbMap{k, r, hp_.p_off()});
         u32* conv = tmp((size_t)npl * r);
@@ -1275,11 +1288,6 @@ public:
         launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_mdr_ + off + 2 * (size_t)h * (r + 1) + r, nullptr, nullptr, npl, r);
         cnt_[C_NTT_ROWS] += (size_t)npl * r;
         untmp(conv, (size_t)npl * r);
-        untmp(acc, 2 * (size_t)ne * nb);
-        o.pend = c.pend - 1;
-        o.lazy = c.lazy && o.pend > 0;
-        cnt_[C_KS] += nb;
-        cnt_[C_RELIN]++;
         cnt_[C_RESCALE]++;
         return o;
     }
@@ -1681,6 +1689,9 @@ public:
             LinMacArgs m{};
             m.B = g.B, m.G = gn, m.c1 = c1;
             m.nb = nb, m.q_ms = qs, m.p_ms = ps;
+            // rotated giant steps: P (out0, out1) folded into outp, ModDown fused with the rescale
+            const bool fold = fuse_rr_ && l >= 1 && mdr_off_[l] != SIZE_MAX;
+            m.gad = fold ? d_gadget_ : nullptr;
             for (int b = 0; b < g.B; ++b) m.a[b] = b == 0 ? c0 : a[b], m.u[b] = b ? u[b] : nullptr;
             bool any[kLinG] = {}, rot[kLinG] = {};
             for (int j = 0; j < gn; ++j) {
@@ -1689,16 +1700,19 @@ public:
                     any[j] = any[j] || P[g0 + j][b];
                     rot[j] = rot[j] || (b && P[g0 + j][b]);
                 }
-                m.out0[j] = tmp(2 * (size_t)nl * nb);  // member stride qs, first nl rows used
-                m.out1[j] = P[g0 + j][0] ? tmp(2 * (size_t)nl * nb) : nullptr;
+                const bool folded = fold && rot[j];
+                m.out0[j] = folded ? nullptr : tmp(2 * (size_t)nl * nb);  // member stride qs, first nl rows used
+                m.out1[j] = (P[g0 + j][0] && !folded) ? tmp(2 * (size_t)nl * nb) : nullptr;
                 m.outp[j] = rot[j] ? tmp(2 * (size_t)ne * nb) : nullptr;
             }
             launch_lin_mac(S(), T_, m, nl, ne, extmap(nl));
             for (int j = 0; j < gn; ++j) {
                 const int gg = g0 + j;
                 if (any[j]) {
-                    Ct inner;
-                    if (rot[j]) {
+                    Ct inner, rs;
+                    if (rot[j] && fold) {
+                        rs = moddown_rescale(m.outp[j], l, nb);
+                    } else if (rot[j]) {
                         inner = moddown(m.outp[j], l, m.out0[j], m.out1[j], nb, qs);
                     } else {  // only the unrotated diagonal
                         inner = alloc_ct(l, 2 * nb, nb);
@@ -1709,8 +1723,10 @@ public:
                                                   hipMemcpyDeviceToDevice, S()));
                         }
                     }
-                    Ct rs = rescale(inner);
-                    release(inner);
+                    if (!(rot[j] && fold)) {
+                        rs = rescale(inner);
+                        release(inner);
+                    }
                     Ct part = g.giant[gg] ? rotl(rs, g.giant[gg]) : rs;
                     if (g.giant[gg]) release(rs);
                     if (!have) {
@@ -1722,7 +1738,7 @@ public:
                         out = s2;
                     }
                 }
-                untmp(m.out0[j], 2 * (size_t)nl * nb);
+                if (m.out0[j]) untmp(m.out0[j], 2 * (size_t)nl * nb);
                 if (m.out1[j]) untmp(m.out1[j], 2 * (size_t)nl * nb);
                 if (m.outp[j]) untmp(m.outp[j], 2 * (size_t)ne * nb);
             }

@@ -206,6 +206,9 @@ struct LinMacArgs {
     int B, G;
     int nb = 1;
     size_t q_ms = 0, p_ms = 0;
+    // gad (P mod q_t Shoup pairs): giant steps with outp fold P * (out0, out1) into outp's Q
+    // rows instead of storing out0 / out1 (ModDown fused with the rescale)
+    const u32* gad = nullptr;
 };
 void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int nl, int ne, LimbMap map);
 

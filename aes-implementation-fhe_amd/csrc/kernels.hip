@@ -755,13 +755,25 @@ __device__ __forceinline__ void lin_mac_body(const LinMacArgs& m, int nl, int ne
 #pragma unroll
         for (int g = 0; g < kLinG; ++g) {
             if (g >= m.G) continue;
+            u32 o0 = 0, o1 = 0;
             if (qrow) {
-                m.out0[g][b * m.q_ms + at] = reduce64(acc0[b][g], P.q, P.mu, P.r32);
-                if (m.out1[g]) m.out1[g][b * m.q_ms + at] = reduce64((u64)c1v * m.pt[g][0][at], P.q, P.mu, P.r32);
+                o0 = reduce64(acc0[b][g], P.q, P.mu, P.r32);
+                if (m.pt[g][0]) o1 = reduce64((u64)c1v * m.pt[g][0][at], P.q, P.mu, P.r32);
+            }
+            const bool fold = m.gad && m.outp[g];
+            if (qrow && !fold) {
+                m.out0[g][b * m.q_ms + at] = o0;
+                if (m.out1[g]) m.out1[g][b * m.q_ms + at] = o1;
             }
             if (m.outp[g]) {
-                m.outp[g][b * m.p_ms + at] = reduce64(ap0[b][g], P.q, P.mu, P.r32);
-                m.outp[g][b * m.p_ms + po + at] = reduce64(ap1[b][g], P.q, P.mu, P.r32);
+                u32 p0 = reduce64(ap0[b][g], P.q, P.mu, P.r32), p1 = reduce64(ap1[b][g], P.q, P.mu, P.r32);
+                if (fold && qrow) {
+                    const u32 gv = m.gad[2 * t], gp = m.gad[2 * t + 1];
+                    p0 = add_mod(p0, shoup_mul(o0, gv, gp, P.q), P.q);
+                    p1 = add_mod(p1, shoup_mul(o1, gv, gp, P.q), P.q);
+                }
+                m.outp[g][b * m.p_ms + at] = p0;
+                m.outp[g][b * m.p_ms + po + at] = p1;
             }
         }
     }
@@ -785,7 +797,8 @@ void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int
             if (m.pt[g][b]) reads += ne;
     }
     reads += nl;  // c1
-    for (int g = 0; g < m.G; ++g) writes += nl + (m.out1[g] ? nl : 0) + (m.outp[g] ? 2.0 * ne : 0);
+    for (int g = 0; g < m.G; ++g)
+        writes += (m.gad && m.outp[g]) ? 2.0 * ne : nl + (m.out1[g] ? nl : 0) + (m.outp[g] ? 2.0 * ne : 0);
     double shared = 0;  // the diagonals, read once for every batched ciphertext
     for (int b = 0; b < m.B; ++b)
         for (int g = 0; g < m.G; ++g)
