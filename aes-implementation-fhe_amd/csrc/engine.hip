@@ -1661,7 +1661,8 @@ public:
         const size_t qs = (size_t)2 * nl * n, ps = (size_t)2 * ne * n;
         const u32* c0 = in.data;
         const u32* c1 = in.data + (size_t)nl * n;
-        std::vector<u32*> u(g.B, nullptr), a(g.B, nullptr);
+        std::vector<u32*> u(g.B, nullptr);
+        std::vector<u64> gals(g.B, 0);
         bool any_baby = false;
         for (int b = 1; b < g.B; ++b)
             for (int gg = 0; gg < g.G; ++gg) any_baby = any_baby || P[gg][b];
@@ -1674,8 +1675,7 @@ public:
                 const u64 gal = rot_galois(-(int)((long)g.h * b));  // left rotation by h b
                 u[b] = tmp(2 * (size_t)ne * nb);
                 key_inner(u[b], ext, c1, ksk(gal), l, gal, nb, qs);
-                a[b] = tmp(2 * (size_t)nl * nb);  // member stride qs, first nl rows used
-                for (int mb = 0; mb < nb; ++mb) launch_automorph(S(), T_, a[b] + mb * qs, c0 + mb * qs, gal, nl);
+                gals[b] = gal;  // c0's automorphism is read inside k_lin_mac
                 cnt_[C_ROT] += nb;
             }
             untmp(ext, (size_t)nb * ext_rows(l));
@@ -1692,7 +1692,7 @@ public:
             // rotated giant steps: P (out0, out1) folded into outp, ModDown fused with the rescale
             const bool fold = fuse_rr_ && l >= 1 && mdr_off_[l] != SIZE_MAX;
             m.gad = fold ? d_gadget_ : nullptr;
-            for (int b = 0; b < g.B; ++b) m.a[b] = b == 0 ? c0 : a[b], m.u[b] = b ? u[b] : nullptr;
+            for (int b = 0; b < g.B; ++b) m.a[b] = (b == 0 || u[b]) ? c0 : nullptr, m.u[b] = b ? u[b] : nullptr, m.gal[b] = gals[b];
             bool any[kLinG] = {}, rot[kLinG] = {};
             for (int j = 0; j < gn; ++j) {
                 for (int b = 0; b < g.B; ++b) {
@@ -1745,7 +1745,6 @@ public:
         }
         for (int b = 1; b < g.B; ++b) {
             if (u[b]) untmp(u[b], 2 * (size_t)ne * nb);
-            if (a[b]) untmp(a[b], 2 * (size_t)nl * nb);
         }
         return out;
     }

@@ -209,6 +209,9 @@ struct LinMacArgs {
     // gad (P mod q_t Shoup pairs): giant steps with outp fold P * (out0, out1) into outp's Q
     // rows instead of storing out0 / out1 (ModDown fused with the rescale)
     const u32* gad = nullptr;
+    // gal[b] != 0: a[b] is read through X -> X^gal[b] (the baby step's automorphism of c0,
+    // fused: no rotated copy of c0 is written)
+    u64 gal[kLinB] = {};
 };
 void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int nl, int ne, LimbMap map);
 

@@ -733,7 +733,9 @@ __device__ __forceinline__ void lin_mac_body(const LinMacArgs& m, int nl, int ne
         u32 av[NB], u0[NB], u1[NB];
 #pragma unroll
         for (int b = 0; b < NB; ++b) {
-            av[b] = (qrow && m.a[j]) ? m.a[j][b * m.q_ms + at] : 0u;
+            av[b] = 0u;
+            if (qrow && m.a[j])
+                av[b] = m.a[j][b * m.q_ms + ((size_t)t << logn) + (m.gal[j] ? galois_src((u32)k, m.gal[j], logn) : k)];
             u0[b] = u1[b] = 0;
             if (m.u[j]) u0[b] = m.u[j][b * m.p_ms + at], u1[b] = m.u[j][b * m.p_ms + po + at];
         }
