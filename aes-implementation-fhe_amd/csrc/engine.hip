@@ -1188,11 +1188,11 @@ public:
     // acc (2 x ne rows, Q*P) = sum_j ext_j * key_j; g != 0 reads ext and d through X -> X^g
     // nb batched ciphertexts (ext = [m][nd][ne], d + m d_ms, acc = [m][2][ne]) share the key reads
     void key_inner(u32* acc, const u32* ext, const u32* d, const u32* key, int level, u64 g, int nb = 1, size_t d_ms = 0,
-                   KsFold fold = {}) {
+                   KsFold fold = {}, bool accum = false) {
         const int nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, n = hp_.n;
         const int nd = (nl + hp_.alpha - 1) / hp_.alpha;
         launch_key_inner(S(), T_, acc, ext, d, key, nd, ne, nl, hp_.alpha, hp_.n_ks + np, hp_.n_ks, extmap(nl), g, nb,
-                         (size_t)nd * ne * n, d_ms, (size_t)2 * ne * n, fold);
+                         (size_t)nd * ne * n, d_ms, (size_t)2 * ne * n, fold, accum);
     }
     // ModDown by P: coefficients of the P rows (read in place from acc), conversion of both
     // polys in one launch, NTT fused with (acc_Q - conv) P^{-1} (+ add)
@@ -1682,6 +1682,13 @@ public:
         }
         Ct out;
         bool have = false;
+        // double hoisting: the rotated giant steps' key inner products are summed in Q*P and
+        // share ONE ModDown (their permuted c0 summed beside), the unrotated step folded in
+        const bool dh = double_hoist_;
+        u32* dh_acc = nullptr;
+        u32* dh_c0 = nullptr;
+        int dh_n = 0;
+        bool continue_giant = false;
         // all giant steps' diagonal sums in one pass per chunk of kLinG giant steps (k_lin_mac):
         // every baby-step residue is read once instead of once per giant step
         for (int g0 = 0; g0 < g.G; g0 += kLinG) {
@@ -1727,9 +1734,19 @@ public:
                         rs = rescale(inner);
                         release(inner);
                     }
-                    Ct part = g.giant[gg] ? rotl(rs, g.giant[gg]) : rs;
-                    if (g.giant[gg]) release(rs);
-                    if (!have) {
+                    if (dh && g.giant[gg]) {
+                        giant_accumulate(rs, rot_galois(-(int)g.giant[gg]), dh_acc, dh_c0, dh_n);
+                        release(rs);
+                        continue_giant = true;
+                    }
+                    Ct part;
+                    if (!continue_giant) {
+                        part = g.giant[gg] ? rotl(rs, g.giant[gg]) : rs;
+                        if (g.giant[gg]) release(rs);
+                    }
+                    if (continue_giant) {
+                        continue_giant = false;
+                    } else if (!have) {
                         out = part, have = true;
                     } else {
                         Ct s2 = add_sub(out, part, false);
@@ -1746,7 +1763,46 @@ public:
         for (int b = 1; b < g.B; ++b) {
             if (u[b]) untmp(u[b], 2 * (size_t)ne * nb);
         }
+        if (dh_n > 0) {
+            const int lv = l - 1, r = hp_.nl(lv), ne2 = r + np;
+            const size_t ms = (size_t)2 * r * n;
+            const u32* add1 = nullptr;
+            if (have) {  // the unrotated giant step: c0 into the sum, c1 as the second addend
+                if (out.level != lv || pm(out) != 2 || out.pend) throw std::runtime_error("lin_group: unrotated part off level");
+                for (int mb = 0; mb < nb; ++mb) launch_add(S(), T_, dh_c0 + mb * ms, dh_c0 + mb * ms, out.data + mb * ms, r, r, qmap());
+                add1 = out.data + (size_t)r * n;
+            }
+            Ct res = moddown(dh_acc, lv, dh_c0, add1, nb, ms);
+            if (have) release(out);
+            untmp(dh_acc, 2 * (size_t)ne2 * nb);
+            untmp(dh_c0, 2 * (size_t)r * nb);
+            out = res;
+        }
         return out;
+    }
+    // one rotated giant step of a double-hoisted group: rs permuted by X -> X^gal, its c1
+    // key switched into the running Q*P sum acc (allocated on the first call), its c0 summed
+    // into c0sum (the first permuted buffer, member stride 2 r N)
+    void giant_accumulate(const Ct& rs, u64 gal, u32*& acc, u32*& c0sum, int& count) {
+        if (vis_npoly(rs) != 2 || rs.pend || rs.lazy) throw std::runtime_error("giant_accumulate: canonical input expected");
+        const int lv = rs.level, r = hp_.nl(lv), ne2 = r + hp_.n_p, nb = rs.nb, n = hp_.n;
+        const size_t ms = (size_t)2 * r * n;
+        u32* perm = tmp(2 * (size_t)r * nb);
+        launch_automorph(S(), T_, perm, rs.data, gal, 2 * r * nb);
+        const u32* p1 = perm + (size_t)r * n;
+        u32* ext = modup(p1, lv, nb, ms);
+        if (!acc) acc = tmp(2 * (size_t)ne2 * nb);
+        key_inner(acc, ext, p1, ksk(gal), lv, 0, nb, ms, KsFold{}, count > 0);
+        untmp(ext, (size_t)nb * ext_rows(lv));
+        if (count == 0) {
+            c0sum = perm;
+        } else {
+            for (int mb = 0; mb < nb; ++mb) launch_add(S(), T_, c0sum + mb * ms, c0sum + mb * ms, perm + mb * ms, r, r, qmap());
+            untmp(perm, 2 * (size_t)r * nb);
+        }
+        ++count;
+        cnt_[C_ROT] += nb;
+        cnt_[C_KS] += nb;
     }
 
     Ct lin_transform(const Ct& in, std::vector<BootGroupDev>& groups) {
@@ -2341,6 +2397,7 @@ private:
     std::vector<size_t> moddown_off_;
     u32* d_mdr_ = nullptr;       // ModDown fused with the rescale, per level (see build_tables)
     std::vector<size_t> mdr_off_;
+    bool double_hoist_ = std::getenv("AESFHE_DOUBLE_HOIST") == nullptr || std::getenv("AESFHE_DOUBLE_HOIST")[0] != '0';
     bool fuse_rr_ = std::getenv("AESFHE_FUSED_RESCALE") == nullptr || std::getenv("AESFHE_FUSED_RESCALE")[0] != '0';
     u32* d_pinv_ = nullptr;
     u32* d_negp_ = nullptr;

@@ -164,6 +164,7 @@ void launch_base_convert(hipStream_t st, const DevTables& T, const ConvBatch& cb
 // nb > 1: nb ciphertexts' key switches with the SAME key in one launch (the key is read once
 // per residue for all of them); member m uses ext + m ext_ms, d + m d_ms, acc + m acc_ms (words)
 constexpr int kMaxKsBatch = 4;
+// accum: acc += the inner product (giant steps summed in Q*P, one ModDown for all of them)
 // fold (g == 0 only): acc[p][x] += gad_x add_p[x] on the Q rows x < nl (member m: add_p + m ms),
 // gad = P mod q_x Shoup pairs -- the relinearised P (c0, c1) + acc before a ModDown that also
 // divides by the dropped limbs
@@ -175,7 +176,7 @@ struct KsFold {
 };
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
                       int alpha, int nkey, int nks, LimbMap map, u64 g = 0, int nb = 1, size_t ext_ms = 0, size_t d_ms = 0,
-                      size_t acc_ms = 0, KsFold fold = {});
+                      size_t acc_ms = 0, KsFold fold = {}, bool accum = false);
 // out[p][t] = sum_j x_j[p][t] pt_j[t] over rows t < rows, polys p < npoly (x poly stride xs,
 // out poly stride os, in words)
 constexpr int kMacMax = 16;

@@ -231,7 +231,7 @@ __device__ __forceinline__ u32 galois_src(u32 i, u64 g, int logn) {
 // rotation: one ModUp of c1 serves every rotation of the same ciphertext
 __global__ void k_key_inner(u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl, int alpha, int nkey, int nks,
                             u64 g, LimbMap map, const PrimeConst* pc, int logn, int nb, size_t ext_ms, size_t d_ms, size_t acc_ms,
-                            KsFold fold, unsigned long long* ts) {
+                            KsFold fold, int accum, unsigned long long* ts) {
     ts_begin(ts);
     const int x = blockIdx.y;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
@@ -269,8 +269,11 @@ __global__ void k_key_inner(u32* acc, const u32* ext, const u32* d, const u32* k
             r0 = add_mod(r0, shoup_mul(fold.add0[at], gv, gp, P.q), P.q);
             r1 = add_mod(r1, shoup_mul(fold.add1[at], gv, gp, P.q), P.q);
         }
-        acc[m * acc_ms + ((size_t)x << logn) + k] = r0;
-        acc[m * acc_ms + (((size_t)ne + x) << logn) + k] = r1;
+        u32* a0 = acc + m * acc_ms + ((size_t)x << logn) + k;
+        u32* a1 = acc + m * acc_ms + (((size_t)ne + x) << logn) + k;
+        if (accum) r0 = add_mod(r0, *a0, P.q), r1 = add_mod(r1, *a1, P.q);
+        *a0 = r0;
+        *a1 = r1;
     }
     ts_end(ts);
 }
@@ -821,14 +824,16 @@ void launch_mac(hipStream_t st, const DevTables& T, u32* out, const MacTerms& m,
 }
 
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
-                      int alpha, int nkey, int nks, LimbMap map, u64 g, int nb, size_t ext_ms, size_t d_ms, size_t acc_ms, KsFold fold) {
+                      int alpha, int nkey, int nks, LimbMap map, u64 g, int nb, size_t ext_ms, size_t d_ms, size_t acc_ms, KsFold fold,
+                      bool accum) {
     if (nb < 1 || nb > kMaxKsBatch) throw std::runtime_error("launch_key_inner: 1..4 batched ciphertexts");
     if (fold.gad && g) throw std::runtime_error("launch_key_inner: fold with an automorphism");
     // per ciphertext ext/d (nd x ne) read and acc (2 x ne) written; the key (nd x 2 x ne) once;
     // the fold reads 2 x nl more rows per ciphertext
-    const double fw = fold.gad ? 2.0 * nb * nl : 0.0;
+    const double fw = (fold.gad ? 2.0 * nb * nl : 0.0) + (accum ? 2.0 * nb * ne : 0.0);
     prof_launch_ts(KID_KEY_INNER, words(((nb * (nd + 2.0) + 2.0 * nd) * ne + fw) * (1u << T.logn)), k_key_inner, ew_grid(T.logn, ne),
-                   dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g, map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold);
+                   dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g, map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold,
+                   (int)accum);
 }
 void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, u64 seed, u64 stream, int kind) {
     prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_small, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, nl, map, seed, stream, kind, T.pc,
