@@ -357,10 +357,10 @@ public:
         if (g == 0) {
             launch_square(S(), T_, sp, d_s_, nks, nks, qmap());
         } else if (g == tag_d2s()) {  // dense s -> sparse ephemeral s_sp (bootstrapping)
-            HIP_OK(hipMemcpyAsync(sp, d_s_, sizeof(u32) * nks * n, hipMemcpyDeviceToDevice, S()));
+            launch_copy_rows(S(), T_, sp, d_s_, nks);
             target = sparse_secret();
         } else if (g == tag_s2d()) {  // sparse s_sp -> dense s
-            HIP_OK(hipMemcpyAsync(sp, sparse_secret(), sizeof(u32) * nks * n, hipMemcpyDeviceToDevice, S()));
+            launch_copy_rows(S(), T_, sp, sparse_secret(), nks);
         } else {
             launch_automorph(S(), T_, sp, d_s_, g, nks);
         }
@@ -478,7 +478,7 @@ public:
         }
         const double scale = c.level >= 0 ? raw_scale(c.level, c.pend) : (bs_.ready ? bs_.s_bt : 1.0);
         u32* x = tmp(kd);
-        HIP_OK(hipMemcpyAsync(x, c.data, sizeof(u32) * kd * n, hipMemcpyDeviceToDevice, S()));
+        launch_copy_rows(S(), T_, x, c.data, kd);
         u32* spow = nullptr;
         for (int p = 1; p < c.npoly; ++p) {
             const u32* s_use = d_s_;
@@ -534,7 +534,7 @@ public:
     Ct copy(const Ct& c) {
         Ct o = alloc_ct(c.level, c.npoly);
         copy_meta(o, c);
-        HIP_OK(hipMemcpyAsync(o.data, c.data, c.words * sizeof(u32), hipMemcpyDeviceToDevice, S()));
+        launch_copy_rows(S(), T_, o.data, c.data, c.words / hp_.n);
         return o;
     }
     // returns c itself (same data) when already in NTT form, else a converted copy
@@ -1481,7 +1481,7 @@ public:
             }
             const int nl = hp_.nl(c.level);
             u32* xw = x + (size_t)w * 4 * n;
-            HIP_OK(hipMemcpyAsync(xw, c.data, sizeof(u32) * kd[w] * n, hipMemcpyDeviceToDevice, S()));
+            launch_copy_rows(S(), T_, xw, c.data, kd[w]);
             for (int p = 1; p < c.npoly; ++p)
                 launch_fma_poly(S(), T_, xw, xw, c.data + (size_t)p * nl * n, p == 2 ? s_sq4() : d_s_, kd[w], kd[w], qmap());
             intt(xw, kd[w], kd[w], qmap());
@@ -1724,10 +1724,8 @@ public:
                     } else {  // only the unrotated diagonal
                         inner = alloc_ct(l, 2 * nb, nb);
                         for (int mb = 0; mb < nb; ++mb) {
-                            HIP_OK(hipMemcpyAsync(inner.data + mb * qs, m.out0[j] + mb * qs, (size_t)nl * n * sizeof(u32),
-                                                  hipMemcpyDeviceToDevice, S()));
-                            HIP_OK(hipMemcpyAsync(inner.data + mb * qs + (size_t)nl * n, m.out1[j] + mb * qs, (size_t)nl * n * sizeof(u32),
-                                                  hipMemcpyDeviceToDevice, S()));
+                            launch_copy_rows(S(), T_, inner.data + mb * qs, m.out0[j] + mb * qs, nl);
+                            launch_copy_rows(S(), T_, inner.data + mb * qs + (size_t)nl * n, m.out1[j] + mb * qs, nl);
                         }
                     }
                     if (!(rot[j] && fold)) {
@@ -1986,7 +1984,7 @@ public:
             Ct c = normalize(*in[m]);
             Ct zm = level_down(c, 0);
             if (c.data != in[m]->data) release(c);
-            HIP_OK(hipMemcpyAsync(z.data + (size_t)m * 2 * nl0 * n, zm.data, sizeof(u32) * 2 * nl0 * n, hipMemcpyDeviceToDevice, S()));
+            launch_copy_rows(S(), T_, z.data + (size_t)m * 2 * nl0 * n, zm.data, 2 * nl0);
             release(zm);
         }
         Ct out = bootstrap_l0(z, 99);
@@ -1995,7 +1993,7 @@ public:
         for (int m = 0; m < 2; ++m) {
             Ct o = alloc_ct(out.level, 2);
             o.ntt = out.ntt;
-            HIP_OK(hipMemcpyAsync(o.data, out.data + (size_t)m * 2 * nlo * n, sizeof(u32) * 2 * nlo * n, hipMemcpyDeviceToDevice, S()));
+            launch_copy_rows(S(), T_, o.data, out.data + (size_t)m * 2 * nlo * n, 2 * nlo);
             *dst[m] = put_ct(o);
         }
         release(out);

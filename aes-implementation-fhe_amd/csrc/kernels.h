@@ -105,6 +105,8 @@ void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* data, int rows, int
 void launch_add(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int rows, int nl, LimbMap map);
 void launch_sub(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int rows, int nl, LimbMap map);
 void launch_neg(hipStream_t st, const DevTables& T, u32* out, const u32* a, int rows, int nl, LimbMap map);
+// out = in over `rows` rows of N words (device to device)
+void launch_copy_rows(hipStream_t st, const DevTables& T, u32* out, const u32* in, size_t rows);
 // out = (a0 b0, a0 b1 + a1 b0, a1 b1); a, b: 2 x nl rows; out: 3 x nl rows
 // nb > 1: nb ciphertexts stacked ([m][2][nl] in, [m][3][nl] out), one launch
 void launch_tensor(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int nl, LimbMap map, int nb = 1);

@@ -54,6 +54,11 @@ __global__ void k_addsub_tail(u32* out, const u32* a, const u32* b, int common, 
         out[idx] = sub ? (v ? P.q - v : 0u) : v;
     }
 }
+// plain device copy of whole rows (16 B per lane): cheaper to issue than a runtime D2D blit
+__global__ void k_copy_rows(uint4* out, const uint4* in, int logn) {
+    const size_t i = ((size_t)blockIdx.y << (logn - 2)) + (size_t)blockIdx.x * kBlock + threadIdx.x;
+    out[i] = in[i];
+}
 __global__ void k_neg(u32* out, const u32* a, int nl, LimbMap map, const PrimeConst* pc, int logn) {
     EW_PROLOGUE
     u32 v = a[idx];
@@ -645,6 +650,12 @@ void launch_add(hipStream_t st, const DevTables& T, u32* out, const u32* a, cons
 }
 void launch_sub(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int rows, int nl, LimbMap map) {
     prof_launch(KID_ELEMENTWISE, EW_BYTES(3.0 * rows), k_sub, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, b, nl, map, T.pc, T.logn);
+}
+void launch_copy_rows(hipStream_t st, const DevTables& T, u32* out, const u32* in, size_t rows) {
+    if (rows == 0 || out == in) return;
+    if (rows > 65535) throw std::runtime_error("launch_copy_rows: too many rows");
+    prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows), k_copy_rows, dim3((1u << T.logn) / (4 * kBlock), (unsigned)rows), dim3(kBlock), 0, st,
+                reinterpret_cast<uint4*>(out), reinterpret_cast<const uint4*>(in), T.logn);
 }
 void launch_neg(hipStream_t st, const DevTables& T, u32* out, const u32* a, int rows, int nl, LimbMap map) {
     prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows), k_neg, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, nl, map, T.pc, T.logn);
