@@ -2039,13 +2039,36 @@ public:
         release(dif);
         if (stop_after == 6) return release(im), re;
         if (stop_after == 7) return release(re), im;
-        // 7. EvalMod on both halves
-        Ct fre = eval_mod(re);
-        release(re);
-        if (stop_after == 8) return release(im), fre;
-        Ct fim = eval_mod(im);
-        release(im);
-        if (stop_after == 9) return release(fre), fim;
+        // 7. EvalMod on both halves: stacked into ONE batched ciphertext (2 nb members) so
+        // every key switch of the polynomial evaluation reads its key once for both halves
+        Ct fre, fim;
+        if (stop_after > 9 && stack_evalmod_ && 2 * nb <= kMaxKsBatch && re.level == im.level && re.pend == im.pend &&
+            !re.lazy && !im.lazy && pm(re) == 2 && pm(im) == 2 && re.ntt == im.ntt) {
+            Ct st = alloc_ct(re.level, re.npoly + im.npoly, 2 * nb);
+            st.ntt = re.ntt, st.pend = re.pend;
+            launch_copy_rows(S(), T_, st.data, re.data, re.words / n);
+            launch_copy_rows(S(), T_, st.data + re.words, im.data, im.words / n);
+            release(re);
+            release(im);
+            Ct f = eval_mod(st);
+            release(st);
+            Ct* half[2] = {&fre, &fim};
+            for (int h = 0; h < 2; ++h) {
+                Ct& o = *half[h];
+                o = alloc_ct(f.level, f.npoly / 2, nb);
+                copy_meta(o, f);
+                o.nb = nb;
+                launch_copy_rows(S(), T_, o.data, f.data + h * o.words, o.words / n);
+            }
+            release(f);
+        } else {
+            fre = eval_mod(re);
+            release(re);
+            if (stop_after == 8) return release(im), fre;
+            fim = eval_mod(im);
+            release(im);
+            if (stop_after == 9) return release(fre), fim;
+        }
         Ct ifim = mul_scalar(fim, 0.0, 1.0);
         release(fim);
         Ct wp = add_sub(fre, ifim, false);
@@ -2395,6 +2418,7 @@ private:
     std::vector<size_t> moddown_off_;
     u32* d_mdr_ = nullptr;       // ModDown fused with the rescale, per level (see build_tables)
     std::vector<size_t> mdr_off_;
+    bool stack_evalmod_ = std::getenv("AESFHE_STACK_EVALMOD") == nullptr || std::getenv("AESFHE_STACK_EVALMOD")[0] != '0';
     bool double_hoist_ = std::getenv("AESFHE_DOUBLE_HOIST") == nullptr || std::getenv("AESFHE_DOUBLE_HOIST")[0] != '0';
     bool fuse_rr_ = std::getenv("AESFHE_FUSED_RESCALE") == nullptr || std::getenv("AESFHE_FUSED_RESCALE")[0] != '0';
     u32* d_pinv_ = nullptr;

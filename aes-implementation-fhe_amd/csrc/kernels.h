@@ -144,7 +144,7 @@ void launch_rescale_spread(hipStream_t st, const DevTables& T, u32* v, const u32
 // [skip0, skip0 + h) are skipped (the digit's own limbs; 1 << 30 = none).
 // tab: [h][nt] Shoup pairs of (qhat_i mod t); qhinv: [h] Shoup pairs of qhat_i^{-1} mod q_i;
 // negq: [nt] values of (-Q mod t), Q = prod of the h source primes (centred conversion)
-constexpr int kMaxConvGroups = 16;  // ModUp digits (or ModDown polys) x batched ciphertexts
+constexpr int kMaxConvGroups = 24;  // ModUp digits (or ModDown polys) x batched ciphertexts
 constexpr int kMaxConvH = 16;
 struct ConvBatch {
     int n = 0;
