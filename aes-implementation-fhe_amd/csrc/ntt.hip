@@ -23,6 +23,8 @@
 //
 // Rows of one launch are addressed through a RowMap (out-of-place, strided groups), so
 // callers never copy limbs around just to transform them.
+#include <cstdlib>
+
 #include "kernels.h"
 #include "launch.h"
 
@@ -45,6 +47,17 @@ __device__ __forceinline__ void gs_bfly(u32& a, u32& b, u32 w, u32 wp, u32 q) {
 __device__ __forceinline__ int swz(int w) { return w ^ ((w >> 4) & 15); }
 
 enum { kPlain = 0, kSpread = 1, kFinish = 1, kSpread2 = 2 };
+
+// rows below which a launch of 512-thread blocks (8 per row) leaves CUs idle: half-size
+// blocks instead (AESFHE_NTT_SMALL_ROWS overrides, 0 = never)
+inline int small_rows_limit() {
+    static const int v = [] {
+        const char* e = std::getenv("AESFHE_NTT_SMALL_ROWS");
+        return e ? std::atoi(e) : 16;
+    }();
+    return v;
+}
+inline bool small_launch(int rows) { return rows < small_rows_limit(); }
 
 // key-switching ModUp: digit g's own limbs [g alpha, min(nl, (g + 1) alpha)) are not
 // transformed (they are already in NTT form in the input); block-uniform early exit
@@ -76,10 +89,10 @@ __device__ __forceinline__ RowAddr row_addr(u32* dst, const u32* src, const RowM
 // MODE kPlain: x = src row.  MODE kSpread (rescale): the source is one coefficient-form
 // row per group modulo aux.q_last (src row = src_off + g * src_stride, independent of the
 // limb) and x = its centred representative reduced mod the target prime.
-template <int LOGR1, int MODE>
-__global__ void __launch_bounds__(kThreads) k_ntt1_fwd(u32* dst, const u32* src, RowMap rm, LimbMap map, const PrimeConst* pc,
+template <int LOGR1, int MODE, int NT>
+__global__ void __launch_bounds__(NT) k_ntt1_fwd(u32* dst, const u32* src, RowMap rm, LimbMap map, const PrimeConst* pc,
                                                        const uint2* tw, NttAux aux, unsigned long long* ts) {
-    constexpr int LOGN = LOGR1 + 8, R1 = 1 << LOGR1, T = R1 / 16, CB = kThreads / T;
+    constexpr int LOGN = LOGR1 + 8, R1 = 1 << LOGR1, T = R1 / 16, CB = NT / T;
     __shared__ u32 sm[R1 * CB];
     if (skipped(rm)) return;
     ts_begin(ts);
@@ -161,18 +174,18 @@ __global__ void __launch_bounds__(kThreads) k_ntt1_fwd(u32* dst, const u32* src,
 // MODE kPlain: result stored in place.  MODE kFinish (rescale / ModDown): with
 // g = group, i = limb, out[g][i] = (cur[g][i] - x) * qinv_i (+ add_g[i]), rows addressed
 // through aux (cur row g * cur_stride + i, out row g * out_stride + i).
-template <int LOGR1, int MODE>
-__global__ void __launch_bounds__(kThreads) k_ntt2_fwd(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const uint2* tw,
+template <int LOGR1, int MODE, int NT>
+__global__ void __launch_bounds__(NT) k_ntt2_fwd(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const uint2* tw,
                                                        NttAux aux, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8;
-    __shared__ u32 sm[kRowsP2 * kPitchP2];
+    __shared__ u32 sm[(NT / 16) * kPitchP2];
     if (skipped(rm)) return;
     ts_begin(ts);
     const RowAddr ra = row_addr<LOGN>(data, data, rm, map);
     const u32 q = pc[ra.prime].q;
     const uint2* w = tw + ((size_t)ra.prime << LOGN);  // {psi^brv, Shoup companion} pairs
     const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
-    const int R = blockIdx.x * kRowsP2 + r;
+    const int R = blockIdx.x * (NT / 16) + r;
     u32* p = ra.dst + (size_t)R * 256;
     u32 x[16];
 #pragma unroll
@@ -238,18 +251,18 @@ __global__ void __launch_bounds__(kThreads) k_ntt2_fwd(u32* data, RowMap rm, Lim
 }
 
 // ---------------------------------------------------------------- inverse, pass 2 (src -> dst)
-template <int LOGR1>
-__global__ void __launch_bounds__(kThreads) k_ntt2_inv(u32* dst, const u32* src, RowMap rm, LimbMap map, const PrimeConst* pc,
+template <int LOGR1, int NT>
+__global__ void __launch_bounds__(NT) k_ntt2_inv(u32* dst, const u32* src, RowMap rm, LimbMap map, const PrimeConst* pc,
                                                        const uint2* tw, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8;
-    __shared__ u32 sm[kRowsP2 * kPitchP2];
+    __shared__ u32 sm[(NT / 16) * kPitchP2];
     if (skipped(rm)) return;
     ts_begin(ts);
     const RowAddr ra = row_addr<LOGN>(dst, src, rm, map);
     const u32 q = pc[ra.prime].q;
     const uint2* w = tw + ((size_t)ra.prime << LOGN);  // {psi^-brv, Shoup companion} pairs
     const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
-    const int R = blockIdx.x * kRowsP2 + r;
+    const int R = blockIdx.x * (NT / 16) + r;
     u32 x[16];
     const uint4* in = reinterpret_cast<const uint4*>(ra.src + (size_t)R * 256 + 16 * j);
 #pragma unroll
@@ -292,10 +305,10 @@ __global__ void __launch_bounds__(kThreads) k_ntt2_inv(u32* dst, const u32* src,
 }
 
 // ---------------------------------------------------------------- inverse, pass 1 (in place on dst rows)
-template <int LOGR1>
-__global__ void __launch_bounds__(kThreads) k_ntt1_inv(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const uint2* tw,
+template <int LOGR1, int NT>
+__global__ void __launch_bounds__(NT) k_ntt1_inv(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const uint2* tw,
                                                        unsigned long long* ts) {
-    constexpr int LOGN = LOGR1 + 8, R1 = 1 << LOGR1, T = R1 / 16, CB = kThreads / T;
+    constexpr int LOGN = LOGR1 + 8, R1 = 1 << LOGR1, T = R1 / 16, CB = NT / T;
     __shared__ u32 sm[R1 * CB];
     if (skipped(rm)) return;
     ts_begin(ts);
@@ -342,25 +355,44 @@ __global__ void __launch_bounds__(kThreads) k_ntt1_inv(u32* data, RowMap rm, Lim
 template <int LOGR1, int M1, int M2>
 void ntt_fwd_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, int io_rows, RowMap rm, LimbMap map,
                const NttAux& aux) {
-    constexpr int R1 = 1 << LOGR1, CB = kThreads / (R1 / 16);
+    constexpr int R1 = 1 << LOGR1;
     const double row_bytes = 4.0 * 256.0 * R1;
     const double io1 = 2.0 * io_rows * row_bytes;
     const double io2 = (M2 == kFinish ? (3.0 + (aux.add0 ? 0.5 : 0.0) + (aux.add1 ? 0.5 : 0.0)) : 2.0) * io_rows * row_bytes;
     const double bfly = (double)io_rows * 128.0 * R1;  // N / 2 butterflies per stage and row
-    prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, M1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, src,
-                    rm, map, Tb.pc, Tb.tw, aux);
-    prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, rm,
-                    map, Tb.pc, Tb.tw, aux);
+    // launches of few rows: half-size blocks, so that the grid still spreads over every CU
+    if (small_launch(rows)) {
+        constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
+        prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, M1, NT>, dim3(256 / CB, rows), dim3(NT), 0, st, dst, src,
+                        rm, map, Tb.pc, Tb.tw, aux);
+        prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2, NT>, dim3(R1 / (NT / 16), rows), dim3(NT), 0, st, dst,
+                        rm, map, Tb.pc, Tb.tw, aux);
+        return;
+    }
+    constexpr int CB = kThreads / (R1 / 16);
+    prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, M1, kThreads>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst,
+                    src, rm, map, Tb.pc, Tb.tw, aux);
+    prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2, kThreads>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st,
+                    dst, rm, map, Tb.pc, Tb.tw, aux);
 }
 template <int LOGR1>
 void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {
-    constexpr int R1 = 1 << LOGR1, CB = kThreads / (R1 / 16);
+    constexpr int R1 = 1 << LOGR1;
     const double io = 4.0 * 2.0 * rows * (256.0 * R1);  // the inverse is never launched with skips
     const double bfly = (double)rows * 128.0 * R1;
-    prof_launch_tsw(KID_NTT_ROWS_INV, io, bfly * 8.0, k_ntt2_inv<LOGR1>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, src, rm,
+    if (small_launch(rows)) {
+        constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
+        prof_launch_tsw(KID_NTT_ROWS_INV, io, bfly * 8.0, k_ntt2_inv<LOGR1, NT>, dim3(R1 / (NT / 16), rows), dim3(NT), 0, st, dst, src, rm,
+                        map, Tb.pc, Tb.itw);
+        prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, NT>, dim3(256 / CB, rows), dim3(NT), 0, st, dst, rm, map,
+                        Tb.pc, Tb.itw);
+        return;
+    }
+    constexpr int CB = kThreads / (R1 / 16);
+    prof_launch_tsw(KID_NTT_ROWS_INV, io, bfly * 8.0, k_ntt2_inv<LOGR1, kThreads>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, src,
+                    rm, map, Tb.pc, Tb.itw);
+    prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, kThreads>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, rm,
                     map, Tb.pc, Tb.itw);
-    prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, rm, map,
-                    Tb.pc, Tb.itw);
 }
 
 }  // namespace
