@@ -30,5 +30,7 @@ class AddRoundKey:
         self.xor4 = xor4
 
     def __call__(self, ct_hi, ct_lo, key_hi, key_lo, out_level=None) -> Tuple[Any, Any]:
+        if hasattr(self.xor4, "apply_pair"):
+            return self.xor4.apply_pair(ct_hi, key_hi, ct_lo, key_lo, out_level)
         return pair(self.xor4.ctx, lambda: self.xor4.apply(ct_hi, key_hi, out_level),
                     lambda: self.xor4.apply(ct_lo, key_lo, out_level))

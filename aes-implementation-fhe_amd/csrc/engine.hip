@@ -1332,6 +1332,136 @@ public:
         return o;
     }
 
+    // n independent products a_i b_i, relinearised and rescaled, batched:
+    // pairs whose aligned operands sit at one level share ONE tensor launch and one fused
+    // relinearisation + rescale per chunk of kMaxKsBatch members (each key residue read once
+    // per chunk, every launch carrying the chunk's rows); the results equal n mul() calls
+    std::vector<Ct> mul_many(const std::vector<const Ct*>& A, const std::vector<const Ct*>& B) {
+        const int n = (int)A.size();
+        std::vector<Ct> out(n);
+        bool batch = batch_ops_ && n >= 2;
+        for (int i = 0; i < n; ++i) {
+            if (vis_npoly(*A[i]) != 2 || vis_npoly(*B[i]) != 2) throw std::runtime_error("multiply expects 2-polynomial ciphertexts");
+            if (A[i]->level - A[i]->pend < 1 || B[i]->level - B[i]->pend < 1)
+                throw std::runtime_error("not enough level to multiply (level 0)");
+            batch = batch && A[i]->nb == 1 && B[i]->nb == 1;
+        }
+        if (!batch) {
+            for (int i = 0; i < n; ++i) out[i] = mul(*A[i], *B[i], true, false);
+            return out;
+        }
+        struct Prep {
+            Ct a, b, x, y;
+            bool oa = false, ob = false, fa = false, fb = false;
+        };
+        std::vector<Prep> pr(n);
+        for (int i = 0; i < n; ++i) {
+            Prep& P = pr[i];
+            P.a = normalize(*A[i]);
+            P.b = B[i]->data == A[i]->data ? P.a : normalize(*B[i]);
+            P.oa = P.a.data != A[i]->data;
+            P.ob = P.b.data != B[i]->data && P.b.data != P.a.data;
+            auto xy = align(P.a, P.b, P.fa, P.fb, true);
+            P.x = xy.first, P.y = xy.second;
+        }
+        auto drop = [&](Prep& P) {
+            if (P.fa) release(P.x);
+            if (P.fb && P.y.data != P.x.data) release(P.y);
+            if (P.oa) release(P.a);
+            if (P.ob) release(P.b);
+        };
+        std::vector<bool> done(n, false);
+        for (int i = 0; i < n; ++i) {
+            if (done[i]) continue;
+            std::vector<int> grp;  // members at the same level, up to kMaxMembers
+            for (int j = i; j < n && (int)grp.size() < kMaxMembers; ++j)
+                if (!done[j] && pr[j].x.level == pr[i].x.level) grp.push_back(j), done[j] = true;
+            const int g = (int)grp.size(), L = pr[i].x.level, nl = hp_.nl(L), nn = hp_.n;
+            Ct d = alloc_ct(L, 3 * g, g);
+            d.pend = 1;
+            TensorPtrs tp;
+            for (int m = 0; m < g; ++m) tp.a[m] = pr[grp[m]].x.data, tp.b[m] = pr[grp[m]].y.data;
+            launch_tensor_ptrs(S(), T_, d.data, tp, g, nl, qmap());
+            cnt_[C_MUL] += g;
+            for (int m = 0; m < g; ++m) drop(pr[grp[m]]);
+            for (int m0 = 0; m0 < g; m0 += kMaxKsBatch) {
+                const int c = std::min(kMaxKsBatch, g - m0);
+                Ct v = d;  // view of members m0 .. m0 + c - 1 (not released on its own)
+                v.data = d.data + (size_t)m0 * 3 * nl * nn, v.npoly = 3 * c, v.nb = c, v.words = (size_t)3 * c * nl * nn;
+                Ct o;
+                if (fused_relin_rescale_ok(v)) {
+                    o = relin_rescale(v);
+                } else {
+                    Ct r = relin_raw(v);
+                    o = rescale(r);
+                    release(r);
+                }
+                unstack(o, &out[0], grp.data() + m0);
+                release(o);
+            }
+            release(d);
+        }
+        return out;
+    }
+    // members of a stacked canonical ciphertext -> separate ciphertexts out[idx[m]]
+    void unstack(const Ct& o, Ct* out, const int* idx) {
+        const int c = o.nb, nlo = hp_.nl(o.level), nn = hp_.n, per = o.npoly / c;
+        MemberPtrs mp;
+        for (int m = 0; m < c; ++m) {
+            Ct r = alloc_ct(o.level, per);
+            copy_meta(r, o);
+            r.nb = 1;
+            mp.src[m] = o.data + (size_t)m * per * nlo * nn;
+            mp.dst[m] = r.data;
+            out[idx[m]] = r;
+        }
+        launch_copy_members(S(), T_, mp, c, per * nlo);
+    }
+    // X -> X^g of n independent ciphertexts: canonical inputs at one level are stacked and key
+    // switched together (chunks of kMaxKsBatch); results equal n galois() calls
+    std::vector<Ct> galois_many(const std::vector<const Ct*>& C, u64 g) {
+        const int n = (int)C.size();
+        std::vector<Ct> out(n);
+        std::vector<Ct> cn(n);
+        std::vector<bool> own(n), done(n, false);
+        for (int i = 0; i < n; ++i) {
+            if (vis_npoly(*C[i]) != 2) throw std::runtime_error("rotation/conjugation expects a 2-polynomial ciphertext");
+            cn[i] = normalize(*C[i]);
+            own[i] = cn[i].data != C[i]->data;
+        }
+        for (int i = 0; i < n; ++i) {
+            if (done[i]) continue;
+            std::vector<int> grp;
+            for (int j = i; j < n && (int)grp.size() < kMaxKsBatch; ++j)
+                if (!done[j] && batch_ops_ && cn[j].level == cn[i].level && cn[j].nb == 1 && cn[i].nb == 1) grp.push_back(j), done[j] = true;
+            if (grp.size() < 2) {
+                done[i] = true;
+                out[i] = galois(cn[i], g);
+                for (int j : grp) if (j != i) done[j] = false;
+                continue;
+            }
+            const int c = (int)grp.size(), nl = hp_.nl(cn[i].level), nn = hp_.n;
+            Ct st = alloc_ct(cn[i].level, 2 * c, c);
+            copy_meta(st, cn[i]);
+            st.nb = c;
+            MemberPtrs mp;
+            for (int m = 0; m < c; ++m) mp.src[m] = cn[grp[m]].data, mp.dst[m] = st.data + (size_t)m * 2 * nl * nn;
+            launch_copy_members(S(), T_, mp, c, 2 * nl);
+            Ct o = galois(st, g);
+            release(st);
+            unstack(o, &out[0], grp.data());
+            release(o);
+        }
+        for (int i = 0; i < n; ++i)
+            if (own[i]) release(cn[i]);
+        return out;
+    }
+
+    std::vector<Ct> conjugate_many(const std::vector<const Ct*>& C) {
+        cnt_[C_CONJ] += C.size();
+        return galois_many(C, conj_galois());
+    }
+
     Ct relinearize(const Ct& c_in) {
         if (vis_npoly(c_in) != 3) throw std::runtime_error("relinearize: ciphertext should have 3 polynomials");
         Ct c = ensure_ntt(c_in);
@@ -1378,11 +1508,20 @@ public:
                                      std::to_string(x.level));
         std::vector<aesfhe_handle> pw(degree + 1, 0);
         pw[1] = put_ct(copy(x));
-        for (int k = 2; k <= degree; ++k) {
-            int t = 1;
-            while ((t << 1) <= k) t <<= 1;
-            if (t == k) pw[k] = put_ct(mul(ct(pw[t / 2]), ct(pw[t / 2]), true));
-            else pw[k] = put_ct(mul(ct(pw[t]), ct(pw[k - t]), true));
+        // x^k = x^h x^(k - h), h the largest power of two below k; the products of one depth
+        // (k in (h, 2h]) only read lower depths, so each depth is one mul_many batch
+        for (int h = 1; h < degree; h *= 2) {
+            const int hi = std::min(2 * h, degree);
+            for (int k0 = h + 1; k0 <= hi; k0 += kMaxMembers) {
+                std::vector<const Ct*> A, B;
+                const int k1 = std::min(hi, k0 + kMaxMembers - 1);
+                for (int k = k0; k <= k1; ++k) {
+                    A.push_back(&ct(pw[h]));
+                    B.push_back(&ct(pw[k - h]));
+                }
+                std::vector<Ct> r = mul_many(A, B);
+                for (int k = k0; k <= k1; ++k) pw[k] = put_ct(r[k - k0]);
+            }
         }
         for (int k = 1; k <= degree; ++k) out[k - 1] = pw[k];
     }
@@ -2418,6 +2557,7 @@ private:
     std::vector<size_t> moddown_off_;
     u32* d_mdr_ = nullptr;       // ModDown fused with the rescale, per level (see build_tables)
     std::vector<size_t> mdr_off_;
+    bool batch_ops_ = std::getenv("AESFHE_BATCH_OPS") == nullptr || std::getenv("AESFHE_BATCH_OPS")[0] != '0';
     bool stack_evalmod_ = std::getenv("AESFHE_STACK_EVALMOD") == nullptr || std::getenv("AESFHE_STACK_EVALMOD")[0] != '0';
     bool double_hoist_ = std::getenv("AESFHE_DOUBLE_HOIST") == nullptr || std::getenv("AESFHE_DOUBLE_HOIST")[0] != '0';
     bool fuse_rr_ = std::getenv("AESFHE_FUSED_RESCALE") == nullptr || std::getenv("AESFHE_FUSED_RESCALE")[0] != '0';
@@ -2627,6 +2767,24 @@ int aesfhe_rescale(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) {
 int aesfhe_level_down(aesfhe_ctx* ctx, aesfhe_handle c, int level, aesfhe_handle* out) { CT_OP(e.level_down(e.canon(c), level)) }
 int aesfhe_rotate(aesfhe_ctx* ctx, aesfhe_handle c, int steps, aesfhe_handle* out) { CT_OP(e.rotate(e.canon(c), steps)) }
 int aesfhe_conjugate(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.conjugate(e.canon(c))) }
+int aesfhe_mul_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* a, const aesfhe_handle* b, aesfhe_handle* out) {
+    API_BEGIN Engine& e = *ctx->eng;
+    if (n < 0 || (n > 0 && (!a || !b || !out))) throw std::runtime_error("mul_many: bad arguments");
+    std::vector<const Ct*> A(n), B(n);
+    for (int i = 0; i < n; ++i) A[i] = &e.canon(a[i]), B[i] = &e.canon(b[i]);
+    std::vector<Ct> r = e.mul_many(A, B);
+    for (int i = 0; i < n; ++i) out[i] = e.put_ct(r[i]);
+    API_END
+}
+int aesfhe_conjugate_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, aesfhe_handle* out) {
+    API_BEGIN Engine& e = *ctx->eng;
+    if (n < 0 || (n > 0 && (!in || !out))) throw std::runtime_error("conjugate_many: bad arguments");
+    std::vector<const Ct*> C(n);
+    for (int i = 0; i < n; ++i) C[i] = &e.canon(in[i]);
+    std::vector<Ct> r = e.conjugate_many(C);
+    for (int i = 0; i < n; ++i) out[i] = e.put_ct(r[i]);
+    API_END
+}
 int aesfhe_power_basis(aesfhe_ctx* ctx, aesfhe_handle c, int degree, aesfhe_handle* out) {
     API_BEGIN ctx->eng->power_basis(c, degree, out);
     API_END

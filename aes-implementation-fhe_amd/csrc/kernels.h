@@ -107,6 +107,21 @@ void launch_sub(hipStream_t st, const DevTables& T, u32* out, const u32* a, cons
 void launch_neg(hipStream_t st, const DevTables& T, u32* out, const u32* a, int rows, int nl, LimbMap map);
 // out = in over `rows` rows of N words (device to device)
 void launch_copy_rows(hipStream_t st, const DevTables& T, u32* out, const u32* in, size_t rows);
+// n (<= kMaxMembers) independent copies of `rows` rows each: dst[m] = src[m] (one launch;
+// stacking / unstacking batched ciphertexts)
+constexpr int kMaxMembers = 8;
+struct MemberPtrs {
+    const u32* src[kMaxMembers] = {};
+    u32* dst[kMaxMembers] = {};
+};
+void launch_copy_members(hipStream_t st, const DevTables& T, const MemberPtrs& mp, int n, int rows);
+// tensor products of n independent pairs (a[m], b[m]: 2 x nl rows each) into one stacked
+// [m][3][nl] output (mul_many)
+struct TensorPtrs {
+    const u32* a[kMaxMembers] = {};
+    const u32* b[kMaxMembers] = {};
+};
+void launch_tensor_ptrs(hipStream_t st, const DevTables& T, u32* out, const TensorPtrs& tp, int n, int nl, LimbMap map);
 // out = (a0 b0, a0 b1 + a1 b0, a1 b1); a, b: 2 x nl rows; out: 3 x nl rows
 // nb > 1: nb ciphertexts stacked ([m][2][nl] in, [m][3][nl] out), one launch
 void launch_tensor(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int nl, LimbMap map, int nb = 1);

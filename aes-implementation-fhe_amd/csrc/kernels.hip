@@ -59,6 +59,25 @@ __global__ void k_copy_rows(uint4* out, const uint4* in, int logn) {
     const size_t i = ((size_t)blockIdx.y << (logn - 2)) + (size_t)blockIdx.x * kBlock + threadIdx.x;
     out[i] = in[i];
 }
+__global__ void k_copy_members(MemberPtrs mp, int logn) {
+    const size_t i = ((size_t)blockIdx.y << (logn - 2)) + (size_t)blockIdx.x * kBlock + threadIdx.x;
+    reinterpret_cast<uint4*>(mp.dst[blockIdx.z])[i] = reinterpret_cast<const uint4*>(mp.src[blockIdx.z])[i];
+}
+__global__ void k_tensor_ptrs(u32* out, TensorPtrs tp, int nl, LimbMap map, const PrimeConst* pc, int logn) {
+    const int row = blockIdx.y;
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const int m = row / nl, limb = row - m * nl;
+    const PrimeConst P = pc[map.prime(limb)];
+    const size_t off = (size_t)nl << logn, idx = ((size_t)limb << logn) + k;
+    const u32* a = tp.a[m];
+    const u32* b = tp.b[m];
+    out += (size_t)m * 3 * off;
+    const u32 q = P.q, mu = P.mu;
+    const u32 a0 = a[idx], a1 = a[idx + off], b0 = b[idx], b1 = b[idx + off];
+    out[idx] = barrett_mul(a0, b0, q, mu);
+    out[idx + off] = add_mod(barrett_mul(a0, b1, q, mu), barrett_mul(a1, b0, q, mu), q);
+    out[idx + 2 * off] = barrett_mul(a1, b1, q, mu);
+}
 __global__ void k_neg(u32* out, const u32* a, int nl, LimbMap map, const PrimeConst* pc, int logn) {
     EW_PROLOGUE
     u32 v = a[idx];
@@ -656,6 +675,17 @@ void launch_copy_rows(hipStream_t st, const DevTables& T, u32* out, const u32* i
     if (rows > 65535) throw std::runtime_error("launch_copy_rows: too many rows");
     prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows), k_copy_rows, dim3((1u << T.logn) / (4 * kBlock), (unsigned)rows), dim3(kBlock), 0, st,
                 reinterpret_cast<uint4*>(out), reinterpret_cast<const uint4*>(in), T.logn);
+}
+void launch_copy_members(hipStream_t st, const DevTables& T, const MemberPtrs& mp, int n, int rows) {
+    if (n <= 0 || rows <= 0) return;
+    if (n > kMaxMembers) throw std::runtime_error("launch_copy_members: too many members");
+    prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * n * rows), k_copy_members, dim3((1u << T.logn) / (4 * kBlock), rows, n), dim3(kBlock), 0,
+                st, mp, T.logn);
+}
+void launch_tensor_ptrs(hipStream_t st, const DevTables& T, u32* out, const TensorPtrs& tp, int n, int nl, LimbMap map) {
+    if (n <= 0 || n > kMaxMembers) throw std::runtime_error("launch_tensor_ptrs: 1..8 products");
+    prof_launch(KID_TENSOR, words(7.0 * n * nl * (1u << T.logn)), k_tensor_ptrs, ew_grid(T.logn, n * nl), dim3(kBlock), 0, st, out, tp, nl,
+                map, T.pc, T.logn);
 }
 void launch_neg(hipStream_t st, const DevTables& T, u32* out, const u32* a, int rows, int nl, LimbMap map) {
     prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows), k_neg, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, nl, map, T.pc, T.logn);

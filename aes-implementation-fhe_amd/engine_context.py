@@ -104,6 +104,14 @@ class EngineContext:
     def conjugate(self, ct):
         return self.engine.conjugate(ct, self.conjugation_key)
 
+    # batched variants (include/aesfhe.h aesfhe_mul_many / aesfhe_conjugate_many): independent
+    # products / conjugations stacked into shared launches; results equal the separate calls
+    def multiply_many(self, pairs):
+        return self.engine.multiply_many(pairs)
+
+    def conjugate_many(self, cts):
+        return self.engine.conjugate_many(cts)
+
     def rotate(self, ct, steps: int):
         """np.roll(slots, steps) semantics."""
         return self.engine.rotate(ct, self.rotation_key, steps)

@@ -47,6 +47,12 @@ class InvMixColumnsFHE:
             out = ctx.add(out, ctx.rotate(ctx.multiply(ct, mask), k_rows * self.stride))
         return out
 
+    def _xor_pair(self, a, b, out_level=None):
+        """(XOR4(a_hi, b_hi), XOR4(a_lo, b_lo)), batched when the XOR4 has apply_pair"""
+        if hasattr(self.xor4, "apply_pair"):
+            return self.xor4.apply_pair(a[0], b[0], a[1], b[1], out_level)
+        return pair(self.ctx, lambda: self._xor(a[0], b[0], out_level), lambda: self._xor(a[1], b[1], out_level))
+
     def _gf(self, mult, hi, lo, out_level=None):
         return gf_mult_pair(self.ctx, self._coeffs, mult, hi, lo, out_level)
 
@@ -81,14 +87,13 @@ class InvMixColumnsFHE:
         e9 = self.gf_mult_9(*rot[3])
         log("mul9", e9)
         fl = self._xor_level
-        acc = pair(self.ctx, lambda: self._xor(e14[0], e11[0], fl), lambda: self._xor(e14[1], e11[1], fl))
+        acc = self._xor_pair(e14, e11, fl)
         log("acc1", acc)
         acc = self._renorm_pair(*acc, level=NEED_XOR)  # internal: only the next XOR4 reads it
-        acc = pair(self.ctx, lambda: self._xor(acc[0], e13[0], fl), lambda: self._xor(acc[1], e13[1], fl))
+        acc = self._xor_pair(acc, e13, fl)
         log("acc2", acc)
         acc = self._renorm_pair(*acc, level=NEED_XOR)
-        out = self._renorm_pair(*pair(self.ctx, lambda: self._xor(acc[0], e9[0], fl), lambda: self._xor(acc[1], e9[1], fl)),
-                                level=NEED_BOOTSTRAP if do_final_bootstrap else None)
+        out = self._renorm_pair(*self._xor_pair(acc, e9, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
         if do_final_bootstrap:
             out = bootstrap2(self.ctx, out[0], out[1])
         log("out", out)

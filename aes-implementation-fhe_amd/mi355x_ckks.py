@@ -35,6 +35,7 @@ EXPORTED = [
     "aesfhe_level", "aesfhe_plaintext", "aesfhe_encrypt", "aesfhe_decrypt", "aesfhe_add", "aesfhe_sub",
     "aesfhe_add_pt", "aesfhe_add_scalar", "aesfhe_mul_scalar", "aesfhe_mul_pt", "aesfhe_mul",
     "aesfhe_relinearize", "aesfhe_rescale", "aesfhe_level_down", "aesfhe_rotate", "aesfhe_conjugate",
+    "aesfhe_mul_many", "aesfhe_conjugate_many",
     "aesfhe_power_basis", "aesfhe_to_ntt", "aesfhe_to_intt", "aesfhe_bootstrap", "aesfhe_bootstrap_pair", "aesfhe_renorm_pair", "aesfhe_renorm_states", "aesfhe_renorm_at",
     "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
     "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
@@ -84,6 +85,7 @@ def load_library(path: Optional[Path] = None):
         "aesfhe_relinearize": [vp, _H, _Hp], "aesfhe_rescale": [vp, _H, _Hp],
         "aesfhe_level_down": [vp, _H, c_int, _Hp], "aesfhe_rotate": [vp, _H, c_int, _Hp],
         "aesfhe_conjugate": [vp, _H, _Hp], "aesfhe_power_basis": [vp, _H, c_int, _Hp],
+        "aesfhe_mul_many": [vp, c_int, _Hp, _Hp, _Hp], "aesfhe_conjugate_many": [vp, c_int, _Hp, _Hp],
         "aesfhe_to_ntt": [vp, _H, _Hp], "aesfhe_to_intt": [vp, _H, _Hp], "aesfhe_bootstrap": [vp, _H, _Hp],
         "aesfhe_renorm_pair": [vp, _H, _H, _Hp, _Hp],
         "aesfhe_bootstrap_pair": [vp, _H, _H, _Hp, _Hp],
@@ -442,6 +444,28 @@ class Engine:
 
     def conjugate(self, ct, conjugation_key=None):
         return self._new(self._lib.aesfhe_conjugate, ct.handle)
+
+    # batched variants (include/aesfhe.h, DESIGN.md §3.12): results equal the separate calls
+    def multiply_many(self, pairs) -> List[Ciphertext]:
+        """[a * b (relinearised, rescaled) for a, b in pairs] as one batched engine call"""
+        pairs = list(pairs)
+        n = len(pairs)
+        if n == 0:
+            return []
+        H = ctypes.c_uint64 * n
+        a, b, out = H(*[p[0].handle for p in pairs]), H(*[p[1].handle for p in pairs]), H()
+        self._ctx.check(self._lib.aesfhe_mul_many(self._ctx.ptr, n, a, b, out))
+        return [Ciphertext(self._ctx, out[i]) for i in range(n)]
+
+    def conjugate_many(self, cts) -> List[Ciphertext]:
+        cts = list(cts)
+        n = len(cts)
+        if n == 0:
+            return []
+        H = ctypes.c_uint64 * n
+        src, out = H(*[c.handle for c in cts]), H()
+        self._ctx.check(self._lib.aesfhe_conjugate_many(self._ctx.ptr, n, src, out))
+        return [Ciphertext(self._ctx, out[i]) for i in range(n)]
 
     def rotate(self, ct, rotation_key=None, delta: int = 0):
         """np.roll(slots, delta)."""

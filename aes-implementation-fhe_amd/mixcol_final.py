@@ -15,7 +15,7 @@ import numpy as np
 
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
-from xor4_lut import XOR4LUT, SplitLUT2, powers, std_basis
+from xor4_lut import XOR4LUT, SplitLUT2, batched, eval_two, joint_bases, powers, std_basis
 from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap2, drop_to, fused_lut, pair
 
 
@@ -102,16 +102,24 @@ def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo, out_level=Non
     if getattr(ctx, "fused_luts", False):
         sh, sl = cache.split(mult, "hi"), cache.split(mult, "lo")
         try:
-            A, B = pair(ctx, lambda: powers(ctx, ct_hi, sh.need_a | sl.need_a),
-                        lambda: std_basis(ctx, ct_lo, sh.need_b | sl.need_b))
+            if batched(ctx):  # one pair of bases, products / conjugations batched
+                A, B = joint_bases(ctx, [(ct_hi, sh.need_a | sl.need_a, "pow"), (ct_lo, sh.need_b | sl.need_b, "std")])
+            else:
+                A, B = pair(ctx, lambda: powers(ctx, ct_hi, sh.need_a | sl.need_a),
+                            lambda: std_basis(ctx, ct_lo, sh.need_b | sl.need_b))
         except RuntimeError as e:
             if "level" not in str(e):
                 raise
         else:
-            out = pair(ctx, lambda: sh.eval(ctx, ("gf", mult, "hi"), A, B), lambda: sl.eval(ctx, ("gf", mult, "lo"), A, B),
-                       shared=(*A.values(), *B.values()))
-            if out[0] is not None and out[1] is not None:
-                return out
+            if batched(ctx):
+                out = eval_two(ctx, (sh, ("gf", mult, "hi"), A, B), (sl, ("gf", mult, "lo"), A, B))
+                if out is not None:
+                    return out
+            else:
+                out = pair(ctx, lambda: sh.eval(ctx, ("gf", mult, "hi"), A, B), lambda: sl.eval(ctx, ("gf", mult, "lo"), A, B),
+                           shared=(*A.values(), *B.values()))
+                if out[0] is not None and out[1] is not None:
+                    return out
     return pair(ctx, lambda: gf_eval(ctx, cache, mult, "hi", ct_hi, ct_lo),
                 lambda: gf_eval(ctx, cache, mult, "lo", ct_hi, ct_lo), shared=(ct_hi, ct_lo))
 
@@ -153,6 +161,12 @@ class MixColFinal:
     def _xor_ct(self, a, b, out_level=None):
         return self.xor4.apply(a, b, out_level)
 
+    def _xor_pair(self, a, b, out_level=None):
+        """(XOR4(a_hi, b_hi), XOR4(a_lo, b_lo))"""
+        if hasattr(self.xor4, "apply_pair"):
+            return self.xor4.apply_pair(a[0], b[0], a[1], b[1], out_level)
+        return pair(self.ctx, lambda: self._xor_ct(a[0], b[0], out_level), lambda: self._xor_ct(a[1], b[1], out_level))
+
     def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
         log = (lambda k, v: debug.__setitem__(k, v)) if isinstance(debug, dict) else (lambda k, v: None)
         rh, rl = pair(self.ctx, lambda: [self._col_shift_rowmajor(ct_hi, k) for k in (1, 2, 3)],
@@ -168,16 +182,14 @@ class MixColFinal:
         thr = self.gf_mult_3(*rot[1], out_level=fl + LUT2_DEPTH)
         log("two", two)
         log("thr", thr)
-        acc = pair(self.ctx, lambda: self._xor_ct(two[0], thr[0], fl), lambda: self._xor_ct(two[1], thr[1], fl))
+        acc = self._xor_pair(two, thr, fl)
         log("acc1", acc)
         acc = self._renorm_pair(*acc, level=NEED_XOR)  # internal: only the next XOR4 reads it
-        acc = pair(self.ctx, lambda: self._xor_ct(acc[0], rot[2][0], fl), lambda: self._xor_ct(acc[1], rot[2][1], fl))
+        acc = self._xor_pair(acc, rot[2], fl)
         log("acc2", acc)
         acc = self._renorm_pair(*acc, level=NEED_XOR)
         # the output is bootstrapped next (from level 0) or returned at the fresh level
-        acc = self._renorm_pair(*pair(self.ctx, lambda: self._xor_ct(acc[0], rot[3][0], fl),
-                                      lambda: self._xor_ct(acc[1], rot[3][1], fl)),
-                                level=NEED_BOOTSTRAP if do_final_bootstrap else None)
+        acc = self._renorm_pair(*self._xor_pair(acc, rot[3], fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
         log("acc3", acc)
         out_hi, out_lo = acc
         if do_final_bootstrap:

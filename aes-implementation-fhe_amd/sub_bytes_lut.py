@@ -21,7 +21,7 @@ Evaluation forms (same polynomials, same output level, outputs equal up to CKKS 
 from typing import Any, Dict, Tuple
 
 import numpy as np
-from utils import SUBBYTES_DEPTH, drop_to, fused_lut, pair
+from utils import SUBBYTES_DEPTH, conj_many, drop_to, fused_lut, mul_many, pair
 
 _TOL = 1e-12
 
@@ -134,8 +134,16 @@ class SubBytesLUTFastCached:
         pw = ctx.make_power_basis(ct_b, 16)
         baby = {k: pw[k - 1] for k in range(1, 16)}
         g = {1: pw[15]}
-        for i, (u, v) in ((2, (1, 1)), (4, (2, 2)), (3, (1, 2)), (5, (1, 4)), (6, (2, 4)), (7, (3, 4)), (8, (4, 4))):
-            g[i] = ctx.multiply(g[u], g[v])  # depth: G_2 +1, G_3 / G_4 +2, G_5..G_8 +3 over b^16
+        batch = getattr(ctx, "multiply_many", None) is not None
+        if batch:  # one mul_many per depth
+            for stage in (((2, (1, 1)),), ((3, (1, 2)), (4, (2, 2))), ((5, (1, 4)), (6, (2, 4)), (7, (3, 4)), (8, (4, 4)))):
+                for (i, _), r in zip(stage, mul_many(ctx, [(g[u], g[v]) for _, (u, v) in stage])):
+                    g[i] = r
+        else:
+            for i, (u, v) in ((2, (1, 1)), (4, (2, 2)), (3, (1, 2)), (5, (1, 4)), (6, (2, 4)), (7, (3, 4)), (8, (4, 4))):
+                g[i] = ctx.multiply(g[u], g[v])  # depth: G_2 +1, G_3 / G_4 +2, G_5..G_8 +3 over b^16
+        if batch:
+            return self._outputs_batched(baby, g, ct_b)
 
         # 3) out = P(b) + conj(Q(b)) per output nibble
         def lut(which):
@@ -144,6 +152,38 @@ class SubBytesLUTFastCached:
                            ctx.conjugate(self._poly_bsgs((which, "q"), Q, baby, g, ct_b)))
 
         return pair(ctx, lambda: lut("hi"), lambda: lut("lo"), shared=(*baby.values(), *g.values()))
+
+    def _outputs_batched(self, baby, g, ct_b):
+        """both output nibbles: every chunk sum S_i (one fused kernel each), ALL the products
+        S_i G_i of both outputs in mul_many batches, the two conj(Q) in one conj_many"""
+        ctx = self.ctx
+        terms, prods = {}, []
+        for which in ("hi", "lo"):
+            for part, coef in zip(("p", "q"), self._bsgs[which]):
+                terms[(which, part)] = []
+                for i in range((len(coef) + 15) // 16):
+                    chunk = np.zeros(16, np.complex128)
+                    seg = coef[16 * i: 16 * i + 16]
+                    chunk[: len(seg)] = seg
+                    if not np.any(chunk):
+                        continue
+                    key = ((which, part), i)
+                    if i == 0:
+                        terms[(which, part)].append(self._lin(key, np.r_[0, chunk[1:]], baby, chunk[0], ct_b))
+                    elif not np.any(chunk[1:]):
+                        terms[(which, part)].append(ctx.multiply(g[i], complex(chunk[0])))
+                    else:
+                        prods.append(((which, part), self._lin(key, np.r_[0, chunk[1:]], baby, chunk[0], ct_b), g[i]))
+        for (wp, _, _), r in zip(prods, mul_many(ctx, [(s_, g_) for _, s_, g_ in prods])):
+            terms[wp].append(r)
+        acc = {}
+        for wp, ts in terms.items():
+            a = ts[0] if ts else ctx.multiply(ct_b, 0.0)
+            for t in ts[1:]:
+                a = ctx.add(a, t)
+            acc[wp] = a
+        cq = conj_many(ctx, [acc[("hi", "q")], acc[("lo", "q")]])
+        return ctx.add(acc[("hi", "p")], cq[0]), ctx.add(acc[("lo", "p")], cq[1])
 
     # ------------------------------------------------------------------ direct (reference) form
     def _apply_direct(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:

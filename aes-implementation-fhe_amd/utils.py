@@ -74,6 +74,25 @@ def bootstrap2(ctx, a, b):
     return pair(ctx, lambda: ctx.bootstrap(ctx.to_intt(a)), lambda: ctx.bootstrap(ctx.to_intt(b)))
 
 
+def mul_many(ctx, pairs):
+    """[ctx.multiply(a, b) for a, b in pairs] as one batched engine call when the context has
+    it (identical results)"""
+    pairs = list(pairs)
+    f = getattr(ctx, "multiply_many", None)
+    if f is not None and len(pairs) > 1:
+        return f(pairs)
+    return [ctx.multiply(a, b) for a, b in pairs]
+
+
+def conj_many(ctx, cts):
+    """[ctx.conjugate(c) for c in cts], batched like mul_many"""
+    cts = list(cts)
+    f = getattr(ctx, "conjugate_many", None)
+    if f is not None and len(cts) > 1:
+        return f(cts)
+    return [ctx.conjugate(c) for c in cts]
+
+
 def fused_lut(ctx, key, coeffs, a, b=None, c0: complex = 0j):
     """The LUT sum sum_{p,q} C[p,q] a[p] b[q] (b given) or c0 + sum_k C[k] a[k] as one engine
     call, or None when the context has no fused form or the elements sit too

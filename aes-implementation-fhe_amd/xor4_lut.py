@@ -17,7 +17,7 @@ x^8 are skipped for XOR4), and each S is one fused kernel.  Output level unchang
 from typing import Any, Dict
 
 import numpy as np
-from utils import LUT2_DEPTH, drop_to, fused_lut, pair
+from utils import LUT2_DEPTH, conj_many, drop_to, fused_lut, mul_many, pair
 
 
 def basis16(ctx, ct, *, retry_intt: bool = True) -> Dict[int, Any]:
@@ -76,6 +76,38 @@ def powers(ctx, ct, need) -> Dict[int, Any]:
     return {k: pw[k] for k in need}
 
 
+def _depth(k: int) -> int:
+    return (k - 1).bit_length()  # ceil(log2 k): the multiplicative depth of x^k
+
+
+def joint_bases(ctx, specs):
+    """[(ct, need, kind)] -> [{k: element}], kind "pow" (powers(), x^k) or "std" (std_basis():
+    conj(x^(16-q)) for q >= 9).  The products of one depth across ALL inputs form one
+    mul_many batch and every conjugation one conj_many batch; the elements
+    equal powers() / std_basis() of each input."""
+    needs = [set(need) if kind == "pow" else {q if q <= 8 else 16 - q for q in need} for _, need, kind in specs]
+    pws = [{1: ct} for ct, _, _ in specs]
+    chains = [_chain(n) for n in needs]
+    top = max((_depth(k) for ch in chains for k, _, _ in ch), default=0)
+    for d in range(1, top + 1):
+        jobs = [(i, k, u, v) for i, ch in enumerate(chains) for k, u, v in ch if _depth(k) == d]
+        for (i, k, _, _), r in zip(jobs, mul_many(ctx, [(pws[i][u], pws[i][v]) for i, _, u, v in jobs])):
+            pws[i][k] = r
+    for i, (ct, _, _) in enumerate(specs):
+        if 0 in needs[i]:
+            pws[i][0] = ctx.add_plain(ctx.multiply(ct, 0.0), 1.0)
+    out = [{k: pws[i][k] for k in (need if kind == "pow" else [q for q in need if q <= 8])}
+           for i, (_, need, kind) in enumerate(specs)]
+    cj = [(i, q) for i, (_, need, kind) in enumerate(specs) if kind == "std" for q in sorted(need) if q >= 9]
+    for (i, q), c in zip(cj, conj_many(ctx, [pws[i][16 - q] for i, q in cj])):
+        out[i][q] = c
+    return out
+
+
+def batched(ctx) -> bool:
+    return getattr(ctx, "multiply_many", None) is not None
+
+
 def std_basis(ctx, ct, need) -> Dict[int, Any]:
     """{q: B[q]} for q in need, B[q] = x^q (q <= 8), conj(x^(16-q)) (q >= 9)"""
     pos = powers(ctx, ct, {q if q <= 8 else 16 - q for q in need})
@@ -99,7 +131,14 @@ class SplitLUT2:
         self.has2 = bool(np.any(self.c2))
 
     def bases(self, ctx, a, b):
+        if batched(ctx):
+            A, B = joint_bases(ctx, [(a, self.need_a, "pow"), (b, self.need_b, "std")])
+            return A, B
         return pair(ctx, lambda: powers(ctx, a, self.need_a), lambda: std_basis(ctx, b, self.need_b))
+
+    def eval_pair(self, ctx, key, AB0, AB1):
+        """(eval(A0, B0), eval(A1, B1)) with the two conjugations batched"""
+        return eval_two(ctx, (self, key, *AB0), (self, key, *AB1))
 
     def eval(self, ctx, key, A, B):
         s1 = fused_lut(ctx, (key, 1), self.c1, A, B)
@@ -109,6 +148,23 @@ class SplitLUT2:
             return s1
         s2 = fused_lut(ctx, (key, 2), self.c2, A, B)
         return None if s2 is None else ctx.add(s1, ctx.conjugate(s2))
+
+
+def eval_two(ctx, j0, j1):
+    """two split-LUT evaluations j = (split, key, A, B) as S1 + conj(S2) each, the two
+    conjugations in one conj_many batch; None if a fused sum is unavailable (level)"""
+    out, s2 = [], []
+    for sp, key, A, B in (j0, j1):
+        s1 = fused_lut(ctx, (key, 1), sp.c1, A, B)
+        t2 = fused_lut(ctx, (key, 2), sp.c2, A, B) if sp.has2 else None
+        if s1 is None or (sp.has2 and t2 is None):
+            return None
+        out.append(s1)
+        s2.append(t2)
+    idx = [i for i in (0, 1) if s2[i] is not None]
+    for i, c in zip(idx, conj_many(ctx, [s2[i] for i in idx])):
+        out[i] = ctx.add(out[i], c)
+    return out[0], out[1]
 
 
 def split_lut2(ctx, split: SplitLUT2, key, a, b):
@@ -154,5 +210,30 @@ class XOR4LUT:
         for (p, q), pt in self.pt.items():
             acc = ctx.add(acc, ctx.multiply(ctx.multiply(A[p], B[q]), pt))
         return acc
+
+    def apply_pair(self, a0, b0, a1, b1, out_level=None):
+        """(XOR4(a0, b0), XOR4(a1, b1)) -- the hi / lo halves of an AES step.  With a batching
+        context the four inputs' bases share mul_many / conj_many batches and the two
+        conjugations of the split sums one more; otherwise the two XORs run
+        on the two branch streams."""
+        ctx = self.ctx
+        if getattr(ctx, "fused_luts", False) and batched(ctx):
+            if out_level is not None:
+                lv = out_level + LUT2_DEPTH
+                a0, b0, a1, b1 = (drop_to(ctx, c, lv) for c in (a0, b0, a1, b1))
+            if not hasattr(self, "_split"):
+                self._split = SplitLUT2(self.coeffs)
+            sp = self._split
+            try:
+                A0, B0, A1, B1 = joint_bases(ctx, [(a0, sp.need_a, "pow"), (b0, sp.need_b, "std"),
+                                                   (a1, sp.need_a, "pow"), (b1, sp.need_b, "std")])
+            except RuntimeError as e:
+                if "level" not in str(e):
+                    raise
+            else:
+                out = sp.eval_pair(ctx, ("xor4", id(self)), (A0, B0), (A1, B1))
+                if out is not None:
+                    return out
+        return pair(ctx, lambda: self.apply(a0, b0, out_level), lambda: self.apply(a1, b1, out_level))
 
     __call__ = apply

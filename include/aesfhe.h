@@ -125,6 +125,14 @@ int aesfhe_level_down(aesfhe_ctx* ctx, aesfhe_handle ct, int level, aesfhe_handl
 int aesfhe_rotate(aesfhe_ctx* ctx, aesfhe_handle ct, int steps, aesfhe_handle* out);
 /* engine.conjugate(ct, conjugation_key), REF/engine_context.py:103-104 */
 int aesfhe_conjugate(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
+/* Batched variants (SURVEY.md §8(b) "optional batched variants taking h[] arrays"; DESIGN.md
+ * §3.12): n independent engine.multiply(a[i], b[i], relinearization_key) products
+ * (REF/engine_context.py:65-67, always relinearised and rescaled) resp. n
+ * engine.conjugate(in[i], conjugation_key) calls (REF/engine_context.py:103-104).  Operands
+ * at one level are stacked and share one tensor launch and one key switch per chunk of four;
+ * the results equal the separate calls bit for bit.  out[i] receives a new handle. */
+int aesfhe_mul_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* a, const aesfhe_handle* b, aesfhe_handle* out);
+int aesfhe_conjugate_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, aesfhe_handle* out);
 /* engine.make_power_basis(ct, degree, relinearization_key), REF/engine_context.py:100-101;
  * out[k-1] = ct^k, k = 1..degree */
 int aesfhe_power_basis(aesfhe_ctx* ctx, aesfhe_handle ct, int degree, aesfhe_handle* out);
