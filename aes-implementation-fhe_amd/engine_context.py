@@ -176,6 +176,10 @@ class EngineContext:
                                      self.bootstrap_key)
 
     # -------------------------------------------------------------- MI355X extras
+    def can_fork(self) -> bool:
+        """whether run_parallel branches would run concurrently (False inside a branch)"""
+        return self.engine.can_fork()
+
     def run_parallel(self, *fns):
         """Independent branches (e.g. the hi and lo nibble halves of an AES step) on separate
         HIP streams; sequential when the context was built with concurrent=False."""

@@ -328,6 +328,10 @@ class Engine:
             raise err
         return out
 
+    def can_fork(self) -> bool:
+        """True when parallel() would really run its branches on separate streams"""
+        return bool(self.concurrent) and not getattr(self._tls, "worker", False)
+
     def settle(self, *cts):
         """Apply deferred work of shared inputs before they are used by parallel branches."""
         for c in cts:

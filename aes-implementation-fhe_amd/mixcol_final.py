@@ -16,7 +16,7 @@ import numpy as np
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT, SplitLUT2, batched, eval_two, joint_bases, powers, std_basis
-from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap2, drop_to, fused_lut, pair
+from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap2, can_fork, drop_to, fused_lut, pair
 
 
 class _CoeffCache:
@@ -102,7 +102,7 @@ def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo, out_level=Non
     if getattr(ctx, "fused_luts", False):
         sh, sl = cache.split(mult, "hi"), cache.split(mult, "lo")
         try:
-            if batched(ctx):  # one pair of bases, products / conjugations batched
+            if batched(ctx) and not can_fork(ctx):  # one pair of bases, batched products (§3.12)
                 A, B = joint_bases(ctx, [(ct_hi, sh.need_a | sl.need_a, "pow"), (ct_lo, sh.need_b | sl.need_b, "std")])
             else:
                 A, B = pair(ctx, lambda: powers(ctx, ct_hi, sh.need_a | sl.need_a),
@@ -111,7 +111,7 @@ def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo, out_level=Non
             if "level" not in str(e):
                 raise
         else:
-            if batched(ctx):
+            if batched(ctx) and not can_fork(ctx):
                 out = eval_two(ctx, (sh, ("gf", mult, "hi"), A, B), (sl, ("gf", mult, "lo"), A, B))
                 if out is not None:
                     return out

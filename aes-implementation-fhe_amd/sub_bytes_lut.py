@@ -21,7 +21,7 @@ Evaluation forms (same polynomials, same output level, outputs equal up to CKKS 
 from typing import Any, Dict, Tuple
 
 import numpy as np
-from utils import SUBBYTES_DEPTH, conj_many, drop_to, fused_lut, mul_many, pair
+from utils import SUBBYTES_DEPTH, can_fork, conj_many, drop_to, fused_lut, mul_many, pair
 
 _TOL = 1e-12
 
@@ -143,6 +143,10 @@ class SubBytesLUTFastCached:
             for i, (u, v) in ((2, (1, 1)), (4, (2, 2)), (3, (1, 2)), (5, (1, 4)), (6, (2, 4)), (7, (3, 4)), (8, (4, 4))):
                 g[i] = ctx.multiply(g[u], g[v])  # depth: G_2 +1, G_3 / G_4 +2, G_5..G_8 +3 over b^16
         if batch:
+            if can_fork(ctx):  # each output nibble batches its own products, on its own stream
+                shared = (*baby.values(), *g.values())
+                return pair(ctx, lambda: self._outputs_batched(baby, g, ct_b, ("hi",))[0],
+                            lambda: self._outputs_batched(baby, g, ct_b, ("lo",))[0], shared=shared)
             return self._outputs_batched(baby, g, ct_b)
 
         # 3) out = P(b) + conj(Q(b)) per output nibble
@@ -153,12 +157,12 @@ class SubBytesLUTFastCached:
 
         return pair(ctx, lambda: lut("hi"), lambda: lut("lo"), shared=(*baby.values(), *g.values()))
 
-    def _outputs_batched(self, baby, g, ct_b):
-        """both output nibbles: every chunk sum S_i (one fused kernel each), ALL the products
-        S_i G_i of both outputs in mul_many batches, the two conj(Q) in one conj_many"""
+    def _outputs_batched(self, baby, g, ct_b, whiches=("hi", "lo")):
+        """the output nibbles `whiches`: every chunk sum S_i (one fused kernel each), ALL their
+        products S_i G_i in mul_many batches, the conj(Q) in one conj_many"""
         ctx = self.ctx
         terms, prods = {}, []
-        for which in ("hi", "lo"):
+        for which in whiches:
             for part, coef in zip(("p", "q"), self._bsgs[which]):
                 terms[(which, part)] = []
                 for i in range((len(coef) + 15) // 16):
@@ -182,8 +186,8 @@ class SubBytesLUTFastCached:
             for t in ts[1:]:
                 a = ctx.add(a, t)
             acc[wp] = a
-        cq = conj_many(ctx, [acc[("hi", "q")], acc[("lo", "q")]])
-        return ctx.add(acc[("hi", "p")], cq[0]), ctx.add(acc[("lo", "p")], cq[1])
+        cq = conj_many(ctx, [acc[(w, "q")] for w in whiches])
+        return tuple(ctx.add(acc[(w, "p")], c) for w, c in zip(whiches, cq))
 
     # ------------------------------------------------------------------ direct (reference) form
     def _apply_direct(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:

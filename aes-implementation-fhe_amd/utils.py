@@ -74,6 +74,13 @@ def bootstrap2(ctx, a, b):
     return pair(ctx, lambda: ctx.bootstrap(ctx.to_intt(a)), lambda: ctx.bootstrap(ctx.to_intt(b)))
 
 
+def can_fork(ctx) -> bool:
+    """two independent halves would run on two streams (utils.pair): then each half batches
+    its own products; otherwise both halves' products go into shared batches"""
+    f = getattr(ctx, "can_fork", None)
+    return bool(f()) if f is not None else False
+
+
 def mul_many(ctx, pairs):
     """[ctx.multiply(a, b) for a, b in pairs] as one batched engine call when the context has
     it (identical results)"""

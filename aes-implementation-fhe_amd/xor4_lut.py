@@ -17,7 +17,7 @@ x^8 are skipped for XOR4), and each S is one fused kernel.  Output level unchang
 from typing import Any, Dict
 
 import numpy as np
-from utils import LUT2_DEPTH, conj_many, drop_to, fused_lut, mul_many, pair
+from utils import LUT2_DEPTH, can_fork, conj_many, drop_to, fused_lut, mul_many, pair
 
 
 def basis16(ctx, ct, *, retry_intt: bool = True) -> Dict[int, Any]:
@@ -68,6 +68,8 @@ def _chain(need):
 
 def powers(ctx, ct, need) -> Dict[int, Any]:
     """{k: x^k} for k in need (0 = the constant 1 at x's level)"""
+    if batched(ctx):
+        return joint_bases(ctx, [(ct, need, "pow")])[0]
     pw = {1: ct}
     for k, u, v in _chain(need):
         pw[k] = ctx.multiply(pw[u], pw[v])
@@ -110,6 +112,8 @@ def batched(ctx) -> bool:
 
 def std_basis(ctx, ct, need) -> Dict[int, Any]:
     """{q: B[q]} for q in need, B[q] = x^q (q <= 8), conj(x^(16-q)) (q >= 9)"""
+    if batched(ctx):
+        return joint_bases(ctx, [(ct, need, "std")])[0]
     pos = powers(ctx, ct, {q if q <= 8 else 16 - q for q in need})
     return {q: pos[q] if q <= 8 else ctx.conjugate(pos[16 - q]) for q in need}
 
@@ -131,7 +135,7 @@ class SplitLUT2:
         self.has2 = bool(np.any(self.c2))
 
     def bases(self, ctx, a, b):
-        if batched(ctx):
+        if batched(ctx) and not can_fork(ctx):
             A, B = joint_bases(ctx, [(a, self.need_a, "pow"), (b, self.need_b, "std")])
             return A, B
         return pair(ctx, lambda: powers(ctx, a, self.need_a), lambda: std_basis(ctx, b, self.need_b))
@@ -212,12 +216,13 @@ class XOR4LUT:
         return acc
 
     def apply_pair(self, a0, b0, a1, b1, out_level=None):
-        """(XOR4(a0, b0), XOR4(a1, b1)) -- the hi / lo halves of an AES step.  With a batching
-        context the four inputs' bases share mul_many / conj_many batches and the two
-        conjugations of the split sums one more; otherwise the two XORs run
-        on the two branch streams."""
+        """(XOR4(a0, b0), XOR4(a1, b1)) -- the hi / lo halves of an AES step.  On two branch
+        streams when the context can fork (each XOR batching its own two inputs' bases: on
+        this GPU two concurrent half-size batches beat one full batch, DESIGN.md §3.12);
+        otherwise the four inputs' bases share mul_many / conj_many batches and the two
+        conjugations of the split sums one more."""
         ctx = self.ctx
-        if getattr(ctx, "fused_luts", False) and batched(ctx):
+        if getattr(ctx, "fused_luts", False) and batched(ctx) and not can_fork(ctx):
             if out_level is not None:
                 lv = out_level + LUT2_DEPTH
                 a0, b0, a1, b1 = (drop_to(ctx, c, lv) for c in (a0, b0, a1, b1))
