@@ -253,51 +253,81 @@ __device__ __forceinline__ u32 galois_src(u32 i, u64 g, int logn) {
 
 // g != 0: the inputs (ext and d) are read through the automorphism X -> X^g -- a hoisted
 // rotation: one ModUp of c1 serves every rotation of the same ciphertext
-__global__ void k_key_inner(u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl, int alpha, int nkey, int nks,
-                            u64 g, LimbMap map, const PrimeConst* pc, int logn, int nb, size_t ext_ms, size_t d_ms, size_t acc_ms,
-                            KsFold fold, int accum, unsigned long long* ts) {
+// four consecutive coefficients per thread: 16-byte key / ext / acc accesses (the kernel is
+// HBM-bound on the key and ext reads); g != 0 gathers ext and d through X -> X^g
+template <int NBM>
+__global__ void __launch_bounds__(kBlock) k_key_inner(u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
+                                                      int alpha, int nkey, int nks, u64 g, LimbMap map, const PrimeConst* pc, int logn,
+                                                      int nb, size_t ext_ms, size_t d_ms, size_t acc_ms, KsFold fold, int accum,
+                                                      unsigned long long* ts) {
     ts_begin(ts);
     const int x = blockIdx.y;
-    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    const size_t ks = g ? galois_src((u32)k, g, logn) : k;
+    const size_t k = ((size_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+    u32 ks[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) ks[v] = g ? galois_src((u32)(k + v), g, logn) : (u32)(k + v);
     const PrimeConst P = pc[map.prime(x)];
     const int krow = x < nl ? x : nks + (x - nl);
     const int own = x < nl ? x / alpha : -1;
     // 64-bit multiply-adds (operands < q < 2^32/3: eight products fit), folded every 8 digits;
     // the key residues are loaded once for every batched ciphertext
-    u64 s0[kMaxKsBatch] = {}, s1[kMaxKsBatch] = {};
+    u64 s0[NBM][4] = {}, s1[NBM][4] = {};
     for (int j = 0; j < nd; ++j) {
         if (j && (j & 7) == 0) {
 #pragma unroll
-            for (int m = 0; m < kMaxKsBatch; ++m)
-                if (m < nb) s0[m] = fold64(s0[m], P.q, P.r32), s1[m] = fold64(s1[m], P.q, P.r32);
-        }
-        const u32* kb = key + (((size_t)j * 2 * nkey + krow) << logn) + k;
-        const u32* ka = kb + ((size_t)nkey << logn);
-        const u64 vb = *kb, va = *ka;
+            for (int m = 0; m < NBM; ++m)
 #pragma unroll
-        for (int m = 0; m < kMaxKsBatch; ++m) {
+                for (int v = 0; v < 4; ++v) s0[m][v] = fold64(s0[m][v], P.q, P.r32), s1[m][v] = fold64(s1[m][v], P.q, P.r32);
+        }
+        const size_t kr = (((size_t)j * 2 * nkey + krow) << logn) + k;
+        const uint4 vb = *reinterpret_cast<const uint4*>(key + kr);
+        const uint4 va = *reinterpret_cast<const uint4*>(key + kr + ((size_t)nkey << logn));
+        const u32 kb4[4] = {vb.x, vb.y, vb.z, vb.w}, ka4[4] = {va.x, va.y, va.z, va.w};
+#pragma unroll
+        for (int m = 0; m < NBM; ++m) {
             if (m >= nb) break;
-            const u32 e = j == own ? d[m * d_ms + ((size_t)x << logn) + ks] : ext[m * ext_ms + (((size_t)j * ne + x) << logn) + ks];
-            s0[m] += e * vb;
-            s1[m] += e * va;
+            const u32* src = j == own ? d + m * d_ms + ((size_t)x << logn) : ext + m * ext_ms + (((size_t)j * ne + x) << logn);
+            u32 e[4];
+            if (g) {
+#pragma unroll
+                for (int v = 0; v < 4; ++v) e[v] = src[ks[v]];
+            } else {
+                const uint4 t = *reinterpret_cast<const uint4*>(src + k);
+                e[0] = t.x, e[1] = t.y, e[2] = t.z, e[3] = t.w;
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                s0[m][v] += (u64)e[v] * kb4[v];
+                s1[m][v] += (u64)e[v] * ka4[v];
+            }
         }
     }
 #pragma unroll
-    for (int m = 0; m < kMaxKsBatch; ++m) {
+    for (int m = 0; m < NBM; ++m) {
         if (m >= nb) break;
-        u32 r0 = reduce64(s0[m], P.q, P.mu, P.r32), r1 = reduce64(s1[m], P.q, P.mu, P.r32);
+        u32 r0[4], r1[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) r0[v] = reduce64(s0[m][v], P.q, P.mu, P.r32), r1[v] = reduce64(s1[m][v], P.q, P.mu, P.r32);
         if (fold.gad && x < nl) {
             const u32 gv = fold.gad[2 * x], gp = fold.gad[2 * x + 1];
             const size_t at = m * fold.ms + ((size_t)x << logn) + k;
-            r0 = add_mod(r0, shoup_mul(fold.add0[at], gv, gp, P.q), P.q);
-            r1 = add_mod(r1, shoup_mul(fold.add1[at], gv, gp, P.q), P.q);
+            const uint4 f0 = *reinterpret_cast<const uint4*>(fold.add0 + at), f1 = *reinterpret_cast<const uint4*>(fold.add1 + at);
+            const u32 a0v[4] = {f0.x, f0.y, f0.z, f0.w}, a1v[4] = {f1.x, f1.y, f1.z, f1.w};
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                r0[v] = add_mod(r0[v], shoup_mul(a0v[v], gv, gp, P.q), P.q);
+                r1[v] = add_mod(r1[v], shoup_mul(a1v[v], gv, gp, P.q), P.q);
+            }
         }
-        u32* a0 = acc + m * acc_ms + ((size_t)x << logn) + k;
-        u32* a1 = acc + m * acc_ms + (((size_t)ne + x) << logn) + k;
-        if (accum) r0 = add_mod(r0, *a0, P.q), r1 = add_mod(r1, *a1, P.q);
-        *a0 = r0;
-        *a1 = r1;
+        uint4* a0 = reinterpret_cast<uint4*>(acc + m * acc_ms + ((size_t)x << logn) + k);
+        uint4* a1 = reinterpret_cast<uint4*>(acc + m * acc_ms + (((size_t)ne + x) << logn) + k);
+        if (accum) {
+            const uint4 p0 = *a0, p1 = *a1;
+            r0[0] = add_mod(r0[0], p0.x, P.q), r0[1] = add_mod(r0[1], p0.y, P.q), r0[2] = add_mod(r0[2], p0.z, P.q), r0[3] = add_mod(r0[3], p0.w, P.q);
+            r1[0] = add_mod(r1[0], p1.x, P.q), r1[1] = add_mod(r1[1], p1.y, P.q), r1[2] = add_mod(r1[2], p1.z, P.q), r1[3] = add_mod(r1[3], p1.w, P.q);
+        }
+        *a0 = make_uint4(r0[0], r0[1], r0[2], r0[3]);
+        *a1 = make_uint4(r1[0], r1[1], r1[2], r1[3]);
     }
     ts_end(ts);
 }
@@ -872,9 +902,18 @@ void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* e
     // per ciphertext ext/d (nd x ne) read and acc (2 x ne) written; the key (nd x 2 x ne) once;
     // the fold reads 2 x nl more rows per ciphertext
     const double fw = (fold.gad ? 2.0 * nb * nl : 0.0) + (accum ? 2.0 * nb * ne : 0.0);
-    prof_launch_ts(KID_KEY_INNER, words(((nb * (nd + 2.0) + 2.0 * nd) * ne + fw) * (1u << T.logn)), k_key_inner, ew_grid(T.logn, ne),
-                   dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g, map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold,
-                   (int)accum);
+    const double bytes = words(((nb * (nd + 2.0) + 2.0 * nd) * ne + fw) * (1u << T.logn));
+    const dim3 grid((1u << T.logn) / (4 * kBlock), ne);
+    // register footprint follows the batch: 1, 2 or 4 ciphertexts
+    if (nb == 1)
+        prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<1>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g,
+                       map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum);
+    else if (nb == 2)
+        prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<2>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g,
+                       map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum);
+    else
+        prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<4>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g,
+                       map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum);
 }
 void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, u64 seed, u64 stream, int kind) {
     prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_small, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, nl, map, seed, stream, kind, T.pc,

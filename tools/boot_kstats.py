@@ -18,12 +18,14 @@ def main(n=5):
     E = ctx.engine
     z = np.exp(2j * np.pi * np.random.default_rng(0).random(E.slot_count))
     ct = E.intt(ctx.encrypt(z))
-    E.bootstrap(ct)
+    pair = "--pair" in sys.argv  # the batched hi / lo bootstrap C2 uses
+    boot = (lambda: E.bootstrap_pair(ct, ct)) if pair else (lambda: E.bootstrap(ct))
+    boot()
     E.sync()
     E.profile(list(KERNEL_IDS), every=1)
     E.kernel_stats(reset=True)
     for _ in range(n):
-        E.bootstrap(ct)
+        boot()
     E.sync()
     st = E.kernel_stats(reset=True)
     E.profile(())
