@@ -1840,20 +1840,44 @@ public:
             m.gad = fold ? d_gadget_ : nullptr;
             for (int b = 0; b < g.B; ++b) m.a[b] = (b == 0 || u[b]) ? c0 : nullptr, m.u[b] = b ? u[b] : nullptr, m.gal[b] = gals[b];
             bool any[kLinG] = {}, rot[kLinG] = {};
-            for (int j = 0; j < gn; ++j) {
+            for (int j = 0; j < gn; ++j)
                 for (int b = 0; b < g.B; ++b) {
                     m.pt[j][b] = P[g0 + j][b];
                     any[j] = any[j] || P[g0 + j][b];
                     rot[j] = rot[j] || (b && P[g0 + j][b]);
                 }
+            // rotated giant steps of a double-hoisted group: their Q*P sums side by side in one
+            // block (stacked members [j][b]) -> ONE ModDown + rescale, stacked ModUps
+            std::vector<int> bj;
+            if (dh && fold && giant_batch_)
+                for (int j = 0; j < gn; ++j)
+                    if (any[j] && rot[j] && g.giant[g0 + j]) bj.push_back(j);
+            if ((int)bj.size() < 2 || 2 * nb * (int)bj.size() > kMaxConvGroups) bj.clear();
+            u32* blk = bj.empty() ? nullptr : tmp(bj.size() * 2 * (size_t)ne * nb);
+            bool in_blk[kLinG] = {};
+            for (size_t i = 0; i < bj.size(); ++i) in_blk[bj[i]] = true;
+            for (int j = 0, i = 0; j < gn; ++j) {
                 const bool folded = fold && rot[j];
                 m.out0[j] = folded ? nullptr : tmp(2 * (size_t)nl * nb);  // member stride qs, first nl rows used
                 m.out1[j] = (P[g0 + j][0] && !folded) ? tmp(2 * (size_t)nl * nb) : nullptr;
-                m.outp[j] = rot[j] ? tmp(2 * (size_t)ne * nb) : nullptr;
+                m.outp[j] = in_blk[j] ? blk + (size_t)(i++) * nb * ps : rot[j] ? tmp(2 * (size_t)ne * nb) : nullptr;
             }
             launch_lin_mac(S(), T_, m, nl, ne, extmap(nl));
+            if (!bj.empty()) {
+                Ct rs = moddown_rescale(blk, l, nb * (int)bj.size());
+                std::vector<u64> gs;
+                for (int j : bj) gs.push_back(rot_galois(-(int)g.giant[g0 + j]));
+                giant_accumulate_many(rs, gs, nb, dh_acc, dh_c0, dh_n);
+                release(rs);
+                untmp(blk, bj.size() * 2 * (size_t)ne * nb);
+            }
             for (int j = 0; j < gn; ++j) {
                 const int gg = g0 + j;
+                if (in_blk[j]) {
+                    if (m.out0[j]) untmp(m.out0[j], 2 * (size_t)nl * nb);
+                    if (m.out1[j]) untmp(m.out1[j], 2 * (size_t)nl * nb);
+                    continue;
+                }
                 if (any[j]) {
                     Ct inner, rs;
                     if (rot[j] && fold) {
@@ -1916,6 +1940,41 @@ public:
             out = res;
         }
         return out;
+    }
+    // K rotated giant steps at once: rs holds K x nb stacked members ([j][b]), step j permuted
+    // by X -> X^gals[j]; their c1 ModUp'ed together (chunks within kMaxConvGroups), each key
+    // inner product accumulated into acc, the permuted c0 summed into c0sum per member
+    void giant_accumulate_many(const Ct& rs, const std::vector<u64>& gals, int nb, u32*& acc, u32*& c0sum, int& count) {
+        const int K = (int)gals.size(), lv = rs.level, r = hp_.nl(lv), ne2 = r + hp_.n_p, n = hp_.n;
+        const size_t ms = (size_t)2 * r * n;
+        if (rs.nb != K * nb || K > kMaxMembers) throw std::runtime_error("giant_accumulate_many: batch shape");
+        u32* perm = tmp(2 * (size_t)r * nb * K);
+        for (int j = 0; j < K; ++j) launch_automorph(S(), T_, perm + (size_t)j * nb * ms, rs.data + (size_t)j * nb * ms, gals[j], 2 * r * nb);
+        if (!acc) acc = tmp(2 * (size_t)ne2 * nb);
+        const int nd = (r + hp_.alpha - 1) / hp_.alpha;
+        const int per = std::max(1, std::min(kMaxConvGroups / (nd * nb), kMaxKsBatch));  // steps per ModUp
+        for (int j0 = 0; j0 < K; j0 += per) {
+            const int k = std::min(per, K - j0);
+            const u32* c1 = perm + (size_t)j0 * nb * ms + (size_t)r * n;
+            u32* ext = modup(c1, lv, nb * k, ms);
+            const size_t er = (size_t)ext_rows(lv) * n;
+            for (int j = j0; j < j0 + k; ++j) {
+                key_inner(acc, ext + (size_t)(j - j0) * nb * er, perm + (size_t)j * nb * ms + (size_t)r * n, ksk(gals[j]), lv, 0, nb, ms, KsFold{},
+                          count > 0 || j > 0);
+            }
+            untmp(ext, (size_t)nb * k * ext_rows(lv));
+        }
+        const bool fresh = c0sum == nullptr;
+        if (fresh) c0sum = tmp(2 * (size_t)r * nb);
+        for (int b = 0; b < nb; ++b) {
+            MemberPtrs mp;
+            for (int j = 0; j < K; ++j) mp.src[j] = perm + ((size_t)j * nb + b) * ms;
+            launch_add_members(S(), T_, c0sum + (size_t)b * ms, mp, K, r, qmap(), !fresh);
+        }
+        untmp(perm, 2 * (size_t)r * nb * K);
+        count += K;
+        cnt_[C_ROT] += K * nb;
+        cnt_[C_KS] += K * nb;
     }
     // one rotated giant step of a double-hoisted group: rs permuted by X -> X^gal, its c1
     // key switched into the running Q*P sum acc (allocated on the first call), its c0 summed
@@ -2559,6 +2618,7 @@ private:
     std::vector<size_t> mdr_off_;
     bool batch_ops_ = std::getenv("AESFHE_BATCH_OPS") == nullptr || std::getenv("AESFHE_BATCH_OPS")[0] != '0';
     bool stack_evalmod_ = std::getenv("AESFHE_STACK_EVALMOD") == nullptr || std::getenv("AESFHE_STACK_EVALMOD")[0] != '0';
+    bool giant_batch_ = std::getenv("AESFHE_GIANT_BATCH") == nullptr || std::getenv("AESFHE_GIANT_BATCH")[0] != '0';
     bool double_hoist_ = std::getenv("AESFHE_DOUBLE_HOIST") == nullptr || std::getenv("AESFHE_DOUBLE_HOIST")[0] != '0';
     bool fuse_rr_ = std::getenv("AESFHE_FUSED_RESCALE") == nullptr || std::getenv("AESFHE_FUSED_RESCALE")[0] != '0';
     u32* d_pinv_ = nullptr;

@@ -115,6 +115,8 @@ struct MemberPtrs {
     u32* dst[kMaxMembers] = {};
 };
 void launch_copy_members(hipStream_t st, const DevTables& T, const MemberPtrs& mp, int n, int rows);
+// out = (accumulate ? out : 0) + sum_{s < n} mp.src[s] over `rows` rows (limb = row, map)
+void launch_add_members(hipStream_t st, const DevTables& T, u32* out, const MemberPtrs& mp, int n, int rows, LimbMap map, bool accumulate);
 // tensor products of n independent pairs (a[m], b[m]: 2 x nl rows each) into one stacked
 // [m][3][nl] output (mul_many)
 struct TensorPtrs {

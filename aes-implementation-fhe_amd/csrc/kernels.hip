@@ -63,6 +63,14 @@ __global__ void k_copy_members(MemberPtrs mp, int logn) {
     const size_t i = ((size_t)blockIdx.y << (logn - 2)) + (size_t)blockIdx.x * kBlock + threadIdx.x;
     reinterpret_cast<uint4*>(mp.dst[blockIdx.z])[i] = reinterpret_cast<const uint4*>(mp.src[blockIdx.z])[i];
 }
+__global__ void k_add_members(u32* out, MemberPtrs mp, int n, LimbMap map, const PrimeConst* pc, int logn, int accumulate) {
+    const int row = blockIdx.y;
+    const size_t at = ((size_t)row << logn) + (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const u32 q = pc[map.prime(row)].q;
+    u32 v = accumulate ? out[at] : 0u;
+    for (int s = 0; s < n; ++s) v = add_mod(v, mp.src[s][at], q);
+    out[at] = v;
+}
 __global__ void k_tensor_ptrs(u32* out, TensorPtrs tp, int nl, LimbMap map, const PrimeConst* pc, int logn) {
     const int row = blockIdx.y;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
@@ -711,6 +719,11 @@ void launch_copy_members(hipStream_t st, const DevTables& T, const MemberPtrs& m
     if (n > kMaxMembers) throw std::runtime_error("launch_copy_members: too many members");
     prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * n * rows), k_copy_members, dim3((1u << T.logn) / (4 * kBlock), rows, n), dim3(kBlock), 0,
                 st, mp, T.logn);
+}
+void launch_add_members(hipStream_t st, const DevTables& T, u32* out, const MemberPtrs& mp, int n, int rows, LimbMap map, bool accumulate) {
+    if (n <= 0 || n > kMaxMembers) throw std::runtime_error("launch_add_members: 1..8 sources");
+    prof_launch(KID_ELEMENTWISE, EW_BYTES((n + 1.0 + (accumulate ? 1.0 : 0.0)) * rows), k_add_members, ew_grid(T.logn, rows), dim3(kBlock), 0,
+                st, out, mp, n, map, T.pc, T.logn, (int)accumulate);
 }
 void launch_tensor_ptrs(hipStream_t st, const DevTables& T, u32* out, const TensorPtrs& tp, int n, int nl, LimbMap map) {
     if (n <= 0 || n > kMaxMembers) throw std::runtime_error("launch_tensor_ptrs: 1..8 products");
