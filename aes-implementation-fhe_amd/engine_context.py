@@ -5,8 +5,9 @@ Same constructor keywords, same methods, same error-string behaviour; the AES ro
 modules only ever talk to this object.  Extra keywords: ``log_n`` (N = 2^log_n, default
 2^16 as in the reference harness; config 1 of BASELINE.json uses 2^15), ``dnum`` and
 ``seed`` (deterministic key material), ``lazy`` (deferred relinearisation),
-``concurrent`` (hi / lo halves on two HIP streams) and ``fused_luts`` (one-kernel LUT sums,
-DESIGN.md §3.8).
+``concurrent`` (hi / lo halves on two HIP streams), ``fused_luts`` (one-kernel LUT sums,
+DESIGN.md §3.8) and ``allow_insecure`` (parameter sets above the 128-bit bound, for small
+test / smoke sets only).
 """
 from __future__ import annotations
 
@@ -24,7 +25,7 @@ class EngineContext:
     def __init__(self, signature: int, *, max_level: int = 17, use_bootstrap: bool = True,
                  use_multiparty: bool = False, mode: str = "cpu", device_id: int = 0,
                  thread_count: int | None = None, log_n: int = 16, dnum: int | None = None, seed: int = 0x5EED,
-                 lazy: bool = True, concurrent: bool = True, fused_luts: bool = True):
+                 lazy: bool = True, concurrent: bool = True, fused_luts: bool = True, allow_insecure: bool = False):
         # REF/engine_context.py:17-42: signature selects the engine constructor form
         if signature == 1:
             kw = dict(use_bootstrap=use_bootstrap, max_level=_SIG_DEFAULT_LEVEL)
@@ -37,7 +38,7 @@ class EngineContext:
         self.signature = signature
         self.engine = Engine(mode=mode, use_multiparty=use_multiparty, thread_count=thread_count or 0,
                              device_id=device_id, log_n=log_n, dnum=dnum, seed=seed, lazy=lazy,
-                             concurrent=concurrent, **kw)
+                             concurrent=concurrent, allow_insecure=allow_insecure, **kw)
         eng = self.engine
         # REF/engine_context.py:44-50
         self.secret_key = eng.create_secret_key()
