@@ -78,13 +78,12 @@ class InvMixColumnsFHE:
         rot = {k: (rh[k - 1], rl[k - 1]) for k in (1, 2, 3)}
         for k in (1, 2, 3):
             log(f"rotc{k}", rot[k])
-        e14 = self.gf_mult_14(ct_hi, ct_lo)
+        # independent GF multiplier pairs two at a time on the branch streams
+        e14, e11 = pair(self.ctx, lambda: self.gf_mult_14(ct_hi, ct_lo), lambda: self.gf_mult_11(*rot[1]))
         log("mul14", e14)
-        e11 = self.gf_mult_11(*rot[1])
         log("mul11", e11)
-        e13 = self.gf_mult_13(*rot[2])
+        e13, e9 = pair(self.ctx, lambda: self.gf_mult_13(*rot[2]), lambda: self.gf_mult_9(*rot[3]))
         log("mul13", e13)
-        e9 = self.gf_mult_9(*rot[3])
         log("mul9", e9)
         fl = self._xor_level
         acc = self._xor_pair(e14, e11, fl)

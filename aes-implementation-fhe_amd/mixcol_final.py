@@ -178,8 +178,10 @@ class MixColFinal:
         # every XOR pair below is renormalised right away (REF :104-106), so the LUTs run on
         # inputs dropped to the lowest level that leaves their output at RENORM_FLOOR
         fl = RENORM_FLOOR
-        two = self.gf_mult_2(ct_hi, ct_lo, out_level=fl + LUT2_DEPTH)
-        thr = self.gf_mult_3(*rot[1], out_level=fl + LUT2_DEPTH)
+        # the two GF multiplier pairs are independent: one per branch stream, each batching
+        # its own bases and evaluations
+        two, thr = pair(self.ctx, lambda: self.gf_mult_2(ct_hi, ct_lo, out_level=fl + LUT2_DEPTH),
+                        lambda: self.gf_mult_3(*rot[1], out_level=fl + LUT2_DEPTH))
         log("two", two)
         log("thr", thr)
         acc = self._xor_pair(two, thr, fl)
