@@ -86,13 +86,13 @@ class InvMixColumnsFHE:
         log("mul13", e13)
         log("mul9", e9)
         fl = self._xor_level
-        acc = self._xor_pair(e14, e11, fl)
-        log("acc1", acc)
-        acc = self._renorm_pair(*acc, level=NEED_XOR)  # internal: only the next XOR4 reads it
-        acc = self._xor_pair(acc, e13, fl)
-        log("acc2", acc)
-        acc = self._renorm_pair(*acc, level=NEED_XOR)
-        out = self._renorm_pair(*self._xor_pair(acc, e9, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
+        # (e14 ^ e11) ^ (e13 ^ e9): the reference's chain regrouped (see MixColFinal), the two
+        # inner XOR pairs on the two branch streams
+        x1, x2 = pair(self.ctx, lambda: self._renorm_pair(*self._xor_pair(e14, e11, fl), level=NEED_XOR),
+                      lambda: self._renorm_pair(*self._xor_pair(e13, e9, fl), level=NEED_XOR))
+        log("acc1", x1)
+        log("acc23", x2)
+        out = self._renorm_pair(*self._xor_pair(x1, x2, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
         if do_final_bootstrap:
             out = bootstrap2(self.ctx, out[0], out[1])
         log("out", out)

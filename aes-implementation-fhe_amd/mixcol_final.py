@@ -184,14 +184,15 @@ class MixColFinal:
                         lambda: self.gf_mult_3(*rot[1], out_level=fl + LUT2_DEPTH))
         log("two", two)
         log("thr", thr)
-        acc = self._xor_pair(two, thr, fl)
-        log("acc1", acc)
-        acc = self._renorm_pair(*acc, level=NEED_XOR)  # internal: only the next XOR4 reads it
-        acc = self._xor_pair(acc, rot[2], fl)
-        log("acc2", acc)
-        acc = self._renorm_pair(*acc, level=NEED_XOR)
+        # out = (2x ^ 3r1) ^ (r2 ^ r3): the reference's chain ((2x ^ 3r1) ^ r2) ^ r3 regrouped
+        # (XOR is associative, every XOR pair still renormalised, the same three XOR pairs and
+        # renorms), so the first two XOR pairs are independent and run on the two branch streams
+        x1, x2 = pair(self.ctx, lambda: self._renorm_pair(*self._xor_pair(two, thr, fl), level=NEED_XOR),
+                      lambda: self._renorm_pair(*self._xor_pair(rot[2], rot[3], fl), level=NEED_XOR))
+        log("acc1", x1)
+        log("acc23", x2)
         # the output is bootstrapped next (from level 0) or returned at the fresh level
-        acc = self._renorm_pair(*self._xor_pair(acc, rot[3], fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
+        acc = self._renorm_pair(*self._xor_pair(x1, x2, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
         log("acc3", acc)
         out_hi, out_lo = acc
         if do_final_bootstrap:
