@@ -1805,19 +1805,31 @@ public:
         bool any_baby = false;
         for (int b = 1; b < g.B; ++b)
             for (int gg = 0; gg < g.G; ++gg) any_baby = any_baby || P[gg][b];
+        // baby steps' key inner products inside k_lin_mac when every giant step fits one pass
+        // (each is then computed once), else materialised by k_key_inner
+        const bool fused_baby = fused_baby_ && g.G <= kLinG;
+        std::vector<const u32*> bkey(g.B, nullptr);
+        u32* ext = nullptr;
         if (any_baby) {
-            u32* ext = modup(c1, l, nb, qs);
+            ext = modup(c1, l, nb, qs);
             for (int b = 1; b < g.B; ++b) {
                 bool used = false;
                 for (int gg = 0; gg < g.G; ++gg) used = used || P[gg][b];
                 if (!used) continue;
                 const u64 gal = rot_galois(-(int)((long)g.h * b));  // left rotation by h b
-                u[b] = tmp(2 * (size_t)ne * nb);
-                key_inner(u[b], ext, c1, ksk(gal), l, gal, nb, qs);
+                if (fused_baby) {
+                    bkey[b] = ksk(gal);
+                } else {
+                    u[b] = tmp(2 * (size_t)ne * nb);
+                    key_inner(u[b], ext, c1, ksk(gal), l, gal, nb, qs);
+                }
                 gals[b] = gal;  // c0's automorphism is read inside k_lin_mac
                 cnt_[C_ROT] += nb;
             }
-            untmp(ext, (size_t)nb * ext_rows(l));
+            if (!fused_baby) {
+                untmp(ext, (size_t)nb * ext_rows(l));
+                ext = nullptr;
+            }
         }
         Ct out;
         bool have = false;
@@ -1838,7 +1850,12 @@ public:
             // rotated giant steps: P (out0, out1) folded into outp, ModDown fused with the rescale
             const bool fold = fuse_rr_ && l >= 1 && mdr_off_[l] != SIZE_MAX;
             m.gad = fold ? d_gadget_ : nullptr;
-            for (int b = 0; b < g.B; ++b) m.a[b] = (b == 0 || u[b]) ? c0 : nullptr, m.u[b] = b ? u[b] : nullptr, m.gal[b] = gals[b];
+            for (int b = 0; b < g.B; ++b)
+                m.a[b] = (b == 0 || u[b] || bkey[b]) ? c0 : nullptr, m.u[b] = b ? u[b] : nullptr, m.gal[b] = gals[b], m.key[b] = bkey[b];
+            if (ext) {
+                m.ks_ext = ext, m.ks_d = c1, m.ext_ms = (size_t)ext_rows(l) * n, m.d_ms = qs;
+                m.nd = (nl + hp_.alpha - 1) / hp_.alpha, m.alpha = hp_.alpha, m.nkey = hp_.n_ks + np, m.nks = hp_.n_ks;
+            }
             bool any[kLinG] = {}, rot[kLinG] = {};
             for (int j = 0; j < gn; ++j)
                 for (int b = 0; b < g.B; ++b) {
@@ -1924,6 +1941,7 @@ public:
         for (int b = 1; b < g.B; ++b) {
             if (u[b]) untmp(u[b], 2 * (size_t)ne * nb);
         }
+        if (ext) untmp(ext, (size_t)nb * ext_rows(l));
         if (dh_n > 0) {
             const int lv = l - 1, r = hp_.nl(lv), ne2 = r + np;
             const size_t ms = (size_t)2 * r * n;
@@ -2618,6 +2636,7 @@ private:
     std::vector<size_t> mdr_off_;
     bool batch_ops_ = std::getenv("AESFHE_BATCH_OPS") == nullptr || std::getenv("AESFHE_BATCH_OPS")[0] != '0';
     bool stack_evalmod_ = std::getenv("AESFHE_STACK_EVALMOD") == nullptr || std::getenv("AESFHE_STACK_EVALMOD")[0] != '0';
+    bool fused_baby_ = std::getenv("AESFHE_FUSED_BABY") == nullptr || std::getenv("AESFHE_FUSED_BABY")[0] != '0';
     bool giant_batch_ = std::getenv("AESFHE_GIANT_BATCH") == nullptr || std::getenv("AESFHE_GIANT_BATCH")[0] != '0';
     bool double_hoist_ = std::getenv("AESFHE_DOUBLE_HOIST") == nullptr || std::getenv("AESFHE_DOUBLE_HOIST")[0] != '0';
     bool fuse_rr_ = std::getenv("AESFHE_FUSED_RESCALE") == nullptr || std::getenv("AESFHE_FUSED_RESCALE")[0] != '0';

@@ -212,7 +212,7 @@ void launch_mac(hipStream_t st, const DevTables& T, u32* out, const MacTerms& m,
 //   outp[gg] = sum_{b>=1} u_b P[gg][b]   (2 polys of ne rows; u_b = hoisted key inner products)
 // Each input residue is read once for all giant steps (the per-giant k_mac re-read every
 // rotated baby step and every diagonal twice).  Null pointers mark absent terms.
-constexpr int kLinB = 16, kLinG = 4;
+constexpr int kLinB = 16, kLinG = 5;
 // nb > 1 batched ciphertexts share the diagonals: member m's a / c1 / out0 / out1 are at
 // + m * q_ms words, its u / outp at + m * p_ms words
 struct LinMacArgs {
@@ -232,6 +232,14 @@ struct LinMacArgs {
     // gal[b] != 0: a[b] is read through X -> X^gal[b] (the baby step's automorphism of c0,
     // fused: no rotated copy of c0 is written)
     u64 gal[kLinB] = {};
+    // key[b] set: baby step b's key inner product is computed in the kernel from the hoisted
+    // ModUp (ks_ext: [member][nd][ne], ks_d: the input's c1 on the own-digit limbs), both read
+    // through X -> X^gal[b], instead of being read from u[b]
+    const u32* key[kLinB] = {};
+    const u32* ks_ext = nullptr;
+    const u32* ks_d = nullptr;
+    int nd = 0, alpha = 1, nkey = 0, nks = 0;
+    size_t ext_ms = 0, d_ms = 0;
 };
 void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int nl, int ne, LimbMap map);
 

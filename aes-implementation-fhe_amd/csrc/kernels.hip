@@ -826,6 +826,29 @@ __device__ __forceinline__ void lin_mac_body(const LinMacArgs& m, int nl, int ne
             u0[b] = u1[b] = 0;
             if (m.u[j]) u0[b] = m.u[j][b * m.p_ms + at], u1[b] = m.u[j][b * m.p_ms + po + at];
         }
+        if (m.key[j]) {  // the baby step's key inner product, in place (k_key_inner's sum)
+            const size_t ks = galois_src((u32)k, m.gal[j], logn);
+            const int krow = qrow ? t : m.nks + (t - nl);
+            const int own = qrow ? t / m.alpha : -1;
+            u64 s0[NB] = {}, s1[NB] = {};
+            for (int dj = 0; dj < m.nd; ++dj) {
+                if (dj && (dj & 7) == 0) {
+#pragma unroll
+                    for (int b = 0; b < NB; ++b) s0[b] = fold64(s0[b], P.q, P.r32), s1[b] = fold64(s1[b], P.q, P.r32);
+                }
+                const u32* kb = m.key[j] + (((size_t)dj * 2 * m.nkey + krow) << logn) + k;
+                const u64 vb = kb[0], va = kb[(size_t)m.nkey << logn];
+#pragma unroll
+                for (int b = 0; b < NB; ++b) {
+                    const u32 e = dj == own ? m.ks_d[b * m.d_ms + ((size_t)t << logn) + ks]
+                                            : m.ks_ext[b * m.ext_ms + (((size_t)dj * ne + t) << logn) + ks];
+                    s0[b] += e * vb;
+                    s1[b] += e * va;
+                }
+            }
+#pragma unroll
+            for (int b = 0; b < NB; ++b) u0[b] = reduce64(s0[b], P.q, P.mu, P.r32), u1[b] = reduce64(s1[b], P.q, P.mu, P.r32);
+        }
 #pragma unroll
         for (int g = 0; g < kLinG; ++g) {
             if (g >= m.G || !m.pt[g][j]) continue;
@@ -877,21 +900,24 @@ __global__ void __launch_bounds__(kBlock) k_lin_mac(LinMacArgs m, int nl, int ne
 }  // namespace
 
 void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int nl, int ne, LimbMap map) {
-    if (m.B < 1 || m.B > kLinB || m.G < 1 || m.G > kLinG) throw std::runtime_error("launch_lin_mac: 1..16 baby, 1..4 giant steps");
+    if (m.B < 1 || m.B > kLinB || m.G < 1 || m.G > kLinG) throw std::runtime_error("launch_lin_mac: 1..16 baby, 1..5 giant steps");
     double reads = 0, writes = 0;  // rows of N words
     for (int b = 0; b < m.B; ++b) {
         if (m.a[b]) reads += nl;
         if (m.u[b]) reads += 2.0 * ne;
+        if (m.key[b]) reads += (double)m.nd * ne;  // ext per member (the key is counted as shared below)
         for (int g = 0; g < m.G; ++g)
             if (m.pt[g][b]) reads += ne;
     }
     reads += nl;  // c1
     for (int g = 0; g < m.G; ++g)
         writes += (m.gad && m.outp[g]) ? 2.0 * ne : nl + (m.out1[g] ? nl : 0) + (m.outp[g] ? 2.0 * ne : 0);
-    double shared = 0;  // the diagonals, read once for every batched ciphertext
-    for (int b = 0; b < m.B; ++b)
+    double shared = 0;  // the diagonals (and in-kernel keys), read once for every batched ciphertext
+    for (int b = 0; b < m.B; ++b) {
         for (int g = 0; g < m.G; ++g)
             if (m.pt[g][b]) shared += ne;
+        if (m.key[b]) shared += 2.0 * m.nd * ne;
+    }
     const double bytes = words((m.nb * (reads - shared + writes) + shared) * (1u << T.logn));
     if (m.nb == 1)
         prof_launch(KID_ELEMENTWISE, bytes, k_lin_mac<1>, ew_grid(T.logn, ne), dim3(kBlock), 0, st, m, nl, ne, map, T.pc, T.logn);
