@@ -1485,6 +1485,44 @@ public:
         if (c.data != c_in.data) release(c);
         return o;
     }
+    // several rotations of ONE ciphertext, hoisted: c1 is ModUp'ed once, each step is a key
+    // inner product read through its automorphism plus a ModDown adding the permuted c0
+    // (the same arithmetic as rotate(): ModUp commutes with the automorphism)
+    std::vector<Ct> rotate_hoisted(const Ct& c_in, const std::vector<int>& steps) {
+        std::vector<Ct> out(steps.size());
+        if (vis_npoly(c_in) != 2) throw std::runtime_error("rotation/conjugation expects a 2-polynomial ciphertext");
+        Ct c = normalize(c_in);
+        const long sc = slot_count();
+        int nrot = 0;
+        for (int st : steps) nrot += (((long)st % sc + sc) % sc) != 0;
+        if (c.nb != 1 || nrot < 2 || !batch_ops_) {
+            for (size_t i = 0; i < steps.size(); ++i) out[i] = rotate(c, steps[i]);
+            if (c.data != c_in.data) release(c);
+            return out;
+        }
+        const int l = c.level, nl = hp_.nl(l), ne = nl + hp_.n_p, n = hp_.n;
+        const u32* c1 = c.data + (size_t)nl * n;
+        u32* ext = modup(c1, l, 1, 0);
+        for (size_t i = 0; i < steps.size(); ++i) {
+            if ((((long)steps[i] % sc + sc) % sc) == 0) {
+                out[i] = copy(c);
+                continue;
+            }
+            const u64 g = rot_galois(steps[i]);
+            u32* acc = tmp(2 * (size_t)ne);
+            key_inner(acc, ext, c1, ksk(g), l, g);
+            u32* p0 = tmp(nl);
+            launch_automorph(S(), T_, p0, c.data, g, nl);
+            out[i] = moddown(acc, l, p0, nullptr);
+            untmp(p0, nl);
+            untmp(acc, 2 * (size_t)ne);
+            cnt_[C_ROT]++;
+            cnt_[C_KS]++;
+        }
+        untmp(ext, ext_rows(l));
+        if (c.data != c_in.data) release(c);
+        return out;
+    }
     Ct rotate(const Ct& c, int steps) {
         const long s = slot_count();
         if (((long)steps % s + s) % s == 0) return copy(c);
@@ -2846,6 +2884,13 @@ int aesfhe_rescale(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) {
 int aesfhe_level_down(aesfhe_ctx* ctx, aesfhe_handle c, int level, aesfhe_handle* out) { CT_OP(e.level_down(e.canon(c), level)) }
 int aesfhe_rotate(aesfhe_ctx* ctx, aesfhe_handle c, int steps, aesfhe_handle* out) { CT_OP(e.rotate(e.canon(c), steps)) }
 int aesfhe_conjugate(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.conjugate(e.canon(c))) }
+int aesfhe_rotate_hoisted(aesfhe_ctx* ctx, aesfhe_handle c, int n, const int* steps, aesfhe_handle* out) {
+    API_BEGIN Engine& e = *ctx->eng;
+    if (n < 0 || (n > 0 && (!steps || !out))) throw std::runtime_error("rotate_hoisted: bad arguments");
+    std::vector<Ct> r = e.rotate_hoisted(e.canon(c), std::vector<int>(steps, steps + n));
+    for (int i = 0; i < n; ++i) out[i] = e.put_ct(r[i]);
+    API_END
+}
 int aesfhe_mul_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* a, const aesfhe_handle* b, aesfhe_handle* out) {
     API_BEGIN Engine& e = *ctx->eng;
     if (n < 0 || (n > 0 && (!a || !b || !out))) throw std::runtime_error("mul_many: bad arguments");

@@ -113,6 +113,10 @@ class EngineContext:
     def conjugate_many(self, cts):
         return self.engine.conjugate_many(cts)
 
+    def rotate_many(self, ct, steps):
+        """[rotate(ct, s) for s in steps], hoisted (one ModUp)"""
+        return self.engine.rotate_many(ct, steps)
+
     def rotate(self, ct, steps: int):
         """np.roll(slots, steps) semantics."""
         return self.engine.rotate(ct, self.rotation_key, steps)

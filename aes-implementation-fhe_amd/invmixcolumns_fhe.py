@@ -10,7 +10,7 @@ from mixcol_final import _CoeffCache, gf_basis16, gf_eval, gf_mult_pair
 from shift_rows import row_masks
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT
-from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap2, pair
+from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap2, pair, rot_many
 
 
 class InvMixColumnsFHE:
@@ -73,8 +73,8 @@ class InvMixColumnsFHE:
 
     def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
         log = (lambda k, v: debug.__setitem__(k, v)) if debug is not None else (lambda k, v: None)
-        rh, rl = pair(self.ctx, lambda: [self._col_shift_rowmajor(ct_hi, k) for k in (1, 2, 3)],
-                      lambda: [self._col_shift_rowmajor(ct_lo, k) for k in (1, 2, 3)])
+        steps = [-4 * k * self.stride for k in (1, 2, 3)]  # _col_shift_rowmajor(ct, k), hoisted
+        rh, rl = pair(self.ctx, lambda: rot_many(self.ctx, ct_hi, steps), lambda: rot_many(self.ctx, ct_lo, steps))
         rot = {k: (rh[k - 1], rl[k - 1]) for k in (1, 2, 3)}
         for k in (1, 2, 3):
             log(f"rotc{k}", rot[k])

@@ -16,7 +16,7 @@ import numpy as np
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT, SplitLUT2, batched, eval_two, joint_bases, powers, std_basis
-from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap2, can_fork, drop_to, fused_lut, pair
+from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap2, can_fork, drop_to, fused_lut, pair, rot_many
 
 
 class _CoeffCache:
@@ -169,8 +169,8 @@ class MixColFinal:
 
     def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
         log = (lambda k, v: debug.__setitem__(k, v)) if isinstance(debug, dict) else (lambda k, v: None)
-        rh, rl = pair(self.ctx, lambda: [self._col_shift_rowmajor(ct_hi, k) for k in (1, 2, 3)],
-                      lambda: [self._col_shift_rowmajor(ct_lo, k) for k in (1, 2, 3)])
+        steps = [-4 * k * self.stride for k in (1, 2, 3)]  # _col_shift_rowmajor(ct, k), hoisted
+        rh, rl = pair(self.ctx, lambda: rot_many(self.ctx, ct_hi, steps), lambda: rot_many(self.ctx, ct_lo, steps))
         rot = {k: (rh[k - 1], rl[k - 1]) for k in (1, 2, 3)}
         for k in (1, 2, 3):
             log(f"rotc{k}", rot[k])

@@ -91,6 +91,15 @@ def mul_many(ctx, pairs):
     return [ctx.multiply(a, b) for a, b in pairs]
 
 
+def rot_many(ctx, ct, steps):
+    """[ctx.rotate(ct, s) for s in steps], hoisted when the context has it (same results)"""
+    steps = list(steps)
+    f = getattr(ctx, "rotate_many", None)
+    if f is not None and len(steps) > 1:
+        return f(ct, steps)
+    return [ctx.rotate(ct, s) for s in steps]
+
+
 def conj_many(ctx, cts):
     """[ctx.conjugate(c) for c in cts], batched like mul_many"""
     cts = list(cts)

@@ -133,6 +133,11 @@ int aesfhe_conjugate(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
  * the results equal the separate calls bit for bit.  out[i] receives a new handle. */
 int aesfhe_mul_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* a, const aesfhe_handle* b, aesfhe_handle* out);
 int aesfhe_conjugate_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, aesfhe_handle* out);
+/* n rotations of ONE ciphertext, engine.rotate(ct, rotation_key, steps[i])
+ * (REF/engine_context.py:127-132; the column shifts of REF/mixcol_final.py:124-154 and the
+ * row rotations of REF/shift_rows.py:39-56), hoisted: one ModUp for all of them.  Same
+ * results as n aesfhe_rotate calls. */
+int aesfhe_rotate_hoisted(aesfhe_ctx* ctx, aesfhe_handle ct, int n, const int* steps, aesfhe_handle* out);
 /* engine.make_power_basis(ct, degree, relinearization_key), REF/engine_context.py:100-101;
  * out[k-1] = ct^k, k = 1..degree */
 int aesfhe_power_basis(aesfhe_ctx* ctx, aesfhe_handle ct, int degree, aesfhe_handle* out);

@@ -72,3 +72,13 @@ def test_batched_aes_blocks_decode_exactly(coeff_dir):
     assert np.array_equal(enc.decode(*g), A.GF_MUL[3][s1])
     sb = SubBytesLUT(ctx, co["sub_hi"], co["sub_lo"])
     assert np.array_equal(enc.decode(*sb.apply(*a, out_level=RENORM_FLOOR)), A.SBOX[s1])
+
+
+def test_rotate_hoisted_bit_exact(E):
+    """one ModUp for several rotations of one ciphertext equals separate rotations"""
+    c = _cts(E, 1, 31)[0]
+    s = E.slot_count
+    steps = [-(s // 4), -(s // 2), 0, 3 * s // 4, 5]
+    got = E.rotate_many(c, steps)
+    for st, g in zip(steps, got):
+        assert np.array_equal(E.export(g), E.export(E.rotate(c, None, st))), st
