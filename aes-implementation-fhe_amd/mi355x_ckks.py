@@ -287,7 +287,8 @@ class Engine:
         if early:
             self.profile([k for k in early.split(",") if k])
         self.set_lazy(lazy)
-        self.concurrent = bool(concurrent)
+        # AESFHE_SERIAL=1: every context runs its branches sequentially on one stream (A/B runs)
+        self.concurrent = bool(concurrent) and os.environ.get("AESFHE_SERIAL") != "1"
         self._pool = None
         self._tls = threading.local()
 
