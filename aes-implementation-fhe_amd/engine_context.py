@@ -11,6 +11,7 @@ test / smoke sets only).
 """
 from __future__ import annotations
 
+import hashlib
 import threading
 import time
 
@@ -201,11 +202,16 @@ class EngineContext:
         return self.engine.renorm_pair(hi, lo, states, level)
 
     def lut(self, key, coeffs, c0: complex = 0j):
-        """Engine-side coefficient set of a LUT polynomial, created once per key."""
+        """Engine-side coefficient set of a LUT polynomial, created once per key AND coefficient
+        content: callers key by object identity (id()), which Python reuses once an object is
+        collected, so a digest of the coefficients guards against a stale set"""
+        arr = np.ascontiguousarray(coeffs, dtype=np.complex128)
+        digest = hashlib.blake2b(arr.tobytes() + repr(arr.shape).encode() + np.complex128(c0).tobytes(), digest_size=16).digest()
+        full = (key, digest)
         with self._lut_lock:
-            t = self._luts.get(key)
+            t = self._luts.get(full)
             if t is None:
-                t = self._luts[key] = self.engine.lut_create(coeffs, c0)
+                t = self._luts[full] = self.engine.lut_create(coeffs, c0)
             return t
 
     def lut_eval(self, lut, a, b=None):
