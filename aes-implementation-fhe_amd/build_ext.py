@@ -34,14 +34,29 @@ def needs_build() -> bool:
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
+    """Each source is compiled to an object in parallel (no device code crosses translation
+    units: engine.hip reaches the kernels only through the host launch wrappers), then linked."""
     if not force and not needs_build():
         return LIB
-    cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-o", str(LIB)]
-    cmd += [str(CSRC / s) for s in SOURCES]
+    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"]
+    objdir = PKG / "build"
+    objdir.mkdir(exist_ok=True)
+    objs = [objdir / (s + ".o") for s in SOURCES]
+
+    def compile_one(i: int) -> None:
+        cmd = [_hipcc(), *flags, "-c", str(CSRC / SOURCES[i]), "-o", str(objs[i])]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True)
+
+    from concurrent.futures import ThreadPoolExecutor
+    workers = max(1, min(len(SOURCES), os.cpu_count() or 1, 8))
+    with ThreadPoolExecutor(workers) as ex:
+        list(ex.map(compile_one, range(len(SOURCES))))
+    tmp = LIB.with_suffix(".so.tmp")
+    cmd = [_hipcc(), *flags, "-shared", "-o", str(tmp), *map(str, objs)]
     if verbose:
         print(" ".join(cmd))
-    tmp = LIB.with_suffix(".so.tmp")
-    cmd[cmd.index("-o") + 1] = str(tmp)
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
     return LIB

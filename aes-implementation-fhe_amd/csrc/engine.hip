@@ -342,23 +342,54 @@ public:
         }
         return g;
     }
-    size_t ksk_words() const { return (size_t)hp_.dnum * 2 * (hp_.n_ks + hp_.n_p) * hp_.n; }
+    // The dense -> sparse key of the bootstrap (step 2) is an RLWE sample under
+    // the h = 32 sparse secret, so its modulus must stay small: it lives modulo q0 * P' only,
+    // P' = the first kD2sP special primes (~95 bits), not on all n_ks + n_p limbs (~1,700 bits,
+    // where a sparse secret is recoverable and with it the dense secret).  Layout [2][1 + kD2sP][N].
+    static constexpr int kD2sP = 2;
+    int d2s_np() const { return std::min(kD2sP, hp_.n_p); }
+    size_t ksk_words(u64 g) const {
+        if (g == tag_d2s()) return (size_t)2 * (1 + d2s_np()) * hp_.n;
+        return (size_t)hp_.dnum * 2 * (hp_.n_ks + hp_.n_p) * hp_.n;
+    }
+    double d2s_modulus_bits() const {
+        double b = std::log2((double)hp_.mod[0]);
+        for (int k = 0; k < d2s_np(); ++k) b += std::log2((double)hp_.mod[hp_.p_off() + k]);
+        return b;
+    }
+    const u32* ksk_d2s() {
+        const u64 g = tag_d2s();
+        const int n = hp_.n, ne = 1 + d2s_np();
+        void* raw = nullptr;
+        HIP_OK(hipMalloc(&raw, ksk_words(g) * sizeof(u32)));
+        u32* b = (u32*)raw;
+        u32* a = b + (size_t)ne * n;
+        const LimbMap em = extmap(1);  // row 0: q0, rows 1..: the first special primes
+        u32* e = tmp(ne);
+        launch_sample_uniform(S(), T_, a, ne, em, hp_.seed, stream_id(4, g, 0));
+        launch_sample_small(S(), T_, e, ne, em, hp_.seed, stream_id(5, g, 0), 1);
+        ntt(e, ne, ne, em);
+        // b = -a s_sp + e + (P' mod q0) s on the q0 row
+        launch_keygen_combine(S(), T_, b, a, sparse_secret(), e, d_s_, d_d2s_, ne, em, 0, 1);
+        untmp(e, ne);
+        ksk_[g] = b;
+        HIP_OK(hipStreamSynchronize(S()));
+        return b;
+    }
     const u32* ksk(u64 g) {
         auto it = ksk_.find(g);
         if (it != ksk_.end()) return it->second;
         if (!d_s_) throw std::runtime_error("keys not generated");
+        if (g == tag_d2s()) return ksk_d2s();
         const int n = hp_.n, nks = hp_.n_ks, np = hp_.n_p, nkey = nks + np;
         void* raw = nullptr;
-        HIP_OK(hipMalloc(&raw, ksk_words() * sizeof(u32)));
+        HIP_OK(hipMalloc(&raw, ksk_words(g) * sizeof(u32)));
         u32* key = (u32*)raw;
         // source secret s' (Q limbs 0..n_ks-1) and target secret (all primes) of the key
         u32* sp = tmp(nks);
         const u32* target = d_s_;
         if (g == 0) {
             launch_square(S(), T_, sp, d_s_, nks, nks, qmap());
-        } else if (g == tag_d2s()) {  // dense s -> sparse ephemeral s_sp (bootstrapping)
-            launch_copy_rows(S(), T_, sp, d_s_, nks);
-            target = sparse_secret();
         } else if (g == tag_s2d()) {  // sparse s_sp -> dense s
             launch_copy_rows(S(), T_, sp, sparse_secret(), nks);
         } else {
@@ -1236,6 +1267,60 @@ public:
         cnt_[C_KS] += nb;
         return o;
     }
+    // bootstrapping step 2: the single-limb (q0) ciphertexts' d = c1 switched to the sparse
+    // secret with ksk_d2s (modulus q0 * P', P' = d2s_np() special primes); (c0', c1') with
+    // c0' = add0 + ...; nb members at d + m ms / add0 + m ms
+    Ct keyswitch_d2s(const u32* d, const u32* add0, int nb, size_t ms) {
+        const int n = hp_.n, np = d2s_np(), ne = 1 + np, npl = 2 * nb;
+        if (npl > kMaxConvGroups || nb > kMaxKsBatch) throw std::runtime_error("keyswitch_d2s: batch too large");
+        const LimbMap em = extmap(1);
+        const u32* key = ksk(tag_d2s());
+        // ModUp q0 -> P': the level-0 digit-0 table (h = 1; its [1][1 + n_p] rows start with P')
+        u32* coef = tmp(nb);
+        intt(coef, d, nb, RowMap{1, (int)(ms / n), 1, 0, 0}, single(0));
+        u32* ext = tmp((size_t)nb * ne);
+        ConvBatch up;
+        up.n = nb;
+        for (int m = 0; m < nb; ++m) {
+            up.h[m] = 1, up.d0[m] = 0, up.skip0[m] = 0;
+            up.src[m] = coef + (size_t)m * n;
+            up.dst[m] = ext + (size_t)m * ne * n;
+            up.tab[m] = d_modup_ + modup_off_[(size_t)1 * hp_.dnum];
+            up.qhinv[m] = up.tab[m] + (size_t)2 * (1 + hp_.n_p);
+            up.negq[m] = up.qhinv[m] + 2;
+        }
+        launch_base_convert(S(), T_, up, ne, em);
+        untmp(coef, nb);
+        RowMap xr = rows_dense(ne);
+        xr.skip_alpha = hp_.alpha, xr.skip_nl = 1, xr.skip_groups = 1;
+        ntt(ext, ext, nb * ne, xr, em);
+        u32* acc = tmp((size_t)npl * ne);
+        launch_key_inner(S(), T_, acc, ext, d, key, 1, ne, 1, hp_.alpha, ne, 1, em, 0, nb, (size_t)ne * n, ms, (size_t)2 * ne * n);
+        untmp(ext, (size_t)nb * ne);
+        // ModDown by P' onto q0, + add0
+        u32* yp = tmp((size_t)npl * np);
+        intt(yp, acc, npl * np, RowMap{np, ne, np, 1, 0}, LimbMap{np, hp_.p_off(), 0});
+        u32* conv = tmp(npl);
+        ConvBatch dn;
+        dn.n = npl;
+        for (int p = 0; p < npl; ++p) {
+            dn.h[p] = np, dn.d0[p] = hp_.p_off(), dn.skip0[p] = 1 << 30;
+            dn.src[p] = yp + (size_t)p * np * n;
+            dn.dst[p] = conv + (size_t)p * n;
+            dn.tab[p] = d_d2s_ + 2;                     // [np][1] pairs: P'/p_k mod q0
+            dn.qhinv[p] = d_d2s_ + 2 + 2 * np;          // [np] pairs: (P'/p_k)^-1 mod p_k
+            dn.negq[p] = d_d2s_ + 2 + 4 * np;           // -P' mod q0
+        }
+        launch_base_convert(S(), T_, dn, 1, qmap());
+        untmp(yp, (size_t)npl * np);
+        Ct o = alloc_ct(-1, npl, nb);
+        launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_d2s_ + 3 + 4 * np, add0, nullptr, npl, 1, ms);
+        cnt_[C_NTT_ROWS] += (size_t)npl;
+        untmp(conv, npl);
+        untmp(acc, (size_t)npl * ne);
+        cnt_[C_KS] += nb;
+        return o;
+    }
 
     // relinearisation fused with the rescale that follows it: one ModDown by
     // Q' = P * (the dropped limbs of level l).  key_inner folds P (c0, c1) into acc's Q rows, so
@@ -1791,6 +1876,9 @@ public:
         out[3] = kBootK;
         out[4] = kBootR;
         out[5] = kBootDeg;
+        out[6] = d2s_modulus_bits();
+        out[7] = kSparseH;
+        out[8] = d2s_np();
     }
 
     // diagonals of one group encoded at `level` (scale ptscale_level) on the Q limbs AND the
@@ -2263,7 +2351,7 @@ public:
         release(z);
         if (stop_after == 1) return b;
         // 2. sparse-secret encapsulation: dense s -> sparse s_sp at modulus q0
-        Ct sp = keyswitch(b.data + n, -1, ksk(tag_d2s()), b.data, nullptr, nb, 2 * (size_t)n, 2 * (size_t)n);
+        Ct sp = keyswitch_d2s(b.data + n, b.data, nb, 2 * (size_t)n);
         release(b);
         if (stop_after == 2) return sp;
         // 3. ModRaise: centred lift of both polynomials to every limb of the top level
@@ -2364,7 +2452,7 @@ public:
         if (!d_pk_) throw std::runtime_error("keys not generated");
         export_dev(d_pk_, (size_t)2 * hp_.n_q * hp_.n, out);
     }
-    void export_ksk(u64 g, u32* out) { export_dev(ksk(g), ksk_words(), out); }
+    void export_ksk(u64 g, u32* out) { export_dev(ksk(g), ksk_words(g), out); }
     void debug_ntt(u32* data, int rows, int first_prime, int inverse) {
         u32* d = tmp(rows);
         HIP_OK(hipMemcpyAsync(d, data, sizeof(u32) * rows * hp_.n, hipMemcpyHostToDevice, S()));
@@ -2637,6 +2725,34 @@ private:
         }
         d_mdr_ = dev_upload(mdr);
 
+        // dense -> sparse key switch over q0 * P' (ksk_d2s): [P' mod q0 pair][np pairs P'/p_k mod q0]
+        // [np pairs (P'/p_k)^-1 mod p_k][-P' mod q0][P'^-1 mod q0 pair]
+        {
+            const int npd = d2s_np();
+            std::vector<u32> t;
+            u32 pq = 1;
+            for (int k = 0; k < npd; ++k) pq = mulm(pq, q[hp_.p_off() + k], q[0]);
+            t.push_back(pq), t.push_back(shoup_pre(pq, q[0]));
+            for (int k = 0; k < npd; ++k) {
+                u32 v = 1;
+                for (int m2 = 0; m2 < npd; ++m2)
+                    if (m2 != k) v = mulm(v, q[hp_.p_off() + m2], q[0]);
+                t.push_back(v), t.push_back(shoup_pre(v, q[0]));
+            }
+            for (int k = 0; k < npd; ++k) {
+                const u32 pk = q[hp_.p_off() + k];
+                u32 v = 1;
+                for (int m2 = 0; m2 < npd; ++m2)
+                    if (m2 != k) v = mulm(v, q[hp_.p_off() + m2], pk);
+                const u32 inv = hinvm(v, pk);
+                t.push_back(inv), t.push_back(shoup_pre(inv, pk));
+            }
+            t.push_back(pq ? q[0] - pq : 0);
+            const u32 inv = hinvm(pq, q[0]);
+            t.push_back(inv), t.push_back(shoup_pre(inv, q[0]));
+            d_d2s_ = dev_upload(t);
+        }
+
     }
 
     HostParams hp_;
@@ -2671,6 +2787,7 @@ private:
     u32* d_moddown_phinv_ = nullptr;
     std::vector<size_t> moddown_off_;
     u32* d_mdr_ = nullptr;       // ModDown fused with the rescale, per level (see build_tables)
+    u32* d_d2s_ = nullptr;       // dense -> sparse key switch constants over q0 * P' (see build_tables)
     std::vector<size_t> mdr_off_;
     bool batch_ops_ = std::getenv("AESFHE_BATCH_OPS") == nullptr || std::getenv("AESFHE_BATCH_OPS")[0] != '0';
     bool stack_evalmod_ = std::getenv("AESFHE_STACK_EVALMOD") == nullptr || std::getenv("AESFHE_STACK_EVALMOD")[0] != '0';

@@ -8,7 +8,6 @@
 #include <algorithm>
 #include "launch.h"
 
-#define CHECK_LAUNCH() (void)hipGetLastError()
 
 namespace {
 
@@ -974,6 +973,7 @@ void launch_decode16(hipStream_t st, const DevTables& T, const u32* x, const int
 }
 void launch_snap16(hipStream_t st, const double* acc, double* w, int* nib) {
     hipLaunchKernelGGL(k_snap16, dim3(1), dim3(64), 0, st, acc, w, nib);
+    launch_check();
 }
 void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq) {
     prof_launch(KID_ELEMENTWISE, words(2.0 * nq * (1u << T.logn)), k_encode16, dim3((1u << T.logn) / kBlock, 2), dim3(kBlock), 0, st, out,

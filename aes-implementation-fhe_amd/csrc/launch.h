@@ -8,9 +8,19 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <stdexcept>
+#include <string>
+
 #include "kernels.h"
 
 extern thread_local KernelProfiler* g_prof;
+
+// every launch is checked: a bad configuration fails the API call that issued it (the C-ABI
+// turns the exception into an error status) instead of surfacing later as wrong data
+inline void launch_check() {
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) throw std::runtime_error(std::string("kernel launch failed: ") + hipGetErrorString(e));
+}
 
 template <typename F, typename... Args>
 inline void prof_launch(int kid, double bytes, F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st, Args... args) {
@@ -22,6 +32,7 @@ inline void prof_launch(int kid, double bytes, F kernel, dim3 grid, dim3 block, 
     } else {
         hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
     }
+    launch_check();
 }
 
 // launch of a kernel whose last parameter is an in-kernel clock slot (nullptr = untimed);
@@ -33,6 +44,7 @@ inline void prof_launch_tsw(int kid, double bytes, double work, F kernel, dim3 g
     unsigned long long* ts = nullptr;
     if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) ts = p->ts_slot(kid, bytes, work);
     hipLaunchKernelGGL(kernel, grid, block, lds, st, args..., ts);
+    launch_check();
 }
 template <typename F, typename... Args>
 inline void prof_launch_ts(int kid, double bytes, F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st, Args... args) {

@@ -4,7 +4,8 @@ the MI355X engine (mi355x_ckks, a ctypes binding of libaesfhe.so).
 Same constructor keywords, same methods, same error-string behaviour; the AES round
 modules only ever talk to this object.  Extra keywords: ``log_n`` (N = 2^log_n, default
 2^16 as in the reference harness; config 1 of BASELINE.json uses 2^15), ``dnum`` and
-``seed`` (deterministic key material), ``lazy`` (deferred relinearisation),
+``seed`` (key material; drawn from ``os.urandom`` when None, pinned only by tests, smoke and
+multi-rank runs that share one key set), ``lazy`` (deferred relinearisation),
 ``concurrent`` (hi / lo halves on two HIP streams), ``fused_luts`` (one-kernel LUT sums,
 DESIGN.md §3.8) and ``allow_insecure`` (parameter sets above the 128-bit bound, for small
 test / smoke sets only).
@@ -25,7 +26,7 @@ _SIG_DEFAULT_LEVEL = 17
 class EngineContext:
     def __init__(self, signature: int, *, max_level: int = 17, use_bootstrap: bool = True,
                  use_multiparty: bool = False, mode: str = "cpu", device_id: int = 0,
-                 thread_count: int | None = None, log_n: int = 16, dnum: int | None = None, seed: int = 0x5EED,
+                 thread_count: int | None = None, log_n: int = 16, dnum: int | None = None, seed: int | None = None,
                  lazy: bool = True, concurrent: bool = True, fused_luts: bool = True, allow_insecure: bool = False):
         # REF/engine_context.py:17-42: signature selects the engine constructor form
         if signature == 1:
@@ -202,17 +203,24 @@ class EngineContext:
         return self.engine.renorm_pair(hi, lo, states, level)
 
     def lut(self, key, coeffs, c0: complex = 0j):
-        """Engine-side coefficient set of a LUT polynomial, created once per key AND coefficient
-        content: callers key by object identity (id()), which Python reuses once an object is
-        collected, so a digest of the coefficients guards against a stale set"""
+        """Engine-side coefficient set of a LUT polynomial, created once per coefficient CONTENT
+        (a digest of the coefficients, their shape and c0).  `key` is the caller's label and is
+        not part of the cache key: a label built from id() can be inherited by a new object with
+        other coefficients once the old one is collected (the stale-set failure of DESIGN.md §9),
+        and keying by content lets every module with the same set share one device copy, so the
+        cache is bounded by the number of distinct sets (the 22 coefficient files and their splits)."""
         arr = np.ascontiguousarray(coeffs, dtype=np.complex128)
         digest = hashlib.blake2b(arr.tobytes() + repr(arr.shape).encode() + np.complex128(c0).tobytes(), digest_size=16).digest()
-        full = (key, digest)
         with self._lut_lock:
-            t = self._luts.get(full)
+            t = self._luts.get(digest)
             if t is None:
-                t = self._luts[full] = self.engine.lut_create(coeffs, c0)
+                t = self._luts[digest] = self.engine.lut_create(coeffs, c0)
             return t
+
+    def clear_luts(self):
+        """drop the cached coefficient sets (their device memory is freed with the last reference)"""
+        with self._lut_lock:
+            self._luts.clear()
 
     def lut_eval(self, lut, a, b=None):
         """sum C[p,q] a[p] b[q] (or c0 + sum C[k] a[k]) in one fused kernel."""

@@ -251,7 +251,7 @@ class Engine:
 
     def __init__(self, *, mode: str = "gpu", use_bootstrap: bool = False, use_multiparty: bool = False,
                  thread_count: int = 0, device_id: int = 0, max_level: int = 17, log_n: int = 16,
-                 dnum: int | None = None, seed: int = 0x5EED, lazy: bool = True, concurrent: bool = True,
+                 dnum: int | None = None, seed: int | None = None, lazy: bool = True, concurrent: bool = True,
                  allow_insecure: bool = False):
         if use_multiparty:
             raise ValueError("multiparty key generation is not supported")
@@ -263,7 +263,13 @@ class Engine:
         # ~5 % more time (more ModUp rows per key switch)
         if dnum is None:
             dnum = int(os.environ.get("AESFHE_BOOT_DNUM", "5")) if use_bootstrap else 3
-        self._ctx = _Context(log_n, max_level, dnum, device_id, seed, bootstrappable=use_bootstrap)
+        # key material and encryption randomness derive from `seed`: drawn from
+        # the OS entropy source unless the caller pins it (parity tests, smoke, multi-rank runs
+        # that broadcast one seed so every rank holds the same keys)
+        if seed is None:
+            seed = int.from_bytes(os.urandom(8), "little")
+        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+        self._ctx = _Context(log_n, max_level, dnum, device_id, self.seed, bootstrappable=use_bootstrap)
         L = self._ctx.lib
         self.fresh_level = max_level
         self.slot_count = int(L.aesfhe_slot_count(self._ctx.ptr))
@@ -509,9 +515,10 @@ class Engine:
 
     def boot_info(self) -> dict:
         self._ensure_keys()
-        out = np.zeros(6)
+        out = np.zeros(9)
         self._ctx.check(self._lib.aesfhe_boot_info(self._ctx.ptr, out))
-        return dict(zip(["s_bt", "k1", "top", "K", "r", "deg"], out.tolist()))
+        return dict(zip(["s_bt", "k1", "top", "K", "r", "deg", "d2s_log_modulus", "sparse_h", "d2s_special_primes"],
+                        out.tolist()))
 
     def ntt(self, ct):
         return self._new(self._lib.aesfhe_to_ntt, ct.handle)
@@ -604,7 +611,11 @@ class Engine:
 
     def export_ksk(self, galois: int) -> np.ndarray:
         self._ensure_keys()
-        out = np.zeros((self.dnum, 2, self.n_ks + self.n_p, self.n), np.uint32)
+        if galois == 2 * self.n + 1:  # dense -> sparse bootstrapping key: [2][q0 + P' limbs][N]
+            np_d2s = int(self.boot_info()["d2s_special_primes"])
+            out = np.zeros((1, 2, 1 + np_d2s, self.n), np.uint32)
+        else:
+            out = np.zeros((self.dnum, 2, self.n_ks + self.n_p, self.n), np.uint32)
         self._ctx.check(self._lib.aesfhe_export_ksk(self._ctx.ptr, int(galois), out))
         return out
 

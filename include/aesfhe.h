@@ -157,12 +157,14 @@ int aesfhe_bootstrap_depth(void);
 /* host self-check of the bootstrap plan: err[0] SlotToCoeff, err[1] CoeffToSlot vs the
  * canonical embedding, err[2] EvalMod Chebyshev error (no GPU needed) */
 int aesfhe_debug_bootplan(int log_n, double* err3);
-/* debug: run bootstrap up to a stage (1..11, see engine.hip) and return that ciphertext;
- * ephemeral sparse secret (NTT form, all limbs); [s_bt, k1, top, K, r, deg] */
+/* debug: run bootstrap up to a stage (1..11, see engine.hip) and return that ciphertext */
 int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle ct, int stage, aesfhe_handle* out);
+/* ephemeral sparse secret (NTT form, all limbs) */
 int aesfhe_export_sparse(aesfhe_ctx* ctx, uint32_t* out);
 int aesfhe_debug_lin_group(aesfhe_ctx* ctx, aesfhe_handle ct, int which, aesfhe_handle* out);
-int aesfhe_boot_info(aesfhe_ctx* ctx, double* out6);
+/* [s_bt, k1, top, K, r, deg, log2 modulus of the dense->sparse key (q0 P'), sparse
+ * secret weight h, special primes in P'] */
+int aesfhe_boot_info(aesfhe_ctx* ctx, double* out9);
 /* Zeta16 secret-key renorm of a (hi, lo) state pair (REF/pipeline.py:65-69): decrypt,
  * snap the 16 strided slots to the nearest codeword, refill others with 1, re-encrypt */
 int aesfhe_renorm_pair(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle* out_hi, aesfhe_handle* out_lo);

@@ -97,3 +97,34 @@ def test_bootstrap_pair_bit_exact(ctx):
     assert np.array_equal(E.export(pa), E.export(sa))
     assert np.array_equal(E.export(pb), E.export(sb))
     assert np.abs(ctx.decrypt(pb) - zb).max() < BOOT_TOL
+
+
+def test_dense_to_sparse_key_modulus(ctx):
+    """The dense -> sparse bootstrapping key is an RLWE sample under the h = 32 sparse
+    secret, so it lives modulo q0 * P' only (~95 bits), never on the full
+    Q * P chain.  Checks the width and the key equation b + a s_sp = e + (P' mod q0) s on
+    q0 and e on the P' limbs, with e a centred binomial (|e| <= 21)."""
+    E = ctx.engine
+    info = E.boot_info()
+    assert info["sparse_h"] == 32
+    assert info["d2s_log_modulus"] < 100.0
+    npd = int(info["d2s_special_primes"])
+    key = E.export_ksk(2 * E.n + 1).astype(np.uint64)
+    assert key.shape == (1, 2, 1 + npd, E.n)
+    q = E.moduli().astype(np.uint64)
+    primes = [0] + [E.n_q + k for k in range(npd)]
+    assert abs(sum(np.log2(float(q[p])) for p in primes) - info["d2s_log_modulus"]) < 1e-9
+    s_sp = E.export_sparse().astype(np.uint64)
+    s = E.export_secret().astype(np.uint64)
+    b, a = key[0, 0], key[0, 1]
+    pq = 1
+    for k in range(npd):
+        pq = pq * int(q[E.n_q + k]) % int(q[0])
+    for row, p in enumerate(primes):
+        qt = q[p]
+        r = (b[row] + a[row] * s_sp[p] % qt) % qt
+        if row == 0:
+            r = (r + qt - np.uint64(pq) * s[0] % qt) % qt
+        e = E.debug_ntt(r.astype(np.uint32)[None], p, inverse=True)[0].astype(np.int64)
+        e = np.where(e > int(qt) // 2, e - int(qt), e)
+        assert np.abs(e).max() <= 21, (row, np.abs(e).max())

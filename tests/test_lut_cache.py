@@ -1,5 +1,5 @@
-"""EngineContext.lut keys its cache by the caller's key AND a digest of the coefficients:
-callers key by id(), which Python reuses once an object is collected, and a stale
+"""EngineContext.lut keys its cache by a digest of the coefficient content only: callers
+label sets with id(), which Python reuses once an object is collected, and a stale
 coefficient set was the cause of an intermittent all-states-wrong packed run.
 CPU-only: the engine is replaced by a recorder."""
 import threading
@@ -36,3 +36,13 @@ def test_same_key_different_coefficients_get_different_luts():
     t2 = ctx.lut(key, b)
     assert t2 != t1 and len(ctx.engine.made) == 2
     assert ctx.lut(key, a, c0=1j) not in (t1, t2)  # the constant term is part of the set
+
+
+def test_cache_is_bounded_by_content():
+    """Many short-lived owners of the same coefficient set share one device LUT (no growth)."""
+    ctx = _ctx()
+    a = np.arange(16, dtype=np.complex128)
+    handles = {ctx.lut(("xor4", i), a) for i in range(100)}
+    assert len(handles) == 1 and len(ctx._luts) == 1 and len(ctx.engine.made) == 1
+    ctx.clear_luts()
+    assert not ctx._luts
