@@ -57,8 +57,13 @@ def parse():
                     help="hi/lo halves on one stream (same launches, no overlap): for rocprofv3 --pmc passes, whose "
                          "counter collection crashes on launches from the branch threads")
     ap.add_argument("--dry-run", action="store_true",
-                    help="host orchestration only (process group, sharding, barrier, max-over-ranks, rank-0 line) with the "
-                         "byte-level AES in place of the FHE engine; prints value null -- a test harness, not a measurement")
+                    help="the N-rank host path on CPU (process group, shared-seed key broadcast, sharding, barrier, "
+                         "max-over-ranks, rank-0 line) with one CPU oracle engine per rank running AddRoundKey (config C1 "
+                         "shape at N=2^13) in place of the GPU engine; prints value null -- a test harness, not a measurement")
+    ap.add_argument("--seed", type=int, default=None,
+                    help="key seed shared by every rank (default: drawn from os.urandom on rank 0 and broadcast)")
+    ap.add_argument("--c5-states", type=int, default=1024,
+                    help="BASELINE config 5: total states of the enc->dec round trip, split evenly across ranks")
     ap.add_argument("--batch-states", type=int, default=1024,
                     help="secondary measurement (BASELINE configs 3/4): this many independent states per rank, "
                          "slot-packed into one ciphertext pair (SURVEY.md 8(f)1); 0 = skip")
@@ -90,6 +95,35 @@ def dist_setup(want: int):
     if want > 1:
         raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one process per GPU)")
     return 0, 1, 0, None
+
+
+def shared_seed(dist, seed: int | None) -> int:
+    """One key set for the whole job: rank 0 draws the seed (or takes --seed)
+    and broadcasts it once, before any timed region; every rank then derives identical keys.
+    This is the only collective outside the timing barriers and the max-over-ranks."""
+    if seed is None:
+        seed = int.from_bytes(os.urandom(8), "little") >> 1  # int64-safe
+    if dist is None:
+        return int(seed)
+    import torch
+    gpu = dist.get_backend() == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
+    t = torch.tensor([seed], dtype=torch.int64, device=dev)
+    dist.broadcast(t, src=0)
+    return int(t.item())
+
+
+def all_gather_ints(dist, vals):
+    """rank-ordered list of every rank's small int list (host bookkeeping after timing)"""
+    if dist is None:
+        return [list(vals)]
+    import torch
+    gpu = dist.get_backend() == "nccl"
+    dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
+    t = torch.tensor(list(vals), dtype=torch.int64, device=dev)
+    got = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(got, t)
+    return [[int(x) for x in g.cpu().tolist()] for g in got]
 
 
 def barrier(dist):
@@ -187,19 +221,38 @@ def run_batch(ctx, coeffs, rks, args, rank, world, dist) -> dict:
     for b, o in zip(batches[1:], outs):
         got = pipe.encoder.decode(*o)
         ok &= all(np.array_equal(got[j], aes_plain.ref_encrypt(b[j], rks)) for j in range(B))
+    ok = all(r[0] for r in all_gather_ints(dist, [int(ok)]))
     rt = None
     if args.batch_roundtrip:
-        # BASELINE config 5: decrypt the same batch (InvMixColumns inserted)
+        # BASELINE config 5: enc -> dec of --c5-states states in total, split across the ranks
+        # (1024 = 128 per GPU at N = 8); decrypt inserts InvMixColumns
+        B5 = max(1, -(-args.c5_states // world))
+        if B5 == B:  # same shape as the batch leg: decrypt its outputs
+            pipe5, ins5, outs5, enc_s = pipe, batches[1:], outs, elapsed
+        else:
+            pipe5 = AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=True, states=B5)
+            ins5 = [rng.integers(0, 256, (B5, 16), dtype=np.uint8) for _ in range(args.batch_steps)]
+            pipe5.encrypt(ins5[0], rks)  # warmup of the new shape
+            E.sync()
+            barrier(dist)
+            t1 = time.perf_counter()
+            outs5 = [pipe5.encrypt(b, rks) for b in ins5]
+            E.sync()
+            barrier(dist)
+            enc_s = max_over_ranks(dist, time.perf_counter() - t1)
         barrier(dist)
         t1 = time.perf_counter()
-        backs = [pipe.decrypt(*o, rks) for o in outs]
+        backs = [pipe5.decrypt(*o, rks) for o in outs5]
         E.sync()
         barrier(dist)
         dec_s = max_over_ranks(dist, time.perf_counter() - t1)
-        exact = all(np.array_equal(pipe.encoder.decode(*bk), b) for bk, b in zip(backs, batches[1:]))
-        rt = {"workload": "C5: decrypt of the encrypted batch (InvMixColumns + bootstrap + snap), enc->dec round trip",
+        exact = all(np.array_equal(pipe5.encoder.decode(*bk), b) for bk, b in zip(backs, ins5))
+        exact = all(r[0] for r in all_gather_ints(dist, [int(exact)]))
+        rt = {"workload": f"C5: enc->dec round trip (InvMixColumns + bootstrap + snap) of {B5 * world} states, "
+                          f"{B5} per GPU slot-packed in one ciphertext pair",
+              "states_per_rank": B5, "enc_ms_per_step": enc_s / args.batch_steps * 1e3,
               "dec_ms_per_step": dec_s / args.batch_steps * 1e3,
-              "roundtrip_blocks_per_s": B * args.batch_steps * world / (elapsed + dec_s),
+              "roundtrip_blocks_per_s": B5 * args.batch_steps * world / (enc_s + dec_s),
               "roundtrip_bit_exact": bool(exact)}
     blocks = B * args.batch_steps * world
     return {"workload": f"C3/C4: {B} independent states per GPU slot-packed in one ciphertext pair (SURVEY.md 8(f)1), "
@@ -211,27 +264,39 @@ def run_batch(ctx, coeffs, rks, args, rank, world, dist) -> dict:
 
 
 def dry_run(args, rank, world, dist):
-    from aes_keyschedule import expand_aes128_key
-    from oracle import aes_plain
+    """The N > 1 host path with a real engine per rank, on CPU: one oracle CKKS engine per rank
+    (oracle/ckks_cpu.py, N = 2^13) keyed by the broadcast seed, AddRoundKey on the rank's own
+    states under one shared round key, decoded and checked per rank."""
+    from add_round_key import AddRoundKey, default_xor4_coeffs
+    from oracle.ckks_cpu import OracleContext
+    from state_encoder import StateEncoder
+    from xor4_lut import XOR4LUT
+    seed = shared_seed(dist, args.seed)
+    ctx = OracleContext(log_n=13, max_level=6, seed=seed & 0x7FFFFFFF)
+    enc = StateEncoder(ctx)
+    ark = AddRoundKey(XOR4LUT(ctx, default_xor4_coeffs()))
     np.random.seed(7)
-    rks = expand_aes128_key(np.random.randint(0, 256, 16, dtype=np.uint8))
+    key = np.random.randint(0, 256, 16, dtype=np.uint8)
     states = rank_states(rank, args.warmup + args.steps)
+    kc = enc.encode(key)
+    for i in range(args.warmup):
+        ark(*enc.encode(states[i]), *kc)
     barrier(dist)
     t0 = time.perf_counter()
-    outs = [aes_plain.ref_encrypt(states[i], rks) for i in range(args.warmup, args.warmup + args.steps)]
+    outs = [ark(*enc.encode(states[i]), *kc) for i in range(args.warmup, args.warmup + args.steps)]
     barrier(dist)
     elapsed = max_over_ranks(dist, time.perf_counter() - t0)
-    firsts = [int(states[args.warmup][0])]
-    if dist is not None:
-        import torch
-        t = torch.tensor(firsts, dtype=torch.int64)
-        got = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(got, t)
-        firsts = [int(g.item()) for g in got]
+    ok = all(np.array_equal(enc.decode(*o), states[args.warmup + j] ^ key) for j, o in enumerate(outs))
+    sk = ctx.eng.p.secret()
+    fp = int(np.bitwise_xor.reduce((sk[:64].astype(np.int64) + 2) * np.arange(1, 65)))  # secret-key fingerprint
+    rows = all_gather_ints(dist, [int(states[args.warmup][0]), int(ok), fp])
     if rank == 0:
         print(json.dumps({"metric": "homomorphic AES-128 rounds/sec (enc) at N=2^16", "value": None, "dry_run": True,
-                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "elapsed_max_s": elapsed,
-                          "first_byte_per_rank": firsts, "outputs": len(outs) * world}), flush=True)
+                          "engine": "CPU oracle per rank (N=2^13, AddRoundKey)", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "elapsed_max_s": elapsed,
+                          "first_byte_per_rank": [r[0] for r in rows], "ark_exact_per_rank": [bool(r[1]) for r in rows],
+                          "same_keys_on_every_rank": len({r[2] for r in rows}) == 1, "outputs": len(outs) * world}),
+              flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
@@ -251,7 +316,8 @@ def main():
 
     coeffs = load_all_coeffs()
     signature = 2 if args.no_final_bootstrap else 1
-    ctx = EngineContext(signature=signature, max_level=17, thread_count=1, device_id=local, seed=0x5EED + rank, lazy=not args.eager,
+    seed = shared_seed(dist, args.seed)  # one key set for every rank (broadcast once, untimed)
+    ctx = EngineContext(signature=signature, max_level=17, thread_count=1, device_id=local, seed=seed, lazy=not args.eager,
                         concurrent=not args.serial)
     xor4 = XOR4LUT(ctx, coeffs["xor4"])
     mix = MixColFinal(ctx, xor4)
@@ -293,6 +359,7 @@ def main():
     # correctness of the timed outputs (outside the timed region)
     ok = all(np.array_equal(pipe.encoder.decode(*o), aes_plain.ref_encrypt(states[args.warmup + j], rks))
              for j, o in enumerate(outs))
+    ok = all(r[0] for r in all_gather_ints(dist, [int(ok)]))  # every rank's outputs verified
 
     states_done = args.steps * world
     value = 10.0 * states_done / elapsed
@@ -344,7 +411,12 @@ def main():
                                "N=2^16, renorm on" + ("" if not args.no_final_bootstrap else ", FINAL BOOTSTRAP SKIPPED"),
                    "log_n": 16, "states_per_rank_per_step": 1, "parallelism": f"replicas x{world}",
                    "evaluation": "eager (relinearise + rescale after every product)" if args.eager else
-                   "deferred relinearisation/rescale of products (DESIGN.md 3.7); module call sequence unchanged",
+                   ("optimised evaluation, same module interfaces and outputs: deferred relinearisation/rescale "
+                    "(DESIGN.md 3.7), fused LUT kernels with one relinearisation per LUT, XOR4/GF LUTs over a conjugate "
+                    "split, SubBytes by baby-step giant-step (3.8), XOR chain as a tree (6), hoisted column rotations, "
+                    "inputs dropped to the renorm floor before renormalised steps (3.11), batched products (3.12); "
+                    "the engine op counts per round are in op_counts_per_round (REF's call sequence issues ~1,034 "
+                    "relinearisations per round, SURVEY.md 8(a))"),
                    "blocks_per_s": states_done / elapsed, "verified_against_plaintext_model": bool(ok)},
         "roofline": roofline(args.kernel, "dominant kernel by time (NTT pass 2 incl. fused rescale/ModDown epilogue); "
                                           "VALU-bound by 3 u32 multiplies per butterfly (DESIGN.md 5)"),
