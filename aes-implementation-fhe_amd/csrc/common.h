@@ -1,11 +1,12 @@
 // common.h -- shared types and 32-bit modular arithmetic for the MI355X CKKS engine.
 //
-// Every RNS prime q lies in (2^30, floor(2^32/3)), which lets all
-// modular products run on 32-bit VALU multiplies (v_mul_lo_u32 / v_mul_hi_u32) with
-// no 64-bit emulation:
+// Every RNS prime q lies in (2^29, 2^30), which lets all modular
+// products run on 32-bit VALU multiplies (v_mul_lo_u32 / v_mul_hi_u32) with no 64-bit
+// emulation:
 //   * Shoup    (constant operand w, w' = floor(w*2^32/q)):  3 multiplies, result < 2q
-//   * Barrett  (two variable operands, mu = floor(2^62/q)): 4 multiplies, result < 3q
-// 3q < 2^32, so the wrapped 32-bit differences below are exact.
+//   * Barrett  (two variable operands, mu = floor(2^61/q)): 4 multiplies, result < 3q
+// 4q < 2^32, so the wrapped 32-bit differences below are exact, and the NTT keeps its
+// residues lazily in [0, 4q) between butterflies (Harvey; ntt.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -36,32 +37,34 @@ HD u32 shoup_mul(u32 a, u32 w, u32 wp, u32 q) {
 }
 HD u32 shoup_pre(u32 w, u32 q) { return (u32)(((u64)w << 32) / q); }
 
-// a * b mod q for a, b < q; mu = floor(2^62 / q) (fits 32 bits since q > 2^30)
+// a * b mod q for a, b < q; mu = floor(2^61 / q) (fits 32 bits since q > 2^29)
 HD u32 barrett_mul(u32 a, u32 b, u32 q, u32 mu) {
     u32 lo = a * b, hi = mulhi32(a, b);
-    u32 t = (hi << 2) | (lo >> 30);          // floor(a*b / 2^30) < 2^32
+    u32 t = (hi << 3) | (lo >> 29);          // floor(a*b / 2^29) < 2^31
     u32 qh = mulhi32(t, mu);                  // within 2 of floor(a*b/q)
     u32 r = lo - qh * q;                      // < 3q < 2^32
     r = csub(r, q);
     return csub(r, q);
 }
-HD u32 barrett_pre(u32 q) { return (u32)((1ull << 62) / q); }
+HD u32 barrett_pre(u32 q) { return (u32)((1ull << 61) / q); }
 
-// reduce a 64-bit accumulator (x < 2^62) with the Barrett constant
+// reduce a 64-bit accumulator (x < 2^61) with the Barrett constant
 HD u32 barrett_reduce64(u64 x, u32 q, u32 mu) {
     u32 lo = (u32)x, hi = (u32)(x >> 32);
-    u32 t = (hi << 2) | (lo >> 30);
+    u32 t = (hi << 3) | (lo >> 29);
     u32 qh = mulhi32(t, mu);
     u32 r = lo - qh * q;
     r = csub(r, q);
     return csub(r, q);
 }
 
-// fold a full 64-bit accumulator below 2^61 (x mod q unchanged); r32 = 2^32 mod q
+// fold a full 64-bit accumulator below 2^61 (x mod q unchanged); r32 = 2^32 mod q.
+// hi < 2^32 < 8q -> hi < 2q after two steps; 2q r32 + 2^32 < 1.6 * 2^60 + 2^32 for every
+// q in (2^29, 2^30) (r32 = 2^32 - 4q < 0.8 * 2^30 when q > 0.8 * 2^30, else r32 < q)
 HD u64 fold64(u64 x, u32 q, u32 r32) {
     u32 hi = (u32)(x >> 32);
-    hi = hi >= 2 * q ? hi - 2 * q : hi;  // hi < 2^32 < 4q
-    hi = csub(hi, q);
+    hi = hi >= 4 * q ? hi - 4 * q : hi;
+    hi = hi >= 2 * q ? hi - 2 * q : hi;
     return (u64)hi * r32 + (u32)x;
 }
 // any 64-bit x mod q
@@ -70,7 +73,7 @@ HD u32 reduce64(u64 x, u32 q, u32 mu, u32 r32) { return barrett_reduce64(fold64(
 // per-prime constant table kept in device memory
 struct PrimeConst {
     u32 q;       // modulus
-    u32 mu;      // floor(2^62 / q)
+    u32 mu;      // floor(2^61 / q)
     u32 ninv;    // N^{-1} mod q
     u32 ninv_p;  // Shoup companion
     u32 im;      // psi^{N/2}: the "imaginary unit" of Z_q (X^{N/2} at psi)

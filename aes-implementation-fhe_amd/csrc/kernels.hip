@@ -189,7 +189,7 @@ __device__ __forceinline__ void conv_body(const u32* __restrict__ x, u32* __rest
 #pragma unroll
     for (int i = 0; i < H; ++i) {
         y[i] = shoup_mul(y[i], s_src[i][2], s_src[i][3], s_src[i][0]);
-        f += ((u64)y[i] * s_src[i][1]) >> 30;
+        f += ((u64)y[i] * s_src[i][1]) >> 29;  // y_i / q_i in 32.32 fixed point (mu = 2^61 / q)
     }
     const u32 u = (u32)((f + (1ull << 31)) >> 32);
 #pragma unroll
@@ -276,7 +276,7 @@ __global__ void __launch_bounds__(kBlock) k_key_inner(u32* acc, const u32* ext, 
     const PrimeConst P = pc[map.prime(x)];
     const int krow = x < nl ? x : nks + (x - nl);
     const int own = x < nl ? x / alpha : -1;
-    // 64-bit multiply-adds (operands < q < 2^32/3: eight products fit), folded every 8 digits;
+    // 64-bit multiply-adds (operands < q < 2^30: eight products fit beside a folded sum), folded every 8 digits;
     // the key residues are loaded once for every batched ciphertext
     u64 s0[NBM][4] = {}, s1[NBM][4] = {};
     for (int j = 0; j < nd; ++j) {
@@ -854,7 +854,7 @@ __device__ __forceinline__ void lin_mac_body(const LinMacArgs& m, int nl, int ne
             const u32 pv = m.pt[g][j][at];
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
-                acc0[b][g] += (u64)av[b] * pv;  // q < 2^32 / 3: 8 products fit beside a folded accumulator
+                acc0[b][g] += (u64)av[b] * pv;  // q < 2^30: 8 products fit beside a folded accumulator
                 ap0[b][g] += (u64)u0[b] * pv;
                 ap1[b][g] += (u64)u1[b] * pv;
             }

@@ -70,8 +70,8 @@ std::string HostParams::build(int logn_, int L1_, int n_double, int dnum_, uint6
     fresh = L1;
     mod.assign(n_tot(), 0);
 
-    const uint64_t kMax = 1431655765ull;  // floor(2^32 / 3): keeps 3q < 2^32
-    const uint64_t kMin = 1ull << 30;     // q > 2^30: Barrett mu fits 32 bits
+    const uint64_t kMax = 1ull << 30;     // q < 2^30: 4q < 2^32 (lazy NTT butterflies in [0, 4q))
+    const uint64_t kMin = 1ull << 29;     // q > 2^29: Barrett mu = 2^61 / q fits 32 bits
     const uint64_t two_n = 2ull << logn;
     std::set<u32> taken;
 
@@ -106,7 +106,7 @@ std::string HostParams::build(int logn_, int L1_, int n_double, int dnum_, uint6
         return best;
     };
 
-    const double kT = 1342177280.0;  // 1.25 * 2^30
+    const double kT = 966367641.6;  // 0.9 * 2^30: the scale target, inside the prime range
     delta.assign(L + 1, 0.0);
     // single-prime region: delta_L1 = T; limb nl(l)-1 = l+1 is the prime closest to delta_l^2 / T
     delta[L1] = kT;

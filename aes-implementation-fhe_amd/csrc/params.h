@@ -2,7 +2,7 @@
 //
 // Limb layout: Q limbs 0..n_q-1 = [2 base][rescaling primes][1 encryption prime], then the
 // n_p special (key-switching) primes.  Levels 0..L1 drop one prime per rescale (scale
-// delta ~ 1.25 * 2^30); levels L1+1..L drop two primes per rescale (scale ~ 2^60.6, the
+// delta ~ 0.9 * 2^30); levels L1+1..L drop two primes per rescale (scale ~ 2^59.7, the
 // bootstrapping region).  A ciphertext at level l lives on Q limbs
 // 0..nl(l)-1; level -1 (one limb, q0) exists only inside bootstrapping.
 #pragma once

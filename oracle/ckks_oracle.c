@@ -131,9 +131,9 @@ void *orc_create(int logn, int L, int dnum, u64 seed) {
     u32 *used = (u32 *)calloc(tot, sizeof(u32));
     int nused = 0;
     u64 twon = 2ull << logn;
-    /* every prime lies in (2^30, floor(2^32/3)) so that 3q < 2^32.
+    /* every prime lies in (2^29, 2^30) so that 4q < 2^32.
      * Largest such NTT-friendly primes: base(2), special(alpha), encryption(1). */
-    const u64 PMAX = 1431655765ull, PMIN = 1ull << 30;
+    const u64 PMAX = 1ull << 30, PMIN = 1ull << 29;
     u64 cand = (PMAX - 1) / twon * twon + 1;
     int want = 2 + o->n_p + 1, got = 0;
     u32 big[64];
@@ -142,9 +142,9 @@ void *orc_create(int logn, int L, int dnum, u64 seed) {
     for (int k = 0; k < o->n_p; k++) o->mod[o->n_q + k] = big[2 + k];
     o->mod[o->n_q - 1] = big[2 + o->n_p];
     for (int i = 0; i < want; i++) used[nused++] = big[i];
-    /* rescaling chain: level l drops limb l+1; delta_L = 1.25 * 2^30 and each
-     * chain prime is the unused one closest to delta_l^2 / (1.25 * 2^30) */
-    const double TARGET = 1342177280.0;
+    /* rescaling chain: level l drops limb l+1; delta_L = 0.9 * 2^30 and each
+     * chain prime is the unused one closest to delta_l^2 / (0.9 * 2^30) */
+    const double TARGET = 966367641.6;
     o->delta = (double *)calloc(L + 1, sizeof(double));
     o->delta[L] = TARGET;
     for (int l = L; l >= 1; l--) {
@@ -474,14 +474,14 @@ void orc_rescale(void *h, int level, int npoly, const u32 *in, u32 *out) {
 /* ------------------------------------------------------------------ */
 /* centred fast base conversion                       */
 /* y_i in [0, q_i): u = round(sum_i y_i / q_i) from a 32-bit fixed-point */
-/* estimate, mu_i = floor(2^62 / q_i); sum_i y_i qhat_i - u Q is the   */
+/* estimate, mu_i = floor(2^61 / q_i); sum_i y_i qhat_i - u Q is the   */
 /* centred representative of the digit (up to rare boundary ties).     */
 /* ------------------------------------------------------------------ */
 static u32 overflow_count(const u32 *y, size_t stride, int h, const u32 *primes) {
     u64 f = 0;
     for (int i = 0; i < h; i++) {
-        u64 mu = (1ull << 62) / primes[i];
-        f += ((u64)y[(size_t)i * stride] * mu) >> 30;
+        u64 mu = (1ull << 61) / primes[i];
+        f += ((u64)y[(size_t)i * stride] * mu) >> 29;
     }
     return (u32)((f + (1ull << 31)) >> 32);
 }

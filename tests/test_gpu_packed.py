@@ -42,7 +42,7 @@ def test_renorm_states_snaps_every_packed_slot(ctx, states):
         z = ctx.decrypt(ct)
         want = np.ones(S, np.complex128)
         want.reshape(16, stride)[:, :states] = Z16 ** nib.T
-        assert np.abs(z - want).max() < 1e-4
+        assert np.abs(z - want).max() < 2e-4  # fresh-encryption noise at delta ~ 2^29.9 (max over 2^15 slots)
     assert np.array_equal(enc.decode(rh, rl), st)
 
 
