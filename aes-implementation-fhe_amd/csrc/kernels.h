@@ -12,7 +12,7 @@
 // (every input word read once, every output word written once).
 enum KernelId {
     KID_NTT_COLS_FWD, KID_NTT_ROWS_FWD, KID_NTT_ROWS_INV, KID_NTT_COLS_INV, KID_BASE_CONVERT, KID_KEY_INNER,
-    KID_MODDOWN, KID_TENSOR, KID_RESCALE, KID_AUTOMORPH, KID_ELEMENTWISE, KID_SAMPLE, KID_N
+    KID_MODDOWN, KID_TENSOR, KID_RESCALE, KID_AUTOMORPH, KID_ELEMENTWISE, KID_SAMPLE, KID_LIN_MAC, KID_N
 };
 struct KernelProfiler {
     unsigned mask = 0;  // bit k enables event timing of KernelId k

@@ -795,7 +795,11 @@ __global__ void k_mac(u32* out, MacTerms m, size_t xs, size_t os, LimbMap map, c
 // see launch_lin_mac (kernels.h); grid (N / 256, ne rows, nb batched ciphertexts).  The
 // diagonals are read once per residue and applied to every batched ciphertext (member loop
 // inside the thread); kLinG x 3 accumulators per member.
-template <int NB>
+// ND > 0: the digit count is a compile-time constant, so the digit loop of a baby step's key
+// inner product unrolls and its 2 * ND key loads and NB * ND ext gathers are all in flight
+// together (the loop with a run-time bound waited for each digit's loads in turn: the
+// kernel was load-latency-bound at ~1.3 TB/s); ND = 0 keeps the run-time loop (nd > 8)
+template <int NB, int ND>
 __device__ __forceinline__ void lin_mac_body(const LinMacArgs& m, int nl, int ne, const PrimeConst& P, int t, size_t k, int logn) {
     const bool qrow = t < nl;
     const size_t at = ((size_t)t << logn) + k;
@@ -830,7 +834,9 @@ __device__ __forceinline__ void lin_mac_body(const LinMacArgs& m, int nl, int ne
             const int krow = qrow ? t : m.nks + (t - nl);
             const int own = qrow ? t / m.alpha : -1;
             u64 s0[NB] = {}, s1[NB] = {};
-            for (int dj = 0; dj < m.nd; ++dj) {
+            const int nd = ND > 0 ? ND : m.nd;
+#pragma unroll
+            for (int dj = 0; dj < nd; ++dj) {
                 if (dj && (dj & 7) == 0) {
 #pragma unroll
                     for (int b = 0; b < NB; ++b) s0[b] = fold64(s0[b], P.q, P.r32), s1[b] = fold64(s1[b], P.q, P.r32);
@@ -889,12 +895,23 @@ __device__ __forceinline__ void lin_mac_body(const LinMacArgs& m, int nl, int ne
         }
     }
 }
-template <int NB>
+template <int NB, int ND>
 __global__ void __launch_bounds__(kBlock) k_lin_mac(LinMacArgs m, int nl, int ne, LimbMap map, const PrimeConst* pc, int logn) {
     const int t = blockIdx.y;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const PrimeConst P = pc[map.prime(t)];
-    lin_mac_body<NB>(m, nl, ne, P, t, k, logn);
+    lin_mac_body<NB, ND>(m, nl, ne, P, t, k, logn);
+}
+template <int NB>
+void launch_lin_mac_nb(hipStream_t st, const DevTables& T, const LinMacArgs& m, int nl, int ne, LimbMap map, double bytes) {
+    const dim3 g = ew_grid(T.logn, ne), b(kBlock);
+    switch (m.nd) {  // the digit counts of the bootstrap plans (dnum <= 8); others take the run-time loop
+#define LIN_MAC_ND(D) \
+    case D: prof_launch(KID_LIN_MAC, bytes, k_lin_mac<NB, D>, g, b, 0, st, m, nl, ne, map, T.pc, T.logn); break;
+        LIN_MAC_ND(1) LIN_MAC_ND(2) LIN_MAC_ND(3) LIN_MAC_ND(4) LIN_MAC_ND(5) LIN_MAC_ND(6) LIN_MAC_ND(7) LIN_MAC_ND(8)
+#undef LIN_MAC_ND
+        default: prof_launch(KID_LIN_MAC, bytes, k_lin_mac<NB, 0>, g, b, 0, st, m, nl, ne, map, T.pc, T.logn);
+    }
 }
 }  // namespace
 
@@ -919,9 +936,9 @@ void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int
     }
     const double bytes = words((m.nb * (reads - shared + writes) + shared) * (1u << T.logn));
     if (m.nb == 1)
-        prof_launch(KID_ELEMENTWISE, bytes, k_lin_mac<1>, ew_grid(T.logn, ne), dim3(kBlock), 0, st, m, nl, ne, map, T.pc, T.logn);
+        launch_lin_mac_nb<1>(st, T, m, nl, ne, map, bytes);
     else if (m.nb == 2)
-        prof_launch(KID_ELEMENTWISE, bytes, k_lin_mac<2>, ew_grid(T.logn, ne), dim3(kBlock), 0, st, m, nl, ne, map, T.pc, T.logn);
+        launch_lin_mac_nb<2>(st, T, m, nl, ne, map, bytes);
     else
         throw std::runtime_error("launch_lin_mac: 1 or 2 batched ciphertexts");
 }

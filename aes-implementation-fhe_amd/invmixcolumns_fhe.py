@@ -86,13 +86,20 @@ class InvMixColumnsFHE:
         log("mul13", e13)
         log("mul9", e9)
         fl = self._xor_level
-        # (e14 ^ e11) ^ (e13 ^ e9): the reference's chain regrouped (see MixColFinal), the two
-        # inner XOR pairs on the two branch streams
-        x1, x2 = pair(self.ctx, lambda: self._renorm_pair(*self._xor_pair(e14, e11, fl), level=NEED_XOR),
-                      lambda: self._renorm_pair(*self._xor_pair(e13, e9, fl), level=NEED_XOR))
-        log("acc1", x1)
-        log("acc23", x2)
-        out = self._renorm_pair(*self._xor_pair(x1, x2, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
+        last = NEED_BOOTSTRAP if do_final_bootstrap else None
+        if debug is not None:
+            # the reference's chain ((e14 ^ e11) ^ e13) ^ e9 and its debug keys (REF :123-134)
+            a1 = self._xor_pair(e14, e11, fl)
+            log("acc1", a1)
+            a2 = self._xor_pair(self._renorm_pair(*a1, level=NEED_XOR), e13, fl)
+            log("acc2", a2)
+            out = self._renorm_pair(*self._xor_pair(self._renorm_pair(*a2, level=NEED_XOR), e9, fl), level=last)
+        else:
+            # (e14 ^ e11) ^ (e13 ^ e9): the chain regrouped (see MixColFinal), the two inner XOR
+            # pairs on the two branch streams
+            x1, x2 = pair(self.ctx, lambda: self._renorm_pair(*self._xor_pair(e14, e11, fl), level=NEED_XOR),
+                          lambda: self._renorm_pair(*self._xor_pair(e13, e9, fl), level=NEED_XOR))
+            out = self._renorm_pair(*self._xor_pair(x1, x2, fl), level=last)
         if do_final_bootstrap:
             out = bootstrap2(self.ctx, out[0], out[1])
         log("out", out)

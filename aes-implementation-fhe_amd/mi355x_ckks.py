@@ -49,11 +49,12 @@ EXPORTED = [
 SECURITY_LOG_PQ_128 = {13: 218, 14: 438, 15: 881, 16: 1772, 17: 3544}
 
 KERNEL_IDS = ["ntt_cols_fwd", "ntt_rows_fwd", "ntt_rows_inv", "ntt_cols_inv", "base_convert", "key_inner",
-              "moddown", "tensor", "rescale", "automorph", "elementwise", "sample"]
+              "moddown", "tensor", "rescale", "automorph", "elementwise", "sample", "lin_mac"]
 # the __global__ symbol behind each kernel id (for matching rocprofv3 summaries)
 KERNEL_SYMBOLS = {"ntt_cols_fwd": "k_ntt_cols_fwd", "ntt_rows_fwd": "k_ntt_rows_fwd", "ntt_rows_inv": "k_ntt_rows_inv",
                   "ntt_cols_inv": "k_ntt_cols_inv", "base_convert": "k_base_convert", "key_inner": "k_key_inner",
-                  "moddown": "k_moddown_finish", "tensor": "k_tensor", "automorph": "k_automorph"}
+                  "moddown": "k_moddown_finish", "tensor": "k_tensor", "automorph": "k_automorph",
+                  "lin_mac": "k_lin_mac"}
 
 COUNTER_NAMES = ["mul", "relin", "rot", "conj", "ptmul", "scalar", "rescale", "ntt_rows", "keyswitch",
                  "encrypt", "decrypt", "bootstrap", "add", "lut"]

@@ -184,15 +184,22 @@ class MixColFinal:
                         lambda: self.gf_mult_3(*rot[1], out_level=fl + LUT2_DEPTH))
         log("two", two)
         log("thr", thr)
-        # out = (2x ^ 3r1) ^ (r2 ^ r3): the reference's chain ((2x ^ 3r1) ^ r2) ^ r3 regrouped
-        # (XOR is associative, every XOR pair still renormalised, the same three XOR pairs and
-        # renorms), so the first two XOR pairs are independent and run on the two branch streams
-        x1, x2 = pair(self.ctx, lambda: self._renorm_pair(*self._xor_pair(two, thr, fl), level=NEED_XOR),
-                      lambda: self._renorm_pair(*self._xor_pair(rot[2], rot[3], fl), level=NEED_XOR))
-        log("acc1", x1)
-        log("acc23", x2)
-        # the output is bootstrapped next (from level 0) or returned at the fresh level
-        acc = self._renorm_pair(*self._xor_pair(x1, x2, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
+        last = NEED_BOOTSTRAP if do_final_bootstrap else None  # bootstrapped next (from level 0), else fresh
+        if isinstance(debug, dict):
+            # the reference's chain ((2x ^ 3r1) ^ r2) ^ r3 and its debug keys (REF :127-163): acc1 and
+            # acc2 before their renorm, acc3 after it
+            a1 = self._xor_pair(two, thr, fl)
+            log("acc1", a1)
+            a2 = self._xor_pair(self._renorm_pair(*a1, level=NEED_XOR), rot[2], fl)
+            log("acc2", a2)
+            acc = self._renorm_pair(*self._xor_pair(self._renorm_pair(*a2, level=NEED_XOR), rot[3], fl), level=last)
+        else:
+            # out = (2x ^ 3r1) ^ (r2 ^ r3): the chain regrouped (XOR is associative, every XOR pair
+            # still renormalised, the same three XOR pairs and renorms), so the first two XOR pairs
+            # are independent and run on the two branch streams
+            x1, x2 = pair(self.ctx, lambda: self._renorm_pair(*self._xor_pair(two, thr, fl), level=NEED_XOR),
+                          lambda: self._renorm_pair(*self._xor_pair(rot[2], rot[3], fl), level=NEED_XOR))
+            acc = self._renorm_pair(*self._xor_pair(x1, x2, fl), level=last)
         log("acc3", acc)
         out_hi, out_lo = acc
         if do_final_bootstrap:

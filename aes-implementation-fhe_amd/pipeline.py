@@ -126,12 +126,28 @@ class AESPipeline:
         return self.invmix(ct_hi, ct_lo)
 
     # ---------------------------------------------------------------- encrypt
-    def encrypt_round(self, ct, key_pair):
-        """One middle round r = 1..9: SB, renorm, SR, MC, ARK, renorm (REF :142-151)."""
-        ct = self._sub_renorm(ct, level=NEED_SR_MIX)
+    def encrypt_round(self, ct, key_pair, debug=None, r: int = 0):
+        """One middle round r = 1..9: SB, renorm, SR, MC, ARK, renorm (REF :142-151).  With a
+        debug dict every step is logged under enc.r{r}.<step> (the names of the reference's
+        one-round debug block, REF :154-171)."""
+        if debug is None:
+            ct = self._sub_renorm(ct, level=NEED_SR_MIX)
+            ct = self.shift_rows(*ct)
+            ct = self.mix_columns(*ct)
+            return self._ark_renorm(ct, key_pair, level=NEED_SUBBYTES)
+        ct = self.sub.apply(*ct, out_level=self._floor())
+        self._log_pair(debug, f"enc.r{r}.sub", *ct)
+        ct = self._renorm_pair(*ct, level=NEED_SR_MIX)
+        self._log_pair(debug, f"enc.r{r}.sub.renorm", *ct)
         ct = self.shift_rows(*ct)
+        self._log_pair(debug, f"enc.r{r}.sr", *ct)
         ct = self.mix_columns(*ct)
-        return self._ark_renorm(ct, key_pair, level=NEED_SUBBYTES)
+        self._log_pair(debug, f"enc.r{r}.mc", *ct)
+        ct = self.ark(*ct, *key_pair, out_level=self._floor())
+        self._log_pair(debug, f"enc.r{r}.ark", *ct)
+        ct = self._renorm_pair(*ct, level=NEED_SUBBYTES)
+        self._log_pair(debug, f"enc.r{r}.ark.renorm", *ct)
+        return ct
 
     def encrypt(self, state: np.ndarray, round_keys: List[np.ndarray], debug: Dict[str, Any] | None = None):
         if debug is not None:
@@ -144,7 +160,7 @@ class AESPipeline:
         ct = self._renorm_pair(*ct, level=NEED_SUBBYTES)
         self._log_pair(debug, "enc.r0.renorm", *ct)
         for r in range(1, 10):
-            ct = self.encrypt_round(ct, rk[r])
+            ct = self.encrypt_round(ct, rk[r], debug, r)
         ct = self.sub.apply(*ct, out_level=self._floor())
         self._log_pair(debug, "enc.final.sub", *ct)
         ct = self._renorm_pair(*ct, level=NEED_SR_ARK)

@@ -70,6 +70,10 @@ def parse():
     ap.add_argument("--batch-steps", type=int, default=1)
     ap.add_argument("--no-batch-roundtrip", dest="batch_roundtrip", action="store_false",
                     help="skip the decrypt leg of the batch (BASELINE config 5)")
+    ap.add_argument("--whole-stats", default=None,
+                    help="with AESFHE_PROFILE_FROM_START=<ids>: keep the engine's per-kernel accounting from the first "
+                         "launch on (no reset, every launch) and write it to this JSON file -- the algorithmic bytes of "
+                         "exactly the launches a whole-process rocprofv3 --pmc pass counts")
     ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r1_pmc_traffic.json"), help="per-launch HBM bytes from a rocprofv3 PMC pass")
     return ap.parse_args()
 
@@ -143,29 +147,27 @@ def max_over_ranks(dist, x: float) -> float:
 
 
 def cpu_baseline(coeffs) -> dict:
-    """Oracle CPU CKKS engine (oracle/ckks_cpu.py), same parameters, timed on one XOR4 LUT
-    (half of an AddRoundKey) and scaled to a round by key-switch count."""
-    from oracle.ckks_cpu import OracleContext
-    from state_encoder import StateEncoder
-    from xor4_lut import XOR4LUT
-    ctx = OracleContext(log_n=16, max_level=17, seed=7)
-    enc = StateEncoder(ctx)
-    xor4 = XOR4LUT(ctx, coeffs["xor4"])
-    rng = np.random.default_rng(0)
-    a = enc.encode(rng.integers(0, 256, 16).astype(np.uint8))
-    b = enc.encode(rng.integers(0, 256, 16).astype(np.uint8))
-    xor4.apply(a[0], b[0])  # warm: relin + conjugation keys
-    t0 = time.perf_counter()
-    xor4.apply(a[0], b[0])
-    dt = time.perf_counter() - t0
-    # SURVEY.md §8(a): one encrypt round = 1,034 relin + 302 conj + 12 rot key switches;
-    # one XOR4 = 78 relin + 14 conj (bootstraps not included in the extrapolation)
-    round_s = dt * (1034 + 302 + 12) / (78 + 14)
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    return {"value": 1.0 / round_s, "unit": "rounds/s", "cores": threads, "kind": "port",
-            "sample": f"one XOR4 LUT (78 relin + 14 conj key switches) on the C oracle at N=2^16, L=17: "
-                      f"{dt:.2f} s; scaled x{(1034 + 302 + 12) / (78 + 14):.2f} to one encrypt round "
-                      f"(key-switch count, bootstraps excluded)"}
+    """The C oracle CPU CKKS engine (oracle/ckks_cpu.py, OpenMP over OMP_NUM_THREADS host
+    threads), measured on a bounded sample (tools/cpu_round.py): BASELINE config 1 in full
+    (AddRoundKey at N = 2^15) and the SubBytes + renorm step of a middle C2 round at N = 2^16.
+    The round rate divides the SubBytes time by that step's share of a whole middle round,
+    measured in full on the same host by `tools/cpu_round.py --full` (profiles/r2_cpu_round.json:
+    98 s per round on 16 threads, bootstraps excluded -- the oracle does not bootstrap)."""
+    sys.path.insert(0, str(ROOT / "tools"))
+    import cpu_round
+    c1 = cpu_round.c1(coeffs)
+    c2 = cpu_round.c2_round(coeffs, full=False)
+    full = json.loads((ROOT / "profiles" / "r2_cpu_round.json").read_text())
+    share = full["c2"]["steps_s"]["subbytes+renorm"] / full["c2"]["round_s"]
+    sb_s = c2["steps_s"]["subbytes+renorm"]
+    round_s = sb_s / share
+    return {"value": 1.0 / round_s, "unit": "rounds/s", "cores": cpu_round.threads(), "kind": "port",
+            "sample": f"C oracle on the host: config 1 (AddRoundKey, N=2^15) in full {c1['ark_s']:.2f} s (exact: {c1['exact']}); "
+                      f"SubBytes+renorm of C2 round 1 at N=2^16 {sb_s:.2f} s (exact: {c2['exact']}), divided by its measured "
+                      f"share {share:.3f} of a full middle round (profiles/r2_cpu_round.json, {full['c2']['round_s']:.1f} s on "
+                      f"{full['threads']} threads); bootstraps excluded (the oracle does not bootstrap)",
+            "c1_ark_s": c1["ark_s"], "c2_subbytes_renorm_s": sb_s, "c2_round_s_estimate": round_s,
+            "c2_round_s_measured_full": full["c2"]["round_s"]}
 
 
 class _NoFinalBootstrap:
@@ -336,8 +338,13 @@ def main():
         pipe.encrypt(states[i], rks)
     E.sync()
     kernels = list(__import__("mi355x_ckks").KERNEL_IDS) if args.profile_all else [args.kernel, args.kernel2]
-    E.profile(kernels, every=1 if args.profile_all else args.profile_every)
-    E.kernel_stats(reset=True)
+    whole = args.whole_stats and os.environ.get("AESFHE_PROFILE_FROM_START")
+    pre = {}
+    if whole:  # whole-process accounting: keep the from-start configuration, fold the pre-timed part in
+        pre = E.kernel_stats(reset=True)
+    else:
+        E.profile(kernels, every=1 if args.profile_all else args.profile_every)
+        E.kernel_stats(reset=True)
     E.reset_counters()
 
     outs = []
@@ -353,6 +360,9 @@ def main():
     work = E.kernel_work()
     stats = E.kernel_stats(reset=True)
     counters = E.counters()
+    if whole:
+        tot = {k: {f: pre.get(k, {}).get(f, 0) + v.get(f, 0) for f in ("launches", "ms", "bytes")} for k, v in stats.items()}
+        Path(args.whole_stats).write_text(json.dumps(tot, indent=1))
     E.profile(())
     batch = run_batch(ctx, coeffs, rks, args, rank, world, dist) if args.batch_states > 0 else None
 
