@@ -168,10 +168,16 @@ class MixColFinal:
         return pair(self.ctx, lambda: self._xor_ct(a[0], b[0], out_level), lambda: self._xor_ct(a[1], b[1], out_level))
 
     def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
-        log = (lambda k, v: debug.__setitem__(k, v)) if isinstance(debug, dict) else (lambda k, v: None)
         steps = [-4 * k * self.stride for k in (1, 2, 3)]  # _col_shift_rowmajor(ct, k), hoisted
         rh, rl = pair(self.ctx, lambda: rot_many(self.ctx, ct_hi, steps), lambda: rot_many(self.ctx, ct_lo, steps))
         rot = {k: (rh[k - 1], rl[k - 1]) for k in (1, 2, 3)}
+        return self.mix_rotated((ct_hi, ct_lo), rot, do_final_bootstrap, debug)
+
+    def mix_rotated(self, x, rot, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
+        """GF2(x) ^ GF3(r1) ^ r2 ^ r3 from the state pair x and its column shifts rot[k] = r_k
+        (the rest of __call__; shiftrows_mixcolumns.py supplies ShiftRows-permuted shifts)"""
+        log = (lambda k, v: debug.__setitem__(k, v)) if isinstance(debug, dict) else (lambda k, v: None)
+        ct_hi, ct_lo = x
         for k in (1, 2, 3):
             log(f"rotc{k}", rot[k])
         log("in", (ct_hi, ct_lo))

@@ -9,6 +9,14 @@ never applies InvMixColumns, so it cannot invert encrypt.  ``decrypt`` here inse
 after AddRoundKey as the reference README prescribes (REF/README.md:87-94);
 ``with_inv_mix_columns=False`` reproduces the shipped order.
 
+``fuse_sub_ark=True`` evaluates SubBytes ⊕ AddRoundKey as one fused LUT per nibble
+(sub_bytes_ark.py, SURVEY.md §8(f)4, REF/README.md:133-135): the last encrypt round and every
+decrypt round, across the (Inv)ShiftRows between them via permuted round keys; one XOR4 pair
+and one renorm fewer per fused step, the same bytes.
+
+``fuse_sr_mc=True`` merges ShiftRows into MixColumns' rotations (shiftrows_mixcolumns.py, the
+GHS12 refinement of REF/README.md:137-138): three hoisted rotations per nibble instead of six.
+
 ``states`` = B > 1 runs B independent AES states per ciphertext pair in the slot-packed
 layout (state_encoder.py): ``encrypt`` / ``decrypt`` take and return
 (B, 16) arrays through the same step sequence, and a (16,) round key is shared by all B
@@ -26,15 +34,20 @@ from inv_shiftrows import InvShiftRows
 from mixcol_final import MixColFinal
 from shift_rows import ShiftRows
 from state_encoder import StateEncoder
+from shift_rows import shift_rows_bytes
+from shiftrows_mixcolumns import ShiftRowsMixColumnsFusedEnc
+from sub_bytes_ark import SubBytesARK
 from sub_bytes_lut import SubBytesLUT
-from utils import NEED_GF, NEED_ISR_ISB, NEED_SR_ARK, NEED_SR_MIX, NEED_SUBBYTES, NEED_XOR, RENORM_FLOOR
+from utils import (NEED_GF, NEED_ISR_ISB, NEED_SR_ARK, NEED_SR_MIX, NEED_SUB_ARK_SR, NEED_SUBBYTES, NEED_XOR,
+                   RENORM_FLOOR)
 from xor4_lut import XOR4LUT
 
 
 class AESPipeline:
     def __init__(self, ctx, coeffs: Dict[str, Any], *, mixcolumns: MixColFinal | None = None,
                  inv_mixcolumns: InvMixColumnsFHE | None = None, use_hard_renorm_between_steps: bool = False,
-                 with_inv_mix_columns: bool = True, states: int = 1):
+                 with_inv_mix_columns: bool = True, states: int = 1, fuse_sub_ark: bool = False,
+                 fuse_sr_mc: bool = False):
         self.ctx = ctx
         self.states = states
         self.encoder = StateEncoder(ctx, states)
@@ -56,6 +69,17 @@ class AESPipeline:
         self.with_inv_mix_columns = with_inv_mix_columns
         self._rk_cache: List[Tuple[Any, Any]] | None = None
         self._rk_tag = b""
+        self.fuse_sub_ark = fuse_sub_ark
+        if fuse_sub_ark:
+            self.sbark = SubBytesARK(self.sub, coeffs["xor4"])
+            self.isbark = SubBytesARK(self.isub, coeffs["xor4"]) if self.isub is not None else None
+        self.srmc = None
+        if fuse_sr_mc:
+            if not hasattr(self.mix, "mix_rotated"):
+                raise TypeError("fuse_sr_mc needs a MixColFinal (mix_rotated) as mixcolumns")
+            self.srmc = ShiftRowsMixColumnsFusedEnc(ctx, self.mix, states)
+        self._fk_cache: Dict[Tuple[int, int], Tuple[Any, Any]] = {}
+        self._fk_tag = b""
 
     # ---------------------------------------------------------------- utils
     def _renorm_pair(self, hi, lo, level=None):
@@ -89,6 +113,16 @@ class AESPipeline:
             self._rk_cache = [self._encode_key(np.asarray(k, dtype=np.uint8)) for k in round_keys]
             self._rk_tag = tag
         return self._rk_cache
+
+    def _fused_key(self, round_keys, r: int, direction: int):
+        """round key r permuted by ShiftRows (direction -1) / InvShiftRows (+1), encrypted once:
+        the key of a SubBytes-AddRoundKey fusion across a ShiftRows (sub_bytes_ark.py)"""
+        tag = b"".join(np.ascontiguousarray(k, dtype=np.uint8).tobytes() for k in round_keys)
+        if tag != self._fk_tag:
+            self._fk_cache, self._fk_tag = {}, tag
+        if (r, direction) not in self._fk_cache:
+            self._fk_cache[(r, direction)] = self._encode_key(shift_rows_bytes(np.asarray(round_keys[r], np.uint8), direction))
+        return self._fk_cache[(r, direction)]
 
     def _log_pair(self, dbg, tag: str, ct_hi, ct_lo, **meta) -> None:
         if dbg is None:
@@ -126,26 +160,30 @@ class AESPipeline:
         return self.invmix(ct_hi, ct_lo)
 
     # ---------------------------------------------------------------- encrypt
-    def encrypt_round(self, ct, key_pair, debug=None, r: int = 0):
+    def encrypt_round(self, ct, key_pair, debug=None, r: int = 0, next_level: int = NEED_SUBBYTES):
         """One middle round r = 1..9: SB, renorm, SR, MC, ARK, renorm (REF :142-151).  With a
         debug dict every step is logged under enc.r{r}.<step> (the names of the reference's
         one-round debug block, REF :154-171)."""
         if debug is None:
             ct = self._sub_renorm(ct, level=NEED_SR_MIX)
-            ct = self.shift_rows(*ct)
-            ct = self.mix_columns(*ct)
-            return self._ark_renorm(ct, key_pair, level=NEED_SUBBYTES)
+            ct = self.srmc(*ct) if self.srmc is not None else self.mix_columns(*self.shift_rows(*ct))
+            return self._ark_renorm(ct, key_pair, level=next_level)
         ct = self.sub.apply(*ct, out_level=self._floor())
         self._log_pair(debug, f"enc.r{r}.sub", *ct)
         ct = self._renorm_pair(*ct, level=NEED_SR_MIX)
         self._log_pair(debug, f"enc.r{r}.sub.renorm", *ct)
-        ct = self.shift_rows(*ct)
-        self._log_pair(debug, f"enc.r{r}.sr", *ct)
-        ct = self.mix_columns(*ct)
+        if self.srmc is not None:  # ShiftRows and MixColumns merged (shiftrows_mixcolumns.py)
+            inner = {}
+            ct = self.srmc(*ct, debug=inner)
+            self._log_pair(debug, f"enc.r{r}.sr", *inner["sr"])
+        else:
+            ct = self.shift_rows(*ct)
+            self._log_pair(debug, f"enc.r{r}.sr", *ct)
+            ct = self.mix_columns(*ct)
         self._log_pair(debug, f"enc.r{r}.mc", *ct)
         ct = self.ark(*ct, *key_pair, out_level=self._floor())
         self._log_pair(debug, f"enc.r{r}.ark", *ct)
-        ct = self._renorm_pair(*ct, level=NEED_SUBBYTES)
+        ct = self._renorm_pair(*ct, level=next_level)
         self._log_pair(debug, f"enc.r{r}.ark.renorm", *ct)
         return ct
 
@@ -160,7 +198,17 @@ class AESPipeline:
         ct = self._renorm_pair(*ct, level=NEED_SUBBYTES)
         self._log_pair(debug, "enc.r0.renorm", *ct)
         for r in range(1, 10):
-            ct = self.encrypt_round(ct, rk[r], debug, r)
+            nxt = NEED_SUB_ARK_SR if (self.fuse_sub_ark and r == 9) else NEED_SUBBYTES
+            ct = self.encrypt_round(ct, rk[r], debug, r, next_level=nxt)
+        if self.fuse_sub_ark:
+            # SR(SB(x)) ^ k10 = SR(SB(x) ^ InvShiftRows(k10)): one fused LUT, then ShiftRows
+            ct = self.sbark(*ct, *self._fused_key(round_keys, 10, +1))
+            self._log_pair(debug, "enc.final.sub_ark", *ct)
+            ct = self.shift_rows(*ct)
+            self._log_pair(debug, "enc.final.ark10", *ct)
+            ct = self._renorm_pair(*ct)
+            self._log_pair(debug, "enc.output", *ct)
+            return ct
         ct = self.sub.apply(*ct, out_level=self._floor())
         self._log_pair(debug, "enc.final.sub", *ct)
         ct = self._renorm_pair(*ct, level=NEED_SR_ARK)
@@ -181,9 +229,23 @@ class AESPipeline:
         self._log_pair(debug, "dec.input", ct_hi, ct_lo)
         ct = self.ark(ct_hi, ct_lo, *rk[10], out_level=self._floor())
         self._log_pair(debug, "dec.init.ark10", *ct)
-        ct = self._renorm_pair(*ct, level=NEED_ISR_ISB)
+        fuse = self.fuse_sub_ark
+        if fuse and self.isub is None:
+            raise KeyError("inv_sub_hi")
+        ct = self._renorm_pair(*ct, level=NEED_SUB_ARK_SR if fuse else NEED_ISR_ISB)
         self._log_pair(debug, "dec.init.ark10.renorm", *ct)
         for r in range(9, 0, -1):
+            if fuse:
+                # ISB(ISR(x)) ^ k_r = ISR(ISB(x) ^ ShiftRows(k_r)): one fused LUT, then InvShiftRows
+                ct = self.isbark(*ct, *self._fused_key(round_keys, r, -1))
+                self._log_pair(debug, f"dec.r{r}.isb_ark", *ct)
+                ct = self.inv_shift_rows(*ct)
+                ct = self._renorm_pair(*ct, level=NEED_GF if self.with_inv_mix_columns else NEED_SUB_ARK_SR)
+                self._log_pair(debug, f"dec.r{r}.ark", *ct)
+                if self.with_inv_mix_columns:
+                    ct = self._renorm_pair(*self.inv_mix_columns(*ct), level=NEED_SUB_ARK_SR)
+                    self._log_pair(debug, f"dec.r{r}.imc", *ct)
+                continue
             ct = self.inv_shift_rows(*ct)
             self._log_pair(debug, f"dec.r{r}.isr", *ct)
             ct = self._sub_renorm(ct, inverse=True, level=NEED_XOR)
@@ -194,6 +256,14 @@ class AESPipeline:
                 # InvSubBytes' LUT needs a clean input, as SubBytes gets one after ARK in encrypt
                 ct = self._renorm_pair(*self.inv_mix_columns(*ct), level=NEED_ISR_ISB)
                 self._log_pair(debug, f"dec.r{r}.imc", *ct)
+        if fuse:
+            ct = self.isbark(*ct, *self._fused_key(round_keys, 0, -1))
+            self._log_pair(debug, "dec.final.isb_ark", *ct)
+            ct = self.inv_shift_rows(*ct)
+            self._log_pair(debug, "dec.final.ark0", *ct)
+            ct = self._renorm_pair(*ct)
+            self._log_pair(debug, "dec.output", *ct)
+            return ct
         ct = self.inv_shift_rows(*ct)
         self._log_pair(debug, "dec.final.isr", *ct)
         if self.isub is None:

@@ -12,6 +12,18 @@ import numpy as np
 from utils import pair
 
 
+def shift_rows_bytes(state: np.ndarray, direction: int = -1) -> np.ndarray:
+    """the byte permutation ShiftRows (direction -1) / InvShiftRows (+1) applies to a (16,) or
+    (B, 16) column-first state: row r (bytes r + 4c) rotated by direction * r columns; used
+    to permute plaintext round keys for the SubBytes-AddRoundKey fusion (sub_bytes_ark.py)"""
+    s = np.asarray(state, np.uint8)
+    M = s.reshape(*s.shape[:-1], 4, 4)  # [..., c, r]
+    out = np.empty_like(M)
+    for r in range(4):
+        out[..., :, r] = np.roll(M[..., :, r], direction * r, axis=-1)
+    return out.reshape(s.shape)
+
+
 def row_masks(ctx, sc: int, states: int = 1) -> List[Any]:
     stride = sc // 16
     masks = []

@@ -117,13 +117,37 @@ class SubBytesLUTFastCached:
             acc = term if acc is None else ctx.add(acc, term)
         return acc if acc is not None else ctx.multiply(like, 0.0)
 
-    def _apply_bsgs(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:
-        ctx = self.ctx
+    def _ensure_bsgs(self):
+        """the conjugate-split coefficient sets: lift, hi, lo (sub_bytes_ark adds its own)"""
         if not hasattr(self, "_bsgs"):
             lift = np.fft.ifft(np.exp(-2j * np.pi * np.arange(16) / 256))
             lp, lq = self._split(lift, 8)
             self._bsgs = dict(lift=(lp, lq), hi=self._split(self.hi, 128), lo=self._split(self.lo, 128))
-        lp, lq = self._bsgs["lift"]
+        return self._bsgs
+
+    def _apply_bsgs(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:
+        ctx = self.ctx
+        baby, g, ct_b = self._bsgs_bases(ct_hi, ct_lo)
+        batch = getattr(ctx, "multiply_many", None) is not None
+        if batch:
+            if can_fork(ctx):  # each output nibble batches its own products, on its own stream
+                shared = (*baby.values(), *g.values())
+                return pair(ctx, lambda: self._outputs_batched(baby, g, ct_b, ("hi",))[0],
+                            lambda: self._outputs_batched(baby, g, ct_b, ("lo",))[0], shared=shared)
+            return self._outputs_batched(baby, g, ct_b)
+
+        # 3) out = P(b) + conj(Q(b)) per output nibble
+        def lut(which):
+            P, Q = self._bsgs[which]
+            return ctx.add(self._poly_bsgs((which, "p"), P, baby, g, ct_b),
+                           ctx.conjugate(self._poly_bsgs((which, "q"), Q, baby, g, ct_b)))
+
+        return pair(ctx, lambda: lut("hi"), lambda: lut("lo"), shared=(*baby.values(), *g.values()))
+
+    def _bsgs_bases(self, ct_hi: Any, ct_lo: Any):
+        """steps 1-2 of the BSGS form: (baby steps b^1..b^15, giant steps G_1..G_8, b)"""
+        ctx = self.ctx
+        lp, lq = self._ensure_bsgs()["lift"]
         # 1) zeta16^l -> zeta256^l: L(y) = P(y) + conj(Q(y)) over y^1..y^8
         pos16 = ctx.make_power_basis(ct_lo, 8)
         y = {k: pos16[k - 1] for k in range(1, 9)}
@@ -142,20 +166,7 @@ class SubBytesLUTFastCached:
         else:
             for i, (u, v) in ((2, (1, 1)), (4, (2, 2)), (3, (1, 2)), (5, (1, 4)), (6, (2, 4)), (7, (3, 4)), (8, (4, 4))):
                 g[i] = ctx.multiply(g[u], g[v])  # depth: G_2 +1, G_3 / G_4 +2, G_5..G_8 +3 over b^16
-        if batch:
-            if can_fork(ctx):  # each output nibble batches its own products, on its own stream
-                shared = (*baby.values(), *g.values())
-                return pair(ctx, lambda: self._outputs_batched(baby, g, ct_b, ("hi",))[0],
-                            lambda: self._outputs_batched(baby, g, ct_b, ("lo",))[0], shared=shared)
-            return self._outputs_batched(baby, g, ct_b)
-
-        # 3) out = P(b) + conj(Q(b)) per output nibble
-        def lut(which):
-            P, Q = self._bsgs[which]
-            return ctx.add(self._poly_bsgs((which, "p"), P, baby, g, ct_b),
-                           ctx.conjugate(self._poly_bsgs((which, "q"), Q, baby, g, ct_b)))
-
-        return pair(ctx, lambda: lut("hi"), lambda: lut("lo"), shared=(*baby.values(), *g.values()))
+        return baby, g, ct_b
 
     def _outputs_batched(self, baby, g, ct_b, whiches=("hi", "lo")):
         """the output nibbles `whiches`: every chunk sum S_i (one fused kernel each), ALL their

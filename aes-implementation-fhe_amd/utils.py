@@ -38,6 +38,11 @@ NEED_SR_MIX = NEED_GF + SHIFTROWS_DEPTH              # ShiftRows -> MixColumns
 NEED_SR_ARK = NEED_XOR + SHIFTROWS_DEPTH             # ShiftRows -> AddRoundKey (last round)
 NEED_ISR_ISB = NEED_SUBBYTES + SHIFTROWS_DEPTH       # InvShiftRows -> InvSubBytes
 NEED_BOOTSTRAP = 0                                   # bootstrapping starts from level 0
+# SubBytes-AddRoundKey fusion (sub_bytes_ark.py): SubBytes + the key product and its
+# coefficient, then the (Inv)ShiftRows it is fused across, down to level 1 (the renorm reads
+# any level; the fused step has no room for the usual floor below the fresh level 17)
+SUB_ARK_DEPTH = SUBBYTES_DEPTH + 2
+NEED_SUB_ARK_SR = 1 + SHIFTROWS_DEPTH + SUB_ARK_DEPTH
 
 
 def drop_to(ctx, ct, level):
