@@ -120,7 +120,8 @@ std::vector<cplx> apply_group_plain(const LinGroup& g, const std::vector<cplx>& 
     return out;
 }
 
-BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts_scale, double stc_scale, int K, int r, int deg) {
+BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts_scale, double stc_scale, int K, int r, int deg,
+                        double stc_boost) {
     BootPlan P;
     P.logn = logn;
     P.M = 1 << (logn - 1);
@@ -141,10 +142,17 @@ BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts
         D[0] = std::vector<cplx>(M, 1.0);
         for (int s : sg[gi]) D = compose(stage(logn, s, false), D, M);
         // the gain goes into the FIRST group: the signal is smallest right after EvalMod,
-        // where SlotToCoeff crosses into the single-prime (2^30-scale) region
+        // where SlotToCoeff crosses into the single-prime (2^30-scale) region.  stc_boost
+        // also lifts the intermediate groups' signal (undone by the LAST group): the
+        // butterfly stages grow the signal ~sqrt(2) each, so without it the first groups'
+        // outputs sit far below 1 at a 2^30 scale and their rescale noise (absolute, 2^-16)
+        // is amplified by every later group -- the bootstrap's noise floor
         if (gi == 0)
             for (auto& kv : D)
-                for (auto& x : kv.second) x *= stc_scale;
+                for (auto& x : kv.second) x *= stc_scale * (sg.size() > 1 ? stc_boost : 1.0);
+        if (gi + 1 == sg.size() && sg.size() > 1)
+            for (auto& kv : D)
+                for (auto& x : kv.second) x /= stc_boost;
         P.stc.push_back(layout(D, 1 << (sg[gi].front() - 1), M));
     }
     // CoeffToSlot: inverse stages logm..1 (output bit-reversed w)
@@ -183,7 +191,7 @@ BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts
 
 extern "C" int aesfhe_debug_bootplan(int logn, double* err) {
     const int n = 1 << logn, M = n / 2;
-    BootPlan P = make_boot_plan(logn, 3, 3, 1.0, 1.0, 12, 3, 27);
+    BootPlan P = make_boot_plan(logn, 3, 3, 1.0, 1.0, 12, 3, 27, 32.0);  // with the engine's SlotToCoeff boost
     Embedding emb(logn);
     std::mt19937_64 rng(1);
     std::normal_distribution<double> nd;

@@ -31,7 +31,10 @@ struct BootPlan {
 
 // cts_scale multiplies CoeffToSlot (folded into its first group), stc_scale multiplies
 // SlotToCoeff (folded into its first group)
-BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts_scale, double stc_scale, int K, int r, int deg);
+// stc_boost: intermediate SlotToCoeff groups carry the signal times stc_boost (first group
+// x stc_boost, last group / stc_boost; same transform)
+BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts_scale, double stc_scale, int K, int r, int deg,
+                        double stc_boost = 1.0);
 
 // reference evaluation of the planned transforms on plain vectors (self-check)
 std::vector<cplx> apply_group_plain(const LinGroup& g, const std::vector<cplx>& v);

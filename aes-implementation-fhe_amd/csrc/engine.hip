@@ -343,34 +343,37 @@ public:
         return g;
     }
     // The dense -> sparse key of the bootstrap (step 2) is an RLWE sample under
-    // the h = 32 sparse secret, so its modulus must stay small: it lives modulo q0 * P' only,
-    // P' = the first kD2sP special primes (~95 bits), not on all n_ks + n_p limbs (~1,700 bits,
-    // where a sparse secret is recoverable and with it the dense secret).  Layout [2][1 + kD2sP][N].
-    static constexpr int kD2sP = 2;
+    // the h = 32 sparse secret, so its modulus must stay small: it lives modulo
+    // Q0 * P' only -- Q0 = q0 q1, the two base limbs of level 0 the bootstrap starts from, P' =
+    // the first kD2sP special primes (~120 bits) -- not on all n_ks + n_p limbs (~1,700 bits,
+    // where a sparse secret is recoverable and with it the dense secret).
+    // Layout [2][kD2sQ + kD2sP][N].
+    static constexpr int kD2sP = 2, kD2sQ = 2;
     int d2s_np() const { return std::min(kD2sP, hp_.n_p); }
     size_t ksk_words(u64 g) const {
-        if (g == tag_d2s()) return (size_t)2 * (1 + d2s_np()) * hp_.n;
+        if (g == tag_d2s()) return (size_t)2 * (kD2sQ + d2s_np()) * hp_.n;
         return (size_t)hp_.dnum * 2 * (hp_.n_ks + hp_.n_p) * hp_.n;
     }
     double d2s_modulus_bits() const {
-        double b = std::log2((double)hp_.mod[0]);
+        double b = 0;
+        for (int t = 0; t < kD2sQ; ++t) b += std::log2((double)hp_.mod[t]);
         for (int k = 0; k < d2s_np(); ++k) b += std::log2((double)hp_.mod[hp_.p_off() + k]);
         return b;
     }
     const u32* ksk_d2s() {
         const u64 g = tag_d2s();
-        const int n = hp_.n, ne = 1 + d2s_np();
+        const int n = hp_.n, ne = kD2sQ + d2s_np();
         void* raw = nullptr;
         HIP_OK(hipMalloc(&raw, ksk_words(g) * sizeof(u32)));
         u32* b = (u32*)raw;
         u32* a = b + (size_t)ne * n;
-        const LimbMap em = extmap(1);  // row 0: q0, rows 1..: the first special primes
+        const LimbMap em = extmap(kD2sQ);  // rows 0, 1: q0, q1; then the first special primes
         u32* e = tmp(ne);
         launch_sample_uniform(S(), T_, a, ne, em, hp_.seed, stream_id(4, g, 0));
         launch_sample_small(S(), T_, e, ne, em, hp_.seed, stream_id(5, g, 0), 1);
         ntt(e, ne, ne, em);
-        // b = -a s_sp + e + (P' mod q0) s on the q0 row
-        launch_keygen_combine(S(), T_, b, a, sparse_secret(), e, d_s_, d_d2s_, ne, em, 0, 1);
+        // b = -a s_sp + e + (P' mod q_t) s on the q0, q1 rows
+        launch_keygen_combine(S(), T_, b, a, sparse_secret(), e, d_s_, d_d2s_ + d2s_off_.gad, ne, em, 0, kD2sQ);
         untmp(e, ne);
         ksk_[g] = b;
         HIP_OK(hipStreamSynchronize(S()));
@@ -793,7 +796,8 @@ public:
     // (data level t, owing p rescales), logical level t - p <= the input's.  Owed rescales
     // are applied first down to the target data level; the rest is one exact-scale step:
     // keep nl(t) + k limbs, multiply by c = round(S(t,p) q_{nl(t)} ... q_{nl(t)+k-1} / S(l,q))
-    // and divide the k limbs away, k the smallest count keeping c >= 2^24.  Always returns a
+    // and divide the k limbs away, k the smallest count keeping c >= 2^24 (2^51 on the
+    // double-prime levels).  Always returns a
     // new buffer.
     Ct convert(const Ct& c_in, int t, int p) {
         if (p < 0 || t > c_in.level || t - p > c_in.level - c_in.pend)
@@ -804,7 +808,13 @@ public:
         const int n = hp_.n, nb = hp_.nl(t), na = hp_.nl(c.level);
         int k = 0;
         double ratio = raw_scale(t, p) / raw_scale(c.level, c.pend);
-        while (ratio < 16777216.0 && nb + k < na) ratio *= (double)hp_.mod[nb + k], ++k;
+        // the constant's rounding is a relative scale error of up to 0.5 / c: 2^-25 is far below
+        // the noise at the single-prime scale (~2^30), but on the double-prime levels (scale
+        // ~2^60: CoeffToSlot, EvalMod) it would dominate -- EvalMod's T_k recurrences align
+        // operands across levels and its double angles amplify the error 4^r-fold -- so there c
+        // keeps ~51 bits (one more limb kept and divided away)
+        const double need = t > hp_.L1 ? 2251799813685248.0 : 16777216.0;  // 2^51 : 2^24
+        while (ratio < need && nb + k < na) ratio *= (double)hp_.mod[nb + k], ++k;
         if (!(ratio >= 0.999999 && ratio < 9.0e18)) throw std::runtime_error("level_down: scale ratio out of range");
         if (pm(c) == 3 && k > 0 && raw_scale(t, p) < 1.0e15) {  // see normalize()
             Ct r = relin_raw(c);
@@ -1270,53 +1280,55 @@ public:
     // bootstrapping step 2: the single-limb (q0) ciphertexts' d = c1 switched to the sparse
     // secret with ksk_d2s (modulus q0 * P', P' = d2s_np() special primes); (c0', c1') with
     // c0' = add0 + ...; nb members at d + m ms / add0 + m ms
+    // d: c1 of nb members (NTT form, the two base limbs q0, q1, member stride ms words);
+    // returns the key-switched (c0', c1') over (q0, q1) with add0 (c0) added to c0'
     Ct keyswitch_d2s(const u32* d, const u32* add0, int nb, size_t ms) {
-        const int n = hp_.n, np = d2s_np(), ne = 1 + np, npl = 2 * nb;
+        const int n = hp_.n, nq = kD2sQ, np = d2s_np(), ne = nq + np, npl = 2 * nb;
         if (npl > kMaxConvGroups || nb > kMaxKsBatch) throw std::runtime_error("keyswitch_d2s: batch too large");
-        const LimbMap em = extmap(1);
+        const LimbMap em = extmap(nq);
         const u32* key = ksk(tag_d2s());
-        // ModUp q0 -> P': the level-0 digit-0 table (h = 1; its [1][1 + n_p] rows start with P')
-        u32* coef = tmp(nb);
-        intt(coef, d, nb, RowMap{1, (int)(ms / n), 1, 0, 0}, single(0));
+        // ModUp Q0 -> P' (the own limbs q0, q1 are read from d by the key inner product)
+        u32* coef = tmp((size_t)nb * nq);
+        intt(coef, d, nb * nq, RowMap{nq, (int)(ms / n), nq, 0, 0}, qmap());
         u32* ext = tmp((size_t)nb * ne);
         ConvBatch up;
         up.n = nb;
         for (int m = 0; m < nb; ++m) {
-            up.h[m] = 1, up.d0[m] = 0, up.skip0[m] = 0;
-            up.src[m] = coef + (size_t)m * n;
+            up.h[m] = nq, up.d0[m] = 0, up.skip0[m] = 0;
+            up.src[m] = coef + (size_t)m * nq * n;
             up.dst[m] = ext + (size_t)m * ne * n;
-            up.tab[m] = d_modup_ + modup_off_[(size_t)1 * hp_.dnum];
-            up.qhinv[m] = up.tab[m] + (size_t)2 * (1 + hp_.n_p);
-            up.negq[m] = up.qhinv[m] + 2;
+            up.tab[m] = d_d2s_ + d2s_off_.up_tab;      // [nq][ne] pairs: (Q0 / q_i) mod target
+            up.qhinv[m] = d_d2s_ + d2s_off_.up_qhinv;  // [nq] pairs: (Q0 / q_i)^-1 mod q_i
+            up.negq[m] = d_d2s_ + d2s_off_.up_negq;    // [ne]: -Q0 mod target
         }
         launch_base_convert(S(), T_, up, ne, em);
-        untmp(coef, nb);
+        untmp(coef, (size_t)nb * nq);
         RowMap xr = rows_dense(ne);
-        xr.skip_alpha = hp_.alpha, xr.skip_nl = 1, xr.skip_groups = 1;
+        xr.skip_alpha = hp_.alpha, xr.skip_nl = nq, xr.skip_groups = 1;
         ntt(ext, ext, nb * ne, xr, em);
         u32* acc = tmp((size_t)npl * ne);
-        launch_key_inner(S(), T_, acc, ext, d, key, 1, ne, 1, hp_.alpha, ne, 1, em, 0, nb, (size_t)ne * n, ms, (size_t)2 * ne * n);
+        launch_key_inner(S(), T_, acc, ext, d, key, 1, ne, nq, hp_.alpha, ne, nq, em, 0, nb, (size_t)ne * n, ms, (size_t)2 * ne * n);
         untmp(ext, (size_t)nb * ne);
-        // ModDown by P' onto q0, + add0
+        // ModDown by P' onto (q0, q1), + add0
         u32* yp = tmp((size_t)npl * np);
-        intt(yp, acc, npl * np, RowMap{np, ne, np, 1, 0}, LimbMap{np, hp_.p_off(), 0});
-        u32* conv = tmp(npl);
+        intt(yp, acc, npl * np, RowMap{np, ne, np, nq, 0}, LimbMap{np, hp_.p_off(), 0});
+        u32* conv = tmp((size_t)npl * nq);
         ConvBatch dn;
         dn.n = npl;
         for (int p = 0; p < npl; ++p) {
             dn.h[p] = np, dn.d0[p] = hp_.p_off(), dn.skip0[p] = 1 << 30;
             dn.src[p] = yp + (size_t)p * np * n;
-            dn.dst[p] = conv + (size_t)p * n;
-            dn.tab[p] = d_d2s_ + 2;                     // [np][1] pairs: P'/p_k mod q0
-            dn.qhinv[p] = d_d2s_ + 2 + 2 * np;          // [np] pairs: (P'/p_k)^-1 mod p_k
-            dn.negq[p] = d_d2s_ + 2 + 4 * np;           // -P' mod q0
+            dn.dst[p] = conv + (size_t)p * nq * n;
+            dn.tab[p] = d_d2s_ + d2s_off_.dn_tab;      // [np][nq] pairs: (P' / p_k) mod q_t
+            dn.qhinv[p] = d_d2s_ + d2s_off_.dn_qhinv;  // [np] pairs: (P' / p_k)^-1 mod p_k
+            dn.negq[p] = d_d2s_ + d2s_off_.dn_negq;    // [nq]: -P' mod q_t
         }
-        launch_base_convert(S(), T_, dn, 1, qmap());
+        launch_base_convert(S(), T_, dn, nq, qmap());
         untmp(yp, (size_t)npl * np);
-        Ct o = alloc_ct(-1, npl, nb);
-        launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_d2s_ + 3 + 4 * np, add0, nullptr, npl, 1, ms);
-        cnt_[C_NTT_ROWS] += (size_t)npl;
-        untmp(conv, npl);
+        Ct o = alloc_ct(0, npl, nb);
+        launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_d2s_ + d2s_off_.pinv, add0, nullptr, npl, nq, ms);
+        cnt_[C_NTT_ROWS] += (size_t)npl * nq;
+        untmp(conv, (size_t)npl * nq);
         untmp(acc, (size_t)npl * ne);
         cnt_[C_KS] += nb;
         return o;
@@ -1783,7 +1795,9 @@ public:
     }
 
     // ------------------------------------------------------------------ bootstrapping
-    static constexpr int kBootCts = 3, kBootStc = 3, kBootK = 12, kBootR = 3, kBootDeg = 27, kBootMsgBits = 5, kSparseH = 32;
+    static constexpr int kBootCts = 3, kBootStc = 3, kBootK = 12, kBootR = 4, kBootDeg = 27, kSparseH = 32;
+    // message bits b: s_bt = Q0 / 2^b (AESFHE_BOOT_MSG_BITS overrides, for accuracy sweeps)
+    int boot_msg_bits_ = std::getenv("AESFHE_BOOT_MSG_BITS") ? std::atoi(std::getenv("AESFHE_BOOT_MSG_BITS")) : 9;
     // depth of cheb_eval for a degree-d series: baby T_k at ceil(log2 k), a leaf one more
     // (its scalar products), giant T_m at log2 m, p = q + T_m r at max(q, 1 + max(T_m, r))
     static int cheb_depth(int d) {
@@ -1836,8 +1850,8 @@ public:
         bool ready = false;
         BootPlan plan;
         int top = 0;
-        double s_bt = 0.0;  // scale of the single-limb (q0) ciphertext
-        i64 k1 = 0;         // integer factor taking delta_0 to s_bt before dropping q1
+        double s_bt = 0.0;  // message scale of the level-0 (mod Q0 = q0 q1) ciphertext
+        i64 k1 = 0;         // integer factor taking delta_0 to s_bt
         std::vector<BootGroupDev> cts, stc;
     } bs_;
 
@@ -1847,12 +1861,17 @@ public:
             throw std::runtime_error("bootstrap needs the bootstrappable parameter set (use_bootstrap=True): chain has " +
                                      std::to_string(hp_.L - hp_.fresh) + " spare levels, need " + std::to_string(boot_depth()));
         bs_.top = hp_.L;
-        const double q0 = hp_.mod[0], q1 = hp_.mod[1];
-        bs_.k1 = std::llround(q0 / std::ldexp(1.0, kBootMsgBits) * q1 / hp_.delta[0]);
-        bs_.s_bt = hp_.delta[0] * (double)bs_.k1 / q1;
-        const double cts_scale = hp_.delta[bs_.top] / (2.0 * q0 * kBootK);
-        const double stc_scale = q0 / (2.0 * M_PI * bs_.s_bt);
-        bs_.plan = make_boot_plan(hp_.logn, kBootCts, kBootStc, cts_scale, stc_scale, kBootK, kBootR, kBootDeg);
+        // the bootstrap starts modulo Q0 = q0 q1 (level 0) with the message at s_bt = Q0 / 2^b
+        const double Q0 = (double)hp_.mod[0] * (double)hp_.mod[1];
+        bs_.k1 = std::llround(Q0 / std::ldexp(1.0, boot_msg_bits_) / hp_.delta[0]);
+        bs_.s_bt = hp_.delta[0] * (double)bs_.k1;
+        const double cts_scale = hp_.delta[bs_.top] / (2.0 * Q0 * kBootK);
+        const double stc_scale = Q0 / (2.0 * M_PI * bs_.s_bt);
+        // intermediate SlotToCoeff signal lifted by the later groups' butterfly gain,
+        // 2^(stages after the first group / 2) (AESFHE_STC_BOOST overrides; 1 = off)
+        const int later = (hp_.logn - 1) - (hp_.logn - 1 + kBootStc - 1) / kBootStc;
+        const double boost = std::getenv("AESFHE_STC_BOOST") ? std::atof(std::getenv("AESFHE_STC_BOOST")) : std::ldexp(1.0, later / 2);
+        bs_.plan = make_boot_plan(hp_.logn, kBootCts, kBootStc, cts_scale, stc_scale, kBootK, kBootR, kBootDeg, boost);
         bs_.cts.assign(bs_.plan.cts.size(), {});
         bs_.stc.assign(bs_.plan.stc.size(), {});
         for (size_t i = 0; i < bs_.cts.size(); ++i) bs_.cts[i].g = &bs_.plan.cts[i];
@@ -1879,6 +1898,8 @@ public:
         out[6] = d2s_modulus_bits();
         out[7] = kSparseH;
         out[8] = d2s_np();
+        out[9] = kD2sQ;
+        out[10] = boot_msg_bits_;
     }
 
     // diagonals of one group encoded at `level` (scale ptscale_level) on the Q limbs AND the
@@ -2343,21 +2364,22 @@ public:
     // z: level-0 ciphertext(s), nb batched members, consumed here
     Ct bootstrap_l0(Ct z, int stop_after) {
         const int n = hp_.n, top = bs_.top, nb = z.nb;
-        // 1. scale delta_0 -> s_bt and drop q1: a single-limb ciphertext mod q0
-        std::vector<u32> r(2);
-        for (int t = 0; t < 2; ++t) r[t] = mod_i64(bs_.k1, hp_.mod[t]);
-        launch_mul_const_half(S(), T_, z.data, z.data, const_half(r, r), 2 * z.npoly, 2, qmap());
-        Ct b = rescale(z, true);
+        // 1. scale delta_0 -> s_bt = Q0 / 2^b (an exact integer product) on the two
+        // base limbs: the ciphertext stays modulo Q0 = q0 q1 (no rescale, no rounding noise)
+        const int nq = kD2sQ;
+        if (hp_.nl(0) != nq) throw std::runtime_error("bootstrap: level 0 must hold the two base limbs");
+        std::vector<u32> r(nq);
+        for (int t = 0; t < nq; ++t) r[t] = mod_i64(bs_.k1, hp_.mod[t]);
+        launch_mul_const_half(S(), T_, z.data, z.data, const_half(r, r), z.npoly * nq, nq, qmap());
+        if (stop_after == 1) return z;
+        // 2. sparse-secret encapsulation: dense s -> sparse s_sp at modulus Q0
+        Ct sp = keyswitch_d2s(z.data + (size_t)nq * n, z.data, nb, (size_t)2 * nq * n);
         release(z);
-        if (stop_after == 1) return b;
-        // 2. sparse-secret encapsulation: dense s -> sparse s_sp at modulus q0
-        Ct sp = keyswitch_d2s(b.data + n, b.data, nb, 2 * (size_t)n);
-        release(b);
         if (stop_after == 2) return sp;
-        // 3. ModRaise: centred lift of both polynomials to every limb of the top level
-        intt(sp.data, 2 * nb, 1, single(0));
+        // 3. ModRaise: centred CRT lift of both polynomials to every limb of the top level
+        intt(sp.data, 2 * nb * nq, nq, qmap());
         Ct raised = alloc_ct(top, 2 * nb, nb);
-        launch_rescale_spread(S(), T_, raised.data, sp.data, 2 * nb, hp_.nl(top), hp_.mod[0]);
+        launch_crt2_spread(S(), T_, raised.data, sp.data, 2 * nb, hp_.nl(top), hp_.mod[0], hp_.mod[1]);
         release(sp);
         const int nlt = hp_.nl(top);
         ntt(raised.data, 2 * nb * nlt, nlt, qmap());
@@ -2727,29 +2749,66 @@ private:
 
         // dense -> sparse key switch over q0 * P' (ksk_d2s): [P' mod q0 pair][np pairs P'/p_k mod q0]
         // [np pairs (P'/p_k)^-1 mod p_k][-P' mod q0][P'^-1 mod q0 pair]
-        {
-            const int npd = d2s_np();
+        {  // dense -> sparse key switch over Q0 * P' (keyswitch_d2s): offsets in d2s_off_
+            const int nq = kD2sQ, npd = d2s_np(), ne = nq + npd;
+            auto tq = [&](int x) { return x < nq ? q[x] : q[hp_.p_off() + x - nq]; };
             std::vector<u32> t;
-            u32 pq = 1;
-            for (int k = 0; k < npd; ++k) pq = mulm(pq, q[hp_.p_off() + k], q[0]);
-            t.push_back(pq), t.push_back(shoup_pre(pq, q[0]));
-            for (int k = 0; k < npd; ++k) {
+            auto pair_ = [&](u32 v, u32 m) { t.push_back(v), t.push_back(shoup_pre(v, m)); };
+            d2s_off_.gad = t.size();  // [nq] pairs: P' mod q_t (the key's gadget)
+            for (int x = 0; x < nq; ++x) {
                 u32 v = 1;
-                for (int m2 = 0; m2 < npd; ++m2)
-                    if (m2 != k) v = mulm(v, q[hp_.p_off() + m2], q[0]);
-                t.push_back(v), t.push_back(shoup_pre(v, q[0]));
+                for (int k = 0; k < npd; ++k) v = mulm(v, q[hp_.p_off() + k], q[x]);
+                pair_(v, q[x]);
             }
+            d2s_off_.up_tab = t.size();  // [nq][ne] pairs: (Q0 / q_i) mod target x
+            for (int i = 0; i < nq; ++i)
+                for (int x = 0; x < ne; ++x) {
+                    u32 v = 1;
+                    for (int k = 0; k < nq; ++k)
+                        if (k != i) v = mulm(v, q[k], tq(x));
+                    pair_(v, tq(x));
+                }
+            d2s_off_.up_qhinv = t.size();  // [nq] pairs: (Q0 / q_i)^-1 mod q_i
+            for (int i = 0; i < nq; ++i) {
+                u32 v = 1;
+                for (int k = 0; k < nq; ++k)
+                    if (k != i) v = mulm(v, q[k], q[i]);
+                pair_(hinvm(v, q[i]), q[i]);
+            }
+            d2s_off_.up_negq = t.size();  // [ne]: -Q0 mod target x
+            for (int x = 0; x < ne; ++x) {
+                u32 v = 1;
+                for (int k = 0; k < nq; ++k) v = mulm(v, q[k], tq(x));
+                t.push_back(v ? tq(x) - v : 0);
+            }
+            d2s_off_.dn_tab = t.size();  // [np][nq] pairs: (P' / p_k) mod q_t
+            for (int k = 0; k < npd; ++k)
+                for (int x = 0; x < nq; ++x) {
+                    u32 v = 1;
+                    for (int m2 = 0; m2 < npd; ++m2)
+                        if (m2 != k) v = mulm(v, q[hp_.p_off() + m2], q[x]);
+                    pair_(v, q[x]);
+                }
+            d2s_off_.dn_qhinv = t.size();  // [np] pairs: (P' / p_k)^-1 mod p_k
             for (int k = 0; k < npd; ++k) {
                 const u32 pk = q[hp_.p_off() + k];
                 u32 v = 1;
                 for (int m2 = 0; m2 < npd; ++m2)
                     if (m2 != k) v = mulm(v, q[hp_.p_off() + m2], pk);
-                const u32 inv = hinvm(v, pk);
-                t.push_back(inv), t.push_back(shoup_pre(inv, pk));
+                pair_(hinvm(v, pk), pk);
             }
-            t.push_back(pq ? q[0] - pq : 0);
-            const u32 inv = hinvm(pq, q[0]);
-            t.push_back(inv), t.push_back(shoup_pre(inv, q[0]));
+            d2s_off_.dn_negq = t.size();  // [nq]: -P' mod q_t
+            for (int x = 0; x < nq; ++x) {
+                u32 v = 1;
+                for (int k = 0; k < npd; ++k) v = mulm(v, q[hp_.p_off() + k], q[x]);
+                t.push_back(v ? q[x] - v : 0);
+            }
+            d2s_off_.pinv = t.size();  // [nq] pairs: P'^-1 mod q_t
+            for (int x = 0; x < nq; ++x) {
+                u32 v = 1;
+                for (int k = 0; k < npd; ++k) v = mulm(v, q[hp_.p_off() + k], q[x]);
+                pair_(hinvm(v, q[x]), q[x]);
+            }
             d_d2s_ = dev_upload(t);
         }
 
@@ -2787,7 +2846,8 @@ private:
     u32* d_moddown_phinv_ = nullptr;
     std::vector<size_t> moddown_off_;
     u32* d_mdr_ = nullptr;       // ModDown fused with the rescale, per level (see build_tables)
-    u32* d_d2s_ = nullptr;       // dense -> sparse key switch constants over q0 * P' (see build_tables)
+    u32* d_d2s_ = nullptr;       // dense -> sparse key switch constants over Q0 * P' (see build_tables)
+    struct { size_t gad, up_tab, up_qhinv, up_negq, dn_tab, dn_qhinv, dn_negq, pinv; } d2s_off_{};
     std::vector<size_t> mdr_off_;
     bool batch_ops_ = std::getenv("AESFHE_BATCH_OPS") == nullptr || std::getenv("AESFHE_BATCH_OPS")[0] != '0';
     bool stack_evalmod_ = std::getenv("AESFHE_STACK_EVALMOD") == nullptr || std::getenv("AESFHE_STACK_EVALMOD")[0] != '0';

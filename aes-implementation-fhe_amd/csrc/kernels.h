@@ -153,6 +153,9 @@ void launch_automorph(hipStream_t st, const DevTables& T, u32* out, const u32* i
 // --- rescale -------------------------------------------------------------------------
 // last: npoly rows (coefficient form, prime q_last); writes v[p][t] = centred(last) mod q_t
 void launch_rescale_spread(hipStream_t st, const DevTables& T, u32* v, const u32* last, int npoly, int nt, u32 q_last);
+// ModRaise of coefficient-form polynomials over the two base limbs (q0, q1): src [npoly][2][N]
+// -> v [npoly][nt][N], the centred CRT value mod primes 0 .. nt - 1
+void launch_crt2_spread(hipStream_t st, const DevTables& T, u32* v, const u32* src, int npoly, int nt, u32 q0, u32 q1);
 
 // --- key switching -----------------------------------------------------------------
 // fast base conversion of several groups in one launch (ModUp: one group per digit,

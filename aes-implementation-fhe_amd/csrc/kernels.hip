@@ -164,6 +164,26 @@ __global__ void k_rescale_spread(u32* v, const u32* last, int nt, u32 q_last, co
     }
     v[(((size_t)p * nt + t) << logn) + k] = r;
 }
+// ModRaise from the two base limbs (q0, q1): x = x0 + q0 ((x1 - x0) q0^{-1} mod q1) in
+// [0, q0 q1), centred (x - q0 q1 when x > q0 q1 / 2), reduced mod every target prime
+__global__ void k_crt2_spread(u32* v, const u32* src, int nt, u32 q0, u32 q1, u32 q0inv, u32 q0inv_p, const PrimeConst* pc,
+                              int logn) {
+    const int p = blockIdx.z, t = blockIdx.y;
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const u32 x0 = src[((size_t)(2 * p) << logn) + k], x1 = src[((size_t)(2 * p + 1) << logn) + k];
+    const u32 d = x1 >= x0 % q1 ? x1 - x0 % q1 : x1 + q1 - x0 % q1;
+    const u32 y = shoup_mul(d, q0inv, q0inv_p, q1);
+    const u64 Q = (u64)q0 * q1, x = (u64)x0 + (u64)q0 * y;
+    const PrimeConst P = pc[t];
+    u32 r;
+    if (x > (Q >> 1)) {  // negative representative x - Q
+        const u32 m = reduce64(Q - x, P.q, P.mu, P.r32);
+        r = m ? P.q - m : 0;
+    } else {
+        r = reduce64(x, P.q, P.mu, P.r32);
+    }
+    v[(((size_t)p * nt + t) << logn) + k] = r;
+}
 // ------------------------------------------------------------------------------------
 // key switching
 // ------------------------------------------------------------------------------------
@@ -765,6 +785,17 @@ void launch_automorph(hipStream_t st, const DevTables& T, u32* out, const u32* i
 void launch_rescale_spread(hipStream_t st, const DevTables& T, u32* v, const u32* last, int npoly, int nt, u32 q_last) {
     prof_launch(KID_RESCALE, words((double)npoly * (1 + nt) * (1u << T.logn)), k_rescale_spread, dim3((1u << T.logn) / kBlock, nt, npoly), dim3(kBlock), 0, st, v, last, nt, q_last, T.pc,
                        T.logn);
+}
+void launch_crt2_spread(hipStream_t st, const DevTables& T, u32* v, const u32* src, int npoly, int nt, u32 q0, u32 q1) {
+    if (q0 >= q1 && q0 % q1 == 0) throw std::runtime_error("launch_crt2_spread: bad primes");
+    u64 inv = 1, b = q0 % q1, e = q1 - 2;  // q0^{-1} mod q1 (Fermat)
+    while (e) {
+        if (e & 1) inv = inv * b % q1;
+        b = b * b % q1;
+        e >>= 1;
+    }
+    prof_launch(KID_RESCALE, words((double)npoly * (2 + nt) * (1u << T.logn)), k_crt2_spread, dim3((1u << T.logn) / kBlock, nt, npoly),
+                dim3(kBlock), 0, st, v, src, nt, q0, q1, (u32)inv, shoup_pre((u32)inv, q1), T.pc, T.logn);
 }
 void launch_base_convert(hipStream_t st, const DevTables& T, const ConvBatch& cb, int nt, LimbMap map) {
     double w = 0;

@@ -516,10 +516,10 @@ class Engine:
 
     def boot_info(self) -> dict:
         self._ensure_keys()
-        out = np.zeros(9)
+        out = np.zeros(11)
         self._ctx.check(self._lib.aesfhe_boot_info(self._ctx.ptr, out))
-        return dict(zip(["s_bt", "k1", "top", "K", "r", "deg", "d2s_log_modulus", "sparse_h", "d2s_special_primes"],
-                        out.tolist()))
+        return dict(zip(["s_bt", "k1", "top", "K", "r", "deg", "d2s_log_modulus", "sparse_h", "d2s_special_primes",
+                         "d2s_base_limbs", "msg_bits"], out.tolist()))
 
     def ntt(self, ct):
         return self._new(self._lib.aesfhe_to_ntt, ct.handle)
@@ -612,9 +612,9 @@ class Engine:
 
     def export_ksk(self, galois: int) -> np.ndarray:
         self._ensure_keys()
-        if galois == 2 * self.n + 1:  # dense -> sparse bootstrapping key: [2][q0 + P' limbs][N]
-            np_d2s = int(self.boot_info()["d2s_special_primes"])
-            out = np.zeros((1, 2, 1 + np_d2s, self.n), np.uint32)
+        if galois == 2 * self.n + 1:  # dense -> sparse bootstrapping key: [2][q0, q1 + P' limbs][N]
+            info = self.boot_info()
+            out = np.zeros((1, 2, int(info["d2s_base_limbs"]) + int(info["d2s_special_primes"]), self.n), np.uint32)
         else:
             out = np.zeros((self.dnum, 2, self.n_ks + self.n_p, self.n), np.uint32)
         self._ctx.check(self._lib.aesfhe_export_ksk(self._ctx.ptr, int(galois), out))

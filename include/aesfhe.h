@@ -162,9 +162,10 @@ int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle ct, int stage, aesfhe
 /* ephemeral sparse secret (NTT form, all limbs) */
 int aesfhe_export_sparse(aesfhe_ctx* ctx, uint32_t* out);
 int aesfhe_debug_lin_group(aesfhe_ctx* ctx, aesfhe_handle ct, int which, aesfhe_handle* out);
-/* [s_bt, k1, top, K, r, deg, log2 modulus of the dense->sparse key (q0 P'), sparse
- * secret weight h, special primes in P'] */
-int aesfhe_boot_info(aesfhe_ctx* ctx, double* out9);
+/* [s_bt, k1, top, K, r, deg, log2 modulus of the dense->sparse key (Q0 P', Q0 = q0 q1), sparse
+ * secret weight h, special primes in P', base limbs in Q0, message bits b (s_bt = Q0 / 2^b)]
+ *  */
+int aesfhe_boot_info(aesfhe_ctx* ctx, double* out11);
 /* Zeta16 secret-key renorm of a (hi, lo) state pair (REF/pipeline.py:65-69): decrypt,
  * snap the 16 strided slots to the nearest codeword, refill others with 1, re-encrypt */
 int aesfhe_renorm_pair(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle* out_hi, aesfhe_handle* out_lo);

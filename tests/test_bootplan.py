@@ -16,4 +16,4 @@ def test_bootstrap_plan_factorisation(log_n):
 
 def test_bootstrap_depth():
     import mi355x_ckks
-    assert mi355x_ckks.bootstrap_depth() == 14  # CtS 3 + EvalMod (Chebyshev PS 5 + 3 double angles) + StC 3
+    assert mi355x_ckks.bootstrap_depth() == 15  # CtS 3 + EvalMod (Chebyshev PS 5 + 4 double angles) + StC 3

@@ -7,7 +7,9 @@ from conftest import gpu_context
 
 pytestmark = pytest.mark.gpu
 
-BOOT_TOL = 0.02  # max |slot error| for |z| <= 1 inputs at N = 2^16 (decode margin pi/16 = 0.196)
+# max |slot error| for |z| <= 1 inputs at N = 2^16: ~2x the measured 2.4e-4 (profiles/r2_boot_error.json;
+# DESIGN.md §4).  The decode margin of a Zeta16 slot is pi/16 = 0.196.
+BOOT_TOL = 5e-4
 
 
 @pytest.fixture(scope="module")
@@ -30,7 +32,8 @@ def test_bootstrap_accuracy_and_level(ctx):
         low = ctx.multiply(low, 1.0 + 0j) if False else E.multiply(low, 0.999)
     assert low.level == 0
     out = ctx.bootstrap(ctx.to_intt(low))
-    assert np.abs(ctx.decrypt(out) - z * 0.999 ** E.fresh_level).max() < BOOT_TOL
+    # 17 rescales of input noise ride along (the bootstrap is linear in its input's error)
+    assert np.abs(ctx.decrypt(out) - z * 0.999 ** E.fresh_level).max() < 2 * BOOT_TOL
     assert ctx.bootstrap_stats()["count"] >= 2
 
 
@@ -44,7 +47,7 @@ def test_bootstrap_zeta16_state(ctx):
     assert np.array_equal(enc.decode(bh, bl), state)
     sc = E_slots = ctx.engine.slot_count
     z = ctx.decrypt(bh)[:: sc // 16][:16]
-    assert np.abs(np.angle(z / np.exp(-2j * np.pi * (state >> 4) / 16))).max() < np.pi / 64
+    assert np.abs(np.angle(z / np.exp(-2j * np.pi * (state >> 4) / 16))).max() < 2 * BOOT_TOL
 
 
 def test_mixcolumns_with_final_bootstrap(ctx, coeff_dir):
@@ -101,30 +104,32 @@ def test_bootstrap_pair_bit_exact(ctx):
 
 def test_dense_to_sparse_key_modulus(ctx):
     """The dense -> sparse bootstrapping key is an RLWE sample under the h = 32 sparse
-    secret, so it lives modulo q0 * P' only (~95 bits), never on the full
-    Q * P chain.  Checks the width and the key equation b + a s_sp = e + (P' mod q0) s on
-    q0 and e on the P' limbs, with e a centred binomial (|e| <= 21)."""
+    secret, so it lives modulo Q0 * P' only (Q0 = q0 q1, the level-0 limbs the bootstrap
+    starts from; ~120 bits), never on the full Q * P chain.  Checks the width
+    and the key equation b + a s_sp = e + (P' mod q_t) s on q0, q1 and e on the P' limbs, with e
+    a centred binomial (|e| <= 21)."""
     E = ctx.engine
     info = E.boot_info()
     assert info["sparse_h"] == 32
-    assert info["d2s_log_modulus"] < 100.0
-    npd = int(info["d2s_special_primes"])
+    assert info["d2s_log_modulus"] < 125.0
+    nq, npd = int(info["d2s_base_limbs"]), int(info["d2s_special_primes"])
+    assert nq == 2
     key = E.export_ksk(2 * E.n + 1).astype(np.uint64)
-    assert key.shape == (1, 2, 1 + npd, E.n)
+    assert key.shape == (1, 2, nq + npd, E.n)
     q = E.moduli().astype(np.uint64)
-    primes = [0] + [E.n_q + k for k in range(npd)]
+    primes = list(range(nq)) + [E.n_q + k for k in range(npd)]
     assert abs(sum(np.log2(float(q[p])) for p in primes) - info["d2s_log_modulus"]) < 1e-9
     s_sp = E.export_sparse().astype(np.uint64)
     s = E.export_secret().astype(np.uint64)
     b, a = key[0, 0], key[0, 1]
-    pq = 1
-    for k in range(npd):
-        pq = pq * int(q[E.n_q + k]) % int(q[0])
     for row, p in enumerate(primes):
         qt = q[p]
         r = (b[row] + a[row] * s_sp[p] % qt) % qt
-        if row == 0:
-            r = (r + qt - np.uint64(pq) * s[0] % qt) % qt
+        if row < nq:
+            pq = 1
+            for k in range(npd):
+                pq = pq * int(q[E.n_q + k]) % int(qt)
+            r = (r + qt - np.uint64(pq) * s[p] % qt) % qt
         e = E.debug_ntt(r.astype(np.uint32)[None], p, inverse=True)[0].astype(np.int64)
         e = np.where(e > int(qt) // 2, e - int(qt), e)
         assert np.abs(e).max() <= 21, (row, np.abs(e).max())
