@@ -2325,18 +2325,20 @@ public:
 
     // stop_after (debug): 1 q0-only, 2 after SSE, 3 ModRaise, 4 back to dense, 5 CoeffToSlot,
     // 6 real part, 7 imaginary part, 8 EvalMod(real), 9 EvalMod(imag), 10 recombined, 11 output
-    Ct bootstrap(const Ct& in, int stop_after = 99) {
+    // gain: the output carries gain * message (folded into the level-0 scaling integer k1,
+    // relative precision 2^-k1bits; the true-FHE snap's kappa, zeta16_noise_reducer.py)
+    Ct bootstrap(const Ct& in, int stop_after = 99, double gain = 1.0) {
         boot_setup();
         if (vis_npoly(in) != 2 || in.nb != 1) throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
         Ct c = normalize(in);
         Ct z = level_down(c, 0);
         if (c.data != in.data) release(c);
-        return bootstrap_l0(z, stop_after);
+        return bootstrap_l0(z, stop_after, gain);
     }
     // the hi / lo bootstraps of an AES step (MixColumns' final bootstrap) as ONE batched
     // bootstrap of two stacked ciphertexts: every key switch reads its key, and every linear
     // transform its diagonals, once for both; half the launches
-    void bootstrap_pair(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob) {
+    void bootstrap_pair(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob, double gain = 1.0) {
         boot_setup();
         if (vis_npoly(a_in) != 2 || vis_npoly(b_in) != 2 || a_in.nb != 1 || b_in.nb != 1)
             throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
@@ -2350,7 +2352,7 @@ public:
             launch_copy_rows(S(), T_, z.data + (size_t)m * 2 * nl0 * n, zm.data, 2 * nl0);
             release(zm);
         }
-        Ct out = bootstrap_l0(z, 99);
+        Ct out = bootstrap_l0(z, 99, gain);
         const int nlo = hp_.nl(out.level);
         aesfhe_handle* dst[2] = {oa, ob};
         for (int m = 0; m < 2; ++m) {
@@ -2362,14 +2364,16 @@ public:
         release(out);
     }
     // z: level-0 ciphertext(s), nb batched members, consumed here
-    Ct bootstrap_l0(Ct z, int stop_after) {
+    Ct bootstrap_l0(Ct z, int stop_after, double gain = 1.0) {
         const int n = hp_.n, top = bs_.top, nb = z.nb;
         // 1. scale delta_0 -> s_bt = Q0 / 2^b (an exact integer product) on the two
         // base limbs: the ciphertext stays modulo Q0 = q0 q1 (no rescale, no rounding noise)
         const int nq = kD2sQ;
         if (hp_.nl(0) != nq) throw std::runtime_error("bootstrap: level 0 must hold the two base limbs");
         std::vector<u32> r(nq);
-        for (int t = 0; t < nq; ++t) r[t] = mod_i64(bs_.k1, hp_.mod[t]);
+        if (!(gain > 0.0 && gain <= 1.0)) throw std::runtime_error("bootstrap: gain must lie in (0, 1]");
+        const i64 k1 = gain == 1.0 ? bs_.k1 : std::llround(gain * (double)bs_.k1);
+        for (int t = 0; t < nq; ++t) r[t] = mod_i64(k1, hp_.mod[t]);
         launch_mul_const_half(S(), T_, z.data, z.data, const_half(r, r), z.npoly * nq, nq, qmap());
         if (stop_after == 1) return z;
         // 2. sparse-secret encapsulation: dense s -> sparse s_sp at modulus Q0
@@ -3098,6 +3102,17 @@ int aesfhe_bootstrap_pair(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, aes
     const Ct& ca = e.canon(a);
     const Ct& cb = e.canon(b);
     e.bootstrap_pair(ca, cb, out_a, out_b);
+    API_END
+}
+int aesfhe_bootstrap_scaled(aesfhe_ctx* ctx, aesfhe_handle c, double gain, aesfhe_handle* out) {
+    CT_OP(e.bootstrap(e.canon(c), 99, gain))
+}
+int aesfhe_bootstrap_pair_scaled(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, double gain, aesfhe_handle* out_a,
+                                 aesfhe_handle* out_b) {
+    API_BEGIN Engine& e = *ctx->eng;
+    const Ct& ca = e.canon(a);
+    const Ct& cb = e.canon(b);
+    e.bootstrap_pair(ca, cb, out_a, out_b, gain);
     API_END
 }
 int aesfhe_bootstrap_depth(void) { return Engine::boot_depth(); }

@@ -150,6 +150,15 @@ class EngineContext:
         self._bs_total_s += time.perf_counter() - t0
         return out
 
+    def bootstrap_pair_scaled(self, a, b, gain: float):
+        """(gain * bootstrap(a), gain * bootstrap(b)), gain in (0, 1] at no extra level (the
+        true-FHE renorm, zeta16_noise_reducer.BootstrapSnap)"""
+        t0 = time.perf_counter()
+        out = self.engine.bootstrap_pair_scaled(a, b, gain)
+        self._bs_count += 2
+        self._bs_total_s += time.perf_counter() - t0
+        return out
+
     def bootstrap_stats(self):
         n = self._bs_count
         return {"count": n, "total_s": self._bs_total_s, "avg_s": self._bs_total_s / n if n else 0.0}

@@ -71,7 +71,10 @@ class InvMixColumnsFHE:
     def _col_shift_rowmajor(self, ct, k_up: int):
         return self.ctx.rotate(ct, -4 * k_up * self.stride)
 
-    def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
+    def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None,
+                 final_renorm: bool = True):
+        """final_renorm=False returns the last XOR pair before its renorm (and without the final
+        bootstrap): true-FHE decrypt applies the next round's InvShiftRows there first"""
         log = (lambda k, v: debug.__setitem__(k, v)) if debug is not None else (lambda k, v: None)
         steps = [-4 * k * self.stride for k in (1, 2, 3)]  # _col_shift_rowmajor(ct, k), hoisted
         rh, rl = pair(self.ctx, lambda: rot_many(self.ctx, ct_hi, steps), lambda: rot_many(self.ctx, ct_lo, steps))
@@ -93,14 +96,19 @@ class InvMixColumnsFHE:
             log("acc1", a1)
             a2 = self._xor_pair(self._renorm_pair(*a1, level=NEED_XOR), e13, fl)
             log("acc2", a2)
-            out = self._renorm_pair(*self._xor_pair(self._renorm_pair(*a2, level=NEED_XOR), e9, fl), level=last)
+            a3 = self._xor_pair(self._renorm_pair(*a2, level=NEED_XOR), e9, fl)
+            if not final_renorm:
+                return a3
+            out = self._renorm_pair(*a3, level=last)
         else:
             # (e14 ^ e11) ^ (e13 ^ e9): the chain regrouped (see MixColFinal), the two inner XOR
             # pairs on the two branch streams
             x1, x2 = pair(self.ctx, lambda: self._renorm_pair(*self._xor_pair(e14, e11, fl), level=NEED_XOR),
                           lambda: self._renorm_pair(*self._xor_pair(e13, e9, fl), level=NEED_XOR))
+            if not final_renorm:
+                return self._xor_pair(x1, x2, fl)
             out = self._renorm_pair(*self._xor_pair(x1, x2, fl), level=last)
-        if do_final_bootstrap:
+        if do_final_bootstrap and self.enc.renorm_hook is None:
             out = bootstrap2(self.ctx, out[0], out[1])
         log("out", out)
         return out

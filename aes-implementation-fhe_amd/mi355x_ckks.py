@@ -43,6 +43,7 @@ EXPORTED = [
     "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_kernel_work", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan",
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_lut_create", "aesfhe_lut_eval",
+    "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled",
 ]
 
 # largest log2(PQ) for 128-bit classical security with a ternary secret (HE standard)
@@ -108,6 +109,8 @@ def load_library(path: Optional[Path] = None):
         "aesfhe_kernel_work": [vp, _dp, c_int],
     }
     sig["aesfhe_bootstrap_depth"] = []
+    sig["aesfhe_bootstrap_scaled"] = [vp, _H, c_dbl, _Hp]
+    sig["aesfhe_bootstrap_pair_scaled"] = [vp, _H, _H, c_dbl, _Hp, _Hp]
     sig["aesfhe_debug_bootplan"] = [c_int, _dp]
     sig["aesfhe_debug_boot_stage"] = [vp, _H, c_int, _Hp]
     sig["aesfhe_export_sparse"] = [vp, _up]
@@ -501,6 +504,16 @@ class Engine:
         """bootstrap(a), bootstrap(b) as one batched bootstrap (shared key / diagonal reads)"""
         x, y = ctypes.c_uint64(), ctypes.c_uint64()
         self._ctx.check(self._lib.aesfhe_bootstrap_pair(self._ctx.ptr, a.handle, b.handle, ctypes.byref(x), ctypes.byref(y)))
+        return Ciphertext(self._ctx, x.value), Ciphertext(self._ctx, y.value)
+
+    def bootstrap_scaled(self, ct, gain: float):
+        """gain * bootstrap(ct), gain in (0, 1] folded into the bootstrap's level-0 scaling"""
+        return self._new(self._lib.aesfhe_bootstrap_scaled, ct.handle, float(gain))
+
+    def bootstrap_pair_scaled(self, a, b, gain: float):
+        x, y = ctypes.c_uint64(), ctypes.c_uint64()
+        self._ctx.check(self._lib.aesfhe_bootstrap_pair_scaled(self._ctx.ptr, a.handle, b.handle, float(gain), ctypes.byref(x),
+                                                               ctypes.byref(y)))
         return Ciphertext(self._ctx, x.value), Ciphertext(self._ctx, y.value)
 
     def debug_boot_stage(self, ct, stage: int):

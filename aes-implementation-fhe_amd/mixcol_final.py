@@ -191,9 +191,17 @@ class MixColFinal:
         log("two", two)
         log("thr", thr)
         last = NEED_BOOTSTRAP if do_final_bootstrap else None  # bootstrapped next (from level 0), else fresh
-        if isinstance(debug, dict):
+        fhe = self.enc.renorm_hook is not None
+        if fhe:
+            # true-FHE: the GF multipliers amplify their inputs' errors up to ~20x, so their outputs
+            # are renormalised (bootstrap + two snaps) before the first XOR; then the reference's
+            # chain, each of r2 / r3 meeting a freshly snapped partner (zeta16_noise_reducer.py)
+            two, thr = pair(self.ctx, lambda: self._renorm_pair(*two, level=NEED_XOR),
+                            lambda: self._renorm_pair(*thr, level=NEED_XOR))
+        if isinstance(debug, dict) or fhe:
             # the reference's chain ((2x ^ 3r1) ^ r2) ^ r3 and its debug keys (REF :127-163): acc1 and
-            # acc2 before their renorm, acc3 after it
+            # acc2 before their renorm, acc3 after it.  True-FHE mode keeps this order: each of r2 / r3
+            # meets a freshly snapped partner (the tree's r2 ^ r3 would add two residuals)
             a1 = self._xor_pair(two, thr, fl)
             log("acc1", a1)
             a2 = self._xor_pair(self._renorm_pair(*a1, level=NEED_XOR), rot[2], fl)
@@ -208,7 +216,8 @@ class MixColFinal:
             acc = self._renorm_pair(*self._xor_pair(x1, x2, fl), level=last)
         log("acc3", acc)
         out_hi, out_lo = acc
-        if do_final_bootstrap:
+        # true-FHE mode: the renorm above already is a bootstrap (+ snap), the final one merges in
+        if do_final_bootstrap and self.enc.renorm_hook is None:
             out_hi, out_lo = bootstrap2(self.ctx, out_hi, out_lo)
             log("out", (out_hi, out_lo))
         return out_hi, out_lo

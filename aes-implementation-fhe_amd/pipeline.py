@@ -17,6 +17,13 @@ and one renorm fewer per fused step, the same bytes.
 ``fuse_sr_mc=True`` merges ShiftRows into MixColumns' rotations (shiftrows_mixcolumns.py, the
 GHS12 refinement of REF/README.md:137-138): three hoisted rotations per nibble instead of six.
 
+``true_fhe=True`` replaces every secret-key renorm by a bootstrap + homomorphic Zeta16 snap
+(zeta16_noise_reducer.BootstrapSnap): the XOR4 coefficients are normalised
+by 1/256 (REF/gen/generate_xor4_coeffs.py:17) so every LUT output has unit magnitude,
+MixColumns' / InvMixColumns' final bootstraps merge into their last renorm, and decrypt
+applies each InvShiftRows before the renorm that precedes InvSubBytes (the snap leaves
+exactly SubBytes' 13 levels).  No secret key is used between encryption and decryption.
+
 ``states`` = B > 1 runs B independent AES states per ciphertext pair in the slot-packed
 layout (state_encoder.py): ``encrypt`` / ``decrypt`` take and return
 (B, 16) arrays through the same step sequence, and a (16,) round key is shared by all B
@@ -38,7 +45,7 @@ from shift_rows import shift_rows_bytes
 from shiftrows_mixcolumns import ShiftRowsMixColumnsFusedEnc
 from sub_bytes_ark import SubBytesARK
 from sub_bytes_lut import SubBytesLUT
-from utils import (NEED_GF, NEED_ISR_ISB, NEED_SR_ARK, NEED_SR_MIX, NEED_SUB_ARK_SR, NEED_SUBBYTES, NEED_XOR,
+from utils import (pair, NEED_GF, NEED_ISR_ISB, NEED_SR_ARK, NEED_SR_MIX, NEED_SUB_ARK_SR, NEED_SUBBYTES, NEED_XOR,
                    RENORM_FLOOR)
 from xor4_lut import XOR4LUT
 
@@ -47,13 +54,15 @@ class AESPipeline:
     def __init__(self, ctx, coeffs: Dict[str, Any], *, mixcolumns: MixColFinal | None = None,
                  inv_mixcolumns: InvMixColumnsFHE | None = None, use_hard_renorm_between_steps: bool = False,
                  with_inv_mix_columns: bool = True, states: int = 1, fuse_sub_ark: bool = False,
-                 fuse_sr_mc: bool = False):
+                 fuse_sr_mc: bool = False, true_fhe: bool = False):
         self.ctx = ctx
         self.states = states
         self.encoder = StateEncoder(ctx, states)
         self.sc = ctx.engine.slot_count
         self.stride = self.sc // 16
-        self.xor4 = XOR4LUT(ctx, coeffs["xor4"])
+        self.true_fhe = true_fhe
+        # true-FHE: unit-magnitude XOR4 (REF/gen/generate_xor4_coeffs.py:17), so the snap sees codewords
+        self.xor4 = XOR4LUT(ctx, np.asarray(coeffs["xor4"]) / 256.0 if true_fhe else coeffs["xor4"])
         self.sub = SubBytesLUT(ctx, coeffs["sub_hi"], coeffs["sub_lo"])
         self.isub = SubBytesLUT(ctx, coeffs["inv_sub_hi"], coeffs["inv_sub_lo"]) if "inv_sub_hi" in coeffs else None
         self.shift = ShiftRows(ctx, states=states)
@@ -65,6 +74,14 @@ class AESPipeline:
             if enc is not None and getattr(enc, "states", 1) != states:
                 raise ValueError("mixcolumns / inv_mixcolumns were built for a different states-per-ciphertext count")
         self.ark = AddRoundKey(self.xor4)
+        self.snapper = None
+        if true_fhe:
+            from zeta16_noise_reducer import BootstrapSnap
+            self.snapper = BootstrapSnap(ctx)
+            for enc in (self.encoder, getattr(self.mix, "enc", None), getattr(self.invmix, "enc", None)):
+                if enc is not None:
+                    enc.renorm_hook = self.snapper.apply_pair
+
         self.use_hard_renorm_between_steps = use_hard_renorm_between_steps
         self.with_inv_mix_columns = with_inv_mix_columns
         self._rk_cache: List[Tuple[Any, Any]] | None = None
@@ -84,10 +101,14 @@ class AESPipeline:
     # ---------------------------------------------------------------- utils
     def _renorm_pair(self, hi, lo, level=None):
         """renorm between steps; `level` = what the next step needs (utils.NEED_*; None = fresh)"""
-        return self.encoder.renorm(hi, lo, level) if self.use_hard_renorm_between_steps else (hi, lo)
+        if self.true_fhe or self.use_hard_renorm_between_steps:
+            return self.encoder.renorm(hi, lo, level)
+        return hi, lo
 
     def _floor(self) -> Optional[int]:
         """output level a step needs when a renorm follows it (utils.RENORM_FLOOR), else None"""
+        if self.true_fhe:
+            return 1  # the bootstrap reads any level; decrypt's InvShiftRows needs one above 0
         return RENORM_FLOOR if self.use_hard_renorm_between_steps else None
 
     def _ark_renorm(self, ct, key_pair, level=None):
@@ -98,6 +119,9 @@ class AESPipeline:
         lut = self.isub if inverse else self.sub
         if lut is None:
             raise KeyError("inv_sub_hi")
+        if self.true_fhe:
+            level = NEED_SR_ARK  # true-FHE: SubBytes' ~3e-2 output errors get two snaps (ShiftRows +
+            #                      the GF multipliers need 6 levels, MixColumns renormalises after them)
         return self._renorm_pair(*lut.apply(*ct, out_level=self._floor()), level=level)
 
     def _encode_key(self, key_bytes: np.ndarray):
@@ -227,6 +251,8 @@ class AESPipeline:
             debug.clear()
         rk = self._prepare_round_keys(round_keys)
         self._log_pair(debug, "dec.input", ct_hi, ct_lo)
+        if self.true_fhe and not self.fuse_sub_ark:
+            return self._decrypt_fhe(ct_hi, ct_lo, rk, debug)
         ct = self.ark(ct_hi, ct_lo, *rk[10], out_level=self._floor())
         self._log_pair(debug, "dec.init.ark10", *ct)
         fuse = self.fuse_sub_ark
@@ -277,3 +303,32 @@ class AESPipeline:
         ct = self._renorm_pair(*ct)
         self._log_pair(debug, "dec.output", *ct)
         return ct
+
+    def _decrypt_fhe(self, ct_hi, ct_lo, rk, debug):
+        """decrypt in true-FHE mode: the same steps, each InvShiftRows applied BEFORE the renorm
+        (bootstrap + snap) that precedes InvSubBytes -- after the snap exactly InvSubBytes' 13
+        levels remain.  InvShiftRows is a masked permutation, so moving it across the renorm
+        changes no byte (ISB(ISR(x)) with x renormalised either side)."""
+        if self.isub is None:
+            raise KeyError("inv_sub_hi")
+        fl = self._floor()
+        ct = self.ark(ct_hi, ct_lo, *rk[10], out_level=fl)
+        self._log_pair(debug, "dec.init.ark10", *ct)
+        ct = self._renorm_pair(*self.inv_shift_rows(*ct), level=NEED_SUBBYTES)
+        self._log_pair(debug, "dec.r9.isr", *ct)
+        for r in range(9, -1, -1):
+            # InvSubBytes' output error is ~3e-2: its renorm snaps twice before AddRoundKey's XOR4
+            ct = self._renorm_pair(*self.isub.apply(*ct, out_level=fl), level=NEED_XOR)
+            self._log_pair(debug, f"dec.r{r}.isb" if r else "dec.final.isb.renorm", *ct)
+            ct = self.ark(*ct, *rk[r], out_level=fl)
+            if r == 0:
+                self._log_pair(debug, "dec.final.ark0", *ct)
+                ct = self._renorm_pair(*ct)
+                self._log_pair(debug, "dec.output", *ct)
+                return ct
+            if self.with_inv_mix_columns:
+                ct = self._renorm_pair(*ct, level=NEED_GF)
+                self._log_pair(debug, f"dec.r{r}.ark", *ct)
+                ct = self.invmix(*ct, final_renorm=False)
+            ct = self._renorm_pair(*self.inv_shift_rows(*ct), level=NEED_SUBBYTES)
+            self._log_pair(debug, f"dec.r{r}.imc" if self.with_inv_mix_columns else f"dec.r{r}.ark", *ct)

@@ -28,6 +28,9 @@ class StateEncoder:
         if not 1 <= states <= self.stride:
             raise ValueError(f"states per ciphertext must be in [1, {self.stride}], got {states}")
         self.states = states
+        # set by AESPipeline(true_fhe=True): renorm(hi, lo) -> hook(hi, lo), the bootstrap + snap
+        # that replaces the secret-key renorm (zeta16_noise_reducer.BootstrapSnap)
+        self.renorm_hook = None
 
     def _as_batch(self, state: np.ndarray) -> np.ndarray:
         state = np.asarray(state, dtype=np.uint8)
@@ -60,7 +63,10 @@ class StateEncoder:
 
     def renorm(self, ct_hi, ct_lo, level=None) -> Tuple[Any, Any]:
         """decode -> re-encode (REF/pipeline.py:65-69), done on the device when available;
-        `level`: the level the next step needs (None = fresh), honoured by the device path."""
+        `level`: the level the next step needs (None = fresh), honoured by the device path.
+        With a renorm_hook (true-FHE mode) the hook runs instead (it reads `level` as the next step's need)."""
+        if self.renorm_hook is not None:
+            return self.renorm_hook(ct_hi, ct_lo, level)
         fast = getattr(self.ctx, "renorm_pair", None)
         if fast is not None:
             if level is not None and not _RENORM_FRESH:

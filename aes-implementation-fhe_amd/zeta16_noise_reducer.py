@@ -1,0 +1,128 @@
+"""Homomorphic Zeta16 snaps: the true-FHE replacement of the secret-key renorm
+(REF/zeta16_noise_reducter.py:6-169, REF/noise_reduction.py:14-82).
+
+A renorm re-anchors every state slot to the nearest 16th root of unity ζ.  Without the
+secret key it is a bootstrap (fresh levels, REF bootstrap_before=True) followed by a
+polynomial f with f(ζ) = ζ and f'(ζ) = 0 at every codeword, so an error ε becomes O(ε²).
+
+``Zeta16NoiseReducer`` -- the reference's f(x) = (17x - x^17)/16 (REF :6-57): x^1..x^8 by the
+power basis, x^16 = (x^8)^2, x^17 = x^16 x (depth 5) and its -1/16 scalar: depth 6 as written.  (The reference's ``Zeta16Snap``,
+:108-169, forms x^17 as x^8 conj(x^7), which equals x on the unit circle -- the identity, no
+snap; it is not rebuilt.)
+
+``Zeta16Snap15`` -- the depth-4 snap this engine's parameter set needs.  After a bootstrap
+the state sits at the fresh level 17 and SubBytes needs 13 levels, so the snap may use 4.
+Over x and conj(x) (conjugation is a free key switch), with e = x/ζ - 1:
+
+    f(x) = (30 x - 15 x^2 conj(x) + conj(x)^15) / 16
+    f(ζ(1+e)) = ζ (1 + O(e^2))      (value 1, both first-order terms cancel; 16 f = 30 - 15 + 1)
+
+conj(x)^15 = conj(x^8 x^7) has depth 4, but its coefficient 1/16 would cost a fifth level.
+The bootstrap therefore returns u = κ x with κ^15 = 1/16 (gain folded into its level-0
+scaling integer, aesfhe_bootstrap_pair_scaled), so in u
+
+    f = a1 u + a3 u^2 conj(u) + conj(u)^15,   a1 = 30 / (16 κ),  a3 = -15 / (16 κ^3)
+
+with the depth-4 term's coefficient exactly 1 and the others on depth <= 2 products.
+
+``BootstrapSnap`` -- the pair renorm the pipeline uses in true-FHE mode: one batched
+scaled bootstrap of (hi, lo), then Zeta16Snap15 on each half (two branch streams), and a second
+snap (x κ, then the snap: 5 levels) when the step after the renorm is an XOR4 (<= 8 levels
+needed) rather than SubBytes (13): an error ε leaves one snap as ~9 ε², two as ~729 ε^4.
+SubBytes / InvSubBytes outputs carry ~3e-2 slot errors (their polynomials' derivatives
+amplify the CKKS noise ~60x on average), and an XOR4 can amplify its inputs' errors up to
+~17x, so one snap between them is not enough at the tails of a batch (measured:
+profiles/r2_true_fhe.json).
+"""
+from __future__ import annotations
+
+from typing import Any, Tuple
+
+from utils import NEED_SR_ARK, pair
+from xor4_lut import powers
+
+SNAP15_DEPTH = 4
+DOUBLE_SNAP_MAX_LEVEL = NEED_SR_ARK  # renorms whose consumer needs at most this many levels snap twice
+KAPPA = 16.0 ** (-1.0 / 15.0)  # bootstrap gain: conj(u)^15 carries coefficient 1
+
+
+class Zeta16NoiseReducer:
+    """f(x) = (17/16) x - (1/16) x^17 (REF/zeta16_noise_reducter.py:6-57); depth 6 as written."""
+
+    def __init__(self, ctx, bootstrap_before: bool = False, bootstrap_after: bool = False):
+        self.ctx = ctx
+        self.alpha = 17.0 / 16.0
+        self.beta = -1.0 / 16.0
+        self.bootstrap_before = bootstrap_before
+        self.bootstrap_after = bootstrap_after
+
+    def _ensure_power_basis(self, ct):
+        """x^1..x^8, one bootstrap on a level complaint (REF :20-29)"""
+        try:
+            return ct, self.ctx.make_power_basis(ct, 8)
+        except RuntimeError:
+            ct = self.ctx.bootstrap(ct)
+            return ct, self.ctx.make_power_basis(ct, 8)
+
+    def apply(self, ct):
+        ctx = self.ctx
+        x = ctx.bootstrap(ct) if self.bootstrap_before else ct
+        x, pos = self._ensure_power_basis(x)
+        x16 = ctx.multiply(pos[7], pos[7])
+        x17 = ctx.multiply(x16, pos[0])
+        y = ctx.add(ctx.multiply_plain(pos[0], self.alpha), ctx.multiply_plain(x17, self.beta))
+        return ctx.bootstrap(y) if self.bootstrap_after else y
+
+    def apply_pair(self, ct_hi, ct_lo):
+        return pair(self.ctx, lambda: self.apply(ct_hi), lambda: self.apply(ct_lo))
+
+
+class Zeta16Snap15:
+    """f = a1 u + a3 u^2 conj(u) + conj(u)^15 on u = κ x (module docstring); depth 4."""
+
+    def __init__(self, ctx, kappa: float = KAPPA):
+        self.ctx = ctx
+        self.kappa = kappa
+        self.a1 = 30.0 / (16.0 * kappa)
+        self.a3 = -15.0 / (16.0 * kappa ** 3)
+        self.c15 = 1.0 / (16.0 * kappa ** 15)  # 1 for the default κ: an exact (free) coefficient
+
+    def apply_scaled(self, u):
+        """the snap of x given u = κ x"""
+        ctx = self.ctx
+        pw = powers(ctx, u, {2, 7, 8})               # u^2 (1), u^7, u^8 (3): five products
+        ub = ctx.conjugate(u)
+        u15 = ctx.multiply(pw[8], pw[7])             # depth 4
+        t3 = ctx.multiply(pw[2], ub)                 # u^2 conj(u), depth 2
+        c15 = ctx.conjugate(u15)
+        if abs(self.c15 - 1.0) > 1e-12:
+            c15 = ctx.multiply(c15, self.c15)
+        return ctx.add(ctx.add(ctx.multiply(u, self.a1), ctx.multiply(t3, self.a3)), c15)
+
+    def apply(self, x):
+        """the snap of a ciphertext at unit gain (scales by κ first: one more level)"""
+        return self.apply_scaled(self.ctx.multiply(x, self.kappa))
+
+
+class BootstrapSnap:
+    """True-FHE renorm of a (hi, lo) pair: scaled bootstrap, then the depth-4 snap."""
+
+    def __init__(self, ctx, snap: Zeta16Snap15 | None = None):
+        if getattr(ctx, "bootstrap_pair_scaled", None) is None:
+            raise RuntimeError("true-FHE renorm needs the engine's scaled pair bootstrap (bootstrappable context)")
+        self.ctx = ctx
+        self.snap = snap or Zeta16Snap15(ctx)
+
+    def apply_pair(self, ct_hi, ct_lo, level=None) -> Tuple[Any, Any]:
+        """level: what the next step needs (the pipeline's renorm hint); None or <= 8 (an XOR4,
+        ShiftRows + XOR4, or the output) -> two snaps when the fresh level leaves room"""
+        ctx = self.ctx
+        fresh = ctx.engine.fresh_level
+        twice = (level is None or level <= DOUBLE_SNAP_MAX_LEVEL) and fresh - 2 * SNAP15_DEPTH - 1 >= (level or 0)
+        uh, ul = ctx.bootstrap_pair_scaled(ctx.to_intt(ct_hi), ctx.to_intt(ct_lo), self.snap.kappa)
+        sn = self.snap
+        if twice:
+            return pair(ctx, lambda: sn.apply(sn.apply_scaled(uh)), lambda: sn.apply(sn.apply_scaled(ul)), shared=(uh, ul))
+        return pair(ctx, lambda: sn.apply_scaled(uh), lambda: sn.apply_scaled(ul), shared=(uh, ul))
+
+    __call__ = apply_pair

@@ -68,6 +68,9 @@ def parse():
                     help="secondary measurement (BASELINE configs 3/4): this many independent states per rank, "
                          "slot-packed into one ciphertext pair (SURVEY.md 8(f)1); 0 = skip")
     ap.add_argument("--batch-steps", type=int, default=1)
+    ap.add_argument("--true-fhe-steps", type=int, default=1,
+                    help="SURVEY.md 8(f)3 line beside the headline: C2 encrypts with every secret-key renorm replaced "
+                         "by bootstrap + homomorphic Zeta16 snap (AESPipeline(true_fhe=True)); 0 = skip")
     ap.add_argument("--no-batch-roundtrip", dest="batch_roundtrip", action="store_false",
                     help="skip the decrypt leg of the batch (BASELINE config 5)")
     ap.add_argument("--whole-stats", default=None,
@@ -265,6 +268,33 @@ def run_batch(ctx, coeffs, rks, args, rank, world, dist) -> dict:
             **({"roundtrip": rt} if rt else {})}
 
 
+def run_true_fhe(ctx, coeffs, rks, args, rank, world, dist) -> dict:
+    """the C2 workload with no secret key between encryption and decryption --
+    every renorm point is a bootstrap + homomorphic Zeta16 snap (zeta16_noise_reducer.py), XOR4
+    normalised by 1/256.  One state per rank per step, checked after the timed region."""
+    from oracle import aes_plain  # checker only, after the timed region
+    from pipeline import AESPipeline
+    pipe = AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=False, true_fhe=True)
+    sts = rank_states(rank + 1000, 1 + args.true_fhe_steps)
+    pipe.encrypt(sts[0], rks)  # warmup: snap constants, normalised XOR4 coefficient sets
+    ctx.engine.sync()
+    barrier(dist)
+    n0 = ctx.bootstrap_stats()["count"]
+    t0 = time.perf_counter()
+    outs = [pipe.encrypt(s, rks) for s in sts[1:]]
+    ctx.engine.sync()
+    barrier(dist)
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    nboot = (ctx.bootstrap_stats()["count"] - n0) / args.true_fhe_steps
+    ok = all(np.array_equal(pipe.encoder.decode(*o), aes_plain.ref_encrypt(s, rks)) for s, o in zip(sts[1:], outs))
+    ok = all(r[0] for r in all_gather_ints(dist, [int(ok)]))
+    done = args.true_fhe_steps * world
+    return {"workload": "C2 in true-FHE mode: every secret-key renorm replaced by bootstrap + depth-4 Zeta16 snap "
+                        "(two snaps where the next step is an XOR4); no secret key between encryption and decryption",
+            "rounds_per_s": 10.0 * done / elapsed, "ms_per_step": elapsed / args.true_fhe_steps * 1e3,
+            "bootstraps_per_encrypt": nboot, "steps": args.true_fhe_steps, "verified_against_plaintext_model": bool(ok)}
+
+
 def dry_run(args, rank, world, dist):
     """The N > 1 host path with a real engine per rank, on CPU: one oracle CKKS engine per rank
     (oracle/ckks_cpu.py, N = 2^13) keyed by the broadcast seed, AddRoundKey on the rank's own
@@ -365,6 +395,7 @@ def main():
         Path(args.whole_stats).write_text(json.dumps(tot, indent=1))
     E.profile(())
     batch = run_batch(ctx, coeffs, rks, args, rank, world, dist) if args.batch_states > 0 else None
+    true_fhe = run_true_fhe(ctx, coeffs, rks, args, rank, world, dist) if args.true_fhe_steps > 0 and not args.no_final_bootstrap else None
 
     # correctness of the timed outputs (outside the timed region)
     ok = all(np.array_equal(pipe.encoder.decode(*o), aes_plain.ref_encrypt(states[args.warmup + j], rks))
@@ -436,6 +467,8 @@ def main():
     }
     if batch is not None:
         line["batch"] = batch
+    if true_fhe is not None:
+        line["true_fhe"] = true_fhe
     if args.profile_all:
         line["kernels"] = {k: {"launches": v["launches"], "ms": v["ms"], "GBps": v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] else 0}
                            for k, v in stats.items()}

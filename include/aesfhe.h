@@ -153,6 +153,12 @@ int aesfhe_bootstrap(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
  * as one batched bootstrap: same results as two aesfhe_bootstrap calls, each key switch reads
  * its key and each linear transform its diagonals once for both */
 int aesfhe_bootstrap_pair(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, aesfhe_handle* out_a, aesfhe_handle* out_b);
+/* bootstrap(ct) * gain and its pair form, gain in (0, 1] folded into the level-0 scaling (no
+ * extra level): the true-FHE renorm's bootstrap hands the snap u = kappa x (REF
+ * zeta16_noise_reducter.py:6-57 bootstrap_before=True) */
+int aesfhe_bootstrap_scaled(aesfhe_ctx* ctx, aesfhe_handle ct, double gain, aesfhe_handle* out);
+int aesfhe_bootstrap_pair_scaled(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, double gain, aesfhe_handle* out_a,
+                                 aesfhe_handle* out_b);
 int aesfhe_bootstrap_depth(void);
 /* host self-check of the bootstrap plan: err[0] SlotToCoeff, err[1] CoeffToSlot vs the
  * canonical embedding, err[2] EvalMod Chebyshev error (no GPU needed) */
