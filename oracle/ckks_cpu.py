@@ -44,6 +44,9 @@ def lib():
     vp, c_int, c_u64, c_i64, c_dbl = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_double
     sig = {
         "orc_create": (vp, [c_int, c_int, c_int, c_u64]),
+        "orc_create_boot": (vp, [c_int, c_int, c_int, c_int, c_u64]),
+        "orc_rescale2": (None, [vp, c_int, c_int, u32p, u32p]),
+        "orc_keyswitch_d2s": (None, [vp, c_int, u32p, u32p, u32p]),
         "orc_destroy": (None, [vp]),
         "orc_info": (None, [vp, i32p]),
         "orc_moduli": (None, [vp, u32p]),
@@ -77,9 +80,15 @@ def lib():
 class OracleParams:
     """Parameter set + raw primitives."""
 
-    def __init__(self, log_n: int = 16, max_level: int = 17, dnum: int = 3, seed: int = 0):
+    def __init__(self, log_n: int = 16, max_level: int = 17, dnum: int = 3, seed: int = 0, boot_double: int = 0):
+        """boot_double > 0: the bootstrappable chain (params.cpp), single-prime levels 0..max_level
+        and boot_double double-prime levels above (top level max_level + boot_double)"""
         self._L = lib()
-        self.h = self._L.orc_create(log_n, max_level, dnum, seed)
+        self.L1 = max_level
+        if boot_double:
+            self.h = self._L.orc_create_boot(log_n, max_level, boot_double, dnum, seed)
+        else:
+            self.h = self._L.orc_create(log_n, max_level, dnum, seed)
         info = np.zeros(8, np.int32)
         self._L.orc_info(self.h, info)
         self.n, self.L, self.n_q, self.n_ks, self.n_p, self.alpha, self.dnum, self.log_n = map(int, info)
@@ -156,7 +165,7 @@ class OracleParams:
         return out
 
     def keyswitch(self, level: int, d: np.ndarray, ksk: np.ndarray) -> np.ndarray:
-        out = np.zeros((2, level + 2, self.n), np.uint32)
+        out = np.zeros((2, self.nl(level), self.n), np.uint32)
         self._L.orc_keyswitch(self.h, level, np.ascontiguousarray(d, np.uint32), np.ascontiguousarray(ksk, np.uint32), out)
         return out
 
@@ -192,6 +201,25 @@ class OracleParams:
         ct = np.ascontiguousarray(ct, np.uint32)
         out = np.zeros(self.n, np.float64)
         self._L.orc_decrypt_coeffs(self.h, level, ct.shape[0], ct, np.ascontiguousarray(s_ntt, np.uint32), out)
+        return out
+
+    def nl(self, level: int) -> int:
+        """limbs at a level: l + 2 up to L1, two more per double-prime level above"""
+        if level > self.L:  # transient level L + 1 of a top-level encryption
+            return self.nl(self.L) + 1
+        return level + 2 if level <= self.L1 else self.L1 + 2 + 2 * (level - self.L1)
+
+    def rescale2(self, level: int, x: np.ndarray) -> np.ndarray:
+        """double-prime rescale from `level` (drops the two last limbs, one rounding)"""
+        x = np.ascontiguousarray(x, np.uint32)
+        out = np.zeros((x.shape[0], self.nl(level) - 2, self.n), np.uint32)
+        self._L.orc_rescale2(self.h, level, x.shape[0], x, out)
+        return out
+
+    def keyswitch_d2s(self, np_d2s: int, d: np.ndarray, ksk: np.ndarray) -> np.ndarray:
+        """the bootstrap's dense -> sparse key switch over Q0 P' (d: c1 on q0, q1)"""
+        out = np.zeros((2, 2, self.n), np.uint32)
+        self._L.orc_keyswitch_d2s(self.h, int(np_d2s), np.ascontiguousarray(d, np.uint32), np.ascontiguousarray(ksk, np.uint32), out)
         return out
 
     # -- helpers -----------------------------------------------------------------------

@@ -46,7 +46,14 @@ typedef struct {
     u32 *ninv;
     double *delta; /* delta[l], l = 0..L */
     u64 seed;
+    int L1;        /* top of the single-prime region (== L without the bootstrapping region) */
 } orc_t;
+
+/* limbs of a level: l + 2 up to L1, two more per level above */
+static int NL(const orc_t *o, int l) {
+    if (l > o->L) return NL(o, o->L) + 1;  /* transient level L + 1 of a top-level encryption */
+    return l <= o->L1 ? l + 2 : o->L1 + 2 + 2 * (l - o->L1);
+}
 
 /* ------------------------------------------------------------------ */
 /* scalar modular arithmetic                                           */
@@ -122,7 +129,7 @@ static int prime_used(const u32 *list, int cnt, u32 p) {
 
 void *orc_create(int logn, int L, int dnum, u64 seed) {
     orc_t *o = (orc_t *)calloc(1, sizeof(orc_t));
-    o->logn = logn; o->n = 1 << logn; o->L = L; o->dnum = dnum; o->seed = seed;
+    o->logn = logn; o->n = 1 << logn; o->L = L; o->dnum = dnum; o->seed = seed; o->L1 = L;
     o->n_q = L + 3; o->n_ks = L + 2;
     o->alpha = (o->n_ks + dnum - 1) / dnum;
     o->n_p = o->alpha + 1; /* P exceeds every digit modulus by one prime */
@@ -164,6 +171,92 @@ void *orc_create(int logn, int L, int dnum, u64 seed) {
         o->mod[l + 1] = best;
         used[nused++] = best;
         o->delta[l - 1] = o->delta[l] * o->delta[l] / (double)best;
+    }
+    free(used);
+    o->psi_rev = (u32 **)calloc(tot, sizeof(u32 *));
+    o->ipsi_rev = (u32 **)calloc(tot, sizeof(u32 *));
+    o->ninv = (u32 *)calloc(tot, sizeof(u32));
+    for (int i = 0; i < tot; i++) {
+        u32 q = o->mod[i];
+        u32 psi = find_psi(q, logn), ipsi = invm(psi, q);
+        o->psi_rev[i] = (u32 *)malloc(sizeof(u32) * o->n);
+        o->ipsi_rev[i] = (u32 *)malloc(sizeof(u32) * o->n);
+        u32 p = 1, ip = 1;
+        for (int k = 0; k < o->n; k++) {
+            u32 r = bitrev((u32)k, logn);
+            o->psi_rev[i][r] = p; o->ipsi_rev[i][r] = ip;
+            p = mulm(p, psi, q); ip = mulm(ip, ipsi, q);
+        }
+        o->ninv[i] = invm((u32)o->n, q);
+    }
+    return o;
+}
+
+/* the bootstrappable chain (params.cpp HostParams::build): single-prime levels 0..L1 as
+ * above, then n_double levels each dropping a prime pair (qa closest to sqrt(want), qb
+ * closest to want / qa, want = delta_l^2 / T^2), delta_L = T^2, and the transition pair at
+ * level L1 + 1 (two primes closest to T).  The same "unused prime closest to" rule and the
+ * same selection order, so both builders pick the same primes. */
+static u32 closest_prime(u32 *used, int *nused, u64 twon, double want) {
+    const u64 PMAX = 1ull << 30, PMIN = 1ull << 29;
+    u64 center = (u64)((want - 1.0) / (double)twon + 0.5) * twon + 1;
+    u32 best = 0; double bestd = 1e300;
+    for (i64 s = 0; s < 100000; s++) {
+        for (int sgn = -1; sgn <= 1; sgn += 2) {
+            i64 c = (i64)center + sgn * s * (i64)twon;
+            if (c <= (i64)PMIN || c >= (i64)PMAX) continue;
+            if (!is_prime32((u32)c) || prime_used(used, *nused, (u32)c)) continue;
+            double d = fabs((double)c - want);
+            if (d < bestd || (d == bestd && (u32)c < best)) { bestd = d; best = (u32)c; }
+        }
+        if (best && (double)s * twon > bestd + twon) break;
+    }
+    if (best) used[(*nused)++] = best;
+    return best;
+}
+
+void *orc_create_boot(int logn, int L1, int n_double, int dnum, u64 seed) {
+    orc_t *o = (orc_t *)calloc(1, sizeof(orc_t));
+    int L = L1 + n_double;
+    o->logn = logn; o->n = 1 << logn; o->L = L; o->L1 = L1; o->dnum = dnum; o->seed = seed;
+    o->n_ks = NL(o, L); o->n_q = o->n_ks + 1;
+    o->alpha = (o->n_ks + dnum - 1) / dnum;
+    o->n_p = o->alpha + 1;
+    int tot = o->n_q + o->n_p;
+    o->mod = (u32 *)calloc(tot, sizeof(u32));
+    u32 *used = (u32 *)calloc(tot + 8, sizeof(u32));
+    int nused = 0;
+    u64 twon = 2ull << logn;
+    const u64 PMAX = 1ull << 30;
+    u64 cand = (PMAX - 1) / twon * twon + 1;
+    int want = 2 + o->n_p + 1, got = 0;
+    u32 big[96];
+    while (got < want) { if (cand < PMAX && is_prime32((u32)cand)) big[got++] = (u32)cand; cand -= twon; }
+    o->mod[0] = big[0]; o->mod[1] = big[1];
+    for (int k = 0; k < o->n_p; k++) o->mod[o->n_q + k] = big[2 + k];
+    o->mod[o->n_q - 1] = big[2 + o->n_p];
+    for (int i = 0; i < want; i++) used[nused++] = big[i];
+    const double T = 966367641.6;
+    o->delta = (double *)calloc(L + 1, sizeof(double));
+    o->delta[L1] = T;
+    for (int l = L1; l >= 1; l--) {
+        u32 q = closest_prime(used, &nused, twon, o->delta[l] * o->delta[l] / T);
+        o->mod[l + 1] = q;
+        o->delta[l - 1] = o->delta[l] * o->delta[l] / (double)q;
+    }
+    if (L > L1) {
+        o->delta[L] = T * T;
+        for (int l = L; l >= L1 + 2; l--) {
+            double w = o->delta[l] * o->delta[l] / (T * T);
+            u32 qa = closest_prime(used, &nused, twon, sqrt(w));
+            u32 qb = closest_prime(used, &nused, twon, w / (double)qa);
+            o->mod[NL(o, l) - 1] = qa;
+            o->mod[NL(o, l) - 2] = qb;
+            o->delta[l - 1] = o->delta[l] * o->delta[l] / ((double)qa * (double)qb);
+        }
+        u32 qa = closest_prime(used, &nused, twon, T), qb = closest_prime(used, &nused, twon, T);
+        o->mod[NL(o, L1 + 1) - 1] = qa;
+        o->mod[NL(o, L1 + 1) - 2] = qb;
     }
     free(used);
     o->psi_rev = (u32 **)calloc(tot, sizeof(u32 *));
@@ -444,7 +537,7 @@ void orc_gen_ksk(void *h, u64 g, u32 *out) {
 /* ------------------------------------------------------------------ */
 void orc_rescale(void *h, int level, int npoly, const u32 *in, u32 *out) {
     orc_t *o = (orc_t *)h;
-    int n = o->n, nl = level + 2, r = nl - 1;
+    int n = o->n, nl = NL(o, level), r = nl - 1;
     u32 qr = o->mod[r];
     for (int p = 0; p < npoly; p++) {
         const u32 *src = in + (size_t)p * nl * n;
@@ -492,7 +585,7 @@ static u32 overflow_count(const u32 *y, size_t stride, int h, const u32 *primes)
 /* ------------------------------------------------------------------ */
 void orc_keyswitch(void *h, int level, const u32 *d, const u32 *ksk, u32 *out) {
     orc_t *o = (orc_t *)h;
-    int n = o->n, nl = level + 2, np = o->n_p, next_key = o->n_ks + o->n_p;
+    int n = o->n, nl = NL(o, level), np = o->n_p, next_key = o->n_ks + o->n_p;
     int ne = nl + np; /* extended basis: Q limbs 0..nl-1, then P */
     int *gid = (int *)malloc(sizeof(int) * ne);  /* global prime index */
     int *kid = (int *)malloc(sizeof(int) * ne);  /* key limb index */
@@ -597,12 +690,142 @@ void orc_keyswitch(void *h, int level, const u32 *d, const u32 *ksk, u32 *out) {
 }
 
 /* ------------------------------------------------------------------ */
+/* double-prime rescale (bootstrapping region): divide by  */
+/* the two dropped primes at once.  qa = the last limb, qb = the one    */
+/* before; X = xa + qa ((xb - xa) qa^-1 mod qb) in [0, qa qb), centred; */
+/* out_t = (in_t - X mod q_t) (qa qb)^-1.  in: npoly x nl(l) limbs NTT. */
+/* ------------------------------------------------------------------ */
+void orc_rescale2(void *h, int level, int npoly, const u32 *in, u32 *out) {
+    orc_t *o = (orc_t *)h;
+    int n = o->n, nl = NL(o, level), r = nl - 2;
+    u32 qa = o->mod[nl - 1], qb = o->mod[nl - 2];
+    u32 ainv = invm(qa % qb, qb);
+    u64 Q = (u64)qa * qb;
+    for (int p = 0; p < npoly; p++) {
+        const u32 *src = in + (size_t)p * nl * n;
+        u32 *dst = out + (size_t)p * r * n;
+        u32 *xa = (u32 *)malloc(sizeof(u32) * n), *xb = (u32 *)malloc(sizeof(u32) * n);
+        memcpy(xa, src + (size_t)(nl - 1) * n, sizeof(u32) * n);
+        memcpy(xb, src + (size_t)(nl - 2) * n, sizeof(u32) * n);
+        intt_limb(o, nl - 1, xa);
+        intt_limb(o, nl - 2, xb);
+        i64 *X = (i64 *)malloc(sizeof(i64) * n);
+        for (int k = 0; k < n; k++) {
+            u32 d = subm(xb[k], xa[k] % qb, qb);
+            u64 x = (u64)xa[k] + (u64)qa * mulm(d, ainv, qb);
+            X[k] = x > Q / 2 ? (i64)x - (i64)Q : (i64)x;
+        }
+#pragma omp parallel for schedule(static)
+        for (int t = 0; t < r; t++) {
+            u32 q = o->mod[t];
+            u32 *v = (u32 *)malloc(sizeof(u32) * n);
+            for (int k = 0; k < n; k++) v[k] = signed_to_mod(X[k], q);
+            ntt_limb(o, t, v);
+            u32 qinv = invm(mulm(qa % q, qb % q, q), q);
+            for (int k = 0; k < n; k++)
+                dst[(size_t)t * n + k] = mulm(subm(src[(size_t)t * n + k], v[k], q), qinv, q);
+            free(v);
+        }
+        free(xa); free(xb); free(X);
+    }
+}
+
+/* ------------------------------------------------------------------ */
+/* dense -> sparse key switch of the bootstrap:    */
+/* modulus Q0 P' with Q0 = q0 q1 (one digit) and P' = the first np      */
+/* special primes.  d: c1 on (q0, q1), NTT form; ksk [2][2 + np][N];    */
+/* out [2][2][N] = key-switched (c0', c1') (c0 not added).              */
+/* ------------------------------------------------------------------ */
+void orc_keyswitch_d2s(void *h, int np, const u32 *d, const u32 *ksk, u32 *out) {
+    orc_t *o = (orc_t *)h;
+    int n = o->n, nq = 2, ne = nq + np;
+    int gid[64];
+    for (int x = 0; x < ne; x++) gid[x] = x < nq ? x : o->n_q + (x - nq);
+    u32 *coef = (u32 *)malloc(sizeof(u32) * (size_t)nq * n);
+    memcpy(coef, d, sizeof(u32) * (size_t)nq * n);
+    for (int i = 0; i < nq; i++) intt_limb(o, i, coef + (size_t)i * n);
+    u32 *y = (u32 *)malloc(sizeof(u32) * (size_t)nq * n);
+    for (int i = 0; i < nq; i++) {
+        u32 q = o->mod[i], qh = o->mod[1 - i] % q, qhi = invm(qh, q);
+        for (int k = 0; k < n; k++) y[(size_t)i * n + k] = mulm(coef[(size_t)i * n + k], qhi, q);
+    }
+    u32 *ucnt = (u32 *)malloc(sizeof(u32) * n);
+    for (int k = 0; k < n; k++) ucnt[k] = overflow_count(y + k, n, nq, o->mod);
+    u32 *ext = (u32 *)malloc(sizeof(u32) * (size_t)ne * n);
+    for (int x = 0; x < ne; x++) {
+        u32 *dst = ext + (size_t)x * n;
+        if (x < nq) { memcpy(dst, d + (size_t)x * n, sizeof(u32) * n); continue; }
+        u32 t = o->mod[gid[x]];
+        u32 qh0 = o->mod[1] % t, qh1 = o->mod[0] % t;
+        u32 negQ = mulm(o->mod[0] % t, o->mod[1] % t, t);
+        negQ = negQ ? t - negQ : 0;
+        for (int k = 0; k < n; k++) {
+            u128 s = (u64)ucnt[k] * negQ;
+            s += (u64)y[k] * qh0;
+            s += (u64)y[(size_t)n + k] * qh1;
+            dst[k] = (u32)(s % t);
+        }
+        ntt_limb(o, gid[x], dst);
+    }
+    u32 *acc = (u32 *)calloc((size_t)2 * ne * n, sizeof(u32));
+    const u32 *kb = ksk, *ka = ksk + (size_t)ne * n;
+    for (int x = 0; x < ne; x++) {
+        u32 t = o->mod[gid[x]];
+        for (int k = 0; k < n; k++) {
+            u32 e = ext[(size_t)x * n + k];
+            acc[(size_t)x * n + k] = mulm(e, kb[(size_t)x * n + k], t);
+            acc[(size_t)(ne + x) * n + k] = mulm(e, ka[(size_t)x * n + k], t);
+        }
+    }
+    /* ModDown by P' onto (q0, q1) */
+    for (int p = 0; p < 2; p++) {
+        u32 *a = acc + (size_t)p * ne * n;
+        u32 *yp = (u32 *)malloc(sizeof(u32) * (size_t)np * n);
+        for (int k2 = 0; k2 < np; k2++) {
+            int g = o->n_q + k2;
+            u32 q = o->mod[g], ph = 1;
+            for (int m = 0; m < np; m++) if (m != k2) ph = mulm(ph, o->mod[o->n_q + m] % q, q);
+            u32 phi = invm(ph, q);
+            memcpy(yp + (size_t)k2 * n, a + (size_t)(nq + k2) * n, sizeof(u32) * n);
+            intt_limb(o, g, yp + (size_t)k2 * n);
+            for (int k = 0; k < n; k++) yp[(size_t)k2 * n + k] = mulm(yp[(size_t)k2 * n + k], phi, q);
+        }
+        u32 *uc = (u32 *)malloc(sizeof(u32) * n);
+        for (int k = 0; k < n; k++) uc[k] = overflow_count(yp + k, n, np, o->mod + o->n_q);
+        for (int t = 0; t < nq; t++) {
+            u32 q = o->mod[t], pinv = 1;
+            u32 ph_t[16];
+            for (int k2 = 0; k2 < np; k2++) {
+                u32 v = 1;
+                for (int m = 0; m < np; m++) if (m != k2) v = mulm(v, o->mod[o->n_q + m] % q, q);
+                ph_t[k2] = v;
+                pinv = mulm(pinv, o->mod[o->n_q + k2] % q, q);
+            }
+            u32 negP = pinv ? q - pinv : 0;
+            pinv = invm(pinv, q);
+            u32 *conv = (u32 *)malloc(sizeof(u32) * n);
+            for (int k = 0; k < n; k++) {
+                u128 s = (u64)uc[k] * negP;
+                for (int k2 = 0; k2 < np; k2++) s += (u64)yp[(size_t)k2 * n + k] * ph_t[k2];
+                conv[k] = (u32)(s % q);
+            }
+            ntt_limb(o, t, conv);
+            u32 *dst = out + (size_t)p * nq * n + (size_t)t * n;
+            for (int k = 0; k < n; k++) dst[k] = mulm(subm(a[(size_t)t * n + k], conv[k], q), pinv, q);
+            free(conv);
+        }
+        free(yp); free(uc);
+    }
+    free(coef); free(y); free(ucnt); free(ext); free(acc);
+}
+
+/* ------------------------------------------------------------------ */
 /* ciphertext-level primitives                                         */
 /* ------------------------------------------------------------------ */
 /* (a0,a1) x (b0,b1) -> (d0,d1,d2), level l, NTT form */
 void orc_tensor(void *h, int level, const u32 *a, const u32 *b, u32 *out) {
     orc_t *o = (orc_t *)h;
-    int n = o->n, nl = level + 2;
+    int n = o->n, nl = NL(o, level);
     size_t P = (size_t)nl * n;
 #pragma omp parallel for schedule(static)
     for (int t = 0; t < nl; t++) {
@@ -633,7 +856,7 @@ void orc_mul_limb_consts(void *h, int nl, int npoly, const u32 *c, const u32 *in
 /* automorphism of a ciphertext-like array (npoly x (l+2) limbs), NTT form */
 void orc_automorph(void *h, int level, u64 g, int npoly, const u32 *in, u32 *out) {
     orc_t *o = (orc_t *)h;
-    int n = o->n, nl = level + 2;
+    int n = o->n, nl = NL(o, level);
     for (int p = 0; p < npoly; p++)
 #pragma omp parallel for schedule(static)
         for (int t = 0; t < nl; t++)
@@ -671,7 +894,7 @@ void orc_encrypt(void *h, int f, const u32 *pt, const u32 *pk, u64 ctr, u32 *out
 /* decrypt at level l: returns real coefficient vector (message * delta_l, as double) */
 void orc_decrypt_coeffs(void *h, int level, int npoly, const u32 *ct, const u32 *s_ntt, double *m_out) {
     orc_t *o = (orc_t *)h;
-    int n = o->n, nl = level + 2;
+    int n = o->n, nl = NL(o, level);
     u32 *x = (u32 *)malloc(sizeof(u32) * 2 * n);
     for (int t = 0; t < 2; t++) {
         u32 q = o->mod[t];

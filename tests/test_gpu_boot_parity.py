@@ -1,0 +1,115 @@
+"""Limb-level parity of the bootstrap's building blocks against the CPU oracle, on the
+N = 2^13 bootstrappable set (fresh level 3 -> L1 = 5, 13 double-prime levels, dnum 5).
+
+Same parameters and seed on both sides -> identical primes, scales and keys; identical input
+limbs -> identical output limbs for:
+- a key switch at double-prime levels (the CtS / EvalMod / StC rotations);
+- the double-prime rescale (oracle orc_rescale2: both limbs of the pair dropped, one rounding);
+- bootstrap stage 1, the level-0 scaling by k1 on the two base limbs Q0 = q0 q1;
+- stage 2, the dense -> sparse key switch over Q0 P' (oracle orc_keyswitch_d2s, with the
+  engine's exported d2s key; c0 added);
+- stage 3, ModRaise: the centred CRT lift of (q0, q1) to every limb of the top level;
+- stage 4, the sparse -> dense key switch at the top level (the oracle's generic key switch
+  with the exported s2d key).
+Stages are produced by aesfhe_debug_boot_stage (engine.hip bootstrap_l0 stop_after).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+LOG_N, FRESH, SEED = 13, 3, 7
+
+
+@pytest.fixture(scope="module")
+def pair():
+    from mi355x_ckks import Engine
+    from oracle.ckks_cpu import OracleParams
+    E = Engine(log_n=LOG_N, use_bootstrap=True, max_level=FRESH, dnum=5, seed=SEED, allow_insecure=True)
+    # the engine's chain: L1 = fresh + 2 single-prime levels, then the bootstrap's double-prime levels
+    L1 = max(l for l in range(E.L + 1) if E.level_limbs[l] == l + 2)
+    O = OracleParams(log_n=LOG_N, max_level=L1, dnum=E.dnum, seed=SEED, boot_double=E.L - L1)
+    return E, O
+
+
+def rand_rows(O, limbs, rng):
+    return np.stack([rng.integers(0, int(O.moduli[t]), O.n, dtype=np.uint64) for t in limbs]).astype(np.uint32)
+
+
+def rand_ct(O, level, npoly, rng):
+    return np.stack([rand_rows(O, range(O.nl(level)), rng) for _ in range(npoly)])
+
+
+def addmod(a, b, q):
+    return ((a.astype(np.uint64) + b) % q).astype(np.uint32)
+
+
+def test_boot_chain_matches(pair):
+    E, O = pair
+    assert O.L == E.L and O.n_q == E.n_q and O.n_p == E.n_p and O.n_ks == E.n_ks
+    assert [O.nl(l) for l in range(O.L + 1)] == E.level_limbs
+    assert np.array_equal(E.moduli(), O.moduli)
+    assert np.array_equal(E.scales(), O.deltas)
+
+
+@pytest.mark.parametrize("which", ["relin", "conj", "rot"])
+def test_keyswitch_double_prime_levels(pair, which):
+    E, O = pair
+    g = {"relin": 0, "conj": E.galois_conj, "rot": E.galois_rotate(E.slot_count // 8)}[which]
+    key = O.gen_ksk(g)
+    assert np.array_equal(E.export_ksk(g), key)
+    rng = np.random.default_rng(11)
+    for level in sorted({O.L, O.L - 1, O.L1 + 2, O.L1 + 1}):
+        d = rand_rows(O, range(O.nl(level)), rng)
+        assert np.array_equal(E.debug_keyswitch(level, g, d), O.keyswitch(level, d, key)), level
+
+
+def test_rescale_double_prime(pair):
+    E, O = pair
+    rng = np.random.default_rng(12)
+    for level in sorted({O.L, O.L - 3, O.L1 + 2, O.L1 + 1}):
+        x = rand_ct(O, level, 2, rng)
+        got = E.export(E.rescale(E.import_ct(x, level)))
+        assert np.array_equal(got, O.rescale2(level, x)), level
+
+
+def _boot_stages(E, O, seed):
+    rng = np.random.default_rng(seed)
+    x = rand_ct(O, 0, 2, rng)
+    ct = E.import_ct(x, 0)
+    return x, [E.export(E.debug_boot_stage(ct, s)) for s in (1, 2, 3, 4)]
+
+
+@pytest.mark.parametrize("seed", [13, 14])
+def test_bootstrap_stages_bitexact(pair, seed):
+    E, O = pair
+    info = E.boot_info()
+    x, (s1, s2, s3, s4) = _boot_stages(E, O, seed)
+    q0, q1 = int(O.moduli[0]), int(O.moduli[1])
+    Q01 = O.limbs_mod(2)
+    # 1. scaling by the integer k1 on (q0, q1)
+    k1 = int(info["k1"])
+    r = np.array([[k1 % q0], [k1 % q1]], np.uint64)
+    assert s1.shape == (2, 2, O.n)
+    assert np.array_equal(s1, ((x.astype(np.uint64) * r) % Q01).astype(np.uint32))
+    # 2. dense -> sparse over Q0 P' (the exported key is the one the engine switches with)
+    npd = int(info["d2s_special_primes"])
+    key = E.export_ksk(2 * E.n + 1)[0]
+    ks = O.keyswitch_d2s(npd, s1[1], key)
+    want2 = np.stack([addmod(ks[0], s1[0], Q01), ks[1]])
+    assert np.array_equal(s2, want2)
+    # 3. ModRaise: X = x0 + q0 ((x1 - x0) q0^-1 mod q1), centred in (-Q0/2, Q0/2], to every top limb
+    top = int(info["top"])
+    nlt = O.nl(top)
+    co = O.intt(s2.reshape(4, O.n), [0, 1, 0, 1]).reshape(2, 2, O.n).astype(np.int64)
+    q0inv = pow(q0, -1, q1)
+    X = co[:, 0] + q0 * ((((co[:, 1] - co[:, 0]) % q1) * q0inv) % q1)
+    X = np.where(X > (q0 * q1) // 2, X - q0 * q1, X)
+    lifted = np.stack([np.stack([(X[p] % int(O.moduli[t])) for t in range(nlt)]) for p in range(2)]).astype(np.uint32)
+    want3 = O.ntt(lifted.reshape(2 * nlt, O.n), list(range(nlt)) * 2).reshape(2, nlt, O.n)
+    assert s3.shape == (2, nlt, O.n)
+    assert np.array_equal(s3, want3)
+    # 4. sparse -> dense at the top level
+    ks = O.keyswitch(top, s3[1], E.export_ksk(2 * E.n + 3))
+    want4 = np.stack([addmod(ks[0], s3[0], O.limbs_mod(nlt)), ks[1]])
+    assert np.array_equal(s4, want4)
