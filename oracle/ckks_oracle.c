@@ -869,6 +869,7 @@ void orc_automorph(void *h, int level, u64 g, int npoly, const u32 *in, u32 *out
 void orc_encrypt(void *h, int f, const u32 *pt, const u32 *pk, u64 ctr, u32 *out) {
     orc_t *o = (orc_t *)h;
     int n = o->n, nq = f + 3, npk = o->n_q;
+    if (NL(o, f + 1) != nq) abort();  /* level f + 1 must be single-prime (or the transient L + 1) */
     size_t P = (size_t)nq * n, PK = (size_t)npk * n;
     int *ids = (int *)malloc(sizeof(int) * nq);
     for (int i = 0; i < nq; i++) ids[i] = i;
