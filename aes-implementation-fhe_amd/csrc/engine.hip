@@ -261,6 +261,10 @@ public:
             pts_.erase(ip);
         }
     }
+    void free_lut(aesfhe_handle h) {
+        if (!luts_.count(h)) throw std::runtime_error("aesfhe_lut_free: not a LUT handle");
+        free_handle(h);
+    }
     aesfhe_handle new_pt(const double* re, const double* im, int n) {
         Pt p;
         const int s = slot_count();
@@ -3047,6 +3051,10 @@ int aesfhe_lut_create(aesfhe_ctx* ctx, int n_a, int n_b, const double* re, const
 }
 int aesfhe_lut_eval(aesfhe_ctx* ctx, aesfhe_handle lut, const aesfhe_handle* a, const aesfhe_handle* b, aesfhe_handle* out) {
     CT_OP(e.lut_eval(lut, a, b))
+}
+int aesfhe_lut_free(aesfhe_ctx* ctx, aesfhe_handle lut) {
+    API_BEGIN ctx->eng->free_lut(lut);
+    API_END
 }
 int aesfhe_set_lazy(aesfhe_ctx* ctx, int on) {
     API_BEGIN ctx->eng->set_lazy(on != 0);

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import hashlib
 import threading
+import weakref
 import time
 
 import numpy as np
@@ -52,8 +53,7 @@ class EngineContext:
         self._bs_count = 0
         self._bs_total_s = 0.0
         self.fused_luts = bool(fused_luts)
-        self._luts = {}
-        self._lut_lock = threading.Lock()
+        self._init_lut_cache()
 
     # -------------------------------------------------------------- codec
     def encrypt(self, data: np.ndarray):
@@ -211,25 +211,74 @@ class EngineContext:
         `level`: re-encrypt at that level instead of the fresh one."""
         return self.engine.renorm_pair(hi, lo, states, level)
 
-    def lut(self, key, coeffs, c0: complex = 0j):
+    def _init_lut_cache(self):
+        self._luts = {}                                  # digest -> LookupTable
+        self._lut_pinned = set()                         # digests requested without an owner
+        self._lut_refs = {}                              # digest -> live owners holding it
+        self._lut_owned = weakref.WeakKeyDictionary()    # owner -> digests it holds
+        self._lut_lock = threading.RLock()               # RLock: an owner's finalizer may run in a GC pass inside the lock
+
+    def lut(self, key, coeffs, c0: complex = 0j, owner=None):
         """Engine-side coefficient set of a LUT polynomial, created once per coefficient CONTENT
-        (a digest of the coefficients, their shape and c0).  `key` is the caller's label and is
-        not part of the cache key: a label built from id() can be inherited by a new object with
-        other coefficients once the old one is collected (the stale-set failure of DESIGN.md §9),
-        and keying by content lets every module with the same set share one device copy, so the
-        cache is bounded by the number of distinct sets (the 22 coefficient files and their splits)."""
+        (a digest of the coefficients, their shape and c0).  `key` is the caller's label only: a
+        label built from id() can be inherited by a new object with other coefficients once the old
+        one is collected (the stale-set failure of DESIGN.md §9), and keying by content lets every
+        module with the same set share one device copy.
+        `owner` (the SubBytes / XOR4 / GF module object using the set): the set is evicted, and its
+        device memory released (aesfhe_lut_free), once every owner holding it has been collected
+        (weakref.finalize); sets requested without an owner stay for the context's lifetime."""
         arr = np.ascontiguousarray(coeffs, dtype=np.complex128)
         digest = hashlib.blake2b(arr.tobytes() + repr(arr.shape).encode() + np.complex128(c0).tobytes(), digest_size=16).digest()
         with self._lut_lock:
             t = self._luts.get(digest)
             if t is None:
                 t = self._luts[digest] = self.engine.lut_create(coeffs, c0)
+            if owner is None:
+                self._lut_pinned.add(digest)
+            else:
+                held = self._lut_owned.get(owner)
+                if held is None:
+                    held = self._lut_owned[owner] = set()
+                    weakref.finalize(owner, self._release_owner, weakref.ref(self), held).atexit = False
+                if digest not in held:
+                    held.add(digest)
+                    self._lut_refs[digest] = self._lut_refs.get(digest, 0) + 1
             return t
+
+    @staticmethod
+    def _release_owner(ctx_ref, held):
+        """finalizer of a LUT owner: drop its references, evict the sets nobody holds any more"""
+        ctx = ctx_ref()
+        if ctx is None:
+            return
+        dead = []
+        with ctx._lut_lock:
+            for d in held:
+                n = ctx._lut_refs.get(d, 0) - 1
+                if n > 0:
+                    ctx._lut_refs[d] = n
+                    continue
+                ctx._lut_refs.pop(d, None)
+                if d not in ctx._lut_pinned:
+                    t = ctx._luts.pop(d, None)
+                    if t is not None:
+                        dead.append(t)
+            held.clear()
+        free = getattr(ctx.engine, "lut_free", None)
+        for t in dead:
+            if free is not None:
+                free(t)
+
+    def lut_cache_size(self) -> int:
+        with self._lut_lock:
+            return len(self._luts)
 
     def clear_luts(self):
         """drop the cached coefficient sets (their device memory is freed with the last reference)"""
         with self._lut_lock:
             self._luts.clear()
+            self._lut_pinned.clear()
+            self._lut_refs.clear()
 
     def lut_eval(self, lut, a, b=None):
         """sum C[p,q] a[p] b[q] (or c0 + sum C[k] a[k]) in one fused kernel."""

@@ -42,7 +42,7 @@ EXPORTED = [
     "aesfhe_streams", "aesfhe_bind_stream", "aesfhe_fork", "aesfhe_join", "aesfhe_settle",
     "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_kernel_work", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan",
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot",
-    "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_lut_create", "aesfhe_lut_eval",
+    "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_lut_create", "aesfhe_lut_eval", "aesfhe_lut_free",
     "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled",
 ]
 
@@ -119,6 +119,7 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_create_boot"] = [pp, c_int, c_int, c_int, c_int, ctypes.c_uint64]
     sig["aesfhe_lut_create"] = [vp, c_int, c_int, _dp, _dp, c_dbl, c_dbl, _Hp]
     sig["aesfhe_lut_eval"] = [vp, _H, _Hp, _Hp, _Hp]
+    sig["aesfhe_lut_free"] = [vp, _H]
     sig["aesfhe_level_limbs"] = [vp, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")]
     for name in EXPORTED:
         fn = getattr(L, name)
@@ -166,7 +167,7 @@ class _Handle:
 
     def __del__(self):
         ctx = getattr(self, "_ctx", None)
-        if ctx is not None and ctx.ptr:
+        if ctx is not None and ctx.ptr and self.handle:
             try:
                 ctx.lib.aesfhe_free(ctx.ptr, self.handle)
             except Exception:
@@ -588,6 +589,12 @@ class Engine:
         ha = handles(a, lut.n_a)
         hb = handles(b, lut.n_b) if lut.n_b > 1 else None
         return self._new(self._lib.aesfhe_lut_eval, lut.handle, ha, hb)
+
+    def lut_free(self, lut: LookupTable):
+        """release a LUT's device coefficient set now (otherwise: when the handle is collected)"""
+        h, lut.handle = lut.handle, 0
+        if h:
+            self._ctx.check(self._lib.aesfhe_lut_free(self._ctx.ptr, h))
 
     # ------------------------------------------------------------------ raw access (tests)
     def moduli(self) -> np.ndarray:

@@ -85,7 +85,7 @@ def gf_eval(ctx, cache: _CoeffCache, mult: int, which: str, ct_hi, ct_lo) -> Any
     """gf_mult{mult}_{which}(hi, lo): the 2-variable LUT as one fused engine call when the
     context has it, else the reference's product loop."""
     bx, by = gf_basis16(ctx, ct_hi), gf_basis16(ctx, ct_lo)
-    out = fused_lut(ctx, ("gf", mult, which), cache.matrix(mult, which), bx, by)
+    out = fused_lut(ctx, ("gf", mult, which), cache.matrix(mult, which), bx, by, owner=cache)
     if out is not None:
         return out
     return _gf_sum(ctx, cache.load_plaintexts(ctx, mult, which), bx, by, ct_hi)

@@ -74,7 +74,7 @@ class SubBytesLUTFastCached:
     # ------------------------------------------------------------------ BSGS form
     def _lin(self, key, vec, elems, c0, like):
         """c0 + sum_k vec[k] elems[k]: one fused kernel, or scalar products if unavailable"""
-        out = fused_lut(self.ctx, (key, id(self)), vec, elems, c0=c0)
+        out = fused_lut(self.ctx, key, vec, elems, c0=c0, owner=self)
         if out is not None:
             return out
         ctx = self.ctx
@@ -206,7 +206,7 @@ class SubBytesLUTFastCached:
         # 1) ζ16^l -> ζ256^l
         pos16 = ctx.make_power_basis(ct_lo, self.deg16) if self.deg16 > 0 else []
         p16 = {k: self._power(pos16, k, 16, ctx) for k in self.ks_lift}
-        lifted = fused_lut(ctx, ("sb-lift", id(self)), self.vec_lift, p16, c0=self.c0_lift)
+        lifted = fused_lut(ctx, "sb-lift", self.vec_lift, p16, c0=self.c0_lift, owner=self)
         if lifted is None:
             lifted = ctx.add_plain(ctx.multiply(ct_lo, 0.0), self.c0_lift)
             for k in self.ks_lift:
@@ -224,8 +224,8 @@ class SubBytesLUTFastCached:
         bk.update({k: pos256[k - 1] for k in self.ks_union if k <= len(pos256)})
 
         def lut(pts, c0):
-            res = fused_lut(ctx, ("sb", id(self), pts is self.pt_hi), self.vec_hi if pts is self.pt_hi else self.vec_lo,
-                            bk, c0=c0)
+            res = fused_lut(ctx, ("sb", pts is self.pt_hi), self.vec_hi if pts is self.pt_hi else self.vec_lo,
+                            bk, c0=c0, owner=self)
             if res is not None:
                 return res
             res = ctx.add_plain(ctx.multiply(ct_b, 0.0), c0)

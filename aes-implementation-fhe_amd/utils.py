@@ -114,14 +114,15 @@ def conj_many(ctx, cts):
     return [ctx.conjugate(c) for c in cts]
 
 
-def fused_lut(ctx, key, coeffs, a, b=None, c0: complex = 0j):
+def fused_lut(ctx, key, coeffs, a, b=None, c0: complex = 0j, owner=None):
     """The LUT sum sum_{p,q} C[p,q] a[p] b[q] (b given) or c0 + sum_k C[k] a[k] as one engine
     call, or None when the context has no fused form or the elements sit too
-    low for it -- the caller then runs the reference's per-term product loop."""
+    low for it -- the caller then runs the reference's per-term product loop.  `owner`: the
+    module object holding the coefficients (the device set is evicted once it is collected)."""
     if not getattr(ctx, "fused_luts", False):
         return None
     try:
-        return ctx.lut_eval(ctx.lut(key, coeffs, c0), a, b)
+        return ctx.lut_eval(ctx.lut(key, coeffs, c0, owner=owner), a, b)
     except RuntimeError as e:
         if "level" in str(e):
             return None

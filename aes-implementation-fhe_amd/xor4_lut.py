@@ -145,12 +145,12 @@ class SplitLUT2:
         return eval_two(ctx, (self, key, *AB0), (self, key, *AB1))
 
     def eval(self, ctx, key, A, B):
-        s1 = fused_lut(ctx, (key, 1), self.c1, A, B)
+        s1 = fused_lut(ctx, (key, 1), self.c1, A, B, owner=self)
         if s1 is None:
             return None
         if not self.has2:
             return s1
-        s2 = fused_lut(ctx, (key, 2), self.c2, A, B)
+        s2 = fused_lut(ctx, (key, 2), self.c2, A, B, owner=self)
         return None if s2 is None else ctx.add(s1, ctx.conjugate(s2))
 
 
@@ -159,8 +159,8 @@ def eval_two(ctx, j0, j1):
     conjugations in one conj_many batch; None if a fused sum is unavailable (level)"""
     out, s2 = [], []
     for sp, key, A, B in (j0, j1):
-        s1 = fused_lut(ctx, (key, 1), sp.c1, A, B)
-        t2 = fused_lut(ctx, (key, 2), sp.c2, A, B) if sp.has2 else None
+        s1 = fused_lut(ctx, (key, 1), sp.c1, A, B, owner=sp)
+        t2 = fused_lut(ctx, (key, 2), sp.c2, A, B, owner=sp) if sp.has2 else None
         if s1 is None or (sp.has2 and t2 is None):
             return None
         out.append(s1)
@@ -203,11 +203,11 @@ class XOR4LUT:
             a_ct, b_ct = drop_to(ctx, a_ct, out_level + LUT2_DEPTH), drop_to(ctx, b_ct, out_level + LUT2_DEPTH)
         if not hasattr(self, "_split"):
             self._split = SplitLUT2(self.coeffs)
-        out = split_lut2(ctx, self._split, ("xor4", id(self)), a_ct, b_ct)
+        out = split_lut2(ctx, self._split, "xor4", a_ct, b_ct)
         if out is not None:
             return out
         A, B = pair(ctx, lambda: self._build_power_basis_16(a_ct), lambda: self._build_power_basis_16(b_ct))
-        out = fused_lut(ctx, "xor4", self.coeffs, A, B)  # one kernel for all 64 terms
+        out = fused_lut(ctx, "xor4", self.coeffs, A, B, owner=self)  # one kernel for all 64 terms
         if out is not None:
             return out
         acc = ctx.sub(A[0], A[0])
@@ -236,7 +236,7 @@ class XOR4LUT:
                 if "level" not in str(e):
                     raise
             else:
-                out = sp.eval_pair(ctx, ("xor4", id(self)), (A0, B0), (A1, B1))
+                out = sp.eval_pair(ctx, "xor4", (A0, B0), (A1, B1))
                 if out is not None:
                     return out
         return pair(ctx, lambda: self.apply(a0, b0, out_level), lambda: self.apply(a1, b1, out_level))

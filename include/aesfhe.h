@@ -109,6 +109,10 @@ int aesfhe_mul(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int relin, aes
 int aesfhe_lut_create(aesfhe_ctx* ctx, int n_a, int n_b, const double* re, const double* im, double c0_re, double c0_im,
                       aesfhe_handle* out);
 int aesfhe_lut_eval(aesfhe_ctx* ctx, aesfhe_handle lut, const aesfhe_handle* a, const aesfhe_handle* b, aesfhe_handle* out);
+/* Releases a LUT's coefficient set and every per-level device constant cached for it (the
+ * evaluator's plaintext caches, REF/lut.py:71-94 keeps them per object); fails if `lut` is not
+ * a LUT handle.  aesfhe_free also accepts LUT handles; this entry states the intent. */
+int aesfhe_lut_free(aesfhe_ctx* ctx, aesfhe_handle lut);
 /* Deferred evaluation switch, default on: API-level ct x ct products
  * leave relinearisation and their rescale to the first consumer that needs a
  * 2-polynomial canonical ciphertext (rotate, conjugate, ct x ct, power basis, bootstrap,

@@ -124,6 +124,27 @@ def test_lut_level_error_message(pair):
         E.lut_eval(lut, a, a)
 
 
+def test_lut_free(pair):
+    """aesfhe_lut_free releases a set (and its per-level constants); a freed handle is refused,
+    and so is a ciphertext handle passed as a LUT"""
+    E, O = pair
+    rng = np.random.default_rng(24)
+    top = min(O.L, 6)
+    lut = E.lut_create(np.ones(2), 0.5)
+    x = [E.import_ct(rand_ct(O, top, rng), top) for _ in range(2)]
+    out = E.lut_eval(lut, x)
+    h = lut.handle
+    E.lut_free(lut)
+    assert lut.handle == 0
+    lut.handle = h
+    with pytest.raises(RuntimeError):
+        E.lut_eval(lut, x)
+    lut.handle = 0
+    with pytest.raises(RuntimeError, match="not a LUT"):
+        E._ctx.check(E._lib.aesfhe_lut_free(E._ctx.ptr, out.handle))
+    assert out.level == top - 1  # the ciphertext is untouched
+
+
 # ---------------------------------------------------------------- module level, fused vs loop
 @pytest.fixture(scope="module")
 def coeffs(coeff_dir):

@@ -2,7 +2,7 @@
 label sets with id(), which Python reuses once an object is collected, and a stale
 coefficient set was the cause of an intermittent all-states-wrong packed run.
 CPU-only: the engine is replaced by a recorder."""
-import threading
+import gc
 
 import numpy as np
 
@@ -12,17 +12,20 @@ from engine_context import EngineContext
 class _Rec:
     def __init__(self):
         self.made = []
+        self.freed = []
 
     def lut_create(self, coeffs, c0):
         self.made.append((np.array(coeffs), c0))
         return len(self.made)
 
+    def lut_free(self, t):
+        self.freed.append(t)
+
 
 def _ctx():
     ctx = object.__new__(EngineContext)
     ctx.engine = _Rec()
-    ctx._luts = {}
-    ctx._lut_lock = threading.Lock()
+    ctx._init_lut_cache()
     return ctx
 
 
@@ -46,3 +49,47 @@ def test_cache_is_bounded_by_content():
     assert len(handles) == 1 and len(ctx._luts) == 1 and len(ctx.engine.made) == 1
     ctx.clear_luts()
     assert not ctx._luts
+
+
+class _Owner:  # a SubBytes / XOR4 module stand-in
+    pass
+
+
+def test_sets_are_evicted_when_their_owners_die():
+    """weakref.finalize on the owning module: a set is released (aesfhe_lut_free) once every
+    owner holding it is gone; a set still held by a live owner, or requested without an owner,
+    stays"""
+    ctx = _ctx()
+    a = np.arange(16, dtype=np.complex128)
+    b = a[::-1].copy()
+    c = a * 2
+    o1, o2 = _Owner(), _Owner()
+    ta = ctx.lut("sb", a, owner=o1)
+    assert ctx.lut("sb", a, owner=o2) == ta  # shared by two owners
+    tb = ctx.lut("sb", b, owner=o1)
+    tc = ctx.lut("gf", c)  # pinned
+    assert ctx.lut("gf", c, owner=o1) == tc
+    assert ctx.lut_cache_size() == 3
+    del o1
+    gc.collect()
+    assert ctx.engine.freed == [tb]  # a is still held by o2, c is pinned
+    assert ctx.lut_cache_size() == 2
+    del o2
+    gc.collect()
+    assert sorted(ctx.engine.freed) == sorted([tb, ta]) and ctx.lut_cache_size() == 1
+    # a new owner of an evicted set gets a fresh device copy
+    o3 = _Owner()
+    assert ctx.lut("sb", a, owner=o3) not in (ta, tb, tc)
+    assert len(ctx.engine.made) == 4
+
+
+def test_many_module_generations_stay_bounded():
+    """the leak the cache had: every new SubBytes object added a set that lived forever"""
+    ctx = _ctx()
+    rng = np.random.default_rng(0)
+    for _ in range(50):
+        o = _Owner()
+        ctx.lut("sb", rng.standard_normal(8).astype(np.complex128), owner=o)
+        del o
+        gc.collect()
+    assert ctx.lut_cache_size() == 0 and len(ctx.engine.freed) == 50
