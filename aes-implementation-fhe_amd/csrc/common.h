@@ -48,6 +48,41 @@ HD u32 barrett_mul(u32 a, u32 b, u32 q, u32 mu) {
 }
 HD u32 barrett_pre(u32 q) { return (u32)((1ull << 61) / q); }
 
+// ---------------------------------------------------------------------------------
+// Randomness: ChaCha20 (Bernstein 2008; 20 rounds, 64-bit block counter and
+// 64-bit nonce) as a counter-mode PRF.  A sample is the first 64 bits of the block with
+// key = the context's 256-bit key, counter = the sample index, nonce = the stream id (what is
+// sampled: secret, pk, key-switch key g/digit, encryption counter, ...); every coefficient is
+// an independent block, so any thread computes its own sample with no state.
+// ---------------------------------------------------------------------------------
+struct PrngKey {
+    u32 w[8];
+};
+HD u32 rotl32(u32 x, int r) { return (x << r) | (x >> (32 - r)); }
+HD void chacha_qr(u32& a, u32& b, u32& c, u32& d) {
+    a += b; d ^= a; d = rotl32(d, 16);
+    c += d; b ^= c; b = rotl32(b, 12);
+    a += b; d ^= a; d = rotl32(d, 8);
+    c += d; b ^= c; b = rotl32(b, 7);
+}
+HD u64 chacha_u64(const PrngKey& k, u64 stream, u64 ctr) {
+    u32 x[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, k.w[0], k.w[1], k.w[2], k.w[3],
+                 k.w[4],      k.w[5],      k.w[6],      k.w[7],      (u32)ctr, (u32)(ctr >> 32), (u32)stream,
+                 (u32)(stream >> 32)};
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        chacha_qr(x[0], x[4], x[8], x[12]);
+        chacha_qr(x[1], x[5], x[9], x[13]);
+        chacha_qr(x[2], x[6], x[10], x[14]);
+        chacha_qr(x[3], x[7], x[11], x[15]);
+        chacha_qr(x[0], x[5], x[10], x[15]);
+        chacha_qr(x[1], x[6], x[11], x[12]);
+        chacha_qr(x[2], x[7], x[8], x[13]);
+        chacha_qr(x[3], x[4], x[9], x[14]);
+    }
+    return (u64)(x[0] + 0x61707865u) | ((u64)(x[1] + 0x3320646eu) << 32);
+}
+
 // reduce a 64-bit accumulator (x < 2^61) with the Barrett constant
 HD u32 barrett_reduce64(u64 x, u32 q, u32 mu) {
     u32 lo = (u32)x, hi = (u32)(x >> 32);

@@ -38,18 +38,11 @@ namespace {
 
 inline u64 stream_id(u64 kind, u64 a, u64 b) { return (kind << 56) | (a << 16) | b; }
 
-// host copy of the counter-based PRNG of kernels.hip
-inline u64 hmix64(u64 z) {
-    z ^= z >> 30;
-    z *= 0xbf58476d1ce4e5b9ULL;
-    z ^= z >> 27;
-    z *= 0x94d049bb133111ebULL;
-    z ^= z >> 31;
-    return z;
-}
-inline u64 hprng(u64 seed, u64 stream, u64 ctr) {
-    const u64 k = hmix64(seed ^ hmix64(stream + 0x9E3779B97F4A7C15ULL));
-    return hmix64(k + (ctr + 1) * 0x9E3779B97F4A7C15ULL);
+// 256-bit key of a 64-bit seed (test / parity contexts): the seed in key words 0, 1
+inline void seed_key(u64 seed, u32 key[8]) {
+    for (int i = 0; i < 8; ++i) key[i] = 0;
+    key[0] = (u32)seed;
+    key[1] = (u32)(seed >> 32);
 }
 
 // ---------------------------------------------------------------------------------
@@ -134,8 +127,13 @@ enum Counter { C_MUL, C_RELIN, C_ROT, C_CONJ, C_PTMUL, C_SCALAR, C_RESCALE, C_NT
 class Engine {
 public:
     static constexpr int kStreams = 3;  // see fork() / join()
-    Engine(int logn, int L1, int n_double, int dnum, int device, u64 seed) : emb_(logn) {
-        std::string err = hp_.build(logn, L1, n_double, dnum, seed);
+    PrngKey pkey() const {
+        PrngKey k;
+        for (int i = 0; i < 8; ++i) k.w[i] = hp_.key[i];
+        return k;
+    }
+    Engine(int logn, int L1, int n_double, int dnum, int device, const u32 key[8]) : emb_(logn) {
+        std::string err = hp_.build(logn, L1, n_double, dnum, key);
         if (!err.empty()) throw std::runtime_error(err);
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
@@ -318,15 +316,15 @@ public:
         const int n = hp_.n, nt = hp_.n_tot();
         if (!d_s_) {
             d_s_ = dev_alloc((size_t)nt * n);
-            launch_sample_small(S(), T_, d_s_, nt, qmap(), hp_.seed, stream_id(1, 0, 0), 0);
+            launch_sample_small(S(), T_, d_s_, nt, qmap(), pkey(), stream_id(1, 0, 0), 0);
             ntt(d_s_, nt, nt, qmap());
         }
         if (!d_pk_) {
             const int nq = hp_.n_q;
             d_pk_ = dev_alloc((size_t)2 * nq * n);
             u32* e = tmp(nq);
-            launch_sample_uniform(S(), T_, d_pk_ + (size_t)nq * n, nq, qmap(), hp_.seed, stream_id(2, 0, 0));
-            launch_sample_small(S(), T_, e, nq, qmap(), hp_.seed, stream_id(3, 0, 0), 1);
+            launch_sample_uniform(S(), T_, d_pk_ + (size_t)nq * n, nq, qmap(), pkey(), stream_id(2, 0, 0));
+            launch_sample_small(S(), T_, e, nq, qmap(), pkey(), stream_id(3, 0, 0), 1);
             ntt(e, nq, nq, qmap());
             launch_keygen_combine(S(), T_, d_pk_, d_pk_ + (size_t)nq * n, d_s_, e, nullptr, nullptr, nq, qmap(), 0, 0);
             untmp(e, nq);
@@ -373,8 +371,8 @@ public:
         u32* a = b + (size_t)ne * n;
         const LimbMap em = extmap(kD2sQ);  // rows 0, 1: q0, q1; then the first special primes
         u32* e = tmp(ne);
-        launch_sample_uniform(S(), T_, a, ne, em, hp_.seed, stream_id(4, g, 0));
-        launch_sample_small(S(), T_, e, ne, em, hp_.seed, stream_id(5, g, 0), 1);
+        launch_sample_uniform(S(), T_, a, ne, em, pkey(), stream_id(4, g, 0));
+        launch_sample_small(S(), T_, e, ne, em, pkey(), stream_id(5, g, 0), 1);
         ntt(e, ne, ne, em);
         // b = -a s_sp + e + (P' mod q_t) s on the q0, q1 rows
         launch_keygen_combine(S(), T_, b, a, sparse_secret(), e, d_s_, d_d2s_ + d2s_off_.gad, ne, em, 0, kD2sQ);
@@ -407,8 +405,8 @@ public:
         for (int j = 0; j < hp_.dnum; ++j) {
             u32* b = key + (size_t)j * 2 * nkey * n;
             u32* a = b + (size_t)nkey * n;
-            launch_sample_uniform(S(), T_, a, nkey, em, hp_.seed, stream_id(4, g, j));
-            launch_sample_small(S(), T_, e, nkey, em, hp_.seed, stream_id(5, g, j), 1);
+            launch_sample_uniform(S(), T_, a, nkey, em, pkey(), stream_id(4, g, j));
+            launch_sample_small(S(), T_, e, nkey, em, pkey(), stream_id(5, g, j), 1);
             ntt(e, nkey, nkey, em);
             const int lo = j * hp_.alpha, hi = std::min(nks, lo + hp_.alpha);
             launch_keygen_combine(S(), T_, b, a, target, e, sp, d_gadget_, nkey, em, lo, hi);
@@ -475,9 +473,9 @@ public:
         u32* v = tmp(nq);
         u32* e = tmp(2 * nq);
         const u64 ctr = enc_ctr_++;
-        launch_sample_small(S(), T_, v, nq, qmap(), hp_.seed, stream_id(6, 0, ctr), 0);
-        launch_sample_small(S(), T_, e, nq, qmap(), hp_.seed, stream_id(7, 0, ctr), 1);
-        launch_sample_small(S(), T_, e + (size_t)nq * n, nq, qmap(), hp_.seed, stream_id(8, 0, ctr), 1);
+        launch_sample_small(S(), T_, v, nq, qmap(), pkey(), stream_id(6, 0, ctr), 0);
+        launch_sample_small(S(), T_, e, nq, qmap(), pkey(), stream_id(7, 0, ctr), 1);
+        launch_sample_small(S(), T_, e + (size_t)nq * n, nq, qmap(), pkey(), stream_id(8, 0, ctr), 1);
         ntt(v, nq, nq, qmap());
         ntt(e, 2 * nq, nq, qmap());
         Ct top = alloc_ct(L + 1, 2);
@@ -1823,7 +1821,7 @@ public:
         std::vector<int> s(hp_.n, 0);
         int cnt = 0;
         for (u64 ctr = 0; cnt < kSparseH; ++ctr) {
-            const u64 r = hprng(hp_.seed, stream_id(9, 0, 0), ctr);
+            const u64 r = chacha_u64(pkey(), stream_id(9, 0, 0), ctr);
             const u64 pos = r % (u64)hp_.n;
             if (s[pos] == 0) {
                 s[pos] = (r >> 63) ? -1 : 1;
@@ -2912,32 +2910,39 @@ static thread_local std::string t_err;
 
 extern "C" {
 
-int aesfhe_create(aesfhe_ctx** out, int log_n, int max_level, int dnum, int device_id, uint64_t seed) {
+static int create_keyed(aesfhe_ctx** out, int log_n, int max_level, int dnum, int device_id, const u32 key[8], int boot) {
     *out = nullptr;
     auto* c = new aesfhe_ctx();
+    *out = c;
     try {
-        c->eng.reset(new Engine(log_n, max_level, 0, dnum, device_id, seed));
+        if (boot) {
+            const int L1 = max_level + Engine::kBootStc - 1;
+            c->eng.reset(new Engine(log_n, L1, Engine::boot_double_levels(), dnum, device_id, key));
+            c->eng->set_fresh(max_level);
+        } else {
+            c->eng.reset(new Engine(log_n, max_level, 0, dnum, device_id, key));
+        }
     } catch (const std::exception& e) {
         t_err = e.what();
-        *out = c;
         return -1;
     }
-    *out = c;
     return 0;
 }
+int aesfhe_create(aesfhe_ctx** out, int log_n, int max_level, int dnum, int device_id, uint64_t seed) {
+    u32 key[8];
+    seed_key(seed, key);
+    return create_keyed(out, log_n, max_level, dnum, device_id, key, 0);
+}
 int aesfhe_create_boot(aesfhe_ctx** out, int log_n, int fresh_level, int dnum, int device_id, uint64_t seed) {
-    *out = nullptr;
-    auto* c = new aesfhe_ctx();
-    *out = c;
-    try {
-        const int L1 = fresh_level + Engine::kBootStc - 1;
-        c->eng.reset(new Engine(log_n, L1, Engine::boot_double_levels(), dnum, device_id, seed));
-        c->eng->set_fresh(fresh_level);
-    } catch (const std::exception& e) {
-        t_err = e.what();
-        return -1;
-    }
-    return 0;
+    u32 key[8];
+    seed_key(seed, key);
+    return create_keyed(out, log_n, fresh_level, dnum, device_id, key, 1);
+}
+int aesfhe_create_keyed(aesfhe_ctx** out, int log_n, int max_level, int dnum, int device_id, const uint8_t* key, int bootstrappable) {
+    u32 k[8];
+    for (int i = 0; i < 8; ++i)
+        k[i] = (u32)key[4 * i] | ((u32)key[4 * i + 1] << 8) | ((u32)key[4 * i + 2] << 16) | ((u32)key[4 * i + 3] << 24);
+    return create_keyed(out, log_n, max_level, dnum, device_id, k, bootstrappable);
 }
 int aesfhe_level_limbs(aesfhe_ctx* ctx, int32_t* out) {
     API_BEGIN const HostParams& p = ctx->eng->hp();

@@ -248,9 +248,9 @@ void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int
 
 // --- sampling --------------------------------------------------------
 // kind: 0 ternary, 1 centred binomial (eta = 21); writes value mod prime into nl rows
-void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, u64 seed, u64 stream, int kind);
+void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, const PrngKey& key, u64 stream, int kind);
 // uniform residues: row l gets prng(seed, stream, prime(l) * N + k) mod q
-void launch_sample_uniform(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, u64 seed, u64 stream);
+void launch_sample_uniform(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, const PrngKey& key, u64 stream);
 // b = -a*s + e (+ gadget*s' on rows with flag) : used by key generation
 void launch_keygen_combine(hipStream_t st, const DevTables& T, u32* b, const u32* a, const u32* s, const u32* e, const u32* sp,
                            const u32* gadget, int nl, LimbMap map, int gadget_lo, int gadget_hi);

@@ -13,13 +13,6 @@ namespace {
 
 constexpr int kBlock = 256;
 
-__device__ __forceinline__ u64 mix64(u64 z) {
-    z ^= z >> 30; z *= 0xbf58476d1ce4e5b9ULL;
-    z ^= z >> 27; z *= 0x94d049bb133111ebULL;
-    z ^= z >> 31; return z;
-}
-__device__ __forceinline__ u64 prng_key(u64 seed, u64 stream) { return mix64(seed ^ mix64(stream + 0x9E3779B97F4A7C15ULL)); }
-__device__ __forceinline__ u64 prng_at(u64 key, u64 ctr) { return mix64(key + (ctr + 1) * 0x9E3779B97F4A7C15ULL); }
 
 // ------------------------------------------------------------------------------------
 // element-wise kernels: one thread per coefficient, rows on blockIdx.y
@@ -362,9 +355,9 @@ __global__ void __launch_bounds__(kBlock) k_key_inner(u32* acc, const u32* ext, 
 // ------------------------------------------------------------------------------------
 // sampling and key generation
 // ------------------------------------------------------------------------------------
-__global__ void k_sample_small(u32* out, int nl, LimbMap map, u64 seed, u64 stream, int kind, const PrimeConst* pc, int logn) {
+__global__ void k_sample_small(u32* out, int nl, LimbMap map, PrngKey key, u64 stream, int kind, const PrimeConst* pc, int logn) {
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    const u64 r = prng_at(prng_key(seed, stream), k);
+    const u64 r = chacha_u64(key, stream, k);
     int v;
     if (kind == 0) v = (int)(r % 3) - 1;
     else v = __popcll(r & 0x1FFFFFull) - __popcll((r >> 21) & 0x1FFFFFull);
@@ -373,13 +366,12 @@ __global__ void k_sample_small(u32* out, int nl, LimbMap map, u64 seed, u64 stre
         out[((size_t)l << logn) + k] = v >= 0 ? (u32)v : q - (u32)(-v);
     }
 }
-__global__ void k_sample_uniform(u32* out, int nl, LimbMap map, u64 seed, u64 stream, const PrimeConst* pc, int logn) {
+__global__ void k_sample_uniform(u32* out, int nl, LimbMap map, PrngKey key, u64 stream, const PrimeConst* pc, int logn) {
     const int l = blockIdx.y;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const int prime = map.prime(l);
-    const u64 key = prng_key(seed, stream);
     const u32 q = pc[prime].q;
-    out[((size_t)l << logn) + k] = (u32)(prng_at(key, ((u64)prime << logn) + k) % q);
+    out[((size_t)l << logn) + k] = (u32)(chacha_u64(key, stream, ((u64)prime << logn) + k) % q);
 }
 __global__ void k_keygen_combine(u32* b, const u32* a, const u32* s, const u32* e, const u32* sp, const u32* gadget, int nl,
                                  LimbMap map, int glo, int ghi, const PrimeConst* pc, int logn) {
@@ -1001,12 +993,12 @@ void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* e
         prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<4>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g,
                        map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum);
 }
-void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, u64 seed, u64 stream, int kind) {
-    prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_small, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, nl, map, seed, stream, kind, T.pc,
+void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, const PrngKey& key, u64 stream, int kind) {
+    prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_small, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, nl, map, key, stream, kind, T.pc,
                        T.logn);
 }
-void launch_sample_uniform(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, u64 seed, u64 stream) {
-    prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_uniform, ew_grid(T.logn, nl), dim3(kBlock), 0, st, out, nl, map, seed, stream, T.pc, T.logn);
+void launch_sample_uniform(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, const PrngKey& key, u64 stream) {
+    prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_uniform, ew_grid(T.logn, nl), dim3(kBlock), 0, st, out, nl, map, key, stream, T.pc, T.logn);
 }
 void launch_keygen_combine(hipStream_t st, const DevTables& T, u32* b, const u32* a, const u32* s, const u32* e, const u32* sp,
                            const u32* gadget, int nl, LimbMap map, int glo, int ghi) {

@@ -54,11 +54,12 @@ static u32 root_2n(u32 q, int logn) {
 
 bool HostParams::homogeneous(int level) const { return !(L > L1 && level == L1 + 1); }
 
-std::string HostParams::build(int logn_, int L1_, int n_double, int dnum_, uint64_t seed_) {
+std::string HostParams::build(int logn_, int L1_, int n_double, int dnum_, const uint32_t key_[8]) {
     if (logn_ < 13 || logn_ > 16) return "log_n must lie in [13, 16] (NTT kernels, ntt.hip)";
     if (L1_ < 1 || L1_ > 60 || n_double < 0 || n_double > 30) return "max_level must lie in [1, 60]";
     if (dnum_ < 1) return "dnum must be >= 1";
-    logn = logn_; n = 1 << logn; L1 = L1_; L = L1 + n_double; dnum = dnum_; seed = seed_;
+    logn = logn_; n = 1 << logn; L1 = L1_; L = L1 + n_double; dnum = dnum_;
+    for (int i = 0; i < 8; ++i) key[i] = key_[i];
     nl_of.assign(L + 3, 0);
     nl_of[0] = 1;  // level -1: q0 only
     for (int l = 0; l <= L; ++l) nl_of[l + 1] = l <= L1 ? l + 2 : L1 + 2 + 2 * (l - L1);

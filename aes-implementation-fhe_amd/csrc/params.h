@@ -22,7 +22,7 @@ struct HostParams {
     int n_ks = 19;     // limbs reachable by key switching
     int n_p = 8;       // special primes (alpha + 1)
     int fresh = 17;    // level of fresh encryptions (<= L1)
-    uint64_t seed = 0;
+    uint32_t key[8] = {};  // 256-bit ChaCha20 key of the context's randomness
 
     std::vector<u32> mod;        // n_q + n_p primes
     std::vector<double> delta;   // delta[l], l = 0..L
@@ -38,7 +38,7 @@ struct HostParams {
     bool homogeneous(int level) const;
 
     // builds the prime chain and scales; returns "" or an error message
-    std::string build(int logn, int L1, int n_double, int dnum, uint64_t seed);
+    std::string build(int logn, int L1, int n_double, int dnum, const uint32_t key[8]);
 };
 
 // host modular helpers (64-bit, used for table generation only)

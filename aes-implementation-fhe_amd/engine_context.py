@@ -27,7 +27,7 @@ _SIG_DEFAULT_LEVEL = 17
 class EngineContext:
     def __init__(self, signature: int, *, max_level: int = 17, use_bootstrap: bool = True,
                  use_multiparty: bool = False, mode: str = "cpu", device_id: int = 0,
-                 thread_count: int | None = None, log_n: int = 16, dnum: int | None = None, seed: int | None = None,
+                 thread_count: int | None = None, log_n: int = 16, dnum: int | None = None, seed: int | bytes | None = None,
                  lazy: bool = True, concurrent: bool = True, fused_luts: bool = True, allow_insecure: bool = False):
         # REF/engine_context.py:17-42: signature selects the engine constructor form
         if signature == 1:

@@ -41,7 +41,7 @@ EXPORTED = [
     "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
     "aesfhe_streams", "aesfhe_bind_stream", "aesfhe_fork", "aesfhe_join", "aesfhe_settle",
     "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_kernel_work", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan",
-    "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot",
+    "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot", "aesfhe_create_keyed",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_lut_create", "aesfhe_lut_eval", "aesfhe_lut_free",
     "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled",
 ]
@@ -117,6 +117,7 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_boot_info"] = [vp, _dp]
     sig["aesfhe_debug_lin_group"] = [vp, _H, c_int, _Hp]
     sig["aesfhe_create_boot"] = [pp, c_int, c_int, c_int, c_int, ctypes.c_uint64]
+    sig["aesfhe_create_keyed"] = [pp, c_int, c_int, c_int, c_int, ctypes.c_char_p, c_int]
     sig["aesfhe_lut_create"] = [vp, c_int, c_int, _dp, _dp, c_dbl, c_dbl, _Hp]
     sig["aesfhe_lut_eval"] = [vp, _H, _Hp, _Hp, _Hp]
     sig["aesfhe_lut_free"] = [vp, _H]
@@ -135,8 +136,14 @@ class _Context:
     def __init__(self, log_n, max_level, dnum, device_id, seed, bootstrappable=False):
         self.lib = load_library()
         ptr = ctypes.c_void_p()
-        create = self.lib.aesfhe_create_boot if bootstrappable else self.lib.aesfhe_create
-        rc = create(ctypes.byref(ptr), log_n, max_level, dnum, device_id, seed)
+        if isinstance(seed, (bytes, bytearray)):  # the full 256-bit ChaCha20 key
+            if len(seed) != 32:
+                raise ValueError("a key must be 32 bytes")
+            rc = self.lib.aesfhe_create_keyed(ctypes.byref(ptr), log_n, max_level, dnum, device_id, bytes(seed),
+                                              int(bootstrappable))
+        else:
+            create = self.lib.aesfhe_create_boot if bootstrappable else self.lib.aesfhe_create
+            rc = create(ctypes.byref(ptr), log_n, max_level, dnum, device_id, seed)
         self.ptr = ptr
         if rc != 0:
             msg = self.lib.aesfhe_last_error(ptr).decode() if ptr.value else "aesfhe_create failed"
@@ -268,12 +275,13 @@ class Engine:
         # ~5 % more time (more ModUp rows per key switch)
         if dnum is None:
             dnum = int(os.environ.get("AESFHE_BOOT_DNUM", "5")) if use_bootstrap else 3
-        # key material and encryption randomness derive from `seed`: drawn from
-        # the OS entropy source unless the caller pins it (parity tests, smoke, multi-rank runs
-        # that broadcast one seed so every rank holds the same keys)
+        # key material and encryption randomness are ChaCha20 blocks under a 256-bit key
+        # (DESIGN.md §3.4): 32 bytes from the OS entropy source unless the caller pins it -- an
+        # int seed (parity tests, smoke: key words 0-1) or a 32-byte key (multi-rank runs that
+        # broadcast one key so every rank holds the same key set)
         if seed is None:
-            seed = int.from_bytes(os.urandom(8), "little")
-        self.seed = int(seed) & 0xFFFFFFFFFFFFFFFF
+            seed = os.urandom(32)
+        self.seed = bytes(seed) if isinstance(seed, (bytes, bytearray)) else int(seed) & 0xFFFFFFFFFFFFFFFF
         self._ctx = _Context(log_n, max_level, dnum, device_id, self.seed, bootstrappable=use_bootstrap)
         L = self._ctx.lib
         self.fresh_level = max_level

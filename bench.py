@@ -104,20 +104,22 @@ def dist_setup(want: int):
     return 0, 1, 0, None
 
 
-def shared_seed(dist, seed: int | None) -> int:
-    """One key set for the whole job: rank 0 draws the seed (or takes --seed)
-    and broadcasts it once, before any timed region; every rank then derives identical keys.
-    This is the only collective outside the timing barriers and the max-over-ranks."""
-    if seed is None:
-        seed = int.from_bytes(os.urandom(8), "little") >> 1  # int64-safe
-    if dist is None:
+def shared_seed(dist, seed: int | None):
+    """One key set for the whole job: rank 0 draws a 256-bit ChaCha20 key from
+    os.urandom (or takes the integer --seed) and broadcasts it once, before any timed region;
+    every rank then derives identical keys.  This is the only collective outside the timing
+    barriers and the max-over-ranks.  Returns the 32-byte key, or the int seed if one was given."""
+    if seed is not None:
         return int(seed)
+    key = os.urandom(32)
+    if dist is None:
+        return key
     import torch
     gpu = dist.get_backend() == "nccl"
     dev = torch.device("cuda", torch.cuda.current_device()) if gpu else torch.device("cpu")
-    t = torch.tensor([seed], dtype=torch.int64, device=dev)
+    t = torch.tensor(list(key), dtype=torch.uint8, device=dev)
     dist.broadcast(t, src=0)
-    return int(t.item())
+    return bytes(t.cpu().tolist())
 
 
 def all_gather_ints(dist, vals):
@@ -304,7 +306,7 @@ def dry_run(args, rank, world, dist):
     from state_encoder import StateEncoder
     from xor4_lut import XOR4LUT
     seed = shared_seed(dist, args.seed)
-    ctx = OracleContext(log_n=13, max_level=6, seed=seed & 0x7FFFFFFF)
+    ctx = OracleContext(log_n=13, max_level=6, seed=seed)
     enc = StateEncoder(ctx)
     ark = AddRoundKey(XOR4LUT(ctx, default_xor4_coeffs()))
     np.random.seed(7)

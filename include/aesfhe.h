@@ -37,6 +37,13 @@ int aesfhe_create(aesfhe_ctx** out, int log_n, int max_level, int dnum, int devi
 /* bootstrappable parameter set: fresh ciphertexts at fresh_level, the chain extended by
  * aesfhe_bootstrap_depth() levels (CoeffToSlot/EvalMod on double-prime levels) */
 int aesfhe_create_boot(aesfhe_ctx** out, int log_n, int fresh_level, int dnum, int device_id, uint64_t seed);
+/* Randomness: every key and encryption sample is a ChaCha20 block under a 256-bit context key
+ * (DESIGN.md §3.4).  aesfhe_create / aesfhe_create_boot take a 64-bit seed as key words 0-1
+ * (reproducible test and parity contexts); aesfhe_create_keyed takes the full 32-byte key
+ * (little-endian words; the Python Engine draws it from os.urandom unless a seed is given).
+ * bootstrappable != 0: max_level is the fresh level of a bootstrappable set (aesfhe_create_boot). */
+int aesfhe_create_keyed(aesfhe_ctx** out, int log_n, int max_level, int dnum, int device_id, const uint8_t* key,
+                        int bootstrappable);
 /* limbs per level 0..max_level (a ciphertext at level l has npoly x limbs[l] x N words) */
 int aesfhe_level_limbs(aesfhe_ctx* ctx, int32_t* out);
 int aesfhe_destroy(aesfhe_ctx* ctx);

@@ -48,6 +48,8 @@ def lib():
         "orc_rescale2": (None, [vp, c_int, c_int, u32p, u32p]),
         "orc_keyswitch_d2s": (None, [vp, c_int, u32p, u32p, u32p]),
         "orc_destroy": (None, [vp]),
+        "orc_set_key": (None, [vp, ctypes.c_char_p]),
+        "orc_chacha_block": (None, [u32p, c_u64, c_u64, u32p]),
         "orc_info": (None, [vp, i32p]),
         "orc_moduli": (None, [vp, u32p]),
         "orc_deltas": (None, [vp, f64p]),
@@ -80,15 +82,22 @@ def lib():
 class OracleParams:
     """Parameter set + raw primitives."""
 
-    def __init__(self, log_n: int = 16, max_level: int = 17, dnum: int = 3, seed: int = 0, boot_double: int = 0):
+    def __init__(self, log_n: int = 16, max_level: int = 17, dnum: int = 3, seed: int | bytes = 0, boot_double: int = 0):
         """boot_double > 0: the bootstrappable chain (params.cpp), single-prime levels 0..max_level
-        and boot_double double-prime levels above (top level max_level + boot_double)"""
+        and boot_double double-prime levels above (top level max_level + boot_double).
+        seed: an int (ChaCha20 key words 0-1, aesfhe_create) or the 32-byte key (aesfhe_create_keyed)"""
         self._L = lib()
         self.L1 = max_level
+        key = bytes(seed) if isinstance(seed, (bytes, bytearray)) else None
+        if key is not None and len(key) != 32:
+            raise ValueError("a key must be 32 bytes")
+        s = 0 if key is not None else int(seed) & 0xFFFFFFFFFFFFFFFF
         if boot_double:
-            self.h = self._L.orc_create_boot(log_n, max_level, boot_double, dnum, seed)
+            self.h = self._L.orc_create_boot(log_n, max_level, boot_double, dnum, s)
         else:
-            self.h = self._L.orc_create(log_n, max_level, dnum, seed)
+            self.h = self._L.orc_create(log_n, max_level, dnum, s)
+        if key is not None:
+            self._L.orc_set_key(self.h, key)
         info = np.zeros(8, np.int32)
         self._L.orc_info(self.h, info)
         self.n, self.L, self.n_q, self.n_ks, self.n_p, self.alpha, self.dnum, self.log_n = map(int, info)
@@ -249,7 +258,7 @@ class OracleEngine:
     REF/engine_context.py:56-204).  Same conventions as the HIP engine
      so that levels, scales and key streams coincide."""
 
-    def __init__(self, log_n: int = 16, max_level: int = 17, dnum: int = 3, seed: int = 0, fresh_level: int | None = None):
+    def __init__(self, log_n: int = 16, max_level: int = 17, dnum: int = 3, seed: int | bytes = 0, fresh_level: int | None = None):
         self.p = OracleParams(log_n, max_level, dnum, seed)
         self.fresh = self.p.L if fresh_level is None else fresh_level
         self.slot_count = self.p.slot_count
@@ -387,7 +396,7 @@ class OracleContext:
     """EngineContext surface (REF/engine_context.py:56-204) over OracleEngine, so the
     build's AES modules can run on the CPU oracle (tests, cpu_baseline)."""
 
-    def __init__(self, log_n: int = 16, max_level: int = 17, dnum: int = 3, seed: int = 0):
+    def __init__(self, log_n: int = 16, max_level: int = 17, dnum: int = 3, seed: int | bytes = 0):
         self.eng = OracleEngine(log_n, max_level, dnum, seed)
         self.engine = _EngineView(self.eng.slot_count)
 
@@ -460,3 +469,10 @@ class OracleContext:
 
     def to_ntt(self, ct):
         return ct
+
+
+def chacha_block(key_words, ctr: int, nonce: int) -> np.ndarray:
+    """the oracle's ChaCha20 block function (16 output words; tests pin it to RFC 8439 2.3.2)"""
+    out = np.zeros(16, np.uint32)
+    lib().orc_chacha_block(np.ascontiguousarray(key_words, np.uint32), int(ctr), int(nonce), out)
+    return out

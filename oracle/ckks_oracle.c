@@ -45,7 +45,7 @@ typedef struct {
     u32 **psi_rev, **ipsi_rev;
     u32 *ninv;
     double *delta; /* delta[l], l = 0..L */
-    u64 seed;
+    u32 key[8];    /* ChaCha20 key of all sampling */
     int L1;        /* top of the single-prime region (== L without the bootstrapping region) */
 } orc_t;
 
@@ -101,16 +101,43 @@ static u32 find_psi(u32 q, int logn) {
 }
 
 /* ------------------------------------------------------------------ */
-/* PRNG: splitmix64 finaliser, counter based          */
+/* PRNG: ChaCha20 block function (Bernstein 2008: 20   */
+/* rounds, words 12-13 a 64-bit block counter, 14-15 a 64-bit nonce) as */
+/* a PRF; a sample = the first 64 bits of block(key, ctr, stream)       */
 /* ------------------------------------------------------------------ */
-static u64 mix64(u64 z) {
-    z ^= z >> 30; z *= 0xbf58476d1ce4e5b9ULL;
-    z ^= z >> 27; z *= 0x94d049bb133111ebULL;
-    z ^= z >> 31; return z;
+#define ROTL32(x, r) (((x) << (r)) | ((x) >> (32 - (r))))
+#define QR(a, b, c, d)                          \
+    a += b; d ^= a; d = ROTL32(d, 16);          \
+    c += d; b ^= c; b = ROTL32(b, 12);          \
+    a += b; d ^= a; d = ROTL32(d, 8);           \
+    c += d; b ^= c; b = ROTL32(b, 7);
+void orc_chacha_block(const u32 *key, u64 ctr, u64 nonce, u32 *out) {
+    static const u32 sigma[4] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u};
+    u32 in[16], x[16];
+    for (int i = 0; i < 4; i++) in[i] = sigma[i];
+    for (int i = 0; i < 8; i++) in[4 + i] = key[i];
+    in[12] = (u32)ctr; in[13] = (u32)(ctr >> 32); in[14] = (u32)nonce; in[15] = (u32)(nonce >> 32);
+    memcpy(x, in, sizeof(x));
+    for (int r = 0; r < 10; r++) {
+        QR(x[0], x[4], x[8], x[12]) QR(x[1], x[5], x[9], x[13]) QR(x[2], x[6], x[10], x[14]) QR(x[3], x[7], x[11], x[15])
+        QR(x[0], x[5], x[10], x[15]) QR(x[1], x[6], x[11], x[12]) QR(x[2], x[7], x[8], x[13]) QR(x[3], x[4], x[9], x[14])
+    }
+    for (int i = 0; i < 16; i++) out[i] = x[i] + in[i];
 }
-static u64 prng(u64 seed, u64 stream, u64 ctr) {
-    u64 k = mix64(seed ^ mix64(stream + 0x9E3779B97F4A7C15ULL));
-    return mix64(k + (ctr + 1) * 0x9E3779B97F4A7C15ULL);
+static u64 prng(const u32 *key, u64 stream, u64 ctr) {
+    u32 b[16];
+    orc_chacha_block(key, ctr, stream, b);
+    return (u64)b[0] | ((u64)b[1] << 32);
+}
+static void seed_key(orc_t *o, u64 seed) {
+    memset(o->key, 0, sizeof(o->key));
+    o->key[0] = (u32)seed; o->key[1] = (u32)(seed >> 32);
+}
+/* the full 256-bit key (32 bytes, little-endian words; aesfhe_create_keyed) */
+void orc_set_key(void *h, const unsigned char *k) {
+    orc_t *o = (orc_t *)h;
+    for (int i = 0; i < 8; i++)
+        o->key[i] = (u32)k[4 * i] | ((u32)k[4 * i + 1] << 8) | ((u32)k[4 * i + 2] << 16) | ((u32)k[4 * i + 3] << 24);
 }
 #define STREAM(kind, a, b) (((u64)(kind) << 56) | ((u64)(a) << 16) | (u64)(b))
 static int ternary(u64 r) { return (int)(r % 3) - 1; }
@@ -129,7 +156,7 @@ static int prime_used(const u32 *list, int cnt, u32 p) {
 
 void *orc_create(int logn, int L, int dnum, u64 seed) {
     orc_t *o = (orc_t *)calloc(1, sizeof(orc_t));
-    o->logn = logn; o->n = 1 << logn; o->L = L; o->dnum = dnum; o->seed = seed; o->L1 = L;
+    o->logn = logn; o->n = 1 << logn; o->L = L; o->dnum = dnum; seed_key(o, seed); o->L1 = L;
     o->n_q = L + 3; o->n_ks = L + 2;
     o->alpha = (o->n_ks + dnum - 1) / dnum;
     o->n_p = o->alpha + 1; /* P exceeds every digit modulus by one prime */
@@ -218,7 +245,7 @@ static u32 closest_prime(u32 *used, int *nused, u64 twon, double want) {
 void *orc_create_boot(int logn, int L1, int n_double, int dnum, u64 seed) {
     orc_t *o = (orc_t *)calloc(1, sizeof(orc_t));
     int L = L1 + n_double;
-    o->logn = logn; o->n = 1 << logn; o->L = L; o->L1 = L1; o->dnum = dnum; o->seed = seed;
+    o->logn = logn; o->n = 1 << logn; o->L = L; o->L1 = L1; o->dnum = dnum; seed_key(o, seed);
     o->n_ks = NL(o, L); o->n_q = o->n_ks + 1;
     o->alpha = (o->n_ks + dnum - 1) / dnum;
     o->n_p = o->alpha + 1;
@@ -420,7 +447,7 @@ void orc_encode(void *h, const double *zre, const double *zim, double scale, int
 /* ------------------------------------------------------------------ */
 void orc_secret(void *h, int *s_out) {
     orc_t *o = (orc_t *)h;
-    for (int k = 0; k < o->n; k++) s_out[k] = ternary(prng(o->seed, STREAM(1, 0, 0), (u64)k));
+    for (int k = 0; k < o->n; k++) s_out[k] = ternary(prng(o->key, STREAM(1, 0, 0), (u64)k));
 }
 
 /* small signed polynomial -> NTT form on global limb ids */
@@ -447,7 +474,7 @@ void orc_secret_ntt(void *h, u32 *out) {
 }
 
 static void cbd_poly(const orc_t *o, u64 stream, int *c) {
-    for (int k = 0; k < o->n; k++) c[k] = cbd21(prng(o->seed, stream, (u64)k));
+    for (int k = 0; k < o->n; k++) c[k] = cbd21(prng(o->key, stream, (u64)k));
 }
 
 /* public key (b, a) over Q limbs 0..n_q-1: b = -a*s + e */
@@ -464,7 +491,7 @@ void orc_gen_pk(void *h, u32 *out) {
     for (int i = 0; i < nq; i++) {
         u32 q = o->mod[i];
         for (int k = 0; k < n; k++) {
-            u32 av = (u32)(prng(o->seed, STREAM(2, 0, 0), (u64)i * n + k) % q);
+            u32 av = (u32)(prng(o->key, STREAM(2, 0, 0), (u64)i * n + k) % q);
             a[(size_t)i * n + k] = av;
             b[(size_t)i * n + k] = subm(b[(size_t)i * n + k], mulm(av, s[(size_t)i * n + k], q), q);
         }
@@ -520,7 +547,7 @@ void orc_gen_ksk(void *h, u64 g, u32 *out) {
             for (int k = 0; k < o->n_p; k++) pmod = mulm(pmod, o->mod[o->n_q + k] % q, q);
             int in_digit = (x < o->n_ks) && (x / o->alpha == j);
             for (int k = 0; k < n; k++) {
-                u32 av = (u32)(prng(o->seed, STREAM(4, g, j), (u64)li * n + k) % q);
+                u32 av = (u32)(prng(o->key, STREAM(4, g, j), (u64)li * n + k) % q);
                 u32 v = subm(eN[(size_t)x * n + k], mulm(av, s[(size_t)li * n + k], q), q);
                 if (in_digit) v = addm(v, mulm(pmod, sp[(size_t)x * n + k], q), q);
                 a[(size_t)x * n + k] = av;
@@ -875,7 +902,7 @@ void orc_encrypt(void *h, int f, const u32 *pt, const u32 *pk, u64 ctr, u32 *out
     for (int i = 0; i < nq; i++) ids[i] = i;
     int *v = (int *)malloc(sizeof(int) * n), *e = (int *)malloc(sizeof(int) * n);
     u32 *vN = (u32 *)malloc(sizeof(u32) * P), *e0 = (u32 *)malloc(sizeof(u32) * P), *e1 = (u32 *)malloc(sizeof(u32) * P);
-    for (int k = 0; k < n; k++) v[k] = ternary(prng(o->seed, STREAM(6, 0, ctr), (u64)k));
+    for (int k = 0; k < n; k++) v[k] = ternary(prng(o->key, STREAM(6, 0, ctr), (u64)k));
     small_to_ntt(o, v, ids, nq, vN);
     cbd_poly(o, STREAM(7, 0, ctr), e); small_to_ntt(o, e, ids, nq, e0);
     cbd_poly(o, STREAM(8, 0, ctr), e); small_to_ntt(o, e, ids, nq, e1);

@@ -56,6 +56,18 @@ def test_secret_and_public_key_bitexact(pair):
     assert np.array_equal(E.export_pk(), O.gen_pk())
 
 
+def test_keyed_context_bitexact():
+    """aesfhe_create_keyed: a full 256-bit ChaCha20 key gives the oracle's keys bit for bit"""
+    from mi355x_ckks import Engine
+    from oracle.ckks_cpu import OracleParams
+    key = bytes((7 * i + 3) & 0xFF for i in range(32))
+    E = Engine(log_n=13, max_level=4, dnum=3, seed=key, allow_insecure=True)
+    O = OracleParams(log_n=13, max_level=4, dnum=3, seed=key)
+    assert np.array_equal(E.export_secret(), O.secret_ntt())
+    assert np.array_equal(E.export_pk(), O.gen_pk())
+    assert np.array_equal(E.export_ksk(E.galois_conj), O.gen_ksk(E.galois_conj))
+
+
 @pytest.mark.parametrize("which", ["relin", "conj", "rot"])
 def test_keyswitch_keys_bitexact(pair, which):
     E, O = pair
