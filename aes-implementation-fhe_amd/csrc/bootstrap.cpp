@@ -2,6 +2,7 @@
 #include "bootstrap.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <map>
 
 namespace {
@@ -80,8 +81,9 @@ LinGroup layout(const Diags& D, int h, int M) {
     // baby steps are hoisted (one ModUp for all of them, no ModDown each) and cost a key
     // inner product; giant steps are full key switches: about 2 sqrt(n) babies, a power of
     // two (<= 16), and offsets starting at a multiple of B so that one giant step is 0
+    static const int bmax = std::getenv("AESFHE_BOOT_BMAX") ? std::atoi(std::getenv("AESFHE_BOOT_BMAX")) : 16;
     int B = 1;
-    while (B < 16 && B < 2.0 * std::sqrt((double)n)) B *= 2;
+    while (B < bmax && B < 2.0 * std::sqrt((double)n)) B *= 2;
     const int R0 = (R + B - 1) / B * B;
     g.R = R0;
     g.B = B;

@@ -1797,7 +1797,12 @@ public:
     }
 
     // ------------------------------------------------------------------ bootstrapping
-    static constexpr int kBootCts = 3, kBootStc = 3, kBootK = 12, kBootR = 4, kBootDeg = 27, kSparseH = 32;
+    static constexpr int kBootStc = 3, kBootK = 12, kBootR = 4, kBootDeg = 27, kSparseH = 32;
+    // CoeffToSlot groups (one double-prime level each; AESFHE_BOOT_CTS overrides, for sweeps)
+    static int boot_cts() {
+        static const int v = std::getenv("AESFHE_BOOT_CTS") ? std::atoi(std::getenv("AESFHE_BOOT_CTS")) : 3;
+        return v;
+    }
     // message bits b: s_bt = Q0 / 2^b (AESFHE_BOOT_MSG_BITS overrides, for accuracy sweeps)
     int boot_msg_bits_ = std::getenv("AESFHE_BOOT_MSG_BITS") ? std::atoi(std::getenv("AESFHE_BOOT_MSG_BITS")) : 9;
     // depth of cheb_eval for a degree-d series: baby T_k at ceil(log2 k), a leaf one more
@@ -1810,9 +1815,9 @@ public:
         return std::max(cheb_depth(m - 1), 1 + std::max(clog2(m), cheb_depth(d - m)));
     }
     static int boot_evalmod_depth() { return cheb_depth(kBootDeg) + kBootR; }
-    static int boot_depth() { return kBootCts + boot_evalmod_depth() + kBootStc; }
+    static int boot_depth() { return boot_cts() + boot_evalmod_depth() + kBootStc; }
     // double-prime levels: CoeffToSlot + EvalMod + the region-crossing first SlotToCoeff group
-    static int boot_double_levels() { return kBootCts + boot_evalmod_depth() + 1; }
+    static int boot_double_levels() { return boot_cts() + boot_evalmod_depth() + 1; }
     u64 tag_d2s() const { return 2ull * hp_.n + 1; }
     u64 tag_s2d() const { return 2ull * hp_.n + 3; }
 
@@ -1873,7 +1878,7 @@ public:
         // 2^(stages after the first group / 2) (AESFHE_STC_BOOST overrides; 1 = off)
         const int later = (hp_.logn - 1) - (hp_.logn - 1 + kBootStc - 1) / kBootStc;
         const double boost = std::getenv("AESFHE_STC_BOOST") ? std::atof(std::getenv("AESFHE_STC_BOOST")) : std::ldexp(1.0, later / 2);
-        bs_.plan = make_boot_plan(hp_.logn, kBootCts, kBootStc, cts_scale, stc_scale, kBootK, kBootR, kBootDeg, boost);
+        bs_.plan = make_boot_plan(hp_.logn, boot_cts(), kBootStc, cts_scale, stc_scale, kBootK, kBootR, kBootDeg, boost);
         bs_.cts.assign(bs_.plan.cts.size(), {});
         bs_.stc.assign(bs_.plan.stc.size(), {});
         for (size_t i = 0; i < bs_.cts.size(); ++i) bs_.cts[i].g = &bs_.plan.cts[i];
@@ -1887,7 +1892,7 @@ public:
     // debug: apply CoeffToSlot group `which` (0..2) or SlotToCoeff group (3..5)
     Ct debug_lin_group(const Ct& c, int which) {
         boot_setup();
-        auto& G = which < kBootCts ? bs_.cts[which] : bs_.stc[which - kBootCts];
+        auto& G = which < boot_cts() ? bs_.cts[which] : bs_.stc[which - boot_cts()];
         return lin_group(c, G);
     }
     void boot_info(double* out) const {

@@ -6,6 +6,9 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
 #include "launch.h"
 
 
@@ -940,24 +943,34 @@ void launch_lin_mac_nb(hipStream_t st, const DevTables& T, const LinMacArgs& m, 
 
 void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int nl, int ne, LimbMap map) {
     if (m.B < 1 || m.B > kLinB || m.G < 1 || m.G > kLinG) throw std::runtime_error("launch_lin_mac: 1..16 baby, 1..5 giant steps");
-    double reads = 0, writes = 0;  // rows of N words
+    // algorithmic bytes: every distinct input row read once (the baby steps re-read c0 and the
+    // hoisted ext through their automorphisms -- from L2 / MALL), every output written once
+    double member = 0, writes = 0, shared = 0;  // rows of N words; member: per batched ciphertext
+    bool any_a = false, any_key = false;
     for (int b = 0; b < m.B; ++b) {
-        if (m.a[b]) reads += nl;
-        if (m.u[b]) reads += 2.0 * ne;
-        if (m.key[b]) reads += (double)m.nd * ne;  // ext per member (the key is counted as shared below)
+        any_a = any_a || m.a[b];
+        any_key = any_key || m.key[b];
+        if (m.u[b]) member += 2.0 * ne;
+        if (m.key[b]) shared += 2.0 * m.nd * ne;  // the key, read once for every batched ciphertext
         for (int g = 0; g < m.G; ++g)
-            if (m.pt[g][b]) reads += ne;
+            if (m.pt[g][b]) shared += ne;         // the diagonals likewise
     }
-    reads += nl;  // c1
+    if (any_a) member += nl;                      // c0
+    if (any_key) member += (double)m.nd * ne;     // the hoisted ModUp of c1 (ext)
+    member += nl;                                 // c1
     for (int g = 0; g < m.G; ++g)
         writes += (m.gad && m.outp[g]) ? 2.0 * ne : nl + (m.out1[g] ? nl : 0) + (m.outp[g] ? 2.0 * ne : 0);
-    double shared = 0;  // the diagonals (and in-kernel keys), read once for every batched ciphertext
-    for (int b = 0; b < m.B; ++b) {
-        for (int g = 0; g < m.G; ++g)
-            if (m.pt[g][b]) shared += ne;
-        if (m.key[b]) shared += 2.0 * m.nd * ne;
+    const double bytes = words((m.nb * (member + writes) + shared) * (1u << T.logn));
+    static const bool trace = std::getenv("AESFHE_LINMAC_TRACE") != nullptr;
+    if (trace) {
+        int nkeys = 0, npt = 0, na = 0, nu = 0;
+        for (int b = 0; b < m.B; ++b) {
+            nkeys += m.key[b] != nullptr, na += m.a[b] != nullptr, nu += m.u[b] != nullptr;
+            for (int g = 0; g < m.G; ++g) npt += m.pt[g][b] != nullptr;
+        }
+        std::fprintf(stderr, "lin_mac B=%d G=%d nb=%d nd=%d nl=%d ne=%d keys=%d pts=%d a=%d u=%d rows_member=%.0f rows_write=%.0f rows_shared=%.0f MB=%.1f\n",
+                     m.B, m.G, m.nb, m.nd, nl, ne, nkeys, npt, na, nu, member, writes, shared, bytes / 1e6);
     }
-    const double bytes = words((m.nb * (reads - shared + writes) + shared) * (1u << T.logn));
     if (m.nb == 1)
         launch_lin_mac_nb<1>(st, T, m, nl, ne, map, bytes);
     else if (m.nb == 2)

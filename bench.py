@@ -34,9 +34,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 # VALU roofline of the NTT passes: u32 VALU issue rate measured on this chip with
 # tools/valu_rate.hip (v_mul_lo_u32 / v_mul_hi_u32 / v_min_u32 all at ~3.85e13 lane-instr/s,
 # i.e. the 32-bit multiplies are NOT quarter rate on gfx950) over the VALU instructions per
-# radix-2 butterfly in k_ntt2_fwd's ISA (1006 per thread for 64 butterflies)
+# radix-2 butterfly in k_ntt2_fwd's ISA (884 per thread for 64 butterflies with Harvey's lazy
+# butterflies: hipcc --save-temps, v_* lines of k_ntt2_fwd<8, 0, 512>)
 VALU_LANE_INSTR_PER_S = 3.85e13
-NTT_VALU_INSTR_PER_BFLY = 1006.0 / 64.0
+NTT_VALU_INSTR_PER_BFLY = 884.0 / 64.0
 
 
 def parse():
@@ -77,7 +78,8 @@ def parse():
                     help="with AESFHE_PROFILE_FROM_START=<ids>: keep the engine's per-kernel accounting from the first "
                          "launch on (no reset, every launch) and write it to this JSON file -- the algorithmic bytes of "
                          "exactly the launches a whole-process rocprofv3 --pmc pass counts")
-    ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r1_pmc_traffic.json"), help="per-launch HBM bytes from a rocprofv3 PMC pass")
+    ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r2_pmc_traffic_round.json"),
+                    help="per-kernel HBM/algorithmic byte ratios from rocprofv3 PMC passes (tools/r2_pmc_filtered.sh)")
     return ap.parse_args()
 
 
@@ -435,7 +437,7 @@ def main():
         return {"kernel": kid, "bound": "valu", "achieved": achieved, "peak": peak, "unit": "butterfly/s", "frac": achieved / peak,
                 "butterflies_per_launch": work[kid] / max(ks["launches"], 1),
                 "note": "peak = measured u32 VALU issue rate (tools/valu_rate.hip) / VALU instructions per butterfly in the "
-                        "kernel's ISA; the NTT passes are VALU-bound (HBM traffic = algorithmic bytes, profiles/r1_pmc_traffic.json)"}
+                        "kernel's ISA; the NTT passes are VALU-bound (HBM traffic ~ algorithmic bytes, profiles/r2_pmc_traffic_round.json)"}
 
     line = {
         "metric": "homomorphic AES-128 rounds/sec (enc) at N=2^16",
@@ -462,7 +464,7 @@ def main():
                     "relinearisations per round, SURVEY.md 8(a))"),
                    "blocks_per_s": states_done / elapsed, "verified_against_plaintext_model": bool(ok)},
         "roofline": roofline(args.kernel, "dominant kernel by time (NTT pass 2 incl. fused rescale/ModDown epilogue); "
-                                          "VALU-bound by 3 u32 multiplies per butterfly (DESIGN.md 5)"),
+                                          "VALU-bound: ~13.8 VALU instructions per lazy butterfly, u32 multiplies at full rate (DESIGN.md 5)"),
         "roofline_secondary": roofline(args.kernel2, "key-switch inner product: HBM-bound"),
         "roofline_valu": valu_roofline(args.kernel),
         "op_counts_per_round": {k: v / (10.0 * args.steps) for k, v in counters.items()},
