@@ -191,7 +191,10 @@ __global__ void k_crt2_spread(u32* v, const u32* src, int nt, u32 q0, u32 q1, u3
 // The block's constants (source primes, qhat^{-1}, the h x kConvTargets table slice, -Q,
 // target primes) are staged in LDS first: read from global memory next to the stores to
 // ext they would be re-fetched, one dependent load per multiply-add.
-constexpr int kConvTargets = 8;
+#ifndef AESFHE_CONV_TARGETS
+#define AESFHE_CONV_TARGETS 16
+#endif
+constexpr int kConvTargets = AESFHE_CONV_TARGETS;
 // H sources, compile-time: every load issued up front, the multiply-adds unrolled without
 // branches; targets outside [t0, t1) or inside the own range compute on zero weights and
 // are not stored
@@ -235,22 +238,21 @@ __global__ void __launch_bounds__(kBlock) k_base_convert(ConvBatch cb, int nt, L
     __shared__ u32 s_tq[kConvTargets][4];  // q, mu, r32, -Q mod q
     __shared__ u32 s_src[kMaxConvH][4];    // q, mu, qhat^-1, Shoup companion
     const int tid = threadIdx.x;
-    if (tid < kConvTargets * kMaxConvH) {
-        const int tl = tid / kMaxConvH, i = tid % kMaxConvH, t = t0 + tl;
+    for (int x = tid; x < kConvTargets * kMaxConvH; x += kBlock) {
+        const int tl = x / kMaxConvH, i = x % kMaxConvH, t = t0 + tl;
         s_w[tl][i] = (i < h && t < t1) ? cb.tab[gi][2 * ((size_t)i * nt + t)] : 0u;
-    } else if (tid < kConvTargets * kMaxConvH + kConvTargets) {
-        const int tl = tid - kConvTargets * kMaxConvH, t = t0 + tl;
+    }
+    for (int tl = tid; tl < kConvTargets; tl += kBlock) {
+        const int t = t0 + tl;
         if (t < t1) {
             const PrimeConst P = pc[map.prime(t)];
             s_tq[tl][0] = P.q, s_tq[tl][1] = P.mu, s_tq[tl][2] = P.r32, s_tq[tl][3] = cb.negq[gi][t];
         }
-    } else if (tid < kConvTargets * kMaxConvH + kConvTargets + kMaxConvH) {
-        const int i = tid - kConvTargets * kMaxConvH - kConvTargets;
-        if (i < h) {
-            const int sp = cb.split[gi];
-            const PrimeConst P = pc[(sp > 0 && i >= sp) ? cb.d1[gi] + (i - sp) : d0 + i];
-            s_src[i][0] = P.q, s_src[i][1] = P.mu, s_src[i][2] = cb.qhinv[gi][2 * i], s_src[i][3] = cb.qhinv[gi][2 * i + 1];
-        }
+    }
+    for (int i = tid; i < h; i += kBlock) {
+        const int sp = cb.split[gi];
+        const PrimeConst P = pc[(sp > 0 && i >= sp) ? cb.d1[gi] + (i - sp) : d0 + i];
+        s_src[i][0] = P.q, s_src[i][1] = P.mu, s_src[i][2] = cb.qhinv[gi][2 * i], s_src[i][3] = cb.qhinv[gi][2 * i + 1];
     }
     __syncthreads();
     const size_t k = (size_t)blockIdx.x * kBlock + tid;

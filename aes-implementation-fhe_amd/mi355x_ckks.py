@@ -66,7 +66,8 @@ def load_library(path: Optional[Path] = None):
     global _lib
     if _lib is not None and path is None:
         return _lib
-    p = Path(path) if path else _LIB_PATH
+    # AESFHE_LIB: another build of the same library (A/B runs, tools/gpu_ab*.sh)
+    p = Path(path) if path else Path(os.environ.get("AESFHE_LIB") or _LIB_PATH)
     if not p.exists():
         raise RuntimeError(f"MI355X engine library missing: {p} (run build_ext.py / __graft_entry__.build())")
     L = ctypes.CDLL(str(p))

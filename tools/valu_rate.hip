@@ -9,8 +9,9 @@
 template <int OP>
 __global__ void __launch_bounds__(256) k_rate(unsigned* out, unsigned seed, int iters) {
     unsigned x[8];
+    unsigned long long acc[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) x[i] = seed * (threadIdx.x + 1) + i * 0x9E3779B9u;
+    for (int i = 0; i < 8; ++i) x[i] = seed * (threadIdx.x + 1) + i * 0x9E3779B9u, acc[i] = x[i];
     const unsigned c = seed | 1u;
     for (int it = 0; it < iters; ++it) {
 #pragma unroll
@@ -22,11 +23,15 @@ __global__ void __launch_bounds__(256) k_rate(unsigned* out, unsigned seed, int 
                 if (OP == 1) asm volatile("v_min_u32 %0, %0, %1" : "+v"(x[i]) : "v"(c));
                 if (OP == 2) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(x[i]) : "v"(c));
                 if (OP == 3) asm volatile("v_mul_hi_u32 %0, %0, %1" : "+v"(x[i]) : "v"(c));
+                if (OP == 4) {  // the 32x32 -> 64-bit multiply-add of the base conversion / key inner product
+                    unsigned long long cc;
+                    asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc[i]), "=s"(cc) : "v"(x[i]), "v"(c));
+                }
             }
     }
     unsigned s = 0;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s ^= x[i];
+    for (int i = 0; i < 8; ++i) s ^= x[i] ^ (unsigned)acc[i];
     if (s == 0x12345678u) out[0] = s;  // keeps the chains alive
 }
 
@@ -57,5 +62,6 @@ int main() {
     rate<1>("v_min_u32", 1);
     rate<2>("v_mul_lo_u32", 1);
     rate<3>("v_mul_hi_u32", 1);
+    rate<4>("v_mad_u64_u32", 1);
     return 0;
 }
