@@ -2589,7 +2589,7 @@ private:
             for (int k = 0; k < n; ++k) {
                 const u32 r = hbitrev((u32)k, logn);
                 const size_t at = (size_t)i * n + r;
-                tw[at] = make_uint2((u32)p, shoup_pre((u32)p, q));
+                tw[at] = make_uint2(0u - (u32)p, shoup_pre((u32)p, q));  // -w mod 2^32 (ntt.hip ct_bfly)
                 itw[at] = make_uint2((u32)ip, shoup_pre((u32)ip, q));
                 p = p * w % q;
                 ip = ip * iw % q;

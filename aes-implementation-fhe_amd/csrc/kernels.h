@@ -51,7 +51,7 @@ void prof_set(KernelProfiler* p);
 
 struct DevTables {
     const PrimeConst* pc = nullptr;  // [n_tot]
-    const uint2* tw = nullptr;       // [n_tot][N]  {psi^{bitrev(k)}, Shoup companion}: one 8-byte load per twiddle
+    const uint2* tw = nullptr;       // [n_tot][N]  {-psi^{bitrev(k)} mod 2^32, Shoup companion of psi^{bitrev(k)}}: one 8-byte load per twiddle
     const uint2* itw = nullptr;      // [n_tot][N]  {psi^{-bitrev(k)}, Shoup companion}
     int logn = 16;
 };

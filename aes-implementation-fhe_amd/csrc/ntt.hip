@@ -36,21 +36,25 @@ constexpr int kPitchP2 = 272;
 
 // Harvey's lazy butterflies (every prime < 2^30, so 4q < 2^32): the forward transform keeps
 // residues in [0, 4q) and the inverse in [0, 2q) between stages; only the last stage of a
-// transform reduces to [0, q).  9 VALU operations per butterfly instead of 13 (Shoup product
-// without its correction, one min-based reduction of the sum operand).
-__device__ __forceinline__ u32 lazy_shoup(u32 a, u32 w, u32 wp, u32 q) { return a * w - mulhi32(a, wp) * q; }  // [0, 2q)
+// transform reduces to [0, q).  Shoup's product without its correction, one min-based
+// reduction of the sum operand, and the product's last two steps as ONE 32x32+64 multiply-add
+// (v_mad_u64_u32, full rate on gfx950): the forward table holds -w mod 2^32, so
+//   tn = mulhi(b, w') q - b w = -t (mod 2^32),  a' = x - tn,  b' = x + 2q + tn  (v_add3_u32)
+// -- 7 VALU operations per forward butterfly (9 before), 8 per inverse one; the values are
+// the same as the plain lazy butterfly's, bit for bit.
 __device__ __forceinline__ u32 red2(u32 x, u32 q2) { return min(x, x - q2); }  // [0, 2 q2) -> [0, q2)
 __device__ __forceinline__ u32 canon4(u32 x, u32 q) { return red2(red2(x, 2 * q), q); }  // [0, 4q) -> [0, q)
-__device__ __forceinline__ void ct_bfly(u32& a, u32& b, u32 w, u32 wp, u32 q2, u32 q) {
-    const u32 t = lazy_shoup(b, w, wp, q);  // b < 4q, t < 2q
-    const u32 x = red2(a, q2);              // [0, 2q)
-    a = x + t;                              // [0, 4q)
-    b = x - t + q2;                         // (0, 4q)
+__device__ __forceinline__ void ct_bfly(u32& a, u32& b, u32 nw, u32 wp, u32 q2, u32 q) {
+    const u32 tn = (u32)((u64)mulhi32(b, wp) * q + (u32)(b * nw));  // -(b w - floor(b w'/2^32) q), t in [0, 2q)
+    const u32 x = red2(a, q2);                                        // [0, 2q)
+    a = x - tn;                                                       // x + t in [0, 4q)
+    b = x + q2 + tn;                                                  // x - t + 2q in (0, 4q)
 }
-__device__ __forceinline__ void gs_bfly(u32& a, u32& b, u32 w, u32 wp, u32 q2, u32 q) {
-    const u32 u = a, v = b;                        // [0, 2q)
-    a = red2(u + v, q2);                           // [0, 2q)
-    b = lazy_shoup(u - v + q2, w, wp, q);          // [0, 2q)
+__device__ __forceinline__ void gs_bfly(u32& a, u32& b, u32 w, u32 wp, u32 q2, u32 nq) {
+    const u32 u = a, v = b;                                           // [0, 2q)
+    a = red2(u + v, q2);                                              // [0, 2q)
+    const u32 d = u - v + q2;                                         // (0, 4q)
+    b = (u32)((u64)mulhi32(d, wp) * nq + (u32)(d * w));              // d w - floor(d w'/2^32) q in [0, 2q)
 }
 __device__ __forceinline__ int swz(int w) { return w ^ ((w >> 4) & 15); }
 
@@ -288,7 +292,7 @@ __global__ void __launch_bounds__(NT) k_ntt2_inv(u32* dst, const u32* src, RowMa
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
                 const int ti = base + ((16 * j + k) >> (8 - s));
-                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, q);
+                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, 0u - q);
             }
     }
     u32* row = sm + r * kPitchP2;
@@ -305,7 +309,7 @@ __global__ void __launch_bounds__(NT) k_ntt2_inv(u32* dst, const u32* src, RowMa
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
                 const int ti = base + (k >> (4 - s));
-                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, q);
+                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, 0u - q);
             }
     }
     u32* p = ra.dst + (size_t)R * 256;
@@ -338,7 +342,7 @@ __global__ void __launch_bounds__(NT) k_ntt1_inv(u32* data, RowMap rm, LimbMap m
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
                 const int ti = (1 << s) + ((16 * g + k) >> (LOGR1 - s));
-                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, q);
+                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, 0u - q);
             }
     }
 #pragma unroll
@@ -353,7 +357,7 @@ __global__ void __launch_bounds__(NT) k_ntt1_inv(u32* data, RowMap rm, LimbMap m
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
                 const int ti = (1 << s) + (k >> (4 - s));
-                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, q);
+                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, 0u - q);
             }
     }
 #pragma unroll
