@@ -34,10 +34,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 # VALU roofline of the NTT passes: u32 VALU issue rate measured on this chip with
 # tools/valu_rate.hip (v_mul_lo_u32 / v_mul_hi_u32 / v_min_u32 all at ~3.85e13 lane-instr/s,
 # i.e. the 32-bit multiplies are NOT quarter rate on gfx950) over the VALU instructions per
-# radix-2 butterfly in k_ntt2_fwd's ISA (884 per thread for 64 butterflies with Harvey's lazy
-# butterflies: hipcc --save-temps, v_* lines of k_ntt2_fwd<8, 0, 512>)
+# radix-2 butterfly in k_ntt2_fwd's ISA (756 per thread for 64 butterflies with the 7-operation
+# lazy butterfly: hipcc --save-temps, v_* lines of k_ntt2_fwd<8, 0, 512>)
 VALU_LANE_INSTR_PER_S = 3.85e13
-NTT_VALU_INSTR_PER_BFLY = 884.0 / 64.0
+NTT_VALU_INSTR_PER_BFLY = 756.0 / 64.0
 
 
 def parse():
@@ -464,7 +464,7 @@ def main():
                     "relinearisations per round, SURVEY.md 8(a))"),
                    "blocks_per_s": states_done / elapsed, "verified_against_plaintext_model": bool(ok)},
         "roofline": roofline(args.kernel, "dominant kernel by time (NTT pass 2 incl. fused rescale/ModDown epilogue); "
-                                          "VALU-bound: ~13.8 VALU instructions per lazy butterfly, u32 multiplies at full rate (DESIGN.md 5)"),
+                                          "VALU / latency-bound: ~11.8 VALU instructions per lazy butterfly, u32 multiplies at full rate (DESIGN.md 5)"),
         "roofline_secondary": roofline(args.kernel2, "key-switch inner product: HBM-bound"),
         "roofline_valu": valu_roofline(args.kernel),
         "op_counts_per_round": {k: v / (10.0 * args.steps) for k, v in counters.items()},
