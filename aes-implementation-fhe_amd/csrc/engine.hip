@@ -1797,7 +1797,16 @@ public:
     }
 
     // ------------------------------------------------------------------ bootstrapping
-    static constexpr int kBootStc = 3, kBootK = 12, kBootR = 4, kBootDeg = 27, kSparseH = 32;
+    static constexpr int kBootStc = 3, kSparseH = 32;
+    // EvalMod: range K (|I| < K), r double angles, Chebyshev degree (AESFHE_BOOT_K / _R / _DEG
+    // override, for sweeps; read once per process)
+    static int env_int(const char* name, int dflt) {
+        const char* e = std::getenv(name);
+        return e ? std::atoi(e) : dflt;
+    }
+    static int boot_k() { static const int v = env_int("AESFHE_BOOT_K", 12); return v; }
+    static int boot_r() { static const int v = env_int("AESFHE_BOOT_R", 4); return v; }
+    static int boot_deg() { static const int v = env_int("AESFHE_BOOT_DEG", 27); return v; }
     // CoeffToSlot groups (one double-prime level each; AESFHE_BOOT_CTS overrides, for sweeps)
     static int boot_cts() {
         static const int v = std::getenv("AESFHE_BOOT_CTS") ? std::atoi(std::getenv("AESFHE_BOOT_CTS")) : 3;
@@ -1814,7 +1823,7 @@ public:
         while (2 * m <= d) m *= 2;
         return std::max(cheb_depth(m - 1), 1 + std::max(clog2(m), cheb_depth(d - m)));
     }
-    static int boot_evalmod_depth() { return cheb_depth(kBootDeg) + kBootR; }
+    static int boot_evalmod_depth() { return cheb_depth(boot_deg()) + boot_r(); }
     static int boot_depth() { return boot_cts() + boot_evalmod_depth() + kBootStc; }
     // double-prime levels: CoeffToSlot + EvalMod + the region-crossing first SlotToCoeff group
     static int boot_double_levels() { return boot_cts() + boot_evalmod_depth() + 1; }
@@ -1872,13 +1881,13 @@ public:
         const double Q0 = (double)hp_.mod[0] * (double)hp_.mod[1];
         bs_.k1 = std::llround(Q0 / std::ldexp(1.0, boot_msg_bits_) / hp_.delta[0]);
         bs_.s_bt = hp_.delta[0] * (double)bs_.k1;
-        const double cts_scale = hp_.delta[bs_.top] / (2.0 * Q0 * kBootK);
+        const double cts_scale = hp_.delta[bs_.top] / (2.0 * Q0 * boot_k());
         const double stc_scale = Q0 / (2.0 * M_PI * bs_.s_bt);
         // intermediate SlotToCoeff signal lifted by the later groups' butterfly gain,
         // 2^(stages after the first group / 2) (AESFHE_STC_BOOST overrides; 1 = off)
         const int later = (hp_.logn - 1) - (hp_.logn - 1 + kBootStc - 1) / kBootStc;
         const double boost = std::getenv("AESFHE_STC_BOOST") ? std::atof(std::getenv("AESFHE_STC_BOOST")) : std::ldexp(1.0, later / 2);
-        bs_.plan = make_boot_plan(hp_.logn, boot_cts(), kBootStc, cts_scale, stc_scale, kBootK, kBootR, kBootDeg, boost);
+        bs_.plan = make_boot_plan(hp_.logn, boot_cts(), kBootStc, cts_scale, stc_scale, boot_k(), boot_r(), boot_deg(), boost);
         bs_.cts.assign(bs_.plan.cts.size(), {});
         bs_.stc.assign(bs_.plan.stc.size(), {});
         for (size_t i = 0; i < bs_.cts.size(); ++i) bs_.cts[i].g = &bs_.plan.cts[i];
@@ -1899,9 +1908,9 @@ public:
         out[0] = bs_.s_bt;
         out[1] = (double)bs_.k1;
         out[2] = bs_.top;
-        out[3] = kBootK;
-        out[4] = kBootR;
-        out[5] = kBootDeg;
+        out[3] = boot_k();
+        out[4] = boot_r();
+        out[5] = boot_deg();
         out[6] = d2s_modulus_bits();
         out[7] = kSparseH;
         out[8] = d2s_np();
