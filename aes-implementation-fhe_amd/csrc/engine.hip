@@ -1870,6 +1870,44 @@ public:
         i64 k1 = 0;         // integer factor taking delta_0 to s_bt
         std::vector<BootGroupDev> cts, stc;
     } bs_;
+    // sparse-slot bootstrap of an n-periodic message (slot j == slot j mod n):
+    // the message lies in the subring Z[X^(N/2n)], the ring of dimension 2n with n slots, so
+    // after ModRaise a trace (log2(M/n) rotations by n 2^i, summed) removes the overflow's
+    // components outside that subring and CoeffToSlot / SlotToCoeff are the small ring's
+    // transforms (log2 n stages), their diagonals tiled with period n
+    struct SparseBoot {
+        int n = 0, top = 0, out_level = 0;
+        BootPlan plan;
+        std::vector<BootGroupDev> cts, stc;
+    };
+    std::map<int, SparseBoot> sparse_;
+    SparseBoot& sparse_variant(int n) {
+        auto it = sparse_.find(n);
+        if (it != sparse_.end()) return it->second;
+        const int M = slot_count();
+        int logm = 0;
+        while ((1 << logm) < n) ++logm;
+        if ((1 << logm) != n || n < 16 || n >= M) throw std::runtime_error("sparse bootstrap: period must be a power of two in [16, slot_count)");
+        SparseBoot& sv = sparse_[n];
+        sv.n = n;
+        const int groups = std::max(1, (logm + 4) / 5);  // <= 5 butterfly stages per group, like the full plan
+        // StC's first group crosses the single / double-prime transition (plaintext products only)
+        sv.top = hp_.L1 + 1 + groups + boot_evalmod_depth();
+        sv.out_level = hp_.L1 + 1 - groups;
+        if (sv.top > hp_.L) throw std::runtime_error("sparse bootstrap: chain too short");
+        const double Q0 = (double)hp_.mod[0] * (double)hp_.mod[1];
+        // the trace multiplies by M / n: folded into CoeffToSlot
+        const double cts_scale = hp_.delta[sv.top] / (2.0 * Q0 * boot_k() * ((double)M / n));
+        const double stc_scale = Q0 / (2.0 * M_PI * bs_.s_bt);
+        const int later = logm - (logm + groups - 1) / groups;
+        const double boost = groups > 1 ? std::ldexp(1.0, later / 2) : 1.0;
+        sv.plan = make_boot_plan(logm + 1, groups, groups, cts_scale, stc_scale, boot_k(), boot_r(), boot_deg(), boost);
+        sv.cts.assign(sv.plan.cts.size(), {});
+        sv.stc.assign(sv.plan.stc.size(), {});
+        for (size_t i = 0; i < sv.cts.size(); ++i) sv.cts[i].g = &sv.plan.cts[i];
+        for (size_t i = 0; i < sv.stc.size(); ++i) sv.stc[i].g = &sv.plan.stc[i];
+        return sv;
+    }
 
     void boot_setup() {
         if (bs_.ready) return;
@@ -1932,7 +1970,8 @@ public:
             for (int b = 0; b < g.B; ++b) {
                 const auto& d = g.diag[gg][b];
                 if (d.empty()) continue;
-                for (int p = 0; p < M; ++p) re[p] = d[p].real(), im[p] = d[p].imag();
+                const size_t dn = d.size();  // M, or n for a sparse plan (tiled with period n)
+                for (int p = 0; p < M; ++p) re[p] = d[p % dn].real(), im[p] = d[p % dn].imag();
                 const int nl = hp_.nl(level), ne = nl + hp_.n_p;
                 encode_host(re.data(), im.data(), hp_.ptscale[level], nl, host, hp_.n_p);
                 u32* dv = tmp(ne);
@@ -2343,19 +2382,21 @@ public:
     // 6 real part, 7 imaginary part, 8 EvalMod(real), 9 EvalMod(imag), 10 recombined, 11 output
     // gain: the output carries gain * message (folded into the level-0 scaling integer k1,
     // relative precision 2^-k1bits; the true-FHE snap's kappa, zeta16_noise_reducer.py)
-    Ct bootstrap(const Ct& in, int stop_after = 99, double gain = 1.0) {
+    Ct bootstrap(const Ct& in, int stop_after = 99, double gain = 1.0, int period = 0) {
         boot_setup();
         if (vis_npoly(in) != 2 || in.nb != 1) throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
+        SparseBoot* sv = (period > 0 && period < slot_count()) ? &sparse_variant(period) : nullptr;
         Ct c = normalize(in);
         Ct z = level_down(c, 0);
         if (c.data != in.data) release(c);
-        return bootstrap_l0(z, stop_after, gain);
+        return bootstrap_l0(z, stop_after, gain, sv);
     }
     // the hi / lo bootstraps of an AES step (MixColumns' final bootstrap) as ONE batched
     // bootstrap of two stacked ciphertexts: every key switch reads its key, and every linear
     // transform its diagonals, once for both; half the launches
-    void bootstrap_pair(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob, double gain = 1.0) {
+    void bootstrap_pair(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob, double gain = 1.0, int period = 0) {
         boot_setup();
+        SparseBoot* sv = (period > 0 && period < slot_count()) ? &sparse_variant(period) : nullptr;
         if (vis_npoly(a_in) != 2 || vis_npoly(b_in) != 2 || a_in.nb != 1 || b_in.nb != 1)
             throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
         const int n = hp_.n, nl0 = hp_.nl(0);
@@ -2368,7 +2409,7 @@ public:
             launch_copy_rows(S(), T_, z.data + (size_t)m * 2 * nl0 * n, zm.data, 2 * nl0);
             release(zm);
         }
-        Ct out = bootstrap_l0(z, 99, gain);
+        Ct out = bootstrap_l0(z, 99, gain, sv);
         const int nlo = hp_.nl(out.level);
         aesfhe_handle* dst[2] = {oa, ob};
         for (int m = 0; m < 2; ++m) {
@@ -2380,8 +2421,8 @@ public:
         release(out);
     }
     // z: level-0 ciphertext(s), nb batched members, consumed here
-    Ct bootstrap_l0(Ct z, int stop_after, double gain = 1.0) {
-        const int n = hp_.n, top = bs_.top, nb = z.nb;
+    Ct bootstrap_l0(Ct z, int stop_after, double gain = 1.0, SparseBoot* sv = nullptr) {
+        const int n = hp_.n, top = sv ? sv->top : bs_.top, nb = z.nb;
         // 1. scale delta_0 -> s_bt = Q0 / 2^b (an exact integer product) on the two
         // base limbs: the ciphertext stays modulo Q0 = q0 q1 (no rescale, no rounding noise)
         const int nq = kD2sQ;
@@ -2408,9 +2449,19 @@ public:
         const size_t tms = (size_t)2 * nlt * n;
         Ct u = keyswitch(raised.data + (size_t)nlt * n, top, ksk(tag_s2d()), raised.data, nullptr, nb, tms, tms);
         release(raised);
+        // 4b. sparse: the trace to the subring, x += rot(x, n 2^i) for 2^i < M / n (the overflow's
+        // components outside the subring cancel, the rest is multiplied by M / n)
+        if (sv)
+            for (int st = sv->n; st < slot_count(); st *= 2) {
+                Ct r = rotate(u, -st);
+                Ct s2 = add_sub(u, r, false);
+                release(r);
+                release(u);
+                u = s2;
+            }
         if (stop_after == 4) return u;
         // 5. CoeffToSlot (bit-reversed coefficient halves / (2 q0 K))
-        Ct w = lin_transform(u, bs_.cts);
+        Ct w = lin_transform(u, sv ? sv->cts : bs_.cts);
         release(u);
         if (stop_after == 5) return w;
         // 6. real / imaginary parts (exact: conjugation, add, multiply by -i)
@@ -2460,9 +2511,14 @@ public:
         release(ifim);
         if (stop_after == 10) return wp;
         // 8. SlotToCoeff (scaled back to the message)
-        Ct out = lin_transform(wp, bs_.stc);
+        Ct out = lin_transform(wp, sv ? sv->stc : bs_.stc);
         release(wp);
         cnt_[C_BOOT] += nb;
+        if (out.level > hp_.fresh) {  // a sparse plan's SlotToCoeff ends above the fresh level
+            Ct o = level_down(out, hp_.fresh);
+            release(out);
+            out = o;
+        }
         return out;
     }
 
@@ -3142,8 +3198,23 @@ int aesfhe_bootstrap_pair_scaled(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle
     e.bootstrap_pair(ca, cb, out_a, out_b, gain);
     API_END
 }
+int aesfhe_bootstrap_sparse(aesfhe_ctx* ctx, aesfhe_handle c, int period, double gain, aesfhe_handle* out) {
+    CT_OP(e.bootstrap(e.canon(c), 99, gain, period))
+}
+int aesfhe_bootstrap_pair_sparse(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int period, double gain, aesfhe_handle* out_a,
+                                 aesfhe_handle* out_b) {
+    API_BEGIN Engine& e = *ctx->eng;
+    const Ct& ca = e.canon(a);
+    const Ct& cb = e.canon(b);
+    e.bootstrap_pair(ca, cb, out_a, out_b, gain, period);
+    API_END
+}
 int aesfhe_bootstrap_depth(void) { return Engine::boot_depth(); }
-int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle c, int stage, aesfhe_handle* out) { CT_OP(e.bootstrap(e.canon(c), stage)) }
+int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle c, int stage, aesfhe_handle* out) {
+    // AESFHE_DEBUG_PERIOD: the stages of the sparse-slot bootstrap of that period (profiling)
+    static const int period = std::getenv("AESFHE_DEBUG_PERIOD") ? std::atoi(std::getenv("AESFHE_DEBUG_PERIOD")) : 0;
+    CT_OP(e.bootstrap(e.canon(c), stage, 1.0, period))
+}
 int aesfhe_debug_lin_group(aesfhe_ctx* ctx, aesfhe_handle c, int which, aesfhe_handle* out) {
     CT_OP(e.debug_lin_group(e.canon(c), which))
 }

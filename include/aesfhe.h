@@ -168,6 +168,17 @@ int aesfhe_bootstrap_pair(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, aes
  * extra level): the true-FHE renorm's bootstrap hands the snap u = kappa x (REF
  * zeta16_noise_reducter.py:6-57 bootstrap_before=True) */
 int aesfhe_bootstrap_scaled(aesfhe_ctx* ctx, aesfhe_handle ct, double gain, aesfhe_handle* out);
+/* Sparse-slot bootstrap: for a message whose slots repeat with period `period`
+ * (slot j == slot j mod period; a power of two in [16, slot_count)), i.e. a polynomial in the
+ * subring Z[X^(N / 2 period)].  Same result as aesfhe_bootstrap on such a message (within the
+ * bootstrap's error) at a fraction of the cost: a trace to the subring after ModRaise, then the
+ * period-sized CoeffToSlot / SlotToCoeff; it starts from a lower level.  A message that is not
+ * periodic is NOT refreshed correctly.  gain as for aesfhe_bootstrap_scaled (1.0 = none).
+ * Replaces the same engine.bootstrap calls (REF/engine_context.py:147-162) when the caller
+ * knows its layout is periodic (StateEncoder(periodic=True)). */
+int aesfhe_bootstrap_sparse(aesfhe_ctx* ctx, aesfhe_handle ct, int period, double gain, aesfhe_handle* out);
+int aesfhe_bootstrap_pair_sparse(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int period, double gain, aesfhe_handle* out_a,
+                                 aesfhe_handle* out_b);
 int aesfhe_bootstrap_pair_scaled(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, double gain, aesfhe_handle* out_a,
                                  aesfhe_handle* out_b);
 int aesfhe_bootstrap_depth(void);

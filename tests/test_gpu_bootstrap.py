@@ -133,3 +133,23 @@ def test_dense_to_sparse_key_modulus(ctx):
         e = E.debug_ntt(r.astype(np.uint32)[None], p, inverse=True)[0].astype(np.int64)
         e = np.where(e > int(qt) // 2, e - int(qt), e)
         assert np.abs(e).max() <= 21, (row, np.abs(e).max())
+
+
+@pytest.mark.parametrize("period", [16, 1024])
+def test_sparse_bootstrap_periodic_message(ctx, period):
+    """aesfhe_bootstrap[_pair]_sparse: an n-periodic message (a subring
+    element) refreshed by the trace + small-ring transforms; pair == single bit for bit"""
+    E = ctx.engine
+    S = E.slot_count
+    rng = np.random.default_rng(period)
+    za = np.tile(np.exp(2j * np.pi * rng.random(period)) * rng.random(period), S // period)
+    zb = np.tile(np.exp(2j * np.pi * rng.random(period)), S // period)
+    a, b = ctx.encrypt(za), ctx.encrypt(zb)
+    pa, pb = E.bootstrap_pair_sparse(a, b, period)
+    sa = E.bootstrap_sparse(a, period)
+    assert pa.level == pb.level == E.fresh_level
+    assert np.array_equal(E.export(pa), E.export(sa))
+    assert np.abs(ctx.decrypt(pa) - za).max() < BOOT_TOL
+    assert np.abs(ctx.decrypt(pb) - zb).max() < BOOT_TOL
+    with pytest.raises(RuntimeError, match="period"):
+        E.bootstrap_sparse(a, 24)
