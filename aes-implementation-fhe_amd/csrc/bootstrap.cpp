@@ -103,6 +103,50 @@ LinGroup layout(const Diags& D, int h, int M) {
     return g;
 }
 
+// The packed real form of a sparse plan (pack = true).  CoeffToSlot's last group
+// also multiplies its output by a (2n-periodic), so w' + conj(w') holds 2 Re w on the first half
+// of every 2n block and 2 Im w on the second (the unpacked path's re / im): ONE EvalMod instead of two.  SlotToCoeff's first
+// group reads the halves back, u = s b1 + rot_n(s) b2, folded into its diagonals:
+//   sum_o d_o rot_o(u) = sum_o (d_o rot_o(b1)) rot_o(s) + sum_o (d_o rot_o(b2)) rot_{o+n}(s).
+// n-space offsets are taken signed (|o| <= n/2), valid for the n-periodic vectors they act on.
+Diags lift_out(const Diags& D, int n, const std::vector<cplx>& a) {
+    Diags L;
+    const int n2 = 2 * n;
+    for (const auto& kv : D) {
+        const int o = kv.first <= n / 2 ? kv.first : kv.first - n;
+        std::vector<cplx> v(n2);
+        for (int p = 0; p < n2; ++p) v[p] = a[p] * kv.second[p % n];
+        L[((o % n2) + n2) % n2] = v;
+    }
+    return L;
+}
+Diags lift_in(const Diags& D, int n, const std::vector<cplx>& b1, const std::vector<cplx>& b2) {
+    Diags L;
+    const int n2 = 2 * n;
+    auto add = [&](int off, const std::vector<cplx>& v) {
+        const int k = ((off % n2) + n2) % n2;
+        auto it = L.find(k);
+        if (it == L.end()) {
+            L.emplace(k, v);
+        } else {
+            for (int p = 0; p < n2; ++p) it->second[p] += v[p];
+        }
+    };
+    for (const auto& kv : D) {
+        const int o = kv.first <= n / 2 ? kv.first : kv.first - n;
+        std::vector<cplx> v1(n2), v2(n2);
+        for (int p = 0; p < n2; ++p) {
+            const cplx d = kv.second[p % n];
+            const int q = (((p + o) % n2) + n2) % n2;
+            v1[p] = d * b1[q];
+            v2[p] = d * b2[q];
+        }
+        add(o, v1);
+        add(o + n, v2);
+    }
+    return L;
+}
+
 }  // namespace
 
 std::vector<cplx> apply_group_plain(const LinGroup& g, const std::vector<cplx>& v) {
@@ -123,7 +167,7 @@ std::vector<cplx> apply_group_plain(const LinGroup& g, const std::vector<cplx>& 
 }
 
 BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts_scale, double stc_scale, int K, int r, int deg,
-                        double stc_boost) {
+                        double stc_boost, bool pack) {
     BootPlan P;
     P.logn = logn;
     P.M = 1 << (logn - 1);
@@ -131,6 +175,18 @@ BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts
     P.r = r;
     P.deg = deg;
     const int M = P.M, logm = logn - 1;
+    // packed real form: the 2M-periodic half masks (first half of every 2M block)
+    std::vector<cplx> pa, pb1, pb2;
+    if (pack) {
+        const cplx I(0.0, 1.0);
+        pa.resize(2 * M), pb1.resize(2 * M), pb2.resize(2 * M);
+        for (int p = 0; p < 2 * M; ++p) {
+            const double m = p < M ? 1.0 : 0.0;
+            pa[p] = m - I * (1.0 - m);  // w' + conj(w') = (2 Re w | 2 Im w): the unpacked re / im halves
+            pb1[p] = m + I * (1.0 - m);
+            pb2[p] = I * m + (1.0 - m);
+        }
+    }
 
     auto split = [&](int groups) {
         std::vector<std::vector<int>> out(groups);
@@ -155,7 +211,12 @@ BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts
         if (gi + 1 == sg.size() && sg.size() > 1)
             for (auto& kv : D)
                 for (auto& x : kv.second) x /= stc_boost;
-        P.stc.push_back(layout(D, 1 << (sg[gi].front() - 1), M));
+        if (pack && gi == 0) {
+            D = lift_in(D, M, pb1, pb2);
+            P.stc.push_back(layout(D, 1 << (sg[gi].front() - 1), 2 * M));
+        } else {
+            P.stc.push_back(layout(D, 1 << (sg[gi].front() - 1), M));
+        }
     }
     // CoeffToSlot: inverse stages logm..1 (output bit-reversed w)
     auto cg = split(n_groups_cts);
@@ -166,7 +227,12 @@ BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts
         if (gi == (int)cg.size() - 1)
             for (auto& kv : D)
                 for (auto& x : kv.second) x *= cts_scale;
-        P.cts.push_back(layout(D, 1 << (cg[gi].front() - 1), M));
+        if (pack && gi == 0) {  // the last group applied
+            D = lift_out(D, M, pa);
+            P.cts.push_back(layout(D, 1 << (cg[gi].front() - 1), 2 * M));
+        } else {
+            P.cts.push_back(layout(D, 1 << (cg[gi].front() - 1), M));
+        }
     }
     // Chebyshev interpolation of cos(2 pi (K y - 1/4) / 2^r) at the deg+1 Chebyshev nodes
     const int n = deg + 1;
@@ -233,5 +299,72 @@ extern "C" int aesfhe_debug_bootplan(int logn, double* err) {
         e3 = std::max(e3, std::abs(s - std::cos(2 * M_PI * (P.K * y - 0.25) / std::ldexp(1.0, P.r))));
     }
     err[2] = e3;
+    return 0;
+}
+
+// self-check of a sparse (small-ring, M = n slots) plan, packed or not: random subring
+// coefficients t (2n reals) -> slots z; CoeffToSlot then w' + conj(w') (packed: the 2n-periodic
+// (Re | Im) of the bit-reversed coefficient halves; unpacked: 2 Re), SlotToCoeff of the same
+// (EvalMod taken as the identity) -> z (2z packed).  err: [StC error, CtS error]
+extern "C" int aesfhe_debug_sparseplan(int n, int pack, double* err) {
+    int logm = 0;
+    while ((1 << logm) < n) ++logm;
+    const int groups = std::max(1, (logm + 4) / 5);
+    BootPlan P = make_boot_plan(logm + 1, groups, groups, 1.0, 1.0, 12, 3, 27, 1.0, pack != 0);
+    Embedding emb(logm + 1);
+    std::mt19937_64 rng(2);
+    std::normal_distribution<double> nd;
+    const int M = n, n2 = 2 * n;
+    std::vector<double> m(2 * M), re(M), im(M);
+    for (auto& x : m) x = nd(rng);
+    emb.forward(m.data(), re.data(), im.data());
+    auto brv = [logm](int x) {
+        int r = 0;
+        for (int i = 0; i < logm; ++i) r = (r << 1) | ((x >> i) & 1);
+        return r;
+    };
+    std::vector<cplx> z(M), wb(M);
+    for (int j = 0; j < M; ++j) z[j] = cplx(re[j], im[j]);
+    for (int k = 0; k < M; ++k) wb[k] = cplx(m[brv(k)], m[brv(k) + M]);
+    auto tile = [](const std::vector<cplx>& v, int len) {
+        std::vector<cplx> o(len);
+        for (int p = 0; p < len; ++p) o[p] = v[p % v.size()];
+        return o;
+    };
+    // CoeffToSlot: each group on vectors of its own diagonal length
+    std::vector<cplx> v = z;
+    for (const auto& g : P.cts) {
+        size_t len = v.size();
+        for (const auto& row : g.diag)
+            for (const auto& d : row)
+                if (!d.empty()) len = d.size();
+        v = apply_group_plain(g, tile(v, (int)len));
+    }
+    double e2 = 0;
+    std::vector<cplx> s(v.size());
+    for (size_t p = 0; p < v.size(); ++p) s[p] = v[p] + std::conj(v[p]);
+    if (pack) {
+        for (int p = 0; p < n2; ++p) {
+            const cplx want = p < M ? cplx(2 * wb[p].real(), 0) : cplx(2 * wb[p - M].imag(), 0);
+            e2 = std::max(e2, std::abs(s[p] - want));
+        }
+    } else {
+        for (int p = 0; p < M; ++p) e2 = std::max(e2, std::abs(v[p] - wb[p]));
+        s = v;  // the unpacked path recombines re + i im = w itself
+    }
+    // SlotToCoeff
+    std::vector<cplx> u = s;
+    for (const auto& g : P.stc) {
+        size_t len = u.size();
+        for (const auto& row : g.diag)
+            for (const auto& d : row)
+                if (!d.empty()) len = d.size();
+        u = apply_group_plain(g, tile(u, (int)len));
+    }
+    double e1 = 0;
+    const double gain = pack ? 2.0 : 1.0;  // packed: u = (2 Re w) + i (2 Im w) = 2 w
+    for (int j = 0; j < (int)u.size(); ++j) e1 = std::max(e1, std::abs(u[j] - gain * z[j % M]));
+    err[0] = e1;
+    err[1] = e2;
     return 0;
 }

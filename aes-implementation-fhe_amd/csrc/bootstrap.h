@@ -33,8 +33,10 @@ struct BootPlan {
 // SlotToCoeff (folded into its first group)
 // stc_boost: intermediate SlotToCoeff groups carry the signal times stc_boost (first group
 // x stc_boost, last group / stc_boost; same transform)
+// pack (sparse plans, 2M <= the ring's slot count): CoeffToSlot's last group and SlotToCoeff's
+// first work on 2M-periodic vectors so that the real and imaginary halves share ONE EvalMod
 BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts_scale, double stc_scale, int K, int r, int deg,
-                        double stc_boost = 1.0);
+                        double stc_boost = 1.0, bool pack = false);
 
 // reference evaluation of the planned transforms on plain vectors (self-check)
 std::vector<cplx> apply_group_plain(const LinGroup& g, const std::vector<cplx>& v);

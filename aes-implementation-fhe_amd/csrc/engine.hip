@@ -1877,6 +1877,7 @@ public:
     // transforms (log2 n stages), their diagonals tiled with period n
     struct SparseBoot {
         int n = 0, top = 0, out_level = 0;
+        bool packed = false;  // real / imaginary halves in one 2n-periodic ciphertext (one EvalMod)
         BootPlan plan;
         std::vector<BootGroupDev> cts, stc;
     };
@@ -1901,7 +1902,10 @@ public:
         const double stc_scale = Q0 / (2.0 * M_PI * bs_.s_bt);
         const int later = logm - (logm + groups - 1) / groups;
         const double boost = groups > 1 ? std::ldexp(1.0, later / 2) : 1.0;
-        sv.plan = make_boot_plan(logm + 1, groups, groups, cts_scale, stc_scale, boot_k(), boot_r(), boot_deg(), boost);
+        // packed form while the half-folded SlotToCoeff group stays small (offsets up to n + R)
+        const char* pk = std::getenv("AESFHE_SPARSE_PACK");  // "0": two EvalMods (A/B)
+        sv.packed = n <= 64 && !(pk && std::atoi(pk) == 0);
+        sv.plan = make_boot_plan(logm + 1, groups, groups, cts_scale, stc_scale, boot_k(), boot_r(), boot_deg(), boost, sv.packed);
         sv.cts.assign(sv.plan.cts.size(), {});
         sv.stc.assign(sv.plan.stc.size(), {});
         for (size_t i = 0; i < sv.cts.size(); ++i) sv.cts[i].g = &sv.plan.cts[i];
@@ -2464,6 +2468,27 @@ public:
         Ct w = lin_transform(u, sv ? sv->cts : bs_.cts);
         release(u);
         if (stop_after == 5) return w;
+        if (sv && sv->packed) {
+            // packed sparse form: w' + conj(w') = (Re w | Im w) per 2n block, one EvalMod, and
+            // SlotToCoeff's first group recombines the halves
+            Ct cj = conjugate(w);
+            Ct v = add_sub(w, cj, false);
+            release(w);
+            release(cj);
+            if (stop_after <= 9) return v;
+            Ct f = eval_mod(v);
+            release(v);
+            if (stop_after == 10) return f;
+            Ct out = lin_transform(f, sv->stc);
+            release(f);
+            cnt_[C_BOOT] += nb;
+            if (out.level > hp_.fresh) {
+                Ct o = level_down(out, hp_.fresh);
+                release(out);
+                out = o;
+            }
+            return out;
+        }
         // 6. real / imaginary parts (exact: conjugation, add, multiply by -i)
         Ct cj = conjugate(w);
         Ct re = add_sub(w, cj, false);

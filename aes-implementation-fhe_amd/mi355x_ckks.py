@@ -40,7 +40,7 @@ EXPORTED = [
     "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
     "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
     "aesfhe_streams", "aesfhe_bind_stream", "aesfhe_fork", "aesfhe_join", "aesfhe_settle",
-    "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_kernel_work", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan",
+    "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_kernel_work", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan", "aesfhe_debug_sparseplan",
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot", "aesfhe_create_keyed", "aesfhe_bootstrap_sparse", "aesfhe_bootstrap_pair_sparse",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_lut_create", "aesfhe_lut_eval", "aesfhe_lut_free",
     "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled",
@@ -113,6 +113,7 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_bootstrap_scaled"] = [vp, _H, c_dbl, _Hp]
     sig["aesfhe_bootstrap_pair_scaled"] = [vp, _H, _H, c_dbl, _Hp, _Hp]
     sig["aesfhe_debug_bootplan"] = [c_int, _dp]
+    sig["aesfhe_debug_sparseplan"] = [c_int, c_int, _dp]
     sig["aesfhe_debug_boot_stage"] = [vp, _H, c_int, _Hp]
     sig["aesfhe_export_sparse"] = [vp, _up]
     sig["aesfhe_boot_info"] = [vp, _dp]
@@ -731,4 +732,11 @@ def debug_bootplan(log_n: int = 16) -> np.ndarray:
     """Host self-check of the bootstrap plan (errors of StC, CtS, EvalMod polynomial)."""
     err = np.zeros(3)
     load_library().aesfhe_debug_bootplan(int(log_n), err)
+    return err
+
+
+def debug_sparseplan(n: int, pack: bool) -> np.ndarray:
+    """host self-check of a sparse bootstrap plan (aesfhe_debug_sparseplan): [StC error, CtS error]"""
+    err = np.zeros(2)
+    load_library().aesfhe_debug_sparseplan(int(n), int(bool(pack)), err)
     return err

@@ -185,6 +185,8 @@ int aesfhe_bootstrap_depth(void);
 /* host self-check of the bootstrap plan: err[0] SlotToCoeff, err[1] CoeffToSlot vs the
  * canonical embedding, err[2] EvalMod Chebyshev error (no GPU needed) */
 int aesfhe_debug_bootplan(int log_n, double* err3);
+/* the same self-check for a sparse (period-n) plan, packed real form or not: err2 = [StC, CtS] */
+int aesfhe_debug_sparseplan(int n, int pack, double* err2);
 /* debug: run bootstrap up to a stage (1..11, see engine.hip) and return that ciphertext */
 int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle ct, int stage, aesfhe_handle* out);
 /* ephemeral sparse secret (NTT form, all limbs) */

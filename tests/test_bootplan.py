@@ -17,3 +17,14 @@ def test_bootstrap_plan_factorisation(log_n):
 def test_bootstrap_depth():
     import mi355x_ckks
     assert mi355x_ckks.bootstrap_depth() == 15  # CtS 3 + EvalMod (Chebyshev PS 5 + 4 double angles) + StC 3
+
+
+@pytest.mark.parametrize("n,pack", [(16, True), (32, True), (64, True), (16, False), (1024, False)])
+def test_sparse_plan_factorisation(n, pack):
+    """the sparse (period-n, small-ring) plans: CoeffToSlot to the bit-reversed coefficient
+    halves (packed: the 2n-periodic (2 Re | 2 Im) real form), SlotToCoeff back"""
+    import build_ext
+    import mi355x_ckks
+    build_ext.build()
+    err = mi355x_ckks.debug_sparseplan(n, pack)
+    assert err[0] < 1e-10 and err[1] < 1e-10, err
