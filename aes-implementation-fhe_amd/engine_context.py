@@ -150,11 +150,23 @@ class EngineContext:
         self._bs_total_s += time.perf_counter() - t0
         return out
 
-    def bootstrap_pair_scaled(self, a, b, gain: float):
+    def bootstrap_pair_scaled(self, a, b, gain: float, period=None):
         """(gain * bootstrap(a), gain * bootstrap(b)), gain in (0, 1] at no extra level (the
-        true-FHE renorm, zeta16_noise_reducer.BootstrapSnap)"""
+        true-FHE renorm, zeta16_noise_reducer.BootstrapSnap); `period`: sparse-slot form"""
         t0 = time.perf_counter()
-        out = self.engine.bootstrap_pair_scaled(a, b, gain)
+        if period is not None:
+            out = self.engine.bootstrap_pair_sparse(a, b, period, gain)
+        else:
+            out = self.engine.bootstrap_pair_scaled(a, b, gain)
+        self._bs_count += 2
+        self._bs_total_s += time.perf_counter() - t0
+        return out
+
+    def bootstrap_pair_sparse(self, a, b, period: int):
+        """bootstrap_pair of two messages whose slots repeat with period `period` (the periodic
+        state layout, state_encoder.SlotLayout): the sparse-slot bootstrap"""
+        t0 = time.perf_counter()
+        out = self.engine.bootstrap_pair_sparse(a, b, period)
         self._bs_count += 2
         self._bs_total_s += time.perf_counter() - t0
         return out

@@ -14,15 +14,17 @@ from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap2
 
 
 class InvMixColumnsFHE:
-    def __init__(self, ctx, xor4: XOR4LUT, use_hard_renorm: bool = True, states: int = 1):
+    def __init__(self, ctx, xor4: XOR4LUT, use_hard_renorm: bool = True, states: int = 1, layout=None):
         self.ctx = ctx
         self.xor4 = xor4
         self.sc = ctx.engine.slot_count
-        self.stride = self.sc // 16
+        # states > 1: slot-packed batch; layout.periodic: the periodic layout (state_encoder.py)
+        self.enc = StateEncoder(ctx, states, periodic=bool(layout is not None and layout.periodic))
+        self.layout = self.enc.layout
+        self.stride = self.layout.unit
         self._coeffs = _CoeffCache()
-        self.enc = StateEncoder(ctx, states)  # states > 1: slot-packed batch (state_encoder.py)
         self.use_hard_renorm = use_hard_renorm
-        self._pt_row: List[Any] = row_masks(ctx, self.sc, states)
+        self._pt_row: List[Any] = row_masks(ctx, self.sc, states, self.layout)
         # with the renorm after every XOR pair, the LUTs run just above RENORM_FLOOR (utils.py)
         self._xor_level = RENORM_FLOOR if use_hard_renorm else None
         self._gf_level = RENORM_FLOOR + LUT2_DEPTH if use_hard_renorm else None
@@ -109,6 +111,6 @@ class InvMixColumnsFHE:
                 return self._xor_pair(x1, x2, fl)
             out = self._renorm_pair(*self._xor_pair(x1, x2, fl), level=last)
         if do_final_bootstrap and self.enc.renorm_hook is None:
-            out = bootstrap2(self.ctx, out[0], out[1])
+            out = bootstrap2(self.ctx, out[0], out[1], self.layout.boot_period)
         log("out", out)
         return out

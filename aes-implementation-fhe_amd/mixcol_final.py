@@ -125,13 +125,15 @@ def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo, out_level=Non
 
 
 class MixColFinal:
-    def __init__(self, ctx, xor4: XOR4LUT, stride: int | None = None, states: int = 1):
+    def __init__(self, ctx, xor4: XOR4LUT, stride: int | None = None, states: int = 1, layout=None):
         self.ctx = ctx
         self.xor4 = xor4
         self.sc = ctx.engine.slot_count
-        self.stride = stride if stride is not None else self.sc // 16
+        # states > 1: slot-packed batch; layout.periodic: the periodic layout (state_encoder.py)
+        self.enc = StateEncoder(ctx, states, periodic=bool(layout is not None and layout.periodic))
+        self.layout = self.enc.layout
+        self.stride = stride if stride is not None else self.layout.unit
         self._coeffs = _CoeffCache()
-        self.enc = StateEncoder(ctx, states)  # states > 1: slot-packed batch (state_encoder.py)
         self._zero = None
 
     # zero-state pair, built lazily (REF :58-62 builds it eagerly; only _normalize_via_xor_zero uses it)
@@ -218,6 +220,6 @@ class MixColFinal:
         out_hi, out_lo = acc
         # true-FHE mode: the renorm above already is a bootstrap (+ snap), the final one merges in
         if do_final_bootstrap and self.enc.renorm_hook is None:
-            out_hi, out_lo = bootstrap2(self.ctx, out_hi, out_lo)
+            out_hi, out_lo = bootstrap2(self.ctx, out_hi, out_lo, self.layout.boot_period)
             log("out", (out_hi, out_lo))
         return out_hi, out_lo

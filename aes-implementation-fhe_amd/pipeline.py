@@ -54,30 +54,43 @@ class AESPipeline:
     def __init__(self, ctx, coeffs: Dict[str, Any], *, mixcolumns: MixColFinal | None = None,
                  inv_mixcolumns: InvMixColumnsFHE | None = None, use_hard_renorm_between_steps: bool = False,
                  with_inv_mix_columns: bool = True, states: int = 1, fuse_sub_ark: bool = False,
-                 fuse_sr_mc: bool = False, true_fhe: bool = False):
+                 fuse_sr_mc: bool = False, true_fhe: bool = False, periodic: bool | None = None):
         self.ctx = ctx
         self.states = states
-        self.encoder = StateEncoder(ctx, states)
+        # periodic layout (state_encoder.SlotLayout): default on where the engine
+        # has the sparse-slot bootstrap and the state count is a power of two
+        if periodic is None:
+            periodic = getattr(ctx, "bootstrap_pair_sparse", None) is not None and states & (states - 1) == 0
+            for mod in (mixcolumns, inv_mixcolumns):
+                lay = getattr(mod, "layout", None)
+                if lay is not None:
+                    periodic = lay.periodic
+        self.encoder = StateEncoder(ctx, states, periodic=periodic)
+        self.layout = self.encoder.layout
         self.sc = ctx.engine.slot_count
-        self.stride = self.sc // 16
+        self.stride = self.layout.unit
         self.true_fhe = true_fhe
         # true-FHE: unit-magnitude XOR4 (REF/gen/generate_xor4_coeffs.py:17), so the snap sees codewords
         self.xor4 = XOR4LUT(ctx, np.asarray(coeffs["xor4"]) / 256.0 if true_fhe else coeffs["xor4"])
         self.sub = SubBytesLUT(ctx, coeffs["sub_hi"], coeffs["sub_lo"])
         self.isub = SubBytesLUT(ctx, coeffs["inv_sub_hi"], coeffs["inv_sub_lo"]) if "inv_sub_hi" in coeffs else None
-        self.shift = ShiftRows(ctx, states=states)
-        self.invshift = InvShiftRows(ctx, states=states)
-        self.mix = mixcolumns if mixcolumns is not None else MixColFinal(ctx, self.xor4, states=states)
-        self.invmix = inv_mixcolumns if inv_mixcolumns is not None else InvMixColumnsFHE(ctx, self.xor4, states=states)
+        self.shift = ShiftRows(ctx, states=states, layout=self.layout)
+        self.invshift = InvShiftRows(ctx, states=states, layout=self.layout)
+        self.mix = mixcolumns if mixcolumns is not None else MixColFinal(ctx, self.xor4, states=states, layout=self.layout)
+        self.invmix = (inv_mixcolumns if inv_mixcolumns is not None else
+                       InvMixColumnsFHE(ctx, self.xor4, states=states, layout=self.layout))
         for mod in (self.mix, self.invmix):
             enc = getattr(mod, "enc", None)
             if enc is not None and getattr(enc, "states", 1) != states:
                 raise ValueError("mixcolumns / inv_mixcolumns were built for a different states-per-ciphertext count")
+            lay = getattr(mod, "layout", None)
+            if lay is not None and not self.layout.same(lay):
+                raise ValueError("mixcolumns / inv_mixcolumns were built for a different slot layout")
         self.ark = AddRoundKey(self.xor4)
         self.snapper = None
         if true_fhe:
             from zeta16_noise_reducer import BootstrapSnap
-            self.snapper = BootstrapSnap(ctx)
+            self.snapper = BootstrapSnap(ctx, period=self.layout.boot_period)
             for enc in (self.encoder, getattr(self.mix, "enc", None), getattr(self.invmix, "enc", None)):
                 if enc is not None:
                     enc.renorm_hook = self.snapper.apply_pair

@@ -24,26 +24,24 @@ def shift_rows_bytes(state: np.ndarray, direction: int = -1) -> np.ndarray:
     return out.reshape(s.shape)
 
 
-def row_masks(ctx, sc: int, states: int = 1) -> List[Any]:
-    stride = sc // 16
-    masks = []
-    for r in range(4):
-        m = np.zeros(sc, dtype=np.complex128)
-        for c in range(4):
-            m[(r + 4 * c) * stride:(r + 4 * c) * stride + states] = 1.0
-        masks.append(ctx.encode(m))
-    return masks
+def row_masks(ctx, sc: int, states: int = 1, layout=None) -> List[Any]:
+    """the four row masks (REF/shift_rows.py:20-33) in `layout` (default: the reference's)"""
+    from state_encoder import SlotLayout
+    lay = layout or SlotLayout(sc, states)
+    return [ctx.encode(lay.row_mask(r)) for r in range(4)]
 
 
 class ShiftRows:
     direction = -1
 
-    def __init__(self, ctx, states: int = 1):
+    def __init__(self, ctx, states: int = 1, layout=None):
+        from state_encoder import SlotLayout
         self.ctx = ctx
         self.sc = ctx.engine.slot_count
-        self.stride = self.sc // 16
+        self.layout = layout or SlotLayout(self.sc, states)
+        self.stride = self.layout.unit
         self.states = states
-        self._pt_masks = row_masks(ctx, self.sc, states)
+        self._pt_masks = row_masks(ctx, self.sc, states, self.layout)
         self._rot_steps = [self.direction * 4 * r * self.stride for r in range(4)]
 
     def _apply_one(self, ct: Any) -> Any:

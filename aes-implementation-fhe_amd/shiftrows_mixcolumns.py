@@ -32,8 +32,9 @@ class ShiftRowsMixColumnsFusedEnc:
         self.ctx = ctx
         self.mix = mix
         self.sc = ctx.engine.slot_count
-        self.stride = self.sc // 16
-        self.masks = row_masks(ctx, self.sc, states)  # D_r
+        layout = getattr(mix, "layout", None)  # mix may be None in the plain-slot tests
+        self.stride = layout.unit if layout is not None else self.sc // 16
+        self.masks = row_masks(ctx, self.sc, states, layout)  # D_r
 
     def _shifts(self, ct) -> Dict[int, Any]:
         """{k: Y_k} for one nibble ciphertext"""

@@ -8,6 +8,13 @@ REF/main.py:121-140): state b of a batch of B <= stride states holds byte i in s
 i*stride + b.  Every rotation the AES modules issue is a multiple of stride, so the B
 columns never mix; slots with (j mod stride) >= B hold 1+0j as in the reference.
 ``encode`` then takes a (B, 16) uint8 array and ``decode`` returns one.
+
+``periodic=True`` (the pipeline's default) packs the same bytes with rotation
+unit B instead of stride: byte i of state b in slot i*B + b, and that 16B-slot block repeated
+over all slots.  Every AES step is slot-wise or a rotation by a multiple of the unit, so the
+message stays 16B-periodic -- a polynomial in the subring Z[X^(N/32B)] -- and the final
+bootstraps of MixColumns / InvMixColumns run as sparse-slot bootstraps (aesfhe_bootstrap_pair_sparse,
+a trace plus period-sized transforms).  Decoded states are the same in both layouts.
 """
 import os
 from typing import Any, Tuple
@@ -20,13 +27,50 @@ from utils import ZetaEncoder
 _RENORM_FRESH = os.environ.get("AESFHE_RENORM_FRESH") == "1"
 
 
+class SlotLayout:
+    """Where the bytes of B states sit: the reference layout (byte i of state b in slot
+    i*stride + b, stride = slot_count/16, every other slot 1) or the periodic one (unit = B, the
+    16B-slot block repeated).  `unit` is the rotation unit of ShiftRows / MixColumns."""
+
+    def __init__(self, sc: int, states: int = 1, periodic: bool = False):
+        if not 1 <= states <= sc // 16:
+            raise ValueError(f"states per ciphertext must be in [1, {sc // 16}], got {states}")
+        if periodic and states & (states - 1):
+            raise ValueError("the periodic layout needs a power-of-two number of states")
+        self.sc, self.states, self.periodic = sc, states, periodic
+        self.unit = states if periodic else sc // 16
+        self.period = 16 * self.unit
+
+    @property
+    def boot_period(self):
+        """the slot period a sparse bootstrap may use (None: the full-slot bootstrap)"""
+        return self.period if self.period < self.sc else None
+
+    @property
+    def renorm_states(self) -> int:
+        """the engine renorm's `states` (periodic: every slot holds state data)"""
+        return self.sc // 16 if self.periodic else self.states
+
+    def tile(self, block: np.ndarray) -> np.ndarray:
+        return np.tile(block, self.sc // self.period)
+
+    def row_mask(self, r: int) -> np.ndarray:
+        """ones on row r (bytes r + 4c) of every state"""
+        m = np.zeros(self.period, dtype=np.complex128)
+        for c in range(4):
+            m[(r + 4 * c) * self.unit:(r + 4 * c) * self.unit + self.states] = 1.0
+        return self.tile(m)
+
+    def same(self, other) -> bool:
+        return other is not None and (self.sc, self.states, self.periodic) == (other.sc, other.states, other.periodic)
+
+
 class StateEncoder:
-    def __init__(self, ctx, states: int = 1):
+    def __init__(self, ctx, states: int = 1, periodic: bool = False):
         self.ctx = ctx
         self.sc = ctx.engine.slot_count
-        self.stride = self.sc // 16
-        if not 1 <= states <= self.stride:
-            raise ValueError(f"states per ciphertext must be in [1, {self.stride}], got {states}")
+        self.layout = SlotLayout(self.sc, states, periodic)
+        self.stride = self.layout.unit  # rotation unit (REF: slot_count / 16)
         self.states = states
         # set by AESPipeline(true_fhe=True): renorm(hi, lo) -> hook(hi, lo), the bootstrap + snap
         # that replaces the secret-key renorm (zeta16_noise_reducer.BootstrapSnap)
@@ -41,11 +85,10 @@ class StateEncoder:
         return state
 
     def _pack(self, nibbles: np.ndarray) -> np.ndarray:
-        """nibbles (B, 16) -> slot vector; slot i*stride + b <- zeta^nibbles[b, i]"""
-        vec = np.ones(self.sc, dtype=np.complex128)
-        grid = vec[:16 * self.stride].reshape(16, self.stride)
+        """nibbles (B, 16) -> slot vector; slot i*unit + b <- zeta^nibbles[b, i] (periodic: tiled)"""
+        grid = np.ones((16, self.stride), dtype=np.complex128)
         grid[:, :nibbles.shape[0]] = ZetaEncoder.to_zeta(nibbles.astype(np.uint8).T, 16)
-        return vec
+        return self.layout.tile(grid.reshape(-1))
 
     def _take(self, slots: np.ndarray) -> np.ndarray:
         """slot vector -> (B, 16) state slots"""
@@ -69,7 +112,8 @@ class StateEncoder:
             return self.renorm_hook(ct_hi, ct_lo, level)
         fast = getattr(self.ctx, "renorm_pair", None)
         if fast is not None:
+            st = self.layout.renorm_states
             if level is not None and not _RENORM_FRESH:
-                return fast(ct_hi, ct_lo, states=self.states, level=level)
-            return fast(ct_hi, ct_lo) if self.states == 1 else fast(ct_hi, ct_lo, states=self.states)
+                return fast(ct_hi, ct_lo, states=st, level=level)
+            return fast(ct_hi, ct_lo) if st == 1 else fast(ct_hi, ct_lo, states=st)
         return self.encode(self.decode(ct_hi, ct_lo))

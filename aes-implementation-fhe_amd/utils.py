@@ -69,10 +69,14 @@ def pair(ctx, fa, fb, shared=()):
     return a, b
 
 
-def bootstrap2(ctx, a, b):
+def bootstrap2(ctx, a, b, period=None):
     """(bootstrap(a), bootstrap(b)) of the hi / lo halves (REF/mixcol_final.py:158-162): one
     batched engine bootstrap when the context has it (identical results, shared key and
-    diagonal reads), else the two calls on the two branch streams"""
+    diagonal reads), else the two calls on the two branch streams.  `period`:
+    the messages' slot period in the periodic layout -> the sparse-slot bootstrap (§4b)"""
+    sparse = getattr(ctx, "bootstrap_pair_sparse", None)
+    if period is not None and sparse is not None:
+        return sparse(ctx.to_intt(a), ctx.to_intt(b), period)
     both = getattr(ctx, "bootstrap_pair", None)
     if both is not None and os.environ.get("AESFHE_BOOT_PAIR", "1") != "0":  # "0": A/B measurements
         return both(ctx.to_intt(a), ctx.to_intt(b))

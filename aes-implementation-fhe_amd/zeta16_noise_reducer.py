@@ -107,11 +107,12 @@ class Zeta16Snap15:
 class BootstrapSnap:
     """True-FHE renorm of a (hi, lo) pair: scaled bootstrap, then the depth-4 snap."""
 
-    def __init__(self, ctx, snap: Zeta16Snap15 | None = None):
+    def __init__(self, ctx, snap: Zeta16Snap15 | None = None, period: int | None = None):
         if getattr(ctx, "bootstrap_pair_scaled", None) is None:
             raise RuntimeError("true-FHE renorm needs the engine's scaled pair bootstrap (bootstrappable context)")
         self.ctx = ctx
         self.snap = snap or Zeta16Snap15(ctx)
+        self.period = period  # the states' slot period (periodic layout): sparse-slot bootstraps
 
     def apply_pair(self, ct_hi, ct_lo, level=None) -> Tuple[Any, Any]:
         """level: what the next step needs (the pipeline's renorm hint); None or <= 8 (an XOR4,
@@ -119,7 +120,10 @@ class BootstrapSnap:
         ctx = self.ctx
         fresh = ctx.engine.fresh_level
         twice = (level is None or level <= DOUBLE_SNAP_MAX_LEVEL) and fresh - 2 * SNAP15_DEPTH - 1 >= (level or 0)
-        uh, ul = ctx.bootstrap_pair_scaled(ctx.to_intt(ct_hi), ctx.to_intt(ct_lo), self.snap.kappa)
+        if self.period is not None:
+            uh, ul = ctx.bootstrap_pair_scaled(ctx.to_intt(ct_hi), ctx.to_intt(ct_lo), self.snap.kappa, self.period)
+        else:
+            uh, ul = ctx.bootstrap_pair_scaled(ctx.to_intt(ct_hi), ctx.to_intt(ct_lo), self.snap.kappa)
         sn = self.snap
         if twice:
             return pair(ctx, lambda: sn.apply(sn.apply_scaled(uh)), lambda: sn.apply(sn.apply_scaled(ul)), shared=(uh, ul))

@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--profile-every", type=int, default=8,
                     help="time one launch in N of the roofline kernels (live sample over the timed region)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ref-layout", action="store_true",
+                    help="the reference's slot layout (byte i at slot i*N/32, full-slot bootstraps) instead of the periodic "
+                         "one (sparse-slot bootstraps, DESIGN.md 4b); A/B only")
     ap.add_argument("--no-final-bootstrap", action="store_true",
                     help="diagnostic only: skip MixColFinal's final bootstrap (not the benchmark workload)")
     ap.add_argument("--eager", action="store_true", help="relinearise and rescale after every product (no deferred evaluation)")
@@ -182,6 +185,7 @@ class _NoFinalBootstrap:
 
     def __init__(self, mix):
         self.mix = mix
+        self.layout = mix.layout
 
     def __call__(self, ct_hi, ct_lo, **kw):
         return self.mix(ct_hi, ct_lo, do_final_bootstrap=False)
@@ -356,10 +360,12 @@ def main():
     ctx = EngineContext(signature=signature, max_level=17, thread_count=1, device_id=local, seed=seed, lazy=not args.eager,
                         concurrent=not args.serial)
     xor4 = XOR4LUT(ctx, coeffs["xor4"])
-    mix = MixColFinal(ctx, xor4)
+    from state_encoder import SlotLayout
+    layout = SlotLayout(ctx.engine.slot_count, 1, periodic=not args.ref_layout)
+    mix = MixColFinal(ctx, xor4, layout=layout)
     if args.no_final_bootstrap:
         mix = _NoFinalBootstrap(mix)
-    pipe = AESPipeline(ctx, coeffs, mixcolumns=mix, use_hard_renorm_between_steps=True)
+    pipe = AESPipeline(ctx, coeffs, mixcolumns=mix, use_hard_renorm_between_steps=True, periodic=layout.periodic)
 
     np.random.seed(7)
     key = np.random.randint(0, 256, 16, dtype=np.uint8)
@@ -455,6 +461,9 @@ def main():
         "config": {"workload": "C2: full AES-128 encrypt (10 rounds), 1 packed state per ciphertext pair, "
                                "N=2^16, renorm on" + ("" if not args.no_final_bootstrap else ", FINAL BOOTSTRAP SKIPPED"),
                    "log_n": 16, "states_per_rank_per_step": 1, "parallelism": f"replicas x{world}",
+                   "slot_layout": ("reference (byte i at slot i*N/32; full-slot bootstraps)" if args.ref_layout else
+                                   "periodic (the 16-slot state block repeated; MixColumns' final bootstraps as "
+                                   "sparse-slot bootstraps, DESIGN.md 4b)"),
                    "evaluation": "eager (relinearise + rescale after every product)" if args.eager else
                    ("optimised evaluation, same module interfaces and outputs: deferred relinearisation/rescale "
                     "(DESIGN.md 3.7), fused LUT kernels with one relinearisation per LUT, XOR4/GF LUTs over a conjugate "

@@ -153,3 +153,23 @@ def test_sparse_bootstrap_periodic_message(ctx, period):
     assert np.abs(ctx.decrypt(pb) - zb).max() < BOOT_TOL
     with pytest.raises(RuntimeError, match="period"):
         E.bootstrap_sparse(a, 24)
+
+
+def test_config2_reference_layout_roundtrip(ctx, coeff_dir):
+    """the reference's slot layout (AESPipeline(periodic=False): byte i at slot i*N/32, full-slot
+    bootstraps) gives the same ciphertext bytes as the default periodic layout"""
+    from aes_keyschedule import expand_aes128_key, load_all_coeffs
+    from oracle import aes_plain
+    from pipeline import AESPipeline
+    co = load_all_coeffs(coeff_dir)
+    np.random.seed(11)
+    rks = expand_aes128_key(np.random.randint(0, 256, 16, dtype=np.uint8))
+    pt = np.random.randint(0, 256, 16, dtype=np.uint8)
+    ref = AESPipeline(ctx, co, use_hard_renorm_between_steps=True, periodic=False)
+    per = AESPipeline(ctx, co, use_hard_renorm_between_steps=True)
+    assert not ref.layout.periodic and per.layout.periodic and per.layout.boot_period == 16
+    want = aes_plain.ref_encrypt(pt, rks)
+    ct_ref, ct_per = ref.encrypt(pt, rks), per.encrypt(pt, rks)
+    assert np.array_equal(ref.encoder.decode(*ct_ref), want)
+    assert np.array_equal(per.encoder.decode(*ct_per), want)
+    assert np.array_equal(ref.encoder.decode(*ref.decrypt(*ct_ref, rks)), pt)

@@ -117,3 +117,40 @@ def test_golden_packed_encrypt_decrypt(coeff_dir):
         assert bytes(stages[tag][2]) == bytes(v), tag
     back = G.decode_state(*g.decrypt(ct, rks), B)
     assert np.array_equal(back, states)
+
+
+@pytest.mark.parametrize("states", [1, 4])
+def test_periodic_layout(states):
+    """periodic layout (state_encoder.SlotLayout): the 16B-slot block repeated,
+    rotation unit B; ShiftRows / InvShiftRows and MixColumns' column shifts act per state exactly
+    as on the reference layout, and the vectors stay 16B-periodic (the sparse bootstrap's premise)"""
+    from shift_rows import ShiftRows
+    from inv_shiftrows import InvShiftRows
+    from state_encoder import StateEncoder
+    ctx = _SlotCtx()
+    enc = StateEncoder(ctx, states, periodic=True)
+    lay = enc.layout
+    assert lay.unit == states and lay.period == 16 * states and lay.renorm_states == 16
+    assert lay.boot_period == (16 * states if 16 * states < 256 else None)
+    rng = np.random.default_rng(10 + states)
+    st = rng.integers(0, 256, (states, 16), dtype=np.uint8)
+    hi, lo = enc.encode(st[0] if states == 1 else st)
+    P = lay.period
+    assert np.allclose(hi, np.tile(hi[:P], 256 // P)) and np.allclose(lo, np.tile(lo[:P], 256 // P))
+    for b in range(states):
+        for i in range(16):
+            assert np.isclose(hi[i * states + b], np.exp(-2j * np.pi * (st[b, i] >> 4) / 16))
+    assert np.array_equal(enc.decode(hi, lo), st[0] if states == 1 else st)
+    sr, isr = ShiftRows(ctx, states, layout=lay), InvShiftRows(ctx, states, layout=lay)
+    h2, l2 = sr.apply(hi, lo)
+    want = np.stack([A.shift_rows(s) for s in st])
+    assert np.array_equal(enc.decode(h2, l2), want[0] if states == 1 else want)
+    assert np.allclose(h2, np.tile(h2[:P], 256 // P))
+    h3, l3 = isr.apply(h2, l2)
+    assert np.array_equal(enc.decode(h3, l3), st[0] if states == 1 else st)
+    # MixColumns' column shift by k (mixcol_final._col_shift_rowmajor): rotate by -4 k unit
+    for k in (1, 2, 3):
+        r = np.roll(hi, -4 * k * lay.unit)
+        got = enc.decode(r, np.roll(lo, -4 * k * lay.unit))
+        exp = np.stack([np.roll(s.reshape(4, 4), -k, axis=0).reshape(16) for s in st])
+        assert np.array_equal(got, exp[0] if states == 1 else exp), k
