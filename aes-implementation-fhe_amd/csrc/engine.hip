@@ -1714,8 +1714,17 @@ public:
     // level >= 0 re-encrypts at min(level, fresh) instead of the fresh level:
     // callers that know what the next step needs save the limbs
     void renorm_pair(aesfhe_handle hh, aesfhe_handle hl, aesfhe_handle* oh, aesfhe_handle* ol) { renorm_states(hh, hl, 1, oh, ol); }
-    void renorm_states(aesfhe_handle hh, aesfhe_handle hl, int states, aesfhe_handle* oh, aesfhe_handle* ol, int level = -1) {
+    // period > 0: the periodic layout (slot j == slot j mod period, state_encoder.SlotLayout):
+    // period 16 decodes / re-encodes its 16 slots directly (5^i positions), other periods snap
+    // every slot (states = slot_count / 16)
+    void renorm_states(aesfhe_handle hh, aesfhe_handle hl, int states, aesfhe_handle* oh, aesfhe_handle* ol, int level = -1,
+                       int period = 0) {
         if (!d_pk_) throw std::runtime_error("keys not generated");
+        if (period > 0) {
+            if (period & (period - 1) || period < 16 || period > slot_count()) throw std::runtime_error("renorm: bad period");
+            states = period == 16 ? 1 : slot_count() / 16;
+        }
+        const bool per16 = period == 16;
         if (level > hp_.fresh) level = hp_.fresh;  // never above a fresh encryption
         const int n = hp_.n, s = slot_count(), stride = s / 16;
         if (states < 1 || states > stride)
@@ -1733,6 +1742,7 @@ public:
             u64 e = 1;
             for (int j = 0; j < s; ++j) {
                 if (j % stride == 0) slots_.e[j / stride] = (u32)e;
+                if (j < 16) slots_p_.e[j] = (u32)e;
                 e = e * 5 % two_n;
             }
             for (int k = 0; k < kStreams; ++k) {
@@ -1773,9 +1783,10 @@ public:
             double* acc = d_codec_[t_sidx];
             double* wv = acc + 64;
             HIP_OK(hipMemsetAsync(acc, 0, 64 * sizeof(double), S()));
-            launch_decode16(S(), T_, x, kd, cc, slots_, isc, acc);
+            const Slot16& sl = per16 ? slots_p_ : slots_;
+            launch_decode16(S(), T_, x, kd, cc, sl, isc, acc);
             launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
-            launch_encode16(S(), T_, m, wv, slots_, enc_scale, nq);
+            launch_encode16(S(), T_, m, wv, sl, enc_scale, nq, per16);
         } else {
             double*& zbuf = d_fft_[t_sidx];
             if (!zbuf) zbuf = (double*)dev_alloc((size_t)2 * 2 * 2 * 2 * n);  // 2 buffers x [2][N] complex double
@@ -2961,7 +2972,8 @@ private:
     u64 cnt_[C_N] = {};
     CrtConsts crt_[4] = {};
     std::unordered_map<aesfhe_handle, Lut> luts_;
-    Slot16 slots_ = {};
+    Slot16 slots_ = {};    // the reference layout's 16 state slots, 5^(i N/32)
+    Slot16 slots_p_ = {};  // the 16-periodic layout's, 5^i
     double* d_codec_[kStreams] = {};
     int* d_nib_[kStreams] = {};
     double* d_fft_[kStreams] = {};  // slot-packed renorm: [2 buffers][2 cts][N] complex double
@@ -3256,6 +3268,11 @@ int aesfhe_boot_info(aesfhe_ctx* ctx, double* out) {
 }
 int aesfhe_renorm_pair(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle* out_hi, aesfhe_handle* out_lo) {
     API_BEGIN ctx->eng->renorm_pair(hi, lo, out_hi, out_lo);
+    API_END
+}
+int aesfhe_renorm_periodic(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, int period, int level, aesfhe_handle* out_hi,
+                           aesfhe_handle* out_lo) {
+    API_BEGIN ctx->eng->renorm_states(hi, lo, 1, out_hi, out_lo, level, period);
     API_END
 }
 int aesfhe_renorm_states(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, int states, aesfhe_handle* out_hi,

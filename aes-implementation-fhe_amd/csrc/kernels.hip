@@ -526,20 +526,24 @@ __global__ void k_snap16(const double* acc, double* w, int* nib) {
     w[2 * t + 1] = sn;
 }
 
+// kmask = 0: the reference layout (16 slots deviate from 1; every coefficient, factor 2/N);
+// kmask = N/32 - 1: the 16-periodic layout (slot j == slot j mod 16, sl.e = 5^i): only the
+// coefficients k == 0 mod N/32 are nonzero, m_k = (1/16) sum_i Re(w_i zeta^(-e_i k)) (+1 at k = 0)
 __global__ void __launch_bounds__(kBlock) k_encode16(u32* out, const double* w, Slot16 sl, double scale, int nq, const PrimeConst* pc,
-                                                     int logn) {
+                                                     int logn, u32 kmask, double fac) {
     const int c = blockIdx.y;
     const int n = 1 << logn;
     const int k = blockIdx.x * kBlock + threadIdx.x;
     const u32 mask = 2u * n - 1;
     const double inv_n = 1.0 / n;
     double v = 0.0;
-    for (int i = 0; i < 16; ++i) {
-        double sn, cs;
-        sincospi((double)((sl.e[i] * (u32)k) & mask) * inv_n, &sn, &cs);
-        v += w[c * 32 + 2 * i] * cs + w[c * 32 + 2 * i + 1] * sn;
-    }
-    v = v * 2.0 * inv_n + (k == 0 ? 1.0 : 0.0);
+    if (((u32)k & kmask) == 0)
+        for (int i = 0; i < 16; ++i) {
+            double sn, cs;
+            sincospi((double)((sl.e[i] * (u32)k) & mask) * inv_n, &sn, &cs);
+            v += w[c * 32 + 2 * i] * cs + w[c * 32 + 2 * i + 1] * sn;
+        }
+    v = v * fac + (k == 0 ? 1.0 : 0.0);
     const double x = rint(v * scale);
     for (int t = 0; t < nq; ++t) {
         const double q = (double)pc[t].q;
@@ -1030,9 +1034,12 @@ void launch_snap16(hipStream_t st, const double* acc, double* w, int* nib) {
     hipLaunchKernelGGL(k_snap16, dim3(1), dim3(64), 0, st, acc, w, nib);
     launch_check();
 }
-void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq) {
+void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq, bool periodic) {
+    const u32 n = 1u << T.logn;
+    const u32 kmask = periodic ? n / 32 - 1 : 0u;
+    const double fac = periodic ? 1.0 / 16.0 : 2.0 / n;
     prof_launch(KID_ELEMENTWISE, words(2.0 * nq * (1u << T.logn)), k_encode16, dim3((1u << T.logn) / kBlock, 2), dim3(kBlock), 0, st, out,
-                w, sl, scale, nq, T.pc, T.logn);
+                w, sl, scale, nq, T.pc, T.logn, kmask, fac);
 }
 
 void launch_decode_twist(hipStream_t st, const DevTables& T, const u32* x, const int kd[2], const CrtConsts cc[2],

@@ -223,6 +223,10 @@ class EngineContext:
         `level`: re-encrypt at that level instead of the fresh one."""
         return self.engine.renorm_pair(hi, lo, states, level)
 
+    def renorm_periodic(self, hi, lo, period: int, level=None):
+        """renorm_pair for the periodic state layout (state_encoder.SlotLayout)"""
+        return self.engine.renorm_periodic(hi, lo, period, level)
+
     def _init_lut_cache(self):
         self._luts = {}                                  # digest -> LookupTable
         self._lut_pinned = set()                         # digests requested without an owner

@@ -41,7 +41,7 @@ EXPORTED = [
     "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
     "aesfhe_streams", "aesfhe_bind_stream", "aesfhe_fork", "aesfhe_join", "aesfhe_settle",
     "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_kernel_work", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan", "aesfhe_debug_sparseplan",
-    "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot", "aesfhe_create_keyed", "aesfhe_bootstrap_sparse", "aesfhe_bootstrap_pair_sparse",
+    "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot", "aesfhe_create_keyed", "aesfhe_bootstrap_sparse", "aesfhe_bootstrap_pair_sparse", "aesfhe_renorm_periodic",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_lut_create", "aesfhe_lut_eval", "aesfhe_lut_free",
     "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled",
 ]
@@ -119,6 +119,7 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_boot_info"] = [vp, _dp]
     sig["aesfhe_debug_lin_group"] = [vp, _H, c_int, _Hp]
     sig["aesfhe_create_boot"] = [pp, c_int, c_int, c_int, c_int, ctypes.c_uint64]
+    sig["aesfhe_renorm_periodic"] = [vp, _H, _H, c_int, c_int, _Hp, _Hp]
     sig["aesfhe_bootstrap_sparse"] = [vp, _H, c_int, c_dbl, _Hp]
     sig["aesfhe_bootstrap_pair_sparse"] = [vp, _H, _H, c_int, c_dbl, _Hp, _Hp]
     sig["aesfhe_create_keyed"] = [pp, c_int, c_int, c_int, c_int, ctypes.c_char_p, c_int]
@@ -575,6 +576,13 @@ class Engine:
         else:
             rc = self._lib.aesfhe_renorm_states(self._ctx.ptr, hi.handle, lo.handle, int(states), ctypes.byref(a), ctypes.byref(b))
         self._ctx.check(rc)
+        return Ciphertext(self._ctx, a.value), Ciphertext(self._ctx, b.value)
+
+    def renorm_periodic(self, hi, lo, period: int, level=None):
+        """secret-key renorm of a pair in the periodic layout (aesfhe_renorm_periodic)"""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        self._ctx.check(self._lib.aesfhe_renorm_periodic(self._ctx.ptr, hi.handle, lo.handle, int(period),
+                                                         -1 if level is None else int(level), ctypes.byref(a), ctypes.byref(b)))
         return Ciphertext(self._ctx, a.value), Ciphertext(self._ctx, b.value)
 
     def sync(self):

@@ -110,6 +110,9 @@ class StateEncoder:
         With a renorm_hook (true-FHE mode) the hook runs instead (it reads `level` as the next step's need)."""
         if self.renorm_hook is not None:
             return self.renorm_hook(ct_hi, ct_lo, level)
+        per = getattr(self.ctx, "renorm_periodic", None)
+        if self.layout.periodic and per is not None:
+            return per(ct_hi, ct_lo, self.layout.period, None if _RENORM_FRESH else level)
         fast = getattr(self.ctx, "renorm_pair", None)
         if fast is not None:
             st = self.layout.renorm_states

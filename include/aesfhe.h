@@ -177,6 +177,11 @@ int aesfhe_bootstrap_scaled(aesfhe_ctx* ctx, aesfhe_handle ct, double gain, aesf
  * Replaces the same engine.bootstrap calls (REF/engine_context.py:147-162) when the caller
  * knows its layout is periodic (StateEncoder(periodic=True)). */
 int aesfhe_bootstrap_sparse(aesfhe_ctx* ctx, aesfhe_handle ct, int period, double gain, aesfhe_handle* out);
+/* Secret-key renorm of a (hi, lo) pair in the periodic layout (slot j == slot j mod period,
+ * a power of two >= 16): period 16 decodes / re-encodes its 16 slots directly, other periods
+ * snap every slot; level < 0 = the fresh level (as aesfhe_renorm_at otherwise). */
+int aesfhe_renorm_periodic(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, int period, int level, aesfhe_handle* out_hi,
+                           aesfhe_handle* out_lo);
 int aesfhe_bootstrap_pair_sparse(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int period, double gain, aesfhe_handle* out_a,
                                  aesfhe_handle* out_b);
 int aesfhe_bootstrap_pair_scaled(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, double gain, aesfhe_handle* out_a,

@@ -173,3 +173,22 @@ def test_config2_reference_layout_roundtrip(ctx, coeff_dir):
     assert np.array_equal(ref.encoder.decode(*ct_ref), want)
     assert np.array_equal(per.encoder.decode(*ct_per), want)
     assert np.array_equal(ref.encoder.decode(*ref.decrypt(*ct_ref, rks)), pt)
+
+
+@pytest.mark.parametrize("states", [1, 4])
+def test_periodic_renorm(ctx, states):
+    """aesfhe_renorm_periodic: the periodic layout's secret-key renorm (period 16: the direct
+    16-slot codec at positions 5^i; other periods: every slot snapped) returns the snapped,
+    re-encrypted periodic vector at the requested level"""
+    from state_encoder import StateEncoder
+    E = ctx.engine
+    enc = StateEncoder(ctx, states, periodic=True)
+    rng = np.random.default_rng(30 + states)
+    st = rng.integers(0, 256, (states, 16), dtype=np.uint8)
+    hi, lo = enc.encode(st[0] if states == 1 else st)
+    hi, lo = E.multiply(hi, 1.0 + 0.01j), E.multiply(lo, 1.0 - 0.01j)  # a small phase error to snap away
+    rh, rl = enc.renorm(hi, lo, level=11)
+    assert rh.level == rl.level == 11
+    assert np.array_equal(enc.decode(rh, rl), st[0] if states == 1 else st)
+    clean_hi, _ = enc.encode(st[0] if states == 1 else st)
+    assert np.abs(ctx.decrypt(rh) - ctx.decrypt(clean_hi)).max() < 1e-3
