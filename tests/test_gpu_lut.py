@@ -145,6 +145,28 @@ def test_lut_free(pair):
     assert out.level == top - 1  # the ciphertext is untouched
 
 
+def test_lut_cache_same_label_different_sets():
+    """a deterministic regression for the stale-coefficient failure -- two
+    coefficient sets requested under ONE caller label (as an id() reused after collection would
+    produce) get two device sets, and each evaluates to its own polynomial"""
+    ctx = gpu_context(log_n=16, signature=2)
+    E = ctx.engine
+    rng = np.random.default_rng(25)
+    z = np.exp(2j * np.pi * rng.random(E.slot_count))
+    x = ctx.encrypt(z)
+    pb = ctx.make_power_basis(x, 3)
+    label = ("sb", 140000000000000)
+    c1 = np.array([0.5, -0.25 + 0.1j, 0.3])
+    c2 = np.array([-0.2, 0.4, 0.1 - 0.3j])
+    l1 = ctx.lut(label, c1, 0.1)
+    l2 = ctx.lut(label, c2, 0.1)
+    assert l1 is not l2
+    for c, lut in ((c1, l1), (c2, l2)):
+        out = ctx.decrypt(ctx.lut_eval(lut, pb))
+        want = 0.1 + c[0] * z + c[1] * z ** 2 + c[2] * z ** 3
+        assert np.abs(out - want).max() < 1e-3
+
+
 # ---------------------------------------------------------------- module level, fused vs loop
 @pytest.fixture(scope="module")
 def coeffs(coeff_dir):
