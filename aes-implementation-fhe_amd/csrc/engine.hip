@@ -1893,6 +1893,44 @@ public:
         std::vector<BootGroupDev> cts, stc;
     };
     std::map<int, SparseBoot> sparse_;
+    bool trace4_ = std::getenv("AESFHE_TRACE4") ? std::atoi(std::getenv("AESFHE_TRACE4")) != 0 : true;
+    // x + rot(x, -a) + rot(x, -2a) + rot(x, -3a) for the nb members of x: the three rotations
+    // hoisted (one ModUp of c1, key inner products read through each automorphism) and summed
+    // in Q*P (one ModDown adding c0 + the permuted c0s and c1) -- two trace doublings for ~1.5
+    // rotations' work
+    Ct trace4(const Ct& x_in, int a) {
+        if (vis_npoly(x_in) != 2) throw std::runtime_error("trace4: 2-polynomial ciphertext expected");
+        Ct x = normalize(x_in);
+        const int l = x.level, nl = hp_.nl(l), ne = nl + hp_.n_p, n = hp_.n, nb = x.nb;
+        const size_t qs = (size_t)2 * nl * n;
+        const u32* c1 = x.data + (size_t)nl * n;
+        u32* ext = modup(c1, l, nb, qs);
+        u32* acc = tmp(2 * (size_t)ne * nb);
+        u32* perm = tmp(3 * (size_t)nl * nb);
+        for (int j = 1; j <= 3; ++j) {
+            const u64 g = rot_galois(-j * a);
+            key_inner(acc, ext, c1, ksk(g), l, g, nb, qs, KsFold{}, j > 1);
+            for (int m = 0; m < nb; ++m)
+                launch_automorph(S(), T_, perm + ((size_t)(j - 1) * nb + m) * nl * n, x.data + (size_t)m * qs, g, nl);
+        }
+        untmp(ext, (size_t)nb * ext_rows(l));
+        u32* c0s = tmp(2 * (size_t)nl * nb);  // member stride qs, first nl rows used (moddown's add0)
+        for (int m = 0; m < nb; ++m) {
+            MemberPtrs mp;
+            mp.src[0] = x.data + (size_t)m * qs;
+            for (int j = 1; j <= 3; ++j) mp.src[j] = perm + ((size_t)(j - 1) * nb + m) * nl * n;
+            launch_add_members(S(), T_, c0s + (size_t)m * qs, mp, 4, nl, qmap(), false);
+        }
+        untmp(perm, 3 * (size_t)nl * nb);
+        Ct o = moddown(acc, l, c0s, c1, nb, qs);
+        o.ntt = x.ntt;
+        untmp(acc, 2 * (size_t)ne * nb);
+        untmp(c0s, 2 * (size_t)nl * nb);
+        if (x.data != x_in.data) release(x);
+        cnt_[C_ROT] += 3 * nb;
+        cnt_[C_KS] += 3 * nb;
+        return o;
+    }
     SparseBoot& sparse_variant(int n) {
         auto it = sparse_.find(n);
         if (it != sparse_.end()) return it->second;
@@ -2467,12 +2505,20 @@ public:
         // 4b. sparse: the trace to the subring, x += rot(x, n 2^i) for 2^i < M / n (the overflow's
         // components outside the subring cancel, the rest is multiplied by M / n)
         if (sv)
-            for (int st = sv->n; st < slot_count(); st *= 2) {
+            for (int st = sv->n; st < slot_count();) {
+                if (trace4_ && 4 * st <= slot_count()) {  // two doublings at once (hoisted)
+                    Ct s4 = trace4(u, st);
+                    release(u);
+                    u = s4;
+                    st *= 4;
+                    continue;
+                }
                 Ct r = rotate(u, -st);
                 Ct s2 = add_sub(u, r, false);
                 release(r);
                 release(u);
                 u = s2;
+                st *= 2;
             }
         if (stop_after == 4) return u;
         // 5. CoeffToSlot (bit-reversed coefficient halves / (2 q0 K))
