@@ -111,7 +111,7 @@ LinGroup layout(const Diags& D, int h, int M) {
 // n-space offsets are taken signed (|o| <= n/2), valid for the n-periodic vectors they act on.
 Diags lift_out(const Diags& D, int n, const std::vector<cplx>& a) {
     Diags L;
-    const int n2 = 2 * n;
+    const int n2 = (int)a.size();  // 2n (single packing) or 4n (pair packing)
     for (const auto& kv : D) {
         const int o = kv.first <= n / 2 ? kv.first : kv.first - n;
         std::vector<cplx> v(n2);
@@ -147,6 +147,37 @@ Diags lift_in(const Diags& D, int n, const std::vector<cplx>& b1, const std::vec
     return L;
 }
 
+// Pair packing (pack = 2): the hi / lo members of a pair bootstrap share ONE EvalMod.
+// CoeffToSlot's last group multiplies by a4 = (1 | -i | 0 | 0) per 4n block (both members,
+// shared diagonals); the engine adds the lo member rotated right by 2n and w'' + conj(w'')
+// holds (2 Re hi | 2 Im hi | 2 Re lo | 2 Im lo).  SlotToCoeff's first group then comes in two
+// forms reading block pair `which` (0: hi, 1: lo) back into an n-periodic u:
+//   u[p] = s[(p mod n) + 2n which] + i s[(p mod n) + 2n which + n]
+// folded into its diagonals: for q = (p + o) mod 4n in block t, rot_o(u)[p] reads s at
+// p + o - t n + 2n which (and + n, times i).
+Diags lift_in4(const Diags& D, int n, int which) {
+    Diags L;
+    const int n4 = 4 * n, base = 2 * n * which;
+    const cplx I(0.0, 1.0);
+    auto add = [&](int off, int p, cplx v) {
+        const int k = ((off % n4) + n4) % n4;
+        auto it = L.find(k);
+        if (it == L.end()) it = L.emplace(k, std::vector<cplx>(n4, 0.0)).first;
+        it->second[p] += v;
+    };
+    for (const auto& kv : D) {
+        const int o = kv.first <= n / 2 ? kv.first : kv.first - n;
+        for (int p = 0; p < n4; ++p) {
+            const cplx d = kv.second[p % n];
+            if (d == 0.0) continue;
+            const int q = (((p + o) % n4) + n4) % n4, t = q / n;
+            add(o - t * n + base, p, d);
+            add(o - t * n + base + n, p, I * d);
+        }
+    }
+    return L;
+}
+
 }  // namespace
 
 std::vector<cplx> apply_group_plain(const LinGroup& g, const std::vector<cplx>& v) {
@@ -167,7 +198,7 @@ std::vector<cplx> apply_group_plain(const LinGroup& g, const std::vector<cplx>& 
 }
 
 BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts_scale, double stc_scale, int K, int r, int deg,
-                        double stc_boost, bool pack) {
+                        double stc_boost, int pack) {
     BootPlan P;
     P.logn = logn;
     P.M = 1 << (logn - 1);
@@ -176,8 +207,12 @@ BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts
     P.deg = deg;
     const int M = P.M, logm = logn - 1;
     // packed real form: the 2M-periodic half masks (first half of every 2M block)
-    std::vector<cplx> pa, pb1, pb2;
-    if (pack) {
+    std::vector<cplx> pa, pb1, pb2, pa4;
+    if (pack == 2) {
+        pa4.assign(4 * M, 0.0);
+        for (int p = 0; p < M; ++p) pa4[p] = 1.0, pa4[p + M] = cplx(0.0, -1.0);
+    }
+    if (pack == 1) {
         const cplx I(0.0, 1.0);
         pa.resize(2 * M), pb1.resize(2 * M), pb2.resize(2 * M);
         for (int p = 0; p < 2 * M; ++p) {
@@ -211,7 +246,11 @@ BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts
         if (gi + 1 == sg.size() && sg.size() > 1)
             for (auto& kv : D)
                 for (auto& x : kv.second) x /= stc_boost;
-        if (pack && gi == 0) {
+        if (pack == 2 && gi == 0) {
+            const int h = 1 << (sg[gi].front() - 1);
+            P.stc.push_back(layout(lift_in4(D, M, 0), h, 4 * M));
+            P.stc_lo = layout(lift_in4(D, M, 1), h, 4 * M);
+        } else if (pack == 1 && gi == 0) {
             D = lift_in(D, M, pb1, pb2);
             P.stc.push_back(layout(D, 1 << (sg[gi].front() - 1), 2 * M));
         } else {
@@ -227,7 +266,10 @@ BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts
         if (gi == (int)cg.size() - 1)
             for (auto& kv : D)
                 for (auto& x : kv.second) x *= cts_scale;
-        if (pack && gi == 0) {  // the last group applied
+        if (pack == 2 && gi == 0) {  // the last group applied
+            D = lift_out(D, M, pa4);  // lift_out tiles to the mask's length (4 M here)
+            P.cts.push_back(layout(D, 1 << (cg[gi].front() - 1), 4 * M));
+        } else if (pack == 1 && gi == 0) {
             D = lift_out(D, M, pa);
             P.cts.push_back(layout(D, 1 << (cg[gi].front() - 1), 2 * M));
         } else {
@@ -302,68 +344,94 @@ extern "C" int aesfhe_debug_bootplan(int logn, double* err) {
     return 0;
 }
 
-// self-check of a sparse (small-ring, M = n slots) plan, packed or not: random subring
-// coefficients t (2n reals) -> slots z; CoeffToSlot then w' + conj(w') (packed: the 2n-periodic
-// (Re | Im) of the bit-reversed coefficient halves; unpacked: 2 Re), SlotToCoeff of the same
-// (EvalMod taken as the identity) -> z (2z packed).  err: [StC error, CtS error]
+// self-check of a sparse (small-ring, M = n slots) plan: random subring coefficients t (2n
+// reals) -> slots z; CoeffToSlot then w' + conj(w') (pack 1: the 2n-periodic (2 Re | 2 Im) of
+// the bit-reversed coefficient halves; pack 2: two inputs, the lo one rotated right by 2n, the
+// 4n-periodic (2 Re hi | 2 Im hi | 2 Re lo | 2 Im lo); unpacked: w itself), SlotToCoeff of the
+// same (EvalMod taken as the identity) -> z (2z packed; pack 2: stc[0] -> 2 z_hi, stc_lo ->
+// 2 z_lo).  err: [StC error, CtS error]
 extern "C" int aesfhe_debug_sparseplan(int n, int pack, double* err) {
     int logm = 0;
     while ((1 << logm) < n) ++logm;
     const int groups = std::max(1, (logm + 4) / 5);
-    BootPlan P = make_boot_plan(logm + 1, groups, groups, 1.0, 1.0, 12, 3, 27, 1.0, pack != 0);
+    BootPlan P = make_boot_plan(logm + 1, groups, groups, 1.0, 1.0, 12, 3, 27, 1.0, pack);
     Embedding emb(logm + 1);
     std::mt19937_64 rng(2);
     std::normal_distribution<double> nd;
-    const int M = n, n2 = 2 * n;
-    std::vector<double> m(2 * M), re(M), im(M);
-    for (auto& x : m) x = nd(rng);
-    emb.forward(m.data(), re.data(), im.data());
+    const int M = n;
     auto brv = [logm](int x) {
         int r = 0;
         for (int i = 0; i < logm; ++i) r = (r << 1) | ((x >> i) & 1);
         return r;
     };
-    std::vector<cplx> z(M), wb(M);
-    for (int j = 0; j < M; ++j) z[j] = cplx(re[j], im[j]);
-    for (int k = 0; k < M; ++k) wb[k] = cplx(m[brv(k)], m[brv(k) + M]);
     auto tile = [](const std::vector<cplx>& v, int len) {
         std::vector<cplx> o(len);
         for (int p = 0; p < len; ++p) o[p] = v[p % v.size()];
         return o;
     };
-    // CoeffToSlot: each group on vectors of its own diagonal length
-    std::vector<cplx> v = z;
-    for (const auto& g : P.cts) {
-        size_t len = v.size();
+    auto glen = [](const LinGroup& g, size_t cur) {
         for (const auto& row : g.diag)
             for (const auto& d : row)
-                if (!d.empty()) len = d.size();
-        v = apply_group_plain(g, tile(v, (int)len));
-    }
-    double e2 = 0;
-    std::vector<cplx> s(v.size());
-    for (size_t p = 0; p < v.size(); ++p) s[p] = v[p] + std::conj(v[p]);
-    if (pack) {
-        for (int p = 0; p < n2; ++p) {
-            const cplx want = p < M ? cplx(2 * wb[p].real(), 0) : cplx(2 * wb[p - M].imag(), 0);
-            e2 = std::max(e2, std::abs(s[p] - want));
+                if (!d.empty()) return d.size();
+        return cur;
+    };
+    struct In {
+        std::vector<cplx> z, wb;
+    };
+    auto draw = [&]() {
+        std::vector<double> m(2 * M), re(M), im(M);
+        for (auto& x : m) x = nd(rng);
+        emb.forward(m.data(), re.data(), im.data());
+        In r{std::vector<cplx>(M), std::vector<cplx>(M)};
+        for (int j = 0; j < M; ++j) r.z[j] = cplx(re[j], im[j]);
+        for (int k = 0; k < M; ++k) r.wb[k] = cplx(m[brv(k)], m[brv(k) + M]);
+        return r;
+    };
+    auto cts = [&](const std::vector<cplx>& z) {
+        std::vector<cplx> v = z;
+        for (const auto& g : P.cts) v = apply_group_plain(g, tile(v, (int)glen(g, v.size())));
+        return v;
+    };
+    auto stc = [&](std::vector<cplx> u, bool lo) {
+        for (size_t k = 0; k < P.stc.size(); ++k) {
+            const LinGroup& g = (k == 0 && lo) ? P.stc_lo : P.stc[k];
+            u = apply_group_plain(g, tile(u, (int)glen(g, u.size())));
         }
+        return u;
+    };
+    double e1 = 0, e2 = 0;
+    In a = draw();
+    if (pack == 2) {
+        In b = draw();
+        const int n4 = 4 * M;
+        std::vector<cplx> wa = cts(a.z), wb = cts(b.z), w(n4), v(n4);
+        for (int p = 0; p < n4; ++p) w[p] = wa[p] + wb[((p - 2 * M) % n4 + n4) % n4];  // lo rotated right by 2n
+        for (int p = 0; p < n4; ++p) v[p] = w[p] + std::conj(w[p]);
+        for (int p = 0; p < n4; ++p) {
+            const int blk = p / M, k = p % M;
+            const In& src = blk < 2 ? a : b;
+            const double want = (blk % 2 == 0) ? 2 * src.wb[k].real() : 2 * src.wb[k].imag();
+            e2 = std::max(e2, std::abs(v[p] - want));
+        }
+        std::vector<cplx> uh = stc(v, false), ul = stc(v, true);
+        for (size_t j = 0; j < uh.size(); ++j) e1 = std::max(e1, std::abs(uh[j] - 2.0 * a.z[j % M]));
+        for (size_t j = 0; j < ul.size(); ++j) e1 = std::max(e1, std::abs(ul[j] - 2.0 * b.z[j % M]));
     } else {
-        for (int p = 0; p < M; ++p) e2 = std::max(e2, std::abs(v[p] - wb[p]));
-        s = v;  // the unpacked path recombines re + i im = w itself
+        std::vector<cplx> v = cts(a.z), s(v.size());
+        for (size_t p = 0; p < v.size(); ++p) s[p] = v[p] + std::conj(v[p]);
+        if (pack) {
+            for (int p = 0; p < 2 * M; ++p) {
+                const cplx want = p < M ? cplx(2 * a.wb[p].real(), 0) : cplx(2 * a.wb[p - M].imag(), 0);
+                e2 = std::max(e2, std::abs(s[p] - want));
+            }
+        } else {
+            for (int p = 0; p < M; ++p) e2 = std::max(e2, std::abs(v[p] - a.wb[p]));
+            s = v;  // the unpacked path recombines re + i im = w itself
+        }
+        std::vector<cplx> u = stc(s, false);
+        const double gain = pack ? 2.0 : 1.0;
+        for (size_t j = 0; j < u.size(); ++j) e1 = std::max(e1, std::abs(u[j] - gain * a.z[j % M]));
     }
-    // SlotToCoeff
-    std::vector<cplx> u = s;
-    for (const auto& g : P.stc) {
-        size_t len = u.size();
-        for (const auto& row : g.diag)
-            for (const auto& d : row)
-                if (!d.empty()) len = d.size();
-        u = apply_group_plain(g, tile(u, (int)len));
-    }
-    double e1 = 0;
-    const double gain = pack ? 2.0 : 1.0;  // packed: u = (2 Re w) + i (2 Im w) = 2 w
-    for (int j = 0; j < (int)u.size(); ++j) e1 = std::max(e1, std::abs(u[j] - gain * z[j % M]));
     err[0] = e1;
     err[1] = e2;
     return 0;

@@ -27,16 +27,18 @@ struct BootPlan {
     int deg = 27;   // Chebyshev degree of cos(2 pi (K y - 1/4) / 2^r) on [-1, 1]
     std::vector<double> cheb;
     std::vector<LinGroup> cts, stc;  // in application order
+    LinGroup stc_lo;                 // pack 2: the lo member's form of stc[0]
 };
 
 // cts_scale multiplies CoeffToSlot (folded into its first group), stc_scale multiplies
 // SlotToCoeff (folded into its first group)
 // stc_boost: intermediate SlotToCoeff groups carry the signal times stc_boost (first group
 // x stc_boost, last group / stc_boost; same transform)
-// pack (sparse plans, 2M <= the ring's slot count): CoeffToSlot's last group and SlotToCoeff's
-// first work on 2M-periodic vectors so that the real and imaginary halves share ONE EvalMod
+// pack (sparse plans): 1 = CoeffToSlot's last group and SlotToCoeff's first work on 2M-periodic
+// vectors so that the real and imaginary halves share ONE EvalMod; 2 = 4M-periodic, the hi / lo
+// members of a pair bootstrap also share it (stc[0] reads the hi blocks, stc_lo the lo blocks)
 BootPlan make_boot_plan(int logn, int n_groups_cts, int n_groups_stc, double cts_scale, double stc_scale, int K, int r, int deg,
-                        double stc_boost = 1.0, bool pack = false);
+                        double stc_boost = 1.0, int pack = 0);
 
 // reference evaluation of the planned transforms on plain vectors (self-check)
 std::vector<cplx> apply_group_plain(const LinGroup& g, const std::vector<cplx>& v);

@@ -1889,10 +1889,12 @@ public:
     struct SparseBoot {
         int n = 0, top = 0, out_level = 0;
         bool packed = false;  // real / imaginary halves in one 2n-periodic ciphertext (one EvalMod)
+        bool pair4 = false;   // pair bootstraps: hi and lo as well, 4n-periodic (one EvalMod for both)
         BootPlan plan;
         std::vector<BootGroupDev> cts, stc;
+        BootGroupDev stc_lo;  // pair4: the lo member's form of stc[0]
     };
-    std::map<int, SparseBoot> sparse_;
+    std::map<int, SparseBoot> sparse_;  // key n (single / unpacked pair), -n (pair4)
     bool trace4_ = std::getenv("AESFHE_TRACE4") ? std::atoi(std::getenv("AESFHE_TRACE4")) != 0 : true;
     // x + rot(x, -a) + rot(x, -2a) + rot(x, -3a) for the nb members of x: the three rotations
     // hoisted (one ModUp of c1, key inner products read through each automorphism) and summed
@@ -1931,14 +1933,16 @@ public:
         cnt_[C_KS] += 3 * nb;
         return o;
     }
-    SparseBoot& sparse_variant(int n) {
-        auto it = sparse_.find(n);
+    SparseBoot& sparse_variant(int n, bool pair = false) {
+        const char* p4 = std::getenv("AESFHE_SPARSE_PAIR4");  // "0": the pair keeps two EvalMod members (A/B)
+        pair = pair && n <= 32 && !(p4 && std::atoi(p4) == 0);
+        auto it = sparse_.find(pair ? -n : n);
         if (it != sparse_.end()) return it->second;
         const int M = slot_count();
         int logm = 0;
         while ((1 << logm) < n) ++logm;
         if ((1 << logm) != n || n < 16 || n >= M) throw std::runtime_error("sparse bootstrap: period must be a power of two in [16, slot_count)");
-        SparseBoot& sv = sparse_[n];
+        SparseBoot& sv = sparse_[pair ? -n : n];
         sv.n = n;
         const int groups = std::max(1, (logm + 4) / 5);  // <= 5 butterfly stages per group, like the full plan
         // StC's first group crosses the single / double-prime transition (plaintext products only)
@@ -1954,11 +1958,14 @@ public:
         // packed form while the half-folded SlotToCoeff group stays small (offsets up to n + R)
         const char* pk = std::getenv("AESFHE_SPARSE_PACK");  // "0": two EvalMods (A/B)
         sv.packed = n <= 64 && !(pk && std::atoi(pk) == 0);
-        sv.plan = make_boot_plan(logm + 1, groups, groups, cts_scale, stc_scale, boot_k(), boot_r(), boot_deg(), boost, sv.packed);
+        sv.pair4 = pair && sv.packed;
+        sv.plan = make_boot_plan(logm + 1, groups, groups, cts_scale, stc_scale, boot_k(), boot_r(), boot_deg(), boost,
+                                 sv.pair4 ? 2 : sv.packed ? 1 : 0);
         sv.cts.assign(sv.plan.cts.size(), {});
         sv.stc.assign(sv.plan.stc.size(), {});
         for (size_t i = 0; i < sv.cts.size(); ++i) sv.cts[i].g = &sv.plan.cts[i];
         for (size_t i = 0; i < sv.stc.size(); ++i) sv.stc[i].g = &sv.plan.stc[i];
+        sv.stc_lo.g = &sv.plan.stc_lo;
         return sv;
     }
 
@@ -2449,7 +2456,7 @@ public:
     // transform its diagonals, once for both; half the launches
     void bootstrap_pair(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob, double gain = 1.0, int period = 0) {
         boot_setup();
-        SparseBoot* sv = (period > 0 && period < slot_count()) ? &sparse_variant(period) : nullptr;
+        SparseBoot* sv = (period > 0 && period < slot_count()) ? &sparse_variant(period, true) : nullptr;
         if (vis_npoly(a_in) != 2 || vis_npoly(b_in) != 2 || a_in.nb != 1 || b_in.nb != 1)
             throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
         const int n = hp_.n, nl0 = hp_.nl(0);
@@ -2525,6 +2532,53 @@ public:
         Ct w = lin_transform(u, sv ? sv->cts : bs_.cts);
         release(u);
         if (stop_after == 5) return w;
+        if (sv && sv->pair4 && nb == 2) {
+            // pair-packed sparse form: lo rotated right by 2n beside hi, w'' + conj(w'') =
+            // (2 Re hi | 2 Im hi | 2 Re lo | 2 Im lo) per 4n block, ONE EvalMod for both, and
+            // SlotToCoeff's first group in its hi / lo forms
+            const int lv = w.level, nlw = hp_.nl(lv);
+            Ct half[2];
+            for (int m = 0; m < 2; ++m) {
+                half[m] = alloc_ct(lv, 2);
+                copy_meta(half[m], w);
+                half[m].nb = 1;
+                launch_copy_rows(S(), T_, half[m].data, w.data + (size_t)m * 2 * nlw * n, 2 * nlw);
+            }
+            release(w);
+            Ct wr = rotate(half[1], 2 * sv->n);
+            release(half[1]);
+            Ct ws = add_sub(half[0], wr, false);
+            release(half[0]);
+            release(wr);
+            Ct cj = conjugate(ws);
+            Ct v = add_sub(ws, cj, false);
+            release(ws);
+            release(cj);
+            Ct f = eval_mod(v);
+            release(v);
+            Ct oh = lin_group(f, sv->stc[0]), ol = lin_group(f, sv->stc_lo);
+            release(f);
+            const int nlo = hp_.nl(oh.level);
+            Ct st = alloc_ct(oh.level, 4, 2);
+            copy_meta(st, oh);
+            st.nb = 2;
+            launch_copy_rows(S(), T_, st.data, oh.data, 2 * nlo);
+            launch_copy_rows(S(), T_, st.data + (size_t)2 * nlo * n, ol.data, 2 * nlo);
+            release(oh);
+            release(ol);
+            for (size_t k = 1; k < sv->stc.size(); ++k) {
+                Ct nx = lin_group(st, sv->stc[k]);
+                release(st);
+                st = nx;
+            }
+            cnt_[C_BOOT] += nb;
+            if (st.level > hp_.fresh) {
+                Ct o = level_down(st, hp_.fresh);
+                release(st);
+                st = o;
+            }
+            return st;
+        }
         if (sv && sv->packed) {
             // packed sparse form: w' + conj(w') = (Re w | Im w) per 2n block, one EvalMod, and
             // SlotToCoeff's first group recombines the halves

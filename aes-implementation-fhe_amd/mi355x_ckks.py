@@ -743,8 +743,9 @@ def debug_bootplan(log_n: int = 16) -> np.ndarray:
     return err
 
 
-def debug_sparseplan(n: int, pack: bool) -> np.ndarray:
-    """host self-check of a sparse bootstrap plan (aesfhe_debug_sparseplan): [StC error, CtS error]"""
+def debug_sparseplan(n: int, pack: int) -> np.ndarray:
+    """host self-check of a sparse bootstrap plan (aesfhe_debug_sparseplan; pack 0 / 1 single /
+    2 pair): [StC error, CtS error]"""
     err = np.zeros(2)
-    load_library().aesfhe_debug_sparseplan(int(n), int(bool(pack)), err)
+    load_library().aesfhe_debug_sparseplan(int(n), int(pack), err)
     return err

@@ -19,10 +19,11 @@ def test_bootstrap_depth():
     assert mi355x_ckks.bootstrap_depth() == 15  # CtS 3 + EvalMod (Chebyshev PS 5 + 4 double angles) + StC 3
 
 
-@pytest.mark.parametrize("n,pack", [(16, True), (32, True), (64, True), (16, False), (1024, False)])
+@pytest.mark.parametrize("n,pack", [(16, 1), (32, 1), (64, 1), (16, 2), (32, 2), (16, 0), (1024, 0)])
 def test_sparse_plan_factorisation(n, pack):
     """the sparse (period-n, small-ring) plans: CoeffToSlot to the bit-reversed coefficient
-    halves (packed: the 2n-periodic (2 Re | 2 Im) real form), SlotToCoeff back"""
+    halves (pack 1: the 2n-periodic (2 Re | 2 Im) real form; pack 2: a pair's hi and lo in one
+    4n-periodic vector), SlotToCoeff back"""
     import build_ext
     import mi355x_ckks
     build_ext.build()

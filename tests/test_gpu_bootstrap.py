@@ -147,8 +147,11 @@ def test_sparse_bootstrap_periodic_message(ctx, period):
     a, b = ctx.encrypt(za), ctx.encrypt(zb)
     pa, pb = E.bootstrap_pair_sparse(a, b, period)
     sa = E.bootstrap_sparse(a, period)
-    assert pa.level == pb.level == E.fresh_level
-    assert np.array_equal(E.export(pa), E.export(sa))
+    assert pa.level == pb.level == sa.level == E.fresh_level
+    if period > 32:  # same evaluation as two single bootstraps: bit for bit
+        assert np.array_equal(E.export(pa), E.export(sa))
+    else:  # pair-packed (hi and lo share one EvalMod): same values within the bootstrap error
+        assert np.abs(ctx.decrypt(sa) - za).max() < BOOT_TOL
     assert np.abs(ctx.decrypt(pa) - za).max() < BOOT_TOL
     assert np.abs(ctx.decrypt(pb) - zb).max() < BOOT_TOL
     with pytest.raises(RuntimeError, match="period"):
