@@ -2456,9 +2456,10 @@ public:
     // transform its diagonals, once for both; half the launches
     void bootstrap_pair(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob, double gain = 1.0, int period = 0) {
         boot_setup();
-        SparseBoot* sv = (period > 0 && period < slot_count()) ? &sparse_variant(period, true) : nullptr;
         if (vis_npoly(a_in) != 2 || vis_npoly(b_in) != 2 || a_in.nb != 1 || b_in.nb != 1)
             throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
+        if (period > 0 && 2 * period <= slot_count() && mono_pair_) return bootstrap_pair_mono(a_in, b_in, oa, ob, gain, period);
+        SparseBoot* sv = (period > 0 && period < slot_count()) ? &sparse_variant(period, true) : nullptr;
         const int n = hp_.n, nl0 = hp_.nl(0);
         Ct z = alloc_ct(0, 4, 2);
         const Ct* in[2] = {&a_in, &b_in};
@@ -2479,6 +2480,60 @@ public:
             *dst[m] = put_ct(o);
         }
         release(out);
+    }
+    // The pair of n-periodic messages a, b (2n <= slots) as ONE 2n-periodic message
+    // (DESIGN.md §4b): a, b lie in the subring Z[X^2k], k = N / 4n, so z = a + X^k b lies in
+    // Z[X^k] -- the 2n-periodic messages -- exactly (a monomial product only permutes and
+    // negates coefficients).  One bootstrap at period 2n (the full-slot one when 2n = slots)
+    // with gain / 2 (|z| <= |a| + |b|) refreshes both; the rotation by n slots is
+    // X -> X^(4n+1) (5^n = 4n + 1 mod 8n), which fixes X^2k and negates X^k, so with
+    // m = gain z / 2 and r = rot_n(m):  gain a = m + r,  gain b = X^-k (m - r).
+    bool mono_pair_ = !(std::getenv("AESFHE_PAIR_MONO") && std::atoi(std::getenv("AESFHE_PAIR_MONO")) == 0);
+    void bootstrap_pair_mono(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob, double gain, int period) {
+        const int n = hp_.n, k = n / (4 * period), nl0 = hp_.nl(0);
+        Ct z0[2];
+        const Ct* in[2] = {&a_in, &b_in};
+        for (int m = 0; m < 2; ++m) {
+            Ct c = normalize(*in[m]);
+            z0[m] = level_down(c, 0);
+            if (c.data != in[m]->data) release(c);
+        }
+        Ct z = alloc_ct(0, 2);
+        launch_fma_poly(S(), T_, z.data, z0[0].data, z0[1].data, monomial(k), 2 * nl0, nl0, qmap());
+        release(z0[0]);
+        release(z0[1]);
+        SparseBoot* sv = 2 * period < slot_count() ? &sparse_variant(2 * period) : nullptr;
+        Ct mz = bootstrap_l0(z, 99, 0.5 * gain, sv);
+        Ct r = rotate(mz, period);
+        Ct hi = add_sub(mz, r, false);
+        Ct d = add_sub(mz, r, true);
+        release(mz);
+        release(r);
+        Ct dn = ensure_ntt(d);
+        if (dn.data != d.data) release(d);
+        Ct lo = alloc_ct(dn.level, 2);
+        copy_meta(lo, dn);
+        launch_mul_poly(S(), T_, lo.data, dn.data, monomial(2 * n - k), 2, hp_.nl(dn.level), qmap());
+        release(dn);
+        cnt_[C_BOOT] += 1;  // bootstrap_l0 counted one: two messages refreshed
+        *oa = put_ct(hi);
+        *ob = put_ct(lo);
+    }
+    // NTT form of the monomial X^e (X^N = -1, e in [0, 2N)) on every Q limb: the product by
+    // it is exact (coefficients shifted, the wrapped ones negated; no level, no noise)
+    std::map<int, u32*> mono_;
+    const u32* monomial(int e) {
+        auto it = mono_.find(e);
+        if (it != mono_.end()) return it->second;
+        const int n = hp_.n, nq = hp_.n_q;
+        std::vector<u32> h((size_t)nq * n, 0u);
+        for (int t = 0; t < nq; ++t) h[(size_t)t * n + e % n] = (e / n) % 2 ? hp_.mod[t] - 1 : 1u;
+        u32* d = dev_alloc((size_t)nq * n);
+        HIP_OK(hipMemcpy(d, h.data(), h.size() * sizeof(u32), hipMemcpyHostToDevice));
+        ntt(d, nq, nq, qmap());
+        HIP_OK(hipStreamSynchronize(S()));
+        mono_[e] = d;
+        return d;
     }
     // z: level-0 ciphertext(s), nb batched members, consumed here
     Ct bootstrap_l0(Ct z, int stop_after, double gain = 1.0, SparseBoot* sv = nullptr) {

@@ -22,7 +22,7 @@ from xor4_lut import XOR4LUT  # noqa: E402
 
 
 def main(reps=10):
-    ctx = EngineContext(signature=1, max_level=17)
+    ctx = EngineContext(signature=1, max_level=17, concurrent="--serial" not in sys.argv)
     E = ctx.engine
     co = load_all_coeffs()
     enc = StateEncoder(ctx)
@@ -49,6 +49,8 @@ def main(reps=10):
 
     fl = RENORM_FLOOR
     x = timed("xor4_pair@floor", lambda: pair(ctx, lambda: xor4.apply(ax[0], bx[0], fl), lambda: xor4.apply(ax[1], bx[1], fl)))
+    if hasattr(xor4, "apply_pair"):
+        timed("xor4.apply_pair@floor", lambda: xor4.apply_pair(ax[0], bx[0], ax[1], bx[1], fl))
     timed("xor4_single@floor", lambda: xor4.apply(ax[0], bx[0], fl))
     timed("renorm_pair->NEED_XOR", lambda: enc.renorm(*x, level=NEED_XOR))
     timed("gf2_pair", lambda: mix.gf_mult_2(*ag, out_level=fl + LUT2_DEPTH))
