@@ -62,9 +62,12 @@ struct DevTables {
 // skip_alpha > 0 (forward only): rows with i < skip_nl and i / skip_alpha == g are left
 // untouched (ModUp: a digit's own limbs); skip_groups > 0: g taken mod skip_groups (the
 // digits of several batched ciphertexts in one launch)
+// launch row y = g * cnt + i: group g (grid z), row i of the group (grid y) -- a 3-D grid, so
+// kernels read g and i from blockIdx without a (VALU-emulated) integer division
 struct RowMap {
     int cnt, src_stride, dst_stride, src_off, dst_off;
     int skip_alpha = 0, skip_nl = 0, skip_groups = 0;
+    int nrows = 0;  // launch rows (set by the launcher; the last group may be partial)
 };
 inline RowMap rows_dense(int nl) { return RowMap{nl, nl, nl, 0, 0}; }
 // fused prologue / epilogue operands of the forward NTT (ntt.hip)

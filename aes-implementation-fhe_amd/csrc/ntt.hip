@@ -74,10 +74,10 @@ inline bool small_launch(int rows) { return rows < small_rows_limit(); }
 // key-switching ModUp: digit g's own limbs [g alpha, min(nl, (g + 1) alpha)) are not
 // transformed (they are already in NTT form in the input); block-uniform early exit
 __device__ __forceinline__ bool skipped(const RowMap& rm) {
+    const int g0 = blockIdx.z, i = blockIdx.y;
+    if (g0 * rm.cnt + i >= rm.nrows) return true;  // past the last row of a partial group
     if (rm.skip_alpha <= 0) return false;
-    int g = blockIdx.y / rm.cnt;
-    const int i = blockIdx.y - g * rm.cnt;
-    if (rm.skip_groups > 0) g %= rm.skip_groups;
+    const int g = rm.skip_groups > 0 ? g0 % rm.skip_groups : g0;
     return i < rm.skip_nl && i / rm.skip_alpha == g;
 }
 
@@ -88,8 +88,7 @@ struct RowAddr {
 };
 template <int LOGN>
 __device__ __forceinline__ RowAddr row_addr(u32* dst, const u32* src, const RowMap& rm, const LimbMap& map) {
-    const int y = blockIdx.y;
-    const int g = y / rm.cnt, i = y - g * rm.cnt;
+    const int g = blockIdx.z, i = blockIdx.y;
     RowAddr a;
     a.src = src + ((size_t)(rm.src_off + g * rm.src_stride + i) << LOGN);
     a.dst = dst + ((size_t)(rm.dst_off + g * rm.dst_stride + i) << LOGN);
@@ -115,7 +114,7 @@ __global__ void __launch_bounds__(NT) k_ntt1_fwd(u32* dst, const u32* src, RowMa
     const int c = blockIdx.x * CB + col;
     u32 x[16];
     if (MODE == kSpread) {
-        const int grp = blockIdx.y / rm.cnt;
+        const int grp = blockIdx.z;
         ra.src = src + ((size_t)(rm.src_off + grp * rm.src_stride) << LOGN);
         const u32 ql = aux.q_last, half = ql >> 1;
 #pragma unroll
@@ -127,7 +126,7 @@ __global__ void __launch_bounds__(NT) k_ntt1_fwd(u32* dst, const u32* src, RowMa
     } else if (MODE == kSpread2) {
         // two dropped limbs a, b (rows src_off + grp * src_stride + {0, 1}): mixed-radix CRT
         // v = x_a + qa ((x_b - x_a) qa^{-1} mod qb) in [0, qa qb), centred, reduced mod q
-        const int grp = blockIdx.y / rm.cnt;
+        const int grp = blockIdx.z;
         const u32* sa = src + ((size_t)(rm.src_off + grp * rm.src_stride) << LOGN);
         const u32* sb = sa + ((size_t)1 << LOGN);
         const u32 qa = aux.q_last, qb = aux.q_last2;
@@ -234,7 +233,7 @@ __global__ void __launch_bounds__(NT) k_ntt2_fwd(u32* data, RowMap rm, LimbMap m
 #pragma unroll
     for (int k = 0; k < 16; ++k) x[k] = canon4(x[k], q);  // last stage: [0, 4q) -> [0, q)
     if (MODE == kFinish) {
-        const int grp = blockIdx.y / rm.cnt, li = blockIdx.y - grp * rm.cnt;
+        const int grp = blockIdx.z, li = blockIdx.y;
         const size_t woff = (size_t)R * 256 + 16 * j;
         const uint4* cu = reinterpret_cast<const uint4*>(aux.cur + ((size_t)(grp * aux.cur_stride + li) << LOGN) + woff);
         const u32* addp = (grp & 1) ? aux.add1 : aux.add0;
@@ -370,6 +369,8 @@ template <int LOGR1, int M1, int M2>
 void ntt_fwd_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, int io_rows, RowMap rm, LimbMap map,
                const NttAux& aux) {
     constexpr int R1 = 1 << LOGR1;
+    rm.nrows = rows;
+    const int groups = (rows + rm.cnt - 1) / rm.cnt;
     const double row_bytes = 4.0 * 256.0 * R1;
     const double io1 = 2.0 * io_rows * row_bytes;
     const double io2 = (M2 == kFinish ? (3.0 + (aux.add0 ? 0.5 : 0.0) + (aux.add1 ? 0.5 : 0.0)) : 2.0) * io_rows * row_bytes;
@@ -377,35 +378,37 @@ void ntt_fwd_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
     // launches of few rows: half-size blocks, so that the grid still spreads over every CU
     if (small_launch(rows)) {
         constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
-        prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, M1, NT>, dim3(256 / CB, rows), dim3(NT), 0, st, dst, src,
+        prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, M1, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, dst, src,
                         rm, map, Tb.pc, Tb.tw, aux);
-        prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2, NT>, dim3(R1 / (NT / 16), rows), dim3(NT), 0, st, dst,
+        prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2, NT>, dim3(R1 / (NT / 16), rm.cnt, groups), dim3(NT), 0, st, dst,
                         rm, map, Tb.pc, Tb.tw, aux);
         return;
     }
     constexpr int CB = kThreads / (R1 / 16);
-    prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, M1, kThreads>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst,
+    prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, M1, kThreads>, dim3(256 / CB, rm.cnt, groups), dim3(kThreads), 0, st, dst,
                     src, rm, map, Tb.pc, Tb.tw, aux);
-    prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2, kThreads>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st,
+    prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2, kThreads>, dim3(R1 / kRowsP2, rm.cnt, groups), dim3(kThreads), 0, st,
                     dst, rm, map, Tb.pc, Tb.tw, aux);
 }
 template <int LOGR1>
 void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {
     constexpr int R1 = 1 << LOGR1;
+    rm.nrows = rows;
+    const int groups = (rows + rm.cnt - 1) / rm.cnt;
     const double io = 4.0 * 2.0 * rows * (256.0 * R1);  // the inverse is never launched with skips
     const double bfly = (double)rows * 128.0 * R1;
     if (small_launch(rows)) {
         constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
-        prof_launch_tsw(KID_NTT_ROWS_INV, io, bfly * 8.0, k_ntt2_inv<LOGR1, NT>, dim3(R1 / (NT / 16), rows), dim3(NT), 0, st, dst, src, rm,
+        prof_launch_tsw(KID_NTT_ROWS_INV, io, bfly * 8.0, k_ntt2_inv<LOGR1, NT>, dim3(R1 / (NT / 16), rm.cnt, groups), dim3(NT), 0, st, dst, src, rm,
                         map, Tb.pc, Tb.itw);
-        prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, NT>, dim3(256 / CB, rows), dim3(NT), 0, st, dst, rm, map,
+        prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, dst, rm, map,
                         Tb.pc, Tb.itw);
         return;
     }
     constexpr int CB = kThreads / (R1 / 16);
-    prof_launch_tsw(KID_NTT_ROWS_INV, io, bfly * 8.0, k_ntt2_inv<LOGR1, kThreads>, dim3(R1 / kRowsP2, rows), dim3(kThreads), 0, st, dst, src,
+    prof_launch_tsw(KID_NTT_ROWS_INV, io, bfly * 8.0, k_ntt2_inv<LOGR1, kThreads>, dim3(R1 / kRowsP2, rm.cnt, groups), dim3(kThreads), 0, st, dst, src,
                     rm, map, Tb.pc, Tb.itw);
-    prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, kThreads>, dim3(256 / CB, rows), dim3(kThreads), 0, st, dst, rm,
+    prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, kThreads>, dim3(256 / CB, rm.cnt, groups), dim3(kThreads), 0, st, dst, rm,
                     map, Tb.pc, Tb.itw);
 }
 

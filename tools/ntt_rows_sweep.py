@@ -16,7 +16,7 @@ def main():
     top = 4 * (E.n_q + E.n_p)
     out = {"small_rows": os.environ.get("AESFHE_NTT_SMALL_ROWS", "default")}
     for op in ("ntt", "intt"):
-        out[op] = {r: round(E.bench_op(op, r, 200), 2) for r in (4, 8, 12, 20, 30, 40, 60, 80, 120, 160) if r <= top}
+        out[op] = {r: round(E.bench_op(op, r, 200), 2) for r in (4, 8, 12, 16, 20, 24, 30, 32, 36, 40, 44, 48, 56, 64, 72, 80, 96, 120, 160) if r <= top}
     print(json.dumps(out), flush=True)
 
 
