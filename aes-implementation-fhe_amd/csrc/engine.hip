@@ -1717,9 +1717,20 @@ public:
     // period > 0: the periodic layout (slot j == slot j mod period, state_encoder.SlotLayout):
     // period 16 decodes / re-encodes its 16 slots directly (5^i positions), other periods snap
     // every slot (states = slot_count / 16)
+    //
+    // unpack = n > 0: hh is a packed state (hi | lo halves of every 2n-slot block, the
+    // pipeline's packed XOR stage) and hl must be hh; oh / ol get its hi / lo halves as
+    // n-periodic states.  single: hh == hl, one output (ol untouched) with every slot snapped.
     void renorm_states(aesfhe_handle hh, aesfhe_handle hl, int states, aesfhe_handle* oh, aesfhe_handle* ol, int level = -1,
-                       int period = 0) {
+                       int period = 0, int unpack = 0, bool single = false) {
         if (!d_pk_) throw std::runtime_error("keys not generated");
+        if (unpack || single) {
+            if (hl != hh) throw std::runtime_error("renorm: a packed / single renorm reads one ciphertext");
+            if (unpack && (unpack & (unpack - 1) || unpack < 16 || 2 * unpack > slot_count()))
+                throw std::runtime_error("renorm: bad packed period");
+            period = 0;
+            states = slot_count() / 16;  // every slot snapped (FFT codec)
+        }
         if (period > 0) {
             if (period & (period - 1) || period < 16 || period > slot_count()) throw std::runtime_error("renorm: bad period");
             states = period == 16 ? 1 : slot_count() / 16;
@@ -1794,17 +1805,16 @@ public:
             double* w = zbuf + (size_t)2 * 2 * n;
             launch_decode_twist(S(), T_, x, kd, cc, isc, z);
             launch_fft2(S(), T_, z, 1);
-            launch_snap_slots(S(), T_, z, w, d_slot_pos_, states);
+            launch_snap_slots(S(), T_, z, w, d_slot_pos_, states, unpack);
             launch_fft2(S(), T_, w, -1);
             launch_encode_untwist(S(), T_, m, w, enc_scale, nq);
         }
-        ntt(m, 2 * nq, nq, qmap());
+        ntt(m, (single ? 1 : 2) * nq, nq, qmap());
         Ct a = encrypt_ntt(m, f);
-        Ct b = encrypt_ntt(m + (size_t)nq * n, f);
+        *oh = put_ct(a);
+        if (!single) *ol = put_ct(encrypt_ntt(m + (size_t)nq * n, f));
         untmp(m, 2 * (size_t)nq);
         untmp(x, 8);
-        *oh = put_ct(a);
-        *ol = put_ct(b);
     }
 
     // ------------------------------------------------------------------ bootstrapping
@@ -3428,6 +3438,14 @@ int aesfhe_renorm_pair(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesf
 int aesfhe_renorm_periodic(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, int period, int level, aesfhe_handle* out_hi,
                            aesfhe_handle* out_lo) {
     API_BEGIN ctx->eng->renorm_states(hi, lo, 1, out_hi, out_lo, level, period);
+    API_END
+}
+int aesfhe_renorm_unpack(aesfhe_ctx* ctx, aesfhe_handle packed, int period, int level, aesfhe_handle* out_hi, aesfhe_handle* out_lo) {
+    API_BEGIN ctx->eng->renorm_states(packed, packed, 1, out_hi, out_lo, level, 0, period);
+    API_END
+}
+int aesfhe_renorm_single(aesfhe_ctx* ctx, aesfhe_handle c, int level, aesfhe_handle* out) {
+    API_BEGIN ctx->eng->renorm_states(c, c, 1, out, nullptr, level, 0, 0, true);
     API_END
 }
 int aesfhe_renorm_states(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, int states, aesfhe_handle* out_hi,

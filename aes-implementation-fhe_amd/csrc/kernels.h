@@ -294,7 +294,9 @@ void launch_decode_twist(hipStream_t st, const DevTables& T, const u32* x, const
 void launch_fft2(hipStream_t st, const DevTables& T, double* z, int sign);
 // snap: slot j (value at fft_loc(slot_pos[j]) of zin) -> zeta16 power if (j mod stride) < states,
 // else 1; writes w[slot_pos[j]] = v and w[N - 1 - slot_pos[j]] = conj(v) (natural order)
-void launch_snap_slots(hipStream_t st, const DevTables& T, const double* zin, double* w, const u32* slot_pos, int states);
+// unpack = n > 0: both outputs read the first input's 2n-periodic packed state, output 0 its
+// slots (j mod n), output 1 its slots (j mod n) + n
+void launch_snap_slots(hipStream_t st, const DevTables& T, const double* zin, double* w, const u32* slot_pos, int states, int unpack = 0);
 // out[c][t][k] = round(scale Re(v[fft_loc(k)] zeta^{-k}) / N) mod q_t, t < nq
 void launch_encode_untwist(hipStream_t st, const DevTables& T, u32* out, const double* v, double scale, int nq);
 

@@ -626,7 +626,10 @@ __device__ __forceinline__ size_t fft_loc(u32 t, int logn) {
     return ((size_t)(t & ((1u << l1) - 1)) << (logn - l1)) + (t >> l1);
 }
 
-__global__ void __launch_bounds__(kBlock) k_snap_slots(const double2* zin, double2* w, const u32* slot_pos, int states, int logn) {
+// unpack > 0: output c (0 = hi, 1 = lo) takes slot (j mod unpack) + c unpack of the FIRST input
+// -- the hi | lo halves of a 2 unpack-periodic packed state (pipeline's packed XOR stage)
+__global__ void __launch_bounds__(kBlock) k_snap_slots(const double2* zin, double2* w, const u32* slot_pos, int states, int unpack,
+                                                       int logn) {
     const int c = blockIdx.y;
     const int j = blockIdx.x * kBlock + threadIdx.x;  // slot < N/2
     const int n = 1 << logn;
@@ -634,7 +637,9 @@ __global__ void __launch_bounds__(kBlock) k_snap_slots(const double2* zin, doubl
     const int stride = (n / 2) / 16;
     double2 v = make_double2(1.0, 0.0);
     if (j % stride < states) {
-        const double2 z = zin[((size_t)c << logn) + fft_loc(t, logn)];
+        const int src_c = unpack ? 0 : c;
+        const u32 ts = unpack ? slot_pos[(j & (unpack - 1)) + c * unpack] : t;
+        const double2 z = zin[((size_t)src_c << logn) + fft_loc(ts, logn)];
         const double kf = rint(-atan2(z.y, z.x) * 16.0 / (2.0 * M_PI));
         const int nib = (int)((((long)kf) % 16 + 16) % 16);
         double sn, cs;
@@ -1054,10 +1059,10 @@ void launch_fft2(hipStream_t st, const DevTables& T, double* z, int sign) {
         prof_launch(KID_ELEMENTWISE, 64.0 * (1u << T.logn), k_fft_pass, dim3((1u << (pass ? l1 : l2)) / kFftTpb, 2), dim3(kBlock), 0, st,
                     (double2*)z, T.logn, pass, sign);
 }
-void launch_snap_slots(hipStream_t st, const DevTables& T, const double* zin, double* w, const u32* slot_pos, int states) {
+void launch_snap_slots(hipStream_t st, const DevTables& T, const double* zin, double* w, const u32* slot_pos, int states, int unpack) {
     const double s = (double)(1u << (T.logn - 1));
     prof_launch(KID_ELEMENTWISE, 2.0 * (16.0 * s + 4.0 * s + 32.0 * s), k_snap_slots, dim3((1u << (T.logn - 1)) / kBlock, 2),
-                dim3(kBlock), 0, st, (const double2*)zin, (double2*)w, slot_pos, states, T.logn);
+                dim3(kBlock), 0, st, (const double2*)zin, (double2*)w, slot_pos, states, unpack, T.logn);
 }
 void launch_encode_untwist(hipStream_t st, const DevTables& T, u32* out, const double* v, double scale, int nq) {
     const double n = (double)(1u << T.logn);

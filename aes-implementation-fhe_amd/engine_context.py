@@ -227,6 +227,14 @@ class EngineContext:
         """renorm_pair for the periodic state layout (state_encoder.SlotLayout)"""
         return self.engine.renorm_periodic(hi, lo, period, level)
 
+    def renorm_single(self, ct, level=None):
+        """renorm of one packed-state ciphertext, every slot snapped"""
+        return self.engine.renorm_single(ct, level)
+
+    def renorm_unpack(self, packed, period: int, level=None):
+        """renorm of a packed hi | lo state (2 period-periodic) into its (hi, lo) pair"""
+        return self.engine.renorm_unpack(packed, period, level)
+
     def _init_lut_cache(self):
         self._luts = {}                                  # digest -> LookupTable
         self._lut_pinned = set()                         # digests requested without an owner

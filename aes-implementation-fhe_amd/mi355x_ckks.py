@@ -42,6 +42,7 @@ EXPORTED = [
     "aesfhe_streams", "aesfhe_bind_stream", "aesfhe_fork", "aesfhe_join", "aesfhe_settle",
     "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_kernel_work", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan", "aesfhe_debug_sparseplan",
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot", "aesfhe_create_keyed", "aesfhe_bootstrap_sparse", "aesfhe_bootstrap_pair_sparse", "aesfhe_renorm_periodic",
+    "aesfhe_renorm_single", "aesfhe_renorm_unpack",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_lut_create", "aesfhe_lut_eval", "aesfhe_lut_free",
     "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled",
 ]
@@ -120,6 +121,8 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_debug_lin_group"] = [vp, _H, c_int, _Hp]
     sig["aesfhe_create_boot"] = [pp, c_int, c_int, c_int, c_int, ctypes.c_uint64]
     sig["aesfhe_renorm_periodic"] = [vp, _H, _H, c_int, c_int, _Hp, _Hp]
+    sig["aesfhe_renorm_single"] = [vp, _H, c_int, _Hp]
+    sig["aesfhe_renorm_unpack"] = [vp, _H, c_int, c_int, _Hp, _Hp]
     sig["aesfhe_bootstrap_sparse"] = [vp, _H, c_int, c_dbl, _Hp]
     sig["aesfhe_bootstrap_pair_sparse"] = [vp, _H, _H, c_int, c_dbl, _Hp, _Hp]
     sig["aesfhe_create_keyed"] = [pp, c_int, c_int, c_int, c_int, ctypes.c_char_p, c_int]
@@ -583,6 +586,17 @@ class Engine:
         a, b = ctypes.c_uint64(), ctypes.c_uint64()
         self._ctx.check(self._lib.aesfhe_renorm_periodic(self._ctx.ptr, hi.handle, lo.handle, int(period),
                                                          -1 if level is None else int(level), ctypes.byref(a), ctypes.byref(b)))
+        return Ciphertext(self._ctx, a.value), Ciphertext(self._ctx, b.value)
+
+    def renorm_single(self, ct, level=None):
+        """secret-key renorm of one ciphertext, every slot snapped (aesfhe_renorm_single)"""
+        return self._new(self._lib.aesfhe_renorm_single, ct.handle, -1 if level is None else int(level))
+
+    def renorm_unpack(self, packed, period: int, level=None):
+        """secret-key renorm of a packed hi | lo state into its (hi, lo) pair (aesfhe_renorm_unpack)"""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        self._ctx.check(self._lib.aesfhe_renorm_unpack(self._ctx.ptr, packed.handle, int(period), -1 if level is None else int(level),
+                                                       ctypes.byref(a), ctypes.byref(b)))
         return Ciphertext(self._ctx, a.value), Ciphertext(self._ctx, b.value)
 
     def sync(self):

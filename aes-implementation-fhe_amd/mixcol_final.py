@@ -16,7 +16,7 @@ import numpy as np
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT, SplitLUT2, batched, eval_two, joint_bases, powers, std_basis
-from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap2, can_fork, drop_to, fused_lut, pair, rot_many
+from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, can_fork, drop_to, fused_lut, pair, rot_many
 
 
 class _CoeffCache:
@@ -174,6 +174,38 @@ class MixColFinal:
         rh, rl = pair(self.ctx, lambda: rot_many(self.ctx, ct_hi, steps), lambda: rot_many(self.ctx, ct_lo, steps))
         rot = {k: (rh[k - 1], rl[k - 1]) for k in (1, 2, 3)}
         return self.mix_rotated((ct_hi, ct_lo), rot, do_final_bootstrap, debug)
+
+    # ---------------------------------------------------------------- packed XOR stage
+    def packed_ok(self) -> bool:
+        """the packed XOR stage applies: periodic layout with room for hi | lo side by side, the
+        secret-key renorm (not true-FHE), fused LUTs and the engine's packed renorms"""
+        ctx = self.ctx
+        return (self.layout.packable and self.enc.renorm_hook is None and getattr(ctx, "fused_luts", False)
+                and getattr(ctx, "renorm_unpack", None) is not None)
+
+    def mix_packed(self, ct_hi, ct_lo, do_final_bootstrap: bool = True):
+        """MixColumns with its XOR stage on packed states (StateEncoder.pack: hi and lo side by side
+        in one ciphertext, the XOR4 LUT being the same for both halves): the three XOR pairs of
+        mix_rotated become three single XOR4s, their renorms single-ciphertext renorms, and the
+        final bootstrap one sparse bootstrap at period 2P.  Returns the PACKED output (the caller's
+        AddRoundKey XORs it with a packed round key and unpacks in its renorm).  The GF
+        multipliers stay pairs (they mix hi and lo); their outputs and r2, r3 are packed (one
+        level: inputs one level higher than mix_rotated's, pipeline NEED_SR_MIX_PACKED)."""
+        ctx, enc = self.ctx, self.enc
+        steps = [-4 * k * self.stride for k in (1, 2, 3)]
+        rh, rl = pair(ctx, lambda: rot_many(ctx, ct_hi, steps), lambda: rot_many(ctx, ct_lo, steps))
+        fl = RENORM_FLOOR
+        gl = fl + LUT2_DEPTH + enc.PACK_DEPTH
+        two, thr = pair(ctx, lambda: self.gf_mult_2(ct_hi, ct_lo, out_level=gl),
+                        lambda: self.gf_mult_3(rh[0], rl[0], out_level=gl))
+        p2, p3 = pair(ctx, lambda: enc.pack(*two), lambda: enc.pack(*thr), shared=(*two, *thr))
+        r2, r3 = pair(ctx, lambda: enc.pack(rh[1], rl[1]), lambda: enc.pack(rh[2], rl[2]), shared=(*rh, *rl))
+        x1, x2 = pair(ctx, lambda: enc.renorm_packed(self._xor_ct(p2, p3, fl), level=NEED_XOR),
+                      lambda: enc.renorm_packed(self._xor_ct(r2, r3, fl), level=NEED_XOR))
+        acc = enc.renorm_packed(self._xor_ct(x1, x2, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
+        if do_final_bootstrap:
+            acc = bootstrap1(ctx, acc, 2 * self.layout.period)
+        return acc
 
     def mix_rotated(self, x, rot, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
         """GF2(x) ^ GF3(r1) ^ r2 ^ r3 from the state pair x and its column shifts rot[k] = r_k

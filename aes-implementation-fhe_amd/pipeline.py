@@ -24,6 +24,12 @@ MixColumns' / InvMixColumns' final bootstraps merge into their last renorm, and 
 applies each InvShiftRows before the renorm that precedes InvSubBytes (the snap leaves
 exactly SubBytes' 13 levels).  No secret key is used between encryption and decryption.
 
+``packed_xor`` (default: wherever it applies) runs MixColumns' XOR stage and the AddRoundKey
+after it on packed states -- hi and lo side by side in ONE ciphertext, the XOR4 LUT being the
+same for both halves (MixColFinal.mix_packed): single XOR4s instead of pairs,
+single-ciphertext renorms, one sparse bootstrap; the renorm after AddRoundKey unpacks into the
+(hi, lo) pair SubBytes reads.  The debug path keeps the reference's pair steps.
+
 ``states`` = B > 1 runs B independent AES states per ciphertext pair in the slot-packed
 layout (state_encoder.py): ``encrypt`` / ``decrypt`` take and return
 (B, 16) arrays through the same step sequence, and a (16,) round key is shared by all B
@@ -31,6 +37,7 @@ states (a (B, 16) key array gives each state its own).
 """
 from __future__ import annotations
 
+import os
 from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
@@ -54,7 +61,8 @@ class AESPipeline:
     def __init__(self, ctx, coeffs: Dict[str, Any], *, mixcolumns: MixColFinal | None = None,
                  inv_mixcolumns: InvMixColumnsFHE | None = None, use_hard_renorm_between_steps: bool = False,
                  with_inv_mix_columns: bool = True, states: int = 1, fuse_sub_ark: bool = False,
-                 fuse_sr_mc: bool = False, true_fhe: bool = False, periodic: bool | None = None):
+                 fuse_sr_mc: bool = False, true_fhe: bool = False, periodic: bool | None = None,
+                 packed_xor: bool | None = None):
         self.ctx = ctx
         self.states = states
         # periodic layout (state_encoder.SlotLayout): default on where the engine
@@ -110,6 +118,13 @@ class AESPipeline:
             self.srmc = ShiftRowsMixColumnsFusedEnc(ctx, self.mix, states)
         self._fk_cache: Dict[Tuple[int, int], Tuple[Any, Any]] = {}
         self._fk_tag = b""
+        # packed XOR stage of encrypt rounds 1..9; AESFHE_PACKED_XOR=0 for A/B
+        if packed_xor is None:
+            packed_xor = os.environ.get("AESFHE_PACKED_XOR", "1") != "0"
+        self.packed_xor = bool(packed_xor and use_hard_renorm_between_steps and not true_fhe and self.srmc is None
+                               and hasattr(self.mix, "packed_ok") and self.mix.packed_ok())
+        self._pk_cache: List[Any] | None = None
+        self._pk_tag = b""
 
     # ---------------------------------------------------------------- utils
     def _renorm_pair(self, hi, lo, level=None):
@@ -148,8 +163,20 @@ class AESPipeline:
         tag = b"".join(np.ascontiguousarray(k, dtype=np.uint8).tobytes() for k in round_keys)
         if self._rk_cache is None or self._rk_tag != tag:  # encrypted round keys are reused across calls
             self._rk_cache = [self._encode_key(np.asarray(k, dtype=np.uint8)) for k in round_keys]
+            self._rk_raw = [np.array(k, dtype=np.uint8) for k in round_keys]
             self._rk_tag = tag
         return self._rk_cache
+
+    def _packed_round_key(self, r: int):
+        """round key r encrypted in the packed form (after _prepare_round_keys of the same keys)"""
+        if self._pk_cache is None or self._pk_tag != self._rk_tag:
+            self._pk_cache, self._pk_tag = [None] * len(self._rk_cache), self._rk_tag
+        if self._pk_cache[r] is None:
+            key = self._rk_raw[r]
+            if self.states > 1 and key.shape == (16,):
+                key = np.broadcast_to(key, (self.states, 16))
+            self._pk_cache[r] = self.encoder.encode_packed(key)
+        return self._pk_cache[r]
 
     def _fused_key(self, round_keys, r: int, direction: int):
         """round key r permuted by ShiftRows (direction -1) / InvShiftRows (+1), encrypted once:
@@ -202,6 +229,13 @@ class AESPipeline:
         debug dict every step is logged under enc.r{r}.<step> (the names of the reference's
         one-round debug block, REF :154-171)."""
         if debug is None:
+            if self.packed_xor and r > 0:
+                # packed XOR stage (DESIGN.md §4c): MixColumns returns the packed state, AddRoundKey
+                # XORs it with the packed round key, its renorm unpacks into the (hi, lo) pair
+                ct = self._sub_renorm(ct, level=NEED_SR_MIX + self.encoder.PACK_DEPTH)
+                acc = self.mix.mix_packed(*self.shift_rows(*ct))
+                x = self.xor4.apply(acc, self._packed_round_key(r), out_level=self._floor())
+                return self.encoder.renorm_unpack(x, level=next_level)
             ct = self._sub_renorm(ct, level=NEED_SR_MIX)
             ct = self.srmc(*ct) if self.srmc is not None else self.mix_columns(*self.shift_rows(*ct))
             return self._ark_renorm(ct, key_pair, level=next_level)

@@ -61,6 +61,18 @@ class SlotLayout:
             m[(r + 4 * c) * self.unit:(r + 4 * c) * self.unit + self.states] = 1.0
         return self.tile(m)
 
+    @property
+    def packable(self) -> bool:
+        """hi and lo fit side by side in one ciphertext: the packed form holds the
+        hi nibbles in slots (j mod 2P) < P and the lo nibbles in the others (P = period)"""
+        return self.periodic and 2 * self.period <= self.sc
+
+    def half_mask(self, which: int) -> np.ndarray:
+        """ones on the hi (0) / lo (1) half of every 2P-slot block of the packed form"""
+        m = np.zeros(2 * self.period, dtype=np.complex128)
+        m[which * self.period:(which + 1) * self.period] = 1.0
+        return np.tile(m, self.sc // (2 * self.period))
+
     def same(self, other) -> bool:
         return other is not None and (self.sc, self.states, self.periodic) == (other.sc, other.states, other.periodic)
 
@@ -103,6 +115,42 @@ class StateEncoder:
         lo = ZetaEncoder.from_zeta(self._take(self.ctx.decrypt(ct_lo)), 16)
         out = ((hi << 4) | lo).astype(np.uint8)
         return out[0] if self.states == 1 else out
+
+    # ---------------------------------------------------------------- packed form
+    PACK_DEPTH = 1  # pack(): one plaintext product
+
+    def pack(self, ct_hi, ct_lo):
+        """(hi, lo) -> ONE ciphertext, hi on the first half of every 2P-slot block and lo on the
+        second: hi * mask_0 + lo * mask_1 (one level; both halves are P-periodic, so no rotation)"""
+        if not self.layout.packable:
+            raise ValueError("the packed form needs the periodic layout with 2 * period <= slot count")
+        ctx = self.ctx
+        if getattr(self, "_half_pts", None) is None:
+            self._half_pts = [ctx.encode(self.layout.half_mask(w)) for w in (0, 1)]
+        return ctx.add(ctx.multiply(ct_hi, self._half_pts[0]), ctx.multiply(ct_lo, self._half_pts[1]))
+
+    def _packed_slots(self, st: np.ndarray) -> np.ndarray:
+        hi, lo = self._pack(st >> 4), self._pack(st & 0x0F)
+        return np.where(self.layout.half_mask(0).real > 0.5, hi, lo)
+
+    def encode_packed(self, state: np.ndarray):
+        """a state (batch) encrypted directly in the packed form"""
+        return self.ctx.encrypt(self._packed_slots(self._as_batch(state)))
+
+    def decode_packed(self, ct) -> np.ndarray:
+        z = self.ctx.decrypt(ct)
+        hi = ZetaEncoder.from_zeta(self._take(z), 16)
+        lo = ZetaEncoder.from_zeta(self._take(z[self.layout.period:]), 16)
+        out = ((hi << 4) | lo).astype(np.uint8)
+        return out[0] if self.states == 1 else out
+
+    def renorm_packed(self, ct, level=None):
+        """renorm of a packed state, packed again"""
+        return self.ctx.renorm_single(ct, None if _RENORM_FRESH else level)
+
+    def renorm_unpack(self, ct, level=None) -> Tuple[Any, Any]:
+        """renorm of a packed state into the (hi, lo) pair"""
+        return self.ctx.renorm_unpack(ct, self.layout.period, None if _RENORM_FRESH else level)
 
     def renorm(self, ct_hi, ct_lo, level=None) -> Tuple[Any, Any]:
         """decode -> re-encode (REF/pipeline.py:65-69), done on the device when available;

@@ -83,6 +83,14 @@ def bootstrap2(ctx, a, b, period=None):
     return pair(ctx, lambda: ctx.bootstrap(ctx.to_intt(a)), lambda: ctx.bootstrap(ctx.to_intt(b)))
 
 
+def bootstrap1(ctx, ct, period=None):
+    """bootstrap(ct); `period` < slot count: the message's slot period -> the sparse-slot bootstrap"""
+    sparse = getattr(ctx.engine, "bootstrap_sparse", None)
+    if period is not None and period < ctx.engine.slot_count and sparse is not None:
+        return sparse(ctx.to_intt(ct), period)
+    return ctx.bootstrap(ctx.to_intt(ct))
+
+
 def can_fork(ctx) -> bool:
     """two independent halves would run on two streams (utils.pair): then each half batches
     its own products; otherwise both halves' products go into shared batches"""

@@ -182,6 +182,16 @@ int aesfhe_bootstrap_sparse(aesfhe_ctx* ctx, aesfhe_handle ct, int period, doubl
  * snap every slot; level < 0 = the fresh level (as aesfhe_renorm_at otherwise). */
 int aesfhe_renorm_periodic(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, int period, int level, aesfhe_handle* out_hi,
                            aesfhe_handle* out_lo);
+/* Secret-key renorm of ONE ciphertext whose every slot holds a Zeta16 nibble (a packed state
+ * of the pipeline's packed XOR stage): every slot snapped and re-encrypted at
+ * `level` (< 0 = fresh).  Replaces the renorm of REF/pipeline.py:65-69 for that form. */
+int aesfhe_renorm_single(aesfhe_ctx* ctx, aesfhe_handle ct, int level, aesfhe_handle* out);
+/* Secret-key renorm that unpacks: `packed` holds the hi nibbles of an n-periodic state pair in
+ * slots (j mod 2n) < n and the lo nibbles in the others (period = n, a power of two, 2n <=
+ * slots); out_hi / out_lo are the snapped n-periodic hi / lo states at `level` -- the
+ * (hi, lo) pair REF/pipeline.py:65-69's renorm returns. */
+int aesfhe_renorm_unpack(aesfhe_ctx* ctx, aesfhe_handle packed, int period, int level, aesfhe_handle* out_hi,
+                         aesfhe_handle* out_lo);
 int aesfhe_bootstrap_pair_sparse(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int period, double gain, aesfhe_handle* out_a,
                                  aesfhe_handle* out_b);
 int aesfhe_bootstrap_pair_scaled(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, double gain, aesfhe_handle* out_a,

@@ -1,0 +1,98 @@
+"""The packed XOR stage: hi and lo side by side in ONE ciphertext for the steps
+whose LUT is the same for both halves -- MixColumns' XOR4s and the AddRoundKey after it.
+
+- StateEncoder.pack / encode_packed / decode_packed and the two packed renorms
+  (aesfhe_renorm_single, aesfhe_renorm_unpack) against the byte model;
+- one XOR4 on packed states == the XOR pair (REF/xor4_lut.py:10-78 per nibble);
+- MixColFinal.mix_packed == REF/mixcol_final.py's MixColumns bytes (final bootstrap on);
+- full C2 encrypts through the packed path (no debug dict: the debug path keeps the pair steps)
+  == aes_plain.ref_encrypt, one state and a 64-state batch, and == the pair path's bytes.
+Decoded bytes must be exact.
+"""
+import numpy as np
+import pytest
+
+from conftest import gpu_context
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return gpu_context(log_n=16, signature=1)
+
+
+@pytest.fixture(scope="module")
+def co(coeff_dir):
+    from aes_keyschedule import load_all_coeffs
+    return load_all_coeffs(coeff_dir)
+
+
+@pytest.mark.parametrize("states", [1, 64])
+def test_pack_renorm_roundtrip(ctx, states):
+    from state_encoder import StateEncoder
+    from utils import NEED_XOR
+    enc = StateEncoder(ctx, states, periodic=True)
+    rng = np.random.default_rng(states)
+    st = rng.integers(0, 256, (states, 16) if states > 1 else 16).astype(np.uint8)
+    p = enc.pack(*enc.encode(st))
+    assert np.array_equal(enc.decode_packed(p), st)
+    assert np.array_equal(enc.decode_packed(enc.encode_packed(st)), st)
+    q = enc.renorm_packed(p, level=NEED_XOR)
+    assert q.level == NEED_XOR and np.array_equal(enc.decode_packed(q), st)
+    hi, lo = enc.renorm_unpack(p, level=NEED_XOR)
+    assert hi.level == lo.level == NEED_XOR
+    assert np.array_equal(enc.decode(hi, lo), st)
+    with pytest.raises(RuntimeError, match="packed period"):
+        ctx.engine.renorm_unpack(p, 24)
+
+
+def test_xor4_on_packed_states(ctx, co):
+    from state_encoder import StateEncoder
+    from utils import NEED_XOR, RENORM_FLOOR
+    from xor4_lut import XOR4LUT
+    enc = StateEncoder(ctx, periodic=True)
+    xor4 = XOR4LUT(ctx, co["xor4"])
+    rng = np.random.default_rng(5)
+    a, b = rng.integers(0, 256, 16).astype(np.uint8), rng.integers(0, 256, 16).astype(np.uint8)
+    pa = enc.renorm_packed(enc.encode_packed(a), level=NEED_XOR)
+    pb = enc.pack(*enc.renorm(*enc.encode(b), level=NEED_XOR + enc.PACK_DEPTH))
+    x = xor4.apply(pa, pb, out_level=RENORM_FLOOR)
+    assert np.array_equal(enc.decode_packed(x), a ^ b)
+    assert np.array_equal(enc.decode(*enc.renorm_unpack(x)), a ^ b)
+
+
+def test_mix_packed_matches_mixcolumns(ctx, co):
+    from mixcol_final import MixColFinal
+    from oracle import aes_plain
+    from state_encoder import StateEncoder
+    from utils import NEED_SR_MIX, SHIFTROWS_DEPTH
+    from xor4_lut import XOR4LUT
+    enc = StateEncoder(ctx, periodic=True)
+    mc = MixColFinal(ctx, XOR4LUT(ctx, co["xor4"]), layout=enc.layout)
+    assert mc.packed_ok()
+    rng = np.random.default_rng(6)
+    st = rng.integers(0, 256, 16).astype(np.uint8)
+    x = enc.renorm(*enc.encode(st), level=NEED_SR_MIX + enc.PACK_DEPTH - SHIFTROWS_DEPTH)
+    out = mc.mix_packed(*x)
+    assert out.level == ctx.engine.fresh_level
+    assert np.array_equal(enc.decode_packed(out), aes_plain.ref_mix_columns(st))
+
+
+@pytest.mark.parametrize("states,seed", [(1, 7), (1, 42), (64, 3)])
+def test_encrypt_through_packed_stage(ctx, co, states, seed):
+    from aes_keyschedule import expand_aes128_key
+    from oracle import aes_plain
+    from pipeline import AESPipeline
+    pipe = AESPipeline(ctx, co, use_hard_renorm_between_steps=True, states=states)
+    assert pipe.packed_xor
+    rng = np.random.default_rng(seed)
+    rks = expand_aes128_key(rng.integers(0, 256, 16).astype(np.uint8))
+    pt = rng.integers(0, 256, (states, 16) if states > 1 else 16).astype(np.uint8)
+    got = pipe.encoder.decode(*pipe.encrypt(pt, rks))
+    want = aes_plain.ref_encrypt(pt, rks) if states == 1 else np.stack([aes_plain.ref_encrypt(p, rks) for p in pt])
+    assert np.array_equal(got, want)
+    if states == 1:
+        ref = AESPipeline(ctx, co, use_hard_renorm_between_steps=True, packed_xor=False)
+        assert not ref.packed_xor
+        assert np.array_equal(ref.encoder.decode(*ref.encrypt(pt, rks)), want)

@@ -33,12 +33,12 @@ def run(rounds):
     st = np.random.randint(0, 256, 16, dtype=np.uint8)
     rk = pipe._prepare_round_keys(rks)
     ct = pipe._ark_renorm(pipe.encoder.encode(st), rk[0], level=15)
-    c = pipe.encrypt_round(ct, rk[1])  # warm: keys, plaintext encodings, bootstrap plan
+    c = pipe.encrypt_round(ct, rk[1], r=1)  # warm: keys, plaintext encodings, bootstrap plan
     E.sync()
     time.sleep(0.1)
     t = time.perf_counter()
     for r in range(rounds):
-        c = pipe.encrypt_round(c, rk[2 + r % 8])
+        c = pipe.encrypt_round(c, rk[2 + r % 8], r=2 + r % 8)
     host = (time.perf_counter() - t) * 1e3 / rounds  # enqueue time: the host returns before the GPU ends
     E.sync()
     ms = (time.perf_counter() - t) * 1e3 / rounds

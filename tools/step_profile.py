@@ -29,7 +29,9 @@ def main():
     st = np.random.randint(0, 256, 16, dtype=np.uint8)
     rk = pipe._prepare_round_keys(rks)
     ct = pipe._ark_renorm(pipe.encoder.encode(st), rk[0], level=15)
-    pipe.encrypt_round(ct, rk[1])  # warm caches (plaintext encodings, keys, bootstrap plan)
+    pipe.encrypt_round(ct, rk[1], r=1)  # warm caches (plaintext encodings, keys, bootstrap plan)
+    if pipe.packed_xor:
+        pipe._packed_round_key(2)  # the packed round key the timed AddRoundKey uses
     E.sync()
     res = {}
 
@@ -45,19 +47,24 @@ def main():
         round_steps(pipe, ct, rk, res, timed)
     res = {k: v / reps for k, v in res.items()}
     res["mc.final_bootstrap_pair(derived)"] = res["mix_columns(total)"] - res["mix_columns(no final bootstrap)"]
-    print(json.dumps({"lazy": lazy, "serial": serial, "reps": reps, "ms": {k: round(v, 2) for k, v in res.items()}}, indent=1))
+    print(json.dumps({"lazy": lazy, "serial": serial, "packed_xor": pipe.packed_xor, "reps": reps, "ms": {k: round(v, 2) for k, v in res.items()}}, indent=1))
 
 
 def round_steps(pipe, ct, rk, res, timed):
     from utils import NEED_SR_MIX, NEED_SUBBYTES
     t0 = time.perf_counter()
-    c = timed("sub_bytes+renorm", lambda: pipe._sub_renorm(ct, level=NEED_SR_MIX))
+    packed = pipe.packed_xor  # MixColumns' XOR stage + AddRoundKey on packed states
+    c = timed("sub_bytes+renorm", lambda: pipe._sub_renorm(ct, level=NEED_SR_MIX + (pipe.encoder.PACK_DEPTH if packed else 0)))
     c = timed("shift_rows", pipe.shift_rows, *c)
-    mix = pipe.mix
+    mix = pipe.mix.mix_packed if packed else pipe.mix
     nb0 = res.get("mix_columns(no final bootstrap)", 0.0)
     c_nb = timed("mix_columns(no final bootstrap)", lambda: mix(*c, do_final_bootstrap=False))
     c = timed("mix_columns(total)", lambda: mix(*c))
-    c = timed("add_round_key+renorm", lambda: pipe._ark_renorm(c, rk[2], level=NEED_SUBBYTES))
+    if packed:
+        c = timed("add_round_key+renorm", lambda: pipe.encoder.renorm_unpack(
+            pipe.xor4.apply(c, pipe._packed_round_key(2), out_level=pipe._floor()), level=NEED_SUBBYTES))
+    else:
+        c = timed("add_round_key+renorm", lambda: pipe._ark_renorm(c, rk[2], level=NEED_SUBBYTES))
     res["round_total"] = res.get("round_total", 0.0) + (time.perf_counter() - t0) * 1e3 - (res["mix_columns(no final bootstrap)"] - nb0)
 
 
