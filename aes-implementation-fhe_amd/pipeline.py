@@ -125,6 +125,13 @@ class AESPipeline:
                                and hasattr(self.mix, "packed_ok") and self.mix.packed_ok())
         self._pk_cache: List[Any] | None = None
         self._pk_tag = b""
+        # the level encrypt's renorms hand SubBytes: one above its depth in renorm mode, so that it
+        # takes the bivariate giant-step form (sub_bytes_lut._outputs_biv; AESFHE_SB_BIV=0 for A/B)
+        self.need_sub = NEED_SUBBYTES
+        fresh = getattr(ctx.engine, "fresh_level", None)
+        if (use_hard_renorm_between_steps and not true_fhe and fresh is not None and getattr(ctx, "fused_luts", False)
+                and os.environ.get("AESFHE_SB_BIV", "1") != "0"):
+            self.need_sub = min(NEED_SUBBYTES + 1, fresh)
 
     # ---------------------------------------------------------------- utils
     def _renorm_pair(self, hi, lo, level=None):
@@ -224,10 +231,12 @@ class AESPipeline:
         return self.invmix(ct_hi, ct_lo)
 
     # ---------------------------------------------------------------- encrypt
-    def encrypt_round(self, ct, key_pair, debug=None, r: int = 0, next_level: int = NEED_SUBBYTES):
+    def encrypt_round(self, ct, key_pair, debug=None, r: int = 0, next_level: int | None = None):
         """One middle round r = 1..9: SB, renorm, SR, MC, ARK, renorm (REF :142-151).  With a
         debug dict every step is logged under enc.r{r}.<step> (the names of the reference's
         one-round debug block, REF :154-171)."""
+        if next_level is None:
+            next_level = self.need_sub
         if debug is None:
             if self.packed_xor and r > 0:
                 # packed XOR stage (DESIGN.md §4c): MixColumns returns the packed state, AddRoundKey
@@ -266,10 +275,10 @@ class AESPipeline:
         rk = self._prepare_round_keys(round_keys)
         ct = self.ark(*ct, *rk[0], out_level=self._floor())
         self._log_pair(debug, "enc.r0.ark", *ct)
-        ct = self._renorm_pair(*ct, level=NEED_SUBBYTES)
+        ct = self._renorm_pair(*ct, level=self.need_sub)
         self._log_pair(debug, "enc.r0.renorm", *ct)
         for r in range(1, 10):
-            nxt = NEED_SUB_ARK_SR if (self.fuse_sub_ark and r == 9) else NEED_SUBBYTES
+            nxt = NEED_SUB_ARK_SR if (self.fuse_sub_ark and r == 9) else self.need_sub
             ct = self.encrypt_round(ct, rk[r], debug, r, next_level=nxt)
         if self.fuse_sub_ark:
             # SR(SB(x)) ^ k10 = SR(SB(x) ^ InvShiftRows(k10)): one fused LUT, then ShiftRows

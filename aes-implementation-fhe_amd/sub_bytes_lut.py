@@ -18,6 +18,7 @@ Evaluation forms (same polynomials, same output level, outputs equal up to CKKS 
   b^1..b^15 (one fused LUT kernel each) and giant steps G_i = b^(16 i).  The lift is split
   the same way over y^1..y^8.  Key switches per SubBytes drop from ~270 to ~37.
 """
+import os
 from typing import Any, Dict, Tuple
 
 import numpy as np
@@ -63,12 +64,16 @@ class SubBytesLUTFastCached:
 
     def apply(self, ct_hi: Any, ct_lo: Any, out_level=None) -> Tuple[Any, Any]:
         """(S_hi, S_lo)(hi, lo); out_level: the lowest level the caller needs the result at
-        (inputs dropped to out_level + SUBBYTES_DEPTH first, utils.drop_to); None = as given."""
+        (inputs dropped to out_level + SUBBYTES_DEPTH first, utils.drop_to); None = as given.
+        Inputs one level higher than that take the bivariate giant-step form (_outputs_biv)."""
+        biv = False
         if out_level is not None:
             lv = out_level + SUBBYTES_DEPTH
+            if os.environ.get("AESFHE_SB_BIV", "1") != "0" and min(getattr(c, "level", -1) for c in (ct_hi, ct_lo)) > lv:
+                biv, lv = True, lv + 1
             ct_hi, ct_lo = drop_to(self.ctx, ct_hi, lv), drop_to(self.ctx, ct_lo, lv)
         if getattr(self.ctx, "fused_luts", False):
-            return self._apply_bsgs(ct_hi, ct_lo)
+            return self._apply_bsgs(ct_hi, ct_lo, biv)
         return self._apply_direct(ct_hi, ct_lo)
 
     # ------------------------------------------------------------------ BSGS form
@@ -125,9 +130,13 @@ class SubBytesLUTFastCached:
             self._bsgs = dict(lift=(lp, lq), hi=self._split(self.hi, 128), lo=self._split(self.lo, 128))
         return self._bsgs
 
-    def _apply_bsgs(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:
+    def _apply_bsgs(self, ct_hi: Any, ct_lo: Any, biv: bool = False) -> Tuple[Any, Any]:
         ctx = self.ctx
         baby, g, ct_b = self._bsgs_bases(ct_hi, ct_lo)
+        if biv:
+            out = self._outputs_biv(baby, g, ct_b)
+            if out is not None:
+                return out
         batch = getattr(ctx, "multiply_many", None) is not None
         if batch:
             if can_fork(ctx):  # each output nibble batches its own products, on its own stream
@@ -199,6 +208,42 @@ class SubBytesLUTFastCached:
             acc[wp] = a
         cq = conj_many(ctx, [acc[(w, "q")] for w in whiches])
         return tuple(ctx.add(acc[(w, "p")], c) for w, c in zip(whiches, cq))
+
+    def _outputs_biv(self, baby, g, ct_b):
+        """both output nibbles with every part P, Q (f = P(b) + conj(Q(b))) as three fused sums:
+        the chunk-0 sum c_0 + sum_j c_j b^j (univariate over the baby steps), the column
+        sum_i c_16i G_i (univariate over the giant steps), and the rest, sum_{i>=1, j>=1}
+        c_(16i+j) b^j G_i, as ONE bivariate LUT over (baby, giant) -- the chunk sums S_i and their
+        products S_i G_i fused into one kernel and one relinearisation instead
+        of 8 LUT kernels, 8 products and their rescales per part.  The coefficients meet the
+        products at the giant steps' level: one level more than _outputs_batched (the caller's
+        inputs sit one level higher).  None when a fused sum is unavailable (level)."""
+        ctx = self.ctx
+        acc = {}
+        for which in ("hi", "lo"):
+            for part, coef in zip(("p", "q"), self._bsgs[which]):
+                nch = (len(coef) + 15) // 16
+                key = (which, part)
+                C = np.zeros((16, nch), np.complex128)
+                gcol = np.zeros(nch, np.complex128)
+                for i in range(1, nch):
+                    seg = coef[16 * i: 16 * i + 16]
+                    gcol[i] = seg[0]
+                    C[1:len(seg), i] = seg[1:]
+                c0 = coef[:16]
+                t = [self._lin((key, 0), np.r_[0, c0[1:]], baby, c0[0], ct_b)]
+                for sub, vec, args in (("g", gcol, (g,)), ("bg", C, (baby, g))):
+                    if np.any(vec):
+                        r = fused_lut(ctx, (key, sub), vec, *args, owner=self)
+                        if r is None:
+                            return None
+                        t.append(r)
+                a = t[0]
+                for x in t[1:]:
+                    a = ctx.add(a, x)
+                acc[key] = a
+        cq = conj_many(ctx, [acc[(w, "q")] for w in ("hi", "lo")])
+        return tuple(ctx.add(acc[(w, "p")], c) for w, c in zip(("hi", "lo"), cq))
 
     # ------------------------------------------------------------------ direct (reference) form
     def _apply_direct(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:

@@ -6,7 +6,8 @@ whose LUT is the same for both halves -- MixColumns' XOR4s and the AddRoundKey a
 - one XOR4 on packed states == the XOR pair (REF/xor4_lut.py:10-78 per nibble);
 - MixColFinal.mix_packed == REF/mixcol_final.py's MixColumns bytes (final bootstrap on);
 - full C2 encrypts through the packed path (no debug dict: the debug path keeps the pair steps)
-  == aes_plain.ref_encrypt, one state and a 64-state batch, and == the pair path's bytes.
+  == aes_plain.ref_encrypt, one state and a 64-state batch, and == the pair path's bytes;
+- SubBytes' bivariate giant-step form (sub_bytes_lut._outputs_biv) == the S-box on all bytes.
 Decoded bytes must be exact.
 """
 import numpy as np
@@ -96,3 +97,25 @@ def test_encrypt_through_packed_stage(ctx, co, states, seed):
         ref = AESPipeline(ctx, co, use_hard_renorm_between_steps=True, packed_xor=False)
         assert not ref.packed_xor
         assert np.array_equal(ref.encoder.decode(*ref.encrypt(pt, rks)), want)
+
+
+def test_subbytes_bivariate_giant_step_form(ctx, co):
+    """SubBytes from one level above its depth takes the bivariate giant-step form
+    (sub_bytes_lut._outputs_biv: chunk sums and their giant-step products as ONE bivariate LUT):
+    the S-box on all 256 byte values (16 states x 16 bytes), like the batched-product form"""
+    from oracle import aes_plain
+    from state_encoder import StateEncoder
+    from sub_bytes_lut import SubBytesLUT
+    from utils import NEED_SUBBYTES, RENORM_FLOOR
+    enc = StateEncoder(ctx, 16, periodic=True)
+    sb = SubBytesLUT(ctx, co["sub_hi"], co["sub_lo"])
+    st = np.arange(256, dtype=np.uint8).reshape(16, 16)
+    want = np.asarray(aes_plain.SBOX, np.uint8)[st]
+    x = enc.renorm(*enc.encode(st), level=NEED_SUBBYTES + 1)
+    hi, lo = sb.apply(*x, out_level=RENORM_FLOOR)
+    assert hi.level >= RENORM_FLOOR and lo.level >= RENORM_FLOOR
+    got = enc.decode(hi, lo)
+    y = enc.renorm(*enc.encode(st), level=NEED_SUBBYTES)
+    ref = enc.decode(*sb.apply(*y, out_level=RENORM_FLOOR))  # the batched-product form
+    assert np.array_equal(got, want)
+    assert np.array_equal(ref, want)

@@ -26,7 +26,7 @@ def main():
     rks = expand_aes128_key(np.random.randint(0, 256, 16, dtype=np.uint8))
     st = np.random.randint(0, 256, 16, dtype=np.uint8)
     rk = pipe._prepare_round_keys(rks)
-    ct = pipe._ark_renorm(pipe.encoder.encode(st), rk[0], level=15)
+    ct = pipe._ark_renorm(pipe.encoder.encode(st), rk[0], level=pipe.need_sub)
     ct = pipe.encrypt_round(ct, rk[1], r=1)
     E.sync()
     print(json.dumps({"round1_state_decodes": pipe.encoder.decode(*ct).tolist()}), flush=True)

@@ -32,7 +32,7 @@ def run(rounds):
     rks = expand_aes128_key(np.random.randint(0, 256, 16, dtype=np.uint8))
     st = np.random.randint(0, 256, 16, dtype=np.uint8)
     rk = pipe._prepare_round_keys(rks)
-    ct = pipe._ark_renorm(pipe.encoder.encode(st), rk[0], level=15)
+    ct = pipe._ark_renorm(pipe.encoder.encode(st), rk[0], level=pipe.need_sub)
     c = pipe.encrypt_round(ct, rk[1], r=1)  # warm: keys, plaintext encodings, bootstrap plan
     E.sync()
     time.sleep(0.1)

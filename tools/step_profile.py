@@ -28,7 +28,7 @@ def main():
     rks = expand_aes128_key(np.random.randint(0, 256, 16, dtype=np.uint8))
     st = np.random.randint(0, 256, 16, dtype=np.uint8)
     rk = pipe._prepare_round_keys(rks)
-    ct = pipe._ark_renorm(pipe.encoder.encode(st), rk[0], level=15)
+    ct = pipe._ark_renorm(pipe.encoder.encode(st), rk[0], level=pipe.need_sub)
     pipe.encrypt_round(ct, rk[1], r=1)  # warm caches (plaintext encodings, keys, bootstrap plan)
     if pipe.packed_xor:
         pipe._packed_round_key(2)  # the packed round key the timed AddRoundKey uses
@@ -62,9 +62,9 @@ def round_steps(pipe, ct, rk, res, timed):
     c = timed("mix_columns(total)", lambda: mix(*c))
     if packed:
         c = timed("add_round_key+renorm", lambda: pipe.encoder.renorm_unpack(
-            pipe.xor4.apply(c, pipe._packed_round_key(2), out_level=pipe._floor()), level=NEED_SUBBYTES))
+            pipe.xor4.apply(c, pipe._packed_round_key(2), out_level=pipe._floor()), level=pipe.need_sub))
     else:
-        c = timed("add_round_key+renorm", lambda: pipe._ark_renorm(c, rk[2], level=NEED_SUBBYTES))
+        c = timed("add_round_key+renorm", lambda: pipe._ark_renorm(c, rk[2], level=pipe.need_sub))
     res["round_total"] = res.get("round_total", 0.0) + (time.perf_counter() - t0) * 1e3 - (res["mix_columns(no final bootstrap)"] - nb0)
 
 

@@ -1,8 +1,10 @@
-"""Kernel breakdown of one XOR4 at the renorm floor (the most frequent AES step op) for
-rocprofv3 --kernel-trace: run mode repeats it after a marker gap; analyse mode reports per
-kernel family calls / us per XOR4 and the NTT launches' row counts (Grid_Size / 4096 at N = 2^16).
-usage: xor4_trace.py run [ITERS] | xor4_trace.py analyse OUT.json DIR ITERS"""
+"""Kernel breakdown of one AES step op for rocprofv3 --kernel-trace: one XOR4 at the renorm
+floor (the most frequent op) or, with OP=sub, one SubBytes (no renorm) from its input level.
+run mode repeats it after a marker gap; analyse mode reports per kernel family calls / us per
+op and the NTT launches' row counts (Grid_Size / 4096 at N = 2^16).
+usage: xor4_trace.py run [ITERS] [OP] | xor4_trace.py analyse OUT.json DIR ITERS"""
 import csv
+import os
 import json
 import re
 import sys
@@ -14,7 +16,7 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path[:0] = [str(ROOT), str(ROOT / "aes-implementation-fhe_amd")]
 
 
-def run(iters):
+def run(iters, op="xor4"):
     import numpy as np
     from aes_keyschedule import load_all_coeffs
     from engine_context import EngineContext
@@ -28,14 +30,21 @@ def run(iters):
     st = np.arange(16, dtype=np.uint8)
     a = enc.renorm(*enc.encode(st), level=NEED_XOR)
     b = enc.renorm(*enc.encode(st[::-1].copy()), level=NEED_XOR)
-    xor4.apply(a[0], b[0], RENORM_FLOOR)
+    fn = lambda: xor4.apply(a[0], b[0], RENORM_FLOOR)
+    if op == "sub":
+        from sub_bytes_lut import SubBytesLUT
+        from utils import NEED_SUBBYTES
+        sb = SubBytesLUT(ctx, *[load_all_coeffs()[k] for k in ("sub_hi", "sub_lo")])
+        x = enc.renorm(*enc.encode(st), level=NEED_SUBBYTES + (os.environ.get('AESFHE_SB_BIV', '1') != '0'))
+        fn = lambda: sb.apply(*x, out_level=RENORM_FLOOR)
+    fn()
     E.sync()
     time.sleep(0.1)
     t = time.perf_counter()
     for _ in range(iters):
-        xor4.apply(a[0], b[0], RENORM_FLOOR)
+        fn()
     E.sync()
-    print(json.dumps({"iters": iters, "ms_per_xor4": (time.perf_counter() - t) * 1e3 / iters}), flush=True)
+    print(json.dumps({"op": op, "iters": iters, "ms_per_op": (time.perf_counter() - t) * 1e3 / iters}), flush=True)
 
 
 def analyse(out, d, iters):
@@ -63,8 +72,8 @@ def analyse(out, d, iters):
         if "k_ntt" in n2:
             ntt_rows[(m.group(1), g // 4096)] += 1
     span = sel[-1][1] - sel[0][0]
-    res = {"iters": iters, "launches_per_xor4": len(sel) / iters, "span_us_per_xor4": span / 1e3 / iters,
-           "kernel_us_per_xor4": sum(e - s for s, e, _, _ in sel) / 1e3 / iters,
+    res = {"iters": iters, "launches_per_op": len(sel) / iters, "span_us_per_op": span / 1e3 / iters,
+           "kernel_us_per_op": sum(e - s for s, e, _, _ in sel) / 1e3 / iters,
            "families": {k: {"calls": v[0] / iters, "us": round(v[1] / 1e3 / iters, 2), "avg_us": round(v[1] / 1e3 / v[0], 2)}
                         for k, v in sorted(fam.items(), key=lambda kv: -kv[1][1])},
            "ntt_rows": {f"{k[0]}:{k[1]}": v / iters for k, v in sorted(ntt_rows.items())}}
@@ -74,6 +83,6 @@ def analyse(out, d, iters):
 
 if __name__ == "__main__":
     if sys.argv[1] == "run":
-        run(int(sys.argv[2]) if len(sys.argv) > 2 else 20)
+        run(int(sys.argv[2]) if len(sys.argv) > 2 else 20, sys.argv[3] if len(sys.argv) > 3 else "xor4")
     else:
         analyse(sys.argv[2], sys.argv[3], int(sys.argv[4]))
