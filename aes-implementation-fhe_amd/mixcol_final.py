@@ -9,6 +9,7 @@ result is bootstrapped (do_final_bootstrap, default True).
 from __future__ import annotations
 
 import json
+import os
 from typing import Any, Dict, Tuple
 
 import numpy as np
@@ -189,13 +190,30 @@ class MixColFinal:
         mix_rotated become three single XOR4s, their renorms single-ciphertext renorms, and the
         final bootstrap one sparse bootstrap at period 2P.  Returns the PACKED output (the caller's
         AddRoundKey XORs it with a packed round key and unpacks in its renorm).  The GF
-        multipliers stay pairs (they mix hi and lo); their outputs and r2, r3 are packed (one
-        level: inputs one level higher than mix_rotated's, pipeline NEED_SR_MIX_PACKED)."""
+        multipliers stay pairs (they mix hi and lo); their outputs and the column shifts are
+        packed (one level: inputs one level higher than mix_rotated's).  Default form
+        (AESFHE_MC_FORM=xtime): 2x ^ 3 r1 ^ r2 ^ r3 = 2 (x ^ r1) ^ (r1 ^ r2 ^ r3), xtime being
+        GF(2)-linear -- one GF multiplier pair on the renormalised, unpacked x ^ r1 and four single
+        XOR4s; AESFHE_MC_FORM=2gf keeps the reference's two multiplier pairs (GF2(x), GF3(r1)).
+        The bytes are the same either way."""
         ctx, enc = self.ctx, self.enc
         steps = [-4 * k * self.stride for k in (1, 2, 3)]
         rh, rl = pair(ctx, lambda: rot_many(ctx, ct_hi, steps), lambda: rot_many(ctx, ct_lo, steps))
         fl = RENORM_FLOOR
         gl = fl + LUT2_DEPTH + enc.PACK_DEPTH
+        if os.environ.get("AESFHE_MC_FORM", "xtime") == "xtime":
+            # 2x ^ 3 r1 ^ r2 ^ r3 = 2 (x ^ r1) ^ (r1 ^ r2 ^ r3) (xtime is GF(2)-linear): ONE GF
+            # multiplier pair and four single XOR4s instead of two pairs and three XOR4s
+            p1, p0 = pair(ctx, lambda: enc.pack(rh[0], rl[0]), lambda: enc.pack(ct_hi, ct_lo), shared=(ct_hi, ct_lo, *rh, *rl))
+            r2, r3 = pair(ctx, lambda: enc.pack(rh[1], rl[1]), lambda: enc.pack(rh[2], rl[2]))
+            u, v = pair(ctx, lambda: enc.renorm_unpack(self._xor_ct(p0, p1, fl), level=gl + LUT2_DEPTH),
+                        lambda: enc.renorm_packed(self._xor_ct(r2, r3, fl), level=NEED_XOR), shared=(p1,))
+            two, w = pair(ctx, lambda: enc.pack(*self.gf_mult_2(*u, out_level=gl)),
+                          lambda: enc.renorm_packed(self._xor_ct(p1, v, fl), level=NEED_XOR))
+            acc = enc.renorm_packed(self._xor_ct(two, w, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
+            if do_final_bootstrap:
+                acc = bootstrap1(ctx, acc, 2 * self.layout.period)
+            return acc
         two, thr = pair(ctx, lambda: self.gf_mult_2(ct_hi, ct_lo, out_level=gl),
                         lambda: self.gf_mult_3(rh[0], rl[0], out_level=gl))
         p2, p3 = pair(ctx, lambda: enc.pack(*two), lambda: enc.pack(*thr), shared=(*two, *thr))
