@@ -10,7 +10,7 @@ from mixcol_final import _CoeffCache, gf_basis16, gf_eval, gf_mult_pair
 from shift_rows import row_masks
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT
-from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap2, pair, rot_many
+from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, pair, rot_many
 
 
 class InvMixColumnsFHE:
@@ -72,6 +72,31 @@ class InvMixColumnsFHE:
 
     def _col_shift_rowmajor(self, ct, k_up: int):
         return self.ctx.rotate(ct, -4 * k_up * self.stride)
+
+    def packed_ok(self) -> bool:
+        """the packed XOR stage applies (see MixColFinal.packed_ok)"""
+        return (self.use_hard_renorm and self.layout.packable and self.enc.renorm_hook is None
+                and getattr(self.ctx, "fused_luts", False) and getattr(self.ctx, "renorm_unpack", None) is not None)
+
+    def imc_packed(self, ct_hi, ct_lo, do_final_bootstrap: bool = True):
+        """InvMixColumns with its XOR stage on packed states (MixColFinal.mix_packed):
+        the four GF multiplier pairs' outputs packed (inputs one level higher than __call__'s),
+        three single XOR4s and single renorms, one sparse bootstrap at period 2P.  Returns the
+        PACKED output; the caller's renorm unpacks it."""
+        ctx, enc = self.ctx, self.enc
+        steps = [-4 * k * self.stride for k in (1, 2, 3)]
+        rh, rl = pair(ctx, lambda: rot_many(ctx, ct_hi, steps), lambda: rot_many(ctx, ct_lo, steps))
+        fl = RENORM_FLOOR
+        gl = fl + LUT2_DEPTH + enc.PACK_DEPTH
+        gf = lambda m, hi, lo: enc.pack(*self._gf(m, hi, lo, gl))
+        p14, p11 = pair(ctx, lambda: gf(14, ct_hi, ct_lo), lambda: gf(11, rh[0], rl[0]))
+        p13, p9 = pair(ctx, lambda: gf(13, rh[1], rl[1]), lambda: gf(9, rh[2], rl[2]))
+        x1, x2 = pair(ctx, lambda: enc.renorm_packed(self._xor(p14, p11, fl), level=NEED_XOR),
+                      lambda: enc.renorm_packed(self._xor(p13, p9, fl), level=NEED_XOR))
+        acc = enc.renorm_packed(self._xor(x1, x2, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
+        if do_final_bootstrap:
+            acc = bootstrap1(ctx, acc, 2 * self.layout.period)
+        return acc
 
     def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None,
                  final_renorm: bool = True):

@@ -125,6 +125,9 @@ class AESPipeline:
                                and hasattr(self.mix, "packed_ok") and self.mix.packed_ok())
         self._pk_cache: List[Any] | None = None
         self._pk_tag = b""
+        # the same for decrypt rounds 9..1: AddRoundKey + InvMixColumns (with_inv_mix_columns)
+        self.packed_dec = bool(self.packed_xor and with_inv_mix_columns and not fuse_sub_ark
+                               and hasattr(self.invmix, "packed_ok") and self.invmix.packed_ok())
         # the level encrypt's renorms hand SubBytes: one above its depth in renorm mode, so that it
         # takes the bivariate giant-step form (sub_bytes_lut._outputs_biv; AESFHE_SB_BIV=0 for A/B)
         self.need_sub = NEED_SUBBYTES
@@ -327,6 +330,14 @@ class AESPipeline:
                 if self.with_inv_mix_columns:
                     ct = self._renorm_pair(*self.inv_mix_columns(*ct), level=NEED_SUB_ARK_SR)
                     self._log_pair(debug, f"dec.r{r}.imc", *ct)
+                continue
+            if debug is None and self.packed_dec:
+                # packed XOR stage: AddRoundKey on the packed state, its renorm
+                # unpacking; InvMixColumns' XOR stage packed, unpacked by the renorm after it
+                ct = self._sub_renorm(self.inv_shift_rows(*ct), inverse=True, level=NEED_XOR + self.encoder.PACK_DEPTH)
+                x = self.xor4.apply(self.encoder.pack(*ct), self._packed_round_key(r), out_level=self._floor())
+                ct = self.encoder.renorm_unpack(x, level=NEED_GF + self.encoder.PACK_DEPTH)
+                ct = self.encoder.renorm_unpack(self.invmix.imc_packed(*ct), level=NEED_ISR_ISB)
                 continue
             ct = self.inv_shift_rows(*ct)
             self._log_pair(debug, f"dec.r{r}.isr", *ct)

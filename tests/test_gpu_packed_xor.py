@@ -6,7 +6,8 @@ whose LUT is the same for both halves -- MixColumns' XOR4s and the AddRoundKey a
 - one XOR4 on packed states == the XOR pair (REF/xor4_lut.py:10-78 per nibble);
 - MixColFinal.mix_packed == REF/mixcol_final.py's MixColumns bytes (final bootstrap on);
 - full C2 encrypts through the packed path (no debug dict: the debug path keeps the pair steps)
-  == aes_plain.ref_encrypt, one state and a 64-state batch, and == the pair path's bytes;
+  == aes_plain.ref_encrypt, one state and a 64-state batch, and == the pair path's bytes, and
+  decrypt through the packed AddRoundKey / InvMixColumns stage returns the plaintext;
 - SubBytes' bivariate giant-step form (sub_bytes_lut._outputs_biv) == the S-box on all bytes.
 Decoded bytes must be exact.
 """
@@ -86,13 +87,16 @@ def test_encrypt_through_packed_stage(ctx, co, states, seed):
     from oracle import aes_plain
     from pipeline import AESPipeline
     pipe = AESPipeline(ctx, co, use_hard_renorm_between_steps=True, states=states)
-    assert pipe.packed_xor
+    assert pipe.packed_xor and pipe.packed_dec
     rng = np.random.default_rng(seed)
     rks = expand_aes128_key(rng.integers(0, 256, 16).astype(np.uint8))
     pt = rng.integers(0, 256, (states, 16) if states > 1 else 16).astype(np.uint8)
-    got = pipe.encoder.decode(*pipe.encrypt(pt, rks))
+    ct = pipe.encrypt(pt, rks)
+    got = pipe.encoder.decode(*ct)
     want = aes_plain.ref_encrypt(pt, rks) if states == 1 else np.stack([aes_plain.ref_encrypt(p, rks) for p in pt])
     assert np.array_equal(got, want)
+    # decrypt rounds through the packed AddRoundKey + InvMixColumns XOR stage
+    assert np.array_equal(pipe.encoder.decode(*pipe.decrypt(*ct, rks)), pt)
     if states == 1:
         ref = AESPipeline(ctx, co, use_hard_renorm_between_steps=True, packed_xor=False)
         assert not ref.packed_xor
