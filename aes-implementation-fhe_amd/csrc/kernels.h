@@ -21,7 +21,7 @@ struct KernelProfiler {
     struct Rec {
         hipEvent_t a, b;
         int kid;
-        double bytes;
+        double bytes, work;
     };
     std::vector<Rec> recs;
     std::vector<hipEvent_t> pool;
@@ -32,9 +32,11 @@ struct KernelProfiler {
     void flush();   // waits for recorded events and clock slots and folds them into the totals
     void reset();
     // In-kernel clock (s_memrealtime, 100 MHz) for the NTT, base-conversion and key-switch
-    // kernels: a timed launch gets a slot {earliest block start, latest block end}, the span
-    // rocprofv3 reports.  HIP event pairs around a launch add ~4 us per launch on this stack
-    // (DESIGN.md §5), so they are kept only for the element-wise kernels.
+    // kernels: a timed launch gets a slot {earliest sampled block start, latest sampled block
+    // end}; it agrees with rocprofv3 --kernel-trace averages of the same launches within ~3 %
+    // (DESIGN.md §5).  Dispatch-stamped event pairs (hipExtLaunchKernelGGL; the element-wise
+    // kernels, or every kernel with AESFHE_PROF_EVENTS=1) read ~3 us longer per launch than
+    // rocprofv3 does: the event's completion signal adds its own end-of-kernel release.
     static constexpr int kTsSlots = 1 << 15;
     unsigned long long* d_ts = nullptr;  // [2][kTsSlots]: starts, then ends
     int ts_next = 0;

@@ -418,6 +418,7 @@ void KernelProfiler::flush() {
         (void)hipEventElapsedTime(&t, r.a, r.b);
         ms[r.kid] += t;
         bytes[r.kid] += r.bytes;
+        work[r.kid] += r.work;
         launches[r.kid] += 1;
         pool.push_back(r.a);
         pool.push_back(r.b);

@@ -8,6 +8,7 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -28,7 +29,7 @@ inline void prof_launch(int kid, double bytes, F kernel, dim3 grid, dim3 block, 
     if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) {
         hipEvent_t a = p->get(), b = p->get();
         hipExtLaunchKernelGGL(kernel, grid, block, (std::uint32_t)lds, st, a, b, 0u, args...);
-        p->recs.push_back({a, b, kid, bytes});
+        p->recs.push_back({a, b, kid, bytes, 0.0});
     } else {
         hipLaunchKernelGGL(kernel, grid, block, lds, st, args...);
     }
@@ -42,7 +43,18 @@ inline void prof_launch_tsw(int kid, double bytes, double work, F kernel, dim3 g
                             Args... args) {
     KernelProfiler* p = g_prof;
     unsigned long long* ts = nullptr;
-    if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) ts = p->ts_slot(kid, bytes, work);
+    if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) {
+        static const bool events = std::getenv("AESFHE_PROF_EVENTS") && std::getenv("AESFHE_PROF_EVENTS")[0] == '1';
+        if (!events) {
+            ts = p->ts_slot(kid, bytes, work);
+        } else {  // AESFHE_PROF_EVENTS=1: dispatch-stamped events (~3 us longer per timed launch)
+            hipEvent_t a = p->get(), b = p->get();
+            hipExtLaunchKernelGGL(kernel, grid, block, (std::uint32_t)lds, st, a, b, 0u, args..., ts);
+            p->recs.push_back({a, b, kid, bytes, work});
+            launch_check();
+            return;
+        }
+    }
     hipLaunchKernelGGL(kernel, grid, block, lds, st, args..., ts);
     launch_check();
 }
