@@ -2007,10 +2007,21 @@ public:
 
     Ct rotl(const Ct& c, long k) { return rotate(c, (int)(-k)); }
     // debug: apply CoeffToSlot group `which` (0..2) or SlotToCoeff group (3..5)
-    Ct debug_lin_group(const Ct& c, int which) {
+    BootGroupDev& debug_group(int which) {
         boot_setup();
-        auto& G = which < boot_cts() ? bs_.cts[which] : bs_.stc[which - boot_cts()];
-        return lin_group(c, G);
+        if (which < 0 || which >= boot_cts() + kBootStc) throw std::runtime_error("debug_lin_group: no such group");
+        return which < boot_cts() ? bs_.cts[which] : bs_.stc[which - boot_cts()];
+    }
+    Ct debug_lin_group(const Ct& c, int which) { return lin_group(c, debug_group(which)); }
+    // the same group applied to slot values on the host (bootstrap.cpp apply_group_plain): the
+    // model debug_lin_group's decryption is checked against
+    void debug_lin_group_plain(int which, const double* re, const double* im, double* ore, double* oim) {
+        const LinGroup& g = *debug_group(which).g;
+        const int M = slot_count();
+        std::vector<cplx> v(M);
+        for (int j = 0; j < M; ++j) v[j] = cplx(re[j], im[j]);
+        v = apply_group_plain(g, v);
+        for (int j = 0; j < M; ++j) ore[j] = v[j].real(), oim[j] = v[j].imag();
     }
     void boot_info(double* out) const {
         out[0] = bs_.s_bt;
@@ -3419,6 +3430,11 @@ int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle c, int stage, aesfhe_
 }
 int aesfhe_debug_lin_group(aesfhe_ctx* ctx, aesfhe_handle c, int which, aesfhe_handle* out) {
     CT_OP(e.debug_lin_group(e.canon(c), which))
+}
+int aesfhe_debug_lin_group_plain(aesfhe_ctx* ctx, int which, const double* re, const double* im, double* out_re, double* out_im) {
+    API_BEGIN if (!re || !im || !out_re || !out_im) throw std::runtime_error("debug_lin_group_plain: null buffer");
+    ctx->eng->debug_lin_group_plain(which, re, im, out_re, out_im);
+    API_END
 }
 int aesfhe_export_sparse(aesfhe_ctx* ctx, uint32_t* out) {
     API_BEGIN Engine& e = *ctx->eng;

@@ -43,7 +43,7 @@ EXPORTED = [
     "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_kernel_work", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan", "aesfhe_debug_sparseplan",
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot", "aesfhe_create_keyed", "aesfhe_bootstrap_sparse", "aesfhe_bootstrap_pair_sparse", "aesfhe_renorm_periodic",
     "aesfhe_renorm_single", "aesfhe_renorm_unpack",
-    "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_lut_create", "aesfhe_lut_eval", "aesfhe_lut_free",
+    "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_debug_lin_group_plain", "aesfhe_lut_create", "aesfhe_lut_eval", "aesfhe_lut_free",
     "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled",
 ]
 
@@ -119,6 +119,7 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_export_sparse"] = [vp, _up]
     sig["aesfhe_boot_info"] = [vp, _dp]
     sig["aesfhe_debug_lin_group"] = [vp, _H, c_int, _Hp]
+    sig["aesfhe_debug_lin_group_plain"] = [vp, c_int, _dp, _dp, _dp, _dp]
     sig["aesfhe_create_boot"] = [pp, c_int, c_int, c_int, c_int, ctypes.c_uint64]
     sig["aesfhe_renorm_periodic"] = [vp, _H, _H, c_int, c_int, _Hp, _Hp]
     sig["aesfhe_renorm_single"] = [vp, _H, c_int, _Hp]
@@ -548,6 +549,15 @@ class Engine:
 
     def debug_lin_group(self, ct, which: int):
         return self._new(self._lib.aesfhe_debug_lin_group, ct.handle, int(which))
+
+    def debug_lin_group_plain(self, which: int, z: np.ndarray) -> np.ndarray:
+        """bootstrap linear-transform group `which` (CoeffToSlot 0.., then SlotToCoeff) applied
+        to slot values on the host: the plan model of debug_lin_group"""
+        z = np.asarray(z, np.complex128)
+        re, im = np.ascontiguousarray(z.real), np.ascontiguousarray(z.imag)
+        ore, oim = np.zeros(self.slot_count), np.zeros(self.slot_count)
+        self._ctx.check(self._lib.aesfhe_debug_lin_group_plain(self._ctx.ptr, int(which), re, im, ore, oim))
+        return ore + 1j * oim
 
     def export_sparse(self) -> np.ndarray:
         out = np.zeros((self.n_q + self.n_p, self.n), np.uint32)

@@ -207,6 +207,10 @@ int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle ct, int stage, aesfhe
 /* ephemeral sparse secret (NTT form, all limbs) */
 int aesfhe_export_sparse(aesfhe_ctx* ctx, uint32_t* out);
 int aesfhe_debug_lin_group(aesfhe_ctx* ctx, aesfhe_handle ct, int which, aesfhe_handle* out);
+/* The same group applied on the host to slot_count complex slots (re, im) -> (out_re, out_im):
+ * the plan model a decryption of aesfhe_debug_lin_group is checked against (test only). */
+int aesfhe_debug_lin_group_plain(aesfhe_ctx* ctx, int which, const double* re, const double* im, double* out_re,
+                                 double* out_im);
 /* [s_bt, k1, top, K, r, deg, log2 modulus of the dense->sparse key (Q0 P', Q0 = q0 q1), sparse
  * secret weight h, special primes in P', base limbs in Q0, message bits b (s_bt = Q0 / 2^b)]
  *  */

@@ -113,3 +113,28 @@ def test_bootstrap_stages_bitexact(pair, seed):
     ks = O.keyswitch(top, s3[1], E.export_ksk(2 * E.n + 3))
     want4 = np.stack([addmod(ks[0], s3[0], O.limbs_mod(nlt)), ks[1]])
     assert np.array_equal(s4, want4)
+
+
+@pytest.mark.parametrize("which", range(6))
+def test_lin_group_matches_plan(pair, which):
+    """One hoisted BSGS linear-transform group of the bootstrap (k_lin_mac: baby-step key inner
+    products, diagonals in Q*P, giant-step rotations, one ModDown + rescale) against the plan's
+    matrix applied to the decrypted input on the host (bootstrap.cpp apply_group_plain).  Groups
+    0..2 are CoeffToSlot, run from the top level on the bootstrap's own stage-4 ciphertext
+    (ModRaise + sparse -> dense key switch); 3..5 are SlotToCoeff, run further down the same
+    chain.  Linear in the message, so the check holds for any input: a wrong diagonal, offset
+    or key shows up at the scale of the output.  Measured on MI355X: relative error 1.5e-14 ..
+    6.7e-14 (CoeffToSlot), ~6e-16 (SlotToCoeff) -- the double-prime scale's noise."""
+    E, _ = pair
+    rng = np.random.default_rng(20 + which)
+    z = 0.5 * (rng.uniform(-1, 1, E.slot_count) + 1j * rng.uniform(-1, 1, E.slot_count))
+    x = E.debug_boot_stage(E.encrypt(z), 4)
+    for w in range(which):
+        x = E.debug_lin_group(x, w)
+    want = E.debug_lin_group_plain(which, E.decrypt(x))
+    got = E.decrypt(E.debug_lin_group(x, which))
+    scale = np.abs(want).max()
+    err = np.abs(got - want).max() / scale
+    print(f"group {which}: level {x.level}, max |out| {scale:.3g}, relative error {err:.2e}")
+    assert scale > 1e-3
+    assert err < 1e-9
