@@ -138,3 +138,40 @@ def test_lin_group_matches_plan(pair, which):
     print(f"group {which}: level {x.level}, max |out| {scale:.3g}, relative error {err:.2e}")
     assert scale > 1e-3
     assert err < 1e-9
+
+
+def _evalmod_plain(y, K, r, deg):
+    """the plan's EvalMod (bootstrap.cpp make_boot_plan + engine.hip eval_mod): the degree-deg
+    Chebyshev interpolant of cos(2 pi (K y - 1/4) / 2^r) on [-1, 1], then r double angles"""
+    n = deg + 1
+    j = np.arange(n)
+    f = np.cos(2 * np.pi * (K * np.cos(np.pi * (j + 0.5) / n) - 0.25) / 2.0 ** r)
+    c = np.array([(1.0 if k == 0 else 2.0) * np.dot(f, np.cos(np.pi * k * (j + 0.5) / n)) / n for k in range(n)])
+    g = np.polynomial.chebyshev.chebval(y, c)
+    for _ in range(r):
+        g = 2 * g * g - 1
+    return g
+
+
+def test_evalmod_matches_plan(pair):
+    """EvalMod on the bootstrap's own CoeffToSlot output (stages 6 / 7: the real and imaginary
+    parts, slots in [-1, 1]) against the plan's polynomial on the host: stage 8 (real half alone)
+    and stage 10 (both halves stacked in one batched ciphertext, recombined as f(re) + i f(im),
+    the production path).  The double angles amplify the input noise 4^r-fold, so the tolerance
+    is absolute (outputs lie in [-1, 1]).  Measured on MI355X: 1.2e-11 / 1.5e-11."""
+    E, _ = pair
+    info = E.boot_info()
+    K, r, deg = int(info["K"]), int(info["r"]), int(info["deg"])
+    rng = np.random.default_rng(31)
+    z = 0.5 * (rng.uniform(-1, 1, E.slot_count) + 1j * rng.uniform(-1, 1, E.slot_count))
+    ct = E.encrypt(z)
+    re, im = E.decrypt(E.debug_boot_stage(ct, 6)), E.decrypt(E.debug_boot_stage(ct, 7))
+    assert np.abs(re.imag).max() < 1e-6 and np.abs(im.imag).max() < 1e-6
+    assert np.abs(re.real).max() <= 1.0 and np.abs(im.real).max() <= 1.0
+    want_re, want_im = _evalmod_plain(re.real, K, r, deg), _evalmod_plain(im.real, K, r, deg)
+    got8 = E.decrypt(E.debug_boot_stage(ct, 8))
+    got10 = E.decrypt(E.debug_boot_stage(ct, 10))
+    e8 = np.abs(got8 - want_re).max()
+    e10 = np.abs(got10 - (want_re + 1j * want_im)).max()
+    print(f"EvalMod K {K} r {r} deg {deg}: stage 8 max error {e8:.2e}, stage 10 {e10:.2e}")
+    assert e8 < 1e-8 and e10 < 1e-8
