@@ -2426,13 +2426,24 @@ public:
         const int d = (int)c.size() - 1;
         std::vector<Ct> T(kBabyDeg + 1);
         T[1] = copy(y);
-        for (int k = 2; k <= kBabyDeg; ++k) {
-            const int a = (k + 1) / 2, b = k / 2;
-            Ct p = mul(T[a], T[b], true);
-            Ct p2 = mul_scalar(p, 2.0, 0.0);
-            release(p);
-            T[k] = (a == b) ? add_scalar(p2, -1.0, 0.0) : add_sub(p2, T[a - b], true);
-            release(p2);
+        // baby steps by depth: T_k = 2 T_a T_b - T_{a-b} (a = ceil(k/2), b = floor(k/2)) needs
+        // only T_1 .. T_{lo-1}, so T_lo .. T_{2 lo - 2} are independent products -- T_2, then
+        // T_3..T_4, then T_5..T_8 -- each group ONE batched multiply (mul_many: one stacked
+        // relinearisation, bit-exact with mul; AESFHE_EVALMOD_BATCH=0 for A/B)
+        static const bool batch_baby = env_int("AESFHE_EVALMOD_BATCH", 1) != 0;
+        for (int lo = 2; lo <= kBabyDeg;) {
+            const int hi = batch_baby ? std::min(kBabyDeg, 2 * lo - 2) : lo;
+            std::vector<const Ct*> A, B;
+            for (int k = lo; k <= hi; ++k) A.push_back(&T[(k + 1) / 2]), B.push_back(&T[k / 2]);
+            std::vector<Ct> P = mul_many(A, B);
+            for (int k = lo; k <= hi; ++k) {
+                const int a = (k + 1) / 2, b = k / 2;
+                Ct p2 = mul_scalar(P[k - lo], 2.0, 0.0);
+                release(P[k - lo]);
+                T[k] = (a == b) ? add_scalar(p2, -1.0, 0.0) : add_sub(p2, T[a - b], true);
+                release(p2);
+            }
+            lo = hi + 1;
         }
         std::map<int, Ct> giant;
         giant[kBabyDeg] = T[kBabyDeg];

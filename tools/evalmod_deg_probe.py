@@ -2,6 +2,7 @@
 under the EvalMod configuration in the environment (AESFHE_BOOT_K / _R / _DEG, read once per
 process): time and slot error on 32-periodic inputs of modulus <= 1 and on Zeta16 codewords.
 One JSON line; run once per configuration (tools/evalmod sweep in DESIGN.md §4)."""
+import hashlib
 import json
 import os
 import sys
@@ -33,6 +34,8 @@ def main(n=32, reps=10):
     E.sync()
     ms = (time.perf_counter() - t) / reps * 1e3
     print(json.dumps({"K_r_deg": [os.environ.get(k, "default") for k in ("AESFHE_BOOT_K", "AESFHE_BOOT_R", "AESFHE_BOOT_DEG")],
+                      "evalmod_batch": os.environ.get("AESFHE_EVALMOD_BATCH", "1"),
+                      "digest": hashlib.md5(E.export(out).tobytes() + E.export(oz).tobytes()).hexdigest(),
                       "n": n, "level": out.level, "ms": ms,
                       "max_err": float(np.abs(ctx.decrypt(out) - za).max()),
                       "max_err_zeta16": float(np.abs(ctx.decrypt(oz) - zz).max())}), flush=True)
