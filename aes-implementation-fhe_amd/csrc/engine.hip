@@ -2400,22 +2400,52 @@ public:
     }
     // p = q + T_m r with q_i = c_i - c_{2m-i} (i < m), r_0 = c_m, r_j = 2 c_{m+j}; recurse
     // until the degree is within the baby table (Paterson-Stockmeyer in the Chebyshev basis)
+    // Paterson-Stockmeyer style split c = q + T_m r (m the largest power-of-two giant step <= d),
+    // applied to several polynomials at once: the giant-step products of one recursion depth are
+    // independent, so they run as ONE batched multiply (mul_many, bit-exact with mul); the sums
+    // are the same as the one-polynomial recursion's
+    std::vector<Ct> cheb_eval_many(const std::vector<Ct>& T, const std::map<int, Ct>& giant,
+                                   const std::vector<std::vector<double>>& cs) {
+        std::vector<Ct> out(cs.size());
+        std::vector<std::vector<double>> sub;  // q_0, r_0, q_1, r_1, ...
+        std::vector<int> idx, ms;
+        for (size_t i = 0; i < cs.size(); ++i) {
+            const auto& c = cs[i];
+            const int d = (int)c.size() - 1;
+            if (d <= kBabyDeg) {
+                out[i] = cheb_leaf(T, c);
+                continue;
+            }
+            int m = kBabyDeg;
+            while (2 * m <= d) m *= 2;
+            std::vector<double> q(m), r(d - m + 1);
+            for (int k = 0; k < m; ++k) q[k] = c[k] - (2 * m - k <= d ? c[2 * m - k] : 0.0);
+            r[0] = c[m];
+            for (int j = 1; j <= d - m; ++j) r[j] = 2.0 * c[m + j];
+            idx.push_back((int)i), ms.push_back(m);
+            sub.push_back(std::move(q)), sub.push_back(std::move(r));
+        }
+        if (idx.empty()) return out;
+        std::vector<Ct> v = cheb_eval_many(T, giant, sub);
+        static const bool batch = env_int("AESFHE_EVALMOD_BATCH", 1) != 0;
+        std::vector<Ct> P(idx.size());
+        if (batch) {
+            std::vector<const Ct*> A, B;
+            for (size_t j = 0; j < idx.size(); ++j) A.push_back(&giant.at(ms[j])), B.push_back(&v[2 * j + 1]);
+            P = mul_many(A, B);
+        } else {
+            for (size_t j = 0; j < idx.size(); ++j) P[j] = mul(giant.at(ms[j]), v[2 * j + 1], true);
+        }
+        for (size_t j = 0; j < idx.size(); ++j) {
+            release(v[2 * j + 1]);
+            out[idx[j]] = add_sub(v[2 * j], P[j], false);
+            release(v[2 * j]);
+            release(P[j]);
+        }
+        return out;
+    }
     Ct cheb_eval(const std::vector<Ct>& T, const std::map<int, Ct>& giant, const std::vector<double>& c) {
-        const int d = (int)c.size() - 1;
-        if (d <= kBabyDeg) return cheb_leaf(T, c);
-        int m = kBabyDeg;
-        while (2 * m <= d) m *= 2;
-        std::vector<double> q(m), r(d - m + 1);
-        for (int i = 0; i < m; ++i) q[i] = c[i] - (2 * m - i <= d ? c[2 * m - i] : 0.0);
-        r[0] = c[m];
-        for (int j = 1; j <= d - m; ++j) r[j] = 2.0 * c[m + j];
-        Ct qv = cheb_eval(T, giant, q), rv = cheb_eval(T, giant, r);
-        Ct tr = mul(giant.at(m), rv, true);
-        release(rv);
-        Ct o = add_sub(qv, tr, false);
-        release(qv);
-        release(tr);
-        return o;
+        return std::move(cheb_eval_many(T, giant, {c})[0]);
     }
     static constexpr int kBabyDeg = 8;
 
