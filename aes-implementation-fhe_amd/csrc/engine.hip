@@ -2404,16 +2404,19 @@ public:
     // applied to several polynomials at once: the giant-step products of one recursion depth are
     // independent, so they run as ONE batched multiply (mul_many, bit-exact with mul); the sums
     // are the same as the one-polynomial recursion's
-    std::vector<Ct> cheb_eval_many(const std::vector<Ct>& T, const std::map<int, Ct>& giant,
-                                   const std::vector<std::vector<double>>& cs) {
+    // applied to several polynomials at once, item i on input in[i] (its T / giant sets): the
+    // giant-step products of one recursion depth are independent, so they run as ONE batched
+    // multiply (mul_many, bit-exact with mul); the sums are the one-polynomial recursion's
+    std::vector<Ct> cheb_eval_many(const std::vector<std::vector<Ct>>& T, const std::vector<std::map<int, Ct>>& giant,
+                                   const std::vector<int>& in, const std::vector<std::vector<double>>& cs) {
         std::vector<Ct> out(cs.size());
         std::vector<std::vector<double>> sub;  // q_0, r_0, q_1, r_1, ...
-        std::vector<int> idx, ms;
+        std::vector<int> idx, ms, sub_in;
         for (size_t i = 0; i < cs.size(); ++i) {
             const auto& c = cs[i];
             const int d = (int)c.size() - 1;
             if (d <= kBabyDeg) {
-                out[i] = cheb_leaf(T, c);
+                out[i] = cheb_leaf(T[in[i]], c);
                 continue;
             }
             int m = kBabyDeg;
@@ -2424,18 +2427,13 @@ public:
             for (int j = 1; j <= d - m; ++j) r[j] = 2.0 * c[m + j];
             idx.push_back((int)i), ms.push_back(m);
             sub.push_back(std::move(q)), sub.push_back(std::move(r));
+            sub_in.push_back(in[i]), sub_in.push_back(in[i]);
         }
         if (idx.empty()) return out;
-        std::vector<Ct> v = cheb_eval_many(T, giant, sub);
-        static const bool batch = env_int("AESFHE_EVALMOD_BATCH", 1) != 0;
-        std::vector<Ct> P(idx.size());
-        if (batch) {
-            std::vector<const Ct*> A, B;
-            for (size_t j = 0; j < idx.size(); ++j) A.push_back(&giant.at(ms[j])), B.push_back(&v[2 * j + 1]);
-            P = mul_many(A, B);
-        } else {
-            for (size_t j = 0; j < idx.size(); ++j) P[j] = mul(giant.at(ms[j]), v[2 * j + 1], true);
-        }
+        std::vector<Ct> v = cheb_eval_many(T, giant, sub_in, sub);
+        std::vector<const Ct*> A, B;
+        for (size_t j = 0; j < idx.size(); ++j) A.push_back(&giant[in[idx[j]]].at(ms[j])), B.push_back(&v[2 * j + 1]);
+        std::vector<Ct> P = mul_list(A, B);
         for (size_t j = 0; j < idx.size(); ++j) {
             release(v[2 * j + 1]);
             out[idx[j]] = add_sub(v[2 * j], P[j], false);
@@ -2444,58 +2442,79 @@ public:
         }
         return out;
     }
-    Ct cheb_eval(const std::vector<Ct>& T, const std::map<int, Ct>& giant, const std::vector<double>& c) {
-        return std::move(cheb_eval_many(T, giant, {c})[0]);
+    // products of a list of pairs: one batched multiply (AESFHE_EVALMOD_BATCH=0: one at a time)
+    std::vector<Ct> mul_list(const std::vector<const Ct*>& A, const std::vector<const Ct*>& B) {
+        static const bool batch = env_int("AESFHE_EVALMOD_BATCH", 1) != 0;
+        if (batch) return mul_many(A, B);
+        std::vector<Ct> P(A.size());
+        for (size_t j = 0; j < A.size(); ++j) P[j] = mul(*A[j], *B[j], true);
+        return P;
     }
     static constexpr int kBabyDeg = 8;
 
     // EvalMod: sin(2 pi K y) via the Chebyshev interpolant of cos(2 pi (K y - 1/4) / 2^r)
     // (baby T_1..T_8, giant T_8, T_16, ...) and r double angles
-    Ct eval_mod(const Ct& y) {
+    Ct eval_mod(const Ct& y) { return std::move(eval_mod_many({&y})[0]); }
+    // EvalMod of several ciphertexts at once (the bootstrap's re / im halves): every product of
+    // one step -- a baby-step depth group, a giant step, a Chebyshev recursion depth, a double
+    // angle -- for all inputs as ONE batched multiply.  Baby steps by depth: T_k = 2 T_a T_b -
+    // T_{a-b} (a = ceil(k/2), b = floor(k/2)) needs only T_1 .. T_{lo-1}, so T_lo .. T_{2 lo - 2}
+    // are independent -- T_2, then T_3..T_4, then T_5..T_8
+    std::vector<Ct> eval_mod_many(const std::vector<const Ct*>& ys) {
         const auto& c = bs_.plan.cheb;
-        const int d = (int)c.size() - 1;
-        std::vector<Ct> T(kBabyDeg + 1);
-        T[1] = copy(y);
-        // baby steps by depth: T_k = 2 T_a T_b - T_{a-b} (a = ceil(k/2), b = floor(k/2)) needs
-        // only T_1 .. T_{lo-1}, so T_lo .. T_{2 lo - 2} are independent products -- T_2, then
-        // T_3..T_4, then T_5..T_8 -- each group ONE batched multiply (mul_many: one stacked
-        // relinearisation, bit-exact with mul; AESFHE_EVALMOD_BATCH=0 for A/B)
+        const int d = (int)c.size() - 1, ni = (int)ys.size();
+        std::vector<std::vector<Ct>> T(ni, std::vector<Ct>(kBabyDeg + 1));
+        for (int i = 0; i < ni; ++i) T[i][1] = copy(*ys[i]);
         static const bool batch_baby = env_int("AESFHE_EVALMOD_BATCH", 1) != 0;
         for (int lo = 2; lo <= kBabyDeg;) {
             const int hi = batch_baby ? std::min(kBabyDeg, 2 * lo - 2) : lo;
             std::vector<const Ct*> A, B;
-            for (int k = lo; k <= hi; ++k) A.push_back(&T[(k + 1) / 2]), B.push_back(&T[k / 2]);
-            std::vector<Ct> P = mul_many(A, B);
-            for (int k = lo; k <= hi; ++k) {
-                const int a = (k + 1) / 2, b = k / 2;
-                Ct p2 = mul_scalar(P[k - lo], 2.0, 0.0);
-                release(P[k - lo]);
-                T[k] = (a == b) ? add_scalar(p2, -1.0, 0.0) : add_sub(p2, T[a - b], true);
-                release(p2);
-            }
+            for (int i = 0; i < ni; ++i)
+                for (int k = lo; k <= hi; ++k) A.push_back(&T[i][(k + 1) / 2]), B.push_back(&T[i][k / 2]);
+            std::vector<Ct> P = mul_list(A, B);
+            int j = 0;
+            for (int i = 0; i < ni; ++i)
+                for (int k = lo; k <= hi; ++k, ++j) {
+                    const int a = (k + 1) / 2, b = k / 2;
+                    Ct p2 = mul_scalar(P[j], 2.0, 0.0);
+                    release(P[j]);
+                    T[i][k] = (a == b) ? add_scalar(p2, -1.0, 0.0) : add_sub(p2, T[i][a - b], true);
+                    release(p2);
+                }
             lo = hi + 1;
         }
-        std::map<int, Ct> giant;
-        giant[kBabyDeg] = T[kBabyDeg];
+        std::vector<std::map<int, Ct>> giant(ni);
+        for (int i = 0; i < ni; ++i) giant[i][kBabyDeg] = T[i][kBabyDeg];
         for (int m = 2 * kBabyDeg; m <= d; m *= 2) {
-            const Ct& h = giant.at(m / 2);
-            Ct p = mul(h, h, true);
-            Ct p2 = mul_scalar(p, 2.0, 0.0);
-            release(p);
-            giant[m] = add_scalar(p2, -1.0, 0.0);
-            release(p2);
+            std::vector<const Ct*> A;
+            for (int i = 0; i < ni; ++i) A.push_back(&giant[i].at(m / 2));
+            std::vector<Ct> P = mul_list(A, A);
+            for (int i = 0; i < ni; ++i) {
+                Ct p2 = mul_scalar(P[i], 2.0, 0.0);
+                release(P[i]);
+                giant[i][m] = add_scalar(p2, -1.0, 0.0);
+                release(p2);
+            }
         }
-        Ct g = cheb_eval(T, giant, c);
-        for (int k = 1; k <= kBabyDeg; ++k) release(T[k]);
-        for (auto& kv : giant)
-            if (kv.first != kBabyDeg) release(kv.second);
-        for (int i = 0; i < bs_.plan.r; ++i) {
-            Ct sq = mul(g, g, true);
-            Ct sq2 = mul_scalar(sq, 2.0, 0.0);
-            release(sq);
-            release(g);
-            g = add_scalar(sq2, -1.0, 0.0);
-            release(sq2);
+        std::vector<int> in(ni);
+        for (int i = 0; i < ni; ++i) in[i] = i;
+        std::vector<Ct> g = cheb_eval_many(T, giant, in, std::vector<std::vector<double>>(ni, c));
+        for (int i = 0; i < ni; ++i) {
+            for (int k = 1; k <= kBabyDeg; ++k) release(T[i][k]);
+            for (auto& kv : giant[i])
+                if (kv.first != kBabyDeg) release(kv.second);
+        }
+        for (int it = 0; it < bs_.plan.r; ++it) {
+            std::vector<const Ct*> A;
+            for (int i = 0; i < ni; ++i) A.push_back(&g[i]);
+            std::vector<Ct> P = mul_list(A, A);
+            for (int i = 0; i < ni; ++i) {
+                release(g[i]);
+                Ct sq2 = mul_scalar(P[i], 2.0, 0.0);
+                release(P[i]);
+                g[i] = add_scalar(sq2, -1.0, 0.0);
+                release(sq2);
+            }
         }
         return g;
     }
@@ -2730,6 +2749,8 @@ public:
         // 7. EvalMod on both halves: stacked into ONE batched ciphertext (2 nb members) so
         // every key switch of the polynomial evaluation reads its key once for both halves
         Ct fre, fim;
+        // (eval_mod_many({re, im}) is bit-exact with the stacked form below but measured no faster:
+        // the stacked halves already share every key read; profiles/r2_evalmod_batch_ab.json)
         if (stop_after > 9 && stack_evalmod_ && 2 * nb <= kMaxKsBatch && re.level == im.level && re.pend == im.pend &&
             !re.lazy && !im.lazy && pm(re) == 2 && pm(im) == 2 && re.ntt == im.ntt) {
             Ct st = alloc_ct(re.level, re.npoly + im.npoly, 2 * nb);
