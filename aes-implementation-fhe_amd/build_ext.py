@@ -25,12 +25,30 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: cannot build the MI355X engine")
 
 
+STAMP = LIB.with_suffix(".so.sha256")  # content hash the library was built from (travels with it)
+
+
+def source_digest() -> str:
+    """sha256 over the compiler flags and every source / header the library is built from:
+    the rebuild decision never depends on file modification times (a checkout or copy that
+    reorders mtimes cannot ship a stale binary)"""
+    import hashlib
+    h = hashlib.sha256()
+    h.update(" ".join(_flags()).encode())
+    for d in [CSRC / s for s in SOURCES + HEADERS] + [PKG.parent / "include" / "aesfhe.h"]:
+        h.update(d.name.encode() + b"\0")
+        h.update(d.read_bytes() if d.exists() else b"<missing>")
+    return h.hexdigest()
+
+
 def needs_build() -> bool:
-    if not LIB.exists():
+    if not LIB.exists() or not STAMP.exists():
         return True
-    t = LIB.stat().st_mtime
-    deps = [CSRC / s for s in SOURCES + HEADERS] + [PKG.parent / "include" / "aesfhe.h"]
-    return any(d.stat().st_mtime > t for d in deps if d.exists())
+    return STAMP.read_text().strip() != source_digest()
+
+
+def _flags() -> list:
+    return [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"]
 
 
 def build(force: bool = False, verbose: bool = False) -> Path:
@@ -38,7 +56,8 @@ def build(force: bool = False, verbose: bool = False) -> Path:
     units: engine.hip reaches the kernels only through the host launch wrappers), then linked."""
     if not force and not needs_build():
         return LIB
-    flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC"]
+    flags = _flags()
+    digest = source_digest()
     objdir = PKG / "build"
     objdir.mkdir(exist_ok=True)
     objs = [objdir / (s + ".o") for s in SOURCES]
@@ -59,6 +78,7 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(tmp, LIB)
+    STAMP.write_text(digest + "\n")
     return LIB
 
 

@@ -466,6 +466,18 @@ public:
     // delta_f q_{nl(f)}): c = (v pk0 + e0 + m, v pk1 + e1) at level f + 1, rescaled to f;
     // level < 0: the fresh level; any level 0..fresh works the same way (the public key
     // restricted to the first nl(f) + 1 limbs)
+    // Encryption randomness (v, e0, e1) is drawn under its OWN key: the context key with the
+    // per-process 64-bit nonce folded into key words 6-7 (aesfhe_set_enc_nonce).  Ranks of a
+    // multi-GPU job share the context key (identical key sets) but not the nonce, so their i-th
+    // encryptions never reuse (v, e) -- a reuse would make c_r - c_0 a noiseless encoding of
+    // m_r - m_0.  Nonce 0 (the default of the C ABI) leaves the context key unchanged.
+    PrngKey enc_key() const {
+        PrngKey k = pkey();
+        k.w[6] ^= (u32)enc_nonce_;
+        k.w[7] ^= (u32)(enc_nonce_ >> 32);
+        return k;
+    }
+    void set_enc_nonce(u64 nonce) { enc_nonce_ = nonce; }
     Ct encrypt_ntt(const u32* m, int level = -1) {
         const int f = level < 0 ? hp_.fresh : level;
         const int n = hp_.n, nq = hp_.nl(f) + 1;
@@ -473,9 +485,10 @@ public:
         u32* v = tmp(nq);
         u32* e = tmp(2 * nq);
         const u64 ctr = enc_ctr_++;
-        launch_sample_small(S(), T_, v, nq, qmap(), pkey(), stream_id(6, 0, ctr), 0);
-        launch_sample_small(S(), T_, e, nq, qmap(), pkey(), stream_id(7, 0, ctr), 1);
-        launch_sample_small(S(), T_, e + (size_t)nq * n, nq, qmap(), pkey(), stream_id(8, 0, ctr), 1);
+        const PrngKey ek = enc_key();
+        launch_sample_small(S(), T_, v, nq, qmap(), ek, stream_id(6, 0, ctr), 0);
+        launch_sample_small(S(), T_, e, nq, qmap(), ek, stream_id(7, 0, ctr), 1);
+        launch_sample_small(S(), T_, e + (size_t)nq * n, nq, qmap(), ek, stream_id(8, 0, ctr), 1);
         ntt(v, nq, nq, qmap());
         ntt(e, 2 * nq, nq, qmap());
         Ct top = alloc_ct(L + 1, 2);
@@ -1766,7 +1779,11 @@ public:
         CrtConsts cc[2];
         double isc[2];
         const aesfhe_handle in[2] = {hh, hl};
-        for (int w = 0; w < 2; ++w) {
+        // unpack / single read ONE ciphertext: it is decrypted once and the codec runs on one input
+        // channel (k_snap_slots' unpack gathers both outputs from channel 0; single has one output)
+        const int n_in = (unpack || single) ? 1 : 2, n_out = single ? 1 : 2;
+        kd[1] = 0;
+        for (int w = 0; w < n_in; ++w) {
             Ct c = ensure_ntt(ct(in[w]));
             bool own = c.data != ct(in[w]).data;
             kd[w] = crt_limbs(c);
@@ -1803,11 +1820,12 @@ public:
             if (!zbuf) zbuf = (double*)dev_alloc((size_t)2 * 2 * 2 * 2 * n);  // 2 buffers x [2][N] complex double
             double* z = zbuf;
             double* w = zbuf + (size_t)2 * 2 * n;
-            launch_decode_twist(S(), T_, x, kd, cc, isc, z);
-            launch_fft2(S(), T_, z, 1);
-            launch_snap_slots(S(), T_, z, w, d_slot_pos_, states, unpack);
-            launch_fft2(S(), T_, w, -1);
-            launch_encode_untwist(S(), T_, m, w, enc_scale, nq);
+            if (n_in == 1) cc[1] = cc[0], isc[1] = isc[0];
+            launch_decode_twist(S(), T_, x, kd, cc, isc, z, n_in);
+            launch_fft2(S(), T_, z, 1, n_in);
+            launch_snap_slots(S(), T_, z, w, d_slot_pos_, states, unpack, n_out);
+            launch_fft2(S(), T_, w, -1, n_out);
+            launch_encode_untwist(S(), T_, m, w, enc_scale, nq, n_out);
         }
         ntt(m, (single ? 1 : 2) * nq, nq, qmap());
         Ct a = encrypt_ntt(m, f);
@@ -3184,6 +3202,7 @@ private:
     u32* d_ssp_ = nullptr;
     std::map<u64, u32*> ksk_;
     u64 enc_ctr_ = 0;
+    u64 enc_nonce_ = 0;  // see enc_key()
     std::vector<u32> im_;
     u32* d_rescale_qinv_ = nullptr;
     u32* d_rescale2_qinv_ = nullptr;
@@ -3404,6 +3423,10 @@ int aesfhe_lut_eval(aesfhe_ctx* ctx, aesfhe_handle lut, const aesfhe_handle* a, 
 }
 int aesfhe_lut_free(aesfhe_ctx* ctx, aesfhe_handle lut) {
     API_BEGIN ctx->eng->free_lut(lut);
+    API_END
+}
+int aesfhe_set_enc_nonce(aesfhe_ctx* ctx, uint64_t nonce) {
+    API_BEGIN ctx->eng->set_enc_nonce(nonce);
     API_END
 }
 int aesfhe_set_lazy(aesfhe_ctx* ctx, int on) {

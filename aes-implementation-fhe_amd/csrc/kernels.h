@@ -290,17 +290,19 @@ void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double*
 // Element t of a transform's output is stored at fft_loc(t) = (t mod N1) N2 + t / N1.
 // x: [2][4][N] coefficient residues (kd[c] limbs) -> z[c][k] = m_k / scale_c * zeta^k
 void launch_decode_twist(hipStream_t st, const DevTables& T, const u32* x, const int kd[2], const CrtConsts cc[2],
-                         const double inv_scale[2], double* z);
+                         const double inv_scale[2], double* z, int nch = 2);
 // in-place X_k = sum_n x_n e^{sign 2 pi i n k / N} on 2 vectors (complex double, [2][N]);
 // input in natural order, output at fft_loc
-void launch_fft2(hipStream_t st, const DevTables& T, double* z, int sign);
+void launch_fft2(hipStream_t st, const DevTables& T, double* z, int sign, int nch = 2);
 // snap: slot j (value at fft_loc(slot_pos[j]) of zin) -> zeta16 power if (j mod stride) < states,
 // else 1; writes w[slot_pos[j]] = v and w[N - 1 - slot_pos[j]] = conj(v) (natural order)
 // unpack = n > 0: both outputs read the first input's 2n-periodic packed state, output 0 its
 // slots (j mod n), output 1 its slots (j mod n) + n
-void launch_snap_slots(hipStream_t st, const DevTables& T, const double* zin, double* w, const u32* slot_pos, int states, int unpack = 0);
+void launch_snap_slots(hipStream_t st, const DevTables& T, const double* zin, double* w, const u32* slot_pos, int states, int unpack = 0,
+                       int nch = 2);
 // out[c][t][k] = round(scale Re(v[fft_loc(k)] zeta^{-k}) / N) mod q_t, t < nq
-void launch_encode_untwist(hipStream_t st, const DevTables& T, u32* out, const double* v, double scale, int nq);
+void launch_encode_untwist(hipStream_t st, const DevTables& T, u32* out, const double* v, double scale, int nq, int nch = 2);
+// nch (all four): channels processed (grid y); 1 = channel 0 only (one input decrypted, or one output)
 
 // --- fused LUT evaluation ---------------------------
 // Elements are canonical ciphertexts at data levels >= the output level l; only their first

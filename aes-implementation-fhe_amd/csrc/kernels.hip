@@ -8,6 +8,9 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
+#include <stdexcept>
+#include <unordered_map>
 
 #include "launch.h"
 
@@ -399,6 +402,26 @@ inline dim3 ew_grid(int logn, int rows) { return dim3((1u << logn) / kBlock, row
 // ======================================================================================
 thread_local KernelProfiler* g_prof = nullptr;
 void prof_set(KernelProfiler* p) { g_prof = p; }
+
+// ======================================================================================
+// launch validation (launch.h launch_validate): per-kernel limits, queried once
+// ======================================================================================
+const LaunchLimits& launch_limits(const void* fn) {
+    static std::mutex mu;
+    static std::unordered_map<const void*, LaunchLimits> cache;
+    std::lock_guard<std::mutex> lock(mu);
+    auto it = cache.find(fn);
+    if (it != cache.end()) return it->second;
+    hipFuncAttributes a{};
+    if (hipFuncGetAttributes(&a, fn) != hipSuccess) throw std::runtime_error("launch validation: hipFuncGetAttributes failed");
+    return cache.emplace(fn, LaunchLimits{a.maxThreadsPerBlock, a.sharedSizeBytes}).first->second;
+}
+void launch_reject(const void* fn, const char* what, dim3 grid, dim3 block, size_t lds, size_t kernarg) {
+    char buf[256];
+    std::snprintf(buf, sizeof buf, "launch rejected (%s): kernel %p grid (%u, %u, %u) block (%u, %u, %u) lds %zu kernarg %zu", what, fn,
+                  grid.x, grid.y, grid.z, block.x, block.y, block.z, lds, kernarg);
+    throw std::runtime_error(buf);
+}
 
 hipEvent_t KernelProfiler::get() {
     if (!pool.empty()) {
@@ -1037,8 +1060,7 @@ void launch_decode16(hipStream_t st, const DevTables& T, const u32* x, const int
                 dim3(kBlock), 0, st, x, kd[0], kd[1], cc[0], cc[1], sl, inv_scale[0], inv_scale[1], acc, T.logn);
 }
 void launch_snap16(hipStream_t st, const double* acc, double* w, int* nib) {
-    hipLaunchKernelGGL(k_snap16, dim3(1), dim3(64), 0, st, acc, w, nib);
-    launch_check();
+    prof_launch(KID_ELEMENTWISE, 0.0, k_snap16, dim3(1), dim3(64), 0, st, acc, w, nib);
 }
 void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq, bool periodic) {
     const u32 n = 1u << T.logn;
@@ -1049,25 +1071,26 @@ void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double*
 }
 
 void launch_decode_twist(hipStream_t st, const DevTables& T, const u32* x, const int kd[2], const CrtConsts cc[2],
-                         const double inv_scale[2], double* z) {
+                         const double inv_scale[2], double* z, int nch) {
     const double n = (double)(1u << T.logn);
-    prof_launch(KID_ELEMENTWISE, words((kd[0] + kd[1]) * n) + 32.0 * n, k_decode_twist, dim3((1u << T.logn) / kBlock, 2), dim3(kBlock),
+    prof_launch(KID_ELEMENTWISE, words((kd[0] + (nch > 1 ? kd[1] : 0)) * n) + 16.0 * nch * n, k_decode_twist, dim3((1u << T.logn) / kBlock, nch), dim3(kBlock),
                 0, st, x, kd[0], kd[1], cc[0], cc[1], inv_scale[0], inv_scale[1], (double2*)z, T.logn);
 }
-void launch_fft2(hipStream_t st, const DevTables& T, double* z, int sign) {
+void launch_fft2(hipStream_t st, const DevTables& T, double* z, int sign, int nch) {
     const int l1 = T.logn - T.logn / 2, l2 = T.logn - l1;
     for (int pass = 0; pass < 2; ++pass)
-        prof_launch(KID_ELEMENTWISE, 64.0 * (1u << T.logn), k_fft_pass, dim3((1u << (pass ? l1 : l2)) / kFftTpb, 2), dim3(kBlock), 0, st,
+        prof_launch(KID_ELEMENTWISE, 32.0 * nch * (1u << T.logn), k_fft_pass, dim3((1u << (pass ? l1 : l2)) / kFftTpb, nch), dim3(kBlock), 0, st,
                     (double2*)z, T.logn, pass, sign);
 }
-void launch_snap_slots(hipStream_t st, const DevTables& T, const double* zin, double* w, const u32* slot_pos, int states, int unpack) {
+void launch_snap_slots(hipStream_t st, const DevTables& T, const double* zin, double* w, const u32* slot_pos, int states, int unpack,
+                       int nch) {
     const double s = (double)(1u << (T.logn - 1));
-    prof_launch(KID_ELEMENTWISE, 2.0 * (16.0 * s + 4.0 * s + 32.0 * s), k_snap_slots, dim3((1u << (T.logn - 1)) / kBlock, 2),
+    prof_launch(KID_ELEMENTWISE, nch * (16.0 * s + 4.0 * s + 32.0 * s), k_snap_slots, dim3((1u << (T.logn - 1)) / kBlock, nch),
                 dim3(kBlock), 0, st, (const double2*)zin, (double2*)w, slot_pos, states, unpack, T.logn);
 }
-void launch_encode_untwist(hipStream_t st, const DevTables& T, u32* out, const double* v, double scale, int nq) {
+void launch_encode_untwist(hipStream_t st, const DevTables& T, u32* out, const double* v, double scale, int nq, int nch) {
     const double n = (double)(1u << T.logn);
-    prof_launch(KID_ELEMENTWISE, 32.0 * n + words(2.0 * nq * n), k_encode_untwist, dim3((1u << T.logn) / kBlock, 2), dim3(kBlock), 0,
+    prof_launch(KID_ELEMENTWISE, 16.0 * nch * n + words((double)nch * nq * n), k_encode_untwist, dim3((1u << T.logn) / kBlock, nch), dim3(kBlock), 0,
                 st, out, (const double2*)v, scale, nq, T.pc, T.logn);
 }
 

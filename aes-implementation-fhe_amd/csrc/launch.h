@@ -23,8 +23,44 @@ inline void launch_check() {
     if (e != hipSuccess) throw std::runtime_error(std::string("kernel launch failed: ") + hipGetErrorString(e));
 }
 
+// Host-side validation of every launch configuration BEFORE it is queued:
+// a malformed dispatch must fail the API call that issued it, never reach the queue.
+//  - grid: every dimension >= 1 (an empty launch is a caller bug: the wrappers return before
+//    launching nothing) and within the hardware limits (x < 2^31, y / z <= 65535);
+//  - block: 1 .. the kernel's __launch_bounds__ (hipFuncGetAttributes maxThreadsPerBlock);
+//  - LDS: static + dynamic <= 160 KiB (gfx950 per-CU LDS);
+//  - kernarg: the by-value argument block (NttAux, LinMacArgs, ConvBatch, LimbConsts ...) laid
+//    out with the C alignment rules, <= kMaxKernarg.
+constexpr size_t kMaxKernarg = 4096;
+constexpr size_t kMaxLds = 160 * 1024;
+template <typename... Args>
+constexpr size_t kernarg_bytes() {
+    size_t off = 0;
+    ((off = (off + alignof(Args) - 1) / alignof(Args) * alignof(Args) + sizeof(Args)), ...);
+    return off;
+}
+struct LaunchLimits {
+    int max_threads;
+    size_t static_lds;
+};
+const LaunchLimits& launch_limits(const void* fn);  // cached hipFuncGetAttributes (kernels.hip)
+[[noreturn]] void launch_reject(const void* fn, const char* what, dim3 grid, dim3 block, size_t lds, size_t kernarg);
+template <typename F, typename... Args>
+inline void launch_validate(F kernel, dim3 grid, dim3 block, size_t lds) {
+    static_assert(kernarg_bytes<Args...>() <= kMaxKernarg, "kernel argument block exceeds the kernarg limit");
+    const void* fn = reinterpret_cast<const void*>(kernel);
+    constexpr size_t ka = kernarg_bytes<Args...>();
+    if (grid.x < 1 || grid.y < 1 || grid.z < 1 || grid.x > 0x7fffffffu || grid.y > 65535u || grid.z > 65535u)
+        launch_reject(fn, "grid dimension out of range", grid, block, lds, ka);
+    const LaunchLimits& lim = launch_limits(fn);
+    const unsigned threads = block.x * block.y * block.z;
+    if (threads < 1 || (int)threads > lim.max_threads) launch_reject(fn, "block larger than the kernel's launch bounds", grid, block, lds, ka);
+    if (lds + lim.static_lds > kMaxLds) launch_reject(fn, "LDS above 160 KiB", grid, block, lds, ka);
+}
+
 template <typename F, typename... Args>
 inline void prof_launch(int kid, double bytes, F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st, Args... args) {
+    launch_validate<F, Args...>(kernel, grid, block, lds);
     KernelProfiler* p = g_prof;
     if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) {
         hipEvent_t a = p->get(), b = p->get();
@@ -41,6 +77,7 @@ inline void prof_launch(int kid, double bytes, F kernel, dim3 grid, dim3 block, 
 template <typename F, typename... Args>
 inline void prof_launch_tsw(int kid, double bytes, double work, F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st,
                             Args... args) {
+    launch_validate<F, Args..., unsigned long long*>(kernel, grid, block, lds);
     KernelProfiler* p = g_prof;
     unsigned long long* ts = nullptr;
     if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) {

@@ -7,8 +7,9 @@ modules only ever talk to this object.  Extra keywords: ``log_n`` (N = 2^log_n, 
 ``seed`` (key material; drawn from ``os.urandom`` when None, pinned only by tests, smoke and
 multi-rank runs that share one key set), ``lazy`` (deferred relinearisation),
 ``concurrent`` (hi / lo halves on two HIP streams), ``fused_luts`` (one-kernel LUT sums,
-DESIGN.md §3.8) and ``allow_insecure`` (parameter sets above the 128-bit bound, for small
-test / smoke sets only).
+DESIGN.md §3.8), ``allow_insecure`` (parameter sets above the 128-bit bound, for small
+test / smoke sets only) and ``enc_nonce`` (the per-process nonce of the encryption
+randomness, include/aesfhe.h aesfhe_set_enc_nonce; random unless pinned).
 """
 from __future__ import annotations
 
@@ -28,7 +29,8 @@ class EngineContext:
     def __init__(self, signature: int, *, max_level: int = 17, use_bootstrap: bool = True,
                  use_multiparty: bool = False, mode: str = "cpu", device_id: int = 0,
                  thread_count: int | None = None, log_n: int = 16, dnum: int | None = None, seed: int | bytes | None = None,
-                 lazy: bool = True, concurrent: bool = True, fused_luts: bool = True, allow_insecure: bool = False):
+                 lazy: bool = True, concurrent: bool = True, fused_luts: bool = True, allow_insecure: bool = False,
+                 enc_nonce: int | None = None):
         # REF/engine_context.py:17-42: signature selects the engine constructor form
         if signature == 1:
             kw = dict(use_bootstrap=use_bootstrap, max_level=_SIG_DEFAULT_LEVEL)
@@ -41,7 +43,7 @@ class EngineContext:
         self.signature = signature
         self.engine = Engine(mode=mode, use_multiparty=use_multiparty, thread_count=thread_count or 0,
                              device_id=device_id, log_n=log_n, dnum=dnum, seed=seed, lazy=lazy,
-                             concurrent=concurrent, allow_insecure=allow_insecure, **kw)
+                             concurrent=concurrent, allow_insecure=allow_insecure, enc_nonce=enc_nonce, **kw)
         eng = self.engine
         # REF/engine_context.py:44-50
         self.secret_key = eng.create_secret_key()
@@ -241,6 +243,7 @@ class EngineContext:
         self._lut_refs = {}                              # digest -> live owners holding it
         self._lut_owned = weakref.WeakKeyDictionary()    # owner -> digests it holds
         self._lut_lock = threading.RLock()               # RLock: an owner's finalizer may run in a GC pass inside the lock
+        self._lut_gen = 0                                # bumped by clear_luts: older owners' finalizers do nothing
 
     def lut(self, key, coeffs, c0: complex = 0j, owner=None):
         """Engine-side coefficient set of a LUT polynomial, created once per coefficient CONTENT
@@ -263,20 +266,24 @@ class EngineContext:
                 held = self._lut_owned.get(owner)
                 if held is None:
                     held = self._lut_owned[owner] = set()
-                    weakref.finalize(owner, self._release_owner, weakref.ref(self), held).atexit = False
+                    weakref.finalize(owner, self._release_owner, weakref.ref(self), held, self._lut_gen).atexit = False
                 if digest not in held:
                     held.add(digest)
                     self._lut_refs[digest] = self._lut_refs.get(digest, 0) + 1
             return t
 
     @staticmethod
-    def _release_owner(ctx_ref, held):
-        """finalizer of a LUT owner: drop its references, evict the sets nobody holds any more"""
+    def _release_owner(ctx_ref, held, gen=0):
+        """finalizer of a LUT owner: drop its references, evict the sets nobody holds any more.
+        An owner registered before the last clear_luts (older generation) holds nothing."""
         ctx = ctx_ref()
         if ctx is None:
             return
         dead = []
         with ctx._lut_lock:
+            if gen != ctx._lut_gen:
+                held.clear()
+                return
             for d in held:
                 n = ctx._lut_refs.get(d, 0) - 1
                 if n > 0:
@@ -298,11 +305,18 @@ class EngineContext:
             return len(self._luts)
 
     def clear_luts(self):
-        """drop the cached coefficient sets (their device memory is freed with the last reference)"""
+        """drop the cached coefficient sets (their device memory is freed with the last reference).
+        Every live owner's record is emptied too and a new generation starts: an owner still
+        alive from before the clear must not release (lut_free) a set that a later request made
+        with the same content -- that set belongs to the new generation's owners only."""
         with self._lut_lock:
+            for held in list(self._lut_owned.values()):
+                held.clear()
+            self._lut_owned = weakref.WeakKeyDictionary()
             self._luts.clear()
             self._lut_pinned.clear()
             self._lut_refs.clear()
+            self._lut_gen += 1
 
     def lut_eval(self, lut, a, b=None):
         """sum C[p,q] a[p] b[q] (or c0 + sum C[k] a[k]) in one fused kernel."""

@@ -44,7 +44,7 @@ EXPORTED = [
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot", "aesfhe_create_keyed", "aesfhe_bootstrap_sparse", "aesfhe_bootstrap_pair_sparse", "aesfhe_renorm_periodic",
     "aesfhe_renorm_single", "aesfhe_renorm_unpack",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_debug_lin_group_plain", "aesfhe_lut_create", "aesfhe_lut_eval", "aesfhe_lut_free",
-    "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled",
+    "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled", "aesfhe_set_enc_nonce",
 ]
 
 # largest log2(PQ) for 128-bit classical security with a ternary secret (HE standard)
@@ -131,6 +131,7 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_lut_eval"] = [vp, _H, _Hp, _Hp, _Hp]
     sig["aesfhe_lut_free"] = [vp, _H]
     sig["aesfhe_level_limbs"] = [vp, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")]
+    sig["aesfhe_set_enc_nonce"] = [vp, ctypes.c_uint64]
     for name in EXPORTED:
         fn = getattr(L, name)
         fn.restype = ctypes.c_char_p if name == "aesfhe_last_error" else ctypes.c_int
@@ -273,7 +274,7 @@ class Engine:
     def __init__(self, *, mode: str = "gpu", use_bootstrap: bool = False, use_multiparty: bool = False,
                  thread_count: int = 0, device_id: int = 0, max_level: int = 17, log_n: int = 16,
                  dnum: int | None = None, seed: int | None = None, lazy: bool = True, concurrent: bool = True,
-                 allow_insecure: bool = False):
+                 allow_insecure: bool = False, enc_nonce: int | None = None):
         if use_multiparty:
             raise ValueError("multiparty key generation is not supported")
         self.mode = mode
@@ -293,6 +294,13 @@ class Engine:
         self.seed = bytes(seed) if isinstance(seed, (bytes, bytearray)) else int(seed) & 0xFFFFFFFFFFFFFFFF
         self._ctx = _Context(log_n, max_level, dnum, device_id, self.seed, bootstrappable=use_bootstrap)
         L = self._ctx.lib
+        # encryption randomness has its own per-process nonce (aesfhe_set_enc_nonce): processes
+        # that share the key set (multi-rank jobs) never reuse (v, e); pinned only for tests and
+        # bit-exact A/B digests (AESFHE_ENC_NONCE)
+        if enc_nonce is None and os.environ.get("AESFHE_ENC_NONCE"):
+            enc_nonce = int(os.environ["AESFHE_ENC_NONCE"], 0)
+        self.enc_nonce = (int.from_bytes(os.urandom(8), "little") if enc_nonce is None else int(enc_nonce)) & 0xFFFFFFFFFFFFFFFF
+        self._ctx.check(L.aesfhe_set_enc_nonce(self._ctx.ptr, self.enc_nonce))
         self.fresh_level = max_level
         self.slot_count = int(L.aesfhe_slot_count(self._ctx.ptr))
         self.max_level = int(L.aesfhe_max_level(self._ctx.ptr))

@@ -28,7 +28,8 @@ exactly SubBytes' 13 levels).  No secret key is used between encryption and decr
 after it on packed states -- hi and lo side by side in ONE ciphertext, the XOR4 LUT being the
 same for both halves (MixColFinal.mix_packed): single XOR4s instead of pairs,
 single-ciphertext renorms, one sparse bootstrap; the renorm after AddRoundKey unpacks into the
-(hi, lo) pair SubBytes reads.  The debug path keeps the reference's pair steps.
+(hi, lo) pair SubBytes reads.  A debug dict logs the packed path's own stages (``packed_xor=False``
+runs the reference's pair steps).
 
 ``states`` = B > 1 runs B independent AES states per ciphertext pair in the slot-packed
 layout (state_encoder.py): ``encrypt`` / ``decrypt`` take and return
@@ -198,6 +199,18 @@ class AESPipeline:
             self._fk_cache[(r, direction)] = self._encode_key(shift_rows_bytes(np.asarray(round_keys[r], np.uint8), direction))
         return self._fk_cache[(r, direction)]
 
+    def _log_packed(self, dbg, tag: str, ct, **meta) -> None:
+        """debug snapshot of a packed (hi | lo) state, decoded to bytes"""
+        if dbg is None:
+            return
+        entry = {"ct_packed": ct, "meta": dict(meta, packed=True)}
+        try:
+            entry["plain"] = self.encoder.decode_packed(ct)
+        except Exception as err:
+            entry["plain"] = None
+            entry["plain_err"] = repr(err)
+        dbg[tag] = entry
+
     def _log_pair(self, dbg, tag: str, ct_hi, ct_lo, **meta) -> None:
         if dbg is None:
             return
@@ -240,14 +253,25 @@ class AESPipeline:
         one-round debug block, REF :154-171)."""
         if next_level is None:
             next_level = self.need_sub
+        if self.packed_xor and r > 0:
+            # packed XOR stage (DESIGN.md §4c): MixColumns returns the packed state, AddRoundKey
+            # XORs it with the packed round key, its renorm unpacks into the (hi, lo) pair.  A debug
+            # dict logs THIS path's stages under the reference's names (the packed ones decoded from
+            # the hi | lo halves), so the golden stage test observes the headline path itself.
+            ct = self.sub.apply(*ct, out_level=self._floor())
+            self._log_pair(debug, f"enc.r{r}.sub", *ct)
+            ct = self._renorm_pair(*ct, level=NEED_SR_MIX + self.encoder.PACK_DEPTH)
+            self._log_pair(debug, f"enc.r{r}.sub.renorm", *ct)
+            ct = self.shift_rows(*ct)
+            self._log_pair(debug, f"enc.r{r}.sr", *ct)
+            acc = self.mix.mix_packed(*ct)
+            self._log_packed(debug, f"enc.r{r}.mc", acc)
+            x = self.xor4.apply(acc, self._packed_round_key(r), out_level=self._floor())
+            self._log_packed(debug, f"enc.r{r}.ark", x)
+            ct = self.encoder.renorm_unpack(x, level=next_level)
+            self._log_pair(debug, f"enc.r{r}.ark.renorm", *ct)
+            return ct
         if debug is None:
-            if self.packed_xor and r > 0:
-                # packed XOR stage (DESIGN.md §4c): MixColumns returns the packed state, AddRoundKey
-                # XORs it with the packed round key, its renorm unpacks into the (hi, lo) pair
-                ct = self._sub_renorm(ct, level=NEED_SR_MIX + self.encoder.PACK_DEPTH)
-                acc = self.mix.mix_packed(*self.shift_rows(*ct))
-                x = self.xor4.apply(acc, self._packed_round_key(r), out_level=self._floor())
-                return self.encoder.renorm_unpack(x, level=next_level)
             ct = self._sub_renorm(ct, level=NEED_SR_MIX)
             ct = self.srmc(*ct) if self.srmc is not None else self.mix_columns(*self.shift_rows(*ct))
             return self._ark_renorm(ct, key_pair, level=next_level)
@@ -331,13 +355,19 @@ class AESPipeline:
                     ct = self._renorm_pair(*self.inv_mix_columns(*ct), level=NEED_SUB_ARK_SR)
                     self._log_pair(debug, f"dec.r{r}.imc", *ct)
                 continue
-            if debug is None and self.packed_dec:
+            if self.packed_dec:
                 # packed XOR stage: AddRoundKey on the packed state, its renorm
                 # unpacking; InvMixColumns' XOR stage packed, unpacked by the renorm after it
-                ct = self._sub_renorm(self.inv_shift_rows(*ct), inverse=True, level=NEED_XOR + self.encoder.PACK_DEPTH)
+                # (a debug dict logs this path's stages under the reference's names)
+                ct = self.inv_shift_rows(*ct)
+                self._log_pair(debug, f"dec.r{r}.isr", *ct)
+                ct = self._sub_renorm(ct, inverse=True, level=NEED_XOR + self.encoder.PACK_DEPTH)
+                self._log_pair(debug, f"dec.r{r}.isb", *ct)
                 x = self.xor4.apply(self.encoder.pack(*ct), self._packed_round_key(r), out_level=self._floor())
                 ct = self.encoder.renorm_unpack(x, level=NEED_GF + self.encoder.PACK_DEPTH)
+                self._log_pair(debug, f"dec.r{r}.ark", *ct)
                 ct = self.encoder.renorm_unpack(self.invmix.imc_packed(*ct), level=NEED_ISR_ISB)
+                self._log_pair(debug, f"dec.r{r}.imc", *ct)
                 continue
             ct = self.inv_shift_rows(*ct)
             self._log_pair(debug, f"dec.r{r}.isr", *ct)

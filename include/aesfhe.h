@@ -44,6 +44,14 @@ int aesfhe_create_boot(aesfhe_ctx** out, int log_n, int fresh_level, int dnum, i
  * bootstrappable != 0: max_level is the fresh level of a bootstrappable set (aesfhe_create_boot). */
 int aesfhe_create_keyed(aesfhe_ctx** out, int log_n, int max_level, int dnum, int device_id, const uint8_t* key,
                         int bootstrappable);
+/* Encryption randomness (v, e0, e1 of every encryption, the renorms' re-encryptions included)
+ * is drawn under the context key with `nonce` folded into key words 6-7; key material is not
+ * affected.  Processes sharing one context key (the ranks of a multi-GPU job) must
+ * set different nonces, otherwise their i-th encryptions reuse (v, e) and the difference of two
+ * ranks' ciphertexts is a noiseless encoding of the plaintext difference.  Default 0; the Python
+ * Engine draws a random one per process (os.urandom) unless pinned.  No reference counterpart:
+ * desilofhe.Engine.encrypt (REF/engine_context.py:56-57) samples internally. */
+int aesfhe_set_enc_nonce(aesfhe_ctx* ctx, uint64_t nonce);
 /* limbs per level 0..max_level (a ciphertext at level l has npoly x limbs[l] x N words) */
 int aesfhe_level_limbs(aesfhe_ctx* ctx, int32_t* out);
 int aesfhe_destroy(aesfhe_ctx* ctx);

@@ -43,3 +43,34 @@ def test_engine_without_gpu_fails_loudly():
     from mi355x_ckks import Engine
     with pytest.raises(RuntimeError, match="HIP device|no CPU fallback|hip"):
         Engine(log_n=12, max_level=4)
+
+
+def test_integration_import_line_resolves():
+    """INTEGRATION.md §3's one-line swap of REF/engine_context.py:1 must bind BOTH names the
+    reference uses (Engine for construction, Ciphertext for the isinstance dispatch at :66)."""
+    text = (ROOT / "INTEGRATION.md").read_text()
+    m = re.search(r"^(from mi355x_ckks import [^\n#]+?)\s*(#.*)?$", text, re.M)
+    assert m, "INTEGRATION.md lost its import line"
+    line = m.group(1).strip()
+    ns = {}
+    exec(line, ns)  # the documented line itself, not a paraphrase of it
+    import mi355x_ckks
+    assert ns.get("Engine") is mi355x_ckks.Engine
+    assert ns.get("Ciphertext") is mi355x_ckks.Ciphertext
+
+
+def test_build_reuse_is_content_addressed(tmp_path, monkeypatch):
+    """build_ext.needs_build compares a sha256 of the sources and headers (never mtimes): touching
+    a file leaves the digest alone, changing one byte changes it"""
+    import os
+    import shutil
+    import build_ext
+    src = tmp_path / "csrc"
+    shutil.copytree(build_ext.CSRC, src)
+    monkeypatch.setattr(build_ext, "CSRC", src)
+    d0 = build_ext.source_digest()
+    f = src / build_ext.HEADERS[0]
+    os.utime(f, (1, 1))  # an old mtime, then a new one: no effect
+    assert build_ext.source_digest() == d0
+    f.write_bytes(f.read_bytes() + b"\n// changed\n")
+    assert build_ext.source_digest() != d0

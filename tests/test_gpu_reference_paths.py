@@ -149,15 +149,18 @@ _FINAL = {"enc.final.sub": "r10.sb", "enc.final.sub.renorm": "r10.sb", "enc.fina
           "enc.final.ark10": "r10.ark", "enc.output": "r10.ark", "enc.r0.ark": "r0.ark", "enc.r0.renorm": "r0.ark"}
 
 
-@pytest.mark.parametrize("seed", [0, 7, 42])
-def test_encrypt_every_debug_stage_matches_golden(ctx, coeff_dir, seed):
+@pytest.mark.parametrize("seed,packed", [(0, None), (7, None), (42, None), (7, False)])
+def test_encrypt_every_debug_stage_matches_golden(ctx, coeff_dir, seed, packed):
     """Each logged stage of a full C2 encrypt decodes to the bytes of tests/golden/stages.json
     (the byte-level reference model, REF/pipeline.py:123-188, inputs drawn as
-    REF/test/test_aes_pipeline_roundtrip.py:136-140)"""
+    REF/test/test_aes_pipeline_roundtrip.py:136-140).  packed None: the bench's own path (the
+    packed XOR stage of rounds 1..9) logs its stages; False: the reference's pair
+    steps."""
     from aes_keyschedule import load_all_coeffs
     from pipeline import AESPipeline
     fx = {s["seed"]: s for s in json.loads((GOLDEN / "stages.json").read_text())["seeds"]}[seed]
-    pipe = AESPipeline(ctx, load_all_coeffs(coeff_dir), use_hard_renorm_between_steps=True)
+    pipe = AESPipeline(ctx, load_all_coeffs(coeff_dir), use_hard_renorm_between_steps=True, packed_xor=packed)
+    assert pipe.packed_xor == (packed is None)  # the default IS the packed path in renorm mode
     pt = np.array(fx["plaintext"], np.uint8)
     rks = [np.array(k, np.uint8) for k in fx["round_keys"]]
     dbg = {}
@@ -171,4 +174,34 @@ def test_encrypt_every_debug_stage_matches_golden(ctx, coeff_dir, seed):
     assert set(dbg) == set(want)
     bad = [t for t, exp in want.items() if dbg[t]["plain"] is None or not np.array_equal(dbg[t]["plain"], exp)]
     assert not bad, bad
+    # the packed path's MixColumns / AddRoundKey outputs are single packed ciphertexts
+    assert all(("ct_packed" in dbg[f"enc.r{r}.{k}"]) == (packed is None) for r in range(1, 10) for k in ("mc", "ark"))
     assert np.array_equal(pipe.encoder.decode(*ct), np.array(fx["ciphertext"], np.uint8))
+
+
+@pytest.mark.parametrize("packed", [None, False])
+def test_decrypt_every_debug_stage_matches_byte_model(ctx, coeff_dir, packed):
+    """Each logged stage of a full C2 decrypt (REF/pipeline.py:193-254 with InvMixColumns after
+    AddRoundKey, README.md:87-94) decodes to the byte model's intermediate state: the packed
+    decrypt rounds under the same stage names as the reference's pair steps."""
+    from aes_keyschedule import load_all_coeffs
+    from oracle import aes_plain as A
+    from pipeline import AESPipeline
+    fx = {s["seed"]: s for s in json.loads((GOLDEN / "stages.json").read_text())["seeds"]}[7]
+    pipe = AESPipeline(ctx, load_all_coeffs(coeff_dir), use_hard_renorm_between_steps=True, packed_xor=packed)
+    assert pipe.packed_dec == (packed is None)
+    pt = np.array(fx["plaintext"], np.uint8)
+    rks = [np.array(k, np.uint8) for k in fx["round_keys"]]
+    ct = pipe.encoder.encode(A.ref_encrypt(pt, rks))
+    dbg = {}
+    back = pipe.decrypt(*ct, rks, debug=dbg)
+    s = A.ref_encrypt(pt, rks) ^ rks[10]
+    want = {"dec.init.ark10": s}
+    for r in range(9, 0, -1):
+        want[f"dec.r{r}.isr"] = A.inv_shift_rows(s)
+        want[f"dec.r{r}.isb"] = A.INV_SBOX[want[f"dec.r{r}.isr"]]
+        want[f"dec.r{r}.ark"] = want[f"dec.r{r}.isb"] ^ rks[r]
+        s = want[f"dec.r{r}.imc"] = A.ref_inv_mix_columns(want[f"dec.r{r}.ark"])
+    bad = [t for t, exp in want.items() if t not in dbg or dbg[t]["plain"] is None or not np.array_equal(dbg[t]["plain"], exp)]
+    assert not bad, bad
+    assert np.array_equal(pipe.encoder.decode(*back), pt)

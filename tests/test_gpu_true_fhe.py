@@ -61,10 +61,35 @@ def test_reference_noise_reducer_contracts(ctx):
     assert np.all(e_out < 12 * e_in ** 2 + 50 * e_in ** 3 + 1e-3), (e_out.max(), e_in.max())
 
 
+# every entry point that touches the secret key, on the context AND on the engine underneath it
+# (state_encoder's periodic-layout renorms call renorm_periodic / renorm_single / renorm_unpack,
+# decode calls decrypt): none may run between encryption of the input and the output
+SECRET_KEY_CALLS = ("decrypt", "renorm_pair", "renorm_periodic", "renorm_single", "renorm_unpack")
+ENGINE_SECRET_CALLS = SECRET_KEY_CALLS + ("export_secret",)
+
+
 def _no_secret_renorm(ctx, monkeypatch):
-    def refuse(*a, **k):
-        raise AssertionError("secret-key renorm called in true-FHE mode")
-    monkeypatch.setattr(ctx, "renorm_pair", refuse)
+    def refuse(name):
+        def f(*a, **k):
+            raise AssertionError(f"secret-key call {name} in true-FHE mode")
+        return f
+    for name in SECRET_KEY_CALLS:
+        monkeypatch.setattr(ctx, name, refuse("ctx." + name))
+    for name in ENGINE_SECRET_CALLS:
+        monkeypatch.setattr(ctx.engine, name, refuse("engine." + name))
+
+
+def test_guard_covers_every_secret_key_entry(ctx, monkeypatch):
+    """the guard itself: each secret-key entry point of the context and the engine raises"""
+    x = ctx.encrypt(np.ones(ctx.engine.slot_count))
+    _no_secret_renorm(ctx, monkeypatch)
+    for name in SECRET_KEY_CALLS:
+        with pytest.raises(AssertionError, match=name):
+            getattr(ctx, name)(x)
+        with pytest.raises(AssertionError, match=name):
+            getattr(ctx.engine, name)(x)
+    monkeypatch.undo()
+    assert np.abs(ctx.decrypt(x) - 1).max() < 1e-3  # restored
 
 
 def test_true_fhe_config2_encrypt_decrypt(ctx, coeff_dir, monkeypatch):

@@ -93,3 +93,38 @@ def test_many_module_generations_stay_bounded():
         del o
         gc.collect()
     assert ctx.lut_cache_size() == 0 and len(ctx.engine.freed) == 50
+
+
+def test_clear_with_live_owners_never_frees_a_newer_set():
+    """owner A holds digest d; clear_luts(); owner B requests d and gets a
+    new set t'.  A's stale record must not release t' when A dies -- B still evaluates with it."""
+    ctx = _ctx()
+    a = np.arange(16, dtype=np.complex128)
+    oa, ob = _Owner(), _Owner()
+    t = ctx.lut("sb", a, owner=oa)
+    ctx.clear_luts()
+    t2 = ctx.lut("sb", a, owner=ob)
+    assert t2 != t and ctx.lut_cache_size() == 1
+    assert ctx.lut("sb", a, owner=oa) == t2  # A asks again after the clear: shares t'
+    del oa
+    gc.collect()
+    assert t2 not in ctx.engine.freed and ctx.lut_cache_size() == 1  # B still holds t'
+    del ob
+    gc.collect()
+    assert t2 in ctx.engine.freed and ctx.lut_cache_size() == 0
+
+
+def test_clear_then_old_owner_dies_first():
+    """the same with A not asking again: its death after the clear is a no-op"""
+    ctx = _ctx()
+    a = np.arange(16, dtype=np.complex128)
+    oa, ob = _Owner(), _Owner()
+    ctx.lut("sb", a, owner=oa)
+    ctx.clear_luts()
+    t2 = ctx.lut("sb", a, owner=ob)
+    del oa
+    gc.collect()
+    assert ctx.engine.freed == [] and ctx.lut_cache_size() == 1
+    del ob
+    gc.collect()
+    assert ctx.engine.freed == [t2]

@@ -40,3 +40,26 @@ def test_kappa_folding_matches():
     u = KAPPA * x
     g = s.a1 * u + s.a3 * u * u * np.conj(u) + s.c15 * np.conj(u) ** 15
     assert np.abs(g - _snap15(x)).max() < 1e-12
+
+
+def _snap1d_eval(c, x):
+    """sum_k c_k B_k(x), B_k = x^k (k <= 8), conj(x^(16-k)) (k >= 9), k > 15 folded (REF/snapper_1d_z16.py:36-90)"""
+    out = np.zeros_like(x)
+    for k, ck in enumerate(c):
+        kk = k % 16
+        out = out + ck * (x ** kk if kk <= 8 else np.conj(x ** (16 - kk)))
+    return out
+
+
+def test_snapper_1d_coefficients_and_codewords(coeff_dir, ref_coeffs):
+    """snapper_1d_z16.load_coeff1d on the generated zeta16_snap_coeffs.json equals the reference's
+    file (tests/golden/ref_coeff.npz), and every codeword maps onto itself within 1e-2 (the fitted
+    polynomial's own residual, REF/gen/make_zeta16_snap_coeffs.py) -- nibbles decode exactly"""
+    from snapper_1d_z16 import load_coeff1d
+    c = load_coeff1d(coeff_dir / "zeta16_snap_coeffs.json")
+    ref = ref_coeffs["zeta16_snap_coeffs"]
+    assert c.shape == ref.shape and np.abs(c - ref).max() < 1e-12
+    y = _snap1d_eval(c, Z)
+    assert np.abs(y - Z).max() < 1e-2
+    nib = np.round(-np.angle(y) * 16 / (2 * np.pi)).astype(int) % 16
+    assert np.array_equal(nib, np.arange(16))
