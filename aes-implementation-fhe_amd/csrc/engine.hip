@@ -25,6 +25,7 @@
 #include "bootstrap.h"
 #include "encoder.h"
 #include "kernels.h"
+#include "launch.h"
 #include "params.h"
 
 namespace {
@@ -1354,9 +1355,15 @@ public:
     // acc = P * (relinearised ciphertext); the dropped and P rows (contiguous in acc) go to
     // coefficients together, one conversion to the r kept limbs, and the NTT finish computes
     // (acc - conv) Q'^{-1}.  Saves the separate rescale's INTT + spread + NTT of 2 r rows.
+    // members one batched key switch at `level` can carry: the key inner product's batch and the
+    // ModUp conversion's groups (members x digits) both bound it
+    int ks_chunk(int level) const {
+        const int nd = (hp_.nl(level) + hp_.alpha - 1) / hp_.alpha;
+        return std::max(1, std::min(kMaxKsBatch, kMaxConvGroups / nd));
+    }
     bool fused_relin_rescale_ok(const Ct& c) const {
         if (!fuse_rr_ || pm(c) != 3 || c.pend < 1 || c.level < 1 || c.zero) return false;
-        return mdr_off_[c.level] != SIZE_MAX && 2 * c.nb <= kMaxConvGroups && c.nb <= kMaxKsBatch;
+        return mdr_off_[c.level] != SIZE_MAX && 2 * c.nb <= kMaxConvGroups && c.nb <= ks_chunk(c.level);
     }
     Ct relin_rescale(const Ct& c) {
         const int l = c.level, n = hp_.n, nl = hp_.nl(l), ne = nl + hp_.n_p, nb = c.nb;
@@ -1496,8 +1503,9 @@ public:
             launch_tensor_ptrs(S(), T_, d.data, tp, g, nl, qmap());
             cnt_[C_MUL] += g;
             for (int m = 0; m < g; ++m) drop(pr[grp[m]]);
-            for (int m0 = 0; m0 < g; m0 += kMaxKsBatch) {
-                const int c = std::min(kMaxKsBatch, g - m0);
+            const int chunk = ks_chunk(L);
+            for (int m0 = 0; m0 < g; m0 += chunk) {
+                const int c = std::min(chunk, g - m0);
                 Ct v = d;  // view of members m0 .. m0 + c - 1 (not released on its own)
                 v.data = d.data + (size_t)m0 * 3 * nl * nn, v.npoly = 3 * c, v.nb = c, v.words = (size_t)3 * c * nl * nn;
                 Ct o;
@@ -1544,7 +1552,7 @@ public:
         for (int i = 0; i < n; ++i) {
             if (done[i]) continue;
             std::vector<int> grp;
-            for (int j = i; j < n && (int)grp.size() < kMaxKsBatch; ++j)
+            for (int j = i; j < n && (int)grp.size() < ks_chunk(cn[i].level); ++j)
                 if (!done[j] && batch_ops_ && cn[j].level == cn[i].level && cn[j].nb == 1 && cn[i].nb == 1) grp.push_back(j), done[j] = true;
             if (grp.size() < 2) {
                 done[i] = true;
@@ -1569,6 +1577,160 @@ public:
         return out;
     }
 
+    // ------------------------------------------------------------------ heterogeneous batched key switch
+    // n automorphisms X -> X^G[i] of possibly different ciphertexts (rotations by different steps,
+    // conjugations, or a mix), each followed by its key switch.  Inputs are brought to canonical
+    // form first -- deferred scalar / plaintext products owing ONE rescale at a common level are
+    // stacked and rescaled together (one INTT + one spread-NTT-finish for all of them).  Items at
+    // one level then form ONE batched key switch per chunk: one ModUp per distinct source (a
+    // source's several automorphisms read its extension through X -> X^g: hoisted), ONE key inner
+    // product launch with a key and a Galois element per member, ONE automorphism launch for the
+    // c0s and ONE stacked ModDown.  Results equal galois(C[i], G[i]) bit for bit.
+    struct KsSrc {
+        const u32* c0;
+        const u32* c1;
+        int level;
+    };
+    std::vector<Ct> galois_multi(const std::vector<const Ct*>& C, const std::vector<u64>& G) {
+        const int n = (int)C.size(), nn = hp_.n;
+        if ((int)G.size() != n) throw std::runtime_error("galois_multi: one Galois element per ciphertext");
+        const u64 two_n = 2ull * nn;
+        for (u64 g : G)
+            if (!(g & 1) || g >= two_n) throw std::runtime_error("galois_multi: Galois elements must be odd and below 2N");
+        std::vector<Ct> out(n);
+        std::vector<Ct> owned;                      // buffers released at the end
+        std::map<const u32*, KsSrc> src_of;         // input data -> canonical source
+        // 1. canonical sources; lazy 2-polynomial tensors owing one rescale, grouped by level, are
+        //    stacked and rescaled together
+        std::map<int, std::vector<const Ct*>> lazy1;
+        for (int i = 0; i < n; ++i) {
+            const Ct& c = *C[i];
+            if (vis_npoly(c) != 2) throw std::runtime_error("rotation/conjugation expects a 2-polynomial ciphertext");
+            if (src_of.count(c.data)) continue;
+            if (c.lazy && c.pend == 1 && pm(c) == 2 && c.nb == 1 && c.ntt && !c.zero) {
+                auto& v = lazy1[c.level];
+                if (std::find(v.begin(), v.end(), &c) == v.end()) v.push_back(&c);
+                src_of[c.data] = KsSrc{nullptr, nullptr, -1};  // filled below
+                continue;
+            }
+            Ct cn = normalize(c);
+            if (cn.data != c.data) owned.push_back(cn);
+            src_of[c.data] = KsSrc{cn.data, cn.data + (size_t)hp_.nl(cn.level) * nn, cn.level};
+        }
+        for (auto& kv : lazy1) {
+            const auto& v = kv.second;
+            for (size_t m0 = 0; m0 < v.size(); m0 += kMaxMembers) {
+                const int cnt = (int)std::min<size_t>(kMaxMembers, v.size() - m0), l = kv.first, nl = hp_.nl(l);
+                if (cnt == 1) {
+                    Ct cn = normalize(*v[m0]);
+                    owned.push_back(cn);
+                    src_of[v[m0]->data] = KsSrc{cn.data, cn.data + (size_t)hp_.nl(cn.level) * nn, cn.level};
+                    continue;
+                }
+                Ct st = alloc_ct(l, 2 * cnt, cnt);
+                MemberPtrs mp;
+                for (int m = 0; m < cnt; ++m) mp.src[m] = v[m0 + m]->data, mp.dst[m] = st.data + (size_t)m * 2 * nl * nn;
+                launch_copy_members(S(), T_, mp, cnt, 2 * nl);
+                st.pend = 1;
+                st.lazy = true;
+                Ct rs = rescale(st);  // one rescale of all members (rescale handles npoly = 2 cnt)
+                release(st);
+                owned.push_back(rs);
+                const int nlo = hp_.nl(rs.level);
+                for (int m = 0; m < cnt; ++m) {
+                    const u32* c0 = rs.data + (size_t)m * 2 * nlo * nn;
+                    src_of[v[m0 + m]->data] = KsSrc{c0, c0 + (size_t)nlo * nn, rs.level};
+                }
+            }
+        }
+        // 2. items by level, chunked: members <= kMaxMembers, sources x digits <= kMaxConvGroups
+        std::map<int, std::vector<int>> by_level;
+        for (int i = 0; i < n; ++i) {
+            const KsSrc& s = src_of.at(C[i]->data);
+            if (G[i] == 1) {  // identity: a copy of the canonical source
+                Ct o = alloc_ct(s.level, 2);
+                launch_copy_rows(S(), T_, o.data, s.c0, 2 * (size_t)hp_.nl(s.level));
+                out[i] = o;
+                continue;
+            }
+            by_level[s.level].push_back(i);
+        }
+        for (auto& kv : by_level) {
+            const int l = kv.first, nl = hp_.nl(l), ne = nl + hp_.n_p, nd = (nl + hp_.alpha - 1) / hp_.alpha;
+            const auto& items = kv.second;
+            const int max_src = std::max(1, kMaxConvGroups / nd);
+            size_t pos = 0;
+            while (pos < items.size()) {
+                std::vector<int> chunk;
+                std::vector<KsSrc> srcs;  // distinct sources, in first-use order
+                auto src_index = [&](const KsSrc& s) {
+                    for (size_t j = 0; j < srcs.size(); ++j)
+                        if (srcs[j].c0 == s.c0) return (int)j;
+                    return -1;
+                };
+                while (pos < items.size() && (int)chunk.size() < kMaxMembers) {
+                    const KsSrc& s = src_of.at(C[items[pos]]->data);
+                    const bool known = src_index(s) >= 0;
+                    if (!known && (int)srcs.size() >= max_src) break;
+                    if (!known) srcs.push_back(s);
+                    chunk.push_back(items[pos++]);
+                }
+                const int nm = (int)chunk.size(), ns = (int)srcs.size();
+                // c1 of every source, stacked: used in place when the sources already sit at a
+                // member stride of 2 nl N (e.g. one stack rescaled above), else gathered
+                const u32* c1s = srcs[0].c1;
+                size_t d_ms = 0;
+                u32* c1buf = nullptr;
+                if (ns > 1) {
+                    const size_t stride = (size_t)2 * nl * nn;
+                    bool regular = true;
+                    for (int j = 0; j < ns; ++j) regular = regular && srcs[j].c1 == srcs[0].c1 + j * stride;
+                    if (regular) {
+                        d_ms = stride;
+                    } else {
+                        std::vector<const u32*> c1v(ns);
+                        for (int j = 0; j < ns; ++j) c1v[j] = srcs[j].c1;
+                        c1buf = tmp((size_t)ns * nl);
+                        MemberPtrs mp;
+                        for (int j = 0; j < ns; ++j) mp.src[j] = c1v[j], mp.dst[j] = c1buf + (size_t)j * nl * nn;
+                        launch_copy_members(S(), T_, mp, ns, nl);
+                        c1s = c1buf, d_ms = (size_t)nl * nn;
+                    }
+                }
+                u32* ext = modup(c1s, l, ns, d_ms);
+                u32* acc = tmp((size_t)nm * 2 * ne);
+                KsMultiArgs ka;
+                AutoMulti am;
+                for (int m = 0; m < nm; ++m) {
+                    const int i = chunk[m];
+                    const KsSrc& s = src_of.at(C[i]->data);
+                    ka.key[m] = ksk(G[i]);
+                    ka.g[m] = G[i];
+                    ka.src[m] = src_index(s);
+                    am.src[m] = s.c0;
+                    am.g[m] = G[i];
+                }
+                launch_key_inner_multi(S(), T_, acc, ext, c1s, ka, nm, ns, nd, ne, nl, hp_.alpha, hp_.n_ks + hp_.n_p, hp_.n_ks, extmap(nl),
+                                       (size_t)ext_rows(l) * nn, d_ms, (size_t)2 * ne * nn);
+                untmp(ext, (size_t)ns * ext_rows(l));
+                if (c1buf) untmp(c1buf, (size_t)ns * nl);
+                const size_t ms = (size_t)2 * nl * nn;
+                u32* c0p = tmp((size_t)nm * 2 * nl);  // member stride 2 nl N (moddown's add stride), first nl rows used
+                launch_automorph_multi(S(), T_, c0p, ms, am, nm, nl);
+                Ct o = moddown(acc, l, c0p, nullptr, nm, ms);
+                untmp(acc, (size_t)nm * 2 * ne);
+                untmp(c0p, (size_t)nm * 2 * nl);
+                unstack(o, &out[0], chunk.data());
+                release(o);
+                cnt_[C_KS] += nm;
+            }
+        }
+        for (const Ct& c : owned) release(c);
+        return out;
+    }
+
+    void count_conj() { cnt_[C_CONJ]++; }
+    void count_rot() { cnt_[C_ROT]++; }
     std::vector<Ct> conjugate_many(const std::vector<const Ct*>& C) {
         cnt_[C_CONJ] += C.size();
         return galois_many(C, conj_galois());
@@ -2031,6 +2193,36 @@ public:
         return which < boot_cts() ? bs_.cts[which] : bs_.stc[which - boot_cts()];
     }
     Ct debug_lin_group(const Ct& c, int which) { return lin_group(c, debug_group(which)); }
+    // the same for the sparse-slot plan of period n: CoeffToSlot groups first,
+    // then SlotToCoeff (stc[0..], then -- pair4 plans -- stc_lo last)
+    BootGroupDev& debug_sparse_group(int period, int which, bool pair = false) {
+        boot_setup();
+        SparseBoot& sv = sparse_variant(period, pair);
+        const int nc = (int)sv.cts.size(), ns = (int)sv.stc.size();
+        if (which < 0 || which >= nc + ns + (sv.pair4 ? 1 : 0)) throw std::runtime_error("debug_sparse_group: no such group");
+        return which < nc ? sv.cts[which] : which < nc + ns ? sv.stc[which - nc] : sv.stc_lo;
+    }
+    // the group applied on the host: the plan is the small ring's (its diagonals one period dn
+    // long), so it acts on the first dn slots of the (dn-periodic) input and the result is tiled
+    // over all slots -- the model of debug_sparse_group on a periodic message
+    void debug_sparse_group_plain(int period, int which, bool pair, const double* re, const double* im, double* ore, double* oim,
+                                  int* info) {
+        const LinGroup& g = *debug_sparse_group(period, which, pair).g;
+        const SparseBoot& sv = sparse_variant(period, pair);
+        info[1] = (int)sv.cts.size();
+        info[2] = (int)(sv.cts.size() + sv.stc.size() + (sv.pair4 ? 1 : 0));
+        int dn = 0;
+        for (const auto& row : g.diag)
+            for (const auto& d : row)
+                if (!d.empty()) dn = (int)d.size();
+        const int M = slot_count();
+        if (dn <= 0 || M % dn) throw std::runtime_error("debug_sparse_group_plain: bad diagonal period");
+        std::vector<cplx> v(dn);
+        for (int j = 0; j < dn; ++j) v[j] = cplx(re[j], im[j]);
+        v = apply_group_plain(g, v);
+        for (int j = 0; j < M; ++j) ore[j] = v[j % dn].real(), oim[j] = v[j % dn].imag();
+        info[0] = dn;
+    }
     // the same group applied to slot values on the host (bootstrap.cpp apply_group_plain): the
     // model debug_lin_group's decryption is checked against
     void debug_lin_group_plain(int which, const double* re, const double* im, double* ore, double* oim) {
@@ -2588,8 +2780,11 @@ public:
     // X -> X^(4n+1) (5^n = 4n + 1 mod 8n), which fixes X^2k and negates X^k, so with
     // m = gain z / 2 and r = rot_n(m):  gain a = m + r,  gain b = X^-k (m - r).
     bool mono_pair_ = !(std::getenv("AESFHE_PAIR_MONO") && std::atoi(std::getenv("AESFHE_PAIR_MONO")) == 0);
-    void bootstrap_pair_mono(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob, double gain, int period) {
+    // z = a + X^k b at level 0 (k = N / 4 period): exact, one fused multiply-add with the NTT form
+    // of the monomial
+    Ct mono_pack(const Ct& a_in, const Ct& b_in, int period) {
         const int n = hp_.n, k = n / (4 * period), nl0 = hp_.nl(0);
+        if (period < 1 || 2 * period > slot_count() || n % (4 * period)) throw std::runtime_error("mono_pack: bad period");
         Ct z0[2];
         const Ct* in[2] = {&a_in, &b_in};
         for (int m = 0; m < 2; ++m) {
@@ -2601,19 +2796,30 @@ public:
         launch_fma_poly(S(), T_, z.data, z0[0].data, z0[1].data, monomial(k), 2 * nl0, nl0, qmap());
         release(z0[0]);
         release(z0[1]);
-        SparseBoot* sv = 2 * period < slot_count() ? &sparse_variant(2 * period) : nullptr;
-        Ct mz = bootstrap_l0(z, 99, 0.5 * gain, sv);
+        return z;
+    }
+    // m = (a + X^k b) / 2 -> (a, b): r = rot_period(m) fixes X^2k and negates X^k, so a = m + r and
+    // b = X^-k (m - r)
+    void mono_split(const Ct& mz, int period, Ct& hi, Ct& lo) {
+        const int n = hp_.n, k = n / (4 * period);
         Ct r = rotate(mz, period);
-        Ct hi = add_sub(mz, r, false);
+        hi = add_sub(mz, r, false);
         Ct d = add_sub(mz, r, true);
-        release(mz);
         release(r);
         Ct dn = ensure_ntt(d);
         if (dn.data != d.data) release(d);
-        Ct lo = alloc_ct(dn.level, 2);
+        lo = alloc_ct(dn.level, 2);
         copy_meta(lo, dn);
         launch_mul_poly(S(), T_, lo.data, dn.data, monomial(2 * n - k), 2, hp_.nl(dn.level), qmap());
         release(dn);
+    }
+    void bootstrap_pair_mono(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob, double gain, int period) {
+        Ct z = mono_pack(a_in, b_in, period);
+        SparseBoot* sv = 2 * period < slot_count() ? &sparse_variant(2 * period) : nullptr;
+        Ct mz = bootstrap_l0(z, 99, 0.5 * gain, sv);
+        Ct hi, lo;
+        mono_split(mz, period, hi, lo);
+        release(mz);
         cnt_[C_BOOT] += 1;  // bootstrap_l0 counted one: two messages refreshed
         *oa = put_ct(hi);
         *ob = put_ct(lo);
@@ -2663,6 +2869,7 @@ public:
         const size_t tms = (size_t)2 * nlt * n;
         Ct u = keyswitch(raised.data + (size_t)nlt * n, top, ksk(tag_s2d()), raised.data, nullptr, nb, tms, tms);
         release(raised);
+        if (stop_after == 12) return u;  // debug: back on the dense secret, before the sparse trace
         // 4b. sparse: the trace to the subring, x += rot(x, n 2^i) for 2^i < M / n (the overflow's
         // components outside the subring cancel, the rest is multiplied by M / n)
         if (sv)
@@ -2769,7 +2976,7 @@ public:
         Ct fre, fim;
         // (eval_mod_many({re, im}) is bit-exact with the stacked form below but measured no faster:
         // the stacked halves already share every key read; profiles/r2_evalmod_batch_ab.json)
-        if (stop_after > 9 && stack_evalmod_ && 2 * nb <= kMaxKsBatch && re.level == im.level && re.pend == im.pend &&
+        if (stop_after > 9 && stack_evalmod_ && 2 * nb <= std::min(4, ks_chunk(re.level)) && re.level == im.level && re.pend == im.pend &&
             !re.lazy && !im.lazy && pm(re) == 2 && pm(im) == 2 && re.ntt == im.ntt) {
             Ct st = alloc_ct(re.level, re.npoly + im.npoly, 2 * nb);
             st.ntt = re.ntt, st.pend = re.pend;
@@ -3462,6 +3669,20 @@ int aesfhe_mul_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* a, const aesfhe
     for (int i = 0; i < n; ++i) out[i] = e.put_ct(r[i]);
     API_END
 }
+int aesfhe_galois_multi(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, const uint64_t* galois, aesfhe_handle* out) {
+    API_BEGIN Engine& e = *ctx->eng;
+    if (n < 0 || (n > 0 && (!in || !galois || !out))) throw std::runtime_error("galois_multi: bad arguments");
+    std::vector<const Ct*> C(n);
+    std::vector<u64> G(galois, galois + n);
+    for (int i = 0; i < n; ++i) C[i] = &e.ct(in[i]);  // deferred work is resolved inside (batched)
+    std::vector<Ct> r = e.galois_multi(C, G);
+    for (int i = 0; i < n; ++i) {
+        if (G[i] == e.conj_galois()) e.count_conj();
+        else if (G[i] != 1) e.count_rot();
+        out[i] = e.put_ct(r[i]);
+    }
+    API_END
+}
 int aesfhe_conjugate_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, aesfhe_handle* out) {
     API_BEGIN Engine& e = *ctx->eng;
     if (n < 0 || (n > 0 && (!in || !out))) throw std::runtime_error("conjugate_many: bad arguments");
@@ -3512,6 +3733,29 @@ int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle c, int stage, aesfhe_
     // AESFHE_DEBUG_PERIOD: the stages of the sparse-slot bootstrap of that period (profiling)
     static const int period = std::getenv("AESFHE_DEBUG_PERIOD") ? std::atoi(std::getenv("AESFHE_DEBUG_PERIOD")) : 0;
     CT_OP(e.bootstrap(e.canon(c), stage, 1.0, period))
+}
+int aesfhe_debug_boot_stage_sparse(aesfhe_ctx* ctx, aesfhe_handle c, int stage, int period, aesfhe_handle* out) {
+    CT_OP(e.bootstrap(e.canon(c), stage, 1.0, period))
+}
+int aesfhe_debug_sparse_group(aesfhe_ctx* ctx, aesfhe_handle c, int period, int which, int pair, aesfhe_handle* out) {
+    CT_OP(e.lin_group(e.canon(c), e.debug_sparse_group(period, which, pair != 0)))
+}
+int aesfhe_debug_sparse_group_plain(aesfhe_ctx* ctx, int period, int which, int pair, const double* re, const double* im,
+                                    double* out_re, double* out_im, int* info3) {
+    API_BEGIN if (!re || !im || !out_re || !out_im || !info3) throw std::runtime_error("debug_sparse_group_plain: null buffer");
+    ctx->eng->debug_sparse_group_plain(period, which, pair != 0, re, im, out_re, out_im, info3);
+    API_END
+}
+int aesfhe_debug_mono_pack(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int period, aesfhe_handle* out) {
+    CT_OP(e.mono_pack(e.canon(a), e.canon(b), period))
+}
+int aesfhe_debug_mono_split(aesfhe_ctx* ctx, aesfhe_handle m, int period, aesfhe_handle* out_hi, aesfhe_handle* out_lo) {
+    API_BEGIN Engine& e = *ctx->eng;
+    Ct hi, lo;
+    e.mono_split(e.canon(m), period, hi, lo);
+    *out_hi = e.put_ct(hi);
+    *out_lo = e.put_ct(lo);
+    API_END
 }
 int aesfhe_debug_lin_group(aesfhe_ctx* ctx, aesfhe_handle c, int which, aesfhe_handle* out) {
     CT_OP(e.debug_lin_group(e.canon(c), which))
@@ -3622,6 +3866,7 @@ int aesfhe_kernel_work(aesfhe_ctx* ctx, double* out, int n) {
     for (int k = 0; k < n && k < KID_N; ++k) out[k] = p.work[k];
     API_END
 }
+uint64_t aesfhe_launch_count(void) { return g_launches.load(std::memory_order_relaxed); }
 int aesfhe_reset_counters(aesfhe_ctx* ctx) {
     API_BEGIN ctx->eng->reset_counters();
     API_END

@@ -190,7 +190,7 @@ void launch_base_convert(hipStream_t st, const DevTables& T, const ConvBatch& cb
 // g != 0: ext and d are read through the automorphism X -> X^g (hoisted rotation)
 // nb > 1: nb ciphertexts' key switches with the SAME key in one launch (the key is read once
 // per residue for all of them); member m uses ext + m ext_ms, d + m d_ms, acc + m acc_ms (words)
-constexpr int kMaxKsBatch = 4;
+constexpr int kMaxKsBatch = 8;
 // accum: acc += the inner product (giant steps summed in Q*P, one ModDown for all of them)
 // fold (g == 0 only): acc[p][x] += gad_x add_p[x] on the Q rows x < nl (member m: add_p + m ms),
 // gad = P mod q_x Shoup pairs -- the relinearised P (c0, c1) + acc before a ModDown that also
@@ -204,6 +204,26 @@ struct KsFold {
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
                       int alpha, int nkey, int nks, LimbMap map, u64 g = 0, int nb = 1, size_t ext_ms = 0, size_t d_ms = 0,
                       size_t acc_ms = 0, KsFold fold = {}, bool accum = false);
+// Heterogeneous batched key switch (Engine::ks_multi): member m of one launch
+// reads its own key and Galois element.  acc_m [2][ne] (acc + m acc_ms) = sum_j e_j ⊙ key_m[j]
+// with e_j = ext_{src_m}[j] (ext + src_m ext_ms), d_{src_m} (d + src_m d_ms) on digit j's own
+// limbs, both read through X -> X^g_m (g_m = 0: identity).  Several members may share a source:
+// the hoisted rotations of one ciphertext (one ModUp for all of them).
+constexpr int kKsMulti = 16;
+struct KsMultiArgs {
+    const u32* key[kKsMulti] = {};
+    u64 g[kKsMulti] = {};
+    int src[kKsMulti] = {};
+};
+void launch_key_inner_multi(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const KsMultiArgs& ka, int nm,
+                            int nsrc, int nd, int ne, int nl, int alpha, int nkey, int nks, LimbMap map, size_t ext_ms, size_t d_ms,
+                            size_t acc_ms);
+// out + m out_ms (rows rows) = in_m through X -> X^g_m, m < n (one launch; g_m = 1: a copy)
+struct AutoMulti {
+    const u32* src[kKsMulti] = {};
+    u64 g[kKsMulti] = {};
+};
+void launch_automorph_multi(hipStream_t st, const DevTables& T, u32* out, size_t out_ms, const AutoMulti& am, int n, int rows);
 // out[p][t] = sum_j x_j[p][t] pt_j[t] over rows t < rows, polys p < npoly (x poly stride xs,
 // out poly stride os, in words)
 constexpr int kMacMax = 16;

@@ -360,6 +360,69 @@ __global__ void __launch_bounds__(kBlock) k_key_inner(u32* acc, const u32* ext, 
     ts_end(ts);
 }
 
+// heterogeneous members (KsMultiArgs): grid z = member, each member its own key, Galois element
+// and ModUp source; otherwise the arithmetic of k_key_inner<1> (four coefficients per thread,
+// 64-bit multiply-adds folded every 8 digits)
+__global__ void __launch_bounds__(kBlock) k_key_inner_multi(u32* acc, const u32* ext, const u32* d, KsMultiArgs ka, int nd, int ne,
+                                                            int nl, int alpha, int nkey, int nks, LimbMap map, const PrimeConst* pc,
+                                                            int logn, size_t ext_ms, size_t d_ms, size_t acc_ms, unsigned long long* ts) {
+    ts_begin(ts);
+    const int x = blockIdx.y, m = blockIdx.z;
+    const u64 g = ka.g[m];
+    const u32* key = ka.key[m];
+    const int sm = ka.src[m];
+    const size_t k = ((size_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+    u32 ks[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) ks[v] = g ? galois_src((u32)(k + v), g, logn) : (u32)(k + v);
+    const PrimeConst P = pc[map.prime(x)];
+    const int krow = x < nl ? x : nks + (x - nl);
+    const int own = x < nl ? x / alpha : -1;
+    u64 s0[4] = {}, s1[4] = {};
+    for (int j = 0; j < nd; ++j) {
+        if (j && (j & 7) == 0) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) s0[v] = fold64(s0[v], P.q, P.r32), s1[v] = fold64(s1[v], P.q, P.r32);
+        }
+        const size_t kr = (((size_t)j * 2 * nkey + krow) << logn) + k;
+        const uint4 vb = *reinterpret_cast<const uint4*>(key + kr);
+        const uint4 va = *reinterpret_cast<const uint4*>(key + kr + ((size_t)nkey << logn));
+        const u32 kb4[4] = {vb.x, vb.y, vb.z, vb.w}, ka4[4] = {va.x, va.y, va.z, va.w};
+        const u32* src = j == own ? d + sm * d_ms + ((size_t)x << logn) : ext + sm * ext_ms + (((size_t)j * ne + x) << logn);
+        u32 e[4];
+        if (g) {
+#pragma unroll
+            for (int v = 0; v < 4; ++v) e[v] = src[ks[v]];
+        } else {
+            const uint4 t = *reinterpret_cast<const uint4*>(src + k);
+            e[0] = t.x, e[1] = t.y, e[2] = t.z, e[3] = t.w;
+        }
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            s0[v] += (u64)e[v] * kb4[v];
+            s1[v] += (u64)e[v] * ka4[v];
+        }
+    }
+    u32 r0[4], r1[4];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) r0[v] = reduce64(s0[v], P.q, P.mu, P.r32), r1[v] = reduce64(s1[v], P.q, P.mu, P.r32);
+    uint4* a0 = reinterpret_cast<uint4*>(acc + m * acc_ms + ((size_t)x << logn) + k);
+    uint4* a1 = reinterpret_cast<uint4*>(acc + m * acc_ms + (((size_t)ne + x) << logn) + k);
+    *a0 = make_uint4(r0[0], r0[1], r0[2], r0[3]);
+    *a1 = make_uint4(r1[0], r1[1], r1[2], r1[3]);
+    ts_end(ts);
+}
+__global__ void k_automorph_multi(u32* out, size_t out_ms, AutoMulti am, int logn) {
+    const int row = blockIdx.y, m = blockIdx.z;
+    const u32 i = blockIdx.x * kBlock + threadIdx.x;
+    const u64 g = am.g[m];
+    const u32 mask2n = (2u << logn) - 1;
+    const u32 e = 2u * (__brev(i) >> (32 - logn)) + 1u;
+    const u32 eg = (u32)(((u64)e * (g & mask2n)) & mask2n);
+    const u32 j = __brev((eg - 1u) >> 1) >> (32 - logn);
+    out[m * out_ms + ((size_t)row << logn) + i] = am.src[m][((size_t)row << logn) + j];
+}
+
 // ------------------------------------------------------------------------------------
 // sampling and key generation
 // ------------------------------------------------------------------------------------
@@ -402,6 +465,7 @@ inline dim3 ew_grid(int logn, int rows) { return dim3((1u << logn) / kBlock, row
 // ======================================================================================
 thread_local KernelProfiler* g_prof = nullptr;
 void prof_set(KernelProfiler* p) { g_prof = p; }
+std::atomic<unsigned long long> g_launches{0};
 
 // ======================================================================================
 // launch validation (launch.h launch_validate): per-kernel limits, queried once
@@ -1023,23 +1087,42 @@ void launch_mac(hipStream_t st, const DevTables& T, u32* out, const MacTerms& m,
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
                       int alpha, int nkey, int nks, LimbMap map, u64 g, int nb, size_t ext_ms, size_t d_ms, size_t acc_ms, KsFold fold,
                       bool accum) {
-    if (nb < 1 || nb > kMaxKsBatch) throw std::runtime_error("launch_key_inner: 1..4 batched ciphertexts");
+    if (nb < 1 || nb > kMaxKsBatch) throw std::runtime_error("launch_key_inner: 1..8 batched ciphertexts");
     if (fold.gad && g) throw std::runtime_error("launch_key_inner: fold with an automorphism");
     // per ciphertext ext/d (nd x ne) read and acc (2 x ne) written; the key (nd x 2 x ne) once;
     // the fold reads 2 x nl more rows per ciphertext
     const double fw = (fold.gad ? 2.0 * nb * nl : 0.0) + (accum ? 2.0 * nb * ne : 0.0);
     const double bytes = words(((nb * (nd + 2.0) + 2.0 * nd) * ne + fw) * (1u << T.logn));
     const dim3 grid((1u << T.logn) / (4 * kBlock), ne);
-    // register footprint follows the batch: 1, 2 or 4 ciphertexts
+    // register footprint follows the batch: 1, 2, 4 or 8 ciphertexts
     if (nb == 1)
         prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<1>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g,
                        map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum);
     else if (nb == 2)
         prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<2>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g,
                        map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum);
-    else
+    else if (nb <= 4)
         prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<4>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g,
                        map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum);
+    else
+        prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<8>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g,
+                       map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum);
+}
+void launch_key_inner_multi(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const KsMultiArgs& ka, int nm,
+                            int nsrc, int nd, int ne, int nl, int alpha, int nkey, int nks, LimbMap map, size_t ext_ms, size_t d_ms,
+                            size_t acc_ms) {
+    if (nm < 1 || nm > kKsMulti) throw std::runtime_error("launch_key_inner_multi: 1..16 members");
+    for (int m = 0; m < nm; ++m)
+        if (!ka.key[m] || ka.src[m] < 0 || ka.src[m] >= nsrc) throw std::runtime_error("launch_key_inner_multi: bad member");
+    // each member reads its source's ext / d and its key, writes acc; distinct sources' ext once
+    const double bytes = words(((nsrc * (double)nd + nm * (2.0 * nd + 2.0)) * ne) * (1u << T.logn));
+    prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner_multi, dim3((1u << T.logn) / (4 * kBlock), ne, nm), dim3(kBlock), 0, st, acc, ext, d,
+                   ka, nd, ne, nl, alpha, nkey, nks, map, T.pc, T.logn, ext_ms, d_ms, acc_ms);
+}
+void launch_automorph_multi(hipStream_t st, const DevTables& T, u32* out, size_t out_ms, const AutoMulti& am, int n, int rows) {
+    if (n < 1 || n > kKsMulti) throw std::runtime_error("launch_automorph_multi: 1..16 members");
+    prof_launch(KID_AUTOMORPH, words(2.0 * n * rows * (1u << T.logn)), k_automorph_multi, dim3((1u << T.logn) / kBlock, rows, n),
+                dim3(kBlock), 0, st, out, out_ms, am, T.logn);
 }
 void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, const PrngKey& key, u64 stream, int kind) {
     prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_small, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, nl, map, key, stream, kind, T.pc,

@@ -15,6 +15,9 @@
 #include "kernels.h"
 
 extern thread_local KernelProfiler* g_prof;
+#include <atomic>
+// every kernel launch of the process (aesfhe_launch_count): launch census per API call / step
+extern std::atomic<unsigned long long> g_launches;
 
 // every launch is checked: a bad configuration fails the API call that issued it (the C-ABI
 // turns the exception into an error status) instead of surfacing later as wrong data
@@ -50,6 +53,7 @@ inline void launch_validate(F kernel, dim3 grid, dim3 block, size_t lds) {
     static_assert(kernarg_bytes<Args...>() <= kMaxKernarg, "kernel argument block exceeds the kernarg limit");
     const void* fn = reinterpret_cast<const void*>(kernel);
     constexpr size_t ka = kernarg_bytes<Args...>();
+    g_launches.fetch_add(1, std::memory_order_relaxed);
     if (grid.x < 1 || grid.y < 1 || grid.z < 1 || grid.x > 0x7fffffffu || grid.y > 65535u || grid.z > 65535u)
         launch_reject(fn, "grid dimension out of range", grid, block, lds, ka);
     const LaunchLimits& lim = launch_limits(fn);

@@ -117,6 +117,15 @@ class EngineContext:
     def conjugate_many(self, cts):
         return self.engine.conjugate_many(cts)
 
+    def rotate_multi(self, items):
+        """[rotate(ct, s) for ct, s in items] -- different ciphertexts, different steps -- as one
+        heterogeneous batched key switch (include/aesfhe.h aesfhe_galois_multi)"""
+        return self.engine.rotate_multi(items)
+
+    def galois_multi(self, items):
+        """[(ct, g)]: rotations / conjugations by Galois element, batched (aesfhe_galois_multi)"""
+        return self.engine.galois_multi(items)
+
     def rotate_many(self, ct, steps):
         """[rotate(ct, s) for s in steps], hoisted (one ModUp)"""
         return self.engine.rotate_many(ct, steps)

@@ -10,7 +10,7 @@ from mixcol_final import _CoeffCache, gf_basis16, gf_eval, gf_mult_pair
 from shift_rows import row_masks
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT
-from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, pair, rot_many
+from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, pair, rot_many, rot_pair
 
 
 class InvMixColumnsFHE:
@@ -85,7 +85,7 @@ class InvMixColumnsFHE:
         PACKED output; the caller's renorm unpacks it."""
         ctx, enc = self.ctx, self.enc
         steps = [-4 * k * self.stride for k in (1, 2, 3)]
-        rh, rl = pair(ctx, lambda: rot_many(ctx, ct_hi, steps), lambda: rot_many(ctx, ct_lo, steps))
+        rh, rl = rot_pair(ctx, ct_hi, ct_lo, steps)
         fl = RENORM_FLOOR
         gl = fl + LUT2_DEPTH + enc.PACK_DEPTH
         gf = lambda m, hi, lo: enc.pack(*self._gf(m, hi, lo, gl))
@@ -104,7 +104,7 @@ class InvMixColumnsFHE:
         bootstrap): true-FHE decrypt applies the next round's InvShiftRows there first"""
         log = (lambda k, v: debug.__setitem__(k, v)) if debug is not None else (lambda k, v: None)
         steps = [-4 * k * self.stride for k in (1, 2, 3)]  # _col_shift_rowmajor(ct, k), hoisted
-        rh, rl = pair(self.ctx, lambda: rot_many(self.ctx, ct_hi, steps), lambda: rot_many(self.ctx, ct_lo, steps))
+        rh, rl = rot_pair(self.ctx, ct_hi, ct_lo, steps)
         rot = {k: (rh[k - 1], rl[k - 1]) for k in (1, 2, 3)}
         for k in (1, 2, 3):
             log(f"rotc{k}", rot[k])

@@ -44,7 +44,9 @@ EXPORTED = [
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot", "aesfhe_create_keyed", "aesfhe_bootstrap_sparse", "aesfhe_bootstrap_pair_sparse", "aesfhe_renorm_periodic",
     "aesfhe_renorm_single", "aesfhe_renorm_unpack",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_debug_lin_group_plain", "aesfhe_lut_create", "aesfhe_lut_eval", "aesfhe_lut_free",
-    "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled", "aesfhe_set_enc_nonce",
+    "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled", "aesfhe_set_enc_nonce", "aesfhe_launch_count",
+    "aesfhe_galois_multi", "aesfhe_debug_boot_stage_sparse", "aesfhe_debug_sparse_group", "aesfhe_debug_sparse_group_plain",
+    "aesfhe_debug_mono_pack", "aesfhe_debug_mono_split",
 ]
 
 # largest log2(PQ) for 128-bit classical security with a ternary secret (HE standard)
@@ -132,9 +134,17 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_lut_free"] = [vp, _H]
     sig["aesfhe_level_limbs"] = [vp, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")]
     sig["aesfhe_set_enc_nonce"] = [vp, ctypes.c_uint64]
+    sig["aesfhe_launch_count"] = []
+    sig["aesfhe_galois_multi"] = [vp, c_int, _Hp, _Hp, _Hp]
+    sig["aesfhe_debug_boot_stage_sparse"] = [vp, _H, c_int, c_int, _Hp]
+    sig["aesfhe_debug_sparse_group"] = [vp, _H, c_int, c_int, c_int, _Hp]
+    sig["aesfhe_debug_sparse_group_plain"] = [vp, c_int, c_int, c_int, _dp, _dp, _dp, _dp, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")]
+    sig["aesfhe_debug_mono_pack"] = [vp, _H, _H, c_int, _Hp]
+    sig["aesfhe_debug_mono_split"] = [vp, _H, c_int, _Hp, _Hp]
     for name in EXPORTED:
         fn = getattr(L, name)
-        fn.restype = ctypes.c_char_p if name == "aesfhe_last_error" else ctypes.c_int
+        fn.restype = (ctypes.c_char_p if name == "aesfhe_last_error" else ctypes.c_uint64 if name == "aesfhe_launch_count"
+                      else ctypes.c_int)
         fn.argtypes = [vp] if name == "aesfhe_last_error" else sig[name]
     _lib = L
     return L
@@ -509,6 +519,23 @@ class Engine:
         self._ctx.check(self._lib.aesfhe_rotate_hoisted(self._ctx.ptr, ct.handle, n, st, out))
         return [Ciphertext(self._ctx, out[i]) for i in range(n)]
 
+    def galois_multi(self, items) -> List[Ciphertext]:
+        """[(ct, g)] -> [ct through X -> X^g, key-switched] for odd g < 2N (aesfhe_galois_multi):
+        rotations (g = galois_rotate(steps)) and conjugations (g = galois_conj) of different
+        ciphertexts as one batched key switch per level; same results as the separate calls"""
+        items = list(items)
+        n = len(items)
+        if n == 0:
+            return []
+        H = ctypes.c_uint64 * n
+        src, gal, out = H(*[c.handle for c, _ in items]), H(*[int(g) for _, g in items]), H()
+        self._ctx.check(self._lib.aesfhe_galois_multi(self._ctx.ptr, n, src, gal, out))
+        return [Ciphertext(self._ctx, out[i]) for i in range(n)]
+
+    def rotate_multi(self, items) -> List[Ciphertext]:
+        """[(ct, steps)] -> [np.roll(slots(ct), steps)] as one galois_multi"""
+        return self.galois_multi([(c, self.galois_rotate(s)) for c, s in items])
+
     def conjugate_many(self, cts) -> List[Ciphertext]:
         cts = list(cts)
         n = len(cts)
@@ -554,6 +581,30 @@ class Engine:
 
     def debug_boot_stage(self, ct, stage: int):
         return self._new(self._lib.aesfhe_debug_boot_stage, ct.handle, int(stage))
+
+    def debug_boot_stage_sparse(self, ct, stage: int, period: int):
+        return self._new(self._lib.aesfhe_debug_boot_stage_sparse, ct.handle, int(stage), int(period))
+
+    def debug_sparse_group(self, ct, period: int, which: int, pair: bool = False):
+        return self._new(self._lib.aesfhe_debug_sparse_group, ct.handle, int(period), int(which), int(pair))
+
+    def debug_sparse_group_plain(self, period: int, which: int, z: np.ndarray, pair: bool = False):
+        """(host model of debug_sparse_group on the first dn slots of z, tiled; dn, #CtS groups,
+        #groups)"""
+        z = np.asarray(z, np.complex128)
+        re, im = np.ascontiguousarray(z.real), np.ascontiguousarray(z.imag)
+        ore, oim, info = np.zeros(self.slot_count), np.zeros(self.slot_count), np.zeros(3, np.int32)
+        self._ctx.check(self._lib.aesfhe_debug_sparse_group_plain(self._ctx.ptr, int(period), int(which), int(pair), re, im, ore, oim,
+                                                                  info))
+        return ore + 1j * oim, int(info[0]), int(info[1]), int(info[2])
+
+    def debug_mono_pack(self, a, b, period: int):
+        return self._new(self._lib.aesfhe_debug_mono_pack, a.handle, b.handle, int(period))
+
+    def debug_mono_split(self, m, period: int):
+        x, y = ctypes.c_uint64(), ctypes.c_uint64()
+        self._ctx.check(self._lib.aesfhe_debug_mono_split(self._ctx.ptr, m.handle, int(period), ctypes.byref(x), ctypes.byref(y)))
+        return Ciphertext(self._ctx, x.value), Ciphertext(self._ctx, y.value)
 
     def debug_lin_group(self, ct, which: int):
         return self._new(self._lib.aesfhe_debug_lin_group, ct.handle, int(which))
@@ -762,6 +813,11 @@ class Engine:
     @property
     def galois_conj(self) -> int:
         return 2 * self.n - 1
+
+
+def launch_count() -> int:
+    """kernel launches issued by this process so far (aesfhe_launch_count)"""
+    return int(load_library().aesfhe_launch_count())
 
 
 def bootstrap_depth() -> int:

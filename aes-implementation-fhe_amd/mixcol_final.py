@@ -17,7 +17,7 @@ import numpy as np
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT, SplitLUT2, batched, eval_two, joint_bases, powers, std_basis
-from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, can_fork, drop_to, fused_lut, pair, rot_many
+from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, can_fork, drop_to, fused_lut, pair, rot_many, rot_pair
 
 
 class _CoeffCache:
@@ -172,7 +172,7 @@ class MixColFinal:
 
     def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
         steps = [-4 * k * self.stride for k in (1, 2, 3)]  # _col_shift_rowmajor(ct, k), hoisted
-        rh, rl = pair(self.ctx, lambda: rot_many(self.ctx, ct_hi, steps), lambda: rot_many(self.ctx, ct_lo, steps))
+        rh, rl = rot_pair(self.ctx, ct_hi, ct_lo, steps)
         rot = {k: (rh[k - 1], rl[k - 1]) for k in (1, 2, 3)}
         return self.mix_rotated((ct_hi, ct_lo), rot, do_final_bootstrap, debug)
 
@@ -198,7 +198,7 @@ class MixColFinal:
         The bytes are the same either way."""
         ctx, enc = self.ctx, self.enc
         steps = [-4 * k * self.stride for k in (1, 2, 3)]
-        rh, rl = pair(ctx, lambda: rot_many(ctx, ct_hi, steps), lambda: rot_many(ctx, ct_lo, steps))
+        rh, rl = rot_pair(ctx, ct_hi, ct_lo, steps)
         fl = RENORM_FLOOR
         gl = fl + LUT2_DEPTH + enc.PACK_DEPTH
         if os.environ.get("AESFHE_MC_FORM", "xtime") == "xtime":

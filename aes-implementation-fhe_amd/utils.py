@@ -117,6 +117,33 @@ def rot_many(ctx, ct, steps):
     return [ctx.rotate(ct, s) for s in steps]
 
 
+# heterogeneous batched key switch (EngineContext.rotate_multi, DESIGN.md §3.13); "0": the
+# per-half hoisted rotations on the two branch streams (A/B measurements)
+_MULTI = os.environ.get("AESFHE_GALOIS_MULTI", "1") != "0"
+
+
+def rotate_multi(ctx, items):
+    """[ctx.rotate(ct, s) for ct, s in items] -- different ciphertexts, different steps -- as ONE
+    batched engine call when the context has it (same results); steps 0 return the canonical
+    input (its deferred rescale shared with the batch)"""
+    items = list(items)
+    f = getattr(ctx, "rotate_multi", None)
+    if f is not None and _MULTI and len(items) > 1:
+        return f(items)
+    return [ctx.rotate(ct, s) if s else ct for ct, s in items]
+
+
+def rot_pair(ctx, ct_hi, ct_lo, steps):
+    """(rot_many(hi, steps), rot_many(lo, steps)) -- the column shifts of both nibble halves
+    (REF/mixcol_final.py:124-154) -- as one rotate_multi when available, else per half on the
+    two branch streams"""
+    steps = list(steps)
+    if getattr(ctx, "rotate_multi", None) is not None and _MULTI:
+        r = ctx.rotate_multi([(ct_hi, s) for s in steps] + [(ct_lo, s) for s in steps])
+        return r[:len(steps)], r[len(steps):]
+    return pair(ctx, lambda: rot_many(ctx, ct_hi, steps), lambda: rot_many(ctx, ct_lo, steps))
+
+
 def conj_many(ctx, cts):
     """[ctx.conjugate(c) for c in cts], batched like mul_many"""
     cts = list(cts)

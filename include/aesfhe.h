@@ -152,6 +152,15 @@ int aesfhe_conjugate(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
  * the results equal the separate calls bit for bit.  out[i] receives a new handle. */
 int aesfhe_mul_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* a, const aesfhe_handle* b, aesfhe_handle* out);
 int aesfhe_conjugate_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, aesfhe_handle* out);
+/* n automorphisms of possibly DIFFERENT ciphertexts, each with its own Galois element galois[i]
+ * (odd, < 2N): engine.rotate(ct, rotation_key, steps) (REF/engine_context.py:127-132; Galois
+ * element 5^(-steps) mod 2N) and engine.conjugate(ct, conjugation_key) (:103-104; 2N - 1) calls
+ * of one AES step -- the masked row rotations of ShiftRows (REF/shift_rows.py:39-56) and the
+ * column shifts of MixColumns (REF/mixcol_final.py:124-154) for both nibble halves -- as ONE
+ * heterogeneous batched key switch per level: one ModUp per distinct input,
+ * one key-inner-product launch with a key per member, one stacked ModDown.  Same results as the
+ * separate calls; galois[i] = 1 returns a copy. */
+int aesfhe_galois_multi(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, const uint64_t* galois, aesfhe_handle* out);
 /* n rotations of ONE ciphertext, engine.rotate(ct, rotation_key, steps[i])
  * (REF/engine_context.py:127-132; the column shifts of REF/mixcol_final.py:124-154 and the
  * row rotations of REF/shift_rows.py:39-56), hoisted: one ModUp for all of them.  Same
@@ -212,6 +221,23 @@ int aesfhe_debug_bootplan(int log_n, double* err3);
 int aesfhe_debug_sparseplan(int n, int pack, double* err2);
 /* debug: run bootstrap up to a stage (1..11, see engine.hip) and return that ciphertext */
 int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle ct, int stage, aesfhe_handle* out);
+/* Sparse-slot bootstrap stages and groups (tests only, no reference counterpart:
+ * the pieces of the bootstrap that replaces engine.bootstrap at REF/mixcol_final.py:158-162).
+ * debug_boot_stage_sparse: the period-`period` bootstrap stopped after a stage (as
+ * aesfhe_debug_boot_stage; 12 = back on the dense secret BEFORE the trace to the subring, 4 =
+ * after it, 9 = the packed real form w' + conj(w'), 10 = after EvalMod).  debug_sparse_group:
+ * one CoeffToSlot (which < #CtS) / SlotToCoeff group of that plan (pair != 0: the pair-packed
+ * plan; its last index is the lo form of SlotToCoeff's first group); debug_sparse_group_plain:
+ * the same group on the host on the first info3[0] slots (one period of its diagonals), tiled
+ * over all slot_count outputs; info3[1] = CoeffToSlot groups, info3[2] = all groups.  debug_mono_pack: a + X^(N / 4 period) b at level 0;
+ * debug_mono_split: (m + rot_period(m), X^-k (m - rot_period(m))) -- the monomial pair packing
+ * and its split around ONE bootstrap of both messages. */
+int aesfhe_debug_boot_stage_sparse(aesfhe_ctx* ctx, aesfhe_handle ct, int stage, int period, aesfhe_handle* out);
+int aesfhe_debug_sparse_group(aesfhe_ctx* ctx, aesfhe_handle ct, int period, int which, int pair, aesfhe_handle* out);
+int aesfhe_debug_sparse_group_plain(aesfhe_ctx* ctx, int period, int which, int pair, const double* re, const double* im,
+                                    double* out_re, double* out_im, int* info3);
+int aesfhe_debug_mono_pack(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int period, aesfhe_handle* out);
+int aesfhe_debug_mono_split(aesfhe_ctx* ctx, aesfhe_handle m, int period, aesfhe_handle* out_hi, aesfhe_handle* out_lo);
 /* ephemeral sparse secret (NTT form, all limbs) */
 int aesfhe_export_sparse(aesfhe_ctx* ctx, uint32_t* out);
 int aesfhe_debug_lin_group(aesfhe_ctx* ctx, aesfhe_handle ct, int which, aesfhe_handle* out);
@@ -269,6 +295,9 @@ int aesfhe_kernel_stats(aesfhe_ctx* ctx, double* out, int n, int reset);
  * aesfhe_kernel_stats): the numerator of the NTT's VALU roofline */
 int aesfhe_kernel_work(aesfhe_ctx* ctx, double* out, int n);
 int aesfhe_reset_counters(aesfhe_ctx* ctx);
+/* kernel launches issued by this process so far (all contexts): the launch census of
+ * tools/launch_census.py and bench.py's launches-per-encrypt (MI355X-side tooling) */
+uint64_t aesfhe_launch_count(void);
 
 #ifdef __cplusplus
 }

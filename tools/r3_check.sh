@@ -15,4 +15,5 @@ echo bench done
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --steps 2 --warmup 1 \
     --no-cpu-baseline --batch-states 0 --true-fhe-steps 0 > $O/bench_under_rocprof.json 2> $O/trace.err
 find $O/trace -name '*kernel_trace.csv' -delete
+timeout -k 10 300 python3 tools/launch_census.py > $O/launch_census.json
 echo done
