@@ -335,6 +335,10 @@ public:
         sync();
     }
     u64 conj_galois() const { return 2ull * hp_.n - 1; }
+    // key tag of sigma_g(s)^2 -> s (g odd, < 2N): the third polynomial of a deferred tensor read
+    // through X -> X^g (galois_lazy)
+    u64 tag_sq(u64 g) const { return 4ull * hp_.n + g; }
+    bool is_tag_sq(u64 t) const { return t > 4ull * hp_.n && t < 6ull * hp_.n; }
     u64 rot_galois(int steps) const {
         const long s = slot_count();
         long k = ((-(long)steps) % s + s) % s;  // np.roll(slots, steps) = left rotation by -steps
@@ -398,6 +402,11 @@ public:
             launch_square(S(), T_, sp, d_s_, nks, nks, qmap());
         } else if (g == tag_s2d()) {  // sparse s_sp -> dense s
             launch_copy_rows(S(), T_, sp, sparse_secret(), nks);
+        } else if (is_tag_sq(g)) {    // sigma_g'(s)^2 -> s: the automorphism of a 3-polynomial tensor
+            u32* s2 = tmp(nks);
+            launch_square(S(), T_, s2, d_s_, nks, nks, qmap());
+            launch_automorph(S(), T_, sp, s2, g - 4ull * n, nks);
+            untmp(s2, nks);
         } else {
             launch_automorph(S(), T_, sp, d_s_, g, nks);
         }
@@ -501,6 +510,28 @@ public:
         Ct out = rescale(top);
         release(top);
         cnt_[C_ENC]++;
+        return out;
+    }
+
+    // B <= kEncMax messages (NTT form, member m at m + b m_ms words, nl(f) + 1 limbs each, scale
+    // delta_f q_{nl(f)}) encrypted together: ONE sampling launch for every v, e0, e1, ONE NTT of
+    // all of them, ONE combine, ONE rescale of the stacked result (nb = B) -- the same residues as
+    // B encrypt_ntt calls (same PRNG streams, same arithmetic), 8 launches instead of 14 B
+    Ct encrypt_many(const u32* m, int B, size_t m_ms, int level = -1) {
+        if (B < 1 || B > kEncMax) throw std::runtime_error("encrypt_many: 1..4 messages");
+        const int f = level < 0 ? hp_.fresh : level;
+        const int nq = hp_.nl(f) + 1;
+        u32* vee = tmp((size_t)B * 3 * nq);
+        EncCtrs ec;
+        for (int b = 0; b < B; ++b) ec.ctr[b] = enc_ctr_++;
+        launch_sample_enc(S(), T_, vee, nq, B, enc_key(), ec);
+        ntt(vee, B * 3 * nq, nq, qmap());
+        Ct top = alloc_ct(f + 1, 2 * B, B);
+        launch_enc_combine(S(), T_, top.data, vee, m, m_ms, d_pk_, hp_.n_q, nq, B);
+        untmp(vee, (size_t)B * 3 * nq);
+        Ct out = rescale(top);
+        release(top);
+        cnt_[C_ENC] += B;
         return out;
     }
 
@@ -1471,24 +1502,78 @@ public:
         }
         struct Prep {
             Ct a, b, x, y;
-            bool oa = false, ob = false, fa = false, fb = false;
         };
         std::vector<Prep> pr(n);
+        std::vector<Ct> owned;  // normalised inputs and level-aligned copies, released after the tensors
         for (int i = 0; i < n; ++i) {
             Prep& P = pr[i];
             P.a = normalize(*A[i]);
+            if (P.a.data != A[i]->data) owned.push_back(P.a);
             P.b = B[i]->data == A[i]->data ? P.a : normalize(*B[i]);
-            P.oa = P.a.data != A[i]->data;
-            P.ob = P.b.data != B[i]->data && P.b.data != P.a.data;
-            auto xy = align(P.a, P.b, P.fa, P.fb, true);
-            P.x = xy.first, P.y = xy.second;
+            if (P.b.data != B[i]->data && P.b.data != P.a.data) owned.push_back(P.b);
         }
-        auto drop = [&](Prep& P) {
-            if (P.fa) release(P.x);
-            if (P.fb && P.y.data != P.x.data) release(P.y);
-            if (P.oa) release(P.a);
-            if (P.ob) release(P.b);
+        // level alignment of every pair (as align(..., for_mul)), the exact-scale drops of inputs at one
+        // (level, owed rescales) to one target batched: ONE copy-and-scale launch and ONE limb drop
+        // for the group (convert_many) instead of one convert each
+        struct Need {
+            const Ct* src;
+            int t;
+            Ct res;
         };
+        std::vector<Need> needs;
+        auto want = [&](const Ct& c, int t) -> int {
+            if (c.level == t && !c.pend) return -1;
+            for (size_t j = 0; j < needs.size(); ++j)
+                if (needs[j].src->data == c.data && needs[j].t == t) return (int)j;
+            needs.push_back({&c, t, Ct{}});
+            return (int)needs.size() - 1;
+        };
+        std::vector<int> wa(n), wb(n);
+        for (int i = 0; i < n; ++i) {
+            int lv = std::min(pr[i].a.level - pr[i].a.pend, pr[i].b.level - pr[i].b.pend);
+            if (!hp_.homogeneous(lv)) --lv;
+            wa[i] = want(pr[i].a, lv);
+            wb[i] = want(pr[i].b, lv);
+        }
+        std::vector<bool> conv_done(needs.size(), false);
+        for (size_t j = 0; j < needs.size(); ++j) {
+            if (conv_done[j]) continue;
+            const Ct& c = *needs[j].src;
+            std::vector<size_t> grp{j};
+            for (size_t k = j + 1; k < needs.size() && (int)grp.size() < kMaxMembers; ++k) {
+                const Ct& d = *needs[k].src;
+                if (!conv_done[k] && needs[k].t == needs[j].t && d.level == c.level && d.pend == c.pend && d.npoly == c.npoly &&
+                    d.nb == 1 && c.nb == 1 && d.ntt && c.ntt)
+                    grp.push_back(k);
+            }
+            for (size_t k : grp) conv_done[k] = true;
+            if (grp.size() == 1) {
+                needs[j].res = level_down(c, needs[j].t);
+                owned.push_back(needs[j].res);
+                continue;
+            }
+            std::vector<const Ct*> srcs;
+            for (size_t k : grp) srcs.push_back(needs[k].src);
+            Ct st;
+            if (!convert_many(srcs, needs[j].t, 0, st)) {  // no batched form: one convert each
+                for (size_t k : grp) {
+                    needs[k].res = level_down(*needs[k].src, needs[k].t);
+                    owned.push_back(needs[k].res);
+                }
+                continue;
+            }
+            owned.push_back(st);
+            const size_t per = st.words / grp.size();
+            for (size_t m = 0; m < grp.size(); ++m) {
+                Ct v = st;
+                v.data = st.data + m * per, v.words = per, v.npoly = st.npoly / (int)grp.size(), v.nb = 1;
+                needs[grp[m]].res = v;
+            }
+        }
+        for (int i = 0; i < n; ++i) {
+            pr[i].x = wa[i] < 0 ? pr[i].a : needs[wa[i]].res;
+            pr[i].y = wb[i] < 0 ? pr[i].b : needs[wb[i]].res;
+        }
         std::vector<bool> done(n, false);
         for (int i = 0; i < n; ++i) {
             if (done[i]) continue;
@@ -1502,7 +1587,6 @@ public:
             for (int m = 0; m < g; ++m) tp.a[m] = pr[grp[m]].x.data, tp.b[m] = pr[grp[m]].y.data;
             launch_tensor_ptrs(S(), T_, d.data, tp, g, nl, qmap());
             cnt_[C_MUL] += g;
-            for (int m = 0; m < g; ++m) drop(pr[grp[m]]);
             const int chunk = ks_chunk(L);
             for (int m0 = 0; m0 < g; m0 += chunk) {
                 const int c = std::min(chunk, g - m0);
@@ -1521,7 +1605,42 @@ public:
             }
             release(d);
         }
+        for (const Ct& c : owned) release(c);  // stream-ordered: the tensors above were queued first
         return out;
+    }
+    // convert(c, t, p) of several ciphertexts at one (data level, owed rescales, polys): ONE
+    // copy-and-scale launch into a stack and ONE limb drop for all of them.  st: the stack (nb =
+    // members, member m = S[m] converted, the same residues as convert(S[m], t, p)).  false when
+    // the conversion needs the relinearise-first path of convert()
+    bool convert_many(const std::vector<const Ct*>& Sv, int t, int p, Ct& st) {
+        const Ct& c = *Sv[0];
+        const int m = (int)Sv.size();
+        if (m > kMaxMembers || p < 0 || t > c.level || t - p > c.level - c.pend) return false;
+        const int n = hp_.n, nb = hp_.nl(t), na = hp_.nl(c.level);
+        int k = 0;
+        double ratio = raw_scale(t, p) / raw_scale(c.level, c.pend);
+        const double need = t > hp_.L1 ? 2251799813685248.0 : 16777216.0;  // as convert()
+        while (ratio < need && nb + k < na) ratio *= (double)hp_.mod[nb + k], ++k;
+        if (!(ratio >= 0.999999 && ratio < 9.0e18)) return false;
+        if (pm(c) == 3 && k > 0 && raw_scale(t, p) < 1.0e15) return false;
+        const int nk = nb + k, np = c.npoly;
+        u32* mid = tmp((size_t)m * np * nk);
+        const i64 cst = std::llround(ratio);
+        std::vector<u32> r(nk);
+        for (int i = 0; i < nk; ++i) r[i] = mod_i64(cst, hp_.mod[i]);
+        MemberPtrs mp;
+        for (int i = 0; i < m; ++i) mp.src[i] = Sv[i]->data;
+        launch_mul_const_half_members(S(), T_, mid, mp, m, const_half(r, r), np * nk, nk, qmap(), na);
+        st = Ct{};
+        st.level = t, st.npoly = m * np, st.nb = m, st.pend = p, st.lazy = c.lazy || p > 0, st.zero = false;
+        st.words = (size_t)m * np * nb * n;
+        if (k == 0) {
+            st.data = mid;
+        } else {
+            st.data = drop_limbs(mid, m * np, nk, k);
+            untmp(mid, (size_t)m * np * nk);
+        }
+        return true;
     }
     // members of a stacked canonical ciphertext -> separate ciphertexts out[idx[m]]
     void unstack(const Ct& o, Ct* out, const int* idx) {
@@ -1733,7 +1852,55 @@ public:
     void count_rot() { cnt_[C_ROT]++; }
     std::vector<Ct> conjugate_many(const std::vector<const Ct*>& C) {
         cnt_[C_CONJ] += C.size();
-        return galois_many(C, conj_galois());
+        // deferred inputs (a LUT sum owing its relinearisation and rescales) are conjugated as they
+        // are (galois_lazy), the rest batched as before
+        std::vector<Ct> out(C.size());
+        std::vector<const Ct*> canon_in;
+        std::vector<size_t> idx;
+        for (size_t i = 0; i < C.size(); ++i) {
+            if (lazy_galois_ok(*C[i])) out[i] = galois_lazy(*C[i], conj_galois());
+            else canon_in.push_back(C[i]), idx.push_back(i);
+        }
+        if (!canon_in.empty()) {
+            std::vector<Ct> r = galois_many(canon_in, conj_galois());
+            for (size_t j = 0; j < idx.size(); ++j) out[idx[j]] = r[j];
+        }
+        return out;
+    }
+
+    // ------------------------------------------------------------------ automorphism of a deferred tensor
+    // X -> X^g of a tensor that still owes work, WITHOUT resolving it: c0' = sigma(d0), plus the key
+    // switch of sigma(d1) (sigma(s) -> s) and, for a 3-polynomial tensor, of sigma(d2) with the key
+    // sigma(s)^2 -> s (tag_sq), both inner products summed in Q*P and ONE ModDown by P.  The owed
+    // rescales stay owed (same data level, pend, raw scale): the caller's sum S1 + conj(S2) of two
+    // deferred LUT tensors is then one addition at the same (level, pend), and a renorm reads it
+    // raw -- no relinearisation, no rescale of either part (the conjugate-split LUTs of XOR4, the GF
+    // multipliers and SubBytes).  Key-switching noise is added at the raw scale
+    // S(l, pend) >= Delta^2 q, far below the message.
+    bool lazy_galois_ok(const Ct& c) const {
+        if (!lazy_galois_ || !c.ntt || c.zero || c.nb != 1) return false;
+        return pm(c) == 3 ? c.lazy : (pm(c) == 2 && c.pend > 0);  // an explicit 3-polynomial product stays an error
+    }
+    bool lazy_galois_ = std::getenv("AESFHE_LAZY_GALOIS") == nullptr || std::getenv("AESFHE_LAZY_GALOIS")[0] != '0';
+    Ct galois_lazy(const Ct& c, u64 g) {
+        const int l = c.level, nl = hp_.nl(l), np = hp_.n_p, ne = nl + np, n = hp_.n, k = pm(c);
+        u32* perm = tmp((size_t)k * nl);
+        launch_automorph(S(), T_, perm, c.data, g, k * nl);
+        // d1 (and d2) of the permuted tensor are consecutive rows: ONE ModUp for both sources
+        const int nsrc = k - 1;
+        u32* ext = modup(perm + (size_t)nl * n, l, nsrc, (size_t)nl * n);
+        u32* acc = tmp(2 * (size_t)ne);
+        key_inner(acc, ext, perm + (size_t)nl * n, ksk(g), l, 0);
+        if (nsrc == 2)
+            key_inner(acc, ext + (size_t)ext_rows(l) * n, perm + (size_t)2 * nl * n, ksk(tag_sq(g)), l, 0, 1, 0, KsFold{}, true);
+        untmp(ext, (size_t)nsrc * ext_rows(l));
+        Ct o = moddown(acc, l, perm, nullptr);
+        untmp(acc, 2 * (size_t)ne);
+        untmp(perm, (size_t)k * nl);
+        o.pend = c.pend;
+        o.lazy = c.pend > 0;
+        cnt_[C_KS] += nsrc;
+        return o;
     }
 
     Ct relinearize(const Ct& c_in) {
@@ -1805,6 +1972,7 @@ public:
     }
     Ct conjugate(const Ct& c) {
         cnt_[C_CONJ]++;
+        if (lazy_galois_ok(c)) return galois_lazy(c, conj_galois());
         return galois(c, conj_galois());
     }
 
@@ -1945,6 +2113,12 @@ public:
         // channel (k_snap_slots' unpack gathers both outputs from channel 0; single has one output)
         const int n_in = (unpack || single) ? 1 : 2, n_out = single ? 1 : 2;
         kd[1] = 0;
+        // raw decryption of the inputs: ONE launch forms c0 + c1 s (+ c2 s^2) on the CRT limbs of
+        // both, one inverse NTT when their limb counts agree
+        DecRaw dr;
+        Ct dc[2];
+        bool down[2] = {false, false};
+        bool need_s2 = false;
         for (int w = 0; w < n_in; ++w) {
             Ct c = ensure_ntt(ct(in[w]));
             bool own = c.data != ct(in[w]).data;
@@ -1955,17 +2129,21 @@ public:
                 c = nc, own = nc.data != ct(in[w]).data;
                 kd[w] = crt_limbs(c);
             }
-            const int nl = hp_.nl(c.level);
-            u32* xw = x + (size_t)w * 4 * n;
-            launch_copy_rows(S(), T_, xw, c.data, kd[w]);
-            for (int p = 1; p < c.npoly; ++p)
-                launch_fma_poly(S(), T_, xw, xw, c.data + (size_t)p * nl * n, p == 2 ? s_sq4() : d_s_, kd[w], kd[w], qmap());
-            intt(xw, kd[w], kd[w], qmap());
+            dc[w] = c, down[w] = own;
+            dr.ct[w] = c.data, dr.npoly[w] = c.npoly, dr.nlc[w] = hp_.nl(c.level), dr.kd[w] = kd[w];
+            need_s2 = need_s2 || c.npoly == 3;
             cc[w] = crt_consts(kd[w]);
             isc[w] = 1.0 / (c.level >= 0 ? raw_scale(c.level, c.pend) : 1.0);
-            if (own) release(c);
             cnt_[C_DEC]++;
         }
+        launch_dec_raw(S(), T_, x, dr, n_in, d_s_, need_s2 ? s_sq4() : d_s_);
+        if (n_in == 2 && kd[0] == kd[1]) {
+            intt(x, x, 2 * kd[0], RowMap{kd[0], 4, 4, 0, 0}, qmap());
+        } else {
+            for (int w = 0; w < n_in; ++w) intt(x + (size_t)w * 4 * n, kd[w], kd[w], qmap());
+        }
+        for (int w = 0; w < n_in; ++w)
+            if (down[w]) release(dc[w]);
         const int f = level < 0 ? hp_.fresh : level, nq = hp_.nl(f) + 1;
         const double enc_scale = hp_.delta[f] * (double)hp_.mod[hp_.nl(f)];
         u32* m = tmp(2 * (size_t)nq);
@@ -1990,9 +2168,18 @@ public:
             launch_encode_untwist(S(), T_, m, w, enc_scale, nq, n_out);
         }
         ntt(m, (single ? 1 : 2) * nq, nq, qmap());
-        Ct a = encrypt_ntt(m, f);
-        *oh = put_ct(a);
-        if (!single) *ol = put_ct(encrypt_ntt(m + (size_t)nq * n, f));
+        Ct enc = encrypt_many(m, n_out, (size_t)nq * n, f);  // both re-encryptions in one set of launches
+        if (n_out == 1) {
+            enc.nb = 1;
+            *oh = put_ct(enc);
+        } else {
+            Ct parts[2];
+            const int idx[2] = {0, 1};
+            unstack(enc, parts, idx);
+            release(enc);
+            *oh = put_ct(parts[0]);
+            *ol = put_ct(parts[1]);
+        }
         untmp(m, 2 * (size_t)nq);
         untmp(x, 8);
     }
@@ -3652,7 +3839,7 @@ int aesfhe_rescale(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) {
 }
 int aesfhe_level_down(aesfhe_ctx* ctx, aesfhe_handle c, int level, aesfhe_handle* out) { CT_OP(e.level_down(e.canon(c), level)) }
 int aesfhe_rotate(aesfhe_ctx* ctx, aesfhe_handle c, int steps, aesfhe_handle* out) { CT_OP(e.rotate(e.canon(c), steps)) }
-int aesfhe_conjugate(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.conjugate(e.canon(c))) }
+int aesfhe_conjugate(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle* out) { CT_OP(e.conjugate(e.ct(c))) }
 int aesfhe_rotate_hoisted(aesfhe_ctx* ctx, aesfhe_handle c, int n, const int* steps, aesfhe_handle* out) {
     API_BEGIN Engine& e = *ctx->eng;
     if (n < 0 || (n > 0 && (!steps || !out))) throw std::runtime_error("rotate_hoisted: bad arguments");
@@ -3687,7 +3874,7 @@ int aesfhe_conjugate_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, aesfh
     API_BEGIN Engine& e = *ctx->eng;
     if (n < 0 || (n > 0 && (!in || !out))) throw std::runtime_error("conjugate_many: bad arguments");
     std::vector<const Ct*> C(n);
-    for (int i = 0; i < n; ++i) C[i] = &e.canon(in[i]);
+    for (int i = 0; i < n; ++i) C[i] = &e.ct(in[i]);  // deferred work resolved inside, where needed
     std::vector<Ct> r = e.conjugate_many(C);
     for (int i = 0; i < n; ++i) out[i] = e.put_ct(r[i]);
     API_END
@@ -3867,6 +4054,14 @@ int aesfhe_kernel_work(aesfhe_ctx* ctx, double* out, int n) {
     API_END
 }
 uint64_t aesfhe_launch_count(void) { return g_launches.load(std::memory_order_relaxed); }
+int aesfhe_alg_bytes(double* bytes, uint64_t* launches, int n) {
+    if (!bytes || !launches) return -2;
+    for (int k = 0; k < n && k < KID_N; ++k) {
+        bytes[k] = (double)g_alg_bytes[k].load(std::memory_order_relaxed);
+        launches[k] = g_alg_launches[k].load(std::memory_order_relaxed);
+    }
+    return 0;
+}
 int aesfhe_reset_counters(aesfhe_ctx* ctx) {
     API_BEGIN ctx->eng->reset_counters();
     API_END

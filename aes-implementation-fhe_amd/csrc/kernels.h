@@ -147,6 +147,10 @@ struct LimbConsts {
 // src_nl > 0: `in` holds polys of src_nl >= nl limbs (first nl read), e.g. a level drop
 void launch_mul_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const LimbConsts& cst, int rows, int nl, LimbMap map,
                            int src_nl = 0);
+// the same for n members read from separate ciphertexts (mp.src[m], polys of src_nl limbs) into one
+// stacked output [m][rows] (mp.dst unused): the copy-and-scale step of n exact-scale level drops
+void launch_mul_const_half_members(hipStream_t st, const DevTables& T, u32* out, const MemberPtrs& mp, int n, const LimbConsts& cst,
+                                   int rows, int nl, LimbMap map, int src_nl);
 // out = a +- b on the first `common` rows, then the longer operand alone (+-b when b is longer)
 void launch_addsub_tail(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int common, int rows, bool a_longer,
                         bool sub, int nl, LimbMap map);
@@ -270,6 +274,26 @@ struct LinMacArgs {
     size_t ext_ms = 0, d_ms = 0;
 };
 void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int nl, int ne, LimbMap map);
+
+// --- fused public-key encryption of up to kEncMax messages (renorm re-encryption) -------
+// one launch samples v, e0, e1 of every member (member m: streams stream_id(6|7|8, 0, ctr[m]),
+// the same samples as launch_sample_small), one combines c0 = (e0 + msg) + pk0 v, c1 = e1 + pk1 v
+constexpr int kEncMax = 4;
+struct EncCtrs {
+    u64 ctr[kEncMax] = {};
+};
+// out: [m][3][nl] (v, e0, e1 residues, coefficient form)
+void launch_sample_enc(hipStream_t st, const DevTables& T, u32* out, int nl, int nm, const PrngKey& key, const EncCtrs& ctr);
+// top: [m][2][nl]; vee: [m][3][nl] NTT form; msg: member m at msg + m msg_ms words; pk: [2][pk_rows][N]
+void launch_enc_combine(hipStream_t st, const DevTables& T, u32* top, const u32* vee, const u32* msg, size_t msg_ms, const u32* pk,
+                        int pk_rows, int nl, int nm);
+// raw decryption of up to 2 channels on their first kd[c] limbs: x[c][t] = c0 + c1 s (+ c2 s^2),
+// x: [2][4][N]; channel c reads ct[c] (npoly[c] polys of nlc[c] limbs); s, s2: NTT rows of s, s^2
+struct DecRaw {
+    const u32* ct[2] = {};
+    int npoly[2] = {}, nlc[2] = {}, kd[2] = {};
+};
+void launch_dec_raw(hipStream_t st, const DevTables& T, u32* x, const DecRaw& dr, int nch, const u32* s, const u32* s2);
 
 // --- sampling --------------------------------------------------------
 // kind: 0 ternary, 1 centred binomial (eta = 21); writes value mod prime into nl rows

@@ -127,6 +127,17 @@ __global__ void k_mul_const_half(u32* out, const u32* in, LimbConsts cst, int nl
     const size_t sidx = ((size_t)((row / nl) * src_nl + limb) << logn) + k;
     out[idx] = shoup_mul(in[sidx], c[0], c[1], P.q);
 }
+__global__ void k_mul_const_half_members(u32* out, MemberPtrs mp, LimbConsts cst, int rows, int nl, int src_nl, LimbMap map,
+                                         const PrimeConst* pc, int logn) {
+    const int m = blockIdx.z;
+    const u32* in = mp.src[m];
+    out += ((size_t)m * rows) << logn;
+    EW_PROLOGUE
+    const int hi = (int)(k >> (logn - 1));
+    const u32* c = cst.v + 4 * limb + 2 * hi;
+    const size_t sidx = ((size_t)((row / nl) * src_nl + limb) << logn) + k;
+    out[idx] = shoup_mul(in[sidx], c[0], c[1], P.q);
+}
 __global__ void k_add_const_half(u32* out, const u32* in, LimbConsts cst, int nl, LimbMap map, const PrimeConst* pc, int logn) {
     EW_PROLOGUE
     const int hi = (int)(k >> (logn - 1));
@@ -437,6 +448,46 @@ __global__ void k_sample_small(u32* out, int nl, LimbMap map, PrngKey key, u64 s
         out[((size_t)l << logn) + k] = v >= 0 ? (u32)v : q - (u32)(-v);
     }
 }
+// v (ternary), e0, e1 (binomial) of nm encryptions: grid (N / kBlock, 3 nm), row block y = 3 m + w
+__global__ void k_sample_enc(u32* out, int nl, PrngKey key, EncCtrs ctr, const PrimeConst* pc, int logn) {
+    const int y = blockIdx.y, m = y / 3, w = y - 3 * m;
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const u64 stream = ((u64)(6 + w) << 56) | ctr.ctr[m];  // stream_id(6 + w, 0, ctr)
+    const u64 r = chacha_u64(key, stream, k);
+    const int v = w == 0 ? (int)(r % 3) - 1 : __popcll(r & 0x1FFFFFull) - __popcll((r >> 21) & 0x1FFFFFull);
+    u32* o = out + ((size_t)y * nl << logn);
+    for (int l = 0; l < nl; ++l) {
+        const u32 q = pc[l].q;
+        o[((size_t)l << logn) + k] = v >= 0 ? (u32)v : q - (u32)(-v);
+    }
+}
+// c0 = (e0 + msg) + pk0 v, c1 = e1 + pk1 v (the add / fma sequence of Engine::encrypt_ntt, bit for bit)
+__global__ void k_enc_combine(u32* top, const u32* vee, const u32* msg, size_t msg_ms, const u32* pk, int pk_rows, int nl,
+                              const PrimeConst* pc, int logn) {
+    const int y = blockIdx.y, m = y / nl, l = y - m * nl;
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const PrimeConst P = pc[l];
+    const size_t row = (size_t)l << logn, pl = (size_t)nl << logn;
+    const u32* V = vee + (size_t)m * 3 * pl;
+    const u32 v = V[row + k], e0 = V[pl + row + k], e1 = V[2 * pl + row + k];
+    const u32 mv = msg[m * msg_ms + row + k];
+    u32* o = top + (size_t)m * 2 * pl;
+    o[row + k] = add_mod(add_mod(e0, mv, P.q), barrett_mul(pk[row + k], v, P.q, P.mu), P.q);
+    o[pl + row + k] = add_mod(e1, barrett_mul(pk[((size_t)pk_rows << logn) + row + k], v, P.q, P.mu), P.q);
+}
+// raw decryption rows of up to two channels (renorm): x[c][t] = c0 + c1 s + c2 s^2 on t < kd[c]
+__global__ void k_dec_raw(u32* x, DecRaw dr, const u32* s, const u32* s2, const PrimeConst* pc, int logn) {
+    const int c = blockIdx.y >> 2, t = blockIdx.y & 3;
+    if (t >= dr.kd[c]) return;
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const PrimeConst P = pc[t];
+    const size_t row = ((size_t)t << logn) + k, pl = (size_t)dr.nlc[c] << logn;
+    const u32* ct = dr.ct[c];
+    u32 v = ct[row];
+    v = add_mod(v, barrett_mul(ct[pl + row], s[row], P.q, P.mu), P.q);
+    if (dr.npoly[c] == 3) v = add_mod(v, barrett_mul(ct[2 * pl + row], s2[row], P.q, P.mu), P.q);
+    x[((size_t)(c * 4 + t) << logn) + k] = v;
+}
 __global__ void k_sample_uniform(u32* out, int nl, LimbMap map, PrngKey key, u64 stream, const PrimeConst* pc, int logn) {
     const int l = blockIdx.y;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
@@ -466,6 +517,8 @@ inline dim3 ew_grid(int logn, int rows) { return dim3((1u << logn) / kBlock, row
 thread_local KernelProfiler* g_prof = nullptr;
 void prof_set(KernelProfiler* p) { g_prof = p; }
 std::atomic<unsigned long long> g_launches{0};
+std::atomic<unsigned long long> g_alg_bytes[KID_N] = {};
+std::atomic<unsigned long long> g_alg_launches[KID_N] = {};
 
 // ======================================================================================
 // launch validation (launch.h launch_validate): per-kernel limits, queried once
@@ -865,6 +918,12 @@ void launch_mul_const_half(hipStream_t st, const DevTables& T, u32* out, const u
     prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows), k_mul_const_half, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, cst, nl,
                 src_nl > 0 ? src_nl : nl, map, T.pc, T.logn);
 }
+void launch_mul_const_half_members(hipStream_t st, const DevTables& T, u32* out, const MemberPtrs& mp, int n, const LimbConsts& cst,
+                                   int rows, int nl, LimbMap map, int src_nl) {
+    if (n < 1 || n > kMaxMembers) throw std::runtime_error("launch_mul_const_half_members: 1..8 members");
+    prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows * n), k_mul_const_half_members, dim3((1u << T.logn) / kBlock, rows, n), dim3(kBlock), 0,
+                st, out, mp, cst, rows, nl, src_nl, map, T.pc, T.logn);
+}
 void launch_addsub_tail(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int common, int rows, bool a_longer,
                         bool sub, int nl, LimbMap map) {
     prof_launch(KID_ELEMENTWISE, EW_BYTES(3.0 * common + 2.0 * (rows - common)), k_addsub_tail, ew_grid(T.logn, rows), dim3(kBlock), 0,
@@ -1127,6 +1186,26 @@ void launch_automorph_multi(hipStream_t st, const DevTables& T, u32* out, size_t
 void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, const PrngKey& key, u64 stream, int kind) {
     prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_small, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, nl, map, key, stream, kind, T.pc,
                        T.logn);
+}
+void launch_sample_enc(hipStream_t st, const DevTables& T, u32* out, int nl, int nm, const PrngKey& key, const EncCtrs& ctr) {
+    if (nm < 1 || nm > kEncMax) throw std::runtime_error("launch_sample_enc: 1..4 encryptions");
+    prof_launch(KID_SAMPLE, words(3.0 * nm * nl * (1u << T.logn)), k_sample_enc, dim3((1u << T.logn) / kBlock, 3 * nm), dim3(kBlock), 0, st,
+                out, nl, key, ctr, T.pc, T.logn);
+}
+void launch_enc_combine(hipStream_t st, const DevTables& T, u32* top, const u32* vee, const u32* msg, size_t msg_ms, const u32* pk,
+                        int pk_rows, int nl, int nm) {
+    prof_launch(KID_ELEMENTWISE, words((3.0 + 1.0 + 2.0 + 2.0) * nm * nl * (1u << T.logn)), k_enc_combine, ew_grid(T.logn, nm * nl),
+                dim3(kBlock), 0, st, top, vee, msg, msg_ms, pk, pk_rows, nl, T.pc, T.logn);
+}
+void launch_dec_raw(hipStream_t st, const DevTables& T, u32* x, const DecRaw& dr, int nch, const u32* s, const u32* s2) {
+    if (nch < 1 || nch > 2) throw std::runtime_error("launch_dec_raw: 1 or 2 channels");
+    double w = 0;
+    for (int c = 0; c < nch; ++c) {
+        if (dr.kd[c] < 1 || dr.kd[c] > 4 || dr.kd[c] > dr.nlc[c]) throw std::runtime_error("launch_dec_raw: bad limb count");
+        w += (2.0 * dr.npoly[c] + 1.0) * dr.kd[c];
+    }
+    prof_launch(KID_ELEMENTWISE, words(w * (1u << T.logn)), k_dec_raw, dim3((1u << T.logn) / kBlock, 4 * nch), dim3(kBlock), 0, st, x, dr, s,
+                s2, T.pc, T.logn);
 }
 void launch_sample_uniform(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, const PrngKey& key, u64 stream) {
     prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_uniform, ew_grid(T.logn, nl), dim3(kBlock), 0, st, out, nl, map, key, stream, T.pc, T.logn);

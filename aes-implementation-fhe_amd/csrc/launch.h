@@ -18,6 +18,15 @@ extern thread_local KernelProfiler* g_prof;
 #include <atomic>
 // every kernel launch of the process (aesfhe_launch_count): launch census per API call / step
 extern std::atomic<unsigned long long> g_launches;
+// algorithmic bytes (rounded to whole bytes) and launches of EVERY launch per kernel id, timed or
+// not (aesfhe_alg_bytes): the numerator of bench.py's whole-step roofline
+extern std::atomic<unsigned long long> g_alg_bytes[KID_N];
+extern std::atomic<unsigned long long> g_alg_launches[KID_N];
+inline void alg_account(int kid, double bytes) {
+    if (kid < 0 || kid >= KID_N) return;
+    g_alg_bytes[kid].fetch_add((unsigned long long)(bytes + 0.5), std::memory_order_relaxed);
+    g_alg_launches[kid].fetch_add(1, std::memory_order_relaxed);
+}
 
 // every launch is checked: a bad configuration fails the API call that issued it (the C-ABI
 // turns the exception into an error status) instead of surfacing later as wrong data
@@ -65,6 +74,7 @@ inline void launch_validate(F kernel, dim3 grid, dim3 block, size_t lds) {
 template <typename F, typename... Args>
 inline void prof_launch(int kid, double bytes, F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st, Args... args) {
     launch_validate<F, Args...>(kernel, grid, block, lds);
+    alg_account(kid, bytes);
     KernelProfiler* p = g_prof;
     if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) {
         hipEvent_t a = p->get(), b = p->get();
@@ -82,6 +92,7 @@ template <typename F, typename... Args>
 inline void prof_launch_tsw(int kid, double bytes, double work, F kernel, dim3 grid, dim3 block, size_t lds, hipStream_t st,
                             Args... args) {
     launch_validate<F, Args..., unsigned long long*>(kernel, grid, block, lds);
+    alg_account(kid, bytes);
     KernelProfiler* p = g_prof;
     unsigned long long* ts = nullptr;
     if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) {

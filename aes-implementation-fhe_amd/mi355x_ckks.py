@@ -46,7 +46,7 @@ EXPORTED = [
     "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_debug_lin_group_plain", "aesfhe_lut_create", "aesfhe_lut_eval", "aesfhe_lut_free",
     "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled", "aesfhe_set_enc_nonce", "aesfhe_launch_count",
     "aesfhe_galois_multi", "aesfhe_debug_boot_stage_sparse", "aesfhe_debug_sparse_group", "aesfhe_debug_sparse_group_plain",
-    "aesfhe_debug_mono_pack", "aesfhe_debug_mono_split",
+    "aesfhe_debug_mono_pack", "aesfhe_debug_mono_split", "aesfhe_alg_bytes",
 ]
 
 # largest log2(PQ) for 128-bit classical security with a ternary secret (HE standard)
@@ -135,6 +135,7 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_level_limbs"] = [vp, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")]
     sig["aesfhe_set_enc_nonce"] = [vp, ctypes.c_uint64]
     sig["aesfhe_launch_count"] = []
+    sig["aesfhe_alg_bytes"] = [_dp, np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS"), c_int]
     sig["aesfhe_galois_multi"] = [vp, c_int, _Hp, _Hp, _Hp]
     sig["aesfhe_debug_boot_stage_sparse"] = [vp, _H, c_int, c_int, _Hp]
     sig["aesfhe_debug_sparse_group"] = [vp, _H, c_int, c_int, c_int, _Hp]
@@ -202,9 +203,10 @@ class _Handle:
 
 
 class Ciphertext(_Handle):
-    """Device-resident RNS-CKKS ciphertext (opaque handle)."""
+    """Device-resident RNS-CKKS ciphertext (opaque handle).  `layout`: the AES slot layout
+    (state_encoder.SlotLayout) the state encoder tagged it with, unset for plain ciphertexts"""
 
-    __slots__ = ()
+    __slots__ = ("layout",)
 
     @property
     def level(self) -> int:
@@ -818,6 +820,14 @@ class Engine:
 def launch_count() -> int:
     """kernel launches issued by this process so far (aesfhe_launch_count)"""
     return int(load_library().aesfhe_launch_count())
+
+
+def alg_bytes() -> dict:
+    """{kernel id: (algorithmic bytes, launches)} of every launch so far (aesfhe_alg_bytes)"""
+    b = np.zeros(len(KERNEL_IDS))
+    n = np.zeros(len(KERNEL_IDS), np.uint64)
+    load_library().aesfhe_alg_bytes(b, n, len(KERNEL_IDS))
+    return {k: (float(b[i]), int(n[i])) for i, k in enumerate(KERNEL_IDS)}
 
 
 def bootstrap_depth() -> int:

@@ -48,7 +48,7 @@ from invmixcolumns_fhe import InvMixColumnsFHE
 from inv_shiftrows import InvShiftRows
 from mixcol_final import MixColFinal
 from shift_rows import ShiftRows
-from state_encoder import StateEncoder
+from state_encoder import StateEncoder, check_layout, tag_layout
 from shift_rows import shift_rows_bytes
 from shiftrows_mixcolumns import ShiftRowsMixColumnsFusedEnc
 from sub_bytes_ark import SubBytesARK
@@ -315,7 +315,7 @@ class AESPipeline:
             self._log_pair(debug, "enc.final.ark10", *ct)
             ct = self._renorm_pair(*ct)
             self._log_pair(debug, "enc.output", *ct)
-            return ct
+            return tag_layout(self.layout, *ct)
         ct = self.sub.apply(*ct, out_level=self._floor())
         self._log_pair(debug, "enc.final.sub", *ct)
         ct = self._renorm_pair(*ct, level=NEED_SR_ARK)
@@ -326,10 +326,11 @@ class AESPipeline:
         self._log_pair(debug, "enc.final.ark10", *ct)
         ct = self._renorm_pair(*ct)
         self._log_pair(debug, "enc.output", *ct)
-        return ct
+        return tag_layout(self.layout, *ct)
 
     # ---------------------------------------------------------------- decrypt
     def decrypt(self, ct_hi, ct_lo, round_keys: List[np.ndarray], debug: Dict[str, Any] | None = None):
+        check_layout(self.layout, ct_hi, ct_lo)  # a pair from another layout would decrypt to wrong bytes
         if debug is not None:
             debug.clear()
         rk = self._prepare_round_keys(round_keys)

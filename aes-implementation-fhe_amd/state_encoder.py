@@ -15,6 +15,12 @@ over all slots.  Every AES step is slot-wise or a rotation by a multiple of the 
 message stays 16B-periodic -- a polynomial in the subring Z[X^(N/32B)] -- and the final
 bootstraps of MixColumns / InvMixColumns run as sparse-slot bootstraps (aesfhe_bootstrap_pair_sparse,
 a trace plus period-sized transforms).  Decoded states are the same in both layouts.
+
+The two layouts are NOT interchangeable on ciphertexts: the encoder tags what it produces with
+its layout (``tag_layout``) and ``decode`` / ``renorm`` / ``AESPipeline.decrypt`` refuse a
+ciphertext tagged with the other one (``check_layout``).  ``StateEncoder(ctx, B)``
+keeps the reference layout; ``AESPipeline`` picks the periodic one where the context has the
+sparse bootstrap (its ``layout`` attribute says which).
 """
 import os
 from typing import Any, Tuple
@@ -77,6 +83,31 @@ class SlotLayout:
         return other is not None and (self.sc, self.states, self.periodic) == (other.sc, other.states, other.periodic)
 
 
+def tag_layout(layout: SlotLayout, *cts):
+    """mark ciphertexts as holding states in `layout` (checked by check_layout); returns them"""
+    for c in cts:
+        try:
+            c.layout = layout
+        except AttributeError:  # a context whose ciphertexts carry no tag (the CPU oracle's)
+            pass
+    return cts
+
+
+def check_layout(layout: SlotLayout, *cts) -> None:
+    """raise if a ciphertext was tagged with another slot layout (a pair made by an encoder with
+    the reference layout decrypts to wrong bytes under the periodic one, and vice versa);
+    untagged ciphertexts pass"""
+    for c in cts:
+        lay = getattr(c, "layout", None)
+        if lay is not None and not layout.same(lay):
+            raise ValueError(f"ciphertext holds states in the {_describe(lay)} slot layout, "
+                             f"this encoder / pipeline uses the {_describe(layout)} one")
+
+
+def _describe(lay: SlotLayout) -> str:
+    return f"{'periodic' if lay.periodic else 'reference'} (states={lay.states})"
+
+
 class StateEncoder:
     def __init__(self, ctx, states: int = 1, periodic: bool = False):
         self.ctx = ctx
@@ -108,9 +139,10 @@ class StateEncoder:
 
     def encode(self, state: np.ndarray) -> Tuple[Any, Any]:
         st = self._as_batch(state)
-        return self.ctx.encrypt(self._pack(st >> 4)), self.ctx.encrypt(self._pack(st & 0x0F))
+        return tag_layout(self.layout, self.ctx.encrypt(self._pack(st >> 4)), self.ctx.encrypt(self._pack(st & 0x0F)))
 
     def decode(self, ct_hi, ct_lo) -> np.ndarray:
+        check_layout(self.layout, ct_hi, ct_lo)
         hi = ZetaEncoder.from_zeta(self._take(self.ctx.decrypt(ct_hi)), 16)
         lo = ZetaEncoder.from_zeta(self._take(self.ctx.decrypt(ct_lo)), 16)
         out = ((hi << 4) | lo).astype(np.uint8)
@@ -135,9 +167,10 @@ class StateEncoder:
 
     def encode_packed(self, state: np.ndarray):
         """a state (batch) encrypted directly in the packed form"""
-        return self.ctx.encrypt(self._packed_slots(self._as_batch(state)))
+        return tag_layout(self.layout, self.ctx.encrypt(self._packed_slots(self._as_batch(state))))[0]
 
     def decode_packed(self, ct) -> np.ndarray:
+        check_layout(self.layout, ct)
         z = self.ctx.decrypt(ct)
         hi = ZetaEncoder.from_zeta(self._take(z), 16)
         lo = ZetaEncoder.from_zeta(self._take(z[self.layout.period:]), 16)
@@ -150,12 +183,17 @@ class StateEncoder:
 
     def renorm_unpack(self, ct, level=None) -> Tuple[Any, Any]:
         """renorm of a packed state into the (hi, lo) pair"""
-        return self.ctx.renorm_unpack(ct, self.layout.period, None if _RENORM_FRESH else level)
+        check_layout(self.layout, ct)
+        return tag_layout(self.layout, *self.ctx.renorm_unpack(ct, self.layout.period, None if _RENORM_FRESH else level))
 
     def renorm(self, ct_hi, ct_lo, level=None) -> Tuple[Any, Any]:
         """decode -> re-encode (REF/pipeline.py:65-69), done on the device when available;
         `level`: the level the next step needs (None = fresh), honoured by the device path.
         With a renorm_hook (true-FHE mode) the hook runs instead (it reads `level` as the next step's need)."""
+        check_layout(self.layout, ct_hi, ct_lo)
+        return tag_layout(self.layout, *self._renorm(ct_hi, ct_lo, level))
+
+    def _renorm(self, ct_hi, ct_lo, level):
         if self.renorm_hook is not None:
             return self.renorm_hook(ct_hi, ct_lo, level)
         per = getattr(self.ctx, "renorm_periodic", None)

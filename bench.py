@@ -71,7 +71,7 @@ def parse():
     ap.add_argument("--batch-states", type=int, default=1024,
                     help="secondary measurement (BASELINE configs 3/4): this many independent states per rank, "
                          "slot-packed into one ciphertext pair (SURVEY.md 8(f)1); 0 = skip")
-    ap.add_argument("--batch-steps", type=int, default=1)
+    ap.add_argument("--batch-steps", type=int, default=3)
     ap.add_argument("--true-fhe-steps", type=int, default=1,
                     help="SURVEY.md 8(f)3 line beside the headline: C2 encrypts with every secret-key renorm replaced "
                          "by bootstrap + homomorphic Zeta16 snap (AESPipeline(true_fhe=True)); 0 = skip")
@@ -157,27 +157,24 @@ def max_over_ranks(dist, x: float) -> float:
 
 
 def cpu_baseline(coeffs) -> dict:
-    """The C oracle CPU CKKS engine (oracle/ckks_cpu.py, OpenMP over OMP_NUM_THREADS host
-    threads), measured on a bounded sample (tools/cpu_round.py): BASELINE config 1 in full
-    (AddRoundKey at N = 2^15) and the SubBytes + renorm step of a middle C2 round at N = 2^16.
-    The round rate divides the SubBytes time by that step's share of a whole middle round,
-    measured in full on the same host by `tools/cpu_round.py --full` (profiles/r2_cpu_round.json:
-    98 s per round on 16 threads, bootstraps excluded -- the oracle does not bootstrap)."""
+    """The C oracle CPU CKKS engine (oracle/ckks_cpu.py over oracle/ckks_oracle.c: Shoup / Barrett
+    modular products, OpenMP over OMP_NUM_THREADS host threads), timed live on this host
+    (tools/cpu_round.py): BASELINE config 1 in full (AddRoundKey at N = 2^15), then ONE FULL middle
+    round of the C2 encrypt at N = 2^16 (SubBytes, renorm, ShiftRows, MixColumns without its final
+    bootstrap, AddRoundKey, renorm -- the oracle does not bootstrap), checked against the byte
+    model.  Budget: ~1 min on 16 host threads (the CPU work of one round); nothing is read from a
+    file or extrapolated from a step share."""
     sys.path.insert(0, str(ROOT / "tools"))
     import cpu_round
     c1 = cpu_round.c1(coeffs)
-    c2 = cpu_round.c2_round(coeffs, full=False)
-    full = json.loads((ROOT / "profiles" / "r2_cpu_round.json").read_text())
-    share = full["c2"]["steps_s"]["subbytes+renorm"] / full["c2"]["round_s"]
-    sb_s = c2["steps_s"]["subbytes+renorm"]
-    round_s = sb_s / share
+    c2 = cpu_round.c2_round(coeffs, full=True)
+    round_s = c2["round_s"]
     return {"value": 1.0 / round_s, "unit": "rounds/s", "cores": cpu_round.threads(), "kind": "port",
-            "sample": f"C oracle on the host: config 1 (AddRoundKey, N=2^15) in full {c1['ark_s']:.2f} s (exact: {c1['exact']}); "
-                      f"SubBytes+renorm of C2 round 1 at N=2^16 {sb_s:.2f} s (exact: {c2['exact']}), divided by its measured "
-                      f"share {share:.3f} of a full middle round (profiles/r2_cpu_round.json, {full['c2']['round_s']:.1f} s on "
-                      f"{full['threads']} threads); bootstraps excluded (the oracle does not bootstrap)",
-            "c1_ark_s": c1["ark_s"], "c2_subbytes_renorm_s": sb_s, "c2_round_s_estimate": round_s,
-            "c2_round_s_measured_full": full["c2"]["round_s"]}
+            "sample": f"C oracle on the host, timed live: config 1 (AddRoundKey, N=2^15) in full {c1['ark_s']:.2f} s "
+                      f"(exact: {c1['exact']}); one full middle round of C2 at N=2^16 {round_s:.1f} s (exact: {c2['exact']}; "
+                      + ", ".join(f"{k} {v:.1f} s" for k, v in c2["steps_s"].items())
+                      + "); MixColumns' final bootstrap excluded (the oracle does not bootstrap)",
+            "c1_ark_s": c1["ark_s"], "c2_round_s": round_s, "c2_steps_s": c2["steps_s"]}
 
 
 class _NoFinalBootstrap:
@@ -203,6 +200,34 @@ def _progress(ctx, every_s: float = 30.0):
                   file=sys.stderr, flush=True)
 
     threading.Thread(target=run, daemon=True).start()
+
+
+def measure_precision(pipe, ctx, rks, state) -> dict:
+    """CKKS precision of the bench path, measured after the timed region: the scale Delta of the
+    single-prime levels (log2), and the largest angular deviation of any state slot from its
+    Zeta16 codeword over every logged stage of one encrypt (debug dict of the production path,
+    DESIGN.md 4c), against the decode margin pi/16 -- bytes are exact while it stays below"""
+    E = ctx.engine
+    dbg = {}
+    pipe.encrypt(state, rks, debug=dbg)
+    worst, where = 0.0, None
+    for tag, entry in dbg.items():
+        cts = [entry["ct_packed"]] if "ct_packed" in entry else [entry["ct_hi"], entry["ct_lo"]]
+        for c in cts:
+            z = ctx.decrypt(c)[: 16 * pipe.layout.period] if pipe.layout.periodic else ctx.decrypt(c)
+            if not pipe.layout.periodic:
+                z = z[:16 * pipe.stride:pipe.stride]
+            ang = np.angle(z) * 16 / (2 * np.pi)
+            dev = float(np.abs(ang - np.rint(ang)).max() * 2 * np.pi / 16)
+            if dev > worst:
+                worst, where = dev, tag
+    deltas = E.scales()
+    return {"log2_delta_fresh": float(np.log2(deltas[E.fresh_level])), "log2_delta_level0": float(np.log2(deltas[0])),
+            "max_slot_angle_error_rad": worst, "worst_stage": where, "decode_margin_rad": float(np.pi / 16),
+            "stages_checked": len(dbg),
+            "note": "slot error = angular distance of every state slot to the nearest 16th root of unity, over every "
+                    "logged stage of one C2 encrypt (renorm / XOR4 / GF / SubBytes / bootstrap outputs); the bootstrap "
+                    "alone: max 2.4e-4 at |z| <= 1 (profiles/r2_boot_error.json)"}
 
 
 def rank_states(rank: int, n: int):
@@ -377,7 +402,11 @@ def main():
     for i in range(args.warmup):
         pipe.encrypt(states[i], rks)
     E.sync()
-    kernels = list(__import__("mi355x_ckks").KERNEL_IDS) if args.profile_all else [args.kernel, args.kernel2]
+    import mi355x_ckks
+    # the roofline kernels, plus the forward NTT's first pass and the base conversion (per-class
+    # fractions beside the whole-step one)
+    kernels = list(mi355x_ckks.KERNEL_IDS) if args.profile_all else list(dict.fromkeys([args.kernel, args.kernel2, "ntt_cols_fwd",
+                                                                                       "base_convert"]))
     whole = args.whole_stats and os.environ.get("AESFHE_PROFILE_FROM_START")
     pre = {}
     if whole:  # whole-process accounting: keep the from-start configuration, fold the pre-timed part in
@@ -394,12 +423,14 @@ def main():
     outs = []
     barrier(dist)
     E.sync()
+    alg0, launches0 = mi355x_ckks.alg_bytes(), mi355x_ckks.launch_count()
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
         outs.append(pipe.encrypt(states[i], rks))
     E.sync()
     barrier(dist)
     elapsed = time.perf_counter() - t0
+    alg1, launches1 = mi355x_ckks.alg_bytes(), mi355x_ckks.launch_count()
     elapsed = max_over_ranks(dist, elapsed)
     work = E.kernel_work()
     stats = E.kernel_stats(reset=True)
@@ -418,6 +449,20 @@ def main():
 
     states_done = args.steps * world
     value = 10.0 * states_done / elapsed
+    # whole-step roofline: algorithmic bytes of EVERY launch of the
+    # timed steps (engine accounting, per kernel class) / this rank's wall time / 8 TB/s
+    step_bytes = {k: alg1[k][0] - alg0[k][0] for k in alg1}
+    step_launches = {k: alg1[k][1] - alg0[k][1] for k in alg1}
+    rank_elapsed = elapsed  # max over ranks; each rank's bytes are its own steps
+    roofline_step = {"bound": "hbm", "achieved": sum(step_bytes.values()) / rank_elapsed / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": sum(step_bytes.values()) / rank_elapsed / 1e9 / HBM_PEAK_GBS,
+                     "algorithmic_bytes_per_step": sum(step_bytes.values()) / args.steps,
+                     "bytes_per_step_by_class": {k: v / args.steps for k, v in step_bytes.items() if v},
+                     "launches_per_step_by_class": {k: v / args.steps for k, v in step_launches.items() if v},
+                     "note": "sum over every kernel launch of the timed encrypts of its algorithmic bytes (each operand word "
+                             "read once, each result word written once; DESIGN.md 5) / wall time / 8 TB/s"}
+    launches_per_encrypt = (launches1 - launches0) / args.steps
+    precision = measure_precision(pipe, ctx, rks, states[0]) if rank == 0 else None
     tj = json.loads(Path(args.traffic_json).read_text()) if args.traffic_json and Path(args.traffic_json).exists() else {}
 
     def roofline(kid: str, note: str) -> dict:
@@ -460,7 +505,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u32 (RNS residues, primes < 2^32/3)",
+        "dtype": "u32 (RNS residues, 30-bit primes; CKKS scale Delta ~ 2^29.9 on the single-prime levels, see precision)",
         "data": "synthetic random 16-byte states, FIPS key schedule of a seed-7 master key",
         "config": {"workload": "C2: full AES-128 encrypt (10 rounds), 1 packed state per ciphertext pair, "
                                "N=2^16, renorm on" + ("" if not args.no_final_bootstrap else ", FINAL BOOTSTRAP SKIPPED"),
@@ -480,6 +525,11 @@ def main():
                                           "VALU / latency-bound: ~11.8 VALU instructions per lazy butterfly, u32 multiplies at full rate (DESIGN.md 5)"),
         "roofline_secondary": roofline(args.kernel2, "key-switch inner product: HBM-bound"),
         "roofline_valu": valu_roofline(args.kernel),
+        "roofline_step": roofline_step,
+        "roofline_classes": {k: roofline(k, "per-class fraction (live sample)") for k in ("ntt_cols_fwd", "base_convert")
+                             if k in stats},
+        "launches_per_encrypt": launches_per_encrypt,
+        "precision": precision,
         "op_counts_per_round": {k: v / (10.0 * args.steps) for k, v in counters.items()},
     }
     if batch is not None:

@@ -298,6 +298,10 @@ int aesfhe_reset_counters(aesfhe_ctx* ctx);
 /* kernel launches issued by this process so far (all contexts): the launch census of
  * tools/launch_census.py and bench.py's launches-per-encrypt (MI355X-side tooling) */
 uint64_t aesfhe_launch_count(void);
+/* per kernel id (the aesfhe_profile order): algorithmic bytes and launches of
+ * every launch this process issued so far, timed or not -- bench.py's whole-step roofline
+ * (sum of algorithmic bytes of the timed steps / wall / 8 TB/s) */
+int aesfhe_alg_bytes(double* bytes, uint64_t* launches, int n);
 
 #ifdef __cplusplus
 }

@@ -60,6 +60,37 @@ static int NL(const orc_t *o, int l) {
 /* ------------------------------------------------------------------ */
 static u32 mulm(u32 a, u32 b, u32 q) { return (u32)(((u64)a * b) % q); }
 static u32 addm(u32 a, u32 b, u32 q) { u64 s = (u64)a + b; return (u32)(s >= q ? s - q : s); }
+/* Exact Barrett reduction for the hot loops (round 3: the oracle is also the CPU baseline, and a
+ * hardware 64-bit division per product made it a strawman).  bq.mu = floor(2^64 / q); for any
+ * 64-bit x, x - floor(x mu / 2^64) q lies in [0, 3q): at most two corrections.  Same residues as
+ * the % forms, bit for bit. */
+typedef struct { u32 q; u64 mu; u64 r64; } barrett_t;  /* r64 = 2^64 mod q */
+static barrett_t bq_make(u32 q) {
+    barrett_t b;
+    b.q = q;
+    b.mu = (u64)(((u128)1 << 64) / q);
+    b.r64 = (u64)((((u128)1 << 64)) % q);
+    return b;
+}
+static inline u32 bred64(u64 x, const barrett_t *b) {
+    u64 est = (u64)(((u128)x * b->mu) >> 64);
+    u64 r = x - est * b->q;
+    if (r >= b->q) r -= b->q;
+    if (r >= b->q) r -= b->q;
+    return (u32)r;
+}
+static inline u32 bred128(u128 x, const barrett_t *b) {  /* x < 2^64 * 2^32 */
+    u64 hi = (u64)(x >> 64), lo = (u64)x;
+    return addm(bred64(lo, b), bred64(hi * b->r64, b), b->q);  /* hi < 2^32, r64 < 2^30: no overflow */
+}
+static inline u32 bmul(u32 a, u32 c, const barrett_t *b) { return bred64((u64)a * c, b); }
+/* Shoup product by a fixed operand w (wp = floor(w 2^32 / q)): the NTT twiddles */
+static inline u32 shoup_pre32(u32 w, u32 q) { return (u32)(((u64)w << 32) / q); }
+static inline u32 smul(u32 a, u32 w, u32 wp, u32 q) {
+    u32 t = (u32)(((u64)a * wp) >> 32);
+    u32 r = a * w - t * q;
+    return r >= q ? r - q : r;
+}
 static u32 subm(u32 a, u32 b, u32 q) { return a >= b ? a - b : a + q - b; }
 static u32 powm(u32 a, u64 e, u32 q) {
     u64 r = 1, b = a % q;
@@ -329,9 +360,9 @@ static void ntt_limb(const orc_t *o, int li, u32 *a) {
     int n = o->n;
     for (int m = 1, t = n >> 1; m < n; m <<= 1, t >>= 1)
         for (int i = 0; i < m; i++) {
-            u32 wi = w[m + i];
+            u32 wi = w[m + i], wp = shoup_pre32(wi, q);
             for (int j = 2 * i * t; j < 2 * i * t + t; j++) {
-                u32 u = a[j], v = mulm(a[j + t], wi, q);
+                u32 u = a[j], v = smul(a[j + t], wi, wp, q);
                 a[j] = addm(u, v, q); a[j + t] = subm(u, v, q);
             }
         }
@@ -341,13 +372,14 @@ static void intt_limb(const orc_t *o, int li, u32 *a) {
     int n = o->n;
     for (int m = n >> 1, t = 1; m >= 1; m >>= 1, t <<= 1)
         for (int i = 0; i < m; i++) {
-            u32 wi = w[m + i];
+            u32 wi = w[m + i], wp = shoup_pre32(wi, q);
             for (int j = 2 * i * t; j < 2 * i * t + t; j++) {
                 u32 u = a[j], v = a[j + t];
-                a[j] = addm(u, v, q); a[j + t] = mulm(subm(u, v, q), wi, q);
+                a[j] = addm(u, v, q); a[j + t] = smul(subm(u, v, q), wi, wp, q);
             }
         }
-    for (int j = 0; j < n; j++) a[j] = mulm(a[j], o->ninv[li], q);
+    u32 ni = o->ninv[li], nip = shoup_pre32(ni, q);
+    for (int j = 0; j < n; j++) a[j] = smul(a[j], ni, nip, q);
 }
 
 void orc_ntt(void *h, const int *limbs, int nl, u32 *data) {
@@ -516,7 +548,8 @@ static void automorph_limb(const orc_t *o, int li, u64 g, const u32 *in, u32 *ou
     free(c);
 }
 
-/* key-switching key for s' -> s, s' = s^2 (g == 0) or s(X^g) */
+/* key-switching key for s' -> s, s' = s^2 (g == 0), s(X^g) (g < 2N), or s(X^g')^2 for the tag
+ * g = 4N + g' (the conjugation / rotation of a 3-polynomial tensor) */
 void orc_gen_ksk(void *h, u64 g, u32 *out) {
     orc_t *o = (orc_t *)h;
     int n = o->n, tot = o->n_q + o->n_p, next = o->n_ks + o->n_p;
@@ -530,6 +563,11 @@ void orc_gen_ksk(void *h, u64 g, u32 *out) {
         u32 q = o->mod[i];
         if (g == 0) {
             for (int k = 0; k < n; k++) sp[(size_t)i * n + k] = mulm(s[(size_t)i * n + k], s[(size_t)i * n + k], q);
+        } else if (g > 4ull * n && g < 6ull * n) {
+            u32 *sq = (u32 *)malloc(sizeof(u32) * n);
+            for (int k = 0; k < n; k++) sq[k] = mulm(s[(size_t)i * n + k], s[(size_t)i * n + k], q);
+            automorph_limb(o, i, g - 4ull * n, sq, sp + (size_t)i * n);
+            free(sq);
         } else {
             automorph_limb(o, i, g, s + (size_t)i * n, sp + (size_t)i * n);
         }
@@ -582,9 +620,9 @@ void orc_rescale(void *h, int level, int npoly, const u32 *in, u32 *out) {
                 v[k] = signed_to_mod(c, q);
             }
             ntt_limb(o, t, v);
-            u32 qinv = invm(qr % q, q);
+            u32 qinv = invm(qr % q, q), qinvp = shoup_pre32(qinv, q);
             for (int k = 0; k < n; k++)
-                dst[(size_t)t * n + k] = mulm(subm(src[(size_t)t * n + k], v[k], q), qinv, q);
+                dst[(size_t)t * n + k] = smul(subm(src[(size_t)t * n + k], v[k], q), qinv, qinvp, q);
             free(v);
         }
         free(last);
@@ -605,6 +643,17 @@ static u32 overflow_count(const u32 *y, size_t stride, int h, const u32 *primes)
     }
     return (u32)((f + (1ull << 31)) >> 32);
 }
+/* the same for every coefficient k < n, the mu_i hoisted and the coefficients in parallel */
+static void overflow_counts(const u32 *y, int n, int h, const u32 *primes, u32 *ucnt) {
+    u64 mu[64];
+    for (int i = 0; i < h; i++) mu[i] = (1ull << 61) / primes[i];
+#pragma omp parallel for schedule(static)
+    for (int k = 0; k < n; k++) {
+        u64 f = 0;
+        for (int i = 0; i < h; i++) f += ((u64)y[(size_t)i * n + k] * mu[i]) >> 29;
+        ucnt[k] = (u32)((f + (1ull << 31)) >> 32);
+    }
+}
 
 /* ------------------------------------------------------------------ */
 /* hybrid key switching                               */
@@ -624,20 +673,22 @@ void orc_keyswitch(void *h, int level, const u32 *d, const u32 *ksk, u32 *out) {
     u32 *ext = (u32 *)malloc(sizeof(u32) * (size_t)ne * n);
     u32 *coef = (u32 *)malloc(sizeof(u32) * (size_t)nl * n);
     memcpy(coef, d, sizeof(u32) * (size_t)nl * n);
+#pragma omp parallel for schedule(static)
     for (int i = 0; i < nl; i++) intt_limb(o, i, coef + (size_t)i * n);
     int ndig = (nl + o->alpha - 1) / o->alpha;
     for (int j = 0; j < ndig; j++) {
         int lo = j * o->alpha, hi = lo + o->alpha < nl ? lo + o->alpha : nl;
         /* y_i = coef_i * (qhat_i^-1 mod q_i), qhat_i = prod_{k in digit, k != i} q_k */
         u32 *y = (u32 *)malloc(sizeof(u32) * (size_t)(hi - lo) * n);
+#pragma omp parallel for schedule(static)
         for (int i = lo; i < hi; i++) {
             u32 q = o->mod[i], qh = 1;
             for (int k = lo; k < hi; k++) if (k != i) qh = mulm(qh, o->mod[k] % q, q);
-            u32 qhi = invm(qh, q);
-            for (int k = 0; k < n; k++) y[(size_t)(i - lo) * n + k] = mulm(coef[(size_t)i * n + k], qhi, q);
+            u32 qhi = invm(qh, q), qhip = shoup_pre32(qhi, q);
+            for (int k = 0; k < n; k++) y[(size_t)(i - lo) * n + k] = smul(coef[(size_t)i * n + k], qhi, qhip, q);
         }
         u32 *ucnt = (u32 *)malloc(sizeof(u32) * n);
-        for (int k = 0; k < n; k++) ucnt[k] = overflow_count(y + k, n, hi - lo, o->mod + lo);
+        overflow_counts(y, n, hi - lo, o->mod + lo, ucnt);
 #pragma omp parallel for schedule(static)
         for (int x = 0; x < ne; x++) {
             u32 *dst = ext + (size_t)x * n;
@@ -652,10 +703,11 @@ void orc_keyswitch(void *h, int level, const u32 *d, const u32 *ksk, u32 *out) {
             u32 negQ = 1; /* -Q_j mod t */
             for (int k = lo; k < hi; k++) negQ = mulm(negQ, o->mod[k] % t, t);
             negQ = negQ ? t - negQ : 0;
+            barrett_t bt = bq_make(t);
             for (int k = 0; k < n; k++) {
                 u128 s = (u64)ucnt[k] * negQ;
                 for (int i = lo; i < hi; i++) s += (u64)y[(size_t)(i - lo) * n + k] * qh_t[i - lo];
-                dst[k] = (u32)(s % t);
+                dst[k] = bred128(s, &bt);
             }
             free(qh_t);
             ntt_limb(o, gid[x], dst);
@@ -665,10 +717,11 @@ void orc_keyswitch(void *h, int level, const u32 *d, const u32 *ksk, u32 *out) {
 #pragma omp parallel for schedule(static)
         for (int x = 0; x < ne; x++) {
             u32 t = o->mod[gid[x]];
+            barrett_t bt = bq_make(t);
             for (int k = 0; k < n; k++) {
                 u32 e = ext[(size_t)x * n + k];
-                acc[(size_t)x * n + k] = addm(acc[(size_t)x * n + k], mulm(e, kb[(size_t)kid[x] * n + k], t), t);
-                acc[(size_t)(ne + x) * n + k] = addm(acc[(size_t)(ne + x) * n + k], mulm(e, ka[(size_t)kid[x] * n + k], t), t);
+                acc[(size_t)x * n + k] = bred64((u64)acc[(size_t)x * n + k] + (u64)e * kb[(size_t)kid[x] * n + k], &bt);
+                acc[(size_t)(ne + x) * n + k] = bred64((u64)acc[(size_t)(ne + x) * n + k] + (u64)e * ka[(size_t)kid[x] * n + k], &bt);
             }
         }
     }
@@ -676,17 +729,18 @@ void orc_keyswitch(void *h, int level, const u32 *d, const u32 *ksk, u32 *out) {
     for (int p = 0; p < 2; p++) {
         u32 *a = acc + (size_t)p * ne * n;
         u32 *yp = (u32 *)malloc(sizeof(u32) * (size_t)np * n);
+#pragma omp parallel for schedule(static)
         for (int k2 = 0; k2 < np; k2++) {
             int g = o->n_q + k2;
             u32 q = o->mod[g], ph = 1;
             for (int m = 0; m < np; m++) if (m != k2) ph = mulm(ph, o->mod[o->n_q + m] % q, q);
-            u32 phi = invm(ph, q);
+            u32 phi = invm(ph, q), phip = shoup_pre32(phi, q);
             memcpy(yp + (size_t)k2 * n, a + (size_t)(nl + k2) * n, sizeof(u32) * n);
             intt_limb(o, g, yp + (size_t)k2 * n);
-            for (int k = 0; k < n; k++) yp[(size_t)k2 * n + k] = mulm(yp[(size_t)k2 * n + k], phi, q);
+            for (int k = 0; k < n; k++) yp[(size_t)k2 * n + k] = smul(yp[(size_t)k2 * n + k], phi, phip, q);
         }
         u32 *ucnt = (u32 *)malloc(sizeof(u32) * n);
-        for (int k = 0; k < n; k++) ucnt[k] = overflow_count(yp + k, n, np, o->mod + o->n_q);
+        overflow_counts(yp, n, np, o->mod + o->n_q, ucnt);
 #pragma omp parallel for schedule(static)
         for (int t = 0; t < nl; t++) {
             u32 q = o->mod[t];
@@ -700,15 +754,17 @@ void orc_keyswitch(void *h, int level, const u32 *d, const u32 *ksk, u32 *out) {
             }
             u32 negP = pinv ? q - pinv : 0; /* -P mod q */
             pinv = invm(pinv, q);
+            barrett_t bt = bq_make(q);
             u32 *conv = (u32 *)malloc(sizeof(u32) * n);
             for (int k = 0; k < n; k++) {
                 u128 s = (u64)ucnt[k] * negP;
                 for (int k2 = 0; k2 < np; k2++) s += (u64)yp[(size_t)k2 * n + k] * ph_t[k2];
-                conv[k] = (u32)(s % q);
+                conv[k] = bred128(s, &bt);
             }
             ntt_limb(o, t, conv);
             u32 *dst = out + (size_t)p * nl * n + (size_t)t * n;
-            for (int k = 0; k < n; k++) dst[k] = mulm(subm(a[(size_t)t * n + k], conv[k], q), pinv, q);
+            u32 pinvp = shoup_pre32(pinv, q);
+            for (int k = 0; k < n; k++) dst[k] = smul(subm(a[(size_t)t * n + k], conv[k], q), pinv, pinvp, q);
             free(conv); free(ph_t);
         }
         free(yp); free(ucnt);
@@ -786,11 +842,12 @@ void orc_keyswitch_d2s(void *h, int np, const u32 *d, const u32 *ksk, u32 *out) 
         u32 qh0 = o->mod[1] % t, qh1 = o->mod[0] % t;
         u32 negQ = mulm(o->mod[0] % t, o->mod[1] % t, t);
         negQ = negQ ? t - negQ : 0;
+        barrett_t bt = bq_make(t);
         for (int k = 0; k < n; k++) {
             u128 s = (u64)ucnt[k] * negQ;
             s += (u64)y[k] * qh0;
             s += (u64)y[(size_t)n + k] * qh1;
-            dst[k] = (u32)(s % t);
+            dst[k] = bred128(s, &bt);
         }
         ntt_limb(o, gid[x], dst);
     }
@@ -818,7 +875,7 @@ void orc_keyswitch_d2s(void *h, int np, const u32 *d, const u32 *ksk, u32 *out) 
             for (int k = 0; k < n; k++) yp[(size_t)k2 * n + k] = mulm(yp[(size_t)k2 * n + k], phi, q);
         }
         u32 *uc = (u32 *)malloc(sizeof(u32) * n);
-        for (int k = 0; k < n; k++) uc[k] = overflow_count(yp + k, n, np, o->mod + o->n_q);
+        overflow_counts(yp, n, np, o->mod + o->n_q, uc);
         for (int t = 0; t < nq; t++) {
             u32 q = o->mod[t], pinv = 1;
             u32 ph_t[16];
@@ -830,11 +887,12 @@ void orc_keyswitch_d2s(void *h, int np, const u32 *d, const u32 *ksk, u32 *out) 
             }
             u32 negP = pinv ? q - pinv : 0;
             pinv = invm(pinv, q);
+            barrett_t bt = bq_make(q);
             u32 *conv = (u32 *)malloc(sizeof(u32) * n);
             for (int k = 0; k < n; k++) {
                 u128 s = (u64)uc[k] * negP;
                 for (int k2 = 0; k2 < np; k2++) s += (u64)yp[(size_t)k2 * n + k] * ph_t[k2];
-                conv[k] = (u32)(s % q);
+                conv[k] = bred128(s, &bt);
             }
             ntt_limb(o, t, conv);
             u32 *dst = out + (size_t)p * nq * n + (size_t)t * n;
@@ -856,12 +914,12 @@ void orc_tensor(void *h, int level, const u32 *a, const u32 *b, u32 *out) {
     size_t P = (size_t)nl * n;
 #pragma omp parallel for schedule(static)
     for (int t = 0; t < nl; t++) {
-        u32 q = o->mod[t];
+        barrett_t bt = bq_make(o->mod[t]);
         for (int k = 0; k < n; k++) {
             size_t x = (size_t)t * n + k;
-            out[x] = mulm(a[x], b[x], q);
-            out[P + x] = addm(mulm(a[x], b[P + x], q), mulm(a[P + x], b[x], q), q);
-            out[2 * P + x] = mulm(a[P + x], b[P + x], q);
+            out[x] = bmul(a[x], b[x], &bt);
+            out[P + x] = bred64((u64)a[x] * b[P + x] + (u64)a[P + x] * b[x], &bt);
+            out[2 * P + x] = bmul(a[P + x], b[P + x], &bt);
         }
     }
 }
@@ -870,12 +928,13 @@ void orc_tensor(void *h, int level, const u32 *a, const u32 *b, u32 *out) {
 void orc_mul_limb_consts(void *h, int nl, int npoly, const u32 *c, const u32 *in, u32 *out) {
     orc_t *o = (orc_t *)h;
     int n = o->n;
+#pragma omp parallel for collapse(2) schedule(static)
     for (int p = 0; p < npoly; p++)
         for (int t = 0; t < nl; t++) {
-            u32 q = o->mod[t];
+            u32 q = o->mod[t], cp = shoup_pre32(c[t], q);
             for (int k = 0; k < n; k++) {
                 size_t x = ((size_t)p * nl + t) * n + k;
-                out[x] = mulm(in[x], c[t], q);
+                out[x] = smul(in[x], c[t], cp, q);
             }
         }
 }

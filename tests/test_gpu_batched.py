@@ -112,3 +112,24 @@ def test_galois_multi_bit_exact(E, layout):
         want = E.conjugate(c) if a == "conj" else E.rotate(c, None, a)
         assert r.level == want.level
         assert np.array_equal(E.export(r), E.export(want))
+
+
+def test_conjugate_of_deferred_tensor(E):
+    """conjugate() of a deferred LUT-like tensor (3 polynomials owing a rescale: a lazy product,
+    and the same scaled by a non-integer constant owing two) is done without resolving it
+    (engine.hip galois_lazy, keys sigma(s) -> s and sigma(s)^2 -> s summed before one ModDown):
+    the slots equal conj of the resolved tensor's within CKKS noise, the owed work stays owed, and
+    S1 + conj(S2) adds directly"""
+    rng = np.random.default_rng(41)
+    z = np.exp(2j * np.pi * rng.random(E.slot_count))
+    w = np.exp(2j * np.pi * rng.random(E.slot_count))
+    x, y = E.encrypt(z), E.encrypt(w)
+    t = E.multiply(x, y, "rlk")          # deferred: 3 polynomials, one rescale owed
+    t2 = E.multiply(t, 0.3 + 0.1j)       # deferred constant product: two rescales owed
+    for c, want in ((t, z * w), (t2, (0.3 + 0.1j) * z * w)):
+        got = E.conjugate(c)
+        assert got.level == c.level
+        err = np.abs(E.decrypt(got) - np.conj(want)).max()
+        assert err < 1e-3, err
+    s = E.add(t2, E.conjugate(t2))       # the split-LUT sum: 2 Re(...)
+    assert np.abs(E.decrypt(s) - 2 * ((0.3 + 0.1j) * z * w).real).max() < 2e-3

@@ -106,3 +106,19 @@ def test_packed_config2_encrypt_and_roundtrip(ctx, coeff_dir, states):
     assert np.array_equal(got, want), int((got != want).any(axis=1).sum())
     back = pipe.decrypt(*ct, rks)
     assert np.array_equal(pipe.encoder.decode(*back), pts)
+
+
+def test_pipeline_refuses_a_pair_in_the_other_layout(ctx, coeff_dir):
+    """the pipeline's encrypt output carries its slot layout; its decrypt (and its encoder)
+    refuse a pair encoded in the reference layout instead of returning wrong bytes"""
+    from aes_keyschedule import expand_aes128_key, load_all_coeffs
+    from pipeline import AESPipeline
+    from state_encoder import StateEncoder
+    pipe = AESPipeline(ctx, load_all_coeffs(coeff_dir), use_hard_renorm_between_steps=True, states=64)
+    assert pipe.layout.periodic
+    rks = expand_aes128_key(np.arange(16, dtype=np.uint8))
+    other = StateEncoder(ctx, 64).encode(np.zeros((64, 16), np.uint8))  # reference layout
+    with pytest.raises(ValueError, match="slot layout"):
+        pipe.decrypt(*other, rks)
+    with pytest.raises(ValueError, match="slot layout"):
+        pipe.encoder.decode(*other)

@@ -68,10 +68,13 @@ def test_keyed_context_bitexact():
     assert np.array_equal(E.export_ksk(E.galois_conj), O.gen_ksk(E.galois_conj))
 
 
-@pytest.mark.parametrize("which", ["relin", "conj", "rot"])
+@pytest.mark.parametrize("which", ["relin", "conj", "rot", "conj_sq"])
 def test_keyswitch_keys_bitexact(pair, which):
+    """conj_sq: the key sigma(s)^2 -> s (tag 4N + g) of the deferred-tensor conjugation
+    (engine.hip galois_lazy)"""
     E, O = pair
-    g = {"relin": 0, "conj": E.galois_conj, "rot": E.galois_rotate(-(E.slot_count // 4))}[which]
+    g = {"relin": 0, "conj": E.galois_conj, "rot": E.galois_rotate(-(E.slot_count // 4)),
+         "conj_sq": 4 * E.n + E.galois_conj}[which]
     assert np.array_equal(E.export_ksk(g), O.gen_ksk(g))
 
 

@@ -154,3 +154,23 @@ def test_periodic_layout(states):
         got = enc.decode(r, np.roll(lo, -4 * k * lay.unit))
         exp = np.stack([np.roll(s.reshape(4, 4), -k, axis=0).reshape(16) for s in st])
         assert np.array_equal(got, exp[0] if states == 1 else exp), k
+
+
+def test_layout_tags_are_checked():
+    """a ciphertext the encoder tagged with one slot layout is refused by an encoder (and so by
+    AESPipeline.decrypt / renorm) using the other one; untagged ciphertexts pass"""
+    from state_encoder import SlotLayout, check_layout, tag_layout
+
+    class Ct:
+        pass
+
+    ref, per = SlotLayout(256, 4), SlotLayout(256, 4, periodic=True)
+    a, b = tag_layout(ref, Ct(), Ct())
+    check_layout(ref, a, b)
+    check_layout(per, Ct())
+    with pytest.raises(ValueError, match="reference"):
+        check_layout(per, a, b)
+    (c,) = tag_layout(per, Ct())
+    with pytest.raises(ValueError, match="periodic"):
+        check_layout(ref, c)
+    tag_layout(ref, np.zeros(3))  # untaggable ciphertexts (the CPU stand-ins) are left alone

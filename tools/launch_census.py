@@ -65,5 +65,58 @@ def main():
     print(json.dumps({"serial": serial, "packed_xor": packed, "reps": reps, "steps": out}, indent=1))
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--by-op" not in sys.argv:
     main()
+
+
+def by_op():
+    """launches per Engine method (top-level calls only) over one middle round (--by-op)"""
+    import functools
+    import mi355x_ckks
+    from collections import defaultdict
+    stats = defaultdict(lambda: [0, 0])
+    depth = [0]
+
+    def wrap(name, f):
+        @functools.wraps(f)
+        def g(*a, **k):
+            if depth[0]:
+                return f(*a, **k)
+            depth[0] += 1
+            n0 = launch_count()
+            try:
+                return f(*a, **k)
+            finally:
+                depth[0] -= 1
+                s = stats[name]
+                s[0] += 1
+                s[1] += launch_count() - n0
+        return g
+
+    for name in dir(mi355x_ckks.Engine):
+        f = getattr(mi355x_ckks.Engine, name)
+        if callable(f) and not name.startswith("_") and name not in ("sync", "parallel", "can_fork", "settle", "nl", "galois_rotate"):
+            setattr(mi355x_ckks.Engine, name, wrap(name, f))
+    ctx = EngineContext(signature=1, max_level=17, concurrent=False)
+    pipe = AESPipeline(ctx, load_all_coeffs(), use_hard_renorm_between_steps=True)
+    np.random.seed(7)
+    rks = expand_aes128_key(np.random.randint(0, 256, 16, dtype=np.uint8))
+    st = np.random.randint(0, 256, 16, dtype=np.uint8)
+    rk = pipe._prepare_round_keys(rks)
+    ct0 = pipe._ark_renorm(pipe.encoder.encode(st), rk[0], level=pipe.need_sub)
+    pipe.encrypt_round(ct0, rk[1], r=1)
+    pipe._packed_round_key(2)
+    ctx.engine.sync()
+    stats.clear()
+    n0 = launch_count()
+    pipe.encrypt_round(ct0, rk[2], r=2)
+    ctx.engine.sync()
+    total = launch_count() - n0
+    rows = sorted(stats.items(), key=lambda kv: -kv[1][1])
+    print(json.dumps({"round_launches": total, "by_op": {k: {"calls": v[0], "launches": v[1], "per_call": round(v[1] / max(v[0], 1), 1)}
+                                                          for k, v in rows}}, indent=1))
+
+
+if __name__ == "__main__" and "--by-op" in sys.argv:
+    by_op()
+    sys.exit(0)
