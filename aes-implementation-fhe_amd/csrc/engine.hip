@@ -1722,9 +1722,16 @@ public:
         // 1. canonical sources; lazy 2-polynomial tensors owing one rescale, grouped by level, are
         //    stacked and rescaled together
         std::map<int, std::vector<const Ct*>> lazy1;
+        std::vector<bool> done(n, false);
         for (int i = 0; i < n; ++i) {
             const Ct& c = *C[i];
             if (vis_npoly(c) != 2) throw std::runtime_error("rotation/conjugation expects a 2-polynomial ciphertext");
+            // conjugations of deferred tensors stay deferred, exactly as conjugate() does them (§3.14)
+            if (G[i] == conj_galois() && lazy_galois_ok(c)) {
+                out[i] = galois_lazy(c, G[i]);
+                done[i] = true;
+                continue;
+            }
             if (src_of.count(c.data)) continue;
             if (c.lazy && c.pend == 1 && pm(c) == 2 && c.nb == 1 && c.ntt && !c.zero) {
                 auto& v = lazy1[c.level];
@@ -1765,6 +1772,7 @@ public:
         // 2. items by level, chunked: members <= kMaxMembers, sources x digits <= kMaxConvGroups
         std::map<int, std::vector<int>> by_level;
         for (int i = 0; i < n; ++i) {
+            if (done[i]) continue;
             const KsSrc& s = src_of.at(C[i]->data);
             if (G[i] == 1) {  // identity: a copy of the canonical source
                 Ct o = alloc_ct(s.level, 2);

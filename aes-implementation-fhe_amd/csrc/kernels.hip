@@ -1079,22 +1079,55 @@ __device__ __forceinline__ void lin_mac_body(const LinMacArgs& m, int nl, int ne
         }
     }
 }
+// XCD-aware block -> (column block, row) map of a (nbx x rows) grid: workgroups are dealt
+// round-robin over the 8 XCDs (linear id b and b + 8 share one, MI355X_MICROARCH.md "Workgroup
+// dispatch"), so with the plain map the nbx blocks of one row land on all 8 XCDs and EVERY XCD
+// fetches the whole gathered source row into its own L2.  Here the blocks of one row sit on one
+// XCD: rows are taken in bands of 8, row 8 band + (b mod 8) <- blocks b with b / 8 in the band's
+// range; a last partial band keeps the plain map.  A bijection either way (speed only).
+__device__ __forceinline__ void xcd_rows(int lognbx, int rows, int& bx, int& row) {
+    const int nbx = 1 << lognbx;
+    const int id = blockIdx.x + (blockIdx.y << lognbx);
+    const int full = rows & ~7;
+    if (id < (full << lognbx)) {
+        const int m = id >> 3;
+        bx = m & (nbx - 1);
+        row = ((m >> lognbx) << 3) + (id & 7);
+    } else {
+        const int r = id - (full << lognbx);
+        bx = r & (nbx - 1);
+        row = full + (r >> lognbx);
+    }
+}
+
 template <int NB, int ND>
-__global__ void __launch_bounds__(kBlock) k_lin_mac(LinMacArgs m, int nl, int ne, LimbMap map, const PrimeConst* pc, int logn) {
-    const int t = blockIdx.y;
-    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+__global__ void __launch_bounds__(kBlock) k_lin_mac(LinMacArgs m, int nl, int ne, LimbMap map, const PrimeConst* pc, int logn, int xcd) {
+    int t = blockIdx.y, bx = blockIdx.x;
+    // the baby steps gather c0 and ext of row t through B different automorphisms: one XCD per row
+    if (xcd) xcd_rows(logn - 8, ne, bx, t);
+    const size_t k = (size_t)bx * kBlock + threadIdx.x;
     const PrimeConst P = pc[map.prime(t)];
     lin_mac_body<NB, ND>(m, nl, ne, P, t, k, logn);
 }
+// AESFHE_XCD_ROWS=0: the plain block map (A/B runs)
+inline int xcd_rows_on() {
+    static const int v = [] {
+        const char* e = std::getenv("AESFHE_XCD_ROWS");
+        return e ? std::atoi(e) : 1;
+    }();
+    return v;
+}
 template <int NB>
 void launch_lin_mac_nb(hipStream_t st, const DevTables& T, const LinMacArgs& m, int nl, int ne, LimbMap map, double bytes) {
+    static_assert(kBlock == 256, "xcd_rows assumes N / 256 column blocks");
     const dim3 g = ew_grid(T.logn, ne), b(kBlock);
+    const int xcd = xcd_rows_on();
     switch (m.nd) {  // the digit counts of the bootstrap plans (dnum <= 8); others take the run-time loop
 #define LIN_MAC_ND(D) \
-    case D: prof_launch(KID_LIN_MAC, bytes, k_lin_mac<NB, D>, g, b, 0, st, m, nl, ne, map, T.pc, T.logn); break;
+    case D: prof_launch(KID_LIN_MAC, bytes, k_lin_mac<NB, D>, g, b, 0, st, m, nl, ne, map, T.pc, T.logn, xcd); break;
         LIN_MAC_ND(1) LIN_MAC_ND(2) LIN_MAC_ND(3) LIN_MAC_ND(4) LIN_MAC_ND(5) LIN_MAC_ND(6) LIN_MAC_ND(7) LIN_MAC_ND(8)
 #undef LIN_MAC_ND
-        default: prof_launch(KID_LIN_MAC, bytes, k_lin_mac<NB, 0>, g, b, 0, st, m, nl, ne, map, T.pc, T.logn);
+        default: prof_launch(KID_LIN_MAC, bytes, k_lin_mac<NB, 0>, g, b, 0, st, m, nl, ne, map, T.pc, T.logn, xcd);
     }
 }
 }  // namespace

@@ -14,6 +14,7 @@ and the whole LUT is S1 + conj(S2) over the positive powers of a and the standar
 b: a needs no conjugations at all, only the powers the coefficients use are formed (x^6 and
 x^8 are skipped for XOR4), and each S is one fused kernel.  Output level unchanged.
 """
+import os
 from typing import Any, Dict
 
 import numpy as np
@@ -82,11 +83,28 @@ def _depth(k: int) -> int:
     return (k - 1).bit_length()  # ceil(log2 k): the multiplicative depth of x^k
 
 
+# AESFHE_CONJ_CHAIN=0: the std basis' mirrors as conjugations of the powers (one key switch per
+# mirror, at three levels) instead of powers of the conjugated input (A/B runs)
+_CONJ_CHAIN = os.environ.get("AESFHE_CONJ_CHAIN", "1") != "0"
+
+
 def joint_bases(ctx, specs):
     """[(ct, need, kind)] -> [{k: element}], kind "pow" (powers(), x^k) or "std" (std_basis():
-    conj(x^(16-q)) for q >= 9).  The products of one depth across ALL inputs form one
-    mul_many batch and every conjugation one conj_many batch; the elements
-    equal powers() / std_basis() of each input."""
+    the mirrors conj(x)^(16-q) for q >= 9).  The products of one depth across ALL inputs form
+    one mul_many batch.  The mirrors: x is conjugated ONCE (all inputs' in one
+    conj_many) and its powers join the same product batches -- one key switch per input at its
+    own level instead of one per mirror at three levels (conj(x)^k = conj(x^k): same values,
+    same depth); AESFHE_CONJ_CHAIN=0 conjugates the powers instead."""
+    if _CONJ_CHAIN and any(kind == "std" and any(q >= 9 for q in need) for _, need, kind in specs):
+        std = [i for i, (_, need, kind) in enumerate(specs) if kind == "std" and any(q >= 9 for q in need)]
+        bars = conj_many(ctx, [specs[i][0] for i in std])
+        ext = [(ct, {q for q in need if q <= 8} if kind == "std" else need, "pow") for ct, need, kind in specs]
+        ext += [(bar, {16 - q for q in specs[i][1] if q >= 9}, "pow") for i, bar in zip(std, bars)]
+        got = joint_bases(ctx, ext)
+        out = got[:len(specs)]
+        for j, i in enumerate(std):
+            out[i].update({16 - k: v for k, v in got[len(specs) + j].items()})
+        return out
     needs = [set(need) if kind == "pow" else {q if q <= 8 else 16 - q for q in need} for _, need, kind in specs]
     pws = [{1: ct} for ct, _, _ in specs]
     chains = [_chain(n) for n in needs]
