@@ -3354,9 +3354,28 @@ private:
                 ip = ip * iw % q;
             }
         }
+        // the inverse pass 2's factored twiddles (ntt.hip k_ntt2_inv): stage s, row R, word
+        // offset t: psi^-(2^(7-s) (2 brv(R) + 1)) * psi^-((N / 2^s) brv_s(t)) = itw[2^(logn-8+s) + R 2^s + t]
+        const int r1 = n >> 8, logr1 = logn - 8;
+        std::vector<uint2> irow((size_t)nt * r1 * 4, make_uint2(0u, 0u)), igam((size_t)nt * 256, make_uint2(0u, 0u));
+        for (int i = 0; i < nt; ++i) {
+            const u32 q = hp_.mod[i], iw = hinvm(hp_.psi[i], q);
+            for (int R = 0; R < r1; ++R)
+                for (int s = 5; s <= 7; ++s) {
+                    const u32 v = hpowm(iw, (uint64_t)(1u << (7 - s)) * (2u * hbitrev((u32)R, logr1) + 1u), q);
+                    irow[((size_t)i * r1 + R) * 4 + (s - 5)] = make_uint2(v, shoup_pre(v, q));
+                }
+            for (int s = 5; s <= 7; ++s)
+                for (int t = 0; t < (1 << s); ++t) {
+                    const u32 v = hpowm(iw, (uint64_t)(n >> s) * hbitrev((u32)t, s), q);
+                    igam[(size_t)i * 256 + (1 << s) + t] = make_uint2(v, shoup_pre(v, q));
+                }
+        }
         T_.pc = dev_upload(pc);
         T_.tw = dev_upload(tw);
         T_.itw = dev_upload(itw);
+        T_.irow = dev_upload(irow);
+        T_.igam = dev_upload(igam);
         T_.logn = logn;
 
         const auto& q = hp_.mod;

@@ -55,6 +55,9 @@ struct DevTables {
     const PrimeConst* pc = nullptr;  // [n_tot]
     const uint2* tw = nullptr;       // [n_tot][N]  {-psi^{bitrev(k)} mod 2^32, Shoup companion of psi^{bitrev(k)}}: one 8-byte load per twiddle
     const uint2* itw = nullptr;      // [n_tot][N]  {psi^{-bitrev(k)}, Shoup companion}
+    // inverse pass 2, stages 5..7 as twiddle = row factor x shared factor (ntt.hip k_ntt2_inv):
+    const uint2* irow = nullptr;     // [n_tot][R1][4]  {psi^{-2^(7-s) (2 bitrev(R) + 1)}, companion} at [s - 5]
+    const uint2* igam = nullptr;     // [n_tot][256]    {psi^{-(N / 2^s) bitrev_s(t)}, companion} at [2^s + t]
     int logn = 16;
 };
 

@@ -56,6 +56,15 @@ __device__ __forceinline__ void gs_bfly(u32& a, u32& b, u32 w, u32 wp, u32 q2, u
     const u32 d = u - v + q2;                                         // (0, 4q)
     b = (u32)((u64)mulhi32(d, wp) * nq + (u32)(d * w));              // d w - floor(d w'/2^32) q in [0, 2q)
 }
+// the inverse butterfly with its twiddle as a product g r (two lazy Shoup products, each in
+// [0, 2q) for any 32-bit input): k_ntt2_inv's factored stages
+__device__ __forceinline__ void gs_bfly2(u32& a, u32& b, uint2 g, uint2 r, u32 q2, u32 nq) {
+    const u32 u = a, v = b;
+    a = red2(u + v, q2);
+    const u32 d = u - v + q2;
+    const u32 e = (u32)((u64)mulhi32(d, g.y) * nq + (u32)(d * g.x));
+    b = (u32)((u64)mulhi32(e, r.y) * nq + (u32)(e * r.x));
+}
 __device__ __forceinline__ int swz(int w) { return w ^ ((w >> 4) & 15); }
 
 enum { kPlain = 0, kSpread = 1, kFinish = 1, kSpread2 = 2 };
@@ -70,6 +79,8 @@ inline int small_rows_limit() {
     return v;
 }
 inline bool small_launch(int rows) { return rows < small_rows_limit(); }
+template <int LOGR1>
+constexpr int R1_of() { return 1 << LOGR1; }
 
 // key-switching ModUp: digit g's own limbs [g alpha, min(nl, (g + 1) alpha)) are not
 // transformed (they are already in NTT form in the input); block-uniform early exit
@@ -264,9 +275,14 @@ __global__ void __launch_bounds__(NT) k_ntt2_fwd(u32* data, RowMap rm, LimbMap m
 }
 
 // ---------------------------------------------------------------- inverse, pass 2 (src -> dst)
-template <int LOGR1, int NT>
+// FACT: stages 7, 6, 5 (255 - 31 of a row's 255 twiddles, each thread its own) read their
+// twiddle as (row factor) x (shared factor): psi^-(2^(7-s) (2 brv(R) + 1)) -- three per row --
+// times psi^-((N / 2^s) brv_s(t)) -- 224 per prime, shared by every row, L1 / L2 resident --
+// one more lazy Shoup product per butterfly of those stages instead of 8 twiddle bytes, so the
+// launch reads ~280 twiddle bytes per 1 KB row instead of 2 KB
+template <int LOGR1, int NT, bool FACT>
 __global__ void __launch_bounds__(NT) k_ntt2_inv(u32* dst, const u32* src, RowMap rm, LimbMap map, const PrimeConst* pc,
-                                                       const uint2* tw, unsigned long long* ts) {
+                                                       const uint2* tw, const uint2* irow, const uint2* igam, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8;
     __shared__ u32 sm[(NT / 16) * kPitchP2];
     if (skipped(rm)) return;
@@ -283,10 +299,19 @@ __global__ void __launch_bounds__(NT) k_ntt2_inv(u32* dst, const u32* src, RowMa
         const uint4 t = in[v];
         x[4 * v] = t.x, x[4 * v + 1] = t.y, x[4 * v + 2] = t.z, x[4 * v + 3] = t.w;
     }
+    const uint2* rowf = irow + ((size_t)ra.prime << LOGR1) * 4 + (size_t)R * 4;
+    const uint2* gam = igam + ((size_t)ra.prime << 8);
 #pragma unroll
     for (int s = 7; s >= 4; --s) {
         const int h = 1 << (7 - s);
         const int base = (1 << (LOGR1 + s)) + (R << s);
+        if (FACT && s >= 5) {
+            const uint2 rf = rowf[s - 5];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (!(k & h)) gs_bfly2(x[k], x[k + h], gam[(1 << s) + ((16 * j + k) >> (8 - s))], rf, q2, 0u - q);
+            continue;
+        }
 #pragma unroll
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
@@ -390,6 +415,25 @@ void ntt_fwd_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
     prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2, kThreads>, dim3(R1 / kRowsP2, rm.cnt, groups), dim3(kThreads), 0, st,
                     dst, rm, map, Tb.pc, Tb.tw, aux);
 }
+// AESFHE_NTT_INV_FACT=0: the inverse pass 2 reads every twiddle from the table (A/B runs)
+inline bool inv_fact_on() {
+    static const bool v = [] {
+        const char* e = std::getenv("AESFHE_NTT_INV_FACT");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
+template <int LOGR1, int NT>
+void ntt2_inv_launch(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, RowMap rm, LimbMap map, int groups, double io,
+                     double work) {
+    const dim3 grid(R1_of<LOGR1>() / (NT / 16), rm.cnt, groups);
+    if (inv_fact_on())
+        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, true>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
+                        Tb.irow, Tb.igam);
+    else
+        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, false>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
+                        Tb.irow, Tb.igam);
+}
 template <int LOGR1>
 void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {
     constexpr int R1 = 1 << LOGR1;
@@ -399,15 +443,13 @@ void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
     const double bfly = (double)rows * 128.0 * R1;
     if (small_launch(rows)) {
         constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
-        prof_launch_tsw(KID_NTT_ROWS_INV, io, bfly * 8.0, k_ntt2_inv<LOGR1, NT>, dim3(R1 / (NT / 16), rm.cnt, groups), dim3(NT), 0, st, dst, src, rm,
-                        map, Tb.pc, Tb.itw);
+        ntt2_inv_launch<LOGR1, NT>(st, Tb, dst, src, rm, map, groups, io, bfly * 8.0);
         prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, dst, rm, map,
                         Tb.pc, Tb.itw);
         return;
     }
     constexpr int CB = kThreads / (R1 / 16);
-    prof_launch_tsw(KID_NTT_ROWS_INV, io, bfly * 8.0, k_ntt2_inv<LOGR1, kThreads>, dim3(R1 / kRowsP2, rm.cnt, groups), dim3(kThreads), 0, st, dst, src,
-                    rm, map, Tb.pc, Tb.itw);
+    ntt2_inv_launch<LOGR1, kThreads>(st, Tb, dst, src, rm, map, groups, io, bfly * 8.0);
     prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, kThreads>, dim3(256 / CB, rm.cnt, groups), dim3(kThreads), 0, st, dst, rm,
                     map, Tb.pc, Tb.itw);
 }

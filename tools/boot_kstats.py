@@ -1,5 +1,6 @@
 """Per-kernel-id time and algorithmic bytes of one bootstrap (engine profiler, every launch
-timed): where the bootstrap's time goes and how close each kernel class runs to HBM peak."""
+timed): where the bootstrap's time goes and how close each kernel class runs to HBM peak.
+usage: python tools/boot_kstats.py [--pair | --sparse P]"""
 import json
 import sys
 from pathlib import Path
@@ -18,8 +19,16 @@ def main(n=5):
     E = ctx.engine
     z = np.exp(2j * np.pi * np.random.default_rng(0).random(E.slot_count))
     ct = E.intt(ctx.encrypt(z))
-    pair = "--pair" in sys.argv  # the batched hi / lo bootstrap C2 uses
-    boot = (lambda: E.bootstrap_pair(ct, ct)) if pair else (lambda: E.bootstrap(ct))
+    pair = "--pair" in sys.argv  # the batched hi / lo bootstrap
+    # --sparse P: the sparse-slot bootstrap at period P (C2's MixColumns final bootstrap: one
+    # packed ciphertext, P = 2 x 16 = 32); the input is made P-periodic
+    sp = int(sys.argv[sys.argv.index("--sparse") + 1]) if "--sparse" in sys.argv else 0
+    if sp:
+        z = np.tile(z[:sp], E.slot_count // sp)
+        ct = E.intt(ctx.encrypt(z))
+        boot = lambda: E.bootstrap_sparse(ct, sp)  # noqa: E731
+    else:
+        boot = (lambda: E.bootstrap_pair(ct, ct)) if pair else (lambda: E.bootstrap(ct))
     boot()
     E.sync()
     E.profile(list(KERNEL_IDS), every=1)
