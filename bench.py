@@ -81,7 +81,7 @@ def parse():
                     help="with AESFHE_PROFILE_FROM_START=<ids>: keep the engine's per-kernel accounting from the first "
                          "launch on (no reset, every launch) and write it to this JSON file -- the algorithmic bytes of "
                          "exactly the launches a whole-process rocprofv3 --pmc pass counts")
-    ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r2_pmc_traffic_round.json"),
+    ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r3_pmc_traffic_round.json"),
                     help="per-kernel HBM/algorithmic byte ratios from rocprofv3 PMC passes (tools/r2_pmc_filtered.sh)")
     return ap.parse_args()
 
