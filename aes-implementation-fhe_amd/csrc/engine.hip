@@ -518,12 +518,13 @@ public:
     // all of them, ONE combine, ONE rescale of the stacked result (nb = B) -- the same residues as
     // B encrypt_ntt calls (same PRNG streams, same arithmetic), 8 launches instead of 14 B
     Ct encrypt_many(const u32* m, int B, size_t m_ms, int level = -1) {
-        if (B < 1 || B > kEncMax) throw std::runtime_error("encrypt_many: 1..4 messages");
+        if (B < 1 || B > kEncMax) throw std::runtime_error("encrypt_many: batch too large");
         const int f = level < 0 ? hp_.fresh : level;
         const int nq = hp_.nl(f) + 1;
         u32* vee = tmp((size_t)B * 3 * nq);
         EncCtrs ec;
-        for (int b = 0; b < B; ++b) ec.ctr[b] = enc_ctr_++;
+        ec.base = enc_ctr_;  // member b: counter base + b, as B single encryptions in a row
+        enc_ctr_ += B;
         launch_sample_enc(S(), T_, vee, nq, B, enc_key(), ec);
         ntt(vee, B * 3 * nq, nq, qmap());
         Ct top = alloc_ct(f + 1, 2 * B, B);
@@ -601,6 +602,7 @@ public:
         return scale;
     }
     void decrypt(aesfhe_handle h, double* re, double* im) {
+        if (ct(h).nb != 1) throw std::runtime_error("decrypt: a stacked ciphertext (unstack it first)");
         std::vector<double> m;
         const double inv = 1.0 / decrypt_coeffs(ct(h), m);
         for (double& v : m) v *= inv;
@@ -949,10 +951,19 @@ public:
         }
         const int nl = hp_.nl(x.level);
         const int np = std::max(x.npoly, y.npoly);
-        if (x.nb > 1 && x.npoly != y.npoly) throw std::runtime_error("add_sub: batched operands with different polynomial counts");
         Ct o = alloc_ct(x.level, np, x.nb);
         o.pend = x.pend;
         o.lazy = x.lazy || y.lazy;
+        if (x.nb > 1 && x.npoly != y.npoly) {  // stacks of a deferred tensor and a ciphertext: per member
+            const int px = pm(x), py = pm(y), po = pm(o);
+            const size_t rw = (size_t)nl * hp_.n;
+            for (int m = 0; m < x.nb; ++m)
+                launch_addsub_tail(S(), T_, o.data + m * po * rw, x.data + m * px * rw, y.data + m * py * rw, std::min(px, py) * nl, po * nl,
+                                   px > py, sub, nl, qmap());
+            if (fa) release(x);
+            if (fb) release(y);
+            return o;
+        }
         const int common = std::min(x.npoly, y.npoly) * nl;
         if (x.zero && x.npoly == y.npoly) {
             launch_neg(S(), T_, o.data, y.data, common, nl, qmap());
@@ -1013,7 +1024,7 @@ public:
         cnt_[C_SCALAR]++;
         const bool gauss = re == std::floor(re) && im == std::floor(im) && std::fabs(re) < 1048576.0 && std::fabs(im) < 1048576.0;
         if (!gauss && c_in.level - c_in.pend < 1) throw std::runtime_error("not enough level to multiply by a scalar (level 0)");
-        if (c_in.zero) return gauss ? copy(c_in) : zero_ct(c_in.level - c_in.pend - 1);
+        if (c_in.zero) return gauss ? copy(c_in) : zero_ct(c_in.level - c_in.pend - 1, c_in.nb);
         if (gauss) {
             Ct c = ensure_ntt(c_in);
             const int nl = hp_.nl(c.level);
@@ -1078,7 +1089,7 @@ public:
         if (p.constant) return mul_scalar(c_in, p.re[0], p.im[0], allow_lazy);
         if (c_in.level - c_in.pend < 1) throw std::runtime_error("not enough level to multiply by a plaintext (level 0)");
         cnt_[C_PTMUL]++;
-        if (c_in.zero) return zero_ct(c_in.level - c_in.pend - 1);
+        if (c_in.zero) return zero_ct(c_in.level - c_in.pend - 1, c_in.nb);
         bool own;
         Ct c = upto_one_pend(c_in, own);
         Ct o;
@@ -1093,10 +1104,10 @@ public:
             Ct nc = normalize(c, false);
             const int nl = hp_.nl(nc.level);
             u32* e = pt_at(p, nc.level, 1);
-            Ct t = alloc_ct(nc.level, nc.npoly);
+            Ct t = alloc_ct(nc.level, nc.npoly, nc.nb);
             launch_mul_poly(S(), T_, t.data, nc.data, e, nc.npoly, nl, qmap());
             o = rescale(t);
-            o.lazy = c_in.lazy && o.npoly == 3;
+            o.lazy = c_in.lazy && pm(o) == 3;
             release(t);
             if (nc.data != c.data) release(nc);
         }
@@ -1112,8 +1123,11 @@ public:
         u32* e = pt_at(p, c.level, 0);
         Ct o = copy(c);
         o.zero = false;
-        o.lazy = c_in.lazy && o.npoly == 3;
-        launch_add(S(), T_, o.data, c.data, e, nl, nl, qmap());
+        o.lazy = c_in.lazy && pm(o) == 3;
+        for (int m = 0; m < c.nb; ++m) {  // c0 of every stacked member
+            const size_t off = (size_t)m * pm(c) * nl * hp_.n;
+            launch_add(S(), T_, o.data + off, c.data + off, e, nl, nl, qmap());
+        }
         if (c.data != c_in.data) release(c);
         return o;
     }
@@ -1182,8 +1196,10 @@ public:
         for (auto* e : ea) if (e) l = std::min(l, e->level);
         for (auto* e : eb) if (e) l = std::min(l, e->level);
         if (l == (1 << 30)) throw std::runtime_error("lut_eval: all coefficients are zero");
-        for (auto* e : ea) if (e && e->npoly != 2) throw std::runtime_error("lut_eval expects 2-polynomial ciphertexts");
-        for (auto* e : eb) if (e && e->npoly != 2) throw std::runtime_error("lut_eval expects 2-polynomial ciphertexts");
+        int members = 0;  // stacked elements: every element a stack of the same member count
+        for (auto* e : ea) if (e) members = members ? members : e->nb;
+        for (auto* e : ea) if (e && (pm(*e) != 2 || e->nb != members)) throw std::runtime_error("lut_eval expects 2-polynomial ciphertexts (stacks of one size)");
+        for (auto* e : eb) if (e && (pm(*e) != 2 || e->nb != members)) throw std::runtime_error("lut_eval expects 2-polynomial ciphertexts (stacks of one size)");
         const int pend = bi ? 2 : 1;
         if (l - pend < 0 || !headroom(l, pend, mag)) throw std::runtime_error("not enough level for the fused LUT (level)");
         const int nl = hp_.nl(l);
@@ -1210,20 +1226,20 @@ public:
             for (int p = L.n_a; p <= kLutMax; ++p) op.p_start[p] = j;
             for (int q = 0; q < L.n_b; ++q) op.b[q] = eb[q] ? eb[q]->data : nullptr, op.nb[q] = eb[q] ? hp_.nl(eb[q]->level) : 0;
             const u32* cst = lut_consts(L, key, terms, nl);
-            o = alloc_ct(l, 3);
-            launch_lut_bivariate(S(), T_, o.data, op, L.n_a, cst, nl);
+            o = alloc_ct(l, 3 * members, members);
+            launch_lut_bivariate(S(), T_, o.data, op, L.n_a, cst, nl, members);
         } else {
             std::vector<std::pair<int, double>> terms;
             std::vector<int> idx;
             for (int p = 0; p < L.n_a; ++p)
                 if (ea[p]) terms.push_back({p, S_out / hp_.delta[ea[p]->level]}), idx.push_back(p);
             const u32* cst = lut_consts(L, key, terms, nl);
-            o = alloc_ct(l, 2);
+            o = alloc_ct(l, 2 * members, members);
             for (size_t c0 = 0; c0 < idx.size(); c0 += kLutChunk) {
                 LutChunk ch{};
                 const int n = (int)std::min<size_t>(kLutChunk, idx.size() - c0);
                 for (int j = 0; j < n; ++j) ch.x[j] = ea[idx[c0 + j]]->data, ch.nx[j] = hp_.nl(ea[idx[c0 + j]]->level);
-                launch_lut_univariate(S(), T_, o.data, c0 ? o.data : nullptr, ch, n, cst + c0 * (size_t)nl * 4, 2, nl);
+                launch_lut_univariate(S(), T_, o.data, c0 ? o.data : nullptr, ch, n, cst + c0 * (size_t)nl * 4, 2, nl, members);
             }
         }
         o.pend = pend;
@@ -1285,7 +1301,8 @@ public:
     // ModDown by P: coefficients of the P rows (read in place from acc), conversion of both
     // polys in one launch, NTT fused with (acc_Q - conv) P^{-1} (+ add)
     // nb batched ciphertexts: acc = [m][2][ne]; member m adds add0/add1 + m add_ms words
-    Ct moddown(const u32* acc, int level, const u32* add0, const u32* add1, int nb = 1, size_t add_ms = 0) {
+    // dst: write the result there (member stride 2 nl N; the caller owns it) instead of a new buffer
+    Ct moddown(const u32* acc, int level, const u32* add0, const u32* add1, int nb = 1, size_t add_ms = 0, u32* dst = nullptr) {
         const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, npl = 2 * nb;
         if (npl > kMaxConvGroups) throw std::runtime_error("moddown: batch too large");
         u32* yp = tmp((size_t)npl * np);
@@ -1303,7 +1320,12 @@ public:
             dn.negq[p] = d_negp_;
         }
         launch_base_convert(S(), T_, dn, nl, qmap());
-        Ct o = alloc_ct(level, npl, nb);
+        Ct o;
+        if (dst) {
+            o.level = level, o.npoly = npl, o.nb = nb, o.words = (size_t)npl * nl * n, o.data = dst;
+        } else {
+            o = alloc_ct(level, npl, nb);
+        }
         launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_pinv_, add0, add1, npl, nl, add_ms);
         cnt_[C_NTT_ROWS] += (size_t)npl * nl;
         untmp(yp, (size_t)npl * np);
@@ -1312,14 +1334,31 @@ public:
     }
     // key switch of d (nl rows); nb > 1: the d polynomials of nb batched ciphertexts (d + m d_ms
     // words, add0 / add1 + m add_ms), one key read for all of them -> (c0', c1') per member
+    // A stack of more members than one batched key switch carries (ks_chunk) goes through in
+    // chunks, each chunk's ModDown writing its rows of the one stacked result.
     Ct keyswitch(const u32* d, int level, const u32* key, const u32* add0, const u32* add1, int nb = 1, size_t d_ms = 0,
-                 size_t add_ms = 0) {
-        const int ne = hp_.nl(level) + hp_.n_p;
+                 size_t add_ms = 0, u32* dst = nullptr) {
+        const int ne = hp_.nl(level) + hp_.n_p, ch = ks_chunk(level);
+        if (nb > ch) {
+            Ct o;
+            if (dst) {
+                o.level = level, o.npoly = 2 * nb, o.nb = nb, o.words = (size_t)2 * nb * hp_.nl(level) * hp_.n, o.data = dst;
+            } else {
+                o = alloc_ct(level, 2 * nb, nb);
+            }
+            const size_t oms = (size_t)2 * hp_.nl(level) * hp_.n;
+            for (int m0 = 0; m0 < nb; m0 += ch) {
+                const int c = std::min(ch, nb - m0);
+                keyswitch(d + m0 * d_ms, level, key, add0 ? add0 + m0 * add_ms : nullptr, add1 ? add1 + m0 * add_ms : nullptr, c, d_ms, add_ms,
+                          o.data + m0 * oms);
+            }
+            return o;
+        }
         u32* ext = modup(d, level, nb, d_ms);
         u32* acc = tmp(2 * (size_t)ne * nb);
         key_inner(acc, ext, d, key, level, 0, nb, d_ms);
         untmp(ext, (size_t)nb * ext_rows(level));
-        Ct o = moddown(acc, level, add0, add1, nb, add_ms);
+        Ct o = moddown(acc, level, add0, add1, nb, add_ms, dst);
         untmp(acc, 2 * (size_t)ne * nb);
         cnt_[C_KS] += nb;
         return o;
@@ -1394,18 +1433,36 @@ public:
     }
     bool fused_relin_rescale_ok(const Ct& c) const {
         if (!fuse_rr_ || pm(c) != 3 || c.pend < 1 || c.level < 1 || c.zero) return false;
-        return mdr_off_[c.level] != SIZE_MAX && 2 * c.nb <= kMaxConvGroups && c.nb <= ks_chunk(c.level);
+        return mdr_off_[c.level] != SIZE_MAX && 2 * ks_chunk(c.level) <= kMaxConvGroups;
     }
+    // a stack of more than ks_chunk members in chunks, each chunk's ModDown writing its rows of
+    // the one stacked result
     Ct relin_rescale(const Ct& c) {
-        const int l = c.level, n = hp_.n, nl = hp_.nl(l), ne = nl + hp_.n_p, nb = c.nb;
+        const int l = c.level, n = hp_.n, nl = hp_.nl(l), ne = nl + hp_.n_p, nb = c.nb, ch = ks_chunk(l);
         const size_t ms = (size_t)3 * nl * n;
-        const u32* d2 = c.data + (size_t)2 * nl * n;
-        u32* ext = modup(d2, l, nb, ms);
-        u32* acc = tmp(2 * (size_t)ne * nb);
-        key_inner(acc, ext, d2, ksk(0), l, 0, nb, ms, KsFold{c.data, c.data + (size_t)nl * n, ms, d_gadget_});
-        untmp(ext, (size_t)nb * ext_rows(l));
-        Ct o = moddown_rescale(acc, l, nb);
-        untmp(acc, 2 * (size_t)ne * nb);
+        Ct o;
+        if (nb > ch) {
+            o = alloc_ct(l - 1, 2 * nb, nb);
+            const size_t oms = (size_t)2 * hp_.nl(l - 1) * n;
+            for (int m0 = 0; m0 < nb; m0 += ch) {
+                const int k = std::min(ch, nb - m0);
+                const u32* base = c.data + m0 * ms;
+                u32* ext = modup(base + (size_t)2 * nl * n, l, k, ms);
+                u32* acc = tmp(2 * (size_t)ne * k);
+                key_inner(acc, ext, base + (size_t)2 * nl * n, ksk(0), l, 0, k, ms, KsFold{base, base + (size_t)nl * n, ms, d_gadget_});
+                untmp(ext, (size_t)k * ext_rows(l));
+                moddown_rescale(acc, l, k, o.data + m0 * oms);
+                untmp(acc, 2 * (size_t)ne * k);
+            }
+        } else {
+            const u32* d2 = c.data + (size_t)2 * nl * n;
+            u32* ext = modup(d2, l, nb, ms);
+            u32* acc = tmp(2 * (size_t)ne * nb);
+            key_inner(acc, ext, d2, ksk(0), l, 0, nb, ms, KsFold{c.data, c.data + (size_t)nl * n, ms, d_gadget_});
+            untmp(ext, (size_t)nb * ext_rows(l));
+            o = moddown_rescale(acc, l, nb);
+            untmp(acc, 2 * (size_t)ne * nb);
+        }
         o.pend = c.pend - 1;
         o.lazy = c.lazy && o.pend > 0;
         cnt_[C_KS] += nb;
@@ -1414,7 +1471,7 @@ public:
     }
     // acc = [m][2][ne] in Q*P, NTT form, already holding P * (the ciphertext) -> the ciphertext
     // divided by the dropped limbs of level l, at level l - 1 (one ModDown by Q' = P * D)
-    Ct moddown_rescale(const u32* acc, int l, int nb) {
+    Ct moddown_rescale(const u32* acc, int l, int nb, u32* dst = nullptr) {
         const int n = hp_.n, nl = hp_.nl(l), r = hp_.nl(l - 1), k = nl - r, np = hp_.n_p, ne = nl + np;
         const int npl = 2 * nb, h = k + np;
         if (mdr_off_[l] == SIZE_MAX || npl > kMaxConvGroups) throw std::runtime_error("moddown_rescale: unsupported level or batch");
@@ -1434,7 +1491,12 @@ public:
         }
         launch_base_convert(S(), T_, cb, r, qmap());
         untmp(ys, (size_t)npl * h);
-        Ct o = alloc_ct(l - 1, npl, nb);
+        Ct o;
+        if (dst) {
+            o.level = l - 1, o.npoly = npl, o.nb = nb, o.words = (size_t)npl * r * n, o.data = dst;
+        } else {
+            o = alloc_ct(l - 1, npl, nb);
+        }
         launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_mdr_ + off + 2 * (size_t)h * (r + 1) + r, nullptr, nullptr, npl, r);
         cnt_[C_NTT_ROWS] += (size_t)npl * r;
         untmp(conv, (size_t)npl * r);
@@ -1656,6 +1718,74 @@ public:
         }
         launch_copy_members(S(), T_, mp, c, per * nlo);
     }
+    // ------------------------------------------------------------------ stacked ciphertexts (multi-pair batches)
+    // n single ciphertexts -> ONE stacked ciphertext (nb = n members, [m][2][nl] rows): canonical
+    // form, dropped to the lowest member level.  Every op then treats the stack as one operand:
+    // element-wise launches cover all members' rows, key switches read each key once per chunk
+    // of ks_chunk members, LUT sums take a member grid dimension.
+    Ct stack(const std::vector<const Ct*>& C) {
+        const int n = (int)C.size();
+        if (n < 1) throw std::runtime_error("stack: no ciphertexts");
+        std::vector<Ct> cn(n);
+        std::vector<bool> own(n);
+        int lv = 1 << 30;
+        for (int i = 0; i < n; ++i) {
+            if (C[i]->nb != 1) throw std::runtime_error("stack: members must be single ciphertexts");
+            cn[i] = normalize(*C[i]);
+            own[i] = cn[i].data != C[i]->data;
+            if (pm(cn[i]) != 2) throw std::runtime_error("stack: 2-polynomial ciphertexts expected");
+            lv = std::min(lv, cn[i].level);
+        }
+        for (int i = 0; i < n; ++i)
+            if (cn[i].level != lv) {
+                Ct t = level_down(cn[i], lv);
+                if (own[i]) release(cn[i]);
+                cn[i] = t, own[i] = true;
+            }
+        const int nl = hp_.nl(lv), nn = hp_.n;
+        Ct st = alloc_ct(lv, 2 * n, n);
+        st.ntt = true;
+        for (int m0 = 0; m0 < n; m0 += kMaxMembers) {
+            const int c = std::min(kMaxMembers, n - m0);
+            MemberPtrs mp;
+            for (int m = 0; m < c; ++m) mp.src[m] = cn[m0 + m].data, mp.dst[m] = st.data + (size_t)(m0 + m) * 2 * nl * nn;
+            launch_copy_members(S(), T_, mp, c, 2 * nl);
+        }
+        for (int i = 0; i < n; ++i)
+            if (own[i]) release(cn[i]);
+        return st;
+    }
+    // the members of a stack as single canonical ciphertexts
+    std::vector<Ct> unstack_all(const Ct& c_in) {
+        Ct c = normalize(c_in);
+        const int nb = c.nb, per = pm(c), nl = hp_.nl(c.level), nn = hp_.n;
+        std::vector<Ct> out(nb);
+        for (int m0 = 0; m0 < nb; m0 += kMaxMembers) {
+            const int k = std::min(kMaxMembers, nb - m0);
+            MemberPtrs mp;
+            for (int m = 0; m < k; ++m) {
+                Ct r = alloc_ct(c.level, per);
+                copy_meta(r, c);
+                r.nb = 1;
+                mp.src[m] = c.data + (size_t)(m0 + m) * per * nl * nn;
+                mp.dst[m] = r.data;
+                out[m0 + m] = r;
+            }
+            launch_copy_members(S(), T_, mp, k, per * nl);
+        }
+        if (c.data != c_in.data) release(c);
+        return out;
+    }
+    // rows [m0, m0 + cnt) of a canonical stack as a stack of their own (a copy)
+    Ct members_of(const Ct& c, int m0, int cnt) {
+        const int per = pm(c), nl = hp_.nl(c.level);
+        Ct o = alloc_ct(c.level, per * cnt, cnt);
+        copy_meta(o, c);
+        o.nb = cnt;
+        launch_copy_rows(S(), T_, o.data, c.data + (size_t)m0 * per * nl * hp_.n, (size_t)cnt * per * nl);
+        return o;
+    }
+
     // X -> X^g of n independent ciphertexts: canonical inputs at one level are stacked and key
     // switched together (chunks of kMaxKsBatch); results equal n galois() calls
     std::vector<Ct> galois_many(const std::vector<const Ct*>& C, u64 g) {
@@ -1717,6 +1847,15 @@ public:
         for (u64 g : G)
             if (!(g & 1) || g >= two_n) throw std::runtime_error("galois_multi: Galois elements must be odd and below 2N");
         std::vector<Ct> out(n);
+        bool stacked = false;
+        for (const Ct* c : C) stacked = stacked || c->nb != 1;
+        if (stacked) {  // stacks: one galois() each (every member of a stack in one key switch)
+            for (int i = 0; i < n; ++i) {
+                if (G[i] == 1) { Ct cn = normalize(*C[i]); out[i] = cn.data != C[i]->data ? cn : copy(cn); continue; }
+                out[i] = galois(*C[i], G[i]);
+            }
+            return out;
+        }
         std::vector<Ct> owned;                      // buffers released at the end
         std::map<const u32*, KsSrc> src_of;         // input data -> canonical source
         // 1. canonical sources; lazy 2-polynomial tensors owing one rescale, grouped by level, are
@@ -1987,7 +2126,7 @@ public:
     // x^k at depth ceil(log2 k): x^(2^i) by squaring, x^k = x^(2^t) x^(k - 2^t)
     void power_basis(aesfhe_handle h, int degree, aesfhe_handle* out) {
         const Ct& x = canon(h);
-        if (x.npoly != 2) throw std::runtime_error("make_power_basis expects a 2-polynomial ciphertext");
+        if (pm(x) != 2) throw std::runtime_error("make_power_basis expects a 2-polynomial ciphertext");
         if (degree < 1) throw std::runtime_error("power basis degree must be >= 1");
         int depth = 0;
         while ((1 << depth) < degree) ++depth;
@@ -2091,14 +2230,7 @@ public:
         const int n = hp_.n, s = slot_count(), stride = s / 16;
         if (states < 1 || states > stride)
             throw std::runtime_error("renorm: states per ciphertext must be in [1, slot_count / 16]");
-        if (states > 1 && !d_slot_pos_) {
-            std::vector<u32> pos(s);
-            const u64 two_n = 2ull * n;
-            u64 e = 1;
-            for (int j = 0; j < s; ++j) pos[j] = (u32)((e - 1) / 2), e = e * 5 % two_n;
-            d_slot_pos_ = dev_alloc(s);
-            HIP_OK(hipMemcpy(d_slot_pos_, pos.data(), sizeof(u32) * s, hipMemcpyHostToDevice));
-        }
+        if (states > 1 || ct(hh).nb > 1) ensure_slot_pos();
         if (slots_.e[1] == 0) {
             const u64 two_n = 2ull * n;
             u64 e = 1;
@@ -2111,6 +2243,12 @@ public:
                 d_codec_[k] = (double*)dev_alloc(2 * 64 * 2);  // acc[64] + w[64] doubles
                 d_nib_[k] = (int*)dev_alloc(32);
             }
+        }
+        const int P = ct(hh).nb;
+        if (P > 1 || ct(hl).nb > 1) {
+            if (ct(hl).nb != P) throw std::runtime_error("renorm: hi and lo stacks of different sizes");
+            renorm_stacked(hh, hl, period == 16 ? stride : states, oh, ol, level, unpack, single);
+            return;
         }
         u32* x = tmp(8);  // [2][4][N]
         int kd[2];
@@ -2190,6 +2328,92 @@ public:
         }
         untmp(m, 2 * (size_t)nq);
         untmp(x, 8);
+    }
+
+    // NTT position of every slot (5^j mod 2N -> (e - 1) / 2), for the FFT codec
+    void ensure_slot_pos() {
+        if (d_slot_pos_) return;
+        const int n = hp_.n, s = slot_count();
+        std::vector<u32> pos(s);
+        const u64 two_n = 2ull * n;
+        u64 e = 1;
+        for (int j = 0; j < s; ++j) pos[j] = (u32)((e - 1) / 2), e = e * 5 % two_n;
+        d_slot_pos_ = dev_alloc(s);
+        HIP_OK(hipMemcpy(d_slot_pos_, pos.data(), sizeof(u32) * s, hipMemcpyHostToDevice));
+    }
+    // the renorm of P stacked state pairs (multi-pair batches): every member's
+    // channels in ONE set of launches -- one raw decryption, one inverse NTT, the fp64 FFT codec
+    // over all n_in P channels (states = the slots snapped per 16-slot row, as renorm_states), one
+    // encryption of all n_out P messages -- and the outputs as stacks again (hi = members
+    // [0, P), lo = [P, 2P) of the encryption).  Same snapped values as P single renorms.
+    void renorm_stacked(aesfhe_handle hh, aesfhe_handle hl, int states, aesfhe_handle* oh, aesfhe_handle* ol, int level, int unpack,
+                        bool single) {
+        const int n = hp_.n, P = ct(hh).nb;
+        const int n_in = (unpack || single) ? 1 : 2, n_out = single ? 1 : 2;
+        int kd[2] = {0, 0};
+        CrtConsts cc[2];
+        double isc[2] = {1.0, 1.0};
+        DecRaw dr;
+        dr.members = P;
+        Ct dc[2];
+        bool down[2] = {false, false}, need_s2 = false;
+        const aesfhe_handle in[2] = {hh, hl};
+        for (int w = 0; w < n_in; ++w) {
+            Ct c = ensure_ntt(ct(in[w]));
+            bool own = c.data != ct(in[w]).data;
+            kd[w] = crt_limbs(c);
+            if (!kd[w]) {
+                Ct nc = normalize(c, true);
+                if (own) release(c);
+                c = nc, own = nc.data != ct(in[w]).data;
+                kd[w] = crt_limbs(c);
+            }
+            dc[w] = c, down[w] = own;
+            dr.ct[w] = c.data, dr.npoly[w] = pm(c), dr.nlc[w] = hp_.nl(c.level), dr.kd[w] = kd[w];
+            dr.ms[w] = (size_t)pm(c) * hp_.nl(c.level) * n;
+            need_s2 = need_s2 || pm(c) == 3;
+            cc[w] = crt_consts(kd[w]);
+            isc[w] = 1.0 / (c.level >= 0 ? raw_scale(c.level, c.pend) : 1.0);
+            cnt_[C_DEC] += P;
+        }
+        if (n_in == 1) kd[1] = kd[0], cc[1] = cc[0], isc[1] = isc[0];
+        const int chin = n_in * P, chout = n_out * P;
+        u32* x = tmp((size_t)4 * chin);  // [channel][4][N]
+        launch_dec_raw(S(), T_, x, dr, n_in, d_s_, need_s2 ? s_sq4() : d_s_);
+        if (kd[0] == kd[1] || n_in == 1) {
+            intt(x, x, chin * kd[0], RowMap{kd[0], 4, 4, 0, 0}, qmap());
+        } else {
+            for (int w = 0; w < n_in; ++w) intt(x + (size_t)w * P * 4 * n, x + (size_t)w * P * 4 * n, P * kd[w], RowMap{kd[w], 4, 4, 0, 0}, qmap());
+        }
+        for (int w = 0; w < n_in; ++w)
+            if (down[w]) release(dc[w]);
+        ensure_slot_pos();
+        const int f = level < 0 ? hp_.fresh : level, nq = hp_.nl(f) + 1;
+        const double enc_scale = hp_.delta[f] * (double)hp_.mod[hp_.nl(f)];
+        // fp64 codec buffers: a complex double is 4 words, so a channel of N values is 4 rows
+        u32* zb = tmp((size_t)4 * chin);
+        u32* wb = tmp((size_t)4 * chout);
+        double* z = (double*)zb;
+        double* wv = (double*)wb;
+        launch_decode_twist(S(), T_, x, kd, cc, isc, z, chin, P);
+        launch_fft2(S(), T_, z, 1, chin);
+        launch_snap_slots(S(), T_, z, wv, d_slot_pos_, states, unpack, chout, P);
+        launch_fft2(S(), T_, wv, -1, chout);
+        u32* m = tmp((size_t)chout * nq);
+        launch_encode_untwist(S(), T_, m, wv, enc_scale, nq, chout);
+        untmp(zb, (size_t)4 * chin);
+        untmp(wb, (size_t)4 * chout);
+        untmp(x, (size_t)4 * chin);
+        ntt(m, chout * nq, nq, qmap());
+        Ct enc = encrypt_many(m, chout, (size_t)nq * n, f);
+        untmp(m, (size_t)chout * nq);
+        if (n_out == 1) {
+            *oh = put_ct(enc);
+            return;
+        }
+        *oh = put_ct(members_of(enc, 0, P));
+        *ol = put_ct(members_of(enc, P, P));
+        release(enc);
     }
 
     // ------------------------------------------------------------------ bootstrapping
@@ -2928,10 +3152,38 @@ public:
     // 6 real part, 7 imaginary part, 8 EvalMod(real), 9 EvalMod(imag), 10 recombined, 11 output
     // gain: the output carries gain * message (folded into the level-0 scaling integer k1,
     // relative precision 2^-k1bits; the true-FHE snap's kappa, zeta16_noise_reducer.py)
+    // level-0 stack z (nb members, consumed) -> the bootstrapped stack, in chunks of two members
+    // (the pair bootstrap's batch: every key and diagonal read once per chunk)
+    Ct boot_stack(Ct z, double gain, SparseBoot* sv) {
+        const int P = z.nb;
+        if (P <= 2) return bootstrap_l0(z, 99, gain, sv);
+        Ct out;
+        for (int m0 = 0; m0 < P; m0 += 2) {
+            const int c = std::min(2, P - m0);
+            Ct r = bootstrap_l0(members_of(z, m0, c), 99, gain, sv);
+            if (m0 == 0) {
+                out = alloc_ct(r.level, pm(r) * P, P);
+                copy_meta(out, r);
+                out.nb = P;
+            }
+            if (r.level != out.level || pm(r) != pm(out)) throw std::runtime_error("bootstrap: stack chunks at different levels");
+            launch_copy_rows(S(), T_, out.data + (size_t)m0 * pm(r) * hp_.nl(r.level) * hp_.n, r.data, r.words / hp_.n);
+            release(r);
+        }
+        release(z);
+        return out;
+    }
     Ct bootstrap(const Ct& in, int stop_after = 99, double gain = 1.0, int period = 0) {
         boot_setup();
-        if (vis_npoly(in) != 2 || in.nb != 1) throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
+        if (vis_npoly(in) != 2) throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
         SparseBoot* sv = (period > 0 && period < slot_count()) ? &sparse_variant(period) : nullptr;
+        if (in.nb > 1) {  // a stack (multi-pair batch): chunks of two members
+            if (stop_after != 99) throw std::runtime_error("bootstrap: debug stages take a single ciphertext");
+            Ct c = normalize(in);
+            Ct z = level_down(c, 0);
+            if (c.data != in.data) release(c);
+            return boot_stack(z, gain, sv);
+        }
         Ct c = normalize(in);
         Ct z = level_down(c, 0);
         if (c.data != in.data) release(c);
@@ -2942,9 +3194,14 @@ public:
     // transform its diagonals, once for both; half the launches
     void bootstrap_pair(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob, double gain = 1.0, int period = 0) {
         boot_setup();
-        if (vis_npoly(a_in) != 2 || vis_npoly(b_in) != 2 || a_in.nb != 1 || b_in.nb != 1)
+        if (vis_npoly(a_in) != 2 || vis_npoly(b_in) != 2 || a_in.nb != b_in.nb)
             throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
         if (period > 0 && 2 * period <= slot_count() && mono_pair_) return bootstrap_pair_mono(a_in, b_in, oa, ob, gain, period);
+        if (a_in.nb > 1) {  // stacks: a's and b's members bootstrapped in chunks of two
+            *oa = put_ct(bootstrap(a_in, 99, gain, period));
+            *ob = put_ct(bootstrap(b_in, 99, gain, period));
+            return;
+        }
         SparseBoot* sv = (period > 0 && period < slot_count()) ? &sparse_variant(period, true) : nullptr;
         const int n = hp_.n, nl0 = hp_.nl(0);
         Ct z = alloc_ct(0, 4, 2);
@@ -2974,6 +3231,7 @@ public:
     // with gain / 2 (|z| <= |a| + |b|) refreshes both; the rotation by n slots is
     // X -> X^(4n+1) (5^n = 4n + 1 mod 8n), which fixes X^2k and negates X^k, so with
     // m = gain z / 2 and r = rot_n(m):  gain a = m + r,  gain b = X^-k (m - r).
+    int z_members_ = 1;
     bool mono_pair_ = !(std::getenv("AESFHE_PAIR_MONO") && std::atoi(std::getenv("AESFHE_PAIR_MONO")) == 0);
     // z = a + X^k b at level 0 (k = N / 4 period): exact, one fused multiply-add with the NTT form
     // of the monomial
@@ -2987,8 +3245,9 @@ public:
             z0[m] = level_down(c, 0);
             if (c.data != in[m]->data) release(c);
         }
-        Ct z = alloc_ct(0, 2);
-        launch_fma_poly(S(), T_, z.data, z0[0].data, z0[1].data, monomial(k), 2 * nl0, nl0, qmap());
+        if (z0[0].nb != z0[1].nb) throw std::runtime_error("mono_pack: stacks of different sizes");
+        Ct z = alloc_ct(0, z0[0].npoly, z0[0].nb);
+        launch_fma_poly(S(), T_, z.data, z0[0].data, z0[1].data, monomial(k), z0[0].npoly * nl0, nl0, qmap());
         release(z0[0]);
         release(z0[1]);
         return z;
@@ -3003,19 +3262,20 @@ public:
         release(r);
         Ct dn = ensure_ntt(d);
         if (dn.data != d.data) release(d);
-        lo = alloc_ct(dn.level, 2);
+        lo = alloc_ct(dn.level, dn.npoly, dn.nb);
         copy_meta(lo, dn);
-        launch_mul_poly(S(), T_, lo.data, dn.data, monomial(2 * n - k), 2, hp_.nl(dn.level), qmap());
+        launch_mul_poly(S(), T_, lo.data, dn.data, monomial(2 * n - k), dn.npoly, hp_.nl(dn.level), qmap());
         release(dn);
     }
     void bootstrap_pair_mono(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob, double gain, int period) {
         Ct z = mono_pack(a_in, b_in, period);
+        z_members_ = z.nb;
         SparseBoot* sv = 2 * period < slot_count() ? &sparse_variant(2 * period) : nullptr;
-        Ct mz = bootstrap_l0(z, 99, 0.5 * gain, sv);
+        Ct mz = boot_stack(z, 0.5 * gain, sv);  // a stack of P packed pairs: chunks of two
         Ct hi, lo;
         mono_split(mz, period, hi, lo);
         release(mz);
-        cnt_[C_BOOT] += 1;  // bootstrap_l0 counted one: two messages refreshed
+        cnt_[C_BOOT] += z_members_;  // bootstrap_l0 counted one per packed pair: two messages each
         *oa = put_ct(hi);
         *ob = put_ct(lo);
     }
@@ -3881,6 +4141,28 @@ int aesfhe_mul_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* a, const aesfhe
     for (int i = 0; i < n; ++i) A[i] = &e.canon(a[i]), B[i] = &e.canon(b[i]);
     std::vector<Ct> r = e.mul_many(A, B);
     for (int i = 0; i < n; ++i) out[i] = e.put_ct(r[i]);
+    API_END
+}
+int aesfhe_stack(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, aesfhe_handle* out) {
+    API_BEGIN Engine& e = *ctx->eng;
+    if (n < 1 || !in || !out) throw std::runtime_error("stack: bad arguments");
+    std::vector<const Ct*> C(n);
+    for (int i = 0; i < n; ++i) C[i] = &e.ct(in[i]);
+    *out = e.put_ct(e.stack(C));
+    API_END
+}
+int aesfhe_unstack(aesfhe_ctx* ctx, aesfhe_handle in, int n, aesfhe_handle* out) {
+    API_BEGIN Engine& e = *ctx->eng;
+    const Ct& c = e.ct(in);
+    if (!out || n != c.nb) throw std::runtime_error("unstack: n must equal the stack's member count");
+    std::vector<Ct> r = e.unstack_all(c);
+    for (int i = 0; i < n; ++i) out[i] = e.put_ct(r[i]);
+    API_END
+}
+int aesfhe_members(aesfhe_ctx* ctx, aesfhe_handle h, int* members) {
+    API_BEGIN Engine& e = *ctx->eng;
+    if (!members) throw std::runtime_error("members: null output");
+    *members = e.ct(h).nb;
     API_END
 }
 int aesfhe_galois_multi(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, const uint64_t* galois, aesfhe_handle* out) {

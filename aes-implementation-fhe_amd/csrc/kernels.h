@@ -278,12 +278,12 @@ struct LinMacArgs {
 };
 void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int nl, int ne, LimbMap map);
 
-// --- fused public-key encryption of up to kEncMax messages (renorm re-encryption) -------
-// one launch samples v, e0, e1 of every member (member m: streams stream_id(6|7|8, 0, ctr[m]),
+// --- fused public-key encryption of a batch of messages (renorm re-encryption) -----------
+// one launch samples v, e0, e1 of every member (member m: streams stream_id(6|7|8, 0, base + m),
 // the same samples as launch_sample_small), one combines c0 = (e0 + msg) + pk0 v, c1 = e1 + pk1 v
-constexpr int kEncMax = 4;
+constexpr int kEncMax = 16384;  // grid y = 3 members
 struct EncCtrs {
-    u64 ctr[kEncMax] = {};
+    u64 base = 0;  // member m uses encryption counter base + m
 };
 // out: [m][3][nl] (v, e0, e1 residues, coefficient form)
 void launch_sample_enc(hipStream_t st, const DevTables& T, u32* out, int nl, int nm, const PrngKey& key, const EncCtrs& ctr);
@@ -295,7 +295,10 @@ void launch_enc_combine(hipStream_t st, const DevTables& T, u32* top, const u32*
 struct DecRaw {
     const u32* ct[2] = {};
     int npoly[2] = {}, nlc[2] = {}, kd[2] = {};
+    int members = 1;         // stacked inputs: channel c = w members + m reads input w's member m
+    size_t ms[2] = {0, 0};   // member stride (words) of each input
 };
+// x: [channel][4][N] with nch x members channels
 void launch_dec_raw(hipStream_t st, const DevTables& T, u32* x, const DecRaw& dr, int nch, const u32* s, const u32* s2);
 
 // --- sampling --------------------------------------------------------
@@ -336,8 +339,9 @@ void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double*
 // computed as a four-step FFT over an N1 x N2 row-major matrix (N1 = 2^ceil(logn/2)).
 // Element t of a transform's output is stored at fft_loc(t) = (t mod N1) N2 + t / N1.
 // x: [2][4][N] coefficient residues (kd[c] limbs) -> z[c][k] = m_k / scale_c * zeta^k
+// members > 1: channel c belongs to input c / members (stacked renorm)
 void launch_decode_twist(hipStream_t st, const DevTables& T, const u32* x, const int kd[2], const CrtConsts cc[2],
-                         const double inv_scale[2], double* z, int nch = 2);
+                         const double inv_scale[2], double* z, int nch = 2, int members = 1);
 // in-place X_k = sum_n x_n e^{sign 2 pi i n k / N} on 2 vectors (complex double, [2][N]);
 // input in natural order, output at fft_loc
 void launch_fft2(hipStream_t st, const DevTables& T, double* z, int sign, int nch = 2);
@@ -345,8 +349,9 @@ void launch_fft2(hipStream_t st, const DevTables& T, double* z, int sign, int nc
 // else 1; writes w[slot_pos[j]] = v and w[N - 1 - slot_pos[j]] = conj(v) (natural order)
 // unpack = n > 0: both outputs read the first input's 2n-periodic packed state, output 0 its
 // slots (j mod n), output 1 its slots (j mod n) + n
+// members > 1 with unpack: output channel c = half (c / members) of input channel c % members
 void launch_snap_slots(hipStream_t st, const DevTables& T, const double* zin, double* w, const u32* slot_pos, int states, int unpack = 0,
-                       int nch = 2);
+                       int nch = 2, int members = 1);
 // out[c][t][k] = round(scale Re(v[fft_loc(k)] zeta^{-k}) / N) mod q_t, t < nq
 void launch_encode_untwist(hipStream_t st, const DevTables& T, u32* out, const double* v, double scale, int nq, int nch = 2);
 // nch (all four): channels processed (grid y); 1 = channel 0 only (one input decrypted, or one output)
@@ -365,7 +370,10 @@ struct LutOperands {
     unsigned char q_of[kLutMax * kLutMax];
 };
 // out (3 polys, nl rows each) = sum_p A_p (x) (sum_q C_pq B_q)
-void launch_lut_bivariate(hipStream_t st, const DevTables& T, u32* out, const LutOperands& op, int n_a, const u32* cst, int nl);
+// members > 1: every element a stack of `members` ciphertexts (member stride 2 x its limbs x N),
+// the output a stack of 3-polynomial tensors
+void launch_lut_bivariate(hipStream_t st, const DevTables& T, u32* out, const LutOperands& op, int n_a, const u32* cst, int nl,
+                          int members = 1);
 // chunk of a univariate sum: out (npoly x nl) = (acc ? acc : 0) + sum_{k < n} C_k X_k
 constexpr int kLutChunk = 32;
 struct LutChunk {
@@ -373,5 +381,5 @@ struct LutChunk {
     int nx[kLutChunk];
 };
 void launch_lut_univariate(hipStream_t st, const DevTables& T, u32* out, const u32* acc, const LutChunk& ch, int n, const u32* cst,
-                           int npoly, int nl);
+                           int npoly, int nl, int members = 1);
 

@@ -452,7 +452,7 @@ __global__ void k_sample_small(u32* out, int nl, LimbMap map, PrngKey key, u64 s
 __global__ void k_sample_enc(u32* out, int nl, PrngKey key, EncCtrs ctr, const PrimeConst* pc, int logn) {
     const int y = blockIdx.y, m = y / 3, w = y - 3 * m;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    const u64 stream = ((u64)(6 + w) << 56) | ctr.ctr[m];  // stream_id(6 + w, 0, ctr)
+    const u64 stream = ((u64)(6 + w) << 56) | (ctr.base + (u64)m);  // stream_id(6 + w, 0, ctr)
     const u64 r = chacha_u64(key, stream, k);
     const int v = w == 0 ? (int)(r % 3) - 1 : __popcll(r & 0x1FFFFFull) - __popcll((r >> 21) & 0x1FFFFFull);
     u32* o = out + ((size_t)y * nl << logn);
@@ -477,16 +477,17 @@ __global__ void k_enc_combine(u32* top, const u32* vee, const u32* msg, size_t m
 }
 // raw decryption rows of up to two channels (renorm): x[c][t] = c0 + c1 s + c2 s^2 on t < kd[c]
 __global__ void k_dec_raw(u32* x, DecRaw dr, const u32* s, const u32* s2, const PrimeConst* pc, int logn) {
-    const int c = blockIdx.y >> 2, t = blockIdx.y & 3;
+    const int ch = blockIdx.y >> 2, t = blockIdx.y & 3;
+    const int c = ch / dr.members, mb = ch - c * dr.members;
     if (t >= dr.kd[c]) return;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const PrimeConst P = pc[t];
     const size_t row = ((size_t)t << logn) + k, pl = (size_t)dr.nlc[c] << logn;
-    const u32* ct = dr.ct[c];
+    const u32* ct = dr.ct[c] + mb * dr.ms[c];
     u32 v = ct[row];
     v = add_mod(v, barrett_mul(ct[pl + row], s[row], P.q, P.mu), P.q);
     if (dr.npoly[c] == 3) v = add_mod(v, barrett_mul(ct[2 * pl + row], s2[row], P.q, P.mu), P.q);
-    x[((size_t)(c * 4 + t) << logn) + k] = v;
+    x[((size_t)(ch * 4 + t) << logn) + k] = v;
 }
 __global__ void k_sample_uniform(u32* out, int nl, LimbMap map, PrngKey key, u64 stream, const PrimeConst* pc, int logn) {
     const int l = blockIdx.y;
@@ -701,13 +702,13 @@ __global__ void __launch_bounds__(kBlock) k_encode16(u32* out, const double* w, 
 __device__ __forceinline__ int fft_log1(int logn) { return logn - logn / 2; }  // log N1 (N1 >= N2)
 
 __global__ void __launch_bounds__(kBlock) k_decode_twist(const u32* x, int kd0, int kd1, CrtConsts cc0, CrtConsts cc1, double is0,
-                                                         double is1, double2* z, int logn) {
-    const int c = blockIdx.y;
+                                                         double is1, double2* z, int logn, int members) {
+    const int c = blockIdx.y, w = c / members;
     const int k = blockIdx.x * kBlock + threadIdx.x;
-    const int kd = c ? kd1 : kd0;
+    const int kd = w ? kd1 : kd0;
     u32 r[4];
     for (int i = 0; i < kd; ++i) r[i] = x[((size_t)(c * 4 + i) << logn) + k];
-    const double m = crt_centered(r, kd, c ? cc1 : cc0) * (c ? is1 : is0);
+    const double m = crt_centered(r, kd, w ? cc1 : cc0) * (w ? is1 : is0);
     double sn, cs;
     sincospi((double)k / (double)(1 << logn), &sn, &cs);
     z[((size_t)c << logn) + k] = make_double2(m * cs, m * sn);
@@ -770,15 +771,15 @@ __device__ __forceinline__ size_t fft_loc(u32 t, int logn) {
 // unpack > 0: output c (0 = hi, 1 = lo) takes slot (j mod unpack) + c unpack of the FIRST input
 // -- the hi | lo halves of a 2 unpack-periodic packed state (pipeline's packed XOR stage)
 __global__ void __launch_bounds__(kBlock) k_snap_slots(const double2* zin, double2* w, const u32* slot_pos, int states, int unpack,
-                                                       int logn) {
-    const int c = blockIdx.y;
+                                                       int logn, int members) {
+    const int oc = blockIdx.y, c = oc / members, mb = oc - c * members;
     const int j = blockIdx.x * kBlock + threadIdx.x;  // slot < N/2
     const int n = 1 << logn;
     const u32 t = slot_pos[j];
     const int stride = (n / 2) / 16;
     double2 v = make_double2(1.0, 0.0);
     if (j % stride < states) {
-        const int src_c = unpack ? 0 : c;
+        const int src_c = unpack ? mb : oc;
         const u32 ts = unpack ? slot_pos[(j & (unpack - 1)) + c * unpack] : t;
         const double2 z = zin[((size_t)src_c << logn) + fft_loc(ts, logn)];
         const double kf = rint(-atan2(z.y, z.x) * 16.0 / (2.0 * M_PI));
@@ -787,7 +788,7 @@ __global__ void __launch_bounds__(kBlock) k_snap_slots(const double2* zin, doubl
         sincospi(-2.0 * nib / 16.0, &sn, &cs);
         v = make_double2(cs, sn);
     }
-    double2* wc = w + ((size_t)c << logn);
+    double2* wc = w + ((size_t)oc << logn);
     wc[t] = v;
     wc[n - 1 - t] = make_double2(v.x, -v.y);
 }
@@ -813,14 +814,17 @@ __global__ void __launch_bounds__(kBlock) k_encode_untwist(u32* out, const doubl
 // ------------------------------------------------------------------------------------
 // fused LUT evaluation: one launch per LUT instead of a tensor + constant + add per term
 // ------------------------------------------------------------------------------------
+// grid z = member of stacked elements: element p of member m at a[p] + m 2 na[p] N (b likewise),
+// the output at out + m 3 nl N
 __global__ void __launch_bounds__(kBlock) k_lut_bivariate(u32* out, LutOperands op, int n_a, const u32* cst, int nl,
                                                           const PrimeConst* pc, int logn) {
-    const int t = blockIdx.y;
+    const int t = blockIdx.y, mb = blockIdx.z;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const int half = (int)(k >> (logn - 1));
     const PrimeConst P = pc[t];
     const u32 q = P.q;
     const size_t off = ((size_t)t << logn) + k;
+    out += (size_t)mb * 3 * ((size_t)nl << logn);
     u32 acc0 = 0, acc1 = 0, acc2 = 0;
     for (int p = 0; p < n_a; ++p) {
         const int t0 = op.p_start[p], t1 = op.p_start[p + 1];
@@ -828,12 +832,13 @@ __global__ void __launch_bounds__(kBlock) k_lut_bivariate(u32* out, LutOperands 
         u32 u0 = 0, u1 = 0;
         for (int j = t0; j < t1; ++j) {
             const int qq = op.q_of[j];
-            const u32* bq = op.b[qq];
+            const u32* bq = op.b[qq] + (size_t)mb * 2 * ((size_t)op.nb[qq] << logn);
             const u32* c = cst + ((size_t)j * nl + t) * 4 + 2 * half;
             u0 = add_mod(u0, shoup_mul(bq[off], c[0], c[1], q), q);
             u1 = add_mod(u1, shoup_mul(bq[((size_t)op.nb[qq] << logn) + off], c[0], c[1], q), q);
         }
-        const u32 a0 = op.a[p][off], a1 = op.a[p][((size_t)op.na[p] << logn) + off];
+        const u32* ap = op.a[p] + (size_t)mb * 2 * ((size_t)op.na[p] << logn);
+        const u32 a0 = ap[off], a1 = ap[((size_t)op.na[p] << logn) + off];
         acc0 = add_mod(acc0, barrett_mul(a0, u0, q, P.mu), q);
         acc1 = add_mod(acc1, add_mod(barrett_mul(a0, u1, q, P.mu), barrett_mul(a1, u0, q, P.mu), q), q);
         acc2 = add_mod(acc2, barrett_mul(a1, u1, q, P.mu), q);
@@ -843,19 +848,23 @@ __global__ void __launch_bounds__(kBlock) k_lut_bivariate(u32* out, LutOperands 
     out[((size_t)(2 * nl) << logn) + off] = acc2;
 }
 
+// grid z = member of stacked elements (element j of member m at x[j] + m npoly nx[j] N, out / acc
+// at + m npoly nl N)
 __global__ void __launch_bounds__(kBlock) k_lut_univariate(u32* out, const u32* acc, LutChunk ch, int n, const u32* cst, int npoly,
                                                            int nl, const PrimeConst* pc, int logn) {
-    const int t = blockIdx.y;
+    const int t = blockIdx.y, mb = blockIdx.z;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const int half = (int)(k >> (logn - 1));
     const u32 q = pc[t].q;
     const size_t off = ((size_t)t << logn) + k;
+    const size_t mo = (size_t)mb * npoly * ((size_t)nl << logn);
     for (int p = 0; p < npoly; ++p) {
-        const size_t o = ((size_t)(p * nl) << logn) + off;
+        const size_t o = mo + ((size_t)(p * nl) << logn) + off;
         u32 v = acc ? acc[o] : 0;
         for (int j = 0; j < n; ++j) {
             const u32* c = cst + ((size_t)j * nl + t) * 4 + 2 * half;
-            v = add_mod(v, shoup_mul(ch.x[j][((size_t)(p * ch.nx[j]) << logn) + off], c[0], c[1], q), q);
+            const u32* xj = ch.x[j] + (size_t)mb * npoly * ((size_t)ch.nx[j] << logn);
+            v = add_mod(v, shoup_mul(xj[((size_t)(p * ch.nx[j]) << logn) + off], c[0], c[1], q), q);
         }
         out[o] = v;
     }
@@ -1221,7 +1230,7 @@ void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, L
                        T.logn);
 }
 void launch_sample_enc(hipStream_t st, const DevTables& T, u32* out, int nl, int nm, const PrngKey& key, const EncCtrs& ctr) {
-    if (nm < 1 || nm > kEncMax) throw std::runtime_error("launch_sample_enc: 1..4 encryptions");
+    if (nm < 1 || nm > kEncMax) throw std::runtime_error("launch_sample_enc: too many encryptions");
     prof_launch(KID_SAMPLE, words(3.0 * nm * nl * (1u << T.logn)), k_sample_enc, dim3((1u << T.logn) / kBlock, 3 * nm), dim3(kBlock), 0, st,
                 out, nl, key, ctr, T.pc, T.logn);
 }
@@ -1237,8 +1246,9 @@ void launch_dec_raw(hipStream_t st, const DevTables& T, u32* x, const DecRaw& dr
         if (dr.kd[c] < 1 || dr.kd[c] > 4 || dr.kd[c] > dr.nlc[c]) throw std::runtime_error("launch_dec_raw: bad limb count");
         w += (2.0 * dr.npoly[c] + 1.0) * dr.kd[c];
     }
-    prof_launch(KID_ELEMENTWISE, words(w * (1u << T.logn)), k_dec_raw, dim3((1u << T.logn) / kBlock, 4 * nch), dim3(kBlock), 0, st, x, dr, s,
-                s2, T.pc, T.logn);
+    if (dr.members < 1 || 4 * nch * dr.members > 65535) throw std::runtime_error("launch_dec_raw: bad member count");
+    prof_launch(KID_ELEMENTWISE, words(w * dr.members * (1u << T.logn)), k_dec_raw, dim3((1u << T.logn) / kBlock, 4 * nch * dr.members),
+                dim3(kBlock), 0, st, x, dr, s, s2, T.pc, T.logn);
 }
 void launch_sample_uniform(hipStream_t st, const DevTables& T, u32* out, int nl, LimbMap map, const PrngKey& key, u64 stream) {
     prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_uniform, ew_grid(T.logn, nl), dim3(kBlock), 0, st, out, nl, map, key, stream, T.pc, T.logn);
@@ -1266,10 +1276,11 @@ void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double*
 }
 
 void launch_decode_twist(hipStream_t st, const DevTables& T, const u32* x, const int kd[2], const CrtConsts cc[2],
-                         const double inv_scale[2], double* z, int nch) {
+                         const double inv_scale[2], double* z, int nch, int members) {
     const double n = (double)(1u << T.logn);
-    prof_launch(KID_ELEMENTWISE, words((kd[0] + (nch > 1 ? kd[1] : 0)) * n) + 16.0 * nch * n, k_decode_twist, dim3((1u << T.logn) / kBlock, nch), dim3(kBlock),
-                0, st, x, kd[0], kd[1], cc[0], cc[1], inv_scale[0], inv_scale[1], (double2*)z, T.logn);
+    prof_launch(KID_ELEMENTWISE, words((double)kd[0] * n * (nch > members ? 2 : 1) * members) + 16.0 * nch * n, k_decode_twist,
+                dim3((1u << T.logn) / kBlock, nch), dim3(kBlock), 0, st, x, kd[0], kd[1], cc[0], cc[1], inv_scale[0], inv_scale[1], (double2*)z,
+                T.logn, members);
 }
 void launch_fft2(hipStream_t st, const DevTables& T, double* z, int sign, int nch) {
     const int l1 = T.logn - T.logn / 2, l2 = T.logn - l1;
@@ -1278,10 +1289,10 @@ void launch_fft2(hipStream_t st, const DevTables& T, double* z, int sign, int nc
                     (double2*)z, T.logn, pass, sign);
 }
 void launch_snap_slots(hipStream_t st, const DevTables& T, const double* zin, double* w, const u32* slot_pos, int states, int unpack,
-                       int nch) {
+                       int nch, int members) {
     const double s = (double)(1u << (T.logn - 1));
     prof_launch(KID_ELEMENTWISE, nch * (16.0 * s + 4.0 * s + 32.0 * s), k_snap_slots, dim3((1u << (T.logn - 1)) / kBlock, nch),
-                dim3(kBlock), 0, st, (const double2*)zin, (double2*)w, slot_pos, states, unpack, T.logn);
+                dim3(kBlock), 0, st, (const double2*)zin, (double2*)w, slot_pos, states, unpack, T.logn, members);
 }
 void launch_encode_untwist(hipStream_t st, const DevTables& T, u32* out, const double* v, double scale, int nq, int nch) {
     const double n = (double)(1u << T.logn);
@@ -1289,17 +1300,17 @@ void launch_encode_untwist(hipStream_t st, const DevTables& T, u32* out, const d
                 st, out, (const double2*)v, scale, nq, T.pc, T.logn);
 }
 
-void launch_lut_bivariate(hipStream_t st, const DevTables& T, u32* out, const LutOperands& op, int n_a, const u32* cst, int nl) {
+void launch_lut_bivariate(hipStream_t st, const DevTables& T, u32* out, const LutOperands& op, int n_a, const u32* cst, int nl, int members) {
     double reads = 0;
     for (int p = 0; p < n_a; ++p)
         if (op.p_start[p + 1] > op.p_start[p]) reads += 2;
     reads += 2.0 * kLutMax;  // upper bound on the B elements read
-    prof_launch(KID_ELEMENTWISE, words((reads + 3.0) * nl * (1u << T.logn)), k_lut_bivariate, ew_grid(T.logn, nl), dim3(kBlock), 0,
-                st, out, op, n_a, cst, nl, T.pc, T.logn);
+    prof_launch(KID_ELEMENTWISE, words((reads + 3.0) * nl * members * (1u << T.logn)), k_lut_bivariate,
+                dim3((1u << T.logn) / kBlock, nl, members), dim3(kBlock), 0, st, out, op, n_a, cst, nl, T.pc, T.logn);
 }
 void launch_lut_univariate(hipStream_t st, const DevTables& T, u32* out, const u32* acc, const LutChunk& ch, int n, const u32* cst,
-                           int npoly, int nl) {
-    prof_launch(KID_ELEMENTWISE, words((double)(n + (acc ? 2 : 1)) * npoly * nl * (1u << T.logn)), k_lut_univariate,
-                ew_grid(T.logn, nl), dim3(kBlock), 0, st, out, acc, ch, n, cst, npoly, nl, T.pc, T.logn);
+                           int npoly, int nl, int members) {
+    prof_launch(KID_ELEMENTWISE, words((double)(n + (acc ? 2 : 1)) * npoly * nl * members * (1u << T.logn)), k_lut_univariate,
+                dim3((1u << T.logn) / kBlock, nl, members), dim3(kBlock), 0, st, out, acc, ch, n, cst, npoly, nl, T.pc, T.logn);
 }
 

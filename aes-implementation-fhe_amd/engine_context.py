@@ -117,6 +117,14 @@ class EngineContext:
     def conjugate_many(self, cts):
         return self.engine.conjugate_many(cts)
 
+    # stacked ciphertexts (multi-pair batches, include/aesfhe.h aesfhe_stack)
+    def stack(self, cts):
+        """n single ciphertexts -> one stack; every op then runs on all members at once"""
+        return self.engine.stack(cts)
+
+    def unstack(self, ct):
+        return self.engine.unstack(ct)
+
     def rotate_multi(self, items):
         """[rotate(ct, s) for ct, s in items] -- different ciphertexts, different steps -- as one
         heterogeneous batched key switch (include/aesfhe.h aesfhe_galois_multi)"""

@@ -46,7 +46,7 @@ EXPORTED = [
     "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_debug_lin_group_plain", "aesfhe_lut_create", "aesfhe_lut_eval", "aesfhe_lut_free",
     "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled", "aesfhe_set_enc_nonce", "aesfhe_launch_count",
     "aesfhe_galois_multi", "aesfhe_debug_boot_stage_sparse", "aesfhe_debug_sparse_group", "aesfhe_debug_sparse_group_plain",
-    "aesfhe_debug_mono_pack", "aesfhe_debug_mono_split", "aesfhe_alg_bytes",
+    "aesfhe_debug_mono_pack", "aesfhe_debug_mono_split", "aesfhe_alg_bytes", "aesfhe_stack", "aesfhe_unstack", "aesfhe_members",
 ]
 
 # largest log2(PQ) for 128-bit classical security with a ternary secret (HE standard)
@@ -142,6 +142,9 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_debug_sparse_group_plain"] = [vp, c_int, c_int, c_int, _dp, _dp, _dp, _dp, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")]
     sig["aesfhe_debug_mono_pack"] = [vp, _H, _H, c_int, _Hp]
     sig["aesfhe_debug_mono_split"] = [vp, _H, c_int, _Hp, _Hp]
+    sig["aesfhe_stack"] = [vp, c_int, _Hp, _Hp]
+    sig["aesfhe_unstack"] = [vp, _H, c_int, _Hp]
+    sig["aesfhe_members"] = [vp, _H, ctypes.POINTER(c_int)]
     for name in EXPORTED:
         fn = getattr(L, name)
         fn.restype = (ctypes.c_char_p if name == "aesfhe_last_error" else ctypes.c_uint64 if name == "aesfhe_launch_count"
@@ -533,6 +536,28 @@ class Engine:
         src, gal, out = H(*[c.handle for c, _ in items]), H(*[int(g) for _, g in items]), H()
         self._ctx.check(self._lib.aesfhe_galois_multi(self._ctx.ptr, n, src, gal, out))
         return [Ciphertext(self._ctx, out[i]) for i in range(n)]
+
+    # ---------------------------------------------------------------- stacked ciphertexts
+    def stack(self, cts) -> Ciphertext:
+        """n single ciphertexts -> ONE stacked ciphertext of n members (aesfhe_stack): every op
+        then runs on all members at once; operands of one op are stacks of one size"""
+        cts = list(cts)
+        H = ctypes.c_uint64 * len(cts)
+        out = ctypes.c_uint64()
+        self._ctx.check(self._lib.aesfhe_stack(self._ctx.ptr, len(cts), H(*[c.handle for c in cts]), ctypes.byref(out)))
+        return Ciphertext(self._ctx, out.value)
+
+    def unstack(self, ct) -> List[Ciphertext]:
+        """the members of a stack as single ciphertexts (aesfhe_unstack)"""
+        n = self.members(ct)
+        out = (ctypes.c_uint64 * n)()
+        self._ctx.check(self._lib.aesfhe_unstack(self._ctx.ptr, ct.handle, n, out))
+        return [Ciphertext(self._ctx, out[i]) for i in range(n)]
+
+    def members(self, ct) -> int:
+        m = ctypes.c_int()
+        self._ctx.check(self._lib.aesfhe_members(self._ctx.ptr, ct.handle, ctypes.byref(m)))
+        return m.value
 
     def rotate_multi(self, items) -> List[Ciphertext]:
         """[(ct, steps)] -> [np.roll(slots(ct), steps)] as one galois_multi"""

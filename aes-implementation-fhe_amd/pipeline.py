@@ -63,9 +63,12 @@ class AESPipeline:
                  inv_mixcolumns: InvMixColumnsFHE | None = None, use_hard_renorm_between_steps: bool = False,
                  with_inv_mix_columns: bool = True, states: int = 1, fuse_sub_ark: bool = False,
                  fuse_sr_mc: bool = False, true_fhe: bool = False, periodic: bool | None = None,
-                 packed_xor: bool | None = None):
+                 packed_xor: bool | None = None, pairs: int = 1):
         self.ctx = ctx
         self.states = states
+        # pairs > 1: a multi-pair batch -- `pairs` ciphertext pairs of `states` states each, run as
+        # ONE stacked pair through every step (state_encoder.StateEncoder)
+        self.pairs = pairs
         # periodic layout (state_encoder.SlotLayout): default on where the engine
         # has the sparse-slot bootstrap and the state count is a power of two
         if periodic is None:
@@ -74,7 +77,7 @@ class AESPipeline:
                 lay = getattr(mod, "layout", None)
                 if lay is not None:
                     periodic = lay.periodic
-        self.encoder = StateEncoder(ctx, states, periodic=periodic)
+        self.encoder = StateEncoder(ctx, states, periodic=periodic, pairs=pairs)
         self.layout = self.encoder.layout
         self.sc = ctx.engine.slot_count
         self.stride = self.layout.unit

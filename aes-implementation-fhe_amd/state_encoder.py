@@ -109,12 +109,22 @@ def _describe(lay: SlotLayout) -> str:
 
 
 class StateEncoder:
-    def __init__(self, ctx, states: int = 1, periodic: bool = False):
+    """pairs > 1: a multi-pair batch -- `pairs` independent ciphertext pairs,
+    each holding `states` states in this layout, carried as ONE stacked hi and ONE stacked lo
+    ciphertext (ctx.stack): encode takes (pairs, states, 16) / (pairs, 16) bytes, decode returns
+    them, and every AES module runs on the stacks unchanged."""
+
+    def __init__(self, ctx, states: int = 1, periodic: bool = False, pairs: int = 1):
         self.ctx = ctx
         self.sc = ctx.engine.slot_count
         self.layout = SlotLayout(self.sc, states, periodic)
         self.stride = self.layout.unit  # rotation unit (REF: slot_count / 16)
         self.states = states
+        if pairs < 1:
+            raise ValueError("pairs must be >= 1")
+        if pairs > 1 and getattr(ctx, "stack", None) is None:
+            raise ValueError("multi-pair batches need a context with stacked ciphertexts (ctx.stack)")
+        self.pairs = pairs
         # set by AESPipeline(true_fhe=True): renorm(hi, lo) -> hook(hi, lo), the bootstrap + snap
         # that replaces the secret-key renorm (zeta16_noise_reducer.BootstrapSnap)
         self.renorm_hook = None
@@ -137,12 +147,33 @@ class StateEncoder:
         """slot vector -> (B, 16) state slots"""
         return slots[:16 * self.stride].reshape(16, self.stride)[:, :self.states].T
 
+    def _pair_states(self, state: np.ndarray):
+        """(pairs, ...) bytes -> the per-pair state arrays; a single pair's shape broadcasts"""
+        state = np.asarray(state, dtype=np.uint8)
+        one = (16,) if self.states == 1 else (self.states, 16)
+        if state.shape == one:
+            return [state] * self.pairs
+        if state.shape != (self.pairs,) + one:
+            raise ValueError(f"expected a {(self.pairs,) + one} uint8 state array, got {state.shape}")
+        return list(state)
+
     def encode(self, state: np.ndarray) -> Tuple[Any, Any]:
+        if self.pairs > 1:
+            his, los = zip(*[self._encode1(s) for s in self._pair_states(state)])
+            return tag_layout(self.layout, self.ctx.stack(his), self.ctx.stack(los))
+        return self._encode1(state)
+
+    def _encode1(self, state):
         st = self._as_batch(state)
         return tag_layout(self.layout, self.ctx.encrypt(self._pack(st >> 4)), self.ctx.encrypt(self._pack(st & 0x0F)))
 
     def decode(self, ct_hi, ct_lo) -> np.ndarray:
         check_layout(self.layout, ct_hi, ct_lo)
+        if self.pairs > 1:
+            return np.stack([self._decode1(h, l) for h, l in zip(self.ctx.unstack(ct_hi), self.ctx.unstack(ct_lo))])
+        return self._decode1(ct_hi, ct_lo)
+
+    def _decode1(self, ct_hi, ct_lo) -> np.ndarray:
         hi = ZetaEncoder.from_zeta(self._take(self.ctx.decrypt(ct_hi)), 16)
         lo = ZetaEncoder.from_zeta(self._take(self.ctx.decrypt(ct_lo)), 16)
         out = ((hi << 4) | lo).astype(np.uint8)
@@ -167,10 +198,18 @@ class StateEncoder:
 
     def encode_packed(self, state: np.ndarray):
         """a state (batch) encrypted directly in the packed form"""
+        if self.pairs > 1:
+            cts = [self.ctx.encrypt(self._packed_slots(self._as_batch(s))) for s in self._pair_states(state)]
+            return tag_layout(self.layout, self.ctx.stack(cts))[0]
         return tag_layout(self.layout, self.ctx.encrypt(self._packed_slots(self._as_batch(state))))[0]
 
     def decode_packed(self, ct) -> np.ndarray:
         check_layout(self.layout, ct)
+        if self.pairs > 1:
+            return np.stack([self._decode_packed1(c) for c in self.ctx.unstack(ct)])
+        return self._decode_packed1(ct)
+
+    def _decode_packed1(self, ct) -> np.ndarray:
         z = self.ctx.decrypt(ct)
         hi = ZetaEncoder.from_zeta(self._take(z), 16)
         lo = ZetaEncoder.from_zeta(self._take(z[self.layout.period:]), 16)

@@ -72,6 +72,14 @@ def parse():
                     help="secondary measurement (BASELINE configs 3/4): this many independent states per rank, "
                          "slot-packed into one ciphertext pair (SURVEY.md 8(f)1); 0 = skip")
     ap.add_argument("--batch-steps", type=int, default=3)
+    ap.add_argument("--pair-states", type=int, default=64,
+                    help="multi-pair batch, BASELINE config 3's shape (one state per ciphertext pair): this many pairs "
+                         "per rank as stacked ciphertexts (DESIGN.md 3.16); 0 = skip")
+    ap.add_argument("--pair-stack", type=int, default=64,
+                    help="pairs per stack: --pair-states pairs run as ceil(pair-states / pair-stack) stacks in turn")
+    ap.add_argument("--packed-pairs", type=int, default=2,
+                    help="multi-pair slot-packed batch: this many stacked ciphertext pairs of 2048 states each per rank; 0 = skip")
+    ap.add_argument("--pair-steps", type=int, default=3, help="timed steps of the multi-pair legs")
     ap.add_argument("--true-fhe-steps", type=int, default=1,
                     help="SURVEY.md 8(f)3 line beside the headline: C2 encrypts with every secret-key renorm replaced "
                          "by bootstrap + homomorphic Zeta16 snap (AESPipeline(true_fhe=True)); 0 = skip")
@@ -234,6 +242,41 @@ def rank_states(rank: int, n: int):
     """Independent synthetic states of one rank (weak scaling: each rank owns its own)."""
     rng = np.random.default_rng(2025 + rank)
     return [rng.integers(0, 256, 16).astype(np.uint8) for _ in range(n)]
+
+
+def run_pairs(ctx, coeffs, rks, args, rank, world, dist, pairs: int, states: int, stack: int, workload: str) -> dict:
+    """Multi-pair batch: `pairs` independent ciphertext pairs of `states` states each
+    per rank, run as stacked ciphertexts of `stack` pairs (AESPipeline(pairs=...)), one after the
+    other; full 10-round encrypt with renorm and final bootstraps.  Whole-job blocks/s = states
+    encrypted by all ranks / max time; every pair's output checked against the plaintext AES."""
+    from oracle import aes_plain  # checker only, after the timed region
+    from pipeline import AESPipeline
+    chunks = [min(stack, pairs - i) for i in range(0, pairs, stack)]
+    pipes = {c: AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=True, states=states, pairs=c) for c in set(chunks)}
+    rng = np.random.default_rng(8192 + rank)
+    shape = lambda c: (c, 16) if states == 1 else (c, states, 16)  # noqa: E731
+    steps = [[rng.integers(0, 256, shape(c), dtype=np.uint8) for c in chunks] for _ in range(1 + args.pair_steps)]
+    E = ctx.engine
+    for c, b in zip(chunks, steps[0]):  # warmup: masks, LUT constants, codec buffers, stacked keys
+        pipes[c].encrypt(b, rks)
+    E.sync()
+    barrier(dist)
+    t0 = time.perf_counter()
+    outs = [[pipes[c].encrypt(b, rks) for c, b in zip(chunks, st)] for st in steps[1:]]
+    E.sync()
+    barrier(dist)
+    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    ok = True
+    for st, ot in zip(steps[1:], outs):
+        for c, b, o in zip(chunks, st, ot):
+            got = pipes[c].encoder.decode(*o).reshape(-1, 16)
+            ok &= all(np.array_equal(got[j], aes_plain.ref_encrypt(s, rks)) for j, s in enumerate(b.reshape(-1, 16)))
+    ok = all(r[0] for r in all_gather_ints(dist, [int(ok)]))
+    blocks = pairs * states * args.pair_steps * world
+    return {"workload": workload, "pairs_per_rank": pairs, "states_per_pair": states, "pairs_per_stack": stack,
+            "stacks_per_step": len(chunks), "steps": args.pair_steps, "n_gpus": world,
+            "blocks_per_s": blocks / elapsed, "rounds_per_s": 10.0 * blocks / elapsed,
+            "ms_per_step": elapsed / args.pair_steps * 1e3, "verified_against_plaintext_model": bool(ok)}
 
 
 def run_batch(ctx, coeffs, rks, args, rank, world, dist) -> dict:
@@ -440,6 +483,14 @@ def main():
         Path(args.whole_stats).write_text(json.dumps(tot, indent=1))
     E.profile(())
     batch = run_batch(ctx, coeffs, rks, args, rank, world, dist) if args.batch_states > 0 else None
+    pairs_c3 = run_pairs(ctx, coeffs, rks, args, rank, world, dist, args.pair_states, 1, max(1, args.pair_stack),
+                         f"C3 shape: {args.pair_states} ciphertext pairs per GPU with ONE state each (REF/state_encoder.py:17-28), "
+                         f"stacked {args.pair_stack} pairs per operand (DESIGN.md 3.16), full AES-128 encrypt, N=2^16, renorm on, "
+                         f"shared key") if args.pair_states > 0 else None
+    pairs_packed = run_pairs(ctx, coeffs, rks, args, rank, world, dist, args.packed_pairs, 2048, args.packed_pairs,
+                             f"{args.packed_pairs} x 2048 states per GPU: {args.packed_pairs} slot-packed ciphertext pairs stacked "
+                             f"into one operand (DESIGN.md 3.9 + 3.16), full AES-128 encrypt, N=2^16, renorm on, shared key"
+                             ) if args.packed_pairs > 0 else None
     true_fhe = run_true_fhe(ctx, coeffs, rks, args, rank, world, dist) if args.true_fhe_steps > 0 and not args.no_final_bootstrap else None
 
     # correctness of the timed outputs (outside the timed region)
@@ -534,6 +585,10 @@ def main():
     }
     if batch is not None:
         line["batch"] = batch
+    if pairs_c3 is not None:
+        line["batch_pairs"] = pairs_c3
+    if pairs_packed is not None:
+        line["batch_packed_pairs"] = pairs_packed
     if true_fhe is not None:
         line["true_fhe"] = true_fhe
     if args.profile_all:

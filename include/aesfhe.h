@@ -161,6 +161,20 @@ int aesfhe_conjugate_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, aesfh
  * one key-inner-product launch with a key per member, one stacked ModDown.  Same results as the
  * separate calls; galois[i] = 1 returns a copy. */
 int aesfhe_galois_multi(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, const uint64_t* galois, aesfhe_handle* out);
+
+/* Stacked ciphertexts (multi-pair batches, BASELINE configs 3-5 with one state per pair; DESIGN.md
+ * §3.16).  aesfhe_stack: n single ciphertexts -> ONE handle holding n members (canonical form,
+ * dropped to the lowest member level).  Every operation then takes the stack as one operand and
+ * returns a stack: element-wise work in one launch over all members, key switches in chunks of
+ * members that read each key once, LUT sums with a member grid dimension, renorms decrypting /
+ * re-encrypting every member in one set of launches, bootstraps in chunks of two members.
+ * Operands of one operation must be stacks of the same size (no broadcasting); decrypt needs a
+ * single ciphertext.  aesfhe_unstack: the n members as single handles (n = member count);
+ * aesfhe_members: the member count (1 for a single ciphertext).  Replaces the reference's loop
+ * over independent ciphertext pairs (REF/main.py:121-140 runs one pair per state). */
+int aesfhe_stack(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, aesfhe_handle* out);
+int aesfhe_unstack(aesfhe_ctx* ctx, aesfhe_handle in, int n, aesfhe_handle* out);
+int aesfhe_members(aesfhe_ctx* ctx, aesfhe_handle h, int* members);
 /* n rotations of ONE ciphertext, engine.rotate(ct, rotation_key, steps[i])
  * (REF/engine_context.py:127-132; the column shifts of REF/mixcol_final.py:124-154 and the
  * row rotations of REF/shift_rows.py:39-56), hoisted: one ModUp for all of them.  Same

@@ -174,3 +174,29 @@ def test_layout_tags_are_checked():
     with pytest.raises(ValueError, match="periodic"):
         check_layout(ref, c)
     tag_layout(ref, np.zeros(3))  # untaggable ciphertexts (the CPU stand-ins) are left alone
+
+
+def test_multi_pair_encoder_shapes():
+    """StateEncoder(pairs=P): (P, 16) / (P, B, 16) bytes -> one stacked pair and
+    back; a single pair's bytes broadcast to every pair (round keys)"""
+    from state_encoder import StateEncoder
+
+    class StackCtx(_SlotCtx):
+        def stack(self, cts):
+            return np.stack(cts)
+
+        def unstack(self, st):
+            return list(st)
+
+    ctx = StackCtx()
+    rng = np.random.default_rng(3)
+    for states, shape in ((1, (4, 16)), (5, (4, 5, 16))):
+        enc = StateEncoder(ctx, states, pairs=4)
+        st = rng.integers(0, 256, shape, dtype=np.uint8)
+        hi, lo = enc.encode(st)
+        assert hi.shape == (4, 256)
+        assert np.array_equal(enc.decode(hi, lo), st)
+        key = st[0]
+        assert np.array_equal(enc.decode(*enc.encode(key)), np.stack([key] * 4))
+    with pytest.raises(ValueError):
+        StateEncoder(_SlotCtx(), 1, pairs=2)  # no stacked ciphertexts in this context
