@@ -980,12 +980,11 @@ public:
 
     // + constant at the tensor's raw scale: round(c delta_m) times the primes the owed
     // rescales will divide out (m = logical level), so nothing has to be applied first
-    Ct add_scalar(const Ct& c_in, double re, double im) {
-        Ct c = ensure_ntt(c_in);
-        const int nl = hp_.nl(c.level), m = c.level - c.pend;
+    LimbConsts add_consts(int level, int pend, double re, double im) {
+        const int nl = hp_.nl(level), m = level - pend;
         std::vector<u32> lo, hi;
         scalar_residues(std::llround(re * hp_.delta[m]), std::llround(im * hp_.delta[m]), nl, lo, hi);
-        if (c.pend > 0)
+        if (pend > 0)
             for (int t = 0; t < nl; ++t) {
                 u64 f = 1;
                 for (int i = hp_.nl(m); i < nl; ++i) f = f * (hp_.mod[i] % hp_.mod[t]) % hp_.mod[t];
@@ -995,13 +994,55 @@ public:
         if (nl > 2 * kMaxConstLimbs) throw std::runtime_error("add_scalar: too many limbs");
         LimbConsts d{};
         for (int t = 0; t < nl; ++t) d.v[2 * t] = lo[t], d.v[2 * t + 1] = hi[t];
-        Ct o = copy(c);
-        o.zero = false;
-        for (int m = 0; m < c.nb; ++m) {  // the first polynomial of every batched ciphertext
-            const size_t off = (size_t)m * pm(c) * nl * hp_.n;
-            launch_add_const_half(S(), T_, o.data + off, c.data + off, d, nl, nl, qmap());
+        return d;
+    }
+    Ct add_scalar(const Ct& c_in, double re, double im) { return lincomb(c_in, 1, nullptr, 0, re, im); }
+    // k a + s b + c in ONE launch (k a Gaussian integer, s = +1 / -1 / 0 for no b, c a complex
+    // constant): b is first re-expressed at a's (data level, owed rescales) when they differ (a's
+    // logical level not above b's), else the general add_sub path.  EvalMod's recurrences
+    // 2 T_a T_b - T_(a-b) and 2 T^2 - 1, and add_scalar (k = 1, no b)
+    Ct lincomb(const Ct& a_in, i64 k, const Ct* b_in, int s, double cre, double cim) {
+        Ct a = ensure_ntt(a_in);
+        const bool own_a = a.data != a_in.data;
+        Ct b;
+        bool own_b = false;
+        if (b_in && s) {
+            b = ensure_ntt(*b_in);
+            own_b = b.data != b_in->data;
+            const bool same = b.level == a.level && b.pend == a.pend && b.npoly == a.npoly && b.nb == a.nb && !b.zero;
+            if (!same) {
+                const bool can = b.nb == a.nb && pm(b) == pm(a) && !b.zero && a.level <= b.level && a.level - a.pend <= b.level - b.pend;
+                if (!can) {  // the general path
+                    if (own_b) release(b);
+                    Ct ka = k == 1 ? copy(a) : mul_scalar(a, (double)k, 0.0);
+                    if (own_a) release(a);
+                    Ct t = add_sub(ka, *b_in, s < 0);
+                    release(ka);
+                    if (cre == 0.0 && cim == 0.0) return t;
+                    Ct o = lincomb(t, 1, nullptr, 0, cre, cim);
+                    release(t);
+                    return o;
+                }
+                Ct cb = convert(b, a.level, a.pend);
+                if (own_b) release(b);
+                b = cb, own_b = true;
+            }
         }
-        if (c.data != c_in.data) release(c);
+        const int nl = hp_.nl(a.level);
+        std::vector<u32> lo, hi;
+        scalar_residues(k, 0, nl, lo, hi);
+        const bool has_c = cre != 0.0 || cim != 0.0;
+        LimbConsts cadd{};
+        if (has_c) cadd = add_consts(a.level, a.pend, cre, cim);
+        Ct o = alloc_ct(a.level, a.npoly, a.nb);
+        copy_meta(o, a);
+        o.zero = a.zero && !(b_in && s) && !has_c && k != 0;
+        o.lazy = a.lazy || (b_in && s && b.lazy);
+        launch_lincomb(S(), T_, o.data, a.data, const_half(lo, hi), (b_in && s) ? b.data : nullptr, s, has_c ? &cadd : nullptr, pm(a),
+                       a.npoly * nl, nl, qmap());
+        if (own_a) release(a);
+        if (own_b) release(b);
+        if (b_in && s) cnt_[C_ADD]++;
         return o;
     }
 
@@ -1302,7 +1343,9 @@ public:
     // polys in one launch, NTT fused with (acc_Q - conv) P^{-1} (+ add)
     // nb batched ciphertexts: acc = [m][2][ne]; member m adds add0/add1 + m add_ms words
     // dst: write the result there (member stride 2 nl N; the caller owns it) instead of a new buffer
-    Ct moddown(const u32* acc, int level, const u32* add0, const u32* add1, int nb = 1, size_t add_ms = 0, u32* dst = nullptr) {
+    // outm: member m's result into outm[m] (nb <= 8; the returned Ct then carries no data)
+    Ct moddown(const u32* acc, int level, const u32* add0, const u32* add1, int nb = 1, size_t add_ms = 0, u32* dst = nullptr,
+               u32* const* outm = nullptr) {
         const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, npl = 2 * nb;
         if (npl > kMaxConvGroups) throw std::runtime_error("moddown: batch too large");
         u32* yp = tmp((size_t)npl * np);
@@ -1321,12 +1364,12 @@ public:
         }
         launch_base_convert(S(), T_, dn, nl, qmap());
         Ct o;
-        if (dst) {
+        if (dst || outm) {
             o.level = level, o.npoly = npl, o.nb = nb, o.words = (size_t)npl * nl * n, o.data = dst;
         } else {
             o = alloc_ct(level, npl, nb);
         }
-        launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_pinv_, add0, add1, npl, nl, add_ms);
+        launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_pinv_, add0, add1, npl, nl, add_ms, outm);
         cnt_[C_NTT_ROWS] += (size_t)npl * nl;
         untmp(yp, (size_t)npl * np);
         untmp(conv, (size_t)npl * nl);
@@ -1437,8 +1480,10 @@ public:
     }
     // a stack of more than ks_chunk members in chunks, each chunk's ModDown writing its rows of
     // the one stacked result
-    Ct relin_rescale(const Ct& c) {
+    // outm (nb <= ks_chunk): member m's result straight into outm[m]; the returned Ct has no data
+    Ct relin_rescale(const Ct& c, u32* const* outm = nullptr) {
         const int l = c.level, n = hp_.n, nl = hp_.nl(l), ne = nl + hp_.n_p, nb = c.nb, ch = ks_chunk(l);
+        if (outm && nb > ch) throw std::runtime_error("relin_rescale: per-member outputs need one chunk");
         const size_t ms = (size_t)3 * nl * n;
         Ct o;
         if (nb > ch) {
@@ -1460,7 +1505,7 @@ public:
             u32* acc = tmp(2 * (size_t)ne * nb);
             key_inner(acc, ext, d2, ksk(0), l, 0, nb, ms, KsFold{c.data, c.data + (size_t)nl * n, ms, d_gadget_});
             untmp(ext, (size_t)nb * ext_rows(l));
-            o = moddown_rescale(acc, l, nb);
+            o = moddown_rescale(acc, l, nb, nullptr, outm);
             untmp(acc, 2 * (size_t)ne * nb);
         }
         o.pend = c.pend - 1;
@@ -1471,7 +1516,7 @@ public:
     }
     // acc = [m][2][ne] in Q*P, NTT form, already holding P * (the ciphertext) -> the ciphertext
     // divided by the dropped limbs of level l, at level l - 1 (one ModDown by Q' = P * D)
-    Ct moddown_rescale(const u32* acc, int l, int nb, u32* dst = nullptr) {
+    Ct moddown_rescale(const u32* acc, int l, int nb, u32* dst = nullptr, u32* const* outm = nullptr) {
         const int n = hp_.n, nl = hp_.nl(l), r = hp_.nl(l - 1), k = nl - r, np = hp_.n_p, ne = nl + np;
         const int npl = 2 * nb, h = k + np;
         if (mdr_off_[l] == SIZE_MAX || npl > kMaxConvGroups) throw std::runtime_error("moddown_rescale: unsupported level or batch");
@@ -1492,12 +1537,12 @@ public:
         launch_base_convert(S(), T_, cb, r, qmap());
         untmp(ys, (size_t)npl * h);
         Ct o;
-        if (dst) {
+        if (dst || outm) {
             o.level = l - 1, o.npoly = npl, o.nb = nb, o.words = (size_t)npl * r * n, o.data = dst;
         } else {
             o = alloc_ct(l - 1, npl, nb);
         }
-        launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_mdr_ + off + 2 * (size_t)h * (r + 1) + r, nullptr, nullptr, npl, r);
+        launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_mdr_ + off + 2 * (size_t)h * (r + 1) + r, nullptr, nullptr, npl, r, 0, outm);
         cnt_[C_NTT_ROWS] += (size_t)npl * r;
         untmp(conv, (size_t)npl * r);
         cnt_[C_RESCALE]++;
@@ -1654,16 +1699,24 @@ public:
                 const int c = std::min(chunk, g - m0);
                 Ct v = d;  // view of members m0 .. m0 + c - 1 (not released on its own)
                 v.data = d.data + (size_t)m0 * 3 * nl * nn, v.npoly = 3 * c, v.nb = c, v.words = (size_t)3 * c * nl * nn;
-                Ct o;
                 if (fused_relin_rescale_ok(v)) {
-                    o = relin_rescale(v);
+                    // each member's ModDown finish writes its own output buffer: no unstack copy
+                    u32* om[kMaxKsBatch];
+                    for (int m = 0; m < c; ++m) {
+                        Ct& r = out[grp[m0 + m]];
+                        r = alloc_ct(L - 1, 2);
+                        r.ntt = true, r.pend = 0, r.lazy = false;
+                        om[m] = r.data;
+                    }
+                    Ct o = relin_rescale(v, om);
+                    (void)o;
                 } else {
                     Ct r = relin_raw(v);
-                    o = rescale(r);
+                    Ct o = rescale(r);
                     release(r);
+                    unstack(o, &out[0], grp.data() + m0);
+                    release(o);
                 }
-                unstack(o, &out[0], grp.data() + m0);
-                release(o);
             }
             release(d);
         }
@@ -1983,11 +2036,16 @@ public:
                 const size_t ms = (size_t)2 * nl * nn;
                 u32* c0p = tmp((size_t)nm * 2 * nl);  // member stride 2 nl N (moddown's add stride), first nl rows used
                 launch_automorph_multi(S(), T_, c0p, ms, am, nm, nl);
-                Ct o = moddown(acc, l, c0p, nullptr, nm, ms);
+                u32* om[kMaxMembers];  // each member's ModDown finish writes its own buffer: no unstack copy
+                for (int m = 0; m < nm; ++m) {
+                    Ct& r = out[chunk[m]];
+                    r = alloc_ct(l, 2);
+                    r.ntt = true, r.pend = 0, r.lazy = false;
+                    om[m] = r.data;
+                }
+                moddown(acc, l, c0p, nullptr, nm, ms, nullptr, om);
                 untmp(acc, (size_t)nm * 2 * ne);
                 untmp(c0p, (size_t)nm * 2 * nl);
-                unstack(o, &out[0], chunk.data());
-                release(o);
                 cnt_[C_KS] += nm;
             }
         }
@@ -2211,8 +2269,10 @@ public:
     // unpack = n > 0: hh is a packed state (hi | lo halves of every 2n-slot block, the
     // pipeline's packed XOR stage) and hl must be hh; oh / ol get its hi / lo halves as
     // n-periodic states.  single: hh == hl, one output (ol untouched) with every slot snapped.
+    // single with packed_period = 32 (the packed XOR stage's hi | lo form, period 2 x 16): the
+    // 32 slots are decoded / re-encoded directly (decode32 / encode32, no FFT); unpack = 16 likewise
     void renorm_states(aesfhe_handle hh, aesfhe_handle hl, int states, aesfhe_handle* oh, aesfhe_handle* ol, int level = -1,
-                       int period = 0, int unpack = 0, bool single = false) {
+                       int period = 0, int unpack = 0, bool single = false, int packed_period = 0) {
         if (!d_pk_) throw std::runtime_error("keys not generated");
         if (unpack || single) {
             if (hl != hh) throw std::runtime_error("renorm: a packed / single renorm reads one ciphertext");
@@ -2237,6 +2297,7 @@ public:
             for (int j = 0; j < s; ++j) {
                 if (j % stride == 0) slots_.e[j / stride] = (u32)e;
                 if (j < 16) slots_p_.e[j] = (u32)e;
+                if (j < 32) slots32_.e[j] = (u32)e;
                 e = e * 5 % two_n;
             }
             for (int k = 0; k < kStreams; ++k) {
@@ -2293,7 +2354,18 @@ public:
         const int f = level < 0 ? hp_.fresh : level, nq = hp_.nl(f) + 1;
         const double enc_scale = hp_.delta[f] * (double)hp_.mod[hp_.nl(f)];
         u32* m = tmp(2 * (size_t)nq);
-        if (states == 1) {
+        const bool direct32 = direct32_ && ((unpack == 16) || (single && packed_period == 32));
+        if (direct32) {
+            // the 32 slots of the packed period-32 state: one direct decode, the snap as 2 x 16, and
+            // either the two 16-periodic halves (unpack) or the 32-periodic whole (single)
+            double* acc = d_codec_[t_sidx];
+            double* wv = acc + 64;
+            HIP_OK(hipMemsetAsync(acc, 0, 64 * sizeof(double), S()));
+            launch_decode32(S(), T_, x, kd[0], cc[0], slots32_, isc[0], acc);
+            launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
+            if (unpack) launch_encode16(S(), T_, m, wv, slots_p_, enc_scale, nq, true);
+            else launch_encode32(S(), T_, m, wv, slots32_, enc_scale, nq);
+        } else if (states == 1) {
             double* acc = d_codec_[t_sidx];
             double* wv = acc + 64;
             HIP_OK(hipMemsetAsync(acc, 0, 64 * sizeof(double), S()));
@@ -3105,10 +3177,9 @@ public:
             for (int i = 0; i < ni; ++i)
                 for (int k = lo; k <= hi; ++k, ++j) {
                     const int a = (k + 1) / 2, b = k / 2;
-                    Ct p2 = mul_scalar(P[j], 2.0, 0.0);
+                    // 2 T_a T_b - T_(a-b) (a > b) / 2 T_a^2 - 1, one launch each
+                    T[i][k] = (a == b) ? lincomb(P[j], 2, nullptr, 0, -1.0, 0.0) : lincomb(P[j], 2, &T[i][a - b], -1, 0.0, 0.0);
                     release(P[j]);
-                    T[i][k] = (a == b) ? add_scalar(p2, -1.0, 0.0) : add_sub(p2, T[i][a - b], true);
-                    release(p2);
                 }
             lo = hi + 1;
         }
@@ -3119,10 +3190,8 @@ public:
             for (int i = 0; i < ni; ++i) A.push_back(&giant[i].at(m / 2));
             std::vector<Ct> P = mul_list(A, A);
             for (int i = 0; i < ni; ++i) {
-                Ct p2 = mul_scalar(P[i], 2.0, 0.0);
+                giant[i][m] = lincomb(P[i], 2, nullptr, 0, -1.0, 0.0);  // 2 T^2 - 1, one launch
                 release(P[i]);
-                giant[i][m] = add_scalar(p2, -1.0, 0.0);
-                release(p2);
             }
         }
         std::vector<int> in(ni);
@@ -3139,10 +3208,8 @@ public:
             std::vector<Ct> P = mul_list(A, A);
             for (int i = 0; i < ni; ++i) {
                 release(g[i]);
-                Ct sq2 = mul_scalar(P[i], 2.0, 0.0);
+                g[i] = lincomb(P[i], 2, nullptr, 0, -1.0, 0.0);  // double angle 2 g^2 - 1, one launch
                 release(P[i]);
-                g[i] = add_scalar(sq2, -1.0, 0.0);
-                release(sq2);
             }
         }
         return g;
@@ -3911,6 +3978,9 @@ private:
     CrtConsts crt_[4] = {};
     std::unordered_map<aesfhe_handle, Lut> luts_;
     Slot16 slots_ = {};    // the reference layout's 16 state slots, 5^(i N/32)
+    Slot32 slots32_ = {};  // the first 32 slots, 5^j (the packed period-32 form)
+    // AESFHE_RENORM_DIRECT32=0: the packed renorms through the FFT codec (A/B runs)
+    bool direct32_ = !(std::getenv("AESFHE_RENORM_DIRECT32") && std::atoi(std::getenv("AESFHE_RENORM_DIRECT32")) == 0);
     Slot16 slots_p_ = {};  // the 16-periodic layout's, 5^i
     double* d_codec_[kStreams] = {};
     int* d_nib_[kStreams] = {};
@@ -4287,6 +4357,12 @@ int aesfhe_renorm_unpack(aesfhe_ctx* ctx, aesfhe_handle packed, int period, int 
 }
 int aesfhe_renorm_single(aesfhe_ctx* ctx, aesfhe_handle c, int level, aesfhe_handle* out) {
     API_BEGIN ctx->eng->renorm_states(c, c, 1, out, nullptr, level, 0, 0, true);
+    API_END
+}
+int aesfhe_renorm_packed(aesfhe_ctx* ctx, aesfhe_handle c, int period, int level, aesfhe_handle* out) {
+    API_BEGIN
+    if (period < 16 || (period & (period - 1))) throw std::runtime_error("renorm_packed: period must be a power of two >= 16");
+    ctx->eng->renorm_states(c, c, 1, out, nullptr, level, 0, 0, true, period);
     API_END
 }
 int aesfhe_renorm_states(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, int states, aesfhe_handle* out_hi,

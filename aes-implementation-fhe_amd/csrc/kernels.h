@@ -87,6 +87,9 @@ struct NttAux {
     u32 q_last = 0;            // spread: modulus of the source row
     u32 q_last2 = 0;           // spread2: second dropped prime (source rows a, b per group)
     u32 qa_inv = 0, qa_inv_p = 0;  // spread2: q_last^{-1} mod q_last2 (Shoup pair)
+    // finish: member m's result (groups 2m, 2m + 1) written to outm[m] (2 polys x out_stride rows)
+    // when set -- the members of a batched key switch straight into their own buffers, no unstack copy
+    u32* outm[8] = {};
 };
 // out-of-place (src may equal dst); supported ring sizes 2^13 .. 2^16
 void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map);
@@ -104,7 +107,7 @@ void launch_rescale2_ntt(hipStream_t st, const DevTables& T, u32* out, const u32
 // out[p][t] = (cur[p * cur_stride + t] - NTT(conv)[p][t]) * qinv_t (+ add_p[t])   (ModDown)
 // npoly = 2 nb for nb batched ciphertexts: group 2 m + p adds add_p + m add_mstride (words)
 void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, const u32* cur, int cur_stride, const u32* qinv,
-                       const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride = 0);
+                       const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride = 0, u32* const* outm = nullptr);
 // in place on rows = npoly * nl dense rows
 void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map);
 void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map);
@@ -159,6 +162,10 @@ void launch_addsub_tail(hipStream_t st, const DevTables& T, u32* out, const u32*
                         bool sub, int nl, LimbMap map);
 // out[row][k] = in[row][k] + (k < N/2 ? alo[l] : ahi[l]); layout v[2 l .. 2 l + 1]
 void launch_add_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const LimbConsts& cst, int rows, int nl, LimbMap map);
+// out = ka a + bsign b (b optional) + cadd on the rows of the first polynomial of every member
+// (per polys per member); ka: Shoup pairs {lo, lo', hi, hi'} per limb, cadd: {lo, hi} per limb
+void launch_lincomb(hipStream_t st, const DevTables& T, u32* out, const u32* a, const LimbConsts& ka, const u32* b, int bsign,
+                    const LimbConsts* cadd, int per, int rows, int nl, LimbMap map);
 // X -> X^g in the NTT domain (bit-reversed evaluation order)
 void launch_automorph(hipStream_t st, const DevTables& T, u32* out, const u32* in, u64 g, int rows);
 
@@ -332,6 +339,15 @@ void launch_snap16(hipStream_t st, const double* acc, double* w, int* nib);
 // out[c][t][k] = round(scale (delta_{k0} + (2/N) Re sum_i w_ci e^{-i pi e_i k / N})) mod q_t, t < nq
 // periodic: the 16-periodic layout (positions sl.e = 5^i, only k == 0 mod N/32 nonzero)
 void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq, bool periodic = false);
+// direct codec of a small-period packed renorm (period 32: the hi | lo halves of the packed XOR
+// stage): acc[i] = the 32 slot values (slot j at 5^j) of ONE decryption (acc zeroed by the
+// caller); launch_snap16 snaps them as 2 x 16; encode32 re-encodes w as ONE 32-periodic message
+// (unpack instead: launch_encode16(periodic) of the two 16-value halves)
+struct Slot32 {
+    u32 e[32];
+};
+void launch_decode32(hipStream_t st, const DevTables& T, const u32* x, int kd, const CrtConsts& cc, const Slot32& sl, double inv_scale, double* acc);
+void launch_encode32(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot32& sl, double scale, int nq);
 
 // --- slot-packed Zeta16 renorm ----------------------
 // Full canonical-embedding decode / encode on the device in fp64: the slots of a real

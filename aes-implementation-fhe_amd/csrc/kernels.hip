@@ -144,6 +144,20 @@ __global__ void k_add_const_half(u32* out, const u32* in, LimbConsts cst, int nl
     out[idx] = add_mod(in[idx], cst.v[2 * limb + hi], P.q);
 }
 
+// out = ka a + s b + c: ka a Gaussian-integer constant (Shoup pairs per limb and slot half), b
+// optional with sign s = +-1, c an additive constant on the first polynomial of every member
+// (per polys per member) -- EvalMod's 2 T_a T_b - T_(a-b) / 2 T^2 - 1 and add_scalar in one launch
+__global__ void k_lincomb(u32* out, const u32* a, LimbConsts ka, const u32* b, int bsign, LimbConsts cadd, int has_c, int per, int nl,
+                          LimbMap map, const PrimeConst* pc, int logn) {
+    EW_PROLOGUE
+    const int hi = (int)(k >> (logn - 1));
+    const u32* c = ka.v + 4 * limb + 2 * hi;
+    u32 v = shoup_mul(a[idx], c[0], c[1], P.q);
+    if (b) v = bsign > 0 ? add_mod(v, b[idx], P.q) : sub_mod(v, b[idx], P.q);
+    if (has_c && (row / nl) % per == 0) v = add_mod(v, cadd.v[2 * limb + hi], P.q);
+    out[idx] = v;
+}
+
 // X -> X^g: NTT slot i holds a(psi^{2 brv(i) + 1}); the image at i is slot j with
 // 2 brv(j) + 1 = (2 brv(i) + 1) g mod 2N
 __global__ void k_automorph(u32* out, const u32* in, u64 g, int logn) {
@@ -655,6 +669,57 @@ __global__ void __launch_bounds__(kBlock) k_decode16(const u32* x, int kd0, int 
     }
 }
 
+// 32 slot values of one decryption (the packed period-32 state): partial sums per block, atomically added
+__global__ void __launch_bounds__(kBlock) k_decode32(const u32* x, int kd, CrtConsts cc, Slot32 sl, double is, double* acc, int logn) {
+    const int n = 1 << logn;
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    u32 r[4];
+    for (int i = 0; i < kd; ++i) r[i] = x[((size_t)i << logn) + k];
+    const double m = crt_centered(r, kd, cc) * is;
+    __shared__ double red[kBlock / 64][64];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const u32 mask = 2u * n - 1;
+    const double inv_n = 1.0 / n;
+    for (int i = 0; i < 32; ++i) {
+        double sn, cs;
+        sincospi((double)((sl.e[i] * (u32)k) & mask) * inv_n, &sn, &cs);
+        double vr = m * cs, vi = m * sn;
+        for (int o = 32; o > 0; o >>= 1) vr += __shfl_down(vr, o, 64), vi += __shfl_down(vi, o, 64);
+        if (lane == 0) red[wv][2 * i] = vr, red[wv][2 * i + 1] = vi;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        double t = 0.0;
+        for (int w = 0; w < kBlock / 64; ++w) t += red[w][threadIdx.x];
+        atomicAdd(acc + threadIdx.x, t);
+    }
+}
+// ONE 32-periodic message from its 32 snapped slot deviations w (w_j = zeta^nib - 1): only the
+// coefficients k == 0 mod N/64 are nonzero, m_k = (1/32) sum_j Re(w_j zeta^(-e_j k)) (+1 at k = 0)
+__global__ void __launch_bounds__(kBlock) k_encode32(u32* out, const double* w, Slot32 sl, double scale, int nq, const PrimeConst* pc,
+                                                     int logn) {
+    const int n = 1 << logn;
+    const int k = blockIdx.x * kBlock + threadIdx.x;
+    const u32 mask = 2u * n - 1, kmask = (u32)(n / 64) - 1;
+    const double inv_n = 1.0 / n;
+    double v = 0.0;
+    if (((u32)k & kmask) == 0)
+        for (int i = 0; i < 32; ++i) {
+            double sn, cs;
+            sincospi((double)((sl.e[i] * (u32)k) & mask) * inv_n, &sn, &cs);
+            v += w[2 * i] * cs + w[2 * i + 1] * sn;
+        }
+    v = v / 32.0 + (k == 0 ? 1.0 : 0.0);
+    const double x = rint(v * scale);
+    for (int t = 0; t < nq; ++t) {
+        const double q = (double)pc[t].q;
+        double r = fma(-q, floor(x / q), x);
+        if (r < 0) r += q;
+        if (r >= q) r -= q;
+        out[((size_t)t << logn) + k] = (u32)r;
+    }
+}
+
 __global__ void k_snap16(const double* acc, double* w, int* nib) {
     const int t = threadIdx.x;  // 32 = 2 ciphertexts x 16 slots
     if (t >= 32) return;
@@ -825,27 +890,34 @@ __global__ void __launch_bounds__(kBlock) k_lut_bivariate(u32* out, LutOperands 
     const u32 q = P.q;
     const size_t off = ((size_t)t << logn) + k;
     out += (size_t)mb * 3 * ((size_t)nl << logn);
-    u32 acc0 = 0, acc1 = 0, acc2 = 0;
+    // 64-bit multiply-adds (operands < q < 2^30: 8 products fit beside a folded sum), one
+    // reduction per inner sum and per output -- the same residues as a reduction per term
+    u64 acc0 = 0, acc1 = 0, acc2 = 0;
+    int pc_ = 0;
     for (int p = 0; p < n_a; ++p) {
         const int t0 = op.p_start[p], t1 = op.p_start[p + 1];
         if (t0 == t1) continue;
-        u32 u0 = 0, u1 = 0;
+        u64 s0 = 0, s1 = 0;
         for (int j = t0; j < t1; ++j) {
+            if (j > t0 && ((j - t0) & 7) == 0) s0 = fold64(s0, q, P.r32), s1 = fold64(s1, q, P.r32);
             const int qq = op.q_of[j];
             const u32* bq = op.b[qq] + (size_t)mb * 2 * ((size_t)op.nb[qq] << logn);
-            const u32* c = cst + ((size_t)j * nl + t) * 4 + 2 * half;
-            u0 = add_mod(u0, shoup_mul(bq[off], c[0], c[1], q), q);
-            u1 = add_mod(u1, shoup_mul(bq[((size_t)op.nb[qq] << logn) + off], c[0], c[1], q), q);
+            const u32 c = cst[((size_t)j * nl + t) * 4 + 2 * half];
+            s0 += (u64)bq[off] * c;
+            s1 += (u64)bq[((size_t)op.nb[qq] << logn) + off] * c;
         }
+        const u32 u0 = reduce64(s0, q, P.mu, P.r32), u1 = reduce64(s1, q, P.mu, P.r32);
         const u32* ap = op.a[p] + (size_t)mb * 2 * ((size_t)op.na[p] << logn);
         const u32 a0 = ap[off], a1 = ap[((size_t)op.na[p] << logn) + off];
-        acc0 = add_mod(acc0, barrett_mul(a0, u0, q, P.mu), q);
-        acc1 = add_mod(acc1, add_mod(barrett_mul(a0, u1, q, P.mu), barrett_mul(a1, u0, q, P.mu), q), q);
-        acc2 = add_mod(acc2, barrett_mul(a1, u1, q, P.mu), q);
+        if (pc_ == 4) acc0 = fold64(acc0, q, P.r32), acc1 = fold64(acc1, q, P.r32), acc2 = fold64(acc2, q, P.r32), pc_ = 0;
+        acc0 += (u64)a0 * u0;
+        acc1 += (u64)a0 * u1 + (u64)a1 * u0;  // two products per step: fold every 4 steps
+        acc2 += (u64)a1 * u1;
+        ++pc_;
     }
-    out[off] = acc0;
-    out[((size_t)nl << logn) + off] = acc1;
-    out[((size_t)(2 * nl) << logn) + off] = acc2;
+    out[off] = reduce64(acc0, q, P.mu, P.r32);
+    out[((size_t)nl << logn) + off] = reduce64(acc1, q, P.mu, P.r32);
+    out[((size_t)(2 * nl) << logn) + off] = reduce64(acc2, q, P.mu, P.r32);
 }
 
 // grid z = member of stacked elements (element j of member m at x[j] + m npoly nx[j] N, out / acc
@@ -855,18 +927,20 @@ __global__ void __launch_bounds__(kBlock) k_lut_univariate(u32* out, const u32* 
     const int t = blockIdx.y, mb = blockIdx.z;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const int half = (int)(k >> (logn - 1));
-    const u32 q = pc[t].q;
+    const PrimeConst P = pc[t];
+    const u32 q = P.q;
     const size_t off = ((size_t)t << logn) + k;
     const size_t mo = (size_t)mb * npoly * ((size_t)nl << logn);
     for (int p = 0; p < npoly; ++p) {
         const size_t o = mo + ((size_t)(p * nl) << logn) + off;
-        u32 v = acc ? acc[o] : 0;
+        u64 v = acc ? acc[o] : 0;  // 64-bit multiply-adds, folded every 8 terms, one reduction
         for (int j = 0; j < n; ++j) {
-            const u32* c = cst + ((size_t)j * nl + t) * 4 + 2 * half;
+            if (j && (j & 7) == 0) v = fold64(v, q, P.r32);
+            const u32 c = cst[((size_t)j * nl + t) * 4 + 2 * half];
             const u32* xj = ch.x[j] + (size_t)mb * npoly * ((size_t)ch.nx[j] << logn);
-            v = add_mod(v, shoup_mul(xj[((size_t)(p * ch.nx[j]) << logn) + off], c[0], c[1], q), q);
+            v += (u64)xj[((size_t)(p * ch.nx[j]) << logn) + off] * c;
         }
-        out[o] = v;
+        out[o] = reduce64(v, q, P.mu, P.r32);
     }
 }
 
@@ -940,6 +1014,12 @@ void launch_addsub_tail(hipStream_t st, const DevTables& T, u32* out, const u32*
 }
 void launch_add_const_half(hipStream_t st, const DevTables& T, u32* out, const u32* in, const LimbConsts& cst, int rows, int nl, LimbMap map) {
     prof_launch(KID_ELEMENTWISE, EW_BYTES(2.0 * rows), k_add_const_half, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, cst, nl, map, T.pc, T.logn);
+}
+void launch_lincomb(hipStream_t st, const DevTables& T, u32* out, const u32* a, const LimbConsts& ka, const u32* b, int bsign,
+                    const LimbConsts* cadd, int per, int rows, int nl, LimbMap map) {
+    static const LimbConsts kNone{};
+    prof_launch(KID_ELEMENTWISE, EW_BYTES((b ? 3.0 : 2.0) * rows), k_lincomb, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, a, ka, b, bsign,
+                cadd ? *cadd : kNone, cadd ? 1 : 0, per, nl, map, T.pc, T.logn);
 }
 void launch_automorph(hipStream_t st, const DevTables& T, u32* out, const u32* in, u64 g, int rows) {
     prof_launch(KID_AUTOMORPH, words(2.0 * rows * (1u << T.logn)), k_automorph, ew_grid(T.logn, rows), dim3(kBlock), 0, st, out, in, g, T.logn);
@@ -1263,6 +1343,14 @@ void launch_decode16(hipStream_t st, const DevTables& T, const u32* x, const int
                      const double inv_scale[2], double* acc) {
     prof_launch(KID_ELEMENTWISE, words((double)(kd[0] + kd[1]) * (1u << T.logn)), k_decode16, dim3((1u << T.logn) / kBlock, 2),
                 dim3(kBlock), 0, st, x, kd[0], kd[1], cc[0], cc[1], sl, inv_scale[0], inv_scale[1], acc, T.logn);
+}
+void launch_decode32(hipStream_t st, const DevTables& T, const u32* x, int kd, const CrtConsts& cc, const Slot32& sl, double inv_scale, double* acc) {
+    prof_launch(KID_ELEMENTWISE, words((double)kd * (1u << T.logn)), k_decode32, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, x, kd, cc, sl,
+                inv_scale, acc, T.logn);
+}
+void launch_encode32(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot32& sl, double scale, int nq) {
+    prof_launch(KID_ELEMENTWISE, words((double)nq * (1u << T.logn)), k_encode32, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, w, sl,
+                scale, nq, T.pc, T.logn);
 }
 void launch_snap16(hipStream_t st, const double* acc, double* w, int* nib) {
     prof_launch(KID_ELEMENTWISE, 0.0, k_snap16, dim3(1), dim3(64), 0, st, acc, w, nib);

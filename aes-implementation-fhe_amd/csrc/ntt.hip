@@ -24,6 +24,7 @@
 // Rows of one launch are addressed through a RowMap (out-of-place, strided groups), so
 // callers never copy limbs around just to transform them.
 #include <cstdlib>
+#include <stdexcept>
 
 #include "kernels.h"
 #include "launch.h"
@@ -250,7 +251,9 @@ __global__ void __launch_bounds__(NT) k_ntt2_fwd(u32* data, RowMap rm, LimbMap m
         const u32* addp = (grp & 1) ? aux.add1 : aux.add0;
         if (grp > 1) addp = (addp && aux.add_mstride) ? addp + (grp >> 1) * aux.add_mstride : nullptr;
         const uint4* ad = addp ? reinterpret_cast<const uint4*>(addp + ((size_t)li << LOGN) + woff) : nullptr;
-        uint4* o = reinterpret_cast<uint4*>(aux.out + ((size_t)(grp * aux.out_stride + li) << LOGN) + woff);
+        u32* const om = aux.outm[(grp >> 1) & 7];
+        uint4* o = reinterpret_cast<uint4*>((om ? om + ((size_t)((grp & 1) * aux.out_stride + li) << LOGN)
+                                               : aux.out + ((size_t)(grp * aux.out_stride + li) << LOGN)) + woff);
         const u32 qi = aux.qinv[2 * li], qip = aux.qinv[2 * li + 1];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
@@ -494,10 +497,14 @@ void launch_rescale2_ntt(hipStream_t st, const DevTables& T, u32* out, const u32
     ntt_fwd_dispatch<kSpread2, kFinish>(st, T, v, last, npoly * nt, npoly * nt, rm, LimbMap{1 << 30, 0, 0}, aux);
 }
 void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, const u32* cur, int cur_stride, const u32* qinv,
-                       const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride) {
+                       const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride, u32* const* outm) {
     NttAux aux{};
     aux.cur = cur, aux.out = out, aux.qinv = qinv, aux.cur_stride = cur_stride, aux.out_stride = nt, aux.add0 = add0, aux.add1 = add1;
     aux.add_mstride = add_mstride;
+    if (outm) {
+        if (npoly > 16 || npoly % 2) throw std::runtime_error("launch_ntt_finish: per-member outputs for at most 8 two-polynomial members");
+        for (int m = 0; m < npoly / 2; ++m) aux.outm[m] = outm[m];
+    }
     ntt_fwd_dispatch<kPlain, kFinish>(st, T, conv, conv, npoly * nt, npoly * nt, rows_dense(nt), LimbMap{1 << 30, 0, 0}, aux);
 }
 void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {

@@ -246,9 +246,10 @@ class EngineContext:
         """renorm_pair for the periodic state layout (state_encoder.SlotLayout)"""
         return self.engine.renorm_periodic(hi, lo, period, level)
 
-    def renorm_single(self, ct, level=None):
-        """renorm of one packed-state ciphertext, every slot snapped"""
-        return self.engine.renorm_single(ct, level)
+    def renorm_single(self, ct, level=None, period=None):
+        """renorm of one packed-state ciphertext, every slot snapped; period: the
+        packed period when known (2 x the state period)"""
+        return self.engine.renorm_single(ct, level, period)
 
     def renorm_unpack(self, packed, period: int, level=None):
         """renorm of a packed hi | lo state (2 period-periodic) into its (hi, lo) pair"""

@@ -47,6 +47,7 @@ EXPORTED = [
     "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled", "aesfhe_set_enc_nonce", "aesfhe_launch_count",
     "aesfhe_galois_multi", "aesfhe_debug_boot_stage_sparse", "aesfhe_debug_sparse_group", "aesfhe_debug_sparse_group_plain",
     "aesfhe_debug_mono_pack", "aesfhe_debug_mono_split", "aesfhe_alg_bytes", "aesfhe_stack", "aesfhe_unstack", "aesfhe_members",
+    "aesfhe_renorm_packed",
 ]
 
 # largest log2(PQ) for 128-bit classical security with a ternary secret (HE standard)
@@ -145,6 +146,7 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_stack"] = [vp, c_int, _Hp, _Hp]
     sig["aesfhe_unstack"] = [vp, _H, c_int, _Hp]
     sig["aesfhe_members"] = [vp, _H, ctypes.POINTER(c_int)]
+    sig["aesfhe_renorm_packed"] = [vp, _H, c_int, c_int, _Hp]
     for name in EXPORTED:
         fn = getattr(L, name)
         fn.restype = (ctypes.c_char_p if name == "aesfhe_last_error" else ctypes.c_uint64 if name == "aesfhe_launch_count"
@@ -684,8 +686,11 @@ class Engine:
                                                          -1 if level is None else int(level), ctypes.byref(a), ctypes.byref(b)))
         return Ciphertext(self._ctx, a.value), Ciphertext(self._ctx, b.value)
 
-    def renorm_single(self, ct, level=None):
-        """secret-key renorm of one ciphertext, every slot snapped (aesfhe_renorm_single)"""
+    def renorm_single(self, ct, level=None, period=None):
+        """secret-key renorm of one ciphertext, every slot snapped (aesfhe_renorm_single); period:
+        the message's slot period when known (aesfhe_renorm_packed: period 32 skips the FFT codec)"""
+        if period:
+            return self._new(self._lib.aesfhe_renorm_packed, ct.handle, int(period), -1 if level is None else int(level))
         return self._new(self._lib.aesfhe_renorm_single, ct.handle, -1 if level is None else int(level))
 
     def renorm_unpack(self, packed, period: int, level=None):

@@ -161,7 +161,7 @@ class StateEncoder:
         if self.pairs > 1:
             his, los = zip(*[self._encode1(s) for s in self._pair_states(state)])
             return tag_layout(self.layout, self.ctx.stack(his), self.ctx.stack(los))
-        return self._encode1(state)
+        return self._encode1(self._pair_states(state)[0])
 
     def _encode1(self, state):
         st = self._as_batch(state)
@@ -201,7 +201,7 @@ class StateEncoder:
         if self.pairs > 1:
             cts = [self.ctx.encrypt(self._packed_slots(self._as_batch(s))) for s in self._pair_states(state)]
             return tag_layout(self.layout, self.ctx.stack(cts))[0]
-        return tag_layout(self.layout, self.ctx.encrypt(self._packed_slots(self._as_batch(state))))[0]
+        return tag_layout(self.layout, self.ctx.encrypt(self._packed_slots(self._as_batch(self._pair_states(state)[0]))))[0]
 
     def decode_packed(self, ct) -> np.ndarray:
         check_layout(self.layout, ct)
@@ -218,7 +218,10 @@ class StateEncoder:
 
     def renorm_packed(self, ct, level=None):
         """renorm of a packed state, packed again"""
-        return self.ctx.renorm_single(ct, None if _RENORM_FRESH else level)
+        try:
+            return self.ctx.renorm_single(ct, None if _RENORM_FRESH else level, period=2 * self.layout.period)
+        except TypeError:  # a context whose renorm_single takes no period
+            return self.ctx.renorm_single(ct, None if _RENORM_FRESH else level)
 
     def renorm_unpack(self, ct, level=None) -> Tuple[Any, Any]:
         """renorm of a packed state into the (hi, lo) pair"""

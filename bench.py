@@ -77,7 +77,7 @@ def parse():
                          "per rank as stacked ciphertexts (DESIGN.md 3.16); 0 = skip")
     ap.add_argument("--pair-stack", type=int, default=64,
                     help="pairs per stack: --pair-states pairs run as ceil(pair-states / pair-stack) stacks in turn")
-    ap.add_argument("--packed-pairs", type=int, default=2,
+    ap.add_argument("--packed-pairs", type=int, default=4,
                     help="multi-pair slot-packed batch: this many stacked ciphertext pairs of 2048 states each per rank; 0 = skip")
     ap.add_argument("--pair-steps", type=int, default=3, help="timed steps of the multi-pair legs")
     ap.add_argument("--true-fhe-steps", type=int, default=1,

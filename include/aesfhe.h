@@ -217,6 +217,10 @@ int aesfhe_renorm_periodic(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, 
  * of the pipeline's packed XOR stage): every slot snapped and re-encrypted at
  * `level` (< 0 = fresh).  Replaces the renorm of REF/pipeline.py:65-69 for that form. */
 int aesfhe_renorm_single(aesfhe_ctx* ctx, aesfhe_handle ct, int level, aesfhe_handle* out);
+/* aesfhe_renorm_single of a ciphertext known to be `period`-periodic (the packed form: period =
+ * 2 x the state period): period 32 decodes / re-encodes its 32 slots directly (no FFT); other
+ * periods as aesfhe_renorm_single. */
+int aesfhe_renorm_packed(aesfhe_ctx* ctx, aesfhe_handle ct, int period, int level, aesfhe_handle* out);
 /* Secret-key renorm that unpacks: `packed` holds the hi nibbles of an n-periodic state pair in
  * slots (j mod 2n) < n and the lo nibbles in the others (period = n, a power of two, 2n <=
  * slots); out_hi / out_lo are the snapped n-periodic hi / lo states at `level` -- the

@@ -49,6 +49,28 @@ def test_pack_renorm_roundtrip(ctx, states):
         ctx.engine.renorm_unpack(p, 24)
 
 
+def test_direct32_packed_renorm_equals_fft_codec(ctx):
+    """the packed renorms at period 32 decode / re-encode their 32 slots directly (decode32 /
+    encode32, aesfhe_renorm_packed); the FFT codec (aesfhe_renorm_single) gives the same fresh
+    codewords in every slot, and the unpacked halves are the packed halves"""
+    from state_encoder import StateEncoder
+    E = ctx.engine
+    enc = StateEncoder(ctx, 1, periodic=True)
+    rng = np.random.default_rng(32)
+    st = rng.integers(0, 256, 16).astype(np.uint8)
+    p = E.multiply(enc.pack(*enc.encode(st)), 256.0)  # off-scale, as an XOR4 output
+    direct = E.renorm_single(p, None, period=32)
+    fft = E.renorm_single(p)
+    zd, zf = ctx.decrypt(direct), ctx.decrypt(fft)
+    assert np.abs(zd - zf).max() < 4e-4  # two fresh encryptions of the same codewords
+    assert np.abs(np.abs(zd) - 1.0).max() < 2e-4
+    assert np.array_equal(enc.decode_packed(direct), st)
+    hi, lo = E.renorm_unpack(p, 16)
+    zh, zl = ctx.decrypt(hi), ctx.decrypt(lo)
+    assert np.abs(zh - np.tile(zd[:16], len(zd) // 16)).max() < 4e-4
+    assert np.abs(zl - np.tile(zd[16:32], len(zd) // 16)).max() < 4e-4
+
+
 def test_xor4_on_packed_states(ctx, co):
     from state_encoder import StateEncoder
     from utils import NEED_XOR, RENORM_FLOOR
