@@ -2589,22 +2589,17 @@ public:
         const u32* c1 = x.data + (size_t)nl * n;
         u32* ext = modup(c1, l, nb, qs);
         u32* acc = tmp(2 * (size_t)ne * nb);
-        u32* perm = tmp(3 * (size_t)nl * nb);
-        for (int j = 1; j <= 3; ++j) {
-            const u64 g = rot_galois(-j * a);
-            key_inner(acc, ext, c1, ksk(g), l, g, nb, qs, KsFold{}, j > 1);
-            for (int m = 0; m < nb; ++m)
-                launch_automorph(S(), T_, perm + ((size_t)(j - 1) * nb + m) * nl * n, x.data + (size_t)m * qs, g, nl);
-        }
+        // the three rotations' key inner products summed in one launch, c0 + its three
+        // automorphisms in another (bit for bit the separate launches' sums)
+        KsSumArgs ka;
+        ka.J = 3;
+        for (int j = 1; j <= 3; ++j) ka.g[j - 1] = rot_galois(-j * a), ka.key[j - 1] = ksk(ka.g[j - 1]);
+        const int nd = (nl + hp_.alpha - 1) / hp_.alpha;
+        launch_key_inner_sum(S(), T_, acc, ext, c1, ka, nb, nd, ne, nl, hp_.alpha, hp_.n_ks + hp_.n_p, hp_.n_ks, extmap(nl),
+                             (size_t)ext_rows(l) * n, qs, (size_t)2 * ne * n);
         untmp(ext, (size_t)nb * ext_rows(l));
         u32* c0s = tmp(2 * (size_t)nl * nb);  // member stride qs, first nl rows used (moddown's add0)
-        for (int m = 0; m < nb; ++m) {
-            MemberPtrs mp;
-            mp.src[0] = x.data + (size_t)m * qs;
-            for (int j = 1; j <= 3; ++j) mp.src[j] = perm + ((size_t)(j - 1) * nb + m) * nl * n;
-            launch_add_members(S(), T_, c0s + (size_t)m * qs, mp, 4, nl, qmap(), false);
-        }
-        untmp(perm, 3 * (size_t)nl * nb);
+        launch_automorph_sum(S(), T_, c0s, x.data, ka, nb, nl, qs, qmap());
         Ct o = moddown(acc, l, c0s, c1, nb, qs);
         o.ntt = x.ntt;
         untmp(acc, 2 * (size_t)ne * nb);

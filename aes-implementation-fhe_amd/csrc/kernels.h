@@ -232,6 +232,19 @@ struct KsMultiArgs {
 void launch_key_inner_multi(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const KsMultiArgs& ka, int nm,
                             int nsrc, int nd, int ne, int nl, int alpha, int nkey, int nks, LimbMap map, size_t ext_ms, size_t d_ms,
                             size_t acc_ms);
+// acc_m [2][ne] (acc + m acc_ms) = sum_{i < J} sum_j e_j(g_i) ⊙ key_i[j]: J hoisted rotations of the
+// same ModUp'ed ciphertext summed in Q*P in ONE launch (the bootstrap's radix-4 trace step, J = 3),
+// e_j(g) = ext_m[j] / d_m on digit j's own limbs, read through X -> X^g; nb stacked members (grid z)
+struct KsSumArgs {
+    const u32* key[4] = {};
+    u64 g[4] = {};
+    int J = 0;
+};
+void launch_key_inner_sum(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const KsSumArgs& ka, int nb, int nd,
+                          int ne, int nl, int alpha, int nkey, int nks, LimbMap map, size_t ext_ms, size_t d_ms, size_t acc_ms);
+// out_m (rows rows, out + m ms) = in_m + sum_{i < J} in_m through X -> X^g_i (in + m ms), nb members
+void launch_automorph_sum(hipStream_t st, const DevTables& T, u32* out, const u32* in, const KsSumArgs& ka, int nb, int rows, size_t ms,
+                          LimbMap map);
 // out + m out_ms (rows rows) = in_m through X -> X^g_m, m < n (one launch; g_m = 1: a copy)
 struct AutoMulti {
     const u32* src[kKsMulti] = {};

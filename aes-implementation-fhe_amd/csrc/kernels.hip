@@ -385,6 +385,61 @@ __global__ void __launch_bounds__(kBlock) k_key_inner(u32* acc, const u32* ext, 
     ts_end(ts);
 }
 
+// J hoisted rotations summed in one pass (KsSumArgs): the trace step's three key inner products,
+// grid z = stacked member; 64-bit multiply-adds folded every 8 products
+__global__ void __launch_bounds__(kBlock) k_key_inner_sum(u32* acc, const u32* ext, const u32* d, KsSumArgs ka, int nd, int ne, int nl,
+                                                          int alpha, int nkey, int nks, LimbMap map, const PrimeConst* pc, int logn,
+                                                          size_t ext_ms, size_t d_ms, size_t acc_ms, unsigned long long* ts) {
+    ts_begin(ts);
+    const int x = blockIdx.y, m = blockIdx.z;
+    const size_t k = ((size_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+    const PrimeConst P = pc[map.prime(x)];
+    const int krow = x < nl ? x : nks + (x - nl);
+    const int own = x < nl ? x / alpha : -1;
+    u64 s0[4] = {}, s1[4] = {};
+    int cnt = 0;
+    for (int i = 0; i < ka.J; ++i) {
+        u32 ks[4];
+#pragma unroll
+        for (int v = 0; v < 4; ++v) ks[v] = galois_src((u32)(k + v), ka.g[i], logn);
+        const u32* key = ka.key[i];
+        for (int j = 0; j < nd; ++j, ++cnt) {
+            if (cnt && (cnt & 7) == 0) {
+#pragma unroll
+                for (int v = 0; v < 4; ++v) s0[v] = fold64(s0[v], P.q, P.r32), s1[v] = fold64(s1[v], P.q, P.r32);
+            }
+            const size_t kr = (((size_t)j * 2 * nkey + krow) << logn) + k;
+            const uint4 vb = *reinterpret_cast<const uint4*>(key + kr);
+            const uint4 va = *reinterpret_cast<const uint4*>(key + kr + ((size_t)nkey << logn));
+            const u32 kb4[4] = {vb.x, vb.y, vb.z, vb.w}, ka4[4] = {va.x, va.y, va.z, va.w};
+            const u32* src = j == own ? d + m * d_ms + ((size_t)x << logn) : ext + m * ext_ms + (((size_t)j * ne + x) << logn);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                const u32 e = src[ks[v]];
+                s0[v] += (u64)e * kb4[v];
+                s1[v] += (u64)e * ka4[v];
+            }
+        }
+    }
+    uint4* a0 = reinterpret_cast<uint4*>(acc + m * acc_ms + ((size_t)x << logn) + k);
+    uint4* a1 = reinterpret_cast<uint4*>(acc + m * acc_ms + (((size_t)ne + x) << logn) + k);
+    *a0 = make_uint4(reduce64(s0[0], P.q, P.mu, P.r32), reduce64(s0[1], P.q, P.mu, P.r32), reduce64(s0[2], P.q, P.mu, P.r32),
+                     reduce64(s0[3], P.q, P.mu, P.r32));
+    *a1 = make_uint4(reduce64(s1[0], P.q, P.mu, P.r32), reduce64(s1[1], P.q, P.mu, P.r32), reduce64(s1[2], P.q, P.mu, P.r32),
+                     reduce64(s1[3], P.q, P.mu, P.r32));
+    ts_end(ts);
+}
+// c0 + its J automorphisms (the trace step's ModDown addend), one launch for nb members
+__global__ void k_automorph_sum(u32* out, const u32* in, KsSumArgs ka, int nl, size_t ms, LimbMap map, const PrimeConst* pc, int logn) {
+    const int row = blockIdx.y, m = blockIdx.z;
+    const u32 i = blockIdx.x * kBlock + threadIdx.x;
+    const PrimeConst P = pc[map.prime(row % nl)];
+    const u32* src = in + m * ms + ((size_t)row << logn);
+    u32 v = src[i];
+    for (int j = 0; j < ka.J; ++j) v = add_mod(v, src[galois_src(i, ka.g[j], logn)], P.q);
+    out[m * ms + ((size_t)row << logn) + i] = v;
+}
+
 // heterogeneous members (KsMultiArgs): grid z = member, each member its own key, Galois element
 // and ModUp source; otherwise the arithmetic of k_key_inner<1> (four coefficients per thread,
 // 64-bit multiply-adds folded every 8 digits)
@@ -1288,6 +1343,21 @@ void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* e
     else
         prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<8>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g,
                        map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum);
+}
+void launch_key_inner_sum(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const KsSumArgs& ka, int nb, int nd,
+                          int ne, int nl, int alpha, int nkey, int nks, LimbMap map, size_t ext_ms, size_t d_ms, size_t acc_ms) {
+    if (ka.J < 1 || ka.J > 4 || nb < 1) throw std::runtime_error("launch_key_inner_sum: 1..4 rotations");
+    for (int i = 0; i < ka.J; ++i)
+        if (!ka.key[i] || !ka.g[i]) throw std::runtime_error("launch_key_inner_sum: missing key or Galois element");
+    // ext / d read once per member (the J gathers of a row hit L2), the J keys once, acc written
+    const double bytes = words(((nb * (nd + 2.0) + 2.0 * nd * ka.J) * ne) * (1u << T.logn));
+    prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner_sum, dim3((1u << T.logn) / (4 * kBlock), ne, nb), dim3(kBlock), 0, st, acc, ext, d, ka, nd,
+                   ne, nl, alpha, nkey, nks, map, T.pc, T.logn, ext_ms, d_ms, acc_ms);
+}
+void launch_automorph_sum(hipStream_t st, const DevTables& T, u32* out, const u32* in, const KsSumArgs& ka, int nb, int rows, size_t ms,
+                          LimbMap map) {
+    prof_launch(KID_AUTOMORPH, words(2.0 * rows * nb * (1u << T.logn)), k_automorph_sum, dim3((1u << T.logn) / kBlock, rows, nb), dim3(kBlock),
+                0, st, out, in, ka, rows, ms, map, T.pc, T.logn);
 }
 void launch_key_inner_multi(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const KsMultiArgs& ka, int nm,
                             int nsrc, int nd, int ne, int nl, int alpha, int nkey, int nks, LimbMap map, size_t ext_ms, size_t d_ms,
