@@ -385,14 +385,42 @@ __global__ void __launch_bounds__(kBlock) k_key_inner(u32* acc, const u32* ext, 
     ts_end(ts);
 }
 
+// XCD-aware block -> (column block, row) map of a (nbx x rows) grid: workgroups are dealt
+// round-robin over the 8 XCDs (linear id b and b + 8 share one, MI355X_MICROARCH.md "Workgroup
+// dispatch"), so with the plain map the nbx blocks of one row land on all 8 XCDs and EVERY XCD
+// fetches the whole gathered source row into its own L2.  Here the blocks of one row sit on one
+// XCD: rows are taken in bands of 8, row 8 band + (b mod 8) <- blocks b with b / 8 in the band's
+// range.  A last partial band of r < 8 rows: each XCD's r nbx / 8 tail blocks in turn, XCD by
+// XCD, fill the rows one after the other -- a row spans at most ceil(8 / r) + 1 XCDs instead of 8.
+// A bijection either way (speed only; needs 8 | nbx).
+__device__ __forceinline__ void xcd_rows(int lognbx, int rows, int& bx, int& row) {
+    const int nbx = 1 << lognbx;
+    const int id = blockIdx.x + (blockIdx.y << lognbx);
+    const int full = rows & ~7;
+    if (id < (full << lognbx)) {
+        const int m = id >> 3;
+        bx = m & (nbx - 1);
+        row = ((m >> lognbx) << 3) + (id & 7);
+    } else {
+        const int t = id - (full << lognbx), per = ((rows - full) << lognbx) >> 3;  // tail blocks per XCD
+        const int pos = (t & 7) * per + (t >> 3);
+        bx = pos & (nbx - 1);
+        row = full + (pos >> lognbx);
+    }
+}
+
 // J hoisted rotations summed in one pass (KsSumArgs): the trace step's three key inner products,
 // grid z = stacked member; 64-bit multiply-adds folded every 8 products
 __global__ void __launch_bounds__(kBlock) k_key_inner_sum(u32* acc, const u32* ext, const u32* d, KsSumArgs ka, int nd, int ne, int nl,
                                                           int alpha, int nkey, int nks, LimbMap map, const PrimeConst* pc, int logn,
                                                           size_t ext_ms, size_t d_ms, size_t acc_ms, unsigned long long* ts) {
     ts_begin(ts);
-    const int x = blockIdx.y, m = blockIdx.z;
-    const size_t k = ((size_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+    // the J gathers of a row's ext through different automorphisms: all blocks of one row on one
+    // XCD (xcd_rows), so each XCD fetches a gathered row into its L2 once
+    int x = blockIdx.y, bx = blockIdx.x;
+    xcd_rows(logn - 10, ne, bx, x);
+    const int m = blockIdx.z;
+    const size_t k = ((size_t)bx * kBlock + threadIdx.x) * 4;
     const PrimeConst P = pc[map.prime(x)];
     const int krow = x < nl ? x : nks + (x - nl);
     const int own = x < nl ? x / alpha : -1;
@@ -1223,27 +1251,6 @@ __device__ __forceinline__ void lin_mac_body(const LinMacArgs& m, int nl, int ne
         }
     }
 }
-// XCD-aware block -> (column block, row) map of a (nbx x rows) grid: workgroups are dealt
-// round-robin over the 8 XCDs (linear id b and b + 8 share one, MI355X_MICROARCH.md "Workgroup
-// dispatch"), so with the plain map the nbx blocks of one row land on all 8 XCDs and EVERY XCD
-// fetches the whole gathered source row into its own L2.  Here the blocks of one row sit on one
-// XCD: rows are taken in bands of 8, row 8 band + (b mod 8) <- blocks b with b / 8 in the band's
-// range; a last partial band keeps the plain map.  A bijection either way (speed only).
-__device__ __forceinline__ void xcd_rows(int lognbx, int rows, int& bx, int& row) {
-    const int nbx = 1 << lognbx;
-    const int id = blockIdx.x + (blockIdx.y << lognbx);
-    const int full = rows & ~7;
-    if (id < (full << lognbx)) {
-        const int m = id >> 3;
-        bx = m & (nbx - 1);
-        row = ((m >> lognbx) << 3) + (id & 7);
-    } else {
-        const int r = id - (full << lognbx);
-        bx = r & (nbx - 1);
-        row = full + (r >> lognbx);
-    }
-}
-
 template <int NB, int ND>
 __global__ void __launch_bounds__(kBlock) k_lin_mac(LinMacArgs m, int nl, int ne, LimbMap map, const PrimeConst* pc, int logn, int xcd) {
     int t = blockIdx.y, bx = blockIdx.x;
