@@ -10,8 +10,9 @@ B="--no-cpu-baseline --batch-states 0 --true-fhe-steps 0 --pair-states 0 --packe
 timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
 echo tests done
 # 2. kernel trace + stats of the C2 headline leg, and its bench line (live kernel averages)
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 12 --warmup 1 $B > $O/bench_under_rocprof.json
+AESFHE_MARK_TIMED=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --steps 12 --warmup 1 $B > $O/bench_under_rocprof.json
 cp $O/prof/run_kernel_stats.csv $O/kernel_stats.csv
+timeout -k 10 120 python3 tools/trace_window.py $O/kernel_stats_timed.json $O/prof
 rm -f $O/prof/run_kernel_trace.csv
 # 3. the same workload without the profiler
 timeout -k 10 300 python3 bench.py --steps 12 --warmup 1 $B > $O/bench_same_workload.json
