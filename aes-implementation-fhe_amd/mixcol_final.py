@@ -19,6 +19,9 @@ from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT, SplitLUT2, batched, eval_two, joint_bases, powers, std_basis
 from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, can_fork, drop_to, fused_lut, pair, rot_many, rot_pair
 
+# AESFHE_SHARE_R1=0: MixColumns' r1 basis rebuilt in its second XOR4 (A/B runs)
+_SHARE_R1 = os.environ.get("AESFHE_SHARE_R1", "1") != "0"
+
 
 class _CoeffCache:
     """gf_mult{k}_{hi|lo} plaintext coefficients, encoded once per engine (REF :19-37)."""
@@ -161,7 +164,12 @@ class MixColFinal:
     def _renorm_pair(self, hi, lo, level=None):
         return self.enc.renorm(hi, lo, level)
 
-    def _xor_ct(self, a, b, out_level=None):
+    def _xor_ct(self, a, b, out_level=None, keep_b=None):
+        if keep_b is not None:
+            try:
+                return self.xor4.apply(a, b, out_level, keep_b=keep_b)
+            except TypeError:  # an XOR4 without basis sharing
+                pass
         return self.xor4.apply(a, b, out_level)
 
     def _xor_pair(self, a, b, out_level=None):
@@ -206,10 +214,14 @@ class MixColFinal:
             # multiplier pair and four single XOR4s instead of two pairs and three XOR4s
             p1, p0 = pair(ctx, lambda: enc.pack(rh[0], rl[0]), lambda: enc.pack(ct_hi, ct_lo), shared=(ct_hi, ct_lo, *rh, *rl))
             r2, r3 = pair(ctx, lambda: enc.pack(rh[1], rl[1]), lambda: enc.pack(rh[2], rl[2]))
-            u, v = pair(ctx, lambda: enc.renorm_unpack(self._xor_ct(p0, p1, fl), level=gl + LUT2_DEPTH),
+            # r1 (p1) enters two XOR4s: as the second operand of both (XOR is symmetric), its
+            # level drop and std basis (conjugate + power chain) are built once (keep_b)
+            kb = {} if _SHARE_R1 else None
+            u, v = pair(ctx, lambda: enc.renorm_unpack(self._xor_ct(p0, p1, fl, kb), level=gl + LUT2_DEPTH),
                         lambda: enc.renorm_packed(self._xor_ct(r2, r3, fl), level=NEED_XOR), shared=(p1,))
             two, w = pair(ctx, lambda: enc.pack(*self.gf_mult_2(*u, out_level=gl)),
-                          lambda: enc.renorm_packed(self._xor_ct(p1, v, fl), level=NEED_XOR))
+                          lambda: enc.renorm_packed(self._xor_ct(v, p1, fl, kb) if kb is not None else self._xor_ct(p1, v, fl),
+                                                    level=NEED_XOR))
             acc = enc.renorm_packed(self._xor_ct(two, w, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
             if do_final_bootstrap:
                 acc = bootstrap1(ctx, acc, 2 * self.layout.period)

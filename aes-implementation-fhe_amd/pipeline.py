@@ -58,6 +58,10 @@ from utils import (pair, NEED_GF, NEED_ISR_ISB, NEED_SR_ARK, NEED_SR_MIX, NEED_S
 from xor4_lut import XOR4LUT
 
 
+# AESFHE_KEY_BASIS=0: the packed round keys' XOR4 bases rebuilt in every AddRoundKey (A/B runs)
+_KEY_BASIS = os.environ.get("AESFHE_KEY_BASIS", "1") != "0"
+
+
 class AESPipeline:
     def __init__(self, ctx, coeffs: Dict[str, Any], *, mixcolumns: MixColFinal | None = None,
                  inv_mixcolumns: InvMixColumnsFHE | None = None, use_hard_renorm_between_steps: bool = False,
@@ -129,6 +133,8 @@ class AESPipeline:
                                and hasattr(self.mix, "packed_ok") and self.mix.packed_ok())
         self._pk_cache: List[Any] | None = None
         self._pk_tag = b""
+        self._kb_cache: Dict[int, Dict[str, Any]] = {}  # round -> the packed key's dropped form and std basis
+        self._kb_tag = b""
         # the same for decrypt rounds 9..1: AddRoundKey + InvMixColumns (with_inv_mix_columns)
         self.packed_dec = bool(self.packed_xor and with_inv_mix_columns and not fuse_sub_ark
                                and hasattr(self.invmix, "packed_ok") and self.invmix.packed_ok())
@@ -180,6 +186,22 @@ class AESPipeline:
             self._rk_raw = [np.array(k, dtype=np.uint8) for k in round_keys]
             self._rk_tag = tag
         return self._rk_cache
+
+    def _ark_packed(self, x, r: int):
+        """AddRoundKey on a packed state: XOR4(x, packed round key r).  The key's level drop and
+        std basis (its conjugate and power chain) are built once per key schedule and round and
+        reused by every later encrypt / decrypt with the same keys (AESFHE_KEY_BASIS=0: rebuilt
+        per call) -- the XOR4 then forms only the state's powers"""
+        key = self._packed_round_key(r)
+        if not _KEY_BASIS:
+            return self.xor4.apply(x, key, out_level=self._floor())
+        if self._kb_tag != self._rk_tag:
+            self._kb_cache, self._kb_tag = {}, self._rk_tag
+        kb = self._kb_cache.setdefault(r, {})
+        try:
+            return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb)
+        except TypeError:  # an XOR4 without basis sharing
+            return self.xor4.apply(x, key, out_level=self._floor())
 
     def _packed_round_key(self, r: int):
         """round key r encrypted in the packed form (after _prepare_round_keys of the same keys)"""
@@ -269,7 +291,7 @@ class AESPipeline:
             self._log_pair(debug, f"enc.r{r}.sr", *ct)
             acc = self.mix.mix_packed(*ct)
             self._log_packed(debug, f"enc.r{r}.mc", acc)
-            x = self.xor4.apply(acc, self._packed_round_key(r), out_level=self._floor())
+            x = self._ark_packed(acc, r)
             self._log_packed(debug, f"enc.r{r}.ark", x)
             ct = self.encoder.renorm_unpack(x, level=next_level)
             self._log_pair(debug, f"enc.r{r}.ark.renorm", *ct)
@@ -367,7 +389,7 @@ class AESPipeline:
                 self._log_pair(debug, f"dec.r{r}.isr", *ct)
                 ct = self._sub_renorm(ct, inverse=True, level=NEED_XOR + self.encoder.PACK_DEPTH)
                 self._log_pair(debug, f"dec.r{r}.isb", *ct)
-                x = self.xor4.apply(self.encoder.pack(*ct), self._packed_round_key(r), out_level=self._floor())
+                x = self._ark_packed(self.encoder.pack(*ct), r)
                 ct = self.encoder.renorm_unpack(x, level=NEED_GF + self.encoder.PACK_DEPTH)
                 self._log_pair(debug, f"dec.r{r}.ark", *ct)
                 ct = self.encoder.renorm_unpack(self.invmix.imc_packed(*ct), level=NEED_ISR_ISB)

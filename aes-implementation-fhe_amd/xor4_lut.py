@@ -152,7 +152,10 @@ class SplitLUT2:
         self.need_b = cols(self.c1) | cols(self.c2)
         self.has2 = bool(np.any(self.c2))
 
-    def bases(self, ctx, a, b):
+    def bases(self, ctx, a, b, B=None):
+        """(A, B): powers of a, std basis of b -- B given: only a's (a basis of b computed before)"""
+        if B is not None:
+            return powers(ctx, a, self.need_a), B
         if batched(ctx) and not can_fork(ctx):
             A, B = joint_bases(ctx, [(a, self.need_a, "pow"), (b, self.need_b, "std")])
             return A, B
@@ -189,16 +192,23 @@ def eval_two(ctx, j0, j1):
     return out[0], out[1]
 
 
-def split_lut2(ctx, split: SplitLUT2, key, a, b):
-    """the split evaluation, or None (no fused op / not enough level: use the product loop)"""
+def split_lut2(ctx, split: SplitLUT2, key, a, b, keep_b=None):
+    """the split evaluation, or None (no fused op / not enough level: use the product loop).
+    keep_b: a dict caching b's std basis -- filled on the first call, reused by a later call with
+    the same b at the same level (an operand shared by two XOR4s of one step)"""
     if not getattr(ctx, "fused_luts", False):
         return None
+    cached = None
+    if keep_b is not None and keep_b.get("b") is b and keep_b.get("level") == b.level:
+        cached = keep_b["B"]
     try:
-        A, B = split.bases(ctx, a, b)
+        A, B = split.bases(ctx, a, b, cached)
     except RuntimeError as e:
         if "level" in str(e):
             return None
         raise
+    if keep_b is not None and cached is None:
+        keep_b.update(b=b, level=b.level, B=B)
     return split.eval(ctx, key, A, B)
 
 
@@ -213,15 +223,26 @@ class XOR4LUT:
     def _build_power_basis_16(self, ct: Any) -> Dict[int, Any]:
         return basis16(self.ctx, ct)
 
-    def apply(self, a_ct, b_ct, out_level=None):
+    def apply(self, a_ct, b_ct, out_level=None, keep_b=None):
         """XOR4(a, b); out_level: the lowest level the caller needs the result at (the inputs
-        are dropped to out_level + LUT2_DEPTH first, utils.drop_to); None = as given."""
+        are dropped to out_level + LUT2_DEPTH first, utils.drop_to); None = as given.
+        keep_b: a dict shared by two XOR4s whose second operand is the same ciphertext -- b's
+        basis is built once (MixColumns' r1 enters two XOR4s, mixcol_final.mix_packed)."""
         ctx = self.ctx
+        if keep_b is not None and "b_in" in keep_b and keep_b["b_in"] is b_ct and keep_b.get("out_level") == out_level:
+            b_ct = keep_b["b_dropped"]  # the same drop as before: reuse it (and so its basis)
+        elif keep_b is not None:
+            keep_b.clear()
+            keep_b.update(b_in=b_ct, out_level=out_level)
+            b_ct = drop_to(ctx, b_ct, out_level + LUT2_DEPTH) if out_level is not None else b_ct
+            keep_b["b_dropped"] = b_ct
+        elif out_level is not None:
+            b_ct = drop_to(ctx, b_ct, out_level + LUT2_DEPTH)
         if out_level is not None:
-            a_ct, b_ct = drop_to(ctx, a_ct, out_level + LUT2_DEPTH), drop_to(ctx, b_ct, out_level + LUT2_DEPTH)
+            a_ct = drop_to(ctx, a_ct, out_level + LUT2_DEPTH)
         if not hasattr(self, "_split"):
             self._split = SplitLUT2(self.coeffs)
-        out = split_lut2(ctx, self._split, "xor4", a_ct, b_ct)
+        out = split_lut2(ctx, self._split, "xor4", a_ct, b_ct, keep_b)
         if out is not None:
             return out
         A, B = pair(ctx, lambda: self._build_power_basis_16(a_ct), lambda: self._build_power_basis_16(b_ct))

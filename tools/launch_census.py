@@ -55,8 +55,7 @@ def main():
         timed("final_bootstrap", lambda: bootstrap1(ctx, acc, 2 * pipe.layout.period) if packed else None)
         c2 = timed("mix_columns(total)", lambda: mix(*c))
         if packed:
-            timed("add_round_key+renorm", lambda: pipe.encoder.renorm_unpack(
-                pipe.xor4.apply(c2, pipe._packed_round_key(2), out_level=pipe._floor()), level=pipe.need_sub))
+            timed("add_round_key+renorm", lambda: pipe.encoder.renorm_unpack(pipe._ark_packed(c2, 2), level=pipe.need_sub))
         timed("encrypt(10 rounds)", lambda: pipe.encrypt(st, rks))
     out = {k: {"ms": round(v["ms"] / reps, 3), "launches": v["launches"] / reps} for k, v in res.items()}
     steps = ("sub_bytes+renorm", "shift_rows", "mix_columns(total)", "add_round_key+renorm")

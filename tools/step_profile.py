@@ -62,7 +62,7 @@ def round_steps(pipe, ct, rk, res, timed):
     c = timed("mix_columns(total)", lambda: mix(*c))
     if packed:
         c = timed("add_round_key+renorm", lambda: pipe.encoder.renorm_unpack(
-            pipe.xor4.apply(c, pipe._packed_round_key(2), out_level=pipe._floor()), level=pipe.need_sub))
+            pipe._ark_packed(c, 2), level=pipe.need_sub))
     else:
         c = timed("add_round_key+renorm", lambda: pipe._ark_renorm(c, rk[2], level=pipe.need_sub))
     res["round_total"] = res.get("round_total", 0.0) + (time.perf_counter() - t0) * 1e3 - (res["mix_columns(no final bootstrap)"] - nb0)
