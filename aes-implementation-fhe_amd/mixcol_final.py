@@ -200,16 +200,35 @@ class MixColFinal:
         AddRoundKey XORs it with a packed round key and unpacks in its renorm).  The GF
         multipliers stay pairs (they mix hi and lo); their outputs and the column shifts are
         packed (one level: inputs one level higher than mix_rotated's).  Default form
-        (AESFHE_MC_FORM=xtime): 2x ^ 3 r1 ^ r2 ^ r3 = 2 (x ^ r1) ^ (r1 ^ r2 ^ r3), xtime being
-        GF(2)-linear -- one GF multiplier pair on the renormalised, unpacked x ^ r1 and four single
-        XOR4s; AESFHE_MC_FORM=2gf keeps the reference's two multiplier pairs (GF2(x), GF3(r1)).
-        The bytes are the same either way."""
+        (AESFHE_MC_FORM=rot): with u = x ^ r1, the column shift by two of u is r2 ^ r3 (R^2 x =
+        r2, R^2 r1 = r3), so 2x ^ 3 r1 ^ r2 ^ r3 = 2u ^ (r1 ^ R^2 u): one GF multiplier pair on
+        the renormalised, unpacked u, one extra rotation pair of u and three single XOR4s, and
+        only r1 shifted from the input.  AESFHE_MC_FORM=xtime computes r2 ^ r3 from shifted
+        inputs (2 (x ^ r1) ^ (r1 ^ r2 ^ r3), four XOR4s, xtime being GF(2)-linear);
+        AESFHE_MC_FORM=2gf keeps the reference's two multiplier pairs (GF2(x), GF3(r1)).  The
+        bytes are the same in every form."""
         ctx, enc = self.ctx, self.enc
-        steps = [-4 * k * self.stride for k in (1, 2, 3)]
-        rh, rl = rot_pair(ctx, ct_hi, ct_lo, steps)
         fl = RENORM_FLOOR
         gl = fl + LUT2_DEPTH + enc.PACK_DEPTH
-        if os.environ.get("AESFHE_MC_FORM", "xtime") == "xtime":
+        form = os.environ.get("AESFHE_MC_FORM", "rot")
+        if form == "rot":
+            s1 = -4 * self.stride
+            (rh1,), (rl1,) = rot_pair(ctx, ct_hi, ct_lo, [s1])
+            p1, p0 = pair(ctx, lambda: enc.pack(rh1, rl1), lambda: enc.pack(ct_hi, ct_lo), shared=(ct_hi, ct_lo, rh1, rl1))
+            u = enc.renorm_unpack(self._xor_ct(p0, p1, fl), level=gl + LUT2_DEPTH)
+
+            def r1_r2r3():
+                # R^2 u = r2 ^ r3, shifted at the level its pack + XOR4 need (gl), not u's
+                (vh,), (vl,) = rot_pair(ctx, drop_to(ctx, u[0], gl), drop_to(ctx, u[1], gl), [2 * s1])
+                return enc.renorm_packed(self._xor_ct(enc.pack(vh, vl), p1, fl), level=NEED_XOR)
+            two, w = pair(ctx, lambda: enc.pack(*self.gf_mult_2(*u, out_level=gl)), r1_r2r3, shared=(*u, p1))
+            acc = enc.renorm_packed(self._xor_ct(two, w, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
+            if do_final_bootstrap:
+                acc = bootstrap1(ctx, acc, 2 * self.layout.period)
+            return acc
+        steps = [-4 * k * self.stride for k in (1, 2, 3)]
+        rh, rl = rot_pair(ctx, ct_hi, ct_lo, steps)
+        if form == "xtime":
             # 2x ^ 3 r1 ^ r2 ^ r3 = 2 (x ^ r1) ^ (r1 ^ r2 ^ r3) (xtime is GF(2)-linear): ONE GF
             # multiplier pair and four single XOR4s instead of two pairs and three XOR4s
             p1, p0 = pair(ctx, lambda: enc.pack(rh[0], rl[0]), lambda: enc.pack(ct_hi, ct_lo), shared=(ct_hi, ct_lo, *rh, *rl))
