@@ -6,7 +6,8 @@ modules only ever talk to this object.  Extra keywords: ``log_n`` (N = 2^log_n, 
 2^16 as in the reference harness; config 1 of BASELINE.json uses 2^15), ``dnum`` and
 ``seed`` (key material; drawn from ``os.urandom`` when None, pinned only by tests, smoke and
 multi-rank runs that share one key set), ``lazy`` (deferred relinearisation),
-``concurrent`` (hi / lo halves on two HIP streams), ``fused_luts`` (one-kernel LUT sums,
+``concurrent`` (hi / lo halves on two HIP streams; off by default: the batched forms
+on one stream are faster), ``fused_luts`` (one-kernel LUT sums,
 DESIGN.md §3.8), ``allow_insecure`` (parameter sets above the 128-bit bound, for small
 test / smoke sets only) and ``enc_nonce`` (the per-process nonce of the encryption
 randomness, include/aesfhe.h aesfhe_set_enc_nonce; random unless pinned).
@@ -29,7 +30,7 @@ class EngineContext:
     def __init__(self, signature: int, *, max_level: int = 17, use_bootstrap: bool = True,
                  use_multiparty: bool = False, mode: str = "cpu", device_id: int = 0,
                  thread_count: int | None = None, log_n: int = 16, dnum: int | None = None, seed: int | bytes | None = None,
-                 lazy: bool = True, concurrent: bool = True, fused_luts: bool = True, allow_insecure: bool = False,
+                 lazy: bool = True, concurrent: bool = False, fused_luts: bool = True, allow_insecure: bool = False,
                  enc_nonce: int | None = None):
         # REF/engine_context.py:17-42: signature selects the engine constructor form
         if signature == 1:
@@ -227,10 +228,11 @@ class EngineContext:
         """whether run_parallel branches would run concurrently (False inside a branch)"""
         return self.engine.can_fork()
 
-    def run_parallel(self, *fns):
+    def run_parallel(self, *fns, force: bool = False):
         """Independent branches (e.g. the hi and lo nibble halves of an AES step) on separate
-        HIP streams; sequential when the context was built with concurrent=False."""
-        return self.engine.parallel(*fns)
+        HIP streams; sequential when the context was built with concurrent=False, unless
+        `force` (Engine.parallel)."""
+        return self.engine.parallel(*fns, force=force)
 
     def level_down(self, ct, level: int):
         """the same message at a lower level (exact scale; used by utils.drop_to)"""

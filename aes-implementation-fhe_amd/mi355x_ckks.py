@@ -290,7 +290,7 @@ class Engine:
 
     def __init__(self, *, mode: str = "gpu", use_bootstrap: bool = False, use_multiparty: bool = False,
                  thread_count: int = 0, device_id: int = 0, max_level: int = 17, log_n: int = 16,
-                 dnum: int | None = None, seed: int | None = None, lazy: bool = True, concurrent: bool = True,
+                 dnum: int | None = None, seed: int | None = None, lazy: bool = True, concurrent: bool = False,
                  allow_insecure: bool = False, enc_nonce: int | None = None):
         if use_multiparty:
             raise ValueError("multiparty key generation is not supported")
@@ -340,8 +340,13 @@ class Engine:
         if early:
             self.profile([k for k in early.split(",") if k])
         self.set_lazy(lazy)
-        # AESFHE_SERIAL=1: every context runs its branches sequentially on one stream (A/B runs)
-        self.concurrent = bool(concurrent) and os.environ.get("AESFHE_SERIAL") != "1"
+        # branches (utils.pair) on their own streams only when asked: since the batched forms of
+        # round 3 (one launch for both halves' rows) one stream is faster
+        # (C2 57.8 vs 53.1 rounds/s, profiles/r3_serial_ab.json).  AESFHE_CONCURRENT=1 /
+        # AESFHE_SERIAL=1 force either mode for every context (A/B runs)
+        env = os.environ
+        self._serial = env.get("AESFHE_SERIAL") == "1"
+        self.concurrent = (bool(concurrent) or env.get("AESFHE_CONCURRENT") == "1") and not self._serial
         self._pool = None
         self._tls = threading.local()
 
@@ -362,11 +367,12 @@ class Engine:
                                                                thread_name_prefix="aesfhe-stream")
         return self._pool
 
-    def parallel(self, *fns):
+    def parallel(self, *fns, force: bool = False):
         """Run independent branches concurrently: one host thread and one HIP stream each,
         between aesfhe_fork and aesfhe_join.  Results in order; nested calls and
-        concurrent=False run sequentially."""
-        if len(fns) <= 1 or not self.concurrent or getattr(self._tls, "worker", False):
+        concurrent=False run sequentially unless `force` (a call site whose branches are whole
+        bootstraps, where two streams pay; AESFHE_SERIAL=1 still wins)."""
+        if len(fns) <= 1 or not (self.concurrent or (force and not self._serial)) or getattr(self._tls, "worker", False):
             return [f() for f in fns]
         ex = self._executor()
         self._ctx.check(self._ctx.lib.aesfhe_fork(self._ctx.ptr))

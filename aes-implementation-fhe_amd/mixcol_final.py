@@ -21,6 +21,7 @@ from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1
 
 # AESFHE_SHARE_R1=0: MixColumns' r1 basis rebuilt in its second XOR4 (A/B runs)
 _SHARE_R1 = os.environ.get("AESFHE_SHARE_R1", "1") != "0"
+_FHE_FORK = os.environ.get("AESFHE_FHE_FORK", "1") != "0"  # true-FHE MixColumns halves on two streams (A/B)
 
 
 class _CoeffCache:
@@ -268,19 +269,20 @@ class MixColFinal:
         # inputs dropped to the lowest level that leaves their output at RENORM_FLOOR
         fl = RENORM_FLOOR
         # the two GF multiplier pairs are independent: one per branch stream, each batching
-        # its own bases and evaluations
+        # its own bases and evaluations; in true-FHE mode on two streams even
+        # in a one-stream context, with the bootstrap-sized renorms that follow
+        fhe = self.enc.renorm_hook is not None
         two, thr = pair(self.ctx, lambda: self.gf_mult_2(ct_hi, ct_lo, out_level=fl + LUT2_DEPTH),
-                        lambda: self.gf_mult_3(*rot[1], out_level=fl + LUT2_DEPTH))
+                        lambda: self.gf_mult_3(*rot[1], out_level=fl + LUT2_DEPTH), fork=fhe and _FHE_FORK)
         log("two", two)
         log("thr", thr)
         last = NEED_BOOTSTRAP if do_final_bootstrap else None  # bootstrapped next (from level 0), else fresh
-        fhe = self.enc.renorm_hook is not None
         if fhe:
             # true-FHE: the GF multipliers amplify their inputs' errors up to ~20x, so their outputs
             # are renormalised (bootstrap + two snaps) before the first XOR; then the reference's
             # chain, each of r2 / r3 meeting a freshly snapped partner (zeta16_noise_reducer.py)
             two, thr = pair(self.ctx, lambda: self._renorm_pair(*two, level=NEED_XOR),
-                            lambda: self._renorm_pair(*thr, level=NEED_XOR))
+                            lambda: self._renorm_pair(*thr, level=NEED_XOR), fork=_FHE_FORK)
         if isinstance(debug, dict) or fhe:
             # the reference's chain ((2x ^ 3r1) ^ r2) ^ r3 and its debug keys (REF :127-163): acc1 and
             # acc2 before their renorm, acc3 after it.  True-FHE mode keeps this order: each of r2 / r3

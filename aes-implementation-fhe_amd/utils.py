@@ -56,16 +56,17 @@ def drop_to(ctx, ct, level):
     return down(ct, level)
 
 
-def pair(ctx, fa, fb, shared=()):
+def pair(ctx, fa, fb, shared=(), fork=False):
     """(fa(), fb()) -- the hi / lo halves of an AES step, run concurrently on two HIP streams
     when the context supports it (EngineContext.run_parallel); `shared` ciphertexts read by
-    both halves are settled first.  Results are identical to the sequential order."""
+    both halves are settled first.  Results are identical to the sequential order.  fork=True:
+    on two streams even in a one-stream context (halves made of whole bootstraps)."""
     run = getattr(ctx, "run_parallel", None)
     if run is None:
         return fa(), fb()
     if shared:
         ctx.engine.settle(*shared)
-    a, b = run(fa, fb)
+    a, b = run(fa, fb, force=True) if fork else run(fa, fb)
     return a, b
 
 
@@ -89,6 +90,19 @@ def bootstrap1(ctx, ct, period=None):
     if period is not None and period < ctx.engine.slot_count and sparse is not None:
         return sparse(ctx.to_intt(ct), period)
     return ctx.bootstrap(ctx.to_intt(ct))
+
+
+def stacked_pair(ctx, f, a, b):
+    """(f(a), f(b)) for ONE function of one ciphertext applied to both halves: a and b stacked
+    into a two-member operand (include/aesfhe.h aesfhe_stack), so every launch of f covers both
+    halves' rows -- when the engine stacks and the halves would not fork onto
+    two streams; else utils.pair.  Results identical either way (tests/test_gpu_stacked.py);
+    AESFHE_STACK_HALVES=0 keeps the two separate calls (A/B runs)."""
+    E = getattr(ctx, "engine", ctx)
+    if _STACK_HALVES and not can_fork(ctx) and getattr(E, "stack", None) is not None:
+        out = E.unstack(f(E.stack([a, b])))
+        return out[0], out[1]
+    return pair(ctx, lambda: f(a), lambda: f(b), shared=(a, b))
 
 
 def can_fork(ctx) -> bool:
@@ -120,6 +134,7 @@ def rot_many(ctx, ct, steps):
 # heterogeneous batched key switch (EngineContext.rotate_multi); "0": the
 # per-half hoisted rotations on the two branch streams (A/B measurements)
 _MULTI = os.environ.get("AESFHE_GALOIS_MULTI", "1") != "0"
+_STACK_HALVES = os.environ.get("AESFHE_STACK_HALVES", "1") != "0"
 
 
 def rotate_multi(ctx, items):

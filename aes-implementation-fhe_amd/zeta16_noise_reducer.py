@@ -38,7 +38,7 @@ from __future__ import annotations
 
 from typing import Any, Tuple
 
-from utils import NEED_SR_ARK, pair
+from utils import NEED_SR_ARK, pair, stacked_pair
 from xor4_lut import powers
 
 SNAP15_DEPTH = 4
@@ -74,7 +74,9 @@ class Zeta16NoiseReducer:
         return ctx.bootstrap(y) if self.bootstrap_after else y
 
     def apply_pair(self, ct_hi, ct_lo):
-        return pair(self.ctx, lambda: self.apply(ct_hi), lambda: self.apply(ct_lo))
+        if self.bootstrap_before or self.bootstrap_after:  # the bootstrapping variants keep two calls
+            return pair(self.ctx, lambda: self.apply(ct_hi), lambda: self.apply(ct_lo))
+        return stacked_pair(self.ctx, self.apply, ct_hi, ct_lo)
 
 
 class Zeta16Snap15:
@@ -125,8 +127,9 @@ class BootstrapSnap:
         else:
             uh, ul = ctx.bootstrap_pair_scaled(ctx.to_intt(ct_hi), ctx.to_intt(ct_lo), self.snap.kappa)
         sn = self.snap
+        # the same snap on both halves: one stacked evaluation (utils.stacked_pair)
         if twice:
-            return pair(ctx, lambda: sn.apply(sn.apply_scaled(uh)), lambda: sn.apply(sn.apply_scaled(ul)), shared=(uh, ul))
-        return pair(ctx, lambda: sn.apply_scaled(uh), lambda: sn.apply_scaled(ul), shared=(uh, ul))
+            return stacked_pair(ctx, lambda u: sn.apply(sn.apply_scaled(u)), uh, ul)
+        return stacked_pair(ctx, sn.apply_scaled, uh, ul)
 
     __call__ = apply_pair

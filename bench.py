@@ -58,8 +58,9 @@ def parse():
                     help="diagnostic only: skip MixColFinal's final bootstrap (not the benchmark workload)")
     ap.add_argument("--eager", action="store_true", help="relinearise and rescale after every product (no deferred evaluation)")
     ap.add_argument("--serial", action="store_true",
-                    help="hi/lo halves on one stream (same launches, no overlap): for rocprofv3 --pmc passes, whose "
-                         "counter collection crashes on launches from the branch threads")
+                    help="hi/lo halves on one stream, batched (the default since round 3; kept for old command lines)")
+    ap.add_argument("--concurrent", action="store_true",
+                    help="A/B only: hi/lo halves on two HIP streams (each half batching its own products)")
     ap.add_argument("--dry-run", action="store_true",
                     help="the N-rank host path on CPU (process group, shared-seed key broadcast, sharding, barrier, "
                          "max-over-ranks, rank-0 line) with one CPU oracle engine per rank running AddRoundKey (config C1 "
@@ -426,7 +427,7 @@ def main():
     signature = 2 if args.no_final_bootstrap else 1
     seed = shared_seed(dist, args.seed)  # one key set for every rank (broadcast once, untimed)
     ctx = EngineContext(signature=signature, max_level=17, thread_count=1, device_id=local, seed=seed, lazy=not args.eager,
-                        concurrent=not args.serial)
+                        concurrent=args.concurrent and not args.serial)
     xor4 = XOR4LUT(ctx, coeffs["xor4"])
     from state_encoder import SlotLayout
     layout = SlotLayout(ctx.engine.slot_count, 1, periodic=not args.ref_layout)

@@ -1,7 +1,7 @@
 """Launch census of the C2 bench workload: kernel launches (aesfhe_launch_count) and synchronised
 wall time of each AES step of a middle encrypt round, of the sparse bootstrap alone, and of one
 full 10-round encrypt (launches per encrypt, the VERDICT r2 target).  Same steps as
-tools/step_profile.py.  usage: python tools/launch_census.py [--serial]"""
+tools/step_profile.py.  usage: python tools/launch_census.py [--concurrent]"""
 import json
 import sys
 import time
@@ -20,7 +20,7 @@ from utils import NEED_SR_MIX, bootstrap1  # noqa: E402
 
 
 def main():
-    serial = "--serial" in sys.argv
+    serial = "--concurrent" not in sys.argv
     reps = 3
     ctx = EngineContext(signature=1, max_level=17, concurrent=not serial)
     E = ctx.engine

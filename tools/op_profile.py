@@ -22,7 +22,7 @@ from xor4_lut import XOR4LUT  # noqa: E402
 
 
 def main(reps=10):
-    ctx = EngineContext(signature=1, max_level=17, concurrent="--serial" not in sys.argv)
+    ctx = EngineContext(signature=1, max_level=17, concurrent="--concurrent" in sys.argv)
     E = ctx.engine
     co = load_all_coeffs()
     enc = StateEncoder(ctx)

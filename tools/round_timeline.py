@@ -1,6 +1,6 @@
 """GPU timeline of encrypt rounds (C2 bench workload, both branch streams).
 
-run:      python tools/round_timeline.py run [ROUNDS] [--serial]
+run:      python tools/round_timeline.py run [ROUNDS] [--concurrent]
           one warm round, a 100 ms host pause (a marker gap in the trace), then ROUNDS rounds
 analyse:  python tools/round_timeline.py analyse OUT.json DIR
           reads DIR's rocprofv3 --kernel-trace CSV, keeps the kernels after the last gap
@@ -25,7 +25,7 @@ def run(rounds):
     from aes_keyschedule import expand_aes128_key, load_all_coeffs
     from engine_context import EngineContext
     from pipeline import AESPipeline
-    ctx = EngineContext(signature=1, max_level=17, seed=0x5EED, concurrent="--serial" not in sys.argv)
+    ctx = EngineContext(signature=1, max_level=17, seed=0x5EED, concurrent="--concurrent" in sys.argv)
     E = ctx.engine
     pipe = AESPipeline(ctx, load_all_coeffs(), use_hard_renorm_between_steps=True)
     np.random.seed(7)

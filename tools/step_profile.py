@@ -19,7 +19,7 @@ from utils import pair  # noqa: E402
 
 def main():
     lazy = "--eager" not in sys.argv
-    serial = "--serial" in sys.argv
+    serial = "--concurrent" not in sys.argv
     reps = 3
     ctx = EngineContext(signature=1, max_level=17, lazy=lazy, concurrent=not serial)
     E = ctx.engine
