@@ -307,10 +307,14 @@ public:
         launch_ntt_fwd(S(), T_, dst, src, rows, rm, m);
         cnt_[C_NTT_ROWS] += rows;
     }
-    void intt(u32* dst, const u32* src, int rows, RowMap rm, LimbMap m) {
-        launch_ntt_inv(S(), T_, dst, src, rows, rm, m);
+    void intt(u32* dst, const u32* src, int rows, RowMap rm, LimbMap m, const u32* post = nullptr) {
+        launch_ntt_inv(S(), T_, dst, src, rows, rm, m, post);
         cnt_[C_NTT_ROWS] += rows;
     }
+    // a base conversion and the forward NTT of its output: one fused pass-1 launch when the ring
+    // has it (the INTT that made cb's sources then carried the qhat^{-1} factors), else
+    // k_base_convert into cb.dst and the NTT of those rows
+    bool fused_conv(bool up) const { return (ntt_conv_fused_mask(T_) >> (up ? 0 : 1)) & 1; }
 
     // ------------------------------------------------------------------ keys
     void keygen() {
@@ -1306,8 +1310,9 @@ public:
         const int nd = (nl + alpha - 1) / alpha;
         if (alpha > kMaxConvH || np > kMaxConvH || nb * nd > kMaxConvGroups) throw std::runtime_error("keyswitch: digit too large");
         const LimbMap em = extmap(nl);
+        const bool fz = fused_conv(true);
         u32* coef = tmp((size_t)nb * nl);
-        intt(coef, d, nb * nl, RowMap{nl, nb > 1 ? (int)(d_ms / n) : nl, nl, 0, 0}, qmap());
+        intt(coef, d, nb * nl, RowMap{nl, nb > 1 ? (int)(d_ms / n) : nl, nl, 0, 0}, qmap(), fz ? d_modup_qh_ + modup_qh_off_[nl] : nullptr);
         u32* ext = tmp((size_t)nb * nd * ne);
         const size_t* toff = &modup_off_[(size_t)nl * hp_.dnum];
         ConvBatch up;
@@ -1322,10 +1327,15 @@ public:
                 up.qhinv[gi] = up.tab[gi] + (size_t)2 * h * ne;
                 up.negq[gi] = up.qhinv[gi] + 2 * h;
             }
-        launch_base_convert(S(), T_, up, ne, em);
         RowMap xr = rows_dense(ne);
         xr.skip_alpha = alpha, xr.skip_nl = nl, xr.skip_groups = nd;
-        ntt(ext, ext, nb * nd * ne, xr, em);
+        if (fz) {
+            launch_ntt_fwd_conv(S(), T_, ext, up, nb * nd * ne, xr, em);
+            cnt_[C_NTT_ROWS] += nb * nd * ne;
+        } else {
+            launch_base_convert(S(), T_, up, ne, em);
+            ntt(ext, ext, nb * nd * ne, xr, em);
+        }
         untmp(coef, (size_t)nb * nl);
         return ext;
     }
@@ -1348,8 +1358,9 @@ public:
                u32* const* outm = nullptr) {
         const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, npl = 2 * nb;
         if (npl > kMaxConvGroups) throw std::runtime_error("moddown: batch too large");
+        const bool fz = fused_conv(false);
         u32* yp = tmp((size_t)npl * np);
-        intt(yp, acc, npl * np, RowMap{np, ne, np, nl, 0}, LimbMap{np, hp_.p_off(), 0});
+        intt(yp, acc, npl * np, RowMap{np, ne, np, nl, 0}, LimbMap{np, hp_.p_off(), 0}, fz ? d_moddown_phinv_ : nullptr);
         u32* conv = tmp((size_t)npl * nl);
         const size_t doff = moddown_off_[nl];
         ConvBatch dn;
@@ -1362,14 +1373,17 @@ public:
             dn.qhinv[p] = d_moddown_phinv_;
             dn.negq[p] = d_negp_;
         }
-        launch_base_convert(S(), T_, dn, nl, qmap());
+        if (!fz) launch_base_convert(S(), T_, dn, nl, qmap());
         Ct o;
         if (dst || outm) {
             o.level = level, o.npoly = npl, o.nb = nb, o.words = (size_t)npl * nl * n, o.data = dst;
         } else {
             o = alloc_ct(level, npl, nb);
         }
-        launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_pinv_, add0, add1, npl, nl, add_ms, outm);
+        if (fz)
+            launch_ntt_finish_conv(S(), T_, o.data, conv, dn, acc, ne, d_pinv_, add0, add1, npl, nl, add_ms, outm);
+        else
+            launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_pinv_, add0, add1, npl, nl, add_ms, outm);
         cnt_[C_NTT_ROWS] += (size_t)npl * nl;
         untmp(yp, (size_t)npl * np);
         untmp(conv, (size_t)npl * nl);
@@ -1417,8 +1431,9 @@ public:
         const LimbMap em = extmap(nq);
         const u32* key = ksk(tag_d2s());
         // ModUp Q0 -> P' (the own limbs q0, q1 are read from d by the key inner product)
+        const bool fz = fused_conv(true), fzd = fused_conv(false);
         u32* coef = tmp((size_t)nb * nq);
-        intt(coef, d, nb * nq, RowMap{nq, (int)(ms / n), nq, 0, 0}, qmap());
+        intt(coef, d, nb * nq, RowMap{nq, (int)(ms / n), nq, 0, 0}, qmap(), fz ? d_d2s_ + d2s_off_.up_qhinv : nullptr);
         u32* ext = tmp((size_t)nb * ne);
         ConvBatch up;
         up.n = nb;
@@ -1430,17 +1445,22 @@ public:
             up.qhinv[m] = d_d2s_ + d2s_off_.up_qhinv;  // [nq] pairs: (Q0 / q_i)^-1 mod q_i
             up.negq[m] = d_d2s_ + d2s_off_.up_negq;    // [ne]: -Q0 mod target
         }
-        launch_base_convert(S(), T_, up, ne, em);
-        untmp(coef, (size_t)nb * nq);
         RowMap xr = rows_dense(ne);
         xr.skip_alpha = hp_.alpha, xr.skip_nl = nq, xr.skip_groups = 1;
-        ntt(ext, ext, nb * ne, xr, em);
+        if (fz) {
+            launch_ntt_fwd_conv(S(), T_, ext, up, nb * ne, xr, em);
+            cnt_[C_NTT_ROWS] += nb * ne;
+        } else {
+            launch_base_convert(S(), T_, up, ne, em);
+            ntt(ext, ext, nb * ne, xr, em);
+        }
+        untmp(coef, (size_t)nb * nq);
         u32* acc = tmp((size_t)npl * ne);
         launch_key_inner(S(), T_, acc, ext, d, key, 1, ne, nq, hp_.alpha, ne, nq, em, 0, nb, (size_t)ne * n, ms, (size_t)2 * ne * n);
         untmp(ext, (size_t)nb * ne);
         // ModDown by P' onto (q0, q1), + add0
         u32* yp = tmp((size_t)npl * np);
-        intt(yp, acc, npl * np, RowMap{np, ne, np, nq, 0}, LimbMap{np, hp_.p_off(), 0});
+        intt(yp, acc, npl * np, RowMap{np, ne, np, nq, 0}, LimbMap{np, hp_.p_off(), 0}, fzd ? d_d2s_ + d2s_off_.dn_qhinv : nullptr);
         u32* conv = tmp((size_t)npl * nq);
         ConvBatch dn;
         dn.n = npl;
@@ -1452,10 +1472,13 @@ public:
             dn.qhinv[p] = d_d2s_ + d2s_off_.dn_qhinv;  // [np] pairs: (P' / p_k)^-1 mod p_k
             dn.negq[p] = d_d2s_ + d2s_off_.dn_negq;    // [nq]: -P' mod q_t
         }
-        launch_base_convert(S(), T_, dn, nq, qmap());
-        untmp(yp, (size_t)npl * np);
+        if (!fzd) launch_base_convert(S(), T_, dn, nq, qmap());
         Ct o = alloc_ct(0, npl, nb);
-        launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_d2s_ + d2s_off_.pinv, add0, nullptr, npl, nq, ms);
+        if (fzd)
+            launch_ntt_finish_conv(S(), T_, o.data, conv, dn, acc, ne, d_d2s_ + d2s_off_.pinv, add0, nullptr, npl, nq, ms);
+        else
+            launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_d2s_ + d2s_off_.pinv, add0, nullptr, npl, nq, ms);
+        untmp(yp, (size_t)npl * np);
         cnt_[C_NTT_ROWS] += (size_t)npl * nq;
         untmp(conv, (size_t)npl * nq);
         untmp(acc, (size_t)npl * ne);
@@ -1520,10 +1543,11 @@ public:
         const int n = hp_.n, nl = hp_.nl(l), r = hp_.nl(l - 1), k = nl - r, np = hp_.n_p, ne = nl + np;
         const int npl = 2 * nb, h = k + np;
         if (mdr_off_[l] == SIZE_MAX || npl > kMaxConvGroups) throw std::runtime_error("moddown_rescale: unsupported level or batch");
-        u32* ys = tmp((size_t)npl * h);
-        intt(ys, acc, npl * h, RowMap{h, ne, h, r, 0}, LimbMap{k, r, hp_.p_off()});
-        u32* conv = tmp((size_t)npl * r);
+        const bool fz = fused_conv(false);
         const size_t off = mdr_off_[l];
+        u32* ys = tmp((size_t)npl * h);
+        intt(ys, acc, npl * h, RowMap{h, ne, h, r, 0}, LimbMap{k, r, hp_.p_off()}, fz ? d_mdr_ + off + 2 * (size_t)h * r : nullptr);
+        u32* conv = tmp((size_t)npl * r);
         ConvBatch cb;
         cb.n = npl;
         for (int p = 0; p < npl; ++p) {
@@ -1534,15 +1558,19 @@ public:
             cb.qhinv[p] = d_mdr_ + off + 2 * (size_t)h * r;     // [h] pairs
             cb.negq[p] = d_mdr_ + off + 2 * (size_t)h * (r + 1);  // [r]
         }
-        launch_base_convert(S(), T_, cb, r, qmap());
-        untmp(ys, (size_t)npl * h);
+        if (!fz) launch_base_convert(S(), T_, cb, r, qmap());
         Ct o;
         if (dst || outm) {
             o.level = l - 1, o.npoly = npl, o.nb = nb, o.words = (size_t)npl * r * n, o.data = dst;
         } else {
             o = alloc_ct(l - 1, npl, nb);
         }
-        launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_mdr_ + off + 2 * (size_t)h * (r + 1) + r, nullptr, nullptr, npl, r, 0, outm);
+        const u32* qinv = d_mdr_ + off + 2 * (size_t)h * (r + 1) + r;
+        if (fz)
+            launch_ntt_finish_conv(S(), T_, o.data, conv, cb, acc, ne, qinv, nullptr, nullptr, npl, r, 0, outm);
+        else
+            launch_ntt_finish(S(), T_, o.data, conv, acc, ne, qinv, nullptr, nullptr, npl, r, 0, outm);
+        untmp(ys, (size_t)npl * h);
         cnt_[C_NTT_ROWS] += (size_t)npl * r;
         untmp(conv, (size_t)npl * r);
         cnt_[C_RESCALE]++;
@@ -3775,6 +3803,19 @@ private:
             }
         }
         d_modup_ = dev_upload(mu);  // per (level, digit): [h][ne] qhat pairs, [h] qhat^-1 pairs, [ne] -Q
+        // the same qhat^-1 pairs per limb count, limb by limb across the digits (the ModUp INTT's
+        // post factors when the conversion is fused into the NTT: ntt.hip k_ntt1_fwd_conv)
+        std::vector<u32> mq;
+        modup_qh_off_.assign((size_t)hp_.n_ks + 1, 0);
+        for (int nl = 1; nl <= hp_.n_ks; ++nl) {
+            modup_qh_off_[nl] = mq.size();
+            for (int j = 0; j * hp_.alpha < nl; ++j) {
+                const int lo = j * hp_.alpha, h = std::min(hp_.alpha, nl - lo), ne = nl + hp_.n_p;
+                const size_t at = modup_off_[(size_t)nl * hp_.dnum + j] + (size_t)2 * h * ne;
+                for (int i = 0; i < 2 * h; ++i) mq.push_back(mu[at + i]);
+            }
+        }
+        d_modup_qh_ = dev_upload(mq);
 
         // ModDown tables per level: [np][nl] Shoup pairs of phat_k mod q_t; phat_k^{-1} mod p_k; P^{-1} mod q_t
         std::vector<u32> md;
@@ -3954,6 +3995,8 @@ private:
     u32* d_gadget_ = nullptr;
     u32* d_modup_ = nullptr;
     std::vector<size_t> modup_off_;
+    u32* d_modup_qh_ = nullptr;
+    std::vector<size_t> modup_qh_off_;
     u32* d_moddown_ = nullptr;
     u32* d_moddown_phinv_ = nullptr;
     std::vector<size_t> moddown_off_;

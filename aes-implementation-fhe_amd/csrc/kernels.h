@@ -93,7 +93,9 @@ struct NttAux {
 };
 // out-of-place (src may equal dst); supported ring sizes 2^13 .. 2^16
 void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map);
-void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map);
+// post (nullable): [rows per group] Shoup pairs, row i of every group also multiplied by post[i]
+// (a base conversion's qhat^{-1}, folded into the inverse's N^{-1} scaling for k_ntt1_fwd_conv)
+void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map, const u32* post = nullptr);
 // rescale by the prime q_last, fused: v[p][t] = centred(last[p]) mod q_t -> NTT ->
 // out[p][t] = (cur[p][t] - v) * qinv_t;  cur has nl_in rows per poly, out/v have nt
 void launch_rescale_ntt(hipStream_t st, const DevTables& T, u32* out, const u32* cur, const u32* last, u32* v, const u32* qinv,
@@ -198,6 +200,16 @@ struct ConvBatch {
     const u32* negq[kMaxConvGroups] = {};
 };
 void launch_base_convert(hipStream_t st, const DevTables& T, const ConvBatch& cb, int nt, LimbMap map);
+// the base conversion fused into the forward NTT's first pass (ntt.hip k_ntt1_fwd_conv): the
+// conversion of cb (sources already times qhat^{-1}: launch_ntt_inv's post) written as its NTT.
+// Row group z of the RowMap is conversion group z (cb.dst unused).  ntt_conv_fused_mask: where it
+// is used (N = 2^16 only): bit 0 the ModUps, bit 1 the ModDowns (AESFHE_FUSED_CONV, default 0: slower on this GPU)
+int ntt_conv_fused_mask(const DevTables& T);
+void launch_ntt_fwd_conv(hipStream_t st, const DevTables& T, u32* dst, const ConvBatch& cb, int rows, RowMap rm, LimbMap map);
+// launch_ntt_finish with conv computed in the NTT's load from cb (the ModDown conversion)
+void launch_ntt_finish_conv(hipStream_t st, const DevTables& T, u32* out, u32* conv, const ConvBatch& cb, const u32* cur, int cur_stride,
+                            const u32* qinv, const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride = 0,
+                            u32* const* outm = nullptr);
 // acc[0|1][x] = sum_j e_j[x] * key[j][b|a][krow(x)] with e_j = ext[j] except on digit j's
 // own limbs (x < nl, x / alpha == j) where e_j = d (the NTT-form input);
 // ext: [nd][ne][N]; key: [dnum][2][nkey][N]

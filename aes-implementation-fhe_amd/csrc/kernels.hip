@@ -217,21 +217,48 @@ __global__ void k_crt2_spread(u32* v, const u32* src, int nt, u32 q0, u32 q1, u3
 // centred overflow estimate u = round(sum y_i / q_i), then emits its chunk of targets:
 // ext_t = sum_i y_i [qhat_i]_t + u [-Q]_t  (mod t).
 // The block's constants (source primes, qhat^{-1}, the h x kConvTargets table slice, -Q,
-// target primes) are staged in LDS first: read from global memory next to the stores to
+// target primes) are staged in LDS (behind the residue loads): read from global memory next to the stores to
 // ext they would be re-fetched, one dependent load per multiply-add.
 #ifndef AESFHE_CONV_TARGETS
 #define AESFHE_CONV_TARGETS 16
 #endif
 constexpr int kConvTargets = AESFHE_CONV_TARGETS;
-// H sources, compile-time: every load issued up front, the multiply-adds unrolled without
-// branches; targets outside [t0, t1) or inside the own range compute on zero weights and
-// are not stored
+// H sources, compile-time.  The block's source residues are loaded FIRST, then the weight
+// tables staged in LDS behind the barrier: the two memory latencies overlap instead of the
+// residue loads waiting for the table loads and the barrier.  Targets outside [t0, t1) or
+// inside the own range compute on zero weights and are not stored
+__device__ __forceinline__ void conv_stage(const ConvBatch& cb, int gi, int h, int d0, int t0, int t1, int nt, LimbMap map,
+                                           const PrimeConst* pc, u32 (*s_w)[kMaxConvH], u32 (*s_tq)[4], u32 (*s_src)[4]) {
+    const int tid = threadIdx.x;
+    for (int x = tid; x < kConvTargets * kMaxConvH; x += kBlock) {
+        const int tl = x / kMaxConvH, i = x % kMaxConvH, t = t0 + tl;
+        s_w[tl][i] = (i < h && t < t1) ? cb.tab[gi][2 * ((size_t)i * nt + t)] : 0u;
+    }
+    for (int tl = tid; tl < kConvTargets; tl += kBlock) {
+        const int t = t0 + tl;
+        if (t < t1) {
+            const PrimeConst P = pc[map.prime(t)];
+            s_tq[tl][0] = P.q, s_tq[tl][1] = P.mu, s_tq[tl][2] = P.r32, s_tq[tl][3] = cb.negq[gi][t];
+        }
+    }
+    for (int i = tid; i < h; i += kBlock) {
+        const int sp = cb.split[gi];
+        const PrimeConst P = pc[(sp > 0 && i >= sp) ? cb.d1[gi] + (i - sp) : d0 + i];
+        s_src[i][0] = P.q, s_src[i][1] = P.mu, s_src[i][2] = cb.qhinv[gi][2 * i], s_src[i][3] = cb.qhinv[gi][2 * i + 1];
+    }
+}
 template <int H>
-__device__ __forceinline__ void conv_body(const u32* __restrict__ x, u32* __restrict__ ext, size_t k, int t0, int t1, int skip0,
-                                          int logn, const u32 (*s_w)[kMaxConvH], const u32 (*s_tq)[4], const u32 (*s_src)[4]) {
+__device__ __forceinline__ void conv_body(const ConvBatch& cb, int gi, int t0, int t1, int nt, LimbMap map, const PrimeConst* pc, int logn,
+                                          u32 (*s_w)[kMaxConvH], u32 (*s_tq)[4], u32 (*s_src)[4]) {
+    const u32* __restrict__ x = cb.src[gi];
+    u32* __restrict__ ext = cb.dst[gi];
+    const int skip0 = cb.skip0[gi];
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
     u32 y[H];
 #pragma unroll
     for (int i = 0; i < H; ++i) y[i] = x[((size_t)i << logn) + k];
+    conv_stage(cb, gi, H, cb.d0[gi], t0, t1, nt, map, pc, s_w, s_tq, s_src);
+    __syncthreads();
     u64 f = 0;
 #pragma unroll
     for (int i = 0; i < H; ++i) {
@@ -258,35 +285,16 @@ __device__ __forceinline__ void conv_body(const u32* __restrict__ x, u32* __rest
 __global__ void __launch_bounds__(kBlock) k_base_convert(ConvBatch cb, int nt, LimbMap map, const PrimeConst* pc, int logn,
                                                          unsigned long long* ts) {
     const int gi = blockIdx.z;
-    const int h = cb.h[gi], d0 = cb.d0[gi], skip0 = cb.skip0[gi];
+    const int h = cb.h[gi], skip0 = cb.skip0[gi];
     const int t0 = blockIdx.y * kConvTargets, t1 = min(t0 + kConvTargets, nt);
     if (t0 >= skip0 && t1 <= skip0 + h) return;  // chunk entirely inside the own range
     ts_begin(ts);
     __shared__ u32 s_w[kConvTargets][kMaxConvH];
     __shared__ u32 s_tq[kConvTargets][4];  // q, mu, r32, -Q mod q
     __shared__ u32 s_src[kMaxConvH][4];    // q, mu, qhat^-1, Shoup companion
-    const int tid = threadIdx.x;
-    for (int x = tid; x < kConvTargets * kMaxConvH; x += kBlock) {
-        const int tl = x / kMaxConvH, i = x % kMaxConvH, t = t0 + tl;
-        s_w[tl][i] = (i < h && t < t1) ? cb.tab[gi][2 * ((size_t)i * nt + t)] : 0u;
-    }
-    for (int tl = tid; tl < kConvTargets; tl += kBlock) {
-        const int t = t0 + tl;
-        if (t < t1) {
-            const PrimeConst P = pc[map.prime(t)];
-            s_tq[tl][0] = P.q, s_tq[tl][1] = P.mu, s_tq[tl][2] = P.r32, s_tq[tl][3] = cb.negq[gi][t];
-        }
-    }
-    for (int i = tid; i < h; i += kBlock) {
-        const int sp = cb.split[gi];
-        const PrimeConst P = pc[(sp > 0 && i >= sp) ? cb.d1[gi] + (i - sp) : d0 + i];
-        s_src[i][0] = P.q, s_src[i][1] = P.mu, s_src[i][2] = cb.qhinv[gi][2 * i], s_src[i][3] = cb.qhinv[gi][2 * i + 1];
-    }
-    __syncthreads();
-    const size_t k = (size_t)blockIdx.x * kBlock + tid;
     switch (h) {
 #define CONV_CASE(H) \
-    case H: conv_body<H>(cb.src[gi], cb.dst[gi], k, t0, t1, skip0, logn, s_w, s_tq, s_src); break;
+    case H: conv_body<H>(cb, gi, t0, t1, nt, map, pc, logn, s_w, s_tq, s_src); break;
         CONV_CASE(1) CONV_CASE(2) CONV_CASE(3) CONV_CASE(4) CONV_CASE(5) CONV_CASE(6) CONV_CASE(7) CONV_CASE(8)
         CONV_CASE(9) CONV_CASE(10) CONV_CASE(11) CONV_CASE(12) CONV_CASE(13) CONV_CASE(14) CONV_CASE(15) CONV_CASE(16)
 #undef CONV_CASE

@@ -23,6 +23,7 @@
 //
 // Rows of one launch are addressed through a RowMap (out-of-place, strided groups), so
 // callers never copy limbs around just to transform them.
+#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
 
@@ -108,6 +109,42 @@ __device__ __forceinline__ RowAddr row_addr(u32* dst, const u32* src, const RowM
     return a;
 }
 
+// pass 1's butterflies on the 16 elements a thread loaded (rows g + T k of its column), the LDS
+// regroup and the store of rows 16 g + k (dst = the limb's first word of the column)
+template <int LOGR1, int NT>
+__device__ __forceinline__ void ntt1_fwd_stages(u32 (&x)[16], u32* sm, const uint2* w, u32 q, u32 q2, int g, int col, u32* dst) {
+    constexpr int R1 = 1 << LOGR1, T = R1 / 16, CB = NT / T;
+    // stages 0..3: row distance R1 / 2^(s+1) = T * (8 >> s); block index k >> (4 - s)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int h = 8 >> s;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!(k & h)) {
+                const int ti = (1 << s) + (k >> (4 - s));
+                ct_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, q);
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) sm[(g + T * k) * CB + col] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = sm[(16 * g + k) * CB + col];
+    // stages 4..LOGR1-1 on rows 16 g + k
+#pragma unroll
+    for (int s = 4; s < LOGR1; ++s) {
+        const int h = 1 << (LOGR1 - 1 - s);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!(k & h)) {
+                const int ti = (1 << s) + ((16 * g + k) >> (LOGR1 - s));
+                ct_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, q);
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) dst[(size_t)(16 * g + k) * 256] = x[k];
+}
+
 // ---------------------------------------------------------------- forward, pass 1
 // MODE kPlain: x = src row.  MODE kSpread (rescale): the source is one coefficient-form
 // row per group modulo aux.q_last (src row = src_off + g * src_stride, independent of the
@@ -161,35 +198,64 @@ __global__ void __launch_bounds__(NT) k_ntt1_fwd(u32* dst, const u32* src, RowMa
 #pragma unroll
         for (int k = 0; k < 16; ++k) x[k] = ra.src[(size_t)(g + T * k) * 256 + c];
     }
-    // stages 0..3: row distance R1 / 2^(s+1) = T * (8 >> s); block index k >> (4 - s)
+    ntt1_fwd_stages<LOGR1, NT>(x, sm, w, q, q2, g, col, ra.dst + c);
+    ts_end(ts);
+}
+
+// ---------------------------------------------------------------- forward, pass 1 fused with the base conversion
+// The ModUp / ModDown conversion (kernels.hip k_base_convert, same arithmetic in the same order,
+// so bit for bit its values) computed in pass 1's load instead of a separate launch: row t of
+// group z (blockIdx.y / .z, the RowMap's) is target t of ConvBatch group z; every element reads
+// the group's H source residues at its position (y_i, the INTT having already multiplied by
+// qhat_i^{-1}: launch_ntt_inv's `post`), u = round(sum y_i / q_i), and
+// x = (u (-Q mod q_t) + sum y_i (Q / q_i mod q_t)) mod q_t.  Saves the converted rows' write
+// and re-read and one launch per ModUp / ModDown.
+template <int LOGR1, int NT, int H>
+__global__ void __launch_bounds__(NT) k_ntt1_fwd_conv(u32* dst, RowMap rm, LimbMap map, const PrimeConst* pc, const uint2* tw, ConvBatch cb,
+                                                            unsigned long long* ts) {
+    constexpr int LOGN = LOGR1 + 8, R1 = 1 << LOGR1, T = R1 / 16, CB = NT / T;
+    __shared__ u32 sm[R1 * CB];
+    if (skipped(rm)) return;
+    ts_begin(ts);
+    const int z = blockIdx.z, t = blockIdx.y, nt = rm.cnt;
+    const RowAddr ra = row_addr<LOGN>(dst, dst, rm, map);
+    const PrimeConst P = pc[ra.prime];
+    const u32 q = P.q, q2 = 2 * q;
+    const uint2* w = tw + ((size_t)ra.prime << LOGN);
+    const int col = threadIdx.x % CB, g = threadIdx.x / CB;
+    const int c = blockIdx.x * CB + col;
+    const u32* tab = cb.tab[z];
+    const int sp = cb.split[z], hz = cb.h[z];
+    // H = the launch's largest source count; a group with fewer sources (ModUp's last digit)
+    // runs with zero weights on the missing ones (and re-reads its last row: no branch)
+    u32 wt[H], ms[H];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        const int h = 8 >> s;
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if (!(k & h)) {
-                const int ti = (1 << s) + (k >> (4 - s));
-                ct_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, q);
-            }
+    for (int i = 0; i < H; ++i) {
+        wt[i] = i < hz ? tab[2 * ((size_t)i * nt + t)] : 0u;
+        ms[i] = i < hz ? pc[(sp > 0 && i >= sp) ? cb.d1[z] + (i - sp) : cb.d0[z] + i].mu : 0u;
     }
+    const u32 negq = cb.negq[z][t];
+    const u32* src = cb.src[z];
+    u32 x[16];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) sm[(g + T * k) * CB + col] = x[k];
-    __syncthreads();
+    for (int k = 0; k < 16; ++k) {
+        const size_t at = (size_t)(g + T * k) * 256 + c;
+        u32 y[H];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) x[k] = sm[(16 * g + k) * CB + col];
-    // stages 4..LOGR1-1 on rows 16 g + k
+        for (int i = 0; i < H; ++i) y[i] = src[((size_t)min(i, hz - 1) << LOGN) + at];
+        u64 f = 0;
 #pragma unroll
-    for (int s = 4; s < LOGR1; ++s) {
-        const int h = 1 << (LOGR1 - 1 - s);
+        for (int i = 0; i < H; ++i) f += ((u64)y[i] * ms[i]) >> 29;  // y_i / q_i in 32.32 fixed point
+        const u32 u = (u32)((f + (1ull << 31)) >> 32);
+        u64 acc = (u64)u * negq;
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if (!(k & h)) {
-                const int ti = (1 << s) + ((16 * g + k) >> (LOGR1 - s));
-                ct_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, q);
-            }
+        for (int i = 0; i < H; ++i) {
+            if (i == 8) acc = fold64(acc, q, P.r32);
+            acc += (u64)y[i] * wt[i];
+        }
+        x[k] = reduce64(acc, q, P.mu, P.r32);
     }
-#pragma unroll
-    for (int k = 0; k < 16; ++k) ra.dst[(size_t)(16 * g + k) * 256 + c] = x[k];
+    ntt1_fwd_stages<LOGR1, NT>(x, sm, w, q, q2, g, col, ra.dst + c);
     ts_end(ts);
 }
 
@@ -348,7 +414,7 @@ __global__ void __launch_bounds__(NT) k_ntt2_inv(u32* dst, const u32* src, RowMa
 // ---------------------------------------------------------------- inverse, pass 1 (in place on dst rows)
 template <int LOGR1, int NT>
 __global__ void __launch_bounds__(NT) k_ntt1_inv(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const uint2* tw,
-                                                       unsigned long long* ts) {
+                                                       const u32* post, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8, R1 = 1 << LOGR1, T = R1 / 16, CB = NT / T;
     __shared__ u32 sm[R1 * CB];
     if (skipped(rm)) return;
@@ -387,8 +453,14 @@ __global__ void __launch_bounds__(NT) k_ntt1_inv(u32* data, RowMap rm, LimbMap m
                 gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, 0u - q);
             }
     }
+    if (post) {  // then times post[row] (a base conversion's qhat^{-1}: k_ntt1_fwd_conv)
+        const u32 pw = post[2 * blockIdx.y], pwp = post[2 * blockIdx.y + 1];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) ra.dst[(size_t)(g + T * k) * 256 + c] = shoup_mul(x[k], P.ninv, P.ninv_p, q);
+        for (int k = 0; k < 16; ++k) ra.dst[(size_t)(g + T * k) * 256 + c] = shoup_mul(shoup_mul(x[k], P.ninv, P.ninv_p, q), pw, pwp, q);
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) ra.dst[(size_t)(g + T * k) * 256 + c] = shoup_mul(x[k], P.ninv, P.ninv_p, q);
+    }
     ts_end(ts);
 }
 
@@ -438,7 +510,7 @@ void ntt2_inv_launch(hipStream_t st, const DevTables& Tb, u32* dst, const u32* s
                         Tb.irow, Tb.igam);
 }
 template <int LOGR1>
-void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {
+void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map, const u32* post) {
     constexpr int R1 = 1 << LOGR1;
     rm.nrows = rows;
     const int groups = (rows + rm.cnt - 1) / rm.cnt;
@@ -448,16 +520,94 @@ void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
         constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
         ntt2_inv_launch<LOGR1, NT>(st, Tb, dst, src, rm, map, groups, io, bfly * 8.0);
         prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, dst, rm, map,
-                        Tb.pc, Tb.itw);
+                        Tb.pc, Tb.itw, post);
         return;
     }
     constexpr int CB = kThreads / (R1 / 16);
     ntt2_inv_launch<LOGR1, kThreads>(st, Tb, dst, src, rm, map, groups, io, bfly * 8.0);
     prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, kThreads>, dim3(256 / CB, rm.cnt, groups), dim3(kThreads), 0, st, dst, rm,
-                    map, Tb.pc, Tb.itw);
+                    map, Tb.pc, Tb.itw, post);
+}
+
+// pass 1 fused with the base conversion (k_ntt1_fwd_conv), then pass 2 in mode M2
+template <int LOGR1, int NT, int H>
+void ntt1_conv_launch(hipStream_t st, const DevTables& Tb, u32* dst, const ConvBatch& cb, RowMap rm, LimbMap map, int groups, double io,
+                      double work) {
+    constexpr int CB = NT / ((1 << LOGR1) / 16);
+    prof_launch_tsw(KID_NTT_COLS_FWD, io, work, k_ntt1_fwd_conv<LOGR1, NT, H>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, dst, rm, map,
+                    Tb.pc, Tb.tw, cb);
+}
+template <int LOGR1, int NT>
+void ntt1_conv_dispatch(hipStream_t st, const DevTables& Tb, u32* dst, const ConvBatch& cb, int h, RowMap rm, LimbMap map, int groups,
+                        double io, double work) {
+    switch (h) {
+#define CONV_H(H) \
+    case H: ntt1_conv_launch<LOGR1, NT, H>(st, Tb, dst, cb, rm, map, groups, io, work); break;
+        CONV_H(1) CONV_H(2) CONV_H(3) CONV_H(4) CONV_H(5) CONV_H(6) CONV_H(7) CONV_H(8)
+        CONV_H(9) CONV_H(10) CONV_H(11) CONV_H(12) CONV_H(13) CONV_H(14) CONV_H(15) CONV_H(16)
+#undef CONV_H
+        default: throw std::runtime_error("ntt_fwd_conv: unsupported source count");
+    }
+}
+template <int M2>
+void ntt_fwd_conv_t(hipStream_t st, const DevTables& Tb, u32* dst, const ConvBatch& cb, int rows, int io_rows, RowMap rm, LimbMap map,
+                    const NttAux& aux) {
+    constexpr int LOGR1 = 8, R1 = 1 << LOGR1;
+    rm.nrows = rows;
+    const int groups = (rows + rm.cnt - 1) / rm.cnt;
+    if (groups != cb.n) throw std::runtime_error("ntt_fwd_conv: one conversion group per row group expected");
+    int h = 0, src_rows = 0;
+    for (int z = 0; z < cb.n; ++z) {
+        if (cb.h[z] < 1) throw std::runtime_error("ntt_fwd_conv: a conversion group without sources");
+        h = std::max(h, cb.h[z]);
+        src_rows += cb.h[z];
+    }
+    const double row_bytes = 4.0 * 256.0 * R1;
+    const double io1 = (double)(io_rows + src_rows) * row_bytes;  // sources read once, converted rows written
+    const double io2 = (M2 == kFinish ? (3.0 + (aux.add0 ? 0.5 : 0.0) + (aux.add1 ? 0.5 : 0.0)) : 2.0) * io_rows * row_bytes;
+    const double bfly = (double)io_rows * 128.0 * R1;
+    if (small_launch(rows)) {
+        constexpr int NT = kThreads / 2;
+        ntt1_conv_dispatch<LOGR1, NT>(st, Tb, dst, cb, h, rm, map, groups, io1, bfly * LOGR1);
+        prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2, NT>, dim3(R1 / (NT / 16), rm.cnt, groups), dim3(NT), 0, st, dst,
+                        rm, map, Tb.pc, Tb.tw, aux);
+        return;
+    }
+    ntt1_conv_dispatch<LOGR1, kThreads>(st, Tb, dst, cb, h, rm, map, groups, io1, bfly * LOGR1);
+    prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2, kThreads>, dim3(R1 / kRowsP2, rm.cnt, groups), dim3(kThreads), 0, st,
+                    dst, rm, map, Tb.pc, Tb.tw, aux);
 }
 
 }  // namespace
+
+int ntt_conv_fused_mask(const DevTables& T) {
+    static const int m = [] {
+        const char* e = std::getenv("AESFHE_FUSED_CONV");
+        return e ? std::atoi(e) : 0;
+    }();
+    return T.logn == 16 ? m : 0;
+}
+void launch_ntt_fwd_conv(hipStream_t st, const DevTables& T, u32* dst, const ConvBatch& cb, int rows, RowMap rm, LimbMap map) {
+    if (rows <= 0) return;
+    int io_rows = rows;
+    if (rm.skip_alpha > 0)
+        for (int y = 0; y < rows; ++y) {
+            const int g = y / rm.cnt, i = y - g * rm.cnt;
+            if (i < rm.skip_nl && i / rm.skip_alpha == (rm.skip_groups > 0 ? g % rm.skip_groups : g)) --io_rows;
+        }
+    ntt_fwd_conv_t<kPlain>(st, T, dst, cb, rows, io_rows, rm, map, NttAux{});
+}
+void launch_ntt_finish_conv(hipStream_t st, const DevTables& T, u32* out, u32* conv, const ConvBatch& cb, const u32* cur, int cur_stride,
+                            const u32* qinv, const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride, u32* const* outm) {
+    NttAux aux{};
+    aux.cur = cur, aux.out = out, aux.qinv = qinv, aux.cur_stride = cur_stride, aux.out_stride = nt, aux.add0 = add0, aux.add1 = add1;
+    aux.add_mstride = add_mstride;
+    if (outm) {
+        if (npoly > 16 || npoly % 2) throw std::runtime_error("launch_ntt_finish: per-member outputs for at most 8 two-polynomial members");
+        for (int m = 0; m < npoly / 2; ++m) aux.outm[m] = outm[m];
+    }
+    ntt_fwd_conv_t<kFinish>(st, T, conv, cb, npoly * nt, npoly * nt, rows_dense(nt), LimbMap{1 << 30, 0, 0}, aux);
+}
 
 template <int M1, int M2>
 void ntt_fwd_dispatch(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, int io_rows, RowMap rm, LimbMap map,
@@ -507,13 +657,13 @@ void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, 
     }
     ntt_fwd_dispatch<kPlain, kFinish>(st, T, conv, conv, npoly * nt, npoly * nt, rows_dense(nt), LimbMap{1 << 30, 0, 0}, aux);
 }
-void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {
+void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map, const u32* post) {
     if (rows <= 0) return;
     switch (T.logn) {
-        case 13: ntt_inv_t<5>(st, T, dst, src, rows, rm, map); break;
-        case 14: ntt_inv_t<6>(st, T, dst, src, rows, rm, map); break;
-        case 15: ntt_inv_t<7>(st, T, dst, src, rows, rm, map); break;
-        case 16: ntt_inv_t<8>(st, T, dst, src, rows, rm, map); break;
+        case 13: ntt_inv_t<5>(st, T, dst, src, rows, rm, map, post); break;
+        case 14: ntt_inv_t<6>(st, T, dst, src, rows, rm, map, post); break;
+        case 15: ntt_inv_t<7>(st, T, dst, src, rows, rm, map, post); break;
+        case 16: ntt_inv_t<8>(st, T, dst, src, rows, rm, map, post); break;
         default: break;
     }
 }

@@ -21,7 +21,7 @@ from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1
 
 # AESFHE_SHARE_R1=0: MixColumns' r1 basis rebuilt in its second XOR4 (A/B runs)
 _SHARE_R1 = os.environ.get("AESFHE_SHARE_R1", "1") != "0"
-_FHE_FORK = os.environ.get("AESFHE_FHE_FORK", "1") != "0"  # true-FHE MixColumns halves on two streams (A/B)
+_FHE_FORK = os.environ.get("AESFHE_FHE_FORK", "0") == "1"  # true-FHE MixColumns halves forced onto two streams (A/B: no gain measured)
 
 
 class _CoeffCache:

@@ -56,7 +56,9 @@ def gpu_engine(log_n=16, max_level=17, dnum=3, seed=0x5EED):
     if key not in _engines:
         from mi355x_ckks import Engine
         # parity-test sets: the N = 2^13 one is far above the 128-bit bound (bit-exactness only)
-        _engines[key] = Engine(log_n=log_n, max_level=max_level, dnum=dnum, seed=seed, allow_insecure=True)
+        # the encryption nonce pinned too: a test's noise (and so its error margins) is the same
+        # in every run instead of a fresh draw per process
+        _engines[key] = Engine(log_n=log_n, max_level=max_level, dnum=dnum, seed=seed, allow_insecure=True, enc_nonce=seed)
     return _engines[key]
 
 
@@ -67,5 +69,5 @@ def gpu_context(log_n=16, signature=2, max_level=17, seed=0x5EED):
     key = (log_n, signature, max_level, seed)
     if key not in _contexts:
         from engine_context import EngineContext
-        _contexts[key] = EngineContext(signature=signature, max_level=max_level, thread_count=4, log_n=log_n, seed=seed)
+        _contexts[key] = EngineContext(signature=signature, max_level=max_level, thread_count=4, log_n=log_n, seed=seed, enc_nonce=seed)
     return _contexts[key]

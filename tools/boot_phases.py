@@ -1,0 +1,49 @@
+"""Phase breakdown of the sparse-slot bootstrap (C2's MixColumns final bootstrap: one packed
+ciphertext, period P = 32): wall time (synchronised) and kernel launches of the bootstrap run up
+to each debug stage (aesfhe_debug_boot_stage_sparse), and the per-phase differences.
+usage: python tools/boot_phases.py [P] > out.json"""
+import json
+import sys
+import time
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(ROOT), str(ROOT / "aes-implementation-fhe_amd")]
+
+from engine_context import EngineContext  # noqa: E402
+from mi355x_ckks import launch_count  # noqa: E402
+
+# stop_after codes of bootstrap_l0 (engine.hip) in execution order, packed sparse form
+STAGES = [(1, "level-0 scaling"), (2, "dense->sparse key switch"), (3, "ModRaise"), (12, "sparse->dense key switch"),
+          (4, "trace to the subring"), (5, "CoeffToSlot"), (9, "conjugate fold"), (10, "EvalMod"), (99, "SlotToCoeff + level drop")]
+
+
+def main():
+    P = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+    reps = 5
+    ctx = EngineContext(signature=1, max_level=17)
+    E = ctx.engine
+    z = np.exp(2j * np.pi * np.random.default_rng(0).random(P))
+    ct = E.intt(ctx.encrypt(np.tile(z, E.slot_count // P)))
+    cum = {}
+    for code, name in STAGES:
+        run = (lambda: E.bootstrap_sparse(ct, P)) if code == 99 else (lambda: E.debug_boot_stage_sparse(ct, code, P))
+        run()
+        E.sync()
+        t, n0 = time.perf_counter(), launch_count()
+        for _ in range(reps):
+            run()
+        E.sync()
+        cum[name] = ((time.perf_counter() - t) * 1e3 / reps, (launch_count() - n0) / reps)
+    out, prev = {}, (0.0, 0.0)
+    for _, name in STAGES:
+        ms, ln = cum[name]
+        out[name] = {"ms": round(ms - prev[0], 3), "launches": ln - prev[1], "cumulative_ms": round(ms, 3)}
+        prev = (ms, ln)
+    print(json.dumps({"period": P, "reps": reps, "phases": out}, indent=1))
+
+
+if __name__ == "__main__":
+    main()

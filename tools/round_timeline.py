@@ -81,13 +81,20 @@ def analyse(out, d):
         fam[n][0] += 1
         fam[n][1] += e - s
         queues[q] += e - s
-    for s, e, _, _ in sel[1:]:
+    last = sel[0][2]  # the kernel whose end closes the busy interval
+    by_pair = defaultdict(lambda: [0, 0])
+    for s, e, n, _ in sel[1:]:
         if s > ce:
             busy += ce - cs
             gaps.append(s - ce)
+            if s - ce >= 20_000:  # idle >= 20 us: which kernels it sits between
+                k = f"{last} -> {n}"
+                by_pair[k][0] += 1
+                by_pair[k][1] += s - ce
             cs, ce = s, e
-        else:
-            ce = max(ce, e)
+            last = n
+        elif e >= ce:
+            ce, last = e, n
     busy += ce - cs
     span = max(e for _, e, _, _ in sel) - sel[0][0]
     hist = {}
@@ -99,6 +106,8 @@ def analyse(out, d):
         "kernel_sum_ms": total / 1e6, "mean_concurrency_when_busy": total / busy,
         "gaps": hist,
         "per_queue_ms": {k: v / 1e6 for k, v in queues.items()},
+        "gaps_over_20us_by_neighbours": {k: {"count": v[0], "ms": round(v[1] / 1e6, 3)}
+                                         for k, v in sorted(by_pair.items(), key=lambda kv: -kv[1][1])[:25]},
         "families": {k: {"calls": v[0], "ms": round(v[1] / 1e6, 3), "avg_us": round(v[1] / v[0] / 1e3, 2)}
                      for k, v in sorted(fam.items(), key=lambda kv: -kv[1][1])},
     }
