@@ -125,20 +125,30 @@ __device__ __forceinline__ void ntt1_fwd_stages(u32 (&x)[16], u32* sm, const uin
                 ct_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, q);
             }
     }
+    // the twiddles of stages 4..LOGR1-1 (2^(s+4-LOGR1) per stage and thread) loaded BEFORE the
+    // barrier: their latency overlaps the exchange instead of following it
+    constexpr int C4 = 1 << (8 - LOGR1), NB = 16 - C4;
+    uint2 tb[NB > 0 ? NB : 1];
+#pragma unroll
+    for (int s = 4; s < LOGR1; ++s) {
+        const int c = 1 << (s + 4 - LOGR1), base = (1 << s) + (g << (s + 4 - LOGR1));
+#pragma unroll
+        for (int u = 0; u < c; ++u) tb[c - C4 + u] = w[base + u];
+    }
 #pragma unroll
     for (int k = 0; k < 16; ++k) sm[(g + T * k) * CB + col] = x[k];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 16; ++k) x[k] = sm[(16 * g + k) * CB + col];
-    // stages 4..LOGR1-1 on rows 16 g + k
+    // stages 4..LOGR1-1 on rows 16 g + k: twiddle (1 << s) + ((16 g + k) >> (LOGR1 - s))
 #pragma unroll
     for (int s = 4; s < LOGR1; ++s) {
-        const int h = 1 << (LOGR1 - 1 - s);
+        const int h = 1 << (LOGR1 - 1 - s), c = 1 << (s + 4 - LOGR1);
 #pragma unroll
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
-                const int ti = (1 << s) + ((16 * g + k) >> (LOGR1 - s));
-                ct_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, q);
+                const uint2 t = tb[c - C4 + (k >> (LOGR1 - s))];
+                ct_bfly(x[k], x[k + h], t.x, t.y, q2, q);
             }
     }
 #pragma unroll
@@ -291,6 +301,32 @@ __global__ void __launch_bounds__(NT) k_ntt2_fwd(u32* data, RowMap rm, LimbMap m
                 ct_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, q);
             }
     }
+    // phase B's twiddles (stage s: 2^(s-4) per thread, word 16 j + k -> offset k >> (8 - s)) and,
+    // in the finish mode, the cur / add rows loaded BEFORE the barrier (latency overlapped)
+    uint2 tb[15];
+#pragma unroll
+    for (int s = 4; s < 8; ++s) {
+        const int c = 1 << (s - 4), base = (1 << (LOGR1 + s)) + (R << s) + (j << (s - 4));
+#pragma unroll
+        for (int u = 0; u < c; ++u) tb[c - 1 + u] = w[base + u];
+    }
+    uint4 cvp[MODE == kFinish ? 4 : 1], avp[MODE == kFinish ? 4 : 1];
+    bool has_add = false;
+    if (MODE == kFinish) {
+        const int grp = blockIdx.z, li = blockIdx.y;
+        const size_t woff = (size_t)R * 256 + 16 * j;
+        const uint4* cu = reinterpret_cast<const uint4*>(aux.cur + ((size_t)(grp * aux.cur_stride + li) << LOGN) + woff);
+        const u32* addp = (grp & 1) ? aux.add1 : aux.add0;
+        if (grp > 1) addp = (addp && aux.add_mstride) ? addp + (grp >> 1) * aux.add_mstride : nullptr;
+        has_add = addp != nullptr;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) cvp[v] = cu[v];
+        if (has_add) {
+            const uint4* ad = reinterpret_cast<const uint4*>(addp + ((size_t)li << LOGN) + woff);
+#pragma unroll
+            for (int v = 0; v < 4; ++v) avp[v] = ad[v];
+        }
+    }
     u32* row = sm + r * kPitchP2;
 #pragma unroll
     for (int k = 0; k < 16; ++k) row[swz(j + 16 * k)] = x[k];
@@ -299,13 +335,12 @@ __global__ void __launch_bounds__(NT) k_ntt2_fwd(u32* data, RowMap rm, LimbMap m
     for (int k = 0; k < 16; ++k) x[k] = row[swz(16 * j + k)];
 #pragma unroll
     for (int s = 4; s < 8; ++s) {
-        const int h = 1 << (7 - s);
-        const int base = (1 << (LOGR1 + s)) + (R << s);
+        const int h = 1 << (7 - s), c = 1 << (s - 4);
 #pragma unroll
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
-                const int ti = base + ((16 * j + k) >> (8 - s));
-                ct_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, q);
+                const uint2 t = tb[c - 1 + (k >> (8 - s))];  // twiddle base + ((16 j + k) >> (8 - s))
+                ct_bfly(x[k], x[k + h], t.x, t.y, q2, q);
             }
     }
 #pragma unroll
@@ -313,24 +348,20 @@ __global__ void __launch_bounds__(NT) k_ntt2_fwd(u32* data, RowMap rm, LimbMap m
     if (MODE == kFinish) {
         const int grp = blockIdx.z, li = blockIdx.y;
         const size_t woff = (size_t)R * 256 + 16 * j;
-        const uint4* cu = reinterpret_cast<const uint4*>(aux.cur + ((size_t)(grp * aux.cur_stride + li) << LOGN) + woff);
-        const u32* addp = (grp & 1) ? aux.add1 : aux.add0;
-        if (grp > 1) addp = (addp && aux.add_mstride) ? addp + (grp >> 1) * aux.add_mstride : nullptr;
-        const uint4* ad = addp ? reinterpret_cast<const uint4*>(addp + ((size_t)li << LOGN) + woff) : nullptr;
         u32* const om = aux.outm[(grp >> 1) & 7];
         uint4* o = reinterpret_cast<uint4*>((om ? om + ((size_t)((grp & 1) * aux.out_stride + li) << LOGN)
                                                : aux.out + ((size_t)(grp * aux.out_stride + li) << LOGN)) + woff);
         const u32 qi = aux.qinv[2 * li], qip = aux.qinv[2 * li + 1];
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
-            const uint4 cv = cu[v];
+            const uint4 cv = cvp[v];
             uint4 r;
             r.x = shoup_mul(cv.x + q - x[4 * v], qi, qip, q);
             r.y = shoup_mul(cv.y + q - x[4 * v + 1], qi, qip, q);
             r.z = shoup_mul(cv.z + q - x[4 * v + 2], qi, qip, q);
             r.w = shoup_mul(cv.w + q - x[4 * v + 3], qi, qip, q);
-            if (ad) {
-                const uint4 a = ad[v];
+            if (has_add) {
+                const uint4 a = avp[v];
                 r.x = add_mod(r.x, a.x, q), r.y = add_mod(r.y, a.y, q), r.z = add_mod(r.z, a.z, q), r.w = add_mod(r.w, a.w, q);
             }
             o[v] = r;
@@ -388,6 +419,14 @@ __global__ void __launch_bounds__(NT) k_ntt2_inv(u32* dst, const u32* src, RowMa
                 gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, 0u - q);
             }
     }
+    // stages 3..0's twiddles (2^s per thread) loaded before the barrier
+    uint2 tb[15];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int base = (1 << (LOGR1 + s)) + (R << s);
+#pragma unroll
+        for (int u = 0; u < (1 << s); ++u) tb[(1 << s) - 1 + u] = w[base + u];
+    }
     u32* row = sm + r * kPitchP2;
 #pragma unroll
     for (int k = 0; k < 16; ++k) row[swz(16 * j + k)] = x[k];
@@ -397,12 +436,11 @@ __global__ void __launch_bounds__(NT) k_ntt2_inv(u32* dst, const u32* src, RowMa
 #pragma unroll
     for (int s = 3; s >= 0; --s) {
         const int h = 8 >> s;
-        const int base = (1 << (LOGR1 + s)) + (R << s);
 #pragma unroll
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
-                const int ti = base + (k >> (4 - s));
-                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, 0u - q);
+                const uint2 t = tb[(1 << s) - 1 + (k >> (4 - s))];  // twiddle base + (k >> (4 - s))
+                gs_bfly(x[k], x[k + h], t.x, t.y, q2, 0u - q);
             }
     }
     u32* p = ra.dst + (size_t)R * 256;
@@ -438,6 +476,9 @@ __global__ void __launch_bounds__(NT) k_ntt1_inv(u32* data, RowMap rm, LimbMap m
                 gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, 0u - q);
             }
     }
+    uint2 tb[15];  // stages 3..0's twiddles (block-uniform), loaded before the barrier
+#pragma unroll
+    for (int i = 0; i < 15; ++i) tb[i] = w[1 + i];
 #pragma unroll
     for (int k = 0; k < 16; ++k) sm[(16 * g + k) * CB + col] = x[k];
     __syncthreads();
@@ -449,8 +490,8 @@ __global__ void __launch_bounds__(NT) k_ntt1_inv(u32* data, RowMap rm, LimbMap m
 #pragma unroll
         for (int k = 0; k < 16; ++k)
             if (!(k & h)) {
-                const int ti = (1 << s) + (k >> (4 - s));
-                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, 0u - q);
+                const uint2 t = tb[(1 << s) - 1 + (k >> (4 - s))];  // twiddle (1 << s) + (k >> (4 - s))
+                gs_bfly(x[k], x[k + h], t.x, t.y, q2, 0u - q);
             }
     }
     if (post) {  // then times post[row] (a base conversion's qhat^{-1}: k_ntt1_fwd_conv)
