@@ -13,7 +13,7 @@ ROOT = Path(__file__).resolve().parent.parent
 sys.path[:0] = [str(ROOT), str(ROOT / "aes-implementation-fhe_amd")]
 
 from engine_context import EngineContext  # noqa: E402
-from mi355x_ckks import launch_count  # noqa: E402
+from mi355x_ckks import KERNEL_IDS, launch_count  # noqa: E402
 
 # stop_after codes of bootstrap_l0 (engine.hip) in execution order, packed sparse form
 STAGES = [(1, "level-0 scaling"), (2, "dense->sparse key switch"), (3, "ModRaise"), (12, "sparse->dense key switch"),
@@ -27,7 +27,7 @@ def main():
     E = ctx.engine
     z = np.exp(2j * np.pi * np.random.default_rng(0).random(P))
     ct = E.intt(ctx.encrypt(np.tile(z, E.slot_count // P)))
-    cum = {}
+    cum, kcum = {}, {}
     for code, name in STAGES:
         run = (lambda: E.bootstrap_sparse(ct, P)) if code == 99 else (lambda: E.debug_boot_stage_sparse(ct, code, P))
         run()
@@ -37,11 +37,19 @@ def main():
             run()
         E.sync()
         cum[name] = ((time.perf_counter() - t) * 1e3 / reps, (launch_count() - n0) / reps)
-    out, prev = {}, (0.0, 0.0)
+        # launches per kernel class (engine profiler, every launch timed: a separate pass)
+        E.profile(list(KERNEL_IDS), every=1)
+        E.kernel_stats(reset=True)
+        run()
+        E.sync()
+        kcum[name] = {k: v["launches"] for k, v in E.kernel_stats(reset=True).items()}
+        E.profile(())
+    out, prev, kprev = {}, (0.0, 0.0), {}
     for _, name in STAGES:
         ms, ln = cum[name]
-        out[name] = {"ms": round(ms - prev[0], 3), "launches": ln - prev[1], "cumulative_ms": round(ms, 3)}
-        prev = (ms, ln)
+        kc = {k: v - kprev.get(k, 0) for k, v in kcum[name].items() if v - kprev.get(k, 0)}
+        out[name] = {"ms": round(ms - prev[0], 3), "launches": ln - prev[1], "cumulative_ms": round(ms, 3), "by_class": kc}
+        prev, kprev = (ms, ln), kcum[name]
     print(json.dumps({"period": P, "reps": reps, "phases": out}, indent=1))
 
 
