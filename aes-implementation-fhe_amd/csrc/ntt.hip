@@ -4,8 +4,8 @@
 // words.  Forward (Cooley-Tukey, natural -> bit-reversed, psi^{bitrev} twiddles):
 //   pass 1 ("cols"): stages 0..log2(R1)-1, butterflies between rows; a 512-thread block
 //                    owns CB = 512 * 16 / R1 columns of all R1 rows,
-//   pass 2 ("rows"): stages log2(R1)..logn-1 inside each 256-word row; a block owns
-//                    32 rows.
+//   pass 2 ("rows"): stages log2(R1)..logn-1 inside each 256-word row; a block of NT
+//                    threads owns NT / 16 rows (256 threads by default, p2_nt()).
 // Each thread keeps 16 elements in VGPRs.  Phase A holds elements 16 apart (rows
 // g + T k in pass 1, words j + 16 k in pass 2) and runs the first 4 stages in registers;
 // one LDS exchange regroups them into 16 consecutive elements (rows 16 g + k, words
@@ -17,7 +17,7 @@
 // Global access: pass 1 reads/writes 32..256 consecutive columns per row (>= 128 B
 // segments); pass 2's phase-B side moves 16 contiguous words per thread (4 x b128).
 // LDS: pass 1 tile [R1][CB] -- every 32-lane half touches 32 consecutive columns, no
-// conflicts; pass 2 tile [32][272] with the 16-word-group XOR swizzle swz(), conflict-free
+// conflicts; pass 2 tile [NT / 16][272] with the 16-word-group XOR swizzle swz(), conflict-free
 // for both the (j + 16 k) and the (16 j + k) pattern (rows r, r+1 share a half-wave and
 // sit 272 = 16 mod 32 banks apart).
 //
@@ -33,7 +33,6 @@
 namespace {
 
 constexpr int kThreads = 512;
-constexpr int kRowsP2 = 32;
 constexpr int kPitchP2 = 272;
 
 // Harvey's lazy butterflies (every prime < 2^30, so 4q < 2^32): the forward transform keeps
@@ -81,6 +80,31 @@ inline int small_rows_limit() {
     return v;
 }
 inline bool small_launch(int rows) { return rows < small_rows_limit(); }
+// threads per block of the row pass (pass 2) for launches of >= small_rows_limit() rows, forward
+// (AESFHE_NTT_P2_NT) and inverse (AESFHE_NTT_P2I_NT): 512, 256 or 128 (NT / 16 rows per block).
+// Smaller blocks spread a launch of a few hundred blocks more evenly over the 256 CUs (a block is
+// ~2.3 us of VALU work; at 512 threads a 40-row launch leaves 64 CUs with two blocks and 192
+// with one), while pass 1 keeps its 512-thread blocks' 128-byte column segments
+inline int p2_nt(bool inverse) {
+    static const int f = [] {
+        const char* e = std::getenv("AESFHE_NTT_P2_NT");
+        return e ? std::atoi(e) : 256;
+    }();
+    static const int i = [] {
+        const char* e = std::getenv("AESFHE_NTT_P2I_NT");
+        return e ? std::atoi(e) : 256;
+    }();
+    return inverse ? i : f;
+}
+// AESFHE_NTT_FIN_OCC=1: the finish mode capped at 128 VGPRs (A/B runs; off: with 256-thread row
+// blocks the cap's spills cost more than the extra wave per SIMD gains, profiles/r3_ntt_p2_ab.json)
+inline bool fin_occ_on() {
+    static const bool v = [] {
+        const char* e = std::getenv("AESFHE_NTT_FIN_OCC");
+        return e && std::atoi(e) != 0;
+    }();
+    return v;
+}
 template <int LOGR1>
 constexpr int R1_of() { return 1 << LOGR1; }
 
@@ -273,8 +297,11 @@ __global__ void __launch_bounds__(NT) k_ntt1_fwd_conv(u32* dst, RowMap rm, LimbM
 // MODE kPlain: result stored in place.  MODE kFinish (rescale / ModDown): with
 // g = group, i = limb, out[g][i] = (cur[g][i] - x) * qinv_i (+ add_g[i]), rows addressed
 // through aux (cur row g * cur_stride + i, out row g * out_stride + i).
-template <int LOGR1, int MODE, int NT>
-__global__ void __launch_bounds__(NT) k_ntt2_fwd(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const uint2* tw,
+// OCC: minimum waves per SIMD the register allocation must allow.  The finish mode's prefetched
+// cur / add operands take it to 130 VGPRs unconstrained (3 waves per SIMD); OCC = 4 caps it at
+// 128 with 6 dwords spilled (AESFHE_NTT_FIN_OCC, off by default)
+template <int LOGR1, int MODE, int NT, int OCC = 1>
+__global__ void __launch_bounds__(NT, OCC) k_ntt2_fwd(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const uint2* tw,
                                                        NttAux aux, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8;
     __shared__ u32 sm[(NT / 16) * kPitchP2];
@@ -505,6 +532,27 @@ __global__ void __launch_bounds__(NT) k_ntt1_inv(u32* data, RowMap rm, LimbMap m
     ts_end(ts);
 }
 
+// pass 2 (rows) with NT threads per block; AESFHE_NTT_FIN_OCC=1 caps the finish mode at 128 VGPRs
+// (4 waves per SIMD; unconstrained it takes 130)
+template <int LOGR1, int M2, int NT>
+void ntt2_fwd_launch(hipStream_t st, const DevTables& Tb, u32* dst, RowMap rm, LimbMap map, int groups, double io, double work,
+                     const NttAux& aux) {
+    const dim3 grid((1 << LOGR1) / (NT / 16), rm.cnt, groups);
+    if (M2 == kFinish && fin_occ_on())
+        prof_launch_tsw(KID_NTT_ROWS_FWD, io, work, k_ntt2_fwd<LOGR1, M2, NT, 4>, grid, dim3(NT), 0, st, dst, rm, map, Tb.pc, Tb.tw, aux);
+    else
+        prof_launch_tsw(KID_NTT_ROWS_FWD, io, work, k_ntt2_fwd<LOGR1, M2, NT>, grid, dim3(NT), 0, st, dst, rm, map, Tb.pc, Tb.tw, aux);
+}
+template <int LOGR1, int M2>
+void ntt2_fwd_select(hipStream_t st, const DevTables& Tb, u32* dst, RowMap rm, LimbMap map, int groups, double io, double work,
+                     const NttAux& aux) {
+    switch (p2_nt(false)) {
+        case 128: ntt2_fwd_launch<LOGR1, M2, 128>(st, Tb, dst, rm, map, groups, io, work, aux); break;
+        case 512: ntt2_fwd_launch<LOGR1, M2, 512>(st, Tb, dst, rm, map, groups, io, work, aux); break;
+        default: ntt2_fwd_launch<LOGR1, M2, 256>(st, Tb, dst, rm, map, groups, io, work, aux); break;
+    }
+}
+
 // io_rows: rows actually transformed (launch rows minus skipped ones), for the byte count
 template <int LOGR1, int M1, int M2>
 void ntt_fwd_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, int io_rows, RowMap rm, LimbMap map,
@@ -528,8 +576,7 @@ void ntt_fwd_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
     constexpr int CB = kThreads / (R1 / 16);
     prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, M1, kThreads>, dim3(256 / CB, rm.cnt, groups), dim3(kThreads), 0, st, dst,
                     src, rm, map, Tb.pc, Tb.tw, aux);
-    prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2, kThreads>, dim3(R1 / kRowsP2, rm.cnt, groups), dim3(kThreads), 0, st,
-                    dst, rm, map, Tb.pc, Tb.tw, aux);
+    ntt2_fwd_select<LOGR1, M2>(st, Tb, dst, rm, map, groups, io2, bfly * 8.0, aux);
 }
 // AESFHE_NTT_INV_FACT=0: the inverse pass 2 reads every twiddle from the table (A/B runs)
 inline bool inv_fact_on() {
@@ -565,7 +612,11 @@ void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
         return;
     }
     constexpr int CB = kThreads / (R1 / 16);
-    ntt2_inv_launch<LOGR1, kThreads>(st, Tb, dst, src, rm, map, groups, io, bfly * 8.0);
+    switch (p2_nt(true)) {
+        case 128: ntt2_inv_launch<LOGR1, 128>(st, Tb, dst, src, rm, map, groups, io, bfly * 8.0); break;
+        case 256: ntt2_inv_launch<LOGR1, 256>(st, Tb, dst, src, rm, map, groups, io, bfly * 8.0); break;
+        default: ntt2_inv_launch<LOGR1, kThreads>(st, Tb, dst, src, rm, map, groups, io, bfly * 8.0); break;
+    }
     prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, kThreads>, dim3(256 / CB, rm.cnt, groups), dim3(kThreads), 0, st, dst, rm,
                     map, Tb.pc, Tb.itw, post);
 }
@@ -615,8 +666,7 @@ void ntt_fwd_conv_t(hipStream_t st, const DevTables& Tb, u32* dst, const ConvBat
         return;
     }
     ntt1_conv_dispatch<LOGR1, kThreads>(st, Tb, dst, cb, h, rm, map, groups, io1, bfly * LOGR1);
-    prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2, kThreads>, dim3(R1 / kRowsP2, rm.cnt, groups), dim3(kThreads), 0, st,
-                    dst, rm, map, Tb.pc, Tb.tw, aux);
+    ntt2_fwd_select<LOGR1, M2>(st, Tb, dst, rm, map, groups, io2, bfly * 8.0, aux);
 }
 
 }  // namespace
