@@ -1262,7 +1262,7 @@ public:
                 for (int q = 0; q < L.n_b; ++q) {
                     const size_t c = (size_t)p * L.n_b + q;
                     if (L.re[c] == 0.0 && L.im[c] == 0.0) continue;
-                    op.q_of[j++] = (unsigned char)q;
+                    op.q_of[j++] = q;
                     terms.push_back({(int)c, S_out / (hp_.delta[ea[p]->level] * hp_.delta[eb[q]->level])});
                 }
                 op.a[p] = ea[p] ? ea[p]->data : nullptr;
@@ -2581,6 +2581,9 @@ public:
     struct BootGroupDev {
         const LinGroup* g = nullptr;
         std::map<int, std::vector<std::vector<u32*>>> pts;  // level -> [giant][baby] encoded diagonals
+        // compact diagonals (group_pts): log2 of the run length s of equal NTT values and of the
+        // 2 dn values per limb; 0 = full rows
+        int c_shift = 0, c_logc = 0;
     };
     struct BootState {
         bool ready = false;
@@ -2767,10 +2770,32 @@ public:
         auto it = G.pts.find(level);
         if (it != G.pts.end()) return it->second;
         const LinGroup& g = *G.g;
-        const int M = slot_count();
+        const int M = slot_count(), n = hp_.n;
         std::vector<std::vector<u32*>> P(g.G, std::vector<u32*>(g.B, nullptr));
         std::vector<double> re(M), im(M);
         std::vector<u32> host;
+        // a sparse plan's diagonals are dn-periodic slot vectors (dn < M), i.e. elements of the
+        // subring Z[X^s], s = N / (2 dn): their coefficients off the multiples of s are exactly 0
+        // (the fp64 embedding leaves rounding noise there -- ~Delta 2^-52 -- which the projection
+        // below removes).  In NTT form such an element takes the value p(psi^(s (2 brv(i) + 1))),
+        // which depends on i only through its top log2(2 dn) bits: runs of s equal residues.
+        // k_lin_mac then reads 2 dn words per limb (LinMacArgs::pt_shift) instead of N
+        size_t dn0 = 0;
+        bool same = true;
+        for (int gg = 0; gg < g.G; ++gg)
+            for (int b = 0; b < g.B; ++b)
+                if (!g.diag[gg][b].empty()) {
+                    if (!dn0) dn0 = g.diag[gg][b].size();
+                    same = same && g.diag[gg][b].size() == dn0;
+                }
+        const bool tiled = same && dn0 && dn0 < (size_t)M && M % dn0 == 0, compact = tiled && compact_diag_;
+        const size_t sr = tiled ? (size_t)n / (2 * dn0) : 1;
+        if (compact) {
+            int a = 0, c = 0;
+            while (((size_t)1 << a) < sr) ++a;
+            while (((size_t)1 << c) < 2 * dn0) ++c;
+            G.c_shift = a, G.c_logc = c;
+        }
         for (int gg = 0; gg < g.G; ++gg)
             for (int b = 0; b < g.B; ++b) {
                 const auto& d = g.diag[gg][b];
@@ -2779,10 +2804,21 @@ public:
                 for (int p = 0; p < M; ++p) re[p] = d[p % dn].real(), im[p] = d[p % dn].imag();
                 const int nl = hp_.nl(level), ne = nl + hp_.n_p;
                 encode_host(re.data(), im.data(), hp_.ptscale[level], nl, host, hp_.n_p);
+                if (tiled)  // project onto the subring Z[X^s]
+                    for (size_t x = 0; x < host.size(); ++x)
+                        if ((x & (size_t)(n - 1)) % sr) host[x] = 0;
                 u32* dv = tmp(ne);
                 HIP_OK(hipMemcpyAsync(dv, host.data(), host.size() * sizeof(u32), hipMemcpyHostToDevice, S()));
                 HIP_OK(hipStreamSynchronize(S()));
                 ntt(dv, ne, ne, extmap(nl));
+                if (compact) {  // one residue per run: [ne][2 dn]
+                    u32* cv = dev_alloc((size_t)ne * 2 * dn0);
+                    HIP_OK(hipMemcpy2DAsync(cv, sizeof(u32), dv, sr * sizeof(u32), sizeof(u32), (size_t)ne * 2 * dn0,
+                                            hipMemcpyDeviceToDevice, S()));
+                    HIP_OK(hipStreamSynchronize(S()));
+                    untmp(dv, ne);
+                    dv = cv;
+                }
                 P[gg][b] = dv;
             }
         HIP_OK(hipStreamSynchronize(S()));  // cached for every stream
@@ -2853,6 +2889,7 @@ public:
             const int gn = std::min(kLinG, g.G - g0);
             LinMacArgs m{};
             m.B = g.B, m.G = gn, m.c1 = c1;
+            m.pt_shift = G.c_shift, m.pt_logc = G.c_logc;
             m.nb = nb, m.q_ms = qs, m.p_ms = ps;
             // rotated giant steps: P (out0, out1) folded into outp, ModDown fused with the rescale
             const bool fold = fuse_rr_ && l >= 1 && mdr_off_[l] != SIZE_MAX;
@@ -4009,6 +4046,9 @@ private:
     bool fused_baby_ = std::getenv("AESFHE_FUSED_BABY") == nullptr || std::getenv("AESFHE_FUSED_BABY")[0] != '0';
     bool giant_batch_ = std::getenv("AESFHE_GIANT_BATCH") == nullptr || std::getenv("AESFHE_GIANT_BATCH")[0] != '0';
     bool double_hoist_ = std::getenv("AESFHE_DOUBLE_HOIST") == nullptr || std::getenv("AESFHE_DOUBLE_HOIST")[0] != '0';
+    // sparse-plan diagonals as 2 dn residues per limb (group_pts; AESFHE_COMPACT_DIAG=0: full rows of
+    // the same projected diagonals -- bit-identical results, the A/B and the check of the run structure)
+    bool compact_diag_ = std::getenv("AESFHE_COMPACT_DIAG") == nullptr || std::getenv("AESFHE_COMPACT_DIAG")[0] != '0';
     bool fuse_rr_ = std::getenv("AESFHE_FUSED_RESCALE") == nullptr || std::getenv("AESFHE_FUSED_RESCALE")[0] != '0';
     u32* d_pinv_ = nullptr;
     u32* d_negp_ = nullptr;

@@ -307,6 +307,9 @@ struct LinMacArgs {
     const u32* ks_d = nullptr;
     int nd = 0, alpha = 1, nkey = 0, nks = 0;
     size_t ext_ms = 0, d_ms = 0;
+    // pt_shift > 0: compact diagonals (a sparse plan's, engine group_pts): limb t's residue at
+    // coefficient k is pt[(t << pt_logc) + (k >> pt_shift)] -- runs of 2^pt_shift equal values
+    int pt_shift = 0, pt_logc = 0;
 };
 void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int nl, int ne, LimbMap map);
 
@@ -408,7 +411,7 @@ struct LutOperands {
     const u32* b[kLutMax];
     int na[kLutMax], nb[kLutMax];
     int p_start[kLutMax + 1];  // terms of A_p: [p_start[p], p_start[p + 1]) in q_of
-    unsigned char q_of[kLutMax * kLutMax];
+    int q_of[kLutMax * kLutMax];  // int, not byte: a uniform dword read by the scalar unit (a byte load is a vector load + wait)
 };
 // out (3 polys, nl rows each) = sum_p A_p (x) (sum_q C_pq B_q)
 // members > 1: every element a stack of `members` ciphertexts (member stride 2 x its limbs x N),

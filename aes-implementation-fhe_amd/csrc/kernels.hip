@@ -247,25 +247,51 @@ __device__ __forceinline__ void conv_stage(const ConvBatch& cb, int gi, int h, i
         s_src[i][0] = P.q, s_src[i][1] = P.mu, s_src[i][2] = cb.qhinv[gi][2 * i], s_src[i][3] = cb.qhinv[gi][2 * i + 1];
     }
 }
-template <int H>
+// V consecutive coefficients per thread (1 or 2: one 4- / 8-byte access per source and target
+// row; 4 needs 260 VGPRs at H = 16 and spills): each LDS-staged weight then feeds V multiply-adds, and a launch issues V times
+// fewer load / store instructions; the arithmetic per coefficient is unchanged (bit-exact)
+template <int V>
+struct ConvVec;
+template <>
+struct ConvVec<1> {
+    using T = u32;
+    static __device__ __forceinline__ void get(const T& t, u32* o) { o[0] = t; }
+    static __device__ __forceinline__ T make(const u32* o) { return o[0]; }
+};
+template <>
+struct ConvVec<2> {
+    using T = uint2;
+    static __device__ __forceinline__ void get(const T& t, u32* o) { o[0] = t.x, o[1] = t.y; }
+    static __device__ __forceinline__ T make(const u32* o) { return make_uint2(o[0], o[1]); }
+};
+template <int H, int V>
 __device__ __forceinline__ void conv_body(const ConvBatch& cb, int gi, int t0, int t1, int nt, LimbMap map, const PrimeConst* pc, int logn,
                                           u32 (*s_w)[kMaxConvH], u32 (*s_tq)[4], u32 (*s_src)[4]) {
+    using CV = ConvVec<V>;
     const u32* __restrict__ x = cb.src[gi];
     u32* __restrict__ ext = cb.dst[gi];
     const int skip0 = cb.skip0[gi];
-    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    u32 y[H];
+    const size_t k = ((size_t)blockIdx.x * kBlock + threadIdx.x) * V;
+    u32 y[H][V];
 #pragma unroll
-    for (int i = 0; i < H; ++i) y[i] = x[((size_t)i << logn) + k];
+    for (int i = 0; i < H; ++i) CV::get(*reinterpret_cast<const typename CV::T*>(x + ((size_t)i << logn) + k), y[i]);
     conv_stage(cb, gi, H, cb.d0[gi], t0, t1, nt, map, pc, s_w, s_tq, s_src);
     __syncthreads();
-    u64 f = 0;
+    u32 u[V];
+    {
+        u64 f[V] = {};
 #pragma unroll
-    for (int i = 0; i < H; ++i) {
-        y[i] = shoup_mul(y[i], s_src[i][2], s_src[i][3], s_src[i][0]);
-        f += ((u64)y[i] * s_src[i][1]) >> 29;  // y_i / q_i in 32.32 fixed point (mu = 2^61 / q)
+        for (int i = 0; i < H; ++i) {
+            const u32 q = s_src[i][0], mu = s_src[i][1], w = s_src[i][2], wp = s_src[i][3];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                y[i][v] = shoup_mul(y[i][v], w, wp, q);
+                f[v] += ((u64)y[i][v] * mu) >> 29;  // y_i / q_i in 32.32 fixed point (mu = 2^61 / q)
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) u[v] = (u32)((f[v] + (1ull << 31)) >> 32);
     }
-    const u32 u = (u32)((f + (1ull << 31)) >> 32);
 #pragma unroll
     for (int tl = 0; tl < kConvTargets; ++tl) {
         const int t = t0 + tl;
@@ -273,15 +299,27 @@ __device__ __forceinline__ void conv_body(const ConvBatch& cb, int gi, int t0, i
         const u32 q = s_tq[tl][0], r32 = s_tq[tl][2];
         // plain 32x32 -> 64-bit multiply-adds (v_mad_u64_u32); y_i < q_i, w < q_t, so eight
         // products stay below 2^64 and one fold makes room for eight more
-        u64 acc = (u64)u * s_tq[tl][3];
+        u64 acc[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] = (u64)u[v] * s_tq[tl][3];
 #pragma unroll
         for (int i = 0; i < H; ++i) {
-            if (i == 8) acc = fold64(acc, q, r32);
-            acc += (u64)y[i] * s_w[tl][i];
+            const u32 w = s_w[tl][i];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                if (i == 8) acc[v] = fold64(acc[v], q, r32);
+                acc[v] += (u64)y[i][v] * w;
+            }
         }
-        if (t < skip0 || t >= skip0 + H) ext[((size_t)t << logn) + k] = reduce64(acc, q, s_tq[tl][1], r32);
+        if (t < skip0 || t >= skip0 + H) {
+            u32 o[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) o[v] = reduce64(acc[v], q, s_tq[tl][1], r32);
+            *reinterpret_cast<typename CV::T*>(ext + ((size_t)t << logn) + k) = CV::make(o);
+        }
     }
 }
+template <int V>
 __global__ void __launch_bounds__(kBlock) k_base_convert(ConvBatch cb, int nt, LimbMap map, const PrimeConst* pc, int logn,
                                                          unsigned long long* ts) {
     const int gi = blockIdx.z;
@@ -294,7 +332,7 @@ __global__ void __launch_bounds__(kBlock) k_base_convert(ConvBatch cb, int nt, L
     __shared__ u32 s_src[kMaxConvH][4];    // q, mu, qhat^-1, Shoup companion
     switch (h) {
 #define CONV_CASE(H) \
-    case H: conv_body<H>(cb, gi, t0, t1, nt, map, pc, logn, s_w, s_tq, s_src); break;
+    case H: conv_body<H, V>(cb, gi, t0, t1, nt, map, pc, logn, s_w, s_tq, s_src); break;
         CONV_CASE(1) CONV_CASE(2) CONV_CASE(3) CONV_CASE(4) CONV_CASE(5) CONV_CASE(6) CONV_CASE(7) CONV_CASE(8)
         CONV_CASE(9) CONV_CASE(10) CONV_CASE(11) CONV_CASE(12) CONV_CASE(13) CONV_CASE(14) CONV_CASE(15) CONV_CASE(16)
 #undef CONV_CASE
@@ -315,8 +353,11 @@ __device__ __forceinline__ u32 galois_src(u32 i, u64 g, int logn) {
 // g != 0: the inputs (ext and d) are read through the automorphism X -> X^g -- a hoisted
 // rotation: one ModUp of c1 serves every rotation of the same ciphertext
 // four consecutive coefficients per thread: 16-byte key / ext / acc accesses (the kernel is
-// HBM-bound on the key and ext reads); g != 0 gathers ext and d through X -> X^g
-template <int NBM>
+// HBM-bound on the key and ext reads); g != 0 gathers ext and d through X -> X^g.
+// ND > 0: the digit count is a compile-time constant, so the digit loop unrolls and every digit's
+// key and ext loads are in flight together (with the run-time bound each iteration waited for
+// its own loads: one memory round trip per digit); ND = 0 keeps the run-time loop
+template <int NBM, int ND = 0>
 __global__ void __launch_bounds__(kBlock) k_key_inner(u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
                                                       int alpha, int nkey, int nks, u64 g, LimbMap map, const PrimeConst* pc, int logn,
                                                       int nb, size_t ext_ms, size_t d_ms, size_t acc_ms, KsFold fold, int accum,
@@ -333,7 +374,9 @@ __global__ void __launch_bounds__(kBlock) k_key_inner(u32* acc, const u32* ext, 
     // 64-bit multiply-adds (operands < q < 2^30: eight products fit beside a folded sum), folded every 8 digits;
     // the key residues are loaded once for every batched ciphertext
     u64 s0[NBM][4] = {}, s1[NBM][4] = {};
-    for (int j = 0; j < nd; ++j) {
+    const int ndd = ND > 0 ? ND : nd;
+#pragma unroll
+    for (int j = 0; j < ndd; ++j) {
         if (j && (j & 7) == 0) {
 #pragma unroll
             for (int m = 0; m < NBM; ++m)
@@ -419,6 +462,8 @@ __device__ __forceinline__ void xcd_rows(int lognbx, int rows, int& bx, int& row
 
 // J hoisted rotations summed in one pass (KsSumArgs): the trace step's three key inner products,
 // grid z = stacked member; 64-bit multiply-adds folded every 8 products
+// ND > 0: compile-time digit count (k_key_inner's ND: each rotation's digit loads in flight together)
+template <int ND = 0>
 __global__ void __launch_bounds__(kBlock) k_key_inner_sum(u32* acc, const u32* ext, const u32* d, KsSumArgs ka, int nd, int ne, int nl,
                                                           int alpha, int nkey, int nks, LimbMap map, const PrimeConst* pc, int logn,
                                                           size_t ext_ms, size_t d_ms, size_t acc_ms, unsigned long long* ts) {
@@ -439,7 +484,9 @@ __global__ void __launch_bounds__(kBlock) k_key_inner_sum(u32* acc, const u32* e
 #pragma unroll
         for (int v = 0; v < 4; ++v) ks[v] = galois_src((u32)(k + v), ka.g[i], logn);
         const u32* key = ka.key[i];
-        for (int j = 0; j < nd; ++j, ++cnt) {
+        const int ndd = ND > 0 ? ND : nd;
+#pragma unroll
+        for (int j = 0; j < ndd; ++j, ++cnt) {
             if (cnt && (cnt & 7) == 0) {
 #pragma unroll
                 for (int v = 0; v < 4; ++v) s0[v] = fold64(s0[v], P.q, P.r32), s1[v] = fold64(s1[v], P.q, P.r32);
@@ -479,6 +526,8 @@ __global__ void k_automorph_sum(u32* out, const u32* in, KsSumArgs ka, int nl, s
 // heterogeneous members (KsMultiArgs): grid z = member, each member its own key, Galois element
 // and ModUp source; otherwise the arithmetic of k_key_inner<1> (four coefficients per thread,
 // 64-bit multiply-adds folded every 8 digits)
+// ND > 0: compile-time digit count (k_key_inner's ND)
+template <int ND = 0>
 __global__ void __launch_bounds__(kBlock) k_key_inner_multi(u32* acc, const u32* ext, const u32* d, KsMultiArgs ka, int nd, int ne,
                                                             int nl, int alpha, int nkey, int nks, LimbMap map, const PrimeConst* pc,
                                                             int logn, size_t ext_ms, size_t d_ms, size_t acc_ms, unsigned long long* ts) {
@@ -495,7 +544,9 @@ __global__ void __launch_bounds__(kBlock) k_key_inner_multi(u32* acc, const u32*
     const int krow = x < nl ? x : nks + (x - nl);
     const int own = x < nl ? x / alpha : -1;
     u64 s0[4] = {}, s1[4] = {};
-    for (int j = 0; j < nd; ++j) {
+    const int ndd = ND > 0 ? ND : nd;
+#pragma unroll
+    for (int j = 0; j < ndd; ++j) {
         if (j && (j & 7) == 0) {
 #pragma unroll
             for (int v = 0; v < 4; ++v) s0[v] = fold64(s0[v], P.q, P.r32), s1[v] = fold64(s1[v], P.q, P.r32);
@@ -972,11 +1023,14 @@ __global__ void __launch_bounds__(kBlock) k_encode_untwist(u32* out, const doubl
 // ------------------------------------------------------------------------------------
 // grid z = member of stacked elements: element p of member m at a[p] + m 2 na[p] N (b likewise),
 // the output at out + m 3 nl N
-__global__ void __launch_bounds__(kBlock) k_lut_bivariate(u32* out, LutOperands op, int n_a, const u32* cst, int nl,
+// the coefficient half (conjugate split) is block-uniform (kBlock divides N / 2), so the
+// coefficient loads are uniform; the term loops are unrolled by 4 so that four terms' operand
+// loads are in flight together
+__global__ void __launch_bounds__(kBlock) k_lut_bivariate(u32* out, LutOperands op, int n_a, const u32* __restrict__ cst, int nl,
                                                           const PrimeConst* pc, int logn) {
     const int t = blockIdx.y, mb = blockIdx.z;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    const int half = (int)(k >> (logn - 1));
+    const int half = (int)(((size_t)blockIdx.x * kBlock) >> (logn - 1));
     const PrimeConst P = pc[t];
     const u32 q = P.q;
     const size_t off = ((size_t)t << logn) + k;
@@ -989,6 +1043,7 @@ __global__ void __launch_bounds__(kBlock) k_lut_bivariate(u32* out, LutOperands 
         const int t0 = op.p_start[p], t1 = op.p_start[p + 1];
         if (t0 == t1) continue;
         u64 s0 = 0, s1 = 0;
+#pragma unroll 4
         for (int j = t0; j < t1; ++j) {
             if (j > t0 && ((j - t0) & 7) == 0) s0 = fold64(s0, q, P.r32), s1 = fold64(s1, q, P.r32);
             const int qq = op.q_of[j];
@@ -1013,11 +1068,12 @@ __global__ void __launch_bounds__(kBlock) k_lut_bivariate(u32* out, LutOperands 
 
 // grid z = member of stacked elements (element j of member m at x[j] + m npoly nx[j] N, out / acc
 // at + m npoly nl N)
-__global__ void __launch_bounds__(kBlock) k_lut_univariate(u32* out, const u32* acc, LutChunk ch, int n, const u32* cst, int npoly,
-                                                           int nl, const PrimeConst* pc, int logn) {
+// (k_lut_bivariate's uniform coefficient half and unrolled term loop)
+__global__ void __launch_bounds__(kBlock) k_lut_univariate(u32* out, const u32* acc, LutChunk ch, int n, const u32* __restrict__ cst,
+                                                           int npoly, int nl, const PrimeConst* pc, int logn) {
     const int t = blockIdx.y, mb = blockIdx.z;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    const int half = (int)(k >> (logn - 1));
+    const int half = (int)(((size_t)blockIdx.x * kBlock) >> (logn - 1));
     const PrimeConst P = pc[t];
     const u32 q = P.q;
     const size_t off = ((size_t)t << logn) + k;
@@ -1025,6 +1081,7 @@ __global__ void __launch_bounds__(kBlock) k_lut_univariate(u32* out, const u32* 
     for (int p = 0; p < npoly; ++p) {
         const size_t o = mo + ((size_t)(p * nl) << logn) + off;
         u64 v = acc ? acc[o] : 0;  // 64-bit multiply-adds, folded every 8 terms, one reduction
+#pragma unroll 4
         for (int j = 0; j < n; ++j) {
             if (j && (j & 7) == 0) v = fold64(v, q, P.r32);
             const u32 c = cst[((size_t)j * nl + t) * 4 + 2 * half];
@@ -1130,15 +1187,31 @@ void launch_crt2_spread(hipStream_t st, const DevTables& T, u32* v, const u32* s
     prof_launch(KID_RESCALE, words((double)npoly * (2 + nt) * (1u << T.logn)), k_crt2_spread, dim3((1u << T.logn) / kBlock, nt, npoly),
                 dim3(kBlock), 0, st, v, src, nt, q0, q1, (u32)inv, shoup_pre((u32)inv, q1), T.pc, T.logn);
 }
+// coefficients per thread of k_base_convert (AESFHE_CONV_VEC = 1 or 2)
+inline int conv_vec() {
+    static const int v = [] {
+        const char* e = std::getenv("AESFHE_CONV_VEC");
+        const int x = e ? std::atoi(e) : 1;
+        return x == 2 ? 2 : 1;
+    }();
+    return v;
+}
 void launch_base_convert(hipStream_t st, const DevTables& T, const ConvBatch& cb, int nt, LimbMap map) {
     double w = 0;
     for (int g = 0; g < cb.n; ++g) {
         const bool own = cb.skip0[g] >= 0 && cb.skip0[g] < nt;
         w += cb.h[g] + nt - (own ? std::min(cb.h[g], nt - cb.skip0[g]) : 0);
     }
-    prof_launch_ts(KID_BASE_CONVERT, words(w * (1u << T.logn)), k_base_convert,
-                dim3((1u << T.logn) / kBlock, (nt + kConvTargets - 1) / kConvTargets, cb.n), dim3(kBlock), 0, st, cb, nt, map, T.pc,
-                T.logn);
+    const dim3 grid_y((nt + kConvTargets - 1) / kConvTargets, cb.n);
+    switch (conv_vec()) {
+        case 2:
+            prof_launch_ts(KID_BASE_CONVERT, words(w * (1u << T.logn)), k_base_convert<2>, dim3((1u << T.logn) / (2 * kBlock), grid_y.x, grid_y.y),
+                           dim3(kBlock), 0, st, cb, nt, map, T.pc, T.logn);
+            break;
+        default:
+            prof_launch_ts(KID_BASE_CONVERT, words(w * (1u << T.logn)), k_base_convert<1>, dim3((1u << T.logn) / kBlock, grid_y.x, grid_y.y),
+                           dim3(kBlock), 0, st, cb, nt, map, T.pc, T.logn);
+    }
 }
 
 namespace {
@@ -1221,7 +1294,7 @@ __device__ __forceinline__ void lin_mac_body(const LinMacArgs& m, int nl, int ne
 #pragma unroll
         for (int g = 0; g < kLinG; ++g) {
             if (g >= m.G || !m.pt[g][j]) continue;
-            const u32 pv = m.pt[g][j][at];
+            const u32 pv = m.pt_shift ? m.pt[g][j][((size_t)t << m.pt_logc) + (k >> m.pt_shift)] : m.pt[g][j][at];
 #pragma unroll
             for (int b = 0; b < NB; ++b) {
                 acc0[b][g] += (u64)av[b] * pv;  // q < 2^30: 8 products fit beside a folded accumulator
@@ -1239,7 +1312,10 @@ __device__ __forceinline__ void lin_mac_body(const LinMacArgs& m, int nl, int ne
             u32 o0 = 0, o1 = 0;
             if (qrow) {
                 o0 = reduce64(acc0[b][g], P.q, P.mu, P.r32);
-                if (m.pt[g][0]) o1 = reduce64((u64)c1v * m.pt[g][0][at], P.q, P.mu, P.r32);
+                if (m.pt[g][0]) {
+                    const u32 p0 = m.pt_shift ? m.pt[g][0][((size_t)t << m.pt_logc) + (k >> m.pt_shift)] : m.pt[g][0][at];
+                    o1 = reduce64((u64)c1v * p0, P.q, P.mu, P.r32);
+                }
             }
             const bool fold = m.gad && m.outp[g];
             if (qrow && !fold) {
@@ -1303,7 +1379,7 @@ void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int
         if (m.u[b]) member += 2.0 * ne;
         if (m.key[b]) shared += 2.0 * m.nd * ne;  // the key, read once for every batched ciphertext
         for (int g = 0; g < m.G; ++g)
-            if (m.pt[g][b]) shared += ne;         // the diagonals likewise
+            if (m.pt[g][b]) shared += m.pt_shift ? ne * (double)(1 << m.pt_logc) / (1u << T.logn) : ne;  // the diagonals likewise
     }
     if (any_a) member += nl;                      // c0
     if (any_key) member += (double)m.nd * ne;     // the hoisted ModUp of c1 (ext)
@@ -1335,6 +1411,31 @@ void launch_mac(hipStream_t st, const DevTables& T, u32* out, const MacTerms& m,
                 dim3((1u << T.logn) / kBlock, rows, npoly), dim3(kBlock), 0, st, out, m, xs, os, map, T.pc, T.logn);
 }
 
+// AESFHE_KI_UNROLL=0: k_key_inner with the run-time digit loop for every launch (A/B runs)
+inline bool ki_unroll() {
+    static const bool v = [] {
+        const char* e = std::getenv("AESFHE_KI_UNROLL");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return v;
+}
+template <int NBM>
+void key_inner_nd(int ndc, double bytes, dim3 grid, hipStream_t st, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne,
+                  int nl, int alpha, int nkey, int nks, u64 g, LimbMap map, const DevTables& T, int nb, size_t ext_ms, size_t d_ms,
+                  size_t acc_ms, KsFold fold, bool accum) {
+    switch (ndc) {
+#define KI_ND(D) \
+    case D: \
+        prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<NBM, D>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g, \
+                       map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum); \
+        break;
+        KI_ND(1) KI_ND(2) KI_ND(3) KI_ND(4) KI_ND(5) KI_ND(6) KI_ND(7) KI_ND(8)
+#undef KI_ND
+        default:
+            prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<NBM>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks,
+                           g, map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum);
+    }
+}
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
                       int alpha, int nkey, int nks, LimbMap map, u64 g, int nb, size_t ext_ms, size_t d_ms, size_t acc_ms, KsFold fold,
                       bool accum) {
@@ -1345,16 +1446,15 @@ void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* e
     const double fw = (fold.gad ? 2.0 * nb * nl : 0.0) + (accum ? 2.0 * nb * ne : 0.0);
     const double bytes = words(((nb * (nd + 2.0) + 2.0 * nd) * ne + fw) * (1u << T.logn));
     const dim3 grid((1u << T.logn) / (4 * kBlock), ne);
-    // register footprint follows the batch: 1, 2, 4 or 8 ciphertexts
+    // register footprint follows the batch: 1, 2, 4 or 8 ciphertexts; up to 4, the digit count
+    // as a template constant (ki_unroll(), k_key_inner's ND)
+    const int ndc = (ki_unroll() && nd >= 1 && nd <= 8 && nb <= 4) ? nd : 0;
     if (nb == 1)
-        prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<1>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g,
-                       map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum);
+        key_inner_nd<1>(ndc, bytes, grid, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g, map, T, nb, ext_ms, d_ms, acc_ms, fold, accum);
     else if (nb == 2)
-        prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<2>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g,
-                       map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum);
+        key_inner_nd<2>(ndc, bytes, grid, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g, map, T, nb, ext_ms, d_ms, acc_ms, fold, accum);
     else if (nb <= 4)
-        prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<4>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g,
-                       map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum);
+        key_inner_nd<4>(ndc, bytes, grid, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g, map, T, nb, ext_ms, d_ms, acc_ms, fold, accum);
     else
         prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner<8>, grid, dim3(kBlock), 0, st, acc, ext, d, key, nd, ne, nl, alpha, nkey, nks, g,
                        map, T.pc, T.logn, nb, ext_ms, d_ms, acc_ms, fold, (int)accum);
@@ -1366,8 +1466,18 @@ void launch_key_inner_sum(hipStream_t st, const DevTables& T, u32* acc, const u3
         if (!ka.key[i] || !ka.g[i]) throw std::runtime_error("launch_key_inner_sum: missing key or Galois element");
     // ext / d read once per member (the J gathers of a row hit L2), the J keys once, acc written
     const double bytes = words(((nb * (nd + 2.0) + 2.0 * nd * ka.J) * ne) * (1u << T.logn));
-    prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner_sum, dim3((1u << T.logn) / (4 * kBlock), ne, nb), dim3(kBlock), 0, st, acc, ext, d, ka, nd,
-                   ne, nl, alpha, nkey, nks, map, T.pc, T.logn, ext_ms, d_ms, acc_ms);
+    switch ((ki_unroll() && nd >= 1 && nd <= 8) ? nd : 0) {
+#define KIS_ND(D) \
+    case D: \
+        prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner_sum<D>, dim3((1u << T.logn) / (4 * kBlock), ne, nb), dim3(kBlock), 0, st, acc, ext, d, ka, nd, \
+                       ne, nl, alpha, nkey, nks, map, T.pc, T.logn, ext_ms, d_ms, acc_ms); \
+        break;
+        KIS_ND(1) KIS_ND(2) KIS_ND(3) KIS_ND(4) KIS_ND(5) KIS_ND(6) KIS_ND(7) KIS_ND(8)
+#undef KIS_ND
+        default:
+            prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner_sum<>, dim3((1u << T.logn) / (4 * kBlock), ne, nb), dim3(kBlock), 0, st, acc, ext,
+                           d, ka, nd, ne, nl, alpha, nkey, nks, map, T.pc, T.logn, ext_ms, d_ms, acc_ms);
+    }
 }
 void launch_automorph_sum(hipStream_t st, const DevTables& T, u32* out, const u32* in, const KsSumArgs& ka, int nb, int rows, size_t ms,
                           LimbMap map) {
@@ -1382,8 +1492,18 @@ void launch_key_inner_multi(hipStream_t st, const DevTables& T, u32* acc, const 
         if (!ka.key[m] || ka.src[m] < 0 || ka.src[m] >= nsrc) throw std::runtime_error("launch_key_inner_multi: bad member");
     // each member reads its source's ext / d and its key, writes acc; distinct sources' ext once
     const double bytes = words(((nsrc * (double)nd + nm * (2.0 * nd + 2.0)) * ne) * (1u << T.logn));
-    prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner_multi, dim3((1u << T.logn) / (4 * kBlock), ne, nm), dim3(kBlock), 0, st, acc, ext, d,
-                   ka, nd, ne, nl, alpha, nkey, nks, map, T.pc, T.logn, ext_ms, d_ms, acc_ms);
+    switch ((ki_unroll() && nd >= 1 && nd <= 8) ? nd : 0) {
+#define KIM_ND(D) \
+    case D: \
+        prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner_multi<D>, dim3((1u << T.logn) / (4 * kBlock), ne, nm), dim3(kBlock), 0, st, acc, ext, d, \
+                       ka, nd, ne, nl, alpha, nkey, nks, map, T.pc, T.logn, ext_ms, d_ms, acc_ms); \
+        break;
+        KIM_ND(1) KIM_ND(2) KIM_ND(3) KIM_ND(4) KIM_ND(5) KIM_ND(6) KIM_ND(7) KIM_ND(8)
+#undef KIM_ND
+        default:
+        prof_launch_ts(KID_KEY_INNER, bytes, k_key_inner_multi<>, dim3((1u << T.logn) / (4 * kBlock), ne, nm), dim3(kBlock), 0, st, acc, ext, d,
+                       ka, nd, ne, nl, alpha, nkey, nks, map, T.pc, T.logn, ext_ms, d_ms, acc_ms);
+    }
 }
 void launch_automorph_multi(hipStream_t st, const DevTables& T, u32* out, size_t out_ms, const AutoMulti& am, int n, int rows) {
     if (n < 1 || n > kKsMulti) throw std::runtime_error("launch_automorph_multi: 1..16 members");

@@ -141,3 +141,32 @@ def test_mono_split_matches_slot_model(E, n):
     want_lo = (zm - r) * np.exp(-1j * np.pi * k * e / N)
     assert _rel(E.decrypt(hi), want_hi) < REL
     assert _rel(E.decrypt(lo), want_lo) < REL
+
+
+@pytest.mark.parametrize("logn", [13, 16])
+def test_compact_diagonals_bit_identical(logn, monkeypatch):
+    """A sparse plan's diagonals are dn-periodic slot vectors, i.e. subring elements, so their NTT
+    rows are runs of N / (2 dn) equal residues and k_lin_mac reads 2 dn residues per limb (engine
+    group_pts, LinMacArgs::pt_shift).  The full rows of the same projected diagonals
+    (AESFHE_COMPACT_DIAG=0) must give the same sparse bootstraps bit for bit: single at periods 16
+    and 32, and the monomial pair at 16 (the C2 MixColumns form)."""
+    from engine_context import EngineContext
+    from mi355x_ckks import Engine
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("AESFHE_COMPACT_DIAG", flag)  # read when an engine is created
+        if logn == 13:
+            E = Engine(log_n=13, use_bootstrap=True, max_level=3, dnum=5, seed=7, allow_insecure=True, enc_nonce=0)
+        else:
+            E = EngineContext(signature=1, max_level=17, log_n=16, seed=0x5EED, enc_nonce=0).engine
+        rng = np.random.default_rng(3)
+        res = []
+        for n in (16, 32):
+            ct = E.encrypt(_periodic(E, n, rng))
+            res.append(E.export(E.bootstrap_sparse(ct, n)).tobytes())
+        a, b = E.encrypt(_periodic(E, 16, rng)), E.encrypt(_periodic(E, 16, rng))
+        pa, pb = E.bootstrap_pair_sparse(a, b, 16)
+        res += [E.export(pa).tobytes(), E.export(pb).tobytes()]
+        outs.append(res)
+        del E
+    assert all(x == y for x, y in zip(outs[0], outs[1]))

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Generic environment-switch A/B of the C2 bench leg (through gpurun, from the repo root):
+#   bash tools/env_ab.sh OUTDIR "A=1,B=2" "A=0" ...   -- each config (comma-separated VAR=value
+# pairs, "-" for none) runs the 10-step C2 leg, PASSES (default 2) rounds over the list.
+# Each GPU step has its own limit; the first failure ends the script.
+set -e -o pipefail
+O=gpurun_out/$1; shift
+mkdir -p $O
+for pass in $(seq 1 ${PASSES:-2}); do
+  for cfg in "$@"; do
+    envs=()
+    [ "$cfg" != "-" ] && IFS=, read -ra envs <<< "$cfg"
+    env "${envs[@]}" timeout -k 10 150 python3 bench.py --no-cpu-baseline --batch-states 0 --true-fhe-steps 0 --pair-states 0 \
+        --packed-pairs 0 --steps 10 | sed "s/^/$cfg /" >> $O/bench.txt
+  done
+done
+echo done
