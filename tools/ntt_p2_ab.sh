@@ -9,10 +9,10 @@ O=gpurun_out/${1:-p2ab}; mkdir -p $O
   set -- $v
   AESFHE_NTT_P2_NT=$1 AESFHE_NTT_P2I_NT=$2 timeout -k 10 120 python3 tools/ntt_rows_sweep.py | sed "s/^/p2nt=$1 p2int=$2 /" >> $O/sweep.txt
 done
-echo sweep done
+[ "${SWEEP:-1}" = 1 ] && echo sweep done
 for pass in 1 2; do
-  for cfg in ${CFGS:-"512 512 0" "256 512 1" "256 512 0" "128 512 1" "256 256 1" "256 128 1"}; do
-    set -- $cfg
+  for cfg in ${CFGS:-512_512_0 256_512_1 256_512_0 128_512_1 256_256_1 256_128_1}; do
+    set -- ${cfg//_/ }
     AESFHE_NTT_P2_NT=$1 AESFHE_NTT_P2I_NT=$2 AESFHE_NTT_FIN_OCC=$3 timeout -k 10 150 python3 bench.py --no-cpu-baseline --batch-states 0 \
         --true-fhe-steps 0 --pair-states 0 --packed-pairs 0 --steps 10 | sed "s/^/p2nt=$1 p2int=$2 finocc=$3 /" >> $O/bench.txt
   done
