@@ -32,13 +32,17 @@ struct KernelProfiler {
     void flush();   // waits for recorded events and clock slots and folds them into the totals
     void reset();
     // In-kernel clock (s_memrealtime, 100 MHz) for the NTT, base-conversion and key-switch
-    // kernels: a timed launch gets a slot {earliest sampled block start, latest sampled block
-    // end}; it agrees with rocprofv3 --kernel-trace averages of the same launches within ~3 %
-    // (DESIGN.md §5).  Dispatch-stamped event pairs (hipExtLaunchKernelGGL; the element-wise
+    // kernels: a timed launch gets a slot {earliest start, latest end} over a sample of its
+    // blocks (launch.h ts_begin / ts_end); it agrees with rocprofv3 --kernel-trace averages of
+    // the same launches.  Dispatch-stamped event pairs (hipExtLaunchKernelGGL; the element-wise
     // kernels, or every kernel with AESFHE_PROF_EVENTS=1) read ~3 us longer per launch than
     // rocprofv3 does: the event's completion signal adds its own end-of-kernel release.
-    static constexpr int kTsSlots = 1 << 15;
-    unsigned long long* d_ts = nullptr;  // [2][kTsSlots]: starts, then ends
+    // A slot is one record of kTsRec words: kTsSub start lines holding ~(earliest start)
+    // (atomicMax of ~t, so a zeroed line is "unset"), then kTsSub end lines, each word on its own
+    // 128-byte line (a block stamps line (block id mod kTsSub): the atomics of a launch's first
+    // and last waves spread over 8 lines instead of queueing on one address).
+    static constexpr int kTsSlots = 1 << 14, kTsSub = 8, kTsLine = 16, kTsRec = kTsLine * 2 * kTsSub;
+    unsigned long long* d_ts = nullptr;  // [kTsSlots][kTsRec]
     int ts_next = 0;
     struct TsRec {
         int slot, kid;

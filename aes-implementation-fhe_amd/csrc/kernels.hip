@@ -723,34 +723,40 @@ void KernelProfiler::flush() {
     recs.clear();
 }
 unsigned long long* KernelProfiler::ts_slot(int kid, double b, double w) {
+    const size_t words = (size_t)kTsSlots * kTsRec;
     if (!d_ts) {
         void* p = nullptr;
-        if (hipMalloc(&p, sizeof(unsigned long long) * 2 * kTsSlots) != hipSuccess) return nullptr;
+        if (hipMalloc(&p, sizeof(unsigned long long) * words) != hipSuccess) return nullptr;
         d_ts = (unsigned long long*)p;
-        (void)hipMemset(d_ts, 0xFF, sizeof(unsigned long long) * kTsSlots);
-        (void)hipMemset(d_ts + kTsSlots, 0, sizeof(unsigned long long) * kTsSlots);
+        (void)hipMemset(d_ts, 0, sizeof(unsigned long long) * words);
     }
     if (ts_next == kTsSlots) ts_flush();
     ts_recs.push_back({ts_next, kid, b, w});
-    return d_ts + ts_next++;
+    return d_ts + (size_t)kTsRec * ts_next++;
 }
 void KernelProfiler::ts_flush() {
     if (!d_ts || ts_recs.empty()) return;
     (void)hipDeviceSynchronize();
-    std::vector<unsigned long long> h(2 * (size_t)kTsSlots);
-    (void)hipMemcpy(h.data(), d_ts, sizeof(unsigned long long) * 2 * kTsSlots, hipMemcpyDeviceToHost);
+    const size_t words = (size_t)kTsRec * ts_next;
+    std::vector<unsigned long long> h(words);
+    (void)hipMemcpy(h.data(), d_ts, sizeof(unsigned long long) * words, hipMemcpyDeviceToHost);
     for (const auto& r : ts_recs) {
-        const unsigned long long a = h[r.slot], e = h[(size_t)kTsSlots + r.slot];
-        if (a == ~0ull || e < a) continue;
+        const unsigned long long* rec = h.data() + (size_t)kTsRec * r.slot;
+        unsigned long long a = ~0ull, e = 0;
+        for (int j = 0; j < kTsSub; ++j) {
+            if (rec[kTsLine * j]) a = std::min(a, ~rec[kTsLine * j]);
+            e = std::max(e, rec[kTsLine * (kTsSub + j)]);
+        }
+        if (a == ~0ull) continue;  // no block stamped a start
+        if (e < a) continue;
         ms[r.kid] += (double)(e - a) * 1e-5;  // 100 MHz ticks -> ms
         bytes[r.kid] += r.bytes;
         work[r.kid] += r.work;
         launches[r.kid] += 1;
     }
     ts_recs.clear();
+    (void)hipMemset(d_ts, 0, sizeof(unsigned long long) * words);
     ts_next = 0;
-    (void)hipMemset(d_ts, 0xFF, sizeof(unsigned long long) * kTsSlots);
-    (void)hipMemset(d_ts + kTsSlots, 0, sizeof(unsigned long long) * kTsSlots);
 }
 void KernelProfiler::reset() {
     flush();

@@ -115,22 +115,29 @@ inline void prof_launch_ts(int kid, double bytes, F kernel, dim3 grid, dim3 bloc
     prof_launch_tsw(kid, bytes, 0.0, kernel, grid, block, lds, st, args...);
 }
 
-// device side: the first thread of a sample of blocks (<= ~256 evenly spaced ones, always the
-// first and the last) widens the launch's [start, end] span; sampling keeps atomic contention
-// on the slot negligible for grids of thousands of blocks
-__device__ __forceinline__ bool ts_block() {
-    const unsigned nb = gridDim.x * gridDim.y * gridDim.z;
-    const unsigned lin = blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z);
-    const unsigned stride = nb > 256 ? nb / 256 : 1;
-    return lin % stride == 0 || lin == nb - 1;
-}
+// device side.  Start: the first 8 blocks in dispatch order and <= ~256 evenly spaced ones
+// (a skipped block -- a ModUp NTT's own-digit rows -- stamps nothing, so the first blocks alone
+// can be absent).  End: <= ~2048 evenly spaced blocks plus the last 256 in dispatch order, where
+// the last-finishing block almost always is (<= 256 evenly spaced ones missed it on the
+// 256-thread NTT row passes' larger grids: 13.6 us live against rocprofv3's 15.4 us).  Each
+// stamp is an atomicMax into one of kTsSub 128-byte lines (block id mod kTsSub), so the atomics
+// of a launch's first and last waves do not queue on one address (a single line for 1,024
+// sampled blocks read 36 us for a 20 us key_inner).
+__device__ __forceinline__ unsigned ts_lin() { return blockIdx.x + gridDim.x * (blockIdx.y + gridDim.y * blockIdx.z); }
 __device__ __forceinline__ void ts_begin(unsigned long long* ts) {
-    if (ts && threadIdx.x == 0 && ts_block()) atomicMin(ts, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    if (!ts || threadIdx.x != 0) return;
+    const unsigned nb = gridDim.x * gridDim.y * gridDim.z, lin = ts_lin();
+    const unsigned stride = nb > 256 ? nb / 256 : 1;
+    if (lin < 8 || lin % stride == 0)
+        atomicMax(ts + KernelProfiler::kTsLine * (lin & (KernelProfiler::kTsSub - 1)), ~(unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 __device__ __forceinline__ void ts_end(unsigned long long* ts) {
     if (ts) {  // uniform: every thread of the block reaches the barrier
         __syncthreads();
-        if (threadIdx.x == 0 && ts_block())
-            atomicMax(ts + KernelProfiler::kTsSlots, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+        const unsigned nb = gridDim.x * gridDim.y * gridDim.z, lin = ts_lin();
+        const unsigned stride = nb > 2048 ? nb / 2048 : 1;
+        if (threadIdx.x == 0 && (lin % stride == 0 || lin + 256 >= nb))
+            atomicMax(ts + KernelProfiler::kTsLine * (KernelProfiler::kTsSub + (lin & (KernelProfiler::kTsSub - 1))),
+                      (unsigned long long)__builtin_amdgcn_s_memrealtime());
     }
 }

@@ -540,6 +540,9 @@ def main():
                 "traffic_source": tj.get("_source") if t else None,
                 "timed_launches": ks["launches"], "sampled_every": 1 if args.profile_all else args.profile_every,
                 "avg_us": ks["ms"] / max(ks["launches"], 1) * 1e3,
+                "timing": "in-kernel span of each sampled launch (first block start -> last block end, s_memrealtime); "
+                          "rocprofv3 durations of the same launches add the dispatch ramp and drain, 1.9-2.7 us per "
+                          "launch (profiles/r3_live_timing_check.json)",
                 "bytes_per_launch": ks["bytes"] / max(ks["launches"], 1), "note": note}
 
     def valu_roofline(kid: str) -> dict | None:
