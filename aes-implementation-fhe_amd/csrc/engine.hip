@@ -1305,14 +1305,22 @@ public:
     // those straight from d).  Returns nd x ne rows (tmp; the caller untmps).
     // nb > 1: the d polynomials of nb batched ciphertexts (d + m d_ms words), one launch per
     // stage for all of them; ext = [m][nd][ne]
-    u32* modup(const u32* d, int level, int nb = 1, size_t d_ms = 0) {
+    // tp (tensor mode, relin_rescale_tensor): member m's source rows are the products tp->a[m] (.) tp->b[m],
+    // formed inside the inverse NTT (d unused)
+    u32* modup(const u32* d, int level, int nb = 1, size_t d_ms = 0, const TensorPtrs* tp = nullptr) {
         const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, alpha = hp_.alpha;
         const int nd = (nl + alpha - 1) / alpha;
         if (alpha > kMaxConvH || np > kMaxConvH || nb * nd > kMaxConvGroups) throw std::runtime_error("keyswitch: digit too large");
         const LimbMap em = extmap(nl);
         const bool fz = fused_conv(true);
+        if (tp && fz) throw std::runtime_error("modup: the tensor form needs the separate conversion");
         u32* coef = tmp((size_t)nb * nl);
-        intt(coef, d, nb * nl, RowMap{nl, nb > 1 ? (int)(d_ms / n) : nl, nl, 0, 0}, qmap(), fz ? d_modup_qh_ + modup_qh_off_[nl] : nullptr);
+        if (tp) {
+            launch_ntt_inv_prod(S(), T_, coef, *tp, nb * nl, RowMap{nl, nl, nl, 0, 0}, qmap());
+            cnt_[C_NTT_ROWS] += nb * nl;
+        } else {
+            intt(coef, d, nb * nl, RowMap{nl, nb > 1 ? (int)(d_ms / n) : nl, nl, 0, 0}, qmap(), fz ? d_modup_qh_ + modup_qh_off_[nl] : nullptr);
+        }
         u32* ext = tmp((size_t)nb * nd * ne);
         const size_t* toff = &modup_off_[(size_t)nl * hp_.dnum];
         ConvBatch up;
@@ -1537,6 +1545,31 @@ public:
         cnt_[C_RELIN]++;
         return o;
     }
+    // relin_rescale of the products a[m] * b[m] (2-polynomial ciphertexts at one level, NTT form,
+    // pend 0; nb <= ks_chunk) without materialising their tensors: the ModUp's inverse NTT forms
+    // c2 = a1 (.) b1 on load, k_key_inner forms the own digit's c2 and the fold's (c0, c1) -- the
+    // residues k_tensor_ptrs would have written, so the result is the same bit for bit, one launch
+    // and 3 written + 3 re-read tensor rows per limb fewer (AESFHE_FUSED_TENSOR=0: tensor first)
+    void relin_rescale_tensor(const TensorPtrs& tp, int l, int nb, u32* const* outm) {
+        const int n = hp_.n, nl = hp_.nl(l), ne = nl + hp_.n_p;
+        if (nb > ks_chunk(l) || nb > kMaxKsBatch) throw std::runtime_error("relin_rescale_tensor: more members than one chunk");
+        TensorPtrs t1;  // a1, b1
+        KsFold f{nullptr, nullptr, 0, d_gadget_};
+        f.tnl = nl;
+        for (int m = 0; m < nb; ++m) {
+            t1.a[m] = tp.a[m] + (size_t)nl * n, t1.b[m] = tp.b[m] + (size_t)nl * n;
+            f.ta[m] = tp.a[m], f.tb[m] = tp.b[m];
+        }
+        u32* ext = modup(nullptr, l, nb, 0, &t1);
+        u32* acc = tmp(2 * (size_t)ne * nb);
+        key_inner(acc, ext, nullptr, ksk(0), l, 0, nb, 0, f);
+        untmp(ext, (size_t)nb * ext_rows(l));
+        Ct o = moddown_rescale(acc, l, nb, nullptr, outm);
+        (void)o;
+        untmp(acc, 2 * (size_t)ne * nb);
+        cnt_[C_KS] += nb;
+        cnt_[C_RELIN]++;
+    }
     // acc = [m][2][ne] in Q*P, NTT form, already holding P * (the ciphertext) -> the ciphertext
     // divided by the dropped limbs of level l, at level l - 1 (one ModDown by Q' = P * D)
     Ct moddown_rescale(const u32* acc, int l, int nb, u32* dst = nullptr, u32* const* outm = nullptr) {
@@ -1592,6 +1625,25 @@ public:
         const Ct &x = xy.first, &y = xy.second;
         const int nl = hp_.nl(x.level);
         if (x.nb != y.nb) throw std::runtime_error("multiply: batched operands of different sizes");
+        if (relin && !lazy && fused_tensor_ && !fused_conv(true) && x.nb <= std::min(ks_chunk(x.level), kMaxKsBatch)) {
+            Ct probe;
+            probe.level = x.level, probe.npoly = 3 * x.nb, probe.nb = x.nb, probe.pend = 1, probe.ntt = true;
+            if (fused_relin_rescale_ok(probe)) {  // relinearised and rescaled straight from the factors (relin_rescale_tensor)
+                Ct o = alloc_ct(x.level - 1, 2 * x.nb, x.nb);
+                o.ntt = true, o.pend = 0, o.lazy = false;
+                TensorPtrs tp;
+                u32* om[kMaxKsBatch];
+                const size_t ms = (size_t)2 * nl * hp_.n, oms = (size_t)2 * hp_.nl(x.level - 1) * hp_.n;
+                for (int m = 0; m < x.nb; ++m) tp.a[m] = x.data + m * ms, tp.b[m] = y.data + m * ms, om[m] = o.data + m * oms;
+                relin_rescale_tensor(tp, x.level, x.nb, om);
+                cnt_[C_MUL]++;
+                if (fa) release(x);
+                if (fb && y.data != x.data) release(y);
+                if (oa) release(a);
+                if (ob) release(b);
+                return o;
+            }
+        }
         Ct d = alloc_ct(x.level, 3 * x.nb, x.nb);
         d.pend = 1;
         launch_tensor(S(), T_, d.data, x.data, y.data, nl, qmap(), x.nb);
@@ -1716,13 +1768,34 @@ public:
             for (int j = i; j < n && (int)grp.size() < kMaxMembers; ++j)
                 if (!done[j] && pr[j].x.level == pr[i].x.level) grp.push_back(j), done[j] = true;
             const int g = (int)grp.size(), L = pr[i].x.level, nl = hp_.nl(L), nn = hp_.n;
-            Ct d = alloc_ct(L, 3 * g, g);
-            d.pend = 1;
             TensorPtrs tp;
             for (int m = 0; m < g; ++m) tp.a[m] = pr[grp[m]].x.data, tp.b[m] = pr[grp[m]].y.data;
+            const int chunk = ks_chunk(L);
+            {  // every chunk relinearised and rescaled straight from its factors (relin_rescale_tensor)
+                Ct probe;
+                probe.level = L, probe.npoly = 3 * std::min(chunk, g), probe.nb = std::min(chunk, g), probe.pend = 1, probe.ntt = true;
+                if (fused_tensor_ && !fused_conv(true) && fused_relin_rescale_ok(probe)) {
+                    cnt_[C_MUL] += g;
+                    for (int m0 = 0; m0 < g; m0 += chunk) {
+                        const int c = std::min(chunk, g - m0);
+                        TensorPtrs sub;
+                        u32* om[kMaxKsBatch];
+                        for (int m = 0; m < c; ++m) {
+                            sub.a[m] = tp.a[m0 + m], sub.b[m] = tp.b[m0 + m];
+                            Ct& r = out[grp[m0 + m]];
+                            r = alloc_ct(L - 1, 2);
+                            r.ntt = true, r.pend = 0, r.lazy = false;
+                            om[m] = r.data;
+                        }
+                        relin_rescale_tensor(sub, L, c, om);
+                    }
+                    continue;
+                }
+            }
+            Ct d = alloc_ct(L, 3 * g, g);
+            d.pend = 1;
             launch_tensor_ptrs(S(), T_, d.data, tp, g, nl, qmap());
             cnt_[C_MUL] += g;
-            const int chunk = ks_chunk(L);
             for (int m0 = 0; m0 < g; m0 += chunk) {
                 const int c = std::min(chunk, g - m0);
                 Ct v = d;  // view of members m0 .. m0 + c - 1 (not released on its own)
@@ -4049,6 +4122,8 @@ private:
     // sparse-plan diagonals as 2 dn residues per limb (group_pts; AESFHE_COMPACT_DIAG=0: full rows of
     // the same projected diagonals -- bit-identical results, the A/B and the check of the run structure)
     bool compact_diag_ = std::getenv("AESFHE_COMPACT_DIAG") == nullptr || std::getenv("AESFHE_COMPACT_DIAG")[0] != '0';
+    // mul_many: products relinearised straight from their factors (relin_rescale_tensor; AESFHE_FUSED_TENSOR=0: tensor first)
+    bool fused_tensor_ = std::getenv("AESFHE_FUSED_TENSOR") == nullptr || std::getenv("AESFHE_FUSED_TENSOR")[0] != '0';
     bool fuse_rr_ = std::getenv("AESFHE_FUSED_RESCALE") == nullptr || std::getenv("AESFHE_FUSED_RESCALE")[0] != '0';
     u32* d_pinv_ = nullptr;
     u32* d_negp_ = nullptr;

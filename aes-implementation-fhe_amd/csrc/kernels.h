@@ -141,6 +141,10 @@ struct TensorPtrs {
     const u32* b[kMaxMembers] = {};
 };
 void launch_tensor_ptrs(hipStream_t st, const DevTables& T, u32* out, const TensorPtrs& tp, int n, int nl, LimbMap map);
+// inverse NTT of the products a[g] (.) b[g] formed on load (limb i of group g at tp.a[g] + i N and
+// tp.b[g] + i N, Barrett products as k_tensor_ptrs'): a relinearisation's third tensor polynomial
+// transformed without being written (Engine::relin_rescale_tensor)
+void launch_ntt_inv_prod(hipStream_t st, const DevTables& T, u32* dst, const TensorPtrs& tp, int rows, RowMap rm, LimbMap map);
 // out = (a0 b0, a0 b1 + a1 b0, a1 b1); a, b: 2 x nl rows; out: 3 x nl rows
 // nb > 1: nb ciphertexts stacked ([m][2][nl] in, [m][3][nl] out), one launch
 void launch_tensor(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int nl, LimbMap map, int nb = 1);
@@ -230,6 +234,12 @@ struct KsFold {
     const u32* add1 = nullptr;
     size_t ms = 0;
     const u32* gad = nullptr;
+    // tensor mode (ta[0] set): member m is the product of the 2-polynomial ciphertexts ta[m], tb[m]
+    // (tnl limbs per polynomial), never materialised -- the fold's (c0, c1) and the own digit's
+    // c2 rows are formed on load as k_tensor_ptrs forms them (add0 / add1 / d unused)
+    const u32* ta[kMaxKsBatch] = {};
+    const u32* tb[kMaxKsBatch] = {};
+    int tnl = 0;
 };
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
                       int alpha, int nkey, int nks, LimbMap map, u64 g = 0, int nb = 1, size_t ext_ms = 0, size_t d_ms = 0,

@@ -390,14 +390,21 @@ __global__ void __launch_bounds__(kBlock) k_key_inner(u32* acc, const u32* ext, 
 #pragma unroll
         for (int m = 0; m < NBM; ++m) {
             if (m >= nb) break;
-            const u32* src = j == own ? d + m * d_ms + ((size_t)x << logn) : ext + m * ext_ms + (((size_t)j * ne + x) << logn);
             u32 e[4];
-            if (g) {
-#pragma unroll
-                for (int v = 0; v < 4; ++v) e[v] = src[ks[v]];
+            if (fold.ta[0] && j == own) {  // tensor mode (g == 0): the own digit's c2 = a1 (.) b1, formed here
+                const size_t at = ((size_t)(fold.tnl + x) << logn) + k;
+                const uint4 a = *reinterpret_cast<const uint4*>(fold.ta[m] + at), b = *reinterpret_cast<const uint4*>(fold.tb[m] + at);
+                e[0] = barrett_mul(a.x, b.x, P.q, P.mu), e[1] = barrett_mul(a.y, b.y, P.q, P.mu);
+                e[2] = barrett_mul(a.z, b.z, P.q, P.mu), e[3] = barrett_mul(a.w, b.w, P.q, P.mu);
             } else {
-                const uint4 t = *reinterpret_cast<const uint4*>(src + k);
-                e[0] = t.x, e[1] = t.y, e[2] = t.z, e[3] = t.w;
+                const u32* src = j == own ? d + m * d_ms + ((size_t)x << logn) : ext + m * ext_ms + (((size_t)j * ne + x) << logn);
+                if (g) {
+#pragma unroll
+                    for (int v = 0; v < 4; ++v) e[v] = src[ks[v]];
+                } else {
+                    const uint4 t = *reinterpret_cast<const uint4*>(src + k);
+                    e[0] = t.x, e[1] = t.y, e[2] = t.z, e[3] = t.w;
+                }
             }
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
@@ -414,9 +421,24 @@ __global__ void __launch_bounds__(kBlock) k_key_inner(u32* acc, const u32* ext, 
         for (int v = 0; v < 4; ++v) r0[v] = reduce64(s0[m][v], P.q, P.mu, P.r32), r1[v] = reduce64(s1[m][v], P.q, P.mu, P.r32);
         if (fold.gad && x < nl) {
             const u32 gv = fold.gad[2 * x], gp = fold.gad[2 * x + 1];
-            const size_t at = m * fold.ms + ((size_t)x << logn) + k;
-            const uint4 f0 = *reinterpret_cast<const uint4*>(fold.add0 + at), f1 = *reinterpret_cast<const uint4*>(fold.add1 + at);
-            const u32 a0v[4] = {f0.x, f0.y, f0.z, f0.w}, a1v[4] = {f1.x, f1.y, f1.z, f1.w};
+            u32 a0v[4], a1v[4];
+            if (fold.ta[0]) {  // tensor mode: c0 = a0 b0, c1 = a0 b1 + a1 b0 (k_tensor_ptrs' arithmetic)
+                const size_t at = ((size_t)x << logn) + k, o1 = (size_t)fold.tnl << logn;
+                const uint4 A0 = *reinterpret_cast<const uint4*>(fold.ta[m] + at), A1 = *reinterpret_cast<const uint4*>(fold.ta[m] + at + o1);
+                const uint4 B0 = *reinterpret_cast<const uint4*>(fold.tb[m] + at), B1 = *reinterpret_cast<const uint4*>(fold.tb[m] + at + o1);
+                const u32 a0[4] = {A0.x, A0.y, A0.z, A0.w}, a1[4] = {A1.x, A1.y, A1.z, A1.w};
+                const u32 b0[4] = {B0.x, B0.y, B0.z, B0.w}, b1[4] = {B1.x, B1.y, B1.z, B1.w};
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    a0v[v] = barrett_mul(a0[v], b0[v], P.q, P.mu);
+                    a1v[v] = add_mod(barrett_mul(a0[v], b1[v], P.q, P.mu), barrett_mul(a1[v], b0[v], P.q, P.mu), P.q);
+                }
+            } else {
+                const size_t at = m * fold.ms + ((size_t)x << logn) + k;
+                const uint4 f0 = *reinterpret_cast<const uint4*>(fold.add0 + at), f1 = *reinterpret_cast<const uint4*>(fold.add1 + at);
+                a0v[0] = f0.x, a0v[1] = f0.y, a0v[2] = f0.z, a0v[3] = f0.w;
+                a1v[0] = f1.x, a1v[1] = f1.y, a1v[2] = f1.z, a1v[3] = f1.w;
+            }
 #pragma unroll
             for (int v = 0; v < 4; ++v) {
                 r0[v] = add_mod(r0[v], shoup_mul(a0v[v], gv, gp, P.q), P.q);

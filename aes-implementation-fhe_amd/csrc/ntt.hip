@@ -407,9 +407,11 @@ __global__ void __launch_bounds__(NT, OCC) k_ntt2_fwd(u32* data, RowMap rm, Limb
 // times psi^-((N / 2^s) brv_s(t)) -- 224 per prime, shared by every row, L1 / L2 resident --
 // one more lazy Shoup product per butterfly of those stages instead of 8 twiddle bytes, so the
 // launch reads ~280 twiddle bytes per 1 KB row instead of 2 KB
-template <int LOGR1, int NT, bool FACT>
+// PROD: the input row is the product a (.) b of group g's rows (launch_ntt_inv_prod), src unused
+template <int LOGR1, int NT, bool FACT, bool PROD>
 __global__ void __launch_bounds__(NT) k_ntt2_inv(u32* dst, const u32* src, RowMap rm, LimbMap map, const PrimeConst* pc,
-                                                       const uint2* tw, const uint2* irow, const uint2* igam, unsigned long long* ts) {
+                                                       const uint2* tw, const uint2* irow, const uint2* igam, TensorPtrs tp,
+                                                       unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8;
     __shared__ u32 sm[(NT / 16) * kPitchP2];
     if (skipped(rm)) return;
@@ -420,11 +422,24 @@ __global__ void __launch_bounds__(NT) k_ntt2_inv(u32* dst, const u32* src, RowMa
     const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
     const int R = blockIdx.x * (NT / 16) + r;
     u32 x[16];
-    const uint4* in = reinterpret_cast<const uint4*>(ra.src + (size_t)R * 256 + 16 * j);
+    if (PROD) {
+        const u32 mu = pc[ra.prime].mu;
+        const size_t off = ((size_t)blockIdx.y << LOGN) + (size_t)R * 256 + 16 * j;
+        const uint4* pa = reinterpret_cast<const uint4*>(tp.a[blockIdx.z] + off);
+        const uint4* pb = reinterpret_cast<const uint4*>(tp.b[blockIdx.z] + off);
 #pragma unroll
-    for (int v = 0; v < 4; ++v) {
-        const uint4 t = in[v];
-        x[4 * v] = t.x, x[4 * v + 1] = t.y, x[4 * v + 2] = t.z, x[4 * v + 3] = t.w;
+        for (int v = 0; v < 4; ++v) {
+            const uint4 a = pa[v], b = pb[v];
+            x[4 * v] = barrett_mul(a.x, b.x, q, mu), x[4 * v + 1] = barrett_mul(a.y, b.y, q, mu);
+            x[4 * v + 2] = barrett_mul(a.z, b.z, q, mu), x[4 * v + 3] = barrett_mul(a.w, b.w, q, mu);
+        }
+    } else {
+        const uint4* in = reinterpret_cast<const uint4*>(ra.src + (size_t)R * 256 + 16 * j);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const uint4 t = in[v];
+            x[4 * v] = t.x, x[4 * v + 1] = t.y, x[4 * v + 2] = t.z, x[4 * v + 3] = t.w;
+        }
     }
     const uint2* rowf = irow + ((size_t)ra.prime << LOGR1) * 4 + (size_t)R * 4;
     const uint2* gam = igam + ((size_t)ra.prime << 8);
@@ -588,34 +603,42 @@ inline bool inv_fact_on() {
 }
 template <int LOGR1, int NT>
 void ntt2_inv_launch(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, RowMap rm, LimbMap map, int groups, double io,
-                     double work) {
+                     double work, const TensorPtrs* tp) {
     const dim3 grid(R1_of<LOGR1>() / (NT / 16), rm.cnt, groups);
+    if (tp) {
+        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, true, true>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
+                        Tb.irow, Tb.igam, *tp);
+        return;
+    }
+    static const TensorPtrs kNone{};
     if (inv_fact_on())
-        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, true>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
-                        Tb.irow, Tb.igam);
+        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, true, false>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
+                        Tb.irow, Tb.igam, kNone);
     else
-        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, false>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
-                        Tb.irow, Tb.igam);
+        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, false, false>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
+                        Tb.irow, Tb.igam, kNone);
 }
 template <int LOGR1>
-void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map, const u32* post) {
+void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map, const u32* post,
+               const TensorPtrs* tp = nullptr) {
     constexpr int R1 = 1 << LOGR1;
     rm.nrows = rows;
     const int groups = (rows + rm.cnt - 1) / rm.cnt;
     const double io = 4.0 * 2.0 * rows * (256.0 * R1);  // the inverse is never launched with skips
+    const double io2 = tp ? 4.0 * 3.0 * rows * (256.0 * R1) : io;  // the product form reads two rows
     const double bfly = (double)rows * 128.0 * R1;
     if (small_launch(rows)) {
         constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
-        ntt2_inv_launch<LOGR1, NT>(st, Tb, dst, src, rm, map, groups, io, bfly * 8.0);
+        ntt2_inv_launch<LOGR1, NT>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp);
         prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, dst, rm, map,
                         Tb.pc, Tb.itw, post);
         return;
     }
     constexpr int CB = kThreads / (R1 / 16);
     switch (p2_nt(true)) {
-        case 128: ntt2_inv_launch<LOGR1, 128>(st, Tb, dst, src, rm, map, groups, io, bfly * 8.0); break;
-        case 256: ntt2_inv_launch<LOGR1, 256>(st, Tb, dst, src, rm, map, groups, io, bfly * 8.0); break;
-        default: ntt2_inv_launch<LOGR1, kThreads>(st, Tb, dst, src, rm, map, groups, io, bfly * 8.0); break;
+        case 128: ntt2_inv_launch<LOGR1, 128>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp); break;
+        case 256: ntt2_inv_launch<LOGR1, 256>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp); break;
+        default: ntt2_inv_launch<LOGR1, kThreads>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp); break;
     }
     prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, kThreads>, dim3(256 / CB, rm.cnt, groups), dim3(kThreads), 0, st, dst, rm,
                     map, Tb.pc, Tb.itw, post);
@@ -755,6 +778,16 @@ void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* dst, const u32* src
         case 14: ntt_inv_t<6>(st, T, dst, src, rows, rm, map, post); break;
         case 15: ntt_inv_t<7>(st, T, dst, src, rows, rm, map, post); break;
         case 16: ntt_inv_t<8>(st, T, dst, src, rows, rm, map, post); break;
+        default: break;
+    }
+}
+void launch_ntt_inv_prod(hipStream_t st, const DevTables& T, u32* dst, const TensorPtrs& tp, int rows, RowMap rm, LimbMap map) {
+    if (rows <= 0) return;
+    switch (T.logn) {
+        case 13: ntt_inv_t<5>(st, T, dst, nullptr, rows, rm, map, nullptr, &tp); break;
+        case 14: ntt_inv_t<6>(st, T, dst, nullptr, rows, rm, map, nullptr, &tp); break;
+        case 15: ntt_inv_t<7>(st, T, dst, nullptr, rows, rm, map, nullptr, &tp); break;
+        case 16: ntt_inv_t<8>(st, T, dst, nullptr, rows, rm, map, nullptr, &tp); break;
         default: break;
     }
 }
