@@ -1545,12 +1545,19 @@ public:
         cnt_[C_RELIN]++;
         return o;
     }
+    // the 2 x - c epilogue per member of a relinearisation + rescale (EvalMod's 2 T^2 - 1, the
+    // residues of lincomb(P, 2, nullptr, 0, -c, 0)): dbl bit m doubles member m, cst[m] its constant
+    struct Affine {
+        unsigned dbl = 0;
+        const u32* cst[kMaxKsBatch] = {};
+        bool any() const { return dbl != 0; }
+    };
     // relin_rescale of the products a[m] * b[m] (2-polynomial ciphertexts at one level, NTT form,
     // pend 0; nb <= ks_chunk) without materialising their tensors: the ModUp's inverse NTT forms
     // c2 = a1 (.) b1 on load, k_key_inner forms the own digit's c2 and the fold's (c0, c1) -- the
     // residues k_tensor_ptrs would have written, so the result is the same bit for bit, one launch
     // and 3 written + 3 re-read tensor rows per limb fewer (AESFHE_FUSED_TENSOR=0: tensor first)
-    void relin_rescale_tensor(const TensorPtrs& tp, int l, int nb, u32* const* outm) {
+    void relin_rescale_tensor(const TensorPtrs& tp, int l, int nb, u32* const* outm, const Affine* af = nullptr) {
         const int n = hp_.n, nl = hp_.nl(l), ne = nl + hp_.n_p;
         if (nb > ks_chunk(l) || nb > kMaxKsBatch) throw std::runtime_error("relin_rescale_tensor: more members than one chunk");
         TensorPtrs t1;  // a1, b1
@@ -1564,19 +1571,32 @@ public:
         u32* acc = tmp(2 * (size_t)ne * nb);
         key_inner(acc, ext, nullptr, ksk(0), l, 0, nb, 0, f);
         untmp(ext, (size_t)nb * ext_rows(l));
-        Ct o = moddown_rescale(acc, l, nb, nullptr, outm);
+        Ct o = moddown_rescale(acc, l, nb, nullptr, outm, af);
         (void)o;
         untmp(acc, 2 * (size_t)ne * nb);
         cnt_[C_KS] += nb;
         cnt_[C_RELIN]++;
     }
+    // device residues of the constant -c at (level, pend 0), [limb][lo, hi] (k_lincomb's cadd), cached
+    const u32* affine_const(int level, double c) {
+        const auto key = std::make_pair(level, c);
+        auto it = affine_cst_.find(key);
+        if (it != affine_cst_.end()) return it->second;
+        const LimbConsts lc = add_consts(level, 0, -c, 0.0);
+        const int nl = hp_.nl(level);
+        u32* d = dev_alloc((size_t)2 * nl);
+        HIP_OK(hipMemcpy(d, lc.v, sizeof(u32) * 2 * nl, hipMemcpyHostToDevice));
+        return affine_cst_[key] = d;
+    }
+    std::map<std::pair<int, double>, const u32*> affine_cst_;
     // acc = [m][2][ne] in Q*P, NTT form, already holding P * (the ciphertext) -> the ciphertext
     // divided by the dropped limbs of level l, at level l - 1 (one ModDown by Q' = P * D)
-    Ct moddown_rescale(const u32* acc, int l, int nb, u32* dst = nullptr, u32* const* outm = nullptr) {
+    Ct moddown_rescale(const u32* acc, int l, int nb, u32* dst = nullptr, u32* const* outm = nullptr, const Affine* af = nullptr) {
         const int n = hp_.n, nl = hp_.nl(l), r = hp_.nl(l - 1), k = nl - r, np = hp_.n_p, ne = nl + np;
         const int npl = 2 * nb, h = k + np;
         if (mdr_off_[l] == SIZE_MAX || npl > kMaxConvGroups) throw std::runtime_error("moddown_rescale: unsupported level or batch");
         const bool fz = fused_conv(false);
+        if (fz && af && af->any()) throw std::runtime_error("moddown_rescale: the epilogue needs the separate conversion");
         const size_t off = mdr_off_[l];
         u32* ys = tmp((size_t)npl * h);
         intt(ys, acc, npl * h, RowMap{h, ne, h, r, 0}, LimbMap{k, r, hp_.p_off()}, fz ? d_mdr_ + off + 2 * (size_t)h * r : nullptr);
@@ -1602,7 +1622,8 @@ public:
         if (fz)
             launch_ntt_finish_conv(S(), T_, o.data, conv, cb, acc, ne, qinv, nullptr, nullptr, npl, r, 0, outm);
         else
-            launch_ntt_finish(S(), T_, o.data, conv, acc, ne, qinv, nullptr, nullptr, npl, r, 0, outm);
+            launch_ntt_finish(S(), T_, o.data, conv, acc, ne, qinv, nullptr, nullptr, npl, r, 0, outm, af ? af->dbl : 0u,
+                              af && af->any() ? af->cst : nullptr);
         untmp(ys, (size_t)npl * h);
         cnt_[C_NTT_ROWS] += (size_t)npl * r;
         untmp(conv, (size_t)npl * r);
@@ -1613,7 +1634,9 @@ public:
     // ct x ct.  Inputs are brought to canonical form; the tensor owes one rescale.  relin:
     // key switch now (eager) or leave it to the first consumer that needs two polynomials
     // (lazy)
-    Ct mul(const Ct& a_in, const Ct& b_in, bool relin, bool lazy = false) {
+    // aff (relin, not lazy): the product's 2 P - 1 (EvalMod's 2 T^2 - 1) instead of P -- in the
+    // relinearisation's finish when it is fused (Affine), else one lincomb after it
+    Ct mul(const Ct& a_in, const Ct& b_in, bool relin, bool lazy = false, bool aff = false) {
         if (vis_npoly(a_in) != 2 || vis_npoly(b_in) != 2) throw std::runtime_error("multiply expects 2-polynomial ciphertexts");
         if (a_in.level - a_in.pend < 1 || b_in.level - b_in.pend < 1)
             throw std::runtime_error("not enough level to multiply (level 0)");
@@ -1634,8 +1657,12 @@ public:
                 TensorPtrs tp;
                 u32* om[kMaxKsBatch];
                 const size_t ms = (size_t)2 * nl * hp_.n, oms = (size_t)2 * hp_.nl(x.level - 1) * hp_.n;
-                for (int m = 0; m < x.nb; ++m) tp.a[m] = x.data + m * ms, tp.b[m] = y.data + m * ms, om[m] = o.data + m * oms;
-                relin_rescale_tensor(tp, x.level, x.nb, om);
+                Affine af;
+                for (int m = 0; m < x.nb; ++m) {
+                    tp.a[m] = x.data + m * ms, tp.b[m] = y.data + m * ms, om[m] = o.data + m * oms;
+                    if (aff) af.dbl |= 1u << m, af.cst[m] = affine_const(x.level - 1, 1.0);
+                }
+                relin_rescale_tensor(tp, x.level, x.nb, om, aff ? &af : nullptr);
                 cnt_[C_MUL]++;
                 if (fa) release(x);
                 if (fb && y.data != x.data) release(y);
@@ -1657,25 +1684,31 @@ public:
             d.lazy = true;
             return d;
         }
+        Ct o;
         if (fused_relin_rescale_ok(d)) {
-            Ct o = relin_rescale(d);
+            o = relin_rescale(d);
             release(d);
-            return o;
+        } else {
+            Ct r = relin_raw(d);
+            release(d);
+            o = rescale(r);
+            release(r);
         }
-        Ct r = relin_raw(d);
-        release(d);
-        Ct o = rescale(r);
-        release(r);
-        return o;
+        if (!aff) return o;
+        Ct t = lincomb(o, 2, nullptr, 0, -1.0, 0.0);
+        release(o);
+        return t;
     }
 
     // n independent products a_i b_i, relinearised and rescaled, batched:
     // pairs whose aligned operands sit at one level share ONE tensor launch and one fused
     // relinearisation + rescale per chunk of kMaxKsBatch members (each key residue read once
     // per chunk, every launch carrying the chunk's rows); the results equal n mul() calls
-    std::vector<Ct> mul_many(const std::vector<const Ct*>& A, const std::vector<const Ct*>& B) {
+    // aff (nullable, one flag per pair): that product's 2 P - 1 (mul's aff)
+    std::vector<Ct> mul_many(const std::vector<const Ct*>& A, const std::vector<const Ct*>& B, const std::vector<char>* aff = nullptr) {
         const int n = (int)A.size();
         std::vector<Ct> out(n);
+        auto affi = [&](int i) { return aff && (*aff)[i]; };
         bool batch = batch_ops_ && n >= 2;
         for (int i = 0; i < n; ++i) {
             if (vis_npoly(*A[i]) != 2 || vis_npoly(*B[i]) != 2) throw std::runtime_error("multiply expects 2-polynomial ciphertexts");
@@ -1684,7 +1717,7 @@ public:
             batch = batch && A[i]->nb == 1 && B[i]->nb == 1;
         }
         if (!batch) {
-            for (int i = 0; i < n; ++i) out[i] = mul(*A[i], *B[i], true, false);
+            for (int i = 0; i < n; ++i) out[i] = mul(*A[i], *B[i], true, false, affi(i));
             return out;
         }
         struct Prep {
@@ -1780,14 +1813,16 @@ public:
                         const int c = std::min(chunk, g - m0);
                         TensorPtrs sub;
                         u32* om[kMaxKsBatch];
+                        Affine af;
                         for (int m = 0; m < c; ++m) {
                             sub.a[m] = tp.a[m0 + m], sub.b[m] = tp.b[m0 + m];
                             Ct& r = out[grp[m0 + m]];
                             r = alloc_ct(L - 1, 2);
                             r.ntt = true, r.pend = 0, r.lazy = false;
                             om[m] = r.data;
+                            if (affi(grp[m0 + m])) af.dbl |= 1u << m, af.cst[m] = affine_const(L - 1, 1.0);
                         }
-                        relin_rescale_tensor(sub, L, c, om);
+                        relin_rescale_tensor(sub, L, c, om, af.any() ? &af : nullptr);
                     }
                     continue;
                 }
@@ -1820,6 +1855,12 @@ public:
                 }
             }
             release(d);
+            for (int m = 0; m < g; ++m)  // the tensor-first form: 2 P - 1 as its own launch
+                if (affi(grp[m])) {
+                    Ct t = lincomb(out[grp[m]], 2, nullptr, 0, -1.0, 0.0);
+                    release(out[grp[m]]);
+                    out[grp[m]] = t;
+                }
         }
         for (const Ct& c : owned) release(c);  // stream-ordered: the tensors above were queued first
         return out;
@@ -3277,11 +3318,11 @@ public:
         return out;
     }
     // products of a list of pairs: one batched multiply (AESFHE_EVALMOD_BATCH=0: one at a time)
-    std::vector<Ct> mul_list(const std::vector<const Ct*>& A, const std::vector<const Ct*>& B) {
+    std::vector<Ct> mul_list(const std::vector<const Ct*>& A, const std::vector<const Ct*>& B, const std::vector<char>* aff = nullptr) {
         static const bool batch = env_int("AESFHE_EVALMOD_BATCH", 1) != 0;
-        if (batch) return mul_many(A, B);
+        if (batch) return mul_many(A, B, aff);
         std::vector<Ct> P(A.size());
-        for (size_t j = 0; j < A.size(); ++j) P[j] = mul(*A[j], *B[j], true);
+        for (size_t j = 0; j < A.size(); ++j) P[j] = mul(*A[j], *B[j], true, false, aff && (*aff)[j]);
         return P;
     }
     static constexpr int kBabyDeg = 8;
@@ -3303,14 +3344,20 @@ public:
         for (int lo = 2; lo <= kBabyDeg;) {
             const int hi = batch_baby ? std::min(kBabyDeg, 2 * lo - 2) : lo;
             std::vector<const Ct*> A, B;
+            std::vector<char> aff;  // 2 T_a^2 - 1 in the product's own relinearisation (fused_affine_)
             for (int i = 0; i < ni; ++i)
-                for (int k = lo; k <= hi; ++k) A.push_back(&T[i][(k + 1) / 2]), B.push_back(&T[i][k / 2]);
-            std::vector<Ct> P = mul_list(A, B);
+                for (int k = lo; k <= hi; ++k)
+                    A.push_back(&T[i][(k + 1) / 2]), B.push_back(&T[i][k / 2]), aff.push_back(fused_affine_ && (k + 1) / 2 == k / 2);
+            std::vector<Ct> P = mul_list(A, B, &aff);
             int j = 0;
             for (int i = 0; i < ni; ++i)
                 for (int k = lo; k <= hi; ++k, ++j) {
                     const int a = (k + 1) / 2, b = k / 2;
-                    // 2 T_a T_b - T_(a-b) (a > b) / 2 T_a^2 - 1, one launch each
+                    // 2 T_a T_b - T_(a-b) (a > b) / 2 T_a^2 - 1, one launch each (none for the latter when fused)
+                    if (aff[j]) {
+                        T[i][k] = P[j];
+                        continue;
+                    }
                     T[i][k] = (a == b) ? lincomb(P[j], 2, nullptr, 0, -1.0, 0.0) : lincomb(P[j], 2, &T[i][a - b], -1, 0.0, 0.0);
                     release(P[j]);
                 }
@@ -3321,8 +3368,13 @@ public:
         for (int m = 2 * kBabyDeg; m <= d; m *= 2) {
             std::vector<const Ct*> A;
             for (int i = 0; i < ni; ++i) A.push_back(&giant[i].at(m / 2));
-            std::vector<Ct> P = mul_list(A, A);
+            const std::vector<char> aff(ni, fused_affine_ ? 1 : 0);
+            std::vector<Ct> P = mul_list(A, A, &aff);
             for (int i = 0; i < ni; ++i) {
+                if (fused_affine_) {
+                    giant[i][m] = P[i];
+                    continue;
+                }
                 giant[i][m] = lincomb(P[i], 2, nullptr, 0, -1.0, 0.0);  // 2 T^2 - 1, one launch
                 release(P[i]);
             }
@@ -3338,9 +3390,14 @@ public:
         for (int it = 0; it < bs_.plan.r; ++it) {
             std::vector<const Ct*> A;
             for (int i = 0; i < ni; ++i) A.push_back(&g[i]);
-            std::vector<Ct> P = mul_list(A, A);
+            const std::vector<char> aff(ni, fused_affine_ ? 1 : 0);
+            std::vector<Ct> P = mul_list(A, A, &aff);
             for (int i = 0; i < ni; ++i) {
                 release(g[i]);
+                if (fused_affine_) {
+                    g[i] = P[i];
+                    continue;
+                }
                 g[i] = lincomb(P[i], 2, nullptr, 0, -1.0, 0.0);  // double angle 2 g^2 - 1, one launch
                 release(P[i]);
             }
@@ -4124,6 +4181,8 @@ private:
     bool compact_diag_ = std::getenv("AESFHE_COMPACT_DIAG") == nullptr || std::getenv("AESFHE_COMPACT_DIAG")[0] != '0';
     // mul_many: products relinearised straight from their factors (relin_rescale_tensor; AESFHE_FUSED_TENSOR=0: tensor first)
     bool fused_tensor_ = std::getenv("AESFHE_FUSED_TENSOR") == nullptr || std::getenv("AESFHE_FUSED_TENSOR")[0] != '0';
+    // EvalMod's 2 T^2 - 1 in the product's relinearisation finish (AESFHE_FUSED_AFFINE=0: one lincomb each)
+    bool fused_affine_ = std::getenv("AESFHE_FUSED_AFFINE") == nullptr || std::getenv("AESFHE_FUSED_AFFINE")[0] != '0';
     bool fuse_rr_ = std::getenv("AESFHE_FUSED_RESCALE") == nullptr || std::getenv("AESFHE_FUSED_RESCALE")[0] != '0';
     u32* d_pinv_ = nullptr;
     u32* d_negp_ = nullptr;

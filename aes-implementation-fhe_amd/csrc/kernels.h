@@ -94,6 +94,11 @@ struct NttAux {
     // finish: member m's result (groups 2m, 2m + 1) written to outm[m] (2 polys x out_stride rows)
     // when set -- the members of a batched key switch straight into their own buffers, no unstack copy
     u32* outm[8] = {};
+    // finish epilogue per member m (groups 2m, 2m + 1): (dbl >> m & 1) doubles the result, then
+    // cst[m] (nullable, [limb][lo, hi] residues) is added to its polynomial 0 -- an EvalMod
+    // 2 x^2 - c in the relinearisation's own launch, the residues of k_lincomb's (Engine::Affine)
+    unsigned dbl = 0;
+    const u32* cst[8] = {};
 };
 // out-of-place (src may equal dst); supported ring sizes 2^13 .. 2^16
 void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map);
@@ -112,8 +117,10 @@ void launch_rescale2_ntt(hipStream_t st, const DevTables& T, u32* out, const u32
 // NTT of conv (npoly x nt dense rows, destroyed) fused with
 // out[p][t] = (cur[p * cur_stride + t] - NTT(conv)[p][t]) * qinv_t (+ add_p[t])   (ModDown)
 // npoly = 2 nb for nb batched ciphertexts: group 2 m + p adds add_p + m add_mstride (words)
+// dbl / cst: NttAux's per-member epilogue 2 r + c (cst: nb entries, nullable)
 void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, const u32* cur, int cur_stride, const u32* qinv,
-                       const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride = 0, u32* const* outm = nullptr);
+                       const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride = 0, u32* const* outm = nullptr,
+                       unsigned dbl = 0, const u32* const* cst = nullptr);
 // in place on rows = npoly * nl dense rows
 void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map);
 void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map);

@@ -379,6 +379,12 @@ __global__ void __launch_bounds__(NT, OCC) k_ntt2_fwd(u32* data, RowMap rm, Limb
         uint4* o = reinterpret_cast<uint4*>((om ? om + ((size_t)((grp & 1) * aux.out_stride + li) << LOGN)
                                                : aux.out + ((size_t)(grp * aux.out_stride + li) << LOGN)) + woff);
         const u32 qi = aux.qinv[2 * li], qip = aux.qinv[2 * li + 1];
+        // the epilogue 2 r + c (aux.dbl / aux.cst, block-uniform): c on polynomial 0 only, its
+        // half (lo / hi slots) by the row -- words R 256 .. of the limb lie in half R >= R1 / 2
+        const int mem = (grp >> 1) & 7;
+        const bool dbl = (aux.dbl >> mem) & 1u;
+        const u32* cs = (grp & 1) ? nullptr : aux.cst[mem];
+        const u32 cadd = cs ? cs[2 * li + (R >= (1 << LOGR1) / 2 ? 1 : 0)] : 0u;
 #pragma unroll
         for (int v = 0; v < 4; ++v) {
             const uint4 cv = cvp[v];
@@ -391,6 +397,8 @@ __global__ void __launch_bounds__(NT, OCC) k_ntt2_fwd(u32* data, RowMap rm, Limb
                 const uint4 a = avp[v];
                 r.x = add_mod(r.x, a.x, q), r.y = add_mod(r.y, a.y, q), r.z = add_mod(r.z, a.z, q), r.w = add_mod(r.w, a.w, q);
             }
+            if (dbl) r.x = add_mod(r.x, r.x, q), r.y = add_mod(r.y, r.y, q), r.z = add_mod(r.z, r.z, q), r.w = add_mod(r.w, r.w, q);
+            if (cs) r.x = add_mod(r.x, cadd, q), r.y = add_mod(r.y, cadd, q), r.z = add_mod(r.z, cadd, q), r.w = add_mod(r.w, cadd, q);
             o[v] = r;
         }
     } else {
@@ -761,13 +769,20 @@ void launch_rescale2_ntt(hipStream_t st, const DevTables& T, u32* out, const u32
     ntt_fwd_dispatch<kSpread2, kFinish>(st, T, v, last, npoly * nt, npoly * nt, rm, LimbMap{1 << 30, 0, 0}, aux);
 }
 void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, const u32* cur, int cur_stride, const u32* qinv,
-                       const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride, u32* const* outm) {
+                       const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride, u32* const* outm, unsigned dbl,
+                       const u32* const* cst) {
     NttAux aux{};
     aux.cur = cur, aux.out = out, aux.qinv = qinv, aux.cur_stride = cur_stride, aux.out_stride = nt, aux.add0 = add0, aux.add1 = add1;
     aux.add_mstride = add_mstride;
     if (outm) {
         if (npoly > 16 || npoly % 2) throw std::runtime_error("launch_ntt_finish: per-member outputs for at most 8 two-polynomial members");
         for (int m = 0; m < npoly / 2; ++m) aux.outm[m] = outm[m];
+    }
+    if (dbl || cst) {
+        if (npoly > 16 || npoly % 2) throw std::runtime_error("launch_ntt_finish: the 2 r + c epilogue for at most 8 two-polynomial members");
+        aux.dbl = dbl;
+        if (cst)
+            for (int m = 0; m < npoly / 2; ++m) aux.cst[m] = cst[m];
     }
     ntt_fwd_dispatch<kPlain, kFinish>(st, T, conv, conv, npoly * nt, npoly * nt, rows_dense(nt), LimbMap{1 << 30, 0, 0}, aux);
 }

@@ -170,3 +170,27 @@ def test_compact_diagonals_bit_identical(logn, monkeypatch):
         outs.append(res)
         del E
     assert all(x == y for x, y in zip(outs[0], outs[1]))
+
+
+@pytest.mark.parametrize("logn", [13, 16])
+def test_fused_relin_epilogue_bit_identical(logn, monkeypatch):
+    """Products relinearised straight from their factors (AESFHE_FUSED_TENSOR) and EvalMod's
+    2 T^2 - 1 in the relinearisation's finish (AESFHE_FUSED_AFFINE) against the tensor-first,
+    lincomb-after forms: the same sparse and full-slot bootstraps bit for bit."""
+    from engine_context import EngineContext
+    from mi355x_ckks import Engine
+    outs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("AESFHE_FUSED_TENSOR", flag)
+        monkeypatch.setenv("AESFHE_FUSED_AFFINE", flag)
+        if logn == 13:
+            E = Engine(log_n=13, use_bootstrap=True, max_level=3, dnum=5, seed=7, allow_insecure=True, enc_nonce=0)
+        else:
+            E = EngineContext(signature=1, max_level=17, log_n=16, seed=0x5EED, enc_nonce=0).engine
+        rng = np.random.default_rng(4)
+        res = [E.export(E.bootstrap_sparse(E.encrypt(_periodic(E, 32, rng)), 32)).tobytes()]
+        full = E.encrypt(0.5 * np.exp(2j * np.pi * rng.random(E.slot_count)))
+        res.append(E.export(E.bootstrap(full)).tobytes())
+        outs.append(res)
+        del E
+    assert all(x == y for x, y in zip(outs[0], outs[1]))
