@@ -1471,7 +1471,9 @@ void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* e
     if (fold.gad && g) throw std::runtime_error("launch_key_inner: fold with an automorphism");
     // per ciphertext ext/d (nd x ne) read and acc (2 x ne) written; the key (nd x 2 x ne) once;
     // the fold reads 2 x nl more rows per ciphertext
-    const double fw = (fold.gad ? 2.0 * nb * nl : 0.0) + (accum ? 2.0 * nb * ne : 0.0);
+    // tensor mode (fold.ta): the fold reads a0, a1, b0, b1 and the own digit a1, b1 (one row more
+    // per q limb than the materialised c2) instead of c0, c1
+    const double fw = (fold.gad ? (fold.ta[0] ? 5.0 : 2.0) * nb * nl : 0.0) + (accum ? 2.0 * nb * ne : 0.0);
     const double bytes = words(((nb * (nd + 2.0) + 2.0 * nd) * ne + fw) * (1u << T.logn));
     const dim3 grid((1u << T.logn) / (4 * kBlock), ne);
     // register footprint follows the batch: 1, 2, 4 or 8 ciphertexts; up to 4, the digit count
