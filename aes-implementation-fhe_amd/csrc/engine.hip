@@ -521,7 +521,9 @@ public:
     // delta_f q_{nl(f)}) encrypted together: ONE sampling launch for every v, e0, e1, ONE NTT of
     // all of them, ONE combine, ONE rescale of the stacked result (nb = B) -- the same residues as
     // B encrypt_ntt calls (same PRNG streams, same arithmetic), 8 launches instead of 14 B
-    Ct encrypt_many(const u32* m, int B, size_t m_ms, int level = -1) {
+    // m_coef: m is in coefficient form and rides in e0 through the samples' NTT (launch_sample_enc),
+    // the same residues as NTT(m) added in the combine
+    Ct encrypt_many(const u32* m, int B, size_t m_ms, int level = -1, bool m_coef = false) {
         if (B < 1 || B > kEncMax) throw std::runtime_error("encrypt_many: batch too large");
         const int f = level < 0 ? hp_.fresh : level;
         const int nq = hp_.nl(f) + 1;
@@ -529,10 +531,10 @@ public:
         EncCtrs ec;
         ec.base = enc_ctr_;  // member b: counter base + b, as B single encryptions in a row
         enc_ctr_ += B;
-        launch_sample_enc(S(), T_, vee, nq, B, enc_key(), ec);
+        launch_sample_enc(S(), T_, vee, nq, B, enc_key(), ec, m_coef ? m : nullptr, m_ms);
         ntt(vee, B * 3 * nq, nq, qmap());
         Ct top = alloc_ct(f + 1, 2 * B, B);
-        launch_enc_combine(S(), T_, top.data, vee, m, m_ms, d_pk_, hp_.n_q, nq, B);
+        launch_enc_combine(S(), T_, top.data, vee, m_coef ? nullptr : m, m_ms, d_pk_, hp_.n_q, nq, B);
         untmp(vee, (size_t)B * 3 * nq);
         Ct out = rescale(top);
         release(top);
@@ -2527,8 +2529,8 @@ public:
             launch_fft2(S(), T_, w, -1, n_out);
             launch_encode_untwist(S(), T_, m, w, enc_scale, nq, n_out);
         }
-        ntt(m, (single ? 1 : 2) * nq, nq, qmap());
-        Ct enc = encrypt_many(m, n_out, (size_t)nq * n, f);  // both re-encryptions in one set of launches
+        // both re-encryptions in one set of launches, the coefficient-form message added to e0
+        Ct enc = encrypt_many(m, n_out, (size_t)nq * n, f, true);
         if (n_out == 1) {
             enc.nb = 1;
             *oh = put_ct(enc);
@@ -2618,8 +2620,7 @@ public:
         untmp(zb, (size_t)4 * chin);
         untmp(wb, (size_t)4 * chout);
         untmp(x, (size_t)4 * chin);
-        ntt(m, chout * nq, nq, qmap());
-        Ct enc = encrypt_many(m, chout, (size_t)nq * n, f);
+        Ct enc = encrypt_many(m, chout, (size_t)nq * n, f, true);
         untmp(m, (size_t)chout * nq);
         if (n_out == 1) {
             *oh = put_ct(enc);

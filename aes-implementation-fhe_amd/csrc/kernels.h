@@ -342,7 +342,11 @@ struct EncCtrs {
     u64 base = 0;  // member m uses encryption counter base + m
 };
 // out: [m][3][nl] (v, e0, e1 residues, coefficient form)
-void launch_sample_enc(hipStream_t st, const DevTables& T, u32* out, int nl, int nm, const PrngKey& key, const EncCtrs& ctr);
+// msg (nullable): coefficient-form messages (member m at msg + m msg_ms) added to e0 before the
+// NTT -- NTT(e0 + m) = NTT(e0) + NTT(m) residue for residue, so the combine then adds none and
+// the message needs no NTT launch of its own (the renorms' re-encryption)
+void launch_sample_enc(hipStream_t st, const DevTables& T, u32* out, int nl, int nm, const PrngKey& key, const EncCtrs& ctr,
+                       const u32* msg = nullptr, size_t msg_ms = 0);
 // top: [m][2][nl]; vee: [m][3][nl] NTT form; msg: member m at msg + m msg_ms words; pk: [2][pk_rows][N]
 void launch_enc_combine(hipStream_t st, const DevTables& T, u32* top, const u32* vee, const u32* msg, size_t msg_ms, const u32* pk,
                         int pk_rows, int nl, int nm);

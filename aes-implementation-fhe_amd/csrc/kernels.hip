@@ -627,16 +627,19 @@ __global__ void k_sample_small(u32* out, int nl, LimbMap map, PrngKey key, u64 s
     }
 }
 // v (ternary), e0, e1 (binomial) of nm encryptions: grid (N / kBlock, 3 nm), row block y = 3 m + w
-__global__ void k_sample_enc(u32* out, int nl, PrngKey key, EncCtrs ctr, const PrimeConst* pc, int logn) {
+__global__ void k_sample_enc(u32* out, int nl, PrngKey key, EncCtrs ctr, const u32* msg, size_t msg_ms, const PrimeConst* pc, int logn) {
     const int y = blockIdx.y, m = y / 3, w = y - 3 * m;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const u64 stream = ((u64)(6 + w) << 56) | (ctr.base + (u64)m);  // stream_id(6 + w, 0, ctr)
     const u64 r = chacha_u64(key, stream, k);
     const int v = w == 0 ? (int)(r % 3) - 1 : __popcll(r & 0x1FFFFFull) - __popcll((r >> 21) & 0x1FFFFFull);
     u32* o = out + ((size_t)y * nl << logn);
+    const u32* mm = (msg && w == 1) ? msg + m * msg_ms : nullptr;  // e0 + message (launch_sample_enc)
     for (int l = 0; l < nl; ++l) {
         const u32 q = pc[l].q;
-        o[((size_t)l << logn) + k] = v >= 0 ? (u32)v : q - (u32)(-v);
+        u32 x = v >= 0 ? (u32)v : q - (u32)(-v);
+        if (mm) x = add_mod(x, mm[((size_t)l << logn) + k], q);
+        o[((size_t)l << logn) + k] = x;
     }
 }
 // c0 = (e0 + msg) + pk0 v, c1 = e1 + pk1 v (the add / fma sequence of Engine::encrypt_ntt, bit for bit)
@@ -648,7 +651,7 @@ __global__ void k_enc_combine(u32* top, const u32* vee, const u32* msg, size_t m
     const size_t row = (size_t)l << logn, pl = (size_t)nl << logn;
     const u32* V = vee + (size_t)m * 3 * pl;
     const u32 v = V[row + k], e0 = V[pl + row + k], e1 = V[2 * pl + row + k];
-    const u32 mv = msg[m * msg_ms + row + k];
+    const u32 mv = msg ? msg[m * msg_ms + row + k] : 0u;  // null: the message rode in e0 (launch_sample_enc)
     u32* o = top + (size_t)m * 2 * pl;
     o[row + k] = add_mod(add_mod(e0, mv, P.q), barrett_mul(pk[row + k], v, P.q, P.mu), P.q);
     o[pl + row + k] = add_mod(e1, barrett_mul(pk[((size_t)pk_rows << logn) + row + k], v, P.q, P.mu), P.q);
@@ -1544,14 +1547,15 @@ void launch_sample_small(hipStream_t st, const DevTables& T, u32* out, int nl, L
     prof_launch(KID_SAMPLE, words((double)nl * (1u << T.logn)), k_sample_small, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, nl, map, key, stream, kind, T.pc,
                        T.logn);
 }
-void launch_sample_enc(hipStream_t st, const DevTables& T, u32* out, int nl, int nm, const PrngKey& key, const EncCtrs& ctr) {
+void launch_sample_enc(hipStream_t st, const DevTables& T, u32* out, int nl, int nm, const PrngKey& key, const EncCtrs& ctr, const u32* msg,
+                       size_t msg_ms) {
     if (nm < 1 || nm > kEncMax) throw std::runtime_error("launch_sample_enc: too many encryptions");
-    prof_launch(KID_SAMPLE, words(3.0 * nm * nl * (1u << T.logn)), k_sample_enc, dim3((1u << T.logn) / kBlock, 3 * nm), dim3(kBlock), 0, st,
-                out, nl, key, ctr, T.pc, T.logn);
+    prof_launch(KID_SAMPLE, words((3.0 + (msg ? 1.0 : 0.0)) * nm * nl * (1u << T.logn)), k_sample_enc, dim3((1u << T.logn) / kBlock, 3 * nm),
+                dim3(kBlock), 0, st, out, nl, key, ctr, msg, msg_ms, T.pc, T.logn);
 }
 void launch_enc_combine(hipStream_t st, const DevTables& T, u32* top, const u32* vee, const u32* msg, size_t msg_ms, const u32* pk,
                         int pk_rows, int nl, int nm) {
-    prof_launch(KID_ELEMENTWISE, words((3.0 + 1.0 + 2.0 + 2.0) * nm * nl * (1u << T.logn)), k_enc_combine, ew_grid(T.logn, nm * nl),
+    prof_launch(KID_ELEMENTWISE, words((3.0 + (msg ? 1.0 : 0.0) + 2.0 + 2.0) * nm * nl * (1u << T.logn)), k_enc_combine, ew_grid(T.logn, nm * nl),
                 dim3(kBlock), 0, st, top, vee, msg, msg_ms, pk, pk_rows, nl, T.pc, T.logn);
 }
 void launch_dec_raw(hipStream_t st, const DevTables& T, u32* x, const DecRaw& dr, int nch, const u32* s, const u32* s2) {
