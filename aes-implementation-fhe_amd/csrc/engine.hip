@@ -2446,6 +2446,7 @@ public:
             }
             for (int k = 0; k < kStreams; ++k) {
                 d_codec_[k] = (double*)dev_alloc(2 * 64 * 2);  // acc[64] + w[64] doubles
+                HIP_OK(hipMemset(d_codec_[k], 0, 64 * sizeof(double)));  // acc: k_snap16 re-zeroes it after each read
                 d_nib_[k] = (int*)dev_alloc(32);
             }
         }
@@ -2504,7 +2505,6 @@ public:
             // either the two 16-periodic halves (unpack) or the 32-periodic whole (single)
             double* acc = d_codec_[t_sidx];
             double* wv = acc + 64;
-            HIP_OK(hipMemsetAsync(acc, 0, 64 * sizeof(double), S()));
             launch_decode32(S(), T_, x, kd[0], cc[0], slots32_, isc[0], acc);
             launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
             if (unpack) launch_encode16(S(), T_, m, wv, slots_p_, enc_scale, nq, true);
@@ -2512,7 +2512,6 @@ public:
         } else if (states == 1) {
             double* acc = d_codec_[t_sidx];
             double* wv = acc + 64;
-            HIP_OK(hipMemsetAsync(acc, 0, 64 * sizeof(double), S()));
             const Slot16& sl = per16 ? slots_p_ : slots_;
             launch_decode16(S(), T_, x, kd, cc, sl, isc, acc);
             launch_snap16(S(), acc, wv, d_nib_[t_sidx]);

@@ -388,7 +388,7 @@ struct Slot16 {
 void launch_decode16(hipStream_t st, const DevTables& T, const u32* x, const int kd[2], const CrtConsts cc[2], const Slot16& sl,
                      const double inv_scale[2], double* acc);
 // per slot: nibble = round(-angle 16 / 2 pi) mod 16, w = zeta16^nibble - 1 (acc -> w, nib)
-void launch_snap16(hipStream_t st, const double* acc, double* w, int* nib);
+void launch_snap16(hipStream_t st, double* acc, double* w, int* nib);
 // out[c][t][k] = round(scale (delta_{k0} + (2/N) Re sum_i w_ci e^{-i pi e_i k / N})) mod q_t, t < nq
 // periodic: the 16-periodic layout (positions sl.e = 5^i, only k == 0 mod N/32 nonzero)
 void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq, bool periodic = false);

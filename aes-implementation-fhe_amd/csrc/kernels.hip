@@ -893,10 +893,13 @@ __global__ void __launch_bounds__(kBlock) k_encode32(u32* out, const double* w, 
     }
 }
 
-__global__ void k_snap16(const double* acc, double* w, int* nib) {
+// acc is zeroed behind its read: the next renorm's decode accumulates into a clean buffer
+// without a fill launch of its own (the buffer is zeroed once when allocated)
+__global__ void k_snap16(double* acc, double* w, int* nib) {
     const int t = threadIdx.x;  // 32 = 2 ciphertexts x 16 slots
     if (t >= 32) return;
     const double ang = atan2(acc[2 * t + 1], acc[2 * t]);
+    acc[2 * t] = 0.0, acc[2 * t + 1] = 0.0;
     const double kf = rint(-ang * 16.0 / (2.0 * M_PI));
     const int v = (int)((((long)kf) % 16 + 16) % 16);
     nib[t] = v;
@@ -1591,7 +1594,7 @@ void launch_encode32(hipStream_t st, const DevTables& T, u32* out, const double*
     prof_launch(KID_ELEMENTWISE, words((double)nq * (1u << T.logn)), k_encode32, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, w, sl,
                 scale, nq, T.pc, T.logn);
 }
-void launch_snap16(hipStream_t st, const double* acc, double* w, int* nib) {
+void launch_snap16(hipStream_t st, double* acc, double* w, int* nib) {
     prof_launch(KID_ELEMENTWISE, 0.0, k_snap16, dim3(1), dim3(64), 0, st, acc, w, nib);
 }
 void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq, bool periodic) {
