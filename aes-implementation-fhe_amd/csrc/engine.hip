@@ -1309,15 +1309,19 @@ public:
     // stage for all of them; ext = [m][nd][ne]
     // tp (tensor mode, relin_rescale_tensor): member m's source rows are the products tp->a[m] (.) tp->b[m],
     // formed inside the inverse NTT (d unused)
-    u32* modup(const u32* d, int level, int nb = 1, size_t d_ms = 0, const TensorPtrs* tp = nullptr) {
+    // rev: the source rows read in reversed coefficient order (the conjugation's permutation, galois)
+    u32* modup(const u32* d, int level, int nb = 1, size_t d_ms = 0, const TensorPtrs* tp = nullptr, bool rev = false) {
         const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, alpha = hp_.alpha;
         const int nd = (nl + alpha - 1) / alpha;
         if (alpha > kMaxConvH || np > kMaxConvH || nb * nd > kMaxConvGroups) throw std::runtime_error("keyswitch: digit too large");
         const LimbMap em = extmap(nl);
         const bool fz = fused_conv(true);
-        if (tp && fz) throw std::runtime_error("modup: the tensor form needs the separate conversion");
+        if ((tp || rev) && fz) throw std::runtime_error("modup: the tensor / reversed form needs the separate conversion");
         u32* coef = tmp((size_t)nb * nl);
-        if (tp) {
+        if (rev) {
+            launch_ntt_inv_rev(S(), T_, coef, d, nb * nl, RowMap{nl, nb > 1 ? (int)(d_ms / n) : nl, nl, 0, 0}, qmap());
+            cnt_[C_NTT_ROWS] += nb * nl;
+        } else if (tp) {
             launch_ntt_inv_prod(S(), T_, coef, *tp, nb * nl, RowMap{nl, nl, nl, 0, 0}, qmap());
             cnt_[C_NTT_ROWS] += nb * nl;
         } else {
@@ -1364,8 +1368,9 @@ public:
     // nb batched ciphertexts: acc = [m][2][ne]; member m adds add0/add1 + m add_ms words
     // dst: write the result there (member stride 2 nl N; the caller owns it) instead of a new buffer
     // outm: member m's result into outm[m] (nb <= 8; the returned Ct then carries no data)
+    // add_rev: add0 read in reversed coefficient order (the conjugation's c0, galois)
     Ct moddown(const u32* acc, int level, const u32* add0, const u32* add1, int nb = 1, size_t add_ms = 0, u32* dst = nullptr,
-               u32* const* outm = nullptr) {
+               u32* const* outm = nullptr, bool add_rev = false) {
         const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, npl = 2 * nb;
         if (npl > kMaxConvGroups) throw std::runtime_error("moddown: batch too large");
         const bool fz = fused_conv(false);
@@ -1390,10 +1395,11 @@ public:
         } else {
             o = alloc_ct(level, npl, nb);
         }
+        if (fz && add_rev) throw std::runtime_error("moddown: the reversed addend needs the separate conversion");
         if (fz)
             launch_ntt_finish_conv(S(), T_, o.data, conv, dn, acc, ne, d_pinv_, add0, add1, npl, nl, add_ms, outm);
         else
-            launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_pinv_, add0, add1, npl, nl, add_ms, outm);
+            launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_pinv_, add0, add1, npl, nl, add_ms, outm, 0u, nullptr, add_rev);
         cnt_[C_NTT_ROWS] += (size_t)npl * nl;
         untmp(yp, (size_t)npl * np);
         untmp(conv, (size_t)npl * nl);
@@ -2233,6 +2239,26 @@ public:
     bool lazy_galois_ = std::getenv("AESFHE_LAZY_GALOIS") == nullptr || std::getenv("AESFHE_LAZY_GALOIS")[0] != '0';
     Ct galois_lazy(const Ct& c, u64 g) {
         const int l = c.level, nl = hp_.nl(l), np = hp_.n_p, ne = nl + np, n = hp_.n, k = pm(c);
+        if (g == conj_galois() && conj_rev_ && !fused_conv(true) && !fused_conv(false)) {
+            // the conjugation (X -> X^(2N-1)) is the index reversal i -> N - 1 - i in this NTT order:
+            // read reversed where the permuted copy was read -- the ModUp's inverse NTT, the own
+            // digit's key inner product and the ModDown finish's c0 -- no k_automorph, same residues
+            const int nsrc = k - 1;
+            u32* ext = modup(c.data + (size_t)nl * n, l, nsrc, (size_t)nl * n, nullptr, true);
+            u32* acc = tmp(2 * (size_t)ne);
+            KsFold fr{};
+            fr.rev_d = 1;
+            key_inner(acc, ext, c.data + (size_t)nl * n, ksk(g), l, 0, 1, 0, fr);
+            if (nsrc == 2)
+                key_inner(acc, ext + (size_t)ext_rows(l) * n, c.data + (size_t)2 * nl * n, ksk(tag_sq(g)), l, 0, 1, 0, fr, true);
+            untmp(ext, (size_t)nsrc * ext_rows(l));
+            Ct o = moddown(acc, l, c.data, nullptr, 1, 0, nullptr, nullptr, true);
+            untmp(acc, 2 * (size_t)ne);
+            o.pend = c.pend;
+            o.lazy = c.pend > 0;
+            cnt_[C_KS] += nsrc;
+            return o;
+        }
         u32* perm = tmp((size_t)k * nl);
         launch_automorph(S(), T_, perm, c.data, g, k * nl);
         // d1 (and d2) of the permuted tensor are consecutive rows: ONE ModUp for both sources
@@ -2267,6 +2293,21 @@ public:
         Ct c = normalize(c_in);
         const int nl = hp_.nl(c.level), n = hp_.n;
         const u32* key = ksk(g);
+        if (g == conj_galois() && conj_rev_ && c.nb == 1 && !fused_conv(true) && !fused_conv(false)) {
+            // the conjugation as reversed reads (galois_lazy): no permuted copy
+            const int ne = nl + hp_.n_p;
+            u32* ext = modup(c.data + (size_t)nl * n, c.level, 1, 0, nullptr, true);
+            u32* acc = tmp(2 * (size_t)ne);
+            KsFold fr{};
+            fr.rev_d = 1;
+            key_inner(acc, ext, c.data + (size_t)nl * n, key, c.level, 0, 1, 0, fr);
+            untmp(ext, (size_t)ext_rows(c.level));
+            Ct o = moddown(acc, c.level, c.data, nullptr, 1, 0, nullptr, nullptr, true);
+            untmp(acc, 2 * (size_t)ne);
+            cnt_[C_KS]++;
+            if (c.data != c_in.data) release(c);
+            return o;
+        }
         u32* perm = tmp(2 * (size_t)nl * c.nb);
         launch_automorph(S(), T_, perm, c.data, g, 2 * nl * c.nb);
         const size_t ms = (size_t)2 * nl * n;  // member stride of a batched ciphertext
@@ -4183,6 +4224,8 @@ private:
     bool fused_tensor_ = std::getenv("AESFHE_FUSED_TENSOR") == nullptr || std::getenv("AESFHE_FUSED_TENSOR")[0] != '0';
     // EvalMod's 2 T^2 - 1 in the product's relinearisation finish (AESFHE_FUSED_AFFINE=0: one lincomb each)
     bool fused_affine_ = std::getenv("AESFHE_FUSED_AFFINE") == nullptr || std::getenv("AESFHE_FUSED_AFFINE")[0] != '0';
+    // conjugations as reversed reads, no permuted copy (galois / galois_lazy; AESFHE_CONJ_REV=0: k_automorph first)
+    bool conj_rev_ = std::getenv("AESFHE_CONJ_REV") == nullptr || std::getenv("AESFHE_CONJ_REV")[0] != '0';
     bool fuse_rr_ = std::getenv("AESFHE_FUSED_RESCALE") == nullptr || std::getenv("AESFHE_FUSED_RESCALE")[0] != '0';
     u32* d_pinv_ = nullptr;
     u32* d_negp_ = nullptr;

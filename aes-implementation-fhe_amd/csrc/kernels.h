@@ -99,6 +99,9 @@ struct NttAux {
     // 2 x^2 - c in the relinearisation's own launch, the residues of k_lincomb's (Engine::Affine)
     unsigned dbl = 0;
     const u32* cst[8] = {};
+    // finish: add0 read in reversed coefficient order (word N - 1 - i for word i): the conjugation
+    // X -> X^(2N-1) in this NTT order, its c0 addend permuted on load (Engine::galois_lazy)
+    int add_rev = 0;
 };
 // out-of-place (src may equal dst); supported ring sizes 2^13 .. 2^16
 void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map);
@@ -120,7 +123,10 @@ void launch_rescale2_ntt(hipStream_t st, const DevTables& T, u32* out, const u32
 // dbl / cst: NttAux's per-member epilogue 2 r + c (cst: nb entries, nullable)
 void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, const u32* cur, int cur_stride, const u32* qinv,
                        const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride = 0, u32* const* outm = nullptr,
-                       unsigned dbl = 0, const u32* const* cst = nullptr);
+                       unsigned dbl = 0, const u32* const* cst = nullptr, bool add_rev = false);
+// inverse NTT reading each source row in reversed coefficient order (the conjugation's permutation
+// of the source fused into the load; otherwise launch_ntt_inv)
+void launch_ntt_inv_rev(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map);
 // in place on rows = npoly * nl dense rows
 void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map);
 void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map);
@@ -247,6 +253,8 @@ struct KsFold {
     const u32* ta[kMaxKsBatch] = {};
     const u32* tb[kMaxKsBatch] = {};
     int tnl = 0;
+    // rev_d (g == 0): the own digit's rows of d read in reversed coefficient order (the conjugation)
+    int rev_d = 0;
 };
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
                       int alpha, int nkey, int nks, LimbMap map, u64 g = 0, int nb = 1, size_t ext_ms = 0, size_t d_ms = 0,

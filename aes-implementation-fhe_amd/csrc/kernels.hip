@@ -396,6 +396,9 @@ __global__ void __launch_bounds__(kBlock) k_key_inner(u32* acc, const u32* ext, 
                 const uint4 a = *reinterpret_cast<const uint4*>(fold.ta[m] + at), b = *reinterpret_cast<const uint4*>(fold.tb[m] + at);
                 e[0] = barrett_mul(a.x, b.x, P.q, P.mu), e[1] = barrett_mul(a.y, b.y, P.q, P.mu);
                 e[2] = barrett_mul(a.z, b.z, P.q, P.mu), e[3] = barrett_mul(a.w, b.w, P.q, P.mu);
+            } else if (fold.rev_d && j == own) {  // (g == 0) the own digit's d read reversed: element v <- word N - 1 - (k + v)
+                const uint4 t = *reinterpret_cast<const uint4*>(d + m * d_ms + ((size_t)x << logn) + ((size_t)1 << logn) - 4 - k);
+                e[0] = t.w, e[1] = t.z, e[2] = t.y, e[3] = t.x;
             } else {
                 const u32* src = j == own ? d + m * d_ms + ((size_t)x << logn) : ext + m * ext_ms + (((size_t)j * ne + x) << logn);
                 if (g) {

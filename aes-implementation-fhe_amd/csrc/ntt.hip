@@ -348,7 +348,14 @@ __global__ void __launch_bounds__(NT, OCC) k_ntt2_fwd(u32* data, RowMap rm, Limb
         has_add = addp != nullptr;
 #pragma unroll
         for (int v = 0; v < 4; ++v) cvp[v] = cu[v];
-        if (has_add) {
+        if (has_add && aux.add_rev && !(grp & 1)) {  // element e <- word N - 1 - (woff + e)
+            const uint4* ad = reinterpret_cast<const uint4*>(addp + ((size_t)li << LOGN) + ((size_t)1 << LOGN) - 16 - woff);
+            uint4 t[4];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) t[v] = ad[v];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) avp[v] = make_uint4(t[3 - v].w, t[3 - v].z, t[3 - v].y, t[3 - v].x);
+        } else if (has_add) {
             const uint4* ad = reinterpret_cast<const uint4*>(addp + ((size_t)li << LOGN) + woff);
 #pragma unroll
             for (int v = 0; v < 4; ++v) avp[v] = ad[v];
@@ -415,8 +422,9 @@ __global__ void __launch_bounds__(NT, OCC) k_ntt2_fwd(u32* data, RowMap rm, Limb
 // times psi^-((N / 2^s) brv_s(t)) -- 224 per prime, shared by every row, L1 / L2 resident --
 // one more lazy Shoup product per butterfly of those stages instead of 8 twiddle bytes, so the
 // launch reads ~280 twiddle bytes per 1 KB row instead of 2 KB
-// PROD: the input row is the product a (.) b of group g's rows (launch_ntt_inv_prod), src unused
-template <int LOGR1, int NT, bool FACT, bool PROD>
+// IN = 1: the input row is the product a (.) b of group g's rows (launch_ntt_inv_prod), src unused;
+// IN = 2: the source row read in reversed coefficient order (launch_ntt_inv_rev)
+template <int LOGR1, int NT, bool FACT, int IN>
 __global__ void __launch_bounds__(NT) k_ntt2_inv(u32* dst, const u32* src, RowMap rm, LimbMap map, const PrimeConst* pc,
                                                        const uint2* tw, const uint2* irow, const uint2* igam, TensorPtrs tp,
                                                        unsigned long long* ts) {
@@ -430,7 +438,14 @@ __global__ void __launch_bounds__(NT) k_ntt2_inv(u32* dst, const u32* src, RowMa
     const int r = threadIdx.x >> 4, j = threadIdx.x & 15;
     const int R = blockIdx.x * (NT / 16) + r;
     u32 x[16];
-    if (PROD) {
+    if (IN == 2) {  // element e of row R <- word N - 1 - (256 R + 16 j + e) = row R1 - 1 - R, word 255 - 16 j - e
+        const uint4* in = reinterpret_cast<const uint4*>(ra.src + (size_t)((1 << LOGR1) - 1 - R) * 256 + 240 - 16 * j);
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+            const uint4 t = in[v];
+            x[15 - 4 * v] = t.x, x[14 - 4 * v] = t.y, x[13 - 4 * v] = t.z, x[12 - 4 * v] = t.w;
+        }
+    } else if (IN == 1) {
         const u32 mu = pc[ra.prime].mu;
         const size_t off = ((size_t)blockIdx.y << LOGN) + (size_t)R * 256 + 16 * j;
         const uint4* pa = reinterpret_cast<const uint4*>(tp.a[blockIdx.z] + off);
@@ -611,24 +626,27 @@ inline bool inv_fact_on() {
 }
 template <int LOGR1, int NT>
 void ntt2_inv_launch(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, RowMap rm, LimbMap map, int groups, double io,
-                     double work, const TensorPtrs* tp) {
+                     double work, const TensorPtrs* tp, bool rev) {
     const dim3 grid(R1_of<LOGR1>() / (NT / 16), rm.cnt, groups);
     if (tp) {
-        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, true, true>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
+        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, true, 1>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
                         Tb.irow, Tb.igam, *tp);
         return;
     }
     static const TensorPtrs kNone{};
-    if (inv_fact_on())
-        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, true, false>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
+    if (rev)
+        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, true, 2>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
+                        Tb.irow, Tb.igam, kNone);
+    else if (inv_fact_on())
+        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, true, 0>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
                         Tb.irow, Tb.igam, kNone);
     else
-        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, false, false>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
+        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, false, 0>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
                         Tb.irow, Tb.igam, kNone);
 }
 template <int LOGR1>
 void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map, const u32* post,
-               const TensorPtrs* tp = nullptr) {
+               const TensorPtrs* tp = nullptr, bool rev = false) {
     constexpr int R1 = 1 << LOGR1;
     rm.nrows = rows;
     const int groups = (rows + rm.cnt - 1) / rm.cnt;
@@ -637,16 +655,16 @@ void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
     const double bfly = (double)rows * 128.0 * R1;
     if (small_launch(rows)) {
         constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
-        ntt2_inv_launch<LOGR1, NT>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp);
+        ntt2_inv_launch<LOGR1, NT>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp, rev);
         prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, dst, rm, map,
                         Tb.pc, Tb.itw, post);
         return;
     }
     constexpr int CB = kThreads / (R1 / 16);
     switch (p2_nt(true)) {
-        case 128: ntt2_inv_launch<LOGR1, 128>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp); break;
-        case 256: ntt2_inv_launch<LOGR1, 256>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp); break;
-        default: ntt2_inv_launch<LOGR1, kThreads>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp); break;
+        case 128: ntt2_inv_launch<LOGR1, 128>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp, rev); break;
+        case 256: ntt2_inv_launch<LOGR1, 256>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp, rev); break;
+        default: ntt2_inv_launch<LOGR1, kThreads>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp, rev); break;
     }
     prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, kThreads>, dim3(256 / CB, rm.cnt, groups), dim3(kThreads), 0, st, dst, rm,
                     map, Tb.pc, Tb.itw, post);
@@ -770,7 +788,7 @@ void launch_rescale2_ntt(hipStream_t st, const DevTables& T, u32* out, const u32
 }
 void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, const u32* cur, int cur_stride, const u32* qinv,
                        const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride, u32* const* outm, unsigned dbl,
-                       const u32* const* cst) {
+                       const u32* const* cst, bool add_rev) {
     NttAux aux{};
     aux.cur = cur, aux.out = out, aux.qinv = qinv, aux.cur_stride = cur_stride, aux.out_stride = nt, aux.add0 = add0, aux.add1 = add1;
     aux.add_mstride = add_mstride;
@@ -784,6 +802,7 @@ void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, 
         if (cst)
             for (int m = 0; m < npoly / 2; ++m) aux.cst[m] = cst[m];
     }
+    aux.add_rev = add_rev ? 1 : 0;
     ntt_fwd_dispatch<kPlain, kFinish>(st, T, conv, conv, npoly * nt, npoly * nt, rows_dense(nt), LimbMap{1 << 30, 0, 0}, aux);
 }
 void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map, const u32* post) {
@@ -803,6 +822,16 @@ void launch_ntt_inv_prod(hipStream_t st, const DevTables& T, u32* dst, const Ten
         case 14: ntt_inv_t<6>(st, T, dst, nullptr, rows, rm, map, nullptr, &tp); break;
         case 15: ntt_inv_t<7>(st, T, dst, nullptr, rows, rm, map, nullptr, &tp); break;
         case 16: ntt_inv_t<8>(st, T, dst, nullptr, rows, rm, map, nullptr, &tp); break;
+        default: break;
+    }
+}
+void launch_ntt_inv_rev(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {
+    if (rows <= 0) return;
+    switch (T.logn) {
+        case 13: ntt_inv_t<5>(st, T, dst, src, rows, rm, map, nullptr, nullptr, true); break;
+        case 14: ntt_inv_t<6>(st, T, dst, src, rows, rm, map, nullptr, nullptr, true); break;
+        case 15: ntt_inv_t<7>(st, T, dst, src, rows, rm, map, nullptr, nullptr, true); break;
+        case 16: ntt_inv_t<8>(st, T, dst, src, rows, rm, map, nullptr, nullptr, true); break;
         default: break;
     }
 }
