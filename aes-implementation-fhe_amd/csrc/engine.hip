@@ -12,6 +12,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <deque>
+#include <functional>
 #include <chrono>
 #include <map>
 #include <mutex>
@@ -49,8 +50,14 @@ inline void seed_key(u64 seed, u32 key[8]) {
 // ---------------------------------------------------------------------------------
 // device memory pool: exact-size free lists (ciphertext sizes repeat constantly)
 // ---------------------------------------------------------------------------------
+// Out of memory: a failed hipMalloc releases the cached free lists (the
+// engine's on_oom hook: every pool that no branch thread is using), after a device sync so no
+// queued kernel still reads a freed buffer, and retries once; only a second failure throws.
+// AESFHE_POOL_LIMIT_MB caps the bytes a pool may hold (a simulated smaller HBM: tests force the
+// release-and-retry path with it).
 class Pool {
 public:
+    std::function<void()> on_oom;  // set by the engine: release the free lists it may release
     u32* try_get(size_t words) {
         auto it = free_.find(words);
         if (it == free_.end() || it->second.empty()) return nullptr;
@@ -70,24 +77,50 @@ public:
     }
     u32* get(size_t words) {
         if (u32* p = try_get(words)) return p;
+        const size_t b = words * sizeof(u32);
         void* p = nullptr;
-        HIP_OK(hipMalloc(&p, words * sizeof(u32)));
-        bytes_ += words * sizeof(u32);
+        hipError_t e = raw_alloc(&p, b);
+        if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) {
+            (void)hipGetLastError();  // not sticky, but leave no error for the next launch check
+            ++oom_retries_;
+            if (on_oom) on_oom();
+            else trim();
+            e = raw_alloc(&p, b);
+        }
+        if (e != hipSuccess)
+            throw std::runtime_error(std::string("device memory exhausted after releasing the cached buffers: ") + hipGetErrorString(e));
+        bytes_ += b;
         return (u32*)p;
     }
     void put(u32* p, size_t words) {
         if (p) free_[words].push_back(p);
     }
-    void release_all() {
+    // frees every cached (free-list) buffer; the caller has synchronised the device
+    size_t trim() {
+        size_t freed = 0;
         for (auto& kv : free_)
-            for (u32* p : kv.second) (void)hipFree(p);
+            for (u32* p : kv.second) {
+                (void)hipFree(p);
+                freed += kv.first * sizeof(u32);
+            }
         free_.clear();
+        bytes_ = bytes_ > freed ? bytes_ - freed : 0;
+        return freed;
     }
+    void release_all() { trim(); }
     size_t bytes() const { return bytes_; }
+    unsigned long long oom_retries() const { return oom_retries_; }
 
 private:
+    hipError_t raw_alloc(void** p, size_t b) {
+        if (limit_ && bytes_ + b > limit_) return hipErrorOutOfMemory;
+        return hipMalloc(p, b);
+    }
+    // read when the context is created (a test sets it for one context only)
+    size_t limit_ = std::getenv("AESFHE_POOL_LIMIT_MB") ? (size_t)std::atoll(std::getenv("AESFHE_POOL_LIMIT_MB")) << 20 : (size_t)0;
     std::unordered_map<size_t, std::vector<u32*>> free_;
     size_t bytes_ = 0;
+    unsigned long long oom_retries_ = 0;
 };
 
 // A ciphertext tensor.  `level` is the DATA level (nl(level) limbs per polynomial); `pend`
@@ -147,6 +180,23 @@ public:
             HIP_OK(hipEventCreateWithFlags(&fj_ev_[k], hipEventDisableTiming));
         }
         build_tables();
+        for (int k = 0; k < kStreams; ++k)
+            pools_[k].on_oom = [this, k] {
+                (void)hipDeviceSynchronize();  // queued kernels may still read cached buffers
+                pools_[k].trim();
+                if (!fj_active_)  // no branch thread is allocating: every pool's cache may go
+                    for (int j = 0; j < kStreams; ++j) pools_[j].trim();
+            };
+    }
+    unsigned long long oom_retries() const {
+        unsigned long long n = 0;
+        for (const auto& pl : pools_) n += pl.oom_retries();
+        return n;
+    }
+    size_t pool_bytes() const {
+        size_t n = 0;
+        for (const auto& pl : pools_) n += pl.bytes();
+        return n;
     }
     ~Engine() {
         (void)hipSetDevice(device_);
@@ -2487,7 +2537,11 @@ public:
             }
             for (int k = 0; k < kStreams; ++k) {
                 d_codec_[k] = (double*)dev_alloc(2 * 64 * 2);  // acc[64] + w[64] doubles
-                HIP_OK(hipMemset(d_codec_[k], 0, 64 * sizeof(double)));  // acc: k_snap16 re-zeroes it after each read
+                // acc zeroed on the stream the codec launches run on, ordered before the first decode
+                // (hipMemset on the null stream does not order a hipStreamNonBlocking stream); from
+                // then on k_snap16 re-zeroes acc after each read (kernels.h launch_decode16 / 32)
+                HIP_OK(hipMemsetAsync(d_codec_[k], 0, 64 * sizeof(double), S()));
+                HIP_OK(hipStreamSynchronize(S()));
                 d_nib_[k] = (int*)dev_alloc(32);
             }
         }
@@ -4691,6 +4745,20 @@ int aesfhe_kernel_work(aesfhe_ctx* ctx, double* out, int n) {
     API_BEGIN KernelProfiler& p = ctx->eng->prof_;
     p.flush();
     for (int k = 0; k < n && k < KID_N; ++k) out[k] = p.work[k];
+    API_END
+}
+int aesfhe_pool_stats(aesfhe_ctx* ctx, uint64_t* out) {
+    API_BEGIN out[0] = ctx->eng->pool_bytes();
+    out[1] = ctx->eng->oom_retries();
+    API_END
+}
+int aesfhe_kernel_gaps(aesfhe_ctx* ctx, double* out, int n) {
+    API_BEGIN KernelProfiler& p = ctx->eng->prof_;
+    p.flush();
+    for (int k = 0; k < n && k < KID_N; ++k) {
+        out[2 * k] = (double)p.gap_n[k];
+        out[2 * k + 1] = p.gap_ms[k];
+    }
     API_END
 }
 uint64_t aesfhe_launch_count(void) { return g_launches.load(std::memory_order_relaxed); }

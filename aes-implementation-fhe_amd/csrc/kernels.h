@@ -47,10 +47,21 @@ struct KernelProfiler {
     struct TsRec {
         int slot, kid;
         double bytes, work;
+        bool count;  // a sampled launch of its own kid (span accounted); false: stamped only as a successor
+        int prev;    // slot of the sampled launch issued right before it (-1: none): the boundary gap
     };
     std::vector<TsRec> ts_recs;
-    unsigned long long* ts_slot(int kid, double bytes, double work = 0.0);
+    unsigned long long* ts_slot(int kid, double bytes, double work = 0.0, bool count = true, int prev = -1);
     void ts_flush();
+    // Dispatch-inclusive timing: the launch issued right after a sampled one
+    // (next in the process's launch order, a clock-slot kernel) is stamped too, and the gap
+    // start(next) - end(sampled) -- the sampled kernel's drain plus the next one's dispatch ramp,
+    // the time rocprofv3's durations add to the in-kernel span -- is accounted to the NEXT
+    // launch's kid: a kid's dispatch-inclusive average = its span average + its gap average.
+    int pend_slot = -1;
+    unsigned long long pend_idx = 0;
+    double gap_ms[KID_N] = {};
+    unsigned long long gap_n[KID_N] = {};
 };
 // the profiler of the engine currently issuing launches (set per API call)
 void prof_set(KernelProfiler* p);
@@ -393,6 +404,9 @@ struct Slot16 {
 };
 // x: [2][4][N] coefficient residues of the two decryptions (kd[c] limbs used);
 // acc[c][i][re|im] += sum_k (m_k / scale_c) e^{i pi e_i k / N}   (acc zeroed by the caller)
+// CONTRACT: acc must be zero on entry, and every decode must be followed by a launch_snap16 on the
+// same accumulator (same stream): k_snap16 reads acc and re-zeroes it for the next decode -- a decode
+// without its snap leaves stale sums that the next renorm would add onto
 void launch_decode16(hipStream_t st, const DevTables& T, const u32* x, const int kd[2], const CrtConsts cc[2], const Slot16& sl,
                      const double inv_scale[2], double* acc);
 // per slot: nibble = round(-angle 16 / 2 pi) mod 16, w = zeta16^nibble - 1 (acc -> w, nib)
@@ -407,6 +421,7 @@ void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double*
 struct Slot32 {
     u32 e[32];
 };
+// CONTRACT (as launch_decode16): acc zero on entry, a launch_snap16 on acc must follow on the same stream
 void launch_decode32(hipStream_t st, const DevTables& T, const u32* x, int kd, const CrtConsts& cc, const Slot32& sl, double inv_scale, double* acc);
 void launch_encode32(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot32& sl, double scale, int nq);
 

@@ -750,7 +750,7 @@ void KernelProfiler::flush() {
     }
     recs.clear();
 }
-unsigned long long* KernelProfiler::ts_slot(int kid, double b, double w) {
+unsigned long long* KernelProfiler::ts_slot(int kid, double b, double w, bool count, int prev) {
     const size_t words = (size_t)kTsSlots * kTsRec;
     if (!d_ts) {
         void* p = nullptr;
@@ -758,29 +758,46 @@ unsigned long long* KernelProfiler::ts_slot(int kid, double b, double w) {
         d_ts = (unsigned long long*)p;
         (void)hipMemset(d_ts, 0, sizeof(unsigned long long) * words);
     }
-    if (ts_next == kTsSlots) ts_flush();
-    ts_recs.push_back({ts_next, kid, b, w});
+    if (ts_next == kTsSlots) {
+        ts_flush();
+        prev = -1;  // the predecessor's slot was just recycled
+    }
+    ts_recs.push_back({ts_next, kid, b, w, count, prev});
     return d_ts + (size_t)kTsRec * ts_next++;
 }
 void KernelProfiler::ts_flush() {
+    pend_slot = -1;
     if (!d_ts || ts_recs.empty()) return;
     (void)hipDeviceSynchronize();
     const size_t words = (size_t)kTsRec * ts_next;
     std::vector<unsigned long long> h(words);
     (void)hipMemcpy(h.data(), d_ts, sizeof(unsigned long long) * words, hipMemcpyDeviceToHost);
-    for (const auto& r : ts_recs) {
-        const unsigned long long* rec = h.data() + (size_t)kTsRec * r.slot;
-        unsigned long long a = ~0ull, e = 0;
+    // {earliest start, latest end} of a slot (0 / 0 when no block stamped)
+    auto span = [&](int slot, unsigned long long& a, unsigned long long& e) {
+        const unsigned long long* rec = h.data() + (size_t)kTsRec * slot;
+        a = ~0ull, e = 0;
         for (int j = 0; j < kTsSub; ++j) {
             if (rec[kTsLine * j]) a = std::min(a, ~rec[kTsLine * j]);
             e = std::max(e, rec[kTsLine * (kTsSub + j)]);
         }
-        if (a == ~0ull) continue;  // no block stamped a start
-        if (e < a) continue;
-        ms[r.kid] += (double)(e - a) * 1e-5;  // 100 MHz ticks -> ms
-        bytes[r.kid] += r.bytes;
-        work[r.kid] += r.work;
-        launches[r.kid] += 1;
+        return a != ~0ull && e >= a;
+    };
+    for (const auto& r : ts_recs) {
+        unsigned long long a, e;
+        if (!span(r.slot, a, e)) continue;
+        if (r.count) {
+            ms[r.kid] += (double)(e - a) * 1e-5;  // 100 MHz ticks -> ms
+            bytes[r.kid] += r.bytes;
+            work[r.kid] += r.work;
+            launches[r.kid] += 1;
+        }
+        unsigned long long pa, pe;
+        // the boundary gap: this launch's first stamped start after its predecessor's last end, on
+        // one stream (a launch of another stream in between would start before that end: dropped)
+        if (r.prev >= 0 && span(r.prev, pa, pe) && a >= pe && a - pe < 100000) {
+            gap_ms[r.kid] += (double)(a - pe) * 1e-5;
+            gap_n[r.kid] += 1;
+        }
     }
     ts_recs.clear();
     (void)hipMemset(d_ts, 0, sizeof(unsigned long long) * words);
@@ -788,7 +805,7 @@ void KernelProfiler::ts_flush() {
 }
 void KernelProfiler::reset() {
     flush();
-    for (int k = 0; k < KID_N; ++k) ms[k] = bytes[k] = work[k] = 0, launches[k] = 0;
+    for (int k = 0; k < KID_N; ++k) ms[k] = bytes[k] = work[k] = gap_ms[k] = 0, launches[k] = gap_n[k] = 0;
 }
 
 namespace {
@@ -1478,6 +1495,9 @@ void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* e
                       bool accum) {
     if (nb < 1 || nb > kMaxKsBatch) throw std::runtime_error("launch_key_inner: 1..8 batched ciphertexts");
     if (fold.gad && g) throw std::runtime_error("launch_key_inner: fold with an automorphism");
+    // the reversed own-digit read is the conjugation's (identity Galois element, no tensor fold): with
+    // g != 0 the kernel would ignore g on the own digit, in tensor mode it never reaches the branch
+    if (fold.rev_d && (g || fold.ta[0])) throw std::runtime_error("launch_key_inner: reversed d needs g == 0 and no tensor fold");
     // per ciphertext ext/d (nd x ne) read and acc (2 x ne) written; the key (nd x 2 x ne) once;
     // the fold reads 2 x nl more rows per ciphertext
     // tensor mode (fold.ta): the fold reads a0, a1, b0, b1 and the own digit a1, b1 (one row more

@@ -95,17 +95,22 @@ inline void prof_launch_tsw(int kid, double bytes, double work, F kernel, dim3 g
     alg_account(kid, bytes);
     KernelProfiler* p = g_prof;
     unsigned long long* ts = nullptr;
-    if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) {
-        static const bool events = std::getenv("AESFHE_PROF_EVENTS") && std::getenv("AESFHE_PROF_EVENTS")[0] == '1';
-        if (!events) {
-            ts = p->ts_slot(kid, bytes, work);
-        } else {  // AESFHE_PROF_EVENTS=1: dispatch-stamped events (~3 us longer per timed launch)
-            hipEvent_t a = p->get(), b = p->get();
-            hipExtLaunchKernelGGL(kernel, grid, block, (std::uint32_t)lds, st, a, b, 0u, args..., ts);
-            p->recs.push_back({a, b, kid, bytes, work});
-            launch_check();
-            return;
-        }
+    static const bool events = std::getenv("AESFHE_PROF_EVENTS") && std::getenv("AESFHE_PROF_EVENTS")[0] == '1';
+    if (p && p->mask && !events) {
+        // this launch's index in the process's launch order (launch_validate counted it)
+        const unsigned long long idx = g_launches.load(std::memory_order_relaxed);
+        const bool own = (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0;
+        const bool succ = p->pend_slot >= 0 && idx == p->pend_idx + 1;
+        if (own || succ) ts = p->ts_slot(kid, bytes, work, own, succ ? p->pend_slot : -1);
+        p->pend_slot = (own && ts) ? (int)((ts - p->d_ts) / KernelProfiler::kTsRec) : -1;
+        p->pend_idx = idx;
+    } else if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) {
+        // AESFHE_PROF_EVENTS=1: dispatch-stamped events (~3 us longer per timed launch)
+        hipEvent_t a = p->get(), b = p->get();
+        hipExtLaunchKernelGGL(kernel, grid, block, (std::uint32_t)lds, st, a, b, 0u, args..., ts);
+        p->recs.push_back({a, b, kid, bytes, work});
+        launch_check();
+        return;
     }
     hipLaunchKernelGGL(kernel, grid, block, lds, st, args..., ts);
     launch_check();

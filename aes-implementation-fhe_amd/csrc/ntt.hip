@@ -634,8 +634,11 @@ void ntt2_inv_launch(hipStream_t st, const DevTables& Tb, u32* dst, const u32* s
         return;
     }
     static const TensorPtrs kNone{};
-    if (rev)
+    if (rev && inv_fact_on())
         prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, true, 2>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
+                        Tb.irow, Tb.igam, kNone);
+    else if (rev)  // AESFHE_NTT_INV_FACT=0 covers the conjugations' reversed ModUp too
+        prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, false, 2>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
                         Tb.irow, Tb.igam, kNone);
     else if (inv_fact_on())
         prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, true, 0>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,

@@ -40,7 +40,7 @@ EXPORTED = [
     "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
     "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
     "aesfhe_streams", "aesfhe_bind_stream", "aesfhe_fork", "aesfhe_join", "aesfhe_settle",
-    "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_kernel_work", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan", "aesfhe_debug_sparseplan",
+    "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_kernel_work", "aesfhe_kernel_gaps", "aesfhe_pool_stats", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan", "aesfhe_debug_sparseplan",
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot", "aesfhe_create_keyed", "aesfhe_bootstrap_sparse", "aesfhe_bootstrap_pair_sparse", "aesfhe_renorm_periodic",
     "aesfhe_renorm_single", "aesfhe_renorm_unpack",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_debug_lin_group_plain", "aesfhe_lut_create", "aesfhe_lut_eval", "aesfhe_lut_free",
@@ -112,6 +112,8 @@ def load_library(path: Optional[Path] = None):
         "aesfhe_profile": [vp, ctypes.c_uint32], "aesfhe_profile_every": [vp, c_int],
         "aesfhe_kernel_stats": [vp, _dp, c_int, c_int],
         "aesfhe_kernel_work": [vp, _dp, c_int],
+        "aesfhe_kernel_gaps": [vp, _dp, c_int],
+        "aesfhe_pool_stats": [vp, np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS")],
     }
     sig["aesfhe_bootstrap_depth"] = []
     sig["aesfhe_bootstrap_scaled"] = [vp, _H, c_dbl, _Hp]
@@ -838,6 +840,20 @@ class Engine:
         out = np.zeros(len(KERNEL_IDS))
         self._ctx.check(self._lib.aesfhe_kernel_work(self._ctx.ptr, out, len(KERNEL_IDS)))
         return {k: float(out[i]) for i, k in enumerate(KERNEL_IDS)}
+
+    def pool_stats(self) -> dict:
+        """{"bytes": device bytes the buffer pools hold, "oom_retries": allocations retried after
+        releasing the cached free lists} (aesfhe_pool_stats)"""
+        out = np.zeros(2, np.uint64)
+        self._ctx.check(self._lib.aesfhe_pool_stats(self._ctx.ptr, out))
+        return {"bytes": int(out[0]), "oom_retries": int(out[1])}
+
+    def kernel_gaps(self) -> dict:
+        """{kernel id: (gaps, total ms)}: the boundary gap before the launch issued right after a
+        sampled one (drain + dispatch ramp), by that launch's id (read before kernel_stats resets)"""
+        out = np.zeros(2 * len(KERNEL_IDS))
+        self._ctx.check(self._lib.aesfhe_kernel_gaps(self._ctx.ptr, out, len(KERNEL_IDS)))
+        return {k: (int(out[2 * i]), float(out[2 * i + 1])) for i, k in enumerate(KERNEL_IDS) if out[2 * i] > 0}
 
     def kernel_stats(self, reset: bool = True) -> dict:
         out = np.zeros(3 * len(KERNEL_IDS))

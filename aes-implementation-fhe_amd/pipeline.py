@@ -197,11 +197,21 @@ class AESPipeline:
             return self.xor4.apply(x, key, out_level=self._floor())
         if self._kb_tag != self._rk_tag:
             self._kb_cache, self._kb_tag = {}, self._rk_tag
-        kb = self._kb_cache.setdefault(r, {})
-        try:
-            return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb)
-        except TypeError:  # an XOR4 without basis sharing
+        if not self._xor4_keep_b():  # an XOR4 without basis sharing (a caller-supplied LUT object)
             return self.xor4.apply(x, key, out_level=self._floor())
+        kb = self._kb_cache.setdefault(r, {})
+        return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb)
+
+    def _xor4_keep_b(self) -> bool:
+        """whether this pipeline's XOR4 takes keep_b (checked once; a TypeError raised INSIDE the
+        evaluation must surface, not be taken for a missing keyword)"""
+        if not hasattr(self, "_keep_b_ok"):
+            import inspect
+            try:
+                self._keep_b_ok = "keep_b" in inspect.signature(self.xor4.apply).parameters
+            except (TypeError, ValueError):
+                self._keep_b_ok = False
+        return self._keep_b_ok
 
     def _packed_round_key(self, r: int):
         """round key r encrypted in the packed form (after _prepare_round_keys of the same keys)"""

@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--kernel", default="ntt_rows_fwd", help="kernel id timed live for the roofline (the dominant kernel)")
     ap.add_argument("--kernel2", default="key_inner", help="secondary kernel id reported as roofline_secondary")
+    ap.add_argument("--eager-steps", type=int, default=1,
+                    help="the per-primitive drop-in leg (VERDICT r3 item 7): C2 through EngineContext with REF's own call "
+                         "sequence -- eager relinearise/rescale after every product, per-term LUT product loops (no fused "
+                         "LUT kernels), the reference slot layout with full-slot bootstraps; 0 = skip")
     ap.add_argument("--profile-all", action="store_true", help="time every kernel id (diagnostic; slower)")
     ap.add_argument("--profile-every", type=int, default=32,
                     help="time one launch in N of the roofline kernels (live sample over the timed region)")
@@ -73,14 +77,15 @@ def parse():
                     help="secondary measurement (BASELINE configs 3/4): this many independent states per rank, "
                          "slot-packed into one ciphertext pair (SURVEY.md 8(f)1); 0 = skip")
     ap.add_argument("--batch-steps", type=int, default=3)
-    ap.add_argument("--pair-states", type=int, default=64,
-                    help="multi-pair batch, BASELINE config 3's shape (one state per ciphertext pair): this many pairs "
-                         "per rank as stacked ciphertexts (DESIGN.md 3.16); 0 = skip")
+    ap.add_argument("--pair-states", type=int, default=1024,
+                    help="BASELINE config 3 literally (1024 ciphertext pairs hi/lo, ONE state each): this many pairs "
+                         "per rank as stacked ciphertexts (DESIGN.md 3.16), --pair-stack per stack; 0 = skip")
     ap.add_argument("--pair-stack", type=int, default=64,
                     help="pairs per stack: --pair-states pairs run as ceil(pair-states / pair-stack) stacks in turn")
     ap.add_argument("--packed-pairs", type=int, default=4,
                     help="multi-pair slot-packed batch: this many stacked ciphertext pairs of 2048 states each per rank; 0 = skip")
-    ap.add_argument("--pair-steps", type=int, default=3, help="timed steps of the multi-pair legs")
+    ap.add_argument("--pair-steps", type=int, default=1, help="timed steps of the one-state multi-pair leg (C3 literally)")
+    ap.add_argument("--packed-pair-steps", type=int, default=3, help="timed steps of the slot-packed multi-pair leg")
     ap.add_argument("--true-fhe-steps", type=int, default=1,
                     help="SURVEY.md 8(f)3 line beside the headline: C2 encrypts with every secret-key renorm replaced "
                          "by bootstrap + homomorphic Zeta16 snap (AESPipeline(true_fhe=True)); 0 = skip")
@@ -90,8 +95,9 @@ def parse():
                     help="with AESFHE_PROFILE_FROM_START=<ids>: keep the engine's per-kernel accounting from the first "
                          "launch on (no reset, every launch) and write it to this JSON file -- the algorithmic bytes of "
                          "exactly the launches a whole-process rocprofv3 --pmc pass counts")
-    ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r3_pmc_traffic_round.json"),
-                    help="per-kernel HBM/algorithmic byte ratios from rocprofv3 PMC passes (tools/r2_pmc_filtered.sh)")
+    ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r4_pmc_traffic_bench.json"),
+                    help="per-kernel-class HBM / algorithmic byte ratios from rocprofv3 --pmc passes over this bench's own "
+                         "C2 leg (tools/gpu_task.sh pmc)")
     return ap.parse_args()
 
 
@@ -211,32 +217,45 @@ def _progress(ctx, every_s: float = 30.0):
     threading.Thread(target=run, daemon=True).start()
 
 
-def measure_precision(pipe, ctx, rks, state) -> dict:
-    """CKKS precision of the bench path, measured after the timed region: the scale Delta of the
-    single-prime levels (log2), and the largest angular deviation of any state slot from its
-    Zeta16 codeword over every logged stage of one encrypt (debug dict of the production path,
-    DESIGN.md 4c), against the decode margin pi/16 -- bytes are exact while it stays below"""
+def state_slots(pipe, ctx, ct, packed: bool) -> np.ndarray:
+    """decrypted slot values of every state of a (stacked) ciphertext: (hi | lo of a packed one)"""
+    enc = pipe.encoder
+    out = []
+    for c in (ctx.unstack(ct) if enc.pairs > 1 else [ct]):
+        z = ctx.decrypt(c)
+        out.append(enc._take(z).ravel())
+        if packed:
+            out.append(enc._take(z[enc.layout.period:]).ravel())
+    return np.concatenate(out)
+
+
+def measure_precision(pipe, ctx, rks, state, what: str) -> dict:
+    """CKKS precision of a bench leg, measured after its timed region on one more input of the
+    leg's own shape: the largest angular deviation of ANY state slot (every state of the batch,
+    every pair of a stack) from its Zeta16 codeword over every logged stage of one encrypt (debug
+    dict of the production path), against the decode margin pi/16 -- bytes are
+    exact while it stays below (REF/utils.py:15-19, REF/state_encoder.py:30-38)."""
     E = ctx.engine
     dbg = {}
     pipe.encrypt(state, rks, debug=dbg)
-    worst, where = 0.0, None
+    worst, where, nslots = 0.0, None, 0
     for tag, entry in dbg.items():
-        cts = [entry["ct_packed"]] if "ct_packed" in entry else [entry["ct_hi"], entry["ct_lo"]]
-        for c in cts:
-            z = ctx.decrypt(c)[: 16 * pipe.layout.period] if pipe.layout.periodic else ctx.decrypt(c)
-            if not pipe.layout.periodic:
-                z = z[:16 * pipe.stride:pipe.stride]
+        cts = [(entry["ct_packed"], True)] if "ct_packed" in entry else [(entry["ct_hi"], False), (entry["ct_lo"], False)]
+        for c, packed in cts:
+            z = state_slots(pipe, ctx, c, packed)
+            nslots = max(nslots, z.size)
             ang = np.angle(z) * 16 / (2 * np.pi)
             dev = float(np.abs(ang - np.rint(ang)).max() * 2 * np.pi / 16)
             if dev > worst:
                 worst, where = dev, tag
     deltas = E.scales()
+    margin = float(np.pi / 16)
     return {"log2_delta_fresh": float(np.log2(deltas[E.fresh_level])), "log2_delta_level0": float(np.log2(deltas[0])),
-            "max_slot_angle_error_rad": worst, "worst_stage": where, "decode_margin_rad": float(np.pi / 16),
-            "stages_checked": len(dbg),
-            "note": "slot error = angular distance of every state slot to the nearest 16th root of unity, over every "
-                    "logged stage of one C2 encrypt (renorm / XOR4 / GF / SubBytes / bootstrap outputs); the bootstrap "
-                    "alone: max 2.4e-4 at |z| <= 1 (profiles/r2_boot_error.json)"}
+            "max_slot_angle_error_rad": worst, "worst_stage": where, "decode_margin_rad": margin,
+            "margin_factor": margin / worst if worst > 0 else None, "stages_checked": len(dbg),
+            "state_slots_per_stage": nslots,
+            "note": f"slot error = angular distance of every state slot to the nearest 16th root of unity, over every "
+                    f"logged stage of one encrypt of {what} (renorm / XOR4 / GF / SubBytes / bootstrap outputs)"}
 
 
 def rank_states(rank: int, n: int):
@@ -245,60 +264,188 @@ def rank_states(rank: int, n: int):
     return [rng.integers(0, 256, 16).astype(np.uint8) for _ in range(n)]
 
 
-def run_pairs(ctx, coeffs, rks, args, rank, world, dist, pairs: int, states: int, stack: int, workload: str) -> dict:
+def c5_states_per_rank(total: int, world: int) -> int:
+    """BASELINE config 5's split: `total` enc->dec states over `world` ranks, ceil(total / world)
+    each (1024 over 8 MI355X = 128 per GPU; REF/main.py:121-140's batch intent)"""
+    return max(1, -(-total // world))
+
+
+def batch_inputs(rank: int, B: int, steps: int, B5: int | None = None):
+    """the batch leg's inputs of one rank: 1 + steps arrays of (B, 16) states (warmup first), then,
+    when the C5 share B5 differs from B, 1 + steps arrays of (B5, 16) -- one seeded stream per rank,
+    so every rank encrypts its own states"""
+    rng = np.random.default_rng(4096 + rank)
+    batches = [rng.integers(0, 256, (B, 16), dtype=np.uint8) for _ in range(1 + steps)]
+    c5 = [rng.integers(0, 256, (B5, 16), dtype=np.uint8) for _ in range(1 + steps)] if B5 and B5 != B else None
+    return batches, c5
+
+
+# kernel classes timed live (one launch in --profile-every): the roofline kernels and the classes
+# whose fractions VERDICT r3 weak #2 tabulates
+PROF_KIDS = ["ntt_rows_fwd", "ntt_cols_fwd", "ntt_rows_inv", "ntt_cols_inv", "base_convert", "key_inner", "lin_mac"]
+
+
+class Leg:
+    """Live accounting of one timed leg: the algorithmic bytes and launches of
+    EVERY launch (engine counters), and, for the sampled launches of PROF_KIDS, their in-kernel
+    span and the boundary gap before them (the previous launch's drain + this one's dispatch ramp,
+    include/aesfhe.h aesfhe_kernel_gaps) -- span + gap is the dispatch-inclusive duration that
+    rocprofv3 --kernel-trace reports for the same launches."""
+
+    def __init__(self, E):
+        import mi355x_ckks
+        self.E, self.m = E, mi355x_ckks
+
+    def start(self):
+        self.E.kernel_stats(reset=True)  # flushes (device sync) and zeroes spans and gaps
+        self.alg0, self.l0 = self.m.alg_bytes(), self.m.launch_count()
+        return self
+
+    def stop(self):
+        self.alg1, self.l1 = self.m.alg_bytes(), self.m.launch_count()
+        self.work = self.E.kernel_work()
+        self.gaps = self.E.kernel_gaps()
+        self.stats = self.E.kernel_stats(reset=True)
+        return self
+
+    def bytes_by_class(self):
+        return {k: self.alg1[k][0] - self.alg0[k][0] for k in self.alg1}
+
+    def launches_by_class(self):
+        return {k: self.alg1[k][1] - self.alg0[k][1] for k in self.alg1}
+
+    def kernel(self, kid: str):
+        """(launches, span us, gap us or None, gaps measured, bytes per launch, butterflies per launch)"""
+        ks = self.stats.get(kid)
+        if not ks or ks["launches"] == 0:
+            return None
+        n = ks["launches"]
+        gn, gms = self.gaps.get(kid, (0, 0.0))
+        return n, ks["ms"] / n * 1e3, (gms / gn * 1e3 if gn else None), gn, ks["bytes"] / n, self.work.get(kid, 0.0) / n
+
+    def roofline(self, kid: str, tj: dict, every: int, note: str) -> dict | None:
+        """HBM roofline of one kernel class at its DISPATCH-INCLUSIVE average duration (span + gap,
+        comparable with rocprofv3's average for the same launches); frac_span keeps the in-kernel span"""
+        k = self.kernel(kid)
+        if k is None:
+            return None
+        n, span_us, gap_us, gn, bpl, _ = k
+        dur_us = span_us + (gap_us if gap_us is not None else 0.0)
+        achieved = bpl / (dur_us * 1e-6) / 1e9
+        t = tj.get(kid)
+        traffic = None
+        if t and t.get("traffic_over_algorithmic"):  # measured HBM / algorithmic ratio applied to this leg's launches
+            traffic = t["traffic_over_algorithmic"] * bpl
+        return {"kernel": kid, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                "traffic_over_algorithmic": t.get("traffic_over_algorithmic") if t else None,
+                "traffic_source": tj.get("_source") if t else None,
+                "timed_launches": n, "sampled_every": every, "avg_us": dur_us, "avg_us_span": span_us, "avg_us_gap": gap_us,
+                "gaps_measured": gn, "frac_span": bpl / (span_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                "timing": "avg_us = in-kernel span (first block start -> last block end, s_memrealtime) + the boundary gap "
+                          "before the launch (previous launch's last block end -> this launch's first block start), both "
+                          "measured live on the sampled launches: the dispatch-inclusive duration rocprofv3 reports",
+                "bytes_per_launch": bpl, "note": note}
+
+    def valu_roofline(self, kid: str) -> dict | None:
+        k = self.kernel(kid)
+        if k is None or not k[5]:
+            return None
+        n, span_us, gap_us, gn, bpl, bfly = k
+        dur_us = span_us + (gap_us if gap_us is not None else 0.0)
+        achieved = bfly / (dur_us * 1e-6)
+        peak = VALU_LANE_INSTR_PER_S / NTT_VALU_INSTR_PER_BFLY
+        return {"kernel": kid, "bound": "valu", "achieved": achieved, "peak": peak, "unit": "butterfly/s", "frac": achieved / peak,
+                "butterflies_per_launch": bfly, "avg_us": dur_us,
+                "note": "peak = measured u32 VALU issue rate (tools/valu_rate.hip) / VALU instructions per butterfly in the "
+                        "kernel's ISA; at the dispatch-inclusive duration"}
+
+    def step(self, elapsed: float, steps: int, tj: dict, every: int) -> dict:
+        """whole-leg roofline: algorithmic bytes of every launch / this leg's wall time / 8 TB/s, plus
+        the per-class fractions of the sampled classes and launches per step"""
+        b, n = self.bytes_by_class(), self.launches_by_class()
+        tot = sum(b.values())
+        return {"bound": "hbm", "achieved": tot / elapsed / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": tot / elapsed / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_step": tot / steps,
+                "launches_per_step": (self.l1 - self.l0) / steps,
+                "bytes_per_step_by_class": {k: v / steps for k, v in b.items() if v},
+                "launches_per_step_by_class": {k: v / steps for k, v in n.items() if v},
+                "classes": {k: r for k in PROF_KIDS if (r := self.roofline(k, tj, every, "per-class fraction (live sample)"))},
+                "note": "sum over every kernel launch of the leg's timed steps of its algorithmic bytes (each operand word "
+                        "read once, each result word written once; DESIGN.md 5) / wall time / 8 TB/s; classes at the "
+                        "dispatch-inclusive duration"}
+
+
+def run_pairs(ctx, coeffs, rks, args, rank, world, dist, pairs: int, states: int, stack: int, steps_n: int, workload: str,
+              tj: dict) -> dict:
     """Multi-pair batch: `pairs` independent ciphertext pairs of `states` states each
     per rank, run as stacked ciphertexts of `stack` pairs (AESPipeline(pairs=...)), one after the
     other; full 10-round encrypt with renorm and final bootstraps.  Whole-job blocks/s = states
-    encrypted by all ranks / max time; every pair's output checked against the plaintext AES."""
+    encrypted by all ranks / max time; every pair's output checked against the plaintext AES.
+    Warmup: ONE stack of each shape (every stack of a shape runs the same launches)."""
     from oracle import aes_plain  # checker only, after the timed region
     from pipeline import AESPipeline
     chunks = [min(stack, pairs - i) for i in range(0, pairs, stack)]
     pipes = {c: AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=True, states=states, pairs=c) for c in set(chunks)}
     rng = np.random.default_rng(8192 + rank)
     shape = lambda c: (c, 16) if states == 1 else (c, states, 16)  # noqa: E731
-    steps = [[rng.integers(0, 256, shape(c), dtype=np.uint8) for c in chunks] for _ in range(1 + args.pair_steps)]
+    warm = {c: rng.integers(0, 256, shape(c), dtype=np.uint8) for c in set(chunks)}
+    steps = [[rng.integers(0, 256, shape(c), dtype=np.uint8) for c in chunks] for _ in range(steps_n)]
     E = ctx.engine
-    for c, b in zip(chunks, steps[0]):  # warmup: masks, LUT constants, codec buffers, stacked keys
+    for c, b in warm.items():  # warmup: masks, LUT constants, codec buffers, stacked keys
         pipes[c].encrypt(b, rks)
     E.sync()
+    leg = Leg(E).start()
     barrier(dist)
     t0 = time.perf_counter()
-    outs = [[pipes[c].encrypt(b, rks) for c, b in zip(chunks, st)] for st in steps[1:]]
+    outs = [[pipes[c].encrypt(b, rks) for c, b in zip(chunks, st)] for st in steps]
     E.sync()
     barrier(dist)
-    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    elapsed = time.perf_counter() - t0
+    leg.stop()
+    elapsed = max_over_ranks(dist, elapsed)
     ok = True
-    for st, ot in zip(steps[1:], outs):
+    for st, ot in zip(steps, outs):
         for c, b, o in zip(chunks, st, ot):
             got = pipes[c].encoder.decode(*o).reshape(-1, 16)
             ok &= all(np.array_equal(got[j], aes_plain.ref_encrypt(s, rks)) for j, s in enumerate(b.reshape(-1, 16)))
     ok = all(r[0] for r in all_gather_ints(dist, [int(ok)]))
-    blocks = pairs * states * args.pair_steps * world
+    blocks = pairs * states * steps_n * world
+    c0 = chunks[0]
     return {"workload": workload, "pairs_per_rank": pairs, "states_per_pair": states, "pairs_per_stack": stack,
-            "stacks_per_step": len(chunks), "steps": args.pair_steps, "n_gpus": world,
+            "stacks_per_step": len(chunks), "steps": steps_n, "n_gpus": world,
             "blocks_per_s": blocks / elapsed, "rounds_per_s": 10.0 * blocks / elapsed,
-            "ms_per_step": elapsed / args.pair_steps * 1e3, "verified_against_plaintext_model": bool(ok)}
+            "ms_per_step": elapsed / steps_n * 1e3, "ms_per_pair": elapsed / (steps_n * pairs) * 1e3,
+            "verified_against_plaintext_model": bool(ok),
+            "roofline_step": leg.step(elapsed, steps_n, tj, args.profile_every),
+            # one-state pairs: the C2 line's precision is the same path's; a debug-logged stack of 64 would
+            # decrypt ~16k stage ciphertexts
+            "precision": measure_precision(pipes[c0], ctx, rks, warm[c0], f"one stack of {c0} pairs x {states} states")
+            if rank == 0 and states > 1 else None}
 
 
-def run_batch(ctx, coeffs, rks, args, rank, world, dist) -> dict:
+def run_batch(ctx, coeffs, rks, args, rank, world, dist, tj: dict) -> dict:
     """BASELINE configs 3/4: `--batch-states` independent states per rank under one shared
     key, slot-packed in one ciphertext pair (state b in slots i*stride + b), full 10-round
     encrypt with renorm and final bootstraps.  Whole-job blocks/s = states x ranks / max time."""
     from oracle import aes_plain  # checker only, after the timed region
     from pipeline import AESPipeline
     B = args.batch_states
+    B5 = c5_states_per_rank(args.c5_states, world)
     pipe = AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=True, states=B)
-    rng = np.random.default_rng(4096 + rank)
-    batches = [rng.integers(0, 256, (B, 16), dtype=np.uint8) for _ in range(1 + args.batch_steps)]
+    batches, ins5 = batch_inputs(rank, B, args.batch_steps, B5 if args.batch_roundtrip else None)
     E = ctx.engine
     pipe.encrypt(batches[0], rks)  # warmup: masks, LUT constants, FFT buffers
     E.sync()
+    leg = Leg(E).start()
     barrier(dist)
     t0 = time.perf_counter()
     outs = [pipe.encrypt(b, rks) for b in batches[1:]]
     E.sync()
     barrier(dist)
-    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    elapsed = time.perf_counter() - t0
+    leg.stop()
+    elapsed = max_over_ranks(dist, elapsed)
     ok = True
     for b, o in zip(batches[1:], outs):
         got = pipe.encoder.decode(*o)
@@ -308,13 +455,12 @@ def run_batch(ctx, coeffs, rks, args, rank, world, dist) -> dict:
     if args.batch_roundtrip:
         # BASELINE config 5: enc -> dec of --c5-states states in total, split across the ranks
         # (1024 = 128 per GPU at N = 8); decrypt inserts InvMixColumns
-        B5 = max(1, -(-args.c5_states // world))
-        if B5 == B:  # same shape as the batch leg: decrypt its outputs
+        if ins5 is None:  # same shape as the batch leg: decrypt its outputs
             pipe5, ins5, outs5, enc_s = pipe, batches[1:], outs, elapsed
         else:
             pipe5 = AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=True, states=B5)
-            ins5 = [rng.integers(0, 256, (B5, 16), dtype=np.uint8) for _ in range(args.batch_steps)]
             pipe5.encrypt(ins5[0], rks)  # warmup of the new shape
+            ins5 = ins5[1:]
             E.sync()
             barrier(dist)
             t1 = time.perf_counter()
@@ -322,12 +468,17 @@ def run_batch(ctx, coeffs, rks, args, rank, world, dist) -> dict:
             E.sync()
             barrier(dist)
             enc_s = max_over_ranks(dist, time.perf_counter() - t1)
+        pipe5.decrypt(*outs5[0], rks)  # warmup of the decrypt-only constants (InvSubBytes, InvMixColumns)
+        E.sync()
+        leg5 = Leg(E).start()
         barrier(dist)
         t1 = time.perf_counter()
         backs = [pipe5.decrypt(*o, rks) for o in outs5]
         E.sync()
         barrier(dist)
-        dec_s = max_over_ranks(dist, time.perf_counter() - t1)
+        dec_s = time.perf_counter() - t1
+        leg5.stop()
+        dec_s = max_over_ranks(dist, dec_s)
         exact = all(np.array_equal(pipe5.encoder.decode(*bk), b) for bk, b in zip(backs, ins5))
         exact = all(r[0] for r in all_gather_ints(dist, [int(exact)]))
         rt = {"workload": f"C5: enc->dec round trip (InvMixColumns + bootstrap + snap) of {B5 * world} states, "
@@ -335,17 +486,20 @@ def run_batch(ctx, coeffs, rks, args, rank, world, dist) -> dict:
               "states_per_rank": B5, "enc_ms_per_step": enc_s / args.batch_steps * 1e3,
               "dec_ms_per_step": dec_s / args.batch_steps * 1e3,
               "roundtrip_blocks_per_s": B5 * args.batch_steps * world / (enc_s + dec_s),
-              "roundtrip_bit_exact": bool(exact)}
+              "roundtrip_bit_exact": bool(exact),
+              "roofline_step_dec": leg5.step(dec_s, args.batch_steps, tj, args.profile_every)}
     blocks = B * args.batch_steps * world
     return {"workload": f"C3/C4: {B} independent states per GPU slot-packed in one ciphertext pair (SURVEY.md 8(f)1), "
                         f"full AES-128 encrypt, N=2^16, renorm on, shared key",
             "states_per_rank_per_step": B, "steps": args.batch_steps, "n_gpus": world,
             "blocks_per_s": blocks / elapsed, "rounds_per_s": 10.0 * blocks / elapsed,
             "ms_per_step": elapsed / args.batch_steps * 1e3, "verified_against_plaintext_model": bool(ok),
+            "roofline_step": leg.step(elapsed, args.batch_steps, tj, args.profile_every),
+            "precision": measure_precision(pipe, ctx, rks, batches[0], f"{B} slot-packed states") if rank == 0 else None,
             **({"roundtrip": rt} if rt else {})}
 
 
-def run_true_fhe(ctx, coeffs, rks, args, rank, world, dist) -> dict:
+def run_true_fhe(ctx, coeffs, rks, args, rank, world, dist, tj: dict) -> dict:
     """the C2 workload with no secret key between encryption and decryption --
     every renorm point is a bootstrap + homomorphic Zeta16 snap (zeta16_noise_reducer.py), XOR4
     normalised by 1/256.  One state per rank per step, checked after the timed region."""
@@ -355,13 +509,16 @@ def run_true_fhe(ctx, coeffs, rks, args, rank, world, dist) -> dict:
     sts = rank_states(rank + 1000, 1 + args.true_fhe_steps)
     pipe.encrypt(sts[0], rks)  # warmup: snap constants, normalised XOR4 coefficient sets
     ctx.engine.sync()
+    leg = Leg(ctx.engine).start()
     barrier(dist)
     n0 = ctx.bootstrap_stats()["count"]
     t0 = time.perf_counter()
     outs = [pipe.encrypt(s, rks) for s in sts[1:]]
     ctx.engine.sync()
     barrier(dist)
-    elapsed = max_over_ranks(dist, time.perf_counter() - t0)
+    elapsed = time.perf_counter() - t0
+    leg.stop()
+    elapsed = max_over_ranks(dist, elapsed)
     nboot = (ctx.bootstrap_stats()["count"] - n0) / args.true_fhe_steps
     ok = all(np.array_equal(pipe.encoder.decode(*o), aes_plain.ref_encrypt(s, rks)) for s, o in zip(sts[1:], outs))
     ok = all(r[0] for r in all_gather_ints(dist, [int(ok)]))
@@ -369,7 +526,52 @@ def run_true_fhe(ctx, coeffs, rks, args, rank, world, dist) -> dict:
     return {"workload": "C2 in true-FHE mode: every secret-key renorm replaced by bootstrap + depth-4 Zeta16 snap "
                         "(two snaps where the next step is an XOR4); no secret key between encryption and decryption",
             "rounds_per_s": 10.0 * done / elapsed, "ms_per_step": elapsed / args.true_fhe_steps * 1e3,
-            "bootstraps_per_encrypt": nboot, "steps": args.true_fhe_steps, "verified_against_plaintext_model": bool(ok)}
+            "bootstraps_per_encrypt": nboot, "steps": args.true_fhe_steps, "verified_against_plaintext_model": bool(ok),
+            "roofline_step": leg.step(elapsed, args.true_fhe_steps, tj, args.profile_every),
+            "precision": measure_precision(pipe, ctx, rks, sts[0], "one state, true-FHE") if rank == 0 else None}
+
+
+def run_eager(coeffs, rks, args, rank, world, dist, local, seed, tj: dict) -> dict:
+    """The per-primitive drop-in path: C2 through a SEPARATE EngineContext that
+    issues the reference's own call sequence -- every ct x ct product relinearised and rescaled at
+    once (lazy=False, REF/engine_context.py:65-68), every LUT as REF's per-term product loop
+    (fused_luts=False: REF/xor4_lut.py:71-73, REF/sub_bytes_lut.py:66-71), the reference slot
+    layout (byte i at slot i*N/32) with full-slot bootstraps (REF/mixcol_final.py:158-162).  The
+    throughput a caller gets by swapping the import line and changing nothing else."""
+    from engine_context import EngineContext
+    from oracle import aes_plain  # checker only, after the timed region
+    from pipeline import AESPipeline
+    ctx = EngineContext(signature=1, max_level=17, thread_count=1, device_id=local, seed=seed, lazy=False, fused_luts=False)
+    pipe = AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=True, periodic=False)
+    sts = rank_states(rank + 3000, 1 + args.eager_steps)
+    E = ctx.engine
+    pipe.encrypt(sts[0], rks)  # warmup: plaintext constants of the per-term loops
+    E.sync()
+    E.profile(PROF_KIDS, every=args.profile_every)
+    leg = Leg(E).start()
+    E.reset_counters()
+    barrier(dist)
+    t0 = time.perf_counter()
+    outs = [pipe.encrypt(s, rks) for s in sts[1:]]
+    E.sync()
+    barrier(dist)
+    elapsed = time.perf_counter() - t0
+    leg.stop()
+    counters = E.counters()
+    E.profile(())
+    elapsed = max_over_ranks(dist, elapsed)
+    ok = all(np.array_equal(pipe.encoder.decode(*o), aes_plain.ref_encrypt(s, rks)) for s, o in zip(sts[1:], outs))
+    ok = all(r[0] for r in all_gather_ints(dist, [int(ok)]))
+    done = args.eager_steps * world
+    out = {"workload": "C2 through EngineContext with the reference's call sequence: eager relinearise + rescale per "
+                       "product, per-term LUT product loops, reference slot layout, full-slot bootstraps",
+           "rounds_per_s": 10.0 * done / elapsed, "ms_per_step": elapsed / args.eager_steps * 1e3,
+           "steps": args.eager_steps, "verified_against_plaintext_model": bool(ok),
+           "op_counts_per_round": {k: v / (10.0 * args.eager_steps) for k, v in counters.items()},
+           "launches_per_encrypt": (leg.l1 - leg.l0) / args.eager_steps,
+           "roofline_step": leg.step(elapsed, args.eager_steps, tj, args.profile_every)}
+    del pipe, ctx
+    return out
 
 
 def dry_run(args, rank, world, dist):
@@ -398,13 +600,25 @@ def dry_run(args, rank, world, dist):
     ok = all(np.array_equal(enc.decode(*o), states[args.warmup + j] ^ key) for j, o in enumerate(outs))
     sk = ctx.eng.p.secret()
     fp = int(np.bitwise_xor.reduce((sk[:64].astype(np.int64) + 2) * np.arange(1, 65)))  # secret-key fingerprint
-    rows = all_gather_ints(dist, [int(states[args.warmup][0]), int(ok), fp])
+    # the sharding of the batch legs (no engine work): each rank's own C3/C4 batch and C5 share, the
+    # same functions run_batch uses -- digests show the ranks' inputs are distinct
+    import zlib
+    B5 = c5_states_per_rank(args.c5_states, world)
+    batches, ins5 = batch_inputs(rank, max(1, args.batch_states), args.batch_steps, B5)
+    c5_in = ins5[1:] if ins5 is not None else batches[1:]
+    dig = lambda arrs: zlib.crc32(b"".join(a.tobytes() for a in arrs))  # noqa: E731
+    rows = all_gather_ints(dist, [int(states[args.warmup][0]), int(ok), fp, B5, int(c5_in[0].shape[0]), dig(batches[1:]),
+                                  dig(c5_in)])
     if rank == 0:
         print(json.dumps({"metric": "homomorphic AES-128 rounds/sec (enc) at N=2^16", "value": None, "dry_run": True,
                           "engine": "CPU oracle per rank (N=2^13, AddRoundKey)", "n_gpus": world, "steps": args.steps,
                           "warmup": args.warmup, "elapsed_max_s": elapsed,
                           "first_byte_per_rank": [r[0] for r in rows], "ark_exact_per_rank": [bool(r[1]) for r in rows],
-                          "same_keys_on_every_rank": len({r[2] for r in rows}) == 1, "outputs": len(outs) * world}),
+                          "same_keys_on_every_rank": len({r[2] for r in rows}) == 1, "outputs": len(outs) * world,
+                          "key_fingerprints": sorted({r[2] for r in rows}),
+                          "c5_states_per_rank": [r[3] for r in rows], "c5_input_rows_per_rank": [r[4] for r in rows],
+                          "c5_states_total": sum(r[4] for r in rows),
+                          "batch_digest_per_rank": [r[5] for r in rows], "c5_digest_per_rank": [r[6] for r in rows]}),
               flush=True)
     if dist is not None:
         dist.destroy_process_group()
@@ -447,26 +661,25 @@ def main():
         pipe.encrypt(states[i], rks)
     E.sync()
     import mi355x_ckks
-    # the roofline kernels, plus the forward NTT's first pass and the base conversion (per-class
-    # fractions beside the whole-step one)
-    kernels = list(mi355x_ckks.KERNEL_IDS) if args.profile_all else list(dict.fromkeys([args.kernel, args.kernel2, "ntt_cols_fwd",
-                                                                                       "base_convert"]))
+    tj = json.loads(Path(args.traffic_json).read_text()) if args.traffic_json and Path(args.traffic_json).exists() else {}
+    every = 1 if args.profile_all else args.profile_every
+    # the sampled kernel classes (PROF_KIDS: the roofline kernels and the per-class fractions)
+    kernels = list(mi355x_ckks.KERNEL_IDS) if args.profile_all else list(dict.fromkeys([args.kernel, args.kernel2] + PROF_KIDS))
     whole = args.whole_stats and os.environ.get("AESFHE_PROFILE_FROM_START")
     pre = {}
     if whole:  # whole-process accounting: keep the from-start configuration, fold the pre-timed part in
         pre = E.kernel_stats(reset=True)
     else:
-        E.profile(kernels, every=1 if args.profile_all else args.profile_every)
-        # one profiled, untimed encrypt fills the profiler's event pool, so the timed steps
-        # create no HIP events
+        E.profile(kernels, every=every)
+        # one profiled, untimed encrypt allocates the profiler's clock slots outside the timing
         pipe.encrypt(states[0], rks)
         E.sync()
-        E.kernel_stats(reset=True)
     E.reset_counters()
 
     outs = []
-    barrier(dist)
     E.sync()
+    leg = Leg(E).start() if not whole else None
+    barrier(dist)
     # AESFHE_MARK_TIMED=1: a 250 ms idle gap on each side of the timed region (outside the timing),
     # so tools/trace_window.py can pick the timed launches out of a rocprofv3 kernel trace
     mark = os.environ.get("AESFHE_MARK_TIMED") == "1"
@@ -482,24 +695,32 @@ def main():
     alg1, launches1 = mi355x_ckks.alg_bytes(), mi355x_ckks.launch_count()
     if mark:
         time.sleep(0.25)
-    elapsed = max_over_ranks(dist, elapsed)
-    work = E.kernel_work()
-    stats = E.kernel_stats(reset=True)
     counters = E.counters()
     if whole:
+        stats = E.kernel_stats(reset=True)
         tot = {k: {f: pre.get(k, {}).get(f, 0) + v.get(f, 0) for f in ("launches", "ms", "bytes")} for k, v in stats.items()}
         Path(args.whole_stats).write_text(json.dumps(tot, indent=1))
-    E.profile(())
-    batch = run_batch(ctx, coeffs, rks, args, rank, world, dist) if args.batch_states > 0 else None
-    pairs_c3 = run_pairs(ctx, coeffs, rks, args, rank, world, dist, args.pair_states, 1, max(1, args.pair_stack),
-                         f"C3 shape: {args.pair_states} ciphertext pairs per GPU with ONE state each (REF/state_encoder.py:17-28), "
-                         f"stacked {args.pair_stack} pairs per operand (DESIGN.md 3.16), full AES-128 encrypt, N=2^16, renorm on, "
-                         f"shared key") if args.pair_states > 0 else None
+    else:
+        leg.stop()
+    elapsed = max_over_ranks(dist, elapsed)
+    launches_per_encrypt = (launches1 - launches0) / args.steps
+    # (a --whole-stats run skips it: its rocprofv3 --pmc pass must count exactly the accounted launches)
+    precision = measure_precision(pipe, ctx, rks, states[0], "one C2 state") if rank == 0 and not whole else None
+
+    batch = run_batch(ctx, coeffs, rks, args, rank, world, dist, tj) if args.batch_states > 0 else None
+    pairs_c3 = run_pairs(ctx, coeffs, rks, args, rank, world, dist, args.pair_states, 1, max(1, args.pair_stack), args.pair_steps,
+                         f"C3 literally: {args.pair_states} ciphertext pairs (hi/lo) per GPU with ONE state each "
+                         f"(REF/state_encoder.py:17-28), stacked {args.pair_stack} pairs per operand (DESIGN.md 3.16), full "
+                         f"AES-128 encrypt, N=2^16, renorm on, shared key", tj) if args.pair_states > 0 else None
     pairs_packed = run_pairs(ctx, coeffs, rks, args, rank, world, dist, args.packed_pairs, 2048, args.packed_pairs,
+                             args.packed_pair_steps,
                              f"{args.packed_pairs} x 2048 states per GPU: {args.packed_pairs} slot-packed ciphertext pairs stacked "
-                             f"into one operand (DESIGN.md 3.9 + 3.16), full AES-128 encrypt, N=2^16, renorm on, shared key"
-                             ) if args.packed_pairs > 0 else None
-    true_fhe = run_true_fhe(ctx, coeffs, rks, args, rank, world, dist) if args.true_fhe_steps > 0 and not args.no_final_bootstrap else None
+                             f"into one operand (DESIGN.md 3.9 + 3.16), full AES-128 encrypt, N=2^16, renorm on, shared key",
+                             tj) if args.packed_pairs > 0 else None
+    true_fhe = (run_true_fhe(ctx, coeffs, rks, args, rank, world, dist, tj)
+                if args.true_fhe_steps > 0 and not args.no_final_bootstrap else None)
+    E.profile(())
+    eager = run_eager(coeffs, rks, args, rank, world, dist, local, seed, tj) if args.eager_steps > 0 else None
 
     # correctness of the timed outputs (outside the timed region)
     ok = all(np.array_equal(pipe.encoder.decode(*o), aes_plain.ref_encrypt(states[args.warmup + j], rks))
@@ -508,53 +729,17 @@ def main():
 
     states_done = args.steps * world
     value = 10.0 * states_done / elapsed
-    # whole-step roofline: algorithmic bytes of EVERY launch of the
-    # timed steps (engine accounting, per kernel class) / this rank's wall time / 8 TB/s
-    step_bytes = {k: alg1[k][0] - alg0[k][0] for k in alg1}
-    step_launches = {k: alg1[k][1] - alg0[k][1] for k in alg1}
-    rank_elapsed = elapsed  # max over ranks; each rank's bytes are its own steps
-    roofline_step = {"bound": "hbm", "achieved": sum(step_bytes.values()) / rank_elapsed / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": sum(step_bytes.values()) / rank_elapsed / 1e9 / HBM_PEAK_GBS,
-                     "algorithmic_bytes_per_step": sum(step_bytes.values()) / args.steps,
-                     "bytes_per_step_by_class": {k: v / args.steps for k, v in step_bytes.items() if v},
-                     "launches_per_step_by_class": {k: v / args.steps for k, v in step_launches.items() if v},
-                     "note": "sum over every kernel launch of the timed encrypts of its algorithmic bytes (each operand word "
-                             "read once, each result word written once; DESIGN.md 5) / wall time / 8 TB/s"}
-    launches_per_encrypt = (launches1 - launches0) / args.steps
-    precision = measure_precision(pipe, ctx, rks, states[0]) if rank == 0 else None
-    tj = json.loads(Path(args.traffic_json).read_text()) if args.traffic_json and Path(args.traffic_json).exists() else {}
-
-    def roofline(kid: str, note: str) -> dict:
-        ks = stats.get(kid, {"launches": 0, "ms": 0.0, "bytes": 0.0})
-        achieved = ks["bytes"] / (ks["ms"] * 1e-3) / 1e9 if ks["ms"] > 0 else 0.0
-        t = tj.get(kid)
-        bpl = ks["bytes"] / max(ks["launches"], 1)
-        traffic = None
-        if t and t.get("traffic_over_algorithmic"):  # measured HBM/algorithmic ratio applied to this run's launches
-            traffic = t["traffic_over_algorithmic"] * bpl
-        elif t:
-            traffic = t["bytes_per_launch"]
-        return {"kernel": kid, "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                "traffic_over_algorithmic": t.get("traffic_over_algorithmic") if t else None,
-                "traffic_source": tj.get("_source") if t else None,
-                "timed_launches": ks["launches"], "sampled_every": 1 if args.profile_all else args.profile_every,
-                "avg_us": ks["ms"] / max(ks["launches"], 1) * 1e3,
-                "timing": "in-kernel span of each sampled launch (first block start -> last block end, s_memrealtime); "
-                          "rocprofv3 durations of the same launches add the dispatch ramp and drain, 1.9-2.7 us per "
-                          "launch (profiles/r3_live_timing_check.json)",
-                "bytes_per_launch": ks["bytes"] / max(ks["launches"], 1), "note": note}
-
-    def valu_roofline(kid: str) -> dict | None:
-        ks = stats.get(kid, {"ms": 0.0, "launches": 0})
-        if not work.get(kid) or ks["ms"] <= 0:
-            return None
-        achieved = work[kid] / (ks["ms"] * 1e-3)
-        peak = VALU_LANE_INSTR_PER_S / NTT_VALU_INSTR_PER_BFLY
-        return {"kernel": kid, "bound": "valu", "achieved": achieved, "peak": peak, "unit": "butterfly/s", "frac": achieved / peak,
-                "butterflies_per_launch": work[kid] / max(ks["launches"], 1),
-                "note": "peak = measured u32 VALU issue rate (tools/valu_rate.hip) / VALU instructions per butterfly in the "
-                        "kernel's ISA; the NTT passes are VALU-bound (HBM traffic ~ algorithmic bytes, profiles/r2_pmc_traffic_round.json)"}
+    if whole:
+        roof = dict(roofline=None, roofline_secondary=None, roofline_valu=None, roofline_step=None)
+    else:
+        roof = dict(
+            roofline=leg.roofline(args.kernel, tj, every, "dominant kernel by time (NTT pass 2 incl. fused rescale/ModDown "
+                                                          "epilogue); VALU / latency-bound: ~11.8 VALU instructions per lazy "
+                                                          "butterfly, u32 multiplies at full rate (DESIGN.md 5)"),
+            roofline_secondary=leg.roofline(args.kernel2, tj, every, "key-switch inner product: HBM-bound"),
+            roofline_valu=leg.valu_roofline(args.kernel),
+            # whole-step roofline: algorithmic bytes of EVERY launch of the timed steps
+            roofline_step=leg.step(elapsed, args.steps, tj, every))
 
     line = {
         "metric": "homomorphic AES-128 rounds/sec (enc) at N=2^16",
@@ -580,16 +765,13 @@ def main():
                     "(DESIGN.md 3.7), fused LUT kernels with one relinearisation per LUT, XOR4/GF LUTs over a conjugate "
                     "split, SubBytes by baby-step giant-step (3.8), XOR chain as a tree (6), hoisted column rotations, "
                     "inputs dropped to the renorm floor before renormalised steps (3.11), batched products (3.12); "
-                    "the engine op counts per round are in op_counts_per_round (REF's call sequence issues ~1,034 "
-                    "relinearisations per round, SURVEY.md 8(a))"),
+                    "the engine op counts per round are in op_counts_per_round; REF's own call sequence through the "
+                    "same engine is the eager_ref_calls leg"),
                    "blocks_per_s": states_done / elapsed, "verified_against_plaintext_model": bool(ok)},
-        "roofline": roofline(args.kernel, "dominant kernel by time (NTT pass 2 incl. fused rescale/ModDown epilogue); "
-                                          "VALU / latency-bound: ~11.8 VALU instructions per lazy butterfly, u32 multiplies at full rate (DESIGN.md 5)"),
-        "roofline_secondary": roofline(args.kernel2, "key-switch inner product: HBM-bound"),
-        "roofline_valu": valu_roofline(args.kernel),
-        "roofline_step": roofline_step,
-        "roofline_classes": {k: roofline(k, "per-class fraction (live sample)") for k in ("ntt_cols_fwd", "base_convert")
-                             if k in stats},
+        "parity": "decoded bytes verified against FIPS-197 AES (oracle/aes_plain.py) for every timed output of every leg; "
+                  "engine residues bit-exact against the C oracle (oracle/ckks_oracle.c) in tests/test_gpu_parity.py; "
+                  "raw-ciphertext parity with the reference's desilofhe engine is unpinnable (closed binary, absent)",
+        **roof,
         "launches_per_encrypt": launches_per_encrypt,
         "precision": precision,
         "op_counts_per_round": {k: v / (10.0 * args.steps) for k, v in counters.items()},
@@ -602,9 +784,8 @@ def main():
         line["batch_packed_pairs"] = pairs_packed
     if true_fhe is not None:
         line["true_fhe"] = true_fhe
-    if args.profile_all:
-        line["kernels"] = {k: {"launches": v["launches"], "ms": v["ms"], "GBps": v["bytes"] / (v["ms"] * 1e-3) / 1e9 if v["ms"] else 0}
-                           for k, v in stats.items()}
+    if eager is not None:
+        line["eager_ref_calls"] = eager
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(coeffs)

@@ -312,7 +312,16 @@ int aesfhe_kernel_stats(aesfhe_ctx* ctx, double* out, int n, int reset);
 /* radix-2 butterflies of the timed NTT launches per kernel id (out[n]; call before a resetting
  * aesfhe_kernel_stats): the numerator of the NTT's VALU roofline */
 int aesfhe_kernel_work(aesfhe_ctx* ctx, double* out, int n);
+/* dispatch-inclusive timing: per kernel id k, out[2k] = boundary gaps measured, out[2k + 1] = their
+ * total ms -- the gap between the last block end of a sampled launch and the first block start of
+ * the launch issued right after it, accounted to the latter's id (its drain + dispatch ramp, what
+ * rocprofv3 durations add to the in-kernel span); call before a resetting aesfhe_kernel_stats */
+int aesfhe_kernel_gaps(aesfhe_ctx* ctx, double* out, int n);
 int aesfhe_reset_counters(aesfhe_ctx* ctx);
+/* device memory pool: out[0] = bytes the context's buffer pools hold (in use + cached), out[1] =
+ * allocations that failed, released the cached free lists and were retried (a second failure is
+ * an error status).  AESFHE_POOL_LIMIT_MB caps the pool bytes (test switch) */
+int aesfhe_pool_stats(aesfhe_ctx* ctx, uint64_t* out);
 /* kernel launches issued by this process so far (all contexts): the launch census of
  * tools/launch_census.py and bench.py's launches-per-encrypt (MI355X-side tooling) */
 uint64_t aesfhe_launch_count(void);

@@ -1,0 +1,67 @@
+#!/bin/bash
+# One parametrised GPU driver (through gpurun, from the repo root), replacing round 3's one-off
+# r3_*.sh launchers.  usage: bash tools/gpu_task.sh OUT task [task ...]; results under gpurun_out/OUT.
+# Every GPU step has its own time limit; set -e ends the call at the first failure.
+#   tests [-- pytest args]  the -m gpu suite (or the named test files: TESTS="tests/a.py tests/b.py")
+#   smoke                   __graft_entry__.smoke()
+#   bench                   the default bench line (BENCH_rNN's command)
+#   c2                      the C2 leg alone, 12 steps (BENCH_ARGS overrides)
+#   rocwin                  rocprofv3 --kernel-trace --stats of the C2 leg, timed window averages
+#                           (tools/trace_window.py) beside the bench's own live dispatch-inclusive averages
+#   pmc                     FETCH_SIZE / WRITE_SIZE passes (separate runs) over the C2 leg, reduced to
+#                           per-class traffic / algorithmic bytes (tools/pmc_reduce.py)
+#   twogpu                  torchrun --nproc-per-node=2 bench.py --gpus 2 over gloo on ONE MI355X (both ranks
+#                           share it): the N > 1 engine path at the C4 / C5 per-rank shapes
+#   boot                    tools/boot_phases.py 32 (sparse bootstrap phases)
+#   census                  tools/launch_census.py (launches / ms per AES step)
+#   stack                   tools/step_profile.py on the 64-pair stacked leg
+set -e -o pipefail
+O=gpurun_out/${1:?out dir}
+shift
+mkdir -p $O
+export TMPDIR=/tmp
+C2="--no-cpu-baseline --batch-states 0 --true-fhe-steps 0 --pair-states 0 --packed-pairs 0 --eager-steps 0"
+for t in "$@"; do
+  echo "[gpu_task] $t $(date +%T)"
+  case $t in
+    tests)
+      timeout -k 10 900 python3 -u -m pytest ${TESTS:-tests} -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+      tail -2 $O/pytest_gpu.log ;;
+    smoke)
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
+    bench)
+      timeout -k 10 900 python3 bench.py ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err ;;
+    c2)
+      timeout -k 10 400 python3 bench.py --steps 12 --warmup 2 $C2 ${BENCH_ARGS:-} > $O/c2.json 2> $O/c2.err ;;
+    rocwin)
+      AESFHE_MARK_TIMED=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
+          python3 bench.py --steps 12 --warmup 2 $C2 > $O/bench_under_rocprof.json 2> $O/rocwin.err
+      cp $O/prof/run_kernel_stats.csv $O/kernel_stats.csv
+      timeout -k 10 120 python3 tools/trace_window.py $O/kernel_stats_timed.json $O/prof
+      rm -f $O/prof/run_kernel_trace.csv ;;
+    pmc)
+      KIDS=key_inner,base_convert,ntt_cols_fwd,ntt_rows_fwd,ntt_rows_inv,ntt_cols_inv,lin_mac
+      RX='k_ntt1_fwd|k_ntt2_fwd|k_ntt1_inv|k_ntt2_inv|k_lin_mac|k_base_convert|k_key_inner'
+      P="bench.py --steps 2 --warmup 1 $C2"
+      AESFHE_PROFILE_FROM_START=$KIDS timeout -k 10 300 python3 $P --whole-stats $O/pmc_algorithmic.json > $O/pmc_alg.out
+      AESFHE_PROFILE_FROM_START=$KIDS timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$RX" --output-format csv \
+          -d $O/pmc_fetch -o run -- python3 $P --whole-stats $O/pmc_alg_fetch.json > $O/pmc_fetch.out 2> $O/pmc_fetch.err
+      AESFHE_PROFILE_FROM_START=$KIDS timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$RX" --output-format csv \
+          -d $O/pmc_write -o run -- python3 $P --whole-stats $O/pmc_alg_write.json > $O/pmc_write.out 2> $O/pmc_write.err
+      timeout -k 10 300 python3 tools/pmc_reduce.py "--source=rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes (separate runs, --kernel-include-regex on the NTT / conversion / key-switch / lin_mac kernels) over the bench's own C2 leg (bench.py --steps 2 --warmup 1, whole process incl. key generation; algorithmic bytes of exactly those launches from the engine, AESFHE_PROFILE_FROM_START + --whole-stats); FETCH_SIZE x2 for 16-B-per-lane reads, x1 for NTT pass 2 dword reads (tools/ntt_pmc_calib.py); L2-miss bytes (MALL hits included), an upper bound on HBM bytes" \
+          --alg=$O/pmc_algorithmic.json $O/pmc_traffic_bench.json $O/pmc_fetch $O/pmc_write > /dev/null
+      rm -rf $O/pmc_fetch $O/pmc_write ;;
+    twogpu)
+      AESFHE_DIST_BACKEND=gloo timeout -k 10 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr=127.0.0.1 \
+          --master-port=29517 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline --batch-states 1024 --c5-states 256 \
+          --pair-states 0 --packed-pairs 0 --true-fhe-steps 0 --eager-steps 0 > $O/bench_2rank_1gpu.json 2> $O/twogpu.err ;;
+    boot)
+      timeout -k 10 300 python3 tools/boot_phases.py 32 > $O/boot_phases.json 2> $O/boot.err ;;
+    census)
+      timeout -k 10 300 python3 tools/launch_census.py > $O/launch_census.json 2> $O/census.err ;;
+    stack)
+      timeout -k 10 600 python3 tools/step_profile.py ${STACK_ARGS:-pairs=64} > $O/stack_profile.json 2> $O/stack.err ;;
+    *) echo "unknown task $t"; exit 2 ;;
+  esac
+done
+echo "[gpu_task] done $(date +%T)"
