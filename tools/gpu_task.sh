@@ -14,7 +14,9 @@
 #                           share it): the N > 1 engine path at the C4 / C5 per-rank shapes
 #   boot                    tools/boot_phases.py 32 (sparse bootstrap phases)
 #   census                  tools/launch_census.py (launches / ms per AES step)
-#   stack                   tools/step_profile.py on the 64-pair stacked leg
+#   stack                   tools/step_profile.py on the 64-pair stacked leg (STACK_ARGS)
+#   sweep                   tools/ntt_grid_sweep.py (NTT time vs rows per block-size configuration)
+#   probes                  tools/micro/grid_sync_probe + graph_gap_probe (built here by hipcc)
 set -e -o pipefail
 O=gpurun_out/${1:?out dir}
 shift
@@ -60,7 +62,12 @@ for t in "$@"; do
     census)
       timeout -k 10 300 python3 tools/launch_census.py > $O/launch_census.json 2> $O/census.err ;;
     stack)
-      timeout -k 10 600 python3 tools/step_profile.py ${STACK_ARGS:-pairs=64} > $O/stack_profile.json 2> $O/stack.err ;;
+      timeout -k 10 600 python3 tools/step_profile.py ${STACK_ARGS:-pairs=64 reps=1} > $O/stack_profile.json 2> $O/stack.err ;;
+    sweep)
+      timeout -k 10 600 python3 tools/ntt_grid_sweep.py > $O/ntt_grid_sweep.json 2> $O/sweep.err ;;
+    probes)
+      timeout -k 10 120 tools/micro/grid_sync_probe > $O/grid_sync_probe.json
+      timeout -k 10 120 tools/micro/graph_gap_probe > $O/graph_gap_probe.json ;;
     *) echo "unknown task $t"; exit 2 ;;
   esac
 done

@@ -21,6 +21,27 @@ __global__ void __launch_bounds__(512) k_sync(unsigned* buf, int steps) {
     }
     buf[(size_t)blockIdx.x * 512 + threadIdx.x] = v;
 }
+// the same with a hand-written barrier: one monotonic counter, a vector atomic add per block and an
+// acquire spin on a vector atomic load (no cooperative-groups machinery)
+__device__ __forceinline__ void bar_sync(unsigned* bar, unsigned& gen) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned target = (gen + 1) * gridDim.x;
+        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
+    }
+    ++gen;
+    __syncthreads();
+}
+__global__ void __launch_bounds__(512) k_sync2(unsigned* buf, unsigned* bar, int steps) {
+    unsigned v = 0, gen = 0;
+    for (int s = 0; s < steps; ++s) {
+        buf[(size_t)blockIdx.x * 512 + threadIdx.x] = v + s;
+        bar_sync(bar, gen);
+        v += buf[(size_t)((blockIdx.x + 1) % gridDim.x) * 512 + threadIdx.x];
+    }
+    buf[(size_t)blockIdx.x * 512 + threadIdx.x] = v;
+}
 __global__ void __launch_bounds__(512) k_step(unsigned* buf, int s) {
     const unsigned v = buf[(size_t)((blockIdx.x + 1) % gridDim.x) * 512 + threadIdx.x];
     buf[(size_t)blockIdx.x * 512 + threadIdx.x] = v + s;
@@ -57,9 +78,22 @@ int main() {
         for (int s = 0; s <= steps; ++s) k_step<<<blocks, 512, 0, st>>>(buf, s);
         CK(hipStreamSynchronize(st));
         auto t3 = std::chrono::steady_clock::now();
+        unsigned* bar = nullptr;
+        CK(hipMalloc(&bar, 64));
+        CK(hipMemset(bar, 0, 64));
+        void* args2[] = {&buf, &bar, &s_arg};
+        CK(hipLaunchCooperativeKernel((const void*)k_sync2, dim3(blocks), dim3(512), args2, 0, st));
+        CK(hipStreamSynchronize(st));
+        CK(hipMemset(bar, 0, 64));
+        auto t4 = std::chrono::steady_clock::now();
+        CK(hipLaunchCooperativeKernel((const void*)k_sync2, dim3(blocks), dim3(512), args2, 0, st));
+        CK(hipStreamSynchronize(st));
+        auto t5 = std::chrono::steady_clock::now();
+        CK(hipFree(bar));
+        const double us_bar = std::chrono::duration<double, std::micro>(t5 - t4).count() / steps;
         const double us_sync = std::chrono::duration<double, std::micro>(t1 - t0).count() / steps;
         const double us_launch = std::chrono::duration<double, std::micro>(t3 - t2).count() / (steps + 1);
-        std::printf("%s{\"blocks\": %d, \"us_per_grid_sync\": %.3f, \"us_per_kernel_boundary\": %.3f}", first ? "" : ", ", blocks, us_sync, us_launch);
+        std::printf("%s{\"blocks\": %d, \"us_per_grid_sync\": %.3f, \"us_per_atomic_barrier\": %.3f, \"us_per_kernel_boundary\": %.3f}", first ? "" : ", ", blocks, us_sync, us_bar, us_launch);
         first = false;
     }
     std::printf("]}\n");
