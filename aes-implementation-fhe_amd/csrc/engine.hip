@@ -1360,7 +1360,10 @@ public:
     // tp (tensor mode, relin_rescale_tensor): member m's source rows are the products tp->a[m] (.) tp->b[m],
     // formed inside the inverse NTT (d unused)
     // rev: the source rows read in reversed coefficient order (the conjugation's permutation, galois)
-    u32* modup(const u32* d, int level, int nb = 1, size_t d_ms = 0, const TensorPtrs* tp = nullptr, bool rev = false) {
+    // cols_only: the extended rows' forward NTT stops after its column pass (the row pass runs inside
+    // the fused key-switch core, ki_core)
+    u32* modup(const u32* d, int level, int nb = 1, size_t d_ms = 0, const TensorPtrs* tp = nullptr, bool rev = false,
+               bool cols_only = false) {
         const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, alpha = hp_.alpha;
         const int nd = (nl + alpha - 1) / alpha;
         if (alpha > kMaxConvH || np > kMaxConvH || nb * nd > kMaxConvGroups) throw std::runtime_error("keyswitch: digit too large");
@@ -1394,14 +1397,44 @@ public:
         RowMap xr = rows_dense(ne);
         xr.skip_alpha = alpha, xr.skip_nl = nl, xr.skip_groups = nd;
         if (fz) {
+            if (cols_only) throw std::runtime_error("modup: the fused conversion has no column-pass-only form");
             launch_ntt_fwd_conv(S(), T_, ext, up, nb * nd * ne, xr, em);
             cnt_[C_NTT_ROWS] += nb * nd * ne;
         } else {
             launch_base_convert(S(), T_, up, ne, em);
-            ntt(ext, ext, nb * nd * ne, xr, em);
+            if (cols_only) {
+                launch_ntt_fwd_cols(S(), T_, ext, ext, nb * nd * ne, xr, em);
+                cnt_[C_NTT_ROWS] += nb * nd * ne;
+            } else {
+                ntt(ext, ext, nb * nd * ne, xr, em);
+            }
         }
         untmp(coef, (size_t)nb * nl);
         return ext;
+    }
+    // ------------------------------------------------------------------ fused key-switch core
+    // launch_ntt_ki: the ModUp's row pass, the key inner product and the ModDown
+    // INTT's row pass in ONE launch.  acc rows x < kept are written ([m][2][ne], the finish's cur);
+    // rows x >= kept go to ys ([m][2][ne - kept]) transformed by the inverse row pass -- the
+    // ModDown then runs only its INTT column pass on ys.  AESFHE_FUSED_KI=0: the separate launches.
+    bool fused_ki_ = std::getenv("AESFHE_FUSED_KI") == nullptr || std::getenv("AESFHE_FUSED_KI")[0] != '0';
+    bool fused_ki_ok() const { return fused_ki_ && !fused_conv(true) && !fused_conv(false); }
+    struct KiSrc {
+        const u32* ext;
+        const u32* d;
+        const u32* key;
+    };
+    void ki_core(u32* acc, u32* ys, int level, int kept, int nb, const KiSrc* src, int nsrc, size_t d_ms, KsFold fold) {
+        const int nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, n = hp_.n;
+        KiArgs a;
+        for (int i = 0; i < nsrc; ++i) a.ext[i] = src[i].ext, a.d[i] = src[i].d, a.key[i] = src[i].key;
+        a.nsrc = nsrc;
+        a.nd = (nl + hp_.alpha - 1) / hp_.alpha, a.ne = ne, a.nl = nl, a.alpha = hp_.alpha;
+        a.nkey = hp_.n_ks + np, a.nks = hp_.n_ks;
+        a.kept = kept, a.ys_rows = ne - kept, a.nb = nb;
+        a.ext_ms = (size_t)a.nd * ne * n, a.d_ms = d_ms, a.acc_ms = (size_t)2 * ne * n, a.ys_ms = (size_t)2 * (ne - kept) * n;
+        a.acc = acc, a.ys = ys, a.fold = fold;
+        launch_ntt_ki(S(), T_, a, extmap(nl));  // its row passes are counted with the column passes they pair with
     }
     int ext_rows(int level) const { return (hp_.nl(level) + hp_.alpha - 1) / hp_.alpha * (hp_.nl(level) + hp_.n_p); }
     // acc (2 x ne rows, Q*P) = sum_j ext_j * key_j; g != 0 reads ext and d through X -> X^g
@@ -1419,13 +1452,20 @@ public:
     // dst: write the result there (member stride 2 nl N; the caller owns it) instead of a new buffer
     // outm: member m's result into outm[m] (nb <= 8; the returned Ct then carries no data)
     // add_rev: add0 read in reversed coefficient order (the conjugation's c0, galois)
+    // ys_in: the P rows already through the INTT's row pass (ki_core, [m][2][np]): only its column pass runs here
     Ct moddown(const u32* acc, int level, const u32* add0, const u32* add1, int nb = 1, size_t add_ms = 0, u32* dst = nullptr,
-               u32* const* outm = nullptr, bool add_rev = false) {
+               u32* const* outm = nullptr, bool add_rev = false, u32* ys_in = nullptr) {
         const int n = hp_.n, nl = hp_.nl(level), np = hp_.n_p, ne = nl + np, npl = 2 * nb;
         if (npl > kMaxConvGroups) throw std::runtime_error("moddown: batch too large");
         const bool fz = fused_conv(false);
-        u32* yp = tmp((size_t)npl * np);
-        intt(yp, acc, npl * np, RowMap{np, ne, np, nl, 0}, LimbMap{np, hp_.p_off(), 0}, fz ? d_moddown_phinv_ : nullptr);
+        u32* yp = ys_in ? ys_in : tmp((size_t)npl * np);
+        if (ys_in) {
+            if (fz) throw std::runtime_error("moddown: a fused-core input needs the separate conversion");
+            launch_ntt_inv_cols(S(), T_, yp, npl * np, rows_dense(np), LimbMap{np, hp_.p_off(), 0});
+            cnt_[C_NTT_ROWS] += (size_t)npl * np;
+        } else {
+            intt(yp, acc, npl * np, RowMap{np, ne, np, nl, 0}, LimbMap{np, hp_.p_off(), 0}, fz ? d_moddown_phinv_ : nullptr);
+        }
         u32* conv = tmp((size_t)npl * nl);
         const size_t doff = moddown_off_[nl];
         ConvBatch dn;
@@ -1451,7 +1491,7 @@ public:
         else
             launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_pinv_, add0, add1, npl, nl, add_ms, outm, 0u, nullptr, add_rev);
         cnt_[C_NTT_ROWS] += (size_t)npl * nl;
-        untmp(yp, (size_t)npl * np);
+        if (!ys_in) untmp(yp, (size_t)npl * np);
         untmp(conv, (size_t)npl * nl);
         return o;
     }
@@ -1475,6 +1515,20 @@ public:
                 keyswitch(d + m0 * d_ms, level, key, add0 ? add0 + m0 * add_ms : nullptr, add1 ? add1 + m0 * add_ms : nullptr, c, d_ms, add_ms,
                           o.data + m0 * oms);
             }
+            return o;
+        }
+        if (fused_ki_ok()) {
+            const int np = hp_.n_p;
+            u32* ext = modup(d, level, nb, d_ms, nullptr, false, true);
+            u32* acc = tmp(2 * (size_t)ne * nb);
+            u32* ys = tmp(2 * (size_t)np * nb);
+            const KiSrc src{ext, d, key};
+            ki_core(acc, ys, level, hp_.nl(level), nb, &src, 1, d_ms, KsFold{});
+            untmp(ext, (size_t)nb * ext_rows(level));
+            Ct o = moddown(acc, level, add0, add1, nb, add_ms, dst, nullptr, false, ys);
+            untmp(ys, 2 * (size_t)np * nb);
+            untmp(acc, 2 * (size_t)ne * nb);
+            cnt_[C_KS] += nb;
             return o;
         }
         u32* ext = modup(d, level, nb, d_ms);
@@ -1581,21 +1635,49 @@ public:
             for (int m0 = 0; m0 < nb; m0 += ch) {
                 const int k = std::min(ch, nb - m0);
                 const u32* base = c.data + m0 * ms;
+                const KsFold fold{base, base + (size_t)nl * n, ms, d_gadget_};
+                if (fused_ki_ok()) {
+                    const int h = ne - hp_.nl(l - 1);
+                    u32* ext = modup(base + (size_t)2 * nl * n, l, k, ms, nullptr, false, true);
+                    u32* acc = tmp(2 * (size_t)ne * k);
+                    u32* ys = tmp(2 * (size_t)h * k);
+                    const KiSrc src{ext, base + (size_t)2 * nl * n, ksk(0)};
+                    ki_core(acc, ys, l, hp_.nl(l - 1), k, &src, 1, ms, fold);
+                    untmp(ext, (size_t)k * ext_rows(l));
+                    moddown_rescale(acc, l, k, o.data + m0 * oms, nullptr, nullptr, ys);
+                    untmp(ys, 2 * (size_t)h * k);
+                    untmp(acc, 2 * (size_t)ne * k);
+                    continue;
+                }
                 u32* ext = modup(base + (size_t)2 * nl * n, l, k, ms);
                 u32* acc = tmp(2 * (size_t)ne * k);
-                key_inner(acc, ext, base + (size_t)2 * nl * n, ksk(0), l, 0, k, ms, KsFold{base, base + (size_t)nl * n, ms, d_gadget_});
+                key_inner(acc, ext, base + (size_t)2 * nl * n, ksk(0), l, 0, k, ms, fold);
                 untmp(ext, (size_t)k * ext_rows(l));
                 moddown_rescale(acc, l, k, o.data + m0 * oms);
                 untmp(acc, 2 * (size_t)ne * k);
             }
         } else {
             const u32* d2 = c.data + (size_t)2 * nl * n;
-            u32* ext = modup(d2, l, nb, ms);
-            u32* acc = tmp(2 * (size_t)ne * nb);
-            key_inner(acc, ext, d2, ksk(0), l, 0, nb, ms, KsFold{c.data, c.data + (size_t)nl * n, ms, d_gadget_});
-            untmp(ext, (size_t)nb * ext_rows(l));
-            o = moddown_rescale(acc, l, nb, nullptr, outm);
-            untmp(acc, 2 * (size_t)ne * nb);
+            const KsFold fold{c.data, c.data + (size_t)nl * n, ms, d_gadget_};
+            if (fused_ki_ok()) {
+                const int h = ne - hp_.nl(l - 1);
+                u32* ext = modup(d2, l, nb, ms, nullptr, false, true);
+                u32* acc = tmp(2 * (size_t)ne * nb);
+                u32* ys = tmp(2 * (size_t)h * nb);
+                const KiSrc src{ext, d2, ksk(0)};
+                ki_core(acc, ys, l, hp_.nl(l - 1), nb, &src, 1, ms, fold);
+                untmp(ext, (size_t)nb * ext_rows(l));
+                o = moddown_rescale(acc, l, nb, nullptr, outm, nullptr, ys);
+                untmp(ys, 2 * (size_t)h * nb);
+                untmp(acc, 2 * (size_t)ne * nb);
+            } else {
+                u32* ext = modup(d2, l, nb, ms);
+                u32* acc = tmp(2 * (size_t)ne * nb);
+                key_inner(acc, ext, d2, ksk(0), l, 0, nb, ms, fold);
+                untmp(ext, (size_t)nb * ext_rows(l));
+                o = moddown_rescale(acc, l, nb, nullptr, outm);
+                untmp(acc, 2 * (size_t)ne * nb);
+            }
         }
         o.pend = c.pend - 1;
         o.lazy = c.lazy && o.pend > 0;
@@ -1625,6 +1707,21 @@ public:
             t1.a[m] = tp.a[m] + (size_t)nl * n, t1.b[m] = tp.b[m] + (size_t)nl * n;
             f.ta[m] = tp.a[m], f.tb[m] = tp.b[m];
         }
+        if (fused_ki_ok()) {
+            const int h = ne - hp_.nl(l - 1);
+            u32* ext = modup(nullptr, l, nb, 0, &t1, false, true);
+            u32* acc = tmp(2 * (size_t)ne * nb);
+            u32* ys = tmp(2 * (size_t)h * nb);
+            const KiSrc src{ext, nullptr, ksk(0)};
+            ki_core(acc, ys, l, hp_.nl(l - 1), nb, &src, 1, 0, f);
+            untmp(ext, (size_t)nb * ext_rows(l));
+            moddown_rescale(acc, l, nb, nullptr, outm, af, ys);
+            untmp(ys, 2 * (size_t)h * nb);
+            untmp(acc, 2 * (size_t)ne * nb);
+            cnt_[C_KS] += nb;
+            cnt_[C_RELIN]++;
+            return;
+        }
         u32* ext = modup(nullptr, l, nb, 0, &t1);
         u32* acc = tmp(2 * (size_t)ne * nb);
         key_inner(acc, ext, nullptr, ksk(0), l, 0, nb, 0, f);
@@ -1649,15 +1746,23 @@ public:
     std::map<std::pair<int, double>, const u32*> affine_cst_;
     // acc = [m][2][ne] in Q*P, NTT form, already holding P * (the ciphertext) -> the ciphertext
     // divided by the dropped limbs of level l, at level l - 1 (one ModDown by Q' = P * D)
-    Ct moddown_rescale(const u32* acc, int l, int nb, u32* dst = nullptr, u32* const* outm = nullptr, const Affine* af = nullptr) {
+    // ys_in: the dropped + P rows already through the INTT's row pass (ki_core, [m][2][h]): only its column pass runs here
+    Ct moddown_rescale(const u32* acc, int l, int nb, u32* dst = nullptr, u32* const* outm = nullptr, const Affine* af = nullptr,
+                       u32* ys_in = nullptr) {
         const int n = hp_.n, nl = hp_.nl(l), r = hp_.nl(l - 1), k = nl - r, np = hp_.n_p, ne = nl + np;
         const int npl = 2 * nb, h = k + np;
         if (mdr_off_[l] == SIZE_MAX || npl > kMaxConvGroups) throw std::runtime_error("moddown_rescale: unsupported level or batch");
         const bool fz = fused_conv(false);
         if (fz && af && af->any()) throw std::runtime_error("moddown_rescale: the epilogue needs the separate conversion");
         const size_t off = mdr_off_[l];
-        u32* ys = tmp((size_t)npl * h);
-        intt(ys, acc, npl * h, RowMap{h, ne, h, r, 0}, LimbMap{k, r, hp_.p_off()}, fz ? d_mdr_ + off + 2 * (size_t)h * r : nullptr);
+        u32* ys = ys_in ? ys_in : tmp((size_t)npl * h);
+        if (ys_in) {
+            if (fz) throw std::runtime_error("moddown_rescale: a fused-core input needs the separate conversion");
+            launch_ntt_inv_cols(S(), T_, ys, npl * h, rows_dense(h), LimbMap{k, r, hp_.p_off()});
+            cnt_[C_NTT_ROWS] += (size_t)npl * h;
+        } else {
+            intt(ys, acc, npl * h, RowMap{h, ne, h, r, 0}, LimbMap{k, r, hp_.p_off()}, fz ? d_mdr_ + off + 2 * (size_t)h * r : nullptr);
+        }
         u32* conv = tmp((size_t)npl * r);
         ConvBatch cb;
         cb.n = npl;
@@ -1682,7 +1787,7 @@ public:
         else
             launch_ntt_finish(S(), T_, o.data, conv, acc, ne, qinv, nullptr, nullptr, npl, r, 0, outm, af ? af->dbl : 0u,
                               af && af->any() ? af->cst : nullptr);
-        untmp(ys, (size_t)npl * h);
+        if (!ys_in) untmp(ys, (size_t)npl * h);
         cnt_[C_NTT_ROWS] += (size_t)npl * r;
         untmp(conv, (size_t)npl * r);
         cnt_[C_RESCALE]++;
@@ -2294,10 +2399,26 @@ public:
             // read reversed where the permuted copy was read -- the ModUp's inverse NTT, the own
             // digit's key inner product and the ModDown finish's c0 -- no k_automorph, same residues
             const int nsrc = k - 1;
-            u32* ext = modup(c.data + (size_t)nl * n, l, nsrc, (size_t)nl * n, nullptr, true);
-            u32* acc = tmp(2 * (size_t)ne);
             KsFold fr{};
             fr.rev_d = 1;
+            if (fused_ki_ok()) {
+                u32* ext = modup(c.data + (size_t)nl * n, l, nsrc, (size_t)nl * n, nullptr, true, true);
+                u32* acc = tmp(2 * (size_t)ne);
+                u32* ys = tmp(2 * (size_t)np);
+                const KiSrc src[2] = {{ext, c.data + (size_t)nl * n, ksk(g)},
+                                      {ext + (size_t)ext_rows(l) * n, c.data + (size_t)2 * nl * n, nsrc == 2 ? ksk(tag_sq(g)) : nullptr}};
+                ki_core(acc, ys, l, nl, 1, src, nsrc, 0, fr);
+                untmp(ext, (size_t)nsrc * ext_rows(l));
+                Ct o = moddown(acc, l, c.data, nullptr, 1, 0, nullptr, nullptr, true, ys);
+                untmp(ys, 2 * (size_t)np);
+                untmp(acc, 2 * (size_t)ne);
+                o.pend = c.pend;
+                o.lazy = c.pend > 0;
+                cnt_[C_KS] += nsrc;
+                return o;
+            }
+            u32* ext = modup(c.data + (size_t)nl * n, l, nsrc, (size_t)nl * n, nullptr, true);
+            u32* acc = tmp(2 * (size_t)ne);
             key_inner(acc, ext, c.data + (size_t)nl * n, ksk(g), l, 0, 1, 0, fr);
             if (nsrc == 2)
                 key_inner(acc, ext + (size_t)ext_rows(l) * n, c.data + (size_t)2 * nl * n, ksk(tag_sq(g)), l, 0, 1, 0, fr, true);
@@ -2346,10 +2467,25 @@ public:
         if (g == conj_galois() && conj_rev_ && c.nb == 1 && !fused_conv(true) && !fused_conv(false)) {
             // the conjugation as reversed reads (galois_lazy): no permuted copy
             const int ne = nl + hp_.n_p;
-            u32* ext = modup(c.data + (size_t)nl * n, c.level, 1, 0, nullptr, true);
-            u32* acc = tmp(2 * (size_t)ne);
             KsFold fr{};
             fr.rev_d = 1;
+            if (fused_ki_ok()) {
+                const int np = hp_.n_p;
+                u32* ext = modup(c.data + (size_t)nl * n, c.level, 1, 0, nullptr, true, true);
+                u32* acc = tmp(2 * (size_t)ne);
+                u32* ys = tmp(2 * (size_t)np);
+                const KiSrc src{ext, c.data + (size_t)nl * n, key};
+                ki_core(acc, ys, c.level, nl, 1, &src, 1, 0, fr);
+                untmp(ext, (size_t)ext_rows(c.level));
+                Ct o = moddown(acc, c.level, c.data, nullptr, 1, 0, nullptr, nullptr, true, ys);
+                untmp(ys, 2 * (size_t)np);
+                untmp(acc, 2 * (size_t)ne);
+                cnt_[C_KS]++;
+                if (c.data != c_in.data) release(c);
+                return o;
+            }
+            u32* ext = modup(c.data + (size_t)nl * n, c.level, 1, 0, nullptr, true);
+            u32* acc = tmp(2 * (size_t)ne);
             key_inner(acc, ext, c.data + (size_t)nl * n, key, c.level, 0, 1, 0, fr);
             untmp(ext, (size_t)ext_rows(c.level));
             Ct o = moddown(acc, c.level, c.data, nullptr, 1, 0, nullptr, nullptr, true);
@@ -3506,12 +3642,14 @@ public:
     // relative precision 2^-k1bits; the true-FHE snap's kappa, zeta16_noise_reducer.py)
     // level-0 stack z (nb members, consumed) -> the bootstrapped stack, in chunks of two members
     // (the pair bootstrap's batch: every key and diagonal read once per chunk)
+    // members per chunk (AESFHE_BOOT_CHUNK, default 2: the pair bootstrap's packed EvalMod)
+    int boot_chunk_ = std::max(1, env_int("AESFHE_BOOT_CHUNK", 2));
     Ct boot_stack(Ct z, double gain, SparseBoot* sv) {
-        const int P = z.nb;
-        if (P <= 2) return bootstrap_l0(z, 99, gain, sv);
+        const int P = z.nb, B = boot_chunk_;
+        if (P <= B) return bootstrap_l0(z, 99, gain, sv);
         Ct out;
-        for (int m0 = 0; m0 < P; m0 += 2) {
-            const int c = std::min(2, P - m0);
+        for (int m0 = 0; m0 < P; m0 += B) {
+            const int c = std::min(B, P - m0);
             Ct r = bootstrap_l0(members_of(z, m0, c), 99, gain, sv);
             if (m0 == 0) {
                 out = alloc_ct(r.level, pm(r) * P, P);

@@ -270,6 +270,29 @@ struct KsFold {
 void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* ext, const u32* d, const u32* key, int nd, int ne, int nl,
                       int alpha, int nkey, int nks, LimbMap map, u64 g = 0, int nb = 1, size_t ext_ms = 0, size_t d_ms = 0,
                       size_t acc_ms = 0, KsFold fold = {}, bool accum = false);
+// Fused key-switch core (ntt.hip k_ntt2_ki): the ModUp's forward row pass of every
+// digit's extended rows (ext: the column pass's output, [member][nd][ne] rows), the key inner
+// product (k_key_inner's arithmetic: fold / tensor / reversed own digit; up to 2 sources summed,
+// each with its own key, ext and d) and, for the acc rows x >= kept, the row pass of the ModDown's
+// inverse NTT into ys ([member][2][ys_rows], row x - kept); rows x < kept go to acc [member][2][ne].
+// Identity Galois element only (a rotation's automorphism permutes across chunks).
+struct KiArgs {
+    const u32* ext[2] = {};
+    const u32* d[2] = {};
+    const u32* key[2] = {};
+    int nsrc = 1;
+    int nd = 0, ne = 0, nl = 0, alpha = 1, nkey = 0, nks = 0;
+    int kept = 0, ys_rows = 0, nb = 1;
+    size_t ext_ms = 0, d_ms = 0, acc_ms = 0, ys_ms = 0;
+    u32* acc = nullptr;
+    u32* ys = nullptr;
+    KsFold fold;
+};
+void launch_ntt_ki(hipStream_t st, const DevTables& T, const KiArgs& a, LimbMap map);
+// the forward NTT's column pass alone (pass 1; the row pass then runs inside launch_ntt_ki)
+void launch_ntt_fwd_cols(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map);
+// the inverse NTT's column pass alone, in place (its row pass ran inside launch_ntt_ki)
+void launch_ntt_inv_cols(hipStream_t st, const DevTables& T, u32* data, int rows, RowMap rm, LimbMap map, const u32* post = nullptr);
 // Heterogeneous batched key switch (Engine::ks_multi): member m of one launch
 // reads its own key and Galois element.  acc_m [2][ne] (acc + m acc_ms) = sum_j e_j ⊙ key_m[j]
 // with e_j = ext_{src_m}[j] (ext + src_m ext_ms), d_{src_m} (d + src_m d_ms) on digit j's own

@@ -80,6 +80,15 @@ inline int small_rows_limit() {
     return v;
 }
 inline bool small_launch(int rows) { return rows < small_rows_limit(); }
+// threads per block of the column pass (pass 1) at >= small_rows_limit() rows: AESFHE_NTT_P1_NT=256
+// forces the half-size blocks (16-column tiles) at every size (A/B sweeps, tools/ntt_grid_sweep.py)
+inline int p1_nt() {
+    static const int v = [] {
+        const char* e = std::getenv("AESFHE_NTT_P1_NT");
+        return e ? std::atoi(e) : 512;
+    }();
+    return v;
+}
 // threads per block of the row pass (pass 2) for launches of >= small_rows_limit() rows, forward
 // (AESFHE_NTT_P2_NT) and inverse (AESFHE_NTT_P2I_NT): 512, 256 or 128 (NT / 16 rows per block).
 // Smaller blocks spread a launch of a few hundred blocks more evenly over the 256 CUs (a block is
@@ -611,9 +620,15 @@ void ntt_fwd_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
                         rm, map, Tb.pc, Tb.tw, aux);
         return;
     }
-    constexpr int CB = kThreads / (R1 / 16);
-    prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, M1, kThreads>, dim3(256 / CB, rm.cnt, groups), dim3(kThreads), 0, st, dst,
-                    src, rm, map, Tb.pc, Tb.tw, aux);
+    if (p1_nt() == 256) {
+        constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
+        prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, M1, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, dst, src,
+                        rm, map, Tb.pc, Tb.tw, aux);
+    } else {
+        constexpr int CB = kThreads / (R1 / 16);
+        prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, M1, kThreads>, dim3(256 / CB, rm.cnt, groups), dim3(kThreads), 0, st,
+                        dst, src, rm, map, Tb.pc, Tb.tw, aux);
+    }
     ntt2_fwd_select<LOGR1, M2>(st, Tb, dst, rm, map, groups, io2, bfly * 8.0, aux);
 }
 // AESFHE_NTT_INV_FACT=0: the inverse pass 2 reads every twiddle from the table (A/B runs)
@@ -663,14 +678,55 @@ void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
                         Tb.pc, Tb.itw, post);
         return;
     }
-    constexpr int CB = kThreads / (R1 / 16);
     switch (p2_nt(true)) {
         case 128: ntt2_inv_launch<LOGR1, 128>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp, rev); break;
         case 256: ntt2_inv_launch<LOGR1, 256>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp, rev); break;
         default: ntt2_inv_launch<LOGR1, kThreads>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp, rev); break;
     }
+    if (p1_nt() == 256) {
+        constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
+        prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, dst, rm, map,
+                        Tb.pc, Tb.itw, post);
+        return;
+    }
+    constexpr int CB = kThreads / (R1 / 16);
     prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, kThreads>, dim3(256 / CB, rm.cnt, groups), dim3(kThreads), 0, st, dst, rm,
                     map, Tb.pc, Tb.itw, post);
+}
+
+// the column pass alone (the ModUp whose row pass runs inside k_ntt2_ki; the ModDown INTT whose row
+// pass did): the same launches ntt_fwd_t / ntt_inv_t issue for that pass
+template <int LOGR1>
+void ntt_fwd_cols_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, int rows, int io_rows, RowMap rm, LimbMap map) {
+    constexpr int R1 = 1 << LOGR1;
+    rm.nrows = rows;
+    const int groups = (rows + rm.cnt - 1) / rm.cnt;
+    const double io1 = 2.0 * io_rows * 4.0 * 256.0 * R1, bfly = (double)io_rows * 128.0 * R1;
+    if (small_launch(rows) || p1_nt() == 256) {
+        constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
+        prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, kPlain, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, dst,
+                        src, rm, map, Tb.pc, Tb.tw, NttAux{});
+        return;
+    }
+    constexpr int CB = kThreads / (R1 / 16);
+    prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, kPlain, kThreads>, dim3(256 / CB, rm.cnt, groups), dim3(kThreads), 0, st,
+                    dst, src, rm, map, Tb.pc, Tb.tw, NttAux{});
+}
+template <int LOGR1>
+void ntt_inv_cols_t(hipStream_t st, const DevTables& Tb, u32* data, int rows, RowMap rm, LimbMap map, const u32* post) {
+    constexpr int R1 = 1 << LOGR1;
+    rm.nrows = rows;
+    const int groups = (rows + rm.cnt - 1) / rm.cnt;
+    const double io = 4.0 * 2.0 * rows * (256.0 * R1), bfly = (double)rows * 128.0 * R1;
+    if (small_launch(rows) || p1_nt() == 256) {
+        constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
+        prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, data, rm, map,
+                        Tb.pc, Tb.itw, post);
+        return;
+    }
+    constexpr int CB = kThreads / (R1 / 16);
+    prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, kThreads>, dim3(256 / CB, rm.cnt, groups), dim3(kThreads), 0, st, data,
+                    rm, map, Tb.pc, Tb.itw, post);
 }
 
 // pass 1 fused with the base conversion (k_ntt1_fwd_conv), then pass 2 in mode M2
@@ -719,6 +775,266 @@ void ntt_fwd_conv_t(hipStream_t st, const DevTables& Tb, u32* dst, const ConvBat
     }
     ntt1_conv_dispatch<LOGR1, kThreads>(st, Tb, dst, cb, h, rm, map, groups, io1, bfly * LOGR1);
     ntt2_fwd_select<LOGR1, M2>(st, Tb, dst, rm, map, groups, io2, bfly * 8.0, aux);
+}
+
+// ---------------------------------------------------------------- fused key-switch core
+// ONE launch for what was three: the ModUp's forward row pass (pass 2) of every digit's extended
+// rows, the key inner product acc = sum_j ext_j (.) key_j (k_key_inner, incl. its fold / tensor /
+// reversed-own-digit forms and a second summed source), and the row pass of the ModDown's inverse
+// NTT on the acc rows the ModDown converts.  A block owns one 4,096-coefficient chunk (16 rows of
+// 256 words) of one target limb x of one member: the NTT-domain ext values never leave registers
+// (no ext write + re-read), and the rows >= kept go to the ModDown as its inverse pass-1 input (no
+// acc write + re-read of those rows).  Every stored value is the one the separate kernels store
+// (canonical acc; the inverse row pass's lazy residues by the same butterfly sequence), so the
+// ciphertexts are bit-identical (tests/test_gpu_fused_ki.py).
+// forward pass-2 stages on x[k] = word jt + 16 k of row R ([0, 4q) from pass 1) -> x[k] = word
+// 16 jt + k, canonical (k_ntt2_fwd's arithmetic)
+template <int LOGR1>
+__device__ __forceinline__ void ki_fwd_rows(u32 (&x)[16], u32* row, const uint2* w, int R, int j, u32 q, u32 q2) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int h = 8 >> s;
+        const int base = (1 << (LOGR1 + s)) + (R << s);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!(k & h)) {
+                const int ti = base + (k >> (4 - s));
+                ct_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, q);
+            }
+    }
+    uint2 tb[15];
+#pragma unroll
+    for (int s = 4; s < 8; ++s) {
+        const int c = 1 << (s - 4), base = (1 << (LOGR1 + s)) + (R << s) + (j << (s - 4));
+#pragma unroll
+        for (int u = 0; u < c; ++u) tb[c - 1 + u] = w[base + u];
+    }
+    __syncthreads();  // the previous user of the LDS row is done reading it
+#pragma unroll
+    for (int k = 0; k < 16; ++k) row[swz(j + 16 * k)] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = row[swz(16 * j + k)];
+#pragma unroll
+    for (int s = 4; s < 8; ++s) {
+        const int h = 1 << (7 - s), c = 1 << (s - 4);
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!(k & h)) {
+                const uint2 t = tb[c - 1 + (k >> (8 - s))];
+                ct_bfly(x[k], x[k + h], t.x, t.y, q2, q);
+            }
+    }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = canon4(x[k], q);
+}
+// inverse pass-2 stages on x[k] = word 16 jt + k of row R (canonical) -> x[k] = word jt + 16 k, the
+// residues k_ntt2_inv<LOGR1, NT, FACT, 0> stores (same butterflies, same twiddles, same order)
+template <int LOGR1, bool FACT>
+__device__ __forceinline__ void ki_inv_rows(u32 (&x)[16], u32* row, const uint2* w, const uint2* rowf, const uint2* gam, int R, int j,
+                                            u32 q, u32 q2) {
+#pragma unroll
+    for (int s = 7; s >= 4; --s) {
+        const int h = 1 << (7 - s);
+        const int base = (1 << (LOGR1 + s)) + (R << s);
+        if (FACT && s >= 5) {
+            const uint2 rf = rowf[s - 5];
+#pragma unroll
+            for (int k = 0; k < 16; ++k)
+                if (!(k & h)) gs_bfly2(x[k], x[k + h], gam[(1 << s) + ((16 * j + k) >> (8 - s))], rf, q2, 0u - q);
+            continue;
+        }
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!(k & h)) {
+                const int ti = base + ((16 * j + k) >> (8 - s));
+                gs_bfly(x[k], x[k + h], w[ti].x, w[ti].y, q2, 0u - q);
+            }
+    }
+    uint2 tb[15];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const int base = (1 << (LOGR1 + s)) + (R << s);
+#pragma unroll
+        for (int u = 0; u < (1 << s); ++u) tb[(1 << s) - 1 + u] = w[base + u];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) row[swz(16 * j + k)] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 16; ++k) x[k] = row[swz(j + 16 * k)];
+#pragma unroll
+    for (int s = 3; s >= 0; --s) {
+        const int h = 8 >> s;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (!(k & h)) {
+                const uint2 t = tb[(1 << s) - 1 + (k >> (4 - s))];
+                gs_bfly(x[k], x[k + h], t.x, t.y, q2, 0u - q);
+            }
+    }
+}
+__device__ __forceinline__ void ld16(u32 (&e)[16], const u32* p) {
+    const uint4* v = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint4 t = v[i];
+        e[4 * i] = t.x, e[4 * i + 1] = t.y, e[4 * i + 2] = t.z, e[4 * i + 3] = t.w;
+    }
+}
+__device__ __forceinline__ void st16(u32* p, const u32 (&e)[16]) {
+    uint4* v = reinterpret_cast<uint4*>(p);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = make_uint4(e[4 * i], e[4 * i + 1], e[4 * i + 2], e[4 * i + 3]);
+}
+template <int LOGR1, bool FACT>
+__global__ void __launch_bounds__(256) k_ntt2_ki(KiArgs a, LimbMap map, const PrimeConst* pc, const uint2* tw, const uint2* itw,
+                                                 const uint2* irow, const uint2* igam, unsigned long long* ts) {
+    constexpr int LOGN = LOGR1 + 8, CH = (1 << LOGR1) / 16;  // 16-row chunks per limb
+    __shared__ u32 sm[16 * kPitchP2];
+    // block -> (member, limb, chunk): the members of one (limb, chunk) -- which read the same key
+    // chunk -- consecutive on ONE XCD (blocks are dealt round-robin over the 8 XCDs), so the key
+    // chunk is fetched into that XCD's L2 once for all members
+    const int b = blockIdx.x, nb = a.nb;
+    int m, u;
+    if (((CH * a.ne) & 7) == 0) {
+        const int w = b >> 3;
+        m = w % nb;
+        u = (w / nb) * 8 + (b & 7);
+    } else {
+        m = b % nb;
+        u = b / nb;
+    }
+    const int chunk = u % CH, x = u / CH;
+    ts_begin(ts);
+    const int prime = map.prime(x);
+    const PrimeConst P = pc[prime];
+    const u32 q = P.q, q2 = 2 * q;
+    const int r = threadIdx.x >> 4, jt = threadIdx.x & 15, R = chunk * 16 + r;
+    const size_t c0 = (size_t)R * 256 + 16 * jt;  // this thread's 16 consecutive coefficients
+    u32* row = sm + r * kPitchP2;
+    const int krow = x < a.nl ? x : a.nks + (x - a.nl);
+    const int own = x < a.nl ? x / a.alpha : -1;
+    u64 s0[16], s1[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s0[k] = s1[k] = 0;
+    int cnt = 0;
+    for (int src = 0; src < a.nsrc; ++src) {
+        for (int jd = 0; jd < a.nd; ++jd, ++cnt) {
+            if (cnt && (cnt & 7) == 0) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) s0[k] = fold64(s0[k], q, P.r32), s1[k] = fold64(s1[k], q, P.r32);
+            }
+            u32 e[16];
+            if (jd == own) {  // block-uniform: the digit's own limb comes from the NTT-form input
+                if (a.fold.ta[0]) {  // tensor mode: c2 = a1 (.) b1 of the product, formed here
+                    const size_t at = ((size_t)(a.fold.tnl + x) << LOGN) + c0;
+                    const uint4* pa = reinterpret_cast<const uint4*>(a.fold.ta[m] + at);
+                    const uint4* pb = reinterpret_cast<const uint4*>(a.fold.tb[m] + at);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint4 va = pa[i], vb = pb[i];
+                        e[4 * i] = barrett_mul(va.x, vb.x, q, P.mu), e[4 * i + 1] = barrett_mul(va.y, vb.y, q, P.mu);
+                        e[4 * i + 2] = barrett_mul(va.z, vb.z, q, P.mu), e[4 * i + 3] = barrett_mul(va.w, vb.w, q, P.mu);
+                    }
+                } else if (a.fold.rev_d) {  // the conjugation: element v <- word N - 1 - (c0 + v)
+                    const uint4* v = reinterpret_cast<const uint4*>(a.d[src] + m * a.d_ms + ((size_t)x << LOGN) + ((size_t)1 << LOGN) - 16 - c0);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint4 t = v[i];
+                        e[15 - 4 * i] = t.x, e[14 - 4 * i] = t.y, e[13 - 4 * i] = t.z, e[12 - 4 * i] = t.w;
+                    }
+                } else {
+                    ld16(e, a.d[src] + m * a.d_ms + ((size_t)x << LOGN) + c0);
+                }
+            } else {
+                const u32* p = a.ext[src] + m * a.ext_ms + (((size_t)jd * a.ne + x) << LOGN) + (size_t)R * 256;
+#pragma unroll
+                for (int k = 0; k < 16; ++k) e[k] = p[jt + 16 * k];
+                ki_fwd_rows<LOGR1>(e, row, tw + ((size_t)prime << LOGN), R, jt, q, q2);
+            }
+            const u32* kb = a.key[src] + (((size_t)jd * 2 * a.nkey + krow) << LOGN) + c0;
+            const u32* ka = kb + ((size_t)a.nkey << LOGN);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint4 vb = reinterpret_cast<const uint4*>(kb)[i], va = reinterpret_cast<const uint4*>(ka)[i];
+                s0[4 * i] += (u64)e[4 * i] * vb.x, s1[4 * i] += (u64)e[4 * i] * va.x;
+                s0[4 * i + 1] += (u64)e[4 * i + 1] * vb.y, s1[4 * i + 1] += (u64)e[4 * i + 1] * va.y;
+                s0[4 * i + 2] += (u64)e[4 * i + 2] * vb.z, s1[4 * i + 2] += (u64)e[4 * i + 2] * va.z;
+                s0[4 * i + 3] += (u64)e[4 * i + 3] * vb.w, s1[4 * i + 3] += (u64)e[4 * i + 3] * va.w;
+            }
+        }
+    }
+    u32 r0[16], r1[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) r0[k] = reduce64(s0[k], q, P.mu, P.r32), r1[k] = reduce64(s1[k], q, P.mu, P.r32);
+    if (a.fold.gad && x < a.nl) {  // + P (c0, c1) on the Q rows (k_key_inner's fold), four words at a time
+        const u32 gv = a.fold.gad[2 * x], gp = a.fold.gad[2 * x + 1];
+        const bool tens = a.fold.ta[0] != nullptr;
+        const size_t at = tens ? ((size_t)x << LOGN) + c0 : m * a.fold.ms + ((size_t)x << LOGN) + c0;
+        const size_t o1 = (size_t)a.fold.tnl << LOGN;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            u32 f0[4], f1[4];
+            if (tens) {  // tensor mode: c0 = a0 b0, c1 = a0 b1 + a1 b0
+                const uint4 A0 = reinterpret_cast<const uint4*>(a.fold.ta[m] + at)[i], A1 = reinterpret_cast<const uint4*>(a.fold.ta[m] + at + o1)[i];
+                const uint4 B0 = reinterpret_cast<const uint4*>(a.fold.tb[m] + at)[i], B1 = reinterpret_cast<const uint4*>(a.fold.tb[m] + at + o1)[i];
+                const u32 a0[4] = {A0.x, A0.y, A0.z, A0.w}, a1[4] = {A1.x, A1.y, A1.z, A1.w};
+                const u32 b0[4] = {B0.x, B0.y, B0.z, B0.w}, b1[4] = {B1.x, B1.y, B1.z, B1.w};
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    f0[v] = barrett_mul(a0[v], b0[v], q, P.mu);
+                    f1[v] = add_mod(barrett_mul(a0[v], b1[v], q, P.mu), barrett_mul(a1[v], b0[v], q, P.mu), q);
+                }
+            } else {
+                const uint4 F0 = reinterpret_cast<const uint4*>(a.fold.add0 + at)[i], F1 = reinterpret_cast<const uint4*>(a.fold.add1 + at)[i];
+                f0[0] = F0.x, f0[1] = F0.y, f0[2] = F0.z, f0[3] = F0.w;
+                f1[0] = F1.x, f1[1] = F1.y, f1[2] = F1.z, f1[3] = F1.w;
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                r0[4 * i + v] = add_mod(r0[4 * i + v], shoup_mul(f0[v], gv, gp, q), q);
+                r1[4 * i + v] = add_mod(r1[4 * i + v], shoup_mul(f1[v], gv, gp, q), q);
+            }
+        }
+    }
+    if (x < a.kept) {  // kept rows: the ModDown finish's cur operand, acc layout [m][2][ne]
+        st16(a.acc + m * a.acc_ms + ((size_t)x << LOGN) + c0, r0);
+        st16(a.acc + m * a.acc_ms + ((size_t)(a.ne + x) << LOGN) + c0, r1);
+    } else {  // converted rows: the ModDown's inverse row pass, into its pass-1 input ys [m][2][ys_rows]
+        const uint2* iw = itw + ((size_t)prime << LOGN);
+        const uint2* rowf = irow + ((size_t)prime << LOGR1) * 4 + (size_t)R * 4;
+        const uint2* gam = igam + ((size_t)prime << 8);
+        ki_inv_rows<LOGR1, FACT>(r0, row, iw, rowf, gam, R, jt, q, q2);
+        u32* y0 = a.ys + m * a.ys_ms + ((size_t)(x - a.kept) << LOGN) + (size_t)R * 256;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) y0[jt + 16 * k] = r0[k];
+        ki_inv_rows<LOGR1, FACT>(r1, row, iw, rowf, gam, R, jt, q, q2);
+        u32* y1 = a.ys + m * a.ys_ms + ((size_t)(a.ys_rows + x - a.kept) << LOGN) + (size_t)R * 256;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) y1[jt + 16 * k] = r1[k];
+    }
+    ts_end(ts);
+}
+template <int LOGR1>
+void ki_launch(hipStream_t st, const DevTables& Tb, const KiArgs& a, LimbMap map) {
+    constexpr int CH = (1 << LOGR1) / 16;
+    const double row = 4.0 * (256.0 * (1 << LOGR1));
+    // per member: the digits' extended rows read once (own-digit rows from d), the key once per
+    // launch (members share it), acc / ys rows written; fold rows read
+    int ext_rows = 0;
+    for (int x = 0; x < a.ne; ++x)
+        for (int j = 0; j < a.nd; ++j) ext_rows += !(x < a.nl && x / a.alpha == j);
+    const double per_m = a.nsrc * (double)(ext_rows + std::min(a.nl, a.nd * a.alpha)) + 2.0 * a.ne +
+                         (a.fold.gad ? (a.fold.ta[0] ? 4.0 : 2.0) * a.nl : 0.0);
+    const double bytes = row * (a.nb * per_m + a.nsrc * 2.0 * a.nd * a.ne);
+    const double bfly = 128.0 * (1 << LOGR1) * 8.0 * (a.nb * (a.nsrc * (double)ext_rows + 2.0 * (a.ne - a.kept)));
+    const dim3 grid(CH * a.ne * a.nb);
+    if (inv_fact_on())
+        prof_launch_tsw(KID_KEY_INNER, bytes, bfly, k_ntt2_ki<LOGR1, true>, grid, dim3(256), 0, st, a, map, Tb.pc, Tb.tw, Tb.itw, Tb.irow, Tb.igam);
+    else
+        prof_launch_tsw(KID_KEY_INNER, bytes, bfly, k_ntt2_ki<LOGR1, false>, grid, dim3(256), 0, st, a, map, Tb.pc, Tb.tw, Tb.itw, Tb.irow, Tb.igam);
 }
 
 }  // namespace
@@ -835,6 +1151,45 @@ void launch_ntt_inv_rev(hipStream_t st, const DevTables& T, u32* dst, const u32*
         case 14: ntt_inv_t<6>(st, T, dst, src, rows, rm, map, nullptr, nullptr, true); break;
         case 15: ntt_inv_t<7>(st, T, dst, src, rows, rm, map, nullptr, nullptr, true); break;
         case 16: ntt_inv_t<8>(st, T, dst, src, rows, rm, map, nullptr, nullptr, true); break;
+        default: break;
+    }
+}
+void launch_ntt_ki(hipStream_t st, const DevTables& T, const KiArgs& a, LimbMap map) {
+    if (a.nb < 1 || a.nb > kMaxKsBatch || a.nsrc < 1 || a.nsrc > 2 || a.kept < 0 || a.kept > a.ne)
+        throw std::runtime_error("launch_ntt_ki: bad member / source / row counts");
+    if (a.fold.rev_d && a.fold.ta[0]) throw std::runtime_error("launch_ntt_ki: reversed d needs no tensor fold");
+    if (a.kept < a.ne && !a.ys) throw std::runtime_error("launch_ntt_ki: converted rows need a ys buffer");
+    switch (T.logn) {
+        case 13: ki_launch<5>(st, T, a, map); break;
+        case 14: ki_launch<6>(st, T, a, map); break;
+        case 15: ki_launch<7>(st, T, a, map); break;
+        case 16: ki_launch<8>(st, T, a, map); break;
+        default: break;
+    }
+}
+void launch_ntt_fwd_cols(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {
+    if (rows <= 0) return;
+    int io_rows = rows;
+    if (rm.skip_alpha > 0)
+        for (int y = 0; y < rows; ++y) {
+            const int g = y / rm.cnt, i = y - g * rm.cnt;
+            if (i < rm.skip_nl && i / rm.skip_alpha == (rm.skip_groups > 0 ? g % rm.skip_groups : g)) --io_rows;
+        }
+    switch (T.logn) {
+        case 13: ntt_fwd_cols_t<5>(st, T, dst, src, rows, io_rows, rm, map); break;
+        case 14: ntt_fwd_cols_t<6>(st, T, dst, src, rows, io_rows, rm, map); break;
+        case 15: ntt_fwd_cols_t<7>(st, T, dst, src, rows, io_rows, rm, map); break;
+        case 16: ntt_fwd_cols_t<8>(st, T, dst, src, rows, io_rows, rm, map); break;
+        default: break;
+    }
+}
+void launch_ntt_inv_cols(hipStream_t st, const DevTables& T, u32* data, int rows, RowMap rm, LimbMap map, const u32* post) {
+    if (rows <= 0) return;
+    switch (T.logn) {
+        case 13: ntt_inv_cols_t<5>(st, T, data, rows, rm, map, post); break;
+        case 14: ntt_inv_cols_t<6>(st, T, data, rows, rm, map, post); break;
+        case 15: ntt_inv_cols_t<7>(st, T, data, rows, rm, map, post); break;
+        case 16: ntt_inv_cols_t<8>(st, T, data, rows, rm, map, post); break;
         default: break;
     }
 }

@@ -21,13 +21,13 @@ def test_conj_rev_bit_identical(logn, monkeypatch):
         z = np.exp(2j * np.pi * rng.random(E.slot_count))
         w = np.exp(2j * np.pi * rng.random(E.slot_count))
         a, b = E.encrypt(z), E.encrypt(w)
-        tensor = E.multiply(a, b)                 # 3 polynomials, rescale owed
-        deferred = E.relinearize(tensor)          # 2 polynomials, rescale still owed (pend > 0)
-        lazy = E.multiply(a, b, "rlk")            # the engine's deferred product
-        cts = [a, deferred, tensor, lazy]
+        deferred = E.relinearize(E.multiply(a, b))  # 2 polynomials, rescale still owed (pend > 0)
+        lazy = E.multiply(a, b, "rlk")              # the engine's deferred product: a lazy 3-polynomial tensor
+        lazy2 = E.multiply(lazy, 0.3 + 0.1j)        # a deferred constant product owing two rescales
+        cts = [a, deferred, lazy, lazy2]
         res = [E.export(E.conjugate(c)).tobytes() for c in cts]
         res += [E.export(c).tobytes() for c in E.conjugate_many(cts)]
-        got = E.decrypt(E.conjugate(tensor))
+        got = E.decrypt(E.conjugate(lazy))
         assert np.abs(got - np.conj(z * w)).max() < 1e-3
         outs.append(res)
         del E
