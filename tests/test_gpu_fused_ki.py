@@ -52,10 +52,11 @@ def test_fused_ki_bit_identical(logn, monkeypatch):
     assert not bad, f"ciphertexts {bad} differ between the fused and the separate key-switch launches"
 
 
-def test_fused_ki_decrypts():
-    """the fused path (default) decrypts to the right slots: relin, rotation, conjugation"""
-    from conftest import gpu_engine
-    E = gpu_engine(log_n=16, max_level=17)
+def test_fused_ki_decrypts(monkeypatch):
+    """the fused path decrypts to the right slots: relin, rotation, conjugation"""
+    from mi355x_ckks import Engine
+    monkeypatch.setenv("AESFHE_FUSED_KI", "1")
+    E = Engine(log_n=16, max_level=17, dnum=3, seed=0x5EED, allow_insecure=True, enc_nonce=1)
     rng = np.random.default_rng(5)
     z, w = (np.exp(2j * np.pi * rng.random(E.slot_count)) for _ in range(2))
     a, b = E.encrypt(z), E.encrypt(w)
