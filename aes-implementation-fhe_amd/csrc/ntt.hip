@@ -94,6 +94,14 @@ inline int p1_nt() {
 // Smaller blocks spread a launch of a few hundred blocks more evenly over the 256 CUs (a block is
 // ~2.3 us of VALU work; at 512 threads a 40-row launch leaves 64 CUs with two blocks and 192
 // with one), while pass 1 keeps its 512-thread blocks' 128-byte column segments
+// AESFHE_NTT_AUTO=1: block sizes by launch size from the row sweep (profiles/r4_ntt_grid_sweep.json):
+// 128-thread row-pass blocks below 41 rows, 256-thread inverse column-pass blocks at 50..80 rows
+inline bool ntt_auto() {
+    static const bool v = std::getenv("AESFHE_NTT_AUTO") && std::atoi(std::getenv("AESFHE_NTT_AUTO")) != 0;
+    return v;
+}
+inline int p2_nt_rows(bool inverse, int rows);
+inline int p1_nt_rows(bool inverse, int rows);
 inline int p2_nt(bool inverse) {
     static const int f = [] {
         const char* e = std::getenv("AESFHE_NTT_P2_NT");
@@ -104,6 +112,14 @@ inline int p2_nt(bool inverse) {
         return e ? std::atoi(e) : 256;
     }();
     return inverse ? i : f;
+}
+inline int p2_nt_rows(bool inverse, int rows) {
+    if (ntt_auto() && rows >= 12 && rows < 41) return 128;
+    return p2_nt(inverse);
+}
+inline int p1_nt_rows(bool inverse, int rows) {
+    if (ntt_auto() && inverse && rows >= 50 && rows <= 80) return 256;
+    return p1_nt();
 }
 // AESFHE_NTT_FIN_OCC=1: the finish mode capped at 128 VGPRs (A/B runs; off: with 256-thread row
 // blocks the cap's spills cost more than the extra wave per SIMD gains, profiles/r3_ntt_p2_ab.json)
@@ -593,7 +609,7 @@ void ntt2_fwd_launch(hipStream_t st, const DevTables& Tb, u32* dst, RowMap rm, L
 template <int LOGR1, int M2>
 void ntt2_fwd_select(hipStream_t st, const DevTables& Tb, u32* dst, RowMap rm, LimbMap map, int groups, double io, double work,
                      const NttAux& aux) {
-    switch (p2_nt(false)) {
+    switch (p2_nt_rows(false, rm.nrows)) {
         case 128: ntt2_fwd_launch<LOGR1, M2, 128>(st, Tb, dst, rm, map, groups, io, work, aux); break;
         case 512: ntt2_fwd_launch<LOGR1, M2, 512>(st, Tb, dst, rm, map, groups, io, work, aux); break;
         default: ntt2_fwd_launch<LOGR1, M2, 256>(st, Tb, dst, rm, map, groups, io, work, aux); break;
@@ -620,7 +636,7 @@ void ntt_fwd_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
                         rm, map, Tb.pc, Tb.tw, aux);
         return;
     }
-    if (p1_nt() == 256) {
+    if (p1_nt_rows(false, rows) == 256) {
         constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
         prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, M1, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, dst, src,
                         rm, map, Tb.pc, Tb.tw, aux);
@@ -678,12 +694,12 @@ void ntt_inv_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
                         Tb.pc, Tb.itw, post);
         return;
     }
-    switch (p2_nt(true)) {
+    switch (p2_nt_rows(true, rows)) {
         case 128: ntt2_inv_launch<LOGR1, 128>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp, rev); break;
         case 256: ntt2_inv_launch<LOGR1, 256>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp, rev); break;
         default: ntt2_inv_launch<LOGR1, kThreads>(st, Tb, dst, src, rm, map, groups, io2, bfly * 8.0, tp, rev); break;
     }
-    if (p1_nt() == 256) {
+    if (p1_nt_rows(true, rows) == 256) {
         constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
         prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, dst, rm, map,
                         Tb.pc, Tb.itw, post);
@@ -702,7 +718,7 @@ void ntt_fwd_cols_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* sr
     rm.nrows = rows;
     const int groups = (rows + rm.cnt - 1) / rm.cnt;
     const double io1 = 2.0 * io_rows * 4.0 * 256.0 * R1, bfly = (double)io_rows * 128.0 * R1;
-    if (small_launch(rows) || p1_nt() == 256) {
+    if (small_launch(rows) || p1_nt_rows(false, rows) == 256) {
         constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
         prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, kPlain, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, dst,
                         src, rm, map, Tb.pc, Tb.tw, NttAux{});
@@ -718,7 +734,7 @@ void ntt_inv_cols_t(hipStream_t st, const DevTables& Tb, u32* data, int rows, Ro
     rm.nrows = rows;
     const int groups = (rows + rm.cnt - 1) / rm.cnt;
     const double io = 4.0 * 2.0 * rows * (256.0 * R1), bfly = (double)rows * 128.0 * R1;
-    if (small_launch(rows) || p1_nt() == 256) {
+    if (small_launch(rows) || p1_nt_rows(true, rows) == 256) {
         constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
         prof_launch_tsw(KID_NTT_COLS_INV, io, bfly * LOGR1, k_ntt1_inv<LOGR1, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, data, rm, map,
                         Tb.pc, Tb.itw, post);
