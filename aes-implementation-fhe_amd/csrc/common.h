@@ -105,6 +105,25 @@ HD u64 fold64(u64 x, u32 q, u32 r32) {
 // any 64-bit x mod q
 HD u32 reduce64(u64 x, u32 q, u32 mu, u32 r32) { return barrett_reduce64(fold64(x, q, r32), q, mu); }
 
+// 16-byte vector store of a kernel's output.  With AESFHE_WT (a build flag, A/B) it is WRITE-THROUGH
+// (`global_store_dwordx4 ... sc1`, MI355X_MICROARCH.md: the line leaves the XCD's L2 with the store):
+// a dependent kernel boundary costs ~1.7-1.9 us + B / 6 TB/s for the B bytes the predecessor left
+// dirty in L2, so outputs stored through are not written back at the boundary.  The asm store is
+// outside hipcc's wait-count bookkeeping: use it only for a kernel's final stores (nothing in the
+// kernel reads them back); `s_nop 1` pads the store-data hazard.
+#ifndef AESFHE_WT
+#define AESFHE_WT 0
+#endif
+typedef __attribute__((ext_vector_type(4))) unsigned aesfhe_v4u;
+__device__ __forceinline__ void st_out16(void* p, uint4 v) {
+#if AESFHE_WT && defined(__HIP_DEVICE_COMPILE__)
+    const aesfhe_v4u d = {v.x, v.y, v.z, v.w};
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(d) : "memory");
+#else
+    *reinterpret_cast<uint4*>(p) = v;
+#endif
+}
+
 // per-prime constant table kept in device memory
 struct PrimeConst {
     u32 q;       // modulus

@@ -455,8 +455,8 @@ __global__ void __launch_bounds__(kBlock) k_key_inner(u32* acc, const u32* ext, 
             r0[0] = add_mod(r0[0], p0.x, P.q), r0[1] = add_mod(r0[1], p0.y, P.q), r0[2] = add_mod(r0[2], p0.z, P.q), r0[3] = add_mod(r0[3], p0.w, P.q);
             r1[0] = add_mod(r1[0], p1.x, P.q), r1[1] = add_mod(r1[1], p1.y, P.q), r1[2] = add_mod(r1[2], p1.z, P.q), r1[3] = add_mod(r1[3], p1.w, P.q);
         }
-        *a0 = make_uint4(r0[0], r0[1], r0[2], r0[3]);
-        *a1 = make_uint4(r1[0], r1[1], r1[2], r1[3]);
+        st_out16(a0, make_uint4(r0[0], r0[1], r0[2], r0[3]));
+        st_out16(a1, make_uint4(r1[0], r1[1], r1[2], r1[3]));
     }
     ts_end(ts);
 }
@@ -531,10 +531,10 @@ __global__ void __launch_bounds__(kBlock) k_key_inner_sum(u32* acc, const u32* e
     }
     uint4* a0 = reinterpret_cast<uint4*>(acc + m * acc_ms + ((size_t)x << logn) + k);
     uint4* a1 = reinterpret_cast<uint4*>(acc + m * acc_ms + (((size_t)ne + x) << logn) + k);
-    *a0 = make_uint4(reduce64(s0[0], P.q, P.mu, P.r32), reduce64(s0[1], P.q, P.mu, P.r32), reduce64(s0[2], P.q, P.mu, P.r32),
-                     reduce64(s0[3], P.q, P.mu, P.r32));
-    *a1 = make_uint4(reduce64(s1[0], P.q, P.mu, P.r32), reduce64(s1[1], P.q, P.mu, P.r32), reduce64(s1[2], P.q, P.mu, P.r32),
-                     reduce64(s1[3], P.q, P.mu, P.r32));
+    st_out16(a0, make_uint4(reduce64(s0[0], P.q, P.mu, P.r32), reduce64(s0[1], P.q, P.mu, P.r32), reduce64(s0[2], P.q, P.mu, P.r32),
+                            reduce64(s0[3], P.q, P.mu, P.r32)));
+    st_out16(a1, make_uint4(reduce64(s1[0], P.q, P.mu, P.r32), reduce64(s1[1], P.q, P.mu, P.r32), reduce64(s1[2], P.q, P.mu, P.r32),
+                            reduce64(s1[3], P.q, P.mu, P.r32)));
     ts_end(ts);
 }
 // c0 + its J automorphisms (the trace step's ModDown addend), one launch for nb members
@@ -600,8 +600,8 @@ __global__ void __launch_bounds__(kBlock) k_key_inner_multi(u32* acc, const u32*
     for (int v = 0; v < 4; ++v) r0[v] = reduce64(s0[v], P.q, P.mu, P.r32), r1[v] = reduce64(s1[v], P.q, P.mu, P.r32);
     uint4* a0 = reinterpret_cast<uint4*>(acc + m * acc_ms + ((size_t)x << logn) + k);
     uint4* a1 = reinterpret_cast<uint4*>(acc + m * acc_ms + (((size_t)ne + x) << logn) + k);
-    *a0 = make_uint4(r0[0], r0[1], r0[2], r0[3]);
-    *a1 = make_uint4(r1[0], r1[1], r1[2], r1[3]);
+    st_out16(a0, make_uint4(r0[0], r0[1], r0[2], r0[3]));
+    st_out16(a1, make_uint4(r1[0], r1[1], r1[2], r1[3]));
     ts_end(ts);
 }
 __global__ void k_automorph_multi(u32* out, size_t out_ms, AutoMulti am, int logn) {

@@ -431,12 +431,12 @@ __global__ void __launch_bounds__(NT, OCC) k_ntt2_fwd(u32* data, RowMap rm, Limb
             }
             if (dbl) r.x = add_mod(r.x, r.x, q), r.y = add_mod(r.y, r.y, q), r.z = add_mod(r.z, r.z, q), r.w = add_mod(r.w, r.w, q);
             if (cs) r.x = add_mod(r.x, cadd, q), r.y = add_mod(r.y, cadd, q), r.z = add_mod(r.z, cadd, q), r.w = add_mod(r.w, cadd, q);
-            o[v] = r;
+            st_out16(o + v, r);
         }
     } else {
         uint4* o = reinterpret_cast<uint4*>(p + 16 * j);
 #pragma unroll
-        for (int v = 0; v < 4; ++v) o[v] = make_uint4(x[4 * v], x[4 * v + 1], x[4 * v + 2], x[4 * v + 3]);
+        for (int v = 0; v < 4; ++v) st_out16(o + v, make_uint4(x[4 * v], x[4 * v + 1], x[4 * v + 2], x[4 * v + 3]));
     }
     ts_end(ts);
 }
@@ -902,7 +902,7 @@ __device__ __forceinline__ void ld16(u32 (&e)[16], const u32* p) {
 __device__ __forceinline__ void st16(u32* p, const u32 (&e)[16]) {
     uint4* v = reinterpret_cast<uint4*>(p);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) v[i] = make_uint4(e[4 * i], e[4 * i + 1], e[4 * i + 2], e[4 * i + 3]);
+    for (int i = 0; i < 4; ++i) st_out16(v + i, make_uint4(e[4 * i], e[4 * i + 1], e[4 * i + 2], e[4 * i + 3]));
 }
 template <int LOGR1, bool FACT>
 __global__ void __launch_bounds__(256) k_ntt2_ki(KiArgs a, LimbMap map, const PrimeConst* pc, const uint2* tw, const uint2* itw,

@@ -31,7 +31,10 @@ def _run(E, sparse: bool):
         P = 32
         z = np.exp(2j * np.pi * rng.random(P))
         out.append(E.bootstrap_sparse(E.encrypt(np.tile(z, E.slot_count // P)), P))
-    return [E.export(x).tobytes() for x in out]
+    flat = []
+    for x in out:
+        flat += E.unstack(x) if E.members(x) > 1 else [x]
+    return [E.export(x).tobytes() for x in flat]
 
 
 @pytest.mark.parametrize("logn", [13, 16])

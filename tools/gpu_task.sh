@@ -16,7 +16,7 @@
 #   census                  tools/launch_census.py (launches / ms per AES step)
 #   stack                   tools/step_profile.py on the 64-pair stacked leg (STACK_ARGS)
 #   sweep                   tools/ntt_grid_sweep.py (NTT time vs rows per block-size configuration)
-#   probes                  tools/micro/grid_sync_probe + graph_gap_probe (built here by hipcc)
+#   probes                  tools/micro/grid_sync_probe, graph_gap_probe, wt_boundary_probe (built here by hipcc)
 set -e -o pipefail
 O=gpurun_out/${1:?out dir}
 shift
@@ -67,7 +67,8 @@ for t in "$@"; do
       timeout -k 10 600 python3 tools/ntt_grid_sweep.py > $O/ntt_grid_sweep.json 2> $O/sweep.err ;;
     probes)
       timeout -k 10 120 tools/micro/grid_sync_probe > $O/grid_sync_probe.json
-      timeout -k 10 120 tools/micro/graph_gap_probe > $O/graph_gap_probe.json ;;
+      timeout -k 10 120 tools/micro/graph_gap_probe > $O/graph_gap_probe.json
+      timeout -k 10 120 tools/micro/wt_boundary_probe > $O/wt_boundary_probe.json ;;
     *) echo "unknown task $t"; exit 2 ;;
   esac
 done
