@@ -1414,10 +1414,12 @@ public:
     }
     // ------------------------------------------------------------------ fused key-switch core
     // launch_ntt_ki: the ModUp's row pass, the key inner product and the ModDown
-    // INTT's row pass in ONE launch (AESFHE_FUSED_KI=1).  acc rows x < kept are written ([m][2][ne], the finish's cur);
+    // INTT's row pass in ONE launch.  acc rows x < kept are written ([m][2][ne], the finish's cur);
     // rows x >= kept go to ys ([m][2][ne - kept]) transformed by the inverse row pass -- the
-    // ModDown then runs only its INTT column pass on ys.  Unset / 0: the separate launches.
-    bool fused_ki_ = std::getenv("AESFHE_FUSED_KI") != nullptr && std::getenv("AESFHE_FUSED_KI")[0] == '1';
+    // ModDown then runs only its INTT column pass on ys.  AESFHE_FUSED_KI=0: the separate launches
+    // (C2 62.1-62.5 -> 64.8-64.9 rounds/s, 11,762 -> 10,670 launches per encrypt, same box:
+    // profiles/r4_ab_fused_ki_wt_ct8_auto.txt).
+    bool fused_ki_ = std::getenv("AESFHE_FUSED_KI") == nullptr || std::getenv("AESFHE_FUSED_KI")[0] != '0';
     bool fused_ki_ok() const { return fused_ki_ && !fused_conv(true) && !fused_conv(false); }
     struct KiSrc {
         const u32* ext;

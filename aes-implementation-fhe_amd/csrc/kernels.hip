@@ -1451,12 +1451,36 @@ void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int
         std::fprintf(stderr, "lin_mac B=%d G=%d nb=%d nd=%d nl=%d ne=%d keys=%d pts=%d a=%d u=%d rows_member=%.0f rows_write=%.0f rows_shared=%.0f MB=%.1f\n",
                      m.B, m.G, m.nb, m.nd, nl, ne, nkeys, npt, na, nu, member, writes, shared, bytes / 1e6);
     }
-    if (m.nb == 1)
+    if (m.nb == 1) {
         launch_lin_mac_nb<1>(st, T, m, nl, ne, map, bytes);
-    else if (m.nb == 2)
+    } else if (m.nb == 2) {
         launch_lin_mac_nb<2>(st, T, m, nl, ne, map, bytes);
-    else
-        throw std::runtime_error("launch_lin_mac: 1 or 2 batched ciphertexts");
+    } else if (m.nb > 2) {
+        // wider batches (a stacked bootstrap chunk of more than two members): pairs of members, one
+        // launch each, every member-strided operand offset to the pair's first member
+        for (int m0 = 0; m0 < m.nb; m0 += 2) {
+            LinMacArgs s = m;
+            s.nb = std::min(2, m.nb - m0);
+            const size_t qo = (size_t)m0 * m.q_ms, po = (size_t)m0 * m.p_ms;
+            for (int b = 0; b < m.B; ++b) {
+                if (s.a[b]) s.a[b] += qo;
+                if (s.u[b]) s.u[b] += po;
+            }
+            if (s.c1) s.c1 += qo;
+            for (int g = 0; g < m.G; ++g) {
+                if (s.out0[g]) s.out0[g] += qo;
+                if (s.out1[g]) s.out1[g] += qo;
+                if (s.outp[g]) s.outp[g] += po;
+            }
+            if (s.ks_ext) s.ks_ext += (size_t)m0 * m.ext_ms;
+            if (s.ks_d) s.ks_d += (size_t)m0 * m.d_ms;
+            const double b2 = bytes * s.nb / m.nb;
+            if (s.nb == 1) launch_lin_mac_nb<1>(st, T, s, nl, ne, map, b2);
+            else launch_lin_mac_nb<2>(st, T, s, nl, ne, map, b2);
+        }
+    } else {
+        throw std::runtime_error("launch_lin_mac: at least one ciphertext");
+    }
 }
 
 void launch_mac(hipStream_t st, const DevTables& T, u32* out, const MacTerms& m, size_t xs, size_t os, int rows, int npoly, LimbMap map) {
