@@ -904,7 +904,11 @@ __device__ __forceinline__ void st16(u32* p, const u32 (&e)[16]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) st_out16(v + i, make_uint4(e[4 * i], e[4 * i + 1], e[4 * i + 2], e[4 * i + 3]));
 }
-template <int LOGR1, bool FACT>
+// PF: the digit's key rows are loaded right after its ext rows and before the forward row pass, so
+// their latency overlaps the butterflies instead of following them (AESFHE_KI_PF, default on: 44.6
+// -> 43.8 us per launch, C2 +0.3 %, profiles/r4_ab_ki_pf.txt; the loads are issued ext first:
+// vmcnt retires in order, the pass waits only for the ext values; 242 VGPRs, still 2 waves / SIMD)
+template <int LOGR1, bool FACT, bool PF>
 __global__ void __launch_bounds__(256) k_ntt2_ki(KiArgs a, LimbMap map, const PrimeConst* pc, const uint2* tw, const uint2* itw,
                                                  const uint2* irow, const uint2* igam, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8, CH = (1 << LOGR1) / 16;  // 16-row chunks per limb
@@ -943,6 +947,10 @@ __global__ void __launch_bounds__(256) k_ntt2_ki(KiArgs a, LimbMap map, const Pr
                 for (int k = 0; k < 16; ++k) s0[k] = fold64(s0[k], q, P.r32), s1[k] = fold64(s1[k], q, P.r32);
             }
             u32 e[16];
+            const u32* kb = a.key[src] + (((size_t)jd * 2 * a.nkey + krow) << LOGN) + c0;
+            const u32* ka = kb + ((size_t)a.nkey << LOGN);
+            uint4 vk0[4], vk1[4];
+            bool kld = false;
             if (jd == own) {  // block-uniform: the digit's own limb comes from the NTT-form input
                 if (a.fold.ta[0]) {  // tensor mode: c2 = a1 (.) b1 of the product, formed here
                     const size_t at = ((size_t)(a.fold.tnl + x) << LOGN) + c0;
@@ -968,13 +976,19 @@ __global__ void __launch_bounds__(256) k_ntt2_ki(KiArgs a, LimbMap map, const Pr
                 const u32* p = a.ext[src] + m * a.ext_ms + (((size_t)jd * a.ne + x) << LOGN) + (size_t)R * 256;
 #pragma unroll
                 for (int k = 0; k < 16; ++k) e[k] = p[jt + 16 * k];
+                if (PF) {
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) vk0[i] = reinterpret_cast<const uint4*>(kb)[i], vk1[i] = reinterpret_cast<const uint4*>(ka)[i];
+                    kld = true;
+                }
                 ki_fwd_rows<LOGR1>(e, row, tw + ((size_t)prime << LOGN), R, jt, q, q2);
             }
-            const u32* kb = a.key[src] + (((size_t)jd * 2 * a.nkey + krow) << LOGN) + c0;
-            const u32* ka = kb + ((size_t)a.nkey << LOGN);
+            if (!kld)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) vk0[i] = reinterpret_cast<const uint4*>(kb)[i], vk1[i] = reinterpret_cast<const uint4*>(ka)[i];
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-                const uint4 vb = reinterpret_cast<const uint4*>(kb)[i], va = reinterpret_cast<const uint4*>(ka)[i];
+                const uint4 vb = vk0[i], va = vk1[i];
                 s0[4 * i] += (u64)e[4 * i] * vb.x, s1[4 * i] += (u64)e[4 * i] * va.x;
                 s0[4 * i + 1] += (u64)e[4 * i + 1] * vb.y, s1[4 * i + 1] += (u64)e[4 * i + 1] * va.y;
                 s0[4 * i + 2] += (u64)e[4 * i + 2] * vb.z, s1[4 * i + 2] += (u64)e[4 * i + 2] * va.z;
@@ -1033,6 +1047,13 @@ __global__ void __launch_bounds__(256) k_ntt2_ki(KiArgs a, LimbMap map, const Pr
     }
     ts_end(ts);
 }
+inline bool ki_pf() {
+    static const bool v = [] {
+        const char* e = std::getenv("AESFHE_KI_PF");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return v;
+}
 template <int LOGR1>
 void ki_launch(hipStream_t st, const DevTables& Tb, const KiArgs& a, LimbMap map) {
     constexpr int CH = (1 << LOGR1) / 16;
@@ -1047,10 +1068,15 @@ void ki_launch(hipStream_t st, const DevTables& Tb, const KiArgs& a, LimbMap map
     const double bytes = row * (a.nb * per_m + a.nsrc * 2.0 * a.nd * a.ne);
     const double bfly = 128.0 * (1 << LOGR1) * 8.0 * (a.nb * (a.nsrc * (double)ext_rows + 2.0 * (a.ne - a.kept)));
     const dim3 grid(CH * a.ne * a.nb);
-    if (inv_fact_on())
-        prof_launch_tsw(KID_KEY_INNER, bytes, bfly, k_ntt2_ki<LOGR1, true>, grid, dim3(256), 0, st, a, map, Tb.pc, Tb.tw, Tb.itw, Tb.irow, Tb.igam);
-    else
-        prof_launch_tsw(KID_KEY_INNER, bytes, bfly, k_ntt2_ki<LOGR1, false>, grid, dim3(256), 0, st, a, map, Tb.pc, Tb.tw, Tb.itw, Tb.irow, Tb.igam);
+#define KI_GO(F, PF) prof_launch_tsw(KID_KEY_INNER, bytes, bfly, k_ntt2_ki<LOGR1, F, PF>, grid, dim3(256), 0, st, a, map, Tb.pc, Tb.tw, Tb.itw, Tb.irow, Tb.igam)
+    if (inv_fact_on()) {
+        if (ki_pf()) KI_GO(true, true);
+        else KI_GO(true, false);
+    } else {
+        if (ki_pf()) KI_GO(false, true);
+        else KI_GO(false, false);
+    }
+#undef KI_GO
 }
 
 }  // namespace

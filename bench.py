@@ -665,10 +665,15 @@ def main():
     every = 1 if args.profile_all else args.profile_every
     # the sampled kernel classes (PROF_KIDS: the roofline kernels and the per-class fractions)
     kernels = list(mi355x_ckks.KERNEL_IDS) if args.profile_all else list(dict.fromkeys([args.kernel, args.kernel2] + PROF_KIDS))
-    whole = args.whole_stats and os.environ.get("AESFHE_PROFILE_FROM_START")
+    # --whole-stats: the launch sequence of a rocprofv3 --pmc pass (no sampled profiler, no precision
+    # pass).  With AESFHE_PROFILE_FROM_START the engine's accounting of every launch since start-up is
+    # written there (the algorithmic bytes of the counter pass's launches); without it (the counter pass
+    # itself: no in-kernel timestamps under the counters) nothing is written
+    whole = bool(args.whole_stats)
+    account = whole and bool(os.environ.get("AESFHE_PROFILE_FROM_START"))
     pre = {}
     if whole:  # whole-process accounting: keep the from-start configuration, fold the pre-timed part in
-        pre = E.kernel_stats(reset=True)
+        pre = E.kernel_stats(reset=True) if account else {}
     else:
         E.profile(kernels, every=every)
         # one profiled, untimed encrypt allocates the profiler's clock slots outside the timing
@@ -696,11 +701,11 @@ def main():
     if mark:
         time.sleep(0.25)
     counters = E.counters()
-    if whole:
+    if account:
         stats = E.kernel_stats(reset=True)
         tot = {k: {f: pre.get(k, {}).get(f, 0) + v.get(f, 0) for f in ("launches", "ms", "bytes")} for k, v in stats.items()}
         Path(args.whole_stats).write_text(json.dumps(tot, indent=1))
-    else:
+    elif not whole:
         leg.stop()
     elapsed = max_over_ranks(dist, elapsed)
     launches_per_encrypt = (launches1 - launches0) / args.steps
