@@ -1371,7 +1371,16 @@ public:
         const bool fz = fused_conv(true);
         if ((tp || rev) && fz) throw std::runtime_error("modup: the tensor / reversed form needs the separate conversion");
         u32* coef = tmp((size_t)nb * nl);
-        if (rev) {
+        // k_bx_cols: the INTT's row pass here, its column pass + the conversion + the ext rows'
+        // forward column pass in one launch
+        const bool bx = bx_ok() && alpha <= kBxMaxH;
+        if (bx) {
+            const RowMap rm{nl, nb > 1 ? (int)(d_ms / n) : nl, nl, 0, 0};
+            if (rev) launch_ntt_inv_rows(S(), T_, coef, d, nb * nl, rm, qmap(), nullptr, true);
+            else if (tp) launch_ntt_inv_rows(S(), T_, coef, nullptr, nb * nl, RowMap{nl, nl, nl, 0, 0}, qmap(), tp, false);
+            else launch_ntt_inv_rows(S(), T_, coef, d, nb * nl, rm, qmap());
+            cnt_[C_NTT_ROWS] += nb * nl;
+        } else if (rev) {
             launch_ntt_inv_rev(S(), T_, coef, d, nb * nl, RowMap{nl, nb > 1 ? (int)(d_ms / n) : nl, nl, 0, 0}, qmap());
             cnt_[C_NTT_ROWS] += nb * nl;
         } else if (tp) {
@@ -1396,7 +1405,11 @@ public:
             }
         RowMap xr = rows_dense(ne);
         xr.skip_alpha = alpha, xr.skip_nl = nl, xr.skip_groups = nd;
-        if (fz) {
+        if (bx) {
+            launch_bx_cols(S(), T_, up, ne, em);
+            if (!cols_only) launch_ntt_fwd_rows(S(), T_, ext, nb * nd * ne, xr, em);
+            cnt_[C_NTT_ROWS] += nb * nd * ne;
+        } else if (fz) {
             if (cols_only) throw std::runtime_error("modup: the fused conversion has no column-pass-only form");
             launch_ntt_fwd_conv(S(), T_, ext, up, nb * nd * ne, xr, em);
             cnt_[C_NTT_ROWS] += nb * nd * ne;
@@ -1421,6 +1434,12 @@ public:
     // profiles/r4_ab_fused_ki_wt_ct8_auto.txt).
     bool fused_ki_ = std::getenv("AESFHE_FUSED_KI") == nullptr || std::getenv("AESFHE_FUSED_KI")[0] != '0';
     bool fused_ki_ok() const { return fused_ki_ && !fused_conv(true) && !fused_conv(false); }
+    // k_bx_cols for the ModUp / ModDown middles (AESFHE_BX_COLS=1, N = 2^16; groups of at most
+    // kBxMaxH sources: the kernel keeps them in VGPRs -- 242 at 12, 2 waves / SIMD; the double-prime
+    // levels' ModDown + rescale (13 sources) keeps the separate launches)
+    static constexpr int kBxMaxH = 12;
+    bool bx_cols_ = std::getenv("AESFHE_BX_COLS") != nullptr && std::atoi(std::getenv("AESFHE_BX_COLS")) != 0;
+    bool bx_ok() const { return bx_cols_ && bx_cols_on(T_) && !fused_conv(true) && !fused_conv(false); }
     struct KiSrc {
         const u32* ext;
         const u32* d;
@@ -1461,7 +1480,11 @@ public:
         if (npl > kMaxConvGroups) throw std::runtime_error("moddown: batch too large");
         const bool fz = fused_conv(false);
         u32* yp = ys_in ? ys_in : tmp((size_t)npl * np);
-        if (ys_in) {
+        const bool bx = bx_ok() && np <= kBxMaxH;
+        if (bx) {  // the P rows through the INTT's row pass only (k_bx_cols runs the rest)
+            if (!ys_in) launch_ntt_inv_rows(S(), T_, yp, acc, npl * np, RowMap{np, ne, np, nl, 0}, LimbMap{np, hp_.p_off(), 0});
+            cnt_[C_NTT_ROWS] += (size_t)npl * np;
+        } else if (ys_in) {
             if (fz) throw std::runtime_error("moddown: a fused-core input needs the separate conversion");
             launch_ntt_inv_cols(S(), T_, yp, npl * np, rows_dense(np), LimbMap{np, hp_.p_off(), 0});
             cnt_[C_NTT_ROWS] += (size_t)npl * np;
@@ -1480,7 +1503,8 @@ public:
             dn.qhinv[p] = d_moddown_phinv_;
             dn.negq[p] = d_negp_;
         }
-        if (!fz) launch_base_convert(S(), T_, dn, nl, qmap());
+        if (bx) launch_bx_cols(S(), T_, dn, nl, qmap());
+        else if (!fz) launch_base_convert(S(), T_, dn, nl, qmap());
         Ct o;
         if (dst || outm) {
             o.level = level, o.npoly = npl, o.nb = nb, o.words = (size_t)npl * nl * n, o.data = dst;
@@ -1488,7 +1512,9 @@ public:
             o = alloc_ct(level, npl, nb);
         }
         if (fz && add_rev) throw std::runtime_error("moddown: the reversed addend needs the separate conversion");
-        if (fz)
+        if (bx)
+            launch_ntt_finish_rows(S(), T_, o.data, conv, acc, ne, d_pinv_, add0, add1, npl, nl, add_ms, outm, add_rev);
+        else if (fz)
             launch_ntt_finish_conv(S(), T_, o.data, conv, dn, acc, ne, d_pinv_, add0, add1, npl, nl, add_ms, outm);
         else
             launch_ntt_finish(S(), T_, o.data, conv, acc, ne, d_pinv_, add0, add1, npl, nl, add_ms, outm, 0u, nullptr, add_rev);
@@ -1758,7 +1784,11 @@ public:
         if (fz && af && af->any()) throw std::runtime_error("moddown_rescale: the epilogue needs the separate conversion");
         const size_t off = mdr_off_[l];
         u32* ys = ys_in ? ys_in : tmp((size_t)npl * h);
-        if (ys_in) {
+        const bool bx = bx_ok() && h <= kBxMaxH;
+        if (bx) {  // the dropped + P rows through the INTT's row pass only (k_bx_cols runs the rest)
+            if (!ys_in) launch_ntt_inv_rows(S(), T_, ys, acc, npl * h, RowMap{h, ne, h, r, 0}, LimbMap{k, r, hp_.p_off()});
+            cnt_[C_NTT_ROWS] += (size_t)npl * h;
+        } else if (ys_in) {
             if (fz) throw std::runtime_error("moddown_rescale: a fused-core input needs the separate conversion");
             launch_ntt_inv_cols(S(), T_, ys, npl * h, rows_dense(h), LimbMap{k, r, hp_.p_off()});
             cnt_[C_NTT_ROWS] += (size_t)npl * h;
@@ -1776,7 +1806,8 @@ public:
             cb.qhinv[p] = d_mdr_ + off + 2 * (size_t)h * r;     // [h] pairs
             cb.negq[p] = d_mdr_ + off + 2 * (size_t)h * (r + 1);  // [r]
         }
-        if (!fz) launch_base_convert(S(), T_, cb, r, qmap());
+        if (bx) launch_bx_cols(S(), T_, cb, r, qmap());
+        else if (!fz) launch_base_convert(S(), T_, cb, r, qmap());
         Ct o;
         if (dst || outm) {
             o.level = l - 1, o.npoly = npl, o.nb = nb, o.words = (size_t)npl * r * n, o.data = dst;
@@ -1784,7 +1815,10 @@ public:
             o = alloc_ct(l - 1, npl, nb);
         }
         const u32* qinv = d_mdr_ + off + 2 * (size_t)h * (r + 1) + r;
-        if (fz)
+        if (bx)
+            launch_ntt_finish_rows(S(), T_, o.data, conv, acc, ne, qinv, nullptr, nullptr, npl, r, 0, outm, false, af ? af->dbl : 0u,
+                                   af && af->any() ? af->cst : nullptr);
+        else if (fz)
             launch_ntt_finish_conv(S(), T_, o.data, conv, cb, acc, ne, qinv, nullptr, nullptr, npl, r, 0, outm);
         else
             launch_ntt_finish(S(), T_, o.data, conv, acc, ne, qinv, nullptr, nullptr, npl, r, 0, outm, af ? af->dbl : 0u,

@@ -293,6 +293,20 @@ void launch_ntt_ki(hipStream_t st, const DevTables& T, const KiArgs& a, LimbMap 
 void launch_ntt_fwd_cols(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map);
 // the inverse NTT's column pass alone, in place (its row pass ran inside launch_ntt_ki)
 void launch_ntt_inv_cols(hipStream_t st, const DevTables& T, u32* data, int rows, RowMap rm, LimbMap map, const u32* post = nullptr);
+// column-domain basis extension (ntt.hip k_bx_cols, N = 2^16): for every group z of cb, the inverse
+// NTT's column pass of its h[z] source rows src[z] (row pass done), their conversion to the nt
+// targets (k_base_convert's tables and arithmetic; targets in [skip0, skip0 + h) skipped) and the
+// forward NTT's column pass of each target, written to dst[z] + t N.  bx_cols_on: the ring has it
+int bx_cols_on(const DevTables& T);
+void launch_bx_cols(hipStream_t st, const DevTables& T, const ConvBatch& cb, int nt, LimbMap map);
+// single passes around it (N = 2^16): the inverse row pass (plain / product / reversed input), the
+// forward row pass in place (RowMap skips honoured), launch_ntt_finish's row pass
+void launch_ntt_inv_rows(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map,
+                         const TensorPtrs* tp = nullptr, bool rev = false);
+void launch_ntt_fwd_rows(hipStream_t st, const DevTables& T, u32* data, int rows, RowMap rm, LimbMap map);
+void launch_ntt_finish_rows(hipStream_t st, const DevTables& T, u32* out, u32* conv, const u32* cur, int cur_stride, const u32* qinv,
+                            const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride = 0, u32* const* outm = nullptr,
+                            bool add_rev = false, unsigned dbl = 0u, const u32* const* cst = nullptr);
 // Heterogeneous batched key switch (Engine::ks_multi): member m of one launch
 // reads its own key and Galois element.  acc_m [2][ne] (acc + m acc_ms) = sum_j e_j ⊙ key_m[j]
 // with e_j = ext_{src_m}[j] (ext + src_m ext_ms), d_{src_m} (d + src_m d_ms) on digit j's own

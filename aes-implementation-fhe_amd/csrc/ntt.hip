@@ -1079,6 +1079,174 @@ void ki_launch(hipStream_t st, const DevTables& Tb, const KiArgs& a, LimbMap map
 #undef KI_GO
 }
 
+
+// ---------------------------------------------------------------- column-domain basis extension
+// ONE launch for the middle of a ModUp / ModDown: the inverse NTT's column pass of a group's H
+// source limbs (their row pass already done: k_ntt2_inv, or k_ntt2_ki for the ModDown's P rows),
+// the base conversion to the group's target limbs (k_base_convert's arithmetic, in its order) and
+// the forward NTT's column pass of every target limb (k_ntt1_fwd's) -- before, three launches with
+// the coefficient-form sources and the converted rows each written and re-read in between.
+// A block owns an 8-column tile of all 256 rows (N = 2^16: 256 x 256) of one group, for a range of
+// its targets: it runs the H inverse column transforms itself (every target range of the group
+// repeats them -- the price of needing no other block's data), keeps the H x 8 converted-source
+// residues per thread in VGPRs, and transforms each target in three register passes of 3 / 3 / 2
+// butterfly stages with two LDS exchanges (alternating buffers: one barrier each).  The values
+// stored are congruent to the separate kernels' at every hand-off and canonical where those are
+// (the INTT output, the conversion output), so the ciphertexts are bit-identical
+// (tests/test_gpu_bx_cols.py).
+// Thread (p = tid / 8, c = tid % 8) holds column 8 tile + c, rows by layout:
+//   A  p + 32 e                (stages 0-2 forward / 1-0 inverse)
+//   Bf (p&3) + 32 (p>>2) + 4 e (forward stages 3-5)   Bi (p&7) + 64 (p>>3) + 8 e (inverse 4-2)
+//   C  8 p + e                 (forward 6-7 / inverse 7-5)
+// LDS word of (row, c): a 32-word block per 4 rows, rotated by 8 ((row >> 3) & 3): every layout's
+// half-wave touches 32 distinct banks (checked exhaustively, tools/bx_layout_check.py).
+enum { kBxA = 0, kBxBf = 1, kBxBi = 2, kBxC = 3 };
+template <int L>
+__device__ __forceinline__ int bx_row(int p, int e) {
+    return L == kBxA ? p + 32 * e : L == kBxBf ? (p & 3) + 32 * (p >> 2) + 4 * e : L == kBxBi ? (p & 7) + 64 * (p >> 3) + 8 * e : 8 * p + e;
+}
+__device__ __forceinline__ int bx_lds(int row, int c) { return (row >> 2) * 32 + (((row & 3) * 8 + c + 8 * ((row >> 3) & 3)) & 31); }
+// stage S (row distance 128 >> S) on the elements of layout L that differ in bit H of e
+template <int L, int S, int H>
+__device__ __forceinline__ void bx_fwd(u32 (&x)[8], const uint2* w, int p, u32 q2, u32 q) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+        if (!(e & H)) {
+            const uint2 t = w[(1 << S) + (bx_row<L>(p, e) >> (8 - S))];
+            ct_bfly(x[e], x[e + H], t.x, t.y, q2, q);
+        }
+}
+template <int L, int S, int H>
+__device__ __forceinline__ void bx_inv(u32 (&x)[8], const uint2* w, int p, u32 q2, u32 nq) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+        if (!(e & H)) {
+            const uint2 t = w[(1 << S) + (bx_row<L>(p, e) >> (8 - S))];
+            gs_bfly(x[e], x[e + H], t.x, t.y, q2, nq);
+        }
+}
+template <int LA, int LB>
+__device__ __forceinline__ void bx_xchg(u32 (&x)[8], u32* sm, int p, int c) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) sm[bx_lds(bx_row<LA>(p, e), c)] = x[e];
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = sm[bx_lds(bx_row<LB>(p, e), c)];
+}
+// source I of the group (template recursion: every y[I] index is a compile-time constant, so the
+// residues stay in VGPRs at any HM -- a run-time loop this large is not unrolled and goes to scratch)
+template <int I, int HM>
+__device__ __forceinline__ void bx_sources(u32 (&y)[HM][8], const ConvBatch& cb, int z, int hz, int sp, const PrimeConst* pc,
+                                           const uint2* itw, u32 (*sm)[2048], int& buf, int p, int c, int col) {
+    if constexpr (I < HM) {
+        constexpr int LOGN = 16;
+        if (I < hz) {  // block-uniform
+            const int prime = (sp > 0 && I >= sp) ? cb.d1[z] + (I - sp) : cb.d0[z] + I;
+            const PrimeConst P = pc[prime];
+            const u32 q = P.q, q2 = 2 * q, nq = 0u - q;
+            const uint2* w = itw + ((size_t)prime << LOGN);
+            const u32* s = cb.src[z] + ((size_t)I << LOGN);
+            u32 x[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) x[e] = s[(size_t)bx_row<kBxC>(p, e) * 256 + col];
+            bx_inv<kBxC, 7, 1>(x, w, p, q2, nq);
+            bx_inv<kBxC, 6, 2>(x, w, p, q2, nq);
+            bx_inv<kBxC, 5, 4>(x, w, p, q2, nq);
+            bx_xchg<kBxC, kBxBi>(x, sm[buf], p, c);
+            buf ^= 1;
+            bx_inv<kBxBi, 4, 1>(x, w, p, q2, nq);
+            bx_inv<kBxBi, 3, 2>(x, w, p, q2, nq);
+            bx_inv<kBxBi, 2, 4>(x, w, p, q2, nq);
+            bx_xchg<kBxBi, kBxA>(x, sm[buf], p, c);
+            buf ^= 1;
+            bx_inv<kBxA, 1, 2>(x, w, p, q2, nq);
+            bx_inv<kBxA, 0, 4>(x, w, p, q2, nq);
+            // k_ntt1_inv's N^-1 (canonical), then k_base_convert's qhat^-1 and its y / q fixed point
+            const u32 qw = cb.qhinv[z][2 * I], qwp = cb.qhinv[z][2 * I + 1];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[I][e] = shoup_mul(shoup_mul(x[e], P.ninv, P.ninv_p, q), qw, qwp, q);
+        } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) y[I][e] = 0u;
+        }
+        bx_sources<I + 1, HM>(y, cb, z, hz, sp, pc, itw, sm, buf, p, c, col);
+    }
+}
+template <int HM>
+__global__ void __launch_bounds__(256) k_bx_cols(ConvBatch cb, int nt, int ntg, LimbMap map, const PrimeConst* pc, const uint2* tw,
+                                                 const uint2* itw, unsigned long long* ts) {
+    constexpr int LOGN = 16;
+    __shared__ u32 sm[2][2048];
+    // block -> (tile, target range, group): the four tiles of one 128-byte column segment on one
+    // XCD (blocks are dealt round-robin over the 8 XCDs), so a source line is fetched into that
+    // XCD's L2 once for its four tiles and every target range of the group
+    const int b = blockIdx.x;
+    const int tile = 4 * (b & 7) + ((b >> 3) & 3), rest = b >> 5, tg = rest % ntg, z = rest / ntg;
+    const int hz = cb.h[z], sp = cb.split[z], skip0 = cb.skip0[z];
+    const int tper = (nt + ntg - 1) / ntg, t0 = tg * tper, t1 = min(nt, t0 + tper);
+    if (t0 >= t1 || (t0 >= skip0 && t1 <= skip0 + hz)) return;  // nothing to convert (block-uniform)
+    ts_begin(ts);
+    const int c = threadIdx.x & 7, p = threadIdx.x >> 3, col = tile * 8 + c;
+    int buf = 0;
+    u32 y[HM][8];
+    bx_sources<0, HM>(y, cb, z, hz, sp, pc, itw, sm, buf, p, c, col);
+    // u = round(sum y_i / q_i), k_base_convert's 32.32 fixed point in its source order (summed
+    // here, after the transforms, so the sums are not live through them)
+    u32 mu[HM];
+#pragma unroll
+    for (int i = 0; i < HM; ++i) mu[i] = i < hz ? pc[(sp > 0 && i >= sp) ? cb.d1[z] + (i - sp) : cb.d0[z] + i].mu : 0u;
+    u32 u[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        u64 f = 0;
+#pragma unroll
+        for (int i = 0; i < HM; ++i) f += ((u64)y[i][e] * mu[i]) >> 29;
+        u[e] = (u32)((f + (1ull << 31)) >> 32);
+    }
+    u32* dst = cb.dst[z];
+    for (int t = t0; t < t1; ++t) {
+        if (t >= skip0 && t < skip0 + hz) continue;  // the ModUp digit's own limbs (block-uniform)
+        const int prime = map.prime(t);
+        const PrimeConst P = pc[prime];
+        const u32 q = P.q, q2 = 2 * q, negq = cb.negq[z][t];
+        u32 wt[HM];
+#pragma unroll
+        for (int i = 0; i < HM; ++i) wt[i] = i < hz ? cb.tab[z][2 * ((size_t)i * nt + t)] : 0u;
+        u32 x[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            u64 acc = (u64)u[e] * negq;
+#pragma unroll
+            for (int i = 0; i < HM; ++i) {
+                if (i == 8) acc = fold64(acc, q, P.r32);  // (a zero-weight tail may add this fold: same residue)
+                acc += (u64)y[i][e] * wt[i];
+            }
+            x[e] = reduce64(acc, q, P.mu, P.r32);
+        }
+        const uint2* w = tw + ((size_t)prime << LOGN);
+        bx_fwd<kBxA, 0, 4>(x, w, p, q2, q);
+        bx_fwd<kBxA, 1, 2>(x, w, p, q2, q);
+        bx_fwd<kBxA, 2, 1>(x, w, p, q2, q);
+        bx_xchg<kBxA, kBxBf>(x, sm[buf], p, c);
+        buf ^= 1;
+        bx_fwd<kBxBf, 3, 4>(x, w, p, q2, q);
+        bx_fwd<kBxBf, 4, 2>(x, w, p, q2, q);
+        bx_fwd<kBxBf, 5, 1>(x, w, p, q2, q);
+        bx_xchg<kBxBf, kBxC>(x, sm[buf], p, c);
+        buf ^= 1;
+        bx_fwd<kBxC, 6, 2>(x, w, p, q2, q);
+        bx_fwd<kBxC, 7, 1>(x, w, p, q2, q);
+        u32* d = dst + ((size_t)t << LOGN);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[(size_t)bx_row<kBxC>(p, e) * 256 + col] = x[e];
+    }
+    ts_end(ts);
+}
+template <int HM>
+void bx_go(hipStream_t st, const DevTables& Tb, const ConvBatch& cb, int nt, int ntg, LimbMap map, double bytes) {
+    prof_launch_tsw(KID_BASE_CONVERT, bytes, 0.0, k_bx_cols<HM>, dim3(32 * ntg * cb.n), dim3(256), 0, st, cb, nt, ntg, map, Tb.pc, Tb.tw, Tb.itw);
+}
+
 }  // namespace
 
 int ntt_conv_fused_mask(const DevTables& T) {
@@ -1234,6 +1402,100 @@ void launch_ntt_inv_cols(hipStream_t st, const DevTables& T, u32* data, int rows
         case 16: ntt_inv_cols_t<8>(st, T, data, rows, rm, map, post); break;
         default: break;
     }
+}
+
+// k_bx_cols exists for N = 2^16 (the engine's AESFHE_BX_COLS switch decides where it runs)
+int bx_cols_on(const DevTables& T) { return T.logn == 16 ? 1 : 0; }
+void launch_bx_cols(hipStream_t st, const DevTables& T, const ConvBatch& cb, int nt, LimbMap map) {
+    if (T.logn != 16) throw std::runtime_error("launch_bx_cols: N = 2^16 only");
+    if (cb.n < 1 || cb.n > kMaxConvGroups) throw std::runtime_error("launch_bx_cols: bad group count");
+    int hmax = 0, eff = 0;
+    double rows = 0.0;
+    for (int z = 0; z < cb.n; ++z) {
+        if (cb.h[z] < 1 || cb.h[z] > kMaxConvH) throw std::runtime_error("launch_bx_cols: source count out of range");
+        if (!cb.src[z] || !cb.dst[z] || !cb.tab[z] || !cb.qhinv[z] || !cb.negq[z]) throw std::runtime_error("launch_bx_cols: missing operand");
+        hmax = std::max(hmax, cb.h[z]);
+        int own = 0;
+        for (int t = 0; t < nt; ++t) own += t >= cb.skip0[z] && t < cb.skip0[z] + cb.h[z];
+        eff = std::max(eff, nt - own);
+        rows += cb.h[z] + (nt - own);
+    }
+    // target ranges per group: enough blocks to cover the chip (AESFHE_BX_BLOCKS, default 256), at
+    // least 3 targets per block to amortise its H inverse transforms
+    static const int want = [] {
+        const char* e = std::getenv("AESFHE_BX_BLOCKS");
+        return e ? std::max(32, std::atoi(e)) : 256;
+    }();
+    int ntg = (want + 32 * cb.n - 1) / (32 * cb.n);
+    ntg = std::max(1, std::min(ntg, std::max(1, eff / 3)));
+    const double bytes = rows * 4.0 * 65536.0;
+    if (hmax <= 4) bx_go<4>(st, T, cb, nt, ntg, map, bytes);
+    else if (hmax <= 8) bx_go<8>(st, T, cb, nt, ntg, map, bytes);
+    else if (hmax <= 10) bx_go<10>(st, T, cb, nt, ntg, map, bytes);
+    else if (hmax <= 11) bx_go<11>(st, T, cb, nt, ntg, map, bytes);
+    else if (hmax <= 12) bx_go<12>(st, T, cb, nt, ntg, map, bytes);
+    else throw std::runtime_error("launch_bx_cols: more than 12 sources per group (the residues would not fit in VGPRs)");
+}
+// the inverse NTT's row pass alone (k_bx_cols then runs the column pass): plain, product (tp) or
+// reversed (rev) input, the launches ntt_inv_t issues for that pass (N = 2^16)
+void launch_ntt_inv_rows(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map,
+                         const TensorPtrs* tp, bool rev) {
+    if (rows <= 0) return;
+    if (T.logn != 16) throw std::runtime_error("launch_ntt_inv_rows: N = 2^16 only");
+    constexpr int LOGR1 = 8, R1 = 1 << LOGR1;
+    rm.nrows = rows;
+    const int groups = (rows + rm.cnt - 1) / rm.cnt;
+    const double io = (tp ? 3.0 : 2.0) * 4.0 * rows * (256.0 * R1), bfly = (double)rows * 128.0 * R1 * 8.0;
+    if (small_launch(rows)) {
+        ntt2_inv_launch<LOGR1, kThreads / 2>(st, T, dst, src, rm, map, groups, io, bfly, tp, rev);
+        return;
+    }
+    switch (p2_nt_rows(true, rows)) {
+        case 128: ntt2_inv_launch<LOGR1, 128>(st, T, dst, src, rm, map, groups, io, bfly, tp, rev); break;
+        case 256: ntt2_inv_launch<LOGR1, 256>(st, T, dst, src, rm, map, groups, io, bfly, tp, rev); break;
+        default: ntt2_inv_launch<LOGR1, kThreads>(st, T, dst, src, rm, map, groups, io, bfly, tp, rev); break;
+    }
+}
+// the forward NTT's row pass alone, in place (after k_bx_cols), with the RowMap's skips
+void launch_ntt_fwd_rows(hipStream_t st, const DevTables& T, u32* data, int rows, RowMap rm, LimbMap map) {
+    if (rows <= 0) return;
+    if (T.logn != 16) throw std::runtime_error("launch_ntt_fwd_rows: N = 2^16 only");
+    int io_rows = rows;
+    if (rm.skip_alpha > 0)
+        for (int y = 0; y < rows; ++y) {
+            const int g = y / rm.cnt, i = y - g * rm.cnt;
+            if (i < rm.skip_nl && i / rm.skip_alpha == (rm.skip_groups > 0 ? g % rm.skip_groups : g)) --io_rows;
+        }
+    constexpr int LOGR1 = 8, R1 = 1 << LOGR1;
+    rm.nrows = rows;
+    const int groups = (rows + rm.cnt - 1) / rm.cnt;
+    ntt2_fwd_select<LOGR1, kPlain>(st, T, data, rm, map, groups, 2.0 * io_rows * 4.0 * 256.0 * R1, (double)io_rows * 128.0 * R1 * 8.0, NttAux{});
+}
+// launch_ntt_finish's row pass alone (its column pass ran inside k_bx_cols)
+void launch_ntt_finish_rows(hipStream_t st, const DevTables& T, u32* out, u32* conv, const u32* cur, int cur_stride, const u32* qinv,
+                            const u32* add0, const u32* add1, int npoly, int nt, size_t add_mstride, u32* const* outm, bool add_rev,
+                            unsigned dbl, const u32* const* cst) {
+    if (T.logn != 16) throw std::runtime_error("launch_ntt_finish_rows: N = 2^16 only");
+    NttAux aux{};
+    aux.cur = cur, aux.out = out, aux.qinv = qinv, aux.cur_stride = cur_stride, aux.out_stride = nt, aux.add0 = add0, aux.add1 = add1;
+    aux.add_mstride = add_mstride;
+    if (outm) {
+        if (npoly > 16 || npoly % 2) throw std::runtime_error("launch_ntt_finish: per-member outputs for at most 8 two-polynomial members");
+        for (int m = 0; m < npoly / 2; ++m) aux.outm[m] = outm[m];
+    }
+    if (dbl || cst) {
+        if (npoly > 16 || npoly % 2) throw std::runtime_error("launch_ntt_finish: the 2 r + c epilogue for at most 8 two-polynomial members");
+        aux.dbl = dbl;
+        if (cst)
+            for (int m = 0; m < npoly / 2; ++m) aux.cst[m] = cst[m];
+    }
+    aux.add_rev = add_rev ? 1 : 0;
+    constexpr int LOGR1 = 8, R1 = 1 << LOGR1;
+    RowMap rm = rows_dense(nt);
+    const int rows = npoly * nt;
+    rm.nrows = rows;
+    const double io2 = (3.0 + (add0 ? 0.5 : 0.0) + (add1 ? 0.5 : 0.0)) * rows * 4.0 * 256.0 * R1;
+    ntt2_fwd_select<LOGR1, kFinish>(st, T, conv, rm, LimbMap{1 << 30, 0, 0}, npoly, io2, (double)rows * 128.0 * R1 * 8.0, aux);
 }
 void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map) {
     launch_ntt_fwd(st, T, data, data, rows, rows_dense(nl), map);

@@ -42,19 +42,19 @@ for t in "$@"; do
       timeout -k 10 120 python3 tools/trace_window.py $O/kernel_stats_timed.json $O/prof
       rm -f $O/prof/run_kernel_trace.csv ;;
     pmc)
+      # FETCH_SIZE / WRITE_SIZE passes over one middle C2 round (tools/pmc_round.py) with the
+      # engine's algorithmic bytes of the same launches.  The full bench under the counters does not
+      # complete on this image: with --kernel-include-regex no encrypt finished in 270 s (twice), without
+      # it rocprofv3 segfaulted in its own thread 6 s in (profiles/r4_pmc_bench_attempts.txt)
       KIDS=key_inner,base_convert,ntt_cols_fwd,ntt_rows_fwd,ntt_rows_inv,ntt_cols_inv,lin_mac
-      P="bench.py --steps 2 --warmup 1 $C2"
-      AESFHE_PROFILE_FROM_START=$KIDS timeout -k 10 300 python3 $P --whole-stats $O/pmc_algorithmic.json > $O/pmc_alg.out
-      # the counter passes: the bench WITHOUT the engine's in-kernel timestamps and without a
-      # --kernel-include-regex filter (with the filter the bench crawled under the counters -- no
-      # encrypt finished in 270 s, twice, r4e; unfiltered it completes: profiles/r3_pmc_bench_check.txt);
-      # pmc_reduce.py keeps every kernel, the bench line reads the classes it times
-      timeout -s KILL 200 rocprofv3 --pmc FETCH_SIZE --output-format csv \
-          -d $O/pmc_fetch -o run -- python3 $P --whole-stats none > $O/pmc_fetch.out 2> $O/pmc_fetch.err
-      timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv \
-          -d $O/pmc_write -o run -- python3 $P --whole-stats none > $O/pmc_write.out 2> $O/pmc_write.err
-      timeout -k 10 300 python3 tools/pmc_reduce.py "--source=rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes (separate runs, every kernel counted) over the bench's own C2 leg (bench.py --steps 2 --warmup 1, whole process incl. key generation; algorithmic bytes of exactly those launches from the engine, AESFHE_PROFILE_FROM_START + --whole-stats); FETCH_SIZE x2 for 16-B-per-lane reads, x1 for NTT pass 2 dword reads (tools/ntt_pmc_calib.py); L2-miss bytes (MALL hits included), an upper bound on HBM bytes" \
-          --alg=$O/pmc_algorithmic.json $O/pmc_traffic_bench.json $O/pmc_fetch $O/pmc_write > /dev/null
+      RX='k_ntt1_fwd|k_ntt2_fwd|k_ntt1_inv|k_ntt2_inv|k_lin_mac|k_base_convert|k_key_inner|k_ntt2_ki|k_bx_cols'
+      AESFHE_PROFILE_FROM_START=$KIDS timeout -k 10 200 python3 tools/pmc_round.py $O/pmc_algorithmic.json > $O/pmc_alg.out
+      timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$RX" --output-format csv -d $O/pmc_fetch -o run -- \
+          python3 tools/pmc_round.py > $O/pmc_fetch.out 2> $O/pmc_fetch.err
+      timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$RX" --output-format csv -d $O/pmc_write -o run -- \
+          python3 tools/pmc_round.py > $O/pmc_write.out 2> $O/pmc_write.err
+      timeout -k 10 300 python3 tools/pmc_reduce.py "--source=rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes (separate runs, --kernel-include-regex on the NTT / conversion / key-switch / lin_mac kernels) over tools/pmc_round.py: one middle encrypt round of the bench workload, whole process incl. key generation; algorithmic bytes of exactly those launches from the engine (AESFHE_PROFILE_FROM_START); FETCH_SIZE x2 for 16-B-per-lane reads, x1 for NTT pass 2 dword reads (tools/ntt_pmc_calib.py); L2-miss bytes (MALL hits included), an upper bound on HBM bytes" \
+          --alg=$O/pmc_algorithmic.json $O/pmc_traffic_round.json $O/pmc_fetch $O/pmc_write > /dev/null
       rm -rf $O/pmc_fetch $O/pmc_write ;;
     twogpu)
       AESFHE_DIST_BACKEND=gloo timeout -k 10 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr=127.0.0.1 \
