@@ -1135,8 +1135,14 @@ __device__ __forceinline__ void bx_xchg(u32 (&x)[8], u32* sm, int p, int c) {
 }
 // source I of the group (template recursion: every y[I] index is a compile-time constant, so the
 // residues stay in VGPRs at any HM -- a run-time loop this large is not unrolled and goes to scratch)
+// nx: source I's residues, loaded by the previous step; source I + 1's are issued here before
+// source I's transform, so their latency overlaps it
+__device__ __forceinline__ void bx_load(u32 (&x)[8], const u32* s, int p, int col) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] = s[(size_t)bx_row<kBxC>(p, e) * 256 + col];
+}
 template <int I, int HM>
-__device__ __forceinline__ void bx_sources(u32 (&y)[HM][8], const ConvBatch& cb, int z, int hz, int sp, const PrimeConst* pc,
+__device__ __forceinline__ void bx_sources(u32 (&y)[HM][8], u32 (&nx)[8], const ConvBatch& cb, int z, int hz, int sp, const PrimeConst* pc,
                                            const uint2* itw, u32 (*sm)[2048], int& buf, int p, int c, int col) {
     if constexpr (I < HM) {
         constexpr int LOGN = 16;
@@ -1145,10 +1151,10 @@ __device__ __forceinline__ void bx_sources(u32 (&y)[HM][8], const ConvBatch& cb,
             const PrimeConst P = pc[prime];
             const u32 q = P.q, q2 = 2 * q, nq = 0u - q;
             const uint2* w = itw + ((size_t)prime << LOGN);
-            const u32* s = cb.src[z] + ((size_t)I << LOGN);
             u32 x[8];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) x[e] = s[(size_t)bx_row<kBxC>(p, e) * 256 + col];
+            for (int e = 0; e < 8; ++e) x[e] = nx[e];
+            if (I + 1 < hz) bx_load(nx, cb.src[z] + ((size_t)(I + 1) << LOGN), p, col);
             bx_inv<kBxC, 7, 1>(x, w, p, q2, nq);
             bx_inv<kBxC, 6, 2>(x, w, p, q2, nq);
             bx_inv<kBxC, 5, 4>(x, w, p, q2, nq);
@@ -1169,7 +1175,7 @@ __device__ __forceinline__ void bx_sources(u32 (&y)[HM][8], const ConvBatch& cb,
 #pragma unroll
             for (int e = 0; e < 8; ++e) y[I][e] = 0u;
         }
-        bx_sources<I + 1, HM>(y, cb, z, hz, sp, pc, itw, sm, buf, p, c, col);
+        bx_sources<I + 1, HM>(y, nx, cb, z, hz, sp, pc, itw, sm, buf, p, c, col);
     }
 }
 template <int HM>
@@ -1189,7 +1195,9 @@ __global__ void __launch_bounds__(256) k_bx_cols(ConvBatch cb, int nt, int ntg, 
     const int c = threadIdx.x & 7, p = threadIdx.x >> 3, col = tile * 8 + c;
     int buf = 0;
     u32 y[HM][8];
-    bx_sources<0, HM>(y, cb, z, hz, sp, pc, itw, sm, buf, p, c, col);
+    u32 nx[8];
+    bx_load(nx, cb.src[z], p, col);
+    bx_sources<0, HM>(y, nx, cb, z, hz, sp, pc, itw, sm, buf, p, c, col);
     // u = round(sum y_i / q_i), k_base_convert's 32.32 fixed point in its source order (summed
     // here, after the transforms, so the sums are not live through them)
     u32 mu[HM];
