@@ -3678,8 +3678,10 @@ public:
     // relative precision 2^-k1bits; the true-FHE snap's kappa, zeta16_noise_reducer.py)
     // level-0 stack z (nb members, consumed) -> the bootstrapped stack, in chunks of two members
     // (the pair bootstrap's batch: every key and diagonal read once per chunk)
-    // members per chunk (AESFHE_BOOT_CHUNK, default 2: the pair bootstrap's packed EvalMod)
-    int boot_chunk_ = std::max(1, env_int("AESFHE_BOOT_CHUNK", 2));
+    // members per chunk (AESFHE_BOOT_CHUNK, default 4: a 16-pair stack's final bootstraps 98.1 -> 86.4 ms
+    // per round against chunks of 2, profiles/r4_stack16_chunk{2,4}_step_profile.json; every member's
+    // bytes are the same at any chunk size, tests/test_gpu_boot_chunk.py)
+    int boot_chunk_ = std::max(1, env_int("AESFHE_BOOT_CHUNK", 4));
     Ct boot_stack(Ct z, double gain, SparseBoot* sv) {
         const int P = z.nb, B = boot_chunk_;
         if (P <= B) return bootstrap_l0(z, 99, gain, sv);
