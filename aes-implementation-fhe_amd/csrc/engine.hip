@@ -4495,6 +4495,7 @@ static thread_local std::string t_err;
 
 #define API_BEGIN                                      \
     if (!ctx) return -2;                               \
+    g_census_op = __func__;                            \
     std::lock_guard<std::recursive_mutex> lock_(ctx->mu); \
     if (ctx->eng) ctx->eng->activate();                \
     try {
@@ -4938,6 +4939,7 @@ int aesfhe_kernel_gaps(aesfhe_ctx* ctx, double* out, int n) {
     API_END
 }
 uint64_t aesfhe_launch_count(void) { return g_launches.load(std::memory_order_relaxed); }
+uint64_t aesfhe_launch_census(char* buf, uint64_t cap, int reset) { return census_dump(buf, (size_t)cap, reset != 0); }
 int aesfhe_alg_bytes(double* bytes, uint64_t* launches, int n) {
     if (!bytes || !launches) return -2;
     for (int k = 0; k < n && k < KID_N; ++k) {

@@ -3,6 +3,11 @@
 // Data layout in HBM: an RNS tensor is [rows][N] uint32 with rows = npoly * nl, limb
 // l = row % nl living modulo prime map.prime(l).  Wave64 / 256-thread blocks; every
 // global access below is unit-stride across consecutive lanes.
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+
 #include "kernels.h"
 
 #include <algorithm>
@@ -704,6 +709,30 @@ void prof_set(KernelProfiler* p) { g_prof = p; }
 std::atomic<unsigned long long> g_launches{0};
 std::atomic<unsigned long long> g_alg_bytes[KID_N] = {};
 std::atomic<unsigned long long> g_alg_launches[KID_N] = {};
+const bool g_census_on = std::getenv("AESFHE_CENSUS") && std::atoi(std::getenv("AESFHE_CENSUS")) != 0;
+thread_local const char* g_census_op = nullptr;
+static std::mutex g_census_mu;
+static std::map<std::pair<std::string, const void*>, unsigned long long> g_census;
+void census_add(const void* fn) {
+    std::lock_guard<std::mutex> lk(g_census_mu);
+    ++g_census[{g_census_op ? g_census_op : "(internal)", fn}];
+}
+// "op\tkernel\tlaunches\n" lines into buf (NUL-terminated); returns the bytes needed
+size_t census_dump(char* buf, size_t cap, bool reset) {
+    std::lock_guard<std::mutex> lk(g_census_mu);
+    std::string out;
+    for (const auto& kv : g_census) {
+        const char* nm = hipKernelNameRefByPtr(kv.first.second, nullptr);
+        out += kv.first.first + "\t" + (nm ? nm : "?") + "\t" + std::to_string(kv.second) + "\n";
+    }
+    if (buf && cap) {
+        const size_t n = std::min(cap - 1, out.size());
+        std::memcpy(buf, out.data(), n);
+        buf[n] = 0;
+    }
+    if (reset) g_census.clear();
+    return out.size() + 1;
+}
 
 // ======================================================================================
 // launch validation (launch.h launch_validate): per-kernel limits, queried once

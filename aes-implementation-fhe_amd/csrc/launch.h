@@ -22,6 +22,12 @@ extern std::atomic<unsigned long long> g_launches;
 // not (aesfhe_alg_bytes): the numerator of bench.py's whole-step roofline
 extern std::atomic<unsigned long long> g_alg_bytes[KID_N];
 extern std::atomic<unsigned long long> g_alg_launches[KID_N];
+// launch census by (C-ABI entry point, kernel) (AESFHE_CENSUS=1, aesfhe_launch_census): which API
+// call issues which kernels how often -- tools/op_kernel_census.py; off: one predicted branch
+extern const bool g_census_on;
+extern thread_local const char* g_census_op;
+void census_add(const void* fn);
+size_t census_dump(char* buf, size_t cap, bool reset);
 inline void alg_account(int kid, double bytes) {
     if (kid < 0 || kid >= KID_N) return;
     g_alg_bytes[kid].fetch_add((unsigned long long)(bytes + 0.5), std::memory_order_relaxed);
@@ -63,6 +69,7 @@ inline void launch_validate(F kernel, dim3 grid, dim3 block, size_t lds) {
     const void* fn = reinterpret_cast<const void*>(kernel);
     constexpr size_t ka = kernarg_bytes<Args...>();
     g_launches.fetch_add(1, std::memory_order_relaxed);
+    if (g_census_on) census_add(fn);
     if (grid.x < 1 || grid.y < 1 || grid.z < 1 || grid.x > 0x7fffffffu || grid.y > 65535u || grid.z > 65535u)
         launch_reject(fn, "grid dimension out of range", grid, block, lds, ka);
     const LaunchLimits& lim = launch_limits(fn);

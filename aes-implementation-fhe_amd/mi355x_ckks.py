@@ -44,7 +44,7 @@ EXPORTED = [
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot", "aesfhe_create_keyed", "aesfhe_bootstrap_sparse", "aesfhe_bootstrap_pair_sparse", "aesfhe_renorm_periodic",
     "aesfhe_renorm_single", "aesfhe_renorm_unpack",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_debug_lin_group_plain", "aesfhe_lut_create", "aesfhe_lut_eval", "aesfhe_lut_free",
-    "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled", "aesfhe_set_enc_nonce", "aesfhe_launch_count",
+    "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled", "aesfhe_set_enc_nonce", "aesfhe_launch_count", "aesfhe_launch_census",
     "aesfhe_galois_multi", "aesfhe_debug_boot_stage_sparse", "aesfhe_debug_sparse_group", "aesfhe_debug_sparse_group_plain",
     "aesfhe_debug_mono_pack", "aesfhe_debug_mono_split", "aesfhe_alg_bytes", "aesfhe_stack", "aesfhe_unstack", "aesfhe_members",
     "aesfhe_renorm_packed",
@@ -138,6 +138,7 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_level_limbs"] = [vp, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")]
     sig["aesfhe_set_enc_nonce"] = [vp, ctypes.c_uint64]
     sig["aesfhe_launch_count"] = []
+    sig["aesfhe_launch_census"] = [ctypes.c_char_p, ctypes.c_uint64, c_int]
     sig["aesfhe_alg_bytes"] = [_dp, np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS"), c_int]
     sig["aesfhe_galois_multi"] = [vp, c_int, _Hp, _Hp, _Hp]
     sig["aesfhe_debug_boot_stage_sparse"] = [vp, _H, c_int, c_int, _Hp]
@@ -151,8 +152,8 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_renorm_packed"] = [vp, _H, c_int, c_int, _Hp]
     for name in EXPORTED:
         fn = getattr(L, name)
-        fn.restype = (ctypes.c_char_p if name == "aesfhe_last_error" else ctypes.c_uint64 if name == "aesfhe_launch_count"
-                      else ctypes.c_int)
+        fn.restype = (ctypes.c_char_p if name == "aesfhe_last_error"
+                      else ctypes.c_uint64 if name in ("aesfhe_launch_count", "aesfhe_launch_census") else ctypes.c_int)
         fn.argtypes = [vp] if name == "aesfhe_last_error" else sig[name]
     _lib = L
     return L
@@ -872,6 +873,20 @@ class Engine:
 def launch_count() -> int:
     """kernel launches issued by this process so far (aesfhe_launch_count)"""
     return int(load_library().aesfhe_launch_count())
+
+
+def launch_census(reset: bool = False) -> dict:
+    """{C-ABI entry point: {kernel name: launches}} since start-up / the last reset (AESFHE_CENSUS=1
+    at process start; aesfhe_launch_census)"""
+    L = load_library()
+    need = int(L.aesfhe_launch_census(None, 0, 0))
+    buf = ctypes.create_string_buffer(need + 1)
+    L.aesfhe_launch_census(buf, need + 1, 1 if reset else 0)
+    out: dict = {}
+    for line in buf.value.decode().splitlines():
+        op, kern, n = line.split("\t")
+        out.setdefault(op, {})[kern] = out.get(op, {}).get(kern, 0) + int(n)
+    return out
 
 
 def alg_bytes() -> dict:

@@ -325,6 +325,10 @@ int aesfhe_pool_stats(aesfhe_ctx* ctx, uint64_t* out);
 /* kernel launches issued by this process so far (all contexts): the launch census of
  * tools/launch_census.py and bench.py's launches-per-encrypt (MI355X-side tooling) */
 uint64_t aesfhe_launch_count(void);
+/* launch census by (C-ABI entry point, kernel name), collected when the process starts with
+ * AESFHE_CENSUS=1: "entry\tkernel\tlaunches\n" lines into buf (NUL-terminated, truncated to cap);
+ * returns the bytes the whole census needs; reset != 0 clears it (tools/op_kernel_census.py) */
+uint64_t aesfhe_launch_census(char* buf, uint64_t cap, int reset);
 /* per kernel id (the aesfhe_profile order): algorithmic bytes and launches of
  * every launch this process issued so far, timed or not -- bench.py's whole-step roofline
  * (sum of algorithmic bytes of the timed steps / wall / 8 TB/s) */

@@ -14,6 +14,7 @@
 #                           share it): the N > 1 engine path at the C4 / C5 per-rank shapes
 #   boot                    tools/boot_phases.py 32 (sparse bootstrap phases)
 #   census                  tools/launch_census.py (launches / ms per AES step)
+#   opcensus                tools/op_kernel_census.py (launches of one encrypt by C-ABI entry and kernel)
 #   stack                   tools/step_profile.py on the 64-pair stacked leg (STACK_ARGS)
 #   sweep                   tools/ntt_grid_sweep.py (NTT time vs rows per block-size configuration)
 #   probes                  tools/micro/grid_sync_probe, graph_gap_probe, wt_boundary_probe (built here by hipcc)
@@ -64,6 +65,8 @@ for t in "$@"; do
       timeout -k 10 300 python3 tools/boot_phases.py 32 > $O/boot_phases.json 2> $O/boot.err ;;
     census)
       timeout -k 10 300 python3 tools/launch_census.py > $O/launch_census.json 2> $O/census.err ;;
+    opcensus)
+      AESFHE_CENSUS=1 timeout -k 10 300 python3 tools/op_kernel_census.py > $O/op_kernel_census.json 2> $O/opcensus.err ;;
     stack)
       timeout -k 10 600 python3 tools/step_profile.py ${STACK_ARGS:-pairs=64 reps=1} > $O/stack_profile.json 2> $O/stack.err ;;
     sweep)
