@@ -808,8 +808,13 @@ public:
 
     // drop the last k limbs of an npoly x nl tensor, dividing by each dropped prime with
     // rounding; returns a pool buffer of npoly x (nl - k) rows
-    u32* drop_limbs(const u32* x, int np, int nl, int k) {
+    // x: np polys of nl limbs each (poly stride `stride` limbs, default nl) -> the first nl - k limbs,
+    // divided by the k dropped primes.  cc (nullable, [nl] Shoup pairs): x is first multiplied by a
+    // constant (Engine::convert's exact-scale factor) -- folded into the dropped limbs' INTT (post)
+    // and the finish's cur read (cmul), no separate multiply launch and no multiplied copy
+    u32* drop_limbs(const u32* x, int np, int nl, int k, int stride = 0, const u32* cc = nullptr) {
         const int n = hp_.n;
+        if (stride <= 0) stride = nl;
         if (k == 2 && nl >= 3) {
             // both primes at once: INTT of the two dropped rows per poly, then one fused
             // CRT-spread -> NTT -> (cur - v) (q_a q_b)^{-1} pass over the r = nl - 2 kept limbs
@@ -817,11 +822,11 @@ public:
             const u32 qa = hp_.mod[r], qb = hp_.mod[r + 1];
             const u32 ainv = hinvm(qa % qb, qb);
             u32* last = tmp(2 * (size_t)np);
-            intt(last, x, 2 * np, RowMap{2, nl, 2, r, 0}, LimbMap{2, r, 0});
+            intt(last, x, 2 * np, RowMap{2, stride, 2, r, 0}, LimbMap{2, r, 0}, cc ? cc + 2 * (size_t)r : nullptr);
             u32* v = tmp((size_t)np * r);
             u32* o = tmp((size_t)np * r);
-            launch_rescale2_ntt(S(), T_, o, x, last, v, d_rescale2_qinv_ + rescale2_off_[r], np, r, nl, qa, qb, ainv,
-                                shoup_pre(ainv, qb));
+            launch_rescale2_ntt(S(), T_, o, x, last, v, d_rescale2_qinv_ + rescale2_off_[r], np, r, stride, qa, qb, ainv,
+                                shoup_pre(ainv, qb), cc);
             cnt_[C_NTT_ROWS] += (size_t)np * r;
             untmp(last, 2 * (size_t)np);
             untmp(v, (size_t)np * r);
@@ -831,13 +836,15 @@ public:
         u32* owned = nullptr;
         for (int step = 0; step < k; ++step) {
             const int r = nl - 1 - step;  // limb dropped now; cur has r + 1 limbs per poly
+            const int cs = step ? r + 1 : stride;
+            const u32* c0 = step ? nullptr : cc;  // the constant rides on the first drop only
             // coefficients of the dropped limb (one row per poly, read in place), then the
             // fused spread -> NTT -> (cur - v) q_r^{-1} on the r remaining limbs
             u32* last = tmp(np);
-            intt(last, cur, np, RowMap{1, r + 1, 1, r, 0}, single(r));
+            intt(last, cur, np, RowMap{1, cs, 1, r, 0}, single(r), c0 ? c0 + 2 * (size_t)r : nullptr);
             u32* v = tmp((size_t)np * r);
             u32* o = tmp((size_t)np * r);
-            launch_rescale_ntt(S(), T_, o, cur, last, v, d_rescale_qinv_ + rescale_off_[r], np, r, r + 1, hp_.mod[r]);
+            launch_rescale_ntt(S(), T_, o, cur, last, v, d_rescale_qinv_ + rescale_off_[r], np, r, cs, hp_.mod[r], c0);
             cnt_[C_NTT_ROWS] += (size_t)np * r;
             untmp(last, np);
             untmp(v, (size_t)np * r);
@@ -929,8 +936,16 @@ public:
             return o;
         }
         const int nk = nb + k;
-        u32* mid = tmp((size_t)c.npoly * nk);
         const i64 cst = std::llround(ratio);
+        if (k > 0 && fused_convert_) {  // the constant folded into the drop (drop_limbs cc): one launch and one copy fewer
+            Ct o;
+            o.level = t, o.npoly = c.npoly, o.nb = c.nb, o.pend = p, o.lazy = c.lazy || p > 0, o.zero = c.zero;
+            o.words = (size_t)c.npoly * nb * n;
+            o.data = drop_limbs(c.data, c.npoly, nk, k, na, conv_consts(cst, nk));
+            if (own) release(c);
+            return o;
+        }
+        u32* mid = tmp((size_t)c.npoly * nk);
         std::vector<u32> r(nk);
         for (int i = 0; i < nk; ++i) r[i] = mod_i64(cst, hp_.mod[i]);
         // the first nk limbs of every poly, times the constant (copy fused into the multiply)
@@ -946,6 +961,24 @@ public:
         }
         if (own) release(c);
         return o;
+    }
+    // AESFHE_FUSED_CONVERT=0: the conversion's constant as its own launch (A/B, bit-identity test)
+    bool fused_convert_ = !(std::getenv("AESFHE_FUSED_CONVERT") && std::atoi(std::getenv("AESFHE_FUSED_CONVERT")) == 0);
+    // [nk] Shoup pairs of cst mod q_i on the device, cached per (constant, limb count): the same
+    // conversions recur every round
+    std::map<std::pair<i64, int>, u32*> conv_cst_;
+    const u32* conv_consts(i64 cst, int nk) {
+        auto it = conv_cst_.find({cst, nk});
+        if (it != conv_cst_.end()) return it->second;
+        std::vector<u32> h(2 * (size_t)nk);
+        for (int i = 0; i < nk; ++i) {
+            const u32 v = mod_i64(cst, hp_.mod[i]);
+            h[2 * i] = v, h[2 * i + 1] = shoup_pre(v, hp_.mod[i]);
+        }
+        u32* d = dev_alloc(h.size());
+        HIP_OK(hipMemcpyAsync(d, h.data(), h.size() * sizeof(u32), hipMemcpyHostToDevice, S()));
+        HIP_OK(hipStreamSynchronize(S()));
+        return conv_cst_[{cst, nk}] = d;
     }
     // logical level drop of a canonical (pend 0) tensor
     Ct level_down(const Ct& c_in, int level) {
@@ -3309,7 +3342,11 @@ public:
                 Ct rs = moddown_rescale(blk, l, nb * (int)bj.size());
                 std::vector<u64> gs;
                 for (int j : bj) gs.push_back(rot_galois(-(int)g.giant[g0 + j]));
-                giant_accumulate_many(rs, gs, nb, dh_acc, dh_c0, dh_n);
+                // the only accumulation of the group: one chunk, and no other giant step of it rotated
+                bool sole = g.G <= kLinG && dh_n == 0;
+                for (int j = 0; j < gn && sole; ++j)
+                    if (!in_blk[j] && any[j] && dh && g.giant[g0 + j]) sole = false;
+                giant_accumulate_many(rs, gs, nb, dh_acc, dh_c0, dh_n, sole);
                 release(rs);
                 untmp(blk, bj.size() * 2 * (size_t)ne * nb);
             }
@@ -3376,7 +3413,8 @@ public:
                 for (int mb = 0; mb < nb; ++mb) launch_add(S(), T_, dh_c0 + mb * ms, dh_c0 + mb * ms, out.data + mb * ms, r, r, qmap());
                 add1 = out.data + (size_t)r * n;
             }
-            Ct res = moddown(dh_acc, lv, dh_c0, add1, nb, ms);
+            Ct res = moddown(dh_acc, lv, dh_c0, add1, nb, ms, nullptr, nullptr, false, dh_ys_);
+            if (dh_ys_) untmp(dh_ys_, 2 * (size_t)np * nb), dh_ys_ = nullptr;
             if (have) release(out);
             untmp(dh_acc, 2 * (size_t)ne2 * nb);
             untmp(dh_c0, 2 * (size_t)r * nb);
@@ -3387,7 +3425,10 @@ public:
     // K rotated giant steps at once: rs holds K x nb stacked members ([j][b]), step j permuted
     // by X -> X^gals[j]; their c1 ModUp'ed together (chunks within kMaxConvGroups), each key
     // inner product accumulated into acc, the permuted c0 summed into c0sum per member
-    void giant_accumulate_many(const Ct& rs, const std::vector<u64>& gals, int nb, u32*& acc, u32*& c0sum, int& count) {
+    // sole: no other giant step of the group is accumulated (lin_group): the fused-core form may run
+    bool fused_giant_ = !(std::getenv("AESFHE_FUSED_GIANT") && std::atoi(std::getenv("AESFHE_FUSED_GIANT")) == 0);
+    u32* dh_ys_ = nullptr;  // set by the fused form: the P rows after the INTT row pass, for the ModDown
+    void giant_accumulate_many(const Ct& rs, const std::vector<u64>& gals, int nb, u32*& acc, u32*& c0sum, int& count, bool sole = false) {
         const int K = (int)gals.size(), lv = rs.level, r = hp_.nl(lv), ne2 = r + hp_.n_p, n = hp_.n;
         const size_t ms = (size_t)2 * r * n;
         if (rs.nb != K * nb || K > kMaxMembers) throw std::runtime_error("giant_accumulate_many: batch shape");
@@ -3396,7 +3437,20 @@ public:
         if (!acc) acc = tmp(2 * (size_t)ne2 * nb);
         const int nd = (r + hp_.alpha - 1) / hp_.alpha;
         const int per = std::max(1, std::min(kMaxConvGroups / (nd * nb), kMaxKsBatch));  // steps per ModUp
-        for (int j0 = 0; j0 < K; j0 += per) {
+        if (sole && count == 0 && fused_ki_ok() && fused_giant_ && K <= kMaxKiSrc && per >= K) {
+            // the group's only accumulation: the K key inner products summed in ONE fused-core launch
+            // (multi-source k_ntt2_ki: each step's ModUp row pass in registers, no ext written), the P
+            // rows through the ModDown INTT's row pass into dh_ys_ for lin_group's ModDown
+            const u32* c1 = perm + (size_t)r * n;
+            u32* ext = modup(c1, lv, nb * K, ms, nullptr, false, true);
+            const size_t er = (size_t)ext_rows(lv) * n;
+            KiSrc src[kMaxKiSrc];
+            for (int j = 0; j < K; ++j) src[j] = KiSrc{ext + (size_t)j * nb * er, perm + (size_t)j * nb * ms + (size_t)r * n, ksk(gals[j])};
+            dh_ys_ = tmp(2 * (size_t)hp_.n_p * nb);
+            ki_core(acc, dh_ys_, lv, r, nb, src, K, ms, KsFold{});
+            untmp(ext, (size_t)nb * K * ext_rows(lv));
+        }
+        for (int j0 = 0; j0 < K && !dh_ys_; j0 += per) {
             const int k = std::min(per, K - j0);
             const u32* c1 = perm + (size_t)j0 * nb * ms + (size_t)r * n;
             u32* ext = modup(c1, lv, nb * k, ms);

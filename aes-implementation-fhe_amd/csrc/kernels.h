@@ -113,6 +113,9 @@ struct NttAux {
     // finish: add0 read in reversed coefficient order (word N - 1 - i for word i): the conjugation
     // X -> X^(2N-1) in this NTT order, its c0 addend permuted on load (Engine::galois_lazy)
     int add_rev = 0;
+    // finish: cur read times cmul[i] (Shoup pairs per limb, nullable) -- a level conversion's
+    // exact-scale constant folded into the limb drop that follows it (Engine::convert)
+    const u32* cmul = nullptr;
 };
 // out-of-place (src may equal dst); supported ring sizes 2^13 .. 2^16
 void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map);
@@ -121,13 +124,14 @@ void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* dst, const u32* src
 void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map, const u32* post = nullptr);
 // rescale by the prime q_last, fused: v[p][t] = centred(last[p]) mod q_t -> NTT ->
 // out[p][t] = (cur[p][t] - v) * qinv_t;  cur has nl_in rows per poly, out/v have nt
+// cmul (nullable): cur's limb t times cmul[t] (Shoup pairs) first
 void launch_rescale_ntt(hipStream_t st, const DevTables& T, u32* out, const u32* cur, const u32* last, u32* v, const u32* qinv,
-                        int npoly, int nt, int nl_in, u32 q_last);
+                        int npoly, int nt, int nl_in, u32 q_last, const u32* cmul = nullptr);
 // rescale by the two primes qa = q_last, qb = q_last2 at once (double-prime levels):
 // v = centred CRT of last[p][0..1] (mod qa qb) reduced mod q_t -> NTT ->
 // out[p][t] = (cur[p][t] - v) * (qa qb)^{-1}_t;  last has 2 rows per poly
 void launch_rescale2_ntt(hipStream_t st, const DevTables& T, u32* out, const u32* cur, const u32* last, u32* v, const u32* qinv,
-                         int npoly, int nt, int nl_in, u32 qa, u32 qb, u32 qa_inv, u32 qa_inv_p);
+                         int npoly, int nt, int nl_in, u32 qa, u32 qb, u32 qa_inv, u32 qa_inv_p, const u32* cmul = nullptr);
 // NTT of conv (npoly x nt dense rows, destroyed) fused with
 // out[p][t] = (cur[p * cur_stride + t] - NTT(conv)[p][t]) * qinv_t (+ add_p[t])   (ModDown)
 // npoly = 2 nb for nb batched ciphertexts: group 2 m + p adds add_p + m add_mstride (words)
@@ -276,10 +280,14 @@ void launch_key_inner(hipStream_t st, const DevTables& T, u32* acc, const u32* e
 // each with its own key, ext and d) and, for the acc rows x >= kept, the row pass of the ModDown's
 // inverse NTT into ys ([member][2][ys_rows], row x - kept); rows x < kept go to acc [member][2][ne].
 // Identity Galois element only (a rotation's automorphism permutes across chunks).
+// summed key-switch sources of one fused launch: the lazy conjugation's two (sigma(s), sigma(s)^2),
+// or the rotated giant steps of a double-hoisted linear-transform group (each its own ModUp'd
+// input and key), all accumulated in the same 64-bit sums before the one ModDown
+constexpr int kMaxKiSrc = 8;
 struct KiArgs {
-    const u32* ext[2] = {};
-    const u32* d[2] = {};
-    const u32* key[2] = {};
+    const u32* ext[kMaxKiSrc] = {};
+    const u32* d[kMaxKiSrc] = {};
+    const u32* key[kMaxKiSrc] = {};
     int nsrc = 1;
     int nd = 0, ne = 0, nl = 0, alpha = 1, nkey = 0, nks = 0;
     int kept = 0, ys_rows = 0, nb = 1;

@@ -411,6 +411,13 @@ __global__ void __launch_bounds__(NT, OCC) k_ntt2_fwd(u32* data, RowMap rm, Limb
         uint4* o = reinterpret_cast<uint4*>((om ? om + ((size_t)((grp & 1) * aux.out_stride + li) << LOGN)
                                                : aux.out + ((size_t)(grp * aux.out_stride + li) << LOGN)) + woff);
         const u32 qi = aux.qinv[2 * li], qip = aux.qinv[2 * li + 1];
+        if (aux.cmul) {  // block-uniform: a level conversion's constant on cur (canonical in, canonical out)
+            const u32 cm = aux.cmul[2 * li], cmp = aux.cmul[2 * li + 1];
+#pragma unroll
+            for (int v = 0; v < 4; ++v)
+                cvp[v] = make_uint4(shoup_mul(cvp[v].x, cm, cmp, q), shoup_mul(cvp[v].y, cm, cmp, q), shoup_mul(cvp[v].z, cm, cmp, q),
+                                    shoup_mul(cvp[v].w, cm, cmp, q));
+        }
         // the epilogue 2 r + c (aux.dbl / aux.cst, block-uniform): c on polynomial 0 only, its
         // half (lo / hi slots) by the row -- words R 256 .. of the limb lie in half R >= R1 / 2
         const int mem = (grp >> 1) & 7;
@@ -1309,16 +1316,18 @@ void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* dst, const u32* src
     ntt_fwd_dispatch<kPlain, kPlain>(st, T, dst, src, rows, io_rows, rm, map, NttAux{});
 }
 void launch_rescale_ntt(hipStream_t st, const DevTables& T, u32* out, const u32* cur, const u32* last, u32* v, const u32* qinv,
-                        int npoly, int nt, int nl_in, u32 q_last) {
+                        int npoly, int nt, int nl_in, u32 q_last, const u32* cmul) {
     NttAux aux{};
     aux.cur = cur, aux.out = out, aux.qinv = qinv, aux.cur_stride = nl_in, aux.out_stride = nt, aux.q_last = q_last;
+    aux.cmul = cmul;
     const RowMap rm{nt, 1, nt, 0, 0};
     ntt_fwd_dispatch<kSpread, kFinish>(st, T, v, last, npoly * nt, npoly * nt, rm, LimbMap{1 << 30, 0, 0}, aux);
 }
 void launch_rescale2_ntt(hipStream_t st, const DevTables& T, u32* out, const u32* cur, const u32* last, u32* v, const u32* qinv,
-                         int npoly, int nt, int nl_in, u32 qa, u32 qb, u32 qa_inv, u32 qa_inv_p) {
+                         int npoly, int nt, int nl_in, u32 qa, u32 qb, u32 qa_inv, u32 qa_inv_p, const u32* cmul) {
     NttAux aux{};
     aux.cur = cur, aux.out = out, aux.qinv = qinv, aux.cur_stride = nl_in, aux.out_stride = nt;
+    aux.cmul = cmul;
     aux.q_last = qa, aux.q_last2 = qb, aux.qa_inv = qa_inv, aux.qa_inv_p = qa_inv_p;
     const RowMap rm{nt, 2, nt, 0, 0};
     ntt_fwd_dispatch<kSpread2, kFinish>(st, T, v, last, npoly * nt, npoly * nt, rm, LimbMap{1 << 30, 0, 0}, aux);
@@ -1373,7 +1382,7 @@ void launch_ntt_inv_rev(hipStream_t st, const DevTables& T, u32* dst, const u32*
     }
 }
 void launch_ntt_ki(hipStream_t st, const DevTables& T, const KiArgs& a, LimbMap map) {
-    if (a.nb < 1 || a.nb > kMaxKsBatch || a.nsrc < 1 || a.nsrc > 2 || a.kept < 0 || a.kept > a.ne)
+    if (a.nb < 1 || a.nb > kMaxKsBatch || a.nsrc < 1 || a.nsrc > kMaxKiSrc || a.kept < 0 || a.kept > a.ne)
         throw std::runtime_error("launch_ntt_ki: bad member / source / row counts");
     if (a.fold.rev_d && a.fold.ta[0]) throw std::runtime_error("launch_ntt_ki: reversed d needs no tensor fold");
     if (a.kept < a.ne && !a.ys) throw std::runtime_error("launch_ntt_ki: converted rows need a ys buffer");
