@@ -3425,8 +3425,10 @@ public:
     // K rotated giant steps at once: rs holds K x nb stacked members ([j][b]), step j permuted
     // by X -> X^gals[j]; their c1 ModUp'ed together (chunks within kMaxConvGroups), each key
     // inner product accumulated into acc, the permuted c0 summed into c0sum per member
-    // sole: no other giant step of the group is accumulated (lin_group): the fused-core form may run
-    bool fused_giant_ = !(std::getenv("AESFHE_FUSED_GIANT") && std::atoi(std::getenv("AESFHE_FUSED_GIANT")) == 0);
+    // sole: no other giant step of the group is accumulated (lin_group): the fused-core form may run.
+    // AESFHE_FUSED_GIANT=1 (off by default): C2's sparse plans never take it (10,360 launches either
+    // way, profiles/r4_ab_giant_convert.txt), so it has no GPU coverage yet
+    bool fused_giant_ = std::getenv("AESFHE_FUSED_GIANT") && std::atoi(std::getenv("AESFHE_FUSED_GIANT")) != 0;
     u32* dh_ys_ = nullptr;  // set by the fused form: the P rows after the INTT row pass, for the ModDown
     void giant_accumulate_many(const Ct& rs, const std::vector<u64>& gals, int nb, u32*& acc, u32*& c0sum, int& count, bool sole = false) {
         const int K = (int)gals.size(), lv = rs.level, r = hp_.nl(lv), ne2 = r + hp_.n_p, n = hp_.n;
