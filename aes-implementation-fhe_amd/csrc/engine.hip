@@ -2741,11 +2741,11 @@ public:
                 e = e * 5 % two_n;
             }
             for (int k = 0; k < kStreams; ++k) {
-                d_codec_[k] = (double*)dev_alloc(2 * 64 * 2);  // acc[64] + w[64] doubles
-                // acc zeroed on the stream the codec launches run on, ordered before the first decode
+                d_codec_[k] = (double*)dev_alloc(2 * 64 * 2);  // two accumulators acc[64], or acc + w (AESFHE_SNAP_ENCODE=0)
+                // zeroed on the stream the codec launches run on, ordered before the first decode
                 // (hipMemset on the null stream does not order a hipStreamNonBlocking stream); from
-                // then on k_snap16 re-zeroes acc after each read (kernels.h launch_decode16 / 32)
-                HIP_OK(hipMemsetAsync(d_codec_[k], 0, 64 * sizeof(double), S()));
+                // then on each snapping encode zeroes the other accumulator (kernels.h launch_decode16 / 32)
+                HIP_OK(hipMemsetAsync(d_codec_[k], 0, 2 * 64 * sizeof(double), S()));
                 HIP_OK(hipStreamSynchronize(S()));
                 d_nib_[k] = (int*)dev_alloc(32);
             }
@@ -2800,22 +2800,25 @@ public:
         const double enc_scale = hp_.delta[f] * (double)hp_.mod[hp_.nl(f)];
         u32* m = tmp(2 * (size_t)nq);
         const bool direct32 = direct32_ && ((unpack == 16) || (single && packed_period == 32));
+        // the snap inside the encode (AESFHE_SNAP_ENCODE, default on): the two accumulators of this
+        // stream alternate -- this renorm decodes into one, its encode snaps from it and zeroes the other
+        double* acc = d_codec_[t_sidx] + (snap_encode_ ? 64 * codec_flip_[t_sidx] : 0);
+        double* zacc = snap_encode_ ? d_codec_[t_sidx] + 64 * (1 - codec_flip_[t_sidx]) : nullptr;
+        double* wv = snap_encode_ ? acc : d_codec_[t_sidx] + 64;
         if (direct32) {
             // the 32 slots of the packed period-32 state: one direct decode, the snap as 2 x 16, and
             // either the two 16-periodic halves (unpack) or the 32-periodic whole (single)
-            double* acc = d_codec_[t_sidx];
-            double* wv = acc + 64;
             launch_decode32(S(), T_, x, kd[0], cc[0], slots32_, isc[0], acc);
-            launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
-            if (unpack) launch_encode16(S(), T_, m, wv, slots_p_, enc_scale, nq, true);
-            else launch_encode32(S(), T_, m, wv, slots32_, enc_scale, nq);
+            if (!snap_encode_) launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
+            if (unpack) launch_encode16(S(), T_, m, wv, slots_p_, enc_scale, nq, true, zacc);
+            else launch_encode32(S(), T_, m, wv, slots32_, enc_scale, nq, zacc);
+            if (snap_encode_) codec_flip_[t_sidx] ^= 1;
         } else if (states == 1) {
-            double* acc = d_codec_[t_sidx];
-            double* wv = acc + 64;
             const Slot16& sl = per16 ? slots_p_ : slots_;
             launch_decode16(S(), T_, x, kd, cc, sl, isc, acc);
-            launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
-            launch_encode16(S(), T_, m, wv, sl, enc_scale, nq, per16);
+            if (!snap_encode_) launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
+            launch_encode16(S(), T_, m, wv, sl, enc_scale, nq, per16, zacc);
+            if (snap_encode_) codec_flip_[t_sidx] ^= 1;
         } else {
             double*& zbuf = d_fft_[t_sidx];
             if (!zbuf) zbuf = (double*)dev_alloc((size_t)2 * 2 * 2 * 2 * n);  // 2 buffers x [2][N] complex double
@@ -4524,6 +4527,8 @@ private:
     bool direct32_ = !(std::getenv("AESFHE_RENORM_DIRECT32") && std::atoi(std::getenv("AESFHE_RENORM_DIRECT32")) == 0);
     Slot16 slots_p_ = {};  // the 16-periodic layout's, 5^i
     double* d_codec_[kStreams] = {};
+    int codec_flip_[kStreams] = {};  // which of the stream's two accumulators the next decode uses
+    bool snap_encode_ = !(std::getenv("AESFHE_SNAP_ENCODE") && std::atoi(std::getenv("AESFHE_SNAP_ENCODE")) == 0);
     int* d_nib_[kStreams] = {};
     double* d_fft_[kStreams] = {};  // slot-packed renorm: [2 buffers][2 cts][N] complex double
     u32* d_slot_pos_ = nullptr;     // (5^j mod 2N - 1) / 2 for slot j < N/2

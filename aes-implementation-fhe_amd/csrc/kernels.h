@@ -449,16 +449,20 @@ struct Slot16 {
 };
 // x: [2][4][N] coefficient residues of the two decryptions (kd[c] limbs used);
 // acc[c][i][re|im] += sum_k (m_k / scale_c) e^{i pi e_i k / N}   (acc zeroed by the caller)
-// CONTRACT: acc must be zero on entry, and every decode must be followed by a launch_snap16 on the
-// same accumulator (same stream): k_snap16 reads acc and re-zeroes it for the next decode -- a decode
-// without its snap leaves stale sums that the next renorm would add onto
+// CONTRACT: acc must be zero on entry, and every decode must be followed on the same stream by a
+// launch_snap16 on the same accumulator (it reads acc and re-zeroes it for the next decode) or by a
+// snapping encode whose zacc is the OTHER buffer of a double-buffered pair (the next decode then uses
+// that one) -- a decode without either leaves stale sums that the next renorm would add onto
 void launch_decode16(hipStream_t st, const DevTables& T, const u32* x, const int kd[2], const CrtConsts cc[2], const Slot16& sl,
                      const double inv_scale[2], double* acc);
 // per slot: nibble = round(-angle 16 / 2 pi) mod 16, w = zeta16^nibble - 1 (acc -> w, nib)
 void launch_snap16(hipStream_t st, double* acc, double* w, int* nib);
 // out[c][t][k] = round(scale (delta_{k0} + (2/N) Re sum_i w_ci e^{-i pi e_i k / N})) mod q_t, t < nq
 // periodic: the 16-periodic layout (positions sl.e = 5^i, only k == 0 mod N/32 nonzero)
-void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq, bool periodic = false);
+// zacc (nullable): w is the decode's ACCUMULATOR instead -- the encode snaps it itself (no
+// launch_snap16) and zeroes zacc, the other accumulator of a double-buffered pair (Engine::renorm)
+void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq, bool periodic = false,
+                     double* zacc = nullptr);
 // direct codec of a small-period packed renorm (period 32: the hi | lo halves of the packed XOR
 // stage): acc[i] = the 32 slot values (slot j at 5^j) of ONE decryption (acc zeroed by the
 // caller); launch_snap16 snaps them as 2 x 16; encode32 re-encodes w as ONE 32-periodic message
@@ -468,7 +472,7 @@ struct Slot32 {
 };
 // CONTRACT (as launch_decode16): acc zero on entry, a launch_snap16 on acc must follow on the same stream
 void launch_decode32(hipStream_t st, const DevTables& T, const u32* x, int kd, const CrtConsts& cc, const Slot32& sl, double inv_scale, double* acc);
-void launch_encode32(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot32& sl, double scale, int nq);
+void launch_encode32(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot32& sl, double scale, int nq, double* zacc = nullptr);
 
 // --- slot-packed Zeta16 renorm ----------------------
 // Full canonical-embedding decode / encode on the device in fp64: the slots of a real

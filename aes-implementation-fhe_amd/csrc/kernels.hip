@@ -916,10 +916,33 @@ __global__ void __launch_bounds__(kBlock) k_decode32(const u32* x, int kd, CrtCo
         atomicAdd(acc + threadIdx.x, t);
     }
 }
+// slot t's snap: nibble = round(-angle 16 / 2 pi) mod 16, w = zeta16^nibble - 1
+__device__ __forceinline__ int snap_slot(const double* acc, int t, double& wr, double& wi) {
+    const double ang = atan2(acc[2 * t + 1], acc[2 * t]);
+    const double kf = rint(-ang * 16.0 / (2.0 * M_PI));
+    const int v = (int)((((long)kf) % 16 + 16) % 16);
+    double sn, cs;
+    sincospi(-2.0 * v / 16.0, &sn, &cs);
+    wr = cs - 1.0;
+    wi = sn;
+    return v;
+}
+// SNAP: the encode derives the 32 snapped values itself from the decode's accumulator acc (each
+// block, into LDS: no k_snap16 launch), and block 0 zeroes zacc -- the accumulator the PREVIOUS
+// renorm on this stream used, free since that renorm's encode finished -- for the next decode
+__device__ __forceinline__ const double* snap_block(const double* acc, double* zacc, double* sw) {
+    if (threadIdx.x < 32) snap_slot(acc, threadIdx.x, sw[2 * threadIdx.x], sw[2 * threadIdx.x + 1]);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 64) zacc[threadIdx.x] = 0.0;
+    __syncthreads();
+    return sw;
+}
 // ONE 32-periodic message from its 32 snapped slot deviations w (w_j = zeta^nib - 1): only the
 // coefficients k == 0 mod N/64 are nonzero, m_k = (1/32) sum_j Re(w_j zeta^(-e_j k)) (+1 at k = 0)
-__global__ void __launch_bounds__(kBlock) k_encode32(u32* out, const double* w, Slot32 sl, double scale, int nq, const PrimeConst* pc,
-                                                     int logn) {
+template <bool SNAP>
+__global__ void __launch_bounds__(kBlock) k_encode32(u32* out, const double* w, double* zacc, Slot32 sl, double scale, int nq,
+                                                     const PrimeConst* pc, int logn) {
+    __shared__ double sw[SNAP ? 64 : 1];
+    if (SNAP) w = snap_block(w, zacc, sw);
     const int n = 1 << logn;
     const int k = blockIdx.x * kBlock + threadIdx.x;
     const u32 mask = 2u * n - 1, kmask = (u32)(n / 64) - 1;
@@ -947,22 +970,18 @@ __global__ void __launch_bounds__(kBlock) k_encode32(u32* out, const double* w, 
 __global__ void k_snap16(double* acc, double* w, int* nib) {
     const int t = threadIdx.x;  // 32 = 2 ciphertexts x 16 slots
     if (t >= 32) return;
-    const double ang = atan2(acc[2 * t + 1], acc[2 * t]);
+    nib[t] = snap_slot(acc, t, w[2 * t], w[2 * t + 1]);
     acc[2 * t] = 0.0, acc[2 * t + 1] = 0.0;
-    const double kf = rint(-ang * 16.0 / (2.0 * M_PI));
-    const int v = (int)((((long)kf) % 16 + 16) % 16);
-    nib[t] = v;
-    double sn, cs;
-    sincospi(-2.0 * v / 16.0, &sn, &cs);
-    w[2 * t] = cs - 1.0;
-    w[2 * t + 1] = sn;
 }
 
 // kmask = 0: the reference layout (16 slots deviate from 1; every coefficient, factor 2/N);
 // kmask = N/32 - 1: the 16-periodic layout (slot j == slot j mod 16, sl.e = 5^i): only the
 // coefficients k == 0 mod N/32 are nonzero, m_k = (1/16) sum_i Re(w_i zeta^(-e_i k)) (+1 at k = 0)
-__global__ void __launch_bounds__(kBlock) k_encode16(u32* out, const double* w, Slot16 sl, double scale, int nq, const PrimeConst* pc,
-                                                     int logn, u32 kmask, double fac) {
+template <bool SNAP>
+__global__ void __launch_bounds__(kBlock) k_encode16(u32* out, const double* w, double* zacc, Slot16 sl, double scale, int nq,
+                                                     const PrimeConst* pc, int logn, u32 kmask, double fac) {
+    __shared__ double sw[SNAP ? 64 : 1];
+    if (SNAP) w = snap_block(w, zacc, sw);
     const int c = blockIdx.y;
     const int n = 1 << logn;
     const int k = blockIdx.x * kBlock + threadIdx.x;
@@ -1666,19 +1685,28 @@ void launch_decode32(hipStream_t st, const DevTables& T, const u32* x, int kd, c
     prof_launch(KID_ELEMENTWISE, words((double)kd * (1u << T.logn)), k_decode32, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, x, kd, cc, sl,
                 inv_scale, acc, T.logn);
 }
-void launch_encode32(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot32& sl, double scale, int nq) {
-    prof_launch(KID_ELEMENTWISE, words((double)nq * (1u << T.logn)), k_encode32, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out, w, sl,
-                scale, nq, T.pc, T.logn);
+void launch_encode32(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot32& sl, double scale, int nq, double* zacc) {
+    if (zacc)
+        prof_launch(KID_ELEMENTWISE, words((double)nq * (1u << T.logn)), k_encode32<true>, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out,
+                    w, zacc, sl, scale, nq, T.pc, T.logn);
+    else
+        prof_launch(KID_ELEMENTWISE, words((double)nq * (1u << T.logn)), k_encode32<false>, dim3((1u << T.logn) / kBlock), dim3(kBlock), 0, st, out,
+                    w, zacc, sl, scale, nq, T.pc, T.logn);
 }
 void launch_snap16(hipStream_t st, double* acc, double* w, int* nib) {
     prof_launch(KID_ELEMENTWISE, 0.0, k_snap16, dim3(1), dim3(64), 0, st, acc, w, nib);
 }
-void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq, bool periodic) {
+void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot16& sl, double scale, int nq, bool periodic,
+                     double* zacc) {
     const u32 n = 1u << T.logn;
     const u32 kmask = periodic ? n / 32 - 1 : 0u;
     const double fac = periodic ? 1.0 / 16.0 : 2.0 / n;
-    prof_launch(KID_ELEMENTWISE, words(2.0 * nq * (1u << T.logn)), k_encode16, dim3((1u << T.logn) / kBlock, 2), dim3(kBlock), 0, st, out,
-                w, sl, scale, nq, T.pc, T.logn, kmask, fac);
+    if (zacc)
+        prof_launch(KID_ELEMENTWISE, words(2.0 * nq * (1u << T.logn)), k_encode16<true>, dim3((1u << T.logn) / kBlock, 2), dim3(kBlock), 0, st,
+                    out, w, zacc, sl, scale, nq, T.pc, T.logn, kmask, fac);
+    else
+        prof_launch(KID_ELEMENTWISE, words(2.0 * nq * (1u << T.logn)), k_encode16<false>, dim3((1u << T.logn) / kBlock, 2), dim3(kBlock), 0, st,
+                    out, w, zacc, sl, scale, nq, T.pc, T.logn, kmask, fac);
 }
 
 void launch_decode_twist(hipStream_t st, const DevTables& T, const u32* x, const int kd[2], const CrtConsts cc[2],
