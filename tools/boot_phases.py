@@ -1,4 +1,5 @@
-"""Phase breakdown of the sparse-slot bootstrap (C2's MixColumns final bootstrap: one packed
+"""Phase breakdown of the sparse-slot bootstrap (with per-class HBM rooflines per phase: algorithmic
+bytes over the in-kernel span, and over span + boundary gap) (C2's MixColumns final bootstrap: one packed
 ciphertext, period P = 32): wall time (synchronised) and kernel launches of the bootstrap run up
 to each debug stage (aesfhe_debug_boot_stage_sparse), and the per-phase differences.
 usage: python tools/boot_phases.py [P] > out.json"""
@@ -27,7 +28,7 @@ def main():
     E = ctx.engine
     z = np.exp(2j * np.pi * np.random.default_rng(0).random(P))
     ct = E.intt(ctx.encrypt(np.tile(z, E.slot_count // P)))
-    cum, kcum = {}, {}
+    cum, kcum, rcum = {}, {}, {}
     for code, name in STAGES:
         run = (lambda: E.bootstrap_sparse(ct, P)) if code == 99 else (lambda: E.debug_boot_stage_sparse(ct, code, P))
         run()
@@ -42,14 +43,28 @@ def main():
         E.kernel_stats(reset=True)
         run()
         E.sync()
-        kcum[name] = {k: v["launches"] for k, v in E.kernel_stats(reset=True).items()}
+        gaps = E.kernel_gaps()  # read before kernel_stats(reset) clears them
+        ks = E.kernel_stats(reset=True)
+        kcum[name] = {k: v["launches"] for k, v in ks.items()}
+        # per class: span ms (in-kernel clock, or dispatch events for element-wise kernels), the
+        # boundary gaps accounted to the class, algorithmic bytes
+        rcum[name] = {k: (v["ms"], gaps.get(k, (0, 0.0))[1], v["bytes"]) for k, v in ks.items()}
         E.profile(())
-    out, prev, kprev = {}, (0.0, 0.0), {}
+    out, prev, kprev, rprev = {}, (0.0, 0.0), {}, {}
     for _, name in STAGES:
         ms, ln = cum[name]
         kc = {k: v - kprev.get(k, 0) for k, v in kcum[name].items() if v - kprev.get(k, 0)}
-        out[name] = {"ms": round(ms - prev[0], 3), "launches": ln - prev[1], "cumulative_ms": round(ms, 3), "by_class": kc}
-        prev, kprev = (ms, ln), kcum[name]
+        roof = {}
+        for k, (sp, gp, by) in rcum[name].items():
+            p0 = rprev.get(k, (0.0, 0.0, 0.0))
+            dsp, dgp, dby = sp - p0[0], gp - p0[1], by - p0[2]
+            if dsp > 0 and dby > 0:
+                roof[k] = {"span_ms": round(dsp, 4), "gap_ms": round(dgp, 4), "GB": round(dby / 1e9, 4),
+                           "frac_span": round(dby / (dsp * 1e-3) / 8e12, 3),
+                           "frac": round(dby / ((dsp + dgp) * 1e-3) / 8e12, 3)}
+        out[name] = {"ms": round(ms - prev[0], 3), "launches": ln - prev[1], "cumulative_ms": round(ms, 3), "by_class": kc,
+                     "roofline_by_class": roof}
+        prev, kprev, rprev = (ms, ln), kcum[name], rcum[name]
     print(json.dumps({"period": P, "reps": reps, "phases": out}, indent=1))
 
 
