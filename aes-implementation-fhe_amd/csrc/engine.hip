@@ -3430,7 +3430,8 @@ public:
     // inner product accumulated into acc, the permuted c0 summed into c0sum per member
     // sole: no other giant step of the group is accumulated (lin_group): the fused-core form may run.
     // AESFHE_FUSED_GIANT=1 (off by default): C2's sparse plans never take it (10,360 launches either
-    // way, profiles/r4_ab_giant_convert.txt), so it has no GPU coverage yet
+    // way, profiles/r4_ab_giant_convert.txt); bit-identical on the full-slot and sparse bootstraps
+    // (tests/test_gpu_fused_giant.py)
     bool fused_giant_ = std::getenv("AESFHE_FUSED_GIANT") && std::atoi(std::getenv("AESFHE_FUSED_GIANT")) != 0;
     u32* dh_ys_ = nullptr;  // set by the fused form: the P rows after the INTT row pass, for the ModDown
     void giant_accumulate_many(const Ct& rs, const std::vector<u64>& gals, int nb, u32*& acc, u32*& c0sum, int& count, bool sole = false) {
