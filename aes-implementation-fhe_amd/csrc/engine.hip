@@ -3429,10 +3429,10 @@ public:
     // by X -> X^gals[j]; their c1 ModUp'ed together (chunks within kMaxConvGroups), each key
     // inner product accumulated into acc, the permuted c0 summed into c0sum per member
     // sole: no other giant step of the group is accumulated (lin_group): the fused-core form may run.
-    // AESFHE_FUSED_GIANT=1 (off by default): C2's sparse plans never take it (10,360 launches either
-    // way, profiles/r4_ab_giant_convert.txt); bit-identical on the full-slot and sparse bootstraps
-    // (tests/test_gpu_fused_giant.py)
-    bool fused_giant_ = std::getenv("AESFHE_FUSED_GIANT") && std::atoi(std::getenv("AESFHE_FUSED_GIANT")) != 0;
+    // AESFHE_FUSED_GIANT=0 turns it off: the full-slot bootstrap's groups take it (batch leg 11,551 ->
+    // 11,407 launches per step, 4,984-5,000 -> 5,055-5,056 blocks/s, profiles/r4_ab_giant_batch.txt),
+    // C2's sparse plans do not; bit-identical (tests/test_gpu_fused_giant.py)
+    bool fused_giant_ = !(std::getenv("AESFHE_FUSED_GIANT") && std::atoi(std::getenv("AESFHE_FUSED_GIANT")) == 0);
     u32* dh_ys_ = nullptr;  // set by the fused form: the P rows after the INTT row pass, for the ModDown
     void giant_accumulate_many(const Ct& rs, const std::vector<u64>& gals, int nb, u32*& acc, u32*& c0sum, int& count, bool sole = false) {
         const int K = (int)gals.size(), lv = rs.level, r = hp_.nl(lv), ne2 = r + hp_.n_p, n = hp_.n;
