@@ -182,10 +182,13 @@ public:
         build_tables();
         for (int k = 0; k < kStreams; ++k)
             pools_[k].on_oom = [this, k] {
-                (void)hipDeviceSynchronize();  // queued kernels may still read cached buffers
-                pools_[k].trim();
-                if (!fj_active_)  // no branch thread is allocating: every pool's cache may go
-                    for (int j = 0; j < kStreams; ++j) pools_[j].trim();
+                // queued kernels may still read cached buffers; after the device sync none does.  Every
+                // pool's cache goes, also inside fork/join: API calls serialise on ctx->mu, so no other
+                // thread is allocating, and a branch allocating from pools_[0] must still be able to
+                // reclaim what pools_[1..] hold
+                (void)hipDeviceSynchronize();
+                (void)k;
+                for (int j = 0; j < kStreams; ++j) pools_[j].trim();
             };
     }
     unsigned long long oom_retries() const {
@@ -3298,6 +3301,10 @@ public:
         const bool dh = double_hoist_;
         u32* dh_acc = nullptr;
         u32* dh_c0 = nullptr;
+        // the fused-core form's P rows (after the ModDown INTT's row pass), owned by THIS call: an
+        // exception between giant_accumulate_many and the ModDown below cannot leave it to a later
+        // group (it was Engine-wide state that a later call would have taken as its own)
+        u32* dh_ys = nullptr;
         int dh_n = 0;
         bool continue_giant = false;
         // all giant steps' diagonal sums in one pass per chunk of kLinG giant steps (k_lin_mac):
@@ -3349,7 +3356,7 @@ public:
                 bool sole = g.G <= kLinG && dh_n == 0;
                 for (int j = 0; j < gn && sole; ++j)
                     if (!in_blk[j] && any[j] && dh && g.giant[g0 + j]) sole = false;
-                giant_accumulate_many(rs, gs, nb, dh_acc, dh_c0, dh_n, sole);
+                giant_accumulate_many(rs, gs, nb, dh_acc, dh_c0, dh_n, dh_ys, sole);
                 release(rs);
                 untmp(blk, bj.size() * 2 * (size_t)ne * nb);
             }
@@ -3416,8 +3423,8 @@ public:
                 for (int mb = 0; mb < nb; ++mb) launch_add(S(), T_, dh_c0 + mb * ms, dh_c0 + mb * ms, out.data + mb * ms, r, r, qmap());
                 add1 = out.data + (size_t)r * n;
             }
-            Ct res = moddown(dh_acc, lv, dh_c0, add1, nb, ms, nullptr, nullptr, false, dh_ys_);
-            if (dh_ys_) untmp(dh_ys_, 2 * (size_t)np * nb), dh_ys_ = nullptr;
+            Ct res = moddown(dh_acc, lv, dh_c0, add1, nb, ms, nullptr, nullptr, false, dh_ys);
+            if (dh_ys) untmp(dh_ys, 2 * (size_t)np * nb), dh_ys = nullptr;
             if (have) release(out);
             untmp(dh_acc, 2 * (size_t)ne2 * nb);
             untmp(dh_c0, 2 * (size_t)r * nb);
@@ -3433,8 +3440,9 @@ public:
     // 11,407 launches per step, 4,984-5,000 -> 5,055-5,056 blocks/s, profiles/r4_ab_giant_batch.txt),
     // C2's sparse plans do not; bit-identical (tests/test_gpu_fused_giant.py)
     bool fused_giant_ = !(std::getenv("AESFHE_FUSED_GIANT") && std::atoi(std::getenv("AESFHE_FUSED_GIANT")) == 0);
-    u32* dh_ys_ = nullptr;  // set by the fused form: the P rows after the INTT row pass, for the ModDown
-    void giant_accumulate_many(const Ct& rs, const std::vector<u64>& gals, int nb, u32*& acc, u32*& c0sum, int& count, bool sole = false) {
+    // ys (out): set by the fused form to the P rows after the INTT row pass, for the caller's ModDown
+    void giant_accumulate_many(const Ct& rs, const std::vector<u64>& gals, int nb, u32*& acc, u32*& c0sum, int& count, u32*& ys,
+                               bool sole = false) {
         const int K = (int)gals.size(), lv = rs.level, r = hp_.nl(lv), ne2 = r + hp_.n_p, n = hp_.n;
         const size_t ms = (size_t)2 * r * n;
         if (rs.nb != K * nb || K > kMaxMembers) throw std::runtime_error("giant_accumulate_many: batch shape");
@@ -3446,17 +3454,17 @@ public:
         if (sole && count == 0 && fused_ki_ok() && fused_giant_ && K <= kMaxKiSrc && per >= K) {
             // the group's only accumulation: the K key inner products summed in ONE fused-core launch
             // (multi-source k_ntt2_ki: each step's ModUp row pass in registers, no ext written), the P
-            // rows through the ModDown INTT's row pass into dh_ys_ for lin_group's ModDown
+            // rows through the ModDown INTT's row pass into ys for lin_group's ModDown
             const u32* c1 = perm + (size_t)r * n;
             u32* ext = modup(c1, lv, nb * K, ms, nullptr, false, true);
             const size_t er = (size_t)ext_rows(lv) * n;
             KiSrc src[kMaxKiSrc];
             for (int j = 0; j < K; ++j) src[j] = KiSrc{ext + (size_t)j * nb * er, perm + (size_t)j * nb * ms + (size_t)r * n, ksk(gals[j])};
-            dh_ys_ = tmp(2 * (size_t)hp_.n_p * nb);
-            ki_core(acc, dh_ys_, lv, r, nb, src, K, ms, KsFold{});
+            ys = tmp(2 * (size_t)hp_.n_p * nb);
+            ki_core(acc, ys, lv, r, nb, src, K, ms, KsFold{});
             untmp(ext, (size_t)nb * K * ext_rows(lv));
         }
-        for (int j0 = 0; j0 < K && !dh_ys_; j0 += per) {
+        for (int j0 = 0; j0 < K && !ys; j0 += per) {
             const int k = std::min(per, K - j0);
             const u32* c1 = perm + (size_t)j0 * nb * ms + (size_t)r * n;
             u32* ext = modup(c1, lv, nb * k, ms);

@@ -60,6 +60,7 @@ struct KernelProfiler {
     // launch's kid: a kid's dispatch-inclusive average = its span average + its gap average.
     int pend_slot = -1;
     unsigned long long pend_idx = 0;
+    hipStream_t pend_stream = nullptr;  // a gap pairs two launches of ONE stream only
     double gap_ms[KID_N] = {};
     unsigned long long gap_n[KID_N] = {};
 };
@@ -470,7 +471,9 @@ void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double*
 struct Slot32 {
     u32 e[32];
 };
-// CONTRACT (as launch_decode16): acc zero on entry, a launch_snap16 on acc must follow on the same stream
+// CONTRACT (as launch_decode16): acc zero on entry; the snap follows on the same stream, either inside the
+// snapping encode (the default, AESFHE_SNAP_ENCODE: it reads acc and zeroes the other buffer of its
+// double-buffered pair for the next decode) or as launch_snap16 on acc (AESFHE_SNAP_ENCODE=0)
 void launch_decode32(hipStream_t st, const DevTables& T, const u32* x, int kd, const CrtConsts& cc, const Slot32& sl, double inv_scale, double* acc);
 void launch_encode32(hipStream_t st, const DevTables& T, u32* out, const double* w, const Slot32& sl, double scale, int nq, double* zacc = nullptr);
 

@@ -107,10 +107,14 @@ inline void prof_launch_tsw(int kid, double bytes, double work, F kernel, dim3 g
         // this launch's index in the process's launch order (launch_validate counted it)
         const unsigned long long idx = g_launches.load(std::memory_order_relaxed);
         const bool own = (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0;
-        const bool succ = p->pend_slot >= 0 && idx == p->pend_idx + 1;
+        // the successor of a sampled launch: next in the process's launch order AND on the same stream
+        // (with branch threads or several contexts the next launch may be another stream's, whose
+        // start says nothing about this stream's boundary)
+        const bool succ = p->pend_slot >= 0 && idx == p->pend_idx + 1 && st == p->pend_stream;
         if (own || succ) ts = p->ts_slot(kid, bytes, work, own, succ ? p->pend_slot : -1);
         p->pend_slot = (own && ts) ? (int)((ts - p->d_ts) / KernelProfiler::kTsRec) : -1;
         p->pend_idx = idx;
+        p->pend_stream = st;
     } else if (p && (p->mask >> kid & 1u) && (p->seen[kid]++ % p->every) == 0) {
         // AESFHE_PROF_EVENTS=1: dispatch-stamped events (~3 us longer per timed launch)
         hipEvent_t a = p->get(), b = p->get();

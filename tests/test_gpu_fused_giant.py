@@ -1,5 +1,5 @@
 """Double-hoisted giant steps through the multi-source fused key-switch core (engine.hip
-giant_accumulate_many, AESFHE_FUSED_GIANT=1; off by default): a linear-transform group's rotated
+giant_accumulate_many; on by default, AESFHE_FUSED_GIANT=0 restores the separate path): a linear-transform group's rotated
 giant steps summed in one k_ntt2_ki launch must give the same ciphertext bytes as the separate
 k_key_inner accumulation, on the full-slot bootstrap (the plans with multi-step groups) and the
 sparse one.  The launch counts show whether the fused form ran."""
