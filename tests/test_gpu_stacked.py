@@ -147,3 +147,24 @@ def test_pipeline_pairs_encrypt(ctx, coeff_dir, periodic):
     got = pipe.encoder.decode(*ct)
     want = np.stack([A.ref_encrypt(p, rks) for p in pts])
     assert np.array_equal(got, want), int((got != want).any(axis=1).sum())
+
+
+@pytest.mark.parametrize("P", [16, 19])
+def test_pipeline_many_pairs_encrypt(ctx, coeff_dir, P):
+    """BASELINE config 3's shape at a real stack size (VERDICT r4 'do this' 4): P >= 16 one-state
+    ciphertext pairs stacked through AESPipeline(pairs=P) in the default periodic layout -- more
+    members than one key-switch chunk (ks_chunk <= 8) and, for 19, a ragged last chunk and an odd
+    member for the pair bootstrap's chunks of two -- every pair checked against FIPS-197 AES of its
+    own state (REF/state_encoder.py:17-28: one state per pair)"""
+    from aes_keyschedule import expand_aes128_key, load_all_coeffs
+    from oracle import aes_plain as A
+    from pipeline import AESPipeline
+    pipe = AESPipeline(ctx, load_all_coeffs(coeff_dir), use_hard_renorm_between_steps=True, pairs=P)
+    rks = expand_aes128_key(np.arange(16, dtype=np.uint8) * 11 + 3)
+    pts = np.random.default_rng(1000 + P).integers(0, 256, (P, 16), dtype=np.uint8)
+    ct = pipe.encrypt(pts, rks)
+    assert ctx.engine.members(ct[0]) == P and ctx.engine.members(ct[1]) == P
+    got = pipe.encoder.decode(*ct)
+    want = np.stack([A.ref_encrypt(p, rks) for p in pts])
+    bad = np.flatnonzero((got != want).any(axis=1))
+    assert bad.size == 0, f"pairs {bad.tolist()} differ"
