@@ -1054,6 +1054,268 @@ __global__ void __launch_bounds__(256) k_ntt2_ki(KiArgs a, LimbMap map, const Pr
     }
     ts_end(ts);
 }
+// ---- the fused core at 8 residues per thread (k_ntt2_ki8, AESFHE_KI8; VERDICT r4 "do this" 3)
+// k_ntt2_ki holds 16 residues per thread: 64 VGPRs of 64-bit accumulators, 242 in all, 2 waves /
+// SIMD.  Here a 256-thread block owns 8 rows (32 threads per 256-word row, 8 residues each), so
+// the accumulators take 32 VGPRs and the grid has twice the blocks.  The row pass runs its 8
+// stages in three register phases joined by two LDS exchanges:
+//   A  words t + 32 k      stages 0-2 (partners 4, 2, 1 apart in k)
+//   B  words 32 a + 4 m + b (a = t >> 2, b = t & 3)   stages 3-5 (partners 4, 2, 1 apart in m)
+//   C  words 8 t + m       stages 6-7 (partners 2, 1 apart in m)
+// every stage's butterflies and twiddles (index 2^(LOGR1 + s) + R 2^s + (word >> (8 - s))) are
+// k_ntt2_fwd's / k_ntt2_inv's, so every stored residue is the one the 16-residue kernel stores
+// (the inverse's lazy residues may differ in representative, its column pass ends canonical: the
+// ModDown's output is the same bit for bit; tests/test_gpu_fused_ki.py).
+// LDS swizzles (ds_read_b32 / ds_write_b32 bank = dword mod 32, one 32-lane half = one row):
+//   A <-> B: w ^ (((w >> 5) & 7) << 2)     B <-> C: w ^ ((((w >> 5) & 3) << 3) | ((w >> 5) & 7))
+// both conflict-free for both access patterns of their exchange.
+constexpr int kPitch8 = 256;
+__device__ __forceinline__ int swzAB(int w) { return w ^ (((w >> 5) & 7) << 2); }
+__device__ __forceinline__ int swzBC(int w) { return w ^ ((((w >> 5) & 3) << 3) | ((w >> 5) & 7)); }
+__device__ __forceinline__ int ki8_wordB(int t, int m) { return ((t >> 2) << 5) | (m << 2) | (t & 3); }
+template <int LOGR1>
+__device__ __forceinline__ int ki8_tw(int s, int R, int w) { return (1 << (LOGR1 + s)) + (R << s) + (w >> (8 - s)); }
+// forward: x[k] = word t + 32 k of row R (pass-1 output, [0, 4q)) -> x[m] = word 8 t + m, canonical
+template <int LOGR1>
+__device__ __forceinline__ void ki8_fwd_rows(u32 (&x)[8], u32* row, const uint2* w, int R, int t, u32 q, u32 q2) {
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+        const int h = 4 >> s;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (!(k & h)) {
+                const uint2 tw = w[ki8_tw<LOGR1>(s, R, t + 32 * k)];
+                ct_bfly(x[k], x[k + h], tw.x, tw.y, q2, q);
+            }
+    }
+    __syncthreads();  // the previous user of the LDS row is done reading it
+#pragma unroll
+    for (int k = 0; k < 8; ++k) row[swzAB(t + 32 * k)] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) x[m] = row[swzAB(ki8_wordB(t, m))];
+#pragma unroll
+    for (int s = 3; s < 6; ++s) {
+        const int h = 1 << (5 - s);
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+            if (!(m & h)) {
+                const uint2 tw = w[ki8_tw<LOGR1>(s, R, ki8_wordB(t, m))];
+                ct_bfly(x[m], x[m + h], tw.x, tw.y, q2, q);
+            }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) row[swzBC(ki8_wordB(t, m))] = x[m];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) x[m] = row[swzBC(8 * t + m)];
+#pragma unroll
+    for (int s = 6; s < 8; ++s) {
+        const int h = 1 << (7 - s);
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+            if (!(m & h)) {
+                const uint2 tw = w[ki8_tw<LOGR1>(s, R, 8 * t + m)];
+                ct_bfly(x[m], x[m + h], tw.x, tw.y, q2, q);
+            }
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) x[m] = canon4(x[m], q);
+}
+// inverse: x[m] = word 8 t + m of row R (canonical) -> x[k] = word t + 32 k, [0, 2q) (Gentleman-Sande,
+// stages 7 .. 0)
+template <int LOGR1>
+__device__ __forceinline__ void ki8_inv_rows(u32 (&x)[8], u32* row, const uint2* w, int R, int t, u32 q, u32 q2) {
+    const u32 nq = 0u - q;
+#pragma unroll
+    for (int s = 7; s >= 6; --s) {
+        const int h = 1 << (7 - s);
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+            if (!(m & h)) {
+                const uint2 tw = w[ki8_tw<LOGR1>(s, R, 8 * t + m)];
+                gs_bfly(x[m], x[m + h], tw.x, tw.y, q2, nq);
+            }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) row[swzBC(8 * t + m)] = x[m];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) x[m] = row[swzBC(ki8_wordB(t, m))];
+#pragma unroll
+    for (int s = 5; s >= 3; --s) {
+        const int h = 1 << (5 - s);
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+            if (!(m & h)) {
+                const uint2 tw = w[ki8_tw<LOGR1>(s, R, ki8_wordB(t, m))];
+                gs_bfly(x[m], x[m + h], tw.x, tw.y, q2, nq);
+            }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) row[swzAB(ki8_wordB(t, m))] = x[m];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = row[swzAB(t + 32 * k)];
+#pragma unroll
+    for (int s = 2; s >= 0; --s) {
+        const int h = 4 >> s;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (!(k & h)) {
+                const uint2 tw = w[ki8_tw<LOGR1>(s, R, t + 32 * k)];
+                gs_bfly(x[k], x[k + h], tw.x, tw.y, q2, nq);
+            }
+    }
+}
+__device__ __forceinline__ void ld8(u32 (&e)[8], const u32* p) {
+    const uint4* v = reinterpret_cast<const uint4*>(p);
+    const uint4 a = v[0], b = v[1];
+    e[0] = a.x, e[1] = a.y, e[2] = a.z, e[3] = a.w, e[4] = b.x, e[5] = b.y, e[6] = b.z, e[7] = b.w;
+}
+__device__ __forceinline__ void st8(u32* p, const u32 (&e)[8]) {
+    uint4* v = reinterpret_cast<uint4*>(p);
+    st_out16(v, make_uint4(e[0], e[1], e[2], e[3]));
+    st_out16(v + 1, make_uint4(e[4], e[5], e[6], e[7]));
+}
+// k_ntt2_ki's work with 8 residues per thread (see above); the same arguments, block -> (member,
+// limb, 8-row chunk) with the same XCD grouping of a chunk's members
+template <int LOGR1>
+__global__ void __launch_bounds__(256) k_ntt2_ki8(KiArgs a, LimbMap map, const PrimeConst* pc, const uint2* tw, const uint2* itw,
+                                                  unsigned long long* ts) {
+    constexpr int LOGN = LOGR1 + 8, CH = (1 << LOGR1) / 8;  // 8-row chunks per limb
+    __shared__ u32 sm[8 * kPitch8];
+    const int b = blockIdx.x, nb = a.nb;
+    int m, u;
+    if (((CH * a.ne) & 7) == 0) {
+        const int wv = b >> 3;
+        m = wv % nb;
+        u = (wv / nb) * 8 + (b & 7);
+    } else {
+        m = b % nb;
+        u = b / nb;
+    }
+    const int chunk = u % CH, x = u / CH;
+    ts_begin(ts);
+    const int prime = map.prime(x);
+    const PrimeConst P = pc[prime];
+    const u32 q = P.q, q2 = 2 * q;
+    const int r = threadIdx.x >> 5, t = threadIdx.x & 31, R = chunk * 8 + r;
+    const size_t c0 = (size_t)R * 256 + 8 * t;  // this thread's 8 consecutive coefficients (phase C)
+    u32* row = sm + r * kPitch8;
+    const int krow = x < a.nl ? x : a.nks + (x - a.nl);
+    const int own = x < a.nl ? x / a.alpha : -1;
+    u64 s0[8], s1[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s0[k] = s1[k] = 0;
+    int cnt = 0;
+    for (int src = 0; src < a.nsrc; ++src) {
+        for (int jd = 0; jd < a.nd; ++jd, ++cnt) {
+            if (cnt && (cnt & 7) == 0) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) s0[k] = fold64(s0[k], q, P.r32), s1[k] = fold64(s1[k], q, P.r32);
+            }
+            u32 e[8];
+            const u32* kb = a.key[src] + (((size_t)jd * 2 * a.nkey + krow) << LOGN) + c0;
+            const u32* ka = kb + ((size_t)a.nkey << LOGN);
+            if (jd == own) {  // block-uniform: the digit's own limb comes from the NTT-form input
+                if (a.fold.ta[0]) {  // tensor mode: c2 = a1 (.) b1 of the product, formed here
+                    const size_t at = ((size_t)(a.fold.tnl + x) << LOGN) + c0;
+                    const uint4* pa = reinterpret_cast<const uint4*>(a.fold.ta[m] + at);
+                    const uint4* pb = reinterpret_cast<const uint4*>(a.fold.tb[m] + at);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const uint4 va = pa[i], vb = pb[i];
+                        e[4 * i] = barrett_mul(va.x, vb.x, q, P.mu), e[4 * i + 1] = barrett_mul(va.y, vb.y, q, P.mu);
+                        e[4 * i + 2] = barrett_mul(va.z, vb.z, q, P.mu), e[4 * i + 3] = barrett_mul(va.w, vb.w, q, P.mu);
+                    }
+                } else if (a.fold.rev_d) {  // the conjugation: element v <- word N - 1 - (c0 + v)
+                    const uint4* v = reinterpret_cast<const uint4*>(a.d[src] + m * a.d_ms + ((size_t)x << LOGN) + ((size_t)1 << LOGN) - 8 - c0);
+#pragma unroll
+                    for (int i = 0; i < 2; ++i) {
+                        const uint4 tt = v[i];
+                        e[7 - 4 * i] = tt.x, e[6 - 4 * i] = tt.y, e[5 - 4 * i] = tt.z, e[4 - 4 * i] = tt.w;
+                    }
+                } else {
+                    ld8(e, a.d[src] + m * a.d_ms + ((size_t)x << LOGN) + c0);
+                }
+            } else {
+                const u32* p = a.ext[src] + m * a.ext_ms + (((size_t)jd * a.ne + x) << LOGN) + (size_t)R * 256;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) e[k] = p[t + 32 * k];
+                ki8_fwd_rows<LOGR1>(e, row, tw + ((size_t)prime << LOGN), R, t, q, q2);
+            }
+            const uint4* vkb = reinterpret_cast<const uint4*>(kb);
+            const uint4* vka = reinterpret_cast<const uint4*>(ka);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const uint4 vb = vkb[i], va = vka[i];
+                s0[4 * i] += (u64)e[4 * i] * vb.x, s1[4 * i] += (u64)e[4 * i] * va.x;
+                s0[4 * i + 1] += (u64)e[4 * i + 1] * vb.y, s1[4 * i + 1] += (u64)e[4 * i + 1] * va.y;
+                s0[4 * i + 2] += (u64)e[4 * i + 2] * vb.z, s1[4 * i + 2] += (u64)e[4 * i + 2] * va.z;
+                s0[4 * i + 3] += (u64)e[4 * i + 3] * vb.w, s1[4 * i + 3] += (u64)e[4 * i + 3] * va.w;
+            }
+        }
+    }
+    u32 r0[8], r1[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) r0[k] = reduce64(s0[k], q, P.mu, P.r32), r1[k] = reduce64(s1[k], q, P.mu, P.r32);
+    if (a.fold.gad && x < a.nl) {  // + P (c0, c1) on the Q rows (k_key_inner's fold), four words at a time
+        const u32 gv = a.fold.gad[2 * x], gp = a.fold.gad[2 * x + 1];
+        const bool tens = a.fold.ta[0] != nullptr;
+        const size_t at = tens ? ((size_t)x << LOGN) + c0 : m * a.fold.ms + ((size_t)x << LOGN) + c0;
+        const size_t o1 = (size_t)a.fold.tnl << LOGN;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            u32 f0[4], f1[4];
+            if (tens) {  // tensor mode: c0 = a0 b0, c1 = a0 b1 + a1 b0
+                const uint4 A0 = reinterpret_cast<const uint4*>(a.fold.ta[m] + at)[i], A1 = reinterpret_cast<const uint4*>(a.fold.ta[m] + at + o1)[i];
+                const uint4 B0 = reinterpret_cast<const uint4*>(a.fold.tb[m] + at)[i], B1 = reinterpret_cast<const uint4*>(a.fold.tb[m] + at + o1)[i];
+                const u32 a0[4] = {A0.x, A0.y, A0.z, A0.w}, a1[4] = {A1.x, A1.y, A1.z, A1.w};
+                const u32 b0[4] = {B0.x, B0.y, B0.z, B0.w}, b1[4] = {B1.x, B1.y, B1.z, B1.w};
+#pragma unroll
+                for (int v = 0; v < 4; ++v) {
+                    f0[v] = barrett_mul(a0[v], b0[v], q, P.mu);
+                    f1[v] = add_mod(barrett_mul(a0[v], b1[v], q, P.mu), barrett_mul(a1[v], b0[v], q, P.mu), q);
+                }
+            } else {
+                const uint4 F0 = reinterpret_cast<const uint4*>(a.fold.add0 + at)[i], F1 = reinterpret_cast<const uint4*>(a.fold.add1 + at)[i];
+                f0[0] = F0.x, f0[1] = F0.y, f0[2] = F0.z, f0[3] = F0.w;
+                f1[0] = F1.x, f1[1] = F1.y, f1[2] = F1.z, f1[3] = F1.w;
+            }
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+                r0[4 * i + v] = add_mod(r0[4 * i + v], shoup_mul(f0[v], gv, gp, q), q);
+                r1[4 * i + v] = add_mod(r1[4 * i + v], shoup_mul(f1[v], gv, gp, q), q);
+            }
+        }
+    }
+    if (x < a.kept) {  // kept rows: the ModDown finish's cur operand, acc layout [m][2][ne]
+        st8(a.acc + m * a.acc_ms + ((size_t)x << LOGN) + c0, r0);
+        st8(a.acc + m * a.acc_ms + ((size_t)(a.ne + x) << LOGN) + c0, r1);
+    } else {  // converted rows: the ModDown's inverse row pass, into its pass-1 input ys [m][2][ys_rows]
+        const uint2* iw = itw + ((size_t)prime << LOGN);
+        ki8_inv_rows<LOGR1>(r0, row, iw, R, t, q, q2);
+        u32* y0 = a.ys + m * a.ys_ms + ((size_t)(x - a.kept) << LOGN) + (size_t)R * 256;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) y0[t + 32 * k] = r0[k];
+        ki8_inv_rows<LOGR1>(r1, row, iw, R, t, q, q2);
+        u32* y1 = a.ys + m * a.ys_ms + ((size_t)(a.ys_rows + x - a.kept) << LOGN) + (size_t)R * 256;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) y1[t + 32 * k] = r1[k];
+    }
+    ts_end(ts);
+}
+inline bool ki8_on() {
+    static const bool v = [] {
+        const char* e = std::getenv("AESFHE_KI8");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return v;
+}
 inline bool ki_pf() {
     static const bool v = [] {
         const char* e = std::getenv("AESFHE_KI_PF");
@@ -1074,6 +1336,11 @@ void ki_launch(hipStream_t st, const DevTables& Tb, const KiArgs& a, LimbMap map
                          (a.fold.gad ? (a.fold.ta[0] ? 4.0 : 2.0) * a.nl : 0.0);
     const double bytes = row * (a.nb * per_m + a.nsrc * 2.0 * a.nd * a.ne);
     const double bfly = 128.0 * (1 << LOGR1) * 8.0 * (a.nb * (a.nsrc * (double)ext_rows + 2.0 * (a.ne - a.kept)));
+    if (ki8_on()) {
+        prof_launch_tsw(KID_KEY_INNER, bytes, bfly, k_ntt2_ki8<LOGR1>, dim3(2 * CH * a.ne * a.nb), dim3(256), 0, st, a, map, Tb.pc, Tb.tw,
+                        Tb.itw);
+        return;
+    }
     const dim3 grid(CH * a.ne * a.nb);
 #define KI_GO(F, PF) prof_launch_tsw(KID_KEY_INNER, bytes, bfly, k_ntt2_ki<LOGR1, F, PF>, grid, dim3(256), 0, st, a, map, Tb.pc, Tb.tw, Tb.itw, Tb.irow, Tb.igam)
     if (inv_fact_on()) {

@@ -230,9 +230,10 @@ class Ciphertext(_Handle):
 
 
 class Plaintext(_Handle):
-    """Encoded slot vector; encoded at the level of the ciphertext it meets."""
+    """Encoded slot vector; encoded at the level of the ciphertext it meets.  `const`: the value
+    of a constant vector (every slot equal; deferred_calls folds it into LUT coefficients)"""
 
-    __slots__ = ()
+    __slots__ = ("const",)
 
 
 class LookupTable(_Handle):
@@ -294,7 +295,7 @@ class Engine:
     def __init__(self, *, mode: str = "gpu", use_bootstrap: bool = False, use_multiparty: bool = False,
                  thread_count: int = 0, device_id: int = 0, max_level: int = 17, log_n: int = 16,
                  dnum: int | None = None, seed: int | None = None, lazy: bool = True, concurrent: bool = False,
-                 allow_insecure: bool = False, enc_nonce: int | None = None):
+                 allow_insecure: bool = False, enc_nonce: int | None = None, defer_calls: bool | None = None):
         if use_multiparty:
             raise ValueError("multiparty key generation is not supported")
         self.mode = mode
@@ -352,6 +353,12 @@ class Engine:
         self.concurrent = (bool(concurrent) or env.get("AESFHE_CONCURRENT") == "1") and not self._serial
         self._pool = None
         self._tls = threading.local()
+        # deferred call sequences (deferred_calls.py): products / constant products /
+        # sums fused into LUT kernels, rotations and conjugations batched; AESFHE_DEFER_CALLS=0 = off
+        if defer_calls is None:
+            defer_calls = env.get("AESFHE_DEFER_CALLS", "1") != "0"
+        self.defer = bool(defer_calls)
+        self._defer_luts = {}
 
     # ------------------------------------------------------------------ concurrency
     def _executor(self):
@@ -450,7 +457,9 @@ class Engine:
     # ------------------------------------------------------------------ codec
     def encode(self, vec) -> Plaintext:
         re, im = _complex_vec(vec, self.slot_count)
-        return self._new(self._lib.aesfhe_plaintext, re, im, self.slot_count, cls=Plaintext)
+        p = self._new(self._lib.aesfhe_plaintext, re, im, self.slot_count, cls=Plaintext)
+        p.const = complex(re[0], im[0]) if (re == re[0]).all() and (im == im[0]).all() else None
+        return p
 
     def encrypt(self, data, pk=None) -> Ciphertext:
         self._ensure_keys()
@@ -464,7 +473,32 @@ class Engine:
         return re + 1j * im
 
     # ------------------------------------------------------------------ arithmetic
+    # With defer_calls (the default) products, constant products, sums involving them, rotations
+    # and conjugations come back as deferred ciphertexts (deferred_calls.py): the work is issued
+    # when a result is needed, fused / batched.  The _raw_* forms are the undeferred calls.
+    @staticmethod
+    def _settled(x):
+        """a deferred operand that was already resolved acts as its result"""
+        r = getattr(x, "_res", None)
+        return r if r is not None else x
+
     def add(self, a, b):
+        if self.defer:
+            from deferred_calls import Deferred, TermSum, constant_of
+            a, b = self._settled(a), self._settled(b)
+            if isinstance(a, TermSum) and not isinstance(b, Ciphertext):
+                c = constant_of(b)
+                if c is not None:
+                    return TermSum(self, a.c0 + c, a.bil, a.lin)
+            if isinstance(b, Ciphertext) and (isinstance(a, Deferred) or isinstance(b, Deferred)):
+                if isinstance(a, TermSum):
+                    return a.plus(b)
+                if isinstance(b, TermSum):
+                    return b.plus(a)
+                return TermSum(self, 0j, (), [(a, 1.0 + 0j, []), (b, 1.0 + 0j, [])])
+        return self._raw_add(a, b)
+
+    def _raw_add(self, a, b):
         if isinstance(b, Ciphertext):
             return self._new(self._lib.aesfhe_add, a.handle, b.handle)
         if isinstance(b, Plaintext):
@@ -472,29 +506,112 @@ class Engine:
         if isinstance(b, numbers.Number):
             v = complex(b)
             return self._new(self._lib.aesfhe_add_scalar, a.handle, v.real, v.imag)
-        return self.add(a, self.encode(b))
+        return self._raw_add(a, self.encode(b))
 
     def subtract(self, a, b):
+        if self.defer and isinstance(b, Ciphertext):
+            from deferred_calls import Deferred, TermSum
+            a, b = self._settled(a), self._settled(b)
+            if isinstance(a, Deferred) or isinstance(b, Deferred):
+                if isinstance(a, TermSum):
+                    return a.plus(b, -1.0)
+                neg = b.scaled(-1.0, -1.0) if isinstance(b, TermSum) else TermSum(self, 0j, (), [(b, -1.0 + 0j, [-1.0])])
+                return neg.plus(a)
         if isinstance(b, Ciphertext):
-            return self._new(self._lib.aesfhe_sub, a.handle, b.handle)
+            return self._raw_sub(a, b)
         if isinstance(b, numbers.Number):
             return self.add(a, -complex(b))
         return self.add(a, self.encode(-np.asarray(b, dtype=np.complex128)))
+
+    def _raw_sub(self, a, b):
+        return self._new(self._lib.aesfhe_sub, a.handle, b.handle)
 
     def add_plain(self, ct, val):
         return self.add(ct, complex(val) if np.isscalar(val) else val)
 
     def multiply(self, a, b, relinearization_key=None):
-        if isinstance(a, Ciphertext) and isinstance(b, Ciphertext):
-            return self._new(self._lib.aesfhe_mul, a.handle, b.handle, 1 if relinearization_key is not None else 0)
         if isinstance(a, (Plaintext, numbers.Number)) and isinstance(b, Ciphertext):
             a, b = b, a
+        if self.defer and isinstance(a, Ciphertext):
+            from deferred_calls import TermSum, constant_of
+            a, b = self._settled(a), self._settled(b)
+            if isinstance(b, Ciphertext):
+                if relinearization_key is not None:
+                    return TermSum(self, 0j, [(a, b, 1.0 + 0j, [])])
+            else:
+                c = constant_of(b)
+                if c is not None:
+                    if isinstance(a, TermSum):
+                        return a.scaled(b, c)
+                    return TermSum(self, 0j, (), [(a, c, [b])])
+        return self._raw_mul(a, b, relinearization_key is not None)
+
+    def _raw_mul(self, a, b, relin: bool = True):
+        if isinstance(a, Ciphertext) and isinstance(b, Ciphertext):
+            return self._new(self._lib.aesfhe_mul, a.handle, b.handle, 1 if relin else 0)
         if isinstance(b, Plaintext):
             return self._new(self._lib.aesfhe_mul_pt, a.handle, b.handle)
         if isinstance(b, numbers.Number):
             v = complex(b)
             return self._new(self._lib.aesfhe_mul_scalar, a.handle, v.real, v.imag)
-        return self.multiply(a, self.encode(b))
+        return self._raw_mul(a, self.encode(b))
+
+    # -- the deferred-call machinery's entry points (deferred_calls.py)
+    def _raw(self, op, *args):
+        if op == "add":
+            return self._raw_add(*args)
+        if op == "add_scalar":
+            return self._raw_add(args[0], complex(args[1]))
+        if op == "mul":
+            return self._raw_mul(args[0], args[1], True)
+        if op == "mul_by":
+            return self._raw_mul(args[0], args[1])
+        if op == "mul_many":
+            return self.multiply_many(args[0])
+        raise ValueError(op)
+
+    def _raw_lut(self, C, fa, fb, c0=0j):
+        """one fused LUT over the factors (bivariate: C[p, q] fa[p] fb[q]; univariate: c0 + C[k] fa[k]),
+        the coefficient set created once per content"""
+        from deferred_calls import lut_key
+        key = lut_key(C, c0)
+        t = self._defer_luts.get(key)
+        if t is None:
+            if len(self._defer_luts) >= 4096:  # bounded: call sites with ever-new coefficients
+                for old in self._defer_luts.values():
+                    self.lut_free(old)
+                self._defer_luts.clear()
+            t = self._defer_luts[key] = self.lut_create(C, c0)
+        return self.lut_eval(t, fa, fb)
+
+    def _gal_pending(self):
+        lst = getattr(self._tls, "gal", None)
+        if lst is None:
+            lst = self._tls.gal = []
+        return lst
+
+    def _flush_gal(self, target):
+        """resolve every live pending rotation / conjugation of this thread: one galois_multi
+        (a lone one: its own undeferred call); returns target's result"""
+        from deferred_calls import real
+        lst = self._gal_pending()
+        live = [g for g in (w() for w in lst) if g is not None and g._res is None]
+        lst.clear()
+        if target is not None and target not in live:
+            live.append(target)
+        if not live:
+            return None
+        if len(live) == 1:
+            outs = [live[0].raw()]
+        else:
+            outs = self.galois_multi([(real(g.src), g.g) for g in live])
+        res = None
+        for g, o in zip(live, outs):
+            g._res = o
+            g._release_operands()
+            if g is target:
+                res = o
+        return res
 
     def relinearize(self, ct, relinearization_key=None):
         return self._new(self._lib.aesfhe_relinearize, ct.handle)
@@ -511,6 +628,9 @@ class Engine:
         return [Ciphertext(self._ctx, out[i]) for i in range(int(degree))]
 
     def conjugate(self, ct, conjugation_key=None):
+        if self.defer:
+            from deferred_calls import GalPending
+            return GalPending(self, ct, self.galois_conj, lambda: self._new(self._lib.aesfhe_conjugate, ct.handle))
         return self._new(self._lib.aesfhe_conjugate, ct.handle)
 
     # batched variants (include/aesfhe.h): results equal the separate calls
@@ -586,6 +706,10 @@ class Engine:
 
     def rotate(self, ct, rotation_key=None, delta: int = 0):
         """np.roll(slots, delta)."""
+        if self.defer and int(delta) % self.slot_count:
+            from deferred_calls import GalPending
+            d = int(delta)
+            return GalPending(self, ct, self.galois_rotate(d), lambda: self._new(self._lib.aesfhe_rotate, ct.handle, d))
         return self._new(self._lib.aesfhe_rotate, ct.handle, int(delta))
 
     def bootstrap(self, ct, relinearization_key=None, conjugation_key=None, bootstrap_key=None):

@@ -51,6 +51,9 @@ def parse():
                     help="the per-primitive drop-in leg (VERDICT r3 item 7): C2 through EngineContext with REF's own call "
                          "sequence -- eager relinearise/rescale after every product, per-term LUT product loops (no fused "
                          "LUT kernels), the reference slot layout with full-slot bootstraps; 0 = skip")
+    ap.add_argument("--deferred-steps", type=int, default=1,
+                    help="REF's own call sequence through EngineContext (per-term LUT loops, reference slot layout) with the "
+                         "engine's default deferred evaluation (VERDICT r4 item 6); 0 = skip")
     ap.add_argument("--profile-all", action="store_true", help="time every kernel id (diagnostic; slower)")
     ap.add_argument("--profile-every", type=int, default=32,
                     help="time one launch in N of the roofline kernels (live sample over the timed region)")
@@ -534,19 +537,22 @@ def run_true_fhe(ctx, coeffs, rks, args, rank, world, dist, tj: dict) -> dict:
             "precision": measure_precision(pipe, ctx, rks, sts[0], "one state, true-FHE") if rank == 0 else None}
 
 
-def run_eager(coeffs, rks, args, rank, world, dist, local, seed, tj: dict) -> dict:
-    """The per-primitive drop-in path: C2 through a SEPARATE EngineContext that
-    issues the reference's own call sequence -- every ct x ct product relinearised and rescaled at
-    once (lazy=False, REF/engine_context.py:65-68), every LUT as REF's per-term product loop
-    (fused_luts=False: REF/xor4_lut.py:71-73, REF/sub_bytes_lut.py:66-71), the reference slot
-    layout (byte i at slot i*N/32) with full-slot bootstraps (REF/mixcol_final.py:158-162).  The
-    throughput a caller gets by swapping the import line and changing nothing else."""
+def run_ref_calls(coeffs, rks, args, rank, world, dist, local, seed, tj: dict, lazy: bool) -> dict:
+    """The per-primitive drop-in path: C2 through a SEPARATE EngineContext that issues the
+    reference's own call sequence -- every LUT as REF's per-term product loop (fused_luts=False:
+    REF/xor4_lut.py:71-73, REF/sub_bytes_lut.py:66-71, REF/mixcol_final.py:80-91), the reference
+    slot layout (byte i at slot i*N/32) with full-slot bootstraps (REF/mixcol_final.py:158-162).
+    lazy=False: every ct x ct product relinearised and rescaled at once (REF/engine_context.py:65-68,
+    VERDICT r3 item 7); lazy=True: the engine's default deferred evaluation under the
+    same calls.  The throughput a caller gets by swapping the import line and
+    changing nothing else."""
     from engine_context import EngineContext
     from oracle import aes_plain  # checker only, after the timed region
     from pipeline import AESPipeline
-    ctx = EngineContext(signature=1, max_level=17, thread_count=1, device_id=local, seed=seed, lazy=False, fused_luts=False)
+    ctx = EngineContext(signature=1, max_level=17, thread_count=1, device_id=local, seed=seed, lazy=lazy, fused_luts=False)
     pipe = AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=True, periodic=False)
-    sts = rank_states(rank + 3000, 1 + args.eager_steps)
+    steps = args.deferred_steps if lazy else args.eager_steps
+    sts = rank_states(rank + (4000 if lazy else 3000), 1 + steps)
     E = ctx.engine
     pipe.encrypt(sts[0], rks)  # warmup: plaintext constants of the per-term loops
     E.sync()
@@ -565,14 +571,15 @@ def run_eager(coeffs, rks, args, rank, world, dist, local, seed, tj: dict) -> di
     elapsed = max_over_ranks(dist, elapsed)
     ok = all(np.array_equal(pipe.encoder.decode(*o), aes_plain.ref_encrypt(s, rks)) for s, o in zip(sts[1:], outs))
     ok = all(r[0] for r in all_gather_ints(dist, [int(ok)]))
-    done = args.eager_steps * world
-    out = {"workload": "C2 through EngineContext with the reference's call sequence: eager relinearise + rescale per "
-                       "product, per-term LUT product loops, reference slot layout, full-slot bootstraps",
-           "rounds_per_s": 10.0 * done / elapsed, "ms_per_step": elapsed / args.eager_steps * 1e3,
-           "steps": args.eager_steps, "verified_against_plaintext_model": bool(ok),
-           "op_counts_per_round": {k: v / (10.0 * args.eager_steps) for k, v in counters.items()},
-           "launches_per_encrypt": (leg.l1 - leg.l0) / args.eager_steps,
-           "roofline_step": leg.step(elapsed, args.eager_steps, tj, args.profile_every)}
+    done = steps * world
+    out = {"workload": "C2 through EngineContext with the reference's call sequence: per-term LUT product loops, reference "
+                       "slot layout, full-slot bootstraps, " + ("deferred relinearise/rescale (engine default)" if lazy else
+                                                                "eager relinearise + rescale per product"),
+           "rounds_per_s": 10.0 * done / elapsed, "ms_per_step": elapsed / steps * 1e3,
+           "steps": steps, "verified_against_plaintext_model": bool(ok),
+           "op_counts_per_round": {k: v / (10.0 * steps) for k, v in counters.items()},
+           "launches_per_encrypt": (leg.l1 - leg.l0) / steps,
+           "roofline_step": leg.step(elapsed, steps, tj, args.profile_every)}
     del pipe, ctx
     return out
 
@@ -897,7 +904,8 @@ def main():
     true_fhe = (run_true_fhe(ctx, coeffs, rks, args, rank, world, dist, tj)
                 if args.true_fhe_steps > 0 and not args.no_final_bootstrap else None)
     E.profile(())
-    eager = run_eager(coeffs, rks, args, rank, world, dist, local, seed, tj) if args.eager_steps > 0 else None
+    eager = run_ref_calls(coeffs, rks, args, rank, world, dist, local, seed, tj, lazy=False) if args.eager_steps > 0 else None
+    deferred = run_ref_calls(coeffs, rks, args, rank, world, dist, local, seed, tj, lazy=True) if args.deferred_steps > 0 else None
 
     # correctness of the timed outputs (outside the timed region)
     ok = all(np.array_equal(pipe.encoder.decode(*o), aes_plain.ref_encrypt(states[args.warmup + j], rks))
@@ -963,6 +971,8 @@ def main():
         line["true_fhe"] = true_fhe
     if eager is not None:
         line["eager_ref_calls"] = eager
+    if deferred is not None:
+        line["deferred_ref_calls"] = deferred
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline(coeffs)

@@ -23,7 +23,7 @@ O=gpurun_out/${1:?out dir}
 shift
 mkdir -p $O
 export TMPDIR=/tmp
-C2="--no-cpu-baseline --batch-states 0 --true-fhe-steps 0 --pair-states 0 --packed-pairs 0 --eager-steps 0"
+C2="--no-cpu-baseline --batch-states 0 --true-fhe-steps 0 --pair-states 0 --packed-pairs 0 --eager-steps 0 --deferred-steps 0"
 for t in "$@"; do
   echo "[gpu_task] $t $(date +%T)"
   case $t in
@@ -60,7 +60,7 @@ for t in "$@"; do
     twogpu)
       AESFHE_DIST_BACKEND=gloo timeout -k 10 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr=127.0.0.1 \
           --master-port=29517 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline --batch-states 1024 --c5-states 256 \
-          --pair-states 0 --packed-pairs 0 --true-fhe-steps 0 --eager-steps 0 > $O/bench_2rank_1gpu.json 2> $O/twogpu.err ;;
+          --pair-states 0 --packed-pairs 0 --true-fhe-steps 0 --eager-steps 0 --deferred-steps 0 > $O/bench_2rank_1gpu.json 2> $O/twogpu.err ;;
     boot)
       timeout -k 10 300 python3 tools/boot_phases.py 32 > $O/boot_phases.json 2> $O/boot.err ;;
     census)
