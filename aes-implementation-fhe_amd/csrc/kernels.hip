@@ -1454,6 +1454,11 @@ inline int xcd_rows_on() {
     }();
     return v;
 }
+// AESFHE_LIN_MAC_NB4=1: a four-member chunk in one launch (A/B; off: see launch_lin_mac)
+inline bool lin_mac_nb4() {
+    static const bool v = std::getenv("AESFHE_LIN_MAC_NB4") && std::atoi(std::getenv("AESFHE_LIN_MAC_NB4")) != 0;
+    return v;
+}
 template <int NB>
 void launch_lin_mac_nb(hipStream_t st, const DevTables& T, const LinMacArgs& m, int nl, int ne, LimbMap map, double bytes) {
     static_assert(kBlock == 256, "xcd_rows assumes N / 256 column blocks");
@@ -1503,6 +1508,13 @@ void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int
         launch_lin_mac_nb<1>(st, T, m, nl, ne, map, bytes);
     } else if (m.nb == 2) {
         launch_lin_mac_nb<2>(st, T, m, nl, ne, map, bytes);
+    } else if (m.nb == 4 && lin_mac_nb4()) {
+        // a stacked bootstrap chunk of four members in ONE launch (AESFHE_LIN_MAC_NB4=1, off): each
+        // key and diagonal residue read once for all four -- but the baby steps' gathers of c0 and
+        // the hoisted ext rows of four members (~6 MB per row band) no longer fit one XCD's 4 MB L2:
+        // 2,846 us per launch against 2 x 435 us as two pair launches (64-pair stack,
+        // profiles/r5_linmac_nb4_ab.txt)
+        launch_lin_mac_nb<4>(st, T, m, nl, ne, map, bytes);
     } else if (m.nb > 2) {
         // wider batches (a stacked bootstrap chunk of more than two members): pairs of members, one
         // launch each, every member-strided operand offset to the pair's first member

@@ -68,6 +68,147 @@ __device__ __forceinline__ void gs_bfly2(u32& a, u32& b, uint2 g, uint2 r, u32 q
 }
 __device__ __forceinline__ int swz(int w) { return w ^ ((w >> 4) & 15); }
 
+// ---- the fused core at 8 residues per thread (k_ntt2_ki8, AESFHE_KI8; VERDICT r4 "do this" 3)
+// k_ntt2_ki holds 16 residues per thread: 64 VGPRs of 64-bit accumulators, 242 in all, 2 waves /
+// SIMD.  Here a 256-thread block owns 8 rows (32 threads per 256-word row, 8 residues each), so
+// the accumulators take 32 VGPRs and the grid has twice the blocks.  The row pass runs its 8
+// stages in three register phases joined by two LDS exchanges:
+//   A  words t + 32 k      stages 0-2 (partners 4, 2, 1 apart in k)
+//   B  words 32 a + 4 m + b (a = t >> 2, b = t & 3)   stages 3-5 (partners 4, 2, 1 apart in m)
+//   C  words 8 t + m       stages 6-7 (partners 2, 1 apart in m)
+// every stage's butterflies and twiddles (index 2^(LOGR1 + s) + R 2^s + (word >> (8 - s))) are
+// k_ntt2_fwd's / k_ntt2_inv's, so every stored residue is the one the 16-residue kernel stores
+// (the inverse's lazy residues may differ in representative, its column pass ends canonical: the
+// ModDown's output is the same bit for bit; tests/test_gpu_fused_ki.py).
+// LDS swizzles (ds_read_b32 / ds_write_b32 bank = dword mod 32, one 32-lane half = one row):
+//   A <-> B: w ^ (((w >> 5) & 7) << 2)     B <-> C: w ^ ((((w >> 5) & 3) << 3) | ((w >> 5) & 7))
+// both conflict-free for both access patterns of their exchange.
+constexpr int kPitch8 = 256;
+__device__ __forceinline__ int swzAB(int w) { return w ^ (((w >> 5) & 7) << 2); }
+__device__ __forceinline__ int swzBC(int w) { return w ^ ((((w >> 5) & 3) << 3) | ((w >> 5) & 7)); }
+__device__ __forceinline__ int ki8_wordB(int t, int m) { return ((t >> 2) << 5) | (m << 2) | (t & 3); }
+template <int LOGR1>
+__device__ __forceinline__ int ki8_tw(int s, int R, int w) { return (1 << (LOGR1 + s)) + (R << s) + (w >> (8 - s)); }
+// forward: x[k] = word t + 32 k of row R (pass-1 output, [0, 4q)) -> x[m] = word 8 t + m, canonical
+template <int LOGR1>
+__device__ __forceinline__ void ki8_fwd_rows(u32 (&x)[8], u32* row, const uint2* w, int R, int t, u32 q, u32 q2) {
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+        const int h = 4 >> s;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (!(k & h)) {
+                const uint2 tw = w[ki8_tw<LOGR1>(s, R, t + 32 * k)];
+                ct_bfly(x[k], x[k + h], tw.x, tw.y, q2, q);
+            }
+    }
+    __syncthreads();  // the previous user of the LDS row is done reading it
+#pragma unroll
+    for (int k = 0; k < 8; ++k) row[swzAB(t + 32 * k)] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) x[m] = row[swzAB(ki8_wordB(t, m))];
+#pragma unroll
+    for (int s = 3; s < 6; ++s) {
+        const int h = 1 << (5 - s);
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+            if (!(m & h)) {
+                const uint2 tw = w[ki8_tw<LOGR1>(s, R, ki8_wordB(t, m))];
+                ct_bfly(x[m], x[m + h], tw.x, tw.y, q2, q);
+            }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) row[swzBC(ki8_wordB(t, m))] = x[m];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) x[m] = row[swzBC(8 * t + m)];
+#pragma unroll
+    for (int s = 6; s < 8; ++s) {
+        const int h = 1 << (7 - s);
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+            if (!(m & h)) {
+                const uint2 tw = w[ki8_tw<LOGR1>(s, R, 8 * t + m)];
+                ct_bfly(x[m], x[m + h], tw.x, tw.y, q2, q);
+            }
+    }
+#pragma unroll
+    for (int m = 0; m < 8; ++m) x[m] = canon4(x[m], q);
+}
+// inverse: x[m] = word 8 t + m of row R ([0, 2q)) -> x[k] = word t + 32 k, [0, 2q) (Gentleman-Sande,
+// stages 7 .. 0).  FACT: stages 7-5 take their twiddle as (row factor rowf[s - 5]) x (shared factor
+// gam[2^s + (word >> (8 - s))]), k_ntt2_inv's factored form
+template <int LOGR1, bool FACT>
+__device__ __forceinline__ void ki8_inv_rows(u32 (&x)[8], u32* row, const uint2* w, const uint2* rowf, const uint2* gam, int R, int t,
+                                             u32 q, u32 q2) {
+    const u32 nq = 0u - q;
+#pragma unroll
+    for (int s = 7; s >= 6; --s) {
+        const int h = 1 << (7 - s);
+        const uint2 rf = FACT ? rowf[s - 5] : make_uint2(0, 0);
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+            if (!(m & h)) {
+                const int wd = 8 * t + m;
+                if (FACT) {
+                    gs_bfly2(x[m], x[m + h], gam[(1 << s) + (wd >> (8 - s))], rf, q2, nq);
+                } else {
+                    const uint2 tw = w[ki8_tw<LOGR1>(s, R, wd)];
+                    gs_bfly(x[m], x[m + h], tw.x, tw.y, q2, nq);
+                }
+            }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) row[swzBC(8 * t + m)] = x[m];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) x[m] = row[swzBC(ki8_wordB(t, m))];
+#pragma unroll
+    for (int s = 5; s >= 3; --s) {
+        const int h = 1 << (5 - s);
+#pragma unroll
+        for (int m = 0; m < 8; ++m)
+            if (!(m & h)) {
+                const int wd = ki8_wordB(t, m);
+                if (FACT && s == 5) {
+                    gs_bfly2(x[m], x[m + h], gam[(1 << s) + (wd >> (8 - s))], rowf[0], q2, nq);
+                } else {
+                    const uint2 tw = w[ki8_tw<LOGR1>(s, R, wd)];
+                    gs_bfly(x[m], x[m + h], tw.x, tw.y, q2, nq);
+                }
+            }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; ++m) row[swzAB(ki8_wordB(t, m))] = x[m];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = row[swzAB(t + 32 * k)];
+#pragma unroll
+    for (int s = 2; s >= 0; --s) {
+        const int h = 4 >> s;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (!(k & h)) {
+                const uint2 tw = w[ki8_tw<LOGR1>(s, R, t + 32 * k)];
+                gs_bfly(x[k], x[k + h], tw.x, tw.y, q2, nq);
+            }
+    }
+}
+__device__ __forceinline__ void ld8(u32 (&e)[8], const u32* p) {
+    const uint4* v = reinterpret_cast<const uint4*>(p);
+    const uint4 a = v[0], b = v[1];
+    e[0] = a.x, e[1] = a.y, e[2] = a.z, e[3] = a.w, e[4] = b.x, e[5] = b.y, e[6] = b.z, e[7] = b.w;
+}
+__device__ __forceinline__ void st8(u32* p, const u32 (&e)[8]) {
+    uint4* v = reinterpret_cast<uint4*>(p);
+    st_out16(v, make_uint4(e[0], e[1], e[2], e[3]));
+    st_out16(v + 1, make_uint4(e[4], e[5], e[6], e[7]));
+}
+
 enum { kPlain = 0, kSpread = 1, kFinish = 1, kSpread2 = 2 };
 
 // rows below which a launch of 512-thread blocks (8 per row) leaves CUs idle: half-size
@@ -546,6 +687,59 @@ __global__ void __launch_bounds__(NT) k_ntt2_inv(u32* dst, const u32* src, RowMa
     ts_end(ts);
 }
 
+// the inverse row pass at 8 residues per thread (AESFHE_NTT_INV8, default on): 256-thread blocks of
+// 8 rows (twice k_ntt2_inv's blocks per launch, ~half the serial work per thread) through
+// ki8_inv_rows -- the same butterflies and twiddles, so the column pass that follows ends on the
+// same canonical residues (bit-identical transforms); IN as k_ntt2_inv (0 plain, 1 product on load,
+// 2 reversed read)
+template <int LOGR1, bool FACT, int IN>
+__global__ void __launch_bounds__(256) k_ntt2_inv8(u32* dst, const u32* src, RowMap rm, LimbMap map, const PrimeConst* pc,
+                                                   const uint2* tw, const uint2* irow, const uint2* igam, TensorPtrs tp,
+                                                   unsigned long long* ts) {
+    constexpr int LOGN = LOGR1 + 8;
+    __shared__ u32 sm[8 * kPitch8];
+    if (skipped(rm)) return;
+    ts_begin(ts);
+    const RowAddr ra = row_addr<LOGN>(dst, src, rm, map);
+    const u32 q = pc[ra.prime].q, q2 = 2 * q;
+    const int r = threadIdx.x >> 5, t = threadIdx.x & 31;
+    const int R = blockIdx.x * 8 + r;
+    u32 x[8];
+    if (IN == 2) {  // element e of row R <- word N - 1 - (256 R + 8 t + e) = row R1 - 1 - R, word 255 - 8 t - e
+        const uint4* in = reinterpret_cast<const uint4*>(ra.src + (size_t)((1 << LOGR1) - 1 - R) * 256 + 248 - 8 * t);
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            const uint4 a = in[v];
+            x[7 - 4 * v] = a.x, x[6 - 4 * v] = a.y, x[5 - 4 * v] = a.z, x[4 - 4 * v] = a.w;
+        }
+    } else if (IN == 1) {
+        const u32 mu = pc[ra.prime].mu;
+        const size_t off = ((size_t)blockIdx.y << LOGN) + (size_t)R * 256 + 8 * t;
+        const uint4* pa = reinterpret_cast<const uint4*>(tp.a[blockIdx.z] + off);
+        const uint4* pb = reinterpret_cast<const uint4*>(tp.b[blockIdx.z] + off);
+#pragma unroll
+        for (int v = 0; v < 2; ++v) {
+            const uint4 a = pa[v], b = pb[v];
+            x[4 * v] = barrett_mul(a.x, b.x, q, mu), x[4 * v + 1] = barrett_mul(a.y, b.y, q, mu);
+            x[4 * v + 2] = barrett_mul(a.z, b.z, q, mu), x[4 * v + 3] = barrett_mul(a.w, b.w, q, mu);
+        }
+    } else {
+        ld8(x, ra.src + (size_t)R * 256 + 8 * t);
+    }
+    const uint2* w = tw + ((size_t)ra.prime << LOGN);
+    const uint2* rowf = irow + ((size_t)ra.prime << LOGR1) * 4 + (size_t)R * 4;
+    const uint2* gam = igam + ((size_t)ra.prime << 8);
+    ki8_inv_rows<LOGR1, FACT>(x, sm + r * kPitch8, w, rowf, gam, R, t, q, q2);
+    u32* p = ra.dst + (size_t)R * 256;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) p[t + 32 * k] = x[k];
+    ts_end(ts);
+}
+inline bool inv8_on() {
+    static const bool v = !(std::getenv("AESFHE_NTT_INV8") && std::atoi(std::getenv("AESFHE_NTT_INV8")) == 0);
+    return v;
+}
+
 // ---------------------------------------------------------------- inverse, pass 1 (in place on dst rows)
 template <int LOGR1, int NT>
 __global__ void __launch_bounds__(NT) k_ntt1_inv(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const uint2* tw,
@@ -665,6 +859,19 @@ inline bool inv_fact_on() {
 template <int LOGR1, int NT>
 void ntt2_inv_launch(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, RowMap rm, LimbMap map, int groups, double io,
                      double work, const TensorPtrs* tp, bool rev) {
+    if (inv8_on()) {
+        static const TensorPtrs kNone8{};
+        const dim3 g8(R1_of<LOGR1>() / 8, rm.cnt, groups);
+#define INV8(F, IN, TP) prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv8<LOGR1, F, IN>, g8, dim3(256), 0, st, dst, src, rm, map, Tb.pc, \
+                                        Tb.itw, Tb.irow, Tb.igam, TP)
+        if (tp) INV8(true, 1, *tp);
+        else if (rev && inv_fact_on()) INV8(true, 2, kNone8);
+        else if (rev) INV8(false, 2, kNone8);
+        else if (inv_fact_on()) INV8(true, 0, kNone8);
+        else INV8(false, 0, kNone8);
+#undef INV8
+        return;
+    }
     const dim3 grid(R1_of<LOGR1>() / (NT / 16), rm.cnt, groups);
     if (tp) {
         prof_launch_tsw(KID_NTT_ROWS_INV, io, work, k_ntt2_inv<LOGR1, NT, true, 1>, grid, dim3(NT), 0, st, dst, src, rm, map, Tb.pc, Tb.itw,
@@ -1054,138 +1261,11 @@ __global__ void __launch_bounds__(256) k_ntt2_ki(KiArgs a, LimbMap map, const Pr
     }
     ts_end(ts);
 }
-// ---- the fused core at 8 residues per thread (k_ntt2_ki8, AESFHE_KI8; VERDICT r4 "do this" 3)
-// k_ntt2_ki holds 16 residues per thread: 64 VGPRs of 64-bit accumulators, 242 in all, 2 waves /
-// SIMD.  Here a 256-thread block owns 8 rows (32 threads per 256-word row, 8 residues each), so
-// the accumulators take 32 VGPRs and the grid has twice the blocks.  The row pass runs its 8
-// stages in three register phases joined by two LDS exchanges:
-//   A  words t + 32 k      stages 0-2 (partners 4, 2, 1 apart in k)
-//   B  words 32 a + 4 m + b (a = t >> 2, b = t & 3)   stages 3-5 (partners 4, 2, 1 apart in m)
-//   C  words 8 t + m       stages 6-7 (partners 2, 1 apart in m)
-// every stage's butterflies and twiddles (index 2^(LOGR1 + s) + R 2^s + (word >> (8 - s))) are
-// k_ntt2_fwd's / k_ntt2_inv's, so every stored residue is the one the 16-residue kernel stores
-// (the inverse's lazy residues may differ in representative, its column pass ends canonical: the
-// ModDown's output is the same bit for bit; tests/test_gpu_fused_ki.py).
-// LDS swizzles (ds_read_b32 / ds_write_b32 bank = dword mod 32, one 32-lane half = one row):
-//   A <-> B: w ^ (((w >> 5) & 7) << 2)     B <-> C: w ^ ((((w >> 5) & 3) << 3) | ((w >> 5) & 7))
-// both conflict-free for both access patterns of their exchange.
-constexpr int kPitch8 = 256;
-__device__ __forceinline__ int swzAB(int w) { return w ^ (((w >> 5) & 7) << 2); }
-__device__ __forceinline__ int swzBC(int w) { return w ^ ((((w >> 5) & 3) << 3) | ((w >> 5) & 7)); }
-__device__ __forceinline__ int ki8_wordB(int t, int m) { return ((t >> 2) << 5) | (m << 2) | (t & 3); }
-template <int LOGR1>
-__device__ __forceinline__ int ki8_tw(int s, int R, int w) { return (1 << (LOGR1 + s)) + (R << s) + (w >> (8 - s)); }
-// forward: x[k] = word t + 32 k of row R (pass-1 output, [0, 4q)) -> x[m] = word 8 t + m, canonical
-template <int LOGR1>
-__device__ __forceinline__ void ki8_fwd_rows(u32 (&x)[8], u32* row, const uint2* w, int R, int t, u32 q, u32 q2) {
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-        const int h = 4 >> s;
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            if (!(k & h)) {
-                const uint2 tw = w[ki8_tw<LOGR1>(s, R, t + 32 * k)];
-                ct_bfly(x[k], x[k + h], tw.x, tw.y, q2, q);
-            }
-    }
-    __syncthreads();  // the previous user of the LDS row is done reading it
-#pragma unroll
-    for (int k = 0; k < 8; ++k) row[swzAB(t + 32 * k)] = x[k];
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < 8; ++m) x[m] = row[swzAB(ki8_wordB(t, m))];
-#pragma unroll
-    for (int s = 3; s < 6; ++s) {
-        const int h = 1 << (5 - s);
-#pragma unroll
-        for (int m = 0; m < 8; ++m)
-            if (!(m & h)) {
-                const uint2 tw = w[ki8_tw<LOGR1>(s, R, ki8_wordB(t, m))];
-                ct_bfly(x[m], x[m + h], tw.x, tw.y, q2, q);
-            }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < 8; ++m) row[swzBC(ki8_wordB(t, m))] = x[m];
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < 8; ++m) x[m] = row[swzBC(8 * t + m)];
-#pragma unroll
-    for (int s = 6; s < 8; ++s) {
-        const int h = 1 << (7 - s);
-#pragma unroll
-        for (int m = 0; m < 8; ++m)
-            if (!(m & h)) {
-                const uint2 tw = w[ki8_tw<LOGR1>(s, R, 8 * t + m)];
-                ct_bfly(x[m], x[m + h], tw.x, tw.y, q2, q);
-            }
-    }
-#pragma unroll
-    for (int m = 0; m < 8; ++m) x[m] = canon4(x[m], q);
-}
-// inverse: x[m] = word 8 t + m of row R (canonical) -> x[k] = word t + 32 k, [0, 2q) (Gentleman-Sande,
-// stages 7 .. 0)
-template <int LOGR1>
-__device__ __forceinline__ void ki8_inv_rows(u32 (&x)[8], u32* row, const uint2* w, int R, int t, u32 q, u32 q2) {
-    const u32 nq = 0u - q;
-#pragma unroll
-    for (int s = 7; s >= 6; --s) {
-        const int h = 1 << (7 - s);
-#pragma unroll
-        for (int m = 0; m < 8; ++m)
-            if (!(m & h)) {
-                const uint2 tw = w[ki8_tw<LOGR1>(s, R, 8 * t + m)];
-                gs_bfly(x[m], x[m + h], tw.x, tw.y, q2, nq);
-            }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < 8; ++m) row[swzBC(8 * t + m)] = x[m];
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < 8; ++m) x[m] = row[swzBC(ki8_wordB(t, m))];
-#pragma unroll
-    for (int s = 5; s >= 3; --s) {
-        const int h = 1 << (5 - s);
-#pragma unroll
-        for (int m = 0; m < 8; ++m)
-            if (!(m & h)) {
-                const uint2 tw = w[ki8_tw<LOGR1>(s, R, ki8_wordB(t, m))];
-                gs_bfly(x[m], x[m + h], tw.x, tw.y, q2, nq);
-            }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < 8; ++m) row[swzAB(ki8_wordB(t, m))] = x[m];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < 8; ++k) x[k] = row[swzAB(t + 32 * k)];
-#pragma unroll
-    for (int s = 2; s >= 0; --s) {
-        const int h = 4 >> s;
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            if (!(k & h)) {
-                const uint2 tw = w[ki8_tw<LOGR1>(s, R, t + 32 * k)];
-                gs_bfly(x[k], x[k + h], tw.x, tw.y, q2, nq);
-            }
-    }
-}
-__device__ __forceinline__ void ld8(u32 (&e)[8], const u32* p) {
-    const uint4* v = reinterpret_cast<const uint4*>(p);
-    const uint4 a = v[0], b = v[1];
-    e[0] = a.x, e[1] = a.y, e[2] = a.z, e[3] = a.w, e[4] = b.x, e[5] = b.y, e[6] = b.z, e[7] = b.w;
-}
-__device__ __forceinline__ void st8(u32* p, const u32 (&e)[8]) {
-    uint4* v = reinterpret_cast<uint4*>(p);
-    st_out16(v, make_uint4(e[0], e[1], e[2], e[3]));
-    st_out16(v + 1, make_uint4(e[4], e[5], e[6], e[7]));
-}
-// k_ntt2_ki's work with 8 residues per thread (see above); the same arguments, block -> (member,
+// k_ntt2_ki's work with 8 residues per thread (the row-pass helpers ki8_*: top of this file); the same arguments, block -> (member,
 // limb, 8-row chunk) with the same XCD grouping of a chunk's members
 template <int LOGR1>
 __global__ void __launch_bounds__(256) k_ntt2_ki8(KiArgs a, LimbMap map, const PrimeConst* pc, const uint2* tw, const uint2* itw,
-                                                  unsigned long long* ts) {
+                                                  const uint2* irow, const uint2* igam, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8, CH = (1 << LOGR1) / 8;  // 8-row chunks per limb
     __shared__ u32 sm[8 * kPitch8];
     const int b = blockIdx.x, nb = a.nb;
@@ -1298,11 +1378,13 @@ __global__ void __launch_bounds__(256) k_ntt2_ki8(KiArgs a, LimbMap map, const P
         st8(a.acc + m * a.acc_ms + ((size_t)(a.ne + x) << LOGN) + c0, r1);
     } else {  // converted rows: the ModDown's inverse row pass, into its pass-1 input ys [m][2][ys_rows]
         const uint2* iw = itw + ((size_t)prime << LOGN);
-        ki8_inv_rows<LOGR1>(r0, row, iw, R, t, q, q2);
+        const uint2* rowf = irow + ((size_t)prime << LOGR1) * 4 + (size_t)R * 4;
+        const uint2* gam = igam + ((size_t)prime << 8);
+        ki8_inv_rows<LOGR1, true>(r0, row, iw, rowf, gam, R, t, q, q2);
         u32* y0 = a.ys + m * a.ys_ms + ((size_t)(x - a.kept) << LOGN) + (size_t)R * 256;
 #pragma unroll
         for (int k = 0; k < 8; ++k) y0[t + 32 * k] = r0[k];
-        ki8_inv_rows<LOGR1>(r1, row, iw, R, t, q, q2);
+        ki8_inv_rows<LOGR1, true>(r1, row, iw, rowf, gam, R, t, q, q2);
         u32* y1 = a.ys + m * a.ys_ms + ((size_t)(a.ys_rows + x - a.kept) << LOGN) + (size_t)R * 256;
 #pragma unroll
         for (int k = 0; k < 8; ++k) y1[t + 32 * k] = r1[k];
@@ -1338,7 +1420,7 @@ void ki_launch(hipStream_t st, const DevTables& Tb, const KiArgs& a, LimbMap map
     const double bfly = 128.0 * (1 << LOGR1) * 8.0 * (a.nb * (a.nsrc * (double)ext_rows + 2.0 * (a.ne - a.kept)));
     if (ki8_on()) {
         prof_launch_tsw(KID_KEY_INNER, bytes, bfly, k_ntt2_ki8<LOGR1>, dim3(2 * CH * a.ne * a.nb), dim3(256), 0, st, a, map, Tb.pc, Tb.tw,
-                        Tb.itw);
+                        Tb.itw, Tb.irow, Tb.igam);
         return;
     }
     const dim3 grid(CH * a.ne * a.nb);

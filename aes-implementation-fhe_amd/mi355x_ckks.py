@@ -477,6 +477,13 @@ class Engine:
     # and conjugations come back as deferred ciphertexts (deferred_calls.py): the work is issued
     # when a result is needed, fused / batched.  The _raw_* forms are the undeferred calls.
     @staticmethod
+    def _has_level(x) -> bool:
+        """a deferred operand, or a ciphertext above level 0 (a product / non-integer constant
+        product of it can be formed)"""
+        from deferred_calls import Deferred
+        return isinstance(x, Deferred) or x.level > 0
+
+    @staticmethod
     def _settled(x):
         """a deferred operand that was already resolved acts as its result"""
         r = getattr(x, "_res", None)
@@ -536,14 +543,17 @@ class Engine:
             from deferred_calls import TermSum, constant_of
             a, b = self._settled(a), self._settled(b)
             if isinstance(b, Ciphertext):
-                if relinearization_key is not None:
+                # a plain operand without a level to spend raises now, as the undeferred call does
+                # (REF's callers see the "level" error at the call that caused it)
+                if relinearization_key is not None and self._has_level(a) and self._has_level(b):
                     return TermSum(self, 0j, [(a, b, 1.0 + 0j, [])])
             else:
                 c = constant_of(b)
                 if c is not None:
                     if isinstance(a, TermSum):
                         return a.scaled(b, c)
-                    return TermSum(self, 0j, (), [(a, c, [b])])
+                    if (c.real.is_integer() and c.imag.is_integer()) or self._has_level(a):
+                        return TermSum(self, 0j, (), [(a, c, [b])])
         return self._raw_mul(a, b, relinearization_key is not None)
 
     def _raw_mul(self, a, b, relin: bool = True):

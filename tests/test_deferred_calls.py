@@ -15,12 +15,17 @@ N = 8
 
 
 class FakeCt(M.Ciphertext):
-    __slots__ = ("v",)
+    __slots__ = ("v", "lv")
 
-    def __init__(self, v):
+    def __init__(self, v, lv=5):
         self._ctx = None
         self.handle = 1
         self.v = np.asarray(v, np.complex128)
+        self.lv = lv
+
+    @property
+    def level(self):
+        return self.lv
 
 
 class FakePt(M.Plaintext):
@@ -69,6 +74,10 @@ class Stub:
 
     def _raw_mul(self, a, b, relin=True):
         self.log.append("mul")
+        gauss = not isinstance(b, M.Ciphertext) and D.constant_of(b) is not None and \
+            D.constant_of(b).real.is_integer() and D.constant_of(b).imag.is_integer()
+        if not gauss and min(x.level for x in (a, b) if isinstance(x, M.Ciphertext)) < 1:
+            raise RuntimeError("not enough level")
         if isinstance(b, M.Ciphertext):
             return FakeCt(self._val(a) * self._val(b))
         if isinstance(b, M.Plaintext):
@@ -102,6 +111,7 @@ class Stub:
     _gal_pending = M.Engine._gal_pending
     _flush_gal = M.Engine._flush_gal
     _settled = staticmethod(M.Engine._settled)
+    _has_level = staticmethod(M.Engine._has_level)
     add = M.Engine.add
     subtract = M.Engine.subtract
     add_plain = M.Engine.add_plain
@@ -234,3 +244,19 @@ def test_resolved_operand_acts_as_its_result():
     w = E.add(E.multiply(b, 2.0), z)
     s = E.subtract(w, b)
     np.testing.assert_allclose(D.real(s).v, x.v * y.v + 0.5, atol=1e-12)
+
+
+def test_level_error_at_the_call():
+    """a product of a level-0 ciphertext raises at the multiply call, as undeferred (REF's callers
+    branch on the "level" message, REF/engine_context.py:184-195); Gaussian-integer constants need
+    no level and stay deferred"""
+    rng = np.random.default_rng(8)
+    E = Stub(True)
+    x = FakeCt(np.exp(2j * np.pi * rng.random(N)), lv=0)
+    with pytest.raises(RuntimeError, match="level"):
+        E.multiply(x, x, "rlk")
+    with pytest.raises(RuntimeError, match="level"):
+        E.multiply(x, 0.5)
+    z = E.multiply(x, -1j)
+    assert isinstance(z, D.TermSum)
+    np.testing.assert_allclose(D.real(z).v, -1j * x.v)

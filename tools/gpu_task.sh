@@ -10,6 +10,7 @@
 #                           (tools/trace_window.py) beside the bench's own live dispatch-inclusive averages
 #   pmc                     FETCH_SIZE / WRITE_SIZE passes (separate runs) over the C2 leg, reduced to
 #                           per-class traffic / algorithmic bytes (tools/pmc_reduce.py)
+#   pmcbench                FETCH_SIZE / WRITE_SIZE passes over the bench's C2 leg itself (not a one-round proxy)
 #   twogpu                  torchrun --nproc-per-node=2 bench.py --gpus 2 over gloo on ONE MI355X (both ranks
 #                           share it): the N > 1 engine path at the C4 / C5 per-rank shapes
 #   boot                    tools/boot_phases.py 32 (sparse bootstrap phases)
@@ -57,6 +58,21 @@ for t in "$@"; do
       timeout -k 10 300 python3 tools/pmc_reduce.py "--source=rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE passes (separate runs, --kernel-include-regex on the NTT / conversion / key-switch / lin_mac kernels) over tools/pmc_round.py: one middle encrypt round of the bench workload, whole process incl. key generation; algorithmic bytes of exactly those launches from the engine (AESFHE_PROFILE_FROM_START); FETCH_SIZE x2 for 16-B-per-lane reads, x1 for NTT pass 2 dword reads (tools/ntt_pmc_calib.py); L2-miss bytes (MALL hits included), an upper bound on HBM bytes" \
           --alg=$O/pmc_algorithmic.json $O/pmc_traffic_round.json $O/pmc_fetch $O/pmc_write > /dev/null
       rm -rf $O/pmc_fetch $O/pmc_write ;;
+    pmcbench)
+      # FETCH_SIZE / WRITE_SIZE passes (separate runs, every kernel) over the bench's C2 leg itself
+      # (bench.py --whole-stats: no sampled profiler, no precision pass), the same command once more
+      # for the engine's algorithmic bytes of exactly those launches (VERDICT r4 'do this' 7)
+      KIDS=key_inner,base_convert,ntt_cols_fwd,ntt_rows_fwd,ntt_rows_inv,ntt_cols_inv,lin_mac
+      PB="--steps ${PMC_STEPS:-1} --warmup 1 $C2 --detail-json $O/pmcb_detail.json --whole-stats $O/ws_unused.json"
+      AESFHE_PROFILE_FROM_START=$KIDS timeout -k 10 200 python3 bench.py --steps ${PMC_STEPS:-1} --warmup 1 $C2 --detail-json $O/pmcb_detail0.json \
+          --whole-stats $O/pmcb_algorithmic.json > $O/pmcb_alg.out
+      timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmcb_fetch -o run -- \
+          python3 bench.py $PB > $O/pmcb_fetch.out 2> $O/pmcb_fetch.err
+      timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcb_write -o run -- \
+          python3 bench.py $PB > $O/pmcb_write.out 2> $O/pmcb_write.err
+      timeout -k 10 300 python3 tools/pmc_reduce.py "--source=rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate runs, every kernel) over the bench's own C2 leg (bench.py --steps ${PMC_STEPS:-1} --warmup 1, secondary legs off), whole process; algorithmic bytes of the same launches (AESFHE_PROFILE_FROM_START); FETCH x2 for 16-B-per-lane reads, x1 for NTT pass-2 dword reads (MI355X_MICROARCH.md HBM section, tools/ntt_pmc_calib.py)" \
+          --alg=$O/pmcb_algorithmic.json $O/pmc_traffic_bench.json $O/pmcb_fetch $O/pmcb_write > /dev/null
+      rm -rf $O/pmcb_fetch $O/pmcb_write ;;
     twogpu)
       AESFHE_DIST_BACKEND=gloo timeout -k 10 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr=127.0.0.1 \
           --master-port=29517 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline --batch-states 1024 --c5-states 256 \

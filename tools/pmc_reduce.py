@@ -62,7 +62,7 @@ def main():
                   **{c.lower() + "_bytes": v for c, v in per.items()}}
     # aggregate template instances under the engine's kernel ids (launch-weighted)
     ids = {"ntt1_fwd": "ntt_cols_fwd", "ntt2_fwd": "ntt_rows_fwd", "ntt2_inv": "ntt_rows_inv", "ntt1_inv": "ntt_cols_inv",
-           "key_inner": "key_inner", "key_inner_sum": "key_inner", "key_inner_multi": "key_inner", "ntt2_ki": "key_inner",
+           "key_inner": "key_inner", "key_inner_sum": "key_inner", "key_inner_multi": "key_inner", "ntt2_ki": "key_inner", "ntt2_ki8": "key_inner",
            "base_convert": "base_convert", "bx_cols": "base_convert", "lin_mac": "lin_mac"}
     agg = {}
     for k, v in list(res.items()):
