@@ -589,6 +589,73 @@ __global__ void __launch_bounds__(NT, OCC) k_ntt2_fwd(u32* data, RowMap rm, Limb
     ts_end(ts);
 }
 
+// the forward row pass at 8 residues per thread (AESFHE_NTT_FWD8): k_ntt2_fwd's modes (plain, and
+// the finish with its cur / add / cmul / 2 r + c epilogue) on 256-thread blocks of 8 rows through
+// ki8_fwd_rows -- the same butterflies, twiddles and canonical outputs, so the same residues
+template <int LOGR1, int MODE>
+__global__ void __launch_bounds__(256) k_ntt2_fwd8(u32* data, RowMap rm, LimbMap map, const PrimeConst* pc, const uint2* tw, NttAux aux,
+                                                   unsigned long long* ts) {
+    constexpr int LOGN = LOGR1 + 8;
+    __shared__ u32 sm[8 * kPitch8];
+    if (skipped(rm)) return;
+    ts_begin(ts);
+    const RowAddr ra = row_addr<LOGN>(data, data, rm, map);
+    const u32 q = pc[ra.prime].q, q2 = 2 * q;
+    const int r = threadIdx.x >> 5, t = threadIdx.x & 31;
+    const int R = blockIdx.x * 8 + r;
+    u32* p = ra.dst + (size_t)R * 256;
+    u32 x[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) x[k] = p[t + 32 * k];
+    ki8_fwd_rows<LOGR1>(x, sm + r * kPitch8, tw + ((size_t)ra.prime << LOGN), R, t, q, q2);
+    if (MODE == kFinish) {
+        const int grp = blockIdx.z, li = blockIdx.y;
+        const size_t woff = (size_t)R * 256 + 8 * t;
+        u32 cv[8], av[8];
+        ld8(cv, aux.cur + ((size_t)(grp * aux.cur_stride + li) << LOGN) + woff);
+        const u32* addp = (grp & 1) ? aux.add1 : aux.add0;
+        if (grp > 1) addp = (addp && aux.add_mstride) ? addp + (grp >> 1) * aux.add_mstride : nullptr;
+        const bool has_add = addp != nullptr;
+        if (has_add && aux.add_rev && !(grp & 1)) {  // element e <- word N - 1 - (woff + e)
+            u32 tmp[8];
+            ld8(tmp, addp + ((size_t)li << LOGN) + ((size_t)1 << LOGN) - 8 - woff);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) av[e] = tmp[7 - e];
+        } else if (has_add) {
+            ld8(av, addp + ((size_t)li << LOGN) + woff);
+        }
+        u32* const om = aux.outm[(grp >> 1) & 7];
+        u32* o = (om ? om + ((size_t)((grp & 1) * aux.out_stride + li) << LOGN) : aux.out + ((size_t)(grp * aux.out_stride + li) << LOGN)) + woff;
+        const u32 qi = aux.qinv[2 * li], qip = aux.qinv[2 * li + 1];
+        if (aux.cmul) {
+            const u32 cm = aux.cmul[2 * li], cmp = aux.cmul[2 * li + 1];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) cv[e] = shoup_mul(cv[e], cm, cmp, q);
+        }
+        const int mem = (grp >> 1) & 7;
+        const bool dbl = (aux.dbl >> mem) & 1u;
+        const u32* cs = (grp & 1) ? nullptr : aux.cst[mem];
+        const u32 cadd = cs ? cs[2 * li + (R >= (1 << LOGR1) / 2 ? 1 : 0)] : 0u;
+        u32 res[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            u32 v = shoup_mul(cv[e] + q - x[e], qi, qip, q);
+            if (has_add) v = add_mod(v, av[e], q);
+            if (dbl) v = add_mod(v, v, q);
+            if (cs) v = add_mod(v, cadd, q);
+            res[e] = v;
+        }
+        st8(o, res);
+    } else {
+        st8(p + 8 * t, x);
+    }
+    ts_end(ts);
+}
+inline bool fwd8_on() {
+    static const bool v = std::getenv("AESFHE_NTT_FWD8") && std::atoi(std::getenv("AESFHE_NTT_FWD8")) != 0;
+    return v;
+}
+
 // ---------------------------------------------------------------- inverse, pass 2 (src -> dst)
 // FACT: stages 7, 6, 5 (255 - 31 of a row's 255 twiddles, each thread its own) read their
 // twiddle as (row factor) x (shared factor): psi^-(2^(7-s) (2 brv(R) + 1)) -- three per row --
@@ -801,6 +868,11 @@ __global__ void __launch_bounds__(NT) k_ntt1_inv(u32* data, RowMap rm, LimbMap m
 template <int LOGR1, int M2, int NT>
 void ntt2_fwd_launch(hipStream_t st, const DevTables& Tb, u32* dst, RowMap rm, LimbMap map, int groups, double io, double work,
                      const NttAux& aux) {
+    if (fwd8_on()) {
+        prof_launch_tsw(KID_NTT_ROWS_FWD, io, work, k_ntt2_fwd8<LOGR1, M2>, dim3((1 << LOGR1) / 8, rm.cnt, groups), dim3(256), 0, st, dst, rm, map,
+                        Tb.pc, Tb.tw, aux);
+        return;
+    }
     const dim3 grid((1 << LOGR1) / (NT / 16), rm.cnt, groups);
     if (M2 == kFinish && fin_occ_on())
         prof_launch_tsw(KID_NTT_ROWS_FWD, io, work, k_ntt2_fwd<LOGR1, M2, NT, 4>, grid, dim3(NT), 0, st, dst, rm, map, Tb.pc, Tb.tw, aux);
@@ -833,8 +905,7 @@ void ntt_fwd_t(hipStream_t st, const DevTables& Tb, u32* dst, const u32* src, in
         constexpr int NT = kThreads / 2, CB = NT / (R1 / 16);
         prof_launch_tsw(KID_NTT_COLS_FWD, io1, bfly * LOGR1, k_ntt1_fwd<LOGR1, M1, NT>, dim3(256 / CB, rm.cnt, groups), dim3(NT), 0, st, dst, src,
                         rm, map, Tb.pc, Tb.tw, aux);
-        prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2, NT>, dim3(R1 / (NT / 16), rm.cnt, groups), dim3(NT), 0, st, dst,
-                        rm, map, Tb.pc, Tb.tw, aux);
+        ntt2_fwd_launch<LOGR1, M2, NT>(st, Tb, dst, rm, map, groups, io2, bfly * 8.0, aux);
         return;
     }
     if (p1_nt_rows(false, rows) == 256) {
@@ -999,8 +1070,7 @@ void ntt_fwd_conv_t(hipStream_t st, const DevTables& Tb, u32* dst, const ConvBat
     if (small_launch(rows)) {
         constexpr int NT = kThreads / 2;
         ntt1_conv_dispatch<LOGR1, NT>(st, Tb, dst, cb, h, rm, map, groups, io1, bfly * LOGR1);
-        prof_launch_tsw(KID_NTT_ROWS_FWD, io2, bfly * 8.0, k_ntt2_fwd<LOGR1, M2, NT>, dim3(R1 / (NT / 16), rm.cnt, groups), dim3(NT), 0, st, dst,
-                        rm, map, Tb.pc, Tb.tw, aux);
+        ntt2_fwd_launch<LOGR1, M2, NT>(st, Tb, dst, rm, map, groups, io2, bfly * 8.0, aux);
         return;
     }
     ntt1_conv_dispatch<LOGR1, kThreads>(st, Tb, dst, cb, h, rm, map, groups, io1, bfly * LOGR1);

@@ -1,9 +1,20 @@
 set -e -o pipefail
-O=gpurun_out/r5e; mkdir -p $O
-timeout -k 10 600 python3 -u -m pytest tests/test_gpu_boot_chunk.py tests/test_gpu_deferred_calls.py tests/test_gpu_ops.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_a.log 2>&1 || { tail -40 $O/pytest_a.log; exit 1; }
-tail -2 $O/pytest_a.log
-for v in 0 1 0 1; do AESFHE_LIN_MAC_NB4=$v timeout -k 10 300 python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --batch-states 0 --true-fhe-steps 0 --pair-states 64 --pair-stack 64 --pair-steps 1 --packed-pairs 0 --eager-steps 0 --deferred-steps 0 --detail-json $O/pairs_nb4_$v.json > /dev/null 2> $O/pairs.err; python3 -c "
-import json; d=json.load(open('$O/pairs_nb4_$v.json'))['batch_pairs']; c=d['roofline_step']['classes']
-print('nb4=$v', round(d['blocks_per_s'],3), round(d['ms_per_pair'],2), {k: (round(v['frac'],3), round(v['avg_us'],1)) for k, v in c.items()})" | tee -a $O/pairs_ab.txt; done
+O=gpurun_out/r5f; mkdir -p $O
+AESFHE_NTT_INV8=0 timeout -k 10 200 python3 tools/enc_digest.py > $O/digest_inv16.json
+AESFHE_NTT_INV8=1 timeout -k 10 200 python3 tools/enc_digest.py > $O/digest_inv8.json
+AESFHE_NTT_FWD8=1 timeout -k 10 200 python3 tools/enc_digest.py > $O/digest_fwd8.json
+cat $O/digest_inv16.json $O/digest_inv8.json $O/digest_fwd8.json
+PASSES=2 bash tools/env_ab.sh r5f AESFHE_NTT_INV8=0 AESFHE_NTT_INV8=1 AESFHE_NTT_INV8=1,AESFHE_NTT_FWD8=1
+python3 - <<'PY'
+import json
+for l in open('gpurun_out/r5f/bench.txt'):
+    cfg, js = l.split(' ', 1); d = json.loads(js); c = d['roofline_step']['classes']
+    print(cfg, d['value'], d['launches_per_encrypt'], 'rows_inv', c['ntt_rows_inv'][:3], 'rows_fwd', c['ntt_rows_fwd'][:3], 'key_inner', c['key_inner'][:3])
+PY
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest_all.log 2>&1 || { tail -40 $O/pytest_all.log; exit 1; }
 tail -3 $O/pytest_all.log
+bash tools/gpu_task.sh r5f pmcbench
+python3 -c "
+import json; d=json.load(open('gpurun_out/r5f/pmc_traffic_bench.json')); print({k: (round(v.get('traffic_over_algorithmic') or 0,3)) for k,v in d.items() if isinstance(v, dict) and 'traffic_over_algorithmic' in v})"
+bash tools/sq_pmc.sh r5f/sq_c2
+SQ_ARGS="pairs=16" bash tools/sq_pmc.sh r5f/sq_pairs16

@@ -7,6 +7,6 @@ O=gpurun_out/${1:-sqpmc}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_LDS \
-    --output-format csv -d $O/sq -o run -- python3 tools/pmc_round.py > $O/sq.out 2> $O/sq.err
+    --output-format csv -d $O/sq -o run -- python3 tools/pmc_round.py ${SQ_ARGS:-} > $O/sq.out 2> $O/sq.err
 timeout -k 10 120 python3 tools/sq_reduce.py $O/sq_round.json $O/sq > $O/sq_summary.json
 echo done
