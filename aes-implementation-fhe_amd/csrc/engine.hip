@@ -3703,7 +3703,14 @@ public:
         const auto& c = bs_.plan.cheb;
         const int d = (int)c.size() - 1, ni = (int)ys.size();
         std::vector<std::vector<Ct>> T(ni, std::vector<Ct>(kBabyDeg + 1));
-        for (int i = 0; i < ni; ++i) T[i][1] = copy(*ys[i]);
+        // an input on the single / double transition level (the low-level sparse bootstrap's
+        // CoeffToSlot output, §4d) first drops to the single-prime level below it by an exact-scale
+        // conversion: every power and leaf of the evaluation then lives in one scale region (a leaf
+        // coefficient of T_1 at the transition's 2^60 scale would round to an integer)
+        for (int i = 0; i < ni; ++i) {
+            const Ct& y = *ys[i];
+            T[i][1] = hp_.homogeneous(y.level) ? copy(y) : level_down(y, y.level - 1);
+        }
         static const bool batch_baby = env_int("AESFHE_EVALMOD_BATCH", 1) != 0;
         for (int lo = 2; lo <= kBabyDeg;) {
             const int hi = batch_baby ? std::min(kBabyDeg, 2 * lo - 2) : lo;

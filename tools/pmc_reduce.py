@@ -11,6 +11,10 @@ from collections import defaultdict
 from pathlib import Path
 
 SCALE = {"FETCH_SIZE": 2 * 1024.0, "WRITE_SIZE": 1024.0}
+# WRITE_SIZE from its raw TCC requests when the derived counter cannot be collected (on this image a
+# WRITE_SIZE pass over the whole bench crawls): bytes = 64 x WRREQ_64B + 32 x (WRREQ - WRREQ_64B),
+# rocprofv3's own derivation of WRITE_SIZE
+RAW_WRITE = ("TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum")
 # kernels whose bulk reads are 4 B per lane in 64-B segments (not 16-B-per-lane streaming):
 # FETCH_SIZE counts those bytes as they are.  Calibrated with tools/ntt_pmc_calib.py (plain
 # 160-row NTTs): pass 1 (16-B-per-lane-equivalent coalesced reads) FETCH x2 = 1.03 x its
@@ -55,6 +59,12 @@ def main():
                     acc[k][c] += float(row["Counter_Value"]) * sc
                     cnt[k][c] += 1
             f.unlink()
+    for k in acc:  # the raw write requests -> WRITE_SIZE bytes
+        if all(c in acc[k] for c in RAW_WRITE):
+            w, w64 = acc[k].pop(RAW_WRITE[0]), acc[k].pop(RAW_WRITE[1])
+            acc[k]["WRITE_SIZE"] = 64.0 * w64 + 32.0 * (w - w64)
+            cnt[k]["WRITE_SIZE"] = cnt[k].pop(RAW_WRITE[0])
+            cnt[k].pop(RAW_WRITE[1], None)
     res = {}
     for k in acc:
         per = {c: acc[k][c] / cnt[k][c] for c in acc[k]}
