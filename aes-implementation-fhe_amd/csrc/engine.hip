@@ -4908,7 +4908,9 @@ int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle c, int stage, aesfhe_
     CT_OP(e.bootstrap(e.canon(c), stage, 1.0, period))
 }
 int aesfhe_debug_boot_stage_sparse(aesfhe_ctx* ctx, aesfhe_handle c, int stage, int period, aesfhe_handle* out) {
-    CT_OP(e.bootstrap(e.canon(c), stage, 1.0, period))
+    // AESFHE_DEBUG_BOOT_FLOOR=<level>: the stages of the low-level form (tools/boot_low_stages.py)
+    static const int floor = std::getenv("AESFHE_DEBUG_BOOT_FLOOR") ? std::atoi(std::getenv("AESFHE_DEBUG_BOOT_FLOOR")) : -1;
+    CT_OP(e.bootstrap(e.canon(c), stage, 1.0, period, floor))
 }
 int aesfhe_debug_sparse_group(aesfhe_ctx* ctx, aesfhe_handle c, int period, int which, int pair, aesfhe_handle* out) {
     CT_OP(e.lin_group(e.canon(c), e.debug_sparse_group(period, which, pair != 0)))

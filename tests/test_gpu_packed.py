@@ -86,9 +86,10 @@ def test_packed_round_modules(ctx, coeff_dir):
     assert np.array_equal(enc.decode(*ark), want ^ key)
 
 
-@pytest.mark.parametrize("states", [64, 2048])
+@pytest.mark.parametrize("states", [64, 128, 2048])
 def test_packed_config2_encrypt_and_roundtrip(ctx, coeff_dir, states):
-    """BASELINE configs 3/5 in the packed layout: `states` independent states under one
+    """BASELINE configs 3/5 in the packed layout (128 = C5's per-GPU share of 1,024 states on 8
+    GPUs, bench.c5_states_per_rank): `states` independent states under one
     shared key (REF/test/test_aes_pipeline_roundtrip.py:114-163 per state), 10-round
     encrypt with renorm + final bootstraps, then decrypt with InvMixColumns; every state's
     ciphertext equals the reference AES and every plaintext comes back bit-exact."""
