@@ -3026,8 +3026,7 @@ public:
         std::vector<BootGroupDev> cts, stc;
         BootGroupDev stc_lo;  // pair4: the lo member's form of stc[0]
     };
-    std::map<int, SparseBoot> sparse_;  // key n (single / unpacked pair), -n (pair4); + kLowKey: the low-level form
-    static constexpr int kLowKey = 1 << 24;
+    std::map<int, SparseBoot> sparse_;  // key n (single / unpacked pair), -n (pair4)
     bool trace4_ = std::getenv("AESFHE_TRACE4") ? std::atoi(std::getenv("AESFHE_TRACE4")) != 0 : true;
     // x + rot(x, -a) + rot(x, -2a) + rot(x, -3a) for the nb members of x: the three rotations
     // hoisted (one ModUp of c1, key inner products read through each automorphism) and summed
@@ -3061,50 +3060,22 @@ public:
         cnt_[C_KS] += 3 * nb;
         return o;
     }
-    // the low-level form of a sparse bootstrap (round 5, AESFHE_BOOT_LOW, default on): for a caller
-    // whose result only has to reach `min_level` (MixColumns' final bootstrap in the secret-key
-    // renorm mode: its output meets one XOR4 whose result is renormalised, NEED_XOR = 7), ModRaise
-    // goes to the LOWEST double-prime level L1 + 2 (25 limbs instead of 43 at top = 30), the trace
-    // and CoeffToSlot run there (their diagonals keep the 2^60 plaintext scale they need), the
-    // CoeffToSlot output crosses the single / double transition and EvalMod + SlotToCoeff run on
-    // the single-prime levels L1 .. L1 - 9 - groups: every key switch of the bootstrap on ~half the
-    // limbs.  EvalMod at the single-prime scale (~2^30) instead of 2^60 costs precision the Zeta16
-    // decode margin absorbs (measured: bench precision, tests/test_gpu_boot_low.py)
-    bool boot_low_ = !(std::getenv("AESFHE_BOOT_LOW") && std::atoi(std::getenv("AESFHE_BOOT_LOW")) == 0);
-    int low_out_level(int n) const {
-        int logm = 0;
-        while ((1 << logm) < n) ++logm;
-        const int groups = std::max(1, (logm + 4) / 5);
-        return hp_.L1 - boot_evalmod_depth() - groups;
-    }
-    bool use_low(int n, int min_level) const {
-        return boot_low_ && min_level >= 0 && hp_.L >= hp_.L1 + 2 && low_out_level(n) >= std::max(1, min_level);
-    }
-    SparseBoot& sparse_variant(int n, bool pair = false, bool low = false) {
+    SparseBoot& sparse_variant(int n, bool pair = false) {
         const char* p4 = std::getenv("AESFHE_SPARSE_PAIR4");  // "0": the pair keeps two EvalMod members (A/B)
         pair = pair && n <= 32 && !(p4 && std::atoi(p4) == 0);
-        const int key = (pair ? -n : n) + (low ? kLowKey : 0);
-        auto it = sparse_.find(key);
+        auto it = sparse_.find(pair ? -n : n);
         if (it != sparse_.end()) return it->second;
         const int M = slot_count();
         int logm = 0;
         while ((1 << logm) < n) ++logm;
         if ((1 << logm) != n || n < 16 || n >= M) throw std::runtime_error("sparse bootstrap: period must be a power of two in [16, slot_count)");
-        SparseBoot& sv = sparse_[key];
+        SparseBoot& sv = sparse_[pair ? -n : n];
         sv.n = n;
         const int groups = std::max(1, (logm + 4) / 5);  // <= 5 butterfly stages per group, like the full plan
-        if (low) {
-            // CoeffToSlot from the lowest double-prime level down across the transition (its diagonals
-            // are plaintext products: the transition's pair near T is crossed exactly), then EvalMod and
-            // SlotToCoeff on the single-prime levels below L1
-            sv.top = hp_.L1 + 1 + groups;
-            sv.out_level = low_out_level(n);
-        } else {
-            // StC's first group crosses the single / double-prime transition (plaintext products only)
-            sv.top = hp_.L1 + 1 + groups + boot_evalmod_depth();
-            sv.out_level = hp_.L1 + 1 - groups;
-        }
-        if (sv.top > hp_.L || sv.out_level < 1) throw std::runtime_error("sparse bootstrap: chain too short");
+        // StC's first group crosses the single / double-prime transition (plaintext products only)
+        sv.top = hp_.L1 + 1 + groups + boot_evalmod_depth();
+        sv.out_level = hp_.L1 + 1 - groups;
+        if (sv.top > hp_.L) throw std::runtime_error("sparse bootstrap: chain too short");
         const double Q0 = (double)hp_.mod[0] * (double)hp_.mod[1];
         // the trace multiplies by M / n: folded into CoeffToSlot
         const double cts_scale = hp_.delta[sv.top] / (2.0 * Q0 * boot_k() * ((double)M / n));
@@ -3703,14 +3674,7 @@ public:
         const auto& c = bs_.plan.cheb;
         const int d = (int)c.size() - 1, ni = (int)ys.size();
         std::vector<std::vector<Ct>> T(ni, std::vector<Ct>(kBabyDeg + 1));
-        // an input on the single / double transition level (the low-level sparse bootstrap's
-        // CoeffToSlot output, §4d) first drops to the single-prime level below it by an exact-scale
-        // conversion: every power and leaf of the evaluation then lives in one scale region (a leaf
-        // coefficient of T_1 at the transition's 2^60 scale would round to an integer)
-        for (int i = 0; i < ni; ++i) {
-            const Ct& y = *ys[i];
-            T[i][1] = hp_.homogeneous(y.level) ? copy(y) : level_down(y, y.level - 1);
-        }
+        for (int i = 0; i < ni; ++i) T[i][1] = copy(*ys[i]);
         static const bool batch_baby = env_int("AESFHE_EVALMOD_BATCH", 1) != 0;
         for (int lo = 2; lo <= kBabyDeg;) {
             const int hi = batch_baby ? std::min(kBabyDeg, 2 * lo - 2) : lo;
@@ -3805,11 +3769,10 @@ public:
         release(z);
         return out;
     }
-    // min_level >= 0: the caller needs the result only at that level (the low-level sparse form, above)
-    Ct bootstrap(const Ct& in, int stop_after = 99, double gain = 1.0, int period = 0, int min_level = -1) {
+    Ct bootstrap(const Ct& in, int stop_after = 99, double gain = 1.0, int period = 0) {
         boot_setup();
         if (vis_npoly(in) != 2) throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
-        SparseBoot* sv = (period > 0 && period < slot_count()) ? &sparse_variant(period, false, use_low(period, min_level)) : nullptr;
+        SparseBoot* sv = (period > 0 && period < slot_count()) ? &sparse_variant(period) : nullptr;
         if (in.nb > 1) {  // a stack (multi-pair batch): chunks of two members
             if (stop_after != 99) throw std::runtime_error("bootstrap: debug stages take a single ciphertext");
             Ct c = normalize(in);
@@ -3825,19 +3788,17 @@ public:
     // the hi / lo bootstraps of an AES step (MixColumns' final bootstrap) as ONE batched
     // bootstrap of two stacked ciphertexts: every key switch reads its key, and every linear
     // transform its diagonals, once for both; half the launches
-    void bootstrap_pair(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob, double gain = 1.0, int period = 0,
-                        int min_level = -1) {
+    void bootstrap_pair(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob, double gain = 1.0, int period = 0) {
         boot_setup();
         if (vis_npoly(a_in) != 2 || vis_npoly(b_in) != 2 || a_in.nb != b_in.nb)
             throw std::runtime_error("bootstrap expects a 2-polynomial ciphertext");
-        if (period > 0 && 2 * period <= slot_count() && mono_pair_)
-            return bootstrap_pair_mono(a_in, b_in, oa, ob, gain, period, min_level);
+        if (period > 0 && 2 * period <= slot_count() && mono_pair_) return bootstrap_pair_mono(a_in, b_in, oa, ob, gain, period);
         if (a_in.nb > 1) {  // stacks: a's and b's members bootstrapped in chunks of two
-            *oa = put_ct(bootstrap(a_in, 99, gain, period, min_level));
-            *ob = put_ct(bootstrap(b_in, 99, gain, period, min_level));
+            *oa = put_ct(bootstrap(a_in, 99, gain, period));
+            *ob = put_ct(bootstrap(b_in, 99, gain, period));
             return;
         }
-        SparseBoot* sv = (period > 0 && period < slot_count()) ? &sparse_variant(period, true, use_low(period, min_level)) : nullptr;
+        SparseBoot* sv = (period > 0 && period < slot_count()) ? &sparse_variant(period, true) : nullptr;
         const int n = hp_.n, nl0 = hp_.nl(0);
         Ct z = alloc_ct(0, 4, 2);
         const Ct* in[2] = {&a_in, &b_in};
@@ -3902,11 +3863,10 @@ public:
         launch_mul_poly(S(), T_, lo.data, dn.data, monomial(2 * n - k), dn.npoly, hp_.nl(dn.level), qmap());
         release(dn);
     }
-    void bootstrap_pair_mono(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob, double gain, int period,
-                             int min_level = -1) {
+    void bootstrap_pair_mono(const Ct& a_in, const Ct& b_in, aesfhe_handle* oa, aesfhe_handle* ob, double gain, int period) {
         Ct z = mono_pack(a_in, b_in, period);
         z_members_ = z.nb;
-        SparseBoot* sv = 2 * period < slot_count() ? &sparse_variant(2 * period, false, use_low(2 * period, min_level)) : nullptr;
+        SparseBoot* sv = 2 * period < slot_count() ? &sparse_variant(2 * period) : nullptr;
         Ct mz = boot_stack(z, 0.5 * gain, sv);  // a stack of P packed pairs: chunks of two
         Ct hi, lo;
         mono_split(mz, period, hi, lo);
@@ -4890,17 +4850,6 @@ int aesfhe_bootstrap_pair_sparse(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle
     e.bootstrap_pair(ca, cb, out_a, out_b, gain, period);
     API_END
 }
-int aesfhe_bootstrap_sparse_floor(aesfhe_ctx* ctx, aesfhe_handle c, int period, double gain, int min_level, aesfhe_handle* out) {
-    CT_OP(e.bootstrap(e.canon(c), 99, gain, period, min_level))
-}
-int aesfhe_bootstrap_pair_sparse_floor(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int period, double gain, int min_level,
-                                       aesfhe_handle* out_a, aesfhe_handle* out_b) {
-    API_BEGIN Engine& e = *ctx->eng;
-    const Ct& ca = e.canon(a);
-    const Ct& cb = e.canon(b);
-    e.bootstrap_pair(ca, cb, out_a, out_b, gain, period, min_level);
-    API_END
-}
 int aesfhe_bootstrap_depth(void) { return Engine::boot_depth(); }
 int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle c, int stage, aesfhe_handle* out) {
     // AESFHE_DEBUG_PERIOD: the stages of the sparse-slot bootstrap of that period (profiling)
@@ -4908,9 +4857,7 @@ int aesfhe_debug_boot_stage(aesfhe_ctx* ctx, aesfhe_handle c, int stage, aesfhe_
     CT_OP(e.bootstrap(e.canon(c), stage, 1.0, period))
 }
 int aesfhe_debug_boot_stage_sparse(aesfhe_ctx* ctx, aesfhe_handle c, int stage, int period, aesfhe_handle* out) {
-    // AESFHE_DEBUG_BOOT_FLOOR=<level>: the stages of the low-level form (tools/boot_low_stages.py)
-    static const int floor = std::getenv("AESFHE_DEBUG_BOOT_FLOOR") ? std::atoi(std::getenv("AESFHE_DEBUG_BOOT_FLOOR")) : -1;
-    CT_OP(e.bootstrap(e.canon(c), stage, 1.0, period, floor))
+    CT_OP(e.bootstrap(e.canon(c), stage, 1.0, period))
 }
 int aesfhe_debug_sparse_group(aesfhe_ctx* ctx, aesfhe_handle c, int period, int which, int pair, aesfhe_handle* out) {
     CT_OP(e.lin_group(e.canon(c), e.debug_sparse_group(period, which, pair != 0)))

@@ -182,12 +182,11 @@ class EngineContext:
         self._bs_total_s += time.perf_counter() - t0
         return out
 
-    def bootstrap_pair_sparse(self, a, b, period: int, min_level=None):
+    def bootstrap_pair_sparse(self, a, b, period: int):
         """bootstrap_pair of two messages whose slots repeat with period `period` (the periodic
-        state layout, state_encoder.SlotLayout): the sparse-slot bootstrap (DESIGN.md §4b);
-        min_level: the results are needed only at that level (the low-level form, §4d)"""
+        state layout, state_encoder.SlotLayout): the sparse-slot bootstrap"""
         t0 = time.perf_counter()
-        out = self.engine.bootstrap_pair_sparse(a, b, period, min_level=min_level)
+        out = self.engine.bootstrap_pair_sparse(a, b, period)
         self._bs_count += 2
         self._bs_total_s += time.perf_counter() - t0
         return out

@@ -78,7 +78,7 @@ class InvMixColumnsFHE:
         return (self.use_hard_renorm and self.layout.packable and self.enc.renorm_hook is None
                 and getattr(self.ctx, "fused_luts", False) and getattr(self.ctx, "renorm_unpack", None) is not None)
 
-    def imc_packed(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, min_level=None):
+    def imc_packed(self, ct_hi, ct_lo, do_final_bootstrap: bool = True):
         """InvMixColumns with its XOR stage on packed states (MixColFinal.mix_packed):
         the four GF multiplier pairs' outputs packed (inputs one level higher than __call__'s),
         three single XOR4s and single renorms, one sparse bootstrap at period 2P.  Returns the
@@ -95,15 +95,13 @@ class InvMixColumnsFHE:
                       lambda: enc.renorm_packed(self._xor(p13, p9, fl), level=NEED_XOR))
         acc = enc.renorm_packed(self._xor(x1, x2, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
         if do_final_bootstrap:
-            acc = bootstrap1(ctx, acc, 2 * self.layout.period, min_level=min_level)
+            acc = bootstrap1(ctx, acc, 2 * self.layout.period)
         return acc
 
     def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None,
-                 final_renorm: bool = True, min_level=None):
+                 final_renorm: bool = True):
         """final_renorm=False returns the last XOR pair before its renorm (and without the final
-        bootstrap): true-FHE decrypt applies the next round's InvShiftRows there first.
-        min_level: the level the caller needs the result at (its next step a secret-key renorm: the
-        final bootstrap may take the low-level sparse form)"""
+        bootstrap): true-FHE decrypt applies the next round's InvShiftRows there first"""
         log = (lambda k, v: debug.__setitem__(k, v)) if debug is not None else (lambda k, v: None)
         steps = [-4 * k * self.stride for k in (1, 2, 3)]  # _col_shift_rowmajor(ct, k), hoisted
         rh, rl = rot_pair(self.ctx, ct_hi, ct_lo, steps)
@@ -138,6 +136,6 @@ class InvMixColumnsFHE:
                 return self._xor_pair(x1, x2, fl)
             out = self._renorm_pair(*self._xor_pair(x1, x2, fl), level=last)
         if do_final_bootstrap and self.enc.renorm_hook is None:
-            out = bootstrap2(self.ctx, out[0], out[1], self.layout.boot_period, min_level=min_level)
+            out = bootstrap2(self.ctx, out[0], out[1], self.layout.boot_period)
         log("out", out)
         return out

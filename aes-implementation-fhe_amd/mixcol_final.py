@@ -179,11 +179,11 @@ class MixColFinal:
             return self.xor4.apply_pair(a[0], b[0], a[1], b[1], out_level)
         return pair(self.ctx, lambda: self._xor_ct(a[0], b[0], out_level), lambda: self._xor_ct(a[1], b[1], out_level))
 
-    def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None, min_level=None):
+    def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
         steps = [-4 * k * self.stride for k in (1, 2, 3)]  # _col_shift_rowmajor(ct, k), hoisted
         rh, rl = rot_pair(self.ctx, ct_hi, ct_lo, steps)
         rot = {k: (rh[k - 1], rl[k - 1]) for k in (1, 2, 3)}
-        return self.mix_rotated((ct_hi, ct_lo), rot, do_final_bootstrap, debug, min_level=min_level)
+        return self.mix_rotated((ct_hi, ct_lo), rot, do_final_bootstrap, debug)
 
     # ---------------------------------------------------------------- packed XOR stage
     def packed_ok(self) -> bool:
@@ -193,7 +193,7 @@ class MixColFinal:
         return (self.layout.packable and self.enc.renorm_hook is None and getattr(ctx, "fused_luts", False)
                 and getattr(ctx, "renorm_unpack", None) is not None)
 
-    def mix_packed(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, min_level=None):
+    def mix_packed(self, ct_hi, ct_lo, do_final_bootstrap: bool = True):
         """MixColumns with its XOR stage on packed states (StateEncoder.pack: hi and lo side by side
         in one ciphertext, the XOR4 LUT being the same for both halves): the three XOR pairs of
         mix_rotated become three single XOR4s, their renorms single-ciphertext renorms, and the
@@ -207,9 +207,7 @@ class MixColFinal:
         only r1 shifted from the input.  AESFHE_MC_FORM=xtime computes r2 ^ r3 from shifted
         inputs (2 (x ^ r1) ^ (r1 ^ r2 ^ r3), four XOR4s, xtime being GF(2)-linear);
         AESFHE_MC_FORM=2gf keeps the reference's two multiplier pairs (GF2(x), GF3(r1)).  The
-        bytes are the same in every form.  min_level: the level the caller needs the result at (its
-        next step an AddRoundKey that is renormalised: the final bootstrap may take the low-level
-        sparse form)."""
+        bytes are the same in every form."""
         ctx, enc = self.ctx, self.enc
         fl = RENORM_FLOOR
         gl = fl + LUT2_DEPTH + enc.PACK_DEPTH
@@ -227,7 +225,7 @@ class MixColFinal:
             two, w = pair(ctx, lambda: enc.pack(*self.gf_mult_2(*u, out_level=gl)), r1_r2r3, shared=(*u, p1))
             acc = enc.renorm_packed(self._xor_ct(two, w, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
             if do_final_bootstrap:
-                acc = bootstrap1(ctx, acc, 2 * self.layout.period, min_level=min_level)
+                acc = bootstrap1(ctx, acc, 2 * self.layout.period)
             return acc
         steps = [-4 * k * self.stride for k in (1, 2, 3)]
         rh, rl = rot_pair(ctx, ct_hi, ct_lo, steps)
@@ -246,7 +244,7 @@ class MixColFinal:
                                                     level=NEED_XOR))
             acc = enc.renorm_packed(self._xor_ct(two, w, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
             if do_final_bootstrap:
-                acc = bootstrap1(ctx, acc, 2 * self.layout.period, min_level=min_level)
+                acc = bootstrap1(ctx, acc, 2 * self.layout.period)
             return acc
         two, thr = pair(ctx, lambda: self.gf_mult_2(ct_hi, ct_lo, out_level=gl),
                         lambda: self.gf_mult_3(rh[0], rl[0], out_level=gl))
@@ -256,10 +254,10 @@ class MixColFinal:
                       lambda: enc.renorm_packed(self._xor_ct(r2, r3, fl), level=NEED_XOR))
         acc = enc.renorm_packed(self._xor_ct(x1, x2, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
         if do_final_bootstrap:
-            acc = bootstrap1(ctx, acc, 2 * self.layout.period, min_level=min_level)
+            acc = bootstrap1(ctx, acc, 2 * self.layout.period)
         return acc
 
-    def mix_rotated(self, x, rot, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None, min_level=None):
+    def mix_rotated(self, x, rot, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None):
         """GF2(x) ^ GF3(r1) ^ r2 ^ r3 from the state pair x and its column shifts rot[k] = r_k
         (the rest of __call__; shiftrows_mixcolumns.py supplies ShiftRows-permuted shifts)"""
         log = (lambda k, v: debug.__setitem__(k, v)) if isinstance(debug, dict) else (lambda k, v: None)
@@ -305,6 +303,6 @@ class MixColFinal:
         out_hi, out_lo = acc
         # true-FHE mode: the renorm above already is a bootstrap (+ snap), the final one merges in
         if do_final_bootstrap and self.enc.renorm_hook is None:
-            out_hi, out_lo = bootstrap2(self.ctx, out_hi, out_lo, self.layout.boot_period, min_level=min_level)
+            out_hi, out_lo = bootstrap2(self.ctx, out_hi, out_lo, self.layout.boot_period)
             log("out", (out_hi, out_lo))
         return out_hi, out_lo

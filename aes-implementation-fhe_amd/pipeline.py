@@ -131,12 +131,6 @@ class AESPipeline:
             packed_xor = os.environ.get("AESFHE_PACKED_XOR", "1") != "0"
         self.packed_xor = bool(packed_xor and use_hard_renorm_between_steps and not true_fhe and self.srmc is None
                                and hasattr(self.mix, "packed_ok") and self.mix.packed_ok())
-        # MixColumns' final bootstrap feeds an AddRoundKey whose result is renormalised (secret-key
-        # renorm mode): its output is needed only at NEED_XOR, so the engine may run the low-level
-        # sparse bootstrap (AESFHE_BOOT_LOW=0 in the engine turns it off)
-        self._mc_floor = NEED_XOR if (use_hard_renorm_between_steps and not true_fhe) else None
-        # InvMixColumns' final bootstrap feeds a secret-key renorm directly (decrypt rounds 9..1)
-        self._imc_floor = RENORM_FLOOR if self._mc_floor is not None else None
         self._pk_cache: List[Any] | None = None
         self._pk_tag = b""
         self._kb_cache: Dict[int, Dict[str, Any]] = {}  # round -> the packed key's dropped form and std basis
@@ -282,13 +276,9 @@ class AESPipeline:
         return self.invshift.apply(ct_hi, ct_lo)
 
     def mix_columns(self, ct_hi, ct_lo):
-        if self._mc_floor is not None and isinstance(self.mix, MixColFinal):
-            return self.mix(ct_hi, ct_lo, min_level=self._mc_floor)
         return self.mix(ct_hi, ct_lo)
 
     def inv_mix_columns(self, ct_hi, ct_lo):
-        if self._imc_floor is not None and isinstance(self.invmix, InvMixColumnsFHE):
-            return self.invmix(ct_hi, ct_lo, min_level=self._imc_floor)
         return self.invmix(ct_hi, ct_lo)
 
     # ---------------------------------------------------------------- encrypt
@@ -309,7 +299,7 @@ class AESPipeline:
             self._log_pair(debug, f"enc.r{r}.sub.renorm", *ct)
             ct = self.shift_rows(*ct)
             self._log_pair(debug, f"enc.r{r}.sr", *ct)
-            acc = self.mix.mix_packed(*ct, min_level=self._mc_floor)
+            acc = self.mix.mix_packed(*ct)
             self._log_packed(debug, f"enc.r{r}.mc", acc)
             x = self._ark_packed(acc, r)
             self._log_packed(debug, f"enc.r{r}.ark", x)
@@ -412,7 +402,7 @@ class AESPipeline:
                 x = self._ark_packed(self.encoder.pack(*ct), r)
                 ct = self.encoder.renorm_unpack(x, level=NEED_GF + self.encoder.PACK_DEPTH)
                 self._log_pair(debug, f"dec.r{r}.ark", *ct)
-                ct = self.encoder.renorm_unpack(self.invmix.imc_packed(*ct, min_level=self._imc_floor), level=NEED_ISR_ISB)
+                ct = self.encoder.renorm_unpack(self.invmix.imc_packed(*ct), level=NEED_ISR_ISB)
                 self._log_pair(debug, f"dec.r{r}.imc", *ct)
                 continue
             ct = self.inv_shift_rows(*ct)

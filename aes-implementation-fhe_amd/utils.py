@@ -70,16 +70,13 @@ def pair(ctx, fa, fb, shared=(), fork=False):
     return a, b
 
 
-def bootstrap2(ctx, a, b, period=None, min_level=None):
+def bootstrap2(ctx, a, b, period=None):
     """(bootstrap(a), bootstrap(b)) of the hi / lo halves (REF/mixcol_final.py:158-162): one
     batched engine bootstrap when the context has it (identical results, shared key and
     diagonal reads), else the two calls on the two branch streams.  `period`:
-    the messages' slot period in the periodic layout -> the sparse-slot bootstrap (§4b);
-    `min_level`: the level the caller needs the results at (the low-level sparse form, §4d)"""
+    the messages' slot period in the periodic layout -> the sparse-slot bootstrap (§4b)"""
     sparse = getattr(ctx, "bootstrap_pair_sparse", None)
     if period is not None and sparse is not None:
-        if min_level is not None:
-            return sparse(ctx.to_intt(a), ctx.to_intt(b), period, min_level=min_level)
         return sparse(ctx.to_intt(a), ctx.to_intt(b), period)
     both = getattr(ctx, "bootstrap_pair", None)
     if both is not None and os.environ.get("AESFHE_BOOT_PAIR", "1") != "0":  # "0": A/B measurements
@@ -87,13 +84,10 @@ def bootstrap2(ctx, a, b, period=None, min_level=None):
     return pair(ctx, lambda: ctx.bootstrap(ctx.to_intt(a)), lambda: ctx.bootstrap(ctx.to_intt(b)))
 
 
-def bootstrap1(ctx, ct, period=None, min_level=None):
-    """bootstrap(ct); `period` < slot count: the message's slot period -> the sparse-slot bootstrap;
-    `min_level`: the level the caller needs the result at (the low-level sparse form)"""
+def bootstrap1(ctx, ct, period=None):
+    """bootstrap(ct); `period` < slot count: the message's slot period -> the sparse-slot bootstrap"""
     sparse = getattr(ctx.engine, "bootstrap_sparse", None)
     if period is not None and period < ctx.engine.slot_count and sparse is not None:
-        if min_level is not None:
-            return sparse(ctx.to_intt(ct), period, min_level=min_level)
         return sparse(ctx.to_intt(ct), period)
     return ctx.bootstrap(ctx.to_intt(ct))
 

@@ -231,16 +231,6 @@ int aesfhe_bootstrap_pair_sparse(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle
                                  aesfhe_handle* out_b);
 int aesfhe_bootstrap_pair_scaled(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, double gain, aesfhe_handle* out_a,
                                  aesfhe_handle* out_b);
-/* aesfhe_bootstrap_sparse / aesfhe_bootstrap_pair_sparse for a caller that needs the result only
- * at `min_level` (>= 0): the engine may then run the low-level sparse form (ModRaise,
- * trace and CoeffToSlot at the lowest double-prime level, EvalMod and SlotToCoeff on single-prime
- * levels; the result lands at a level >= min_level, below the fresh level).  Replaces the same
- * engine.bootstrap calls as the plain entries (REF/mixcol_final.py:158-162) where the reference's
- * next step is an AddRoundKey whose result is renormalised (REF/pipeline.py:141-150).  min_level < 0
- * (or AESFHE_BOOT_LOW=0): exactly the plain entry. */
-int aesfhe_bootstrap_sparse_floor(aesfhe_ctx* ctx, aesfhe_handle c, int period, double gain, int min_level, aesfhe_handle* out);
-int aesfhe_bootstrap_pair_sparse_floor(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int period, double gain, int min_level,
-                                       aesfhe_handle* out_a, aesfhe_handle* out_b);
 int aesfhe_bootstrap_depth(void);
 /* host self-check of the bootstrap plan: err[0] SlotToCoeff, err[1] CoeffToSlot vs the
  * canonical embedding, err[2] EvalMod Chebyshev error (no GPU needed) */
