@@ -302,8 +302,10 @@ __device__ __forceinline__ void conv_body(const ConvBatch& cb, int gi, int t0, i
         const int t = t0 + tl;
         if (t >= t1) break;
         const u32 q = s_tq[tl][0], r32 = s_tq[tl][2];
-        // plain 32x32 -> 64-bit multiply-adds (v_mad_u64_u32); y_i < q_i, w < q_t, so eight
-        // products stay below 2^64 and one fold makes room for eight more
+        // plain 32x32 -> 64-bit multiply-adds (v_mad_u64_u32); y_i < q_i < 2^30 (fully reduced)
+        // and w < q_t < 2^30, so each product is below 2^60 and the u * (-Q) start below 2^35:
+        // up to 15 sources sum below 2^64 with no fold (the conversion's kernel is VALU-bound,
+        // the fold was ~1/5 of its per-target work); only H = 16 folds once, after eight
         u64 acc[V];
 #pragma unroll
         for (int v = 0; v < V; ++v) acc[v] = (u64)u[v] * s_tq[tl][3];
@@ -312,7 +314,7 @@ __device__ __forceinline__ void conv_body(const ConvBatch& cb, int gi, int t0, i
             const u32 w = s_w[tl][i];
 #pragma unroll
             for (int v = 0; v < V; ++v) {
-                if (i == 8) acc[v] = fold64(acc[v], q, r32);
+                if (H > 15 && i == 8) acc[v] = fold64(acc[v], q, r32);
                 acc[v] += (u64)y[i][v] * w;
             }
         }
@@ -1454,6 +1456,12 @@ inline int xcd_rows_on() {
     }();
     return v;
 }
+// AESFHE_LIN_MAC_NB1=1: stacked members one per launch instead of pairs (A/B of the stacked
+// bootstrap's L2 working set: a pair's gathered c0 / ext row bands are twice a single member's)
+inline bool lin_mac_nb1() {
+    static const bool v = std::getenv("AESFHE_LIN_MAC_NB1") && std::atoi(std::getenv("AESFHE_LIN_MAC_NB1")) != 0;
+    return v;
+}
 // AESFHE_LIN_MAC_NB4=1: a four-member chunk in one launch (A/B; off: see launch_lin_mac)
 inline bool lin_mac_nb4() {
     static const bool v = std::getenv("AESFHE_LIN_MAC_NB4") && std::atoi(std::getenv("AESFHE_LIN_MAC_NB4")) != 0;
@@ -1506,7 +1514,7 @@ void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int
     }
     if (m.nb == 1) {
         launch_lin_mac_nb<1>(st, T, m, nl, ne, map, bytes);
-    } else if (m.nb == 2) {
+    } else if (m.nb == 2 && !lin_mac_nb1()) {
         launch_lin_mac_nb<2>(st, T, m, nl, ne, map, bytes);
     } else if (m.nb == 4 && lin_mac_nb4()) {
         // a stacked bootstrap chunk of four members in ONE launch (AESFHE_LIN_MAC_NB4=1, off): each
@@ -1515,12 +1523,13 @@ void launch_lin_mac(hipStream_t st, const DevTables& T, const LinMacArgs& m, int
         // 2,846 us per launch against 2 x 435 us as two pair launches (64-pair stack,
         // profiles/r5_linmac_nb4_ab.txt)
         launch_lin_mac_nb<4>(st, T, m, nl, ne, map, bytes);
-    } else if (m.nb > 2) {
+    } else if (m.nb >= 2) {
         // wider batches (a stacked bootstrap chunk of more than two members): pairs of members, one
         // launch each, every member-strided operand offset to the pair's first member
-        for (int m0 = 0; m0 < m.nb; m0 += 2) {
+        const int step = lin_mac_nb1() ? 1 : 2;
+        for (int m0 = 0; m0 < m.nb; m0 += step) {
             LinMacArgs s = m;
-            s.nb = std::min(2, m.nb - m0);
+            s.nb = std::min(step, m.nb - m0);
             const size_t qo = (size_t)m0 * m.q_ms, po = (size_t)m0 * m.p_ms;
             for (int b = 0; b < m.B; ++b) {
                 if (s.a[b]) s.a[b] += qo;

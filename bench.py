@@ -98,9 +98,9 @@ def parse():
                     help="with AESFHE_PROFILE_FROM_START=<ids>: keep the engine's per-kernel accounting from the first "
                          "launch on (no reset, every launch) and write it to this JSON file -- the algorithmic bytes of "
                          "exactly the launches a whole-process rocprofv3 --pmc pass counts")
-    ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r4_pmc_traffic_round.json"),
-                    help="per-kernel-class HBM / algorithmic byte ratios from rocprofv3 --pmc passes over one middle round "
-                         "of this bench's C2 workload (tools/gpu_task.sh pmc, tools/pmc_round.py)")
+    ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r5_pmc_traffic_bench.json"),
+                    help="per-kernel-class HBM / algorithmic byte ratios from rocprofv3 --pmc passes over this bench's own "
+                         "C2 leg (tools/gpu_task.sh pmcbench; FETCH_SIZE and raw TCC write requests, separate runs)")
     ap.add_argument("--detail-json", default="gpurun_out/bench_detail.json",
                     help="the full per-leg / per-class record (prose included) is written here; stdout carries the compact "
                          "line (<= 12 KB) that names this file; '' = do not write it")

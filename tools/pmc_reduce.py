@@ -3,7 +3,8 @@
 gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half the bytes of
 wide coalesced reads -> x2; WRITE_SIZE is exact.  Both counters are in KB.  Usage:
   python tools/pmc_reduce.py [--source=LABEL] [--alg=STATS.json] OUT.json DIR [DIR ...]   (one DIR per --pmc pass)
-Deletes the (large) CSVs after reading so gpurun can copy the result back."""
+Deletes the (large) CSVs after reading so gpurun can copy the result back.  A DIR that is an earlier
+OUT.json re-aggregates its per-kernel entries (after a change of the kernel -> class map below)."""
 import csv
 import json
 import sys
@@ -45,7 +46,7 @@ def main():
     acc = defaultdict(lambda: defaultdict(float))
     cnt = defaultdict(lambda: defaultdict(int))
     for d in dirs:
-        for f in Path(d).rglob("*counter_collection.csv"):
+        for f in ([] if d.endswith(".json") else Path(d).rglob("*counter_collection.csv")):
             with open(f) as fh:
                 head = [next(fh, "") for _ in range(3)]
                 out.with_suffix(".sample.txt").write_text("".join(head))
@@ -66,12 +67,19 @@ def main():
             cnt[k]["WRITE_SIZE"] = cnt[k].pop(RAW_WRITE[0])
             cnt[k].pop(RAW_WRITE[1], None)
     res = {}
+    for d in dirs:
+        if d.endswith(".json"):
+            res.update({k: v for k, v in json.loads(Path(d).read_text()).items()
+                        if isinstance(v, dict) and "fetch_size_bytes" in v})
+            if src is None:
+                src = json.loads(Path(d).read_text()).get("_source")
     for k in acc:
         per = {c: acc[k][c] / cnt[k][c] for c in acc[k]}
         res[k] = {"bytes_per_launch": sum(per.values()), "launches": max(cnt[k].values()),
                   **{c.lower() + "_bytes": v for c, v in per.items()}}
     # aggregate template instances under the engine's kernel ids (launch-weighted)
     ids = {"ntt1_fwd": "ntt_cols_fwd", "ntt2_fwd": "ntt_rows_fwd", "ntt2_inv": "ntt_rows_inv", "ntt1_inv": "ntt_cols_inv",
+           "ntt2_fwd8": "ntt_rows_fwd", "ntt2_inv8": "ntt_rows_inv",
            "key_inner": "key_inner", "key_inner_sum": "key_inner", "key_inner_multi": "key_inner", "ntt2_ki": "key_inner", "ntt2_ki8": "key_inner",
            "base_convert": "base_convert", "bx_cols": "base_convert", "lin_mac": "lin_mac"}
     agg = {}
