@@ -36,6 +36,17 @@ HD u32 shoup_mul(u32 a, u32 w, u32 wp, u32 q) {
     return csub(r, q);
 }
 HD u32 shoup_pre(u32 w, u32 q) { return (u32)(((u64)w << 32) / q); }
+// the same floor(w 2^32 / q) for w < q without a 64-bit division: mu = floor(2^61 / q) gives an
+// estimate at most 3 below (w mu / 2^29 = w 2^32 / q - w eps / 2^29, w < 2^30, eps < 1, plus the
+// shift's floor), then exact corrections
+HD u32 shoup_pre_mu(u32 w, u32 q, u32 mu) {
+    u32 est = (u32)(((u64)w * mu) >> 29);
+    u64 r = ((u64)w << 32) - (u64)est * q;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        if (r >= q) r -= q, ++est;
+    return est;
+}
 
 // a * b mod q for a, b < q; mu = floor(2^61 / q) (fits 32 bits since q > 2^29)
 HD u32 barrett_mul(u32 a, u32 b, u32 q, u32 mu) {

@@ -1410,6 +1410,7 @@ public:
         // k_bx_cols: the INTT's row pass here, its column pass + the conversion + the ext rows'
         // forward column pass in one launch
         const bool bx = bx_ok() && alpha <= kBxMaxH;
+        const u32* up_post = conv_pre_ && !bx ? d_modup_qh_ + modup_qh_off_[nl] : nullptr;
         if (bx) {
             const RowMap rm{nl, nb > 1 ? (int)(d_ms / n) : nl, nl, 0, 0};
             if (rev) launch_ntt_inv_rows(S(), T_, coef, d, nb * nl, rm, qmap(), nullptr, true);
@@ -1417,18 +1418,19 @@ public:
             else launch_ntt_inv_rows(S(), T_, coef, d, nb * nl, rm, qmap());
             cnt_[C_NTT_ROWS] += nb * nl;
         } else if (rev) {
-            launch_ntt_inv_rev(S(), T_, coef, d, nb * nl, RowMap{nl, nb > 1 ? (int)(d_ms / n) : nl, nl, 0, 0}, qmap());
+            launch_ntt_inv_rev(S(), T_, coef, d, nb * nl, RowMap{nl, nb > 1 ? (int)(d_ms / n) : nl, nl, 0, 0}, qmap(), up_post);
             cnt_[C_NTT_ROWS] += nb * nl;
         } else if (tp) {
-            launch_ntt_inv_prod(S(), T_, coef, *tp, nb * nl, RowMap{nl, nl, nl, 0, 0}, qmap());
+            launch_ntt_inv_prod(S(), T_, coef, *tp, nb * nl, RowMap{nl, nl, nl, 0, 0}, qmap(), up_post);
             cnt_[C_NTT_ROWS] += nb * nl;
         } else {
-            intt(coef, d, nb * nl, RowMap{nl, nb > 1 ? (int)(d_ms / n) : nl, nl, 0, 0}, qmap(), fz ? d_modup_qh_ + modup_qh_off_[nl] : nullptr);
+            intt(coef, d, nb * nl, RowMap{nl, nb > 1 ? (int)(d_ms / n) : nl, nl, 0, 0}, qmap(), fz ? d_modup_qh_ + modup_qh_off_[nl] : up_post);
         }
         u32* ext = tmp((size_t)nb * nd * ne);
         const size_t* toff = &modup_off_[(size_t)nl * hp_.dnum];
         ConvBatch up;
         up.n = nb * nd;
+        up.pre = up_post != nullptr;
         for (int m = 0; m < nb; ++m)
             for (int j = 0; j < nd; ++j) {
                 const int lo = j * alpha, h = std::min(alpha, nl - lo), gi = m * nd + j;
@@ -1469,6 +1471,10 @@ public:
     // (C2 62.1-62.5 -> 64.8-64.9 rounds/s, 11,762 -> 10,670 launches per encrypt, same box:
     // profiles/r4_ab_fused_ki_wt_ct8_auto.txt).
     bool fused_ki_ = std::getenv("AESFHE_FUSED_KI") == nullptr || std::getenv("AESFHE_FUSED_KI")[0] != '0';
+    // the base conversions' qhat_i^{-1} factors folded into the N^{-1} scaling of the INTT that makes
+    // their sources (launch_ntt_inv's post; ConvBatch::pre): k_base_convert is VALU-bound and every
+    // target chunk of a block redid those H multiplies (AESFHE_CONV_PRE=0: multiplied in the conversion)
+    bool conv_pre_ = !(std::getenv("AESFHE_CONV_PRE") && std::atoi(std::getenv("AESFHE_CONV_PRE")) == 0);
     bool fused_ki_ok() const { return fused_ki_ && !fused_conv(true) && !fused_conv(false); }
     // k_bx_cols for the ModUp / ModDown middles (AESFHE_BX_COLS=1, N = 2^16; groups of at most
     // kBxMaxH sources: the kernel keeps them in VGPRs -- 242 at 12, 2 waves / SIMD; the double-prime
@@ -1522,15 +1528,16 @@ public:
             cnt_[C_NTT_ROWS] += (size_t)npl * np;
         } else if (ys_in) {
             if (fz) throw std::runtime_error("moddown: a fused-core input needs the separate conversion");
-            launch_ntt_inv_cols(S(), T_, yp, npl * np, rows_dense(np), LimbMap{np, hp_.p_off(), 0});
+            launch_ntt_inv_cols(S(), T_, yp, npl * np, rows_dense(np), LimbMap{np, hp_.p_off(), 0}, conv_pre_ ? d_moddown_phinv_ : nullptr);
             cnt_[C_NTT_ROWS] += (size_t)npl * np;
         } else {
-            intt(yp, acc, npl * np, RowMap{np, ne, np, nl, 0}, LimbMap{np, hp_.p_off(), 0}, fz ? d_moddown_phinv_ : nullptr);
+            intt(yp, acc, npl * np, RowMap{np, ne, np, nl, 0}, LimbMap{np, hp_.p_off(), 0}, fz || conv_pre_ ? d_moddown_phinv_ : nullptr);
         }
         u32* conv = tmp((size_t)npl * nl);
         const size_t doff = moddown_off_[nl];
         ConvBatch dn;
         dn.n = npl;
+        dn.pre = conv_pre_ && !bx;
         for (int p = 0; p < npl; ++p) {
             dn.h[p] = np, dn.d0[p] = hp_.p_off(), dn.skip0[p] = 1 << 30;
             dn.src[p] = yp + (size_t)p * np * n;
@@ -1617,10 +1624,11 @@ public:
         // ModUp Q0 -> P' (the own limbs q0, q1 are read from d by the key inner product)
         const bool fz = fused_conv(true), fzd = fused_conv(false);
         u32* coef = tmp((size_t)nb * nq);
-        intt(coef, d, nb * nq, RowMap{nq, (int)(ms / n), nq, 0, 0}, qmap(), fz ? d_d2s_ + d2s_off_.up_qhinv : nullptr);
+        intt(coef, d, nb * nq, RowMap{nq, (int)(ms / n), nq, 0, 0}, qmap(), fz || conv_pre_ ? d_d2s_ + d2s_off_.up_qhinv : nullptr);
         u32* ext = tmp((size_t)nb * ne);
         ConvBatch up;
         up.n = nb;
+        up.pre = conv_pre_;
         for (int m = 0; m < nb; ++m) {
             up.h[m] = nq, up.d0[m] = 0, up.skip0[m] = 0;
             up.src[m] = coef + (size_t)m * nq * n;
@@ -1644,10 +1652,11 @@ public:
         untmp(ext, (size_t)nb * ne);
         // ModDown by P' onto (q0, q1), + add0
         u32* yp = tmp((size_t)npl * np);
-        intt(yp, acc, npl * np, RowMap{np, ne, np, nq, 0}, LimbMap{np, hp_.p_off(), 0}, fzd ? d_d2s_ + d2s_off_.dn_qhinv : nullptr);
+        intt(yp, acc, npl * np, RowMap{np, ne, np, nq, 0}, LimbMap{np, hp_.p_off(), 0}, fzd || conv_pre_ ? d_d2s_ + d2s_off_.dn_qhinv : nullptr);
         u32* conv = tmp((size_t)npl * nq);
         ConvBatch dn;
         dn.n = npl;
+        dn.pre = conv_pre_;
         for (int p = 0; p < npl; ++p) {
             dn.h[p] = np, dn.d0[p] = hp_.p_off(), dn.skip0[p] = 1 << 30;
             dn.src[p] = yp + (size_t)p * np * n;
@@ -1826,14 +1835,15 @@ public:
             cnt_[C_NTT_ROWS] += (size_t)npl * h;
         } else if (ys_in) {
             if (fz) throw std::runtime_error("moddown_rescale: a fused-core input needs the separate conversion");
-            launch_ntt_inv_cols(S(), T_, ys, npl * h, rows_dense(h), LimbMap{k, r, hp_.p_off()});
+            launch_ntt_inv_cols(S(), T_, ys, npl * h, rows_dense(h), LimbMap{k, r, hp_.p_off()}, conv_pre_ ? d_mdr_ + off + 2 * (size_t)h * r : nullptr);
             cnt_[C_NTT_ROWS] += (size_t)npl * h;
         } else {
-            intt(ys, acc, npl * h, RowMap{h, ne, h, r, 0}, LimbMap{k, r, hp_.p_off()}, fz ? d_mdr_ + off + 2 * (size_t)h * r : nullptr);
+            intt(ys, acc, npl * h, RowMap{h, ne, h, r, 0}, LimbMap{k, r, hp_.p_off()}, fz || conv_pre_ ? d_mdr_ + off + 2 * (size_t)h * r : nullptr);
         }
         u32* conv = tmp((size_t)npl * r);
         ConvBatch cb;
         cb.n = npl;
+        cb.pre = conv_pre_ && !bx;
         for (int p = 0; p < npl; ++p) {
             cb.h[p] = h, cb.d0[p] = r, cb.split[p] = k, cb.d1[p] = hp_.p_off(), cb.skip0[p] = 1 << 30;
             cb.src[p] = ys + (size_t)p * h * n;

@@ -142,7 +142,7 @@ void launch_ntt_finish(hipStream_t st, const DevTables& T, u32* out, u32* conv, 
                        unsigned dbl = 0, const u32* const* cst = nullptr, bool add_rev = false);
 // inverse NTT reading each source row in reversed coefficient order (the conjugation's permutation
 // of the source fused into the load; otherwise launch_ntt_inv)
-void launch_ntt_inv_rev(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map);
+void launch_ntt_inv_rev(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map, const u32* post = nullptr);
 // in place on rows = npoly * nl dense rows
 void launch_ntt_fwd(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map);
 void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* data, int rows, int nl, LimbMap map);
@@ -173,7 +173,8 @@ void launch_tensor_ptrs(hipStream_t st, const DevTables& T, u32* out, const Tens
 // inverse NTT of the products a[g] (.) b[g] formed on load (limb i of group g at tp.a[g] + i N and
 // tp.b[g] + i N, Barrett products as k_tensor_ptrs'): a relinearisation's third tensor polynomial
 // transformed without being written (Engine::relin_rescale_tensor)
-void launch_ntt_inv_prod(hipStream_t st, const DevTables& T, u32* dst, const TensorPtrs& tp, int rows, RowMap rm, LimbMap map);
+void launch_ntt_inv_prod(hipStream_t st, const DevTables& T, u32* dst, const TensorPtrs& tp, int rows, RowMap rm, LimbMap map,
+                         const u32* post = nullptr);
 // out = (a0 b0, a0 b1 + a1 b0, a1 b1); a, b: 2 x nl rows; out: 3 x nl rows
 // nb > 1: nb ciphertexts stacked ([m][2][nl] in, [m][3][nl] out), one launch
 void launch_tensor(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int nl, LimbMap map, int nb = 1);
@@ -235,6 +236,9 @@ struct ConvBatch {
     const u32* tab[kMaxConvGroups] = {};
     const u32* qhinv[kMaxConvGroups] = {};
     const u32* negq[kMaxConvGroups] = {};
+    // pre != 0: every group's sources are already times qhat_i^{-1} (folded into the N^{-1} scaling of
+    // the INTT that made them: launch_ntt_inv's `post`), so k_base_convert does not multiply again
+    int pre = 0;
 };
 void launch_base_convert(hipStream_t st, const DevTables& T, const ConvBatch& cb, int nt, LimbMap map);
 // the base conversion fused into the forward NTT's first pass (ntt.hip k_ntt1_fwd_conv): the

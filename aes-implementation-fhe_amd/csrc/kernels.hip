@@ -285,12 +285,13 @@ __device__ __forceinline__ void conv_body(const ConvBatch& cb, int gi, int t0, i
     u32 u[V];
     {
         u64 f[V] = {};
+        const bool pre = cb.pre != 0;  // block-uniform
 #pragma unroll
         for (int i = 0; i < H; ++i) {
             const u32 q = s_src[i][0], mu = s_src[i][1], w = s_src[i][2], wp = s_src[i][3];
 #pragma unroll
             for (int v = 0; v < V; ++v) {
-                y[i][v] = shoup_mul(y[i][v], w, wp, q);
+                if (!pre) y[i][v] = shoup_mul(y[i][v], w, wp, q);
                 f[v] += ((u64)y[i][v] * mu) >> 29;  // y_i / q_i in 32.32 fixed point (mu = 2^61 / q)
             }
         }

@@ -852,10 +852,10 @@ __global__ void __launch_bounds__(NT) k_ntt1_inv(u32* data, RowMap rm, LimbMap m
                 gs_bfly(x[k], x[k + h], t.x, t.y, q2, 0u - q);
             }
     }
-    if (post) {  // then times post[row] (a base conversion's qhat^{-1}: k_ntt1_fwd_conv)
-        const u32 pw = post[2 * blockIdx.y], pwp = post[2 * blockIdx.y + 1];
+    if (post) {  // times post[row] too (a base conversion's qhat^{-1}): ONE multiply by N^{-1} post, formed per thread
+        const u32 pw = shoup_mul(post[2 * blockIdx.y], P.ninv, P.ninv_p, q), pwp = shoup_pre_mu(pw, q, P.mu);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) ra.dst[(size_t)(g + T * k) * 256 + c] = shoup_mul(shoup_mul(x[k], P.ninv, P.ninv_p, q), pw, pwp, q);
+        for (int k = 0; k < 16; ++k) ra.dst[(size_t)(g + T * k) * 256 + c] = shoup_mul(x[k], pw, pwp, q);
     } else {
 #pragma unroll
         for (int k = 0; k < 16; ++k) ra.dst[(size_t)(g + T * k) * 256 + c] = shoup_mul(x[k], P.ninv, P.ninv_p, q);
@@ -1780,23 +1780,23 @@ void launch_ntt_inv(hipStream_t st, const DevTables& T, u32* dst, const u32* src
         default: break;
     }
 }
-void launch_ntt_inv_prod(hipStream_t st, const DevTables& T, u32* dst, const TensorPtrs& tp, int rows, RowMap rm, LimbMap map) {
+void launch_ntt_inv_prod(hipStream_t st, const DevTables& T, u32* dst, const TensorPtrs& tp, int rows, RowMap rm, LimbMap map, const u32* post) {
     if (rows <= 0) return;
     switch (T.logn) {
-        case 13: ntt_inv_t<5>(st, T, dst, nullptr, rows, rm, map, nullptr, &tp); break;
-        case 14: ntt_inv_t<6>(st, T, dst, nullptr, rows, rm, map, nullptr, &tp); break;
-        case 15: ntt_inv_t<7>(st, T, dst, nullptr, rows, rm, map, nullptr, &tp); break;
-        case 16: ntt_inv_t<8>(st, T, dst, nullptr, rows, rm, map, nullptr, &tp); break;
+        case 13: ntt_inv_t<5>(st, T, dst, nullptr, rows, rm, map, post, &tp); break;
+        case 14: ntt_inv_t<6>(st, T, dst, nullptr, rows, rm, map, post, &tp); break;
+        case 15: ntt_inv_t<7>(st, T, dst, nullptr, rows, rm, map, post, &tp); break;
+        case 16: ntt_inv_t<8>(st, T, dst, nullptr, rows, rm, map, post, &tp); break;
         default: break;
     }
 }
-void launch_ntt_inv_rev(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map) {
+void launch_ntt_inv_rev(hipStream_t st, const DevTables& T, u32* dst, const u32* src, int rows, RowMap rm, LimbMap map, const u32* post) {
     if (rows <= 0) return;
     switch (T.logn) {
-        case 13: ntt_inv_t<5>(st, T, dst, src, rows, rm, map, nullptr, nullptr, true); break;
-        case 14: ntt_inv_t<6>(st, T, dst, src, rows, rm, map, nullptr, nullptr, true); break;
-        case 15: ntt_inv_t<7>(st, T, dst, src, rows, rm, map, nullptr, nullptr, true); break;
-        case 16: ntt_inv_t<8>(st, T, dst, src, rows, rm, map, nullptr, nullptr, true); break;
+        case 13: ntt_inv_t<5>(st, T, dst, src, rows, rm, map, post, nullptr, true); break;
+        case 14: ntt_inv_t<6>(st, T, dst, src, rows, rm, map, post, nullptr, true); break;
+        case 15: ntt_inv_t<7>(st, T, dst, src, rows, rm, map, post, nullptr, true); break;
+        case 16: ntt_inv_t<8>(st, T, dst, src, rows, rm, map, post, nullptr, true); break;
         default: break;
     }
 }
