@@ -31,7 +31,7 @@ class EngineContext:
                  use_multiparty: bool = False, mode: str = "cpu", device_id: int = 0,
                  thread_count: int | None = None, log_n: int = 16, dnum: int | None = None, seed: int | bytes | None = None,
                  lazy: bool = True, concurrent: bool = False, fused_luts: bool = True, allow_insecure: bool = False,
-                 enc_nonce: int | None = None):
+                 enc_nonce: int | None = None, defer_calls: bool | None = None):
         # REF/engine_context.py:17-42: signature selects the engine constructor form
         if signature == 1:
             kw = dict(use_bootstrap=use_bootstrap, max_level=_SIG_DEFAULT_LEVEL)
@@ -44,7 +44,7 @@ class EngineContext:
         self.signature = signature
         self.engine = Engine(mode=mode, use_multiparty=use_multiparty, thread_count=thread_count or 0,
                              device_id=device_id, log_n=log_n, dnum=dnum, seed=seed, lazy=lazy,
-                             concurrent=concurrent, allow_insecure=allow_insecure, enc_nonce=enc_nonce, **kw)
+                             concurrent=concurrent, allow_insecure=allow_insecure, enc_nonce=enc_nonce, defer_calls=defer_calls, **kw)
         eng = self.engine
         # REF/engine_context.py:44-50
         self.secret_key = eng.create_secret_key()

@@ -542,14 +542,16 @@ def run_ref_calls(coeffs, rks, args, rank, world, dist, local, seed, tj: dict, l
     reference's own call sequence -- every LUT as REF's per-term product loop (fused_luts=False:
     REF/xor4_lut.py:71-73, REF/sub_bytes_lut.py:66-71, REF/mixcol_final.py:80-91), the reference
     slot layout (byte i at slot i*N/32) with full-slot bootstraps (REF/mixcol_final.py:158-162).
-    lazy=False: every ct x ct product relinearised and rescaled at once (REF/engine_context.py:65-68,
-    VERDICT r3 item 7); lazy=True: the engine's default deferred evaluation under the
-    same calls.  The throughput a caller gets by swapping the import line and
-    changing nothing else."""
+    lazy=False: every call executed when it is made, every ct x ct product relinearised and rescaled at
+    once (REF/engine_context.py:65-68, VERDICT r3 item 7: no deferred calls, no deferred evaluation);
+    lazy=True: the engine's defaults under the same calls -- deferred call sequences
+    and deferred evaluation.  The throughput a caller gets by
+    swapping the import line and changing nothing else."""
     from engine_context import EngineContext
     from oracle import aes_plain  # checker only, after the timed region
     from pipeline import AESPipeline
-    ctx = EngineContext(signature=1, max_level=17, thread_count=1, device_id=local, seed=seed, lazy=lazy, fused_luts=False)
+    ctx = EngineContext(signature=1, max_level=17, thread_count=1, device_id=local, seed=seed, lazy=lazy, fused_luts=False,
+                        defer_calls=lazy)
     pipe = AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=True, periodic=False)
     steps = args.deferred_steps if lazy else args.eager_steps
     sts = rank_states(rank + (4000 if lazy else 3000), 1 + steps)
@@ -574,7 +576,7 @@ def run_ref_calls(coeffs, rks, args, rank, world, dist, local, seed, tj: dict, l
     done = steps * world
     out = {"workload": "C2 through EngineContext with the reference's call sequence: per-term LUT product loops, reference "
                        "slot layout, full-slot bootstraps, " + ("deferred relinearise/rescale (engine default)" if lazy else
-                                                                "eager relinearise + rescale per product"),
+                                                                "every call executed as made, eager relinearise + rescale per product"),
            "rounds_per_s": 10.0 * done / elapsed, "ms_per_step": elapsed / steps * 1e3,
            "steps": steps, "verified_against_plaintext_model": bool(ok),
            "op_counts_per_round": {k: v / (10.0 * steps) for k, v in counters.items()},
