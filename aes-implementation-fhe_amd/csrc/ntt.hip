@@ -1333,11 +1333,8 @@ __global__ void __launch_bounds__(256) k_ntt2_ki(KiArgs a, LimbMap map, const Pr
 }
 // k_ntt2_ki's work with 8 residues per thread (the row-pass helpers ki8_*: top of this file); the same arguments, block -> (member,
 // limb, 8-row chunk) with the same XCD grouping of a chunk's members
-#ifndef AESFHE_KI8_PF
-#define AESFHE_KI8_PF 0
-#endif
 template <int LOGR1>
-__global__ void __launch_bounds__(256, AESFHE_KI8_PF ? 3 : 1) k_ntt2_ki8(KiArgs a, LimbMap map, const PrimeConst* pc, const uint2* tw, const uint2* itw,
+__global__ void __launch_bounds__(256) k_ntt2_ki8(KiArgs a, LimbMap map, const PrimeConst* pc, const uint2* tw, const uint2* itw,
                                                   const uint2* irow, const uint2* igam, unsigned long long* ts) {
     constexpr int LOGN = LOGR1 + 8, CH = (1 << LOGR1) / 8;  // 8-row chunks per limb
     __shared__ u32 sm[8 * kPitch8];
@@ -1374,13 +1371,6 @@ __global__ void __launch_bounds__(256, AESFHE_KI8_PF ? 3 : 1) k_ntt2_ki8(KiArgs 
             u32 e[8];
             const u32* kb = a.key[src] + (((size_t)jd * 2 * a.nkey + krow) << LOGN) + c0;
             const u32* ka = kb + ((size_t)a.nkey << LOGN);
-#if AESFHE_KI8_PF
-            // (build-time A/B) the digit's key residues loaded before its row pass: their latency
-            // overlaps the transform instead of following it
-            uint4 kv[4];
-            kv[0] = reinterpret_cast<const uint4*>(kb)[0], kv[1] = reinterpret_cast<const uint4*>(kb)[1];
-            kv[2] = reinterpret_cast<const uint4*>(ka)[0], kv[3] = reinterpret_cast<const uint4*>(ka)[1];
-#endif
             if (jd == own) {  // block-uniform: the digit's own limb comes from the NTT-form input
                 if (a.fold.ta[0]) {  // tensor mode: c2 = a1 (.) b1 of the product, formed here
                     const size_t at = ((size_t)(a.fold.tnl + x) << LOGN) + c0;
@@ -1410,11 +1400,7 @@ __global__ void __launch_bounds__(256, AESFHE_KI8_PF ? 3 : 1) k_ntt2_ki8(KiArgs 
             }
 #pragma unroll
             for (int i = 0; i < 2; ++i) {
-#if AESFHE_KI8_PF
-                const uint4 vb = kv[i], va = kv[2 + i];
-#else
                 const uint4 vb = reinterpret_cast<const uint4*>(kb)[i], va = reinterpret_cast<const uint4*>(ka)[i];
-#endif
                 s0[4 * i] += (u64)e[4 * i] * vb.x, s1[4 * i] += (u64)e[4 * i] * va.x;
                 s0[4 * i + 1] += (u64)e[4 * i + 1] * vb.y, s1[4 * i + 1] += (u64)e[4 * i + 1] * va.y;
                 s0[4 * i + 2] += (u64)e[4 * i + 2] * vb.z, s1[4 * i + 2] += (u64)e[4 * i + 2] * va.z;
