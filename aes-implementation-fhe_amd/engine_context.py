@@ -269,7 +269,7 @@ class EngineContext:
         """Engine-side coefficient set of a LUT polynomial, created once per coefficient CONTENT
         (a digest of the coefficients, their shape and c0).  `key` is the caller's label only: a
         label built from id() can be inherited by a new object with other coefficients once the old
-        one is collected (the stale-set failure of DESIGN.md §9), and keying by content lets every
+        one is collected (the stale-set failure of DESIGN_HISTORY.md §B), and keying by content lets every
         module with the same set share one device copy.
         `owner` (the SubBytes / XOR4 / GF module object using the set): the set is evicted, and its
         device memory released (aesfhe_lut_free), once every owner holding it has been collected

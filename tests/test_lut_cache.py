@@ -1,6 +1,6 @@
 """EngineContext.lut keys its cache by a digest of the coefficient content only: callers
 label sets with id(), which Python reuses once an object is collected, and a stale
-coefficient set was the cause of an intermittent all-states-wrong packed run.
+coefficient set was the cause of an intermittent all-states-wrong packed run (DESIGN_HISTORY.md §B).
 CPU-only: the engine is replaced by a recorder."""
 import gc
 
