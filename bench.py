@@ -111,7 +111,9 @@ def dist_setup(want: int):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # AESFHE_FORCE_DIST=1 (under torch.distributed.run): the process group even for one rank, so the
+    # RCCL path (key broadcast, barriers, max-over-ranks, all_gather) runs on a one-GPU box
+    if world > 1 or (os.environ.get("AESFHE_FORCE_DIST") == "1" and "MASTER_PORT" in os.environ):
         import torch
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -123,7 +125,9 @@ def dist_setup(want: int):
             local = local % ndev
         if backend == "nccl":
             torch.cuda.set_device(local)
-        dist.init_process_group(backend=backend)
+            dist.init_process_group(backend=backend, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend=backend)
         return rank, world, local, dist
     if want > 1:
         raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one process per GPU)")

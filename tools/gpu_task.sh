@@ -11,6 +11,7 @@
 #   pmc                     FETCH_SIZE / WRITE_SIZE passes (separate runs) over the C2 leg, reduced to
 #                           per-class traffic / algorithmic bytes (tools/pmc_reduce.py)
 #   pmcbench                FETCH_SIZE / WRITE_SIZE passes over the bench's C2 leg itself (not a one-round proxy)
+#   rccl1                   torchrun --nproc-per-node=1 bench.py with AESFHE_FORCE_DIST=1: the RCCL process-group path
 #   twogpu                  torchrun --nproc-per-node=2 bench.py --gpus 2 over gloo on ONE MI355X (both ranks
 #                           share it): the N > 1 engine path at the C4 / C5 per-rank shapes
 #   boot                    tools/boot_phases.py 32 (sparse bootstrap phases)
@@ -77,6 +78,12 @@ for t in "$@"; do
       AESFHE_DIST_BACKEND=gloo timeout -k 10 900 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr=127.0.0.1 \
           --master-port=29517 bench.py --gpus 2 --steps 3 --warmup 1 --no-cpu-baseline --batch-states 1024 --c5-states 256 \
           --pair-states 0 --packed-pairs 0 --true-fhe-steps 0 --eager-steps 0 --deferred-steps 0 > $O/bench_2rank_1gpu.json 2> $O/twogpu.err ;;
+    rccl1)
+      # the RCCL ("nccl") process-group path of bench.py on ONE MI355X: one rank under torch.distributed.run
+      # with AESFHE_FORCE_DIST=1 (key broadcast, barriers, all_gather and max-over-ranks as GPU tensors)
+      AESFHE_FORCE_DIST=1 timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node=1 --master-addr=127.0.0.1 \
+          --master-port=29531 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline --batch-states 256 --c5-states 256 \
+          --pair-states 0 --packed-pairs 0 --true-fhe-steps 0 --eager-steps 0 --deferred-steps 0 > $O/bench_rccl_1rank.json 2> $O/rccl1.err ;;
     boot)
       timeout -k 10 300 python3 tools/boot_phases.py 32 > $O/boot_phases.json 2> $O/boot.err ;;
     census)
