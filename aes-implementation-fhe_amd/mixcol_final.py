@@ -16,7 +16,7 @@ import numpy as np
 
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
-from xor4_lut import XOR4LUT, SplitLUT2, batched, eval_many, eval_two, joint_bases, powers, std_basis
+from xor4_lut import XOR4LUT, SplitLUT2, batched, eval_two, joint_bases, powers, std_basis
 from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, can_fork, drop_to, fused_lut, pair, rot_many, rot_pair
 
 # AESFHE_SHARE_R1=0: MixColumns' r1 basis rebuilt in its second XOR4 (A/B runs)
@@ -129,11 +129,6 @@ def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo, out_level=Non
                 lambda: gf_eval(ctx, cache, mult, "lo", ct_hi, ct_lo), shared=(ct_hi, ct_lo))
 
 
-# AESFHE_MC_JOINT=0: the rot form's two branches (GF multipliers of u, XOR4 of R^2 u with r1) run
-# one after the other instead of through _gf2_xor_joint (A/B runs)
-_MC_JOINT = os.environ.get("AESFHE_MC_JOINT", "1") != "0"
-
-
 class MixColFinal:
     def __init__(self, ctx, xor4: XOR4LUT, stride: int | None = None, states: int = 1, layout=None):
         self.ctx = ctx
@@ -198,37 +193,6 @@ class MixColFinal:
         return (self.layout.packable and self.enc.renorm_hook is None and getattr(ctx, "fused_luts", False)
                 and getattr(ctx, "renorm_unpack", None) is not None)
 
-    def joint_extra(self) -> int:
-        """levels the packed rot form's joint stage wants on its input beyond mix_packed's usual
-        need (AESPipeline adds them to the renorm before ShiftRows): 1 when _gf2_xor_joint runs"""
-        ctx = self.ctx
-        form = os.environ.get("AESFHE_MC_FORM", "rot")
-        ok = (_MC_JOINT and form == "rot" and isinstance(self.xor4, XOR4LUT) and getattr(ctx, "fused_luts", False)
-              and batched(ctx) and not can_fork(ctx))
-        return self.enc.PACK_DEPTH if ok else 0
-
-    def _gf2_xor_joint(self, u, pv, p1, lv):
-        """(gf_mult_2 pair of u, XOR4(pv, p1)), the two independent branches of the rot form, with
-        the products of all four bases in shared mul_many batches per depth and the three split
-        sums' conjugations in one conj_many (round 5): the branches ran one after the other, each
-        a chain of small key switches at one level.  u, pv, p1 dropped to lv first; None if a
-        fused form is unavailable (the caller then runs the branches separately)"""
-        ctx = self.ctx
-        u = (drop_to(ctx, u[0], lv), drop_to(ctx, u[1], lv))
-        pv, p1 = drop_to(ctx, pv, lv), drop_to(ctx, p1, lv)
-        if any(getattr(c, "level", lv) != lv for c in (*u, pv, p1)):
-            return None
-        sh, sl, sx = self._coeffs.split(2, "hi"), self._coeffs.split(2, "lo"), self.xor4.split()
-        try:
-            A, B, XA, XB = joint_bases(ctx, [(u[0], sh.need_a | sl.need_a, "pow"), (u[1], sh.need_b | sl.need_b, "std"),
-                                             (pv, sx.need_a, "pow"), (p1, sx.need_b, "std")])
-        except RuntimeError as e:
-            if "level" not in str(e):
-                raise
-            return None
-        out = eval_many(ctx, [(sh, ("gf", 2, "hi"), A, B), (sl, ("gf", 2, "lo"), A, B), (sx, "xor4", XA, XB)])
-        return None if out is None else ((out[0], out[1]), out[2])
-
     def mix_packed(self, ct_hi, ct_lo, do_final_bootstrap: bool = True):
         """MixColumns with its XOR stage on packed states (StateEncoder.pack: hi and lo side by side
         in one ciphertext, the XOR4 LUT being the same for both halves): the three XOR pairs of
@@ -252,21 +216,7 @@ class MixColFinal:
             s1 = -4 * self.stride
             (rh1,), (rl1,) = rot_pair(ctx, ct_hi, ct_lo, [s1])
             p1, p0 = pair(ctx, lambda: enc.pack(rh1, rl1), lambda: enc.pack(ct_hi, ct_lo), shared=(ct_hi, ct_lo, rh1, rl1))
-            extra = self.joint_extra()
-            u = enc.renorm_unpack(self._xor_ct(p0, p1, fl), level=gl + LUT2_DEPTH + extra)
-            if extra:
-                # joint stage: R^2 u packed at the GF multipliers' input level gl + LUT2_DEPTH, so that
-                # both branches' bases share their key switches (_gf2_xor_joint)
-                lv = gl + LUT2_DEPTH
-                (vh,), (vl,) = rot_pair(ctx, u[0], u[1], [2 * s1])
-                got = self._gf2_xor_joint(u, enc.pack(vh, vl), p1, lv)
-                if got is not None:
-                    (gh, glo), w0 = got
-                    two, w = enc.pack(gh, glo), enc.renorm_packed(w0, level=NEED_XOR)
-                    acc = enc.renorm_packed(self._xor_ct(two, w, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
-                    if do_final_bootstrap:
-                        acc = bootstrap1(ctx, acc, 2 * self.layout.period)
-                    return acc
+            u = enc.renorm_unpack(self._xor_ct(p0, p1, fl), level=gl + LUT2_DEPTH)
 
             def r1_r2r3():
                 # R^2 u = r2 ^ r3, shifted at the level its pack + XOR4 need (gl), not u's

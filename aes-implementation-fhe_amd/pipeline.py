@@ -145,12 +145,6 @@ class AESPipeline:
         if (use_hard_renorm_between_steps and not true_fhe and fresh is not None and getattr(ctx, "fused_luts", False)
                 and os.environ.get("AESFHE_SB_BIV", "1") != "0"):
             self.need_sub = min(NEED_SUBBYTES + 1, fresh)
-        # the level the renorm before ShiftRows hands the packed MixColumns (+1 for its joint stage,
-        # MixColFinal.joint_extra), never above the fresh level
-        self.need_sr_mix_packed = NEED_SR_MIX + self.encoder.PACK_DEPTH
-        if self.packed_xor and fresh is not None:
-            extra = getattr(self.mix, "joint_extra", None)
-            self.need_sr_mix_packed = min(self.need_sr_mix_packed + (extra() if extra else 0), fresh)
 
     # ---------------------------------------------------------------- utils
     def _renorm_pair(self, hi, lo, level=None):
@@ -301,7 +295,7 @@ class AESPipeline:
             # the hi | lo halves), so the golden stage test observes the headline path itself.
             ct = self.sub.apply(*ct, out_level=self._floor())
             self._log_pair(debug, f"enc.r{r}.sub", *ct)
-            ct = self._renorm_pair(*ct, level=self.need_sr_mix_packed)
+            ct = self._renorm_pair(*ct, level=NEED_SR_MIX + self.encoder.PACK_DEPTH)
             self._log_pair(debug, f"enc.r{r}.sub.renorm", *ct)
             ct = self.shift_rows(*ct)
             self._log_pair(debug, f"enc.r{r}.sr", *ct)
