@@ -129,6 +129,11 @@ def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo, out_level=Non
                 lambda: gf_eval(ctx, cache, mult, "lo", ct_hi, ct_lo), shared=(ct_hi, ct_lo))
 
 
+# AESFHE_MC_GF_LOW: the rot form's GF multiplier pair at the XOR4 level with an extra renorm of its
+# packed output (1), or at its own depth above the last XOR4 with no renorm (0)
+_MC_GF_LOW = os.environ.get("AESFHE_MC_GF_LOW", "1") != "0"
+
+
 class MixColFinal:
     def __init__(self, ctx, xor4: XOR4LUT, stride: int | None = None, states: int = 1, layout=None):
         self.ctx = ctx
@@ -193,6 +198,14 @@ class MixColFinal:
         return (self.layout.packable and self.enc.renorm_hook is None and getattr(ctx, "fused_luts", False)
                 and getattr(ctx, "renorm_unpack", None) is not None)
 
+    def packed_input_need(self) -> int:
+        """the level mix_packed needs on its (ShiftRows') output: NEED_XOR + PACK_DEPTH when the rot
+        form's GF multipliers run low (_MC_GF_LOW: every XOR4 input is a pack of the input or of a
+        renormalised ciphertext), else NEED_GF + PACK_DEPTH (the GF pair on the input's level chain)"""
+        if _MC_GF_LOW and os.environ.get("AESFHE_MC_FORM", "rot") == "rot":
+            return NEED_XOR + self.enc.PACK_DEPTH
+        return NEED_XOR + LUT2_DEPTH + self.enc.PACK_DEPTH
+
     def mix_packed(self, ct_hi, ct_lo, do_final_bootstrap: bool = True):
         """MixColumns with its XOR stage on packed states (StateEncoder.pack: hi and lo side by side
         in one ciphertext, the XOR4 LUT being the same for both halves): the three XOR pairs of
@@ -216,6 +229,22 @@ class MixColFinal:
             s1 = -4 * self.stride
             (rh1,), (rl1,) = rot_pair(ctx, ct_hi, ct_lo, [s1])
             p1, p0 = pair(ctx, lambda: enc.pack(rh1, rl1), lambda: enc.pack(ct_hi, ct_lo), shared=(ct_hi, ct_lo, rh1, rl1))
+            if _MC_GF_LOW:
+                # the GF multiplier pair five levels lower (inputs at gl instead of gl + LUT2_DEPTH) and its
+                # packed output renormalised before the last XOR4: a renorm costs less than the pair's
+                # key switches and LUT sums at five more limbs; u at gl serves both branches (round 5)
+                u = enc.renorm_unpack(self._xor_ct(p0, p1, fl), level=gl)
+
+                def r1_r2r3_low():
+                    (vh,), (vl,) = rot_pair(ctx, u[0], u[1], [2 * s1])
+                    return enc.renorm_packed(self._xor_ct(enc.pack(vh, vl), p1, fl), level=NEED_XOR)
+                two, w = pair(ctx, lambda: enc.renorm_packed(enc.pack(*self.gf_mult_2(*u, out_level=fl + enc.PACK_DEPTH)),
+                                                             level=NEED_XOR),
+                              r1_r2r3_low, shared=(*u, p1))
+                acc = enc.renorm_packed(self._xor_ct(two, w, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
+                if do_final_bootstrap:
+                    acc = bootstrap1(ctx, acc, 2 * self.layout.period)
+                return acc
             u = enc.renorm_unpack(self._xor_ct(p0, p1, fl), level=gl + LUT2_DEPTH)
 
             def r1_r2r3():

@@ -53,7 +53,7 @@ from shift_rows import shift_rows_bytes
 from shiftrows_mixcolumns import ShiftRowsMixColumnsFusedEnc
 from sub_bytes_ark import SubBytesARK
 from sub_bytes_lut import SubBytesLUT
-from utils import (pair, NEED_GF, NEED_ISR_ISB, NEED_SR_ARK, NEED_SR_MIX, NEED_SUB_ARK_SR, NEED_SUBBYTES, NEED_XOR,
+from utils import (pair, SHIFTROWS_DEPTH, NEED_GF, NEED_ISR_ISB, NEED_SR_ARK, NEED_SR_MIX, NEED_SUB_ARK_SR, NEED_SUBBYTES, NEED_XOR,
                    RENORM_FLOOR)
 from xor4_lut import XOR4LUT
 
@@ -295,7 +295,8 @@ class AESPipeline:
             # the hi | lo halves), so the golden stage test observes the headline path itself.
             ct = self.sub.apply(*ct, out_level=self._floor())
             self._log_pair(debug, f"enc.r{r}.sub", *ct)
-            ct = self._renorm_pair(*ct, level=NEED_SR_MIX + self.encoder.PACK_DEPTH)
+            need = getattr(self.mix, "packed_input_need", None)
+            ct = self._renorm_pair(*ct, level=(need() + SHIFTROWS_DEPTH) if need else NEED_SR_MIX + self.encoder.PACK_DEPTH)
             self._log_pair(debug, f"enc.r{r}.sub.renorm", *ct)
             ct = self.shift_rows(*ct)
             self._log_pair(debug, f"enc.r{r}.sr", *ct)
