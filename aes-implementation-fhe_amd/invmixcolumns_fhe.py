@@ -4,13 +4,18 @@ are mutually inverse.  Renorm after each XOR pair when use_hard_renorm (default 
 """
 from __future__ import annotations
 
+import os
 from typing import Any, Dict, List
 
 from mixcol_final import _CoeffCache, gf_basis16, gf_eval, gf_mult_pair
 from shift_rows import row_masks
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT
-from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, pair, rot_many, rot_pair
+from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_GF, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, pair, rot_many, rot_pair
+
+# AESFHE_IMC_GF_LOW=0: the packed InvMixColumns' GF multiplier pairs at their own depth above the XOR4s
+# (inputs at NEED_GF + PACK_DEPTH) instead of at the XOR4 level with renormalised outputs (A/B runs)
+_IMC_GF_LOW = os.environ.get("AESFHE_IMC_GF_LOW", "1") != "0"
 
 
 class InvMixColumnsFHE:
@@ -78,6 +83,10 @@ class InvMixColumnsFHE:
         return (self.use_hard_renorm and self.layout.packable and self.enc.renorm_hook is None
                 and getattr(self.ctx, "fused_luts", False) and getattr(self.ctx, "renorm_unpack", None) is not None)
 
+    def packed_input_need(self) -> int:
+        """the level imc_packed needs on its input pair: the GF multipliers' input level"""
+        return (NEED_XOR if _IMC_GF_LOW else NEED_GF) + self.enc.PACK_DEPTH
+
     def imc_packed(self, ct_hi, ct_lo, do_final_bootstrap: bool = True):
         """InvMixColumns with its XOR stage on packed states (MixColFinal.mix_packed):
         the four GF multiplier pairs' outputs packed (inputs one level higher than __call__'s),
@@ -88,7 +97,12 @@ class InvMixColumnsFHE:
         rh, rl = rot_pair(ctx, ct_hi, ct_lo, steps)
         fl = RENORM_FLOOR
         gl = fl + LUT2_DEPTH + enc.PACK_DEPTH
-        gf = lambda m, hi, lo: enc.pack(*self._gf(m, hi, lo, gl))
+        if _IMC_GF_LOW:
+            # the GF multiplier pairs at the XOR4 level, each packed output renormalised (as
+            # MixColFinal.mix_packed's rot form, round 5): inputs at gl = packed_input_need()
+            gf = lambda m, hi, lo: enc.renorm_packed(enc.pack(*self._gf(m, hi, lo, fl + enc.PACK_DEPTH)), level=NEED_XOR)
+        else:
+            gf = lambda m, hi, lo: enc.pack(*self._gf(m, hi, lo, gl))
         p14, p11 = pair(ctx, lambda: gf(14, ct_hi, ct_lo), lambda: gf(11, rh[0], rl[0]))
         p13, p9 = pair(ctx, lambda: gf(13, rh[1], rl[1]), lambda: gf(9, rh[2], rl[2]))
         x1, x2 = pair(ctx, lambda: enc.renorm_packed(self._xor(p14, p11, fl), level=NEED_XOR),

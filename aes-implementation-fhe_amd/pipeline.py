@@ -401,7 +401,8 @@ class AESPipeline:
                 ct = self._sub_renorm(ct, inverse=True, level=NEED_XOR + self.encoder.PACK_DEPTH)
                 self._log_pair(debug, f"dec.r{r}.isb", *ct)
                 x = self._ark_packed(self.encoder.pack(*ct), r)
-                ct = self.encoder.renorm_unpack(x, level=NEED_GF + self.encoder.PACK_DEPTH)
+                need = getattr(self.invmix, "packed_input_need", None)
+                ct = self.encoder.renorm_unpack(x, level=need() if need else NEED_GF + self.encoder.PACK_DEPTH)
                 self._log_pair(debug, f"dec.r{r}.ark", *ct)
                 ct = self.encoder.renorm_unpack(self.invmix.imc_packed(*ct), level=NEED_ISR_ISB)
                 self._log_pair(debug, f"dec.r{r}.imc", *ct)
