@@ -142,9 +142,19 @@ class AESPipeline:
         # takes the bivariate giant-step form (sub_bytes_lut._outputs_biv; AESFHE_SB_BIV=0 for A/B)
         self.need_sub = NEED_SUBBYTES
         fresh = getattr(ctx.engine, "fresh_level", None)
-        if (use_hard_renorm_between_steps and not true_fhe and fresh is not None and getattr(ctx, "fused_luts", False)
+        # (Inv)SubBytes in the nibble-bivariate form (sub_bytes_lut: depth LUT2_DEPTH instead of 13) in the
+        # secret-key renorm mode: its inputs come from a renorm, so they are handed out 9 levels lower
+        for lut in (self.sub, self.isub):
+            if lut is not None and not fuse_sub_ark:
+                lut.use_nibble = bool(use_hard_renorm_between_steps and not true_fhe)
+        if self.sub.nibble_on():
+            self.need_sub = RENORM_FLOOR + self.sub.need_depth()
+        elif (use_hard_renorm_between_steps and not true_fhe and fresh is not None and getattr(ctx, "fused_luts", False)
                 and os.environ.get("AESFHE_SB_BIV", "1") != "0"):
             self.need_sub = min(NEED_SUBBYTES + 1, fresh)
+        # InvShiftRows -> InvSubBytes (decrypt): the inverse LUT's depth + the masked rotations
+        self.need_isr_isb = (RENORM_FLOOR + self.isub.need_depth() + SHIFTROWS_DEPTH
+                             if self.isub is not None and self.isub.nibble_on() else NEED_ISR_ISB)
 
     # ---------------------------------------------------------------- utils
     def _renorm_pair(self, hi, lo, level=None):
@@ -378,7 +388,7 @@ class AESPipeline:
         fuse = self.fuse_sub_ark
         if fuse and self.isub is None:
             raise KeyError("inv_sub_hi")
-        ct = self._renorm_pair(*ct, level=NEED_SUB_ARK_SR if fuse else NEED_ISR_ISB)
+        ct = self._renorm_pair(*ct, level=NEED_SUB_ARK_SR if fuse else self.need_isr_isb)
         self._log_pair(debug, "dec.init.ark10.renorm", *ct)
         for r in range(9, 0, -1):
             if fuse:
@@ -404,18 +414,18 @@ class AESPipeline:
                 need = getattr(self.invmix, "packed_input_need", None)
                 ct = self.encoder.renorm_unpack(x, level=need() if need else NEED_GF + self.encoder.PACK_DEPTH)
                 self._log_pair(debug, f"dec.r{r}.ark", *ct)
-                ct = self.encoder.renorm_unpack(self.invmix.imc_packed(*ct), level=NEED_ISR_ISB)
+                ct = self.encoder.renorm_unpack(self.invmix.imc_packed(*ct), level=self.need_isr_isb)
                 self._log_pair(debug, f"dec.r{r}.imc", *ct)
                 continue
             ct = self.inv_shift_rows(*ct)
             self._log_pair(debug, f"dec.r{r}.isr", *ct)
             ct = self._sub_renorm(ct, inverse=True, level=NEED_XOR)
             self._log_pair(debug, f"dec.r{r}.isb", *ct)
-            ct = self._ark_renorm(ct, rk[r], level=NEED_GF if self.with_inv_mix_columns else NEED_ISR_ISB)
+            ct = self._ark_renorm(ct, rk[r], level=NEED_GF if self.with_inv_mix_columns else self.need_isr_isb)
             self._log_pair(debug, f"dec.r{r}.ark", *ct)
             if self.with_inv_mix_columns:
                 # InvSubBytes' LUT needs a clean input, as SubBytes gets one after ARK in encrypt
-                ct = self._renorm_pair(*self.inv_mix_columns(*ct), level=NEED_ISR_ISB)
+                ct = self._renorm_pair(*self.inv_mix_columns(*ct), level=self.need_isr_isb)
                 self._log_pair(debug, f"dec.r{r}.imc", *ct)
         if fuse:
             ct = self.isbark(*ct, *self._fused_key(round_keys, 0, -1))

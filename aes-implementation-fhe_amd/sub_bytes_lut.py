@@ -22,9 +22,53 @@ import os
 from typing import Any, Dict, Tuple
 
 import numpy as np
-from utils import SUBBYTES_DEPTH, can_fork, conj_many, drop_to, fused_lut, mul_many, pair
+from utils import LUT2_DEPTH, SUBBYTES_DEPTH, can_fork, conj_many, drop_to, fused_lut, mul_many, pair
 
 _TOL = 1e-12
+# AESFHE_SB_NIB=0: the pipeline keeps the reference's 8 -> 4 form (lift to b = ζ256^byte, depth 13)
+# instead of the nibble-bivariate form (depth LUT2_DEPTH) in the secret-key renorm mode (A/B runs)
+_NIB = os.environ.get("AESFHE_SB_NIB", "1") != "0"
+
+
+def nibble_matrix(coef256) -> np.ndarray:
+    """the 8 -> 4 LUT sum_k a_k b^k (b = ζ256^(16h + l), REF/sub_bytes_lut.py:46-73) as the equivalent
+    bivariate sum over the nibble inputs: C[p, q] with sum_{p,q} C[p, q] ζ16^(hp + lq) = the same
+    ζ16^(out nibble) for all 256 (h, l) -- the table from the 1-D coefficients (a forward DFT,
+    F[16h + l] = sum_k a_k ζ256^((16h + l) k), ζ = e^{-2πi/n} as in coeffgen.py), then its 2-D inverse
+    DFT (coeffgen.lut_bivariate's form, the GF multipliers' coefficient layout)"""
+    a = np.zeros(256, np.complex128)
+    c = np.asarray(coef256, np.complex128)
+    a[:min(256, c.size)] = c[:256]
+    C = np.fft.ifft2(np.fft.fft(a).reshape(16, 16))
+    C[np.abs(C) < 1e-12] = 0
+    return C
+
+
+class _NibbleLUTs:
+    """the (hi, lo) output nibbles' bivariate matrices in mixcol_final._CoeffCache's interface, so
+    that mixcol_final.gf_mult_pair evaluates SubBytes as it does the GF multipliers"""
+
+    def __init__(self, hi_coeffs, lo_coeffs):
+        self.mats = {"hi": nibble_matrix(hi_coeffs), "lo": nibble_matrix(lo_coeffs)}
+        self.splits = {}
+        self.pts = {}
+
+    def matrix(self, mult, which: str) -> np.ndarray:
+        return self.mats[which]
+
+    def split(self, mult, which: str):
+        from xor4_lut import SplitLUT2
+        if which not in self.splits:
+            self.splits[which] = SplitLUT2(self.mats[which])
+        return self.splits[which]
+
+    def load_plaintexts(self, ctx, mult, which: str):
+        if which not in self.pts:
+            sc = ctx.engine.slot_count
+            M = self.mats[which]
+            self.pts[which] = {(p, q): ctx.encode(np.full(sc, M[p, q], dtype=np.complex128))
+                               for p in range(16) for q in range(16) if M[p, q] != 0}
+        return self.pts[which]
 
 
 class SubBytesLUTFastCached:
@@ -58,6 +102,26 @@ class SubBytesLUTFastCached:
             self.vec_hi[k] = self.hi[k] if k in self.pt_hi else 0
             self.vec_lo[k] = self.lo[k] if k in self.pt_lo else 0
 
+    # nibble-bivariate form (round 5): out_hi / out_lo = sum_{p,q} C[p,q] hi^p lo^q, 16 x 16 each, by the
+    # GF multipliers' machinery (two conjugate-split fused LUTs over one pair of bases):
+    # depth LUT2_DEPTH = 5 instead of 13.  Off unless the owner enables it (AESPipeline in the
+    # secret-key renorm mode: `use_nibble`)
+    use_nibble = False
+
+    def nibble_on(self) -> bool:
+        from xor4_lut import batched
+        return bool(self.use_nibble and _NIB and getattr(self.ctx, "fused_luts", False) and batched(self.ctx))
+
+    def need_depth(self) -> int:
+        """levels apply() consumes between its inputs and out_level"""
+        return LUT2_DEPTH if self.nibble_on() else SUBBYTES_DEPTH
+
+    def _apply_nibble(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:
+        from mixcol_final import gf_mult_pair
+        if not hasattr(self, "_nib"):
+            self._nib = _NibbleLUTs(self.hi, self.lo)
+        return gf_mult_pair(self.ctx, self._nib, "sbox", ct_hi, ct_lo)
+
     @staticmethod
     def _power(basis, k: int, domain: int, ctx):
         return basis[k - 1] if k <= len(basis) else ctx.conjugate(basis[domain - k - 1])
@@ -66,6 +130,11 @@ class SubBytesLUTFastCached:
         """(S_hi, S_lo)(hi, lo); out_level: the lowest level the caller needs the result at
         (inputs dropped to out_level + SUBBYTES_DEPTH first, utils.drop_to); None = as given.
         Inputs one level higher than that take the bivariate giant-step form (_outputs_biv)."""
+        if self.nibble_on():
+            if out_level is not None:
+                lv = out_level + LUT2_DEPTH
+                ct_hi, ct_lo = drop_to(self.ctx, ct_hi, lv), drop_to(self.ctx, ct_lo, lv)
+            return self._apply_nibble(ct_hi, ct_lo)
         biv = False
         if out_level is not None:
             lv = out_level + SUBBYTES_DEPTH
