@@ -35,12 +35,12 @@ for t in "$@"; do
     smoke)
       timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
     bench)
-      timeout -k 10 900 python3 bench.py ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err ;;
+      timeout -k 10 900 python3 bench.py --detail-json $O/bench_detail.json ${BENCH_ARGS:-} > $O/bench.json 2> $O/bench.err ;;
     c2)
       timeout -k 10 400 python3 bench.py --steps 12 --warmup 2 $C2 ${BENCH_ARGS:-} > $O/c2.json 2> $O/c2.err ;;
     rocwin)
       AESFHE_MARK_TIMED=1 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- \
-          python3 bench.py --steps 12 --warmup 2 $C2 > $O/bench_under_rocprof.json 2> $O/rocwin.err
+          python3 bench.py --steps 12 --warmup 2 $C2 --detail-json $O/bench_under_rocprof_detail.json > $O/bench_under_rocprof.json 2> $O/rocwin.err
       cp $O/prof/run_kernel_stats.csv $O/kernel_stats.csv
       timeout -k 10 120 python3 tools/trace_window.py $O/kernel_stats_timed.json $O/prof
       rm -f $O/prof/run_kernel_trace.csv ;;
