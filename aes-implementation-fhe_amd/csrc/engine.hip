@@ -2949,14 +2949,17 @@ public:
     // ------------------------------------------------------------------ bootstrapping
     static constexpr int kBootStc = 3, kSparseH = 32;
     // EvalMod: range K (|I| < K), r double angles, Chebyshev degree (AESFHE_BOOT_K / _R / _DEG
-    // override, for sweeps; read once per process)
+    // override, for sweeps; read once per process).  Degree 23 (27 until round 5): the same depth and
+    // the same measured error (full-slot 2.1-2.5e-4 max against 2.2-2.8e-4; the interpolation error
+    // 5e-15 against 3e-15) with fewer leaf terms, C2 +1.8 % (profiles/r5_boot_deg_ab.txt); 19 was 10x
+    // less accurate, 15 failed
     static int env_int(const char* name, int dflt) {
         const char* e = std::getenv(name);
         return e ? std::atoi(e) : dflt;
     }
     static int boot_k() { static const int v = env_int("AESFHE_BOOT_K", 12); return v; }
     static int boot_r() { static const int v = env_int("AESFHE_BOOT_R", 4); return v; }
-    static int boot_deg() { static const int v = env_int("AESFHE_BOOT_DEG", 27); return v; }
+    static int boot_deg() { static const int v = env_int("AESFHE_BOOT_DEG", 23); return v; }
     // CoeffToSlot groups (one double-prime level each; AESFHE_BOOT_CTS overrides, for sweeps)
     static int boot_cts() {
         static const int v = std::getenv("AESFHE_BOOT_CTS") ? std::atoi(std::getenv("AESFHE_BOOT_CTS")) : 3;
