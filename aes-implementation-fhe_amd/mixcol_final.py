@@ -232,12 +232,14 @@ class MixColFinal:
             if _MC_GF_LOW:
                 # the GF multiplier pair five levels lower (inputs at gl instead of gl + LUT2_DEPTH) and its
                 # packed output renormalised before the last XOR4: a renorm costs less than the pair's
-                # key switches and LUT sums at five more limbs; u at gl serves both branches (round 5)
-                u = enc.renorm_unpack(self._xor_ct(p0, p1, fl), level=gl)
+                # key switches and LUT sums at five more limbs; u at gl serves both branches (round 5).
+                # r1 is the second operand of both XOR4s at one level: its drop and std basis built once
+                kb = {} if _SHARE_R1 else None
+                u = enc.renorm_unpack(self._xor_ct(p0, p1, fl, kb), level=gl)
 
                 def r1_r2r3_low():
                     (vh,), (vl,) = rot_pair(ctx, u[0], u[1], [2 * s1])
-                    return enc.renorm_packed(self._xor_ct(enc.pack(vh, vl), p1, fl), level=NEED_XOR)
+                    return enc.renorm_packed(self._xor_ct(enc.pack(vh, vl), p1, fl, kb), level=NEED_XOR)
                 two, w = pair(ctx, lambda: enc.renorm_packed(enc.pack(*self.gf_mult_2(*u, out_level=fl + enc.PACK_DEPTH)),
                                                              level=NEED_XOR),
                               r1_r2r3_low, shared=(*u, p1))

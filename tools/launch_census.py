@@ -16,7 +16,7 @@ from aes_keyschedule import expand_aes128_key, load_all_coeffs  # noqa: E402
 from engine_context import EngineContext  # noqa: E402
 from mi355x_ckks import launch_count  # noqa: E402
 from pipeline import AESPipeline  # noqa: E402
-from utils import NEED_SR_MIX, bootstrap1  # noqa: E402
+from utils import NEED_SR_MIX, SHIFTROWS_DEPTH, bootstrap1  # noqa: E402
 
 
 def main():
@@ -48,7 +48,13 @@ def main():
 
     packed = pipe.packed_xor
     for _ in range(reps):
-        c = timed("sub_bytes+renorm", lambda: pipe._sub_renorm(ct0, level=NEED_SR_MIX + (pipe.encoder.PACK_DEPTH if packed else 0)))
+        lv = pipe.mix.packed_input_need() + SHIFTROWS_DEPTH if packed else NEED_SR_MIX  # the pipeline's own level
+
+        def sub_step():
+            out = pipe._sub_renorm(ct0, level=lv)
+            E.settle(*out)  # the step's deferred products executed inside its own timing
+            return out
+        c = timed("sub_bytes+renorm", sub_step)
         c = timed("shift_rows", pipe.shift_rows, *c)
         mix = pipe.mix.mix_packed if packed else pipe.mix
         acc = timed("mix_columns(no final bootstrap)", lambda: mix(*c, do_final_bootstrap=False))

@@ -1,6 +1,7 @@
-"""Sub-step times of MixColumns' packed rot form (mixcol_final.mix_packed, AESFHE_MC_FORM=rot) on
-one C2 state, each step synchronised (launch counts from the engine): where a round's 4.5 ms of
-MixColumns-without-bootstrap goes.  usage: python3 tools/mix_profile.py [reps] (GPU)"""
+"""Sub-step times of MixColumns' packed rot form (mixcol_final.mix_packed, AESFHE_MC_FORM=rot, with
+the GF pair at the XOR4 level: AESFHE_MC_GF_LOW) on one C2 state, each step synchronised and its
+deferred products settled inside it (launch counts from the engine): where a round's MixColumns
+without its bootstrap goes.  usage: python3 tools/mix_profile.py [reps] (GPU)"""
 import json
 import sys
 import time
@@ -15,7 +16,7 @@ from aes_keyschedule import expand_aes128_key, load_all_coeffs  # noqa: E402
 from engine_context import EngineContext  # noqa: E402
 from mi355x_ckks import launch_count  # noqa: E402
 from pipeline import AESPipeline  # noqa: E402
-from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_SR_MIX, NEED_XOR, RENORM_FLOOR, drop_to, rot_pair  # noqa: E402
+from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, SHIFTROWS_DEPTH, rot_pair  # noqa: E402
 
 
 def main():
@@ -26,7 +27,7 @@ def main():
     mix, enc = pipe.mix, pipe.encoder
     rng = np.random.default_rng(3)
     st = rng.integers(0, 256, 16, dtype=np.uint8)
-    x = enc.renorm(*enc.encode(st), level=NEED_SR_MIX + enc.PACK_DEPTH)
+    x = enc.renorm(*enc.encode(st), level=mix.packed_input_need() + SHIFTROWS_DEPTH)
     x = pipe.shift_rows(*x)
     fl = RENORM_FLOOR
     gl = fl + LUT2_DEPTH + enc.PACK_DEPTH
@@ -37,12 +38,19 @@ def main():
         l0 = launch_count()
         t0 = time.perf_counter()
         r = f()
+        flat, todo = [], [r]
+        while todo:
+            v = todo.pop()
+            if isinstance(v, (tuple, list)):
+                todo.extend(v)
+            else:
+                flat.append(v)
+        E.settle(*flat)
         E.sync()
         dt = (time.perf_counter() - t0) * 1e3
-        l1 = launch_count()
         a = times.setdefault(name, [0.0, 0, 0])
         a[0] += dt
-        a[1] += l1 - l0
+        a[1] += launch_count() - l0
         a[2] += 1
         return r
 
@@ -55,10 +63,10 @@ def main():
         p1 = step("pack r1", lambda: enc.pack(rh1, rl1))
         p0 = step("pack x", lambda: enc.pack(ct_hi, ct_lo))
         t = step("XOR4(x, r1)", lambda: mix._xor_ct(p0, p1, fl))
-        u = step("renorm_unpack u", lambda: enc.renorm_unpack(t, level=gl + LUT2_DEPTH))
-        g = step("gf_mult_2(u) pair", lambda: mix.gf_mult_2(*u, out_level=gl))
-        two = step("pack 2u", lambda: enc.pack(*g))
-        (vh,), (vl,) = step("rot R^2 u (pair)", lambda: rot_pair(ctx, drop_to(ctx, u[0], gl), drop_to(ctx, u[1], gl), [2 * s1]))
+        u = step("renorm_unpack u", lambda: enc.renorm_unpack(t, level=gl))
+        g = step("gf_mult_2(u) pair", lambda: mix.gf_mult_2(*u, out_level=fl + enc.PACK_DEPTH))
+        two = step("pack + renorm 2u", lambda: enc.renorm_packed(enc.pack(*g), level=NEED_XOR))
+        (vh,), (vl,) = step("rot R^2 u (pair)", lambda: rot_pair(ctx, u[0], u[1], [2 * s1]))
         pv = step("pack R^2 u", lambda: enc.pack(vh, vl))
         w0 = step("XOR4(R^2 u, r1)", lambda: mix._xor_ct(pv, p1, fl))
         w = step("renorm w", lambda: enc.renorm_packed(w0, level=NEED_XOR))

@@ -1,13 +1,12 @@
 set -e -o pipefail
-O=gpurun_out/${1:-r5aa}; mkdir -p $O
-PASSES=3 bash tools/env_ab.sh ${1:-r5aa} - AESFHE_BOOT_DEG=23 AESFHE_BOOT_DEG=21
+O=gpurun_out/${1:-r5ee}; mkdir -p $O
+PASSES=3 bash tools/env_ab.sh ${1:-r5ee} AESFHE_SHARE_R1=0 -
 python3 - "$O/bench.txt" <<'PY'
 import json, sys
 for ln in open(sys.argv[1]):
     cfg, js = ln.split(' ', 1)
     d = json.loads(js)
-    print(cfg, 'C2', d['value'], 'launches', d['launches_per_encrypt'], 'precision', d['precision']['margin_factor'], d['precision']['max_err_rad'])
+    print(cfg, 'C2', d['value'], 'launches', d['launches_per_encrypt'], 'precision', d['precision']['margin_factor'])
 PY
-AESFHE_BOOT_DEG=21 timeout -k 10 300 python3 tools/boot_error_probe.py > $O/boot_err_21.json 2> $O/boot_err_21.err
-python3 -c "
-import json; d=json.load(open('$O/boot_err_21.json')); print('deg 21', {k: round(v['max_err'],6) for k,v in d.items() if isinstance(v, dict) and 'max_err' in v})"
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_packed_xor.py tests/test_gpu_packed.py tests/test_gpu_aes.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
