@@ -206,21 +206,6 @@ class MixColFinal:
             return NEED_XOR + self.enc.PACK_DEPTH
         return NEED_XOR + LUT2_DEPTH + self.enc.PACK_DEPTH
 
-    def mix_packed_ttable(self, a, b, c, d, do_final_bootstrap: bool = True):
-        """MixColumns from its four terms already formed (the T-table round): a = 2 SR(S x),
-        b = R 3 SR(S x), c = R^2 SR(S x), d = R^3 SR(S x) as (hi, lo) pairs at the packing level;
-        out = (a ^ b) ^ (c ^ d): two packed XOR4s sharing their bases' key switches, their renorms,
-        one XOR4, the renorm to level 0, the sparse bootstrap.  Returns the PACKED output"""
-        ctx, enc = self.ctx, self.enc
-        fl = RENORM_FLOOR
-        pa, pb, pc, pd = (enc.pack(*x) for x in (a, b, c, d))
-        x1, x2 = self.xor4.apply_pair(pa, pb, pc, pd, fl)
-        x1, x2 = enc.renorm_packed(x1, level=NEED_XOR), enc.renorm_packed(x2, level=NEED_XOR)
-        acc = enc.renorm_packed(self._xor_ct(x1, x2, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
-        if do_final_bootstrap:
-            acc = bootstrap1(ctx, acc, 2 * self.layout.period)
-        return acc
-
     def mix_packed(self, ct_hi, ct_lo, do_final_bootstrap: bool = True):
         """MixColumns with its XOR stage on packed states (StateEncoder.pack: hi and lo side by side
         in one ciphertext, the XOR4 LUT being the same for both halves): the three XOR pairs of

@@ -57,9 +57,6 @@ from utils import (pair, SHIFTROWS_DEPTH, NEED_GF, NEED_ISR_ISB, NEED_SR_ARK, NE
                    RENORM_FLOOR)
 from xor4_lut import XOR4LUT
 
-# AESFHE_TTABLE=0: encrypt rounds through SubBytes + the rot-form MixColumns instead of the T-table round
-_TTABLE = os.environ.get("AESFHE_TTABLE", "1") != "0"
-
 
 # AESFHE_KEY_BASIS=0: the packed round keys' XOR4 bases rebuilt in every AddRoundKey (A/B runs)
 _KEY_BASIS = os.environ.get("AESFHE_KEY_BASIS", "1") != "0"
@@ -294,12 +291,6 @@ class AESPipeline:
     def inv_mix_columns(self, ct_hi, ct_lo):
         return self.invmix(ct_hi, ct_lo)
 
-    def _ttable_ok(self) -> bool:
-        """the T-table round applies: nibble-bivariate SubBytes, the pipeline's own ShiftRows and
-        MixColFinal, a batching context (AESFHE_TTABLE=0: the rot-form round, A/B runs)"""
-        return (_TTABLE and self.sub.nibble_on() and isinstance(self.shift, ShiftRows) and hasattr(self.mix, "mix_packed_ttable")
-                and getattr(self.ctx, "rotate_multi", None) is not None and hasattr(self.mix.xor4, "apply_pair"))
-
     # ---------------------------------------------------------------- encrypt
     def encrypt_round(self, ct, key_pair, debug=None, r: int = 0, next_level: int | None = None):
         """One middle round r = 1..9: SB, renorm, SR, MC, ARK, renorm (REF :142-151).  With a
@@ -307,26 +298,6 @@ class AESPipeline:
         one-round debug block, REF :154-171)."""
         if next_level is None:
             next_level = self.need_sub
-        if self.packed_xor and r > 0 and self._ttable_ok():
-            # T-table round (DESIGN.md §4f): S, 2 S and 3 S of the state from ONE pair of bases (no GF
-            # multiplier pair in MixColumns), ShiftRows and MixColumns' column shifts in one batched
-            # rotation, the XOR tree on packed states
-            outs = self.sub.apply_mults(*ct, (1, 2, 3), out_level=self._floor())
-            if outs is not None:
-                self._log_pair(debug, f"enc.r{r}.sub", *outs[0])
-                need = self.encoder.PACK_DEPTH + NEED_XOR + SHIFTROWS_DEPTH
-                s1, s2, s3 = (self._renorm_pair(*o, level=need) for o in outs)
-                self._log_pair(debug, f"enc.r{r}.sub.renorm", *s1)
-                if debug is not None:
-                    self._log_pair(debug, f"enc.r{r}.sr", *self.shift_rows(*s1))
-                a, b, c, d = self.shift.apply_shifted([(*s2, 0), (*s3, 1), (*s1, 2), (*s1, 3)])
-                acc = self.mix.mix_packed_ttable(a, b, c, d)
-                self._log_packed(debug, f"enc.r{r}.mc", acc)
-                x = self._ark_packed(acc, r)
-                self._log_packed(debug, f"enc.r{r}.ark", x)
-                ct = self.encoder.renorm_unpack(x, level=next_level)
-                self._log_pair(debug, f"enc.r{r}.ark.renorm", *ct)
-                return ct
         if self.packed_xor and r > 0:
             # packed XOR stage (DESIGN.md §4c): MixColumns returns the packed state, AddRoundKey
             # XORs it with the packed round key, its renorm unpacks into the (hi, lo) pair.  A debug

@@ -52,29 +52,6 @@ class ShiftRows:
             out = ctx.add(out, ctx.rotate(part, step) if step else part)
         return out
 
-    def apply_shifted(self, items):
-        """[R^k ShiftRows(hi, lo) for (hi, lo, k) in items], R = MixColumns' column shift (rotation by
-        -4 stride, mixcol_final.mix_packed): row r's masked part rotated by ShiftRows' step plus k
-        column shifts, every part of every item in ONE rotate_multi (the T-table round)"""
-        ctx = self.ctx
-        parts, steps = [], []
-        for hi, lo, k in items:
-            for ct in (hi, lo):
-                for r, mask in enumerate(self._pt_masks):
-                    parts.append(ctx.multiply(ct, mask))
-                    steps.append((self._rot_steps[r] + self.direction * 4 * k * self.stride) % self.sc)
-        rots = ctx.rotate_multi(list(zip(parts, steps)))
-        out = []
-        for i in range(0, len(rots), 8):
-            h = rots[i]
-            for x in rots[i + 1:i + 4]:
-                h = ctx.add(h, x)
-            lo = rots[i + 4]
-            for x in rots[i + 5:i + 8]:
-                lo = ctx.add(lo, x)
-            out.append((h, lo))
-        return out
-
     def apply(self, ct_hi: Any, ct_lo: Any):
         """both halves; with a batching context the 8 masked rows (lazy plaintext products) go
         through ONE rotate_multi -- their rescales stacked, the 6 rotations one batched key switch

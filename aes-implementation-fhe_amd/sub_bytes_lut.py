@@ -44,42 +44,12 @@ def nibble_matrix(coef256) -> np.ndarray:
     return C
 
 
-def _gf_mul(a: int, b: int) -> int:
-    out = 0
-    while b:
-        if b & 1:
-            out ^= a
-        a = ((a << 1) ^ (0x1B if a & 0x80 else 0)) & 0xFF
-        b >>= 1
-    return out
-
-
-def byte_table(hi_coeffs, lo_coeffs) -> np.ndarray:
-    """the 256-entry byte table an (hi, lo) pair of 8 -> 4 LUT coefficient vectors encodes: each
-    output nibble is the ζ16 exponent of the forward DFT of its coefficients (ζ = e^{-2πi/16})"""
-    def nib(c):
-        a = np.zeros(256, np.complex128)
-        v = np.asarray(c, np.complex128)
-        a[:min(256, v.size)] = v[:256]
-        return np.round(-np.angle(np.fft.fft(a)) * 16 / (2 * np.pi)).astype(np.int64) % 16
-    return (nib(hi_coeffs) << 4) | nib(lo_coeffs)
-
-
-def table_matrix(table, which: str) -> np.ndarray:
-    """C[p, q] with sum C[p,q] ζ16^(hp + lq) = ζ16^(nibble of table[16h + l]) (coeffgen.lut_bivariate's form)"""
-    t = np.asarray(table, np.int64).reshape(16, 16)
-    nib = (t >> 4) if which == "hi" else (t & 15)
-    C = np.fft.ifft2(np.exp(-2j * np.pi * nib / 16))
-    C[np.abs(C) < 1e-12] = 0
-    return C
-
-
 class _NibbleLUTs:
     """the (hi, lo) output nibbles' bivariate matrices in mixcol_final._CoeffCache's interface, so
     that mixcol_final.gf_mult_pair evaluates SubBytes as it does the GF multipliers"""
 
-    def __init__(self, hi_coeffs=None, lo_coeffs=None, mats=None):
-        self.mats = mats if mats is not None else {"hi": nibble_matrix(hi_coeffs), "lo": nibble_matrix(lo_coeffs)}
+    def __init__(self, hi_coeffs, lo_coeffs):
+        self.mats = {"hi": nibble_matrix(hi_coeffs), "lo": nibble_matrix(lo_coeffs)}
         self.splits = {}
         self.pts = {}
 
@@ -145,40 +115,6 @@ class SubBytesLUTFastCached:
     def need_depth(self) -> int:
         """levels apply() consumes between its inputs and out_level"""
         return LUT2_DEPTH if self.nibble_on() else SUBBYTES_DEPTH
-
-    def _mult_luts(self, m: int) -> "_NibbleLUTs":
-        """the nibble matrices of the byte map x -> m * S(x) in GF(2^8) (m = 1: S itself)"""
-        if not hasattr(self, "_mults"):
-            self._mults = {}
-        if m not in self._mults:
-            S = byte_table(self.hi, self.lo)
-            T = np.array([_gf_mul(int(y), m) for y in S], np.int64)
-            self._mults[m] = _NibbleLUTs(mats={"hi": table_matrix(T, "hi"), "lo": table_matrix(T, "lo")})
-        return self._mults[m]
-
-    def apply_mults(self, ct_hi: Any, ct_lo: Any, mults, out_level=None):
-        """[(m S_hi, m S_lo)(hi, lo) for m in mults] over ONE pair of bases (the MixColumns T-table
-        form: S, 2 S and 3 S of the state): every product of the bases in shared
-        mul_many batches, 2 len(mults) fused LUT pairs, one conj_many; None if unavailable"""
-        from xor4_lut import eval_many, joint_bases
-        if not self.nibble_on():
-            return None
-        ctx = self.ctx
-        if out_level is not None:
-            lv = out_level + LUT2_DEPTH
-            ct_hi, ct_lo = drop_to(ctx, ct_hi, lv), drop_to(ctx, ct_lo, lv)
-        luts = [self._mult_luts(m) for m in mults]
-        sp = [(L.split(m, w), ("sbox", m, w)) for L, m in zip(luts, mults) for w in ("hi", "lo")]
-        need_a = set().union(*(x.need_a for x, _ in sp))
-        need_b = set().union(*(x.need_b for x, _ in sp))
-        try:
-            A, B = joint_bases(ctx, [(ct_hi, need_a, "pow"), (ct_lo, need_b, "std")])
-        except RuntimeError as e:
-            if "level" not in str(e):
-                raise
-            return None
-        out = eval_many(ctx, [(x, key, A, B) for x, key in sp])
-        return None if out is None else [(out[2 * i], out[2 * i + 1]) for i in range(len(mults))]
 
     def _apply_nibble(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:
         from mixcol_final import gf_mult_pair

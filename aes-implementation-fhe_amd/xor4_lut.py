@@ -175,27 +175,21 @@ class SplitLUT2:
         return None if s2 is None else ctx.add(s1, ctx.conjugate(s2))
 
 
-def eval_many(ctx, jobs):
-    """split-LUT evaluations j = (split, key, A, B) as S1 + conj(S2) each, all the conjugations
-    in one conj_many batch; None if a fused sum is unavailable (level)"""
+def eval_two(ctx, j0, j1):
+    """two split-LUT evaluations j = (split, key, A, B) as S1 + conj(S2) each, the two
+    conjugations in one conj_many batch; None if a fused sum is unavailable (level)"""
     out, s2 = [], []
-    for sp, key, A, B in jobs:
+    for sp, key, A, B in (j0, j1):
         s1 = fused_lut(ctx, (key, 1), sp.c1, A, B, owner=sp)
         t2 = fused_lut(ctx, (key, 2), sp.c2, A, B, owner=sp) if sp.has2 else None
         if s1 is None or (sp.has2 and t2 is None):
             return None
         out.append(s1)
         s2.append(t2)
-    idx = [i for i, t in enumerate(s2) if t is not None]
+    idx = [i for i in (0, 1) if s2[i] is not None]
     for i, c in zip(idx, conj_many(ctx, [s2[i] for i in idx])):
         out[i] = ctx.add(out[i], c)
-    return out
-
-
-def eval_two(ctx, j0, j1):
-    """eval_many of two evaluations, as a pair (None if a fused sum is unavailable)"""
-    out = eval_many(ctx, [j0, j1])
-    return None if out is None else (out[0], out[1])
+    return out[0], out[1]
 
 
 def split_lut2(ctx, split: SplitLUT2, key, a, b, keep_b=None):
