@@ -61,6 +61,28 @@ def test_subbytes_and_inverse(coeffs):
     assert np.array_equal(back, state)
 
 
+def test_subbytes_nibble_form(coeffs):
+    """the nibble-bivariate (Inv)SubBytes (sub_bytes_lut.use_nibble) on 256 slot-packed
+    states covering every byte value: the S-box / inverse S-box bytes, the depth LUT2_DEPTH (an input
+    5 levels above out_level suffices), and a slot error far inside the decode margin"""
+    from oracle import aes_plain
+    from state_encoder import StateEncoder
+    from sub_bytes_lut import SubBytesLUT
+    from utils import LUT2_DEPTH, RENORM_FLOOR
+    ctx = gpu_context(log_n=16)
+    enc = StateEncoder(ctx, 256)
+    state = np.arange(256 * 16, dtype=np.int64).reshape(256, 16) % 256
+    state = state.astype(np.uint8)
+    for hi_c, lo_c, table in (("sub_hi", "sub_lo", aes_plain.SBOX), ("inv_sub_hi", "inv_sub_lo", aes_plain.INV_SBOX)):
+        lut = SubBytesLUT(ctx, coeffs[hi_c], coeffs[lo_c])
+        lut.use_nibble = True
+        assert lut.nibble_on() and lut.need_depth() == LUT2_DEPTH
+        hi, lo = enc.renorm(*enc.encode(state), level=RENORM_FLOOR + LUT2_DEPTH)
+        oh, ol = lut.apply(hi, lo, out_level=RENORM_FLOOR)
+        assert min(oh.level, ol.level) >= RENORM_FLOOR
+        assert np.array_equal(enc.decode(oh, ol), table[state])
+
+
 def test_shiftrows_roundtrip():
     from oracle import aes_plain
     from inv_shiftrows import InvShiftRows
