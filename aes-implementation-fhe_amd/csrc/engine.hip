@@ -3665,6 +3665,76 @@ public:
         }
         return out;
     }
+    // The same series as cheb_eval_many with its split tree flattened into a product schedule:
+    // each product T_m r is issued as soon as r's value exists, not after q's subtree.  In the
+    // degree-23 series (q' + T_8 r') + T_16 r both r' and r are leaves, so T_8 r' and T_16 r run as
+    // ONE batched multiply (same level) and the series takes one product round per level of depth
+    // (EvalMod: 10 -> 9 rounds).  Leaves, products and sums are the recursion's own operations on the
+    // same operands, so the result is bit-identical (AESFHE_CHEB_SCHED=0: the recursion, A/B).
+    std::vector<Ct> cheb_eval_sched(const std::vector<std::vector<Ct>>& T, const std::vector<std::map<int, Ct>>& giant,
+                                    const std::vector<int>& in, const std::vector<std::vector<double>>& cs) {
+        struct Node {
+            int in = 0, m = 0, q = -1, r = -1;  // m > 0: value = q + T_m r
+            std::vector<double> c;              // m == 0: a leaf's coefficients
+            Ct val, prod;
+            bool has = false, has_prod = false;
+        };
+        std::vector<Node> nd;  // parents before children (indices only: the vector grows)
+        std::function<int(int, const std::vector<double>&)> build = [&](int i, const std::vector<double>& c) -> int {
+            const int d = (int)c.size() - 1, id = (int)nd.size();
+            nd.emplace_back();
+            nd[id].in = i;
+            if (d <= kBabyDeg) {
+                nd[id].c = c;
+                return id;
+            }
+            int m = kBabyDeg;
+            while (2 * m <= d) m *= 2;
+            std::vector<double> q(m), r(d - m + 1);
+            for (int k = 0; k < m; ++k) q[k] = c[k] - (2 * m - k <= d ? c[2 * m - k] : 0.0);
+            r[0] = c[m];
+            for (int j = 1; j <= d - m; ++j) r[j] = 2.0 * c[m + j];
+            const int qi = build(i, q), ri = build(i, r);
+            nd[id].m = m, nd[id].q = qi, nd[id].r = ri;
+            return id;
+        };
+        std::vector<int> root(cs.size());
+        for (size_t i = 0; i < cs.size(); ++i) root[i] = build(in[i], cs[i]);
+        for (auto& x : nd)
+            if (x.m == 0) x.val = cheb_leaf(T[x.in], x.c), x.has = true;
+        for (;;) {
+            bool all = true;
+            for (int id : root) all = all && nd[id].has;
+            if (all) break;
+            std::vector<const Ct*> A, B;
+            std::vector<int> ids;
+            for (int k = 0; k < (int)nd.size(); ++k)
+                if (nd[k].m > 0 && !nd[k].has_prod && nd[nd[k].r].has)
+                    A.push_back(&giant[nd[k].in].at(nd[k].m)), B.push_back(&nd[nd[k].r].val), ids.push_back(k);
+            bool moved = !ids.empty();
+            if (moved) {
+                std::vector<Ct> P = mul_list(A, B);
+                for (size_t j = 0; j < ids.size(); ++j) {
+                    Node& x = nd[ids[j]];
+                    x.prod = P[j], x.has_prod = true;
+                    release(nd[x.r].val);
+                }
+            }
+            for (int k = (int)nd.size() - 1; k >= 0; --k) {  // children first: a finished sum may finish its parent
+                Node& x = nd[k];
+                if (x.m == 0 || x.has || !x.has_prod || !nd[x.q].has) continue;
+                x.val = add_sub(nd[x.q].val, x.prod, false);
+                release(nd[x.q].val);
+                release(x.prod);
+                x.has = moved = true;
+            }
+            if (!moved) throw std::runtime_error("EvalMod: Chebyshev schedule stalled");
+        }
+        std::vector<Ct> out(cs.size());
+        for (size_t i = 0; i < cs.size(); ++i) out[i] = nd[root[i]].val;
+        return out;
+    }
+    bool cheb_sched_ = env_int("AESFHE_CHEB_SCHED", 1) != 0;
     // products of a list of pairs: one batched multiply (AESFHE_EVALMOD_BATCH=0: one at a time)
     std::vector<Ct> mul_list(const std::vector<const Ct*>& A, const std::vector<const Ct*>& B, const std::vector<char>* aff = nullptr) {
         static const bool batch = env_int("AESFHE_EVALMOD_BATCH", 1) != 0;
@@ -3729,7 +3799,8 @@ public:
         }
         std::vector<int> in(ni);
         for (int i = 0; i < ni; ++i) in[i] = i;
-        std::vector<Ct> g = cheb_eval_many(T, giant, in, std::vector<std::vector<double>>(ni, c));
+        const std::vector<std::vector<double>> cs(ni, c);
+        std::vector<Ct> g = cheb_sched_ ? cheb_eval_sched(T, giant, in, cs) : cheb_eval_many(T, giant, in, cs);
         for (int i = 0; i < ni; ++i) {
             for (int k = 1; k <= kBabyDeg; ++k) release(T[i][k]);
             for (auto& kv : giant[i])
