@@ -1600,6 +1600,7 @@ public:
             untmp(ys, 2 * (size_t)np * nb);
             untmp(acc, 2 * (size_t)ne * nb);
             cnt_[C_KS] += nb;
+            tally(LV_KS, level, nb);
             return o;
         }
         u32* ext = modup(d, level, nb, d_ms);
@@ -1609,6 +1610,7 @@ public:
         Ct o = moddown(acc, level, add0, add1, nb, add_ms, dst);
         untmp(acc, 2 * (size_t)ne * nb);
         cnt_[C_KS] += nb;
+        tally(LV_KS, level, nb);
         return o;
     }
     // bootstrapping step 2: the single-limb (q0) ciphertexts' d = c1 switched to the sparse
@@ -1676,6 +1678,7 @@ public:
         untmp(conv, (size_t)npl * nq);
         untmp(acc, (size_t)npl * ne);
         cnt_[C_KS] += nb;
+        tally(LV_KS, 0, nb);
         return o;
     }
 
@@ -1755,6 +1758,7 @@ public:
         o.pend = c.pend - 1;
         o.lazy = c.lazy && o.pend > 0;
         cnt_[C_KS] += nb;
+        tally(LV_KS, l, nb);
         cnt_[C_RELIN]++;
         return o;
     }
@@ -1792,6 +1796,7 @@ public:
             untmp(ys, 2 * (size_t)h * nb);
             untmp(acc, 2 * (size_t)ne * nb);
             cnt_[C_KS] += nb;
+            tally(LV_KS, l, nb);
             cnt_[C_RELIN]++;
             return;
         }
@@ -1803,6 +1808,7 @@ public:
         (void)o;
         untmp(acc, 2 * (size_t)ne * nb);
         cnt_[C_KS] += nb;
+        tally(LV_KS, l, nb);
         cnt_[C_RELIN]++;
     }
     // device residues of the constant -c at (level, pend 0), [limb][lo, hi] (k_lincomb's cadd), cached
@@ -1909,6 +1915,7 @@ public:
                 }
                 relin_rescale_tensor(tp, x.level, x.nb, om, aff ? &af : nullptr);
                 cnt_[C_MUL]++;
+                tally(LV_MUL, o.level + 1, o.nb);
                 if (fa) release(x);
                 if (fb && y.data != x.data) release(y);
                 if (oa) release(a);
@@ -1924,6 +1931,7 @@ public:
         if (oa) release(a);
         if (ob) release(b);
         cnt_[C_MUL]++;
+        tally(LV_MUL, d.level, d.nb);
         if (!relin) return d;
         if (lazy) {
             d.lazy = true;
@@ -2054,6 +2062,7 @@ public:
                 probe.level = L, probe.npoly = 3 * std::min(chunk, g), probe.nb = std::min(chunk, g), probe.pend = 1, probe.ntt = true;
                 if (fused_tensor_ && !fused_conv(true) && fused_relin_rescale_ok(probe)) {
                     cnt_[C_MUL] += g;
+                    tally(LV_MUL, L, g);
                     for (int m0 = 0; m0 < g; m0 += chunk) {
                         const int c = std::min(chunk, g - m0);
                         TensorPtrs sub;
@@ -2076,6 +2085,7 @@ public:
             d.pend = 1;
             launch_tensor_ptrs(S(), T_, d.data, tp, g, nl, qmap());
             cnt_[C_MUL] += g;
+            tally(LV_MUL, L, g);
             for (int m0 = 0; m0 < g; m0 += chunk) {
                 const int c = std::min(chunk, g - m0);
                 Ct v = d;  // view of members m0 .. m0 + c - 1 (not released on its own)
@@ -2434,6 +2444,7 @@ public:
                 untmp(acc, (size_t)nm * 2 * ne);
                 untmp(c0p, (size_t)nm * 2 * nl);
                 cnt_[C_KS] += nm;
+                tally(LV_KS, l, nm);
             }
         }
         for (const Ct& c : owned) release(c);
@@ -2497,6 +2508,7 @@ public:
                 o.pend = c.pend;
                 o.lazy = c.pend > 0;
                 cnt_[C_KS] += nsrc;
+                tally(LV_KS, l, nsrc);
                 return o;
             }
             u32* ext = modup(c.data + (size_t)nl * n, l, nsrc, (size_t)nl * n, nullptr, true);
@@ -2510,6 +2522,7 @@ public:
             o.pend = c.pend;
             o.lazy = c.pend > 0;
             cnt_[C_KS] += nsrc;
+            tally(LV_KS, l, nsrc);
             return o;
         }
         u32* perm = tmp((size_t)k * nl);
@@ -2528,6 +2541,7 @@ public:
         o.pend = c.pend;
         o.lazy = c.pend > 0;
         cnt_[C_KS] += nsrc;
+        tally(LV_KS, l, nsrc);
         return o;
     }
 
@@ -2563,6 +2577,7 @@ public:
                 untmp(ys, 2 * (size_t)np);
                 untmp(acc, 2 * (size_t)ne);
                 cnt_[C_KS]++;
+                tally(LV_KS, c.level, 1);
                 if (c.data != c_in.data) release(c);
                 return o;
             }
@@ -2573,6 +2588,7 @@ public:
             Ct o = moddown(acc, c.level, c.data, nullptr, 1, 0, nullptr, nullptr, true);
             untmp(acc, 2 * (size_t)ne);
             cnt_[C_KS]++;
+            tally(LV_KS, c.level, 1);
             if (c.data != c_in.data) release(c);
             return o;
         }
@@ -2617,6 +2633,7 @@ public:
             untmp(acc, 2 * (size_t)ne);
             cnt_[C_ROT]++;
             cnt_[C_KS]++;
+            tally(LV_KS, l, 1);
         }
         untmp(ext, ext_rows(l));
         if (c.data != c_in.data) release(c);
@@ -3071,6 +3088,7 @@ public:
         if (x.data != x_in.data) release(x);
         cnt_[C_ROT] += 3 * nb;
         cnt_[C_KS] += 3 * nb;
+        tally(LV_KS, l, 3 * nb);
         return o;
     }
     SparseBoot& sparse_variant(int n, bool pair = false) {
@@ -3301,6 +3319,7 @@ public:
                 }
                 gals[b] = gal;  // c0's automorphism is read inside k_lin_mac
                 cnt_[C_ROT] += nb;
+                tally(LV_KS, l, nb);  // a baby-step rotation: one key switch per member (hoisted ModUp)
             }
             if (!fused_baby) {
                 untmp(ext, (size_t)nb * ext_rows(l));
@@ -3361,6 +3380,9 @@ public:
                 m.outp[j] = in_blk[j] ? blk + (size_t)(i++) * nb * ps : rot[j] ? tmp(2 * (size_t)ne * nb) : nullptr;
             }
             launch_lin_mac(S(), T_, m, nl, ne, extmap(nl));
+            for (int j = 0; j < gn; ++j)
+                for (int b = 0; b < g.B; ++b)
+                    if (P[g0 + j][b]) tally(LV_PTMUL, l, nb);  // one diagonal product per member
             if (!bj.empty()) {
                 Ct rs = moddown_rescale(blk, l, nb * (int)bj.size());
                 std::vector<u64> gs;
@@ -3499,6 +3521,7 @@ public:
         count += K;
         cnt_[C_ROT] += K * nb;
         cnt_[C_KS] += K * nb;
+        tally(LV_KS, lv, K * nb);
     }
     // one rotated giant step of a double-hoisted group: rs permuted by X -> X^gal, its c1
     // key switched into the running Q*P sum acc (allocated on the first call), its c0 summed
@@ -3523,6 +3546,7 @@ public:
         ++count;
         cnt_[C_ROT] += nb;
         cnt_[C_KS] += nb;
+        tally(LV_KS, lv, nb);
     }
 
     Ct lin_transform(const Ct& in, std::vector<BootGroupDev>& groups) {
@@ -4251,7 +4275,15 @@ public:
         prof_.every = (unsigned)every;
     }
     void set_lazy(bool on) { lazy_ = on; }
-    void reset_counters() { std::memset(cnt_, 0, sizeof(cnt_)); }
+    void reset_counters() {
+        std::memset(cnt_, 0, sizeof(cnt_));
+        std::memset(lvl_cnt_, 0, sizeof(lvl_cnt_));
+    }
+    // per-level work tallies (aesfhe_level_counters): the CPU baseline replays a bootstrap's key
+    // switches, ct x ct products and diagonal products on the C oracle at the levels they ran at
+    enum LevelTally { LV_KS, LV_MUL, LV_PTMUL, LV_N };
+    static constexpr int kLvMax = 64;
+    u64 level_counter(int kind, int level) const { return kind >= 0 && kind < LV_N && level >= 0 && level < kLvMax ? lvl_cnt_[kind][level] : 0; }
 
 private:
     u32* dev_alloc(size_t words) {
@@ -4612,6 +4644,10 @@ private:
     u32* d_pinv_ = nullptr;
     u32* d_negp_ = nullptr;
     u64 cnt_[C_N] = {};
+    u64 lvl_cnt_[LV_N][kLvMax] = {};
+    void tally(int kind, int level, u64 n) {
+        if (level >= 0 && level < kLvMax) lvl_cnt_[kind][level] += n;
+    }
     CrtConsts crt_[4] = {};
     std::unordered_map<aesfhe_handle, Lut> luts_;
     Slot16 slots_ = {};    // the reference layout's 16 state slots, 5^(i N/32)
@@ -5101,6 +5137,11 @@ int aesfhe_alg_bytes(double* bytes, uint64_t* launches, int n) {
         launches[k] = g_alg_launches[k].load(std::memory_order_relaxed);
     }
     return 0;
+}
+int aesfhe_level_counters(aesfhe_ctx* ctx, int kind, uint64_t* out, int n) {
+    API_BEGIN if (kind < 0 || kind >= Engine::LV_N) throw std::runtime_error("level_counters: no such kind");
+    for (int l = 0; l < n; ++l) out[l] = ctx->eng->level_counter(kind, l);
+    API_END
 }
 int aesfhe_reset_counters(aesfhe_ctx* ctx) {
     API_BEGIN ctx->eng->reset_counters();

@@ -38,7 +38,7 @@ EXPORTED = [
     "aesfhe_mul_many", "aesfhe_conjugate_many", "aesfhe_rotate_hoisted",
     "aesfhe_power_basis", "aesfhe_to_ntt", "aesfhe_to_intt", "aesfhe_bootstrap", "aesfhe_bootstrap_pair", "aesfhe_renorm_pair", "aesfhe_renorm_states", "aesfhe_renorm_at",
     "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
-    "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
+    "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_level_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
     "aesfhe_streams", "aesfhe_bind_stream", "aesfhe_fork", "aesfhe_join", "aesfhe_settle",
     "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_kernel_work", "aesfhe_kernel_gaps", "aesfhe_pool_stats", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan", "aesfhe_debug_sparseplan",
     "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot", "aesfhe_create_keyed", "aesfhe_bootstrap_sparse", "aesfhe_bootstrap_pair_sparse", "aesfhe_renorm_periodic",
@@ -109,6 +109,7 @@ def load_library(path: Optional[Path] = None):
         "aesfhe_set_lazy": [vp, c_int],
         "aesfhe_streams": [vp], "aesfhe_bind_stream": [vp, c_int], "aesfhe_fork": [vp], "aesfhe_join": [vp], "aesfhe_settle": [vp, _H],
         "aesfhe_reset_counters": [vp],
+        "aesfhe_level_counters": [vp, c_int, np.ctypeslib.ndpointer(np.uint64, flags="C_CONTIGUOUS"), c_int],
         "aesfhe_profile": [vp, ctypes.c_uint32], "aesfhe_profile_every": [vp, c_int],
         "aesfhe_kernel_stats": [vp, _dp, c_int, c_int],
         "aesfhe_kernel_work": [vp, _dp, c_int],
@@ -951,6 +952,18 @@ class Engine:
 
     def reset_counters(self):
         self._ctx.check(self._lib.aesfhe_reset_counters(self._ctx.ptr))
+
+    LEVEL_TALLIES = ("key_switch", "product", "diagonal")
+
+    def level_counters(self) -> dict:
+        """{kind: {level: count}} since reset_counters (aesfhe_level_counters): key switches of one
+        polynomial, ct x ct products (their key switch under key_switch), plaintext-diagonal products"""
+        out = {}
+        for k, name in enumerate(self.LEVEL_TALLIES):
+            v = np.zeros(64, np.uint64)
+            self._ctx.check(self._lib.aesfhe_level_counters(self._ctx.ptr, k, v, 64))
+            out[name] = {int(l): int(c) for l, c in enumerate(v) if c}
+        return out
 
     BENCH_OPS = {"ntt": 0, "intt": 1, "keyswitch": 2, "rescale": 3, "mul_relin_rescale": 4}
 

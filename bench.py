@@ -181,25 +181,55 @@ def max_over_ranks(dist, x: float) -> float:
     return float(t.item())
 
 
-def cpu_baseline(coeffs) -> dict:
+def boot_tallies(ctx, period: int | None) -> dict:
+    """the engine's per-level work tallies (aesfhe_level_counters) of ONE C2 MixColumns final
+    bootstrap: the sparse form at the pipeline's period (tools/boot_phases.py's input), or the
+    full-slot one for the reference layout; read after the timed legs, for the CPU baseline"""
+    E = ctx.engine
+    P = period or E.slot_count
+    z = np.exp(2j * np.pi * np.random.default_rng(0).random(P))
+    ct = E.intt(ctx.encrypt(np.tile(z, E.slot_count // P)))
+    E.sync()
+    E.reset_counters()
+    if period:
+        E.bootstrap_sparse(ct, period)
+    else:
+        E.bootstrap(ct)
+    E.sync()
+    return {"tallies": E.level_counters(), "level_limbs": list(E.level_limbs), "dnum": E.dnum, "log_n": E.log_n}
+
+
+def cpu_baseline(coeffs, boot: dict | None = None) -> dict:
     """The C oracle CPU CKKS engine (oracle/ckks_cpu.py over oracle/ckks_oracle.c: Shoup / Barrett
     modular products, OpenMP over OMP_NUM_THREADS host threads), timed live on this host
     (tools/cpu_round.py): BASELINE config 1 in full (AddRoundKey at N = 2^15), then ONE FULL middle
     round of the C2 encrypt at N = 2^16 (SubBytes, renorm, ShiftRows, MixColumns without its final
-    bootstrap, AddRoundKey, renorm -- the oracle does not bootstrap), checked against the byte
-    model.  Budget: ~1 min on 16 host threads (the CPU work of one round); nothing is read from a
-    file or extrapolated from a step share."""
+    bootstrap, AddRoundKey, renorm), checked against the byte model, plus MixColumns' final
+    bootstrap as a replay of its work (boot: the GPU engine's per-level tallies of one such
+    bootstrap; cpu_round.boot_replay times one key switch / product / diagonal product per level
+    on the oracle and multiplies by the counts -- the oracle has no bootstrap plan).  Budget:
+    ~1.5 min on 16 host threads; nothing is read from a file."""
     sys.path.insert(0, str(ROOT / "tools"))
     import cpu_round
     c1 = cpu_round.c1(coeffs)
     c2 = cpu_round.c2_round(coeffs, full=True)
     round_s = c2["round_s"]
-    return {"value": 1.0 / round_s, "unit": "rounds/s", "cores": cpu_round.threads(), "kind": "port",
-            "sample": f"C oracle on the host, timed live: config 1 (AddRoundKey, N=2^15) in full {c1['ark_s']:.2f} s "
-                      f"(exact: {c1['exact']}); one full middle round of C2 at N=2^16 {round_s:.1f} s (exact: {c2['exact']}; "
-                      + ", ".join(f"{k} {v:.1f} s" for k, v in c2["steps_s"].items())
-                      + "); MixColumns' final bootstrap excluded (the oracle does not bootstrap)",
-            "c1_ark_s": c1["ark_s"], "c2_round_s": round_s, "c2_steps_s": c2["steps_s"]}
+    br = cpu_round.boot_replay(boot["tallies"], boot["level_limbs"], boot["dnum"], boot["log_n"]) if boot else None
+    total_s = round_s + (br["boot_s"] if br else 0.0)
+    boot_txt = (f"; MixColumns' final bootstrap {br['boot_s']:.1f} s as a replay of its work on the oracle (the GPU engine's "
+                f"per-level tallies of one C2 final bootstrap: {br['ops']['key_switch']} key switches, {br['ops'].get('product', 0)} "
+                f"products, {br['ops'].get('diagonal', 0)} diagonal products over levels {br['levels'][0]}-{br['levels'][-1]}; one "
+                f"operation per kind and level timed live ({br['sampled_s']:.1f} s) times its count; key switches unhoisted)"
+                ) if br else "; MixColumns' final bootstrap excluded (no tallies)"
+    out = {"value": 1.0 / total_s, "unit": "rounds/s", "cores": cpu_round.threads(), "kind": "port",
+           "sample": f"C oracle on the host, timed live: config 1 (AddRoundKey, N=2^15) in full {c1['ark_s']:.2f} s "
+                     f"(exact: {c1['exact']}); one full middle round of C2 at N=2^16 {round_s:.1f} s without its final bootstrap "
+                     f"(exact: {c2['exact']}; " + ", ".join(f"{k} {v:.1f} s" for k, v in c2["steps_s"].items()) + ")" + boot_txt,
+           "c1_ark_s": c1["ark_s"], "c2_round_s": total_s, "c2_round_no_boot_s": round_s, "c2_steps_s": c2["steps_s"]}
+    if br:
+        out["c2_boot_s"] = br["boot_s"]
+        out["c2_boot_by_kind_s"] = br["by_kind_s"]
+    return out
 
 
 class _NoFinalBootstrap:
@@ -722,7 +752,7 @@ def compact_line(full: dict, detail_path: str | None = None) -> dict:
     cb = full.get("cpu_baseline")
     if cb:
         line["cpu_baseline"] = {k: _sig(cb[k], 5) if k != "sample" else cb[k] for k in
-                                ("value", "unit", "cores", "kind", "sample", "c1_ark_s", "c2_round_s") if k in cb}
+                                ("value", "unit", "cores", "kind", "sample", "c1_ark_s", "c2_round_s", "c2_boot_s") if k in cb}
     notes = dict(NOTES)
     ts = (full.get("roofline") or {}).get("traffic_source")
     if ts:
@@ -981,7 +1011,7 @@ def main():
         line["deferred_ref_calls"] = deferred
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline(coeffs)
+            line["cpu_baseline"] = cpu_baseline(coeffs, boot_tallies(ctx, 2 * layout.period if layout.periodic else None))
         print(emit_line(line, args.detail_json or None), flush=True)
     if dist is not None:
         dist.destroy_process_group()

@@ -317,6 +317,11 @@ int aesfhe_kernel_work(aesfhe_ctx* ctx, double* out, int n);
  * the launch issued right after it, accounted to the latter's id (its drain + dispatch ramp, what
  * rocprofv3 durations add to the in-kernel span); call before a resetting aesfhe_kernel_stats */
 int aesfhe_kernel_gaps(aesfhe_ctx* ctx, double* out, int n);
+/* per-level work tallies since the last aesfhe_reset_counters: out[l] (l < n) = kind 0 key switches
+ * of one polynomial (hoisted rotations counted one each), 1 ct x ct products (tensor + relinearise +
+ * rescale; their key switch counted in kind 0), 2 plaintext-diagonal products of the linear transforms,
+ * at level l.  The CPU baseline replays a bootstrap's work from them on the C oracle (bench.py). */
+int aesfhe_level_counters(aesfhe_ctx* ctx, int kind, uint64_t* out, int n);
 int aesfhe_reset_counters(aesfhe_ctx* ctx);
 /* device memory pool: out[0] = bytes the context's buffer pools hold (in use + cached), out[1] =
  * allocations that failed, released the cached free lists and were retried (a second failure is

@@ -65,6 +65,7 @@ def lib():
         "orc_rescale": (None, [vp, c_int, c_int, u32p, u32p]),
         "orc_keyswitch": (None, [vp, c_int, u32p, u32p, u32p]),
         "orc_tensor": (None, [vp, c_int, u32p, u32p, u32p]),
+        "orc_mul_poly": (None, [vp, c_int, c_int, u32p, u32p, u32p]),
         "orc_mul_limb_consts": (None, [vp, c_int, c_int, u32p, u32p, u32p]),
         "orc_automorph": (None, [vp, c_int, c_u64, c_int, u32p, u32p]),
         "orc_encrypt": (None, [vp, c_int, u32p, u32p, c_u64, u32p]),
@@ -187,6 +188,13 @@ class OracleParams:
         x = np.ascontiguousarray(x, np.uint32)
         out = np.zeros_like(x)
         self._L.orc_automorph(self.h, level, g, x.shape[0], x, out)
+        return out
+
+    def mul_poly(self, pt: np.ndarray, x: np.ndarray) -> np.ndarray:
+        """x (npoly x nl limbs) times the plaintext polynomial pt (nl limbs), elementwise (NTT form)"""
+        x = np.ascontiguousarray(x, np.uint32)
+        out = np.zeros_like(x)
+        self._L.orc_mul_poly(self.h, x.shape[1], x.shape[0], np.ascontiguousarray(pt, np.uint32), x, out)
         return out
 
     def mul_limb_consts(self, consts: np.ndarray, x: np.ndarray) -> np.ndarray:

@@ -924,6 +924,22 @@ void orc_tensor(void *h, int level, const u32 *a, const u32 *b, u32 *out) {
     }
 }
 
+/* multiply every limb t of npoly polys (nl limbs) by the plaintext polynomial pt (nl limbs), NTT form:
+ * a linear transform's diagonal product (the CPU baseline's bootstrap replay, bench.py) */
+void orc_mul_poly(void *h, int nl, int npoly, const u32 *pt, const u32 *in, u32 *out) {
+    orc_t *o = (orc_t *)h;
+    int n = o->n;
+#pragma omp parallel for collapse(2) schedule(static)
+    for (int p = 0; p < npoly; p++)
+        for (int t = 0; t < nl; t++) {
+            barrett_t bt = bq_make(o->mod[t]);
+            for (int k = 0; k < n; k++) {
+                size_t x = ((size_t)p * nl + t) * n + k;
+                out[x] = bmul(in[x], pt[(size_t)t * n + k], &bt);
+            }
+        }
+}
+
 /* multiply every limb t of npoly polys by c_t (per-limb constants) */
 void orc_mul_limb_consts(void *h, int nl, int npoly, const u32 *c, const u32 *in, u32 *out) {
     orc_t *o = (orc_t *)h;

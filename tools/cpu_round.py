@@ -6,7 +6,7 @@ OpenMP over OMP_NUM_THREADS host threads), measured, not extrapolated:
   C2  one middle round r = 1 of the C2 encrypt at N = 2^16 (SubBytes, renorm, ShiftRows,
       MixColumns, AddRoundKey, renorm; REF/pipeline.py:142-151) with the build's AES modules
       in the reference's per-term product form (the oracle has no fused LUT op), the
-      MixColumns final bootstrap EXCLUDED (the oracle does not bootstrap).
+      MixColumns final bootstrap timed apart by boot_replay (its work replayed on the oracle).
 
 Prints one JSON object; bench.py's cpu_baseline leg runs C1 and the C2 SubBytes step (a
 bounded sample) and tools/cpu_round.py --full the whole middle round (profiles/)."""
@@ -86,6 +86,70 @@ def c2_round(coeffs, full: bool = True) -> dict:
         want = aes_plain.ref_mix_columns(aes_plain.shift_rows(want)) ^ rks[1]
     return {"steps_s": steps, "round_s": sum(steps.values()),
             "exact": bool(np.array_equal(pipe.encoder.decode(*ct), want))}
+
+
+def boot_replay(tallies: dict, level_limbs, dnum: int, log_n: int = 16) -> dict:
+    """MixColumns' final bootstrap on the C oracle, as a replay of its work: the GPU engine's
+    per-level tallies of one C2 final bootstrap (aesfhe_level_counters: key switches of one
+    polynomial, ct x ct products, linear-transform diagonal products) and, for every (kind, level)
+    that occurs, ONE such operation timed live on the oracle over the same bootstrappable chain
+    (oracle.keyswitch / tensor + rescale / mul_poly on random residues and a random key: the same
+    arithmetic as real data), times its count.  The oracle's key switch is the textbook one
+    (ModUp, inner product, ModDown per call), so the replay does not hoist rotations that share an
+    input; the oracle has no bootstrap plan of its own, so no bootstrapped ciphertext comes out --
+    this times the bootstrap's work, it does not compute one."""
+    from oracle.ckks_cpu import OracleParams
+    limbs = [int(x) for x in level_limbs]
+    L = len(limbs) - 1
+    L1 = max(l for l in range(L + 1) if limbs[l] == l + 2)
+    O = OracleParams(log_n=log_n, max_level=L1, dnum=dnum, seed=11, boot_double=L - L1)
+    if [O.nl(l) for l in range(L + 1)] != limbs:
+        raise RuntimeError("boot_replay: the oracle chain does not match the engine's limbs per level")
+    n = O.n
+    rng = np.random.default_rng(5)
+
+    def rand(*shape):  # residues below every 30-bit prime of the chain
+        return rng.integers(0, 1 << 29, shape, dtype=np.uint32)
+
+    key = rand(O.dnum, 2, O.n_ks + O.n_p, n)
+    O.keyswitch(0, rand(O.nl(0), n), key)  # warm: OpenMP pool, tables
+
+    def t_ks(l):
+        d = rand(O.nl(l), n)
+        t = time.perf_counter()
+        O.keyswitch(l, d, key)
+        return time.perf_counter() - t
+
+    def t_mul(l):
+        nl = O.nl(l)
+        a, b, out = rand(2, nl, n), rand(2, nl, n), np.zeros((3, nl, n), np.uint32)
+        t = time.perf_counter()
+        O._L.orc_tensor(O.h, l, a, b, out)
+        if nl - O.nl(l - 1) == 2:
+            O.rescale2(l, out[:2])
+        else:
+            O.rescale(l, out[:2])
+        return time.perf_counter() - t
+
+    def t_pt(l):
+        nl = O.nl(l)
+        pt, x = rand(nl, n), rand(2, nl, n)
+        t = time.perf_counter()
+        O.mul_poly(pt, x)
+        return time.perf_counter() - t
+
+    timers = {"key_switch": t_ks, "product": t_mul, "diagonal": t_pt}
+    by_kind, sampled, ops = {}, 0.0, {}
+    for kind, per_level in tallies.items():
+        tot = 0.0
+        for l, cnt in sorted(per_level.items()):
+            dt = timers[kind](int(l))
+            sampled += dt
+            tot += dt * cnt
+        by_kind[kind] = tot
+        ops[kind] = int(sum(per_level.values()))
+    return {"boot_s": sum(by_kind.values()), "by_kind_s": by_kind, "ops": ops, "sampled_s": sampled,
+            "levels": sorted({int(l) for v in tallies.values() for l in v})}
 
 
 def _heartbeat(every_s: float = 45.0):
