@@ -1,6 +1,6 @@
 """Per-level work tallies (aesfhe_level_counters) of one C2 MixColumns final bootstrap, the input
 of the CPU baseline's bootstrap replay (bench.boot_tallies): every key switch the engine counts is
-tallied at a level, the bootstrap spans level 0 (the dense -> sparse switch) to the top (the trace),
+tallied at a level, the bootstrap spans level 0 (the dense -> sparse switch) to its ModRaise level (the trace),
 and its EvalMod products and linear-transform diagonals are there."""
 import sys
 from pathlib import Path
@@ -21,7 +21,9 @@ def test_boot_tallies_cover_the_bootstrap():
     t = b["tallies"]
     # the engine's keyswitch counter plus the baby-step rotations inside k_lin_mac (counted as rotations)
     assert sum(t["key_switch"].values()) >= E.counters()["keyswitch"] > 0
-    assert min(t["key_switch"]) == 0 and max(t["key_switch"]) == E.L
+    # level 0: the dense -> sparse switch; the top: the sparse plan's ModRaise level (below the chain's
+    # top E.L, which the full-slot plan uses)
+    assert min(t["key_switch"]) == 0 and E.L - 4 <= max(t["key_switch"]) <= E.L
     assert sum(t["product"].values()) >= 14  # EvalMod's Chebyshev series and double angles
     assert sum(t["diagonal"].values()) > 0
     assert b["level_limbs"] == list(E.level_limbs) and len(b["level_limbs"]) == E.L + 1
