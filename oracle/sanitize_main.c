@@ -34,6 +34,7 @@ void orc_rescale2(void *h, int level, int npoly, const u32 *in, u32 *out);
 void orc_keyswitch_d2s(void *h, int np, const u32 *d, const u32 *ksk, u32 *out);
 void orc_tensor(void *h, int level, const u32 *a, const u32 *b, u32 *out);
 void orc_mul_limb_consts(void *h, int nl, int npoly, const u32 *c, const u32 *in, u32 *out);
+void orc_mul_poly(void *h, int nl, int npoly, const u32 *pt, const u32 *in, u32 *out);
 void orc_automorph(void *h, int level, u64 g, int npoly, const u32 *in, u32 *out);
 void orc_encrypt(void *h, int f, const u32 *pt, const u32 *pk, u64 ctr, u32 *out);
 void orc_decrypt_coeffs(void *h, int level, int npoly, const u32 *ct, const u32 *s_ntt, double *m_out);
@@ -113,7 +114,7 @@ static void exercise(chain_t *c) {
     u32 *ct = xalloc((size_t)2 * nl_of(c, f) * n);
     orc_encrypt(c->h, f, pt, pk, 1, ct);
     orc_decrypt_coeffs(c->h, f, 2, ct, sn, m);
-    /* per level: key switch, tensor, automorphism, rescale (single or double prime) */
+    /* per level: key switch, tensor, automorphism, constant and polynomial products, rescale (single or double prime) */
     for (int l = 0; l <= L; l++) {
         const int nl = nl_of(c, l);
         u32 *a = rand_poly(c, 2, nl), *b = rand_poly(c, 2, nl);
@@ -124,6 +125,7 @@ static void exercise(chain_t *c) {
         u32 *cs = xalloc(nl);
         orc_const_residues(c->h, -12345, nl, cs);
         orc_mul_limb_consts(c->h, nl, 2, cs, a, o2);
+        orc_mul_poly(c->h, nl, 2, b, a, o2);
         if (l >= 1 && l <= c->L1) orc_rescale(c->h, l, 2, a, o2);
         if (l > c->L1) orc_rescale2(c->h, l, 2, a, o2);
         free(a); free(b); free(o3); free(o2); free(cs);
