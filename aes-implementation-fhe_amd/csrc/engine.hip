@@ -396,6 +396,9 @@ public:
     // through X -> X^g (galois_lazy)
     u64 tag_sq(u64 g) const { return 4ull * hp_.n + g; }
     bool is_tag_sq(u64 t) const { return t > 4ull * hp_.n && t < 6ull * hp_.n; }
+    // sigma_g(s_sp) -> s: the sparse -> dense switch read through the first trace step's automorphism g
+    u64 tag_s2d_rot(u64 g) const { return 8ull * hp_.n + g; }
+    bool is_tag_s2d_rot(u64 t) const { return t > 8ull * hp_.n && t < 10ull * hp_.n; }
     u64 rot_galois(int steps) const {
         const long s = slot_count();
         long k = ((-(long)steps) % s + s) % s;  // np.roll(slots, steps) = left rotation by -steps
@@ -459,6 +462,8 @@ public:
             launch_square(S(), T_, sp, d_s_, nks, nks, qmap());
         } else if (g == tag_s2d()) {  // sparse s_sp -> dense s
             launch_copy_rows(S(), T_, sp, sparse_secret(), nks);
+        } else if (is_tag_s2d_rot(g)) {  // sigma_g'(s_sp) -> dense s
+            launch_automorph(S(), T_, sp, sparse_secret(), g - 8ull * n, nks);
         } else if (is_tag_sq(g)) {    // sigma_g'(s)^2 -> s: the automorphism of a 3-polynomial tensor
             u32* s2 = tmp(nks);
             launch_square(S(), T_, s2, d_s_, nks, nks, qmap());
@@ -3091,6 +3096,41 @@ public:
         tally(LV_KS, l, 3 * nb);
         return o;
     }
+    // The sparse -> dense switch fused into the first trace step (AESFHE_S2D_TRACE, default on):
+    // raised (under s_sp) -> x + rot(x, -a) + rot(x, -2a) + rot(x, -3a) with x = raised switched to s.
+    // The automorphism of raised decrypts under sigma(s_sp), so each of the four terms is ONE key
+    // inner product from the same hoisted ModUp of raised's c1 (keys s_sp -> s and sigma_j(s_sp) -> s,
+    // tag_s2d_rot) and the four share one ModDown: one ModUp and one ModDown at the top level fewer
+    // than keyswitch(s2d) followed by trace4.  Same plaintext; the key-switch noise terms differ.
+    bool s2d_trace_ = env_int("AESFHE_S2D_TRACE", 1) != 0;
+    Ct s2d_trace4(const Ct& raised, int a) {
+        const int l = raised.level, nl = hp_.nl(l), ne = nl + hp_.n_p, n = hp_.n, nb = raised.nb;
+        const size_t qs = (size_t)2 * nl * n;
+        const u32* c1 = raised.data + (size_t)nl * n;
+        u32* ext = modup(c1, l, nb, qs);
+        u32* acc = tmp(2 * (size_t)ne * nb);
+        KsSumArgs ka;
+        ka.J = 4;
+        ka.g[0] = 1, ka.key[0] = ksk(tag_s2d());
+        for (int j = 1; j <= 3; ++j) ka.g[j] = rot_galois(-j * a), ka.key[j] = ksk(tag_s2d_rot(ka.g[j]));
+        const int nd = (nl + hp_.alpha - 1) / hp_.alpha;
+        launch_key_inner_sum(S(), T_, acc, ext, c1, ka, nb, nd, ne, nl, hp_.alpha, hp_.n_ks + hp_.n_p, hp_.n_ks, extmap(nl),
+                             (size_t)ext_rows(l) * n, qs, (size_t)2 * ne * n);
+        untmp(ext, (size_t)nb * ext_rows(l));
+        KsSumArgs kc;  // c0 + its three automorphisms
+        kc.J = 3;
+        for (int j = 1; j <= 3; ++j) kc.g[j - 1] = ka.g[j];
+        u32* c0s = tmp(2 * (size_t)nl * nb);  // member stride qs, first nl rows used (moddown's add0)
+        launch_automorph_sum(S(), T_, c0s, raised.data, kc, nb, nl, qs, qmap());
+        Ct o = moddown(acc, l, c0s, nullptr, nb, qs);
+        o.ntt = raised.ntt;
+        untmp(acc, 2 * (size_t)ne * nb);
+        untmp(c0s, 2 * (size_t)nl * nb);
+        cnt_[C_ROT] += 3 * nb;
+        cnt_[C_KS] += 4 * nb;
+        tally(LV_KS, l, 4 * nb);
+        return o;
+    }
     SparseBoot& sparse_variant(int n, bool pair = false) {
         const char* p4 = std::getenv("AESFHE_SPARSE_PAIR4");  // "0": the pair keeps two EvalMod members (A/B)
         pair = pair && n <= 32 && !(p4 && std::atoi(p4) == 0);
@@ -4024,15 +4064,17 @@ public:
         const int nlt = hp_.nl(top);
         ntt(raised.data, 2 * nb * nlt, nlt, qmap());
         if (stop_after == 3) return raised;
-        // 4. back to the dense secret
+        // 4. back to the dense secret (sparse: fused into the first trace step, s2d_trace4)
         const size_t tms = (size_t)2 * nlt * n;
-        Ct u = keyswitch(raised.data + (size_t)nlt * n, top, ksk(tag_s2d()), raised.data, nullptr, nb, tms, tms);
+        const bool fuse_s2d = sv && s2d_trace_ && trace4_ && 4 * sv->n <= slot_count() && stop_after != 12;
+        Ct u = fuse_s2d ? s2d_trace4(raised, sv->n)
+                        : keyswitch(raised.data + (size_t)nlt * n, top, ksk(tag_s2d()), raised.data, nullptr, nb, tms, tms);
         release(raised);
         if (stop_after == 12) return u;  // debug: back on the dense secret, before the sparse trace
         // 4b. sparse: the trace to the subring, x += rot(x, n 2^i) for 2^i < M / n (the overflow's
         // components outside the subring cancel, the rest is multiplied by M / n)
         if (sv)
-            for (int st = sv->n; st < slot_count();) {
+            for (int st = fuse_s2d ? 4 * sv->n : sv->n; st < slot_count();) {
                 if (trace4_ && 4 * st <= slot_count()) {  // two doublings at once (hoisted)
                     Ct s4 = trace4(u, st);
                     release(u);
