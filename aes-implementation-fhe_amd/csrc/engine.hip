@@ -2746,9 +2746,35 @@ public:
     // n-periodic states.  single: hh == hl, one output (ol untouched) with every slot snapped.
     // single with packed_period = 32 (the packed XOR stage's hi | lo form, period 2 x 16): the
     // 32 slots are decoded / re-encoded directly (decode32 / encode32, no FFT); unpack = 16 likewise
+    // hc (packed / single renorms): the renorm of hh + conj(hc) -- a conjugate-split LUT's S1 + conj(S2)
+    //  renormalised without its conjugation key switch: both are decrypted in the
+    // one raw-decryption launch and conj(m2) is the automorphism X -> X^-1 of the NTT-form m2, added
+    // on the CRT limbs before the codec.  Inputs that do not share (level, owed rescales, shape) are
+    // summed homomorphically first (same result).
     void renorm_states(aesfhe_handle hh, aesfhe_handle hl, int states, aesfhe_handle* oh, aesfhe_handle* ol, int level = -1,
-                       int period = 0, int unpack = 0, bool single = false, int packed_period = 0) {
+                       int period = 0, int unpack = 0, bool single = false, int packed_period = 0, aesfhe_handle hc = 0) {
         if (!d_pk_) throw std::runtime_error("keys not generated");
+        if (hc) {
+            if (!(unpack || single) || hl != hh) throw std::runtime_error("renorm: a conjugate partner needs a packed / single renorm");
+            const Ct& a = ct(hh);
+            const Ct& b = ct(hc);
+            const bool same = a.nb == 1 && b.nb == 1 && a.level == b.level && a.pend == b.pend && vis_npoly(a) == vis_npoly(b) &&
+                              a.npoly == b.npoly && a.lazy == b.lazy && !a.zero && !b.zero;
+            if (!same) {
+                Ct cj = conjugate(b);
+                Ct sm = add_sub(a, cj, false);
+                release(cj);
+                const aesfhe_handle th = put_ct(sm);
+                try {
+                    renorm_states(th, th, states, oh, ol, level, period, unpack, single, packed_period);
+                } catch (...) {
+                    free_handle(th);
+                    throw;
+                }
+                free_handle(th);
+                return;
+            }
+        }
         if (unpack || single) {
             if (hl != hh) throw std::runtime_error("renorm: a packed / single renorm reads one ciphertext");
             if (unpack && (unpack & (unpack - 1) || unpack < 16 || 2 * unpack > slot_count()))
@@ -2795,10 +2821,11 @@ public:
         int kd[2];
         CrtConsts cc[2];
         double isc[2];
-        const aesfhe_handle in[2] = {hh, hl};
+        const aesfhe_handle in[2] = {hh, hc ? hc : hl};
         // unpack / single read ONE ciphertext: it is decrypted once and the codec runs on one input
-        // channel (k_snap_slots' unpack gathers both outputs from channel 0; single has one output)
-        const int n_in = (unpack || single) ? 1 : 2, n_out = single ? 1 : 2;
+        // channel (k_snap_slots' unpack gathers both outputs from channel 0; single has one output);
+        // a conjugate partner is decrypted as the second channel and folded into the first
+        const int n_in = (unpack || single) ? 1 : 2, n_out = single ? 1 : 2, n_dec = hc ? 2 : n_in;
         kd[1] = 0;
         // raw decryption of the inputs: ONE launch forms c0 + c1 s (+ c2 s^2) on the CRT limbs of
         // both, one inverse NTT when their limb counts agree
@@ -2806,7 +2833,7 @@ public:
         Ct dc[2];
         bool down[2] = {false, false};
         bool need_s2 = false;
-        for (int w = 0; w < n_in; ++w) {
+        for (int w = 0; w < n_dec; ++w) {
             Ct c = ensure_ntt(ct(in[w]));
             bool own = c.data != ct(in[w]).data;
             kd[w] = crt_limbs(c);
@@ -2823,13 +2850,21 @@ public:
             isc[w] = 1.0 / (c.level >= 0 ? raw_scale(c.level, c.pend) : 1.0);
             cnt_[C_DEC]++;
         }
-        launch_dec_raw(S(), T_, x, dr, n_in, d_s_, need_s2 ? s_sq4() : d_s_);
+        launch_dec_raw(S(), T_, x, dr, n_dec, d_s_, need_s2 ? s_sq4() : d_s_);
+        if (hc) {
+            if (kd[1] != kd[0] || isc[1] != isc[0]) throw std::runtime_error("renorm: conjugate partner at another scale");
+            u32* cj = tmp(kd[0]);
+            launch_automorph(S(), T_, cj, x + (size_t)4 * n, conj_galois(), kd[0]);
+            launch_add(S(), T_, x, x, cj, kd[0], kd[0], qmap());
+            untmp(cj, kd[0]);
+            cnt_[C_CONJ]++;
+        }
         if (n_in == 2 && kd[0] == kd[1]) {
             intt(x, x, 2 * kd[0], RowMap{kd[0], 4, 4, 0, 0}, qmap());
         } else {
             for (int w = 0; w < n_in; ++w) intt(x + (size_t)w * 4 * n, kd[w], kd[w], qmap());
         }
-        for (int w = 0; w < n_in; ++w)
+        for (int w = 0; w < n_dec; ++w)
             if (down[w]) release(dc[w]);
         const int f = level < 0 ? hp_.fresh : level, nq = hp_.nl(f) + 1;
         const double enc_scale = hp_.delta[f] * (double)hp_.mod[hp_.nl(f)];
@@ -5071,6 +5106,16 @@ int aesfhe_renorm_periodic(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, 
 }
 int aesfhe_renorm_unpack(aesfhe_ctx* ctx, aesfhe_handle packed, int period, int level, aesfhe_handle* out_hi, aesfhe_handle* out_lo) {
     API_BEGIN ctx->eng->renorm_states(packed, packed, 1, out_hi, out_lo, level, 0, period);
+    API_END
+}
+int aesfhe_renorm_packed_conj(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle c_conj, int period, int level, aesfhe_handle* out) {
+    API_BEGIN if (period < 16 || (period & (period - 1))) throw std::runtime_error("renorm_packed: period must be a power of two >= 16");
+    ctx->eng->renorm_states(c, c, 1, out, nullptr, level, 0, 0, true, period, c_conj);
+    API_END
+}
+int aesfhe_renorm_unpack_conj(aesfhe_ctx* ctx, aesfhe_handle packed, aesfhe_handle packed_conj, int period, int level, aesfhe_handle* out_hi,
+                              aesfhe_handle* out_lo) {
+    API_BEGIN ctx->eng->renorm_states(packed, packed, 1, out_hi, out_lo, level, 0, period, false, 0, packed_conj);
     API_END
 }
 int aesfhe_renorm_single(aesfhe_ctx* ctx, aesfhe_handle c, int level, aesfhe_handle* out) {

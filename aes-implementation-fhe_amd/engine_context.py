@@ -248,13 +248,18 @@ class EngineContext:
         """renorm_pair for the periodic state layout (state_encoder.SlotLayout)"""
         return self.engine.renorm_periodic(hi, lo, period, level)
 
-    def renorm_single(self, ct, level=None, period=None):
+    def renorm_single(self, ct, level=None, period=None, conj=None):
         """renorm of one packed-state ciphertext, every slot snapped; period: the
-        packed period when known (2 x the state period)"""
+        packed period when known (2 x the state period); conj: renormalise ct + conj(conj)"""
+        if conj is not None:
+            return self.engine.renorm_single(ct, level, period, conj=conj)
         return self.engine.renorm_single(ct, level, period)
 
-    def renorm_unpack(self, packed, period: int, level=None):
-        """renorm of a packed hi | lo state (2 period-periodic) into its (hi, lo) pair"""
+    def renorm_unpack(self, packed, period: int, level=None, conj=None):
+        """renorm of a packed hi | lo state (2 period-periodic) into its (hi, lo) pair (DESIGN.md §4c);
+        conj: renormalise packed + conj(conj)"""
+        if conj is not None:
+            return self.engine.renorm_unpack(packed, period, level, conj=conj)
         return self.engine.renorm_unpack(packed, period, level)
 
     def _init_lut_cache(self):

@@ -11,7 +11,7 @@ from mixcol_final import _CoeffCache, gf_basis16, gf_eval, gf_mult_pair
 from shift_rows import row_masks
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT
-from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_GF, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, pair, rot_many, rot_pair
+from utils import CONJ_RENORM, LUT2_DEPTH, NEED_BOOTSTRAP, NEED_GF, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, pair, rot_many, rot_pair
 
 # AESFHE_IMC_GF_LOW=0: the packed InvMixColumns' GF multiplier pairs at their own depth above the XOR4s
 # (inputs at NEED_GF + PACK_DEPTH) instead of at the XOR4 level with renormalised outputs (A/B runs)
@@ -40,7 +40,14 @@ class InvMixColumnsFHE:
     def _poly2_eval(self, ct_hi, ct_lo, mult: int, which: str):
         return gf_eval(self.ctx, self._coeffs, mult, which, ct_hi, ct_lo)
 
-    def _xor(self, a, b, out_level=None):
+    def _xor(self, a, b, out_level=None, defer_conj: bool = False):
+        """XOR4(a, b); defer_conj: straight into a secret-key renorm (utils.ConjSum, as
+        MixColFinal._xor_ct)"""
+        if defer_conj and CONJ_RENORM:
+            try:
+                return self.xor4.apply(a, b, out_level, defer_conj=True)
+            except TypeError:  # an XOR4 without deferred conjugation
+                pass
         return self.xor4.apply(a, b, out_level)
 
     def _renorm_pair(self, hi, lo, level=None):
@@ -105,9 +112,9 @@ class InvMixColumnsFHE:
             gf = lambda m, hi, lo: enc.pack(*self._gf(m, hi, lo, gl))
         p14, p11 = pair(ctx, lambda: gf(14, ct_hi, ct_lo), lambda: gf(11, rh[0], rl[0]))
         p13, p9 = pair(ctx, lambda: gf(13, rh[1], rl[1]), lambda: gf(9, rh[2], rl[2]))
-        x1, x2 = pair(ctx, lambda: enc.renorm_packed(self._xor(p14, p11, fl), level=NEED_XOR),
-                      lambda: enc.renorm_packed(self._xor(p13, p9, fl), level=NEED_XOR))
-        acc = enc.renorm_packed(self._xor(x1, x2, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
+        x1, x2 = pair(ctx, lambda: enc.renorm_packed(self._xor(p14, p11, fl, True), level=NEED_XOR),
+                      lambda: enc.renorm_packed(self._xor(p13, p9, fl, True), level=NEED_XOR))
+        acc = enc.renorm_packed(self._xor(x1, x2, fl, True), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
         if do_final_bootstrap:
             acc = bootstrap1(ctx, acc, 2 * self.layout.period)
         return acc

@@ -47,7 +47,7 @@ EXPORTED = [
     "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled", "aesfhe_set_enc_nonce", "aesfhe_launch_count", "aesfhe_launch_census",
     "aesfhe_galois_multi", "aesfhe_debug_boot_stage_sparse", "aesfhe_debug_sparse_group", "aesfhe_debug_sparse_group_plain",
     "aesfhe_debug_mono_pack", "aesfhe_debug_mono_split", "aesfhe_alg_bytes", "aesfhe_stack", "aesfhe_unstack", "aesfhe_members",
-    "aesfhe_renorm_packed",
+    "aesfhe_renorm_packed", "aesfhe_renorm_packed_conj", "aesfhe_renorm_unpack_conj",
 ]
 
 # largest log2(PQ) for 128-bit classical security with a ternary secret (HE standard)
@@ -151,6 +151,8 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_unstack"] = [vp, _H, c_int, _Hp]
     sig["aesfhe_members"] = [vp, _H, ctypes.POINTER(c_int)]
     sig["aesfhe_renorm_packed"] = [vp, _H, c_int, c_int, _Hp]
+    sig["aesfhe_renorm_packed_conj"] = [vp, _H, _H, c_int, c_int, _Hp]
+    sig["aesfhe_renorm_unpack_conj"] = [vp, _H, _H, c_int, c_int, _Hp, _Hp]
     for name in EXPORTED:
         fn = getattr(L, name)
         fn.restype = (ctypes.c_char_p if name == "aesfhe_last_error"
@@ -830,18 +832,28 @@ class Engine:
                                                          -1 if level is None else int(level), ctypes.byref(a), ctypes.byref(b)))
         return Ciphertext(self._ctx, a.value), Ciphertext(self._ctx, b.value)
 
-    def renorm_single(self, ct, level=None, period=None):
+    def renorm_single(self, ct, level=None, period=None, conj=None):
         """secret-key renorm of one ciphertext, every slot snapped (aesfhe_renorm_single); period:
-        the message's slot period when known (aesfhe_renorm_packed: period 32 skips the FFT codec)"""
+        the message's slot period when known (aesfhe_renorm_packed: period 32 skips the FFT codec);
+        conj: a ciphertext whose conjugate is added first (aesfhe_renorm_packed_conj, period needed)"""
+        if conj is not None:
+            if not period:
+                raise ValueError("renorm_single: a conjugate partner needs the period")
+            return self._new(self._lib.aesfhe_renorm_packed_conj, ct.handle, conj.handle, int(period), -1 if level is None else int(level))
         if period:
             return self._new(self._lib.aesfhe_renorm_packed, ct.handle, int(period), -1 if level is None else int(level))
         return self._new(self._lib.aesfhe_renorm_single, ct.handle, -1 if level is None else int(level))
 
-    def renorm_unpack(self, packed, period: int, level=None):
-        """secret-key renorm of a packed hi | lo state into its (hi, lo) pair (aesfhe_renorm_unpack)"""
+    def renorm_unpack(self, packed, period: int, level=None, conj=None):
+        """secret-key renorm of a packed hi | lo state into its (hi, lo) pair (aesfhe_renorm_unpack);
+        conj: a ciphertext whose conjugate is added first (aesfhe_renorm_unpack_conj)"""
         a, b = ctypes.c_uint64(), ctypes.c_uint64()
-        self._ctx.check(self._lib.aesfhe_renorm_unpack(self._ctx.ptr, packed.handle, int(period), -1 if level is None else int(level),
-                                                       ctypes.byref(a), ctypes.byref(b)))
+        lv = -1 if level is None else int(level)
+        if conj is not None:
+            self._ctx.check(self._lib.aesfhe_renorm_unpack_conj(self._ctx.ptr, packed.handle, conj.handle, int(period), lv,
+                                                                ctypes.byref(a), ctypes.byref(b)))
+        else:
+            self._ctx.check(self._lib.aesfhe_renorm_unpack(self._ctx.ptr, packed.handle, int(period), lv, ctypes.byref(a), ctypes.byref(b)))
         return Ciphertext(self._ctx, a.value), Ciphertext(self._ctx, b.value)
 
     def sync(self):

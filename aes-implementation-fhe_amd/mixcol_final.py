@@ -17,7 +17,7 @@ import numpy as np
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT, SplitLUT2, batched, eval_two, joint_bases, powers, std_basis
-from utils import LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, can_fork, drop_to, fused_lut, pair, rot_many, rot_pair
+from utils import CONJ_RENORM, LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, can_fork, drop_to, fused_lut, pair, rot_many, rot_pair
 
 # AESFHE_SHARE_R1=0: MixColumns' r1 basis rebuilt in its second XOR4 (A/B runs)
 _SHARE_R1 = os.environ.get("AESFHE_SHARE_R1", "1") != "0"
@@ -170,11 +170,16 @@ class MixColFinal:
     def _renorm_pair(self, hi, lo, level=None):
         return self.enc.renorm(hi, lo, level)
 
-    def _xor_ct(self, a, b, out_level=None, keep_b=None):
+    def _xor_ct(self, a, b, out_level=None, keep_b=None, defer_conj: bool = False):
+        """XOR4(a, b); defer_conj: the result goes straight into a secret-key renorm, which may take
+        the split LUT's S1 + conj(S2) unsummed (utils.ConjSum: no conjugation key switch)"""
+        kw = {"defer_conj": True} if defer_conj and CONJ_RENORM else {}
         if keep_b is not None:
+            kw["keep_b"] = keep_b
+        if kw:
             try:
-                return self.xor4.apply(a, b, out_level, keep_b=keep_b)
-            except TypeError:  # an XOR4 without basis sharing
+                return self.xor4.apply(a, b, out_level, **kw)
+            except TypeError:  # an XOR4 without basis sharing / deferred conjugation
                 pass
         return self.xor4.apply(a, b, out_level)
 
@@ -235,15 +240,15 @@ class MixColFinal:
                 # key switches and LUT sums at five more limbs; u at gl serves both branches (round 5).
                 # r1 is the second operand of both XOR4s at one level: its drop and std basis built once
                 kb = {} if _SHARE_R1 else None
-                u = enc.renorm_unpack(self._xor_ct(p0, p1, fl, kb), level=gl)
+                u = enc.renorm_unpack(self._xor_ct(p0, p1, fl, kb, defer_conj=True), level=gl)
 
                 def r1_r2r3_low():
                     (vh,), (vl,) = rot_pair(ctx, u[0], u[1], [2 * s1])
-                    return enc.renorm_packed(self._xor_ct(enc.pack(vh, vl), p1, fl, kb), level=NEED_XOR)
+                    return enc.renorm_packed(self._xor_ct(enc.pack(vh, vl), p1, fl, kb, defer_conj=True), level=NEED_XOR)
                 two, w = pair(ctx, lambda: enc.renorm_packed(enc.pack(*self.gf_mult_2(*u, out_level=fl + enc.PACK_DEPTH)),
                                                              level=NEED_XOR),
                               r1_r2r3_low, shared=(*u, p1))
-                acc = enc.renorm_packed(self._xor_ct(two, w, fl), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
+                acc = enc.renorm_packed(self._xor_ct(two, w, fl, defer_conj=True), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
                 if do_final_bootstrap:
                     acc = bootstrap1(ctx, acc, 2 * self.layout.period)
                 return acc

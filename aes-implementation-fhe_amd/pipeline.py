@@ -53,7 +53,7 @@ from shift_rows import shift_rows_bytes
 from shiftrows_mixcolumns import ShiftRowsMixColumnsFusedEnc
 from sub_bytes_ark import SubBytesARK
 from sub_bytes_lut import SubBytesLUT
-from utils import (pair, SHIFTROWS_DEPTH, NEED_GF, NEED_ISR_ISB, NEED_SR_ARK, NEED_SR_MIX, NEED_SUB_ARK_SR, NEED_SUBBYTES, NEED_XOR,
+from utils import (pair, CONJ_RENORM, SHIFTROWS_DEPTH, NEED_GF, NEED_ISR_ISB, NEED_SR_ARK, NEED_SR_MIX, NEED_SUB_ARK_SR, NEED_SUBBYTES, NEED_XOR,
                    RENORM_FLOOR)
 from xor4_lut import XOR4LUT
 
@@ -197,11 +197,12 @@ class AESPipeline:
             self._rk_tag = tag
         return self._rk_cache
 
-    def _ark_packed(self, x, r: int):
+    def _ark_packed(self, x, r: int, defer_conj: bool = False):
         """AddRoundKey on a packed state: XOR4(x, packed round key r).  The key's level drop and
         std basis (its conjugate and power chain) are built once per key schedule and round and
         reused by every later encrypt / decrypt with the same keys (AESFHE_KEY_BASIS=0: rebuilt
-        per call) -- the XOR4 then forms only the state's powers"""
+        per call) -- the XOR4 then forms only the state's powers.  defer_conj: the result goes into
+        renorm_unpack, which takes the split LUT's S1 + conj(S2) unsummed (utils.ConjSum)"""
         key = self._packed_round_key(r)
         if not _KEY_BASIS:
             return self.xor4.apply(x, key, out_level=self._floor())
@@ -210,7 +211,19 @@ class AESPipeline:
         if not self._xor4_keep_b():  # an XOR4 without basis sharing (a caller-supplied LUT object)
             return self.xor4.apply(x, key, out_level=self._floor())
         kb = self._kb_cache.setdefault(r, {})
+        if defer_conj and CONJ_RENORM and self._xor4_defer_ok():
+            return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb, defer_conj=True)
         return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb)
+
+    def _xor4_defer_ok(self) -> bool:
+        """whether this pipeline's XOR4 takes defer_conj (checked once)"""
+        if not hasattr(self, "_defer_ok"):
+            import inspect
+            try:
+                self._defer_ok = "defer_conj" in inspect.signature(self.xor4.apply).parameters
+            except (TypeError, ValueError):
+                self._defer_ok = False
+        return self._defer_ok
 
     def _xor4_keep_b(self) -> bool:
         """whether this pipeline's XOR4 takes keep_b (checked once; a TypeError raised INSIDE the
@@ -312,7 +325,7 @@ class AESPipeline:
             self._log_pair(debug, f"enc.r{r}.sr", *ct)
             acc = self.mix.mix_packed(*ct)
             self._log_packed(debug, f"enc.r{r}.mc", acc)
-            x = self._ark_packed(acc, r)
+            x = self._ark_packed(acc, r, defer_conj=debug is None)
             self._log_packed(debug, f"enc.r{r}.ark", x)
             ct = self.encoder.renorm_unpack(x, level=next_level)
             self._log_pair(debug, f"enc.r{r}.ark.renorm", *ct)
@@ -410,7 +423,7 @@ class AESPipeline:
                 self._log_pair(debug, f"dec.r{r}.isr", *ct)
                 ct = self._sub_renorm(ct, inverse=True, level=NEED_XOR + self.encoder.PACK_DEPTH)
                 self._log_pair(debug, f"dec.r{r}.isb", *ct)
-                x = self._ark_packed(self.encoder.pack(*ct), r)
+                x = self._ark_packed(self.encoder.pack(*ct), r, defer_conj=debug is None)
                 need = getattr(self.invmix, "packed_input_need", None)
                 ct = self.encoder.renorm_unpack(x, level=need() if need else NEED_GF + self.encoder.PACK_DEPTH)
                 self._log_pair(debug, f"dec.r{r}.ark", *ct)

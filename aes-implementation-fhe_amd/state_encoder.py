@@ -27,7 +27,7 @@ from typing import Any, Tuple
 
 import numpy as np
 
-from utils import ZetaEncoder
+from utils import ConjSum, ZetaEncoder, conj_sum
 
 # AESFHE_RENORM_FRESH=1: ignore renorm target levels (A/B measurements of DESIGN.md §3.11)
 _RENORM_FRESH = os.environ.get("AESFHE_RENORM_FRESH") == "1"
@@ -217,14 +217,28 @@ class StateEncoder:
         return out[0] if self.states == 1 else out
 
     def renorm_packed(self, ct, level=None):
-        """renorm of a packed state, packed again"""
+        """renorm of a packed state, packed again (ct may be a utils.ConjSum: s1 + conj(s2) renormalised
+        with the conjugation folded into the decryption)"""
+        if isinstance(ct, ConjSum):
+            lv = None if _RENORM_FRESH else level
+            try:
+                return self.ctx.renorm_single(ct.s1, lv, period=2 * self.layout.period, conj=ct.s2)
+            except TypeError:  # a context without the folded form
+                ct = conj_sum(self.ctx, ct)
         try:
             return self.ctx.renorm_single(ct, None if _RENORM_FRESH else level, period=2 * self.layout.period)
         except TypeError:  # a context whose renorm_single takes no period
             return self.ctx.renorm_single(ct, None if _RENORM_FRESH else level)
 
     def renorm_unpack(self, ct, level=None) -> Tuple[Any, Any]:
-        """renorm of a packed state into the (hi, lo) pair"""
+        """renorm of a packed state into the (hi, lo) pair (ct may be a utils.ConjSum, as renorm_packed)"""
+        if isinstance(ct, ConjSum):
+            check_layout(self.layout, ct.s1)
+            try:
+                return tag_layout(self.layout, *self.ctx.renorm_unpack(ct.s1, self.layout.period, None if _RENORM_FRESH else level,
+                                                                       conj=ct.s2))
+            except TypeError:
+                ct = conj_sum(self.ctx, ct)
         check_layout(self.layout, ct)
         return tag_layout(self.layout, *self.ctx.renorm_unpack(ct, self.layout.period, None if _RENORM_FRESH else level))
 

@@ -38,6 +38,26 @@ NEED_SR_MIX = NEED_GF + SHIFTROWS_DEPTH              # ShiftRows -> MixColumns
 NEED_SR_ARK = NEED_XOR + SHIFTROWS_DEPTH             # ShiftRows -> AddRoundKey (last round)
 NEED_ISR_ISB = NEED_SUBBYTES + SHIFTROWS_DEPTH       # InvShiftRows -> InvSubBytes
 NEED_BOOTSTRAP = 0                                   # bootstrapping starts from level 0
+
+
+class ConjSum:
+    """s1 + conj(s2) left unsummed for a secret-key renorm that folds the conjugation into its
+    decryption (aesfhe_renorm_packed_conj / _unpack_conj): a conjugate-split LUT
+    whose result is renormalised right away needs no conjugation key switch.  Only the renorms
+    (StateEncoder.renorm_packed / renorm_unpack) take one; conj_sum() materialises it."""
+    __slots__ = ("s1", "s2")
+
+    def __init__(self, s1, s2):
+        self.s1, self.s2 = s1, s2
+
+
+# AESFHE_CONJ_RENORM=0: every conjugate-split LUT sums its conjugation homomorphically (A/B)
+CONJ_RENORM = os.environ.get("AESFHE_CONJ_RENORM", "1") != "0"
+
+
+def conj_sum(ctx, x):
+    """a ConjSum as one ciphertext (s1 + conj(s2)); anything else unchanged"""
+    return ctx.add(x.s1, ctx.conjugate(x.s2)) if isinstance(x, ConjSum) else x
 # SubBytes-AddRoundKey fusion (sub_bytes_ark.py): SubBytes + the key product and its
 # coefficient, then the (Inv)ShiftRows it is fused across, down to level 1 (the renorm reads
 # any level; the fused step has no room for the usual floor below the fresh level 17)

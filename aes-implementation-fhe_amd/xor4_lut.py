@@ -18,7 +18,7 @@ import os
 from typing import Any, Dict
 
 import numpy as np
-from utils import LUT2_DEPTH, can_fork, conj_many, drop_to, fused_lut, mul_many, pair
+from utils import LUT2_DEPTH, ConjSum, can_fork, conj_many, drop_to, fused_lut, mul_many, pair
 
 
 def basis16(ctx, ct, *, retry_intt: bool = True) -> Dict[int, Any]:
@@ -165,14 +165,17 @@ class SplitLUT2:
         """(eval(A0, B0), eval(A1, B1)) with the two conjugations batched"""
         return eval_two(ctx, (self, key, *AB0), (self, key, *AB1))
 
-    def eval(self, ctx, key, A, B):
+    def eval(self, ctx, key, A, B, defer_conj: bool = False):
+        """S1 + conj(S2); defer_conj: as a ConjSum for a renorm that folds the conjugation in"""
         s1 = fused_lut(ctx, (key, 1), self.c1, A, B, owner=self)
         if s1 is None:
             return None
         if not self.has2:
             return s1
         s2 = fused_lut(ctx, (key, 2), self.c2, A, B, owner=self)
-        return None if s2 is None else ctx.add(s1, ctx.conjugate(s2))
+        if s2 is None:
+            return None
+        return ConjSum(s1, s2) if defer_conj else ctx.add(s1, ctx.conjugate(s2))
 
 
 def eval_two(ctx, j0, j1):
@@ -192,7 +195,7 @@ def eval_two(ctx, j0, j1):
     return out[0], out[1]
 
 
-def split_lut2(ctx, split: SplitLUT2, key, a, b, keep_b=None):
+def split_lut2(ctx, split: SplitLUT2, key, a, b, keep_b=None, defer_conj: bool = False):
     """the split evaluation, or None (no fused op / not enough level: use the product loop).
     keep_b: a dict caching b's std basis -- filled on the first call, reused by a later call with
     the same b at the same level (an operand shared by two XOR4s of one step)"""
@@ -209,7 +212,7 @@ def split_lut2(ctx, split: SplitLUT2, key, a, b, keep_b=None):
         raise
     if keep_b is not None and cached is None:
         keep_b.update(b=b, level=b.level, B=B)
-    return split.eval(ctx, key, A, B)
+    return split.eval(ctx, key, A, B, defer_conj)
 
 
 class XOR4LUT:
@@ -223,11 +226,12 @@ class XOR4LUT:
     def _build_power_basis_16(self, ct: Any) -> Dict[int, Any]:
         return basis16(self.ctx, ct)
 
-    def apply(self, a_ct, b_ct, out_level=None, keep_b=None):
+    def apply(self, a_ct, b_ct, out_level=None, keep_b=None, defer_conj: bool = False):
         """XOR4(a, b); out_level: the lowest level the caller needs the result at (the inputs
         are dropped to out_level + LUT2_DEPTH first, utils.drop_to); None = as given.
         keep_b: a dict shared by two XOR4s whose second operand is the same ciphertext -- b's
-        basis is built once (MixColumns' r1 enters two XOR4s, mixcol_final.mix_packed)."""
+        basis is built once (MixColumns' r1 enters two XOR4s, mixcol_final.mix_packed).
+        defer_conj: the split form may return a utils.ConjSum (S1, S2) for a renorm that takes one."""
         ctx = self.ctx
         if keep_b is not None and "b_in" in keep_b and keep_b["b_in"] is b_ct and keep_b.get("out_level") == out_level:
             b_ct = keep_b["b_dropped"]  # the same drop as before: reuse it (and so its basis)
@@ -242,7 +246,7 @@ class XOR4LUT:
             a_ct = drop_to(ctx, a_ct, out_level + LUT2_DEPTH)
         if not hasattr(self, "_split"):
             self._split = SplitLUT2(self.coeffs)
-        out = split_lut2(ctx, self._split, "xor4", a_ct, b_ct, keep_b)
+        out = split_lut2(ctx, self._split, "xor4", a_ct, b_ct, keep_b, defer_conj)
         if out is not None:
             return out
         A, B = pair(ctx, lambda: self._build_power_basis_16(a_ct), lambda: self._build_power_basis_16(b_ct))

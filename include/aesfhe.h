@@ -227,6 +227,13 @@ int aesfhe_renorm_packed(aesfhe_ctx* ctx, aesfhe_handle ct, int period, int leve
  * (hi, lo) pair REF/pipeline.py:65-69's renorm returns. */
 int aesfhe_renorm_unpack(aesfhe_ctx* ctx, aesfhe_handle packed, int period, int level, aesfhe_handle* out_hi,
                          aesfhe_handle* out_lo);
+/* the same two renorms of ct + conj(ct_conj): a conjugate-split LUT's S1 + conj(S2)
+ * renormalised without its conjugation key switch (both decrypted, conj(m2) = m2(X^-1) added before
+ * the codec); inputs of different level / scale are summed homomorphically first.  Engine-side
+ * fusion of REF's `ctx.add(s1, ctx.conjugate(s2))` followed by the renorm (REF/pipeline.py:65-69). */
+int aesfhe_renorm_packed_conj(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle ct_conj, int period, int level, aesfhe_handle* out);
+int aesfhe_renorm_unpack_conj(aesfhe_ctx* ctx, aesfhe_handle packed, aesfhe_handle packed_conj, int period, int level,
+                              aesfhe_handle* out_hi, aesfhe_handle* out_lo);
 int aesfhe_bootstrap_pair_sparse(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, int period, double gain, aesfhe_handle* out_a,
                                  aesfhe_handle* out_b);
 int aesfhe_bootstrap_pair_scaled(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, double gain, aesfhe_handle* out_a,

@@ -1,0 +1,69 @@
+"""The secret-key renorm of s1 + conj(s2) with the conjugation folded into its decryption
+(aesfhe_renorm_packed_conj / aesfhe_renorm_unpack_conj, engine.hip renorm_states' conjugate
+partner; utils.ConjSum): a conjugate-split LUT's output renormalised without its conjugation key
+switch.  Neither input alone decodes to the state (each carries a garbage half that cancels only in
+s1 + conj(s2)); the folded renorm must give the states of renorm(add(s1, conjugate(s2))), on the
+packed (period 32) and unpacking forms, and inputs at different levels take the summed path."""
+import numpy as np
+import pytest
+
+from conftest import gpu_context
+
+pytestmark = pytest.mark.gpu
+
+Z16 = np.exp(-2j * np.pi / 16)
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return gpu_context(log_n=16, signature=1)
+
+
+def _split(ctx, seed):
+    """(s1, s2, nibbles): s1 + conj(s2) = 256 zeta16^nib (32-periodic, with < pi/32 jitter)"""
+    E = ctx.engine
+    S = E.slot_count
+    rng = np.random.default_rng(seed)
+    nib = rng.integers(0, 16, 32)
+    z = 256.0 * Z16 ** nib * np.exp(1j * rng.uniform(-np.pi / 32, np.pi / 32, 32))
+    d = 200.0 * (rng.standard_normal(32) + 1j * rng.standard_normal(32))
+    tile = lambda v: np.tile(v, S // 32)
+    s1 = ctx.encrypt(tile(0.5 * z + d))
+    s2 = ctx.encrypt(tile(np.conj(0.5 * z - d)))
+    return s1, s2, nib
+
+
+def _close(ctx, a, b):
+    za, zb = ctx.decrypt(a), ctx.decrypt(b)
+    assert np.abs(za - zb).max() < 4e-4  # two fresh encryptions of the same codewords
+    return za
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_packed_conj_renorm_matches_summed(ctx, seed):
+    s1, s2, nib = _split(ctx, seed)
+    got = ctx.renorm_single(s1, None, period=32, conj=s2)
+    want = ctx.renorm_single(ctx.add(s1, ctx.conjugate(s2)), None, period=32)
+    z = _close(ctx, got, want)
+    assert np.abs(z[:32] - Z16 ** nib).max() < 2e-4
+    # either input alone is not the state
+    alone = ctx.decrypt(ctx.renorm_single(s1, None, period=32))
+    assert np.abs(alone[:32] - Z16 ** nib).max() > 0.1
+
+
+def test_unpack_conj_renorm_matches_summed(ctx):
+    s1, s2, nib = _split(ctx, 3)
+    gh, gl = ctx.renorm_unpack(s1, 16, None, conj=s2)
+    wh, wl = ctx.renorm_unpack(ctx.add(s1, ctx.conjugate(s2)), 16, None)
+    _close(ctx, gh, wh)
+    _close(ctx, gl, wl)
+
+
+def test_conj_partner_at_another_level_takes_the_summed_path(ctx):
+    from utils import drop_to
+    s1, s2, nib = _split(ctx, 4)
+    s2d = drop_to(ctx, s2, s2.level - 2)
+    got = ctx.renorm_single(s1, None, period=32, conj=s2d)
+    want = ctx.renorm_single(ctx.add(s1, ctx.conjugate(s2d)), None, period=32)
+    z = _close(ctx, got, want)
+    assert np.abs(z[:32] - Z16 ** nib).max() < 2e-4
