@@ -2751,27 +2751,35 @@ public:
     // one raw-decryption launch and conj(m2) is the automorphism X -> X^-1 of the NTT-form m2, added
     // on the CRT limbs before the codec.  Inputs that do not share (level, owed rescales, shape) are
     // summed homomorphically first (same result).
+    // hcl: the lo channel's partner of a pair renorm (hl + conj(hcl)), hc then the hi channel's.
     void renorm_states(aesfhe_handle hh, aesfhe_handle hl, int states, aesfhe_handle* oh, aesfhe_handle* ol, int level = -1,
-                       int period = 0, int unpack = 0, bool single = false, int packed_period = 0, aesfhe_handle hc = 0) {
+                       int period = 0, int unpack = 0, bool single = false, int packed_period = 0, aesfhe_handle hc = 0,
+                       aesfhe_handle hcl = 0) {
         if (!d_pk_) throw std::runtime_error("keys not generated");
-        if (hc) {
-            if (!(unpack || single) || hl != hh) throw std::runtime_error("renorm: a conjugate partner needs a packed / single renorm");
-            const Ct& a = ct(hh);
-            const Ct& b = ct(hc);
-            const bool same = a.nb == 1 && b.nb == 1 && a.level == b.level && a.pend == b.pend && vis_npoly(a) == vis_npoly(b) &&
-                              a.npoly == b.npoly && a.lazy == b.lazy && !a.zero && !b.zero;
-            if (!same) {
-                Ct cj = conjugate(b);
-                Ct sm = add_sub(a, cj, false);
-                release(cj);
-                const aesfhe_handle th = put_ct(sm);
+        if (hc || hcl) {
+            const bool one = unpack || single;
+            if (one ? (hl != hh || hcl) : (!hc || !hcl)) throw std::runtime_error("renorm: conjugate partners: one per input channel");
+            auto same = [&](const Ct& a, const Ct& b) {
+                return a.nb == 1 && b.nb == 1 && a.level == b.level && a.pend == b.pend && vis_npoly(a) == vis_npoly(b) && a.npoly == b.npoly &&
+                       a.lazy == b.lazy && !a.zero && !b.zero;
+            };
+            if (!same(ct(hh), ct(hc)) || (!one && !same(ct(hl), ct(hcl)))) {
+                auto summed = [&](aesfhe_handle a, aesfhe_handle b) {
+                    Ct cj = conjugate(ct(b));
+                    Ct sm = add_sub(ct(a), cj, false);
+                    release(cj);
+                    return put_ct(sm);
+                };
+                const aesfhe_handle th = summed(hh, hc), tl = one ? th : summed(hl, hcl);
                 try {
-                    renorm_states(th, th, states, oh, ol, level, period, unpack, single, packed_period);
+                    renorm_states(th, tl, states, oh, ol, level, period, unpack, single, packed_period);
                 } catch (...) {
                     free_handle(th);
+                    if (tl != th) free_handle(tl);
                     throw;
                 }
                 free_handle(th);
+                if (tl != th) free_handle(tl);
                 return;
             }
         }
@@ -2821,11 +2829,11 @@ public:
         int kd[2];
         CrtConsts cc[2];
         double isc[2];
-        const aesfhe_handle in[2] = {hh, hc ? hc : hl};
+        const aesfhe_handle in[2] = {hh, (hc && (unpack || single)) ? hc : hl};
         // unpack / single read ONE ciphertext: it is decrypted once and the codec runs on one input
         // channel (k_snap_slots' unpack gathers both outputs from channel 0; single has one output);
         // a conjugate partner is decrypted as the second channel and folded into the first
-        const int n_in = (unpack || single) ? 1 : 2, n_out = single ? 1 : 2, n_dec = hc ? 2 : n_in;
+        const int n_in = (unpack || single) ? 1 : 2, n_out = single ? 1 : 2, n_dec = (hc && n_in == 1) ? 2 : n_in;
         kd[1] = 0;
         // raw decryption of the inputs: ONE launch forms c0 + c1 s (+ c2 s^2) on the CRT limbs of
         // both, one inverse NTT when their limb counts agree
@@ -2851,13 +2859,44 @@ public:
             cnt_[C_DEC]++;
         }
         launch_dec_raw(S(), T_, x, dr, n_dec, d_s_, need_s2 ? s_sq4() : d_s_);
-        if (hc) {
+        if (hc && n_in == 1) {
             if (kd[1] != kd[0] || isc[1] != isc[0]) throw std::runtime_error("renorm: conjugate partner at another scale");
             u32* cj = tmp(kd[0]);
             launch_automorph(S(), T_, cj, x + (size_t)4 * n, conj_galois(), kd[0]);
             launch_add(S(), T_, x, x, cj, kd[0], kd[0], qmap());
             untmp(cj, kd[0]);
             cnt_[C_CONJ]++;
+        } else if (hc) {  // pair: the partners of both channels in a second raw decryption
+            DecRaw d2;
+            Ct pc[2];
+            bool pown[2] = {false, false}, ps2 = false;
+            const aesfhe_handle ph[2] = {hc, hcl};
+            for (int w = 0; w < 2; ++w) {
+                Ct c = ensure_ntt(ct(ph[w]));
+                bool own = c.data != ct(ph[w]).data;
+                if (!crt_limbs(c)) {
+                    Ct nc = normalize(c, true);
+                    if (own) release(c);
+                    c = nc, own = nc.data != ct(ph[w]).data;
+                }
+                if (crt_limbs(c) != kd[w] || 1.0 / (c.level >= 0 ? raw_scale(c.level, c.pend) : 1.0) != isc[w])
+                    throw std::runtime_error("renorm: conjugate partner at another scale");
+                pc[w] = c, pown[w] = own;
+                d2.ct[w] = c.data, d2.npoly[w] = c.npoly, d2.nlc[w] = hp_.nl(c.level), d2.kd[w] = kd[w];
+                ps2 = ps2 || c.npoly == 3;
+            }
+            u32* xc = tmp(8);
+            launch_dec_raw(S(), T_, xc, d2, 2, d_s_, ps2 ? s_sq4() : d_s_);
+            u32* cj = tmp(std::max(kd[0], kd[1]));
+            for (int w = 0; w < 2; ++w) {
+                launch_automorph(S(), T_, cj, xc + (size_t)w * 4 * n, conj_galois(), kd[w]);
+                launch_add(S(), T_, x + (size_t)w * 4 * n, x + (size_t)w * 4 * n, cj, kd[w], kd[w], qmap());
+                cnt_[C_CONJ]++;
+            }
+            untmp(cj, std::max(kd[0], kd[1]));
+            untmp(xc, 8);
+            for (int w = 0; w < 2; ++w)
+                if (pown[w]) release(pc[w]);
         }
         if (n_in == 2 && kd[0] == kd[1]) {
             intt(x, x, 2 * kd[0], RowMap{kd[0], 4, 4, 0, 0}, qmap());
@@ -5106,6 +5145,11 @@ int aesfhe_renorm_periodic(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, 
 }
 int aesfhe_renorm_unpack(aesfhe_ctx* ctx, aesfhe_handle packed, int period, int level, aesfhe_handle* out_hi, aesfhe_handle* out_lo) {
     API_BEGIN ctx->eng->renorm_states(packed, packed, 1, out_hi, out_lo, level, 0, period);
+    API_END
+}
+int aesfhe_renorm_periodic_conj(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj, int period,
+                                int level, aesfhe_handle* out_hi, aesfhe_handle* out_lo) {
+    API_BEGIN ctx->eng->renorm_states(hi, lo, 1, out_hi, out_lo, level, period, 0, false, 0, hi_conj, lo_conj);
     API_END
 }
 int aesfhe_renorm_packed_conj(aesfhe_ctx* ctx, aesfhe_handle c, aesfhe_handle c_conj, int period, int level, aesfhe_handle* out) {

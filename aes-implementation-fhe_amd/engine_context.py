@@ -244,8 +244,11 @@ class EngineContext:
         `level`: re-encrypt at that level instead of the fresh one."""
         return self.engine.renorm_pair(hi, lo, states, level)
 
-    def renorm_periodic(self, hi, lo, period: int, level=None):
-        """renorm_pair for the periodic state layout (state_encoder.SlotLayout)"""
+    def renorm_periodic(self, hi, lo, period: int, level=None, conj=None):
+        """renorm_pair for the periodic state layout (state_encoder.SlotLayout, DESIGN.md §4b);
+        conj: the pair whose conjugates are added first (hi + conj(c_hi), lo + conj(c_lo))"""
+        if conj is not None:
+            return self.engine.renorm_periodic(hi, lo, period, level, conj=conj)
         return self.engine.renorm_periodic(hi, lo, period, level)
 
     def renorm_single(self, ct, level=None, period=None, conj=None):

@@ -67,8 +67,8 @@ class InvMixColumnsFHE:
             return self.xor4.apply_pair(a[0], b[0], a[1], b[1], out_level)
         return pair(self.ctx, lambda: self._xor(a[0], b[0], out_level), lambda: self._xor(a[1], b[1], out_level))
 
-    def _gf(self, mult, hi, lo, out_level=None):
-        return gf_mult_pair(self.ctx, self._coeffs, mult, hi, lo, out_level)
+    def _gf(self, mult, hi, lo, out_level=None, defer_conj: bool = False):
+        return gf_mult_pair(self.ctx, self._coeffs, mult, hi, lo, out_level, defer_conj)
 
     def gf_mult_9(self, hi, lo):
         return self._gf(9, hi, lo, self._gf_level)
@@ -107,7 +107,7 @@ class InvMixColumnsFHE:
         if _IMC_GF_LOW:
             # the GF multiplier pairs at the XOR4 level, each packed output renormalised (as
             # MixColFinal.mix_packed's rot form, round 5): inputs at gl = packed_input_need()
-            gf = lambda m, hi, lo: enc.renorm_packed(enc.pack(*self._gf(m, hi, lo, fl + enc.PACK_DEPTH)), level=NEED_XOR)
+            gf = lambda m, hi, lo: enc.renorm_packed(enc.pack(*self._gf(m, hi, lo, fl + enc.PACK_DEPTH, True)), level=NEED_XOR)
         else:
             gf = lambda m, hi, lo: enc.pack(*self._gf(m, hi, lo, gl))
         p14, p11 = pair(ctx, lambda: gf(14, ct_hi, ct_lo), lambda: gf(11, rh[0], rl[0]))

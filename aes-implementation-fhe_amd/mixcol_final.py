@@ -96,12 +96,13 @@ def gf_eval(ctx, cache: _CoeffCache, mult: int, which: str, ct_hi, ct_lo) -> Any
     return _gf_sum(ctx, cache.load_plaintexts(ctx, mult, which), bx, by, ct_hi)
 
 
-def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo, out_level=None):
+def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo, out_level=None, defer_conj: bool = False):
     """(gf_mult{mult}_hi, gf_mult{mult}_lo)(hi, lo).  With a fused-LUT context both LUTs are
     evaluated in the conjugate-split form (xor4_lut.SplitLUT2) over ONE pair
     of bases -- positive powers of hi, standard basis of lo -- instead of four 16-element
     bases; otherwise the reference's per-LUT product loops (REF/mixcol_final.py:80-99).
-    out_level: inputs dropped to out_level + LUT2_DEPTH first (utils.drop_to)."""
+    out_level: inputs dropped to out_level + LUT2_DEPTH first (utils.drop_to).  defer_conj: the
+    batched split form may return utils.ConjSum outputs (for StateEncoder.pack + a renorm)."""
     if out_level is not None:
         ct_hi, ct_lo = drop_to(ctx, ct_hi, out_level + LUT2_DEPTH), drop_to(ctx, ct_lo, out_level + LUT2_DEPTH)
     if getattr(ctx, "fused_luts", False):
@@ -117,7 +118,7 @@ def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo, out_level=Non
                 raise
         else:
             if batched(ctx) and not can_fork(ctx):
-                out = eval_two(ctx, (sh, ("gf", mult, "hi"), A, B), (sl, ("gf", mult, "lo"), A, B))
+                out = eval_two(ctx, (sh, ("gf", mult, "hi"), A, B), (sl, ("gf", mult, "lo"), A, B), defer_conj and CONJ_RENORM)
                 if out is not None:
                     return out
             else:
@@ -158,8 +159,8 @@ class MixColFinal:
     def _gf_poly_eval_2var(self, ct_hi, ct_lo, mult: int, which: str):
         return gf_eval(self.ctx, self._coeffs, mult, which, ct_hi, ct_lo)
 
-    def gf_mult_2(self, ct_hi, ct_lo, out_level=None):
-        return gf_mult_pair(self.ctx, self._coeffs, 2, ct_hi, ct_lo, out_level)
+    def gf_mult_2(self, ct_hi, ct_lo, out_level=None, defer_conj: bool = False):
+        return gf_mult_pair(self.ctx, self._coeffs, 2, ct_hi, ct_lo, out_level, defer_conj)
 
     def gf_mult_3(self, ct_hi, ct_lo, out_level=None):
         return gf_mult_pair(self.ctx, self._coeffs, 3, ct_hi, ct_lo, out_level)
@@ -245,7 +246,7 @@ class MixColFinal:
                 def r1_r2r3_low():
                     (vh,), (vl,) = rot_pair(ctx, u[0], u[1], [2 * s1])
                     return enc.renorm_packed(self._xor_ct(enc.pack(vh, vl), p1, fl, kb, defer_conj=True), level=NEED_XOR)
-                two, w = pair(ctx, lambda: enc.renorm_packed(enc.pack(*self.gf_mult_2(*u, out_level=fl + enc.PACK_DEPTH)),
+                two, w = pair(ctx, lambda: enc.renorm_packed(enc.pack(*self.gf_mult_2(*u, out_level=fl + enc.PACK_DEPTH, defer_conj=True)),
                                                              level=NEED_XOR),
                               r1_r2r3_low, shared=(*u, p1))
                 acc = enc.renorm_packed(self._xor_ct(two, w, fl, defer_conj=True), level=NEED_BOOTSTRAP if do_final_bootstrap else None)

@@ -187,6 +187,12 @@ class StateEncoder:
         second: hi * mask_0 + lo * mask_1 (one level; both halves are P-periodic, so no rotation)"""
         if not self.layout.packable:
             raise ValueError("the packed form needs the periodic layout with 2 * period <= slot count")
+        if isinstance(ct_hi, ConjSum) or isinstance(ct_lo, ConjSum):
+            # the masks are real: pack(conj a, conj b) = conj(pack(a, b)), so a pair of
+            # utils.ConjSum packs into one (both halves' S1 packed, and both S2)
+            if not (isinstance(ct_hi, ConjSum) and isinstance(ct_lo, ConjSum)):
+                return self.pack(conj_sum(self.ctx, ct_hi), conj_sum(self.ctx, ct_lo))
+            return ConjSum(self.pack(ct_hi.s1, ct_lo.s1), self.pack(ct_hi.s2, ct_lo.s2))
         ctx = self.ctx
         if getattr(self, "_half_pts", None) is None:
             self._half_pts = [ctx.encode(self.layout.half_mask(w)) for w in (0, 1)]

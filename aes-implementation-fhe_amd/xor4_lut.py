@@ -178,9 +178,10 @@ class SplitLUT2:
         return ConjSum(s1, s2) if defer_conj else ctx.add(s1, ctx.conjugate(s2))
 
 
-def eval_two(ctx, j0, j1):
+def eval_two(ctx, j0, j1, defer_conj: bool = False):
     """two split-LUT evaluations j = (split, key, A, B) as S1 + conj(S2) each, the two
-    conjugations in one conj_many batch; None if a fused sum is unavailable (level)"""
+    conjugations in one conj_many batch; None if a fused sum is unavailable (level).
+    defer_conj: each result a utils.ConjSum (S1, S2) for a renorm that folds the conjugation in"""
     out, s2 = [], []
     for sp, key, A, B in (j0, j1):
         s1 = fused_lut(ctx, (key, 1), sp.c1, A, B, owner=sp)
@@ -190,6 +191,8 @@ def eval_two(ctx, j0, j1):
         out.append(s1)
         s2.append(t2)
     idx = [i for i in (0, 1) if s2[i] is not None]
+    if defer_conj:
+        return tuple(ConjSum(out[i], s2[i]) if s2[i] is not None else out[i] for i in (0, 1))
     for i, c in zip(idx, conj_many(ctx, [s2[i] for i in idx])):
         out[i] = ctx.add(out[i], c)
     return out[0], out[1]
