@@ -215,6 +215,20 @@ class AESPipeline:
             return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb, defer_conj=True)
         return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb)
 
+    def _sub_apply(self, ct, defer_conj: bool = False):
+        """SubBytes on the pair down to the renorm floor; defer_conj (the output goes straight into
+        _renorm_pair): the nibble form may hand over utils.ConjSum halves for the folded renorm"""
+        if defer_conj and CONJ_RENORM and self.use_hard_renorm_between_steps and not self.true_fhe:
+            if not hasattr(self, "_sub_defer_ok"):
+                import inspect
+                try:
+                    self._sub_defer_ok = "defer_conj" in inspect.signature(self.sub.apply).parameters
+                except (TypeError, ValueError):
+                    self._sub_defer_ok = False
+            if self._sub_defer_ok:
+                return self.sub.apply(*ct, out_level=self._floor(), defer_conj=True)
+        return self.sub.apply(*ct, out_level=self._floor())
+
     def _xor4_defer_ok(self) -> bool:
         """whether this pipeline's XOR4 takes defer_conj (checked once)"""
         if not hasattr(self, "_defer_ok"):
@@ -316,7 +330,7 @@ class AESPipeline:
             # XORs it with the packed round key, its renorm unpacks into the (hi, lo) pair.  A debug
             # dict logs THIS path's stages under the reference's names (the packed ones decoded from
             # the hi | lo halves), so the golden stage test observes the headline path itself.
-            ct = self.sub.apply(*ct, out_level=self._floor())
+            ct = self._sub_apply(ct, defer_conj=debug is None)
             self._log_pair(debug, f"enc.r{r}.sub", *ct)
             need = getattr(self.mix, "packed_input_need", None)
             ct = self._renorm_pair(*ct, level=(need() + SHIFTROWS_DEPTH) if need else NEED_SR_MIX + self.encoder.PACK_DEPTH)
@@ -375,7 +389,7 @@ class AESPipeline:
             ct = self._renorm_pair(*ct)
             self._log_pair(debug, "enc.output", *ct)
             return tag_layout(self.layout, *ct)
-        ct = self.sub.apply(*ct, out_level=self._floor())
+        ct = self._sub_apply(ct, defer_conj=debug is None)
         self._log_pair(debug, "enc.final.sub", *ct)
         ct = self._renorm_pair(*ct, level=NEED_SR_ARK)
         self._log_pair(debug, "enc.final.sub.renorm", *ct)

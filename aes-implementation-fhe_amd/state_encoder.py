@@ -251,7 +251,20 @@ class StateEncoder:
     def renorm(self, ct_hi, ct_lo, level=None) -> Tuple[Any, Any]:
         """decode -> re-encode (REF/pipeline.py:65-69), done on the device when available;
         `level`: the level the next step needs (None = fresh), honoured by the device path.
-        With a renorm_hook (true-FHE mode) the hook runs instead (it reads `level` as the next step's need)."""
+        With a renorm_hook (true-FHE mode) the hook runs instead (it reads `level` as the next step's need).
+        hi / lo may be utils.ConjSum (s1 + conj(s2)): the periodic device renorm folds the conjugation
+        into its decryption; any other path sums them first."""
+        if isinstance(ct_hi, ConjSum) or isinstance(ct_lo, ConjSum):
+            per = getattr(self.ctx, "renorm_periodic", None)
+            if (isinstance(ct_hi, ConjSum) and isinstance(ct_lo, ConjSum) and self.renorm_hook is None and self.layout.periodic
+                    and per is not None):
+                check_layout(self.layout, ct_hi.s1, ct_lo.s1)
+                try:
+                    return tag_layout(self.layout, *per(ct_hi.s1, ct_lo.s1, self.layout.period, None if _RENORM_FRESH else level,
+                                                        conj=(ct_hi.s2, ct_lo.s2)))
+                except TypeError:  # a context without the folded form
+                    pass
+            ct_hi, ct_lo = conj_sum(self.ctx, ct_hi), conj_sum(self.ctx, ct_lo)
         check_layout(self.layout, ct_hi, ct_lo)
         return tag_layout(self.layout, *self._renorm(ct_hi, ct_lo, level))
 

@@ -22,7 +22,7 @@ import os
 from typing import Any, Dict, Tuple
 
 import numpy as np
-from utils import LUT2_DEPTH, SUBBYTES_DEPTH, can_fork, conj_many, drop_to, fused_lut, mul_many, pair
+from utils import CONJ_RENORM, LUT2_DEPTH, SUBBYTES_DEPTH, can_fork, conj_many, drop_to, fused_lut, mul_many, pair
 
 _TOL = 1e-12
 # AESFHE_SB_NIB=0: the pipeline keeps the reference's 8 -> 4 form (lift to b = ζ256^byte, depth 13)
@@ -116,25 +116,26 @@ class SubBytesLUTFastCached:
         """levels apply() consumes between its inputs and out_level"""
         return LUT2_DEPTH if self.nibble_on() else SUBBYTES_DEPTH
 
-    def _apply_nibble(self, ct_hi: Any, ct_lo: Any) -> Tuple[Any, Any]:
+    def _apply_nibble(self, ct_hi: Any, ct_lo: Any, defer_conj: bool = False) -> Tuple[Any, Any]:
         from mixcol_final import gf_mult_pair
         if not hasattr(self, "_nib"):
             self._nib = _NibbleLUTs(self.hi, self.lo)
-        return gf_mult_pair(self.ctx, self._nib, "sbox", ct_hi, ct_lo)
+        return gf_mult_pair(self.ctx, self._nib, "sbox", ct_hi, ct_lo, defer_conj=defer_conj and CONJ_RENORM)
 
     @staticmethod
     def _power(basis, k: int, domain: int, ctx):
         return basis[k - 1] if k <= len(basis) else ctx.conjugate(basis[domain - k - 1])
 
-    def apply(self, ct_hi: Any, ct_lo: Any, out_level=None) -> Tuple[Any, Any]:
+    def apply(self, ct_hi: Any, ct_lo: Any, out_level=None, defer_conj: bool = False) -> Tuple[Any, Any]:
         """(S_hi, S_lo)(hi, lo); out_level: the lowest level the caller needs the result at
         (inputs dropped to out_level + SUBBYTES_DEPTH first, utils.drop_to); None = as given.
-        Inputs one level higher than that take the bivariate giant-step form (_outputs_biv)."""
+        Inputs one level higher than that take the bivariate giant-step form (_outputs_biv).
+        defer_conj: the nibble form may return utils.ConjSum outputs (for StateEncoder.renorm)."""
         if self.nibble_on():
             if out_level is not None:
                 lv = out_level + LUT2_DEPTH
                 ct_hi, ct_lo = drop_to(self.ctx, ct_hi, lv), drop_to(self.ctx, ct_lo, lv)
-            return self._apply_nibble(ct_hi, ct_lo)
+            return self._apply_nibble(ct_hi, ct_lo, defer_conj)
         biv = False
         if out_level is not None:
             lv = out_level + SUBBYTES_DEPTH

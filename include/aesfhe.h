@@ -227,10 +227,12 @@ int aesfhe_renorm_packed(aesfhe_ctx* ctx, aesfhe_handle ct, int period, int leve
  * (hi, lo) pair REF/pipeline.py:65-69's renorm returns. */
 int aesfhe_renorm_unpack(aesfhe_ctx* ctx, aesfhe_handle packed, int period, int level, aesfhe_handle* out_hi,
                          aesfhe_handle* out_lo);
-/* the same two renorms of ct + conj(ct_conj): a conjugate-split LUT's S1 + conj(S2)
+/* aesfhe_renorm_periodic / _packed / _unpack of ct + conj(ct_conj) (per channel for the pair): a conjugate-split LUT's S1 + conj(S2)
  * renormalised without its conjugation key switch (both decrypted, conj(m2) = m2(X^-1) added before
  * the codec); inputs of different level / scale are summed homomorphically first.  Engine-side
  * fusion of REF's `ctx.add(s1, ctx.conjugate(s2))` followed by the renorm (REF/pipeline.py:65-69). */
+int aesfhe_renorm_periodic_conj(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj,
+                                int period, int level, aesfhe_handle* out_hi, aesfhe_handle* out_lo);
 int aesfhe_renorm_packed_conj(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle ct_conj, int period, int level, aesfhe_handle* out);
 int aesfhe_renorm_unpack_conj(aesfhe_ctx* ctx, aesfhe_handle packed, aesfhe_handle packed_conj, int period, int level,
                               aesfhe_handle* out_hi, aesfhe_handle* out_lo);

@@ -67,3 +67,21 @@ def test_conj_partner_at_another_level_takes_the_summed_path(ctx):
     want = ctx.renorm_single(ctx.add(s1, ctx.conjugate(s2d)), None, period=32)
     z = _close(ctx, got, want)
     assert np.abs(z[:32] - Z16 ** nib).max() < 2e-4
+
+
+def test_pair_conj_renorm_matches_summed(ctx):
+    """the periodic pair renorm (SubBytes' nibble LUT pair -> renorm): each channel's partner"""
+    E = ctx.engine
+    S = E.slot_count
+    rng = np.random.default_rng(5)
+    outs = []
+    for _ in range(2):
+        nib = rng.integers(0, 16, 16)
+        z = 256.0 * Z16 ** nib
+        d = 200.0 * (rng.standard_normal(16) + 1j * rng.standard_normal(16))
+        outs.append((ctx.encrypt(np.tile(0.5 * z + d, S // 16)), ctx.encrypt(np.tile(np.conj(0.5 * z - d), S // 16)), nib))
+    (h1, h2, nh), (l1, l2, nl_) = outs
+    gh, gl = ctx.renorm_periodic(h1, l1, 16, None, conj=(h2, l2))
+    wh, wl = ctx.renorm_periodic(ctx.add(h1, ctx.conjugate(h2)), ctx.add(l1, ctx.conjugate(l2)), 16, None)
+    zh, zl = _close(ctx, gh, wh), _close(ctx, gl, wl)
+    assert np.abs(zh[:16] - Z16 ** nh).max() < 2e-4 and np.abs(zl[:16] - Z16 ** nl_).max() < 2e-4
