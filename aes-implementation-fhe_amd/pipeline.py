@@ -180,7 +180,7 @@ class AESPipeline:
         if self.true_fhe:
             level = NEED_SR_ARK  # true-FHE: SubBytes' ~3e-2 output errors get two snaps (ShiftRows +
             #                      the GF multipliers need 6 levels, MixColumns renormalises after them)
-        return self._renorm_pair(*lut.apply(*ct, out_level=self._floor()), level=level)
+        return self._renorm_pair(*self._sub_apply(ct, defer_conj=True, lut=lut), level=level)
 
     def _encode_key(self, key_bytes: np.ndarray):
         key_bytes = np.asarray(key_bytes, dtype=np.uint8)
@@ -215,19 +215,20 @@ class AESPipeline:
             return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb, defer_conj=True)
         return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb)
 
-    def _sub_apply(self, ct, defer_conj: bool = False):
-        """SubBytes on the pair down to the renorm floor; defer_conj (the output goes straight into
-        _renorm_pair): the nibble form may hand over utils.ConjSum halves for the folded renorm"""
+    def _sub_apply(self, ct, defer_conj: bool = False, lut=None):
+        """(Inv)SubBytes (lut, default self.sub) on the pair down to the renorm floor; defer_conj (the
+        output goes straight into _renorm_pair): the nibble form may hand over utils.ConjSum halves
+        for the folded renorm"""
+        lut = self.sub if lut is None else lut
         if defer_conj and CONJ_RENORM and self.use_hard_renorm_between_steps and not self.true_fhe:
-            if not hasattr(self, "_sub_defer_ok"):
-                import inspect
-                try:
-                    self._sub_defer_ok = "defer_conj" in inspect.signature(self.sub.apply).parameters
-                except (TypeError, ValueError):
-                    self._sub_defer_ok = False
-            if self._sub_defer_ok:
-                return self.sub.apply(*ct, out_level=self._floor(), defer_conj=True)
-        return self.sub.apply(*ct, out_level=self._floor())
+            import inspect
+            try:
+                ok = "defer_conj" in inspect.signature(lut.apply).parameters
+            except (TypeError, ValueError):
+                ok = False
+            if ok:
+                return lut.apply(*ct, out_level=self._floor(), defer_conj=True)
+        return lut.apply(*ct, out_level=self._floor())
 
     def _xor4_defer_ok(self) -> bool:
         """whether this pipeline's XOR4 takes defer_conj (checked once)"""
