@@ -2752,10 +2752,15 @@ public:
     // on the CRT limbs before the codec.  Inputs that do not share (level, owed rescales, shape) are
     // summed homomorphically first (same result).
     // hcl: the lo channel's partner of a pair renorm (hl + conj(hcl)), hc then the hi channel's.
+    // pack_out (pair, period 16): ONE output, the snapped hi | lo pair in the packed period-32 form
+    // (StateEncoder.pack's layout) -- the decode's two 16-slot channels are the 32 packed slots in
+    // order, so the encode is the packed renorm's (no mask products, no level for the pack).
     void renorm_states(aesfhe_handle hh, aesfhe_handle hl, int states, aesfhe_handle* oh, aesfhe_handle* ol, int level = -1,
                        int period = 0, int unpack = 0, bool single = false, int packed_period = 0, aesfhe_handle hc = 0,
-                       aesfhe_handle hcl = 0) {
+                       aesfhe_handle hcl = 0, bool pack_out = false) {
         if (!d_pk_) throw std::runtime_error("keys not generated");
+        if (pack_out && (unpack || single || period != 16 || ct(hh).nb > 1 || ct(hl).nb > 1))
+            throw std::runtime_error("renorm: the packed output needs a single period-16 state pair");
         if (hc || hcl) {
             const bool one = unpack || single;
             if (one ? (hl != hh || hcl) : (!hc || !hcl)) throw std::runtime_error("renorm: conjugate partners: one per input channel");
@@ -2772,7 +2777,7 @@ public:
                 };
                 const aesfhe_handle th = summed(hh, hc), tl = one ? th : summed(hl, hcl);
                 try {
-                    renorm_states(th, tl, states, oh, ol, level, period, unpack, single, packed_period);
+                    renorm_states(th, tl, states, oh, ol, level, period, unpack, single, packed_period, 0, 0, pack_out);
                 } catch (...) {
                     free_handle(th);
                     if (tl != th) free_handle(tl);
@@ -2833,7 +2838,7 @@ public:
         // unpack / single read ONE ciphertext: it is decrypted once and the codec runs on one input
         // channel (k_snap_slots' unpack gathers both outputs from channel 0; single has one output);
         // a conjugate partner is decrypted as the second channel and folded into the first
-        const int n_in = (unpack || single) ? 1 : 2, n_out = single ? 1 : 2, n_dec = (hc && n_in == 1) ? 2 : n_in;
+        const int n_in = (unpack || single) ? 1 : 2, n_out = (single || pack_out) ? 1 : 2, n_dec = (hc && n_in == 1) ? 2 : n_in;
         kd[1] = 0;
         // raw decryption of the inputs: ONE launch forms c0 + c1 s (+ c2 s^2) on the CRT limbs of
         // both, one inverse NTT when their limb counts agree
@@ -2926,7 +2931,8 @@ public:
             const Slot16& sl = per16 ? slots_p_ : slots_;
             launch_decode16(S(), T_, x, kd, cc, sl, isc, acc);
             if (!snap_encode_) launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
-            launch_encode16(S(), T_, m, wv, sl, enc_scale, nq, per16, zacc);
+            if (pack_out) launch_encode32(S(), T_, m, wv, slots32_, enc_scale, nq, zacc);  // acc[c][i] = packed slot 16 c + i
+            else launch_encode16(S(), T_, m, wv, sl, enc_scale, nq, per16, zacc);
             if (snap_encode_) codec_flip_[t_sidx] ^= 1;
         } else {
             double*& zbuf = d_fft_[t_sidx];
@@ -5145,6 +5151,12 @@ int aesfhe_renorm_periodic(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, 
 }
 int aesfhe_renorm_unpack(aesfhe_ctx* ctx, aesfhe_handle packed, int period, int level, aesfhe_handle* out_hi, aesfhe_handle* out_lo) {
     API_BEGIN ctx->eng->renorm_states(packed, packed, 1, out_hi, out_lo, level, 0, period);
+    API_END
+}
+int aesfhe_renorm_pack(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj, int period, int level,
+                       aesfhe_handle* out) {
+    API_BEGIN if ((hi_conj != 0) != (lo_conj != 0)) throw std::runtime_error("renorm_pack: give both conjugate partners or none");
+    ctx->eng->renorm_states(hi, lo, 1, out, nullptr, level, period, 0, false, 0, hi_conj, lo_conj, true);
     API_END
 }
 int aesfhe_renorm_periodic_conj(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj, int period,

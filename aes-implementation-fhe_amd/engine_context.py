@@ -251,6 +251,11 @@ class EngineContext:
             return self.engine.renorm_periodic(hi, lo, period, level, conj=conj)
         return self.engine.renorm_periodic(hi, lo, period, level)
 
+    def renorm_pack(self, hi, lo, period: int, level=None, conj=None):
+        """renorm of a period-16 state pair straight into the packed form (StateEncoder.pack's layout);
+        conj: the pair whose conjugates are added first"""
+        return self.engine.renorm_pack(hi, lo, period, level, conj=conj)
+
     def renorm_single(self, ct, level=None, period=None, conj=None):
         """renorm of one packed-state ciphertext, every slot snapped; period: the
         packed period when known (2 x the state period); conj: renormalise ct + conj(conj)"""

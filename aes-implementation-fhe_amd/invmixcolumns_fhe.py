@@ -107,7 +107,10 @@ class InvMixColumnsFHE:
         if _IMC_GF_LOW:
             # the GF multiplier pairs at the XOR4 level, each packed output renormalised (as
             # MixColFinal.mix_packed's rot form, round 5): inputs at gl = packed_input_need()
-            gf = lambda m, hi, lo: enc.renorm_packed(enc.pack(*self._gf(m, hi, lo, fl + enc.PACK_DEPTH, True)), level=NEED_XOR)
+            if getattr(enc, "pack_renorm_direct", lambda: False)():  # the device renorm packs: no pack level
+                gf = lambda m, hi, lo: enc.renorm_pack(*self._gf(m, hi, lo, fl, True), level=NEED_XOR)
+            else:
+                gf = lambda m, hi, lo: enc.renorm_packed(enc.pack(*self._gf(m, hi, lo, fl + enc.PACK_DEPTH, True)), level=NEED_XOR)
         else:
             gf = lambda m, hi, lo: enc.pack(*self._gf(m, hi, lo, gl))
         p14, p11 = pair(ctx, lambda: gf(14, ct_hi, ct_lo), lambda: gf(11, rh[0], rl[0]))

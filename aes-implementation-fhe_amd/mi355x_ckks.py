@@ -47,7 +47,7 @@ EXPORTED = [
     "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled", "aesfhe_set_enc_nonce", "aesfhe_launch_count", "aesfhe_launch_census",
     "aesfhe_galois_multi", "aesfhe_debug_boot_stage_sparse", "aesfhe_debug_sparse_group", "aesfhe_debug_sparse_group_plain",
     "aesfhe_debug_mono_pack", "aesfhe_debug_mono_split", "aesfhe_alg_bytes", "aesfhe_stack", "aesfhe_unstack", "aesfhe_members",
-    "aesfhe_renorm_packed", "aesfhe_renorm_packed_conj", "aesfhe_renorm_unpack_conj", "aesfhe_renorm_periodic_conj",
+    "aesfhe_renorm_packed", "aesfhe_renorm_packed_conj", "aesfhe_renorm_unpack_conj", "aesfhe_renorm_periodic_conj", "aesfhe_renorm_pack",
 ]
 
 # largest log2(PQ) for 128-bit classical security with a ternary secret (HE standard)
@@ -153,6 +153,7 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_renorm_packed"] = [vp, _H, c_int, c_int, _Hp]
     sig["aesfhe_renorm_packed_conj"] = [vp, _H, _H, c_int, c_int, _Hp]
     sig["aesfhe_renorm_periodic_conj"] = [vp, _H, _H, _H, _H, c_int, c_int, _Hp, _Hp]
+    sig["aesfhe_renorm_pack"] = [vp, _H, _H, _H, _H, c_int, c_int, _Hp]
     sig["aesfhe_renorm_unpack_conj"] = [vp, _H, _H, c_int, c_int, _Hp, _Hp]
     for name in EXPORTED:
         fn = getattr(L, name)
@@ -838,6 +839,12 @@ class Engine:
             self._ctx.check(self._lib.aesfhe_renorm_periodic(self._ctx.ptr, hi.handle, lo.handle, int(period), lv, ctypes.byref(a),
                                                              ctypes.byref(b)))
         return Ciphertext(self._ctx, a.value), Ciphertext(self._ctx, b.value)
+
+    def renorm_pack(self, hi, lo, period: int, level=None, conj=None):
+        """secret-key renorm of a period-16 state pair into ONE packed period-32 ciphertext
+        (aesfhe_renorm_pack); conj: the pair (c_hi, c_lo) whose conjugates are added first"""
+        c0, c1 = (0, 0) if conj is None else (conj[0].handle, conj[1].handle)
+        return self._new(self._lib.aesfhe_renorm_pack, hi.handle, lo.handle, c0, c1, int(period), -1 if level is None else int(level))
 
     def renorm_single(self, ct, level=None, period=None, conj=None):
         """secret-key renorm of one ciphertext, every slot snapped (aesfhe_renorm_single); period:

@@ -159,6 +159,14 @@ class MixColFinal:
     def _gf_poly_eval_2var(self, ct_hi, ct_lo, mult: int, which: str):
         return gf_eval(self.ctx, self._coeffs, mult, which, ct_hi, ct_lo)
 
+    def _gf2_renorm_pack(self, u, fl):
+        """renorm_packed(pack(GF2(u))): with the packing renorm (StateEncoder.renorm_pack: the
+        device encode packs) the multipliers run one level lower, no pack level"""
+        enc = self.enc
+        if getattr(enc, "pack_renorm_direct", lambda: False)():
+            return enc.renorm_pack(*self.gf_mult_2(*u, out_level=fl, defer_conj=True), level=NEED_XOR)
+        return enc.renorm_packed(enc.pack(*self.gf_mult_2(*u, out_level=fl + enc.PACK_DEPTH, defer_conj=True)), level=NEED_XOR)
+
     def gf_mult_2(self, ct_hi, ct_lo, out_level=None, defer_conj: bool = False):
         return gf_mult_pair(self.ctx, self._coeffs, 2, ct_hi, ct_lo, out_level, defer_conj)
 
@@ -246,8 +254,7 @@ class MixColFinal:
                 def r1_r2r3_low():
                     (vh,), (vl,) = rot_pair(ctx, u[0], u[1], [2 * s1])
                     return enc.renorm_packed(self._xor_ct(enc.pack(vh, vl), p1, fl, kb, defer_conj=True), level=NEED_XOR)
-                two, w = pair(ctx, lambda: enc.renorm_packed(enc.pack(*self.gf_mult_2(*u, out_level=fl + enc.PACK_DEPTH, defer_conj=True)),
-                                                             level=NEED_XOR),
+                two, w = pair(ctx, lambda: self._gf2_renorm_pack(u, fl),
                               r1_r2r3_low, shared=(*u, p1))
                 acc = enc.renorm_packed(self._xor_ct(two, w, fl, defer_conj=True), level=NEED_BOOTSTRAP if do_final_bootstrap else None)
                 if do_final_bootstrap:

@@ -31,6 +31,8 @@ from utils import ConjSum, ZetaEncoder, conj_sum
 
 # AESFHE_RENORM_FRESH=1: ignore renorm target levels (A/B measurements of DESIGN.md §3.11)
 _RENORM_FRESH = os.environ.get("AESFHE_RENORM_FRESH") == "1"
+# AESFHE_PACK_RENORM=0: renorm_pack packs with the masks, then renormalises (A/B)
+_PACK_RENORM = os.environ.get("AESFHE_PACK_RENORM", "1") != "0"
 
 
 class SlotLayout:
@@ -235,6 +237,26 @@ class StateEncoder:
             return self.ctx.renorm_single(ct, None if _RENORM_FRESH else level, period=2 * self.layout.period)
         except TypeError:  # a context whose renorm_single takes no period
             return self.ctx.renorm_single(ct, None if _RENORM_FRESH else level)
+
+    def pack_renorm_direct(self) -> bool:
+        """whether renorm_pack runs as the device's packing renorm (then its inputs need no pack level)"""
+        return (_PACK_RENORM and getattr(self.ctx, "renorm_pack", None) is not None and self.renorm_hook is None
+                and self.layout.periodic and self.layout.period == 16 and self.pairs == 1)
+
+    def renorm_pack(self, ct_hi, ct_lo, level=None):
+        """renorm_packed(pack(hi, lo)): for one period-16 state pair the device renorm encodes the
+        snapped pair straight into the packed form (aesfhe_renorm_pack: no mask products, no pack
+        level; utils.ConjSum halves folded as in renorm); otherwise pack, then renorm"""
+        if self.pack_renorm_direct():
+            rp = self.ctx.renorm_pack
+            conj = None
+            if isinstance(ct_hi, ConjSum) and isinstance(ct_lo, ConjSum):
+                conj, ct_hi, ct_lo = (ct_hi.s2, ct_lo.s2), ct_hi.s1, ct_lo.s1
+            else:
+                ct_hi, ct_lo = conj_sum(self.ctx, ct_hi), conj_sum(self.ctx, ct_lo)
+            check_layout(self.layout, ct_hi, ct_lo)
+            return tag_layout(self.layout, rp(ct_hi, ct_lo, self.layout.period, None if _RENORM_FRESH else level, conj=conj))[0]
+        return self.renorm_packed(self.pack(ct_hi, ct_lo), level)
 
     def renorm_unpack(self, ct, level=None) -> Tuple[Any, Any]:
         """renorm of a packed state into the (hi, lo) pair (ct may be a utils.ConjSum, as renorm_packed)"""

@@ -231,6 +231,12 @@ int aesfhe_renorm_unpack(aesfhe_ctx* ctx, aesfhe_handle packed, int period, int 
  * renormalised without its conjugation key switch (both decrypted, conj(m2) = m2(X^-1) added before
  * the codec); inputs of different level / scale are summed homomorphically first.  Engine-side
  * fusion of REF's `ctx.add(s1, ctx.conjugate(s2))` followed by the renorm (REF/pipeline.py:65-69). */
+/* the periodic pair renorm (period 16, one state pair) whose output is ONE ciphertext in the packed
+ * period-32 form (hi on slots j mod 32 < 16, lo on the others: StateEncoder.pack's layout) -- the
+ * renorm of pack(hi, lo) without the pack's mask products and level; hi_conj / lo_conj (both or
+ * neither, 0 = none): the pair's conjugate partners as aesfhe_renorm_periodic_conj. */
+int aesfhe_renorm_pack(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj, int period, int level,
+                       aesfhe_handle* out);
 int aesfhe_renorm_periodic_conj(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj,
                                 int period, int level, aesfhe_handle* out_hi, aesfhe_handle* out_lo);
 int aesfhe_renorm_packed_conj(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle ct_conj, int period, int level, aesfhe_handle* out);

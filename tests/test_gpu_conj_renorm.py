@@ -85,3 +85,31 @@ def test_pair_conj_renorm_matches_summed(ctx):
     wh, wl = ctx.renorm_periodic(ctx.add(h1, ctx.conjugate(h2)), ctx.add(l1, ctx.conjugate(l2)), 16, None)
     zh, zl = _close(ctx, gh, wh), _close(ctx, gl, wl)
     assert np.abs(zh[:16] - Z16 ** nh).max() < 2e-4 and np.abs(zl[:16] - Z16 ** nl_).max() < 2e-4
+
+
+@pytest.mark.parametrize("with_conj", [False, True])
+def test_packing_renorm_matches_pack_then_renorm(ctx, with_conj):
+    """aesfhe_renorm_pack: the period-16 pair renormalised straight into the packed period-32 form
+    (no mask products) equals renorm_packed(pack(hi, lo)), with or without conjugate partners"""
+    from state_encoder import StateEncoder
+    enc = StateEncoder(ctx)
+    assert enc.layout.period == 16 and enc.pack_renorm_direct()
+    E = ctx.engine
+    S = E.slot_count
+    rng = np.random.default_rng(6 + with_conj)
+    parts = []
+    for _ in range(2):
+        nib = rng.integers(0, 16, 16)
+        z = 256.0 * Z16 ** nib
+        d = 200.0 * (rng.standard_normal(16) + 1j * rng.standard_normal(16)) if with_conj else 0.0 * z
+        parts.append((ctx.encrypt(np.tile(0.5 * z + d, S // 16)), ctx.encrypt(np.tile(np.conj(0.5 * z - d), S // 16)), nib))
+    (h1, h2, nh), (l1, l2, nl_) = parts
+    if with_conj:
+        got = ctx.renorm_pack(h1, l1, 16, None, conj=(h2, l2))
+        hi, lo = ctx.add(h1, ctx.conjugate(h2)), ctx.add(l1, ctx.conjugate(l2))
+    else:
+        hi, lo = ctx.add(h1, ctx.conjugate(h2)), ctx.add(l1, ctx.conjugate(l2))
+        got = ctx.renorm_pack(hi, lo, 16, None)
+    want = enc.renorm_packed(enc.pack(hi, lo), None)
+    z = _close(ctx, got, want)
+    assert np.abs(z[:16] - Z16 ** nh).max() < 2e-4 and np.abs(z[16:32] - Z16 ** nl_).max() < 2e-4
