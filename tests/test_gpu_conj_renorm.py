@@ -92,7 +92,7 @@ def test_packing_renorm_matches_pack_then_renorm(ctx, with_conj):
     """aesfhe_renorm_pack: the period-16 pair renormalised straight into the packed period-32 form
     (no mask products) equals renorm_packed(pack(hi, lo)), with or without conjugate partners"""
     from state_encoder import StateEncoder
-    enc = StateEncoder(ctx)
+    enc = StateEncoder(ctx, periodic=True)
     assert enc.layout.period == 16 and enc.pack_renorm_direct()
     E = ctx.engine
     S = E.slot_count
