@@ -107,7 +107,8 @@ class InvMixColumnsFHE:
         if _IMC_GF_LOW:
             # the GF multiplier pairs at the XOR4 level, each packed output renormalised (as
             # MixColFinal.mix_packed's rot form, round 5): inputs at gl = packed_input_need()
-            if getattr(enc, "pack_renorm_direct", lambda: False)():  # the device renorm packs: no pack level
+            direct = getattr(enc, "pack_renorm_direct", lambda ct=None: False)(ct_hi)  # the device renorm packs: no pack level
+            if direct:
                 gf = lambda m, hi, lo: enc.renorm_pack(*self._gf(m, hi, lo, fl, True), level=NEED_XOR)
             else:
                 gf = lambda m, hi, lo: enc.renorm_packed(enc.pack(*self._gf(m, hi, lo, fl + enc.PACK_DEPTH, True)), level=NEED_XOR)

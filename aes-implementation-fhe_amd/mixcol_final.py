@@ -163,7 +163,7 @@ class MixColFinal:
         """renorm_packed(pack(GF2(u))): with the packing renorm (StateEncoder.renorm_pack: the
         device encode packs) the multipliers run one level lower, no pack level"""
         enc = self.enc
-        if getattr(enc, "pack_renorm_direct", lambda: False)():
+        if getattr(enc, "pack_renorm_direct", lambda ct=None: False)(u[0]):
             return enc.renorm_pack(*self.gf_mult_2(*u, out_level=fl, defer_conj=True), level=NEED_XOR)
         return enc.renorm_packed(enc.pack(*self.gf_mult_2(*u, out_level=fl + enc.PACK_DEPTH, defer_conj=True)), level=NEED_XOR)
 

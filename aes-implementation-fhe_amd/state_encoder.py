@@ -238,16 +238,20 @@ class StateEncoder:
         except TypeError:  # a context whose renorm_single takes no period
             return self.ctx.renorm_single(ct, None if _RENORM_FRESH else level)
 
-    def pack_renorm_direct(self) -> bool:
-        """whether renorm_pack runs as the device's packing renorm (then its inputs need no pack level)"""
-        return (_PACK_RENORM and getattr(self.ctx, "renorm_pack", None) is not None and self.renorm_hook is None
-                and self.layout.periodic and self.layout.period == 16 and self.pairs == 1)
+    def pack_renorm_direct(self, ct=None) -> bool:
+        """whether renorm_pack runs as the device's packing renorm (then its inputs need no pack level);
+        ct: an input of the pair -- a stack of several state pairs takes pack + renorm"""
+        if not (_PACK_RENORM and getattr(self.ctx, "renorm_pack", None) is not None and self.renorm_hook is None
+                and self.layout.periodic and self.layout.period == 16 and self.pairs == 1):
+            return False
+        members = getattr(getattr(self.ctx, "engine", None), "members", None)
+        return ct is None or members is None or members(ct.s1 if isinstance(ct, ConjSum) else ct) == 1
 
     def renorm_pack(self, ct_hi, ct_lo, level=None):
         """renorm_packed(pack(hi, lo)): for one period-16 state pair the device renorm encodes the
         snapped pair straight into the packed form (aesfhe_renorm_pack: no mask products, no pack
         level; utils.ConjSum halves folded as in renorm); otherwise pack, then renorm"""
-        if self.pack_renorm_direct():
+        if self.pack_renorm_direct(ct_hi):
             rp = self.ctx.renorm_pack
             conj = None
             if isinstance(ct_hi, ConjSum) and isinstance(ct_lo, ConjSum):
