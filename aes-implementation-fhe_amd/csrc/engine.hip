@@ -2757,8 +2757,17 @@ public:
     // order, so the encode is the packed renorm's (no mask products, no level for the pack).
     void renorm_states(aesfhe_handle hh, aesfhe_handle hl, int states, aesfhe_handle* oh, aesfhe_handle* ol, int level = -1,
                        int period = 0, int unpack = 0, bool single = false, int packed_period = 0, aesfhe_handle hc = 0,
-                       aesfhe_handle hcl = 0, bool pack_out = false) {
+                       aesfhe_handle hcl = 0, bool pack_out = false, const int* slot_perm = nullptr) {
         if (!d_pk_) throw std::runtime_error("keys not generated");
+        // slot_perm (pair, period 16): output slot i takes input slot slot_perm[i] -- a byte
+        // permutation such as ShiftRows folded into the renorm: the decode reads each output slot's
+        // value through the permuted root table, the encode writes slot i (no rotation, no level)
+        if (slot_perm) {
+            if (unpack || single || period != 16 || ct(hh).nb > 1 || ct(hl).nb > 1)
+                throw std::runtime_error("renorm: a slot permutation needs a single period-16 state pair");
+            for (int i = 0; i < 16; ++i)
+                if (slot_perm[i] < 0 || slot_perm[i] > 15) throw std::runtime_error("renorm: slot permutation entries must lie in [0, 16)");
+        }
         if (pack_out && (unpack || single || period != 16 || ct(hh).nb > 1 || ct(hl).nb > 1))
             throw std::runtime_error("renorm: the packed output needs a single period-16 state pair");
         if (hc || hcl) {
@@ -2777,7 +2786,7 @@ public:
                 };
                 const aesfhe_handle th = summed(hh, hc), tl = one ? th : summed(hl, hcl);
                 try {
-                    renorm_states(th, tl, states, oh, ol, level, period, unpack, single, packed_period, 0, 0, pack_out);
+                    renorm_states(th, tl, states, oh, ol, level, period, unpack, single, packed_period, 0, 0, pack_out, slot_perm);
                 } catch (...) {
                     free_handle(th);
                     if (tl != th) free_handle(tl);
@@ -2929,7 +2938,10 @@ public:
             if (snap_encode_) codec_flip_[t_sidx] ^= 1;
         } else if (states == 1) {
             const Slot16& sl = per16 ? slots_p_ : slots_;
-            launch_decode16(S(), T_, x, kd, cc, sl, isc, acc);
+            Slot16 sp = sl;
+            if (slot_perm)
+                for (int i = 0; i < 16; ++i) sp.e[i] = sl.e[slot_perm[i]];
+            launch_decode16(S(), T_, x, kd, cc, sp, isc, acc);
             if (!snap_encode_) launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
             if (pack_out) launch_encode32(S(), T_, m, wv, slots32_, enc_scale, nq, zacc);  // acc[c][i] = packed slot 16 c + i
             else launch_encode16(S(), T_, m, wv, sl, enc_scale, nq, per16, zacc);
@@ -5151,6 +5163,15 @@ int aesfhe_renorm_periodic(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, 
 }
 int aesfhe_renorm_unpack(aesfhe_ctx* ctx, aesfhe_handle packed, int period, int level, aesfhe_handle* out_hi, aesfhe_handle* out_lo) {
     API_BEGIN ctx->eng->renorm_states(packed, packed, 1, out_hi, out_lo, level, 0, period);
+    API_END
+}
+int aesfhe_renorm_periodic_perm(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj,
+                                const int32_t* perm16, int pack_out, int period, int level, aesfhe_handle* out_hi, aesfhe_handle* out_lo) {
+    API_BEGIN if ((hi_conj != 0) != (lo_conj != 0)) throw std::runtime_error("renorm_periodic_perm: give both conjugate partners or none");
+    if (!perm16) throw std::runtime_error("renorm_periodic_perm: no permutation");
+    int p[16];
+    for (int i = 0; i < 16; ++i) p[i] = perm16[i];
+    ctx->eng->renorm_states(hi, lo, 1, out_hi, pack_out ? nullptr : out_lo, level, period, 0, false, 0, hi_conj, lo_conj, pack_out != 0, p);
     API_END
 }
 int aesfhe_renorm_pack(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj, int period, int level,

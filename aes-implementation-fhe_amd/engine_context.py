@@ -251,6 +251,10 @@ class EngineContext:
             return self.engine.renorm_periodic(hi, lo, period, level, conj=conj)
         return self.engine.renorm_periodic(hi, lo, period, level)
 
+    def renorm_periodic_perm(self, hi, lo, period: int, perm, level=None, conj=None):
+        """renorm_periodic with a byte permutation folded in (output slot i <- input slot perm[i])"""
+        return self.engine.renorm_periodic_perm(hi, lo, period, perm, level, conj=conj)
+
     def renorm_pack(self, hi, lo, period: int, level=None, conj=None):
         """renorm of a period-16 state pair straight into the packed form (StateEncoder.pack's layout);
         conj: the pair whose conjugates are added first"""

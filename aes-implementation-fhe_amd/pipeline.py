@@ -57,6 +57,9 @@ from utils import (pair, CONJ_RENORM, SHIFTROWS_DEPTH, NEED_GF, NEED_ISR_ISB, NE
                    RENORM_FLOOR)
 from xor4_lut import XOR4LUT
 
+# AESFHE_SR_RENORM=0: ShiftRows as masked rotations after the renorm instead of folded into it (A/B)
+_SR_RENORM = os.environ.get("AESFHE_SR_RENORM", "1") != "0"
+
 
 # AESFHE_KEY_BASIS=0: the packed round keys' XOR4 bases rebuilt in every AddRoundKey (A/B runs)
 _KEY_BASIS = os.environ.get("AESFHE_KEY_BASIS", "1") != "0"
@@ -215,6 +218,21 @@ class AESPipeline:
             return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb, defer_conj=True)
         return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb)
 
+    def _sr_perm(self, ct, debug):
+        """ShiftRows' byte permutation when the renorm before it can fold it (secret-key renorm mode,
+        one period-16 state pair on the device, no debug log of the renorm's own output;
+        AESFHE_SR_RENORM=0: rotate after the renorm), else None"""
+        if debug is not None or not _SR_RENORM or self.true_fhe or not self.use_hard_renorm_between_steps:
+            return None
+        if not hasattr(self, "_sr_perm_v"):
+            sp = getattr(self.shift, "slot_perm", None)
+            self._sr_perm_v = sp() if sp is not None else None
+        if self._sr_perm_v is None:
+            return None
+        ok = getattr(self.encoder, "renorm_perm_ok", None)
+        c0 = ct[0].s1 if hasattr(ct[0], "s1") else ct[0]
+        return self._sr_perm_v if ok is not None and ok(c0) else None
+
     def _sub_apply(self, ct, defer_conj: bool = False, lut=None):
         """(Inv)SubBytes (lut, default self.sub) on the pair down to the renorm floor; defer_conj (the
         output goes straight into _renorm_pair): the nibble form may hand over utils.ConjSum halves
@@ -334,9 +352,14 @@ class AESPipeline:
             ct = self._sub_apply(ct, defer_conj=debug is None)
             self._log_pair(debug, f"enc.r{r}.sub", *ct)
             need = getattr(self.mix, "packed_input_need", None)
-            ct = self._renorm_pair(*ct, level=(need() + SHIFTROWS_DEPTH) if need else NEED_SR_MIX + self.encoder.PACK_DEPTH)
-            self._log_pair(debug, f"enc.r{r}.sub.renorm", *ct)
-            ct = self.shift_rows(*ct)
+            lv = need() if need else NEED_SR_MIX - SHIFTROWS_DEPTH + self.encoder.PACK_DEPTH
+            perm = self._sr_perm(ct, debug)
+            if perm is not None:  # ShiftRows folded into the renorm (a byte permutation of the snap)
+                ct = self.encoder.renorm_perm(*ct, perm, level=lv)
+            else:
+                ct = self._renorm_pair(*ct, level=lv + SHIFTROWS_DEPTH)
+                self._log_pair(debug, f"enc.r{r}.sub.renorm", *ct)
+                ct = self.shift_rows(*ct)
             self._log_pair(debug, f"enc.r{r}.sr", *ct)
             acc = self.mix.mix_packed(*ct)
             self._log_packed(debug, f"enc.r{r}.mc", acc)
@@ -392,9 +415,13 @@ class AESPipeline:
             return tag_layout(self.layout, *ct)
         ct = self._sub_apply(ct, defer_conj=debug is None)
         self._log_pair(debug, "enc.final.sub", *ct)
-        ct = self._renorm_pair(*ct, level=NEED_SR_ARK)
-        self._log_pair(debug, "enc.final.sub.renorm", *ct)
-        ct = self.shift_rows(*ct)
+        perm = self._sr_perm(ct, debug)
+        if perm is not None:  # ShiftRows folded into the renorm
+            ct = self.encoder.renorm_perm(*ct, perm, level=NEED_SR_ARK - SHIFTROWS_DEPTH)
+        else:
+            ct = self._renorm_pair(*ct, level=NEED_SR_ARK)
+            self._log_pair(debug, "enc.final.sub.renorm", *ct)
+            ct = self.shift_rows(*ct)
         self._log_pair(debug, "enc.final.sr", *ct)
         ct = self.ark(*ct, *rk[10], out_level=self._floor())
         self._log_pair(debug, "enc.final.ark10", *ct)

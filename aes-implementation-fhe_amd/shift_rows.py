@@ -44,6 +44,14 @@ class ShiftRows:
         self._pt_masks = row_masks(ctx, self.sc, states, self.layout)
         self._rot_steps = [self.direction * 4 * r * self.stride for r in range(4)]
 
+    def slot_perm(self):
+        """the permutation as output slot i <- input slot perm[i] when the layout holds one state per
+        16-slot block (periodic, unit 1: byte i in slot i), else None -- for a renorm that folds it
+        (StateEncoder.renorm(perm=)); row r's slots rotate by direction * 4 r (np.roll convention)"""
+        if not (self.layout.periodic and self.stride == 1 and self.layout.period == 16):
+            return None
+        return [(i - self.direction * 4 * (i % 4)) % 16 for i in range(16)]
+
     def _apply_one(self, ct: Any) -> Any:
         ctx = self.ctx
         out = ctx.multiply(ct, 0.0)

@@ -238,10 +238,27 @@ class StateEncoder:
         except TypeError:  # a context whose renorm_single takes no period
             return self.ctx.renorm_single(ct, None if _RENORM_FRESH else level)
 
-    def pack_renorm_direct(self, ct=None) -> bool:
+    def renorm_perm(self, ct_hi, ct_lo, perm, level=None):
+        """renorm(hi, lo) followed by a byte permutation (output byte i <- input byte perm[i]), the
+        permutation folded into the device renorm (aesfhe_renorm_periodic_perm); the caller checks
+        renorm_perm_ok first.  utils.ConjSum halves are folded as in renorm"""
+        conj = None
+        if isinstance(ct_hi, ConjSum) and isinstance(ct_lo, ConjSum):
+            conj, ct_hi, ct_lo = (ct_hi.s2, ct_lo.s2), ct_hi.s1, ct_lo.s1
+        else:
+            ct_hi, ct_lo = conj_sum(self.ctx, ct_hi), conj_sum(self.ctx, ct_lo)
+        check_layout(self.layout, ct_hi, ct_lo)
+        return tag_layout(self.layout, *self.ctx.renorm_periodic_perm(ct_hi, ct_lo, self.layout.period, perm,
+                                                                      None if _RENORM_FRESH else level, conj=conj))
+
+    def renorm_perm_ok(self, ct=None) -> bool:
+        """whether renorm_perm runs on this encoder / context (one period-16 state pair on the device)"""
+        return getattr(self.ctx, "renorm_periodic_perm", None) is not None and self.pack_renorm_direct(ct, need_pack=False)
+
+    def pack_renorm_direct(self, ct=None, need_pack: bool = True) -> bool:
         """whether renorm_pack runs as the device's packing renorm (then its inputs need no pack level);
         ct: an input of the pair -- a stack of several state pairs takes pack + renorm"""
-        if not (_PACK_RENORM and getattr(self.ctx, "renorm_pack", None) is not None and self.renorm_hook is None
+        if not ((_PACK_RENORM or not need_pack) and getattr(self.ctx, "renorm_pack", None) is not None and self.renorm_hook is None
                 and self.layout.periodic and self.layout.period == 16 and self.pairs == 1):
             return False
         members = getattr(getattr(self.ctx, "engine", None), "members", None)

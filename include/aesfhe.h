@@ -235,6 +235,12 @@ int aesfhe_renorm_unpack(aesfhe_ctx* ctx, aesfhe_handle packed, int period, int 
  * period-32 form (hi on slots j mod 32 < 16, lo on the others: StateEncoder.pack's layout) -- the
  * renorm of pack(hi, lo) without the pack's mask products and level; hi_conj / lo_conj (both or
  * neither, 0 = none): the pair's conjugate partners as aesfhe_renorm_periodic_conj. */
+/* the periodic pair renorm (period 16, one state pair) with a byte permutation folded in: output slot
+ * i (byte i) takes input byte perm16[i] (ShiftRows: REF/shift_rows.py's slot rotations after the renorm
+ * of REF/pipeline.py:65-69, at no level); optional conjugate partners as aesfhe_renorm_periodic_conj;
+ * pack_out != 0: one packed output as aesfhe_renorm_pack (out_lo unused). */
+int aesfhe_renorm_periodic_perm(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj,
+                                const int32_t* perm16, int pack_out, int period, int level, aesfhe_handle* out_hi, aesfhe_handle* out_lo);
 int aesfhe_renorm_pack(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj, int period, int level,
                        aesfhe_handle* out);
 int aesfhe_renorm_periodic_conj(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj,

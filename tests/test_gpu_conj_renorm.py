@@ -113,3 +113,35 @@ def test_packing_renorm_matches_pack_then_renorm(ctx, with_conj):
     want = enc.renorm_packed(enc.pack(hi, lo), None)
     z = _close(ctx, got, want)
     assert np.abs(z[:16] - Z16 ** nh).max() < 2e-4 and np.abs(z[16:32] - Z16 ** nl_).max() < 2e-4
+
+
+@pytest.mark.parametrize("with_conj", [False, True])
+def test_shift_rows_folded_into_the_renorm(ctx, with_conj):
+    """aesfhe_renorm_periodic_perm with ShiftRows' byte permutation equals ShiftRows (masked
+    rotations) after the renorm, per decoded slot, with or without conjugate partners"""
+    from shift_rows import ShiftRows
+    from state_encoder import StateEncoder
+    enc = StateEncoder(ctx, periodic=True)
+    sr = ShiftRows(ctx, layout=enc.layout)
+    perm = sr.slot_perm()
+    assert perm is not None and enc.renorm_perm_ok()
+    E = ctx.engine
+    S = E.slot_count
+    rng = np.random.default_rng(9 + with_conj)
+    parts = []
+    for _ in range(2):
+        nib = rng.integers(0, 16, 16)
+        z = 256.0 * Z16 ** nib
+        d = 200.0 * (rng.standard_normal(16) + 1j * rng.standard_normal(16)) if with_conj else 0.0 * z
+        parts.append((ctx.encrypt(np.tile(0.5 * z + d, S // 16)), ctx.encrypt(np.tile(np.conj(0.5 * z - d), S // 16)), nib))
+    (h1, h2, nh), (l1, l2, nl_) = parts
+    hi, lo = ctx.add(h1, ctx.conjugate(h2)), ctx.add(l1, ctx.conjugate(l2))
+    if with_conj:
+        gh, gl = ctx.renorm_periodic_perm(h1, l1, 16, perm, None, conj=(h2, l2))
+    else:
+        gh, gl = ctx.renorm_periodic_perm(hi, lo, 16, perm, None)
+    wh, wl = sr.apply(*ctx.renorm_periodic(hi, lo, 16, None))
+    zh, zl = ctx.decrypt(gh), ctx.decrypt(gl)
+    assert np.abs(zh - ctx.decrypt(wh)).max() < 5e-3 and np.abs(zl - ctx.decrypt(wl)).max() < 5e-3
+    p = np.asarray(perm)
+    assert np.abs(zh[:16] - (Z16 ** nh)[p]).max() < 2e-4 and np.abs(zl[:16] - (Z16 ** nl_)[p]).max() < 2e-4
