@@ -2762,8 +2762,9 @@ public:
         // slot_perm (pair, period 16): output slot i takes input slot slot_perm[i] -- a byte
         // permutation such as ShiftRows folded into the renorm: the decode reads each output slot's
         // value through the permuted root table, the encode writes slot i (no rotation, no level)
-        if (slot_perm) {
-            if (unpack || single || period != 16 || ct(hh).nb > 1 || ct(hl).nb > 1)
+        if (slot_perm) {  // a period-16 pair, or the unpacking renorm of one packed period-16 pair
+            const bool pair16 = !unpack && !single && period == 16, unpack16 = unpack == 16 && !single;
+            if (!(pair16 || unpack16) || ct(hh).nb > 1 || ct(hl).nb > 1)
                 throw std::runtime_error("renorm: a slot permutation needs a single period-16 state pair");
             for (int i = 0; i < 16; ++i)
                 if (slot_perm[i] < 0 || slot_perm[i] > 15) throw std::runtime_error("renorm: slot permutation entries must lie in [0, 16)");
@@ -2928,10 +2929,15 @@ public:
         double* acc = d_codec_[t_sidx] + (snap_encode_ ? 64 * codec_flip_[t_sidx] : 0);
         double* zacc = snap_encode_ ? d_codec_[t_sidx] + 64 * (1 - codec_flip_[t_sidx]) : nullptr;
         double* wv = snap_encode_ ? acc : d_codec_[t_sidx] + 64;
+        if (slot_perm && unpack && !direct32) throw std::runtime_error("renorm: a slot permutation needs the direct period-32 codec");
         if (direct32) {
             // the 32 slots of the packed period-32 state: one direct decode, the snap as 2 x 16, and
-            // either the two 16-periodic halves (unpack) or the 32-periodic whole (single)
-            launch_decode32(S(), T_, x, kd[0], cc[0], slots32_, isc[0], acc);
+            // either the two 16-periodic halves (unpack) or the 32-periodic whole (single); a slot
+            // permutation applies within each 16-slot half (hi, lo)
+            Slot32 sp32 = slots32_;
+            if (slot_perm)
+                for (int j = 0; j < 32; ++j) sp32.e[j] = slots32_.e[16 * (j / 16) + slot_perm[j % 16]];
+            launch_decode32(S(), T_, x, kd[0], cc[0], sp32, isc[0], acc);
             if (!snap_encode_) launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
             if (unpack) launch_encode16(S(), T_, m, wv, slots_p_, enc_scale, nq, true, zacc);
             else launch_encode32(S(), T_, m, wv, slots32_, enc_scale, nq, zacc);
@@ -5163,6 +5169,14 @@ int aesfhe_renorm_periodic(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, 
 }
 int aesfhe_renorm_unpack(aesfhe_ctx* ctx, aesfhe_handle packed, int period, int level, aesfhe_handle* out_hi, aesfhe_handle* out_lo) {
     API_BEGIN ctx->eng->renorm_states(packed, packed, 1, out_hi, out_lo, level, 0, period);
+    API_END
+}
+int aesfhe_renorm_unpack_perm(aesfhe_ctx* ctx, aesfhe_handle packed, aesfhe_handle packed_conj, const int32_t* perm16, int period, int level,
+                              aesfhe_handle* out_hi, aesfhe_handle* out_lo) {
+    API_BEGIN if (!perm16) throw std::runtime_error("renorm_unpack_perm: no permutation");
+    int p[16];
+    for (int i = 0; i < 16; ++i) p[i] = perm16[i];
+    ctx->eng->renorm_states(packed, packed, 1, out_hi, out_lo, level, 0, period, false, 0, packed_conj, 0, false, p);
     API_END
 }
 int aesfhe_renorm_periodic_perm(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj,

@@ -251,6 +251,10 @@ class EngineContext:
             return self.engine.renorm_periodic(hi, lo, period, level, conj=conj)
         return self.engine.renorm_periodic(hi, lo, period, level)
 
+    def renorm_unpack_perm(self, packed, period: int, perm, level=None, conj=None):
+        """renorm_unpack with a byte permutation folded in (both halves)"""
+        return self.engine.renorm_unpack_perm(packed, period, perm, level, conj=conj)
+
     def renorm_periodic_perm(self, hi, lo, period: int, perm, level=None, conj=None):
         """renorm_periodic with a byte permutation folded in (output slot i <- input slot perm[i])"""
         return self.engine.renorm_periodic_perm(hi, lo, period, perm, level, conj=conj)

@@ -47,7 +47,7 @@ EXPORTED = [
     "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled", "aesfhe_set_enc_nonce", "aesfhe_launch_count", "aesfhe_launch_census",
     "aesfhe_galois_multi", "aesfhe_debug_boot_stage_sparse", "aesfhe_debug_sparse_group", "aesfhe_debug_sparse_group_plain",
     "aesfhe_debug_mono_pack", "aesfhe_debug_mono_split", "aesfhe_alg_bytes", "aesfhe_stack", "aesfhe_unstack", "aesfhe_members",
-    "aesfhe_renorm_packed", "aesfhe_renorm_packed_conj", "aesfhe_renorm_unpack_conj", "aesfhe_renorm_periodic_conj", "aesfhe_renorm_pack", "aesfhe_renorm_periodic_perm",
+    "aesfhe_renorm_packed", "aesfhe_renorm_packed_conj", "aesfhe_renorm_unpack_conj", "aesfhe_renorm_periodic_conj", "aesfhe_renorm_pack", "aesfhe_renorm_periodic_perm", "aesfhe_renorm_unpack_perm",
 ]
 
 # largest log2(PQ) for 128-bit classical security with a ternary secret (HE standard)
@@ -154,6 +154,7 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_renorm_packed_conj"] = [vp, _H, _H, c_int, c_int, _Hp]
     sig["aesfhe_renorm_periodic_conj"] = [vp, _H, _H, _H, _H, c_int, c_int, _Hp, _Hp]
     sig["aesfhe_renorm_pack"] = [vp, _H, _H, _H, _H, c_int, c_int, _Hp]
+    sig["aesfhe_renorm_unpack_perm"] = [vp, _H, _H, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS"), c_int, c_int, _Hp, _Hp]
     sig["aesfhe_renorm_periodic_perm"] = [vp, _H, _H, _H, _H, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS"), c_int, c_int, c_int, _Hp, _Hp]
     sig["aesfhe_renorm_unpack_conj"] = [vp, _H, _H, c_int, c_int, _Hp, _Hp]
     for name in EXPORTED:
@@ -839,6 +840,17 @@ class Engine:
         else:
             self._ctx.check(self._lib.aesfhe_renorm_periodic(self._ctx.ptr, hi.handle, lo.handle, int(period), lv, ctypes.byref(a),
                                                              ctypes.byref(b)))
+        return Ciphertext(self._ctx, a.value), Ciphertext(self._ctx, b.value)
+
+    def renorm_unpack_perm(self, packed, period: int, perm, level=None, conj=None):
+        """aesfhe_renorm_unpack with a byte permutation folded in (aesfhe_renorm_unpack_perm): output byte
+        i of both halves <- input byte perm[i]; conj: a conjugate partner of packed"""
+        a, b = ctypes.c_uint64(), ctypes.c_uint64()
+        p = np.ascontiguousarray(perm, np.int32)
+        if p.shape != (16,):
+            raise ValueError("renorm_unpack_perm: 16 entries")
+        self._ctx.check(self._lib.aesfhe_renorm_unpack_perm(self._ctx.ptr, packed.handle, 0 if conj is None else conj.handle, p, int(period),
+                                                            -1 if level is None else int(level), ctypes.byref(a), ctypes.byref(b)))
         return Ciphertext(self._ctx, a.value), Ciphertext(self._ctx, b.value)
 
     def renorm_periodic_perm(self, hi, lo, period: int, perm, level=None, conj=None, pack: bool = False):

@@ -218,6 +218,19 @@ class AESPipeline:
             return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb, defer_conj=True)
         return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb)
 
+    def _isr_perm(self, ct, debug):
+        """InvShiftRows' byte permutation when the renorm before it can fold it (as _sr_perm)"""
+        if debug is not None or not _SR_RENORM or self.true_fhe or not self.use_hard_renorm_between_steps:
+            return None
+        if not hasattr(self, "_isr_perm_v"):
+            sp = getattr(self.invshift, "slot_perm", None)
+            self._isr_perm_v = sp() if sp is not None else None
+        if self._isr_perm_v is None:
+            return None
+        ok = getattr(self.encoder, "renorm_perm_ok", None)
+        c0 = ct[0].s1 if hasattr(ct[0], "s1") else ct[0]
+        return self._isr_perm_v if ok is not None and ok(c0) else None
+
     def _sr_perm(self, ct, debug):
         """ShiftRows' byte permutation when the renorm before it can fold it (secret-key renorm mode,
         one period-16 state pair on the device, no debug log of the renorm's own output;
@@ -443,7 +456,13 @@ class AESPipeline:
         fuse = self.fuse_sub_ark
         if fuse and self.isub is None:
             raise KeyError("inv_sub_hi")
-        ct = self._renorm_pair(*ct, level=NEED_SUB_ARK_SR if fuse else self.need_isr_isb)
+        # InvShiftRows folded into the renorm before it (the packed decrypt: this renorm and every
+        # InvMixColumns renorm), as ShiftRows in encrypt (pipeline._sr_perm)
+        isr = self._isr_perm(ct, debug) if self.packed_dec and not fuse else None
+        if isr is not None:
+            ct, isr_done = self.encoder.renorm_perm(*ct, isr, level=self.need_isr_isb - SHIFTROWS_DEPTH), True
+        else:
+            ct, isr_done = self._renorm_pair(*ct, level=NEED_SUB_ARK_SR if fuse else self.need_isr_isb), False
         self._log_pair(debug, "dec.init.ark10.renorm", *ct)
         for r in range(9, 0, -1):
             if fuse:
@@ -461,7 +480,9 @@ class AESPipeline:
                 # packed XOR stage: AddRoundKey on the packed state, its renorm
                 # unpacking; InvMixColumns' XOR stage packed, unpacked by the renorm after it
                 # (a debug dict logs this path's stages under the reference's names)
-                ct = self.inv_shift_rows(*ct)
+                if not isr_done:
+                    ct = self.inv_shift_rows(*ct)
+                isr_done = False
                 self._log_pair(debug, f"dec.r{r}.isr", *ct)
                 ct = self._sub_renorm(ct, inverse=True, level=NEED_XOR + self.encoder.PACK_DEPTH)
                 self._log_pair(debug, f"dec.r{r}.isb", *ct)
@@ -469,7 +490,11 @@ class AESPipeline:
                 need = getattr(self.invmix, "packed_input_need", None)
                 ct = self.encoder.renorm_unpack(x, level=need() if need else NEED_GF + self.encoder.PACK_DEPTH)
                 self._log_pair(debug, f"dec.r{r}.ark", *ct)
-                ct = self.encoder.renorm_unpack(self.invmix.imc_packed(*ct), level=self.need_isr_isb)
+                if isr is not None:
+                    ct = self.encoder.renorm_unpack_perm(self.invmix.imc_packed(*ct), isr, level=self.need_isr_isb - SHIFTROWS_DEPTH)
+                    isr_done = True
+                else:
+                    ct = self.encoder.renorm_unpack(self.invmix.imc_packed(*ct), level=self.need_isr_isb)
                 self._log_pair(debug, f"dec.r{r}.imc", *ct)
                 continue
             ct = self.inv_shift_rows(*ct)
@@ -490,7 +515,8 @@ class AESPipeline:
             ct = self._renorm_pair(*ct)
             self._log_pair(debug, "dec.output", *ct)
             return ct
-        ct = self.inv_shift_rows(*ct)
+        if not isr_done:
+            ct = self.inv_shift_rows(*ct)
         self._log_pair(debug, "dec.final.isr", *ct)
         if self.isub is None:
             raise KeyError("inv_sub_hi")

@@ -251,9 +251,20 @@ class StateEncoder:
         return tag_layout(self.layout, *self.ctx.renorm_periodic_perm(ct_hi, ct_lo, self.layout.period, perm,
                                                                       None if _RENORM_FRESH else level, conj=conj))
 
+    def renorm_unpack_perm(self, ct, perm, level=None):
+        """renorm_unpack followed by a byte permutation of both halves, folded into the device renorm
+        (aesfhe_renorm_unpack_perm); the caller checks renorm_perm_ok.  ct may be a utils.ConjSum"""
+        conj = None
+        if isinstance(ct, ConjSum):
+            conj, ct = ct.s2, ct.s1
+        check_layout(self.layout, ct)
+        return tag_layout(self.layout, *self.ctx.renorm_unpack_perm(ct, self.layout.period, perm, None if _RENORM_FRESH else level,
+                                                                    conj=conj))
+
     def renorm_perm_ok(self, ct=None) -> bool:
         """whether renorm_perm runs on this encoder / context (one period-16 state pair on the device)"""
-        return getattr(self.ctx, "renorm_periodic_perm", None) is not None and self.pack_renorm_direct(ct, need_pack=False)
+        return (getattr(self.ctx, "renorm_periodic_perm", None) is not None and getattr(self.ctx, "renorm_unpack_perm", None) is not None
+                and self.pack_renorm_direct(ct, need_pack=False))
 
     def pack_renorm_direct(self, ct=None, need_pack: bool = True) -> bool:
         """whether renorm_pack runs as the device's packing renorm (then its inputs need no pack level);

@@ -241,6 +241,10 @@ int aesfhe_renorm_unpack(aesfhe_ctx* ctx, aesfhe_handle packed, int period, int 
  * pack_out != 0: one packed output as aesfhe_renorm_pack (out_lo unused). */
 int aesfhe_renorm_periodic_perm(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj,
                                 const int32_t* perm16, int pack_out, int period, int level, aesfhe_handle* out_hi, aesfhe_handle* out_lo);
+/* aesfhe_renorm_unpack (period 16) with a byte permutation folded in, applied to both unpacked
+ * halves (InvShiftRows after the renorm that follows InvMixColumns); packed_conj: 0 or a conjugate partner */
+int aesfhe_renorm_unpack_perm(aesfhe_ctx* ctx, aesfhe_handle packed, aesfhe_handle packed_conj, const int32_t* perm16, int period, int level,
+                              aesfhe_handle* out_hi, aesfhe_handle* out_lo);
 int aesfhe_renorm_pack(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj, int period, int level,
                        aesfhe_handle* out);
 int aesfhe_renorm_periodic_conj(aesfhe_ctx* ctx, aesfhe_handle hi, aesfhe_handle lo, aesfhe_handle hi_conj, aesfhe_handle lo_conj,

@@ -145,3 +145,25 @@ def test_shift_rows_folded_into_the_renorm(ctx, with_conj):
     assert np.abs(zh - ctx.decrypt(wh)).max() < 5e-3 and np.abs(zl - ctx.decrypt(wl)).max() < 5e-3
     p = np.asarray(perm)
     assert np.abs(zh[:16] - (Z16 ** nh)[p]).max() < 2e-4 and np.abs(zl[:16] - (Z16 ** nl_)[p]).max() < 2e-4
+
+
+def test_inv_shift_rows_folded_into_the_unpacking_renorm(ctx):
+    """aesfhe_renorm_unpack_perm with InvShiftRows' permutation equals InvShiftRows (masked
+    rotations) after renorm_unpack, per decoded slot of both halves"""
+    from inv_shiftrows import InvShiftRows
+    from state_encoder import StateEncoder
+    enc = StateEncoder(ctx, periodic=True)
+    isr = InvShiftRows(ctx, layout=enc.layout)
+    perm = isr.slot_perm()
+    assert perm is not None
+    E = ctx.engine
+    S = E.slot_count
+    rng = np.random.default_rng(12)
+    nib = rng.integers(0, 16, 32)
+    packed = ctx.encrypt(np.tile(256.0 * Z16 ** nib, S // 32))
+    gh, gl = ctx.renorm_unpack_perm(packed, 16, perm, None)
+    wh, wl = isr.apply(*ctx.renorm_unpack(packed, 16, None))
+    zh, zl = ctx.decrypt(gh), ctx.decrypt(gl)
+    assert np.abs(zh - ctx.decrypt(wh)).max() < 5e-3 and np.abs(zl - ctx.decrypt(wl)).max() < 5e-3
+    p = np.asarray(perm)
+    assert np.abs(zh[:16] - (Z16 ** nib[:16])[p]).max() < 2e-4 and np.abs(zl[:16] - (Z16 ** nib[16:])[p]).max() < 2e-4
