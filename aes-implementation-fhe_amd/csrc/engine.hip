@@ -2768,6 +2768,8 @@ public:
                 throw std::runtime_error("renorm: a slot permutation needs a single period-16 state pair");
             for (int i = 0; i < 16; ++i)
                 if (slot_perm[i] < 0 || slot_perm[i] > 15) throw std::runtime_error("renorm: slot permutation entries must lie in [0, 16)");
+            // checked before any temporary is taken or launch issued
+            if (unpack16 && !direct32_) throw std::runtime_error("renorm: a slot permutation needs the direct period-32 codec");
         }
         if (pack_out && (unpack || single || period != 16 || ct(hh).nb > 1 || ct(hl).nb > 1))
             throw std::runtime_error("renorm: the packed output needs a single period-16 state pair");

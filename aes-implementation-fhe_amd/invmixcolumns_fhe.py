@@ -11,7 +11,7 @@ from mixcol_final import _CoeffCache, gf_basis16, gf_eval, gf_mult_pair
 from shift_rows import row_masks
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT
-from utils import CONJ_RENORM, LUT2_DEPTH, NEED_BOOTSTRAP, NEED_GF, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, pair, rot_many, rot_pair
+from utils import FOLDS, LUT2_DEPTH, takes_kw, NEED_BOOTSTRAP, NEED_GF, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, pair, rot_many, rot_pair
 
 # AESFHE_IMC_GF_LOW=0: the packed InvMixColumns' GF multiplier pairs at their own depth above the XOR4s
 # (inputs at NEED_GF + PACK_DEPTH) instead of at the XOR4 level with renormalised outputs (A/B runs)
@@ -43,11 +43,8 @@ class InvMixColumnsFHE:
     def _xor(self, a, b, out_level=None, defer_conj: bool = False):
         """XOR4(a, b); defer_conj: straight into a secret-key renorm (utils.ConjSum, as
         MixColFinal._xor_ct)"""
-        if defer_conj and CONJ_RENORM:
-            try:
-                return self.xor4.apply(a, b, out_level, defer_conj=True)
-            except TypeError:  # an XOR4 without deferred conjugation
-                pass
+        if defer_conj and FOLDS.conj and takes_kw(self.xor4.apply, "defer_conj"):
+            return self.xor4.apply(a, b, out_level, defer_conj=True)
         return self.xor4.apply(a, b, out_level)
 
     def _renorm_pair(self, hi, lo, level=None):

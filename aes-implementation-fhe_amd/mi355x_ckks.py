@@ -702,6 +702,17 @@ class Engine:
         self._ctx.check(self._lib.aesfhe_unstack(self._ctx.ptr, ct.handle, n, out))
         return [Ciphertext(self._ctx, out[i]) for i in range(n)]
 
+    @staticmethod
+    def direct32() -> bool:
+        """whether the engine's renorm has the direct period-32 codec (csrc/engine.hip direct32_: off
+        with AESFHE_RENORM_DIRECT32=0, read the same way), which a slot-permuting unpack needs"""
+        v = os.environ.get("AESFHE_RENORM_DIRECT32")
+        if v is None:
+            return True
+        import re
+        m = re.match(r"\s*[+-]?\d+", v)
+        return not (m is None or int(m.group()) == 0)
+
     def members(self, ct) -> int:
         m = ctypes.c_int()
         self._ctx.check(self._lib.aesfhe_members(self._ctx.ptr, ct.handle, ctypes.byref(m)))

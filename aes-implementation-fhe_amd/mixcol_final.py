@@ -17,7 +17,7 @@ import numpy as np
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT, SplitLUT2, batched, eval_two, joint_bases, powers, std_basis
-from utils import CONJ_RENORM, LUT2_DEPTH, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, can_fork, drop_to, fused_lut, pair, rot_many, rot_pair
+from utils import FOLDS, LUT2_DEPTH, takes_kw, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, can_fork, drop_to, fused_lut, pair, rot_many, rot_pair
 
 # AESFHE_SHARE_R1=0: MixColumns' r1 basis rebuilt in its second XOR4 (A/B runs)
 _SHARE_R1 = os.environ.get("AESFHE_SHARE_R1", "1") != "0"
@@ -118,7 +118,7 @@ def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo, out_level=Non
                 raise
         else:
             if batched(ctx) and not can_fork(ctx):
-                out = eval_two(ctx, (sh, ("gf", mult, "hi"), A, B), (sl, ("gf", mult, "lo"), A, B), defer_conj and CONJ_RENORM)
+                out = eval_two(ctx, (sh, ("gf", mult, "hi"), A, B), (sl, ("gf", mult, "lo"), A, B), defer_conj and FOLDS.conj)
                 if out is not None:
                     return out
             else:
@@ -182,14 +182,11 @@ class MixColFinal:
     def _xor_ct(self, a, b, out_level=None, keep_b=None, defer_conj: bool = False):
         """XOR4(a, b); defer_conj: the result goes straight into a secret-key renorm, which may take
         the split LUT's S1 + conj(S2) unsummed (utils.ConjSum: no conjugation key switch)"""
-        kw = {"defer_conj": True} if defer_conj and CONJ_RENORM else {}
+        kw = {"defer_conj": True} if defer_conj and FOLDS.conj else {}
         if keep_b is not None:
             kw["keep_b"] = keep_b
-        if kw:
-            try:
-                return self.xor4.apply(a, b, out_level, **kw)
-            except TypeError:  # an XOR4 without basis sharing / deferred conjugation
-                pass
+        if kw and takes_kw(self.xor4.apply, *kw):
+            return self.xor4.apply(a, b, out_level, **kw)
         return self.xor4.apply(a, b, out_level)
 
     def _xor_pair(self, a, b, out_level=None):

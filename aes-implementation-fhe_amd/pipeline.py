@@ -53,13 +53,9 @@ from shift_rows import shift_rows_bytes
 from shiftrows_mixcolumns import ShiftRowsMixColumnsFusedEnc
 from sub_bytes_ark import SubBytesARK
 from sub_bytes_lut import SubBytesLUT
-from utils import (pair, CONJ_RENORM, SHIFTROWS_DEPTH, NEED_GF, NEED_ISR_ISB, NEED_SR_ARK, NEED_SR_MIX, NEED_SUB_ARK_SR, NEED_SUBBYTES, NEED_XOR,
+from utils import (pair, FOLDS, SHIFTROWS_DEPTH, NEED_GF, NEED_ISR_ISB, NEED_SR_ARK, NEED_SR_MIX, NEED_SUB_ARK_SR, NEED_SUBBYTES, NEED_XOR,
                    RENORM_FLOOR)
 from xor4_lut import XOR4LUT
-
-# AESFHE_SR_RENORM=0: ShiftRows as masked rotations after the renorm instead of folded into it (A/B)
-_SR_RENORM = os.environ.get("AESFHE_SR_RENORM", "1") != "0"
-
 
 # AESFHE_KEY_BASIS=0: the packed round keys' XOR4 bases rebuilt in every AddRoundKey (A/B runs)
 _KEY_BASIS = os.environ.get("AESFHE_KEY_BASIS", "1") != "0"
@@ -214,13 +210,13 @@ class AESPipeline:
         if not self._xor4_keep_b():  # an XOR4 without basis sharing (a caller-supplied LUT object)
             return self.xor4.apply(x, key, out_level=self._floor())
         kb = self._kb_cache.setdefault(r, {})
-        if defer_conj and CONJ_RENORM and self._xor4_defer_ok():
+        if defer_conj and FOLDS.conj and self._xor4_defer_ok():
             return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb, defer_conj=True)
         return self.xor4.apply(x, key, out_level=self._floor(), keep_b=kb)
 
     def _isr_perm(self, ct, debug):
         """InvShiftRows' byte permutation when the renorm before it can fold it (as _sr_perm)"""
-        if debug is not None or not _SR_RENORM or self.true_fhe or not self.use_hard_renorm_between_steps:
+        if not FOLDS.sr or self.true_fhe or not self.use_hard_renorm_between_steps:
             return None
         if not hasattr(self, "_isr_perm_v"):
             sp = getattr(self.invshift, "slot_perm", None)
@@ -232,10 +228,10 @@ class AESPipeline:
         return self._isr_perm_v if ok is not None and ok(c0) else None
 
     def _sr_perm(self, ct, debug):
-        """ShiftRows' byte permutation when the renorm before it can fold it (secret-key renorm mode,
-        one period-16 state pair on the device, no debug log of the renorm's own output;
-        AESFHE_SR_RENORM=0: rotate after the renorm), else None"""
-        if debug is not None or not _SR_RENORM or self.true_fhe or not self.use_hard_renorm_between_steps:
+        """ShiftRows' byte permutation when the renorm before it can fold it (utils.FOLDS.sr: off in the
+        strict default; secret-key renorm mode, one period-16 state pair on the device), else None.  A
+        debug run keeps the fold and logs what it can (no separate log of the renorm's own output)"""
+        if not FOLDS.sr or self.true_fhe or not self.use_hard_renorm_between_steps:
             return None
         if not hasattr(self, "_sr_perm_v"):
             sp = getattr(self.shift, "slot_perm", None)
@@ -251,7 +247,7 @@ class AESPipeline:
         output goes straight into _renorm_pair): the nibble form may hand over utils.ConjSum halves
         for the folded renorm"""
         lut = self.sub if lut is None else lut
-        if defer_conj and CONJ_RENORM and self.use_hard_renorm_between_steps and not self.true_fhe:
+        if defer_conj and FOLDS.conj and self.use_hard_renorm_between_steps and not self.true_fhe:
             import inspect
             try:
                 ok = "defer_conj" in inspect.signature(lut.apply).parameters
@@ -362,7 +358,7 @@ class AESPipeline:
             # XORs it with the packed round key, its renorm unpacks into the (hi, lo) pair.  A debug
             # dict logs THIS path's stages under the reference's names (the packed ones decoded from
             # the hi | lo halves), so the golden stage test observes the headline path itself.
-            ct = self._sub_apply(ct, defer_conj=debug is None)
+            ct = self._sub_apply(ct, defer_conj=True)
             self._log_pair(debug, f"enc.r{r}.sub", *ct)
             need = getattr(self.mix, "packed_input_need", None)
             lv = need() if need else NEED_SR_MIX - SHIFTROWS_DEPTH + self.encoder.PACK_DEPTH
@@ -376,7 +372,7 @@ class AESPipeline:
             self._log_pair(debug, f"enc.r{r}.sr", *ct)
             acc = self.mix.mix_packed(*ct)
             self._log_packed(debug, f"enc.r{r}.mc", acc)
-            x = self._ark_packed(acc, r, defer_conj=debug is None)
+            x = self._ark_packed(acc, r, defer_conj=True)
             self._log_packed(debug, f"enc.r{r}.ark", x)
             ct = self.encoder.renorm_unpack(x, level=next_level)
             self._log_pair(debug, f"enc.r{r}.ark.renorm", *ct)
@@ -426,7 +422,7 @@ class AESPipeline:
             ct = self._renorm_pair(*ct)
             self._log_pair(debug, "enc.output", *ct)
             return tag_layout(self.layout, *ct)
-        ct = self._sub_apply(ct, defer_conj=debug is None)
+        ct = self._sub_apply(ct, defer_conj=True)
         self._log_pair(debug, "enc.final.sub", *ct)
         perm = self._sr_perm(ct, debug)
         if perm is not None:  # ShiftRows folded into the renorm
@@ -486,7 +482,7 @@ class AESPipeline:
                 self._log_pair(debug, f"dec.r{r}.isr", *ct)
                 ct = self._sub_renorm(ct, inverse=True, level=NEED_XOR + self.encoder.PACK_DEPTH)
                 self._log_pair(debug, f"dec.r{r}.isb", *ct)
-                x = self._ark_packed(self.encoder.pack(*ct), r, defer_conj=debug is None)
+                x = self._ark_packed(self.encoder.pack(*ct), r, defer_conj=True)
                 need = getattr(self.invmix, "packed_input_need", None)
                 ct = self.encoder.renorm_unpack(x, level=need() if need else NEED_GF + self.encoder.PACK_DEPTH)
                 self._log_pair(debug, f"dec.r{r}.ark", *ct)

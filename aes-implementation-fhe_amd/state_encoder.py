@@ -27,12 +27,10 @@ from typing import Any, Tuple
 
 import numpy as np
 
-from utils import ConjSum, ZetaEncoder, conj_sum
+from utils import FOLDS, ConjSum, ZetaEncoder, conj_sum, takes_kw, tally_renorm
 
 # AESFHE_RENORM_FRESH=1: ignore renorm target levels (A/B measurements of DESIGN.md §3.11)
 _RENORM_FRESH = os.environ.get("AESFHE_RENORM_FRESH") == "1"
-# AESFHE_PACK_RENORM=0: renorm_pack packs with the masks, then renormalises (A/B)
-_PACK_RENORM = os.environ.get("AESFHE_PACK_RENORM", "1") != "0"
 
 
 class SlotLayout:
@@ -224,62 +222,98 @@ class StateEncoder:
         out = ((hi << 4) | lo).astype(np.uint8)
         return out[0] if self.states == 1 else out
 
+    UNPACK_DEPTH = 1  # unpack(): one mask product after the rotation
+
+    def _fold_conj(self, *cts):
+        """the renorm's inputs with any utils.ConjSum summed homomorphically unless the conjugation
+        fold is on (FOLDS.conj; strict renorms are the identity on the message)"""
+        return tuple(c if FOLDS.conj else conj_sum(self.ctx, c) for c in cts)
+
+    def unpack(self, ct):
+        """the packed state -> its (hi, lo) pair, homomorphically (the inverse of pack): both halves
+        are P-periodic inside the 2P-periodic message, so z = rot_P(ct) holds lo where ct holds hi
+        and vice versa, and hi = z + m0 (ct - z), lo = ct - m0 (ct - z) -- one rotation and one
+        mask product (UNPACK_DEPTH levels), every slot of both outputs as the packed input's"""
+        ctx = self.ctx
+        if getattr(self, "_half_pts", None) is None:
+            self._half_pts = [ctx.encode(self.layout.half_mask(w)) for w in (0, 1)]
+        z = ctx.rotate(ct, self.layout.period)
+        t = ctx.multiply(ctx.sub(ct, z), self._half_pts[0])
+        return tag_layout(self.layout, ctx.add(z, t), ctx.sub(ct, t))
+
     def renorm_packed(self, ct, level=None):
         """renorm of a packed state, packed again (ct may be a utils.ConjSum: s1 + conj(s2) renormalised
-        with the conjugation folded into the decryption)"""
+        with the conjugation folded into the decryption when FOLDS.conj)"""
+        (ct,) = self._fold_conj(ct)
+        lv = None if _RENORM_FRESH else level
+        single = self.ctx.renorm_single
         if isinstance(ct, ConjSum):
-            lv = None if _RENORM_FRESH else level
-            try:
-                return self.ctx.renorm_single(ct.s1, lv, period=2 * self.layout.period, conj=ct.s2)
-            except TypeError:  # a context without the folded form
-                ct = conj_sum(self.ctx, ct)
-        try:
-            return self.ctx.renorm_single(ct, None if _RENORM_FRESH else level, period=2 * self.layout.period)
-        except TypeError:  # a context whose renorm_single takes no period
-            return self.ctx.renorm_single(ct, None if _RENORM_FRESH else level)
+            if takes_kw(single, "period", "conj"):
+                tally_renorm(self.ctx, ct.s1)
+                return single(ct.s1, lv, period=2 * self.layout.period, conj=ct.s2)
+            ct = conj_sum(self.ctx, ct)
+        tally_renorm(self.ctx, ct)
+        if takes_kw(single, "period"):
+            return single(ct, lv, period=2 * self.layout.period)
+        return single(ct, lv)  # a context whose renorm_single takes no period
 
     def renorm_perm(self, ct_hi, ct_lo, perm, level=None):
         """renorm(hi, lo) followed by a byte permutation (output byte i <- input byte perm[i]), the
-        permutation folded into the device renorm (aesfhe_renorm_periodic_perm); the caller checks
-        renorm_perm_ok first.  utils.ConjSum halves are folded as in renorm"""
+        permutation folded into the device renorm (aesfhe_renorm_periodic_perm; FOLDS.sr, the caller
+        checks renorm_perm_ok first).  utils.ConjSum halves are folded as in renorm"""
+        if not FOLDS.sr:
+            raise RuntimeError("renorm_perm: the ShiftRows fold is off (utils.FOLDS.sr)")
+        ct_hi, ct_lo = self._fold_conj(ct_hi, ct_lo)
         conj = None
         if isinstance(ct_hi, ConjSum) and isinstance(ct_lo, ConjSum):
             conj, ct_hi, ct_lo = (ct_hi.s2, ct_lo.s2), ct_hi.s1, ct_lo.s1
         else:
             ct_hi, ct_lo = conj_sum(self.ctx, ct_hi), conj_sum(self.ctx, ct_lo)
         check_layout(self.layout, ct_hi, ct_lo)
+        tally_renorm(self.ctx, ct_hi, ct_lo)
         return tag_layout(self.layout, *self.ctx.renorm_periodic_perm(ct_hi, ct_lo, self.layout.period, perm,
                                                                       None if _RENORM_FRESH else level, conj=conj))
 
     def renorm_unpack_perm(self, ct, perm, level=None):
         """renorm_unpack followed by a byte permutation of both halves, folded into the device renorm
-        (aesfhe_renorm_unpack_perm); the caller checks renorm_perm_ok.  ct may be a utils.ConjSum"""
+        (aesfhe_renorm_unpack_perm; FOLDS.sr and FOLDS.unpack); the caller checks renorm_perm_ok"""
+        if not (FOLDS.sr and FOLDS.unpack):
+            raise RuntimeError("renorm_unpack_perm: the ShiftRows / unpack folds are off (utils.FOLDS)")
+        (ct,) = self._fold_conj(ct)
         conj = None
         if isinstance(ct, ConjSum):
             conj, ct = ct.s2, ct.s1
         check_layout(self.layout, ct)
+        tally_renorm(self.ctx, ct)
         return tag_layout(self.layout, *self.ctx.renorm_unpack_perm(ct, self.layout.period, perm, None if _RENORM_FRESH else level,
                                                                     conj=conj))
 
     def renorm_perm_ok(self, ct=None) -> bool:
-        """whether renorm_perm runs on this encoder / context (one period-16 state pair on the device)"""
-        return (getattr(self.ctx, "renorm_periodic_perm", None) is not None and getattr(self.ctx, "renorm_unpack_perm", None) is not None
-                and self.pack_renorm_direct(ct, need_pack=False))
+        """whether renorm_perm / renorm_unpack_perm run on this encoder / context (the ShiftRows and
+        unpack folds on, one period-16 state pair on the device, the engine's direct period-32 codec)"""
+        if not (FOLDS.sr and FOLDS.unpack):
+            return False
+        if not (getattr(self.ctx, "renorm_periodic_perm", None) is not None and getattr(self.ctx, "renorm_unpack_perm", None) is not None
+                and self.pack_renorm_direct(ct, need_pack=False)):
+            return False
+        direct = getattr(getattr(self.ctx, "engine", None), "direct32", None)
+        return direct is None or bool(direct())
 
     def pack_renorm_direct(self, ct=None, need_pack: bool = True) -> bool:
-        """whether renorm_pack runs as the device's packing renorm (then its inputs need no pack level);
-        ct: an input of the pair -- a stack of several state pairs takes pack + renorm"""
-        if not ((_PACK_RENORM or not need_pack) and getattr(self.ctx, "renorm_pack", None) is not None and self.renorm_hook is None
+        """whether renorm_pack runs as the device's packing renorm (FOLDS.pack; then its inputs need no
+        pack level); ct: an input of the pair -- a stack of several state pairs takes pack + renorm"""
+        if not ((FOLDS.pack or not need_pack) and getattr(self.ctx, "renorm_pack", None) is not None and self.renorm_hook is None
                 and self.layout.periodic and self.layout.period == 16 and self.pairs == 1):
             return False
         members = getattr(getattr(self.ctx, "engine", None), "members", None)
         return ct is None or members is None or members(ct.s1 if isinstance(ct, ConjSum) else ct) == 1
 
     def renorm_pack(self, ct_hi, ct_lo, level=None):
-        """renorm_packed(pack(hi, lo)): for one period-16 state pair the device renorm encodes the
-        snapped pair straight into the packed form (aesfhe_renorm_pack: no mask products, no pack
-        level; utils.ConjSum halves folded as in renorm); otherwise pack, then renorm"""
+        """renorm_packed(pack(hi, lo)): with the pack fold (FOLDS.pack) and one period-16 state pair the
+        device renorm encodes the snapped pair straight into the packed form (aesfhe_renorm_pack: no mask
+        products, no pack level; utils.ConjSum halves folded as in renorm); otherwise pack, then renorm"""
         if self.pack_renorm_direct(ct_hi):
+            ct_hi, ct_lo = self._fold_conj(ct_hi, ct_lo)
             rp = self.ctx.renorm_pack
             conj = None
             if isinstance(ct_hi, ConjSum) and isinstance(ct_lo, ConjSum):
@@ -287,20 +321,26 @@ class StateEncoder:
             else:
                 ct_hi, ct_lo = conj_sum(self.ctx, ct_hi), conj_sum(self.ctx, ct_lo)
             check_layout(self.layout, ct_hi, ct_lo)
+            tally_renorm(self.ctx, ct_hi, ct_lo)
             return tag_layout(self.layout, rp(ct_hi, ct_lo, self.layout.period, None if _RENORM_FRESH else level, conj=conj))[0]
         return self.renorm_packed(self.pack(ct_hi, ct_lo), level)
 
     def renorm_unpack(self, ct, level=None) -> Tuple[Any, Any]:
-        """renorm of a packed state into the (hi, lo) pair (ct may be a utils.ConjSum, as renorm_packed)"""
+        """renorm of a packed state into the (hi, lo) pair at `level`.  Strict (FOLDS.unpack off): the
+        packed renorm at level + UNPACK_DEPTH, then the homomorphic unpack; with the fold the device
+        renorm's encoder gathers the two halves (aesfhe_renorm_unpack).  ct may be a utils.ConjSum"""
+        if not FOLDS.unpack or getattr(self.ctx, "renorm_unpack", None) is None:
+            lv = None if level is None else level + self.UNPACK_DEPTH
+            return self.unpack(self.renorm_packed(ct, lv))
+        (ct,) = self._fold_conj(ct)
+        lv = None if _RENORM_FRESH else level
         if isinstance(ct, ConjSum):
             check_layout(self.layout, ct.s1)
-            try:
-                return tag_layout(self.layout, *self.ctx.renorm_unpack(ct.s1, self.layout.period, None if _RENORM_FRESH else level,
-                                                                       conj=ct.s2))
-            except TypeError:
-                ct = conj_sum(self.ctx, ct)
+            tally_renorm(self.ctx, ct.s1)
+            return tag_layout(self.layout, *self.ctx.renorm_unpack(ct.s1, self.layout.period, lv, conj=ct.s2))
         check_layout(self.layout, ct)
-        return tag_layout(self.layout, *self.ctx.renorm_unpack(ct, self.layout.period, None if _RENORM_FRESH else level))
+        tally_renorm(self.ctx, ct)
+        return tag_layout(self.layout, *self.ctx.renorm_unpack(ct, self.layout.period, lv))
 
     def renorm(self, ct_hi, ct_lo, level=None) -> Tuple[Any, Any]:
         """decode -> re-encode (REF/pipeline.py:65-69), done on the device when available;
@@ -308,18 +348,19 @@ class StateEncoder:
         With a renorm_hook (true-FHE mode) the hook runs instead (it reads `level` as the next step's need).
         hi / lo may be utils.ConjSum (s1 + conj(s2)): the periodic device renorm folds the conjugation
         into its decryption; any other path sums them first."""
+        ct_hi, ct_lo = self._fold_conj(ct_hi, ct_lo)
         if isinstance(ct_hi, ConjSum) or isinstance(ct_lo, ConjSum):
             per = getattr(self.ctx, "renorm_periodic", None)
             if (isinstance(ct_hi, ConjSum) and isinstance(ct_lo, ConjSum) and self.renorm_hook is None and self.layout.periodic
-                    and per is not None):
+                    and per is not None and takes_kw(per, "conj")):
                 check_layout(self.layout, ct_hi.s1, ct_lo.s1)
-                try:
-                    return tag_layout(self.layout, *per(ct_hi.s1, ct_lo.s1, self.layout.period, None if _RENORM_FRESH else level,
-                                                        conj=(ct_hi.s2, ct_lo.s2)))
-                except TypeError:  # a context without the folded form
-                    pass
+                tally_renorm(self.ctx, ct_hi.s1, ct_lo.s1)
+                return tag_layout(self.layout, *per(ct_hi.s1, ct_lo.s1, self.layout.period, None if _RENORM_FRESH else level,
+                                                    conj=(ct_hi.s2, ct_lo.s2)))
             ct_hi, ct_lo = conj_sum(self.ctx, ct_hi), conj_sum(self.ctx, ct_lo)
         check_layout(self.layout, ct_hi, ct_lo)
+        if self.renorm_hook is None:
+            tally_renorm(self.ctx, ct_hi, ct_lo)
         return tag_layout(self.layout, *self._renorm(ct_hi, ct_lo, level))
 
     def _renorm(self, ct_hi, ct_lo, level):

@@ -22,7 +22,7 @@ import os
 from typing import Any, Dict, Tuple
 
 import numpy as np
-from utils import CONJ_RENORM, LUT2_DEPTH, SUBBYTES_DEPTH, can_fork, conj_many, drop_to, fused_lut, mul_many, pair
+from utils import FOLDS, LUT2_DEPTH, SUBBYTES_DEPTH, can_fork, conj_many, drop_to, fused_lut, mul_many, pair
 
 _TOL = 1e-12
 # AESFHE_SB_NIB=0: the pipeline keeps the reference's 8 -> 4 form (lift to b = ζ256^byte, depth 13)
@@ -120,7 +120,7 @@ class SubBytesLUTFastCached:
         from mixcol_final import gf_mult_pair
         if not hasattr(self, "_nib"):
             self._nib = _NibbleLUTs(self.hi, self.lo)
-        return gf_mult_pair(self.ctx, self._nib, "sbox", ct_hi, ct_lo, defer_conj=defer_conj and CONJ_RENORM)
+        return gf_mult_pair(self.ctx, self._nib, "sbox", ct_hi, ct_lo, defer_conj=defer_conj and FOLDS.conj)
 
     @staticmethod
     def _power(basis, k: int, domain: int, ctx):

@@ -51,8 +51,90 @@ class ConjSum:
         self.s1, self.s2 = s1, s2
 
 
-# AESFHE_CONJ_RENORM=0: every conjugate-split LUT sums its conjugation homomorphically (A/B)
-CONJ_RENORM = os.environ.get("AESFHE_CONJ_RENORM", "1") != "0"
+class RenormFolds:
+    """Which AES work the secret-key renorm may fold into its decrypt -> snap -> re-encrypt.
+
+    The reference's renorm is the identity on the message: decrypt, snap every slot to the nearest
+    Zeta16 codeword, re-encrypt (REF/pipeline.py:65-69, REF/mixcol_final.py:104-106).  Each fold
+    below makes the engine's renorm compute a function of the decrypted message instead:
+
+    - ``conj``: a conjugate-split LUT's S1 + conj(S2) summed after the decryption (the reference
+      conjugates by key switch, REF/xor4_lut.py:57-59);
+    - ``sr``: (Inv)ShiftRows as a slot permutation of the snap (the reference rotates masked rows,
+      REF/shift_rows.py:39-56);
+    - ``pack``: the hi | lo packing written by the renorm's encoder (homomorphic: two mask products);
+    - ``unpack``: the packed state gathered into its (hi, lo) pair by the renorm's encoder
+      (homomorphic: one rotation and a mask product, StateEncoder.unpack).
+
+    Strict (the default; the bench's headline): none of them, so every renorm is the identity on
+    the message and all AES work between encryption and decryption is homomorphic.
+    AESFHE_RENORM_FOLDS=1 (or ``set_all(True)``, the bench's secondary ``folded`` leg) enables
+    them; AESFHE_CONJ_RENORM / AESFHE_SR_RENORM / AESFHE_PACK_RENORM / AESFHE_UNPACK_RENORM=0 then
+    switch one off (A/B).  Read at call time, so a process can run both forms."""
+
+    def __init__(self):
+        self.set_all(os.environ.get("AESFHE_RENORM_FOLDS", "0") == "1")
+
+    def set_all(self, on: bool) -> None:
+        env = lambda k: os.environ.get(k, "1") != "0"  # noqa: E731
+        self.conj = bool(on) and env("AESFHE_CONJ_RENORM")
+        self.sr = bool(on) and env("AESFHE_SR_RENORM")
+        self.pack = bool(on) and env("AESFHE_PACK_RENORM")
+        self.unpack = bool(on) and env("AESFHE_UNPACK_RENORM")
+
+    @property
+    def any(self) -> bool:
+        return self.conj or self.sr or self.pack or self.unpack
+
+    def state(self):
+        return (self.conj, self.sr, self.pack, self.unpack)
+
+    def restore(self, st) -> None:
+        self.conj, self.sr, self.pack, self.unpack = st
+
+
+FOLDS = RenormFolds()
+
+
+class renorm_folds:
+    """``with renorm_folds(True): ...`` -- the folds switched for the block (bench.py's folded leg)"""
+
+    def __init__(self, on: bool):
+        self.on = on
+
+    def __enter__(self):
+        self._st = FOLDS.state()
+        FOLDS.set_all(self.on)
+        return FOLDS
+
+    def __exit__(self, *exc):
+        FOLDS.restore(self._st)
+        return False
+
+
+# Secret-key renorm tally (ciphertexts decrypted and re-encrypted; a stack of P members counts P):
+# the bench reports it per encrypt beside the reference's 48 pairs (REF/pipeline.py:123-188)
+RENORM_TALLY = {"calls": 0, "ciphertexts": 0}
+
+
+def tally_renorm(ctx, *cts) -> None:
+    RENORM_TALLY["calls"] += 1
+    members = getattr(getattr(ctx, "engine", None), "members", None)
+    for c in cts:
+        RENORM_TALLY["ciphertexts"] += members(c) if members is not None and hasattr(c, "handle") else 1
+
+
+def takes_kw(fn, *names) -> bool:
+    """whether callable fn accepts every keyword in `names` (checked by signature, so a TypeError
+    raised inside an evaluation is never mistaken for a missing keyword)"""
+    import inspect
+    try:
+        params = inspect.signature(fn).parameters
+    except (TypeError, ValueError):
+        return False
+    if any(p.kind is inspect.Parameter.VAR_KEYWORD for p in params.values()):
+        return True
+    return all(n in params for n in names)
 
 
 def conj_sum(ctx, x):

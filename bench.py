@@ -89,6 +89,8 @@ def parse():
                     help="multi-pair slot-packed batch: this many stacked ciphertext pairs of 2048 states each per rank; 0 = skip")
     ap.add_argument("--pair-steps", type=int, default=1, help="timed steps of the one-state multi-pair leg (C3 literally)")
     ap.add_argument("--packed-pair-steps", type=int, default=3, help="timed steps of the slot-packed multi-pair leg")
+    ap.add_argument("--folded-steps", type=int, default=5,
+                    help="timed steps of the 'folded' leg: C2 with the renorm folds on (utils.RenormFolds; the headline is strict)")
     ap.add_argument("--true-fhe-steps", type=int, default=1,
                     help="SURVEY.md 8(f)3 line beside the headline: C2 encrypts with every secret-key renorm replaced "
                          "by bootstrap + homomorphic Zeta16 snap (AESPipeline(true_fhe=True)); 0 = skip")
@@ -259,8 +261,10 @@ def _progress(ctx, every_s: float = 30.0):
 
 def state_slots(pipe, ctx, ct, packed: bool) -> np.ndarray:
     """decrypted slot values of every state of a (stacked) ciphertext: (hi | lo of a packed one)"""
+    from utils import conj_sum
     enc = pipe.encoder
     out = []
+    ct = conj_sum(ctx, ct)  # a folded-renorm input logged unsummed (utils.ConjSum): its value s1 + conj(s2)
     for c in (ctx.unstack(ct) if enc.pairs > 1 else [ct]):
         z = ctx.decrypt(c)
         out.append(enc._take(z).ravel())
@@ -539,6 +543,48 @@ def run_batch(ctx, coeffs, rks, args, rank, world, dist, tj: dict) -> dict:
             **({"roundtrip": rt} if rt else {})}
 
 
+def run_folded(ctx, coeffs, rks, args, rank, world, dist, mix_layout, strict_value: float) -> dict:
+    """The C2 workload with the secret-key renorm allowed to fold AES work into its decrypt -> snap ->
+    re-encrypt (utils.RenormFolds: ShiftRows as a slot permutation, the conjugate-split LUTs' S1 +
+    conj(S2), the hi | lo pack and unpack).  NOT the reference's workload -- its renorm is the identity
+    on the message (REF/pipeline.py:65-69) -- reported beside the strict headline with the delta."""
+    from mixcol_final import MixColFinal
+    from oracle import aes_plain  # checker only, after the timed region
+    from pipeline import AESPipeline
+    from utils import RENORM_TALLY, renorm_folds
+    from xor4_lut import XOR4LUT
+    with renorm_folds(True) as folds:
+        xor4 = XOR4LUT(ctx, coeffs["xor4"])
+        pipe = AESPipeline(ctx, coeffs, mixcolumns=MixColFinal(ctx, xor4, layout=mix_layout), use_hard_renorm_between_steps=True,
+                           periodic=mix_layout.periodic)
+        sts = rank_states(rank + 5000, 1 + args.folded_steps)
+        pipe.encrypt(sts[0], rks)
+        ctx.engine.sync()
+        import mi355x_ckks
+        l0 = mi355x_ckks.launch_count()
+        r0 = dict(RENORM_TALLY)
+        barrier(dist)
+        t0 = time.perf_counter()
+        outs = [pipe.encrypt(s, rks) for s in sts[1:]]
+        ctx.engine.sync()
+        barrier(dist)
+        elapsed = time.perf_counter() - t0
+        l1 = mi355x_ckks.launch_count()
+        folds_on = dict(conj=folds.conj, sr=folds.sr, pack=folds.pack, unpack=folds.unpack)
+    elapsed = max_over_ranks(dist, elapsed)
+    ok = all(np.array_equal(pipe.encoder.decode(*o), aes_plain.ref_encrypt(s, rks)) for s, o in zip(sts[1:], outs))
+    ok = all(r[0] for r in all_gather_ints(dist, [int(ok)]))
+    steps = args.folded_steps
+    rps = 10.0 * steps * world / elapsed
+    return {"workload": "C2 with the renorm folds on (not REF's workload: the renorm computes ShiftRows, conjugations, "
+                        "pack/unpack on the decrypted message)", "folds": folds_on,
+            "rounds_per_s": rps, "ms_per_step": elapsed / steps * 1e3, "steps": steps,
+            "delta_vs_strict": rps / strict_value - 1.0 if strict_value else None,
+            "launches_per_encrypt": (l1 - l0) / steps,
+            "secret_key_renorms_per_encrypt": (RENORM_TALLY["ciphertexts"] - r0["ciphertexts"]) / steps,
+            "verified_against_plaintext_model": bool(ok)}
+
+
 def run_true_fhe(ctx, coeffs, rks, args, rank, world, dist, tj: dict) -> dict:
     """the C2 workload with no secret key between encryption and decryption --
     every renorm point is a bootstrap + homomorphic Zeta16 snap (zeta16_noise_reducer.py), XOR4
@@ -695,10 +741,14 @@ def _compact_precision(p: dict | None) -> dict | None:
 def _compact_leg(d: dict) -> dict:
     """one secondary leg: its throughput, verification, step roofline (with per-class arrays), precision"""
     num = ("blocks_per_s", "rounds_per_s", "ms_per_step", "ms_per_pair", "steps", "pairs_per_rank", "states_per_pair",
-           "pairs_per_stack", "states_per_rank_per_step", "bootstraps_per_encrypt", "launches_per_encrypt")
+           "pairs_per_stack", "states_per_rank_per_step", "bootstraps_per_encrypt", "launches_per_encrypt", "delta_vs_strict",
+           "secret_key_renorms_per_encrypt")
     out = {k: _sig(d[k], 5) for k in num if k in d}
     out["verified"] = d.get("verified_against_plaintext_model")
-    out["roofline_step"] = _compact_step(d.get("roofline_step"))
+    if d.get("folds") is not None:
+        out["folds"] = d["folds"]
+    if d.get("roofline_step") is not None:
+        out["roofline_step"] = _compact_step(d.get("roofline_step"))
     if d.get("precision"):
         out["precision"] = _compact_precision(d["precision"])
     rt = d.get("roundtrip")
@@ -716,11 +766,13 @@ LEG_NOTES = {
     "batch.roundtrip": "C5: enc->dec round trip of --c5-states states split over the ranks, bit-exact check",
     "batch_pairs": "C3 literally: --pair-states one-state ciphertext pairs per GPU, stacked --pair-stack per operand",
     "batch_packed_pairs": "--packed-pairs slot-packed pairs of 2048 states stacked into one operand",
+    "folded": "C2 with the renorm folds on (ShiftRows / conjugations / pack / unpack computed inside the secret-key renorm): "
+              "NOT REF's workload; delta_vs_strict against the headline value, whose renorms are the identity on the message",
     "true_fhe": "C2 with every secret-key renorm replaced by bootstrap + homomorphic Zeta16 snap",
     "eager_ref_calls": "C2 via EngineContext with REF's call sequence, eager relin/rescale, reference slot layout",
     "deferred_ref_calls": "C2 via EngineContext with REF's call sequence (per-term loops), deferred evaluation on",
 }
-LEG_KEYS = ("batch", "batch_pairs", "batch_packed_pairs", "true_fhe", "eager_ref_calls", "deferred_ref_calls")
+LEG_KEYS = ("batch", "folded", "batch_pairs", "batch_packed_pairs", "true_fhe", "eager_ref_calls", "deferred_ref_calls")
 
 
 def compact_line(full: dict, detail_path: str | None = None) -> dict:
@@ -745,6 +797,8 @@ def compact_line(full: dict, detail_path: str | None = None) -> dict:
     if line["roofline_step"]:
         line["roofline_step"]["traffic_over_algorithmic"] = _traffic_ratios(full.get("roofline_step"))
     line["launches_per_encrypt"] = _sig(full.get("launches_per_encrypt"), 6)
+    if full.get("secret_key_renorms_per_encrypt") is not None:
+        line["secret_key_renorms_per_encrypt"] = {k: _sig(v, 5) for k, v in full["secret_key_renorms_per_encrypt"].items()}
     line["precision"] = _compact_precision(full.get("precision"))
     for k in LEG_KEYS:
         if full.get(k) is not None:
@@ -905,7 +959,9 @@ def main():
     mark = os.environ.get("AESFHE_MARK_TIMED") == "1"
     if mark:
         time.sleep(0.25)
+    from utils import FOLDS, RENORM_TALLY
     alg0, launches0 = mi355x_ckks.alg_bytes(), mi355x_ckks.launch_count()
+    ren0 = dict(RENORM_TALLY)
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
         outs.append(pipe.encrypt(states[i], rks))
@@ -913,6 +969,9 @@ def main():
     barrier(dist)
     elapsed = time.perf_counter() - t0
     alg1, launches1 = mi355x_ckks.alg_bytes(), mi355x_ckks.launch_count()
+    renorms = {"ciphertexts": (RENORM_TALLY["ciphertexts"] - ren0["ciphertexts"]) / args.steps,
+               "calls": (RENORM_TALLY["calls"] - ren0["calls"]) / args.steps,
+               "reference_pairs": 48, "reference_ciphertexts": 96, "strict": not FOLDS.any}
     if mark:
         time.sleep(0.25)
     counters = E.counters()
@@ -937,6 +996,8 @@ def main():
                              f"{args.packed_pairs} x 2048 states per GPU: {args.packed_pairs} slot-packed ciphertext pairs stacked "
                              f"into one operand (DESIGN.md 3.9 + 3.16), full AES-128 encrypt, N=2^16, renorm on, shared key",
                              tj) if args.packed_pairs > 0 else None
+    folded = (run_folded(ctx, coeffs, rks, args, rank, world, dist, layout, 10.0 * args.steps * world / elapsed)
+              if args.folded_steps > 0 and not args.no_final_bootstrap and not whole else None)
     true_fhe = (run_true_fhe(ctx, coeffs, rks, args, rank, world, dist, tj)
                 if args.true_fhe_steps > 0 and not args.no_final_bootstrap else None)
     E.profile(())
@@ -976,7 +1037,7 @@ def main():
         "dtype": "u32 (RNS residues, 30-bit primes; CKKS scale Delta ~ 2^29.9 on the single-prime levels, see precision)",
         "data": "synthetic random 16-byte states, FIPS key schedule of a seed-7 master key",
         "config": {"workload": "C2: full AES-128 encrypt (10 rounds), 1 packed state per ciphertext pair, "
-                               "N=2^16, renorm on" + ("" if not args.no_final_bootstrap else ", FINAL BOOTSTRAP SKIPPED"),
+                               "N=2^16, renorm on (strict: every secret-key renorm the identity on the message, as REF's)" + ("" if not args.no_final_bootstrap else ", FINAL BOOTSTRAP SKIPPED"),
                    "log_n": 16, "states_per_rank_per_step": 1, "parallelism": f"replicas x{world}",
                    "slot_layout": ("reference (byte i at slot i*N/32; full-slot bootstraps)" if args.ref_layout else
                                    "periodic (the 16-slot state block repeated; MixColumns' final bootstraps as "
@@ -994,6 +1055,9 @@ def main():
                   "raw-ciphertext parity with the reference's desilofhe engine is unpinnable (closed binary, absent)",
         **roof,
         "launches_per_encrypt": launches_per_encrypt,
+        # secret-key renorms (decrypt -> snap -> re-encrypt) per encrypt, in ciphertexts; REF: 48 pairs
+        # (REF/pipeline.py:123-188).  strict: every renorm is the identity on the message (utils.RenormFolds)
+        "secret_key_renorms_per_encrypt": renorms,
         "precision": precision,
         "op_counts_per_round": {k: v / (10.0 * args.steps) for k, v in counters.items()},
     }
@@ -1003,6 +1067,8 @@ def main():
         line["batch_pairs"] = pairs_c3
     if pairs_packed is not None:
         line["batch_packed_pairs"] = pairs_packed
+    if folded is not None:
+        line["folded"] = folded
     if true_fhe is not None:
         line["true_fhe"] = true_fhe
     if eager is not None:

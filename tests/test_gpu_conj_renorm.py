@@ -19,6 +19,14 @@ def ctx():
     return gpu_context(log_n=16, signature=1)
 
 
+@pytest.fixture
+def folds_on():
+    """the renorm folds switched on for one test (utils.RenormFolds; the default is strict)"""
+    from utils import renorm_folds
+    with renorm_folds(True) as f:
+        yield f
+
+
 def _split(ctx, seed):
     """(s1, s2, nibbles): s1 + conj(s2) = 256 zeta16^nib (32-periodic, with < pi/32 jitter)"""
     E = ctx.engine
@@ -88,7 +96,7 @@ def test_pair_conj_renorm_matches_summed(ctx):
 
 
 @pytest.mark.parametrize("with_conj", [False, True])
-def test_packing_renorm_matches_pack_then_renorm(ctx, with_conj):
+def test_packing_renorm_matches_pack_then_renorm(ctx, with_conj, folds_on):
     """aesfhe_renorm_pack: the period-16 pair renormalised straight into the packed period-32 form
     (no mask products) equals renorm_packed(pack(hi, lo)), with or without conjugate partners"""
     from state_encoder import StateEncoder
@@ -116,7 +124,7 @@ def test_packing_renorm_matches_pack_then_renorm(ctx, with_conj):
 
 
 @pytest.mark.parametrize("with_conj", [False, True])
-def test_shift_rows_folded_into_the_renorm(ctx, with_conj):
+def test_shift_rows_folded_into_the_renorm(ctx, with_conj, folds_on):
     """aesfhe_renorm_periodic_perm with ShiftRows' byte permutation equals ShiftRows (masked
     rotations) after the renorm, per decoded slot, with or without conjugate partners"""
     from shift_rows import ShiftRows
@@ -167,3 +175,24 @@ def test_inv_shift_rows_folded_into_the_unpacking_renorm(ctx):
     assert np.abs(zh - ctx.decrypt(wh)).max() < 5e-3 and np.abs(zl - ctx.decrypt(wl)).max() < 5e-3
     p = np.asarray(perm)
     assert np.abs(zh[:16] - (Z16 ** nib[:16])[p]).max() < 2e-4 and np.abs(zl[:16] - (Z16 ** nib[16:])[p]).max() < 2e-4
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_homomorphic_unpack_matches_the_unpacking_renorm(ctx, seed):
+    """StateEncoder.renorm_unpack in the strict default (the packed renorm, then one rotation and a
+    mask product) gives the (hi, lo) pair of the engine's gathering renorm (aesfhe_renorm_unpack, the
+    fold), slot for slot, at the same level"""
+    from state_encoder import StateEncoder
+    from utils import FOLDS
+    assert not FOLDS.unpack
+    enc = StateEncoder(ctx, periodic=True)
+    S = ctx.engine.slot_count
+    rng = np.random.default_rng(seed)
+    nib = rng.integers(0, 16, 32)
+    packed = ctx.encrypt(np.tile(256.0 * Z16 ** nib * np.exp(1j * rng.uniform(-np.pi / 32, np.pi / 32, 32)), S // 32))
+    hi, lo = enc.renorm_unpack(packed, level=7)
+    wh, wl = ctx.renorm_unpack(packed, 16, 7)
+    assert hi.level == wh.level == 7 and lo.level == wl.level == 7
+    zh, zl = _close(ctx, hi, wh), _close(ctx, lo, wl)
+    assert np.abs(zh - np.tile(Z16 ** nib[:16], S // 16)).max() < 2e-4
+    assert np.abs(zl - np.tile(Z16 ** nib[16:], S // 16)).max() < 2e-4

@@ -5,9 +5,12 @@ whose LUT is the same for both halves -- MixColumns' XOR4s and the AddRoundKey a
   (aesfhe_renorm_single, aesfhe_renorm_unpack) against the byte model;
 - one XOR4 on packed states == the XOR pair (REF/xor4_lut.py:10-78 per nibble);
 - MixColFinal.mix_packed == REF/mixcol_final.py's MixColumns bytes (final bootstrap on);
-- full C2 encrypts through the packed path (no debug dict: the debug path keeps the pair steps)
-  == aes_plain.ref_encrypt, one state and a 64-state batch, and == the pair path's bytes, and
-  decrypt through the packed AddRoundKey / InvMixColumns stage returns the plaintext;
+- full C2 encrypts through the packed path == aes_plain.ref_encrypt, one state and a 64-state
+  batch, and == the pair path's bytes, and decrypt through the packed AddRoundKey / InvMixColumns
+  stage returns the plaintext;
+- the strict default (utils.RenormFolds): an encrypt + decrypt with every folding renorm entry
+  point of the engine disabled -- each renorm the identity on the message, as REF's -- and the
+  folded form's bytes (the bench's secondary leg);
 - SubBytes' bivariate giant-step form (sub_bytes_lut._outputs_biv) == the S-box on all bytes.
 Decoded bytes must be exact.
 """
@@ -145,3 +148,64 @@ def test_subbytes_bivariate_giant_step_form(ctx, co):
     ref = enc.decode(*sb.apply(*y, out_level=RENORM_FLOOR))  # the batched-product form
     assert np.array_equal(got, want)
     assert np.array_equal(ref, want)
+
+
+class _NoFolds:
+    """the context with every renorm entry point that computes on the decrypted message made to
+    raise: the gathering unpack, the packing renorm, the slot permutations, conjugate partners"""
+
+    def __init__(self, ctx):
+        self._ctx = ctx
+
+    def __getattr__(self, name):
+        if name in ("renorm_unpack", "renorm_unpack_perm", "renorm_periodic_perm", "renorm_pack"):
+            def refuse(*a, **k):
+                raise AssertionError(f"strict renorm path called the folding renorm {name}")
+            return refuse
+        attr = getattr(self._ctx, name)
+        if name in ("renorm_single", "renorm_periodic", "renorm_pair"):
+            def plain(*a, conj=None, **k):
+                assert conj is None, f"strict renorm path passed a conjugate partner to {name}"
+                return attr(*a, **k)
+            return plain
+        return attr
+
+
+@pytest.mark.parametrize("seed", [5, 11])
+def test_strict_path_renorms_are_the_identity(ctx, co, seed):
+    """the headline (strict) encrypt and decrypt never reach a renorm that permutes, packs, unpacks or
+    conjugates the decrypted message, and their bytes are FIPS-197's"""
+    from aes_keyschedule import expand_aes128_key
+    from oracle import aes_plain
+    from pipeline import AESPipeline
+    from utils import FOLDS, RENORM_TALLY
+    assert not FOLDS.any
+    nf = _NoFolds(ctx)
+    pipe = AESPipeline(nf, co, use_hard_renorm_between_steps=True)
+    assert pipe.packed_xor and pipe.packed_dec
+    rng = np.random.default_rng(seed)
+    rks = expand_aes128_key(rng.integers(0, 256, 16).astype(np.uint8))
+    pt = rng.integers(0, 256, 16).astype(np.uint8)
+    n0 = RENORM_TALLY["ciphertexts"]
+    ct = pipe.encrypt(pt, rks)
+    assert np.array_equal(pipe.encoder.decode(*ct), aes_plain.ref_encrypt(pt, rks))
+    # every renorm counted: REF runs 48 pairs (96 ciphertexts); the packed XOR stage renorms single ones
+    assert 40 <= RENORM_TALLY["ciphertexts"] - n0 <= 120
+    assert np.array_equal(pipe.encoder.decode(*pipe.decrypt(*ct, rks)), pt)
+
+
+def test_folded_form_bytes(ctx, co):
+    """the bench's secondary 'folded' leg: the renorm folds on, the same bytes"""
+    from aes_keyschedule import expand_aes128_key
+    from oracle import aes_plain
+    from pipeline import AESPipeline
+    from utils import renorm_folds
+    rng = np.random.default_rng(3)
+    rks = expand_aes128_key(rng.integers(0, 256, 16).astype(np.uint8))
+    pt = rng.integers(0, 256, 16).astype(np.uint8)
+    with renorm_folds(True) as f:
+        assert f.conj and f.sr and f.pack and f.unpack
+        pipe = AESPipeline(ctx, co, use_hard_renorm_between_steps=True)
+        ct = pipe.encrypt(pt, rks)
+        assert np.array_equal(pipe.encoder.decode(*ct), aes_plain.ref_encrypt(pt, rks))
+        assert np.array_equal(pipe.encoder.decode(*pipe.decrypt(*ct, rks)), pt)

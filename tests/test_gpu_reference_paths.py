@@ -205,3 +205,32 @@ def test_decrypt_every_debug_stage_matches_byte_model(ctx, coeff_dir, packed):
     bad = [t for t, exp in want.items() if t not in dbg or dbg[t]["plain"] is None or not np.array_equal(dbg[t]["plain"], exp)]
     assert not bad, bad
     assert np.array_equal(pipe.encoder.decode(*back), pt)
+
+
+def test_encrypt_debug_stages_with_the_renorm_folds(ctx, coeff_dir):
+    """a debug run keeps the renorm folds (utils.RenormFolds, the bench's 'folded' leg) and logs what it
+    can: every stage it logs that decodes matches tests/golden/stages.json; the ShiftRows fold leaves
+    no separate post-renorm log, and a conjugate-split output (utils.ConjSum) is logged undecoded"""
+    from aes_keyschedule import load_all_coeffs
+    from pipeline import AESPipeline
+    from utils import renorm_folds
+    fx = {s["seed"]: s for s in json.loads((GOLDEN / "stages.json").read_text())["seeds"]}[7]
+    pt = np.array(fx["plaintext"], np.uint8)
+    rks = [np.array(k, np.uint8) for k in fx["round_keys"]]
+    with renorm_folds(True):
+        pipe = AESPipeline(ctx, load_all_coeffs(coeff_dir), use_hard_renorm_between_steps=True)
+        dbg = {}
+        ct = pipe.encrypt(pt, rks, debug=dbg)
+    want = {"enc.input": pt}
+    for tag, stage in _FINAL.items():
+        want[tag] = np.array(fx["stages"][stage], np.uint8)
+    for r in range(1, 10):
+        for step, stage in _STAGE.items():
+            want[f"enc.r{r}.{step}"] = np.array(fx["stages"][f"r{r}.{stage}"], np.uint8)
+    assert set(dbg) <= set(want) and set(want) - set(dbg) <= {f"enc.r{r}.sub.renorm" for r in range(1, 10)} | {"enc.final.sub.renorm"}
+    decoded = [t for t in dbg if dbg[t]["plain"] is not None]
+    bad = [t for t in decoded if not np.array_equal(dbg[t]["plain"], want[t])]
+    assert not bad, bad
+    for r in range(1, 10):  # the steps after a folded renorm decode
+        assert all(dbg[f"enc.r{r}.{k}"]["plain"] is not None for k in ("sr", "mc", "ark.renorm"))
+    assert np.array_equal(pipe.encoder.decode(*ct), np.array(fx["ciphertext"], np.uint8))

@@ -10,7 +10,7 @@ for pass in $(seq 1 ${PASSES:-2}); do
   for cfg in "$@"; do
     envs=()
     [ "$cfg" != "-" ] && IFS=, read -ra envs <<< "$cfg"
-    env "${envs[@]}" timeout -k 10 150 python3 bench.py --no-cpu-baseline --batch-states 0 --true-fhe-steps 0 --pair-states 0 \
+    env "${envs[@]}" timeout -k 10 150 python3 bench.py --no-cpu-baseline --batch-states 0 --folded-steps 0 --true-fhe-steps 0 --pair-states 0 \
         --packed-pairs 0 --eager-steps 0 --deferred-steps 0 --steps 10 | sed "s|^|$cfg |" >> $O/bench.txt
   done
 done

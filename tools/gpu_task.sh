@@ -25,7 +25,7 @@ O=gpurun_out/${1:?out dir}
 shift
 mkdir -p $O
 export TMPDIR=/tmp
-C2="--no-cpu-baseline --batch-states 0 --true-fhe-steps 0 --pair-states 0 --packed-pairs 0 --eager-steps 0 --deferred-steps 0"
+C2="--no-cpu-baseline --batch-states 0 --folded-steps 0 --true-fhe-steps 0 --pair-states 0 --packed-pairs 0 --eager-steps 0 --deferred-steps 0"
 for t in "$@"; do
   echo "[gpu_task] $t $(date +%T)"
   case $t in
