@@ -3615,12 +3615,16 @@ public:
     // 11,407 launches per step, 4,984-5,000 -> 5,055-5,056 blocks/s, profiles/r4_ab_giant_batch.txt),
     // C2's sparse plans do not; bit-identical (tests/test_gpu_fused_giant.py)
     bool fused_giant_ = !(std::getenv("AESFHE_FUSED_GIANT") && std::atoi(std::getenv("AESFHE_FUSED_GIANT")) == 0);
+    int test_fail_giant_ = env_int("AESFHE_TEST_FAIL_GIANT", 0);
     // ys (out): set by the fused form to the P rows after the INTT row pass, for the caller's ModDown
     void giant_accumulate_many(const Ct& rs, const std::vector<u64>& gals, int nb, u32*& acc, u32*& c0sum, int& count, u32*& ys,
                                bool sole = false) {
         const int K = (int)gals.size(), lv = rs.level, r = hp_.nl(lv), ne2 = r + hp_.n_p, n = hp_.n;
         const size_t ms = (size_t)2 * r * n;
         if (rs.nb != K * nb || K > kMaxMembers) throw std::runtime_error("giant_accumulate_many: batch shape");
+        // test hook (tests/test_gpu_flag_identity.py): the k-th call of the process fails, after
+        // its group allocated its accumulators -- the next bootstrap must not see any of that group's state
+        if (test_fail_giant_ > 0 && --test_fail_giant_ == 0) throw std::runtime_error("giant_accumulate_many: test failure (AESFHE_TEST_FAIL_GIANT)");
         u32* perm = tmp(2 * (size_t)r * nb * K);
         for (int j = 0; j < K; ++j) launch_automorph(S(), T_, perm + (size_t)j * nb * ms, rs.data + (size_t)j * nb * ms, gals[j], 2 * r * nb);
         if (!acc) acc = tmp(2 * (size_t)ne2 * nb);

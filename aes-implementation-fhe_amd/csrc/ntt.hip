@@ -1487,6 +1487,8 @@ void ki_launch(hipStream_t st, const DevTables& Tb, const KiArgs& a, LimbMap map
     const double bytes = row * (a.nb * per_m + a.nsrc * 2.0 * a.nd * a.ne);
     const double bfly = 128.0 * (1 << LOGR1) * 8.0 * (a.nb * (a.nsrc * (double)ext_rows + 2.0 * (a.ne - a.kept)));
     if (ki8_on()) {
+        // (capped at 128 VGPRs -- 4 waves per SIMD, 36 VGPRs spilled -- it ran slower: C2 80.7 -> 72.8
+        // rounds/s, a 64-pair stack 96.2 -> 106.0 ms per pair, profiles/r6_ki8_occ_ab.txt)
         prof_launch_tsw(KID_KEY_INNER, bytes, bfly, k_ntt2_ki8<LOGR1>, dim3(2 * CH * a.ne * a.nb), dim3(256), 0, st, a, map, Tb.pc, Tb.tw,
                         Tb.itw, Tb.irow, Tb.igam);
         return;

@@ -52,8 +52,13 @@ class Deferred(Ciphertext):
     @property
     def handle(self):
         if self._res is None:
-            self._res = self._resolve()
-            self._release_operands()
+            # one resolution per object even when two branch threads need it at once:
+            # the engine's re-entrant lock (a resolution may resolve the deferred operands it reads)
+            with self._eng._defer_lock:
+                if self._res is None:
+                    res = self._resolve()
+                    self._res = res
+                    self._release_operands()
         return self._res.handle
 
     def resolved(self) -> Ciphertext:

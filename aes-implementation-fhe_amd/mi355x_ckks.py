@@ -360,6 +360,7 @@ class Engine:
         self.concurrent = (bool(concurrent) or env.get("AESFHE_CONCURRENT") == "1") and not self._serial
         self._pool = None
         self._tls = threading.local()
+        self._defer_lock = threading.RLock()  # deferred_calls.Deferred.handle: one resolution per object
         # deferred call sequences (deferred_calls.py): products / constant products /
         # sums fused into LUT kernels, rotations and conjugations batched; AESFHE_DEFER_CALLS=0 = off
         if defer_calls is None:

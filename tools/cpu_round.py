@@ -132,7 +132,8 @@ def boot_replay(tallies: dict, level_limbs, dnum: int, log_n: int = 16) -> dict:
         return time.perf_counter() - t
 
     def t_pt(l):
-        nl = O.nl(l)
+        # k_lin_mac forms the diagonal products in Q.P (the special primes too)
+        nl = O.nl(l) + O.n_p
         pt, x = rand(nl, n), rand(2, nl, n)
         t = time.perf_counter()
         O.mul_poly(pt, x)
