@@ -1253,6 +1253,48 @@ public:
         return o;
     }
 
+    // sum_i c_i (.) p_i over n <= kMaxMembers (ciphertext, plaintext) pairs (aesfhe_mul_pt_sum): the
+    // operands at their common logical level (exact drops), ONE k_mul_poly_sum launch, the rescale owed
+    // as mul_pt's lazy form -- the same value as the n lazy products summed (MixColFinal.sr_entry)
+    Ct mul_pt_sum(const std::vector<const Ct*>& C, const std::vector<aesfhe_handle>& P) {
+        const int n = (int)C.size();
+        if (n < 1 || n > kMaxMembers || (int)P.size() != n) throw std::runtime_error("mul_pt_sum: 1..8 (ciphertext, plaintext) pairs");
+        int l = 1 << 30;
+        for (const Ct* c : C) {
+            if (c->nb != 1 || vis_npoly(*c) != 2 || c->zero) throw std::runtime_error("mul_pt_sum: single, nonzero 2-polynomial ciphertexts");
+            l = std::min(l, c->level - c->pend);
+        }
+        if (l < 1) throw std::runtime_error("not enough level to multiply by a plaintext (level 0)");
+        for (aesfhe_handle h : P)
+            if (pt(h).constant) throw std::runtime_error("mul_pt_sum: constant plaintexts take mul_scalar");
+        std::vector<Ct> own;
+        PtSumArgs a;
+        for (int i = 0; i < n; ++i) {
+            // canonical (NTT, two polynomials, nothing owed), then the exact drop to l
+            Ct x = (pm(*C[i]) != 2 || C[i]->pend || !C[i]->ntt) ? normalize(*C[i], true) : *C[i];
+            if (x.level != l) {
+                Ct t = level_down(x, l);
+                if (x.data != C[i]->data) release(x);
+                x = t;
+            }
+            if (x.data != C[i]->data) own.push_back(x);
+            a.in[i] = x.data;
+            a.pt[i] = pt_at(pt(P[i]), l, 1);
+            cnt_[C_PTMUL]++;
+        }
+        Ct o = alloc_ct(l, 2);
+        launch_mul_poly_sum(S(), T_, o.data, a, n, 2, hp_.nl(l), qmap());
+        for (const Ct& x : own) release(x);
+        o.pend = 1;
+        o.lazy = true;
+        if (!headroom(l, 1, 1.0)) {
+            Ct r = rescale(o);
+            release(o);
+            return r;
+        }
+        return o;
+    }
+
     Ct add_pt(const Ct& c_in, aesfhe_handle hp) {
         Pt& p = pt(hp);
         if (p.constant) return add_scalar(c_in, p.re[0], p.im[0]);
@@ -5033,6 +5075,15 @@ int aesfhe_mul_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* a, const aesfhe
     for (int i = 0; i < n; ++i) A[i] = &e.canon(a[i]), B[i] = &e.canon(b[i]);
     std::vector<Ct> r = e.mul_many(A, B);
     for (int i = 0; i < n; ++i) out[i] = e.put_ct(r[i]);
+    API_END
+}
+int aesfhe_mul_pt_sum(aesfhe_ctx* ctx, int n, const aesfhe_handle* cts, const aesfhe_handle* pts, aesfhe_handle* out) {
+    API_BEGIN Engine& e = *ctx->eng;
+    if (n < 1 || !cts || !pts || !out) throw std::runtime_error("mul_pt_sum: bad arguments");
+    std::vector<const Ct*> C(n);
+    const std::vector<aesfhe_handle> P(pts, pts + n);
+    for (int i = 0; i < n; ++i) C[i] = &e.ct(cts[i]);
+    *out = e.put_ct(e.mul_pt_sum(C, P));
     API_END
 }
 int aesfhe_stack(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, aesfhe_handle* out) {

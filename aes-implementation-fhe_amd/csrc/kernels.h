@@ -180,6 +180,12 @@ void launch_ntt_inv_prod(hipStream_t st, const DevTables& T, u32* dst, const Ten
 void launch_tensor(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, int nl, LimbMap map, int nb = 1);
 // out = in * pt (pt: nl rows), npoly polys
 void launch_mul_poly(hipStream_t st, const DevTables& T, u32* out, const u32* in, const u32* pt, int npoly, int nl, LimbMap map);
+// out = sum_{i < n} in[i] (.) pt[i] (npoly polys of nl limbs each; pt[i]: nl limbs), n <= kMaxMembers
+struct PtSumArgs {
+    const u32* in[kMaxMembers] = {};
+    const u32* pt[kMaxMembers] = {};
+};
+void launch_mul_poly_sum(hipStream_t st, const DevTables& T, u32* out, const PtSumArgs& a, int n, int npoly, int nl, LimbMap map);
 // out = a + b*c  (b, c: rows; used for decryption and encryption)
 void launch_fma_poly(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, const u32* c, int rows, int nl, LimbMap map);
 // per-limb constants passed BY VALUE as a kernel argument (1 KiB kernarg, read with scalar

@@ -109,6 +109,16 @@ __global__ void k_mul_poly(u32* out, const u32* in, const u32* pt, int nl, LimbM
     const size_t pidx = ((size_t)limb << logn) + k;
     out[idx] = barrett_mul(in[idx], pt[pidx], P.q, P.mu);
 }
+// out row (poly, limb) = sum_{i < n} in_i (.) pt_i over n <= kMaxMembers ciphertext x plaintext products
+// (the masked sums of MixColumns' entry, MixColFinal.sr_entry): 64-bit sums of the 60-bit products, one
+// reduction -- one launch for what n lazy plaintext products and n - 1 additions did
+__global__ void k_mul_poly_sum(u32* out, PtSumArgs a, int n, int nl, LimbMap map, const PrimeConst* pc, int logn) {
+    EW_PROLOGUE
+    const size_t pidx = ((size_t)limb << logn) + k;
+    u64 acc = 0;
+    for (int i = 0; i < n; ++i) acc += (u64)a.in[i][idx] * a.pt[i][pidx];
+    out[idx] = reduce64(acc, P.q, P.mu, P.r32);
+}
 __global__ void k_tensor(u32* out, const u32* a, const u32* b, int nl, LimbMap map, const PrimeConst* pc, int logn) {
     // row = m * nl + limb: ciphertext m of a stacked batch ([m][2][nl] in, [m][3][nl] out)
     const int row = blockIdx.y;
@@ -1244,6 +1254,11 @@ void launch_tensor(hipStream_t st, const DevTables& T, u32* out, const u32* a, c
 }
 void launch_mul_poly(hipStream_t st, const DevTables& T, u32* out, const u32* in, const u32* pt, int npoly, int nl, LimbMap map) {
     prof_launch(KID_ELEMENTWISE, EW_BYTES((2.0 * npoly + 1.0) * nl), k_mul_poly, ew_grid(T.logn, npoly * nl), dim3(kBlock), 0, st, out, in, pt, nl, map, T.pc, T.logn);
+}
+void launch_mul_poly_sum(hipStream_t st, const DevTables& T, u32* out, const PtSumArgs& a, int n, int npoly, int nl, LimbMap map) {
+    if (n < 1 || n > kMaxMembers) throw std::runtime_error("launch_mul_poly_sum: 1..8 products");
+    prof_launch(KID_ELEMENTWISE, EW_BYTES((double)npoly * nl * (n + 1) + (double)n * nl), k_mul_poly_sum, ew_grid(T.logn, npoly * nl), dim3(kBlock), 0,
+                st, out, a, n, nl, map, T.pc, T.logn);
 }
 void launch_fma_poly(hipStream_t st, const DevTables& T, u32* out, const u32* a, const u32* b, const u32* c, int rows, int nl,
                      LimbMap map) {

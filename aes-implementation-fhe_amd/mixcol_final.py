@@ -17,7 +17,7 @@ import numpy as np
 from lut import COEFF_DIR, ensure_coeffs
 from state_encoder import StateEncoder
 from xor4_lut import XOR4LUT, SplitLUT2, batched, eval_two, joint_bases, powers, std_basis
-from utils import FOLDS, LUT2_DEPTH, takes_kw, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, can_fork, drop_to, fused_lut, pair, rot_many, rot_pair
+from utils import FOLDS, LUT2_DEPTH, takes_kw, NEED_BOOTSTRAP, NEED_XOR, RENORM_FLOOR, bootstrap1, bootstrap2, can_fork, drop_to, fused_lut, pair, rot_many, rot_pair, rotate_multi
 
 # AESFHE_SHARE_R1=0: MixColumns' r1 basis rebuilt in its second XOR4 (A/B runs)
 _SHARE_R1 = os.environ.get("AESFHE_SHARE_R1", "1") != "0"
@@ -133,6 +133,12 @@ def gf_mult_pair(ctx, cache: _CoeffCache, mult: int, ct_hi, ct_lo, out_level=Non
 # AESFHE_MC_GF_LOW: the rot form's GF multiplier pair at the XOR4 level with an extra renorm of its
 # packed output (1), or at its own depth above the last XOR4 with no renorm (0)
 _MC_GF_LOW = os.environ.get("AESFHE_MC_GF_LOW", "1") != "0"
+# AESFHE_MC_HOIST=0: with the strict renorm, the unpack's rotation and R^2 u as separate key switches (A/B)
+_MC_HOIST = os.environ.get("AESFHE_MC_HOIST", "1") != "0"
+# AESFHE_SR_MC_ENTRY=0: ShiftRows as its own step before MixColumns' first column shift and packs (A/B)
+SR_MC_ENTRY = os.environ.get("AESFHE_SR_MC_ENTRY", "1") != "0"
+# AESFHE_PT_SUM=0: sr_entry's masked sums as separate plaintext products and additions (A/B)
+_PT_SUM = os.environ.get("AESFHE_PT_SUM", "1") != "0"
 
 
 class MixColFinal:
@@ -217,7 +223,51 @@ class MixColFinal:
             return NEED_XOR + self.enc.PACK_DEPTH
         return NEED_XOR + LUT2_DEPTH + self.enc.PACK_DEPTH
 
-    def mix_packed(self, ct_hi, ct_lo, do_final_bootstrap: bool = True):
+    def _plain(self, key, make):
+        """a slot-vector plaintext encoded once per module (make() -> the vector)"""
+        cache = self.__dict__.setdefault("_pt_cache", {})
+        if key not in cache:
+            cache[key] = self.ctx.encode(make())
+        return cache[key]
+
+    def sr_entry(self, x_hi, x_lo, shift):
+        """(p0, p1) = (pack(SR(x)), pack(rot(SR(x), s1))) from the pair x BEFORE ShiftRows, ShiftRows
+        homomorphic and fused with MixColumns' first column shift and the two packs (the GHS12 form of
+        REF/temp/shiftrows_mixcolumns_fused.py:44-258, shiftrows_mixcolumns.py): with R^k x = rot(x, k s1)
+        (s1 = -4 unit; R^4 x = x, x being 16-unit-periodic), SR(x) = sum_k rot(m_k, k s1) R^k x over the
+        row masks m_k (REF/shift_rows.py:20-56) and rot(SR(x), s1) = sum_k rot(m_k, (k+1) s1) R^(k+1) x.
+        The three rotations of each half come from one hoisted key switch (rot_pair: one ModUp per half),
+        the packing masks ride in the row masks, so both packed outputs are ONE level of mask products
+        below x -- against ShiftRows (6 masked rotations, one level), r1 (2 rotations) and the packs (one
+        more level).  Same bytes; the renorm before hands x out one level lower (packed_input_need)."""
+        ctx, lay = self.ctx, self.layout
+        s1 = -4 * self.stride
+        if getattr(shift, "direction", None) != -1 or not lay.same(getattr(shift, "layout", None)) or not lay.packable:
+            raise ValueError("sr_entry: ShiftRows of this module's packed periodic layout")
+        rh, rl = rot_pair(ctx, x_hi, x_lo, [s1, 2 * s1, 3 * s1])
+        R = ((x_hi, *rh), (x_lo, *rl))
+        rows = [lay.row_mask(r).real for r in range(4)]
+        halves = [lay.half_mask(h).real for h in (0, 1)]
+
+        fused = getattr(getattr(ctx, "engine", None), "mul_pt_sum", None) if _PT_SUM else None
+
+        def masked_sum(tag, shift_k):
+            pairs = []
+            for h in (0, 1):
+                for k in range(4):
+                    j = (k + shift_k) % 4
+                    pt = self._plain((tag, h, k), lambda: np.roll(rows[k], (k + shift_k) * s1) * halves[h])
+                    pairs.append((R[h][j], pt))
+            if fused is not None:  # the eight products summed in ONE kernel (aesfhe_mul_pt_sum)
+                return fused(pairs)
+            terms = [ctx.multiply(c, p) for c, p in pairs]
+            while len(terms) > 1:  # a tree of adds (the lazy products combine without rescales)
+                terms = [ctx.add(terms[i], terms[i + 1]) if i + 1 < len(terms) else terms[i] for i in range(0, len(terms), 2)]
+            return terms[0]
+
+        return masked_sum("sr_p0", 0), masked_sum("sr_p1", 1)
+
+    def mix_packed(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, sr=None, on_sr=None):
         """MixColumns with its XOR stage on packed states (StateEncoder.pack: hi and lo side by side
         in one ciphertext, the XOR4 LUT being the same for both halves): the three XOR pairs of
         mix_rotated become three single XOR4s, their renorms single-ciphertext renorms, and the
@@ -231,26 +281,51 @@ class MixColFinal:
         only r1 shifted from the input.  AESFHE_MC_FORM=xtime computes r2 ^ r3 from shifted
         inputs (2 (x ^ r1) ^ (r1 ^ r2 ^ r3), four XOR4s, xtime being GF(2)-linear);
         AESFHE_MC_FORM=2gf keeps the reference's two multiplier pairs (GF2(x), GF3(r1)).  The
-        bytes are the same in every form."""
+        bytes are the same in every form.  sr (rot form): a ShiftRows module -- (ct_hi, ct_lo) is the
+        pair BEFORE ShiftRows, which sr_entry fuses with the first column shift and the packs
+        (AESFHE_SR_MC_ENTRY=0: the caller runs ShiftRows first); on_sr(p0): a debug hook for pack(SR(x))."""
         ctx, enc = self.ctx, self.enc
         fl = RENORM_FLOOR
         gl = fl + LUT2_DEPTH + enc.PACK_DEPTH
         form = os.environ.get("AESFHE_MC_FORM", "rot")
         if form == "rot":
             s1 = -4 * self.stride
-            (rh1,), (rl1,) = rot_pair(ctx, ct_hi, ct_lo, [s1])
-            p1, p0 = pair(ctx, lambda: enc.pack(rh1, rl1), lambda: enc.pack(ct_hi, ct_lo), shared=(ct_hi, ct_lo, rh1, rl1))
+            if sr is not None:
+                p0, p1 = self.sr_entry(ct_hi, ct_lo, sr)
+            else:
+                (rh1,), (rl1,) = rot_pair(ctx, ct_hi, ct_lo, [s1])
+                p1, p0 = pair(ctx, lambda: enc.pack(rh1, rl1), lambda: enc.pack(ct_hi, ct_lo), shared=(ct_hi, ct_lo, rh1, rl1))
+            if on_sr is not None:
+                on_sr(p0)
             if _MC_GF_LOW:
                 # the GF multiplier pair five levels lower (inputs at gl instead of gl + LUT2_DEPTH) and its
                 # packed output renormalised before the last XOR4: a renorm costs less than the pair's
                 # key switches and LUT sums at five more limbs; u at gl serves both branches (round 5).
                 # r1 is the second operand of both XOR4s at one level: its drop and std basis built once
                 kb = {} if _SHARE_R1 else None
-                u = enc.renorm_unpack(self._xor_ct(p0, p1, fl, kb, defer_conj=True), level=gl)
+                x = self._xor_ct(p0, p1, fl, kb, defer_conj=True)
+                if not FOLDS.unpack and _MC_HOIST and self.enc.layout.packable:
+                    # strict renorm: y = renorm(x) packed, then ONE batched key switch of y (aesfhe_galois_multi:
+                    # one ModUp of its one source) for the unpack's half swap rot(y, P) and for R^2 u packed,
+                    # which within each P-slot half is rot(y, 2 s1) on the first 8 unit slots and
+                    # rot(y, 2 s1 + P) on the others -- no rotation waits for the unpack
+                    P = self.layout.period
+                    y = enc.renorm_packed(x, level=gl + enc.UNPACK_DEPTH)
+                    z, ym, yp = rotate_multi(ctx, [(y, P), (y, 2 * s1), (y, 2 * s1 + P)])  # one source: one ModUp
+                    u = enc.unpack(y, z)
+                    lowm = lambda: np.tile((np.arange(P) < -2 * s1).astype(np.float64), self.sc // P)  # noqa: E731
 
-                def r1_r2r3_low():
-                    (vh,), (vl,) = rot_pair(ctx, u[0], u[1], [2 * s1])
-                    return enc.renorm_packed(self._xor_ct(enc.pack(vh, vl), p1, fl, kb, defer_conj=True), level=NEED_XOR)
+                    def r1_r2r3_low():
+                        a = self._plain(("r2u", 0), lowm)
+                        b = self._plain(("r2u", 1), lambda: 1.0 - lowm())
+                        w_pre = ctx.add(ctx.multiply(ym, a), ctx.multiply(yp, b))
+                        return enc.renorm_packed(self._xor_ct(w_pre, p1, fl, kb, defer_conj=True), level=NEED_XOR)
+                else:
+                    u = enc.renorm_unpack(x, level=gl)
+
+                    def r1_r2r3_low():
+                        (vh,), (vl,) = rot_pair(ctx, u[0], u[1], [2 * s1])
+                        return enc.renorm_packed(self._xor_ct(enc.pack(vh, vl), p1, fl, kb, defer_conj=True), level=NEED_XOR)
                 two, w = pair(ctx, lambda: self._gf2_renorm_pack(u, fl),
                               r1_r2r3_low, shared=(*u, p1))
                 acc = enc.renorm_packed(self._xor_ct(two, w, fl, defer_conj=True), level=NEED_BOOTSTRAP if do_final_bootstrap else None)

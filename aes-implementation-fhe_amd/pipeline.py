@@ -242,6 +242,13 @@ class AESPipeline:
         c0 = ct[0].s1 if hasattr(ct[0], "s1") else ct[0]
         return self._sr_perm_v if ok is not None and ok(c0) else None
 
+    def _sr_entry_ok(self) -> bool:
+        """ShiftRows runs inside MixColumns' packed entry (MixColFinal.sr_entry): the rot form with its
+        GF pair low, this pipeline's own ShiftRows layout (AESFHE_SR_MC_ENTRY=0: a separate step)"""
+        from mixcol_final import SR_MC_ENTRY
+        return (SR_MC_ENTRY and hasattr(self.mix, "sr_entry") and os.environ.get("AESFHE_MC_FORM", "rot") == "rot"
+                and self.layout.packable and getattr(self.shift, "direction", None) == -1)
+
     def _sub_apply(self, ct, defer_conj: bool = False, lut=None):
         """(Inv)SubBytes (lut, default self.sub) on the pair down to the renorm floor; defer_conj (the
         output goes straight into _renorm_pair): the nibble form may hand over utils.ConjSum halves
@@ -365,6 +372,19 @@ class AESPipeline:
             perm = self._sr_perm(ct, debug)
             if perm is not None:  # ShiftRows folded into the renorm (a byte permutation of the snap)
                 ct = self.encoder.renorm_perm(*ct, perm, level=lv)
+            elif self._sr_entry_ok():
+                # ShiftRows homomorphic inside MixColumns' entry (MixColFinal.sr_entry: masked rotations
+                # fused with the first column shift and the packs, one level): the renorm hands out lv
+                ct = self._renorm_pair(*ct, level=lv)
+                self._log_pair(debug, f"enc.r{r}.sub.renorm", *ct)
+                log_sr = (lambda p0: self._log_packed(debug, f"enc.r{r}.sr", p0)) if debug is not None else None
+                acc = self.mix.mix_packed(*ct, sr=self.shift, on_sr=log_sr)
+                self._log_packed(debug, f"enc.r{r}.mc", acc)
+                x = self._ark_packed(acc, r, defer_conj=True)
+                self._log_packed(debug, f"enc.r{r}.ark", x)
+                ct = self.encoder.renorm_unpack(x, level=next_level)
+                self._log_pair(debug, f"enc.r{r}.ark.renorm", *ct)
+                return ct
             else:
                 ct = self._renorm_pair(*ct, level=lv + SHIFTROWS_DEPTH)
                 self._log_pair(debug, f"enc.r{r}.sub.renorm", *ct)

@@ -229,15 +229,17 @@ class StateEncoder:
         fold is on (FOLDS.conj; strict renorms are the identity on the message)"""
         return tuple(c if FOLDS.conj else conj_sum(self.ctx, c) for c in cts)
 
-    def unpack(self, ct):
+    def unpack(self, ct, z=None):
         """the packed state -> its (hi, lo) pair, homomorphically (the inverse of pack): both halves
         are P-periodic inside the 2P-periodic message, so z = rot_P(ct) holds lo where ct holds hi
         and vice versa, and hi = z + m0 (ct - z), lo = ct - m0 (ct - z) -- one rotation and one
-        mask product (UNPACK_DEPTH levels), every slot of both outputs as the packed input's"""
+        mask product (UNPACK_DEPTH levels), every slot of both outputs as the packed input's.
+        z: rot_P(ct) when the caller has it (from a hoisted key switch)"""
         ctx = self.ctx
         if getattr(self, "_half_pts", None) is None:
             self._half_pts = [ctx.encode(self.layout.half_mask(w)) for w in (0, 1)]
-        z = ctx.rotate(ct, self.layout.period)
+        if z is None:
+            z = ctx.rotate(ct, self.layout.period)
         t = ctx.multiply(ctx.sub(ct, z), self._half_pts[0])
         return tag_layout(self.layout, ctx.add(z, t), ctx.sub(ct, t))
 

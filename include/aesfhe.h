@@ -151,6 +151,11 @@ int aesfhe_conjugate(aesfhe_ctx* ctx, aesfhe_handle ct, aesfhe_handle* out);
  * at one level are stacked and share one tensor launch and one key switch per chunk of four;
  * the results equal the separate calls bit for bit.  out[i] receives a new handle. */
 int aesfhe_mul_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* a, const aesfhe_handle* b, aesfhe_handle* out);
+/* sum_{i<n} cts[i] * pts[i] (1 <= n <= 8 single ciphertexts times non-constant plaintexts), at the
+ * operands' common lowest level, as ONE kernel; the same value as n engine.multiply(ct, pt) calls summed
+ * with engine.add (REF/engine_context.py:65-68, :77-80) -- the masked rotations of REF/shift_rows.py:39-56
+ * feeding MixColumns (REF/mixcol_final.py:124-154) summed in one launch (MixColFinal.sr_entry). */
+int aesfhe_mul_pt_sum(aesfhe_ctx* ctx, int n, const aesfhe_handle* cts, const aesfhe_handle* pts, aesfhe_handle* out);
 int aesfhe_conjugate_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, aesfhe_handle* out);
 /* n automorphisms of possibly DIFFERENT ciphertexts, each with its own Galois element galois[i]
  * (odd, < 2N): engine.rotate(ct, rotation_key, steps) (REF/engine_context.py:127-132; Galois

@@ -1,11 +1,7 @@
 set -e -o pipefail
 export TMPDIR=/tmp
-TESTS="tests/test_gpu_flag_identity.py" bash tools/gpu_task.sh r6e tests
-PASSES=2 bash tools/env_ab.sh r6e "-" "AESFHE_KI8_OCC=4" "AESFHE_RENORM_FOLDS=1"
-AB_TIMEOUT=200 PASSES=1 AB_ARGS="--no-cpu-baseline --batch-states 0 --folded-steps 0 --true-fhe-steps 0 --pair-states 64 --pair-stack 64 --packed-pairs 0 --eager-steps 0 --deferred-steps 0 --steps 2 --warmup 1" bash tools/env_ab.sh r6e_stack "-" "AESFHE_KI8_OCC=4"
-bash tools/gpu_task.sh r6e pmcbench
-O=gpurun_out/r6e
-C2="--no-cpu-baseline --batch-states 0 --folded-steps 0 --true-fhe-steps 0 --pair-states 0 --packed-pairs 0 --eager-steps 0 --deferred-steps 0"
-timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/ctl_fetch -o run -- python3 bench.py --steps 1 --warmup 1 $C2 --detail-json "" --whole-stats $O/ws_ctl.json > $O/ctl_fetch.out 2> $O/ctl_fetch.err || echo "control rc=$?" > $O/ctl_rc.txt
-rm -rf $O/ctl_fetch
+TESTS="tests/test_gpu_packed_xor.py tests/test_gpu_reference_paths.py tests/test_gpu_packed.py tests/test_gpu_aes.py tests/test_gpu_true_fhe.py" bash tools/gpu_task.sh r6h tests
+PASSES=2 bash tools/env_ab.sh r6h "-" "AESFHE_PT_SUM=0" "AESFHE_MC_HOIST=0"
+O=gpurun_out/r6h
+timeout -s KILL 60 rocprofv3 --pmc TCC_EA0_WRREQ_sum --output-format csv -d $O/wr_tiny -o run -- python3 -c "import torch; x=torch.ones(1<<20, device='cuda'); y=x*2; torch.cuda.synchronize(); print(float(y.sum()))" > $O/wr_tiny.out 2> $O/wr_tiny.err || echo "tiny rc=$?" > $O/wr_tiny_rc.txt
 echo done
