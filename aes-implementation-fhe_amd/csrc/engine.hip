@@ -2966,14 +2966,25 @@ public:
             if (down[w]) release(dc[w]);
         const int f = level < 0 ? hp_.fresh : level, nq = hp_.nl(f) + 1;
         const double enc_scale = hp_.delta[f] * (double)hp_.mod[hp_.nl(f)];
-        u32* m = tmp(2 * (size_t)nq);
         const bool direct32 = direct32_ && ((unpack == 16) || (single && packed_period == 32));
+        // the re-encryption from this stream's pool of zero encryptions (zero_enc) where the snapped
+        // message is sparse: the direct period-32 / period-16 codecs (pooled_ok)
+        const bool pooled = pool_k_ > 0 && hp_.nl(f) <= kRenormMaxLimbs && (direct32 || (states == 1 && (pack_out || per16)));
+        u32* m = pooled ? nullptr : tmp(2 * (size_t)nq);
+        u32* W = pooled ? renorm_w() : nullptr;
+        int ld = 0;  // log2 D of the pooled message
         // the snap inside the encode (AESFHE_SNAP_ENCODE, default on): the two accumulators of this
         // stream alternate -- this renorm decodes into one, its encode snaps from it and zeroes the other
         double* acc = d_codec_[t_sidx] + (snap_encode_ ? 64 * codec_flip_[t_sidx] : 0);
         double* zacc = snap_encode_ ? d_codec_[t_sidx] + 64 * (1 - codec_flip_[t_sidx]) : nullptr;
         double* wv = snap_encode_ ? acc : d_codec_[t_sidx] + 64;
         if (slot_perm && unpack && !direct32) throw std::runtime_error("renorm: a slot permutation needs the direct period-32 codec");
+        // the message's NTT table instead of its coefficients (pooled): 32 slots of one channel (D = 64),
+        // or 16 periodic slots of each of two channels (D = 32)
+        auto wtab = [&](bool one32, const Slot16& s16) {
+            if (one32) launch_renorm_wtab32(S(), T_, W, wv, zacc, slots32_, hp_.delta[f], hp_.nl(f), gtab(64)), ld = 6;
+            else launch_renorm_wtab16(S(), T_, W, wv, zacc, s16, hp_.delta[f], hp_.nl(f), gtab(32)), ld = 5;
+        };
         if (direct32) {
             // the 32 slots of the packed period-32 state: one direct decode, the snap as 2 x 16, and
             // either the two 16-periodic halves (unpack) or the 32-periodic whole (single); a slot
@@ -2983,7 +2994,8 @@ public:
                 for (int j = 0; j < 32; ++j) sp32.e[j] = slots32_.e[16 * (j / 16) + slot_perm[j % 16]];
             launch_decode32(S(), T_, x, kd[0], cc[0], sp32, isc[0], acc);
             if (!snap_encode_) launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
-            if (unpack) launch_encode16(S(), T_, m, wv, slots_p_, enc_scale, nq, true, zacc);
+            if (pooled) wtab(!unpack, slots_p_);
+            else if (unpack) launch_encode16(S(), T_, m, wv, slots_p_, enc_scale, nq, true, zacc);
             else launch_encode32(S(), T_, m, wv, slots32_, enc_scale, nq, zacc);
             if (snap_encode_) codec_flip_[t_sidx] ^= 1;
         } else if (states == 1) {
@@ -2993,7 +3005,8 @@ public:
                 for (int i = 0; i < 16; ++i) sp.e[i] = sl.e[slot_perm[i]];
             launch_decode16(S(), T_, x, kd, cc, sp, isc, acc);
             if (!snap_encode_) launch_snap16(S(), acc, wv, d_nib_[t_sidx]);
-            if (pack_out) launch_encode32(S(), T_, m, wv, slots32_, enc_scale, nq, zacc);  // acc[c][i] = packed slot 16 c + i
+            if (pooled) wtab(pack_out, sl);
+            else if (pack_out) launch_encode32(S(), T_, m, wv, slots32_, enc_scale, nq, zacc);  // acc[c][i] = packed slot 16 c + i
             else launch_encode16(S(), T_, m, wv, sl, enc_scale, nq, per16, zacc);
             if (snap_encode_) codec_flip_[t_sidx] ^= 1;
         } else {
@@ -3007,6 +3020,23 @@ public:
             launch_snap_slots(S(), T_, z, w, d_slot_pos_, states, unpack, n_out);
             launch_fft2(S(), T_, w, -1, n_out);
             launch_encode_untwist(S(), T_, m, w, enc_scale, nq, n_out);
+        }
+        if (pooled) {
+            // out_c = a pooled encryption of zero at level f + the message's NTT (one launch for both)
+            RenormOut ro;
+            Ct outs[2];
+            for (int c = 0; c < n_out; ++c) {
+                outs[c] = alloc_ct(f, 2);
+                ro.pool[c] = zero_enc(f);
+                ro.out[c] = outs[c].data;
+            }
+            launch_renorm_combine(S(), T_, ro, n_out, W, hp_.nl(f), ld);
+            retire_pools();
+            cnt_[C_ENC] += n_out;
+            *oh = put_ct(outs[0]);
+            if (n_out == 2) *ol = put_ct(outs[1]);
+            untmp(x, 8);
+            return;
         }
         // both re-encryptions in one set of launches, the coefficient-form message added to e0
         Ct enc = encrypt_many(m, n_out, (size_t)nq * n, f, true);
@@ -3023,6 +3053,71 @@ public:
         }
         untmp(m, 2 * (size_t)nq);
         untmp(x, 8);
+    }
+
+    // ---- pooled zero encryptions for the renorm (AESFHE_RENORM_POOL = K per refill, default 16; 0: every
+    // renorm encrypts its own message, the round-5 path).  A refill is ONE encrypt_many of K zero
+    // messages at level f (the same sampling, NTT, combine and rescale launches as one renorm's
+    // encryption, K members wide); each member is handed out once (its own PRNG counter: fresh v, e0, e1),
+    // and the renorm adds its message's NTT (k_renorm_combine).  Pools are per stream (the refill, the
+    // consumers and the slab's release stay stream-ordered) and per level; aesfhe_renorm_pool resets them
+    // (bench.py empties them before its timed region: every encryption used there is made there).
+    int pool_k_ = env_int("AESFHE_RENORM_POOL", 16);
+    struct ZPool {
+        Ct slab;
+        int next = 0;
+    };
+    std::map<int, ZPool> zpool_[kStreams];
+    std::vector<Ct> zretired_[kStreams];
+    std::map<int, u32*> gtab_;
+    u32* renorm_w_[kStreams] = {};
+    u32* renorm_w() {
+        u32*& w = renorm_w_[t_sidx];
+        if (!w) w = dev_alloc((size_t)2 * kRenormMaxLimbs * 64);
+        return w;
+    }
+    // [t][e] = g_t^e, g_t = psi_t^(N / D) (a primitive 2D-th root mod q_t), e < 2D, every Q prime
+    const u32* gtab(int D) {
+        auto it = gtab_.find(D);
+        if (it != gtab_.end()) return it->second;
+        const int nq = hp_.n_q;
+        std::vector<u32> h((size_t)nq * 2 * D);
+        for (int t = 0; t < nq; ++t) {
+            const u64 q = hp_.mod[t];
+            u64 g = 1, b = hp_.psi[t];
+            for (u64 e = (u64)hp_.n / D; e; e >>= 1, b = b * b % q)
+                if (e & 1) g = g * b % q;
+            u64 v = 1;
+            for (int e = 0; e < 2 * D; ++e, v = v * g % q) h[(size_t)t * 2 * D + e] = (u32)v;
+        }
+        u32* d = dev_alloc(h.size());
+        HIP_OK(hipMemcpy(d, h.data(), sizeof(u32) * h.size(), hipMemcpyHostToDevice));
+        return gtab_[D] = d;
+    }
+    const u32* zero_enc(int f) {
+        ZPool& zp = zpool_[t_sidx][f];
+        if (!zp.slab.data || zp.next >= zp.slab.nb) {
+            if (zp.slab.data) zretired_[t_sidx].push_back(zp.slab);  // released after this renorm's launches
+            zp.slab = encrypt_many(nullptr, pool_k_, 0, f, true);
+            zp.next = 0;
+        }
+        return zp.slab.data + (size_t)(zp.next++) * 2 * hp_.nl(f) * hp_.n;
+    }
+    void retire_pools() {
+        for (const Ct& c : zretired_[t_sidx]) release(c);
+        zretired_[t_sidx].clear();
+    }
+    void renorm_pool(int k) {  // k < 0: keep the size, empty the pools
+        if (k > 4096) throw std::runtime_error("renorm_pool: size above 4096");
+        HIP_OK(hipDeviceSynchronize());
+        for (int s = 0; s < kStreams; ++s) {
+            for (auto& kv : zpool_[s])
+                if (kv.second.slab.data) pools_[s].put(kv.second.slab.data, kv.second.slab.words);
+            zpool_[s].clear();
+            for (const Ct& c : zretired_[s]) pools_[s].put(c.data, c.words);
+            zretired_[s].clear();
+        }
+        if (k >= 0) pool_k_ = k;
     }
 
     // NTT position of every slot (5^j mod 2N -> (e - 1) / 2), for the FFT codec
@@ -5075,6 +5170,10 @@ int aesfhe_mul_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* a, const aesfhe
     for (int i = 0; i < n; ++i) A[i] = &e.canon(a[i]), B[i] = &e.canon(b[i]);
     std::vector<Ct> r = e.mul_many(A, B);
     for (int i = 0; i < n; ++i) out[i] = e.put_ct(r[i]);
+    API_END
+}
+int aesfhe_renorm_pool(aesfhe_ctx* ctx, int size) {
+    API_BEGIN ctx->eng->renorm_pool(size);
     API_END
 }
 int aesfhe_mul_pt_sum(aesfhe_ctx* ctx, int n, const aesfhe_handle* cts, const aesfhe_handle* pts, aesfhe_handle* out) {

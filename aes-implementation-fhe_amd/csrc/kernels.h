@@ -481,6 +481,24 @@ void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double*
 struct Slot32 {
     u32 e[32];
 };
+// the renorm's pooled re-encryption (k_renorm_wtab / k_renorm_combine, Engine::zero_enc)
+constexpr int kRenormMaxLimbs = 64;
+template <int NS>
+struct SlotTab {
+    u32 e[NS];
+};
+struct RenormOut {
+    const u32* pool[2] = {};
+    u32* out[2] = {};
+};
+// W[c][t][d] (nl limbs, D = 64 = 2 x 32 slots, one channel): the NTT of the snapped 32-periodic message
+void launch_renorm_wtab32(hipStream_t st, const DevTables& T, u32* W, const double* w, double* zacc, const Slot32& sl, double scale, int nl,
+                          const u32* gtab);
+// the same for two 16-periodic channels (D = 32 each)
+void launch_renorm_wtab16(hipStream_t st, const DevTables& T, u32* W, const double* w, double* zacc, const Slot16& sl, double scale, int nl,
+                          const u32* gtab);
+// out_c = pool_c + W_c on c0 (runs of N / 2^ld equal values), nch <= 2 channels of 2 x nl rows
+void launch_renorm_combine(hipStream_t st, const DevTables& T, const RenormOut& ro, int nch, const u32* W, int nl, int ld);
 // CONTRACT (as launch_decode16): acc zero on entry; the snap follows on the same stream, either inside the
 // snapping encode (the default, AESFHE_SNAP_ENCODE: it reads acc and zeroes the other buffer of its
 // double-buffered pair for the next decode) or as launch_snap16 on acc (AESFHE_SNAP_ENCODE=0)

@@ -978,6 +978,69 @@ __global__ void __launch_bounds__(kBlock) k_encode32(u32* out, const double* w, 
     }
 }
 
+// ---- the renorm's re-encryption from a pool of zero encryptions (Engine::zero_enc)
+// The snapped message of a channel of NS slots (period NS per channel: k_encode32 with NS = 32, the
+// periodic k_encode16 with NS = 16) has D = 2 NS nonzero coefficients, k = j N / D, formed here exactly
+// as those kernels form them: x_j = rint((fac sum_i Re(w_i zeta^(-e_i k)) + [k = 0]) scale).  Its
+// negacyclic NTT (Cooley-Tukey, bit-reversed out: value i at psi^(2 brv(i) + 1)) takes D distinct values:
+// NTT(m)[i] = W[i >> (logn - log2 D)], W[d] = sum_j x_j g^((2 brv_D(d) + 1) j), g = psi^(N / D) a
+// primitive 2D-th root (gtab[t][e] = g_t^e, e < 2D).  One block per channel: x into LDS, the residues,
+// the D x D sums (one reduced product per term).
+template <int NS, bool SNAP>
+__global__ void __launch_bounds__(256) k_renorm_wtab(u32* W, const double* w, double* zacc, SlotTab<NS> sl, double scale, int nl,
+                                                     const u32* gtab, const PrimeConst* pc, int logn) {
+    constexpr int D = 2 * NS, LD = (NS == 32) ? 6 : 5;
+    static_assert((1 << LD) == D, "D = 2 NS, a power of two");
+    __shared__ double sw[SNAP ? 64 : 1];
+    __shared__ double xs[D];
+    __shared__ u32 res[kRenormMaxLimbs * D];
+    if (SNAP) w = snap_block(w, zacc, sw);
+    const int c = blockIdx.x, n = 1 << logn;
+    const u32 mask = 2u * n - 1;
+    const double inv_n = 1.0 / n;
+    if (threadIdx.x < D) {
+        const int j = threadIdx.x;
+        const u32 k = (u32)j * (u32)(n / D);
+        double v = 0.0;
+        for (int i = 0; i < NS; ++i) {
+            double sn, cs;
+            sincospi((double)((sl.e[i] * k) & mask) * inv_n, &sn, &cs);
+            v += w[c * 2 * NS + 2 * i] * cs + w[c * 2 * NS + 2 * i + 1] * sn;
+        }
+        v = v / (double)NS + (j == 0 ? 1.0 : 0.0);
+        xs[j] = rint(v * scale);
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < nl * D; idx += blockDim.x) {
+        const int t = idx / D, j = idx - t * D;
+        const double q = (double)pc[t].q, x = xs[j];
+        double r = fma(-q, floor(x / q), x);
+        if (r < 0) r += q;
+        if (r >= q) r -= q;
+        res[idx] = (u32)r;
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < nl * D; idx += blockDim.x) {
+        const int t = idx / D, d = idx - t * D;
+        const u32 q = pc[t].q, mu = pc[t].mu;
+        const u32 rv = (u32)(__brev((unsigned)d) >> (32 - LD));
+        const u32 e1 = 2u * rv + 1u;
+        const u32* g = gtab + (size_t)t * 2 * D;
+        u32 acc = 0;
+        for (int j = 0; j < D; ++j) acc = add_mod(acc, barrett_mul(res[t * D + j], g[(e1 * (u32)j) & (2u * D - 1)], q, mu), q);
+        W[((size_t)c * nl + t) * D + d] = acc;
+    }
+}
+// out_c (2 polys x nl limbs) = the zero encryption pool_c + (W_c broadcast over runs of N / D on c0)
+__global__ void k_renorm_combine(RenormOut ro, const u32* W, int nl, int ld, const PrimeConst* pc, int logn) {
+    const int c = blockIdx.z, row = blockIdx.y, t = row % nl, p = row / nl;
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t idx = ((size_t)row << logn) + k;
+    u32 v = ro.pool[c][idx];
+    if (p == 0) v = add_mod(v, W[((size_t)c * nl + t) * (1u << ld) + (k >> (logn - ld))], pc[t].q);
+    ro.out[c][idx] = v;
+}
+
 // acc is zeroed behind its read: the next renorm's decode accumulates into a clean buffer
 // without a fill launch of its own (the buffer is zeroed once when allocated)
 __global__ void k_snap16(double* acc, double* w, int* nib) {
@@ -1744,6 +1807,32 @@ void launch_encode16(hipStream_t st, const DevTables& T, u32* out, const double*
     else
         prof_launch(KID_ELEMENTWISE, words(2.0 * nq * (1u << T.logn)), k_encode16<false>, dim3((1u << T.logn) / kBlock, 2), dim3(kBlock), 0, st,
                     out, w, zacc, sl, scale, nq, T.pc, T.logn, kmask, fac);
+}
+
+void launch_renorm_wtab32(hipStream_t st, const DevTables& T, u32* W, const double* w, double* zacc, const Slot32& sl, double scale, int nl,
+                          const u32* gtab) {
+    if (nl < 1 || nl > kRenormMaxLimbs) throw std::runtime_error("launch_renorm_wtab: limb count out of range");
+    SlotTab<32> tab;
+    for (int i = 0; i < 32; ++i) tab.e[i] = sl.e[i];
+    if (zacc)
+        prof_launch(KID_ELEMENTWISE, 4.0 * 64 * nl, k_renorm_wtab<32, true>, dim3(1), dim3(256), 0, st, W, w, zacc, tab, scale, nl, gtab, T.pc, T.logn);
+    else
+        prof_launch(KID_ELEMENTWISE, 4.0 * 64 * nl, k_renorm_wtab<32, false>, dim3(1), dim3(256), 0, st, W, w, zacc, tab, scale, nl, gtab, T.pc, T.logn);
+}
+void launch_renorm_wtab16(hipStream_t st, const DevTables& T, u32* W, const double* w, double* zacc, const Slot16& sl, double scale, int nl,
+                          const u32* gtab) {
+    if (nl < 1 || nl > kRenormMaxLimbs) throw std::runtime_error("launch_renorm_wtab: limb count out of range");
+    SlotTab<16> tab;
+    for (int i = 0; i < 16; ++i) tab.e[i] = sl.e[i];
+    if (zacc)
+        prof_launch(KID_ELEMENTWISE, 4.0 * 2 * 32 * nl, k_renorm_wtab<16, true>, dim3(2), dim3(256), 0, st, W, w, zacc, tab, scale, nl, gtab, T.pc, T.logn);
+    else
+        prof_launch(KID_ELEMENTWISE, 4.0 * 2 * 32 * nl, k_renorm_wtab<16, false>, dim3(2), dim3(256), 0, st, W, w, zacc, tab, scale, nl, gtab, T.pc, T.logn);
+}
+void launch_renorm_combine(hipStream_t st, const DevTables& T, const RenormOut& ro, int nch, const u32* W, int nl, int ld) {
+    if (nch < 1 || nch > 2) throw std::runtime_error("launch_renorm_combine: 1 or 2 channels");
+    prof_launch(KID_ELEMENTWISE, words(4.0 * nch * nl * (1u << T.logn)), k_renorm_combine, dim3((1u << T.logn) / kBlock, 2 * nl, nch), dim3(kBlock), 0,
+                st, ro, W, nl, ld, T.pc, T.logn);
 }
 
 void launch_decode_twist(hipStream_t st, const DevTables& T, const u32* x, const int kd[2], const CrtConsts cc[2],

@@ -248,6 +248,14 @@ class _NoFinalBootstrap:
         return self.mix(ct_hi, ct_lo, do_final_bootstrap=False)
 
 
+def empty_pools(E) -> None:
+    """empty the engine's pools of zero encryptions (aesfhe_renorm_pool) before a timed
+    region: every re-encryption a timed renorm uses is then made inside that region"""
+    f = getattr(E, "renorm_pool", None)
+    if f is not None:
+        f(-1)
+
+
 def _progress(ctx, every_s: float = 30.0):
     """stderr heartbeat with real progress (bootstraps done), for long profiled runs."""
     import threading
@@ -442,6 +450,7 @@ def run_pairs(ctx, coeffs, rks, args, rank, world, dist, pairs: int, states: int
     for c, b in warm.items():  # warmup: masks, LUT constants, codec buffers, stacked keys
         pipes[c].encrypt(b, rks)
     E.sync()
+    empty_pools(E)
     leg = Leg(E).start()
     barrier(dist)
     t0 = time.perf_counter()
@@ -484,6 +493,7 @@ def run_batch(ctx, coeffs, rks, args, rank, world, dist, tj: dict) -> dict:
     E = ctx.engine
     pipe.encrypt(batches[0], rks)  # warmup: masks, LUT constants, FFT buffers
     E.sync()
+    empty_pools(E)
     leg = Leg(E).start()
     barrier(dist)
     t0 = time.perf_counter()
@@ -564,6 +574,7 @@ def run_folded(ctx, coeffs, rks, args, rank, world, dist, mix_layout, strict_val
         pipe.encrypt(sts[0], rks)
         ctx.engine.sync()
         import mi355x_ckks
+        empty_pools(ctx.engine)
         l0 = mi355x_ckks.launch_count()
         r0 = dict(RENORM_TALLY)
         barrier(dist)
@@ -642,6 +653,7 @@ def run_ref_calls(coeffs, rks, args, rank, world, dist, local, seed, tj: dict, l
     pipe.encrypt(sts[0], rks)  # warmup: plaintext constants of the per-term loops
     E.sync()
     E.profile(PROF_KIDS, every=args.profile_every)
+    empty_pools(E)
     leg = Leg(E).start()
     E.reset_counters()
     barrier(dist)
@@ -956,6 +968,7 @@ def main():
 
     outs = []
     E.sync()
+    empty_pools(E)
     leg = Leg(E).start() if not whole else None
     barrier(dist)
     # AESFHE_MARK_TIMED=1: a 250 ms idle gap on each side of the timed region (outside the timing),

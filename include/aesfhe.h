@@ -156,6 +156,10 @@ int aesfhe_mul_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* a, const aesfhe
  * with engine.add (REF/engine_context.py:65-68, :77-80) -- the masked rotations of REF/shift_rows.py:39-56
  * feeding MixColumns (REF/mixcol_final.py:124-154) summed in one launch (MixColFinal.sr_entry). */
 int aesfhe_mul_pt_sum(aesfhe_ctx* ctx, int n, const aesfhe_handle* cts, const aesfhe_handle* pts, aesfhe_handle* out);
+/* the secret-key renorm's pool of zero encryptions: size = encryptions made per
+ * refill (0: every renorm encrypts its own message; < 0: keep the size), every pool emptied -- the
+ * re-encryption of REF/pipeline.py:65-69 (decrypt -> snap -> encrypt) drawn as Enc(0) + message */
+int aesfhe_renorm_pool(aesfhe_ctx* ctx, int size);
 int aesfhe_conjugate_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, aesfhe_handle* out);
 /* n automorphisms of possibly DIFFERENT ciphertexts, each with its own Galois element galois[i]
  * (odd, < 2N): engine.rotate(ct, rotation_key, steps) (REF/engine_context.py:127-132; Galois
