@@ -1260,8 +1260,9 @@ public:
         const int n = (int)C.size();
         if (n < 1 || n > kMaxMembers || (int)P.size() != n) throw std::runtime_error("mul_pt_sum: 1..8 (ciphertext, plaintext) pairs");
         int l = 1 << 30;
+        const int nb = C[0]->nb;  // stacks of one size: every member times the same plaintext
         for (const Ct* c : C) {
-            if (c->nb != 1 || vis_npoly(*c) != 2 || c->zero) throw std::runtime_error("mul_pt_sum: single, nonzero 2-polynomial ciphertexts");
+            if (c->nb != nb || vis_npoly(*c) != 2 || c->zero) throw std::runtime_error("mul_pt_sum: nonzero 2-polynomial ciphertexts of one stack size");
             l = std::min(l, c->level - c->pend);
         }
         if (l < 1) throw std::runtime_error("not enough level to multiply by a plaintext (level 0)");
@@ -1282,8 +1283,8 @@ public:
             a.pt[i] = pt_at(pt(P[i]), l, 1);
             cnt_[C_PTMUL]++;
         }
-        Ct o = alloc_ct(l, 2);
-        launch_mul_poly_sum(S(), T_, o.data, a, n, 2, hp_.nl(l), qmap());
+        Ct o = alloc_ct(l, 2 * nb, nb);
+        launch_mul_poly_sum(S(), T_, o.data, a, n, 2 * nb, hp_.nl(l), qmap());
         for (const Ct& x : own) release(x);
         o.pend = 1;
         o.lazy = true;
@@ -2917,6 +2918,39 @@ public:
             isc[w] = 1.0 / (c.level >= 0 ? raw_scale(c.level, c.pend) : 1.0);
             cnt_[C_DEC]++;
         }
+        // the sparse decryption (round 6, AESFHE_SPARSE_DEC, default on with the pool): the packed period-32
+        // renorm and the periodic pair renorm decode only the D subring coefficients the snapped message can
+        // have (launch_renorm_sparse: block sums of c0 + c1 s, a D-point inverse transform, the CRT, the
+        // slots, the snap and the message's NTT table in TWO launches), then the pooled re-encryption: three
+        // launches for the whole renorm instead of six (dec_raw, the INTT's two passes, decode, table, combine)
+        {
+            const int fs = level < 0 ? hp_.fresh : level;
+            const bool one = direct32_ && single && packed_period == 32 && n_in == 1 && n_out == 1;
+            const bool two = states == 1 && per16 && !pack_out && !unpack && !single && n_in == 2 && n_out == 2;
+            if (sparse_dec_ && pool_k_ > 0 && !hc && !slot_perm && hp_.nl(fs) <= kRenormMaxLimbs && (one || two)) {
+                SparseDec sd;
+                for (int w = 0; w < n_in; ++w) sd.kd[w] = kd[w], sd.cc[w] = cc[w];
+                u32* W = renorm_w();
+                launch_renorm_sparse(S(), T_, W, renorm_b(), dr, n_in, sd, slots32_, slots_p_, hp_.delta[fs], hp_.nl(fs), gtab(one ? 64 : 32), d_s_,
+                                     need_s2 ? s_sq4() : d_s_);
+                for (int w = 0; w < n_dec; ++w)
+                    if (down[w]) release(dc[w]);
+                RenormOut ro;
+                Ct outs[2];
+                for (int c = 0; c < n_out; ++c) {
+                    outs[c] = alloc_ct(fs, 2);
+                    ro.pool[c] = zero_enc(fs);
+                    ro.out[c] = outs[c].data;
+                }
+                launch_renorm_combine(S(), T_, ro, n_out, W, hp_.nl(fs), one ? 6 : 5);
+                retire_pools();
+                cnt_[C_ENC] += n_out;
+                *oh = put_ct(outs[0]);
+                if (n_out == 2) *ol = put_ct(outs[1]);
+                untmp(x, 8);
+                return;
+            }
+        }
         launch_dec_raw(S(), T_, x, dr, n_dec, d_s_, need_s2 ? s_sq4() : d_s_);
         if (hc && n_in == 1) {
             if (kd[1] != kd[0] || isc[1] != isc[0]) throw std::runtime_error("renorm: conjugate partner at another scale");
@@ -3071,6 +3105,13 @@ public:
     std::vector<Ct> zretired_[kStreams];
     std::map<int, u32*> gtab_;
     u32* renorm_w_[kStreams] = {};
+    u32* renorm_b_[kStreams] = {};
+    bool sparse_dec_ = env_int("AESFHE_SPARSE_DEC", 1) != 0;
+    u32* renorm_b() {  // [2][4][64] block sums of the sparse decryption
+        u32*& b = renorm_b_[t_sidx];
+        if (!b) b = dev_alloc((size_t)2 * 4 * 64);
+        return b;
+    }
     u32* renorm_w() {
         u32*& w = renorm_w_[t_sidx];
         if (!w) w = dev_alloc((size_t)2 * kRenormMaxLimbs * 64);

@@ -497,6 +497,15 @@ void launch_renorm_wtab32(hipStream_t st, const DevTables& T, u32* W, const doub
 // the same for two 16-periodic channels (D = 32 each)
 void launch_renorm_wtab16(hipStream_t st, const DevTables& T, u32* W, const double* w, double* zacc, const Slot16& sl, double scale, int nl,
                           const u32* gtab);
+// the sparse decryption (k_dec_blocksum + k_renorm_sparse): per channel the CRT limbs and constants
+struct SparseDec {
+    int kd[2] = {};
+    CrtConsts cc[2];
+};
+// nch = 1: one 32-slot channel (D = 64, sl32); nch = 2: two 16-slot channels (D = 32 each, sl16).  B: a
+// [2][4][64] scratch; W as launch_renorm_wtab32 / 16; s, s2: the secret (and its square) in NTT form
+void launch_renorm_sparse(hipStream_t st, const DevTables& T, u32* W, u32* B, const DecRaw& dr, int nch, const SparseDec& sd, const Slot32& sl32,
+                          const Slot16& sl16, double scale, int nl, const u32* gtab, const u32* s, const u32* s2);
 // out_c = pool_c + W_c on c0 (runs of N / 2^ld equal values), nch <= 2 channels of 2 x nl rows
 void launch_renorm_combine(hipStream_t st, const DevTables& T, const RenormOut& ro, int nch, const u32* W, int nl, int ld);
 // CONTRACT (as launch_decode16): acc zero on entry; the snap follows on the same stream, either inside the

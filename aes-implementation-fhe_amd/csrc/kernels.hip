@@ -1031,6 +1031,119 @@ __global__ void __launch_bounds__(256) k_renorm_wtab(u32* W, const double* w, do
         W[((size_t)c * nl + t) * D + d] = acc;
     }
 }
+// ---- the renorm's sparse decryption (round 6): the snap reads only the D subring coefficients k = j N / D of
+// m = c0 + c1 s (+ c2 s^2) -- the coefficients a message of D / 2 slots per channel can have; the others
+// carry noise only, which the decode drops (the trace projection of the decrypted polynomial).  From the
+// NTT form, coefficient j N / D = N^{-1} sum_i a_i psi^{-(2 brv(i) + 1) j N / D}, and the power depends on
+// i only through its top log2 D bits b: with B_b = the sum of the N / D consecutive a_i of block b, it is
+// the D-point inverse transform N^{-1} sum_b B_b g^{-(2 brv_D(b) + 1) j} (g = psi^(N / D)).
+// k_dec_blocksum: one block per (block b, limb t, channel c) -> B[c][t][b]
+template <int D>
+__global__ void __launch_bounds__(256) k_dec_blocksum(u32* B, DecRaw dr, const u32* s, const u32* s2, const PrimeConst* pc, int logn) {
+    const int b = blockIdx.x, t = blockIdx.y, c = blockIdx.z;
+    if (t >= dr.kd[c]) return;
+    const PrimeConst P = pc[t];
+    const int len = (1 << logn) / D;
+    const size_t base = ((size_t)t << logn) + (size_t)b * len, pl = (size_t)dr.nlc[c] << logn;
+    const u32* ct = dr.ct[c];
+    const bool three = dr.npoly[c] == 3;
+    unsigned long long acc = 0;
+    for (int k = threadIdx.x; k < len; k += 256) {
+        const size_t row = base + k;
+        u32 v = add_mod(ct[row], barrett_mul(ct[pl + row], s[row], P.q, P.mu), P.q);
+        if (three) v = add_mod(v, barrett_mul(ct[2 * pl + row], s2[row], P.q, P.mu), P.q);
+        acc += v;
+    }
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    __shared__ unsigned long long red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) B[((size_t)c * 4 + t) * D + b] = (u32)((red[0] + red[1] + red[2] + red[3]) % P.q);
+}
+// one block per channel: the D coefficients' residues (the inverse D-point transform of B), their centred
+// CRT value, the NS slots (m evaluated at zeta^(e_i), as k_decode32 / k_decode16 but over the subring
+// coefficients), the snap (k_snap16's rule), and the snapped message's NTT table W (k_renorm_wtab's)
+template <int NS>
+__global__ void __launch_bounds__(256) k_renorm_sparse(u32* W, const u32* B, SparseDec sd, SlotTab<NS> sl, double scale, int nl,
+                                                       const u32* gtab, const PrimeConst* pc, int logn) {
+    constexpr int D = 2 * NS, LD = (NS == 32) ? 6 : 5;
+    __shared__ u32 cr[4 * D];
+    __shared__ double mv[D];
+    __shared__ double ws[2 * NS];
+    __shared__ double xs[D];
+    __shared__ u32 res[kRenormMaxLimbs * D];
+    const int c = blockIdx.x, kd = sd.kd[c], n = 1 << logn;
+    const u32 mask = 2u * n - 1;
+    const double inv_n = 1.0 / n;
+    for (int idx = threadIdx.x; idx < kd * D; idx += blockDim.x) {
+        const int t = idx / D, j = idx - t * D;
+        const PrimeConst P = pc[t];
+        const u32* g = gtab + (size_t)t * 2 * D;
+        const u32* Bc = B + ((size_t)c * 4 + t) * D;
+        u32 acc = 0;
+        for (int b = 0; b < D; ++b) {
+            const u32 rv = (u32)(__brev((unsigned)b) >> (32 - LD));
+            const u32 e = (2u * D - (((2u * rv + 1u) * (u32)j) & (2u * D - 1))) & (2u * D - 1);
+            acc = add_mod(acc, barrett_mul(Bc[b], g[e], P.q, P.mu), P.q);
+        }
+        cr[idx] = shoup_mul(acc, P.ninv, P.ninv_p, P.q);
+    }
+    __syncthreads();
+    if (threadIdx.x < D) {
+        u32 r[4];
+        for (int t = 0; t < kd; ++t) r[t] = cr[t * D + threadIdx.x];
+        mv[threadIdx.x] = crt_centered(r, kd, sd.cc[c]);
+    }
+    __syncthreads();
+    if (threadIdx.x < NS) {  // slot i: sum_j m_j zeta^(e_i j N / D), snapped (k_snap16 / snap_slot's rule)
+        const int i = threadIdx.x;
+        double vr = 0.0, vi = 0.0;
+        for (int j = 0; j < D; ++j) {
+            double sn, cs;
+            sincospi((double)((sl.e[i] * (u32)(j * (n / D))) & mask) * inv_n, &sn, &cs);
+            vr += mv[j] * cs, vi += mv[j] * sn;
+        }
+        const double ang = atan2(vi, vr);
+        const double kf = rint(-ang * 16.0 / (2.0 * M_PI));
+        const int v = (int)((((long)kf) % 16 + 16) % 16);
+        double sn, cs;
+        sincospi(-2.0 * v / 16.0, &sn, &cs);
+        ws[2 * i] = cs - 1.0, ws[2 * i + 1] = sn;
+    }
+    __syncthreads();
+    if (threadIdx.x < D) {  // k_renorm_wtab's coefficients from the snapped deviations
+        const int j = threadIdx.x;
+        const u32 k = (u32)j * (u32)(n / D);
+        double v = 0.0;
+        for (int i = 0; i < NS; ++i) {
+            double sn, cs;
+            sincospi((double)((sl.e[i] * k) & mask) * inv_n, &sn, &cs);
+            v += ws[2 * i] * cs + ws[2 * i + 1] * sn;
+        }
+        v = v / (double)NS + (j == 0 ? 1.0 : 0.0);
+        xs[j] = rint(v * scale);
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < nl * D; idx += blockDim.x) {
+        const int t = idx / D, j = idx - t * D;
+        const double q = (double)pc[t].q, x = xs[j];
+        double r = fma(-q, floor(x / q), x);
+        if (r < 0) r += q;
+        if (r >= q) r -= q;
+        res[idx] = (u32)r;
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < nl * D; idx += blockDim.x) {
+        const int t = idx / D, d = idx - t * D;
+        const u32 q = pc[t].q, mu = pc[t].mu;
+        const u32 rv = (u32)(__brev((unsigned)d) >> (32 - LD));
+        const u32 e1 = 2u * rv + 1u;
+        const u32* g = gtab + (size_t)t * 2 * D;
+        u32 acc = 0;
+        for (int j = 0; j < D; ++j) acc = add_mod(acc, barrett_mul(res[t * D + j], g[(e1 * (u32)j) & (2u * D - 1)], q, mu), q);
+        W[((size_t)c * nl + t) * D + d] = acc;
+    }
+}
 // out_c (2 polys x nl limbs) = the zero encryption pool_c + (W_c broadcast over runs of N / D on c0)
 __global__ void k_renorm_combine(RenormOut ro, const u32* W, int nl, int ld, const PrimeConst* pc, int logn) {
     const int c = blockIdx.z, row = blockIdx.y, t = row % nl, p = row / nl;
@@ -1828,6 +1941,26 @@ void launch_renorm_wtab16(hipStream_t st, const DevTables& T, u32* W, const doub
         prof_launch(KID_ELEMENTWISE, 4.0 * 2 * 32 * nl, k_renorm_wtab<16, true>, dim3(2), dim3(256), 0, st, W, w, zacc, tab, scale, nl, gtab, T.pc, T.logn);
     else
         prof_launch(KID_ELEMENTWISE, 4.0 * 2 * 32 * nl, k_renorm_wtab<16, false>, dim3(2), dim3(256), 0, st, W, w, zacc, tab, scale, nl, gtab, T.pc, T.logn);
+}
+void launch_renorm_sparse(hipStream_t st, const DevTables& T, u32* W, u32* B, const DecRaw& dr, int nch, const SparseDec& sd, const Slot32& sl32,
+                          const Slot16& sl16, double scale, int nl, const u32* gtab, const u32* s, const u32* s2) {
+    if (nl < 1 || nl > kRenormMaxLimbs) throw std::runtime_error("launch_renorm_sparse: limb count out of range");
+    const double n = (double)(1u << T.logn);
+    double w = 0.0;
+    for (int c = 0; c < nch; ++c) w += (double)dr.kd[c] * (dr.npoly[c] + 1);
+    if (nch == 1) {  // one 32-slot channel (the packed period-32 renorm)
+        SlotTab<32> tab;
+        for (int i = 0; i < 32; ++i) tab.e[i] = sl32.e[i];
+        prof_launch(KID_ELEMENTWISE, words(w * n), k_dec_blocksum<64>, dim3(64, 4, 1), dim3(256), 0, st, B, dr, s, s2, T.pc, T.logn);
+        prof_launch(KID_ELEMENTWISE, 4.0 * 64 * (4 + nl), k_renorm_sparse<32>, dim3(1), dim3(256), 0, st, W, (const u32*)B, sd, tab, scale, nl, gtab,
+                    T.pc, T.logn);
+    } else {  // two 16-slot channels (the periodic pair renorm)
+        SlotTab<16> tab;
+        for (int i = 0; i < 16; ++i) tab.e[i] = sl16.e[i];
+        prof_launch(KID_ELEMENTWISE, words(w * n), k_dec_blocksum<32>, dim3(32, 4, 2), dim3(256), 0, st, B, dr, s, s2, T.pc, T.logn);
+        prof_launch(KID_ELEMENTWISE, 4.0 * 2 * 32 * (4 + nl), k_renorm_sparse<16>, dim3(2), dim3(256), 0, st, W, (const u32*)B, sd, tab, scale, nl,
+                    gtab, T.pc, T.logn);
+    }
 }
 void launch_renorm_combine(hipStream_t st, const DevTables& T, const RenormOut& ro, int nch, const u32* W, int nl, int ld) {
     if (nch < 1 || nch > 2) throw std::runtime_error("launch_renorm_combine: 1 or 2 channels");
