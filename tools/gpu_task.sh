@@ -65,16 +65,18 @@ for t in "$@"; do
       # for the engine's algorithmic bytes of exactly those launches (VERDICT r4 'do this' 7)
       KIDS=key_inner,base_convert,ntt_cols_fwd,ntt_rows_fwd,ntt_rows_inv,ntt_cols_inv,lin_mac
       PB="--steps ${PMC_STEPS:-1} --warmup 1 $C2 --detail-json $O/pmcb_detail.json --whole-stats $O/ws_unused.json"
-      HIP_FORCE_DEV_KERNARG=0 AESFHE_PROFILE_FROM_START=$KIDS timeout -k 10 200 python3 bench.py --steps ${PMC_STEPS:-1} --warmup 1 $C2 \
+      AESFHE_PROFILE_FROM_START=$KIDS timeout -k 10 200 python3 bench.py --steps ${PMC_STEPS:-1} --warmup 1 $C2 \
           --detail-json $O/pmcb_detail0.json --whole-stats $O/pmcb_algorithmic.json > $O/pmcb_alg.out
-      # HIP_FORCE_DEV_KERNARG=0: kernel arguments in host memory under the counter passes.  With them in
-      # device memory (the gfx950 default) rocprofv3's dispatch interception read past the end of a
-      # kernarg mapping (SIGSEGV in a memcpy under hipLaunchKernel, rounds 2, 4 and 5: profiles/README.md)
-      HIP_FORCE_DEV_KERNARG=0 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmcb_fetch -o run -- \
+      # HIP_ENABLE_DEFERRED_LOADING=0: every code object loaded at start-up.  With lazy loading (the default)
+      # the FETCH pass died with SIGSEGV inside rocprofv3's dispatch interception at the FIRST dispatch of a
+      # kernel of a not-yet-loaded translation unit (k_ntt2_inv8 r5, k_lut_bivariate / k_dec_blocksum r6:
+      # a libc copy faulting at a 1 MiB-aligned address, profiles/r6_pmc_sigsegv.txt); the WRITE pass takes
+      # WRITE_SIZE itself (its raw TCC_EA0_WRREQ counters hung the bench at start-up twice in round 6)
+      HIP_ENABLE_DEFERRED_LOADING=0 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/pmcb_fetch -o run -- \
           python3 bench.py $PB > $O/pmcb_fetch.out 2> $O/pmcb_fetch.err
-      HIP_FORCE_DEV_KERNARG=0 timeout -s KILL 200 rocprofv3 --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum --output-format csv -d $O/pmcb_write -o run -- \
+      HIP_ENABLE_DEFERRED_LOADING=0 timeout -s KILL 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/pmcb_write -o run -- \
           python3 bench.py $PB > $O/pmcb_write.out 2> $O/pmcb_write.err
-      timeout -k 10 300 python3 tools/pmc_reduce.py "--source=rocprofv3 --pmc FETCH_SIZE and --pmc TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum (= WRITE_SIZE; separate runs, every kernel) over the bench's own C2 leg (bench.py --steps ${PMC_STEPS:-1} --warmup 1, secondary legs off), whole process; algorithmic bytes of the same launches (AESFHE_PROFILE_FROM_START); FETCH x2 for 16-B-per-lane reads, x1 for NTT pass-2 dword reads (MI355X_MICROARCH.md HBM section, tools/ntt_pmc_calib.py)" \
+      timeout -k 10 300 python3 tools/pmc_reduce.py "--source=rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate runs, every kernel, HIP_ENABLE_DEFERRED_LOADING=0) over the bench's own C2 leg (bench.py --steps ${PMC_STEPS:-1} --warmup 1, secondary legs off), whole process; algorithmic bytes of the same launches (AESFHE_PROFILE_FROM_START); FETCH x2 for 16-B-per-lane reads, x1 for NTT pass-2 dword reads (MI355X_MICROARCH.md HBM section, tools/ntt_pmc_calib.py)" \
           --alg=$O/pmcb_algorithmic.json $O/pmc_traffic_bench.json $O/pmcb_fetch $O/pmcb_write > /dev/null
       rm -rf $O/pmcb_fetch $O/pmcb_write ;;
     twogpu)
