@@ -482,7 +482,7 @@ struct Slot32 {
     u32 e[32];
 };
 // the renorm's pooled re-encryption (k_renorm_wtab / k_renorm_combine, Engine::zero_enc)
-constexpr int kRenormMaxLimbs = 64;
+constexpr int kRenormMaxLimbs = 24;  // the fresh level has 19 limbs
 template <int NS>
 struct SlotTab {
     u32 e[NS];

@@ -1066,20 +1066,35 @@ __global__ void __launch_bounds__(256) k_dec_blocksum(u32* B, DecRaw dr, const u
 template <int NS>
 __global__ void __launch_bounds__(256) k_renorm_sparse(u32* W, const u32* B, SparseDec sd, SlotTab<NS> sl, double scale, int nl,
                                                        const u32* gtab, const PrimeConst* pc, int logn) {
+    // every table the phases read is staged in LDS first: the serial D-term sums then wait on LDS, not on
+    // L2 (a first form read B and gtab from global memory in its inner loops: 31 us per launch)
     constexpr int D = 2 * NS, LD = (NS == 32) ? 6 : 5;
     __shared__ u32 cr[4 * D];
+    __shared__ u32 bs[4 * D];
+    __shared__ u32 gs[kRenormMaxLimbs * 2 * D];
     __shared__ double mv[D];
     __shared__ double ws[2 * NS];
     __shared__ double xs[D];
+    __shared__ double cs_[NS * D], sn_[NS * D];  // the angles pi (e_i j N / D mod 2N) / N of slot i, coefficient j
     __shared__ u32 res[kRenormMaxLimbs * D];
     const int c = blockIdx.x, kd = sd.kd[c], n = 1 << logn;
+    const int nt = nl > kd ? nl : kd;
     const u32 mask = 2u * n - 1;
     const double inv_n = 1.0 / n;
+    for (int idx = threadIdx.x; idx < nt * 2 * D; idx += blockDim.x) gs[idx] = gtab[idx];
+    for (int idx = threadIdx.x; idx < kd * D; idx += blockDim.x) bs[idx] = B[((size_t)c * 4) * D + idx];
+    for (int idx = threadIdx.x; idx < NS * D; idx += blockDim.x) {
+        const int i = idx / D, j = idx - i * D;
+        double sn, cs;
+        sincospi((double)((sl.e[i] * (u32)(j * (n / D))) & mask) * inv_n, &sn, &cs);
+        cs_[idx] = cs, sn_[idx] = sn;
+    }
+    __syncthreads();
     for (int idx = threadIdx.x; idx < kd * D; idx += blockDim.x) {
         const int t = idx / D, j = idx - t * D;
         const PrimeConst P = pc[t];
-        const u32* g = gtab + (size_t)t * 2 * D;
-        const u32* Bc = B + ((size_t)c * 4 + t) * D;
+        const u32* g = gs + t * 2 * D;
+        const u32* Bc = bs + t * D;
         u32 acc = 0;
         for (int b = 0; b < D; ++b) {
             const u32 rv = (u32)(__brev((unsigned)b) >> (32 - LD));
@@ -1098,11 +1113,7 @@ __global__ void __launch_bounds__(256) k_renorm_sparse(u32* W, const u32* B, Spa
     if (threadIdx.x < NS) {  // slot i: sum_j m_j zeta^(e_i j N / D), snapped (k_snap16 / snap_slot's rule)
         const int i = threadIdx.x;
         double vr = 0.0, vi = 0.0;
-        for (int j = 0; j < D; ++j) {
-            double sn, cs;
-            sincospi((double)((sl.e[i] * (u32)(j * (n / D))) & mask) * inv_n, &sn, &cs);
-            vr += mv[j] * cs, vi += mv[j] * sn;
-        }
+        for (int j = 0; j < D; ++j) vr += mv[j] * cs_[i * D + j], vi += mv[j] * sn_[i * D + j];
         const double ang = atan2(vi, vr);
         const double kf = rint(-ang * 16.0 / (2.0 * M_PI));
         const int v = (int)((((long)kf) % 16 + 16) % 16);
@@ -1113,13 +1124,8 @@ __global__ void __launch_bounds__(256) k_renorm_sparse(u32* W, const u32* B, Spa
     __syncthreads();
     if (threadIdx.x < D) {  // k_renorm_wtab's coefficients from the snapped deviations
         const int j = threadIdx.x;
-        const u32 k = (u32)j * (u32)(n / D);
         double v = 0.0;
-        for (int i = 0; i < NS; ++i) {
-            double sn, cs;
-            sincospi((double)((sl.e[i] * k) & mask) * inv_n, &sn, &cs);
-            v += ws[2 * i] * cs + ws[2 * i + 1] * sn;
-        }
+        for (int i = 0; i < NS; ++i) v += ws[2 * i] * cs_[i * D + j] + ws[2 * i + 1] * sn_[i * D + j];
         v = v / (double)NS + (j == 0 ? 1.0 : 0.0);
         xs[j] = rint(v * scale);
     }
@@ -1138,7 +1144,7 @@ __global__ void __launch_bounds__(256) k_renorm_sparse(u32* W, const u32* B, Spa
         const u32 q = pc[t].q, mu = pc[t].mu;
         const u32 rv = (u32)(__brev((unsigned)d) >> (32 - LD));
         const u32 e1 = 2u * rv + 1u;
-        const u32* g = gtab + (size_t)t * 2 * D;
+        const u32* g = gs + t * 2 * D;
         u32 acc = 0;
         for (int j = 0; j < D; ++j) acc = add_mod(acc, barrett_mul(res[t * D + j], g[(e1 * (u32)j) & (2u * D - 1)], q, mu), q);
         W[((size_t)c * nl + t) * D + d] = acc;
