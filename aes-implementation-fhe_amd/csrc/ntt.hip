@@ -589,7 +589,7 @@ __global__ void __launch_bounds__(NT, OCC) k_ntt2_fwd(u32* data, RowMap rm, Limb
     ts_end(ts);
 }
 
-// the forward row pass at 8 residues per thread (AESFHE_NTT_FWD8): k_ntt2_fwd's modes (plain, and
+// the forward row pass at 8 residues per thread (AESFHE_NTT_FWD8, default on): k_ntt2_fwd's modes (plain, and
 // the finish with its cur / add / cmul / 2 r + c epilogue) on 256-thread blocks of 8 rows through
 // ki8_fwd_rows -- the same butterflies, twiddles and canonical outputs, so the same residues
 template <int LOGR1, int MODE>
@@ -651,8 +651,9 @@ __global__ void __launch_bounds__(256) k_ntt2_fwd8(u32* data, RowMap rm, LimbMap
     }
     ts_end(ts);
 }
+// default on since round 6 (strict C2 +0.6 %, three passes each, profiles/r6_fwd8_ab.txt); AESFHE_NTT_FWD8=0: k_ntt2_fwd
 inline bool fwd8_on() {
-    static const bool v = std::getenv("AESFHE_NTT_FWD8") && std::atoi(std::getenv("AESFHE_NTT_FWD8")) != 0;
+    static const bool v = !(std::getenv("AESFHE_NTT_FWD8") && std::atoi(std::getenv("AESFHE_NTT_FWD8")) == 0);
     return v;
 }
 

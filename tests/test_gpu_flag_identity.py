@@ -3,7 +3,7 @@ process, so every configuration runs in a fresh process.
 
 - the 8-residue fused key-switch core (AESFHE_KI8), the 8-residue inverse row pass (AESFHE_NTT_INV8),
   the conversion sources pre-multiplied in the INTT (AESFHE_CONV_PRE), the 8-residue forward row pass
-  (AESFHE_NTT_FWD8, off by default): every
+  (AESFHE_NTT_FWD8, on by default since round 6; its switch-off tested): every
   key-switching path's raw output limbs (tests/helpers/fused_conv_probe.py: relinearisation with and
   without the rescale, rotations, a conjugation, a batched rotation set, a stacked key switch, a sparse
   bootstrap) hash the same as with the default kernels -- bit for bit;
@@ -38,7 +38,7 @@ def default_digests():
 
 
 @pytest.mark.parametrize("flag,value", [("AESFHE_KI8", 0), ("AESFHE_NTT_INV8", 0), ("AESFHE_CONV_PRE", 0),
-                                        ("AESFHE_NTT_FWD8", 1)])
+                                        ("AESFHE_NTT_FWD8", 0)])
 def test_kernel_switch_bit_identical(default_digests, flag, value):
     other = _run("fused_conv_probe.py", **{flag: value})
     assert other.keys() == default_digests.keys()
