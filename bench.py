@@ -34,10 +34,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level para
 # VALU roofline of the NTT passes: u32 VALU issue rate measured on this chip with
 # tools/valu_rate.hip (v_mul_lo_u32 / v_mul_hi_u32 / v_min_u32 all at ~3.85e13 lane-instr/s,
 # i.e. the 32-bit multiplies are NOT quarter rate on gfx950) over the VALU instructions per
-# radix-2 butterfly in k_ntt2_fwd's ISA (756 per thread for 64 butterflies with the 7-operation
-# lazy butterfly: hipcc --save-temps, v_* lines of k_ntt2_fwd<8, 0, 512>)
+# radix-2 butterfly in the row pass's ISA.  Round 6 runs the 8-residue form k_ntt2_fwd8 (AESFHE_NTT_FWD8,
+# default since): 451 v_* lines per thread for its 32 butterflies (plain mode; hipcc --save-temps,
+# k_ntt2_fwd8<8, 0>), against 676 for k_ntt2_fwd<8, 0, 256>'s 64 -- more indexing per butterfly, twice the
+# blocks and half the serial work per thread
 VALU_LANE_INSTR_PER_S = 3.85e13
-NTT_VALU_INSTR_PER_BFLY = 756.0 / 64.0
+NTT_VALU_INSTR_PER_BFLY = 451.0 / 32.0
 
 
 def parse():
