@@ -31,10 +31,13 @@ class EngineContext:
                  use_multiparty: bool = False, mode: str = "cpu", device_id: int = 0,
                  thread_count: int | None = None, log_n: int = 16, dnum: int | None = None, seed: int | bytes | None = None,
                  lazy: bool = True, concurrent: bool = False, fused_luts: bool = True, allow_insecure: bool = False,
-                 enc_nonce: int | None = None, defer_calls: bool | None = None):
-        # REF/engine_context.py:17-42: signature selects the engine constructor form
+                 enc_nonce: int | None = None, defer_calls: bool | None = None, boot_fresh_level: int | None = None):
+        # REF/engine_context.py:17-42: signature selects the engine constructor form.  boot_fresh_level
+        # (an extension; REF's signature 1 takes the engine's default, 17): the fresh level of the
+        # bootstrappable set -- the bootstrap's double-prime region sits above it, so a pipeline that never
+        # needs more levels between its renorms / bootstraps runs every bootstrap on fewer limbs
         if signature == 1:
-            kw = dict(use_bootstrap=use_bootstrap, max_level=_SIG_DEFAULT_LEVEL)
+            kw = dict(use_bootstrap=use_bootstrap, max_level=boot_fresh_level or _SIG_DEFAULT_LEVEL)
         elif signature == 2:
             kw = dict(max_level=max_level)
         elif signature == 3:

@@ -308,6 +308,7 @@ class Engine:
             raise ValueError("multiparty key generation is not supported")
         self.mode = mode
         self.use_bootstrap = use_bootstrap
+        self.device_id = int(device_id)
         # bootstrappable set: the chain is extended by the bootstrap depth above the fresh level;
         # 5 key-switching digits there (alpha = 9, 10 special primes, log2 PQ = 1699) keep log2 PQ
         # under the 128-bit bound (1772 at N = 2^16); 4 digits would cross it (1790), 6 cost

@@ -91,6 +91,10 @@ def parse():
                     help="multi-pair slot-packed batch: this many stacked ciphertext pairs of 2048 states each per rank; 0 = skip")
     ap.add_argument("--pair-steps", type=int, default=1, help="timed steps of the one-state multi-pair leg (C3 literally)")
     ap.add_argument("--packed-pair-steps", type=int, default=3, help="timed steps of the slot-packed multi-pair leg")
+    ap.add_argument("--fresh-level", type=int, default=17,
+                    help="fresh level of the C2 context's bootstrappable set (EngineContext(boot_fresh_level=)); the "
+                         "true-FHE and REF-call legs keep 17")
+    ap.add_argument("--dnum", type=int, default=None, help="key-switching digits of the C2 context (default: the engine's, 5)")
     ap.add_argument("--folded-steps", type=int, default=5,
                     help="timed steps of the 'folded' leg: C2 with the renorm folds on (utils.RenormFolds; the headline is strict)")
     ap.add_argument("--true-fhe-steps", type=int, default=1,
@@ -607,6 +611,12 @@ def run_true_fhe(ctx, coeffs, rks, args, rank, world, dist, tj: dict) -> dict:
     normalised by 1/256.  One state per rank per step, checked after the timed region."""
     from oracle import aes_plain  # checker only, after the timed region
     from pipeline import AESPipeline
+    if ctx.engine.fresh_level < 17:
+        # the true-FHE snaps need SubBytes' 8 -> 4 form's 13 levels after a bootstrap: the engine's default
+        # bootstrappable set (fresh level 17), its own context and key set
+        from engine_context import EngineContext
+        ctx = EngineContext(signature=1, max_level=17, thread_count=1, device_id=ctx.engine.device_id, seed=ctx.engine.seed,
+                            lazy=ctx.engine.lazy)
     pipe = AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=False, true_fhe=True)
     sts = rank_states(rank + 1000, 1 + args.true_fhe_steps)
     pipe.encrypt(sts[0], rks)  # warmup: snap constants, normalised XOR4 coefficient sets
@@ -928,7 +938,7 @@ def main():
     signature = 2 if args.no_final_bootstrap else 1
     seed = shared_seed(dist, args.seed)  # one key set for every rank (broadcast once, untimed)
     ctx = EngineContext(signature=signature, max_level=17, thread_count=1, device_id=local, seed=seed, lazy=not args.eager,
-                        concurrent=args.concurrent and not args.serial)
+                        concurrent=args.concurrent and not args.serial, boot_fresh_level=args.fresh_level, dnum=args.dnum)
     xor4 = XOR4LUT(ctx, coeffs["xor4"])
     from state_encoder import SlotLayout
     layout = SlotLayout(ctx.engine.slot_count, 1, periodic=not args.ref_layout)
