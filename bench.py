@@ -91,10 +91,12 @@ def parse():
                     help="multi-pair slot-packed batch: this many stacked ciphertext pairs of 2048 states each per rank; 0 = skip")
     ap.add_argument("--pair-steps", type=int, default=1, help="timed steps of the one-state multi-pair leg (C3 literally)")
     ap.add_argument("--packed-pair-steps", type=int, default=3, help="timed steps of the slot-packed multi-pair leg")
-    ap.add_argument("--fresh-level", type=int, default=17,
-                    help="fresh level of the C2 context's bootstrappable set (EngineContext(boot_fresh_level=)); the "
-                         "true-FHE and REF-call legs keep 17")
-    ap.add_argument("--dnum", type=int, default=None, help="key-switching digits of the C2 context (default: the engine's, 5)")
+    ap.add_argument("--fresh-level", type=int, default=9,
+                    help="fresh level of the C2 context's bootstrappable set (EngineContext(boot_fresh_level=)): 9, the most "
+                         "any step of the strict pipeline needs between renorms / bootstraps, puts the bootstrap's double-prime "
+                         "region 8 primes lower (DESIGN.md 4); the true-FHE and REF-call legs keep the engine's 17")
+    ap.add_argument("--dnum", type=int, default=4, help="key-switching digits of the C2 context (4: the shorter chain leaves "
+                                                         "room under the 128-bit bound; the engine's default set uses 5)")
     ap.add_argument("--folded-steps", type=int, default=5,
                     help="timed steps of the 'folded' leg: C2 with the renorm folds on (utils.RenormFolds; the headline is strict)")
     ap.add_argument("--true-fhe-steps", type=int, default=1,
@@ -446,6 +448,8 @@ def run_pairs(ctx, coeffs, rks, args, rank, world, dist, pairs: int, states: int
     Warmup: ONE stack of each shape (every stack of a shape runs the same launches)."""
     from oracle import aes_plain  # checker only, after the timed region
     from pipeline import AESPipeline
+    if 2 * 16 * states > ctx.engine.slot_count:  # no packed form for this state count: the pair path's levels
+        ctx = full_levels(ctx)
     chunks = [min(stack, pairs - i) for i in range(0, pairs, stack)]
     pipes = {c: AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=True, states=states, pairs=c) for c in set(chunks)}
     rng = np.random.default_rng(8192 + rank)
@@ -605,18 +609,31 @@ def run_folded(ctx, coeffs, rks, args, rank, world, dist, mix_layout, strict_val
             "verified_against_plaintext_model": bool(ok)}
 
 
+_CTX17 = {}
+
+
+def full_levels(ctx):
+    """ctx itself when its fresh level is the engine's default 17, else ONE extra context with the engine's
+    default bootstrappable set (fresh level 17, dnum 5; same seed, its own keys), made once: for the legs
+    whose path needs more levels between renorms than the C2 set's 9 (true-FHE, the reference pair path
+    of a state count too large for the packed form)"""
+    if ctx.engine.fresh_level >= 17:
+        return ctx
+    if "ctx" not in _CTX17:
+        from engine_context import EngineContext
+        _CTX17["ctx"] = EngineContext(signature=1, max_level=17, thread_count=1, device_id=ctx.engine.device_id, seed=ctx.engine.seed,
+                                      lazy=ctx.engine.lazy)
+    return _CTX17["ctx"]
+
+
 def run_true_fhe(ctx, coeffs, rks, args, rank, world, dist, tj: dict) -> dict:
     """the C2 workload with no secret key between encryption and decryption --
     every renorm point is a bootstrap + homomorphic Zeta16 snap (zeta16_noise_reducer.py), XOR4
     normalised by 1/256.  One state per rank per step, checked after the timed region."""
     from oracle import aes_plain  # checker only, after the timed region
     from pipeline import AESPipeline
-    if ctx.engine.fresh_level < 17:
-        # the true-FHE snaps need SubBytes' 8 -> 4 form's 13 levels after a bootstrap: the engine's default
-        # bootstrappable set (fresh level 17), its own context and key set
-        from engine_context import EngineContext
-        ctx = EngineContext(signature=1, max_level=17, thread_count=1, device_id=ctx.engine.device_id, seed=ctx.engine.seed,
-                            lazy=ctx.engine.lazy)
+    # the true-FHE snaps need SubBytes' 8 -> 4 form's 13 levels after a bootstrap: the engine's default set
+    ctx = full_levels(ctx)
     pipe = AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=False, true_fhe=True)
     sts = rank_states(rank + 1000, 1 + args.true_fhe_steps)
     pipe.encrypt(sts[0], rks)  # warmup: snap constants, normalised XOR4 coefficient sets
@@ -811,7 +828,7 @@ def compact_line(full: dict, detail_path: str | None = None) -> dict:
     line["value"] = _sig(line.get("value"), 6)
     line["ms_per_step"] = _sig(line.get("ms_per_step"), 6)
     cfg = full.get("config", {})
-    line["config"] = {k: cfg[k] for k in ("workload", "log_n", "states_per_rank_per_step", "parallelism", "blocks_per_s",
+    line["config"] = {k: cfg[k] for k in ("workload", "log_n", "params", "states_per_rank_per_step", "parallelism", "blocks_per_s",
                                           "verified_against_plaintext_model") if k in cfg}
     line["config"]["blocks_per_s"] = _sig(line["config"].get("blocks_per_s"), 6)
     r = _compact_roof(full.get("roofline"))
@@ -1068,6 +1085,8 @@ def main():
         "config": {"workload": "C2: full AES-128 encrypt (10 rounds), 1 packed state per ciphertext pair, "
                                "N=2^16, renorm on (strict: every secret-key renorm the identity on the message, as REF's)" + ("" if not args.no_final_bootstrap else ", FINAL BOOTSTRAP SKIPPED"),
                    "log_n": 16, "states_per_rank_per_step": 1, "parallelism": f"replicas x{world}",
+                   "params": {"fresh_level": ctx.engine.fresh_level, "dnum": ctx.engine.dnum, "log2_pq": round(ctx.engine.log_pq, 1),
+                              "top_limbs": int(ctx.engine.level_limbs[-1]), "security_bound_log2_pq": 1772},
                    "slot_layout": ("reference (byte i at slot i*N/32; full-slot bootstraps)" if args.ref_layout else
                                    "periodic (the 16-slot state block repeated; MixColumns' final bootstraps as "
                                    "sparse-slot bootstraps, DESIGN.md 4b)"),
