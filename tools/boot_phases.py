@@ -2,7 +2,8 @@
 bytes over the in-kernel span, and over span + boundary gap) (C2's MixColumns final bootstrap: one packed
 ciphertext, period P = 32): wall time (synchronised) and kernel launches of the bootstrap run up
 to each debug stage (aesfhe_debug_boot_stage_sparse), and the per-phase differences.
-usage: python tools/boot_phases.py [P] > out.json"""
+usage: python tools/boot_phases.py [P] [FRESH_LEVEL DNUM] > out.json   (default: the engine's set, 17 / 5;
+bench.py's C2 set is 9 / 4)"""
 import json
 import sys
 import time
@@ -24,7 +25,9 @@ STAGES = [(1, "level-0 scaling"), (2, "dense->sparse key switch"), (3, "ModRaise
 def main():
     P = int(sys.argv[1]) if len(sys.argv) > 1 else 32
     reps = 5
-    ctx = EngineContext(signature=1, max_level=17)
+    fresh = int(sys.argv[2]) if len(sys.argv) > 2 else None
+    dnum = int(sys.argv[3]) if len(sys.argv) > 3 else None
+    ctx = EngineContext(signature=1, max_level=17, boot_fresh_level=fresh, dnum=dnum)
     E = ctx.engine
     z = np.exp(2j * np.pi * np.random.default_rng(0).random(P))
     ct = E.intt(ctx.encrypt(np.tile(z, E.slot_count // P)))
@@ -65,7 +68,7 @@ def main():
         out[name] = {"ms": round(ms - prev[0], 3), "launches": ln - prev[1], "cumulative_ms": round(ms, 3), "by_class": kc,
                      "roofline_by_class": roof}
         prev, kprev, rprev = (ms, ln), kcum[name], rcum[name]
-    print(json.dumps({"period": P, "reps": reps, "phases": out}, indent=1))
+    print(json.dumps({"period": P, "reps": reps, "fresh_level": ctx.engine.fresh_level, "dnum": ctx.engine.dnum, "phases": out}, indent=1))
 
 
 if __name__ == "__main__":
