@@ -4305,6 +4305,37 @@ public:
         *oa = put_ct(hi);
         *ob = put_ct(lo);
     }
+    // four n-periodic messages (4n <= slots) as ONE 4n-periodic message:
+    // the pairs (a, b) and (c, d) packed as above into the 2n-periodic z1, z2, then
+    // z = z1 + X^(N/8n) z2 in Z[X^(N/8n)] (exact again).  One bootstrap at period 4n with
+    // gain / 4 refreshes all four; rotations by 2n then n slots split it back (mono_split twice)
+    void bootstrap_quad_mono(const Ct* const in[4], aesfhe_handle* out[4], double gain, int period) {
+        boot_setup();
+        for (int m = 0; m < 4; ++m)
+            if (vis_npoly(*in[m]) != 2 || in[m]->nb != in[0]->nb)
+                throw std::runtime_error("bootstrap_quad: four 2-polynomial ciphertexts of one stack size expected");
+        const int n = hp_.n, nl0 = hp_.nl(0);
+        if (period < 1 || 4 * period > slot_count() || n % (8 * period))
+            throw std::runtime_error("bootstrap_quad: the period must satisfy 4 period <= slots");
+        Ct z1 = mono_pack(*in[0], *in[1], period);
+        Ct z2 = mono_pack(*in[2], *in[3], period);
+        Ct z = alloc_ct(0, z1.npoly, z1.nb);
+        launch_fma_poly(S(), T_, z.data, z1.data, z2.data, monomial(n / (8 * period)), z1.npoly * nl0, nl0, qmap());
+        release(z1);
+        release(z2);
+        z_members_ = z.nb;
+        SparseBoot* sv = 4 * period < slot_count() ? &sparse_variant(4 * period) : nullptr;
+        Ct mz = boot_stack(z, 0.25 * gain, sv);
+        Ct h[2], o[4];
+        mono_split(mz, 2 * period, h[0], h[1]);
+        release(mz);
+        for (int j = 0; j < 2; ++j) {
+            mono_split(h[j], period, o[2 * j], o[2 * j + 1]);
+            release(h[j]);
+        }
+        cnt_[C_BOOT] += 3 * z_members_;  // four messages per packed quad
+        for (int m = 0; m < 4; ++m) *out[m] = put_ct(o[m]);
+    }
     // NTT form of the monomial X^e (X^N = -1, e in [0, 2N)) on every Q limb: the product by
     // it is exact (coefficients shifted, the wrapped ones negated; no level, no noise)
     std::map<int, u32*> mono_;
@@ -5305,6 +5336,15 @@ int aesfhe_bootstrap_pair_sparse(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle
     const Ct& ca = e.canon(a);
     const Ct& cb = e.canon(b);
     e.bootstrap_pair(ca, cb, out_a, out_b, gain, period);
+    API_END
+}
+int aesfhe_bootstrap_quad_sparse(aesfhe_ctx* ctx, const aesfhe_handle* in, int period, double gain, aesfhe_handle* out) {
+    API_BEGIN Engine& e = *ctx->eng;
+    if (!in || !out) throw std::runtime_error("bootstrap_quad: null handle array");
+    const Ct* c[4];
+    for (int m = 0; m < 4; ++m) c[m] = &e.canon(in[m]);
+    aesfhe_handle* o[4] = {out, out + 1, out + 2, out + 3};
+    e.bootstrap_quad_mono(c, o, gain, period);
     API_END
 }
 int aesfhe_bootstrap_depth(void) { return Engine::boot_depth(); }

@@ -30,6 +30,7 @@ from __future__ import annotations
 
 import hashlib
 import numbers
+import threading
 import weakref
 
 import numpy as np
@@ -37,6 +38,9 @@ import numpy as np
 from mi355x_ckks import Ciphertext, Plaintext
 
 _LUT_MAX = 16  # kLutMax (csrc/kernels.h): factors per side of one bivariate LUT
+
+
+_FALLBACK_LOCK = threading.RLock()  # engines without their own (test stubs)
 
 
 class Deferred(Ciphertext):
@@ -54,7 +58,7 @@ class Deferred(Ciphertext):
         if self._res is None:
             # one resolution per object even when two branch threads need it at once:
             # the engine's re-entrant lock (a resolution may resolve the deferred operands it reads)
-            with self._eng._defer_lock:
+            with getattr(self._eng, "_defer_lock", None) or _FALLBACK_LOCK:
                 if self._res is None:
                     res = self._resolve()
                     self._res = res

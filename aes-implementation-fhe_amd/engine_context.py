@@ -56,7 +56,8 @@ class EngineContext:
         self.conjugation_key = eng.create_conjugation_key(self.secret_key)
         self.rotation_key = eng.create_rotation_key(self.secret_key)
         self.bootstrap_key = eng.create_bootstrap_key(self.secret_key)
-        self._bs_count = 0
+        self._bs_count = 0  # ciphertexts refreshed
+        self._bs_calls = 0  # bootstrap calls (a pair / quad call on periodic messages: one packed bootstrap)
         self._bs_total_s = 0.0
         self.fused_luts = bool(fused_luts)
         self._init_lut_cache()
@@ -160,6 +161,7 @@ class EngineContext:
         t0 = time.perf_counter()
         out = self.engine.bootstrap(ct, self.relinearization_key, self.conjugation_key, self.bootstrap_key)
         self._bs_count += 1
+        self._bs_calls += 1
         self._bs_total_s += time.perf_counter() - t0
         return out
 
@@ -170,6 +172,7 @@ class EngineContext:
         t0 = time.perf_counter()
         out = self.engine.bootstrap_pair(a, b)
         self._bs_count += 2
+        self._bs_calls += 1
         self._bs_total_s += time.perf_counter() - t0
         return out
 
@@ -182,6 +185,17 @@ class EngineContext:
         else:
             out = self.engine.bootstrap_pair_scaled(a, b, gain)
         self._bs_count += 2
+        self._bs_calls += 1
+        self._bs_total_s += time.perf_counter() - t0
+        return out
+
+    def bootstrap_quad_scaled(self, cts, gain: float, period: int):
+        """[gain * bootstrap(c) for c in cts] for four `period`-periodic ciphertexts as ONE bootstrap
+        at period 4 * period (monomial quad packing)"""
+        t0 = time.perf_counter()
+        out = self.engine.bootstrap_quad_sparse(cts, period, gain)
+        self._bs_count += 4
+        self._bs_calls += 1
         self._bs_total_s += time.perf_counter() - t0
         return out
 
@@ -191,15 +205,17 @@ class EngineContext:
         t0 = time.perf_counter()
         out = self.engine.bootstrap_pair_sparse(a, b, period)
         self._bs_count += 2
+        self._bs_calls += 1
         self._bs_total_s += time.perf_counter() - t0
         return out
 
     def bootstrap_stats(self):
         n = self._bs_count
-        return {"count": n, "total_s": self._bs_total_s, "avg_s": self._bs_total_s / n if n else 0.0}
+        return {"count": n, "calls": self._bs_calls, "total_s": self._bs_total_s, "avg_s": self._bs_total_s / n if n else 0.0}
 
     def reset_bootstrap_stats(self):
         self._bs_count = 0
+        self._bs_calls = 0
         self._bs_total_s = 0
 
     # -------------------------------------------------------------- representation

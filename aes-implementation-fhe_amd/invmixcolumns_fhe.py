@@ -120,6 +120,21 @@ class InvMixColumnsFHE:
             acc = bootstrap1(ctx, acc, 2 * self.layout.period)
         return acc
 
+    def _call_fhe_quad(self, ct_hi, ct_lo, rot, do_final_bootstrap: bool, final_renorm: bool):
+        """true-FHE with the quad bootstrap (zeta16_noise_reducer.BootstrapSnap.apply_quad; as
+        MixColFinal.mix_rotated): the four GF multiplier pairs' outputs renormalised two pairs per
+        bootstrap before any XOR4 (so the input needs the GF multipliers' levels only, not NEED_GF,
+        and each XOR4 meets freshly snapped inputs), then (e14 ^ e11) ^ (e13 ^ e9) with the inner XOR
+        pairs renormalised together"""
+        enc, fl = self.enc, RENORM_FLOOR
+        e14, e11 = enc.renorm_two(self._gf(14, ct_hi, ct_lo, fl), self._gf(11, *rot[1], fl), level=NEED_XOR)
+        e13, e9 = enc.renorm_two(self._gf(13, *rot[2], fl), self._gf(9, *rot[3], fl), level=NEED_XOR)
+        x1, x2 = enc.renorm_two(self._xor_pair(e14, e11, fl), self._xor_pair(e13, e9, fl), level=NEED_XOR)
+        a3 = self._xor_pair(x1, x2, fl)
+        if not final_renorm:
+            return a3
+        return self._renorm_pair(*a3, level=NEED_BOOTSTRAP if do_final_bootstrap else None)
+
     def __call__(self, ct_hi, ct_lo, do_final_bootstrap: bool = True, debug: Dict[str, Any] | None = None,
                  final_renorm: bool = True):
         """final_renorm=False returns the last XOR pair before its renorm (and without the final
@@ -130,6 +145,8 @@ class InvMixColumnsFHE:
         rot = {k: (rh[k - 1], rl[k - 1]) for k in (1, 2, 3)}
         for k in (1, 2, 3):
             log(f"rotc{k}", rot[k])
+        if debug is None and self.enc.renorm_hook is not None and getattr(self.enc, "renorm_quad_hook", None) is not None:
+            return self._call_fhe_quad(ct_hi, ct_lo, rot, do_final_bootstrap, final_renorm)
         # independent GF multiplier pairs two at a time on the branch streams
         e14, e11 = pair(self.ctx, lambda: self.gf_mult_14(ct_hi, ct_lo), lambda: self.gf_mult_11(*rot[1]))
         log("mul14", e14)

@@ -41,7 +41,7 @@ EXPORTED = [
     "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_level_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
     "aesfhe_streams", "aesfhe_bind_stream", "aesfhe_fork", "aesfhe_join", "aesfhe_settle",
     "aesfhe_profile", "aesfhe_profile_every", "aesfhe_kernel_stats", "aesfhe_kernel_work", "aesfhe_kernel_gaps", "aesfhe_pool_stats", "aesfhe_bootstrap_depth", "aesfhe_debug_bootplan", "aesfhe_debug_sparseplan",
-    "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot", "aesfhe_create_keyed", "aesfhe_bootstrap_sparse", "aesfhe_bootstrap_pair_sparse", "aesfhe_renorm_periodic",
+    "aesfhe_debug_boot_stage", "aesfhe_export_sparse", "aesfhe_boot_info", "aesfhe_create_boot", "aesfhe_create_keyed", "aesfhe_bootstrap_sparse", "aesfhe_bootstrap_pair_sparse", "aesfhe_bootstrap_quad_sparse", "aesfhe_renorm_periodic",
     "aesfhe_renorm_single", "aesfhe_renorm_unpack",
     "aesfhe_level_limbs", "aesfhe_debug_lin_group", "aesfhe_debug_lin_group_plain", "aesfhe_lut_create", "aesfhe_lut_eval", "aesfhe_lut_free",
     "aesfhe_bootstrap_scaled", "aesfhe_bootstrap_pair_scaled", "aesfhe_set_enc_nonce", "aesfhe_launch_count", "aesfhe_launch_census",
@@ -133,6 +133,7 @@ def load_library(path: Optional[Path] = None):
     sig["aesfhe_renorm_unpack"] = [vp, _H, c_int, c_int, _Hp, _Hp]
     sig["aesfhe_bootstrap_sparse"] = [vp, _H, c_int, c_dbl, _Hp]
     sig["aesfhe_bootstrap_pair_sparse"] = [vp, _H, _H, c_int, c_dbl, _Hp, _Hp]
+    sig["aesfhe_bootstrap_quad_sparse"] = [vp, _Hp, c_int, c_dbl, _Hp]
     sig["aesfhe_create_keyed"] = [pp, c_int, c_int, c_int, c_int, ctypes.c_char_p, c_int]
     sig["aesfhe_lut_create"] = [vp, c_int, c_int, _dp, _dp, c_dbl, c_dbl, _Hp]
     sig["aesfhe_lut_eval"] = [vp, _H, _Hp, _Hp, _Hp]
@@ -789,6 +790,16 @@ class Engine:
                                                                ctypes.byref(x), ctypes.byref(y)))
         return Ciphertext(self._ctx, x.value), Ciphertext(self._ctx, y.value)
 
+    def bootstrap_quad_sparse(self, cts, period: int, gain: float = 1.0):
+        """four `period`-periodic ciphertexts refreshed by one bootstrap at period 4 * period
+        (aesfhe_bootstrap_quad_sparse), gain * each"""
+        cts = list(cts)
+        if len(cts) != 4:
+            raise ValueError("bootstrap_quad_sparse takes four ciphertexts")
+        H = ctypes.c_uint64 * 4
+        inp, out = H(*[c.handle for c in cts]), H()
+        self._ctx.check(self._lib.aesfhe_bootstrap_quad_sparse(self._ctx.ptr, inp, int(period), float(gain), out))
+        return [Ciphertext(self._ctx, out[m]) for m in range(4)]
     def debug_boot_stage(self, ct, stage: int):
         return self._new(self._lib.aesfhe_debug_boot_stage, ct.handle, int(stage))
 

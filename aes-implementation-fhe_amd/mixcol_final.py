@@ -393,9 +393,26 @@ class MixColFinal:
         log("two", two)
         log("thr", thr)
         last = NEED_BOOTSTRAP if do_final_bootstrap else None  # bootstrapped next (from level 0), else fresh
+        quad = fhe and getattr(self.enc, "renorm_quad_hook", None) is not None
+        if quad:
+            # true-FHE with the quad bootstrap (zeta16_noise_reducer.BootstrapSnap.apply_quad): the GF
+            # outputs renormalised together (one bootstrap for both pairs), then the tree
+            # (2x ^ 3r1) ^ (r2 ^ r3): its two first XOR pairs renormalised together again, so a
+            # round's MixColumns takes two quad bootstraps and one pair bootstrap instead of five
+            # pair bootstraps.  Every XOR4 still meets two freshly snapped inputs (r2 / r3 come
+            # straight from SubBytes' renorm)
+            two, thr = self.enc.renorm_two(two, thr, level=NEED_XOR)
+            a1 = self._xor_pair(two, thr, fl)
+            log("acc1", a1)
+            b1 = self._xor_pair(rot[2], rot[3], fl)
+            log("r23", b1)
+            x1, x2 = self.enc.renorm_two(a1, b1, level=NEED_XOR)
+            acc = self._renorm_pair(*self._xor_pair(x1, x2, fl), level=last)
+            log("acc3", acc)
+            return acc
         if fhe:
             # true-FHE: the GF multipliers amplify their inputs' errors up to ~20x, so their outputs
-            # are renormalised (bootstrap + two snaps) before the first XOR; then the reference's
+            # are renormalised (bootstrap + snap) before the first XOR; then the reference's
             # chain, each of r2 / r3 meeting a freshly snapped partner (zeta16_noise_reducer.py)
             two, thr = pair(self.ctx, lambda: self._renorm_pair(*two, level=NEED_XOR),
                             lambda: self._renorm_pair(*thr, level=NEED_XOR), fork=_FHE_FORK)

@@ -59,6 +59,9 @@ from xor4_lut import XOR4LUT
 
 # AESFHE_KEY_BASIS=0: the packed round keys' XOR4 bases rebuilt in every AddRoundKey (A/B runs)
 _KEY_BASIS = os.environ.get("AESFHE_KEY_BASIS", "1") != "0"
+# AESFHE_FHE_SB_NIB=0: true-FHE mode keeps the reference's 8 -> 4 (Inv)SubBytes (depth 13, double snaps)
+# instead of the nibble-bivariate form (A/B runs)
+_FHE_NIB = os.environ.get("AESFHE_FHE_SB_NIB", "1") != "0"
 
 
 class AESPipeline:
@@ -103,13 +106,6 @@ class AESPipeline:
                 raise ValueError("mixcolumns / inv_mixcolumns were built for a different slot layout")
         self.ark = AddRoundKey(self.xor4)
         self.snapper = None
-        if true_fhe:
-            from zeta16_noise_reducer import BootstrapSnap
-            self.snapper = BootstrapSnap(ctx, period=self.layout.boot_period)
-            for enc in (self.encoder, getattr(self.mix, "enc", None), getattr(self.invmix, "enc", None)):
-                if enc is not None:
-                    enc.renorm_hook = self.snapper.apply_pair
-
         self.use_hard_renorm_between_steps = use_hard_renorm_between_steps
         self.with_inv_mix_columns = with_inv_mix_columns
         self._rk_cache: List[Tuple[Any, Any]] | None = None
@@ -145,7 +141,17 @@ class AESPipeline:
         # secret-key renorm mode: its inputs come from a renorm, so they are handed out 9 levels lower
         for lut in (self.sub, self.isub):
             if lut is not None and not fuse_sub_ark:
-                lut.use_nibble = bool(use_hard_renorm_between_steps and not true_fhe)
+                lut.use_nibble = bool(use_hard_renorm_between_steps and not true_fhe or true_fhe and _FHE_NIB)
+        if true_fhe:
+            from zeta16_noise_reducer import BootstrapSnap
+            # one snap per renorm with the nibble-bivariate (Inv)SubBytes, two where the reference's
+            # 8 -> 4 form's ~3e-2 output errors need them (zeta16_noise_reducer.BootstrapSnap)
+            self.snapper = BootstrapSnap(ctx, period=self.layout.boot_period, max_snaps=1 if self.sub.nibble_on() else 2)
+            quad = self.snapper.apply_quad if self.snapper.quad_ok() else None
+            for enc in (self.encoder, getattr(self.mix, "enc", None), getattr(self.invmix, "enc", None)):
+                if enc is not None:
+                    enc.renorm_hook = self.snapper.apply_pair
+                    enc.renorm_quad_hook = quad
         if self.sub.nibble_on():
             self.need_sub = RENORM_FLOOR + self.sub.need_depth()
         elif (use_hard_renorm_between_steps and not true_fhe and fresh is not None and getattr(ctx, "fused_luts", False)

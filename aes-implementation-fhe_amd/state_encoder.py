@@ -128,6 +128,7 @@ class StateEncoder:
         # set by AESPipeline(true_fhe=True): renorm(hi, lo) -> hook(hi, lo), the bootstrap + snap
         # that replaces the secret-key renorm (zeta16_noise_reducer.BootstrapSnap)
         self.renorm_hook = None
+        self.renorm_quad_hook = None  # true-FHE: two pairs per bootstrap (renorm_two)
 
     def _as_batch(self, state: np.ndarray) -> np.ndarray:
         state = np.asarray(state, dtype=np.uint8)
@@ -364,6 +365,18 @@ class StateEncoder:
         if self.renorm_hook is None:
             tally_renorm(self.ctx, ct_hi, ct_lo)
         return tag_layout(self.layout, *self._renorm(ct_hi, ct_lo, level))
+
+    def renorm_two(self, p, q, level=None):
+        """renorm of two (hi, lo) pairs at one point of a step: in true-FHE mode with a quad hook
+        (zeta16_noise_reducer.BootstrapSnap.apply_quad) ONE bootstrap refreshes all four
+        ciphertexts; otherwise two renorm calls"""
+        if self.renorm_quad_hook is not None:
+            ps, qs = self._fold_conj(*p), self._fold_conj(*q)
+            if not any(isinstance(c, ConjSum) for c in ps + qs):
+                check_layout(self.layout, *ps, *qs)
+                a, b = self.renorm_quad_hook(ps, qs, level)
+                return tag_layout(self.layout, *a), tag_layout(self.layout, *b)
+        return self.renorm(*p, level), self.renorm(*q, level)
 
     def _renorm(self, ct_hi, ct_lo, level):
         if self.renorm_hook is not None:

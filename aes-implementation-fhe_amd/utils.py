@@ -207,6 +207,21 @@ def stacked_pair(ctx, f, a, b):
     return pair(ctx, lambda: f(a), lambda: f(b), shared=(a, b))
 
 
+def stacked_many(ctx, f, cts):
+    """[f(c) for c in cts] as ONE stacked evaluation (stacked_pair's rule for more members),
+    else pairwise"""
+    cts = list(cts)
+    E = getattr(ctx, "engine", ctx)
+    if _STACK_HALVES and not can_fork(ctx) and getattr(E, "stack", None) is not None:
+        return list(E.unstack(f(E.stack(cts))))
+    out = []
+    for i in range(0, len(cts) - 1, 2):
+        out.extend(stacked_pair(ctx, f, cts[i], cts[i + 1]))
+    if len(cts) % 2:
+        out.append(f(cts[-1]))
+    return out
+
+
 def can_fork(ctx) -> bool:
     """two independent halves would run on two streams (utils.pair): then each half batches
     its own products; otherwise both halves' products go into shared batches"""

@@ -36,14 +36,19 @@ profiles/r2_true_fhe.json).
 """
 from __future__ import annotations
 
+import os
 from typing import Any, Tuple
 
-from utils import NEED_SR_ARK, pair, stacked_pair
+from utils import NEED_SR_ARK, NEED_XOR, pair, stacked_many, stacked_pair
 from xor4_lut import powers
 
 SNAP15_DEPTH = 4
 DOUBLE_SNAP_MAX_LEVEL = NEED_SR_ARK  # renorms whose consumer needs at most this many levels snap twice
 KAPPA = 16.0 ** (-1.0 / 15.0)  # bootstrap gain: conj(u)^15 carries coefficient 1
+# AESFHE_FHE_SNAPS=1 / 2: at most that many snaps per renorm (default: the pipeline's choice, max_snaps)
+_ENV_SNAPS = os.environ.get("AESFHE_FHE_SNAPS")
+# AESFHE_FHE_QUAD=0: two pair bootstraps instead of one quad bootstrap for renorm_two (A/B runs)
+_QUAD = os.environ.get("AESFHE_FHE_QUAD", "1") != "0"
 
 
 class Zeta16NoiseReducer:
@@ -107,29 +112,55 @@ class Zeta16Snap15:
 
 
 class BootstrapSnap:
-    """True-FHE renorm of a (hi, lo) pair: scaled bootstrap, then the depth-4 snap."""
+    """True-FHE renorm of a (hi, lo) pair: scaled bootstrap, then the depth-4 snap.
 
-    def __init__(self, ctx, snap: Zeta16Snap15 | None = None, period: int | None = None):
+    max_snaps: 2 (round 2's rule for the reference's 8 -> 4 SubBytes, whose outputs carry ~3e-2
+    errors): a second snap when the consumer needs <= DOUBLE_SNAP_MAX_LEVEL levels; 1 (the
+    pipeline's choice with the nibble-bivariate SubBytes, whose outputs stay ~1e-3 off their
+    codewords): one snap everywhere, so the fresh level only needs snap + 8 levels."""
+
+    def __init__(self, ctx, snap: Zeta16Snap15 | None = None, period: int | None = None, max_snaps: int = 2):
         if getattr(ctx, "bootstrap_pair_scaled", None) is None:
             raise RuntimeError("true-FHE renorm needs the engine's scaled pair bootstrap (bootstrappable context)")
         self.ctx = ctx
         self.snap = snap or Zeta16Snap15(ctx)
         self.period = period  # the states' slot period (periodic layout): sparse-slot bootstraps
+        self.max_snaps = int(_ENV_SNAPS) if _ENV_SNAPS else max_snaps
+
+    def _twice(self, level) -> bool:
+        """a second snap: consumer needs <= DOUBLE_SNAP_MAX_LEVEL (None / 0: the output or a bootstrap
+        -- an XOR4 follows in true-FHE mode) and the fresh level leaves it room"""
+        need = level if level else NEED_XOR
+        return (self.max_snaps > 1 and need <= DOUBLE_SNAP_MAX_LEVEL
+                and self.ctx.engine.fresh_level - 2 * SNAP15_DEPTH - 1 >= need)
+
+    def _snap_fn(self, level):
+        sn = self.snap
+        return (lambda u: sn.apply(sn.apply_scaled(u))) if self._twice(level) else sn.apply_scaled
 
     def apply_pair(self, ct_hi, ct_lo, level=None) -> Tuple[Any, Any]:
-        """level: what the next step needs (the pipeline's renorm hint); None or <= 8 (an XOR4,
-        ShiftRows + XOR4, or the output) -> two snaps when the fresh level leaves room"""
+        """level: what the next step needs (the pipeline's renorm hint)"""
         ctx = self.ctx
-        fresh = ctx.engine.fresh_level
-        twice = (level is None or level <= DOUBLE_SNAP_MAX_LEVEL) and fresh - 2 * SNAP15_DEPTH - 1 >= (level or 0)
         if self.period is not None:
             uh, ul = ctx.bootstrap_pair_scaled(ctx.to_intt(ct_hi), ctx.to_intt(ct_lo), self.snap.kappa, self.period)
         else:
             uh, ul = ctx.bootstrap_pair_scaled(ctx.to_intt(ct_hi), ctx.to_intt(ct_lo), self.snap.kappa)
-        sn = self.snap
         # the same snap on both halves: one stacked evaluation (utils.stacked_pair)
-        if twice:
-            return stacked_pair(ctx, lambda u: sn.apply(sn.apply_scaled(u)), uh, ul)
-        return stacked_pair(ctx, sn.apply_scaled, uh, ul)
+        return stacked_pair(ctx, self._snap_fn(level), uh, ul)
 
     __call__ = apply_pair
+
+    def quad_ok(self) -> bool:
+        ctx = self.ctx
+        return bool(_QUAD and self.period is not None and getattr(ctx, "bootstrap_quad_scaled", None) is not None
+                    and 4 * self.period <= ctx.engine.slot_count)
+
+    def apply_quad(self, p, q, level=None):
+        """two (hi, lo) pairs renormalised at one point of a step: ONE bootstrap at four times the
+        period (EngineContext.bootstrap_quad_scaled) and one snap stacked over the four"""
+        if not self.quad_ok():
+            return self.apply_pair(*p, level), self.apply_pair(*q, level)
+        ctx = self.ctx
+        u = ctx.bootstrap_quad_scaled([ctx.to_intt(c) for c in (*p, *q)], self.snap.kappa, self.period)
+        out = stacked_many(ctx, self._snap_fn(level), u)
+        return (out[0], out[1]), (out[2], out[3])

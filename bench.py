@@ -99,9 +99,13 @@ def parse():
                                                          "room under the 128-bit bound; the engine's default set uses 5)")
     ap.add_argument("--folded-steps", type=int, default=5,
                     help="timed steps of the 'folded' leg: C2 with the renorm folds on (utils.RenormFolds; the headline is strict)")
-    ap.add_argument("--true-fhe-steps", type=int, default=1,
+    ap.add_argument("--true-fhe-steps", type=int, default=2,
                     help="SURVEY.md 8(f)3 line beside the headline: C2 encrypts with every secret-key renorm replaced "
                          "by bootstrap + homomorphic Zeta16 snap (AESPipeline(true_fhe=True)); 0 = skip")
+    ap.add_argument("--fhe-fresh-level", type=int, default=12,
+                    help="fresh level of the true-FHE leg's context: one depth-4 snap + the 8 levels of the deepest step "
+                         "between renorms (ShiftRows -> GF multipliers / XOR4s, nibble-bivariate SubBytes), DESIGN.md 8")
+    ap.add_argument("--fhe-dnum", type=int, default=4, help="key-switching digits of the true-FHE leg's context")
     ap.add_argument("--no-batch-roundtrip", dest="batch_roundtrip", action="store_false",
                     help="skip the decrypt leg of the batch (BASELINE config 5)")
     ap.add_argument("--whole-stats", default=None,
@@ -626,21 +630,35 @@ def full_levels(ctx):
     return _CTX17["ctx"]
 
 
+def fhe_context(ctx, fresh: int, dnum: int):
+    """ctx itself when it has the bootstrappable set (fresh, dnum), else ONE extra context with it (same
+    seed, its own keys), made once: the true-FHE leg's set (--fhe-fresh-level / --fhe-dnum)"""
+    E = ctx.engine
+    if E.fresh_level == fresh and E.dnum == dnum:
+        return ctx
+    key = ("fhe", fresh, dnum)
+    if key not in _CTX17:
+        from engine_context import EngineContext
+        _CTX17[key] = EngineContext(signature=1, boot_fresh_level=fresh, dnum=dnum, thread_count=1, device_id=E.device_id,
+                                    seed=E.seed, lazy=E.lazy)
+    return _CTX17[key]
+
+
 def run_true_fhe(ctx, coeffs, rks, args, rank, world, dist, tj: dict) -> dict:
     """the C2 workload with no secret key between encryption and decryption --
     every renorm point is a bootstrap + homomorphic Zeta16 snap (zeta16_noise_reducer.py), XOR4
     normalised by 1/256.  One state per rank per step, checked after the timed region."""
     from oracle import aes_plain  # checker only, after the timed region
     from pipeline import AESPipeline
-    # the true-FHE snaps need SubBytes' 8 -> 4 form's 13 levels after a bootstrap: the engine's default set
-    ctx = full_levels(ctx)
+    # one snap + the deepest step between renorms (8 levels): the --fhe-fresh-level set (12 / 4)
+    ctx = fhe_context(ctx, args.fhe_fresh_level, args.fhe_dnum)
     pipe = AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=False, true_fhe=True)
     sts = rank_states(rank + 1000, 1 + args.true_fhe_steps)
     pipe.encrypt(sts[0], rks)  # warmup: snap constants, normalised XOR4 coefficient sets
     ctx.engine.sync()
     leg = Leg(ctx.engine).start()
     barrier(dist)
-    n0 = ctx.bootstrap_stats()["count"]
+    b0 = ctx.bootstrap_stats()
     t0 = time.perf_counter()
     outs = [pipe.encrypt(s, rks) for s in sts[1:]]
     ctx.engine.sync()
@@ -648,14 +666,20 @@ def run_true_fhe(ctx, coeffs, rks, args, rank, world, dist, tj: dict) -> dict:
     elapsed = time.perf_counter() - t0
     leg.stop()
     elapsed = max_over_ranks(dist, elapsed)
-    nboot = (ctx.bootstrap_stats()["count"] - n0) / args.true_fhe_steps
+    b1 = ctx.bootstrap_stats()
+    nboot = (b1["count"] - b0["count"]) / args.true_fhe_steps
+    ncalls = (b1["calls"] - b0["calls"]) / args.true_fhe_steps
     ok = all(np.array_equal(pipe.encoder.decode(*o), aes_plain.ref_encrypt(s, rks)) for s, o in zip(sts[1:], outs))
     ok = all(r[0] for r in all_gather_ints(dist, [int(ok)]))
     done = args.true_fhe_steps * world
+    snaps = pipe.snapper.max_snaps
     return {"workload": "C2 in true-FHE mode: every secret-key renorm replaced by bootstrap + depth-4 Zeta16 snap "
-                        "(two snaps where the next step is an XOR4); no secret key between encryption and decryption",
+                        + ("(one snap per renorm, nibble-bivariate SubBytes" if snaps == 1 else "(two snaps where the next step is an XOR4")
+                        + "; MixColumns' paired renorms share one quad bootstrap); no secret key between encryption and decryption",
+            "params": {"fresh_level": ctx.engine.fresh_level, "dnum": ctx.engine.dnum, "log2_pq": round(ctx.engine.log_pq, 1),
+                       "max_snaps": snaps},
             "rounds_per_s": 10.0 * done / elapsed, "ms_per_step": elapsed / args.true_fhe_steps * 1e3,
-            "bootstraps_per_encrypt": nboot, "steps": args.true_fhe_steps, "verified_against_plaintext_model": bool(ok),
+            "bootstraps_per_encrypt": nboot, "bootstrap_calls_per_encrypt": ncalls, "steps": args.true_fhe_steps, "verified_against_plaintext_model": bool(ok),
             "roofline_step": leg.step(elapsed, args.true_fhe_steps, tj, args.profile_every),
             "precision": measure_precision(pipe, ctx, rks, sts[0], "one state, true-FHE") if rank == 0 else None}
 

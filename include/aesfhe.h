@@ -265,6 +265,13 @@ int aesfhe_bootstrap_pair_sparse(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle
                                  aesfhe_handle* out_b);
 int aesfhe_bootstrap_pair_scaled(aesfhe_ctx* ctx, aesfhe_handle a, aesfhe_handle b, double gain, aesfhe_handle* out_a,
                                  aesfhe_handle* out_b);
+/* four n-periodic ciphertexts (4 period <= slots) refreshed by ONE bootstrap at period 4n: the pairs
+ * (in[0], in[1]) and (in[2], in[3]) monomial-packed as in aesfhe_bootstrap_pair_sparse, the two packs
+ * packed once more (X^(N/8n)), split back by rotations by 2n then n slots.  out[m] = gain * in[m]
+ * refreshed (the true-FHE MixColumns renorms of two ciphertext pairs at one point of a round;
+ * replaces two aesfhe_bootstrap_pair_sparse calls, REF/zeta16_noise_reducter.py:108-169 /
+ * REF/mixcol_final.py:104-106's renorm points). */
+int aesfhe_bootstrap_quad_sparse(aesfhe_ctx* ctx, const aesfhe_handle* in, int period, double gain, aesfhe_handle* out);
 int aesfhe_bootstrap_depth(void);
 /* host self-check of the bootstrap plan: err[0] SlotToCoeff, err[1] CoeffToSlot vs the
  * canonical embedding, err[2] EvalMod Chebyshev error (no GPU needed) */

@@ -114,6 +114,54 @@ def test_true_fhe_config2_encrypt_decrypt(ctx, coeff_dir, monkeypatch):
     assert n_enc == 2 * (1 + 9 * 7 + 2), n_enc
 
 
+def test_quad_bootstrap_matches_pair_bootstraps(ctx):
+    """aesfhe_bootstrap_quad_sparse: four 16-periodic messages through ONE bootstrap at period 64 (two
+    monomial packings, three split rotations) come back as the pair bootstraps return them: each
+    within the bootstrap error of its input, at the same level"""
+    from test_gpu_bootstrap import BOOT_TOL
+    E = ctx.engine
+    S, P = E.slot_count, 16
+    rng = np.random.default_rng(61)
+    zs = [np.tile(np.exp(2j * np.pi * rng.random(P)), S // P) for _ in range(4)]
+    cts = [ctx.to_intt(ctx.encrypt(z)) for z in zs]
+    quad = ctx.bootstrap_quad_scaled(cts, 1.0, P)
+    pairs = ctx.bootstrap_pair_scaled(cts[0], cts[1], 1.0, P) + ctx.bootstrap_pair_scaled(cts[2], cts[3], 1.0, P)
+    for z, q, p in zip(zs, quad, pairs):
+        assert q.level == p.level
+        assert np.abs(ctx.decrypt(q) - z).max() < 2 * BOOT_TOL
+        assert np.abs(ctx.decrypt(q) - ctx.decrypt(p)).max() < 3 * BOOT_TOL
+    with pytest.raises(ValueError):
+        ctx.engine.bootstrap_quad_sparse(cts[:3], P)
+
+
+def test_true_fhe_c2_on_the_bench_set(coeff_dir, monkeypatch):
+    """the bench's true-FHE set (bench.py --fhe-fresh-level 12 --fhe-dnum 4): one snap per renorm with
+    the nibble-bivariate SubBytes, MixColumns' paired renorms in quad bootstraps; encrypt and decrypt
+    are FIPS-197's bytes with no secret-key call, 1 + 9 * 5 + 2 bootstrap calls per encrypt for the
+    same 132 refreshed ciphertexts"""
+    from aes_keyschedule import expand_aes128_key, load_all_coeffs
+    from engine_context import EngineContext
+    from oracle import aes_plain as A
+    from pipeline import AESPipeline
+    c12 = EngineContext(signature=1, boot_fresh_level=12, dnum=4, thread_count=4, seed=0xF12, enc_nonce=0xF12)
+    pipe = AESPipeline(c12, load_all_coeffs(coeff_dir), use_hard_renorm_between_steps=False, true_fhe=True)
+    assert pipe.snapper.max_snaps == 1 and pipe.encoder.renorm_quad_hook is not None
+    rng = np.random.default_rng(12)
+    rks = expand_aes128_key(rng.integers(0, 256, 16).astype(np.uint8))
+    for _ in range(2):
+        pt = rng.integers(0, 256, 16).astype(np.uint8)
+        _no_secret_renorm(c12, monkeypatch)
+        b0 = c12.bootstrap_stats()
+        ct = pipe.encrypt(pt, rks)
+        b1 = c12.bootstrap_stats()
+        back = pipe.decrypt(*ct, rks)
+        monkeypatch.undo()
+        assert np.array_equal(pipe.encoder.decode(*ct), A.ref_encrypt(pt, rks))
+        assert np.array_equal(pipe.encoder.decode(*back), pt)
+        assert b1["count"] - b0["count"] == 2 * (1 + 9 * 7 + 2)
+        assert b1["calls"] - b0["calls"] == 1 + 9 * 5 + 2
+
+
 def test_true_fhe_packed_encrypt(ctx, coeff_dir, monkeypatch):
     """256 slot-packed states (8,192 nibble slots per step through every snap), encrypt and
     decrypt: the error tails of a batch, not just one state"""

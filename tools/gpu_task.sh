@@ -15,6 +15,7 @@
 #   twogpu                  torchrun --nproc-per-node=2 bench.py --gpus 2 over gloo on ONE MI355X (both ranks
 #                           share it): the N > 1 engine path at the C4 / C5 per-rank shapes
 #   boot                    tools/boot_phases.py 32 (sparse bootstrap phases)
+#   fhe                     tools/fhe_profile.py (true-FHE encrypt by step); FHE_ENV="A=1 B=0" runs it per setting
 #   census                  tools/launch_census.py (launches / ms per AES step)
 #   opcensus                tools/op_kernel_census.py (launches of one encrypt by C-ABI entry and kernel)
 #   stack                   tools/step_profile.py on the 64-pair stacked leg (STACK_ARGS)
@@ -91,6 +92,11 @@ for t in "$@"; do
           --pair-states 0 --packed-pairs 0 --true-fhe-steps 0 --eager-steps 0 --deferred-steps 0 > $O/bench_rccl_1rank.json 2> $O/rccl1.err ;;
     boot)
       timeout -k 10 300 python3 tools/boot_phases.py 32 ${BOOT_SET:-9 4} > $O/boot_phases.json 2> $O/boot.err ;;
+    fhe)
+      for e in ${FHE_ENV:-AESFHE_NONE=0}; do
+        env $e timeout -k 10 300 python3 tools/fhe_profile.py ${FHE_ARGS:-2} > $O/fhe_profile_$e.json 2> $O/fhe_$e.err
+        cat $O/fhe_profile_$e.json
+      done ;;
     census)
       timeout -k 10 300 python3 tools/launch_census.py > $O/launch_census.json 2> $O/census.err ;;
     opcensus)
