@@ -3926,14 +3926,12 @@ public:
         for (size_t j = 0; j < ks.size(); ++j) ch.x[j] = T[ks[j]].data, ch.nx[j] = hp_.nl(T[ks[j]].level);
         const int nb = T[ks[0]].nb;
         Ct o = alloc_ct(l, 2 * nb, nb);
-        launch_lut_univariate(S(), T_, o.data, nullptr, ch, (int)ks.size(), it->second, 2 * nb, nl);
+        // c_0 added in the same launch (the add_scalar lincomb's constants at the sum's level and owed rescale)
+        LimbConsts cadd{};
+        if (c[0] != 0.0) cadd = add_consts(l, 1, c[0], 0.0);
+        launch_lut_univariate(S(), T_, o.data, nullptr, ch, (int)ks.size(), it->second, 2, nl, nb, c[0] != 0.0 ? &cadd : nullptr);
         o.pend = 1;
         o.lazy = true;
-        if (c[0] != 0.0) {
-            Ct r = add_scalar(o, c[0], 0.0);
-            release(o);
-            o = r;
-        }
         out = normalize(o, true);
         if (out.data != o.data) release(o);
         return true;
@@ -4103,7 +4101,7 @@ public:
         const auto& c = bs_.plan.cheb;
         const int d = (int)c.size() - 1, ni = (int)ys.size();
         std::vector<std::vector<Ct>> T(ni, std::vector<Ct>(kBabyDeg + 1));
-        for (int i = 0; i < ni; ++i) T[i][1] = copy(*ys[i]);
+        for (int i = 0; i < ni; ++i) T[i][1] = *ys[i];  // read only (the caller owns it): no copy, not released below
         static const bool batch_baby = env_int("AESFHE_EVALMOD_BATCH", 1) != 0;
         for (int lo = 2; lo <= kBabyDeg;) {
             const int hi = batch_baby ? std::min(kBabyDeg, 2 * lo - 2) : lo;
@@ -4148,7 +4146,7 @@ public:
         const std::vector<std::vector<double>> cs(ni, c);
         std::vector<Ct> g = cheb_sched_ ? cheb_eval_sched(T, giant, in, cs) : cheb_eval_many(T, giant, in, cs);
         for (int i = 0; i < ni; ++i) {
-            for (int k = 1; k <= kBabyDeg; ++k) release(T[i][k]);
+            for (int k = 2; k <= kBabyDeg; ++k) release(T[i][k]);
             for (auto& kv : giant[i])
                 if (kv.first != kBabyDeg) release(kv.second);
         }

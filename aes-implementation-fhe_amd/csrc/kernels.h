@@ -562,5 +562,5 @@ struct LutChunk {
     int nx[kLutChunk];
 };
 void launch_lut_univariate(hipStream_t st, const DevTables& T, u32* out, const u32* acc, const LutChunk& ch, int n, const u32* cst,
-                           int npoly, int nl, int members = 1);
+                           int npoly, int nl, int members = 1, const LimbConsts* cadd = nullptr);
 

@@ -1366,8 +1366,10 @@ __global__ void __launch_bounds__(kBlock) k_lut_bivariate(u32* out, LutOperands 
 // grid z = member of stacked elements (element j of member m at x[j] + m npoly nx[j] N, out / acc
 // at + m npoly nl N)
 // (k_lut_bivariate's uniform coefficient half and unrolled term loop)
+// has_c: cadd's constant added to every member's first polynomial after the reduction (as k_lincomb's
+// add_scalar launch would: the EvalMod Chebyshev leaves' c_0)
 __global__ void __launch_bounds__(kBlock) k_lut_univariate(u32* out, const u32* acc, LutChunk ch, int n, const u32* __restrict__ cst,
-                                                           int npoly, int nl, const PrimeConst* pc, int logn) {
+                                                           int npoly, int nl, const PrimeConst* pc, int logn, LimbConsts cadd, int has_c) {
     const int t = blockIdx.y, mb = blockIdx.z;
     const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const int half = (int)(((size_t)blockIdx.x * kBlock) >> (logn - 1));
@@ -1385,7 +1387,9 @@ __global__ void __launch_bounds__(kBlock) k_lut_univariate(u32* out, const u32* 
             const u32* xj = ch.x[j] + (size_t)mb * npoly * ((size_t)ch.nx[j] << logn);
             v += (u64)xj[((size_t)(p * ch.nx[j]) << logn) + off] * c;
         }
-        out[o] = reduce64(v, q, P.mu, P.r32);
+        u32 r = reduce64(v, q, P.mu, P.r32);
+        if (has_c && p == 0) r = add_mod(r, cadd.v[2 * t + half], q);
+        out[o] = r;
     }
 }
 
@@ -2008,8 +2012,10 @@ void launch_lut_bivariate(hipStream_t st, const DevTables& T, u32* out, const Lu
                 dim3((1u << T.logn) / kBlock, nl, members), dim3(kBlock), 0, st, out, op, n_a, cst, nl, T.pc, T.logn);
 }
 void launch_lut_univariate(hipStream_t st, const DevTables& T, u32* out, const u32* acc, const LutChunk& ch, int n, const u32* cst,
-                           int npoly, int nl, int members) {
+                           int npoly, int nl, int members, const LimbConsts* cadd) {
+    static const LimbConsts kNoC{};
     prof_launch(KID_ELEMENTWISE, words((double)(n + (acc ? 2 : 1)) * npoly * nl * members * (1u << T.logn)), k_lut_univariate,
-                dim3((1u << T.logn) / kBlock, nl, members), dim3(kBlock), 0, st, out, acc, ch, n, cst, npoly, nl, T.pc, T.logn);
+                dim3((1u << T.logn) / kBlock, nl, members), dim3(kBlock), 0, st, out, acc, ch, n, cst, npoly, nl, T.pc, T.logn,
+                cadd ? *cadd : kNoC, cadd ? 1 : 0);
 }
 
