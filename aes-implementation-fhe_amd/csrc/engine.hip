@@ -4206,6 +4206,7 @@ public:
             Ct c = normalize(in);
             Ct z = level_down(c, 0);
             if (c.data != in.data) release(c);
+            if (period > 0 && stack_pack_ > 1 && in.nb % 2 == 0 && 2 * period <= slot_count()) return boot_stack_packed(z, gain, period);
             return boot_stack(z, gain, sv);
         }
         Ct c = normalize(in);
@@ -4333,6 +4334,52 @@ public:
         }
         cnt_[C_BOOT] += 3 * z_members_;  // four messages per packed quad
         for (int m = 0; m < 4; ++m) *out[m] = put_ct(o[m]);
+    }
+    // a stack of M period-P members bootstrapped G members per bootstrap:
+    // the monomial pair packing applied log2 G times over the stack's halves -- members [0, m/2)
+    // + X^(N/4p) members [m/2, m), exact, one launch per level -- so M / G members of period P G
+    // go through boot_stack with gain / G, then log2 G mono_split levels (one batched rotation of
+    // the stack each) unpack them in the original member order.  G: the largest power of two
+    // <= stack_pack_ dividing M with P G <= slots.  The members' bootstrap errors grow ~G x (the
+    // packed message is G x smaller against the same bootstrap error); stack_pack_ = 1: off
+    // (16: C3 stacks of 64 pairs 78 -> 50 ms per pair, precision margin 121x; profiles/r6_stack_pack_ab.txt)
+    int stack_pack_ = env_int("AESFHE_STACK_PACK", 16);
+    Ct boot_stack_packed(Ct z, double gain, int period) {
+        const int M = z.nb, n = hp_.n, nl0 = hp_.nl(0), per = pm(z);
+        int G = 1;
+        while (2 * G <= stack_pack_ && M % (2 * G) == 0 && 2 * G * period <= slot_count()) G *= 2;
+        Ct cur = z;
+        int p = period, m = M;
+        for (int g = 1; g < G; g *= 2, p *= 2, m /= 2) {
+            const int h = m / 2;
+            Ct nz = alloc_ct(0, per * h, h);
+            copy_meta(nz, cur);
+            nz.nb = h;
+            launch_fma_poly(S(), T_, nz.data, cur.data, cur.data + (size_t)h * per * nl0 * n, monomial(n / (4 * p)), per * h * nl0, nl0,
+                            qmap());
+            release(cur);
+            cur = nz;
+        }
+        SparseBoot* sv = p < slot_count() ? &sparse_variant(p) : nullptr;
+        Ct out = boot_stack(cur, gain / G, sv);  // consumes cur
+        cnt_[C_BOOT] += M - M / G;               // boot_stack counted one per packed member
+        for (; m < M; m *= 2) {
+            p /= 2;
+            Ct hi, lo;
+            mono_split(out, p, hi, lo);
+            release(out);
+            const int nlo = hp_.nl(hi.level), ph = pm(hi);
+            Ct cat = alloc_ct(hi.level, ph * 2 * m, 2 * m);
+            copy_meta(cat, hi);
+            cat.nb = 2 * m;
+            const size_t half = (size_t)m * ph * nlo;
+            launch_copy_rows(S(), T_, cat.data, hi.data, half);
+            launch_copy_rows(S(), T_, cat.data + half * n, lo.data, half);
+            release(hi);
+            release(lo);
+            out = cat;
+        }
+        return out;
     }
     // NTT form of the monomial X^e (X^N = -1, e in [0, 2N)) on every Q limb: the product by
     // it is exact (coefficients shifted, the wrapped ones negated; no level, no noise)
@@ -5244,6 +5291,11 @@ int aesfhe_mul_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* a, const aesfhe
 }
 int aesfhe_renorm_pool(aesfhe_ctx* ctx, int size) {
     API_BEGIN ctx->eng->renorm_pool(size);
+    API_END
+}
+int aesfhe_set_stack_pack(aesfhe_ctx* ctx, int members) {
+    API_BEGIN if (members < 1) throw std::runtime_error("set_stack_pack: members >= 1");
+    ctx->eng->stack_pack_ = members;
     API_END
 }
 int aesfhe_mul_pt_sum(aesfhe_ctx* ctx, int n, const aesfhe_handle* cts, const aesfhe_handle* pts, aesfhe_handle* out) {

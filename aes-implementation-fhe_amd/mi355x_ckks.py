@@ -35,7 +35,7 @@ EXPORTED = [
     "aesfhe_level", "aesfhe_plaintext", "aesfhe_encrypt", "aesfhe_decrypt", "aesfhe_add", "aesfhe_sub",
     "aesfhe_add_pt", "aesfhe_add_scalar", "aesfhe_mul_scalar", "aesfhe_mul_pt", "aesfhe_mul",
     "aesfhe_relinearize", "aesfhe_rescale", "aesfhe_level_down", "aesfhe_rotate", "aesfhe_conjugate",
-    "aesfhe_mul_many", "aesfhe_mul_pt_sum", "aesfhe_renorm_pool", "aesfhe_conjugate_many", "aesfhe_rotate_hoisted",
+    "aesfhe_mul_many", "aesfhe_mul_pt_sum", "aesfhe_renorm_pool", "aesfhe_set_stack_pack", "aesfhe_conjugate_many", "aesfhe_rotate_hoisted",
     "aesfhe_power_basis", "aesfhe_to_ntt", "aesfhe_to_intt", "aesfhe_bootstrap", "aesfhe_bootstrap_pair", "aesfhe_renorm_pair", "aesfhe_renorm_states", "aesfhe_renorm_at",
     "aesfhe_export", "aesfhe_import", "aesfhe_export_secret", "aesfhe_export_pk", "aesfhe_export_ksk",
     "aesfhe_debug_ntt", "aesfhe_debug_keyswitch", "aesfhe_counters", "aesfhe_reset_counters", "aesfhe_level_counters", "aesfhe_bench_op", "aesfhe_set_lazy",
@@ -93,7 +93,7 @@ def load_library(path: Optional[Path] = None):
         "aesfhe_level_down": [vp, _H, c_int, _Hp], "aesfhe_rotate": [vp, _H, c_int, _Hp],
         "aesfhe_conjugate": [vp, _H, _Hp], "aesfhe_power_basis": [vp, _H, c_int, _Hp],
         "aesfhe_mul_many": [vp, c_int, _Hp, _Hp, _Hp], "aesfhe_conjugate_many": [vp, c_int, _Hp, _Hp],
-        "aesfhe_mul_pt_sum": [vp, c_int, _Hp, _Hp, _Hp], "aesfhe_renorm_pool": [vp, c_int],
+        "aesfhe_mul_pt_sum": [vp, c_int, _Hp, _Hp, _Hp], "aesfhe_renorm_pool": [vp, c_int], "aesfhe_set_stack_pack": [vp, c_int],
         "aesfhe_rotate_hoisted": [vp, _H, c_int, ctypes.POINTER(c_int), _Hp],
         "aesfhe_to_ntt": [vp, _H, _Hp], "aesfhe_to_intt": [vp, _H, _Hp], "aesfhe_bootstrap": [vp, _H, _Hp],
         "aesfhe_renorm_pair": [vp, _H, _H, _Hp, _Hp],
@@ -670,6 +670,11 @@ class Engine:
         """the renorm's pool of zero encryptions (aesfhe_renorm_pool): size per refill (0: off, the
         per-renorm encryption; -1: keep), every pool emptied"""
         self._ctx.check(self._lib.aesfhe_renorm_pool(self._ctx.ptr, int(size)))
+
+    def set_stack_pack(self, members: int) -> None:
+        """members per packed bootstrap of a stacked periodic ciphertext (aesfhe_set_stack_pack;
+        1 = every member its own bootstrap)"""
+        self._ctx.check(self._lib.aesfhe_set_stack_pack(self._ctx.ptr, int(members)))
 
     def mul_pt_sum(self, pairs) -> Ciphertext:
         """sum of ct * pt over 1..8 (ciphertext, non-constant plaintext) pairs as one engine call

@@ -488,10 +488,21 @@ def run_pairs(ctx, coeffs, rks, args, rank, world, dist, pairs: int, states: int
             "ms_per_step": elapsed / steps_n * 1e3, "ms_per_pair": elapsed / (steps_n * pairs) * 1e3,
             "verified_against_plaintext_model": bool(ok),
             "roofline_step": leg.step(elapsed, steps_n, tj, args.profile_every),
-            # one-state pairs: the C2 line's precision is the same path's; a debug-logged stack of 64 would
-            # decrypt ~16k stage ciphertexts
-            "precision": measure_precision(pipes[c0], ctx, rks, warm[c0], f"one stack of {c0} pairs x {states} states")
-            if rank == 0 and states > 1 else None}
+            # one-state pairs: a debug-logged stack of 64 would decrypt ~16k stage ciphertexts, so a stack of
+            # 16 (every member of its MixColumns bootstraps packed into one, as in the stacks of 64:
+            # aesfhe_set_stack_pack)
+            "precision": (pair_precision(ctx, coeffs, rks, rng) if states == 1 else
+                          measure_precision(pipes[c0], ctx, rks, warm[c0], f"one stack of {c0} pairs x {states} states"))
+            if rank == 0 else None}
+
+
+def pair_precision(ctx, coeffs, rks, rng, pairs: int = 16) -> dict:
+    """measure_precision of the one-state stacked path on a stack of `pairs` pairs"""
+    from pipeline import AESPipeline
+    pipe = AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=True, pairs=pairs)
+    st = rng.integers(0, 256, (pairs, 16), dtype=np.uint8)
+    pipe.encrypt(st, rks)  # warm: the stack's plaintext caches
+    return measure_precision(pipe, ctx, rks, st, f"one stack of {pairs} one-state pairs")
 
 
 def run_batch(ctx, coeffs, rks, args, rank, world, dist, tj: dict) -> dict:

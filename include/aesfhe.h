@@ -160,6 +160,11 @@ int aesfhe_mul_pt_sum(aesfhe_ctx* ctx, int n, const aesfhe_handle* cts, const ae
  * refill (0: every renorm encrypts its own message; < 0: keep the size), every pool emptied -- the
  * re-encryption of REF/pipeline.py:65-69 (decrypt -> snap -> encrypt) drawn as Enc(0) + message */
 int aesfhe_renorm_pool(aesfhe_ctx* ctx, int size);
+/* members per packed bootstrap of a stacked periodic ciphertext (aesfhe_bootstrap_sparse on a stack):
+ * up to `members` (a power of two dividing the stack size) monomial-packed into one message of
+ * `members` times the period, one bootstrap each.  1: every member its own
+ * bootstrap (bit-exact with single bootstraps); default 16 (AESFHE_STACK_PACK). */
+int aesfhe_set_stack_pack(aesfhe_ctx* ctx, int members);
 int aesfhe_conjugate_many(aesfhe_ctx* ctx, int n, const aesfhe_handle* in, aesfhe_handle* out);
 /* n automorphisms of possibly DIFFERENT ciphertexts, each with its own Galois element galois[i]
  * (odd, < 2N): engine.rotate(ct, rotation_key, steps) (REF/engine_context.py:127-132; Galois

@@ -131,6 +131,31 @@ def test_stacked_bootstraps_bit_exact(ctx):
     _same(E, L, [s[1] for s in singles], "mono pair bootstrap (lo)")
 
 
+@pytest.mark.parametrize("members", [2, 4, 8])
+def test_stacked_bootstrap_packing(ctx, members):
+    """aesfhe_set_stack_pack: an 8-member stack of period-32 ciphertexts bootstrapped `members` per
+    bootstrap (monomial packing over the stack's halves) returns every member
+    in its place, within `members` x the single bootstrap's error of it, at the same level"""
+    from test_gpu_bootstrap import BOOT_TOL
+    E = ctx.engine
+    M, P = 8, 32
+    rng = np.random.default_rng(70 + members)
+    zs = [np.tile(np.exp(2j * np.pi * rng.random(P)), E.slot_count // P) for _ in range(M)]
+    st = E.stack([E.encrypt(z) for z in zs])
+    try:
+        E.set_stack_pack(1)
+        ref = E.unstack(E.bootstrap_sparse(st, P))
+        E.set_stack_pack(members)
+        out = E.unstack(E.bootstrap_sparse(st, P))
+    finally:
+        E.set_stack_pack(16)
+    for z, r, o in zip(zs, ref, out):
+        assert o.level == r.level
+        assert np.abs(E.decrypt(o) - z).max() < members * BOOT_TOL
+    with pytest.raises(RuntimeError):
+        E.set_stack_pack(0)
+
+
 @pytest.mark.parametrize("periodic", [True, False])
 def test_pipeline_pairs_encrypt(ctx, coeff_dir, periodic):
     """AESPipeline(pairs=P): P ciphertext pairs with one state each (BASELINE config 3's shape),

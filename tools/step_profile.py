@@ -2,7 +2,7 @@
 steps as AESPipeline.encrypt_round runs them (level-targeted renorms); the
 final bootstrap pair of MixColumns is the difference of MixColumns with and without it.
 Arguments: pairs=P (stacked ciphertext pairs), states=S (slot-packed states per
-pair), reps=R, --eager, --concurrent.  One more profiled round gives each step's time per kernel
+pair), reps=R, fresh=L dnum=d (the context's set, default the bench's 9 / 4), --eager, --concurrent.  One more profiled round gives each step's time per kernel
 class (engine profiler, every launch: in-kernel spans / dispatch-stamped events)."""
 import json
 import sys
@@ -25,7 +25,8 @@ def main():
     serial = "--concurrent" not in sys.argv
     kv = dict(a.split("=", 1) for a in sys.argv[1:] if "=" in a)
     pairs, states, reps = int(kv.get("pairs", 1)), int(kv.get("states", 1)), int(kv.get("reps", 3))
-    ctx = EngineContext(signature=1, max_level=17, lazy=lazy, concurrent=not serial)
+    fresh, dnum = int(kv.get("fresh", 9)), int(kv.get("dnum", 4))  # the bench's C2 set (bench.py --fresh-level / --dnum)
+    ctx = EngineContext(signature=1, boot_fresh_level=fresh, dnum=dnum, lazy=lazy, concurrent=not serial)
     E = ctx.engine
     pipe = AESPipeline(ctx, load_all_coeffs(), use_hard_renorm_between_steps=True, states=states, pairs=pairs)
     np.random.seed(7)
