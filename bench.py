@@ -112,7 +112,7 @@ def parse():
                     help="with AESFHE_PROFILE_FROM_START=<ids>: keep the engine's per-kernel accounting from the first "
                          "launch on (no reset, every launch) and write it to this JSON file -- the algorithmic bytes of "
                          "exactly the launches a whole-process rocprofv3 --pmc pass counts")
-    ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r6_pmc_traffic_bench.json"),
+    ap.add_argument("--traffic-json", default=str(Path(__file__).resolve().parent / "profiles" / "r6_pmc_traffic_bench_final.json"),
                     help="per-kernel-class HBM / algorithmic byte ratios from rocprofv3 --pmc passes over this bench's own "
                          "C2 leg (tools/gpu_task.sh pmcbench; FETCH_SIZE and raw TCC write requests, separate runs)")
     ap.add_argument("--detail-json", default="gpurun_out/bench_detail.json",

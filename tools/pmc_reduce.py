@@ -4,7 +4,8 @@ gfx950 corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half t
 wide coalesced reads -> x2; WRITE_SIZE is exact.  Both counters are in KB.  Usage:
   python tools/pmc_reduce.py [--source=LABEL] [--alg=STATS.json] OUT.json DIR [DIR ...]   (one DIR per --pmc pass)
 Deletes the (large) CSVs after reading so gpurun can copy the result back.  A DIR that is an earlier
-OUT.json re-aggregates its per-kernel entries (after a change of the kernel -> class map below)."""
+OUT.json re-aggregates its per-kernel entries (after a change of the kernel -> class map below; with
+--refetch also after a kernel joined FETCH_AS_IS: its FETCH bytes halved back)."""
 import csv
 import json
 import sys
@@ -22,7 +23,12 @@ RAW_WRITE = ("TCC_EA0_WRREQ_sum", "TCC_EA0_WRREQ_64B_sum")
 # WRITE bytes, pass 2 (p[j + 16 k] dword reads) FETCH x2 = 2.36 x WRITE, i.e. FETCH x1 =
 # 1.18 x WRITE = its data plus twiddle pairs.  The finish variant's cur / add reads are
 # 16 B per lane, so its total is a lower bound.
-FETCH_AS_IS = ("ntt2_fwd",)
+# k_ntt2_fwd8 (round 6, 8 residues per thread) reads its rows the same way (p[t + 32 k]: 128 B per
+# 32-lane half); its finish mode's cur / add reads are 16 B per lane (a lower bound again)
+FETCH_AS_IS = ("ntt2_fwd", "ntt2_fwd8")
+
+
+REFETCH = False
 
 
 def short(name: str) -> str:
@@ -34,11 +40,14 @@ def short(name: str) -> str:
 
 
 def main():
+    global REFETCH
     src = alg = None
     args = sys.argv[1:]
     while args and args[0].startswith("--"):
         if args[0].startswith("--source="):
             src = args[0].split("=", 1)[1]
+        elif args[0] == "--refetch":
+            REFETCH = True
         elif args[0].startswith("--alg="):  # the probe's own engine kernel_stats (algorithmic bytes)
             alg = json.loads(Path(args[0].split("=", 1)[1]).read_text())
         args = args[1:]
@@ -69,8 +78,12 @@ def main():
     res = {}
     for d in dirs:
         if d.endswith(".json"):
-            res.update({k: v for k, v in json.loads(Path(d).read_text()).items()
-                        if isinstance(v, dict) and "fetch_size_bytes" in v})
+            old = {k: dict(v) for k, v in json.loads(Path(d).read_text()).items() if isinstance(v, dict) and "fetch_size_bytes" in v}
+            for k, v in old.items():  # --refetch: entries reduced with x2 before FETCH_AS_IS named them
+                if REFETCH and k.split("<")[0] in FETCH_AS_IS:
+                    v["fetch_size_bytes"] /= 2.0
+                    v["bytes_per_launch"] = v["fetch_size_bytes"] + v.get("write_size_bytes", 0.0)
+            res.update(old)
             if src is None:
                 src = json.loads(Path(d).read_text()).get("_source")
     for k in acc:
