@@ -26,7 +26,11 @@ class ZetaEncoder:
 # level that still leaves its output at RENORM_FLOOR.  Depths are those of the fused forms
 # from canonical inputs (measured: fresh level 17 -> 12 for XOR4 / GF multipliers, -> 4 for
 # SubBytes).
-RENORM_FLOOR = 2
+# 1 since round 6 (2 before): every renormalised step ends one level lower, so its whole evaluation runs on
+# one limb fewer and the C2 set's fresh level drops to 8 (bench.py --fresh-level): C2 97.5-98.0 -> 101.9-102.3
+# rounds/s, precision margin 322-360x -> 337-423x (profiles/r6_renorm_floor_ab.txt).  0 is too low for the
+# fused LUT sums (the per-term loops take over: 45.5 rounds/s).  AESFHE_RENORM_FLOOR overrides (A/B runs)
+RENORM_FLOOR = int(os.environ.get("AESFHE_RENORM_FLOOR", "1"))
 LUT2_DEPTH = 5       # bivariate nibble LUT (XOR4, GF multipliers): basis 3 + product + coefficient
 SUBBYTES_DEPTH = 13  # lift, b = hi * L(lo), baby/giant steps (sub_bytes_lut.py)
 SHIFTROWS_DEPTH = 1  # masked rotations (shift_rows.py)
