@@ -103,9 +103,10 @@ def parse():
     ap.add_argument("--true-fhe-steps", type=int, default=2,
                     help="SURVEY.md 8(f)3 line beside the headline: C2 encrypts with every secret-key renorm replaced "
                          "by bootstrap + homomorphic Zeta16 snap (AESPipeline(true_fhe=True)); 0 = skip")
-    ap.add_argument("--fhe-fresh-level", type=int, default=12,
-                    help="fresh level of the true-FHE leg's context: one depth-4 snap + the 8 levels of the deepest step "
-                         "between renorms (ShiftRows -> GF multipliers / XOR4s, nibble-bivariate SubBytes), DESIGN.md 8")
+    ap.add_argument("--fhe-fresh-level", type=int, default=11,
+                    help="fresh level of the true-FHE leg's context: one depth-4 snap + the 7 levels of the deepest step "
+                         "between renorms at the renorm floor 1 (ShiftRows -> GF multipliers / XOR4s, nibble-bivariate "
+                         "SubBytes), DESIGN.md 8")
     ap.add_argument("--fhe-dnum", type=int, default=4, help="key-switching digits of the true-FHE leg's context")
     ap.add_argument("--no-batch-roundtrip", dest="batch_roundtrip", action="store_false",
                     help="skip the decrypt leg of the batch (BASELINE config 5)")
@@ -662,7 +663,7 @@ def run_true_fhe(ctx, coeffs, rks, args, rank, world, dist, tj: dict) -> dict:
     normalised by 1/256.  One state per rank per step, checked after the timed region."""
     from oracle import aes_plain  # checker only, after the timed region
     from pipeline import AESPipeline
-    # one snap + the deepest step between renorms (8 levels): the --fhe-fresh-level set (12 / 4)
+    # one snap + the deepest step between renorms (7 levels at the renorm floor 1): the --fhe-fresh-level set (11 / 4)
     ctx = fhe_context(ctx, args.fhe_fresh_level, args.fhe_dnum)
     pipe = AESPipeline(ctx, coeffs, use_hard_renorm_between_steps=False, true_fhe=True)
     sts = rank_states(rank + 1000, 1 + args.true_fhe_steps)

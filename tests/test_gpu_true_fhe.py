@@ -135,7 +135,7 @@ def test_quad_bootstrap_matches_pair_bootstraps(ctx):
 
 
 def test_true_fhe_c2_on_the_bench_set(coeff_dir, monkeypatch):
-    """the bench's true-FHE set (bench.py --fhe-fresh-level 12 --fhe-dnum 4): one snap per renorm with
+    """the bench's true-FHE set (bench.py --fhe-fresh-level 11 --fhe-dnum 4): one snap per renorm with
     the nibble-bivariate SubBytes, MixColumns' paired renorms in quad bootstraps; encrypt and decrypt
     are FIPS-197's bytes with no secret-key call, 1 + 9 * 5 + 2 bootstrap calls per encrypt for the
     same 132 refreshed ciphertexts"""
@@ -143,7 +143,7 @@ def test_true_fhe_c2_on_the_bench_set(coeff_dir, monkeypatch):
     from engine_context import EngineContext
     from oracle import aes_plain as A
     from pipeline import AESPipeline
-    c12 = EngineContext(signature=1, boot_fresh_level=12, dnum=4, thread_count=4, seed=0xF12, enc_nonce=0xF12)
+    c12 = EngineContext(signature=1, boot_fresh_level=11, dnum=4, thread_count=4, seed=0xF12, enc_nonce=0xF12)
     pipe = AESPipeline(c12, load_all_coeffs(coeff_dir), use_hard_renorm_between_steps=False, true_fhe=True)
     assert pipe.snapper.max_snaps == 1 and pipe.encoder.renorm_quad_hook is not None
     rng = np.random.default_rng(12)
