@@ -139,6 +139,10 @@ _MC_HOIST = os.environ.get("AESFHE_MC_HOIST", "1") != "0"
 SR_MC_ENTRY = os.environ.get("AESFHE_SR_MC_ENTRY", "1") != "0"
 # AESFHE_PT_SUM=0: sr_entry's masked sums as separate plaintext products and additions (A/B)
 _PT_SUM = os.environ.get("AESFHE_PT_SUM", "1") != "0"
+# strict hoist: MixColumns' GF pair output renormalised as the (hi, lo) pair and packed after its renorm
+# instead of packed before it -- the multipliers (and the renormalised input u they read) one level lower,
+# so the strict path needs fresh level 7 instead of 8 (AESFHE_GF2_PAIR_RENORM=0: pack, then renorm)
+_GF2_PAIR = os.environ.get("AESFHE_GF2_PAIR_RENORM", "1") != "0"
 
 
 class MixColFinal:
@@ -171,7 +175,19 @@ class MixColFinal:
         enc = self.enc
         if getattr(enc, "pack_renorm_direct", lambda ct=None: False)(u[0]):
             return enc.renorm_pack(*self.gf_mult_2(*u, out_level=fl, defer_conj=True), level=NEED_XOR)
+        if self._gf2_pair_renorm():
+            return enc.pack(*enc.renorm(*self.gf_mult_2(*u, out_level=fl, defer_conj=True), level=NEED_XOR + enc.PACK_DEPTH))
         return enc.renorm_packed(enc.pack(*self.gf_mult_2(*u, out_level=fl + enc.PACK_DEPTH, defer_conj=True)), level=NEED_XOR)
+
+    def _gf2_pair_renorm(self) -> bool:
+        """the GF pair's output renormalised unpacked, packed after (_GF2_PAIR): strict renorms, a periodic
+        layout the pair renorm serves"""
+        return _GF2_PAIR and not FOLDS.pack and self.enc.renorm_hook is None and self.layout.periodic
+
+    def hoist_input_level(self) -> int:
+        """the level the strict hoist's packed renorm hands out (y): the unpack and the GF pair's inputs"""
+        gf_in = RENORM_FLOOR + LUT2_DEPTH + (0 if self._gf2_pair_renorm() else self.enc.PACK_DEPTH)
+        return gf_in + self.enc.UNPACK_DEPTH
 
     def gf_mult_2(self, ct_hi, ct_lo, out_level=None, defer_conj: bool = False):
         return gf_mult_pair(self.ctx, self._coeffs, 2, ct_hi, ct_lo, out_level, defer_conj)
@@ -310,7 +326,7 @@ class MixColFinal:
                     # which within each P-slot half is rot(y, 2 s1) on the first 8 unit slots and
                     # rot(y, 2 s1 + P) on the others -- no rotation waits for the unpack
                     P = self.layout.period
-                    y = enc.renorm_packed(x, level=gl + enc.UNPACK_DEPTH)
+                    y = enc.renorm_packed(x, level=self.hoist_input_level())
                     z, ym, yp = rotate_multi(ctx, [(y, P), (y, 2 * s1), (y, 2 * s1 + P)])  # one source: one ModUp
                     u = enc.unpack(y, z)
                     lowm = lambda: np.tile((np.arange(P) < -2 * s1).astype(np.float64), self.sc // P)  # noqa: E731

@@ -91,10 +91,10 @@ def parse():
                     help="multi-pair slot-packed batch: this many stacked ciphertext pairs of 2048 states each per rank; 0 = skip")
     ap.add_argument("--pair-steps", type=int, default=1, help="timed steps of the one-state multi-pair leg (C3 literally)")
     ap.add_argument("--packed-pair-steps", type=int, default=3, help="timed steps of the slot-packed multi-pair leg")
-    ap.add_argument("--fresh-level", type=int, default=8,
-                    help="fresh level of the C2 context's bootstrappable set (EngineContext(boot_fresh_level=)): 8, the most "
+    ap.add_argument("--fresh-level", type=int, default=7,
+                    help="fresh level of the C2 context's bootstrappable set (EngineContext(boot_fresh_level=)): 7, the most "
                          "any step of the strict pipeline needs between renorms / bootstraps at the renorm floor 1 "
-                         "(utils.RENORM_FLOOR), puts the bootstrap's double-prime region 9 primes lower (DESIGN.md 3.1); the "
+                         "(utils.RENORM_FLOOR), puts the bootstrap's double-prime region 10 primes lower (DESIGN.md 3.1); the "
                          "true-FHE leg has its own set (--fhe-fresh-level), the REF-call legs keep the engine's 17")
     ap.add_argument("--dnum", type=int, default=4, help="key-switching digits of the C2 context (4: the shorter chain leaves "
                                                          "room under the 128-bit bound; the engine's default set uses 5)")

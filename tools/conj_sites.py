@@ -18,7 +18,7 @@ from pipeline import AESPipeline  # noqa: E402
 
 
 def main():
-    ctx = EngineContext(signature=1, boot_fresh_level=8, dnum=4)  # the bench's C2 set
+    ctx = EngineContext(signature=1, boot_fresh_level=7, dnum=4)  # the bench's C2 set
     pipe = AESPipeline(ctx, load_all_coeffs(), use_hard_renorm_between_steps=True)
     rng = np.random.default_rng(7)
     rks = expand_aes128_key(rng.integers(0, 256, 16, dtype=np.uint8))

@@ -91,7 +91,7 @@ for t in "$@"; do
           --master-port=29531 bench.py --gpus 1 --steps 3 --warmup 1 --no-cpu-baseline --batch-states 256 --c5-states 256 \
           --pair-states 0 --packed-pairs 0 --true-fhe-steps 0 --eager-steps 0 --deferred-steps 0 > $O/bench_rccl_1rank.json 2> $O/rccl1.err ;;
     boot)
-      timeout -k 10 300 python3 tools/boot_phases.py 32 ${BOOT_SET:-8 4} > $O/boot_phases.json 2> $O/boot.err ;;
+      timeout -k 10 300 python3 tools/boot_phases.py 32 ${BOOT_SET:-7 4} > $O/boot_phases.json 2> $O/boot.err ;;
     fhe)
       for e in ${FHE_ENV:-AESFHE_NONE=0}; do
         env $e timeout -k 10 300 python3 tools/fhe_profile.py ${FHE_ARGS:-2} > $O/fhe_profile_$e.json 2> $O/fhe_$e.err

@@ -21,7 +21,7 @@ from pipeline import AESPipeline  # noqa: E402
 def main():
     pairs = int(sys.argv[1]) if len(sys.argv) > 1 else 16
     packs = [int(a) for a in sys.argv[2:]] or [1, 2, 4, 8, 16]
-    ctx = EngineContext(signature=1, boot_fresh_level=8, dnum=4, seed=0xC3C3)
+    ctx = EngineContext(signature=1, boot_fresh_level=7, dnum=4, seed=0xC3C3)
     E = ctx.engine
     pipe = AESPipeline(ctx, load_all_coeffs(), use_hard_renorm_between_steps=True, pairs=pairs)
     rng = np.random.default_rng(33)

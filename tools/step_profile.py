@@ -25,7 +25,7 @@ def main():
     serial = "--concurrent" not in sys.argv
     kv = dict(a.split("=", 1) for a in sys.argv[1:] if "=" in a)
     pairs, states, reps = int(kv.get("pairs", 1)), int(kv.get("states", 1)), int(kv.get("reps", 3))
-    fresh, dnum = int(kv.get("fresh", 8)), int(kv.get("dnum", 4))  # the bench's C2 set (bench.py --fresh-level / --dnum)
+    fresh, dnum = int(kv.get("fresh", 7)), int(kv.get("dnum", 4))  # the bench's C2 set (bench.py --fresh-level / --dnum)
     ctx = EngineContext(signature=1, boot_fresh_level=fresh, dnum=dnum, lazy=lazy, concurrent=not serial)
     E = ctx.engine
     pipe = AESPipeline(ctx, load_all_coeffs(), use_hard_renorm_between_steps=True, states=states, pairs=pairs)
