@@ -1095,13 +1095,14 @@ __global__ void __launch_bounds__(256) k_renorm_sparse(u32* W, const u32* B, Spa
         const PrimeConst P = pc[t];
         const u32* g = gs + t * 2 * D;
         const u32* Bc = bs + t * D;
-        u32 acc = 0;
+        unsigned long long acc = 0;  // D reduced products < 2^36: one reduction, no dependent add_mod chain
+#pragma unroll 8
         for (int b = 0; b < D; ++b) {
             const u32 rv = (u32)(__brev((unsigned)b) >> (32 - LD));
             const u32 e = (2u * D - (((2u * rv + 1u) * (u32)j) & (2u * D - 1))) & (2u * D - 1);
-            acc = add_mod(acc, barrett_mul(Bc[b], g[e], P.q, P.mu), P.q);
+            acc += barrett_mul(Bc[b], g[e], P.q, P.mu);
         }
-        cr[idx] = shoup_mul(acc, P.ninv, P.ninv_p, P.q);
+        cr[idx] = shoup_mul((u32)(acc % P.q), P.ninv, P.ninv_p, P.q);
     }
     __syncthreads();
     if (threadIdx.x < D) {
@@ -1145,9 +1146,10 @@ __global__ void __launch_bounds__(256) k_renorm_sparse(u32* W, const u32* B, Spa
         const u32 rv = (u32)(__brev((unsigned)d) >> (32 - LD));
         const u32 e1 = 2u * rv + 1u;
         const u32* g = gs + t * 2 * D;
-        u32 acc = 0;
-        for (int j = 0; j < D; ++j) acc = add_mod(acc, barrett_mul(res[t * D + j], g[(e1 * (u32)j) & (2u * D - 1)], q, mu), q);
-        W[((size_t)c * nl + t) * D + d] = acc;
+        unsigned long long acc = 0;
+#pragma unroll 8
+        for (int j = 0; j < D; ++j) acc += barrett_mul(res[t * D + j], g[(e1 * (u32)j) & (2u * D - 1)], q, mu);
+        W[((size_t)c * nl + t) * D + d] = (u32)(acc % q);
     }
 }
 // out_c (2 polys x nl limbs) = the zero encryption pool_c + (W_c broadcast over runs of N / D on c0)
