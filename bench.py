@@ -630,22 +630,22 @@ _CTX17 = {}
 
 
 def full_levels(ctx):
-    """ctx itself when its fresh level is the engine's default 17, else ONE extra context with the engine's
-    default bootstrappable set (fresh level 17, dnum 5; same seed, its own keys), made once: for the legs
-    whose path needs more levels between renorms than the C2 set's 9 (true-FHE, the reference pair path
-    of a state count too large for the packed form)"""
-    if ctx.engine.fresh_level >= 17:
+    """ctx itself when its fresh level covers the reference pair path, else ONE extra context (same seed, its
+    own keys), made once: for the pair path of a state count too large for the packed form, whose deepest
+    step between renorms is ShiftRows -> GF multipliers -> XOR4 (utils.NEED_SR_MIX levels: 12 at the renorm
+    floor 1), on a bootstrappable set with that fresh level and 4 digits (AESFHE_PAIR_SET_17=1: the engine's
+    default 17 / 5 set, round 5's)"""
+    from utils import NEED_SR_MIX
+    fresh, dnum = (17, 5) if os.environ.get("AESFHE_PAIR_SET_17") == "1" else (max(NEED_SR_MIX, 1), 4)
+    if ctx.engine.fresh_level >= fresh:
         return ctx
-    if "ctx" not in _CTX17:
-        from engine_context import EngineContext
-        _CTX17["ctx"] = EngineContext(signature=1, max_level=17, thread_count=1, device_id=ctx.engine.device_id, seed=ctx.engine.seed,
-                                      lazy=ctx.engine.lazy)
-    return _CTX17["ctx"]
+    return fhe_context(ctx, fresh, dnum)
 
 
 def fhe_context(ctx, fresh: int, dnum: int):
     """ctx itself when it has the bootstrappable set (fresh, dnum), else ONE extra context with it (same
-    seed, its own keys), made once: the true-FHE leg's set (--fhe-fresh-level / --fhe-dnum)"""
+    seed, its own keys), made once per set: the true-FHE leg's (--fhe-fresh-level / --fhe-dnum) and the
+    pair path's (full_levels)"""
     E = ctx.engine
     if E.fresh_level == fresh and E.dnum == dnum:
         return ctx
