@@ -63,3 +63,76 @@ def test_snapper_1d_coefficients_and_codewords(coeff_dir, ref_coeffs):
     assert np.abs(y - Z).max() < 1e-2
     nib = np.round(-np.angle(y) * 16 / (2 * np.pi)).astype(int) % 16
     assert np.array_equal(nib, np.arange(16))
+
+
+class _Eng:
+    """engine stub: fresh level, stack / unstack of tagged members (lists), a slot count"""
+
+    def __init__(self, fresh):
+        self.fresh_level = fresh
+        self.slot_count = 32768
+        self.stacked = []
+
+    def stack(self, cts):
+        self.stacked.append(len(cts))
+        return list(cts)
+
+    def unstack(self, st):
+        return list(st)
+
+
+class _Ctx:
+    def __init__(self, fresh, quad=True):
+        self.engine = _Eng(fresh)
+        self.bootstrap_pair_scaled = lambda *a, **k: None
+        if quad:
+            self.bootstrap_quad_scaled = lambda cts, gain, period: [("boot", c) for c in cts]
+        self.to_intt = lambda c: c
+
+
+def test_snap_count_rule():
+    """BootstrapSnap: one snap everywhere with max_snaps=1 (the nibble SubBytes' rule, round 6); with 2, a
+    second one where the consumer needs <= 8 levels (None / 0: an XOR4 follows) and the fresh level
+    leaves snap + 5 + the need"""
+    from zeta16_noise_reducer import BootstrapSnap
+    one = BootstrapSnap(_Ctx(11), period=16, max_snaps=1)
+    assert not any(one._twice(lv) for lv in (None, 0, 6, 7, 8, 13))
+    from utils import NEED_XOR
+    from zeta16_noise_reducer import DOUBLE_SNAP_MAX_LEVEL as M, SNAP15_DEPTH
+    two = BootstrapSnap(_Ctx(17), period=16, max_snaps=2)
+    for lv in (None, 0, M - 1, M, M + 1, 13):
+        need = lv if lv else NEED_XOR
+        assert two._twice(lv) == (need <= M and 17 - 2 * SNAP15_DEPTH - 1 >= need), lv
+    assert two._twice(None) and two._twice(M) and not two._twice(M + 1)
+    low = BootstrapSnap(_Ctx(NEED_XOR + 2 * SNAP15_DEPTH), period=16, max_snaps=2)  # one level short of two snaps + an XOR4
+    assert not any(low._twice(lv) for lv in (None, 0, NEED_XOR, M))
+
+
+def test_quad_renorm_stacks_four():
+    """apply_quad: ONE quad bootstrap of the two pairs and ONE snap over a four-member stack; without
+    the context's quad bootstrap (or a period) it falls back to two pair renorms"""
+    import utils
+    from zeta16_noise_reducer import BootstrapSnap
+    ctx = _Ctx(11)
+    bs = BootstrapSnap(ctx, period=16, max_snaps=1)
+    assert bs.quad_ok()
+    calls = []
+    bs.snap.apply_scaled = lambda u: calls.append(u) or [("snap", m) for m in u]
+    if utils.can_fork(ctx):
+        return
+    (a, b), (c, d) = bs.apply_quad(("h1", "l1"), ("h2", "l2"))
+    assert (a, b, c, d) == tuple(("snap", ("boot", x)) for x in ("h1", "l1", "h2", "l2"))
+    assert ctx.engine.stacked == [4] and len(calls) == 1
+    assert not BootstrapSnap(_Ctx(11, quad=False), period=16).quad_ok()
+    assert not BootstrapSnap(ctx, period=None).quad_ok()
+
+
+def test_stacked_many_pairs_without_stack():
+    """utils.stacked_many: one stacked call when the engine stacks, else pairwise (odd count: the last alone)"""
+    import utils
+
+    class _NoStack:
+        engine = object()
+
+    got = utils.stacked_many(_NoStack(), lambda x: x * 10 if isinstance(x, int) else x, [1, 2, 3])
+    assert got == [10, 20, 30]
