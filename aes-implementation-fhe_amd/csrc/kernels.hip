@@ -1365,6 +1365,55 @@ __global__ void __launch_bounds__(kBlock) k_lut_bivariate(u32* out, LutOperands 
     out[((size_t)(2 * nl) << logn) + off] = reduce64(acc2, q, P.mu, P.r32);
 }
 
+// k_lut_bivariate with the B elements staged once per thread: each thread reads B_q at its own offset once
+// (into LDS used as per-thread indexable storage: a thread reads back only what it wrote, no barrier) instead
+// of once per A_p term group -- the same terms, folds and reductions in the same order, so the same residues.
+// Dynamic LDS: 2 n_b kBlock words
+// (used: the B indices some term reads -- the others may be unset)
+__global__ void __launch_bounds__(kBlock) k_lut_bivariate_lds(u32* out, LutOperands op, int n_a, int n_b, unsigned used, const u32* __restrict__ cst,
+                                                              int nl, const PrimeConst* pc, int logn) {
+    extern __shared__ u32 sbv[];
+    const int t = blockIdx.y, mb = blockIdx.z;
+    const size_t k = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const int half = (int)(((size_t)blockIdx.x * kBlock) >> (logn - 1));
+    const PrimeConst P = pc[t];
+    const u32 q = P.q;
+    const size_t off = ((size_t)t << logn) + k;
+    out += (size_t)mb * 3 * ((size_t)nl << logn);
+    for (int qq = 0; qq < n_b; ++qq) {
+        if (!((used >> qq) & 1u)) continue;
+        const u32* bq = op.b[qq] + (size_t)mb * 2 * ((size_t)op.nb[qq] << logn);
+        sbv[(2 * qq) * kBlock + threadIdx.x] = bq[off];
+        sbv[(2 * qq + 1) * kBlock + threadIdx.x] = bq[((size_t)op.nb[qq] << logn) + off];
+    }
+    u64 acc0 = 0, acc1 = 0, acc2 = 0;
+    int pc_ = 0;
+    for (int p = 0; p < n_a; ++p) {
+        const int t0 = op.p_start[p], t1 = op.p_start[p + 1];
+        if (t0 == t1) continue;
+        u64 s0 = 0, s1 = 0;
+#pragma unroll 4
+        for (int j = t0; j < t1; ++j) {
+            if (j > t0 && ((j - t0) & 7) == 0) s0 = fold64(s0, q, P.r32), s1 = fold64(s1, q, P.r32);
+            const int qq = op.q_of[j];
+            const u32 c = cst[((size_t)j * nl + t) * 4 + 2 * half];
+            s0 += (u64)sbv[(2 * qq) * kBlock + threadIdx.x] * c;
+            s1 += (u64)sbv[(2 * qq + 1) * kBlock + threadIdx.x] * c;
+        }
+        const u32 u0 = reduce64(s0, q, P.mu, P.r32), u1 = reduce64(s1, q, P.mu, P.r32);
+        const u32* ap = op.a[p] + (size_t)mb * 2 * ((size_t)op.na[p] << logn);
+        const u32 a0 = ap[off], a1 = ap[((size_t)op.na[p] << logn) + off];
+        if (pc_ == 4) acc0 = fold64(acc0, q, P.r32), acc1 = fold64(acc1, q, P.r32), acc2 = fold64(acc2, q, P.r32), pc_ = 0;
+        acc0 += (u64)a0 * u0;
+        acc1 += (u64)a0 * u1 + (u64)a1 * u0;
+        acc2 += (u64)a1 * u1;
+        ++pc_;
+    }
+    out[off] = reduce64(acc0, q, P.mu, P.r32);
+    out[((size_t)nl << logn) + off] = reduce64(acc1, q, P.mu, P.r32);
+    out[((size_t)(2 * nl) << logn) + off] = reduce64(acc2, q, P.mu, P.r32);
+}
+
 // grid z = member of stacked elements (element j of member m at x[j] + m npoly nx[j] N, out / acc
 // at + m npoly nl N)
 // (k_lut_bivariate's uniform coefficient half and unrolled term loop)
@@ -2009,6 +2058,22 @@ void launch_lut_bivariate(hipStream_t st, const DevTables& T, u32* out, const Lu
     double reads = 0;
     for (int p = 0; p < n_a; ++p)
         if (op.p_start[p + 1] > op.p_start[p]) reads += 2;
+    // AESFHE_LUT_LDS=0: every term reads its B element from memory (k_lut_bivariate, A/B runs)
+    static const bool lds = !(std::getenv("AESFHE_LUT_LDS") && std::atoi(std::getenv("AESFHE_LUT_LDS")) == 0);
+    int n_b = 0;
+    unsigned used = 0;
+    for (int j = 0; j < op.p_start[n_a]; ++j) {
+        if (op.q_of[j] < 0 || op.q_of[j] >= kLutMax || !op.b[op.q_of[j]]) throw std::runtime_error("launch_lut_bivariate: bad B operand");
+        n_b = std::max(n_b, op.q_of[j] + 1);
+        used |= 1u << op.q_of[j];
+    }
+    if (lds && n_b > 0) {
+        reads += 2.0 * n_b;
+        prof_launch(KID_ELEMENTWISE, words((reads + 3.0) * nl * members * (1u << T.logn)), k_lut_bivariate_lds,
+                    dim3((1u << T.logn) / kBlock, nl, members), dim3(kBlock), (unsigned)(2 * n_b * kBlock * sizeof(u32)), st, out, op, n_a, n_b,
+                    used, cst, nl, T.pc, T.logn);
+        return;
+    }
     reads += 2.0 * kLutMax;  // upper bound on the B elements read
     prof_launch(KID_ELEMENTWISE, words((reads + 3.0) * nl * members * (1u << T.logn)), k_lut_bivariate,
                 dim3((1u << T.logn) / kBlock, nl, members), dim3(kBlock), 0, st, out, op, n_a, cst, nl, T.pc, T.logn);
