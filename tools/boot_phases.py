@@ -61,7 +61,14 @@ def main():
         for k, (sp, gp, by) in rcum[name].items():
             p0 = rprev.get(k, (0.0, 0.0, 0.0))
             dsp, dgp, dby = sp - p0[0], gp - p0[1], by - p0[2]
-            if dsp > 0 and dby > 0:
+            if dsp > 0 and dby > 0 and kc.get(k):
+                # a phase's class figures are differences of two separately profiled runs: a difference below
+                # their run-to-run spread (a negative gap, or more bytes than 8 TB/s could move in the span) is
+                # reported without fractions instead of as a frac > 1
+                if dgp < 0 or dby / (dsp * 1e-3) > 8e12:
+                    roof[k] = {"span_ms": round(dsp, 4), "GB": round(dby / 1e9, 4), "launches": kc[k],
+                               "frac": None, "note": "below the resolution of the two runs' difference"}
+                    continue
                 roof[k] = {"span_ms": round(dsp, 4), "gap_ms": round(dgp, 4), "GB": round(dby / 1e9, 4),
                            "frac_span": round(dby / (dsp * 1e-3) / 8e12, 3),
                            "frac": round(dby / ((dsp + dgp) * 1e-3) / 8e12, 3)}
